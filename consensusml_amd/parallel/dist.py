@@ -1,0 +1,111 @@
+"""Process-group bootstrap: one process per GPU, torch.distributed over RCCL (backend "nccl" on
+ROCm) or gloo for the CPU plumbing config.
+
+The launcher is ``torchrun`` (or ``python -m torch.distributed.run``) with
+``--master-addr 127.0.0.1``; RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* come from the environment.
+``HSA_ENABLE_IPC_MODE_LEGACY=0`` must stay exported for RCCL on this platform.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_master(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1 and dist.is_available() and dist.is_initialized()
+
+
+_INFO: Optional[DistInfo] = None
+
+
+def init_distributed(backend: str = "auto", device: Optional[str] = None,
+                     timeout_s: float = 600.0) -> DistInfo:
+    """Initialise (once) and return this process's DistInfo."""
+    global _INFO
+    if _INFO is not None:
+        return _INFO
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if device is None:
+        use_gpu = backend != "gloo" and torch.cuda.is_available()
+        dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1)) if use_gpu \
+            else torch.device("cpu")
+    else:
+        dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    if backend == "auto":
+        backend = "nccl" if dev.type == "cuda" else "gloo"
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = dict(backend=backend, rank=rank, world_size=world,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    _INFO = DistInfo(rank, world, local, dev, backend if world > 1 else "none")
+    return _INFO
+
+
+def get_info() -> DistInfo:
+    return _INFO if _INFO is not None else DistInfo()
+
+
+def set_info(info: DistInfo) -> None:
+    """Install a DistInfo (tests that create process groups themselves)."""
+    global _INFO
+    _INFO = info
+
+
+def barrier() -> None:
+    if dist.is_available() and dist.is_initialized():
+        if get_info().device.type == "cuda":
+            dist.barrier(device_ids=[get_info().device.index])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(x: float) -> float:
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=get_info().device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def monitored_barrier(timeout_s: float = 60.0) -> None:
+    """Hang detector: on gloo, names the ranks that failed to arrive."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    if dist.get_backend() == "gloo":
+        dist.monitored_barrier(timeout=datetime.timedelta(seconds=timeout_s), wait_all_ranks=True)
+    else:
+        barrier()
+
+
+def shutdown() -> None:
+    global _INFO
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _INFO = None

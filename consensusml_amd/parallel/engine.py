@@ -1,0 +1,421 @@
+"""Consensus data-parallel engine: exchange topologies x robust rules x fused optimizer (N02-N09).
+
+Per step:  zero grads -> forward/backward (autograd accumulates into the flat gradient buffer;
+bucket collectives launch from post-accumulate hooks while backward runs) -> fault injection ->
+exchange -> robust aggregation fused with the optimizer update -> parameter all-gather.
+
+Topologies:
+  allreduce  baseline DDP: RCCL all-reduce(sum) of bf16 buckets, fused update of the full vector.
+  allgather  topology A: every rank all-gathers all N gradients ([N, L] per bucket) and runs the
+             robust rule on everything (identical, deterministic result on every rank).
+  sharded    topology B ("robust ZeRO"): all-to-all so rank r holds coordinate shard r of every
+             worker ([N, L/N] per bucket), robust rule + optimizer on the shard only (fp32 master
+             and optimizer state are sharded 1/N), then an in-place all-gather of the bf16
+             parameter shards. Gram-space rules (Krum, Multi-Krum, Weiszfeld, centered
+             clipping, Bulyan's selection) all-reduce the [n, n] fp64 partial Gram (<= 32 KB)
+             so every rank derives identical weights. Traffic ~= one ring all-reduce, spread over
+             all 7 xGMI links by the all-to-all.
+  gossip     topology C: local fused step, then ring exchange of bf16 parameters with rank +-1
+             (grouped send/recv, chunked so exchange of chunk k+1 overlaps mixing of chunk k) and
+             a fused, optionally clipped, mixing kernel.
+
+Workers = ranks x virtual_workers (micro-batches whose gradients are kept separately), so the
+robust rules can be exercised at n = 8 on a single GPU.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..config import TrainConfig
+from ..ops import kernels as K
+from .dist import DistInfo
+from .faults import COLLUSION, apply_faults
+from .flat import Bucket, FlatModel
+
+GRAM_RULES = ("krum", "multi_krum", "geomed", "centered_clip", "bulyan")
+
+
+class ConsensusEngine:
+    def __init__(self, model: torch.nn.Module, cfg: TrainConfig, info: DistInfo):
+        self.cfg = cfg
+        self.info = info
+        self.N = info.world
+        self.V = max(1, cfg.virtual_workers)
+        self.n = self.N * self.V
+        cfg.validate(self.n)
+        self.topo = cfg.topology.kind
+        self.rule = cfg.agg.rule
+        if self.topo == "allreduce" and self.rule != "mean":
+            raise ValueError("the allreduce topology only implements the mean rule")
+        pdtype = next(p for p in model.parameters() if p.requires_grad).dtype
+        self.flat = FlatModel(model, self.N, cfg.topology.bucket_mb, grad_rows=self.V,
+                              param_dtype=pdtype)
+        self.device = self.flat.device
+        self.rank = info.rank
+        self.group_active = info.distributed
+        dev = self.device
+        fl = self.flat
+        if self.group_active:   # identical starting point on every replica
+            dist.broadcast(fl.flat_param, src=0)
+
+        # -------------------------------------------------- optimizer state (fp32)
+        if self.topo == "sharded":
+            self.master = fl.gather_shard_vector(fl.flat_param, self.rank).float().contiguous()
+        else:
+            self.master = fl.flat_param.float().clone()
+        self.state_len = self.master.numel()
+        oname = cfg.optim.name
+        self.s1 = torch.zeros_like(self.master) if (oname != "sgd" or cfg.optim.momentum) else None
+        self.s2 = torch.zeros_like(self.master) if oname in ("adam", "adamw") else None
+        self.step_count = 0
+
+        # -------------------------------------------------- exchange buffers
+        extra = 1 if self.rule == "centered_clip" else 0
+        self.rows_total = self.n + extra
+        self.recv: List[torch.Tensor] = []
+        if self.topo == "sharded":
+            for b in fl.buckets:
+                self.recv.append(torch.zeros(self.rows_total, b.shard, dtype=fl.dtype, device=dev))
+        elif self.topo == "allgather":
+            for b in fl.buckets:
+                self.recv.append(torch.zeros(self.rows_total, b.length, dtype=fl.dtype, device=dev))
+        elif self.topo == "gossip":
+            self.nb_left = torch.empty_like(fl.flat_param)
+            self.nb_right = torch.empty_like(fl.flat_param)
+            self.gossip_work = None
+        # -------------------------------------------------- rule buffers
+        self.G = torch.zeros(self.rows_total, self.rows_total, dtype=torch.float64, device=dev)
+        self.w = torch.full((self.rows_total,), 1.0 / self.n, dtype=torch.float32, device=dev)
+        if extra:
+            self.w[-1] = 0.0
+        self.scores = torch.zeros(self.n, dtype=torch.float64, device=dev)
+        self.sel = torch.zeros(self.n + 1, dtype=torch.int32, device=dev)
+        self.sel_counts = torch.zeros(self.n, dtype=torch.float64, device=dev)
+        self.gout = None
+        if self.rule == "centered_clip":
+            self.gout = torch.zeros(self.state_len, dtype=torch.float32, device=dev)
+
+        # -------------------------------------------------- overlap hooks
+        self._pending: Dict[int, object] = {}
+        self._ready_count = [0] * len(fl.buckets)
+        self._hooks = []
+        self.overlap = bool(cfg.topology.overlap and self.V == 1 and self.N > 1
+                            and self.topo in ("allreduce", "allgather", "sharded")
+                            and cfg.fault.kind not in COLLUSION)
+        if self.overlap:
+            for i, p in enumerate(fl.params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self.timings: Dict[str, float] = {}
+
+    # ================================================================ public API
+    @property
+    def model(self) -> torch.nn.Module:
+        return self.flat.model
+
+    def zero_grad(self) -> None:
+        self.flat.zero_grad()
+        self._ready_count = [0] * len(self.flat.buckets)
+        self._pending.clear()
+
+    def bind_worker(self, v: int) -> None:
+        """Route the next backward's gradients into virtual-worker row v."""
+        self.flat.bind_grads(v)
+
+    def step(self) -> None:
+        """Exchange, aggregate and update (call after all backward passes of the step)."""
+        fl = self.flat
+        if not self.overlap or self.cfg.fault.kind in COLLUSION:
+            apply_faults(fl.flat_grad, self.cfg.fault, self.rank, self.step_count,
+                         self.group_active, self.cfg.seed + self.step_count)
+        for b in fl.buckets:
+            if b.index not in self._pending:
+                self._launch_bucket(b, inject=False)
+        if self.topo == "allreduce":
+            self._step_allreduce()
+        elif self.topo == "allgather":
+            self._step_allgather()
+        elif self.topo == "sharded":
+            self._step_sharded()
+        else:
+            self._step_gossip()
+        self._pending.clear()
+        self._ready_count = [0] * len(fl.buckets)
+        self.step_count += 1
+
+    # ================================================================ hooks / launches
+    def _make_hook(self, i: int):
+        b = self.flat.buckets[self.flat.bucket_of[i]]
+        need = len(b.params)
+
+        def hook(_p):
+            self._ready_count[b.index] += 1
+            if self._ready_count[b.index] == need and b.index not in self._pending:
+                self._launch_bucket(b, inject=True)
+        return hook
+
+    def _launch_bucket(self, b: Bucket, inject: bool) -> None:
+        fl = self.flat
+        if inject and self.cfg.fault.kind != "none":
+            apply_faults(fl.flat_grad, self.cfg.fault, self.rank, self.step_count,
+                         self.group_active, self.cfg.seed + self.step_count,
+                         cols=slice(b.offset, b.offset + b.length))
+        if not self.group_active or self.topo == "gossip":
+            self._pending[b.index] = None
+            return
+        g = fl.flat_grad[:, b.offset:b.offset + b.length]      # [V, L]
+        if self.topo == "allreduce":
+            src = g[0] if self.V == 1 else g.sum(0, dtype=torch.float32).to(g.dtype)
+            if self.V > 1:
+                g[0].copy_(src)
+                src = g[0]
+            self._pending[b.index] = dist.all_reduce(src, op=dist.ReduceOp.SUM, async_op=True)
+        elif self.topo == "allgather":
+            out = self.recv[b.index][: self.n]
+            src = g if self.V > 1 else g[0]
+            self._pending[b.index] = dist.all_gather_into_tensor(
+                out.view(-1), src.contiguous().view(-1), async_op=True)
+        else:  # sharded: chunk j of my bucket -> rank j; row (j*V+v) of recv = worker (j,v)'s shard r
+            out = self.recv[b.index][: self.n]
+            if self.V == 1:
+                src = g[0]
+            else:
+                src = g.reshape(self.V, self.N, b.shard).transpose(0, 1).contiguous().view(-1)
+            self._pending[b.index] = dist.all_to_all_single(out.view(-1), src, async_op=True)
+
+    def _wait(self, b: Bucket) -> None:
+        w = self._pending.get(b.index)
+        if w is not None:
+            w.wait()
+
+    # ================================================================ optimizer args
+    def _opt_args(self, gscale: float = 1.0) -> K.OptArgs:
+        o = self.cfg.optim
+        kind = "sgd" if o.name == "sgd" else "adam"
+        wd = o.weight_decay
+        return K.OptArgs(kind=kind, lr=o.lr, momentum=o.momentum if kind == "sgd" else 0.0,
+                         weight_decay=wd, nesterov=o.nesterov, first=self.step_count == 0,
+                         beta1=o.betas[0], beta2=o.betas[1], eps=o.eps,
+                         step=self.step_count + 1, gscale=gscale)
+
+    def _state(self, off: int, length: int):
+        m = self.master[off:off + length]
+        s1 = self.s1[off:off + length] if self.s1 is not None else None
+        s2 = self.s2[off:off + length] if self.s2 is not None else None
+        return m, s1, s2
+
+    # ================================================================ robust weights
+    def _rows(self, b: Bucket) -> torch.Tensor:
+        """Worker matrix of bucket b as seen by this rank ([rows_total, cols])."""
+        fl = self.flat
+        if self.topo == "sharded":
+            if not self.group_active:
+                # world 1: the local rows ARE the full workers; shard == bucket
+                return fl.flat_grad[:, b.offset:b.offset + b.length]
+            return self.recv[b.index]
+        if self.topo == "allgather":
+            if not self.group_active:
+                return fl.flat_grad[:, b.offset:b.offset + b.length]
+            return self.recv[b.index]
+        raise RuntimeError("no worker matrix for this topology")
+
+    def _cclip_rows(self, b: Bucket) -> torch.Tensor:
+        """Worker rows plus the previous-aggregate row (centered clipping)."""
+        X = self._rows(b)
+        if X.shape[0] == self.rows_total:
+            return X
+        # world 1: stage the local rows into the recv-shaped buffer once
+        if not self.recv:
+            raise RuntimeError("centered_clip needs recv buffers")
+        R = self.recv[b.index]
+        R[: self.n].copy_(X)
+        return R
+
+    def _compute_weights(self, cols) -> None:
+        """Gram over every bucket (accumulated), all-reduced across shards, then weights."""
+        cfg = self.cfg.agg
+        self.G.zero_()
+        for b, X, length in cols:
+            K.gram(X, n=self.rows_total, D=length, out=self.G, accumulate=True)
+        if self.group_active and self.topo == "sharded":
+            dist.all_reduce(self.G)
+        rule = "bulyan_select" if self.rule == "bulyan" else self.rule
+        m = cfg.m if cfg.m is not None else self.n - cfg.f
+        iters = cfg.clip_iters if rule == "centered_clip" else cfg.iters
+        K.robust_weights(self.G, rule, self.n, f=cfg.f, m=m, iters=iters, eps=cfg.eps,
+                         tol=cfg.tol, tau=cfg.tau, w_out=self.w, scores=self.scores, sel=self.sel)
+        self.sel_counts += (self.w[: self.n] > 0).double()
+
+    def _bucket_cols(self) -> list:
+        out = []
+        for b in self.flat.buckets:
+            if self.rule == "centered_clip":
+                X = self._cclip_rows(b)
+            else:
+                X = self._rows(b)
+            length = b.shard if (self.topo == "sharded" and self.group_active) else X.shape[1]
+            out.append((b, X, length))
+        return out
+
+    def _aggregate_update(self, b: Bucket, X: torch.Tensor, length: int, state_off: int,
+                          param_out: torch.Tensor, opt: K.OptArgs,
+                          gout: Optional[torch.Tensor]) -> None:
+        cfg = self.cfg.agg
+        m, s1, s2 = self._state(state_off, length)
+        if self.rule in ("median", "trimmed_mean"):
+            trim = cfg.trim if cfg.trim is not None else cfg.f
+            lo, cnt = K.sorted_range(self.rule, self.n, trim)
+            K.agg_update(X, combine="sorted", lo=lo, cnt=cnt, n=self.n, D=length, opt=opt,
+                         master=m, s1=s1, s2=s2, param_out=param_out, gout=gout)
+        elif self.rule == "bulyan":
+            theta = self.n - 2 * cfg.f
+            lo, cnt = K.sorted_range("trimmed_mean", theta, cfg.f)
+            K.agg_update(X, combine="sorted", lo=lo, cnt=cnt, rows=self.sel[:theta], n=theta,
+                         D=length, opt=opt, master=m, s1=s1, s2=s2, param_out=param_out,
+                         gout=gout)
+        else:  # mean and Gram-space rules: weighted
+            K.agg_update(X, combine="weighted", w=self.w, n=self.rows_total, D=length, opt=opt,
+                         master=m, s1=s1, s2=s2, param_out=param_out, gout=gout)
+
+    # ================================================================ topologies
+    def _step_allreduce(self) -> None:
+        fl = self.flat
+        for b in fl.buckets:
+            self._wait(b)
+        if not self.group_active and self.V > 1:
+            fl.flat_grad[0].copy_(fl.flat_grad.float().sum(0).to(fl.dtype))
+        opt = self._opt_args(gscale=1.0 / self.n)
+        m, s1, s2 = self._state(0, fl.total)
+        K.agg_update(fl.flat_grad[0], combine="weighted", n=1, opt=opt, master=m, s1=s1, s2=s2,
+                     param_out=fl.flat_param)
+
+    def _step_allgather(self) -> None:
+        fl = self.flat
+        for b in fl.buckets:
+            self._wait(b)
+        cols = self._bucket_cols()
+        if self.rule in GRAM_RULES:
+            self._compute_weights(cols)
+        opt = self._opt_args()
+        for b, X, length in cols:
+            gout = self.gout[b.offset:b.offset + b.length] if self.gout is not None else None
+            self._aggregate_update(b, X, length, b.offset, fl.flat_param[b.offset:b.offset + b.length],
+                                   opt, gout)
+            if self.rule == "centered_clip":
+                X[self.n].copy_(gout.to(X.dtype))   # v0 <- new aggregate
+
+    def _step_sharded(self) -> None:
+        fl = self.flat
+        for b in fl.buckets:
+            self._wait(b)
+        cols = self._bucket_cols()
+        if self.rule in GRAM_RULES:
+            self._compute_weights(cols)
+        opt = self._opt_args()
+        works = []
+        for b, X, length in cols:
+            if self.group_active:
+                pout = fl.my_shard(fl.flat_param, b, self.rank)
+                soff = b.shard_offset
+            else:
+                pout = fl.flat_param[b.offset:b.offset + b.length]
+                soff = b.offset
+            gout = self.gout[soff:soff + length] if self.gout is not None else None
+            self._aggregate_update(b, X, length, soff, pout, opt, gout)
+            if self.rule == "centered_clip":
+                X[self.n, :length].copy_(gout.to(X.dtype))
+            if self.group_active:
+                full = fl.flat_param[b.offset:b.offset + b.length]
+                works.append(dist.all_gather_into_tensor(full, pout, async_op=True))
+        for w in works:
+            w.wait()
+
+    def _step_gossip(self) -> None:
+        fl = self.flat
+        opt = self._opt_args(gscale=1.0 / self.V)
+        m, s1, s2 = self._state(0, fl.total)
+        K.agg_update(fl.flat_grad, combine="weighted", n=self.V, opt=opt, master=m, s1=s1, s2=s2,
+                     param_out=fl.flat_param)
+        if not self.group_active or self.N == 1:
+            return
+        w0, w1, w2 = self.cfg.topology.gossip_weights
+        clip = self.cfg.topology.gossip_clip
+        left = (self.rank - 1) % self.N
+        right = (self.rank + 1) % self.N
+        chunk = max(int(256 * 1024 * 1024 // 2), 64)   # 256 MB of bf16 per exchange chunk
+        total = fl.total
+        starts = list(range(0, total, chunk))
+
+        def exchange(s):
+            e = min(s + chunk, total)
+            ops = [dist.P2POp(dist.isend, fl.flat_param[s:e], left),
+                   dist.P2POp(dist.isend, fl.flat_param[s:e], right),
+                   dist.P2POp(dist.irecv, self.nb_left[s:e], left),
+                   dist.P2POp(dist.irecv, self.nb_right[s:e], right)]
+            return dist.batch_isend_irecv(ops)
+
+        if clip > 0 and len(starts) > 1:
+            # clipping needs whole-vector neighbour distances: exchange everything first
+            reqs = [exchange(s) for s in starts]
+            for rq in reqs:
+                for w in rq:
+                    w.wait()
+            K.gossip_mix(self.master, self.nb_left, self.nb_right, w0, w1, w2, clip,
+                         param_out=fl.flat_param)
+            return
+        reqs = exchange(starts[0])
+        for k, s in enumerate(starts):
+            nxt = exchange(starts[k + 1]) if k + 1 < len(starts) else None
+            for w in reqs:
+                w.wait()
+            e = min(s + chunk, total)
+            K.gossip_mix(self.master[s:e], self.nb_left[s:e], self.nb_right[s:e], w0, w1, w2,
+                         clip, param_out=fl.flat_param[s:e])
+            reqs = nxt
+
+    # ================================================================ state
+    def state_dict(self) -> dict:
+        sd = {"master": self.master, "step": self.step_count, "sel_counts": self.sel_counts,
+              "rank": self.rank, "world": self.N, "topology": self.topo}
+        if self.s1 is not None:
+            sd["s1"] = self.s1
+        if self.s2 is not None:
+            sd["s2"] = self.s2
+        if self.rule == "centered_clip":
+            sd["v0"] = self.gout
+        return sd
+
+    def load_state_dict(self, sd: dict) -> None:
+        if sd["world"] != self.N or sd["topology"] != self.topo:
+            raise ValueError("checkpoint was written with a different world size / topology")
+        self.master.copy_(sd["master"])
+        if self.s1 is not None and "s1" in sd:
+            self.s1.copy_(sd["s1"])
+        if self.s2 is not None and "s2" in sd:
+            self.s2.copy_(sd["s2"])
+        self.step_count = int(sd["step"])
+        self.sel_counts.copy_(sd["sel_counts"])
+        if "v0" in sd and self.gout is not None:
+            self.gout.copy_(sd["v0"])
+        self.sync_params_from_master()
+
+    def sync_params_from_master(self) -> None:
+        """Rewrite the bf16 parameters from the fp32 master (after a checkpoint load)."""
+        fl = self.flat
+        if self.topo == "sharded" and self.group_active:
+            for b in fl.buckets:
+                pout = fl.my_shard(fl.flat_param, b, self.rank)
+                pout.copy_(self.master[b.shard_offset:b.shard_offset + b.shard].to(fl.dtype))
+                dist.all_gather_into_tensor(fl.flat_param[b.offset:b.offset + b.length], pout)
+        elif self.topo == "sharded":
+            fl.flat_param.copy_(self.master.to(fl.dtype))
+        else:
+            fl.flat_param.copy_(self.master.to(fl.dtype))
+
+    def close(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -1,0 +1,144 @@
+"""ConsensusTrainer — the user-facing trainer API (N11).
+
+Mirrors the reference's "trainer returns a named result list" convention: ``runLasso`` returns
+``training.set, testing.set, contrast, train.fit, cv.fit, confusionMatrix, test.error,
+final.model, nonzero.coef, seed`` (`composite_code/rnotebook/cml_targetaml_seanalysis.Rmd:117-121`)
+and ``runSVM`` ``options_string, svm_model, weightsvect, predictions_*, performance_test, ...``
+(`...seanalysis.Rmd:189-207`). ``fit`` / ``evaluate`` here return dicts with the same spirit
+(snake_case keys): ``final_model, history, confusion_matrix, test_error, tpr, tnr, fdr, for,
+selection_counts, seed, options_string``.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import torch
+
+from ..config import TrainConfig
+from ..models import Task, build_task
+from ..parallel.dist import DistInfo, init_distributed
+from ..parallel.engine import ConsensusEngine
+from ..utils.logging import JsonlLogger, PhaseTimer
+from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
+
+
+class ConsensusTrainer:
+    def __init__(self, cfg: TrainConfig, task: Optional[Task] = None,
+                 info: Optional[DistInfo] = None):
+        self.cfg = cfg
+        self.info = info or init_distributed(cfg.backend)
+        dev = self.info.device
+        dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[cfg.dtype]
+        self.task = task or build_task(cfg.model, dev, dtype, seed=cfg.seed)
+        self.engine = ConsensusEngine(self.task.model, cfg, self.info)
+        # one data stream per (global) worker id, so a run with R ranks x V virtual workers sees
+        # the same batches as a run with 1 rank x R*V virtual workers
+        V = self.engine.V
+        self.gens = []
+        for v in range(V):
+            g = torch.Generator(device=dev)
+            g.manual_seed(cfg.seed * 1000 + self.info.rank * V + v)
+            self.gens.append(g)
+        self.gen = self.gens[0]
+        self.logger = JsonlLogger(cfg.log_path, self.info.rank)
+        self.timer = PhaseTimer(dev, enabled=cfg.profile)
+        self.history: List[float] = []
+
+    @property
+    def model(self) -> torch.nn.Module:
+        return self.engine.model
+
+    # ------------------------------------------------------------------ training
+    def train_step(self) -> torch.Tensor:
+        """One consensus step; returns the mean local loss as a device tensor (no host sync)."""
+        e, t = self.engine, self.timer
+        self.model.train()
+        e.zero_grad()
+        total = None
+        for v in range(e.V):
+            e.bind_worker(v)
+            with t.phase("data"):
+                batch = self.task.make_batch(self.cfg.batch_per_worker, self.gens[v])
+            with t.phase("fwd_bwd"):
+                loss = self.task.loss_fn(self.model, batch)
+                loss.backward()
+            total = loss.detach() if total is None else total + loss.detach()
+        with t.phase("exchange_aggregate_update"):
+            e.step()
+        return total / e.V
+
+    def fit(self, steps: Optional[int] = None, log_every: int = 10,
+            resume: bool = False) -> Dict[str, object]:
+        steps = steps if steps is not None else self.cfg.steps
+        if resume and self.cfg.ckpt_dir and latest_checkpoint(self.cfg.ckpt_dir):
+            load_checkpoint(self.cfg.ckpt_dir, self.engine, self.gens)
+        start = self.engine.step_count
+        t0 = time.perf_counter()
+        losses = []
+        for s in range(start, steps):
+            loss = self.train_step()
+            losses.append(loss)
+            if log_every and (s + 1) % log_every == 0:
+                lv = float(loss)
+                self.logger.log(step=s + 1, loss=lv, phases=self.timer.summary())
+            if self.cfg.ckpt_every and self.cfg.ckpt_dir and (s + 1) % self.cfg.ckpt_every == 0:
+                save_checkpoint(self.cfg.ckpt_dir, self.engine, self.cfg, gens=self.gens)
+        if self.info.device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        hist = [float(l) for l in losses]
+        self.history.extend(hist)
+        n_done = max(steps - start, 0)
+        samples = n_done * self.cfg.batch_per_worker * self.engine.n
+        return {
+            "final_model": self.model,
+            "history": hist,
+            "steps": steps,
+            "seed": self.cfg.seed,
+            "selection_counts": self.engine.sel_counts.cpu().tolist(),
+            "last_weights": self.engine.w[: self.engine.n].cpu().tolist(),
+            "options_string": f"rule={self.cfg.agg.rule} topology={self.cfg.topology.kind} "
+                              f"n={self.engine.n} f={self.cfg.agg.f} optim={self.cfg.optim.name}",
+            "samples_per_sec": samples / dt if dt > 0 else float("nan"),
+            "wall_s": dt,
+        }
+
+    # ------------------------------------------------------------------ evaluation
+    @torch.no_grad()
+    def evaluate(self, batches: int = 4, batch_size: Optional[int] = None) -> Dict[str, object]:
+        """Loss / accuracy / confusion-derived metrics on fresh synthetic batches."""
+        from ..select.metrics import binary_metrics, confusion_matrix
+        self.model.eval()
+        gen = torch.Generator(device=self.info.device)
+        gen.manual_seed(self.cfg.seed + 99991)
+        bs = batch_size or self.cfg.batch_per_worker
+        ys, ps, losses = [], [], []
+        for _ in range(batches):
+            x, y = self.task.make_batch(bs, gen)
+            out = self.model(x).float()
+            losses.append(torch.nn.functional.cross_entropy(out.view(-1, out.shape[-1]),
+                                                            y.view(-1)).item())
+            ps.append(out.argmax(-1).view(-1))
+            ys.append(y.view(-1))
+        y = torch.cat(ys).cpu()
+        p = torch.cat(ps).cpu()
+        res: Dict[str, object] = {"loss": sum(losses) / len(losses),
+                                  "accuracy": float((p == y).float().mean()),
+                                  "test_error": float((p != y).float().mean())}
+        if int(max(y.max(), p.max())) <= 1:
+            res["confusion_matrix"] = confusion_matrix(y, p, 2).tolist()
+            res.update(binary_metrics(y, p))
+        self.model.train()
+        return res
+
+    # ------------------------------------------------------------------ checkpoint
+    def save(self, root: Optional[str] = None) -> str:
+        return save_checkpoint(root or self.cfg.ckpt_dir, self.engine, self.cfg, gens=self.gens)
+
+    def load(self, path: str) -> dict:
+        return load_checkpoint(path, self.engine, self.gens)
+
+    def close(self) -> None:
+        self.logger.close()
+        self.engine.close()

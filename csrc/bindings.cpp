@@ -1,0 +1,183 @@
+// PyTorch bindings of the consensus kernels (_C extension). Argument checking lives here so the
+// kernels stay torch-free; every launch goes on the caller's current HIP stream and none of them
+// synchronises, so the whole aggregation step can be captured in a hipGraph.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "kernels/kernels.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+#define CML_CHECK_HIP(expr)                                                               \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    TORCH_CHECK(_e == hipSuccess, "consensusml_amd HIP error: ", hipGetErrorString(_e)); \
+  } while (0)
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dtype_of(const Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return cml::DT_BF16;
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "expected bf16 or fp32 tensor, got ", t.scalar_type());
+  return cml::DT_F32;
+}
+
+void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+
+template <typename T = void>
+T* opt_ptr(const optional<Tensor>& t, at::ScalarType st, const char* name, int64_t min_numel) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_dev(*t, name);
+  TORCH_CHECK(t->scalar_type() == st, name, " has dtype ", t->scalar_type(), ", expected ", st);
+  TORCH_CHECK(t->is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t->numel() >= min_numel, name, " too small: ", t->numel(), " < ", min_numel);
+  return reinterpret_cast<T*>(t->data_ptr());
+}
+
+// X: [R, C] rows of workers (row stride arbitrary, unit column stride). The aggregation uses n
+// rows (rows[i] indexes X when given) and the first D columns.
+void agg_update(const Tensor& X, int64_t n, int64_t D, const optional<Tensor>& rows, int64_t combine,
+                int64_t lo, int64_t cnt, const optional<Tensor>& w, int64_t opt,
+                const optional<Tensor>& master, const optional<Tensor>& s1,
+                const optional<Tensor>& s2, const optional<Tensor>& param_out,
+                const optional<Tensor>& gout, double lr, double momentum, double weight_decay,
+                double beta1, double beta2, double eps, double step_size, double inv_sqrt_bc2,
+                double gscale, bool nesterov, bool first) {
+  check_dev(X, "X");
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "X must be 2-D with unit column stride");
+  TORCH_CHECK(n >= 1 && n <= 64, "1 <= n <= 64 workers supported, got ", n);
+  TORCH_CHECK(D >= 0 && D <= X.size(1), "D out of range");
+  const c10::DeviceGuard guard(X.device());
+  cml::SrcArgs s{};
+  s.X = X.data_ptr();
+  s.ld = X.stride(0);
+  s.n = static_cast<int>(n);
+  s.rows = opt_ptr<const int>(rows, at::kInt, "rows", n);
+  if (!s.rows) TORCH_CHECK(X.size(0) >= n, "X has fewer rows than n");
+  s.w = opt_ptr<const float>(w, at::kFloat, "w", n);
+  s.lo = static_cast<int>(lo);
+  s.cnt = static_cast<int>(cnt);
+  cml::UpdArgs u{};
+  u.master = opt_ptr<float>(master, at::kFloat, "master", D);
+  u.s1 = opt_ptr<float>(s1, at::kFloat, "s1", D);
+  u.s2 = opt_ptr<float>(s2, at::kFloat, "s2", D);
+  u.param_out = opt_ptr<void>(param_out, at::kBFloat16, "param_out", D);
+  u.gout = opt_ptr<float>(gout, at::kFloat, "gout", D);
+  if (opt != cml::OPT_NONE) TORCH_CHECK(u.master, "optimizer update needs master weights");
+  if (opt == cml::OPT_SGD && momentum != 0.0) TORCH_CHECK(u.s1, "SGD momentum needs s1");
+  if (opt == cml::OPT_ADAM) TORCH_CHECK(u.s1 && u.s2, "Adam needs s1 and s2");
+  if (opt == cml::OPT_NONE) TORCH_CHECK(u.gout, "OPT_NONE needs gout");
+  u.lr = static_cast<float>(lr);
+  u.momentum = static_cast<float>(momentum);
+  u.weight_decay = static_cast<float>(weight_decay);
+  u.beta1 = static_cast<float>(beta1);
+  u.beta2 = static_cast<float>(beta2);
+  u.eps = static_cast<float>(eps);
+  u.step_size = static_cast<float>(step_size);
+  u.inv_sqrt_bc2 = static_cast<float>(inv_sqrt_bc2);
+  u.gscale = static_cast<float>(gscale);
+  u.nesterov = nesterov ? 1 : 0;
+  u.first = first ? 1 : 0;
+  CML_CHECK_HIP(cml::launch_agg_update(dtype_of(X), static_cast<int>(combine), static_cast<int>(opt),
+                                       s, u, D, cur_stream()));
+}
+
+int64_t gram_workspace_bytes(int64_t n, int64_t D) {
+  return static_cast<int64_t>(cml::gram_workspace_bytes(static_cast<int>(n), D));
+}
+
+void gram(const Tensor& X, int64_t n, int64_t D, const optional<Tensor>& rows, Tensor& work,
+          Tensor& G, bool accumulate) {
+  check_dev(X, "X");
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "X must be 2-D with unit column stride");
+  TORCH_CHECK(n >= 1 && n <= 64, "1 <= n <= 64 workers supported");
+  TORCH_CHECK(D >= 1 && D <= X.size(1), "D out of range");
+  const int* r = opt_ptr<const int>(rows, at::kInt, "rows", n);
+  if (!r) TORCH_CHECK(X.size(0) >= n, "X has fewer rows than n");
+  TORCH_CHECK(work.is_cuda() && work.is_contiguous() &&
+                  work.numel() * work.element_size() >= gram_workspace_bytes(n, D),
+              "gram workspace too small");
+  TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kDouble && G.is_contiguous() && G.numel() >= n * n,
+              "G must be a contiguous fp64 [n, n] GPU tensor");
+  const c10::DeviceGuard guard(X.device());
+  CML_CHECK_HIP(cml::launch_gram(dtype_of(X), X.data_ptr(), X.stride(0), static_cast<int>(n), r, D,
+                                 work.data_ptr(), G.data_ptr<double>(), accumulate ? 1 : 0,
+                                 cur_stream()));
+}
+
+void robust_weights(const Tensor& G, int64_t rule, int64_t n, int64_t f, int64_t m, int64_t iters,
+                    double eps, double tol, double tau, Tensor& w, const optional<Tensor>& scores,
+                    const optional<Tensor>& sel) {
+  TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kDouble && G.is_contiguous(), "G: fp64 GPU");
+  const int64_t dim = rule == cml::RULE_CCLIP ? n + 1 : n;
+  TORCH_CHECK(G.numel() >= dim * dim, "G too small");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.numel() >= dim, "w: fp32 GPU [n(+1)]");
+  const c10::DeviceGuard guard(G.device());
+  double* sc = opt_ptr<double>(scores, at::kDouble, "scores", n);
+  int* se = opt_ptr<int>(sel, at::kInt, "sel", n + 1);
+  CML_CHECK_HIP(cml::launch_robust_weights(static_cast<int>(rule), G.data_ptr<double>(),
+                                           static_cast<int>(n), static_cast<int>(f),
+                                           static_cast<int>(m), static_cast<int>(iters), eps, tol,
+                                           tau, w.data_ptr<float>(), sc, se, cur_stream()));
+}
+
+int64_t gossip_workspace_bytes(int64_t D) {
+  return static_cast<int64_t>(cml::gossip_workspace_bytes(D));
+}
+
+void gossip_mix(Tensor& master, const optional<Tensor>& param_out, const Tensor& left,
+                const Tensor& right, double w0, double w1, double w2, double clip, Tensor& work) {
+  check_dev(master, "master");
+  TORCH_CHECK(master.scalar_type() == at::kFloat && master.is_contiguous(), "master: fp32 contiguous");
+  const int64_t D = master.numel();
+  TORCH_CHECK(left.scalar_type() == at::kBFloat16 && right.scalar_type() == at::kBFloat16 &&
+                  left.is_contiguous() && right.is_contiguous() && left.numel() >= D &&
+                  right.numel() >= D,
+              "neighbours: contiguous bf16 of master's size");
+  TORCH_CHECK(work.numel() * work.element_size() >= gossip_workspace_bytes(D), "gossip workspace too small");
+  void* p = opt_ptr<void>(param_out, at::kBFloat16, "param_out", D);
+  const c10::DeviceGuard guard(master.device());
+  CML_CHECK_HIP(cml::launch_gossip_mix(master.data_ptr<float>(), p, left.data_ptr(), right.data_ptr(),
+                                       D, static_cast<float>(w0), static_cast<float>(w1),
+                                       static_cast<float>(w2), static_cast<float>(clip),
+                                       work.data_ptr(), cur_stream()));
+}
+
+void fault(Tensor& g, int64_t kind, double scale, double sigma, int64_t seed) {
+  check_dev(g, "g");
+  TORCH_CHECK(g.is_contiguous(), "g must be contiguous");
+  const c10::DeviceGuard guard(g.device());
+  CML_CHECK_HIP(cml::launch_fault(dtype_of(g), g.data_ptr(), g.numel(), static_cast<int>(kind),
+                                  static_cast<float>(scale), static_cast<float>(sigma),
+                                  static_cast<uint64_t>(seed), cur_stream()));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "consensusml_amd native HIP kernels for gfx950 (MI355X)";
+  m.def("agg_update", &agg_update, "fused robust aggregation + optimizer update");
+  m.def("gram_workspace_bytes", &gram_workspace_bytes);
+  m.def("gram", &gram, "G = X X^T (fp64) on MFMA");
+  m.def("robust_weights", &robust_weights, "robust weights from a Gram matrix");
+  m.def("gossip_workspace_bytes", &gossip_workspace_bytes);
+  m.def("gossip_mix", &gossip_mix, "ring gossip mixing with neighbour clipping");
+  m.def("fault", &fault, "Byzantine fault injection");
+  m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
+  m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);
+  m.attr("OPT_NONE") = static_cast<int>(cml::OPT_NONE);
+  m.attr("OPT_SGD") = static_cast<int>(cml::OPT_SGD);
+  m.attr("OPT_ADAM") = static_cast<int>(cml::OPT_ADAM);
+  m.attr("RULE_MEAN") = static_cast<int>(cml::RULE_MEAN);
+  m.attr("RULE_KRUM") = static_cast<int>(cml::RULE_KRUM);
+  m.attr("RULE_MULTI_KRUM") = static_cast<int>(cml::RULE_MULTI_KRUM);
+  m.attr("RULE_GEOMED") = static_cast<int>(cml::RULE_GEOMED);
+  m.attr("RULE_CCLIP") = static_cast<int>(cml::RULE_CCLIP);
+  m.attr("RULE_BULYAN_SELECT") = static_cast<int>(cml::RULE_BULYAN_SELECT);
+}

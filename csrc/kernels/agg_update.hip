@@ -1,0 +1,274 @@
+// Fused robust aggregation + optimizer update (N04/N05/N08 of SURVEY.md §2.4).
+//
+// One pass over the n worker vectors of a coordinate shard: per coordinate either
+//   * SORTED   : a compile-time Batcher network over NP >= n values held in VGPRs (padding rows
+//                are +inf), then the mean of sorted ranks [lo, lo+cnt) -> median / trimmed mean
+//                / Bulyan's coordinate phase, or
+//   * WEIGHTED : sum_i w_i x_i over the non-zero weights only (Krum, Multi-Krum, Weiszfeld,
+//                centered clipping, plain mean) — zero-weight rows are never read,
+// and then SGD(momentum, nesterov, wd) or Adam/AdamW on the fp32 master, rewriting the bf16
+// parameters in the same pass. The aggregated gradient never round-trips through HBM.
+//
+// Memory-bound streaming kernel: 16 B per lane per worker row (8 bf16 / 4 f32), grid-stride,
+// <= 2048 workgroups of 256 threads. Row addresses are hoisted out of the loop; padded rows load
+// a clamped (valid) row and are replaced by +inf with a select, so no per-row branch sits
+// between the loads (hipcc would otherwise wait vmcnt(0) per row).
+#include "common.h"
+#include "kernels.h"
+
+namespace cml {
+
+constexpr int kBlock = 256;
+constexpr int kMaxRows = 64;
+
+template <int VEC>
+__device__ __forceinline__ void update_and_store(const UpdArgs& u, int opt, int64_t e,
+                                                 float (&g)[VEC]) {
+  if (u.gscale != 1.0f) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) g[v] *= u.gscale;
+  }
+  if (u.gout) store_f32<VEC>(u.gout + e, g);
+  if (opt == OPT_NONE) return;
+  float p[VEC];
+  load_vec<float, VEC>(u.master + e, p);
+  if (opt == OPT_SGD) {
+    if (u.weight_decay != 0.0f) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) g[v] = fmaf(u.weight_decay, p[v], g[v]);
+    }
+    if (u.momentum != 0.0f) {
+      float b[VEC];
+      if (u.first) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) b[v] = g[v];
+      } else {
+        load_vec<float, VEC>(u.s1 + e, b);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) b[v] = fmaf(u.momentum, b[v], g[v]);
+      }
+      store_f32<VEC>(u.s1 + e, b);
+      if (u.nesterov) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) g[v] = fmaf(u.momentum, b[v], g[v]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) g[v] = b[v];
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) p[v] = fmaf(-u.lr, g[v], p[v]);
+  } else {  // OPT_ADAM (decoupled weight decay when weight_decay != 0)
+    float m[VEC], s[VEC];
+    load_vec<float, VEC>(u.s1 + e, m);
+    load_vec<float, VEC>(u.s2 + e, s);
+    const float decay = 1.0f - u.lr * u.weight_decay;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      m[v] = fmaf(u.beta1, m[v], (1.0f - u.beta1) * g[v]);
+      s[v] = fmaf(u.beta2, s[v], (1.0f - u.beta2) * g[v] * g[v]);
+      const float denom = fmaf(sqrtf(s[v]), u.inv_sqrt_bc2, u.eps);
+      p[v] = fmaf(-u.step_size, m[v] / denom, p[v] * decay);
+    }
+    store_f32<VEC>(u.s1 + e, m);
+    store_f32<VEC>(u.s2 + e, s);
+  }
+  store_f32<VEC>(u.master + e, p);
+  if (u.param_out) store_bf16<VEC>(reinterpret_cast<bf16*>(u.param_out) + e, p);
+}
+
+// ----------------------------------------------------------------------------- sorted combine
+template <typename T, int NP, int VEC, int OPT>
+__global__ __launch_bounds__(kBlock) void agg_sorted_kernel(SrcArgs s, UpdArgs u, int64_t base,
+                                                            int64_t nvec) {
+  const T* X = reinterpret_cast<const T*>(s.X);
+  int64_t roff[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int r = i < s.n ? i : s.n - 1;
+    roff[i] = static_cast<int64_t>(s.rows ? s.rows[r] : r) * s.ld + base;
+  }
+  const float inf = __builtin_inff();
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < nvec; t += stride) {
+    const int64_t e = t * VEC;
+    float a[NP][VEC];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) load_vec<T, VEC>(X + roff[i] + e, a[i]);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const bool pad = i >= s.n;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) a[i][v] = (pad || a[i][v] != a[i][v]) ? inf : a[i][v];
+    }
+    sort_columns<NP, VEC>(a);
+    float g[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) g[v] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const bool take = (i >= s.lo) && (i < s.lo + s.cnt);
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) g[v] += take ? a[i][v] : 0.0f;
+    }
+    const float inv = 1.0f / static_cast<float>(s.cnt);
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) g[v] *= inv;
+    update_and_store<VEC>(u, OPT, base + e, g);
+  }
+}
+
+// ----------------------------------------------------------------------------- weighted combine
+template <typename T, int VEC, int OPT>
+__global__ __launch_bounds__(kBlock) void agg_weighted_kernel(SrcArgs s, UpdArgs u, int64_t base,
+                                                              int64_t nvec) {
+  // Compact the non-zero weights once per workgroup (LDS, broadcast reads in the loop).
+  __shared__ int64_t s_off[kMaxRows];
+  __shared__ float s_w[kMaxRows];
+  __shared__ int s_nz;
+  if (threadIdx.x == 0) {
+    int nz = 0;
+    for (int i = 0; i < s.n; ++i) {
+      const float wi = s.w ? s.w[i] : 1.0f;
+      if (wi != 0.0f) {
+        s_off[nz] = static_cast<int64_t>(s.rows ? s.rows[i] : i) * s.ld + base;
+        s_w[nz] = wi;
+        ++nz;
+      }
+    }
+    s_nz = nz;
+  }
+  __syncthreads();
+  const int nz = s_nz;
+  const T* X = reinterpret_cast<const T*>(s.X);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < nvec; t += stride) {
+    const int64_t e = t * VEC;
+    float g[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) g[v] = 0.0f;
+    int i = 0;
+    for (; i + 4 <= nz; i += 4) {  // four rows in flight before the FMAs
+      float x0[VEC], x1[VEC], x2[VEC], x3[VEC];
+      load_vec<T, VEC>(X + s_off[i] + e, x0);
+      load_vec<T, VEC>(X + s_off[i + 1] + e, x1);
+      load_vec<T, VEC>(X + s_off[i + 2] + e, x2);
+      load_vec<T, VEC>(X + s_off[i + 3] + e, x3);
+      const float w0 = s_w[i], w1 = s_w[i + 1], w2 = s_w[i + 2], w3 = s_w[i + 3];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v)
+        g[v] = fmaf(w3, x3[v], fmaf(w2, x2[v], fmaf(w1, x1[v], fmaf(w0, x0[v], g[v]))));
+    }
+    for (; i < nz; ++i) {
+      float x0[VEC];
+      load_vec<T, VEC>(X + s_off[i] + e, x0);
+      const float w0 = s_w[i];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) g[v] = fmaf(w0, x0[v], g[v]);
+    }
+    update_and_store<VEC>(u, OPT, base + e, g);
+  }
+}
+
+// ----------------------------------------------------------------------------- dispatch
+static inline int grid_for(int64_t nvec) {
+  int64_t b = (nvec + kBlock - 1) / kBlock;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return static_cast<int>(b);
+}
+
+template <typename T, int NP, int VEC>
+static void launch_sorted_np(int opt, const SrcArgs& s, const UpdArgs& u, int64_t base,
+                             int64_t nvec, hipStream_t st) {
+  const int g = grid_for(nvec);
+  switch (opt) {
+    case OPT_NONE: agg_sorted_kernel<T, NP, VEC, OPT_NONE><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+    case OPT_SGD: agg_sorted_kernel<T, NP, VEC, OPT_SGD><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+    default: agg_sorted_kernel<T, NP, VEC, OPT_ADAM><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+  }
+}
+
+// VEC per padded row count: keep NP*VEC <= 128 fp32 VGPRs of values.
+template <typename T, bool VECTOR>
+static void launch_sorted(int opt, const SrcArgs& s, const UpdArgs& u, int64_t base, int64_t nvec_or_n,
+                          hipStream_t st) {
+  // nvec_or_n: number of elements when !VECTOR (VEC = 1), else computed by caller per NP.
+  const int n = s.n;
+  constexpr bool BF = sizeof(T) == 2;
+  if constexpr (VECTOR) {
+    const int64_t D = nvec_or_n;
+    if (n <= 2) launch_sorted_np<T, 2, BF ? 8 : 4>(opt, s, u, base, D / (BF ? 8 : 4), st);
+    else if (n <= 4) launch_sorted_np<T, 4, BF ? 8 : 4>(opt, s, u, base, D / (BF ? 8 : 4), st);
+    else if (n <= 8) launch_sorted_np<T, 8, BF ? 8 : 4>(opt, s, u, base, D / (BF ? 8 : 4), st);
+    else if (n <= 16) launch_sorted_np<T, 16, BF ? 8 : 4>(opt, s, u, base, D / (BF ? 8 : 4), st);
+    else if (n <= 32) launch_sorted_np<T, 32, BF ? 4 : 4>(opt, s, u, base, D / 4, st);
+    else launch_sorted_np<T, 64, 2>(opt, s, u, base, D / 2, st);
+  } else {
+    const int64_t D = nvec_or_n;
+    if (n <= 2) launch_sorted_np<T, 2, 1>(opt, s, u, base, D, st);
+    else if (n <= 4) launch_sorted_np<T, 4, 1>(opt, s, u, base, D, st);
+    else if (n <= 8) launch_sorted_np<T, 8, 1>(opt, s, u, base, D, st);
+    else if (n <= 16) launch_sorted_np<T, 16, 1>(opt, s, u, base, D, st);
+    else if (n <= 32) launch_sorted_np<T, 32, 1>(opt, s, u, base, D, st);
+    else launch_sorted_np<T, 64, 1>(opt, s, u, base, D, st);
+  }
+}
+
+template <typename T, int VEC>
+static void launch_weighted(int opt, const SrcArgs& s, const UpdArgs& u, int64_t base, int64_t nvec,
+                            hipStream_t st) {
+  const int g = grid_for(nvec);
+  switch (opt) {
+    case OPT_NONE: agg_weighted_kernel<T, VEC, OPT_NONE><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+    case OPT_SGD: agg_weighted_kernel<T, VEC, OPT_SGD><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+    default: agg_weighted_kernel<T, VEC, OPT_ADAM><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+  }
+}
+
+static inline bool aligned(const void* p, int bytes) {
+  return p == nullptr || (reinterpret_cast<uintptr_t>(p) % bytes) == 0;
+}
+
+static int sorted_vec(int dtype, int n) {
+  if (n > 32) return 2;
+  if (n > 16) return 4;
+  return dtype == DT_BF16 ? 8 : 4;
+}
+
+template <typename T>
+static hipError_t agg_update_t(int combine, int opt, const SrcArgs& s, const UpdArgs& u, int64_t D,
+                               hipStream_t st) {
+  if (D <= 0) return hipSuccess;
+  const int esz = sizeof(T);
+  const int vec = combine == CMB_WEIGHTED ? (esz == 2 ? 8 : 4) : sorted_vec(esz == 2 ? DT_BF16 : DT_F32, s.n);
+  // The vector path needs every row start and every state pointer aligned to VEC elements.
+  bool ok = (s.ld % vec) == 0 && aligned(s.X, vec * esz) && aligned(u.master, vec * 4) &&
+            aligned(u.s1, vec * 4) && aligned(u.s2, vec * 4) && aligned(u.gout, vec * 4) &&
+            aligned(u.param_out, vec * 2);
+  int64_t Dv = ok ? (D / vec) * vec : 0;
+  if (Dv > 0) {
+    if (combine == CMB_WEIGHTED) {
+      if constexpr (sizeof(T) == 2) launch_weighted<T, 8>(opt, s, u, 0, Dv / 8, st);
+      else launch_weighted<T, 4>(opt, s, u, 0, Dv / 4, st);
+    } else {
+      launch_sorted<T, true>(opt, s, u, 0, Dv, st);
+    }
+  }
+  if (D > Dv) {  // scalar tail (or fully unaligned inputs)
+    if (combine == CMB_WEIGHTED) launch_weighted<T, 1>(opt, s, u, Dv, D - Dv, st);
+    else launch_sorted<T, false>(opt, s, u, Dv, D - Dv, st);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_agg_update(int dtype, int combine, int opt, const SrcArgs& src,
+                             const UpdArgs& upd, int64_t D, hipStream_t stream) {
+  if (src.n < 1 || src.n > kMaxRows) return hipErrorInvalidValue;
+  if (combine == CMB_SORTED && (src.cnt < 1 || src.lo < 0 || src.lo + src.cnt > src.n))
+    return hipErrorInvalidValue;
+  if (dtype == DT_BF16) return agg_update_t<bf16>(combine, opt, src, upd, D, stream);
+  return agg_update_t<float>(combine, opt, src, upd, D, stream);
+}
+
+}  // namespace cml

@@ -1,0 +1,173 @@
+// Shared device helpers for the consensus kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace cml {
+
+constexpr int kWave = 64;
+
+using bf16 = __hip_bfloat16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf2f(uint16_t b) {
+  return __uint_as_float(static_cast<uint32_t>(b) << 16);
+}
+// Round-to-nearest-even f32->bf16; hipcc lowers the cast to v_cvt_pk_bf16_f32 (keeps NaN a NaN).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  bf16 h = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+
+// ---------------------------------------------------------------- vector loads of VEC elements
+// VEC elements of T starting at p -> float out[VEC]. Vector widths: 16 B per lane where possible.
+template <typename T, int VEC>
+__device__ __forceinline__ void load_vec(const T* __restrict__ p, float (&out)[VEC]);
+
+template <>
+__device__ __forceinline__ void load_vec<bf16, 8>(const bf16* __restrict__ p, float (&o)[8]) {
+  uint4 u = *reinterpret_cast<const uint4*>(p);
+  uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(w[i] << 16);
+    o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+template <>
+__device__ __forceinline__ void load_vec<bf16, 4>(const bf16* __restrict__ p, float (&o)[4]) {
+  uint2 u = *reinterpret_cast<const uint2*>(p);
+  o[0] = __uint_as_float(u.x << 16);
+  o[1] = __uint_as_float(u.x & 0xffff0000u);
+  o[2] = __uint_as_float(u.y << 16);
+  o[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+template <>
+__device__ __forceinline__ void load_vec<bf16, 2>(const bf16* __restrict__ p, float (&o)[2]) {
+  uint32_t u = *reinterpret_cast<const uint32_t*>(p);
+  o[0] = __uint_as_float(u << 16);
+  o[1] = __uint_as_float(u & 0xffff0000u);
+}
+template <>
+__device__ __forceinline__ void load_vec<bf16, 1>(const bf16* __restrict__ p, float (&o)[1]) {
+  o[0] = bf2f(*reinterpret_cast<const uint16_t*>(p));
+}
+template <>
+__device__ __forceinline__ void load_vec<float, 8>(const float* __restrict__ p, float (&o)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+template <>
+__device__ __forceinline__ void load_vec<float, 4>(const float* __restrict__ p, float (&o)[4]) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+}
+template <>
+__device__ __forceinline__ void load_vec<float, 2>(const float* __restrict__ p, float (&o)[2]) {
+  float2 a = *reinterpret_cast<const float2*>(p);
+  o[0] = a.x; o[1] = a.y;
+}
+template <>
+__device__ __forceinline__ void load_vec<float, 1>(const float* __restrict__ p, float (&o)[1]) {
+  o[0] = *p;
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_f32(float* __restrict__ p, const float (&v)[VEC]) {
+  if constexpr (VEC % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < VEC; i += 4)
+      *reinterpret_cast<float4*>(p + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) p[i] = v[i];
+  }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_bf16(bf16* __restrict__ p, const float (&v)[VEC]) {
+  if constexpr (VEC == 8) {
+    uint4 u;
+    u.x = f2bf(v[0]) | (uint32_t(f2bf(v[1])) << 16);
+    u.y = f2bf(v[2]) | (uint32_t(f2bf(v[3])) << 16);
+    u.z = f2bf(v[4]) | (uint32_t(f2bf(v[5])) << 16);
+    u.w = f2bf(v[6]) | (uint32_t(f2bf(v[7])) << 16);
+    *reinterpret_cast<uint4*>(p) = u;
+  } else if constexpr (VEC == 4) {
+    uint2 u;
+    u.x = f2bf(v[0]) | (uint32_t(f2bf(v[1])) << 16);
+    u.y = f2bf(v[2]) | (uint32_t(f2bf(v[3])) << 16);
+    *reinterpret_cast<uint2*>(p) = u;
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<uint32_t*>(p) = f2bf(v[0]) | (uint32_t(f2bf(v[1])) << 16);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) reinterpret_cast<uint16_t*>(p)[i] = f2bf(v[i]);
+  }
+}
+
+// ---------------------------------------------------------------- Batcher odd-even merge sort
+// Compile-time network over a[NP][VEC] (sorts every column independently, ascending).
+// NP is a power of two; all indices fold to constants, so a[][] stays in VGPRs.
+template <int VEC>
+__device__ __forceinline__ void cswap(float (&x)[VEC], float (&y)[VEC]) {
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    float lo = fminf(x[v], y[v]);
+    float hi = fmaxf(x[v], y[v]);
+    x[v] = lo;
+    y[v] = hi;
+  }
+}
+
+template <int NP, int VEC, int LO, int HI, int R>
+struct OEMerge {
+  static __device__ __forceinline__ void run(float (&a)[NP][VEC]) {
+    constexpr int STEP = R * 2;
+    if constexpr (STEP < HI - LO) {
+      OEMerge<NP, VEC, LO, HI, STEP>::run(a);
+      OEMerge<NP, VEC, LO + R, HI, STEP>::run(a);
+#pragma unroll
+      for (int i = LO + R; i < HI - R; i += STEP) cswap<VEC>(a[i], a[i + R]);
+    } else {
+      cswap<VEC>(a[LO], a[LO + R]);
+    }
+  }
+};
+
+template <int NP, int VEC, int LO, int HI>
+struct OESort {
+  static __device__ __forceinline__ void run(float (&a)[NP][VEC]) {
+    if constexpr (HI - LO >= 1) {
+      constexpr int MID = LO + (HI - LO) / 2;
+      OESort<NP, VEC, LO, MID>::run(a);
+      OESort<NP, VEC, MID + 1, HI>::run(a);
+      OEMerge<NP, VEC, LO, HI, 1>::run(a);
+    }
+  }
+};
+
+template <int NP, int VEC>
+__device__ __forceinline__ void sort_columns(float (&a)[NP][VEC]) {
+  OESort<NP, VEC, 0, NP - 1>::run(a);
+}
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+}  // namespace cml

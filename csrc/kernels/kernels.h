@@ -1,0 +1,75 @@
+// Host-side launch API of the consensus kernels (no torch headers: included by bindings.cpp and
+// by every .hip translation unit). All launches are asynchronous on the given stream and never
+// allocate, synchronise or copy to the host, so callers may capture them in a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cml {
+
+enum DType : int { DT_BF16 = 0, DT_F32 = 1 };
+enum Combine : int { CMB_SORTED = 0, CMB_WEIGHTED = 1 };
+enum Opt : int { OPT_NONE = 0, OPT_SGD = 1, OPT_ADAM = 2 };
+enum Rule : int {
+  RULE_MEAN = 0,
+  RULE_KRUM = 1,
+  RULE_MULTI_KRUM = 2,
+  RULE_GEOMED = 3,
+  RULE_CCLIP = 4,
+  RULE_BULYAN_SELECT = 5,
+};
+
+// Worker rows of a [n, ld] matrix: row i of the aggregation is X + rows[i]*ld (rows == nullptr:
+// identity). Sorted combine averages sorted ranks [lo, lo+cnt); weighted combine computes
+// sum_i w[i] x_i (w == nullptr: all ones), skipping zero-weight rows.
+struct SrcArgs {
+  const void* X;
+  int64_t ld;
+  int n;
+  const int* rows;
+  const float* w;
+  int lo, cnt;
+};
+
+// Optimizer state is fp32 and indexed like the aggregate. Any pointer may be null when unused.
+struct UpdArgs {
+  float* master;     // fp32 master weights (SGD/Adam)
+  float* s1;         // momentum (SGD) or exp_avg (Adam)
+  float* s2;         // exp_avg_sq (Adam)
+  void* param_out;   // bf16 model parameters rewritten from the master
+  float* gout;       // aggregated gradient (fp32), optional
+  float lr, momentum, weight_decay, beta1, beta2, eps, step_size, inv_sqrt_bc2, gscale;
+  int nesterov, first;
+};
+
+// Aggregate n worker vectors of length D and apply the optimizer in the same pass.
+// Returns hipSuccess or the launch error.
+hipError_t launch_agg_update(int dtype, int combine, int opt, const SrcArgs& src,
+                             const UpdArgs& upd, int64_t D, hipStream_t stream);
+
+// Gram matrix G = X X^T (fp64, [n, n], row-major) of n <= 64 worker rows. ``work`` must hold
+// gram_workspace_bytes(n, D) bytes. accumulate != 0: G += X X^T (bucket-by-bucket Gram).
+size_t gram_workspace_bytes(int n, int64_t D);
+hipError_t launch_gram(int dtype, const void* X, int64_t ld, int n, const int* rows, int64_t D,
+                       void* work, double* G, int accumulate, hipStream_t stream);
+
+// Robust weights from a Gram matrix (single workgroup). Outputs:
+//   w[n_out] fp32 (n_out = n, or n+1 for centered clipping whose last row is the previous
+//   aggregate), scores[n] fp64 (Krum scores / final distances), sel[n+1] int32
+//   (Bulyan: sorted selected indices then sel[n] = count; others: sel[i] = 1 if w_i > 0).
+hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m, int iters,
+                                 double eps, double tol, double tau, float* w, double* scores,
+                                 int* sel, hipStream_t stream);
+
+// Gossip: x <- (w0+w1+w2) x + w1*clip(left-x) + w2*clip(right-x); writes fp32 master and bf16
+// params. clip <= 0 disables clipping. ``work`` must hold gossip_workspace_bytes(D) bytes.
+size_t gossip_workspace_bytes(int64_t D);
+hipError_t launch_gossip_mix(float* master, void* param_out, const void* left, const void* right,
+                             int64_t D, float w0, float w1, float w2, float clip, void* work,
+                             hipStream_t stream);
+
+// Elementwise fault injection on a local gradient (Byzantine simulation, N10).
+hipError_t launch_fault(int dtype, void* g, int64_t D, int kind, float scale, float sigma,
+                        uint64_t seed, hipStream_t stream);
+
+}  // namespace cml

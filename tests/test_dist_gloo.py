@@ -1,0 +1,123 @@
+"""Multi-process tests on gloo, world_size 2 and 3 (BASELINE config 1: 2-layer MLP, coordinate-wise
+median) — the "multi-node without a cluster" fixture of SURVEY.md §4.4 item 3.
+
+A run with R ranks x 1 worker must produce bit-for-bit (fp32) the same parameters as 1 rank x R
+virtual workers fed the same per-worker data: that pins the all-to-all / all-gather / all-reduce
+plumbing, the shard layout and the Gram all-reduce to the single-process semantics.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from consensusml_amd import TrainConfig
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg(rule, topo, V, f, steps, fault="none", byz=()):
+    cfg = TrainConfig()
+    cfg.dtype = "fp32"
+    cfg.virtual_workers = V
+    cfg.agg.rule = rule
+    cfg.agg.f = f
+    cfg.topology.kind = topo
+    cfg.topology.bucket_mb = 0.002      # several buckets even for the tiny MLP
+    cfg.optim.lr = 0.1
+    cfg.batch_per_worker = 16
+    cfg.model.extra = {"classes": 2}
+    cfg.fault.kind = fault
+    cfg.fault.ranks = list(byz)
+    cfg.backend = "gloo"
+    cfg.steps = steps
+    return cfg
+
+
+def _worker(rank, world, port, rule, topo, f, steps, out_dir, fault, byz, ckpt):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from consensusml_amd.parallel import dist as D
+    from consensusml_amd.trainer.trainer import ConsensusTrainer
+    D._INFO = None
+    info = D.init_distributed("gloo")
+    cfg = _cfg(rule, topo, 1, f, steps, fault, byz)
+    if ckpt:
+        cfg.ckpt_dir = os.path.join(out_dir, "ckpt")
+    tr = ConsensusTrainer(cfg, info=info)
+    if ckpt:
+        tr.fit(steps // 2, log_every=0)
+        tr.save()
+        tr2 = ConsensusTrainer(cfg, info=info)
+        tr2.load(cfg.ckpt_dir)
+        tr2.fit(steps, log_every=0)
+        tr = tr2
+    else:
+        tr.fit(steps, log_every=0)
+    params = [p.detach().clone() for p in tr.model.parameters()]
+    torch.save({"params": params, "sel": tr.engine.sel_counts.clone()},
+               os.path.join(out_dir, f"r{rank}.pt"))
+    D.monitored_barrier(30)
+    dist.destroy_process_group()
+
+
+def _run_world(world, rule, topo, f, steps, tmp, fault="none", byz=(), ckpt=False):
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, rule, topo, f, steps, str(tmp), fault, list(byz), ckpt),
+             nprocs=world, join=True)
+    return [torch.load(os.path.join(tmp, f"r{r}.pt"), weights_only=True) for r in range(world)]
+
+
+def _single(world, rule, topo, f, steps, fault="none", byz=()):
+    from consensusml_amd.parallel.dist import DistInfo
+    from consensusml_amd.trainer.trainer import ConsensusTrainer
+    cfg = _cfg(rule, topo, world, f, steps, fault, byz)
+    tr = ConsensusTrainer(cfg, info=DistInfo(0, 1, 0, torch.device("cpu"), "none"))
+    tr.fit(steps, log_every=0)
+    return [p.detach().clone() for p in tr.model.parameters()]
+
+
+@pytest.mark.parametrize("topo,rule,world,f", [
+    ("sharded", "median", 2, 0),          # BASELINE config 1
+    ("allgather", "median", 2, 0),
+    ("allreduce", "mean", 2, 0),
+    ("sharded", "krum", 3, 0),
+    ("sharded", "geomed", 3, 0),
+    ("allgather", "multi_krum", 3, 1),
+    ("sharded", "trimmed_mean", 3, 1),
+])
+def test_distributed_equals_virtual(tmp_path, topo, rule, world, f):
+    res = _run_world(world, rule, topo, f, 6, tmp_path)
+    single = _single(world, rule, topo, f, 6)
+    for r in range(world):
+        for a, b in zip(res[r]["params"], single):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_byzantine_rank_excluded_gloo(tmp_path):
+    res = _run_world(3, "krum", "sharded", 0, 8, tmp_path, fault="sign_flip", byz=[1])
+    assert res[0]["sel"][1].item() == 0
+    for a, b in zip(res[0]["params"], res[2]["params"]):
+        torch.testing.assert_close(a, b)
+
+
+def test_gossip_ring_runs(tmp_path):
+    res = _run_world(3, "mean", "gossip", 0, 6, tmp_path)
+    for r in range(3):
+        assert all(torch.isfinite(p).all() for p in res[r]["params"])
+
+
+def test_checkpoint_resume_gloo(tmp_path):
+    """save at step 3, reload into a fresh trainer, continue to 6 == uninterrupted 6 steps."""
+    res = _run_world(2, "median", "sharded", 0, 6, tmp_path, ckpt=True)
+    single = _single(2, "median", "sharded", 0, 6)
+    for a, b in zip(res[0]["params"], single):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)

@@ -1,0 +1,146 @@
+"""Engine tests on CPU with virtual workers (single process) — SURVEY.md §4.4 items 4-5."""
+import copy
+
+import pytest
+import torch
+
+from consensusml_amd import TrainConfig
+from consensusml_amd.parallel.dist import DistInfo
+from consensusml_amd.trainer.trainer import ConsensusTrainer
+
+CPU = DistInfo(0, 1, 0, torch.device("cpu"), "none")
+
+
+def make_cfg(rule="median", topo="sharded", V=5, f=1, fault="none", byz=(), steps=20, opt="sgd"):
+    cfg = TrainConfig()
+    cfg.dtype = "fp32"
+    cfg.virtual_workers = V
+    cfg.agg.rule = rule
+    cfg.agg.f = f
+    cfg.topology.kind = topo
+    cfg.optim.name = opt
+    cfg.optim.lr = 0.1 if opt == "sgd" else 0.01
+    cfg.batch_per_worker = 32
+    cfg.steps = steps
+    cfg.model.extra = {"classes": 2}
+    cfg.fault.kind = fault
+    cfg.fault.ranks = list(byz)
+    return cfg
+
+
+@pytest.mark.parametrize("topo", ["sharded", "allgather"])
+@pytest.mark.parametrize("rule", ["median", "trimmed_mean", "krum", "multi_krum", "geomed",
+                                  "bulyan"])
+def test_robust_rules_survive_sign_flip(topo, rule):
+    V = 7
+    cfg = make_cfg(rule, topo, V=V, f=1, fault="sign_flip", byz=[3])
+    tr = ConsensusTrainer(cfg, info=CPU)
+    r = tr.fit(30, log_every=0)
+    ev = tr.evaluate()
+    assert r["history"][-1] < 0.4, r["history"][-5:]
+    assert ev["accuracy"] > 0.85
+    if rule in ("krum", "multi_krum"):
+        assert r["selection_counts"][3] == 0
+
+
+def test_mean_breaks_under_sign_flip():
+    cfg = make_cfg("mean", "sharded", V=7, f=0, fault="sign_flip", byz=[3])
+    tr = ConsensusTrainer(cfg, info=CPU)
+    r = tr.fit(30, log_every=0)
+    assert r["history"][-1] > 1.0
+
+
+@pytest.mark.parametrize("topo", ["allreduce", "allgather", "sharded", "gossip"])
+def test_mean_topologies_agree(topo):
+    """Without faults, every topology with the mean rule is plain data-parallel SGD."""
+    ref = ConsensusTrainer(make_cfg("mean", "allreduce", V=4), info=CPU)
+    ref.fit(5, log_every=0)
+    tr = ConsensusTrainer(make_cfg("mean", topo, V=4), info=CPU)
+    tr.fit(5, log_every=0)
+    for a, b in zip(ref.model.parameters(), tr.model.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_engine_matches_torch_sgd():
+    """mean over V virtual workers == torch.optim.SGD on the averaged gradient."""
+    cfg = make_cfg("mean", "sharded", V=3)
+    cfg.optim.weight_decay = 0.01
+    cfg.optim.nesterov = True
+    tr = ConsensusTrainer(cfg, info=CPU)
+    ref_model = copy.deepcopy(tr.model)
+    opt = torch.optim.SGD(ref_model.parameters(), lr=0.1, momentum=0.9, weight_decay=0.01,
+                          nesterov=True)
+    gens = [torch.Generator().manual_seed(cfg.seed * 1000 + v) for v in range(3)]
+    for _ in range(4):
+        opt.zero_grad()
+        for v in range(3):
+            b = tr.task.make_batch(32, gens[v])
+            (tr.task.loss_fn(ref_model, b) / 3).backward()
+        opt.step()
+        tr.train_step()
+    for a, b in zip(ref_model.parameters(), tr.model.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_adam_engine_matches_torch():
+    cfg = make_cfg("mean", "allgather", V=2, opt="adamw")
+    cfg.optim.weight_decay = 0.05
+    tr = ConsensusTrainer(cfg, info=CPU)
+    ref_model = copy.deepcopy(tr.model)
+    opt = torch.optim.AdamW(ref_model.parameters(), lr=0.01, weight_decay=0.05)
+    gens = [torch.Generator().manual_seed(cfg.seed * 1000 + v) for v in range(2)]
+    for _ in range(3):
+        opt.zero_grad()
+        for v in range(2):
+            b = tr.task.make_batch(32, gens[v])
+            (tr.task.loss_fn(ref_model, b) / 2).backward()
+        opt.step()
+        tr.train_step()
+    for a, b in zip(ref_model.parameters(), tr.model.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("fault", ["gaussian", "scaled", "zero", "nan", "alie", "ipm"])
+def test_fault_kinds_run(fault):
+    cfg = make_cfg("median", "sharded", V=5, f=1, fault=fault, byz=[0])
+    cfg.fault.scale = 5.0
+    tr = ConsensusTrainer(cfg, info=CPU)
+    r = tr.fit(10, log_every=0)
+    assert all(torch.isfinite(torch.tensor(h)) for h in r["history"])
+
+
+def test_centered_clip_and_gossip_clip_run():
+    cfg = make_cfg("centered_clip", "sharded", V=5)
+    cfg.agg.tau = 0.5
+    r = ConsensusTrainer(cfg, info=CPU).fit(10, log_every=0)
+    assert r["history"][-1] < r["history"][0]
+
+
+def test_result_dict_keys():
+    tr = ConsensusTrainer(make_cfg("krum", "sharded", V=5, f=1), info=CPU)
+    r = tr.fit(3, log_every=0)
+    for k in ["final_model", "history", "seed", "selection_counts", "options_string",
+              "samples_per_sec"]:
+        assert k in r
+    ev = tr.evaluate()
+    for k in ["confusion_matrix", "test_error", "tpr", "tnr", "fdr", "for"]:
+        assert k in ev
+
+
+def test_channels_last_resnet_flat_views():
+    cfg = make_cfg("median", "sharded", V=3)
+    cfg.model.name = "resnet_tiny"
+    cfg.model.num_classes = 10
+    cfg.model.image_size = 16
+    cfg.batch_per_worker = 2
+    tr = ConsensusTrainer(cfg, info=CPU)
+    conv = tr.model.conv1.weight
+    assert conv.is_contiguous(memory_format=torch.channels_last)
+    loss = tr.train_step()
+    assert torch.isfinite(loss)
+    assert conv.grad.is_contiguous(memory_format=torch.channels_last)
+    # every parameter lives inside the flat buffer
+    fp = tr.engine.flat.flat_param
+    lo, hi = fp.data_ptr(), fp.data_ptr() + fp.numel() * fp.element_size()
+    for p in tr.model.parameters():
+        assert lo <= p.data_ptr() < hi
