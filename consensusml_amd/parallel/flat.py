@@ -21,6 +21,14 @@ import torch
 ALIGN = 64   # elements; 128 B of bf16 -> every shard / bucket start is cache-line aligned
 
 
+def _native_plan(numels: List[int], world: int, bucket_elems: int):
+    try:
+        from consensusml_amd import _runtime
+    except ImportError:
+        return None
+    return _runtime.plan_buckets(numels, world, ALIGN, bucket_elems)
+
+
 @dataclass
 class Bucket:
     index: int
@@ -65,15 +73,28 @@ class FlatModel:
             shard_off += L // world
             cur, cur_len = [], 0
 
-        for i in order:
-            n = self.params[i].numel()
-            if cur and cur_len + n > bucket_elems:
-                close()
-            self.param_offset[i] = off + cur_len
-            cur.append(i)
-            # keep each parameter 16-byte aligned inside the bucket
-            cur_len += -(-n // 8) * 8
-        close()
+        plan = _native_plan([self.params[i].numel() for i in order], world, bucket_elems)
+        if plan is not None:   # C++ planner (csrc/runtime) — same rule as the loop below
+            for k, i in enumerate(order):
+                self.param_offset[i] = plan.param_offsets[k]
+            members: Dict[int, List[int]] = {}
+            for k, i in enumerate(order):
+                members.setdefault(plan.param_bucket[k], []).append(i)
+            so = 0
+            for bi, (o, L, S) in enumerate(zip(plan.offsets, plan.lengths, plan.shards)):
+                self.buckets.append(Bucket(bi, o, L, S, so, members[bi]))
+                so += S
+            off, shard_off = plan.total, plan.shard_total
+        else:
+            for i in order:
+                n = self.params[i].numel()
+                if cur and cur_len + n > bucket_elems:
+                    close()
+                self.param_offset[i] = off + cur_len
+                cur.append(i)
+                # keep each parameter 16-byte aligned inside the bucket
+                cur_len += -(-n // 8) * 8
+            close()
         self.total = off
         self.shard_total = shard_off
         self.bucket_of = {i: b.index for b in self.buckets for i in b.params}
