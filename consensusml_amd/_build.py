@@ -86,7 +86,7 @@ def build_kernels(force: bool = False, verbose: bool = False) -> str:
     objs.append(bobj)
     if force or _newer(bobj, [bsrc] + hdrs):
         inc = sum((["-I", p] for p in tinc), [])
-        jobs.append([HIPCC, *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+        jobs.append([HIPCC, f"--offload-arch={ARCH}", *common, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                      "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
                      *inc, "-I", py_inc, "-I", CSRC, "-c", bsrc, "-o", bobj])
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:

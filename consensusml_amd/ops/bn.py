@@ -1,0 +1,102 @@
+"""BatchNormAct2d: training BatchNorm + optional residual add + optional ReLU as one op.
+
+GPU bf16 channels_last inputs run the fused HIP kernels of ``csrc/kernels/bn_act.hip``
+(3 activation passes forward, 5 backward, ReLU mask recomputed from x). Anything else (CPU tests,
+fp32, NCHW) runs the equivalent PyTorch composition. Running statistics are kept in fp32 even
+when the module is cast to bf16.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .native import lib
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, rmean, rvar, mean_in, invstd_in, eps, momentum, relu,
+                training):
+        y, mean, invstd = lib().bn_fwd(x, res, gamma, beta, rmean, rvar, mean_in, invstd_in,
+                                       eps, momentum, relu, training)
+        ctx.save_for_backward(x, res, gamma, beta, mean, invstd)
+        ctx.relu = relu
+        ctx.has_res = res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, res, gamma, beta, mean, invstd = ctx.saved_tensors
+        dx, dg, db, dres = lib().bn_bwd(dy, x, res, gamma, beta, mean, invstd, ctx.relu)
+        return (dx, dg, db, dres if ctx.has_res else None, None, None, None, None, None, None,
+                None, None)
+
+
+def _fused_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and gamma.dtype == torch.bfloat16):
+        return False
+    C = x.shape[1]
+    if C % 8 or C > 2048 or 256 % (C // 8):
+        return False
+    return x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+
+
+def bn_act(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
+           running_mean: Optional[torch.Tensor], running_var: Optional[torch.Tensor],
+           residual: Optional[torch.Tensor] = None, relu: bool = True, training: bool = True,
+           momentum: float = 0.1, eps: float = 1e-5) -> torch.Tensor:
+    if _fused_ok(x, gamma) and (residual is None or residual.is_contiguous(
+            memory_format=torch.channels_last)):
+        if training:
+            return _BNActFn.apply(x, gamma, beta, residual, running_mean, running_var, None, None,
+                                  eps, momentum, relu, True)
+        invstd = torch.rsqrt(running_var.float() + eps)
+        return _BNActFn.apply(x, gamma, beta, residual, None, None, running_mean.float(), invstd,
+                              eps, momentum, relu, False)
+    # reference composition (CPU / unsupported layouts)
+    y = F.batch_norm(x, running_mean, running_var, gamma, beta, training, momentum, eps) \
+        if running_mean is None or running_mean.dtype == x.dtype else \
+        _bn_mixed(x, gamma, beta, running_mean, running_var, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+def _bn_mixed(x, gamma, beta, rm, rv, training, momentum, eps):
+    """F.batch_norm with fp32 running stats and lower-precision activations."""
+    xf = x.float()
+    y = F.batch_norm(xf, rm, rv, gamma.float(), beta.float(), training, momentum, eps)
+    return y.to(x.dtype)
+
+
+class BatchNormAct2d(nn.Module):
+    def __init__(self, num_features: int, relu: bool = True, eps: float = 1e-5,
+                 momentum: float = 0.1):
+        super().__init__()
+        self.num_features = num_features
+        self.relu = relu
+        self.eps = eps
+        self.momentum = momentum
+        self.weight = nn.Parameter(torch.ones(num_features))
+        self.bias = nn.Parameter(torch.zeros(num_features))
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+
+    def _apply(self, fn, recurse=True):
+        super()._apply(fn, recurse)
+        # keep running statistics in fp32 whatever dtype the module is cast to
+        for k in ("running_mean", "running_var"):
+            b = self._buffers[k]
+            if b is not None and b.dtype != torch.float32:
+                self._buffers[k] = b.float()
+        return self
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual,
+                      self.relu, self.training, self.momentum, self.eps)
+
+    def extra_repr(self) -> str:
+        return f"{self.num_features}, relu={self.relu}"

@@ -125,6 +125,22 @@ class FlatModel:
             p.grad = self._view(g, i)
         self.grad_row = row
 
+    def grad_views(self, row: int) -> List[torch.Tensor]:
+        """Per-parameter views of gradient row ``row`` (cached) for the copy-on-ready mode."""
+        cache = getattr(self, "_gv", None)
+        if cache is None:
+            cache = self._gv = {}
+        if row not in cache:
+            g = self.flat_grad[row]
+            cache[row] = [self._view(g, i) for i in range(len(self.params))]
+        return cache[row]
+
+    def release_grads(self, row: int) -> None:
+        """Switch to copy-on-ready mode: autograd owns fresh .grad tensors, hooks copy them."""
+        for p in self.params:
+            p.grad = None
+        self.grad_row = row
+
     def zero_grad(self) -> None:
         self.flat_grad.zero_()
 

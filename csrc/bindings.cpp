@@ -149,6 +149,85 @@ void gossip_mix(Tensor& master, const optional<Tensor>& param_out, const Tensor&
                                        work.data_ptr(), cur_stream()));
 }
 
+// x / res / y: NHWC-contiguous bf16 (4-D channels_last or 2-D [M, C]).
+void check_nhwc(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  if (t.dim() == 4) {
+    TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name, " must be channels_last");
+  } else {
+    TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  }
+}
+
+std::vector<Tensor> bn_fwd(const Tensor& x, const optional<Tensor>& res, const Tensor& gamma,
+                           const Tensor& beta, const optional<Tensor>& rmean,
+                           const optional<Tensor>& rvar, const optional<Tensor>& mean_in,
+                           const optional<Tensor>& invstd_in, double eps, double momentum,
+                           bool relu, bool training) {
+  check_nhwc(x, "x");
+  const int64_t C = x.size(1) * (x.dim() == 4 ? 1 : 0) + (x.dim() == 2 ? x.size(1) : 0);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "bn: C must be 8 * (power of 2) <= 2048");
+  if (res.has_value() && res->defined()) {
+    check_nhwc(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "res shape mismatch");
+  }
+  TORCH_CHECK(gamma.scalar_type() == at::kBFloat16 && beta.scalar_type() == at::kBFloat16 &&
+                  gamma.is_contiguous() && beta.is_contiguous() && gamma.numel() == C,
+              "gamma/beta: contiguous bf16 [C]");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor y = at::empty_like(x);
+  Tensor mean, invstd;
+  if (training) {
+    mean = at::empty({C}, f32);
+    invstd = at::empty({C}, f32);
+  } else {
+    TORCH_CHECK(mean_in.has_value() && invstd_in.has_value(), "eval bn needs mean / invstd");
+    mean = mean_in->contiguous();
+    invstd = invstd_in->contiguous();
+  }
+  float* rm = opt_ptr<float>(rmean, at::kFloat, "running_mean", C);
+  float* rv = opt_ptr<float>(rvar, at::kFloat, "running_var", C);
+  Tensor work = at::empty({static_cast<int64_t>(cml::bn_workspace_bytes(M, static_cast<int>(C)) / 4 + 1)}, f32);
+  const void* rp = (res.has_value() && res->defined()) ? res->data_ptr() : nullptr;
+  CML_CHECK_HIP(cml::launch_bn_fwd(x.data_ptr(), rp, y.data_ptr(), M, static_cast<int>(C),
+                                   gamma.data_ptr(), beta.data_ptr(), mean.data_ptr<float>(),
+                                   invstd.data_ptr<float>(), rm, rv, static_cast<float>(eps),
+                                   static_cast<float>(momentum), relu ? 1 : 0, training ? 1 : 0,
+                                   work.data_ptr(), cur_stream()));
+  return {y, mean, invstd};
+}
+
+std::vector<Tensor> bn_bwd(const Tensor& dy_in, const Tensor& x, const optional<Tensor>& res,
+                           const Tensor& gamma, const Tensor& beta, const Tensor& mean,
+                           const Tensor& invstd, bool relu) {
+  check_nhwc(x, "x");
+  Tensor dy = x.dim() == 4 ? dy_in.contiguous(at::MemoryFormat::ChannelsLast) : dy_in.contiguous();
+  check_nhwc(dy, "dy");
+  const int64_t C = x.dim() == 4 ? x.size(1) : x.size(1);
+  const int64_t M = x.numel() / C;
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) check_nhwc(*res, "res");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor dx = at::empty_like(x);
+  Tensor dres = has_res ? at::empty_like(x) : Tensor();
+  Tensor dgamma = at::empty({C}, gamma.options());
+  Tensor dbeta = at::empty({C}, beta.options());
+  Tensor sdz = at::empty({C}, f32), sdzx = at::empty({C}, f32);
+  Tensor work = at::empty({static_cast<int64_t>(cml::bn_workspace_bytes(M, static_cast<int>(C)) / 4 + 1)}, f32);
+  CML_CHECK_HIP(cml::launch_bn_bwd(dy.data_ptr(), x.data_ptr(), has_res ? res->data_ptr() : nullptr,
+                                   dx.data_ptr(), has_res ? dres.data_ptr() : nullptr, M,
+                                   static_cast<int>(C), gamma.data_ptr(), beta.data_ptr(),
+                                   mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                   dgamma.data_ptr(), dbeta.data_ptr(), sdz.data_ptr<float>(),
+                                   sdzx.data_ptr<float>(), relu ? 1 : 0, work.data_ptr(),
+                                   cur_stream()));
+  return {dx, dgamma, dbeta, dres};
+}
+
 void fault(Tensor& g, int64_t kind, double scale, double sigma, int64_t seed) {
   check_dev(g, "g");
   TORCH_CHECK(g.is_contiguous(), "g must be contiguous");
@@ -169,6 +248,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gossip_workspace_bytes", &gossip_workspace_bytes);
   m.def("gossip_mix", &gossip_mix, "ring gossip mixing with neighbour clipping");
   m.def("fault", &fault, "Byzantine fault injection");
+  m.def("bn_fwd", &bn_fwd, "fused NHWC BatchNorm(+res)(+ReLU) forward");
+  m.def("bn_bwd", &bn_bwd, "fused NHWC BatchNorm(+res)(+ReLU) backward");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);
   m.attr("OPT_NONE") = static_cast<int>(cml::OPT_NONE);

@@ -201,14 +201,26 @@ __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restri
 __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ part, int nblk,
                                                          int P, int n, double* __restrict__ G,
                                                          int accumulate) {
-  for (int e = threadIdx.x; e < P * P; e += blockDim.x) {
-    const int row = e / P, col = e % P;
-    if (row >= n || col >= n || (row / 16) > (col / 16)) continue;
-    double s = 0.0;
-    for (int b = 0; b < nblk; ++b) s += static_cast<double>(part[static_cast<int64_t>(b) * P * P + e]);
-    if (accumulate) s += G[row * n + col];
-    G[row * n + col] = s;
-    if ((row / 16) < (col / 16)) G[col * n + row] = s;   // mirror off-diagonal tiles
+  // one workgroup per Gram element: 256 lanes stride the partials, then a fixed-order LDS tree
+  // (deterministic; one launch of P*P small workgroups instead of a serial 1024-deep loop)
+  __shared__ double red[256];
+  const int e = blockIdx.x;
+  const int row = e / P, col = e % P;
+  if (row >= n || col >= n || (row / 16) > (col / 16)) return;
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x)
+    s += static_cast<double>(part[static_cast<int64_t>(b) * P * P + e]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double v = red[0];
+    if (accumulate) v += G[row * n + col];
+    G[row * n + col] = v;
+    if ((row / 16) < (col / 16)) G[col * n + row] = v;   // mirror off-diagonal tiles
   }
 }
 
@@ -226,7 +238,7 @@ void launch_gram_t(const T* X, int64_t ld, int n, const int* rows, int64_t D, fl
                    double* G, int acc, hipStream_t st) {
   const int nb = gram_blocks(D, GramCols<T>::value);
   gram_partial_kernel<T, TT><<<nb, kGBlock, 0, st>>>(X, ld, n, rows, D, part);
-  gram_reduce_kernel<<<1, 256, 0, st>>>(part, nb, 16 * TT, n, G, acc);
+  gram_reduce_kernel<<<(16 * TT) * (16 * TT), 256, 0, st>>>(part, nb, 16 * TT, n, G, acc);
 }
 }  // namespace
 

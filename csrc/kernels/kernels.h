@@ -68,6 +68,21 @@ hipError_t launch_gossip_mix(float* master, void* param_out, const void* left, c
                              int64_t D, float w0, float w1, float w2, float clip, void* work,
                              hipStream_t stream);
 
+// Fused training BatchNorm (+ residual add) (+ ReLU) on NHWC bf16 rows x[M, C] (C % 8 == 0,
+// C <= 2048). Forward with training != 0 computes batch statistics into mean / invstd (fp32 [C])
+// and updates the fp32 running stats (nullable); training == 0 uses the given mean / invstd.
+// Backward recomputes the ReLU mask from x, writes dx (and dres = dz when res != null), dgamma /
+// dbeta (bf16) and the per-channel sums sdz / sdzx (fp32 [C]). ``work``: bn_workspace_bytes.
+size_t bn_workspace_bytes(int64_t M, int C);
+hipError_t launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C,
+                         const void* gamma, const void* beta, float* mean, float* invstd,
+                         float* rmean, float* rvar, float eps, float momentum, int relu,
+                         int training, void* work, hipStream_t stream);
+hipError_t launch_bn_bwd(const void* dy, const void* x, const void* res, void* dx, void* dres,
+                         int64_t M, int C, const void* gamma, const void* beta, const float* mean,
+                         const float* invstd, void* dgamma, void* dbeta, float* sdz, float* sdzx,
+                         int relu, void* work, hipStream_t stream);
+
 // Elementwise fault injection on a local gradient (Byzantine simulation, N10).
 hipError_t launch_fault(int dtype, void* g, int64_t D, int kind, float scale, float sigma,
                         uint64_t seed, hipStream_t stream);

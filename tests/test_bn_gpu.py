@@ -1,0 +1,95 @@
+"""Fused NHWC BatchNorm(+residual)(+ReLU) HIP kernels vs an fp32 PyTorch reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from consensusml_amd.ops.bn import BatchNormAct2d, bn_act
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, g, b, res, relu, rm, rv):
+    y = F.batch_norm(x.float(), rm, rv, g.float(), b.float(), True, 0.1, 1e-5)
+    if res is not None:
+        y = y + res.float()
+    return F.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("C", [8, 64, 256, 2048])
+@pytest.mark.parametrize("mode", ["relu", "res_relu", "plain", "res"])
+def test_bn_act_fwd_bwd(cuda, C, mode):
+    torch.manual_seed(C)
+    N, H, W = 4, 9, 7
+    relu = "relu" in mode
+    use_res = "res" in mode
+    x = (torch.randn(N, C, H, W, device=cuda) * 3 + 1.5).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    res = None
+    if use_res:
+        res = torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16)
+        res = res.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    g = (torch.rand(C, device=cuda) + 0.5).to(torch.bfloat16).requires_grad_(True)
+    b = torch.randn(C, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y = bn_act(x, g, b, rm, rv, res, relu, True)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    # reference in fp32 on the same bf16 inputs
+    xr = x.detach().float().requires_grad_(True)
+    gr = g.detach().float().requires_grad_(True)
+    br = b.detach().float().requires_grad_(True)
+    resr = res.detach().float().requires_grad_(True) if use_res else None
+    rm2, rv2 = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    yr = _ref(xr, gr, br, resr, relu, rm2, rv2)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(g.grad.float(), gr.grad, rtol=3e-2, atol=0.5)
+    torch.testing.assert_close(b.grad.float(), br.grad, rtol=3e-2, atol=0.5)
+    if use_res:
+        torch.testing.assert_close(res.grad.float(), resr.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(rm, rm2, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(rv, rv2, rtol=1e-3, atol=1e-3)
+
+
+def test_bn_large_mean_small_var(cuda):
+    """Shifted sums keep the variance accurate when |mean| >> std."""
+    C = 64
+    x = (torch.randn(2, C, 32, 32, device=cuda) * 0.05 + 40.0).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    m = BatchNormAct2d(C, relu=False).to(cuda).to(torch.bfloat16)
+    y = m(x)
+    yr = F.batch_norm(x.float(), None, None, None, None, True, 0.1, 1e-5)
+    torch.testing.assert_close(y.float(), yr, rtol=5e-2, atol=6e-2)
+
+
+def test_bn_eval_mode(cuda):
+    C = 128
+    m = BatchNormAct2d(C).to(cuda).to(torch.bfloat16)
+    x = torch.randn(3, C, 5, 5, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    for _ in range(3):
+        m(x)
+    m.eval()
+    y = m(x)
+    yr = F.relu(F.batch_norm(x.float(), m.running_mean, m.running_var, m.weight.float(),
+                             m.bias.float(), False, 0.1, 1e-5))
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    assert m.running_mean.dtype == torch.float32
+
+
+def test_resnet_tiny_fused_vs_reference(cuda):
+    """Whole tiny ResNet: fused kernels (bf16 NHWC) vs the same weights through PyTorch fp32."""
+    from consensusml_amd.models.resnet import resnet_tiny
+    torch.manual_seed(0)
+    m = resnet_tiny(10).to(cuda)
+    for mod in m.modules():
+        if isinstance(mod, BatchNormAct2d):
+            mod.weight.data.uniform_(0.5, 1.5)
+    ref = resnet_tiny(10).to(cuda)
+    ref.load_state_dict(m.state_dict())
+    mb = m.to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(8, 3, 32, 32, device=cuda)
+    out = mb(x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)).float()
+    out_ref = ref(x)   # fp32 NCHW -> composition path
+    torch.testing.assert_close(out, out_ref, rtol=0.1, atol=0.15)

@@ -138,7 +138,10 @@ def test_channels_last_resnet_flat_views():
     assert conv.is_contiguous(memory_format=torch.channels_last)
     loss = tr.train_step()
     assert torch.isfinite(loss)
-    assert conv.grad.is_contiguous(memory_format=torch.channels_last)
+    idx = [i for i, p in enumerate(tr.engine.flat.params) if p is conv][0]
+    gview = tr.engine.flat.grad_views(0)[idx]
+    assert gview.is_contiguous(memory_format=torch.channels_last)
+    assert gview.abs().sum() > 0
     # every parameter lives inside the flat buffer
     fp = tr.engine.flat.flat_param
     lo, hi = fp.data_ptr(), fp.data_ptr() + fp.numel() * fp.element_size()
