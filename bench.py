@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", action="store_true", help="(reserved) capture step in a hipGraph")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--miopen-find", action="store_true",
+                    help="torch.backends.cudnn.benchmark (MIOpen find mode) for conv algorithms")
     return ap.parse_args()
 
 
@@ -116,7 +118,7 @@ def main():
     if world_env != args.gpus:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
     info = init_distributed("nccl" if world_env > 1 else "auto")
-    torch.backends.cudnn.benchmark = False
+    torch.backends.cudnn.benchmark = bool(args.miopen_find)
     n = info.world
     main_res = run(args, args.rule, args.topology, args.steps, args.warmup, info)
     ms = main_res["dt"] / args.steps * 1e3
