@@ -46,8 +46,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", action="store_true", help="(reserved) capture step in a hipGraph")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--miopen-find", action="store_true",
-                    help="torch.backends.cudnn.benchmark (MIOpen find mode) for conv algorithms")
+    ap.add_argument("--no-miopen-find", action="store_true",
+                    help="disable MIOpen find mode (torch.backends.cudnn.benchmark) for convs")
     return ap.parse_args()
 
 
@@ -84,9 +84,13 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info):
         eng.step()
         return loss
 
-    for i in range(warmup):
+    tw = time.perf_counter()
+    for i in range(max(warmup, 1 if torch.backends.cudnn.benchmark else 0)):
         step(i)
     torch.cuda.synchronize()
+    if info.rank == 0:
+        print(f"[bench] {rule}/{topology}: warmup {time.perf_counter() - tw:.1f}s", file=sys.stderr,
+              flush=True)
     if info.distributed:
         dist.barrier(device_ids=[dev.index])
     torch.cuda.synchronize()
@@ -118,7 +122,9 @@ def main():
     if world_env != args.gpus:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
     info = init_distributed("nccl" if world_env > 1 else "auto")
-    torch.backends.cudnn.benchmark = bool(args.miopen_find)
+    # MIOpen find mode: conv solvers are benchmarked on first use of each shape (untimed: the
+    # warmup steps, plus one tuning step when --warmup 0) and cached for the run.
+    torch.backends.cudnn.benchmark = not args.no_miopen_find
     n = info.world
     main_res = run(args, args.rule, args.topology, args.steps, args.warmup, info)
     ms = main_res["dt"] / args.steps * 1e3

@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Runs the BASELINE.json configurations (besides the headline, which is ../bench.py):
+
+  mlp_median      2-layer MLP, coordinate-wise median (CPU/gloo plumbing; any world size)
+  resnet_trimmed  ResNet-50 bf16, trimmed-mean aggregation
+  resnet_mkrum    ResNet-50 bf16, Multi-Krum
+  bert_geomed     BERT-base (MLM, seq 128) bf16, geometric median (Gram-space Weiszfeld)
+  llama_gossip    Llama-3-8B bf16, decentralised gossip ring + fused AdamW (seq 2048)
+
+One JSON line per config on rank 0 (throughput = whole-job samples/s and tokens/s, ms/step,
+phase breakdown). ``--virtual-workers V`` lets a single GPU aggregate V micro-batch gradients
+(robust rules at n = V without more GPUs); default 1 = ranks are the workers.
+
+  python bench/configs.py --config bert_geomed --steps 10 --warmup 3
+  torchrun --nproc-per-node 2 --master-addr 127.0.0.1 bench/configs.py --config mlp_median
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+CONFIGS = {
+    "mlp_median": dict(model="mlp", rule="median", topology="sharded", batch=256, dtype="fp32",
+                       optim="sgd", lr=0.1, backend="gloo"),
+    "resnet_trimmed": dict(model="resnet50", rule="trimmed_mean", topology="sharded", batch=256,
+                           dtype="bf16", optim="sgd", lr=0.1),
+    "resnet_mkrum": dict(model="resnet50", rule="multi_krum", topology="sharded", batch=256,
+                         dtype="bf16", optim="sgd", lr=0.1),
+    "bert_geomed": dict(model="bert_base", rule="geomed", topology="sharded", batch=64,
+                        seq_len=128, dtype="bf16", optim="adamw", lr=1e-4),
+    "llama_gossip": dict(model="llama3_8b", rule="mean", topology="gossip", batch=1,
+                         seq_len=2048, dtype="bf16", optim="adamw", lr=1e-5, bucket_mb=512),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", choices=sorted(CONFIGS), required=True)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--virtual-workers", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--model", default=None, help="override the model (e.g. llama_tiny)")
+    ap.add_argument("--f", type=int, default=-1)
+    ap.add_argument("--json-out", default=None)
+    a = ap.parse_args()
+    c = dict(CONFIGS[a.config])
+    if a.model:
+        c["model"] = a.model
+    from consensusml_amd import TrainConfig
+    from consensusml_amd.parallel.dist import init_distributed
+    from consensusml_amd.trainer.trainer import ConsensusTrainer
+    backend = c.get("backend", "auto")
+    if backend == "gloo" and torch.cuda.is_available() and os.environ.get("CML_MLP_GPU") == "1":
+        backend = "auto"
+    info = init_distributed(backend)
+    torch.backends.cudnn.benchmark = info.device.type == "cuda"
+    cfg = TrainConfig()
+    cfg.model.name = c["model"]
+    cfg.model.seq_len = c.get("seq_len", 128)
+    cfg.model.extra = {"classes": 2} if c["model"] == "mlp" else {}
+    cfg.batch_per_worker = a.batch or c["batch"]
+    cfg.virtual_workers = a.virtual_workers
+    n = info.world * a.virtual_workers
+    cfg.agg.rule = c["rule"]
+    cfg.agg.f = a.f if a.f >= 0 else (max(0, (n - 1) // 2 - 1) if c["rule"] == "trimmed_mean"
+                                     else max(0, (n - 3) // 2))
+    cfg.topology.kind = c["topology"]
+    cfg.topology.bucket_mb = c.get("bucket_mb", 64)
+    cfg.dtype = c["dtype"]
+    cfg.optim.name = c["optim"]
+    cfg.optim.lr = c["lr"]
+    cfg.profile = True
+    tr = ConsensusTrainer(cfg, info=info)
+    sync = torch.cuda.synchronize if info.device.type == "cuda" else (lambda: None)
+    for _ in range(a.warmup):
+        tr.train_step()
+    tr.timer.summary()
+    sync()
+    if info.distributed:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = tr.train_step()
+    sync()
+    if info.distributed:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    phases = {k: round(v / a.steps, 3) for k, v in tr.timer.summary().items()}
+    if info.distributed:
+        t = torch.tensor([dt], dtype=torch.float64, device=info.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    samples = a.steps * cfg.batch_per_worker * n
+    out = {"config": a.config, "model": cfg.model.name, "rule": cfg.agg.rule,
+           "topology": cfg.topology.kind, "n_gpus": info.world, "workers": n, "f": cfg.agg.f,
+           "per_worker_batch": cfg.batch_per_worker, "dtype": cfg.dtype,
+           "optimizer": cfg.optim.name, "params": tr.engine.flat.real_numel,
+           "samples_per_s": round(samples / dt, 2),
+           "tokens_per_s": round(samples * tr.task.samples_per_item / dt, 1),
+           "ms_per_step": round(dt / a.steps * 1e3, 3), "phase_ms_per_step": phases,
+           "loss": float(loss), "data": "synthetic", "steps": a.steps, "warmup": a.warmup}
+    if info.device.type == "cuda":
+        out["max_mem_gb"] = round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)
+    if info.rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "a") as fh:
+                fh.write(line + "\n")
+    tr.close()
+    if info.distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -248,3 +248,17 @@ def test_pipeline_end_to_end(tmp_path):
                 "xg1_imp", "consensus_votes"]:
         assert col in df.columns
     assert out["performance"]["test_error"].max() < 0.5
+
+
+def test_plots(tmp_path):
+    from consensusml_amd.select import plots as P
+    g = np.random.default_rng(0)
+    deg = pd.DataFrame({"logFC": g.normal(0, 2, 200), "p.adj.bh": g.random(200) ** 4},
+                       index=[f"g{i}" for i in range(200)])
+    P.volcano(deg, str(tmp_path / "v.png"), dpi=50)
+    P.heatmap(g.random((20, 12)), str(tmp_path / "h.png"), [f"g{i}" for i in range(20)],
+              [0, 1] * 6, dpi=50)
+    P.importance_bars(deg["logFC"], str(tmp_path / "b.png"), dpi=50)
+    P.rep_performance({"tpr": [0.9, 0.8], "tnr": [0.8, 0.7]}, str(tmp_path / "r.png"), dpi=50)
+    P.correlation_density(np.corrcoef(g.random((10, 30))), str(tmp_path / "c.png"), dpi=50)
+    assert all((tmp_path / f).stat().st_size > 0 for f in ["v.png", "h.png", "b.png", "r.png", "c.png"])
