@@ -119,6 +119,8 @@ class TrainConfig:
     seed: int = 2019             # the reference's split seed (DEL:159)
     dtype: str = "bf16"
     backend: str = "auto"        # auto | nccl | gloo
+    data_path: Optional[str] = None   # record file for the native loader (else synthetic)
+    loader_threads: int = 4
     log_path: Optional[str] = None
     ckpt_dir: Optional[str] = None
     ckpt_every: int = 0

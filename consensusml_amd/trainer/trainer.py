@@ -41,6 +41,16 @@ class ConsensusTrainer:
             g.manual_seed(cfg.seed * 1000 + self.info.rank * V + v)
             self.gens.append(g)
         self.gen = self.gens[0]
+        # native record loader (csrc/runtime): one disjoint data share per global worker
+        self.loaders = []
+        if cfg.data_path:
+            from ..runtime import DeviceLoader
+            shape, fdt, odt = record_spec(cfg, dtype)
+            for v in range(V):
+                self.loaders.append(DeviceLoader(
+                    cfg.data_path, shape, fdt, cfg.batch_per_worker, dev,
+                    rank=self.info.rank * V + v, world=self.engine.n, seed=cfg.seed,
+                    threads=cfg.loader_threads, out_dtype=odt))
         self.logger = JsonlLogger(cfg.log_path, self.info.rank)
         self.timer = PhaseTimer(dev, enabled=cfg.profile)
         self.history: List[float] = []
@@ -59,7 +69,13 @@ class ConsensusTrainer:
         for v in range(e.V):
             e.bind_worker(v)
             with t.phase("data"):
-                batch = self.task.make_batch(self.cfg.batch_per_worker, self.gens[v])
+                if self.loaders:
+                    x, yb, _ = self.loaders[v].next()
+                    if x.dim() == 4:
+                        x = x.contiguous(memory_format=torch.channels_last)
+                    batch = (x, yb)
+                else:
+                    batch = self.task.make_batch(self.cfg.batch_per_worker, self.gens[v])
             with t.phase("fwd_bwd"):
                 loss = self.task.loss_fn(self.model, batch)
                 loss.backward()
@@ -142,3 +158,28 @@ class ConsensusTrainer:
     def close(self) -> None:
         self.logger.close()
         self.engine.close()
+        for l in self.loaders:
+            l.close()
+
+
+def record_spec(cfg: TrainConfig, dtype: torch.dtype):
+    """(feature shape, on-disk dtype, compute dtype) of a model's record files."""
+    m = cfg.model
+    if m.name == "mlp":
+        return (m.in_features,), torch.float32, dtype
+    if m.name.startswith("resnet"):
+        return (3, m.image_size, m.image_size), torch.float16, dtype
+    return (m.seq_len,), torch.int64, None
+
+
+def write_synthetic_records(cfg: TrainConfig, path: str, n: int, seed: int = 0) -> int:
+    """Write ``n`` records of the model's shape drawn from its synthetic generator."""
+    import numpy as np
+    from ..models import build_task
+    from ..runtime import write_records
+    task = build_task(cfg.model, torch.device("cpu"), torch.float32, seed=cfg.seed)
+    g = torch.Generator().manual_seed(seed)
+    x, y = task.make_batch(n, g)
+    shape, fdt, _ = record_spec(cfg, torch.float32)
+    feats = x.to(fdt).contiguous().numpy().reshape(n, -1)
+    return write_records(path, feats, y.numpy().reshape(n, -1)[:, 0])
