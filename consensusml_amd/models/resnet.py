@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.bn import BatchNormAct2d
+from ..ops.pool import max_pool2d
 
 
 class Bottleneck(nn.Module):
@@ -68,7 +69,7 @@ class ResNet(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self.bn1(self.conv1(x))
-        x = F.max_pool2d(x, 3, 2, 1)
+        x = max_pool2d(x, 3, 2, 1)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

@@ -228,6 +228,31 @@ std::vector<Tensor> bn_bwd(const Tensor& dy_in, const Tensor& x, const optional<
   return {dx, dgamma, dbeta, dres};
 }
 
+std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(1) % 8 == 0, "maxpool: 4-D NHWC with C % 8 == 0");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
+  const c10::DeviceGuard guard(x.device());
+  Tensor y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor idx = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+  CML_CHECK_HIP(cml::launch_maxpool_fwd(x.data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C,
+                                        OH, OW, k, s, p, cur_stream()));
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W, int64_t k,
+                   int64_t s, int64_t p) {
+  Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(dy, "dy");
+  const int64_t N = dy.size(0), C = dy.size(1), OH = dy.size(2), OW = dy.size(3);
+  const c10::DeviceGuard guard(dy.device());
+  Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  CML_CHECK_HIP(cml::launch_maxpool_bwd(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), N, H, W, C,
+                                        OH, OW, k, s, p, cur_stream()));
+  return dx;
+}
+
 void fault(Tensor& g, int64_t kind, double scale, double sigma, int64_t seed) {
   check_dev(g, "g");
   TORCH_CHECK(g.is_contiguous(), "g must be contiguous");
@@ -250,6 +275,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fault", &fault, "Byzantine fault injection");
   m.def("bn_fwd", &bn_fwd, "fused NHWC BatchNorm(+res)(+ReLU) forward");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BatchNorm(+res)(+ReLU) backward");
+  m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
+  m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);
   m.attr("OPT_NONE") = static_cast<int>(cml::OPT_NONE);

@@ -83,6 +83,12 @@ hipError_t launch_bn_bwd(const void* dy, const void* x, const void* res, void* d
                          const float* invstd, void* dgamma, void* dbeta, float* sdz, float* sdzx,
                          int relu, void* work, hipStream_t stream);
 
+// NHWC bf16 max-pool with a one-byte argmax per output element; backward is a gather.
+hipError_t launch_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C,
+                              int OH, int OW, int k, int s, int p, hipStream_t stream);
+hipError_t launch_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W,
+                              int C, int OH, int OW, int k, int s, int p, hipStream_t stream);
+
 // Elementwise fault injection on a local gradient (Byzantine simulation, N10).
 hipError_t launch_fault(int dtype, void* g, int64_t D, int kind, float scale, float sigma,
                         uint64_t seed, hipStream_t stream);

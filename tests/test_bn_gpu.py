@@ -93,3 +93,19 @@ def test_resnet_tiny_fused_vs_reference(cuda):
     out = mb(x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)).float()
     out_ref = ref(x)   # fp32 NCHW -> composition path
     torch.testing.assert_close(out, out_ref, rtol=0.1, atol=0.15)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 112, 112), (3, 16, 9, 7)])
+def test_maxpool_nhwc(cuda, shape):
+    from consensusml_amd.ops.pool import max_pool2d
+    torch.manual_seed(1)
+    x = torch.randn(*shape, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    y = max_pool2d(x, 3, 2, 1)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    torch.testing.assert_close(y.float(), yr)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(torch.bfloat16))
+    yr.backward(dy.to(torch.bfloat16).float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
