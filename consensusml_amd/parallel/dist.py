@@ -37,7 +37,7 @@ _INFO: Optional[DistInfo] = None
 
 
 def init_distributed(backend: str = "auto", device: Optional[str] = None,
-                     timeout_s: float = 600.0) -> DistInfo:
+                     timeout_s: float = 1800.0) -> DistInfo:
     """Initialise (once) and return this process's DistInfo."""
     global _INFO
     if _INFO is not None:
