@@ -67,7 +67,10 @@ void agg_update(const Tensor& X, int64_t n, int64_t D, const optional<Tensor>& r
   u.master = opt_ptr<float>(master, at::kFloat, "master", D);
   u.s1 = opt_ptr<float>(s1, at::kFloat, "s1", D);
   u.s2 = opt_ptr<float>(s2, at::kFloat, "s2", D);
-  u.param_out = opt_ptr<void>(param_out, at::kBFloat16, "param_out", D);
+  const bool pf32 = param_out.has_value() && param_out->defined() &&
+                    param_out->scalar_type() == at::kFloat;
+  u.param_out = opt_ptr<void>(param_out, pf32 ? at::kFloat : at::kBFloat16, "param_out", D);
+  u.param_f32 = pf32 ? 1 : 0;
   u.gout = opt_ptr<float>(gout, at::kFloat, "gout", D);
   if (opt != cml::OPT_NONE) TORCH_CHECK(u.master, "optimizer update needs master weights");
   if (opt == cml::OPT_SGD && momentum != 0.0) TORCH_CHECK(u.s1, "SGD momentum needs s1");
@@ -136,14 +139,13 @@ void gossip_mix(Tensor& master, const optional<Tensor>& param_out, const Tensor&
   check_dev(master, "master");
   TORCH_CHECK(master.scalar_type() == at::kFloat && master.is_contiguous(), "master: fp32 contiguous");
   const int64_t D = master.numel();
-  TORCH_CHECK(left.scalar_type() == at::kBFloat16 && right.scalar_type() == at::kBFloat16 &&
-                  left.is_contiguous() && right.is_contiguous() && left.numel() >= D &&
-                  right.numel() >= D,
-              "neighbours: contiguous bf16 of master's size");
+  TORCH_CHECK(left.scalar_type() == right.scalar_type() && left.is_contiguous() &&
+                  right.is_contiguous() && left.numel() >= D && right.numel() >= D,
+              "neighbours: contiguous, same dtype, master's size");
   TORCH_CHECK(work.numel() * work.element_size() >= gossip_workspace_bytes(D), "gossip workspace too small");
-  void* p = opt_ptr<void>(param_out, at::kBFloat16, "param_out", D);
+  void* p = opt_ptr<void>(param_out, left.scalar_type(), "param_out", D);
   const c10::DeviceGuard guard(master.device());
-  CML_CHECK_HIP(cml::launch_gossip_mix(master.data_ptr<float>(), p, left.data_ptr(), right.data_ptr(),
+  CML_CHECK_HIP(cml::launch_gossip_mix(dtype_of(left), master.data_ptr<float>(), p, left.data_ptr(), right.data_ptr(),
                                        D, static_cast<float>(w0), static_cast<float>(w1),
                                        static_cast<float>(w2), static_cast<float>(clip),
                                        work.data_ptr(), cur_stream()));

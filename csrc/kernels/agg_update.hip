@@ -74,7 +74,10 @@ __device__ __forceinline__ void update_and_store(const UpdArgs& u, int opt, int6
     store_f32<VEC>(u.s2 + e, s);
   }
   store_f32<VEC>(u.master + e, p);
-  if (u.param_out) store_bf16<VEC>(reinterpret_cast<bf16*>(u.param_out) + e, p);
+  if (u.param_out) {
+    if (u.param_f32) store_f32<VEC>(reinterpret_cast<float*>(u.param_out) + e, p);
+    else store_bf16<VEC>(reinterpret_cast<bf16*>(u.param_out) + e, p);
+  }
 }
 
 // ----------------------------------------------------------------------------- sorted combine
@@ -245,7 +248,7 @@ static hipError_t agg_update_t(int combine, int opt, const SrcArgs& s, const Upd
   // The vector path needs every row start and every state pointer aligned to VEC elements.
   bool ok = (s.ld % vec) == 0 && aligned(s.X, vec * esz) && aligned(u.master, vec * 4) &&
             aligned(u.s1, vec * 4) && aligned(u.s2, vec * 4) && aligned(u.gout, vec * 4) &&
-            aligned(u.param_out, vec * 2);
+            aligned(u.param_out, vec * (u.param_f32 ? 4 : 2));
   int64_t Dv = ok ? (D / vec) * vec : 0;
   if (Dv > 0) {
     if (combine == CMB_WEIGHTED) {

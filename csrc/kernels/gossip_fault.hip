@@ -17,9 +17,16 @@ namespace {
 constexpr int kBlk = 256;
 constexpr int kMaxBlk = 1024;
 
+template <typename T>
+__device__ __forceinline__ float ld1(const T* p, int64_t e) {
+  if constexpr (sizeof(T) == 2) return bf2f(reinterpret_cast<const uint16_t*>(p)[e]);
+  else return p[e];
+}
+
+template <typename T>
 __global__ __launch_bounds__(kBlk) void pair_sqdist_kernel(const float* __restrict__ x,
-                                                          const bf16* __restrict__ l,
-                                                          const bf16* __restrict__ r, int64_t D,
+                                                          const T* __restrict__ l,
+                                                          const T* __restrict__ r, int64_t D,
                                                           float* __restrict__ part) {
   float sl = 0.f, sr = 0.f;
   const int64_t nv = D / 8;
@@ -27,8 +34,8 @@ __global__ __launch_bounds__(kBlk) void pair_sqdist_kernel(const float* __restri
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlk + threadIdx.x; t < nv; t += stride) {
     float xv[8], lv[8], rv[8];
     load_vec<float, 8>(x + t * 8, xv);
-    load_vec<bf16, 8>(l + t * 8, lv);
-    load_vec<bf16, 8>(r + t * 8, rv);
+    load_vec<T, 8>(l + t * 8, lv);
+    load_vec<T, 8>(r + t * 8, rv);
 #pragma unroll
     for (int v = 0; v < 8; ++v) {
       const float a = lv[v] - xv[v], b = rv[v] - xv[v];
@@ -38,8 +45,8 @@ __global__ __launch_bounds__(kBlk) void pair_sqdist_kernel(const float* __restri
   }
   if (blockIdx.x == 0) {
     for (int64_t e = nv * 8 + threadIdx.x; e < D; e += kBlk) {
-      const float a = bf2f(reinterpret_cast<const uint16_t*>(l)[e]) - x[e];
-      const float b = bf2f(reinterpret_cast<const uint16_t*>(r)[e]) - x[e];
+      const float a = ld1(l, e) - x[e];
+      const float b = ld1(r, e) - x[e];
       sl = fmaf(a, a, sl);
       sr = fmaf(b, b, sr);
     }
@@ -64,10 +71,11 @@ __global__ __launch_bounds__(kBlk) void pair_sqdist_kernel(const float* __restri
   }
 }
 
+template <typename T>
 __global__ __launch_bounds__(kBlk) void gossip_mix_kernel(float* __restrict__ x,
-                                                         bf16* __restrict__ p,
-                                                         const bf16* __restrict__ l,
-                                                         const bf16* __restrict__ r, int64_t D,
+                                                         T* __restrict__ p,
+                                                         const T* __restrict__ l,
+                                                         const T* __restrict__ r, int64_t D,
                                                          float w0, float w1, float w2, float clip,
                                                          const float* __restrict__ part, int nblk) {
   __shared__ float scl[2];
@@ -93,21 +101,25 @@ __global__ __launch_bounds__(kBlk) void gossip_mix_kernel(float* __restrict__ x,
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlk + threadIdx.x; t < nv; t += stride) {
     float xv[8], lv[8], rv[8];
     load_vec<float, 8>(x + t * 8, xv);
-    load_vec<bf16, 8>(l + t * 8, lv);
-    load_vec<bf16, 8>(r + t * 8, rv);
+    load_vec<T, 8>(l + t * 8, lv);
+    load_vec<T, 8>(r + t * 8, rv);
 #pragma unroll
     for (int v = 0; v < 8; ++v) xv[v] = fmaf(cs, xv[v], fmaf(cl, lv[v] - xv[v], cr * (rv[v] - xv[v])));
     store_f32<8>(x + t * 8, xv);
-    if (p) store_bf16<8>(p + t * 8, xv);
+    if (p) {
+      if constexpr (sizeof(T) == 2) store_bf16<8>(p + t * 8, xv);
+      else store_f32<8>(p + t * 8, xv);
+    }
   }
   if (blockIdx.x == 0) {
     for (int64_t e = nv * 8 + threadIdx.x; e < D; e += kBlk) {
       const float xe = x[e];
-      const float le = bf2f(reinterpret_cast<const uint16_t*>(l)[e]);
-      const float re = bf2f(reinterpret_cast<const uint16_t*>(r)[e]);
-      const float v = fmaf(cs, xe, fmaf(cl, le - xe, cr * (re - xe)));
+      const float v = fmaf(cs, xe, fmaf(cl, ld1(l, e) - xe, cr * (ld1(r, e) - xe)));
       x[e] = v;
-      if (p) reinterpret_cast<uint16_t*>(p)[e] = f2bf(v);
+      if (p) {
+        if constexpr (sizeof(T) == 2) reinterpret_cast<uint16_t*>(p)[e] = f2bf(v);
+        else p[e] = v;
+      }
     }
   }
 }
@@ -158,20 +170,27 @@ int nblocks(int64_t work, int cap) {
 
 size_t gossip_workspace_bytes(int64_t) { return 2 * kMaxBlk * sizeof(float); }
 
-hipError_t launch_gossip_mix(float* master, void* param_out, const void* left, const void* right,
-                             int64_t D, float w0, float w1, float w2, float clip, void* work,
-                             hipStream_t stream) {
-  if ((reinterpret_cast<uintptr_t>(master) | reinterpret_cast<uintptr_t>(left) |
-       reinterpret_cast<uintptr_t>(right) | reinterpret_cast<uintptr_t>(param_out)) % 16)
-    return hipErrorInvalidValue;
+template <typename T>
+void gossip_t(float* master, void* param_out, const void* left, const void* right, int64_t D,
+              float w0, float w1, float w2, float clip, void* work, hipStream_t stream) {
   float* part = reinterpret_cast<float*>(work);
   const int nb = nblocks(D / 8, kMaxBlk);
   if (clip > 0.f)
-    pair_sqdist_kernel<<<nb, kBlk, 0, stream>>>(master, reinterpret_cast<const bf16*>(left),
-                                                reinterpret_cast<const bf16*>(right), D, part);
-  gossip_mix_kernel<<<nblocks(D / 8, 2048), kBlk, 0, stream>>>(
-      master, reinterpret_cast<bf16*>(param_out), reinterpret_cast<const bf16*>(left),
-      reinterpret_cast<const bf16*>(right), D, w0, w1, w2, clip, part, nb);
+    pair_sqdist_kernel<T><<<nb, kBlk, 0, stream>>>(master, reinterpret_cast<const T*>(left),
+                                                   reinterpret_cast<const T*>(right), D, part);
+  gossip_mix_kernel<T><<<nblocks(D / 8, 2048), kBlk, 0, stream>>>(
+      master, reinterpret_cast<T*>(param_out), reinterpret_cast<const T*>(left),
+      reinterpret_cast<const T*>(right), D, w0, w1, w2, clip, part, nb);
+}
+
+hipError_t launch_gossip_mix(int dtype, float* master, void* param_out, const void* left,
+                             const void* right, int64_t D, float w0, float w1, float w2,
+                             float clip, void* work, hipStream_t stream) {
+  if ((reinterpret_cast<uintptr_t>(master) | reinterpret_cast<uintptr_t>(left) |
+       reinterpret_cast<uintptr_t>(right) | reinterpret_cast<uintptr_t>(param_out)) % 16)
+    return hipErrorInvalidValue;
+  if (dtype == DT_BF16) gossip_t<bf16>(master, param_out, left, right, D, w0, w1, w2, clip, work, stream);
+  else gossip_t<float>(master, param_out, left, right, D, w0, w1, w2, clip, work, stream);
   return hipGetLastError();
 }
 

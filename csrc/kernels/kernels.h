@@ -36,10 +36,11 @@ struct UpdArgs {
   float* master;     // fp32 master weights (SGD/Adam)
   float* s1;         // momentum (SGD) or exp_avg (Adam)
   float* s2;         // exp_avg_sq (Adam)
-  void* param_out;   // bf16 model parameters rewritten from the master
+  void* param_out;   // model parameters rewritten from the master (bf16, or fp32 if param_f32)
   float* gout;       // aggregated gradient (fp32), optional
   float lr, momentum, weight_decay, beta1, beta2, eps, step_size, inv_sqrt_bc2, gscale;
   int nesterov, first;
+  int param_f32;
 };
 
 // Aggregate n worker vectors of length D and apply the optimizer in the same pass.
@@ -64,9 +65,9 @@ hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m,
 // Gossip: x <- (w0+w1+w2) x + w1*clip(left-x) + w2*clip(right-x); writes fp32 master and bf16
 // params. clip <= 0 disables clipping. ``work`` must hold gossip_workspace_bytes(D) bytes.
 size_t gossip_workspace_bytes(int64_t D);
-hipError_t launch_gossip_mix(float* master, void* param_out, const void* left, const void* right,
-                             int64_t D, float w0, float w1, float w2, float clip, void* work,
-                             hipStream_t stream);
+hipError_t launch_gossip_mix(int dtype, float* master, void* param_out, const void* left,
+                             const void* right, int64_t D, float w0, float w1, float w2,
+                             float clip, void* work, hipStream_t stream);
 
 // Fused training BatchNorm (+ residual add) (+ ReLU) on NHWC bf16 rows x[M, C] (C % 8 == 0,
 // C <= 2048). Forward with training != 0 computes batch statistics into mean / invstd (fp32 [C])
