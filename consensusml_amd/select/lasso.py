@@ -70,20 +70,25 @@ def fista_logistic(X: torch.Tensor, y: torch.Tensor, lambdas: torch.Tensor,
     if intercept:
         s += n
     step = 1.0 / (0.25 * s / nb + lam * (1 - alpha))
-    beta = torch.zeros(p, Bn, device=dev)
-    b0 = torch.zeros(1, Bn, device=dev)
+    out_beta = torch.zeros(p, Bn, device=dev)
+    out_b0 = torch.zeros(1, Bn, device=dev)
+    # working set of unconverged problems; converged columns are written out and dropped, so
+    # the batch shrinks as the easy (large-lambda) problems finish
+    act = torch.arange(Bn, device=dev)
+    beta = out_beta.clone()
+    b0 = out_b0.clone()
     v, v0 = beta.clone(), b0.clone()
     tk = torch.ones(1, Bn, device=dev)
-    converged = False
+    Ma, nba, lama, stepa = M, nb, lam, step
     it = 0
     for it in range(1, max_iter + 1):
         z = X @ v + v0
-        r = (torch.sigmoid(z) - yv) * M / nb                     # d loss / d z
+        r = (torch.sigmoid(z) - yv) * Ma / nba                   # d loss / d z
         g = X.t() @ r
         if alpha < 1:
-            g = g + lam * (1 - alpha) * v
-        nbeta = _soft(v - step * g, step * lam * alpha)
-        nb0 = v0 - step * r.sum(0, keepdim=True) if intercept else b0
+            g = g + lama * (1 - alpha) * v
+        nbeta = _soft(v - stepa * g, stepa * lama * alpha)
+        nb0 = v0 - stepa * r.sum(0, keepdim=True) if intercept else b0
         # adaptive restart (O'Donoghue & Candes): drop momentum where it points uphill
         up = ((v - nbeta) * (nbeta - beta)).sum(0, keepdim=True) > 0
         tn = (1 + torch.sqrt(1 + 4 * tk * tk)) / 2
@@ -93,12 +98,21 @@ def fista_logistic(X: torch.Tensor, y: torch.Tensor, lambdas: torch.Tensor,
         v = nbeta + mom * d
         v0 = nb0 + mom * (nb0 - b0) if intercept else nb0
         beta, b0 = nbeta, nb0
-        if it % check_every == 0:
-            delta = (d.abs().amax(0) / beta.abs().amax(0).clamp_min(1.0)).max().item()
-            if delta < tol:
-                converged = True
-                break
-    return beta, b0.view(-1), it, converged
+        if it % check_every == 0 or it == max_iter:
+            delta = d.abs().amax(0) / beta.abs().amax(0).clamp_min(1.0)
+            done = delta < tol
+            if bool(done.any()) or it == max_iter:
+                keep = ~done if it < max_iter else torch.zeros_like(done)
+                fin = act[~keep]
+                out_beta[:, fin] = beta[:, ~keep]
+                out_b0[:, fin] = b0[:, ~keep]
+                if not bool(keep.any()):
+                    break
+                act = act[keep]
+                beta, b0, v, v0, tk = beta[:, keep], b0[:, keep], v[:, keep], v0[:, keep], tk[:, keep]
+                Ma, nba, lama, stepa = Ma[:, keep], nba[:, keep], lama[:, keep], stepa[:, keep]
+    converged = it < max_iter
+    return out_beta, out_b0.view(-1), it, converged
 
 
 def lasso_path(X: torch.Tensor, y: torch.Tensor, lambdas: Sequence[float] = GLMNET_GRID,

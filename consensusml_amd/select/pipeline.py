@@ -29,7 +29,7 @@ from .lasso import iterative_exclusion
 from .metrics import binary_metrics
 from .normalize import normalize
 from .svm import run_svm
-from .trees import GradientBoostedTrees, RandomForest
+from .hist_trees import HistBoost, HistForest
 
 Member = Tuple[str, Callable[[], Dict[str, object]]]
 
@@ -107,7 +107,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
     # ---------------------------------------------------------------- random forests
     for nt in rf_trees:
         def f(nt=nt):
-            rf = RandomForest(nt, seed=seed).fit(Xtr, ytr)
+            rf = HistForest(nt, max_depth=10, seed=seed).fit(Xtr, ytr)
             pred = rf.predict(Xte).cpu()
             return {"values": rf.mean_decrease_gini.numpy(),
                     "metrics": binary_metrics(yte.cpu(), pred)}
@@ -116,7 +116,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
     # ---------------------------------------------------------------- boosted trees
     for i, cfg in enumerate(xgb_configs):
         def f(cfg=cfg):
-            m = GradientBoostedTrees(cfg.get("n_estimators", 50), cfg.get("eta", 1.0),
+            m = HistBoost(cfg.get("n_estimators", 50), cfg.get("eta", 1.0),
                                      cfg.get("max_depth", 6), seed=seed).fit(Xtr, ytr)
             pred = (m.predict_proba(Xte)[:, 1] > 0.5).long().cpu()
             return {"values": m.feature_importances_.numpy(),

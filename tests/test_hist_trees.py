@@ -1,0 +1,49 @@
+"""Level-synchronous histogram forests / boosting (select/hist_trees.py) — CPU."""
+import numpy as np
+import torch
+
+from consensusml_amd.select.hist_trees import HistBoost, HistForest, bin_with, quantile_bins
+
+
+def _easy(n=300, p=100, seed=1):
+    g = np.random.default_rng(seed)
+    X = g.standard_normal((n, p)).astype(np.float32)
+    y = ((X[:, 0] + 0.7 * X[:, 5]) > 0).astype(np.int64)
+    return torch.tensor(X), torch.tensor(y)
+
+
+def test_quantile_bins_monotone():
+    X, _ = _easy(200, 8)
+    Xb, edges = quantile_bins(X, 16)
+    assert Xb.max() <= 15
+    # binning is monotone in x and reproduced by bin_with
+    for j in range(8):
+        o = torch.argsort(X[:, j])
+        assert (Xb[o, j][1:] >= Xb[o, j][:-1]).all()
+    assert torch.equal(bin_with(X, edges), Xb)
+
+
+def test_hist_forest_learns_and_ranks_features():
+    X, y = _easy()
+    f = HistForest(150, 6, seed=3).fit(X[:200], y[:200])
+    acc = (f.predict(X[200:]) == y[200:]).float().mean()
+    assert acc > 0.75
+    assert set(torch.topk(f.feature_importances_, 2).indices.tolist()) == {0, 5}
+    assert f.mean_decrease_gini.shape == (100,)
+
+
+def test_hist_boost_learns():
+    X, y = _easy()
+    b = HistBoost(60, 0.3, 3, seed=2).fit(X[:200], y[:200])
+    p = b.predict_proba(X[200:])[:, 1]
+    assert ((p > 0.5).long() == y[200:]).float().mean() > 0.85
+    assert set(torch.topk(b.feature_importances_, 2).indices.tolist()) == {0, 5}
+    b2 = HistBoost(20, 0.3, 3, colsample=0.5, seed=2).fit(X[:200], y[:200])
+    assert torch.isfinite(b2.predict_proba(X[200:])).all()
+
+
+def test_depth_zero_is_prior():
+    X, y = _easy(100, 8)
+    f = HistForest(10, 0, seed=0).fit(X, y)
+    p = f.predict_proba(X)[:, 1]
+    assert torch.allclose(p, p[0].expand_as(p))
