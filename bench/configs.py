@@ -37,7 +37,8 @@ CONFIGS = {
     "bert_geomed": dict(model="bert_base", rule="geomed", topology="sharded", batch=64,
                         seq_len=128, dtype="bf16", optim="adamw", lr=1e-4),
     "llama_gossip": dict(model="llama3_8b", rule="mean", topology="gossip", batch=1,
-                         seq_len=2048, dtype="bf16", optim="adamw", lr=1e-5, bucket_mb=512),
+                         seq_len=2048, dtype="bf16", optim="adamw", lr=1e-5, bucket_mb=512,
+                         gossip_async=True),
 }
 
 
@@ -75,6 +76,7 @@ def main():
                                      else max(0, (n - 3) // 2))
     cfg.topology.kind = c["topology"]
     cfg.topology.bucket_mb = c.get("bucket_mb", 64)
+    cfg.topology.gossip_async = c.get("gossip_async", False)
     cfg.dtype = c["dtype"]
     cfg.optim.name = c["optim"]
     cfg.optim.lr = c["lr"]

@@ -75,6 +75,7 @@ class TopologyConfig:
     overlap: bool = True         # launch bucket collectives during backward
     gossip_weights: tuple = (1 / 3, 1 / 3, 1 / 3)   # self, left, right
     gossip_clip: float = 0.0     # 0 disables neighbour-delta clipping
+    gossip_async: bool = False   # delayed gossip: exchange overlaps the next step's compute
 
     def validate(self) -> None:
         if self.kind not in TOPOLOGIES:

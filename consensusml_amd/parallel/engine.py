@@ -86,7 +86,8 @@ class ConsensusEngine:
         elif self.topo == "gossip":
             self.nb_left = torch.empty_like(fl.flat_param)
             self.nb_right = torch.empty_like(fl.flat_param)
-            self.gossip_work = None
+        self._gossip_reqs = None
+        self._send_buf = None
         # -------------------------------------------------- rule buffers
         self.G = torch.zeros(self.rows_total, self.rows_total, dtype=torch.float64, device=dev)
         self.w = torch.full((self.rows_total,), 1.0 / self.n, dtype=torch.float32, device=dev)
@@ -390,13 +391,30 @@ class ConsensusEngine:
         total = fl.total
         starts = list(range(0, total, chunk))
 
-        def exchange(s):
+        def exchange(s, src=None):
+            src = fl.flat_param if src is None else src
             e = min(s + chunk, total)
-            ops = [dist.P2POp(dist.isend, fl.flat_param[s:e], left),
-                   dist.P2POp(dist.isend, fl.flat_param[s:e], right),
+            ops = [dist.P2POp(dist.isend, src[s:e], left),
+                   dist.P2POp(dist.isend, src[s:e], right),
                    dist.P2POp(dist.irecv, self.nb_left[s:e], left),
                    dist.P2POp(dist.irecv, self.nb_right[s:e], right)]
             return dist.batch_isend_irecv(ops)
+
+        if self.cfg.topology.gossip_async:
+            # Delayed gossip: mix with the neighbour parameters that arrived during THIS step's
+            # compute (sent at the end of the previous step), then snapshot the new local
+            # parameters and start the next exchange, which overlaps the next forward/backward.
+            if self._gossip_reqs is not None:
+                for rq in self._gossip_reqs:
+                    for w in rq:
+                        w.wait()
+                K.gossip_mix(self.master, self.nb_left, self.nb_right, w0, w1, w2, clip,
+                             param_out=fl.flat_param)
+            if self._send_buf is None:
+                self._send_buf = torch.empty_like(fl.flat_param)
+            self._send_buf.copy_(fl.flat_param)
+            self._gossip_reqs = [exchange(s, self._send_buf) for s in starts]
+            return
 
         if clip > 0 and len(starts) > 1:
             # clipping needs whole-vector neighbour distances: exchange everything first
@@ -457,6 +475,11 @@ class ConsensusEngine:
             fl.flat_param.copy_(self.master.to(fl.dtype))
 
     def close(self) -> None:
+        if self._gossip_reqs is not None:     # drain the in-flight delayed-gossip exchange
+            for rq in self._gossip_reqs:
+                for w in rq:
+                    w.wait()
+            self._gossip_reqs = None
         for h in self._hooks:
             h.remove()
         self._hooks = []

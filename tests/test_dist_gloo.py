@@ -29,7 +29,8 @@ def _cfg(rule, topo, V, f, steps, fault="none", byz=()):
     cfg.virtual_workers = V
     cfg.agg.rule = rule
     cfg.agg.f = f
-    cfg.topology.kind = topo
+    cfg.topology.kind = "gossip" if topo == "gossip_async" else topo
+    cfg.topology.gossip_async = topo == "gossip_async"
     cfg.topology.bucket_mb = 0.002      # several buckets even for the tiny MLP
     cfg.optim.lr = 0.1
     cfg.batch_per_worker = 16
@@ -109,10 +110,15 @@ def test_byzantine_rank_excluded_gloo(tmp_path):
         torch.testing.assert_close(a, b)
 
 
-def test_gossip_ring_runs(tmp_path):
-    res = _run_world(3, "mean", "gossip", 0, 6, tmp_path)
+@pytest.mark.parametrize("topo", ["gossip", "gossip_async"])
+def test_gossip_ring_runs(tmp_path, topo):
+    res = _run_world(3, "mean", topo, 0, 6, tmp_path)
     for r in range(3):
         assert all(torch.isfinite(p).all() for p in res[r]["params"])
+    # gossip pulls the replicas together: spread across ranks stays small vs the weights
+    for ps in zip(*[res[r]["params"] for r in range(3)]):
+        spread = torch.stack(ps).std(0).max()
+        assert spread < 0.1 * max(p.abs().max() for p in ps) + 1e-3
 
 
 def test_checkpoint_resume_gloo(tmp_path):
