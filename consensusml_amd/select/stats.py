@@ -192,3 +192,51 @@ class PLDA:
         N = torch.outer(s, self.gene_tot)
         sc = X @ torch.log(self.d).t() - N @ self.d.t() + torch.log(self.prior)
         return self.classes[sc.argmax(1)]
+
+
+def voom_transform(counts: torch.Tensor) -> torch.Tensor:
+    """log2-CPM with 0.5 offsets (the voom expression scale used by MLSeq's voomDLDA / voomNSC),
+    samples x genes counts in, samples x genes out."""
+    x = counts.double()
+    lib = x.sum(1, keepdim=True)
+    return torch.log2((x + 0.5) / (lib + 1.0) * 1e6)
+
+
+class VoomDLDA(DLDA):
+    """MLSeq ``voomDLDA``: diagonal LDA on voom-transformed counts."""
+
+    def fit(self, counts, y):
+        return super().fit(voom_transform(counts), y)
+
+    def predict(self, counts):
+        return super().predict(voom_transform(counts))
+
+
+class VoomNSC(NSC):
+    """MLSeq ``voomNSC``: nearest shrunken centroids on voom-transformed counts."""
+
+    def fit(self, counts, y):
+        return super().fit(voom_transform(counts), y)
+
+    def predict(self, counts):
+        return super().predict(voom_transform(counts))
+
+
+def cohort_summary(col_data, label: str = "low_risk", covariates=("gender", "age"),
+                   age_cut: Optional[float] = None) -> Dict[str, object]:
+    """Cohort table and balance tests (C30, `cml_targetaml_seanalysis.Rmd:422-474`): class counts,
+    per-covariate contingency tables vs the label and chi-square p values (numeric covariates
+    are split at the median, or at ``age_cut``)."""
+    import pandas as pd
+    out: Dict[str, object] = {"n": int(len(col_data)),
+                              "classes": col_data[label].value_counts().to_dict()}
+    for cov in covariates:
+        if cov not in col_data:
+            continue
+        v = col_data[cov]
+        if np.issubdtype(v.dtype, np.number):
+            cut = age_cut if age_cut is not None else float(v.median())
+            v = (v > cut).map({True: f">{cut:g}", False: f"<={cut:g}"})
+        tab = pd.crosstab(v, col_data[label])
+        out[cov] = {"table": tab.to_dict(), **chisq_test(tab.to_numpy())}
+    return out
