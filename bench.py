@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--rule", default="krum")
     ap.add_argument("--f", type=int, default=-1, help="Byzantine tolerance (-1: (n-3)//2)")
@@ -117,6 +117,9 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info):
 
 def main():
     args = parse()
+    if not args.no_miopen_find:
+        from consensusml_amd.utils.tuning import use_shipped_miopen_db
+        use_shipped_miopen_db()
     from consensusml_amd.parallel.dist import init_distributed
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:
