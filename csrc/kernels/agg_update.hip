@@ -21,29 +21,48 @@ namespace cml {
 constexpr int kBlock = 256;
 constexpr int kMaxRows = 64;
 
+// Optimizer state of VEC coordinates, loaded BEFORE the combine so those HBM reads are in flight
+// while the sort / weighted sum runs (hipcc does not hoist them above the VALU work by itself).
+template <int VEC>
+struct OptState {
+  float p[VEC];   // fp32 master
+  float a[VEC];   // momentum buffer / Adam m
+  float b[VEC];   // Adam v
+};
+
+template <int VEC>
+__device__ __forceinline__ void load_state(const UpdArgs& u, int opt, int64_t e, OptState<VEC>& st) {
+  if (opt == OPT_NONE) return;
+  load_vec<float, VEC>(u.master + e, st.p);
+  if (opt == OPT_SGD) {
+    if (u.momentum != 0.0f && !u.first) load_vec<float, VEC>(u.s1 + e, st.a);
+  } else {
+    load_vec<float, VEC>(u.s1 + e, st.a);
+    load_vec<float, VEC>(u.s2 + e, st.b);
+  }
+}
+
 template <int VEC>
 __device__ __forceinline__ void update_and_store(const UpdArgs& u, int opt, int64_t e,
-                                                 float (&g)[VEC]) {
+                                                 float (&g)[VEC], OptState<VEC>& st) {
   if (u.gscale != 1.0f) {
 #pragma unroll
     for (int v = 0; v < VEC; ++v) g[v] *= u.gscale;
   }
   if (u.gout) store_f32<VEC>(u.gout + e, g);
   if (opt == OPT_NONE) return;
-  float p[VEC];
-  load_vec<float, VEC>(u.master + e, p);
+  float (&p)[VEC] = st.p;
   if (opt == OPT_SGD) {
     if (u.weight_decay != 0.0f) {
 #pragma unroll
       for (int v = 0; v < VEC; ++v) g[v] = fmaf(u.weight_decay, p[v], g[v]);
     }
     if (u.momentum != 0.0f) {
-      float b[VEC];
+      float (&b)[VEC] = st.a;
       if (u.first) {
 #pragma unroll
         for (int v = 0; v < VEC; ++v) b[v] = g[v];
       } else {
-        load_vec<float, VEC>(u.s1 + e, b);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) b[v] = fmaf(u.momentum, b[v], g[v]);
       }
@@ -59,9 +78,8 @@ __device__ __forceinline__ void update_and_store(const UpdArgs& u, int opt, int6
 #pragma unroll
     for (int v = 0; v < VEC; ++v) p[v] = fmaf(-u.lr, g[v], p[v]);
   } else {  // OPT_ADAM (decoupled weight decay when weight_decay != 0)
-    float m[VEC], s[VEC];
-    load_vec<float, VEC>(u.s1 + e, m);
-    load_vec<float, VEC>(u.s2 + e, s);
+    float (&m)[VEC] = st.a;
+    float (&s)[VEC] = st.b;
     const float decay = 1.0f - u.lr * u.weight_decay;
 #pragma unroll
     for (int v = 0; v < VEC; ++v) {
@@ -81,6 +99,8 @@ __device__ __forceinline__ void update_and_store(const UpdArgs& u, int opt, int6
 }
 
 // ----------------------------------------------------------------------------- sorted combine
+// fp32 rows (and the bf16 scalar tail): sort fp32 values. The rank window [lo, lo+cnt) is
+// wave-uniform (kernel arguments), so the per-rank test is a scalar branch, not a VALU select.
 template <typename T, int NP, int VEC, int OPT>
 __global__ __launch_bounds__(kBlock) void agg_sorted_kernel(SrcArgs s, UpdArgs u, int64_t base,
                                                             int64_t nvec) {
@@ -92,32 +112,106 @@ __global__ __launch_bounds__(kBlock) void agg_sorted_kernel(SrcArgs s, UpdArgs u
     roff[i] = static_cast<int64_t>(s.rows ? s.rows[r] : r) * s.ld + base;
   }
   const float inf = __builtin_inff();
+  const float inv = 1.0f / static_cast<float>(s.cnt);
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < nvec; t += stride) {
     const int64_t e = t * VEC;
     float a[NP][VEC];
 #pragma unroll
     for (int i = 0; i < NP; ++i) load_vec<T, VEC>(X + roff[i] + e, a[i]);
+    OptState<VEC> st;
+    load_state<VEC>(u, OPT, base + e, st);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const bool pad = i >= s.n;
 #pragma unroll
       for (int v = 0; v < VEC; ++v) a[i][v] = (pad || a[i][v] != a[i][v]) ? inf : a[i][v];
     }
-    sort_columns<NP, VEC>(a);
+    sort_columns<float, NP, VEC>(a);
     float g[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) g[v] = 0.0f;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      const bool take = (i >= s.lo) && (i < s.lo + s.cnt);
+      if (i >= s.lo && i < s.lo + s.cnt) {
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) g[v] += take ? a[i][v] : 0.0f;
+        for (int v = 0; v < VEC; ++v) g[v] += a[i][v];
+      }
     }
-    const float inv = 1.0f / static_cast<float>(s.cnt);
 #pragma unroll
     for (int v = 0; v < VEC; ++v) g[v] *= inv;
-    update_and_store<VEC>(u, OPT, base + e, g);
+    update_and_store<VEC>(u, OPT, base + e, g, st);
+  }
+}
+
+// bf16 rows: sort packed u16 keys (two coordinates per v_pk_min/max_u16, see bf16_key), decode
+// only the cnt window ranks. VEC bf16 = VEC/2 32-bit words per row.
+template <int W> struct Words;
+template <> struct Words<4> {
+  static __device__ __forceinline__ void load(const bf16* p, uint32_t (&w)[4]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    w[0] = u.x; w[1] = u.y; w[2] = u.z; w[3] = u.w;
+  }
+};
+template <> struct Words<2> {
+  static __device__ __forceinline__ void load(const bf16* p, uint32_t (&w)[2]) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    w[0] = u.x; w[1] = u.y;
+  }
+};
+template <> struct Words<1> {
+  static __device__ __forceinline__ void load(const bf16* p, uint32_t (&w)[1]) {
+    w[0] = *reinterpret_cast<const uint32_t*>(p);
+  }
+};
+
+template <int NP, int VEC, int OPT>
+__global__ __launch_bounds__(kBlock) void agg_sorted_bf16_kernel(SrcArgs s, UpdArgs u,
+                                                                 int64_t base, int64_t nvec) {
+  constexpr int W = VEC / 2;
+  const bf16* X = reinterpret_cast<const bf16*>(s.X);
+  int64_t roff[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int r = i < s.n ? i : s.n - 1;
+    roff[i] = static_cast<int64_t>(s.rows ? s.rows[r] : r) * s.ld + base;
+  }
+  const float inv = 1.0f / static_cast<float>(s.cnt);
+  const u16x2 kinf = {kKeyInf, kKeyInf};
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < nvec; t += stride) {
+    const int64_t e = t * VEC;
+    uint32_t raw[NP][W];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) Words<W>::load(X + roff[i] + e, raw[i]);
+    OptState<VEC> st;
+    load_state<VEC>(u, OPT, base + e, st);
+    u16x2 k[NP][W];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const bool pad = i >= s.n;
+#pragma unroll
+      for (int w = 0; w < W; ++w) k[i][w] = pad ? kinf : bf16_key(raw[i][w]);
+    }
+    sort_columns<u16x2, NP, W>(k);
+    float g[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) g[v] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      if (i >= s.lo && i < s.lo + s.cnt) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          float lo, hi;
+          bf16_unkey(k[i][w], lo, hi);
+          g[2 * w] += lo;
+          g[2 * w + 1] += hi;
+        }
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) g[v] *= inv;
+    update_and_store<VEC>(u, OPT, base + e, g, st);
   }
 }
 
@@ -147,6 +241,8 @@ __global__ __launch_bounds__(kBlock) void agg_weighted_kernel(SrcArgs s, UpdArgs
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < nvec; t += stride) {
     const int64_t e = t * VEC;
+    OptState<VEC> st;
+    load_state<VEC>(u, OPT, base + e, st);
     float g[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) g[v] = 0.0f;
@@ -169,7 +265,7 @@ __global__ __launch_bounds__(kBlock) void agg_weighted_kernel(SrcArgs s, UpdArgs
 #pragma unroll
       for (int v = 0; v < VEC; ++v) g[v] = fmaf(w0, x0[v], g[v]);
     }
-    update_and_store<VEC>(u, OPT, base + e, g);
+    update_and_store<VEC>(u, OPT, base + e, g, st);
   }
 }
 
@@ -185,30 +281,37 @@ template <typename T, int NP, int VEC>
 static void launch_sorted_np(int opt, const SrcArgs& s, const UpdArgs& u, int64_t base,
                              int64_t nvec, hipStream_t st) {
   const int g = grid_for(nvec);
-  switch (opt) {
-    case OPT_NONE: agg_sorted_kernel<T, NP, VEC, OPT_NONE><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
-    case OPT_SGD: agg_sorted_kernel<T, NP, VEC, OPT_SGD><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
-    default: agg_sorted_kernel<T, NP, VEC, OPT_ADAM><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+  if constexpr (sizeof(T) == 2 && VEC >= 2) {   // packed-key path
+    switch (opt) {
+      case OPT_NONE: agg_sorted_bf16_kernel<NP, VEC, OPT_NONE><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+      case OPT_SGD: agg_sorted_bf16_kernel<NP, VEC, OPT_SGD><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+      default: agg_sorted_bf16_kernel<NP, VEC, OPT_ADAM><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+    }
+  } else {
+    switch (opt) {
+      case OPT_NONE: agg_sorted_kernel<T, NP, VEC, OPT_NONE><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+      case OPT_SGD: agg_sorted_kernel<T, NP, VEC, OPT_SGD><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+      default: agg_sorted_kernel<T, NP, VEC, OPT_ADAM><<<g, kBlock, 0, st>>>(s, u, base, nvec); break;
+    }
   }
 }
 
-// VEC per padded row count: keep NP*VEC <= 128 fp32 VGPRs of values.
+// Vector width per padded row count (sorted_vec below must agree): bf16 keys take half a VGPR
+// per value, so bf16 keeps 16 B loads up to NP = 32; NP = 64 drops to 2 elements per lane.
 template <typename T, bool VECTOR>
-static void launch_sorted(int opt, const SrcArgs& s, const UpdArgs& u, int64_t base, int64_t nvec_or_n,
+static void launch_sorted(int opt, const SrcArgs& s, const UpdArgs& u, int64_t base, int64_t D,
                           hipStream_t st) {
-  // nvec_or_n: number of elements when !VECTOR (VEC = 1), else computed by caller per NP.
+  // D: number of elements; VECTOR: D is a multiple of sorted_vec() and all pointers aligned.
   const int n = s.n;
   constexpr bool BF = sizeof(T) == 2;
   if constexpr (VECTOR) {
-    const int64_t D = nvec_or_n;
     if (n <= 2) launch_sorted_np<T, 2, BF ? 8 : 4>(opt, s, u, base, D / (BF ? 8 : 4), st);
     else if (n <= 4) launch_sorted_np<T, 4, BF ? 8 : 4>(opt, s, u, base, D / (BF ? 8 : 4), st);
     else if (n <= 8) launch_sorted_np<T, 8, BF ? 8 : 4>(opt, s, u, base, D / (BF ? 8 : 4), st);
     else if (n <= 16) launch_sorted_np<T, 16, BF ? 8 : 4>(opt, s, u, base, D / (BF ? 8 : 4), st);
-    else if (n <= 32) launch_sorted_np<T, 32, BF ? 4 : 4>(opt, s, u, base, D / 4, st);
+    else if (n <= 32) launch_sorted_np<T, 32, BF ? 8 : 4>(opt, s, u, base, D / (BF ? 8 : 4), st);
     else launch_sorted_np<T, 64, 2>(opt, s, u, base, D / 2, st);
   } else {
-    const int64_t D = nvec_or_n;
     if (n <= 2) launch_sorted_np<T, 2, 1>(opt, s, u, base, D, st);
     else if (n <= 4) launch_sorted_np<T, 4, 1>(opt, s, u, base, D, st);
     else if (n <= 8) launch_sorted_np<T, 8, 1>(opt, s, u, base, D, st);
@@ -235,7 +338,6 @@ static inline bool aligned(const void* p, int bytes) {
 
 static int sorted_vec(int dtype, int n) {
   if (n > 32) return 2;
-  if (n > 16) return 4;
   return dtype == DT_BF16 ? 8 : 4;
 }
 

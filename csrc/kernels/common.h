@@ -113,49 +113,83 @@ __device__ __forceinline__ void store_bf16(bf16* __restrict__ p, const float (&v
 }
 
 // ---------------------------------------------------------------- Batcher odd-even merge sort
-// Compile-time network over a[NP][VEC] (sorts every column independently, ascending).
-// NP is a power of two; all indices fold to constants, so a[][] stays in VGPRs.
-template <int VEC>
-__device__ __forceinline__ void cswap(float (&x)[VEC], float (&y)[VEC]) {
+// Compile-time network over a[NP][VEC] of E (sorts every column independently, ascending).
+// NP is a power of two; all indices fold to constants, so a[][] stays in VGPRs. E is float
+// (v_min_f32/v_max_f32: one coordinate per instruction) or u16x2 order-preserving bf16 keys
+// (v_pk_min_u16/v_pk_max_u16: two coordinates per instruction, half the VGPRs).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float vmin(float x, float y) { return fminf(x, y); }
+__device__ __forceinline__ float vmax(float x, float y) { return fmaxf(x, y); }
+__device__ __forceinline__ u16x2 vmin(u16x2 x, u16x2 y) { return __builtin_elementwise_min(x, y); }
+__device__ __forceinline__ u16x2 vmax(u16x2 x, u16x2 y) { return __builtin_elementwise_max(x, y); }
+
+template <typename E, int VEC>
+__device__ __forceinline__ void cswap(E (&x)[VEC], E (&y)[VEC]) {
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
-    float lo = fminf(x[v], y[v]);
-    float hi = fmaxf(x[v], y[v]);
+    E lo = vmin(x[v], y[v]);
+    E hi = vmax(x[v], y[v]);
     x[v] = lo;
     y[v] = hi;
   }
 }
 
-template <int NP, int VEC, int LO, int HI, int R>
+template <typename E, int NP, int VEC, int LO, int HI, int R>
 struct OEMerge {
-  static __device__ __forceinline__ void run(float (&a)[NP][VEC]) {
+  static __device__ __forceinline__ void run(E (&a)[NP][VEC]) {
     constexpr int STEP = R * 2;
     if constexpr (STEP < HI - LO) {
-      OEMerge<NP, VEC, LO, HI, STEP>::run(a);
-      OEMerge<NP, VEC, LO + R, HI, STEP>::run(a);
+      OEMerge<E, NP, VEC, LO, HI, STEP>::run(a);
+      OEMerge<E, NP, VEC, LO + R, HI, STEP>::run(a);
 #pragma unroll
-      for (int i = LO + R; i < HI - R; i += STEP) cswap<VEC>(a[i], a[i + R]);
+      for (int i = LO + R; i < HI - R; i += STEP) cswap<E, VEC>(a[i], a[i + R]);
     } else {
-      cswap<VEC>(a[LO], a[LO + R]);
+      cswap<E, VEC>(a[LO], a[LO + R]);
     }
   }
 };
 
-template <int NP, int VEC, int LO, int HI>
+template <typename E, int NP, int VEC, int LO, int HI>
 struct OESort {
-  static __device__ __forceinline__ void run(float (&a)[NP][VEC]) {
+  static __device__ __forceinline__ void run(E (&a)[NP][VEC]) {
     if constexpr (HI - LO >= 1) {
       constexpr int MID = LO + (HI - LO) / 2;
-      OESort<NP, VEC, LO, MID>::run(a);
-      OESort<NP, VEC, MID + 1, HI>::run(a);
-      OEMerge<NP, VEC, LO, HI, 1>::run(a);
+      OESort<E, NP, VEC, LO, MID>::run(a);
+      OESort<E, NP, VEC, MID + 1, HI>::run(a);
+      OEMerge<E, NP, VEC, LO, HI, 1>::run(a);
     }
   }
 };
 
-template <int NP, int VEC>
-__device__ __forceinline__ void sort_columns(float (&a)[NP][VEC]) {
-  OESort<NP, VEC, 0, NP - 1>::run(a);
+template <typename E, int NP, int VEC>
+__device__ __forceinline__ void sort_columns(E (&a)[NP][VEC]) {
+  OESort<E, NP, VEC, 0, NP - 1>::run(a);
+}
+
+// ---------------------------------------------------------------- bf16 sort keys
+// Two bf16 per 32-bit word -> two unsigned 16-bit keys whose integer order is the value order:
+// the classic float radix key (negative: ~w, positive: w | 0x8000), rotated down by 127 so that
+// the negative NaNs (keys 0..126) wrap above +inf; one v_pk_min_u16 against the +inf key then
+// maps every NaN to +inf (the rules' NaN -> +inf convention). Exhaustively checked over all 65536
+// bf16 patterns in tests/test_reference.py::test_bf16_key_roundtrip (numpy model of these ops).
+constexpr unsigned short kKeyInf = 0xFF01;   // key of +inf: (0x7F80 | 0x8000) - 127
+
+__device__ __forceinline__ u16x2 bf16_key(uint32_t w) {
+  const u16x2 x = __builtin_bit_cast(u16x2, w);
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 sgn = __builtin_bit_cast(u16x2, __builtin_bit_cast(s16x2, x) >> 15);
+  const u16x2 k = (x ^ (sgn | static_cast<unsigned short>(0x8000))) - static_cast<unsigned short>(127);
+  return vmin(k, u16x2{kKeyInf, kKeyInf});
+}
+
+__device__ __forceinline__ void bf16_unkey(u16x2 k, float& lo, float& hi) {
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 uk = k + static_cast<unsigned short>(127);
+  const u16x2 sgn = __builtin_bit_cast(u16x2, __builtin_bit_cast(s16x2, uk) >> 15);
+  const uint32_t w = __builtin_bit_cast(uint32_t, uk ^ (~sgn | static_cast<unsigned short>(0x8000)));
+  lo = __uint_as_float(w << 16);
+  hi = __uint_as_float(w & 0xffff0000u);
 }
 
 // ---------------------------------------------------------------- reductions

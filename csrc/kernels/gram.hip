@@ -5,15 +5,22 @@
 // and on gfx950 the 16x16x32 bf16 MFMA gives lane l A[l&15][8(l>>4)+j] and B[8(l>>4)+j][l&15]:
 // both are X[row l&15][k0 + 8(l>>4) + j]. So one 16-byte load per lane feeds both operands —
 // no LDS staging, no transpose. Rows are grouped in TT tiles of 16 (n <= 16*TT); each wave keeps
-// the upper-triangle tile accumulators (TT(TT+1)/2 x 4 fp32) in AGPRs and walks its own
-// 128-column (256 B per row) slices; D is split across every wave of the grid (split-K).
-// fp32 inputs use the exact-f32 16x16x4 MFMA with the same lane trick (float4 per lane feeds 4
-// MFMAs). The kernel is HBM-bound: 1 KiB per wave-instruction, 4 MFMAs per 4 loads.
+// the upper-triangle tile accumulators (TT(TT+1)/2 x 4 fp32) in AGPRs and walks its own column
+// slices; D is split across every wave of the grid (split-K). fp32 inputs use the exact-f32
+// 16x16x4 MFMA with the same lane trick (float4 per lane feeds 4 MFMAs).
+//
+// Small n (<= 8, the common "one row per GPU" case): a 16-row tile would leave 16-n lanes
+// re-loading duplicate rows. Instead the 16 MFMA rows are G = 16/P2 "virtual rows" per real row
+// (P2 = next pow2 >= n): virtual row g*P2 + i reads row i over column group g. The MFMA then
+// produces a block matrix whose diagonal P2 x P2 blocks are partial Grams over disjoint column
+// groups (off-diagonal blocks are cross-group products and are discarded); summing the diagonal
+// blocks gives X X^T. Every lane loads unique bytes, so HBM bytes in flight per wave double
+// (n = 8) or more. Each lane keeps Q 16-byte loads in flight per iteration (Q = 8 for n <= 32).
 //
 // Stage 1 writes one [P, P] fp32 partial per workgroup (fixed-order LDS reduction of its 4
-// waves); stage 2 sums the partials in fp64 in block order -> bitwise reproducible G.
-// Rows >= n load a valid duplicate row (same cache lines, coalesced in the same instruction) and
-// are zeroed by a select, so no lane-divergent branch sits in front of the loads.
+// waves, folded over column groups); stage 2 sums the partials in fp64 in block order ->
+// bitwise reproducible G. Rows >= n load a valid duplicate row and are zeroed by a select, so
+// no lane-divergent branch sits in front of the loads.
 #include "common.h"
 #include "kernels.h"
 
@@ -30,33 +37,102 @@ __device__ __forceinline__ mfma_bf16x8 as_frag(uint4 u) {
   return __builtin_bit_cast(mfma_bf16x8, u);
 }
 
-// Columns per wave per iteration.
-template <typename T> struct GramCols;
-template <> struct GramCols<bf16> { static constexpr int value = 128; };   // 4 x (16 rows x 32)
-template <> struct GramCols<float> { static constexpr int value = 64; };   // 4 x (16 rows x 16)
+// Elements per lane-load (16 B) and columns covered by one load instruction of the wave.
+template <typename T> struct GramVec;
+template <> struct GramVec<bf16> { static constexpr int vec = 8, step = 32; };
+template <> struct GramVec<float> { static constexpr int vec = 4, step = 16; };
 
-template <typename T, int TT>
+template <int TT> struct GramQ { static constexpr int value = TT <= 2 ? 8 : 4; };
+
+// Columns one wave consumes per main-loop iteration.
+template <typename T, int TT, int G>
+constexpr int gram_cols() { return G * GramQ<TT>::value * GramVec<T>::step; }
+
+// acc[idx] += frag(ta) x frag(tb) over the upper-triangle tiles.
+template <int TT>
+__device__ __forceinline__ void gram_mfma(f32x4* acc, const uint4* u) {
+  int idx = 0;
+#pragma unroll
+  for (int ta = 0; ta < TT; ++ta)
+#pragma unroll
+    for (int tb = ta; tb < TT; ++tb) {
+      acc[idx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(u[ta]), as_frag(u[tb]), acc[idx],
+                                                         0, 0, 0);
+      ++idx;
+    }
+}
+
+template <int TT>
+__device__ __forceinline__ void gram_mfma(f32x4* acc, const float4* u) {
+  int idx = 0;
+#pragma unroll
+  for (int ta = 0; ta < TT; ++ta)
+#pragma unroll
+    for (int tb = ta; tb < TT; ++tb) {
+      acc[idx] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[ta].x, u[tb].x, acc[idx], 0, 0, 0);
+      acc[idx] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[ta].y, u[tb].y, acc[idx], 0, 0, 0);
+      acc[idx] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[ta].z, u[tb].z, acc[idx], 0, 0, 0);
+      acc[idx] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[ta].w, u[tb].w, acc[idx], 0, 0, 0);
+      ++idx;
+    }
+}
+
+template <typename T> struct GramLoad;
+template <> struct GramLoad<bf16> {
+  typedef uint4 type;
+  static __device__ __forceinline__ uint4 zero() { return make_uint4(0, 0, 0, 0); }
+  // guarded load of 8 elements at p[c .. c+8) with columns >= D zero
+  static __device__ __forceinline__ uint4 tail(const bf16* p, int64_t c, int64_t D) {
+    if (c + 8 <= D) return *reinterpret_cast<const uint4*>(p + c);
+    uint16_t t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = c + j < D ? reinterpret_cast<const uint16_t*>(p)[c + j] : 0;
+    return make_uint4(t[0] | (uint32_t(t[1]) << 16), t[2] | (uint32_t(t[3]) << 16),
+                      t[4] | (uint32_t(t[5]) << 16), t[6] | (uint32_t(t[7]) << 16));
+  }
+};
+template <> struct GramLoad<float> {
+  typedef float4 type;
+  static __device__ __forceinline__ float4 zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  static __device__ __forceinline__ float4 tail(const float* p, int64_t c, int64_t D) {
+    if (c + 4 <= D) return *reinterpret_cast<const float4*>(p + c);
+    return make_float4(c < D ? p[c] : 0.f, c + 1 < D ? p[c + 1] : 0.f, c + 2 < D ? p[c + 2] : 0.f,
+                       c + 3 < D ? p[c + 3] : 0.f);
+  }
+};
+
+// G = column-group packing factor (1, or 16/P2 when TT == 1 and n <= 8).
+template <typename T, int TT, int G>
 __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restrict__ X, int64_t ld,
                                                               int n, const int* __restrict__ rows,
                                                               int64_t D, float* __restrict__ part) {
+  static_assert(G == 1 || TT == 1, "column-group packing is for a single row tile");
+  typedef typename GramLoad<T>::type V;
   constexpr int P = 16 * TT;
   constexpr int NT = TT * (TT + 1) / 2;
-  constexpr int COLS = GramCols<T>::value;
+  constexpr int Q = GramQ<TT>::value;
+  constexpr int VEC = GramVec<T>::vec;
+  constexpr int STEP = GramVec<T>::step;
+  constexpr int GSPAN = Q * STEP;           // columns of one group per iteration
+  constexpr int COLS = G * GSPAN;
+  constexpr int P2 = 16 / G;
   __shared__ float red[kGWaves][P * P];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r = lane & 15;
   const int h = lane >> 4;
+  const int grp = r / P2;                   // 0 when G == 1
+  const int vr = r % P2;
 
   const T* rowp[TT];
   bool valid[TT];
 #pragma unroll
   for (int t = 0; t < TT; ++t) {
-    const int row = 16 * t + r;
+    const int row = 16 * t + vr;
     valid[t] = row < n;
     const int rr = valid[t] ? row : (row % n);
-    rowp[t] = X + static_cast<int64_t>(rows ? rows[rr] : rr) * ld;
+    rowp[t] = X + static_cast<int64_t>(rows ? rows[rr] : rr) * ld + grp * GSPAN + VEC * h;
   }
 
   f32x4 acc[NT];
@@ -67,105 +143,30 @@ __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restri
   const int64_t W = static_cast<int64_t>(gridDim.x) * kGWaves;
   const int64_t Dmain = (D / COLS) * COLS;
 
-  if constexpr (sizeof(T) == 2) {
-    for (int64_t k0 = gw * COLS; k0 < Dmain; k0 += W * COLS) {
-      uint4 u[4][TT];
+  for (int64_t k0 = gw * COLS; k0 < Dmain; k0 += W * COLS) {
+    V u[Q][TT];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < Q; ++q)
 #pragma unroll
-        for (int t = 0; t < TT; ++t)
-          u[q][t] = *reinterpret_cast<const uint4*>(rowp[t] + k0 + 32 * q + 8 * h);
+      for (int t = 0; t < TT; ++t) u[q][t] = *reinterpret_cast<const V*>(rowp[t] + k0 + STEP * q);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        mfma_bf16x8 f[TT];
+    for (int q = 0; q < Q; ++q) {
 #pragma unroll
-        for (int t = 0; t < TT; ++t) {
-          uint4 z = valid[t] ? u[q][t] : make_uint4(0, 0, 0, 0);
-          f[t] = as_frag(z);
-        }
-        int idx = 0;
-#pragma unroll
-        for (int ta = 0; ta < TT; ++ta)
-#pragma unroll
-          for (int tb = ta; tb < TT; ++tb) {
-            acc[idx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ta], f[tb], acc[idx], 0, 0, 0);
-            ++idx;
-          }
-      }
+      for (int t = 0; t < TT; ++t) u[q][t] = valid[t] ? u[q][t] : GramLoad<T>::zero();
+      gram_mfma<TT>(acc, u[q]);
     }
-    // Tail columns [Dmain, D): one wave, element-wise guarded loads.
-    if (gw == 0 && Dmain < D) {
-      for (int64_t k0 = Dmain; k0 < D; k0 += 32) {
-        mfma_bf16x8 f[TT];
+  }
+  // Tail [Dmain, D): STEP-column chunks strided over all waves; only column group 0 loads
+  // (the other groups' diagonal blocks just add zeros).
+  for (int64_t k0 = Dmain + gw * STEP; k0 < D; k0 += W * STEP) {
+    V u[TT];
 #pragma unroll
-        for (int t = 0; t < TT; ++t) {
-          uint16_t tmp[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int64_t c = k0 + 8 * h + j;
-            tmp[j] = (valid[t] && c < D) ? reinterpret_cast<const uint16_t*>(rowp[t])[c] : 0;
-          }
-          uint4 z;
-          z.x = tmp[0] | (uint32_t(tmp[1]) << 16);
-          z.y = tmp[2] | (uint32_t(tmp[3]) << 16);
-          z.z = tmp[4] | (uint32_t(tmp[5]) << 16);
-          z.w = tmp[6] | (uint32_t(tmp[7]) << 16);
-          f[t] = as_frag(z);
-        }
-        int idx = 0;
-#pragma unroll
-        for (int ta = 0; ta < TT; ++ta)
-#pragma unroll
-          for (int tb = ta; tb < TT; ++tb) {
-            acc[idx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[ta], f[tb], acc[idx], 0, 0, 0);
-            ++idx;
-          }
-      }
+    for (int t = 0; t < TT; ++t) {
+      const T* base = rowp[t] - grp * GSPAN - VEC * h;
+      u[t] = (valid[t] && grp == 0) ? GramLoad<T>::tail(base, k0 + VEC * h, D)
+                                    : GramLoad<T>::zero();
     }
-  } else {
-    for (int64_t k0 = gw * COLS; k0 < Dmain; k0 += W * COLS) {
-      float4 u[4][TT];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int t = 0; t < TT; ++t)
-          u[q][t] = *reinterpret_cast<const float4*>(rowp[t] + k0 + 16 * q + 4 * h);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float4 f[TT];
-#pragma unroll
-        for (int t = 0; t < TT; ++t) f[t] = valid[t] ? u[q][t] : make_float4(0.f, 0.f, 0.f, 0.f);
-        int idx = 0;
-#pragma unroll
-        for (int ta = 0; ta < TT; ++ta)
-#pragma unroll
-          for (int tb = ta; tb < TT; ++tb) {
-            acc[idx] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[ta].x, f[tb].x, acc[idx], 0, 0, 0);
-            acc[idx] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[ta].y, f[tb].y, acc[idx], 0, 0, 0);
-            acc[idx] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[ta].z, f[tb].z, acc[idx], 0, 0, 0);
-            acc[idx] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[ta].w, f[tb].w, acc[idx], 0, 0, 0);
-            ++idx;
-          }
-      }
-    }
-    if (gw == 0 && Dmain < D) {
-      for (int64_t k0 = Dmain; k0 < D; k0 += 4) {
-        float f[TT];
-#pragma unroll
-        for (int t = 0; t < TT; ++t) {
-          const int64_t c = k0 + h;
-          f[t] = (valid[t] && c < D) ? rowp[t][c] : 0.f;
-        }
-        int idx = 0;
-#pragma unroll
-        for (int ta = 0; ta < TT; ++ta)
-#pragma unroll
-          for (int tb = ta; tb < TT; ++tb) {
-            acc[idx] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[ta], f[tb], acc[idx], 0, 0, 0);
-            ++idx;
-          }
-      }
-    }
+    gram_mfma<TT>(acc, u);
   }
 
   // C/D layout (16x16, dtype independent on gfx950): col = lane & 15, row = 4*(lane>>4) + j.
@@ -190,9 +191,18 @@ __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restri
   for (int e = threadIdx.x; e < P * P; e += kGBlock) {
     const int row = e / P, col = e % P;
     float v = 0.f;
-    if ((row / 16) <= (col / 16)) {   // only upper tiles were written
+    if constexpr (G == 1) {
+      if ((row / 16) <= (col / 16)) {   // only upper tiles were written
 #pragma unroll
-      for (int w = 0; w < kGWaves; ++w) v += red[w][e];
+        for (int w = 0; w < kGWaves; ++w) v += red[w][e];
+      }
+    } else {
+      if (row < P2 && col < P2) {       // fold the diagonal column-group blocks
+#pragma unroll
+        for (int w = 0; w < kGWaves; ++w)
+#pragma unroll
+          for (int g = 0; g < G; ++g) v += red[w][(g * P2 + row) * P + g * P2 + col];
+      }
     }
     out[e] = v;
   }
@@ -227,18 +237,33 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
 int gram_tiles(int n) { return (n + 15) / 16; }
 
 int gram_blocks(int64_t D, int cols) {
-  int64_t b = (D + cols * kGWaves - 1) / (cols * kGWaves);
+  int64_t b = (D + static_cast<int64_t>(cols) * kGWaves - 1) / (static_cast<int64_t>(cols) * kGWaves);
   if (b > kMaxGramBlocks) b = kMaxGramBlocks;
   if (b < 1) b = 1;
   return static_cast<int>(b);
 }
 
-template <typename T, int TT>
+template <typename T, int TT, int G>
 void launch_gram_t(const T* X, int64_t ld, int n, const int* rows, int64_t D, float* part,
-                   double* G, int acc, hipStream_t st) {
-  const int nb = gram_blocks(D, GramCols<T>::value);
-  gram_partial_kernel<T, TT><<<nb, kGBlock, 0, st>>>(X, ld, n, rows, D, part);
-  gram_reduce_kernel<<<(16 * TT) * (16 * TT), 256, 0, st>>>(part, nb, 16 * TT, n, G, acc);
+                   double* Gm, int acc, hipStream_t st) {
+  const int nb = gram_blocks(D, gram_cols<T, TT, G>());
+  gram_partial_kernel<T, TT, G><<<nb, kGBlock, 0, st>>>(X, ld, n, rows, D, part);
+  // (packed launches fold into the top-left block; the reduce skips elements >= n anyway)
+  const int P = 16 * TT;
+  gram_reduce_kernel<<<P * P, 256, 0, st>>>(part, nb, P, n, Gm, acc);
+}
+
+template <typename T>
+void launch_gram_dispatch(const T* x, int64_t ld, int n, const int* rows, int64_t D, float* part,
+                          double* G, int acc, hipStream_t st) {
+  if (n == 1) launch_gram_t<T, 1, 16>(x, ld, n, rows, D, part, G, acc, st);
+  else if (n == 2) launch_gram_t<T, 1, 8>(x, ld, n, rows, D, part, G, acc, st);
+  else if (n <= 4) launch_gram_t<T, 1, 4>(x, ld, n, rows, D, part, G, acc, st);
+  else if (n <= 8) launch_gram_t<T, 1, 2>(x, ld, n, rows, D, part, G, acc, st);
+  else if (n <= 16) launch_gram_t<T, 1, 1>(x, ld, n, rows, D, part, G, acc, st);
+  else if (n <= 32) launch_gram_t<T, 2, 1>(x, ld, n, rows, D, part, G, acc, st);
+  else if (n <= 48) launch_gram_t<T, 3, 1>(x, ld, n, rows, D, part, G, acc, st);
+  else launch_gram_t<T, 4, 1>(x, ld, n, rows, D, part, G, acc, st);
 }
 }  // namespace
 
@@ -254,24 +279,12 @@ hipError_t launch_gram(int dtype, const void* X, int64_t ld, int n, const int* r
   const int vec = 16 / es;
   if ((ld % vec) != 0 || (reinterpret_cast<uintptr_t>(X) % 16) != 0) return hipErrorInvalidValue;
   float* part = reinterpret_cast<float*>(work);
-  const int TT = gram_tiles(n);
-  if (dtype == DT_BF16) {
-    const bf16* x = reinterpret_cast<const bf16*>(X);
-    switch (TT) {
-      case 1: launch_gram_t<bf16, 1>(x, ld, n, rows, D, part, G, accumulate, stream); break;
-      case 2: launch_gram_t<bf16, 2>(x, ld, n, rows, D, part, G, accumulate, stream); break;
-      case 3: launch_gram_t<bf16, 3>(x, ld, n, rows, D, part, G, accumulate, stream); break;
-      default: launch_gram_t<bf16, 4>(x, ld, n, rows, D, part, G, accumulate, stream); break;
-    }
-  } else {
-    const float* x = reinterpret_cast<const float*>(X);
-    switch (TT) {
-      case 1: launch_gram_t<float, 1>(x, ld, n, rows, D, part, G, accumulate, stream); break;
-      case 2: launch_gram_t<float, 2>(x, ld, n, rows, D, part, G, accumulate, stream); break;
-      case 3: launch_gram_t<float, 3>(x, ld, n, rows, D, part, G, accumulate, stream); break;
-      default: launch_gram_t<float, 4>(x, ld, n, rows, D, part, G, accumulate, stream); break;
-    }
-  }
+  if (dtype == DT_BF16)
+    launch_gram_dispatch(reinterpret_cast<const bf16*>(X), ld, n, rows, D, part, G, accumulate,
+                         stream);
+  else
+    launch_gram_dispatch(reinterpret_cast<const float*>(X), ld, n, rows, D, part, G, accumulate,
+                         stream);
   return hipGetLastError();
 }
 

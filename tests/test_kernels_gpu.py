@@ -32,20 +32,44 @@ def test_median_trimmed(cuda, dtype, n, D):
         torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-5)
 
 
-def test_median_nan_and_ties(cuda):
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_median_nan_and_ties(cuda, dtype):
     X = torch.zeros(5, 256, device=cuda)
     X[0] = float("nan")
     X[1] = 1.0
     X[2] = 1.0
     X[3] = -1.0
+    X = X.to(dtype)
+    if dtype == torch.bfloat16:    # negative-sign NaN and -0.0 bit patterns for the u16 keys
+        bits = X.view(torch.int16)
+        bits[0, ::2] = -64          # 0xFFC0: -NaN
+        bits[4, 1::2] = -32768      # 0x8000: -0.0
     got = K.aggregate(X, "median")
-    torch.testing.assert_close(got, R.coord_median(X))
+    torch.testing.assert_close(got, R.coord_median(X.float()))
     assert torch.isfinite(got).all()
+
+
+@pytest.mark.parametrize("n", [4, 8, 16])
+def test_sorted_bf16_extremes(cuda, n):
+    """+-inf, +-NaN, +-0 and subnormal bf16 values through the packed-key sort."""
+    g = torch.Generator(device=cuda).manual_seed(n)
+    X = torch.randn(n, 4096, generator=g, device=cuda).to(torch.bfloat16)
+    bits = X.view(torch.int16)
+    special = torch.tensor([0x7F80, -128, 0x7FC0, -64, 0, -32768, 1, -32767],  # +inf -inf +nan -nan +0 -0 sub -sub
+                           dtype=torch.int16, device=cuda)
+    idx = torch.randint(0, n * 4096, (n * 512,), generator=g, device=cuda)
+    bits.view(-1)[idx] = special[torch.arange(idx.numel(), device=cuda) % 8]
+    Xf = X.float()
+    for lo, cnt in [(n // 2 - 1, 2), (1, n - 2), (0, n)]:
+        got = torch.empty(4096, device=cuda)
+        K.agg_update(X, combine="sorted", lo=lo, cnt=cnt, gout=got)
+        ref = torch.where(torch.isnan(Xf), torch.inf, Xf).sort(0).values[lo:lo + cnt].mean(0)
+        torch.testing.assert_close(got, ref, atol=1e-6, rtol=1e-6, equal_nan=True)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("n", NS)
-@pytest.mark.parametrize("D", [8192, 1000, 37])
+@pytest.mark.parametrize("D", [8192, 1000, 37, 65544])
 def test_gram(cuda, dtype, n, D):
     X = _x(n, D, dtype, cuda, 7 * n)
     G = K.gram(X)
@@ -54,9 +78,11 @@ def test_gram(cuda, dtype, n, D):
     assert (G - ref).abs().max().item() <= 1e-5 * scale + 1e-6
 
 
-def test_gram_asymmetric_rows(cuda):
-    # rows with very different scales catch a transposed / row-swapped C write
-    n, D = 20, 4096
+@pytest.mark.parametrize("n", [3, 7, 20])
+def test_gram_asymmetric_rows(cuda, n):
+    # rows with very different scales catch a transposed / row-swapped C write (and, for n <= 8,
+    # a mis-folded column-group block)
+    D = 20488
     X = torch.randn(n, D, device=cuda) * torch.arange(1, n + 1, device=cuda)[:, None]
     G = K.gram(X)
     torch.testing.assert_close(G, R.gram(X), rtol=1e-5, atol=1e-3)

@@ -147,3 +147,20 @@ def test_sgd_adam_oracles_match_torch():
         o.step()
         p, m, v = R.adam_update(p, g, m, v, i + 1, 0.01, 0.9, 0.999, 1e-8, 0.1, decoupled=True)
     torch.testing.assert_close(p, t.detach(), rtol=1e-6, atol=1e-6)
+
+
+def test_bf16_key_roundtrip():
+    """numpy model of common.h bf16_key / bf16_unkey over all 65536 bf16 bit patterns: the u16
+    key order is the value order, NaN -> +inf, and decoding returns the (NaN -> +inf) value."""
+    import numpy as np
+    w = np.arange(65536, dtype=np.uint32)
+    sgn = np.where(w & 0x8000, 0xFFFF, 0)
+    key = np.minimum(((w ^ (sgn | 0x8000)) - 127) & 0xFFFF, 0xFF01)
+    f = (w << 16).astype(np.uint32).view(np.float32)
+    vals = np.where(np.isnan(f), np.inf, f)
+    srt = vals[np.argsort(key, kind="stable")]
+    assert np.all(srt[1:] >= srt[:-1])
+    uk = (key + 127) & 0xFFFF
+    s2 = np.where(uk & 0x8000, 0xFFFF, 0)
+    back = (((uk ^ ((~s2) | 0x8000)) & 0xFFFF).astype(np.uint32) << 16).view(np.float32)
+    assert np.array_equal(back, vals)
