@@ -85,7 +85,9 @@ def test_gram_asymmetric_rows(cuda, n):
     D = 20488
     X = torch.randn(n, D, device=cuda) * torch.arange(1, n + 1, device=cuda)[:, None]
     G = K.gram(X)
-    torch.testing.assert_close(G, R.gram(X), rtol=1e-5, atol=1e-3)
+    ref = R.gram(X)
+    # fp32 products accumulated in fp32 per lane: error scales with the largest squared norm
+    torch.testing.assert_close(G, ref, rtol=0, atol=1e-7 * ref.diagonal().max().item())
 
 
 def test_gram_accumulate_and_rows(cuda):
