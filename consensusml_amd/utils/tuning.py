@@ -32,9 +32,11 @@ def use_shipped_miopen_db(src: str = SHIPPED_DIR) -> Optional[str]:
         return None
     dst = os.path.join(tempfile.gettempdir(), f"cml_miopen_db_{os.getuid()}")
     os.makedirs(dst, exist_ok=True)
-    for f in files:
+    for f in files:   # every rank of a node may get here at once: copy + atomic rename
         target = os.path.join(dst, f)
         if not os.path.exists(target):
-            shutil.copyfile(os.path.join(src, f), target)
+            tmp = f"{target}.{os.getpid()}.tmp"
+            shutil.copyfile(os.path.join(src, f), tmp)
+            os.replace(tmp, target)
     os.environ["MIOPEN_USER_DB_PATH"] = dst
     return dst
