@@ -118,8 +118,8 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info):
 def main():
     args = parse()
     if not args.no_miopen_find:
-        from consensusml_amd.utils.tuning import use_shipped_miopen_db
-        use_shipped_miopen_db()
+        from consensusml_amd.utils.tuning import configure_miopen
+        configure_miopen()
     from consensusml_amd.parallel.dist import init_distributed
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:

@@ -59,6 +59,8 @@ def main():
     from consensusml_amd import TrainConfig
     from consensusml_amd.parallel.dist import init_distributed
     from consensusml_amd.trainer.trainer import ConsensusTrainer
+    from consensusml_amd.utils.tuning import configure_miopen
+    configure_miopen()
     backend = c.get("backend", "auto")
     if backend == "gloo" and torch.cuda.is_available() and os.environ.get("CML_MLP_GPU") == "1":
         backend = "auto"

@@ -25,8 +25,15 @@ def main(argv=None) -> int:
     ap.add_argument("--watchdog", type=float, default=0.0)
     ap.add_argument("--watchdog-abort", action="store_true")
     ap.add_argument("--eval-batches", type=int, default=2)
+    ap.add_argument("--conv-find", action="store_true",
+                    help="MIOpen find mode for convolutions (shipped find-db, no naive solvers)")
     a = ap.parse_args(argv)
     cfg = from_cli(a)
+    if a.conv_find:
+        import torch
+        from .utils.tuning import configure_miopen
+        configure_miopen()
+        torch.backends.cudnn.benchmark = True
     from .parallel.dist import init_distributed, shutdown
     from .trainer.trainer import ConsensusTrainer
     info = init_distributed(cfg.backend)
