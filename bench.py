@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", action="store_true", help="(reserved) capture step in a hipGraph")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--conv1x1", choices=["gemm", "miopen"], default="gemm",
+                    help="1x1 stride-1 convs as hipBLASLt GEMMs (default) or MIOpen convolutions")
+    ap.add_argument("--profile-marker", action="store_true",
+                    help="launch a spin_kernel between warmup and timed steps (prof_summary --after)")
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="disable MIOpen find mode (torch.backends.cudnn.benchmark) for convs")
     return ap.parse_args()
@@ -91,6 +95,8 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info):
     if info.rank == 0:
         print(f"[bench] {rule}/{topology}: warmup {time.perf_counter() - tw:.1f}s", file=sys.stderr,
               flush=True)
+    if args.profile_marker:
+        torch.cuda._sleep(1000)
     if info.distributed:
         dist.barrier(device_ids=[dev.index])
     torch.cuda.synchronize()
@@ -117,6 +123,8 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info):
 
 def main():
     args = parse()
+    from consensusml_amd.models import resnet as _resnet
+    _resnet.CONV1X1_GEMM = args.conv1x1 == "gemm"
     if not args.no_miopen_find:
         from consensusml_amd.utils.tuning import configure_miopen
         configure_miopen()
@@ -157,6 +165,7 @@ def main():
                        "image_size": args.image_size, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{n}", "rule": args.rule, "f": main_res["f"],
                        "topology": args.topology, "optimizer": "sgd-momentum (fused HIP)",
+                       "conv1x1": args.conv1x1,
                        "params": main_res["params"], "buckets": main_res["buckets"]},
             "allreduce_ms_per_step": None if base_ms is None else round(base_ms, 3),
             "agg_overhead_vs_allreduce": None if overhead is None else round(overhead, 4),

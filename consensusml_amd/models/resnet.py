@@ -8,14 +8,73 @@ BASELINE.json config: "ResNet-50 bf16 DP=8 with Krum".
 """
 from __future__ import annotations
 
-from typing import List
+import os
+from typing import List, Optional
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.bn import BatchNormAct2d
+from ..ops.bn import BatchNormAct2d, ResidualLink, fused_ok
 from ..ops.pool import max_pool2d
+
+# 1x1 stride-1 convolutions as plain GEMMs (see Conv1x1); toggled by bench.py --conv1x1.
+CONV1X1_GEMM = os.environ.get("CML_CONV1X1_GEMM", "1") == "1"
+# identity blocks fuse the residual-gradient add into conv1's dX GEMM (see ops.bn.ResidualLink)
+RESIDUAL_LINK = True
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    """y = x W^T on [M, Cin] rows; backward dX = dY W accumulated into a linked residual
+    gradient when one is parked (ResidualLink), dW = dY^T X."""
+
+    @staticmethod
+    def forward(ctx, x2d, w2d, link):
+        ctx.save_for_backward(x2d, w2d)
+        ctx.link = link
+        return torch.mm(x2d, w2d.t())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2d, w2d = ctx.saved_tensors
+        dx = None
+        if ctx.needs_input_grad[0]:
+            link = ctx.link
+            if link is not None and link.grad is not None:
+                g = link.grad
+                link.grad = None
+                dres = g.permute(0, 2, 3, 1).reshape(dy.shape[0], -1) if g.dim() == 4 else g
+                if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
+                    dx = dres.addmm_(dy, w2d)          # beta = 1 GEMM epilogue, in place
+                else:
+                    dx = torch.addmm(dres, dy, w2d)
+            else:
+                dx = torch.mm(dy, w2d)
+        dw = torch.mm(dy.t(), x2d) if ctx.needs_input_grad[1] else None
+        return dx, dw, None
+
+
+class Conv1x1(nn.Conv2d):
+    """1x1 convolution. With stride 1 on a channels_last GPU tensor, the NHWC activation IS a
+    row-major [N*H*W, C] matrix, so the conv is one GEMM (``F.linear`` -> hipBLASLt) and its
+    backward two more (dX = dY W, dW = dY^T X) — no im2col, no layout change, output already
+    channels_last. These are 8/17 of a bottleneck's FLOPs. Strided 1x1 (downsample) convs and CPU
+    tensors use the regular MIOpen / ATen convolution. Same parameter as nn.Conv2d."""
+
+    def __init__(self, cin: int, cout: int, stride: int = 1):
+        super().__init__(cin, cout, 1, stride=stride, bias=False)
+
+    def gemm_ok(self, x: torch.Tensor) -> bool:
+        return (CONV1X1_GEMM and self.stride == (1, 1) and x.is_cuda
+                and x.is_contiguous(memory_format=torch.channels_last))
+
+    def forward(self, x: torch.Tensor, res_link: Optional[ResidualLink] = None) -> torch.Tensor:
+        if self.gemm_ok(x):
+            N, C, H, W = x.shape
+            y = _Conv1x1Fn.apply(x.permute(0, 2, 3, 1).reshape(N * H * W, C),
+                                 self.weight.reshape(self.out_channels, C), res_link)
+            return y.view(N, H, W, self.out_channels).permute(0, 3, 1, 2)
+        return super().forward(x)
 
 
 class Bottleneck(nn.Module):
@@ -23,20 +82,27 @@ class Bottleneck(nn.Module):
 
     def __init__(self, inplanes: int, planes: int, stride: int = 1, downsample: bool = False):
         super().__init__()
-        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.conv1 = Conv1x1(inplanes, planes)
         self.bn1 = BatchNormAct2d(planes, relu=True)
         self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
         self.bn2 = BatchNormAct2d(planes, relu=True)
-        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.conv3 = Conv1x1(planes, planes * 4)
         self.bn3 = BatchNormAct2d(planes * 4, relu=True)      # + residual, fused
         if downsample:
-            self.down_conv = nn.Conv2d(inplanes, planes * 4, 1, stride=stride, bias=False)
+            self.down_conv = Conv1x1(inplanes, planes * 4, stride=stride)
             self.down_bn = BatchNormAct2d(planes * 4, relu=False)
         else:
             self.down_conv = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        idt = x if self.down_conv is None else self.down_bn(self.down_conv(x))
+        if self.down_conv is None:
+            # identity block: conv1's backward GEMM accumulates into bn3's residual gradient
+            link = (ResidualLink() if RESIDUAL_LINK and torch.is_grad_enabled() and self.training
+                    and self.conv1.gemm_ok(x) and fused_ok(x, self.bn3.weight) else None)
+            out = self.bn1(self.conv1(x, res_link=link))
+            out = self.bn2(self.conv2(out))
+            return self.bn3(self.conv3(out), residual=x, res_link=link)
+        idt = self.down_bn(self.down_conv(x))
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
         return self.bn3(self.conv3(out), residual=idt)

@@ -16,23 +16,48 @@ import torch.nn.functional as F
 from .native import lib
 
 
+class ResidualLink:
+    """Hand-off of a residual gradient from a fused BN(+residual) backward to the GEMM that
+    produces the other half of the same tensor's gradient.
+
+    In a ResNet block ``x -> conv1 ... bn3(., residual=x)``, autograd would materialise
+    dres = d(bn3)/d(residual) and later add it to conv1's dX with a separate elementwise kernel
+    (read 2 tensors, write 1). With a link, the BN backward parks dres here and returns no
+    gradient for the residual; conv1's backward (``models.resnet._Conv1x1Fn``) then accumulates
+    its dX GEMM straight into dres (``addmm_``: beta = 1 epilogue), so the add kernel and one
+    full activation write disappear. bn3's backward always runs before conv1's (conv1's output
+    gradient depends on it), so the hand-off is ordered by the graph itself."""
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, res, rmean, rvar, mean_in, invstd_in, eps, momentum, relu,
-                training):
+                training, link):
         y, mean, invstd = lib().bn_fwd(x, res, gamma, beta, rmean, rvar, mean_in, invstd_in,
                                        eps, momentum, relu, training)
         ctx.save_for_backward(x, res, gamma, beta, mean, invstd)
         ctx.relu = relu
         ctx.has_res = res is not None
+        ctx.link = link
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, res, gamma, beta, mean, invstd = ctx.saved_tensors
         dx, dg, db, dres = lib().bn_bwd(dy, x, res, gamma, beta, mean, invstd, ctx.relu)
+        if ctx.has_res and ctx.link is not None:
+            ctx.link.grad = dres
+            dres = None
         return (dx, dg, db, dres if ctx.has_res else None, None, None, None, None, None, None,
-                None, None)
+                None, None, None)
+
+
+def fused_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
+    return _fused_ok(x, gamma)
 
 
 def _fused_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
@@ -47,15 +72,18 @@ def _fused_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
 def bn_act(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
            running_mean: Optional[torch.Tensor], running_var: Optional[torch.Tensor],
            residual: Optional[torch.Tensor] = None, relu: bool = True, training: bool = True,
-           momentum: float = 0.1, eps: float = 1e-5) -> torch.Tensor:
+           momentum: float = 0.1, eps: float = 1e-5,
+           res_link: Optional[ResidualLink] = None) -> torch.Tensor:
+    """``res_link``: see ResidualLink; only honoured on the fused path (the caller checks
+    ``fused_ok`` before relying on it)."""
     if _fused_ok(x, gamma) and (residual is None or residual.is_contiguous(
             memory_format=torch.channels_last)):
         if training:
             return _BNActFn.apply(x, gamma, beta, residual, running_mean, running_var, None, None,
-                                  eps, momentum, relu, True)
+                                  eps, momentum, relu, True, res_link)
         invstd = torch.rsqrt(running_var.float() + eps)
         return _BNActFn.apply(x, gamma, beta, residual, None, None, running_mean.float(), invstd,
-                              eps, momentum, relu, False)
+                              eps, momentum, relu, False, res_link)
     # reference composition (CPU / unsupported layouts)
     y = F.batch_norm(x, running_mean, running_var, gamma, beta, training, momentum, eps) \
         if running_mean is None or running_mean.dtype == x.dtype else \
@@ -94,9 +122,10 @@ class BatchNormAct2d(nn.Module):
                 self._buffers[k] = b.float()
         return self
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                res_link: Optional[ResidualLink] = None) -> torch.Tensor:
         return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual,
-                      self.relu, self.training, self.momentum, self.eps)
+                      self.relu, self.training, self.momentum, self.eps, res_link)
 
     def extra_repr(self) -> str:
         return f"{self.num_features}, relu={self.relu}"
