@@ -54,6 +54,10 @@ class TreeBatch:
 
     def predict(self, Xb: torch.Tensor) -> torch.Tensor:
         """Leaf values [T, m] for binned rows Xb [m, p]."""
+        return torch.gather(self.value, 1, self.apply(Xb))
+
+    def apply(self, Xb: torch.Tensor) -> torch.Tensor:
+        """Leaf node ids [T, m] for binned rows Xb [m, p]."""
         T = self.feature.shape[0]
         m = Xb.shape[0]
         node = torch.zeros(T, m, dtype=torch.long, device=Xb.device)
@@ -65,7 +69,7 @@ class TreeBatch:
             thr = torch.gather(self.thr_bin, 1, node)
             child = 2 * node + 1 + (b > thr).long()
             node = torch.where(leaf, node, child)
-        return torch.gather(self.value, 1, node)
+        return node
 
 
 def grow(Xb: torch.Tensor, stat: torch.Tensor, depth: int, k: int, n_bins: int, crit: str,
@@ -202,6 +206,20 @@ class HistForest:
 
     def predict(self, X: torch.Tensor) -> torch.Tensor:
         return (self.predict_proba(X)[:, 1] > 0.5).long()
+
+    def proximity(self, X: torch.Tensor) -> torch.Tensor:
+        """randomForest(proximity=TRUE): fraction of trees in which two rows share a leaf
+        ([m, m]); accumulated per tree chunk as one-hot(leaf) GEMMs on the device."""
+        Xb = bin_with(X, self.edges)
+        m = Xb.shape[0]
+        P = torch.zeros(m, m, device=Xb.device)
+        for tb in self.batches:
+            leaves = tb.apply(Xb)                                      # [T, m]
+            nodes = tb.feature.shape[1]
+            oh = torch.zeros(leaves.shape[0], m, nodes, device=Xb.device)
+            oh.scatter_(2, leaves[..., None], 1.0)
+            P += torch.einsum("tin,tjn->ij", oh, oh)
+        return P / self.n
 
     @property
     def feature_importances_(self) -> torch.Tensor:

@@ -295,3 +295,66 @@ def xgboost_tuner(X_train, X_test, y_train, y_test, n_estimators_num: Sequence[i
         m = GradientBoostedTrees(100 * k, 0.01, 6, seed=seed).fit(X_train, y_train)
         out[100 * k] = log_loss(y_test.cpu(), m.predict_proba(X_test)[:, 1].cpu())
     return out
+
+
+# ============================================================================ R result lists
+def _perf_testset(y_test: torch.Tensor, prob1: torch.Tensor) -> Dict[str, object]:
+    """``performance_testset`` of the XGB result list (`cml_targetaml_seanalysis.Rmd:1198-1224`):
+    confusion matrix (rows predicted 0/1, cols observed 0/1), mean_err, tpr, tnr, fdr, for —
+    computed from THIS model's predictions (the reference reused a stale ``pred1``, §4.3)."""
+    yt = y_test.cpu().long()
+    pb = (prob1.cpu() > 0.5).long()
+    cm = torch.zeros(2, 2, dtype=torch.long)
+    for a, b in zip(pb.tolist(), yt.tolist()):
+        cm[a, b] += 1
+    tp, fp, tn, fn = int(cm[1, 1]), int(cm[1, 0]), int(cm[0, 0]), int(cm[0, 1])
+    pos, neg = int((yt == 1).sum()), int((yt == 0).sum())
+
+    def div(a, b):
+        return a / b if b else float("nan")
+    return {"confusion_matrix": cm, "mean_err": float((pb != yt).float().mean()),
+            "tpr": div(tp, pos), "tnr": div(tn, neg), "fdr": 1 - div(tp, tp + fp),
+            "for": 1 - div(tn, tn + fn)}
+
+
+XGB_REPS = ((2, 1.0, 2), (50, 1.0, 2), (50, 1.0, 50), (100, 1.0, 50), (100, 1.0, 100))
+
+
+def xgb_resultslist(X_train, y_train, X_test, y_test, reps=XGB_REPS, seed: int = 8):
+    """C25 (`cml_targetaml_seanalysis.Rmd:1148-1239`): the five xgboost configs
+    (max_depth, eta, nrounds); per rep ``{"model", "importance", "performance_testset"}`` plus
+    ``"testperfdf"`` (pandas, rows rep1..repK, cols mean_err/tpr/tnr/fdr/for)."""
+    import pandas as pd
+    out: Dict[str, object] = {}
+    rows = []
+    for i, (depth, eta, rounds) in enumerate(reps, 1):
+        m = GradientBoostedTrees(rounds, eta, depth, seed=seed).fit(X_train, y_train)
+        perf = _perf_testset(y_test, m.predict_proba(X_test)[:, 1])
+        out[f"rep{i}"] = {"model": m, "importance": m.feature_importances_,
+                          "performance_testset": perf, "params": {"max_depth": depth, "eta": eta,
+                                                                  "nrounds": rounds}}
+        rows.append({k: perf[k] for k in ("mean_err", "tpr", "tnr", "fdr", "for")})
+    out["testperfdf"] = pd.DataFrame(rows, index=[f"rep{i}" for i in range(1, len(reps) + 1)])
+    return out
+
+
+def rf_resultslist(X_train, y_train, X_test, y_test, ntrees=(2000, 5000, 10000),
+                   seed: int = 50, proximity: bool = True):
+    """C24 (`cml_targetaml_seanalysis.Rmd:1022-1069`): randomForest with 2k / 5k / 10k trees and
+    proximity; ``{"rf2k_results": {"fitmodel", "conf_matrix", "proximity",
+    "mean_decrease_gini"}, ...}`` with conf_matrix rows observed / cols predicted like R's
+    ``table(observed, predicted)``. Trees are grown with the device histogram forest."""
+    from .hist_trees import HistForest
+    out: Dict[str, object] = {}
+    yt = y_test.cpu().long()
+    for T in ntrees:
+        m = HistForest(T, max_depth=12, seed=seed).fit(X_train, y_train)
+        pred = m.predict(X_test).cpu()
+        cm = torch.zeros(2, 2, dtype=torch.long)
+        for a, b in zip(yt.tolist(), pred.tolist()):
+            cm[a, b] += 1
+        key = f"rf{T // 1000}k_results" if T % 1000 == 0 else f"rf{T}_results"
+        out[key] = {"fitmodel": m, "conf_matrix": cm, "mean_decrease_gini": m.mean_decrease_gini}
+        if proximity:
+            out[key]["proximity"] = m.proximity(X_train).cpu()
+    return out

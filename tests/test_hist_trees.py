@@ -47,3 +47,26 @@ def test_depth_zero_is_prior():
     f = HistForest(10, 0, seed=0).fit(X, y)
     p = f.predict_proba(X)[:, 1]
     assert torch.allclose(p, p[0].expand_as(p))
+
+
+def test_rf_and_xgb_resultslists():
+    from consensusml_amd.select.trees import rf_resultslist, xgb_resultslist
+    torch.manual_seed(0)
+    n, p = 80, 12
+    X = torch.randn(n, p)
+    y = (X[:, 0] + 0.5 * X[:, 1] > 0).long()
+    rf = rf_resultslist(X[:60], y[:60], X[60:], y[60:], ntrees=(200, 1000))
+    assert set(rf) == {"rf200_results", "rf1k_results"}
+    r = rf["rf1k_results"]
+    assert int(r["conf_matrix"].sum()) == 20 and r["conf_matrix"].trace() >= 15
+    P = r["proximity"]
+    assert P.shape == (60, 60) and torch.allclose(P.diagonal(), torch.ones(60))
+    assert torch.allclose(P, P.t()) and (P >= 0).all() and (P <= 1).all()
+    xg = xgb_resultslist(X[:60], y[:60], X[60:], y[60:])
+    df = xg["testperfdf"]
+    assert list(df.index) == [f"rep{i}" for i in range(1, 6)]
+    assert list(df.columns) == ["mean_err", "tpr", "tnr", "fdr", "for"]
+    for i in range(1, 6):
+        perf = xg[f"rep{i}"]["performance_testset"]
+        assert abs(perf["mean_err"] - df.loc[f"rep{i}", "mean_err"]) < 1e-12
+        assert int(perf["confusion_matrix"].sum()) == 20
