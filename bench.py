@@ -46,8 +46,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", action="store_true", help="(reserved) capture step in a hipGraph")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--conv1x1", choices=["gemm", "miopen"], default="gemm",
-                    help="1x1 stride-1 convs as hipBLASLt GEMMs (default) or MIOpen convolutions")
+    ap.add_argument("--conv1x1", choices=["gemm", "miopen"], default="miopen",
+                    help="1x1 stride-1 convs as MIOpen convolutions (default) or hipBLASLt GEMMs")
     ap.add_argument("--profile-marker", action="store_true",
                     help="launch a spin_kernel between warmup and timed steps (prof_summary --after)")
     ap.add_argument("--no-miopen-find", action="store_true",

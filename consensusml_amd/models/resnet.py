@@ -19,7 +19,10 @@ from ..ops.bn import BatchNormAct2d, ResidualLink, fused_ok
 from ..ops.pool import max_pool2d
 
 # 1x1 stride-1 convolutions as plain GEMMs (see Conv1x1); toggled by bench.py --conv1x1.
-CONV1X1_GEMM = os.environ.get("CML_CONV1X1_GEMM", "1") == "1"
+# Off by default: measured on MI355X at batch 512 the hipBLASLt kernels chosen for these
+# tall-skinny shapes (e.g. dW with K = N*H*W = 1.6M and a 64x64 output tile grid of 4) made the
+# step 77 ms vs 55 ms with MIOpen's 1x1 solvers (profiles/r01_bench8_conv1x1_gemm_kernels.md).
+CONV1X1_GEMM = os.environ.get("CML_CONV1X1_GEMM", "0") == "1"
 # identity blocks fuse the residual-gradient add into conv1's dX GEMM (see ops.bn.ResidualLink)
 RESIDUAL_LINK = True
 

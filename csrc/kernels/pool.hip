@@ -17,11 +17,16 @@ constexpr int kPB = 256;
 // thread needs one 32-bit division (w, g from its row offset) instead of three 64-bit div/mods
 // (64-bit integer division is a long emulated sequence on CDNA and made the first version of the
 // backward VALU-bound at 2.2 TB/s).
+// Forward. KK = compile-time window size (3 for the stem; 0 = runtime k): with KK fixed the
+// KK*KK 16-byte loads of a window are all in flight before the max (out-of-image taps load a
+// clamped in-image address and are masked).
+template <int KK>
 __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict__ x,
                                                          bf16* __restrict__ y,
                                                          uint8_t* __restrict__ idx, int N, int H,
-                                                         int W, int C, int OH, int OW, int k, int s,
-                                                         int p) {
+                                                         int W, int C, int OH, int OW, int k_rt,
+                                                         int s, int p) {
+  const int k = KK > 0 ? KK : k_rt;
   const int cg = C / 8;
   const int i = blockIdx.x * kPB + threadIdx.x;
   if (i >= OW * cg) return;
@@ -37,20 +42,45 @@ __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict
       best[v] = -__builtin_inff();
       arg[v] = 0;
     }
-    for (int a = 0; a < k; ++a) {
-      const int h = oh * s - p + a;
-      if (h < 0 || h >= H) continue;
-      const bf16* xrow = x + (static_cast<int64_t>(n) * H + h) * W * C + 8 * g;
-      for (int b = 0; b < k; ++b) {
-        const int w = ow * s - p + b;
-        if (w < 0 || w >= W) continue;
-        float v8[8];
-        load_vec<bf16, 8>(xrow + static_cast<int64_t>(w) * C, v8);
+    if constexpr (KK > 0) {
+      float t[KK][KK][8];
+      bool in[KK][KK];
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-          const bool take = v8[v] > best[v] || (v8[v] != v8[v]);   // NaN propagates
-          best[v] = take ? v8[v] : best[v];
-          arg[v] = take ? static_cast<uint8_t>(a * k + b) : arg[v];
+      for (int a = 0; a < KK; ++a)
+#pragma unroll
+        for (int b = 0; b < KK; ++b) {
+          const int h = oh * s - p + a, w = ow * s - p + b;
+          in[a][b] = h >= 0 && h < H && w >= 0 && w < W;
+          const int hh = in[a][b] ? h : 0, ww = in[a][b] ? w : 0;
+          load_vec<bf16, 8>(x + ((static_cast<int64_t>(n) * H + hh) * W + ww) * C + 8 * g, t[a][b]);
+        }
+#pragma unroll
+      for (int a = 0; a < KK; ++a)
+#pragma unroll
+        for (int b = 0; b < KK; ++b)
+#pragma unroll
+          for (int v = 0; v < 8; ++v) {
+            const float val = t[a][b][v];
+            const bool take = in[a][b] && (val > best[v] || (val != val));   // NaN propagates
+            best[v] = take ? val : best[v];
+            arg[v] = take ? static_cast<uint8_t>(a * KK + b) : arg[v];
+          }
+    } else {
+      for (int a = 0; a < k; ++a) {
+        const int h = oh * s - p + a;
+        if (h < 0 || h >= H) continue;
+        const bf16* xrow = x + (static_cast<int64_t>(n) * H + h) * W * C + 8 * g;
+        for (int b = 0; b < k; ++b) {
+          const int w = ow * s - p + b;
+          if (w < 0 || w >= W) continue;
+          float v8[8];
+          load_vec<bf16, 8>(xrow + static_cast<int64_t>(w) * C, v8);
+#pragma unroll
+          for (int v = 0; v < 8; ++v) {
+            const bool take = v8[v] > best[v] || (v8[v] != v8[v]);
+            best[v] = take ? v8[v] : best[v];
+            arg[v] = take ? static_cast<uint8_t>(a * k + b) : arg[v];
+          }
         }
       }
     }
@@ -63,6 +93,11 @@ __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict
   }
 }
 
+// Backward. KS = ceil(k / s) candidate windows per dimension (2 for the 3x3/s2 stem): with KS a
+// compile-time constant all KS*KS (idx, dy) loads of a pixel are issued before any is consumed
+// (invalid windows load a clamped valid address and contribute zero), instead of a
+// load-wait-accumulate loop per window.
+template <int KS>
 __global__ __launch_bounds__(kPB) void maxpool_bwd_kernel(const bf16* __restrict__ dy,
                                                          const uint8_t* __restrict__ idx,
                                                          bf16* __restrict__ dx, int N, int H, int W,
@@ -73,32 +108,44 @@ __global__ __launch_bounds__(kPB) void maxpool_bwd_kernel(const bf16* __restrict
   if (i0 >= W * cg) return;
   const int w = i0 / cg;
   const int g = i0 - w * cg;
-  // windows ow with ow*s - p <= w <= ow*s - p + k - 1
-  const int ow0 = max(0, (w + p - k + s) / s), ow1 = min(OW - 1, (w + p) / s);
+  // windows ow with ow*s - p <= w <= ow*s - p + k - 1, i.e. ow in [ow0, ow1], ow1 - ow0 < KS
+  const int ow1 = min(OW - 1, (w + p) / s);
   for (int row = blockIdx.y; row < N * H; row += gridDim.y) {
     const int n = row / H;
     const int h = row - n * H;
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int oh0 = max(0, (h + p - k + s) / s), oh1 = min(OH - 1, (h + p) / s);
-    for (int oh = oh0; oh <= oh1; ++oh) {
-      const int a = h - (oh * s - p);
-      if (a < 0 || a >= k) continue;
-      const int64_t orow = (static_cast<int64_t>(n) * OH + oh) * OW;
-      for (int ow = ow0; ow <= ow1; ++ow) {
-        const int b = w - (ow * s - p);
-        if (b < 0 || b >= k) continue;
-        const uint32_t me = static_cast<uint32_t>(a * k + b);
-        const int64_t o = (orow + ow) * C + 8 * g;
-        const uint2 m = *reinterpret_cast<const uint2*>(idx + o);
-        float d8[8];
-        load_vec<bf16, 8>(dy + o, d8);
+    const int oh1 = min(OH - 1, (h + p) / s);
+    uint2 m[KS][KS];
+    float d[KS][KS][8];
+    bool ok[KS][KS];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          acc[v] += (((m.x >> (8 * v)) & 0xff) == me) ? d8[v] : 0.f;
-          acc[v + 4] += (((m.y >> (8 * v)) & 0xff) == me) ? d8[v + 4] : 0.f;
-        }
+    for (int a = 0; a < KS; ++a) {
+      const int oh = oh1 - a;
+      const int ia = h - (oh * s - p);
+      const bool oka = oh >= 0 && ia >= 0 && ia < k;
+#pragma unroll
+      for (int b = 0; b < KS; ++b) {
+        const int ow = ow1 - b;
+        const int ib = w - (ow * s - p);
+        ok[a][b] = oka && ow >= 0 && ib >= 0 && ib < k;
+        const int64_t o = ((static_cast<int64_t>(n) * OH + (ok[a][b] ? oh : 0)) * OW +
+                           (ok[a][b] ? ow : 0)) * C + 8 * g;
+        m[a][b] = *reinterpret_cast<const uint2*>(idx + o);
+        load_vec<bf16, 8>(dy + o, d[a][b]);
       }
     }
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int a = 0; a < KS; ++a)
+#pragma unroll
+      for (int b = 0; b < KS; ++b) {
+        const int ia = h - ((oh1 - a) * s - p), ib = w - ((ow1 - b) * s - p);
+        const uint32_t me = ok[a][b] ? static_cast<uint32_t>(ia * k + ib) : 0xffffffffu;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          acc[v] += (((m[a][b].x >> (8 * v)) & 0xff) == me) ? d[a][b][v] : 0.f;
+          acc[v + 4] += (((m[a][b].y >> (8 * v)) & 0xff) == me) ? d[a][b][v + 4] : 0.f;
+        }
+      }
     store_bf16<8>(dx + (static_cast<int64_t>(row) * W + w) * C + 8 * g, acc);
   }
 }
@@ -113,9 +160,12 @@ hipError_t launch_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, i
                               int OH, int OW, int k, int s, int p, hipStream_t st) {
   if (C % 8 || k * k > 255) return hipErrorInvalidValue;
   if (N * OH < 1) return hipErrorInvalidValue;
-  maxpool_fwd_kernel<<<pgrid(OW * (C / 8), N * OH), kPB, 0, st>>>(
-      reinterpret_cast<const bf16*>(x), reinterpret_cast<bf16*>(y),
-      reinterpret_cast<uint8_t*>(idx), N, H, W, C, OH, OW, k, s, p);
+  const dim3 grid = pgrid(OW * (C / 8), N * OH);
+  const bf16* xp = reinterpret_cast<const bf16*>(x);
+  bf16* yp = reinterpret_cast<bf16*>(y);
+  uint8_t* ip = reinterpret_cast<uint8_t*>(idx);
+  if (k == 3) maxpool_fwd_kernel<3><<<grid, kPB, 0, st>>>(xp, yp, ip, N, H, W, C, OH, OW, k, s, p);
+  else maxpool_fwd_kernel<0><<<grid, kPB, 0, st>>>(xp, yp, ip, N, H, W, C, OH, OW, k, s, p);
   return hipGetLastError();
 }
 
@@ -123,9 +173,17 @@ hipError_t launch_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, 
                               int C, int OH, int OW, int k, int s, int p, hipStream_t st) {
   if (C % 8 || k * k > 255) return hipErrorInvalidValue;
   if (N * H < 1) return hipErrorInvalidValue;
-  maxpool_bwd_kernel<<<pgrid(W * (C / 8), N * H), kPB, 0, st>>>(
-      reinterpret_cast<const bf16*>(dy), reinterpret_cast<const uint8_t*>(idx),
-      reinterpret_cast<bf16*>(dx), N, H, W, C, OH, OW, k, s, p);
+  const int ks = (k + s - 1) / s;
+  const dim3 grid = pgrid(W * (C / 8), N * H);
+  const bf16* dyp = reinterpret_cast<const bf16*>(dy);
+  const uint8_t* ip = reinterpret_cast<const uint8_t*>(idx);
+  bf16* dxp = reinterpret_cast<bf16*>(dx);
+  switch (ks) {
+    case 1: maxpool_bwd_kernel<1><<<grid, kPB, 0, st>>>(dyp, ip, dxp, N, H, W, C, OH, OW, k, s, p); break;
+    case 2: maxpool_bwd_kernel<2><<<grid, kPB, 0, st>>>(dyp, ip, dxp, N, H, W, C, OH, OW, k, s, p); break;
+    case 3: maxpool_bwd_kernel<3><<<grid, kPB, 0, st>>>(dyp, ip, dxp, N, H, W, C, OH, OW, k, s, p); break;
+    default: return hipErrorInvalidValue;   // caller falls back to PyTorch
+  }
   return hipGetLastError();
 }
 

@@ -95,15 +95,18 @@ def test_resnet_tiny_fused_vs_reference(cuda):
     torch.testing.assert_close(out, out_ref, rtol=0.1, atol=0.15)
 
 
-@pytest.mark.parametrize("shape", [(2, 64, 112, 112), (3, 16, 9, 7)])
-def test_maxpool_nhwc(cuda, shape):
+@pytest.mark.parametrize("shape,ksp", [((2, 64, 112, 112), (3, 2, 1)), ((3, 16, 9, 7), (3, 2, 1)),
+                                       ((2, 16, 10, 9), (2, 2, 0)), ((2, 8, 9, 11), (3, 1, 1)),
+                                       ((2, 8, 13, 12), (5, 2, 2))])
+def test_maxpool_nhwc(cuda, shape, ksp):
     from consensusml_amd.ops.pool import max_pool2d
+    k, s, p = ksp
     torch.manual_seed(1)
     x = torch.randn(*shape, device=cuda).to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last).requires_grad_(True)
-    y = max_pool2d(x, 3, 2, 1)
+    y = max_pool2d(x, k, s, p)
     xr = x.detach().float().requires_grad_(True)
-    yr = F.max_pool2d(xr, 3, 2, 1)
+    yr = F.max_pool2d(xr, k, s, p)
     torch.testing.assert_close(y.float(), yr)
     dy = torch.randn_like(yr)
     y.backward(dy.to(torch.bfloat16))
