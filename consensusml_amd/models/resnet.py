@@ -98,17 +98,28 @@ class Bottleneck(nn.Module):
             self.down_conv = None
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        use_links = RESIDUAL_LINK and torch.is_grad_enabled() and self.training
         if self.down_conv is None:
-            # identity block: conv1's backward GEMM accumulates into bn3's residual gradient
-            link = (ResidualLink() if RESIDUAL_LINK and torch.is_grad_enabled() and self.training
-                    and self.conv1.gemm_ok(x) and fused_ok(x, self.bn3.weight) else None)
-            out = self.bn1(self.conv1(x, res_link=link))
+            # identity block: bn3's residual gradient is parked on the link of our input (made by
+            # the producing block); conv1's GEMM backward (if used) or the producer's BN backward
+            # consumes it (see ops.bn.ResidualLink)
+            link = getattr(x, "_cml_link", None) if use_links else None
+            out = self.bn1(self.conv1(x, res_link=link if self.conv1.gemm_ok(x) else None))
             out = self.bn2(self.conv2(out))
-            return self.bn3(self.conv3(out), residual=x, res_link=link)
-        idt = self.down_bn(self.down_conv(x))
-        out = self.bn1(self.conv1(x))
-        out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), residual=idt)
+            z = self.conv3(out)
+            fused = fused_ok(z, self.bn3.weight)
+            out_link = ResidualLink() if use_links and fused else None
+            y = self.bn3(z, residual=x, res_link=link if fused else None, out_link=out_link)
+        else:
+            idt = self.down_bn(self.down_conv(x))
+            out = self.bn1(self.conv1(x))
+            out = self.bn2(self.conv2(out))
+            z = self.conv3(out)
+            out_link = ResidualLink() if use_links and fused_ok(z, self.bn3.weight) else None
+            y = self.bn3(z, residual=idt, out_link=out_link)
+        if out_link is not None:
+            y._cml_link = out_link      # our consumer (an identity block) parks dres here
+        return y
 
 
 class ResNet(nn.Module):

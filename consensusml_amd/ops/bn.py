@@ -1,7 +1,8 @@
 """BatchNormAct2d: training BatchNorm + optional residual add + optional ReLU as one op.
 
 GPU bf16 channels_last inputs run the fused HIP kernels of ``csrc/kernels/bn_act.hip``
-(3 activation passes forward, 5 backward, ReLU mask recomputed from x). Anything else (CPU tests,
+(forward: stats + apply; backward: reduce + apply; the ReLU mask is recomputed from x, or — with a
+residual — kept from the forward as one bit per element). Anything else (CPU tests,
 fp32, NCHW) runs the equivalent PyTorch composition. Running statistics are kept in fp32 even
 when the module is cast to bf16.
 """
@@ -17,43 +18,55 @@ from .native import lib
 
 
 class ResidualLink:
-    """Hand-off of a residual gradient from a fused BN(+residual) backward to the GEMM that
-    produces the other half of the same tensor's gradient.
+    """Hand-off of a residual gradient between the two consumers of a ResNet block input.
 
-    In a ResNet block ``x -> conv1 ... bn3(., residual=x)``, autograd would materialise
-    dres = d(bn3)/d(residual) and later add it to conv1's dX with a separate elementwise kernel
-    (read 2 tensors, write 1). With a link, the BN backward parks dres here and returns no
-    gradient for the residual; conv1's backward (``models.resnet._Conv1x1Fn``) then accumulates
-    its dX GEMM straight into dres (``addmm_``: beta = 1 epilogue), so the add kernel and one
-    full activation write disappear. bn3's backward always runs before conv1's (conv1's output
-    gradient depends on it), so the hand-off is ordered by the graph itself."""
+    A block input x (= the previous block's output y) feeds conv1 and the residual add of the
+    block's last BN. Autograd would materialise dres = d(bn3)/d(residual), then add it to conv1's
+    dX in a separate elementwise pass (read 2 tensors, write 1) before the previous block's BN
+    backward reads the sum twice. With a link (created by the previous block for y):
+      * the block's bn3 backward parks dres here and returns no gradient for the residual;
+      * either conv1's backward GEMM accumulates into it (``models.resnet._Conv1x1Fn``, beta = 1),
+      * or the previous block's BN backward reads it as a second output gradient ``dy2`` and
+        sums it on load (``bn_bwd`` with dy2) — the add pass disappears.
+    bn3's backward always runs before conv1's and before the previous block's BN backward (both
+    depend on it through the graph), so the hand-off is ordered by the graph itself."""
     __slots__ = ("grad",)
 
     def __init__(self):
         self.grad = None
 
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, res, rmean, rvar, mean_in, invstd_in, eps, momentum, relu,
-                training, link):
-        y, mean, invstd = lib().bn_fwd(x, res, gamma, beta, rmean, rvar, mean_in, invstd_in,
-                                       eps, momentum, relu, training)
-        ctx.save_for_backward(x, res, gamma, beta, mean, invstd)
+                training, res_link, out_link):
+        has_res = res is not None
+        want_mask = has_res and relu and any(ctx.needs_input_grad[:4])
+        y, mean, invstd, mask = lib().bn_fwd(x, res, gamma, beta, rmean, rvar, mean_in,
+                                             invstd_in, eps, momentum, relu, training, want_mask)
+        # the residual itself is never needed again: its ReLU contribution lives in the bit mask
+        ctx.save_for_backward(x, mask if want_mask else None, gamma, beta, mean, invstd)
         ctx.relu = relu
-        ctx.has_res = res is not None
-        ctx.link = link
+        ctx.has_res = has_res
+        ctx.res_link = res_link
+        ctx.out_link = out_link
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, res, gamma, beta, mean, invstd = ctx.saved_tensors
-        dx, dg, db, dres = lib().bn_bwd(dy, x, res, gamma, beta, mean, invstd, ctx.relu)
-        if ctx.has_res and ctx.link is not None:
-            ctx.link.grad = dres
+        x, mask, gamma, beta, mean, invstd = ctx.saved_tensors
+        dy2 = ctx.out_link.take() if ctx.out_link is not None else None
+        dx, dg, db, dres = lib().bn_bwd(dy, dy2, x, mask, gamma, beta, mean, invstd, ctx.relu,
+                                        ctx.has_res)
+        if ctx.has_res and ctx.res_link is not None:
+            ctx.res_link.grad = dres
             dres = None
         return (dx, dg, db, dres if ctx.has_res else None, None, None, None, None, None, None,
-                None, None, None)
+                None, None, None, None)
 
 
 def fused_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
@@ -73,17 +86,18 @@ def bn_act(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
            running_mean: Optional[torch.Tensor], running_var: Optional[torch.Tensor],
            residual: Optional[torch.Tensor] = None, relu: bool = True, training: bool = True,
            momentum: float = 0.1, eps: float = 1e-5,
-           res_link: Optional[ResidualLink] = None) -> torch.Tensor:
-    """``res_link``: see ResidualLink; only honoured on the fused path (the caller checks
-    ``fused_ok`` before relying on it)."""
+           res_link: Optional[ResidualLink] = None,
+           out_link: Optional[ResidualLink] = None) -> torch.Tensor:
+    """``res_link`` / ``out_link``: see ResidualLink; only honoured on the fused path (callers
+    check ``fused_ok`` before creating links)."""
     if _fused_ok(x, gamma) and (residual is None or residual.is_contiguous(
             memory_format=torch.channels_last)):
         if training:
             return _BNActFn.apply(x, gamma, beta, residual, running_mean, running_var, None, None,
-                                  eps, momentum, relu, True, res_link)
+                                  eps, momentum, relu, True, res_link, out_link)
         invstd = torch.rsqrt(running_var.float() + eps)
         return _BNActFn.apply(x, gamma, beta, residual, None, None, running_mean.float(), invstd,
-                              eps, momentum, relu, False, res_link)
+                              eps, momentum, relu, False, res_link, out_link)
     # reference composition (CPU / unsupported layouts)
     y = F.batch_norm(x, running_mean, running_var, gamma, beta, training, momentum, eps) \
         if running_mean is None or running_mean.dtype == x.dtype else \
@@ -123,9 +137,10 @@ class BatchNormAct2d(nn.Module):
         return self
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                res_link: Optional[ResidualLink] = None) -> torch.Tensor:
+                res_link: Optional[ResidualLink] = None,
+                out_link: Optional[ResidualLink] = None) -> torch.Tensor:
         return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual,
-                      self.relu, self.training, self.momentum, self.eps, res_link)
+                      self.relu, self.training, self.momentum, self.eps, res_link, out_link)
 
     def extra_repr(self) -> str:
         return f"{self.num_features}, relu={self.relu}"

@@ -166,7 +166,7 @@ std::vector<Tensor> bn_fwd(const Tensor& x, const optional<Tensor>& res, const T
                            const Tensor& beta, const optional<Tensor>& rmean,
                            const optional<Tensor>& rvar, const optional<Tensor>& mean_in,
                            const optional<Tensor>& invstd_in, double eps, double momentum,
-                           bool relu, bool training) {
+                           bool relu, bool training, bool want_mask) {
   check_nhwc(x, "x");
   const int64_t C = x.size(1) * (x.dim() == 4 ? 1 : 0) + (x.dim() == 2 ? x.size(1) : 0);
   const int64_t M = x.numel() / C;
@@ -194,34 +194,56 @@ std::vector<Tensor> bn_fwd(const Tensor& x, const optional<Tensor>& res, const T
   float* rv = opt_ptr<float>(rvar, at::kFloat, "running_var", C);
   Tensor work = at::empty({static_cast<int64_t>(cml::bn_workspace_bytes(M, static_cast<int>(C)) / 4 + 1)}, f32);
   const void* rp = (res.has_value() && res->defined()) ? res->data_ptr() : nullptr;
-  CML_CHECK_HIP(cml::launch_bn_fwd(x.data_ptr(), rp, y.data_ptr(), M, static_cast<int>(C),
-                                   gamma.data_ptr(), beta.data_ptr(), mean.data_ptr<float>(),
-                                   invstd.data_ptr<float>(), rm, rv, static_cast<float>(eps),
-                                   static_cast<float>(momentum), relu ? 1 : 0, training ? 1 : 0,
-                                   work.data_ptr(), cur_stream()));
-  return {y, mean, invstd};
+  Tensor mask;
+  if (want_mask && rp && relu) mask = at::empty({M, C / 8}, x.options().dtype(at::kByte));
+  CML_CHECK_HIP(cml::launch_bn_fwd(x.data_ptr(), rp, y.data_ptr(),
+                                   mask.defined() ? mask.data_ptr() : nullptr, M,
+                                   static_cast<int>(C), gamma.data_ptr(), beta.data_ptr(),
+                                   mean.data_ptr<float>(), invstd.data_ptr<float>(), rm, rv,
+                                   static_cast<float>(eps), static_cast<float>(momentum),
+                                   relu ? 1 : 0, training ? 1 : 0, work.data_ptr(), cur_stream()));
+  return {y, mean, invstd, mask};
 }
 
-std::vector<Tensor> bn_bwd(const Tensor& dy_in, const Tensor& x, const optional<Tensor>& res,
-                           const Tensor& gamma, const Tensor& beta, const Tensor& mean,
-                           const Tensor& invstd, bool relu) {
+// dy2 (optional): second part of the output gradient, summed on load. mask (optional): the
+// forward's ReLU bit mask (required for relu with a residual). want_dres: also return the
+// residual gradient.
+std::vector<Tensor> bn_bwd(const Tensor& dy_in, const optional<Tensor>& dy2_in, const Tensor& x,
+                           const optional<Tensor>& mask, const Tensor& gamma, const Tensor& beta,
+                           const Tensor& mean, const Tensor& invstd, bool relu, bool want_dres) {
   check_nhwc(x, "x");
-  Tensor dy = x.dim() == 4 ? dy_in.contiguous(at::MemoryFormat::ChannelsLast) : dy_in.contiguous();
+  auto as_nhwc = [&](const Tensor& t) {
+    return x.dim() == 4 ? t.contiguous(at::MemoryFormat::ChannelsLast) : t.contiguous();
+  };
+  Tensor dy = as_nhwc(dy_in);
   check_nhwc(dy, "dy");
-  const int64_t C = x.dim() == 4 ? x.size(1) : x.size(1);
+  TORCH_CHECK(dy.sizes() == x.sizes(), "dy shape mismatch");
+  Tensor dy2;
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = as_nhwc(*dy2_in);
+    check_nhwc(dy2, "dy2");
+    TORCH_CHECK(dy2.sizes() == x.sizes(), "dy2 shape mismatch");
+  }
+  const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
-  const bool has_res = res.has_value() && res->defined();
-  if (has_res) check_nhwc(*res, "res");
+  const bool has_mask = mask.has_value() && mask->defined();
+  if (has_mask) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() == M * (C / 8) && mask->device() == x.device(),
+                "mask: contiguous uint8 [M, C/8] on x's device");
+  }
+  TORCH_CHECK(!(relu && want_dres && !has_mask), "bn_bwd: relu + residual needs the forward mask");
   const c10::DeviceGuard guard(x.device());
   auto f32 = x.options().dtype(at::kFloat);
   Tensor dx = at::empty_like(x);
-  Tensor dres = has_res ? at::empty_like(x) : Tensor();
+  Tensor dres = want_dres ? at::empty_like(x) : Tensor();
   Tensor dgamma = at::empty({C}, gamma.options());
   Tensor dbeta = at::empty({C}, beta.options());
   Tensor sdz = at::empty({C}, f32), sdzx = at::empty({C}, f32);
   Tensor work = at::empty({static_cast<int64_t>(cml::bn_workspace_bytes(M, static_cast<int>(C)) / 4 + 1)}, f32);
-  CML_CHECK_HIP(cml::launch_bn_bwd(dy.data_ptr(), x.data_ptr(), has_res ? res->data_ptr() : nullptr,
-                                   dx.data_ptr(), has_res ? dres.data_ptr() : nullptr, M,
+  CML_CHECK_HIP(cml::launch_bn_bwd(dy.data_ptr(), dy2.defined() ? dy2.data_ptr() : nullptr,
+                                   x.data_ptr(), has_mask ? mask->data_ptr() : nullptr,
+                                   dx.data_ptr(), want_dres ? dres.data_ptr() : nullptr, M,
                                    static_cast<int>(C), gamma.data_ptr(), beta.data_ptr(),
                                    mean.data_ptr<float>(), invstd.data_ptr<float>(),
                                    dgamma.data_ptr(), dbeta.data_ptr(), sdz.data_ptr<float>(),

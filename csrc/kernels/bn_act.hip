@@ -174,10 +174,13 @@ __device__ __forceinline__ void chan_affine(int g, const float* mean, const floa
   }
 }
 
-template <bool RES, bool RELU>
+// MASK (RES + RELU blocks): also write the ReLU mask as one bit per element ([M, C/8] bytes), so
+// the backward never reads the residual again (2 B/elem per backward pass -> 1/8 B).
+template <bool RES, bool RELU, bool MASK>
 __global__ __launch_bounds__(kBT) void bn_apply_kernel(const bf16* __restrict__ x,
                                                       const bf16* __restrict__ res,
-                                                      bf16* __restrict__ y, int64_t M, int C,
+                                                      bf16* __restrict__ y,
+                                                      uint8_t* __restrict__ mask, int64_t M, int C,
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ invstd,
                                                       const bf16* __restrict__ gamma,
@@ -192,23 +195,55 @@ __global__ __launch_bounds__(kBT) void bn_apply_kernel(const bf16* __restrict__ 
     ld8(x + r * C + 8 * g, v);
     float rv[8];
     if constexpr (RES) ld8(res + r * C + 8 * g, rv);
+    uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float z = fmaf(v[k], sc[k], bi[k]);
       if constexpr (RES) z += rv[k];
+      if constexpr (MASK) bits |= (z > 0.f ? 1u : 0u) << k;
       if constexpr (RELU) z = fmaxf(z, 0.f);
       v[k] = z;
     }
     store_bf16<8>(y + r * C + 8 * g, v);
+    if constexpr (MASK) mask[r * tpr + g] = static_cast<uint8_t>(bits);
   }
 }
 
 // ----------------------------------------------------------------------------- backward
-template <bool RES, bool RELU>
+// ReLU handling in the backward: RM_NONE (no ReLU), RM_RECOMP (mask recomputed from x: BN-ReLU
+// without residual), RM_MASK (bit mask written by the forward: BN + residual + ReLU).
+// DY2: the output gradient arrives in two parts (dy + dy2, see ops.bn.ResidualLink) and is summed
+// on load, replacing a separate elementwise add pass.
+enum { RM_NONE = 0, RM_RECOMP = 1, RM_MASK = 2 };
+
+template <int RM, bool DY2>
+__device__ __forceinline__ void load_dz(const bf16* __restrict__ dy, const bf16* __restrict__ dy2,
+                                        const uint8_t* __restrict__ mask, int64_t r, int C, int g,
+                                        const float (&v)[8], const float (&sc)[8],
+                                        const float (&bi)[8], float (&dz)[8]) {
+  ld8(dy + r * C + 8 * g, dz);
+  if constexpr (DY2) {
+    float d2[8];
+    ld8(dy2 + r * C + 8 * g, d2);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dz[k] += d2[k];
+  }
+  if constexpr (RM == RM_MASK) {
+    const uint32_t bits = mask[r * (C / 8) + g];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dz[k] = ((bits >> k) & 1u) ? dz[k] : 0.f;
+  } else if constexpr (RM == RM_RECOMP) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dz[k] = fmaf(v[k], sc[k], bi[k]) > 0.f ? dz[k] : 0.f;
+  }
+}
+
+template <int RM, bool DY2>
 __global__ __launch_bounds__(kBT) void bn_bwd_reduce_kernel(const bf16* __restrict__ dy,
+                                                           const bf16* __restrict__ dy2,
                                                            const bf16* __restrict__ x,
-                                                           const bf16* __restrict__ res, int64_t M,
-                                                           int C, int64_t rpb,
+                                                           const uint8_t* __restrict__ mask,
+                                                           int64_t M, int C, int64_t rpb,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
                                                            const bf16* __restrict__ gamma,
@@ -228,20 +263,13 @@ __global__ __launch_bounds__(kBT) void bn_bwd_reduce_kernel(const bf16* __restri
   const int64_t lo = static_cast<int64_t>(blockIdx.x) * rpb;
   const int64_t hi = lo + rpb < M ? lo + rpb : M;
   for (int64_t r = lo + threadIdx.x / tpr; r < hi; r += rpi) {
-    float d[8], v[8], rv[8];
-    ld8(dy + r * C + 8 * g, d);
+    float v[8], dz[8];
     ld8(x + r * C + 8 * g, v);
-    if constexpr (RES && RELU) ld8(res + r * C + 8 * g, rv);
+    load_dz<RM, DY2>(dy, dy2, mask, r, C, g, v, sc, bi, dz);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float dz = d[k];
-      if constexpr (RELU) {
-        float z = fmaf(v[k], sc[k], bi[k]);
-        if constexpr (RES) z += rv[k];
-        dz = z > 0.f ? dz : 0.f;
-      }
-      s[k] += dz;
-      q[k] = fmaf(dz, (v[k] - mu[k]) * is[k], q[k]);
+      s[k] += dz[k];
+      q[k] = fmaf(dz[k], (v[k] - mu[k]) * is[k], q[k]);
     }
   }
   block_partial(s, q, tpr, C, part);
@@ -261,10 +289,12 @@ __global__ __launch_bounds__(kBT) void bn_bwd_finalize_kernel(const float* __res
   reinterpret_cast<uint16_t*>(dgamma)[c] = f2bf(static_cast<float>(q));
 }
 
-template <bool RES, bool RELU>
+// DRES: also write the gradient of the residual input (= the masked output gradient).
+template <int RM, bool DRES, bool DY2>
 __global__ __launch_bounds__(kBT) void bn_bwd_apply_kernel(const bf16* __restrict__ dy,
+                                                          const bf16* __restrict__ dy2,
                                                           const bf16* __restrict__ x,
-                                                          const bf16* __restrict__ res,
+                                                          const uint8_t* __restrict__ mask,
                                                           bf16* __restrict__ dx,
                                                           bf16* __restrict__ dres, int64_t M, int C,
                                                           const float* __restrict__ mean,
@@ -287,24 +317,16 @@ __global__ __launch_bounds__(kBT) void bn_bwd_apply_kernel(const bf16* __restric
   }
   const int64_t rstride = static_cast<int64_t>(gridDim.x) * (kBT / tpr);
   for (int64_t r = static_cast<int64_t>(blockIdx.x) * (kBT / tpr) + threadIdx.x / tpr; r < M; r += rstride) {
-    float d[8], v[8], rv[8], o[8];
-    ld8(dy + r * C + 8 * g, d);
+    float v[8], dz[8], o[8];
     ld8(x + r * C + 8 * g, v);
-    if constexpr (RES && RELU) ld8(res + r * C + 8 * g, rv);
+    load_dz<RM, DY2>(dy, dy2, mask, r, C, g, v, sc, bi, dz);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float dz = d[k];
-      if constexpr (RELU) {
-        float z = fmaf(v[k], sc[k], bi[k]);
-        if constexpr (RES) z += rv[k];
-        dz = z > 0.f ? dz : 0.f;
-      }
-      d[k] = dz;
       const float xh = (v[k] - mu[k]) * is[k];
-      o[k] = sc[k] * (dz - a[k] - xh * b[k]);
+      o[k] = sc[k] * (dz[k] - a[k] - xh * b[k]);
     }
     store_bf16<8>(dx + r * C + 8 * g, o);
-    if constexpr (RES) store_bf16<8>(dres + r * C + 8 * g, d);
+    if constexpr (DRES) store_bf16<8>(dres + r * C + 8 * g, dz);
   }
 }
 
@@ -322,11 +344,12 @@ size_t bn_workspace_bytes(int64_t M, int C) {
   return static_cast<size_t>(g.nb) * 2 * C * sizeof(float);
 }
 
-hipError_t launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C,
+hipError_t launch_bn_fwd(const void* x, const void* res, void* y, void* mask, int64_t M, int C,
                          const void* gamma, const void* beta, float* mean, float* invstd,
                          float* rmean, float* rvar, float eps, float momentum, int relu,
                          int training, void* work, hipStream_t st) {
   if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1) return hipErrorInvalidValue;
+  if (mask && !(res && relu)) return hipErrorInvalidValue;
   const bf16* xb = reinterpret_cast<const bf16*>(x);
   if (training) {
     const BNGeom g = geom(M, C);
@@ -338,40 +361,71 @@ hipError_t launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int
   const int ga = apply_grid(M, C);
   const bf16* rb = reinterpret_cast<const bf16*>(res);
   bf16* yb = reinterpret_cast<bf16*>(y);
+  uint8_t* mk = reinterpret_cast<uint8_t*>(mask);
   const bf16* gm = reinterpret_cast<const bf16*>(gamma);
   const bf16* bt = reinterpret_cast<const bf16*>(beta);
-  if (res && relu) bn_apply_kernel<true, true><<<ga, kBT, 0, st>>>(xb, rb, yb, M, C, mean, invstd, gm, bt);
-  else if (res) bn_apply_kernel<true, false><<<ga, kBT, 0, st>>>(xb, rb, yb, M, C, mean, invstd, gm, bt);
-  else if (relu) bn_apply_kernel<false, true><<<ga, kBT, 0, st>>>(xb, rb, yb, M, C, mean, invstd, gm, bt);
-  else bn_apply_kernel<false, false><<<ga, kBT, 0, st>>>(xb, rb, yb, M, C, mean, invstd, gm, bt);
+  if (mask) bn_apply_kernel<true, true, true><<<ga, kBT, 0, st>>>(xb, rb, yb, mk, M, C, mean, invstd, gm, bt);
+  else if (res && relu) bn_apply_kernel<true, true, false><<<ga, kBT, 0, st>>>(xb, rb, yb, mk, M, C, mean, invstd, gm, bt);
+  else if (res) bn_apply_kernel<true, false, false><<<ga, kBT, 0, st>>>(xb, rb, yb, mk, M, C, mean, invstd, gm, bt);
+  else if (relu) bn_apply_kernel<false, true, false><<<ga, kBT, 0, st>>>(xb, rb, yb, mk, M, C, mean, invstd, gm, bt);
+  else bn_apply_kernel<false, false, false><<<ga, kBT, 0, st>>>(xb, rb, yb, mk, M, C, mean, invstd, gm, bt);
   return hipGetLastError();
 }
 
-hipError_t launch_bn_bwd(const void* dy, const void* x, const void* res, void* dx, void* dres,
-                         int64_t M, int C, const void* gamma, const void* beta, const float* mean,
-                         const float* invstd, void* dgamma, void* dbeta, float* sdz, float* sdzx,
-                         int relu, void* work, hipStream_t st) {
-  if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1) return hipErrorInvalidValue;
+namespace {
+template <int RM, bool DRES, bool DY2>
+void bwd_t(const bf16* d, const bf16* d2, const bf16* xb, const uint8_t* mk, bf16* dxb, bf16* drb,
+           int64_t M, int C, const bf16* gm, const bf16* bt, const float* mean, const float* invstd,
+           bf16* dgamma, bf16* dbeta, float* sdz, float* sdzx, float* part, hipStream_t st) {
   const BNGeom g = geom(M, C);
-  float* part = reinterpret_cast<float*>(work);
+  bn_bwd_reduce_kernel<RM, DY2><<<g.nb, kBT, 0, st>>>(d, d2, xb, mk, M, C, g.rpb, mean, invstd, gm,
+                                                       bt, part);
+  bn_bwd_finalize_kernel<<<(C + kFC - 1) / kFC, kBT, 0, st>>>(part, g.nb, C, sdz, sdzx, dgamma,
+                                                              dbeta);
+  bn_bwd_apply_kernel<RM, DRES, DY2><<<apply_grid(M, C), kBT, 0, st>>>(
+      d, d2, xb, mk, dxb, drb, M, C, mean, invstd, gm, bt, sdz, sdzx);
+}
+
+template <bool DY2>
+hipError_t bwd_dispatch(int rm, bool dres, const bf16* d, const bf16* d2, const bf16* xb,
+                        const uint8_t* mk, bf16* dxb, bf16* drb, int64_t M, int C, const bf16* gm,
+                        const bf16* bt, const float* mean, const float* invstd, bf16* dg, bf16* db,
+                        float* sdz, float* sdzx, float* part, hipStream_t st) {
+#define CML_BWD(RMV, DR) bwd_t<RMV, DR, DY2>(d, d2, xb, mk, dxb, drb, M, C, gm, bt, mean, invstd, dg, db, sdz, sdzx, part, st)
+  if (rm == RM_MASK && dres) CML_BWD(RM_MASK, true);
+  else if (rm == RM_MASK) CML_BWD(RM_MASK, false);
+  else if (rm == RM_RECOMP && !dres) CML_BWD(RM_RECOMP, false);
+  else if (rm == RM_NONE && dres) CML_BWD(RM_NONE, true);
+  else if (rm == RM_NONE) CML_BWD(RM_NONE, false);
+  else return hipErrorInvalidValue;   // ReLU with a residual needs the forward's mask
+#undef CML_BWD
+  return hipSuccess;
+}
+}  // namespace
+
+hipError_t launch_bn_bwd(const void* dy, const void* dy2, const void* x, const void* mask,
+                         void* dx, void* dres, int64_t M, int C, const void* gamma,
+                         const void* beta, const float* mean, const float* invstd, void* dgamma,
+                         void* dbeta, float* sdz, float* sdzx, int relu, void* work,
+                         hipStream_t st) {
+  if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1) return hipErrorInvalidValue;
+  const int rm = !relu ? RM_NONE : (mask ? RM_MASK : RM_RECOMP);
   const bf16* d = reinterpret_cast<const bf16*>(dy);
+  const bf16* d2 = reinterpret_cast<const bf16*>(dy2);
   const bf16* xb = reinterpret_cast<const bf16*>(x);
-  const bf16* rb = reinterpret_cast<const bf16*>(res);
+  const uint8_t* mk = reinterpret_cast<const uint8_t*>(mask);
   const bf16* gm = reinterpret_cast<const bf16*>(gamma);
   const bf16* bt = reinterpret_cast<const bf16*>(beta);
-  if (res && relu) bn_bwd_reduce_kernel<true, true><<<g.nb, kBT, 0, st>>>(d, xb, rb, M, C, g.rpb, mean, invstd, gm, bt, part);
-  else if (relu) bn_bwd_reduce_kernel<false, true><<<g.nb, kBT, 0, st>>>(d, xb, rb, M, C, g.rpb, mean, invstd, gm, bt, part);
-  else bn_bwd_reduce_kernel<false, false><<<g.nb, kBT, 0, st>>>(d, xb, rb, M, C, g.rpb, mean, invstd, gm, bt, part);
-  bn_bwd_finalize_kernel<<<(C + kFC - 1) / kFC, kBT, 0, st>>>(part, g.nb, C, sdz, sdzx,
-                                                              reinterpret_cast<bf16*>(dgamma),
-                                                              reinterpret_cast<bf16*>(dbeta));
-  const int ga = apply_grid(M, C);
   bf16* dxb = reinterpret_cast<bf16*>(dx);
   bf16* drb = reinterpret_cast<bf16*>(dres);
-  if (res && relu) bn_bwd_apply_kernel<true, true><<<ga, kBT, 0, st>>>(d, xb, rb, dxb, drb, M, C, mean, invstd, gm, bt, sdz, sdzx);
-  else if (res) bn_bwd_apply_kernel<true, false><<<ga, kBT, 0, st>>>(d, xb, rb, dxb, drb, M, C, mean, invstd, gm, bt, sdz, sdzx);
-  else if (relu) bn_bwd_apply_kernel<false, true><<<ga, kBT, 0, st>>>(d, xb, rb, dxb, drb, M, C, mean, invstd, gm, bt, sdz, sdzx);
-  else bn_bwd_apply_kernel<false, false><<<ga, kBT, 0, st>>>(d, xb, rb, dxb, drb, M, C, mean, invstd, gm, bt, sdz, sdzx);
+  float* part = reinterpret_cast<float*>(work);
+  hipError_t e = dy2 ? bwd_dispatch<true>(rm, drb != nullptr, d, d2, xb, mk, dxb, drb, M, C, gm, bt,
+                                           mean, invstd, reinterpret_cast<bf16*>(dgamma),
+                                           reinterpret_cast<bf16*>(dbeta), sdz, sdzx, part, st)
+                     : bwd_dispatch<false>(rm, drb != nullptr, d, d2, xb, mk, dxb, drb, M, C, gm, bt,
+                                           mean, invstd, reinterpret_cast<bf16*>(dgamma),
+                                           reinterpret_cast<bf16*>(dbeta), sdz, sdzx, part, st);
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 

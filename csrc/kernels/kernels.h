@@ -75,14 +75,19 @@ hipError_t launch_gossip_mix(int dtype, float* master, void* param_out, const vo
 // Backward recomputes the ReLU mask from x, writes dx (and dres = dz when res != null), dgamma /
 // dbeta (bf16) and the per-channel sums sdz / sdzx (fp32 [C]). ``work``: bn_workspace_bytes.
 size_t bn_workspace_bytes(int64_t M, int C);
-hipError_t launch_bn_fwd(const void* x, const void* res, void* y, int64_t M, int C,
+// mask (optional, only with res && relu): [M, C/8] bytes, one ReLU bit per element.
+hipError_t launch_bn_fwd(const void* x, const void* res, void* y, void* mask, int64_t M, int C,
                          const void* gamma, const void* beta, float* mean, float* invstd,
                          float* rmean, float* rvar, float eps, float momentum, int relu,
                          int training, void* work, hipStream_t stream);
-hipError_t launch_bn_bwd(const void* dy, const void* x, const void* res, void* dx, void* dres,
-                         int64_t M, int C, const void* gamma, const void* beta, const float* mean,
-                         const float* invstd, void* dgamma, void* dbeta, float* sdz, float* sdzx,
-                         int relu, void* work, hipStream_t stream);
+// Backward: output gradient dy (+ dy2 if non-null); ReLU from the forward's bit mask when given,
+// else recomputed from x (only valid without a residual); dres (optional) receives the masked
+// output gradient (the residual input's gradient).
+hipError_t launch_bn_bwd(const void* dy, const void* dy2, const void* x, const void* mask,
+                         void* dx, void* dres, int64_t M, int C, const void* gamma,
+                         const void* beta, const float* mean, const float* invstd, void* dgamma,
+                         void* dbeta, float* sdz, float* sdzx, int relu, void* work,
+                         hipStream_t stream);
 
 // NHWC bf16 max-pool with a one-byte argmax per output element; backward is a gather.
 hipError_t launch_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C,

@@ -134,23 +134,64 @@ def test_conv1x1_gemm_matches_conv(cuda, cin, cout):
     torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=1e-1)
 
 
-def test_residual_link_matches_autograd_add(cuda):
-    """Identity bottleneck: grads with the residual gradient accumulated inside conv1's backward
-    GEMM equal the plain autograd path (separate add)."""
+@pytest.mark.parametrize("gemm", [False, True])
+def test_residual_link_matches_autograd_add(cuda, gemm):
+    """Downsample block + 3 identity blocks: with the residual gradient parked on the producer's
+    link (consumed as dy2 by the producer's BN backward, or by conv1's GEMM epilogue) and the
+    ReLU bit mask, grads equal the plain autograd path (separate add, no links)."""
     from consensusml_amd.models import resnet as R
     torch.manual_seed(0)
-    blk = R.Bottleneck(64, 16).to(cuda, torch.bfloat16).to(memory_format=torch.channels_last)
-    torch.nn.init.normal_(blk.bn3.weight, 1.0, 0.1)
-    x0 = torch.randn(4, 64, 10, 10, device=cuda).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    net = torch.nn.Sequential(R.Bottleneck(32, 16, downsample=True), R.Bottleneck(64, 16),
+                              R.Bottleneck(64, 16), R.Bottleneck(64, 16))
+    net = net.to(cuda, torch.bfloat16).to(memory_format=torch.channels_last)
+    for m in net:
+        torch.nn.init.normal_(m.bn3.weight, 1.0, 0.1)
+    x0 = torch.randn(4, 32, 10, 10, device=cuda).to(torch.bfloat16).to(memory_format=torch.channels_last)
     res = []
-    for link in (True, False):
-        R.RESIDUAL_LINK = link
-        blk.zero_grad(set_to_none=True)
-        x = x0.clone().requires_grad_(True)
-        y = blk(x)
-        y.float().square().sum().backward()
-        res.append((x.grad.clone(), [p.grad.clone() for p in blk.parameters()]))
-    R.RESIDUAL_LINK = True
+    R.CONV1X1_GEMM = gemm
+    try:
+        for link in (True, False):
+            R.RESIDUAL_LINK = link
+            net.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            y = net(x)
+            y.float().square().sum().backward()
+            res.append((x.grad.clone(), [p.grad.clone() for p in net.parameters()]))
+    finally:
+        R.RESIDUAL_LINK = True
+        R.CONV1X1_GEMM = False
     torch.testing.assert_close(res[0][0].float(), res[1][0].float(), rtol=2e-2, atol=2e-2)
     for a, b in zip(res[0][1], res[1][1]):
         torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("mode", ["relu", "res_relu"])
+def test_bn_act_two_part_output_grad(cuda, mode):
+    """out_link: a gradient parked on the link is summed with dy inside the BN backward."""
+    from consensusml_amd.ops.bn import ResidualLink
+    torch.manual_seed(3)
+    C = 64
+    x = (torch.randn(4, C, 6, 5, device=cuda) * 2).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    res = None
+    if mode == "res_relu":
+        res = torch.randn(4, C, 6, 5, device=cuda).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last).requires_grad_(True)
+    g = (torch.rand(C, device=cuda) + 0.5).to(torch.bfloat16).requires_grad_(True)
+    b = torch.randn(C, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    link = ResidualLink()
+    y = bn_act(x, g, b, torch.zeros(C, device=cuda), torch.ones(C, device=cuda), res, True, True,
+               out_link=link)
+    dy = torch.randn_like(y)
+    extra = torch.randn_like(y).contiguous(memory_format=torch.channels_last)
+    link.grad = extra
+    y.backward(dy)
+    assert link.grad is None
+    x2 = x.detach().clone().requires_grad_(True)
+    r2 = res.detach().clone().requires_grad_(True) if res is not None else None
+    y2 = bn_act(x2, g.detach(), b.detach(), torch.zeros(C, device=cuda), torch.ones(C, device=cuda),
+                r2, True, True)
+    y2.backward((dy.float() + extra.float()).to(torch.bfloat16))
+    torch.testing.assert_close(x.grad.float(), x2.grad.float(), rtol=2e-2, atol=3e-2)
+    if res is not None:
+        torch.testing.assert_close(res.grad.float(), r2.grad.float(), rtol=2e-2, atol=3e-2)
