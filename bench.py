@@ -91,6 +91,10 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info):
     tw = time.perf_counter()
     for i in range(max(warmup, 1 if torch.backends.cudnn.benchmark else 0)):
         step(i)
+        if info.rank == 0:   # progress: a cold MIOpen find for new conv shapes can take minutes
+            torch.cuda.synchronize()
+            print(f"[bench] {rule}/{topology}: warmup step {i} done at {time.perf_counter() - tw:.1f}s",
+                  file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if info.rank == 0:
         print(f"[bench] {rule}/{topology}: warmup {time.perf_counter() - tw:.1f}s", file=sys.stderr,
