@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--model", default=None, help="override the model (e.g. llama_tiny)")
     ap.add_argument("--f", type=int, default=-1)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--profile-marker", action="store_true",
+                    help="launch a spin_kernel between warmup and timed steps (prof_summary --after)")
     a = ap.parse_args()
     c = dict(CONFIGS[a.config])
     if a.model:
@@ -88,6 +90,8 @@ def main():
     for _ in range(a.warmup):
         tr.train_step()
     tr.timer.summary()
+    if a.profile_marker and info.device.type == "cuda":
+        torch.cuda._sleep(1000)
     sync()
     if info.distributed:
         dist.barrier()

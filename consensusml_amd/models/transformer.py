@@ -1,21 +1,33 @@
 """BERT-base and Llama-3 transformer families (N12).
 
-Attention goes through ``F.scaled_dot_product_attention`` (the ROCm flash / memory-efficient
-kernels of PyTorch) — the north star keeps model compute in PyTorch and puts the hand-written
-HIP work into aggregation and the optimizer. Random-init weights (no checkpoints offline).
+Attention is ``F.scaled_dot_product_attention`` (ROCm flash kernels); the GEMMs are hipBLASLt via
+``F.linear``. Everything between them runs the hand-written HIP kernels of
+``csrc/kernels/transformer.hip`` (``ops.transformer``) on bf16 GPU tensors:
+  * the q / k / v projections are ONE fused GEMM whose output is split (and, for Llama, rotated)
+    straight into SDPA's head-major layout by one kernel (backward: one kernel back);
+  * every residual add is fused with the following norm (``add_norm``: the residual stream and the
+    normalised sublayer input come out of one pass, and the backward adds the stream's gradient
+    on the way out);
+  * Llama's gate / up projections are one GEMM feeding a one-pass SwiGLU;
+  * linear-layer bias gradients use a bandwidth-bound column-sum kernel;
+  * the loss is the fused bf16 cross-entropy (``models.build_task``).
+CPU / fp32 tensors run the PyTorch compositions of the same ops.
 
 BERT-base: 12 layers, d 768, 12 heads, FFN 3072, vocab 30522, post-LN, GELU, MLM head tied to
 the token embedding. Llama-3-8B: 32 layers, d 4096, 32 q / 8 kv heads (GQA), SwiGLU FFN 14336,
-RMSNorm, RoPE theta 500000, vocab 128256, untied output head.
+RMSNorm, RoPE theta 500000 (interleaved pairs), vocab 128256, untied output head.
+Random-init weights (no checkpoints offline).
 """
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, linear, qkv_split,
+                               rope_tables, swiglu)
 
 
 # =============================================================================== BERT
@@ -34,19 +46,21 @@ class BertLayer(nn.Module):
     def __init__(self, c: BertConfig):
         super().__init__()
         self.h = c.heads
-        self.qkv = nn.Linear(c.d, 3 * c.d)
-        self.o = nn.Linear(c.d, c.d)
-        self.ln1 = nn.LayerNorm(c.d, eps=1e-12)
-        self.fc1 = nn.Linear(c.d, c.ffn)
-        self.fc2 = nn.Linear(c.ffn, c.d)
-        self.ln2 = nn.LayerNorm(c.d, eps=1e-12)
+        self.qkv = Linear(c.d, 3 * c.d)
+        self.o = Linear(c.d, c.d)
+        self.ln1 = LayerNorm(c.d, eps=1e-12)
+        self.fc1 = Linear(c.d, c.ffn)
+        self.fc2 = Linear(c.ffn, c.d)
+        self.ln2 = LayerNorm(c.d, eps=1e-12)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, S, D = x.shape
-        q, k, v = self.qkv(x).view(B, S, 3, self.h, D // self.h).permute(2, 0, 3, 1, 4)
+        q, k, v = qkv_split(self.qkv(x), self.h, self.h, D // self.h)
         a = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, S, D)
-        x = self.ln1(x + self.o(a))
-        return self.ln2(x + self.fc2(F.gelu(self.fc1(x))))
+        _, x = add_norm(x, self.o(a), self.ln1.weight, self.ln1.bias, self.ln1.eps)   # post-LN
+        _, x = add_norm(x, self.fc2(F.gelu(self.fc1(x))), self.ln2.weight, self.ln2.bias,
+                        self.ln2.eps)
+        return x
 
 
 class BertMLM(nn.Module):
@@ -56,10 +70,10 @@ class BertMLM(nn.Module):
         self.tok = nn.Embedding(c.vocab, c.d)
         self.pos = nn.Embedding(c.max_pos, c.d)
         self.typ = nn.Embedding(2, c.d)
-        self.ln = nn.LayerNorm(c.d, eps=1e-12)
+        self.ln = LayerNorm(c.d, eps=1e-12)
         self.layers = nn.ModuleList([BertLayer(c) for _ in range(c.layers)])
-        self.head = nn.Linear(c.d, c.d)
-        self.head_ln = nn.LayerNorm(c.d, eps=1e-12)
+        self.head = Linear(c.d, c.d)
+        self.head_ln = LayerNorm(c.d, eps=1e-12)
         self.bias = nn.Parameter(torch.zeros(c.vocab))
         for m in self.modules():
             if isinstance(m, (nn.Linear, nn.Embedding)):
@@ -75,7 +89,7 @@ class BertMLM(nn.Module):
         for l in self.layers:
             x = l(x)
         x = self.head_ln(F.gelu(self.head(x)))
-        return F.linear(x, self.tok.weight, self.bias)
+        return linear(x, self.tok.weight, self.bias)
 
 
 def bert_base() -> BertMLM:
@@ -100,60 +114,32 @@ class LlamaConfig:
     max_seq: int = 8192
 
 
-class RMSNorm(nn.Module):
-    def __init__(self, d: int, eps: float):
-        super().__init__()
-        self.eps = eps
-        self.weight = nn.Parameter(torch.ones(d))
-
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        xf = x.float()
-        xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)
-        return xf.to(x.dtype) * self.weight
-
-
-def rope_cache(S: int, hd: int, theta: float, device, dtype):
-    inv = 1.0 / (theta ** (torch.arange(0, hd, 2, device=device, dtype=torch.float32) / hd))
-    t = torch.arange(S, device=device, dtype=torch.float32)
-    f = torch.outer(t, inv)
-    return f.cos().to(dtype), f.sin().to(dtype)
-
-
-def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
-    x1, x2 = x[..., 0::2], x[..., 1::2]
-    c, s = cos[None, None], sin[None, None]
-    out = torch.stack((x1 * c - x2 * s, x1 * s + x2 * c), -1)
-    return out.flatten(-2)
-
-
 class LlamaBlock(nn.Module):
+    """Pre-norm block. The residual add that ends a block is fused with the next norm, so a block
+    takes (x, m): the residual stream before the previous block's MLP output m was added
+    (m = None for the first block), and returns its own (x, m)."""
+
     def __init__(self, c: LlamaConfig):
         super().__init__()
         self.c = c
         hd = c.d // c.heads
         self.hd = hd
-        self.wq = nn.Linear(c.d, c.heads * hd, bias=False)
-        self.wk = nn.Linear(c.d, c.kv_heads * hd, bias=False)
-        self.wv = nn.Linear(c.d, c.kv_heads * hd, bias=False)
+        self.wqkv = nn.Linear(c.d, (c.heads + 2 * c.kv_heads) * hd, bias=False)
         self.wo = nn.Linear(c.heads * hd, c.d, bias=False)
-        self.w1 = nn.Linear(c.d, c.ffn, bias=False)
-        self.w3 = nn.Linear(c.d, c.ffn, bias=False)
+        self.w13 = nn.Linear(c.d, 2 * c.ffn, bias=False)   # [gate | up]
         self.w2 = nn.Linear(c.ffn, c.d, bias=False)
         self.n1 = RMSNorm(c.d, c.eps)
         self.n2 = RMSNorm(c.d, c.eps)
 
-    def forward(self, x, cos, sin):
+    def forward(self, x, m, cos, sin):
         B, S, D = x.shape
-        h = self.n1(x)
-        q = self.wq(h).view(B, S, self.c.heads, self.hd).transpose(1, 2)
-        k = self.wk(h).view(B, S, self.c.kv_heads, self.hd).transpose(1, 2)
-        v = self.wv(h).view(B, S, self.c.kv_heads, self.hd).transpose(1, 2)
-        q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
+        x, h = add_norm(x, m, self.n1.weight, None, self.c.eps)
+        q, k, v = qkv_split(self.wqkv(h), self.c.heads, self.c.kv_heads, self.hd, cos, sin)
         a = F.scaled_dot_product_attention(q, k, v, is_causal=True,
                                            enable_gqa=self.c.heads != self.c.kv_heads)
-        x = x + self.wo(a.transpose(1, 2).reshape(B, S, D))
-        h = self.n2(x)
-        return x + self.w2(F.silu(self.w1(h)) * self.w3(h))
+        x, h = add_norm(x, self.wo(a.transpose(1, 2).reshape(B, S, D)), self.n2.weight, None,
+                        self.c.eps)
+        return x, self.w2(swiglu(self.w13(h)))
 
 
 class Llama(nn.Module):
@@ -172,16 +158,22 @@ class Llama(nn.Module):
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         B, S = ids.shape
         x = self.tok(ids)
-        cos, sin = rope_cache(S, self.c.d // self.c.heads, self.c.rope_theta, ids.device, x.dtype)
+        cos, sin = rope_tables(S, self.c.d // self.c.heads, self.c.rope_theta, ids.device)
+        m = None
         for l in self.layers:
             if self.ckpt and self.training:
-                x = torch.utils.checkpoint.checkpoint(l, x, cos, sin, use_reentrant=False)
+                x, m = torch.utils.checkpoint.checkpoint(l, x, m, cos, sin, use_reentrant=False)
             else:
-                x = l(x, cos, sin)
-        return self.out(self.norm(x))
+                x, m = l(x, m, cos, sin)
+        _, h = add_norm(x, m, self.norm.weight, None, self.c.eps)
+        return self.out(h)
 
 
-def llama3_8b(checkpoint_layers: bool = True) -> Llama:
+def llama3_8b(checkpoint_layers: bool = False) -> Llama:
+    """Without activation checkpointing by default: at 2048 tokens per replica the saved
+    activations are ~11 GB, and bf16 params + fp32 master + AdamW state + flat grads + gossip
+    buffers come to ~160 GB, well inside 288 GB of HBM3E — recomputing the forward would cost a
+    third more GEMM work for memory the MI355X does not need back."""
     return Llama(LlamaConfig(), checkpoint_layers)
 
 

@@ -1,0 +1,254 @@
+"""Transformer hot ops: fused cross-entropy, LayerNorm / RMSNorm (+ residual add), QKV split +
+RoPE, SwiGLU and bias-gradient linear layers.
+
+GPU bf16 tensors run the HIP kernels of ``csrc/kernels/transformer.hip``; every other input (CPU
+tests, fp32) runs the equivalent PyTorch composition, which is also the numerics oracle of
+``tests/test_transformer_ops_gpu.py``. Profiles that motivated each op are in
+``profiles/r01_prof13_{bert,llama}_kernels.md`` (PyTorch's unfused paths: ~40 % of the Llama and
+~25 % of the BERT step outside the GEMMs and attention).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .native import lib
+
+
+def _gpu_bf16(*ts: Optional[torch.Tensor]) -> bool:
+    return all(t is None or (t.is_cuda and t.dtype == torch.bfloat16) for t in ts)
+
+
+# ============================================================================ cross-entropy
+class _CEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        lse, rows = lib().ce_fwd(logits, labels, ignore_index)
+        count = (labels != ignore_index).sum().clamp_(min=1).float()
+        ctx.save_for_backward(logits, labels, lse, count)
+        ctx.ignore = ignore_index
+        return rows.sum() / count
+
+    @staticmethod
+    def backward(ctx, go):
+        logits, labels, lse, count = ctx.saved_tensors
+        scale = (go.float() / count).reshape(1)
+        return lib().ce_bwd(logits, labels, lse, scale, ctx.ignore), None, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor,
+                  ignore_index: int = -100) -> torch.Tensor:
+    """Mean cross-entropy of ``logits [..., V]`` against integer ``labels [...]``.
+
+    bf16 GPU logits never get an fp32 copy: one read for the loss, one read + one bf16 write for
+    the gradient (fp32 math inside). Other inputs use ``F.cross_entropy`` in fp32."""
+    V = logits.shape[-1]
+    if _gpu_bf16(logits) and labels.is_cuda:
+        x = logits.reshape(-1, V)
+        if not x.is_contiguous():
+            x = x.contiguous()
+        if x.data_ptr() % 16:   # misaligned view (the kernel reads 16-B vectors)
+            x = x.clone()
+        return _CEFn.apply(x, labels.reshape(-1).long().contiguous(), int(ignore_index))
+    return F.cross_entropy(logits.float().reshape(-1, V), labels.reshape(-1),
+                           ignore_index=ignore_index)
+
+
+# ============================================================================ norms
+class _NormFn(torch.autograd.Function):
+    """y = norm(x) (no residual)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        y, _, mean, rstd = lib().norm_fwd(x, None, w, b, eps)
+        ctx.save_for_backward(x, w, mean if b is not None else None, rstd)
+        ctx.ln = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = lib().norm_bwd(dy, None, x, w, mean, rstd)
+        return dx, dw, (db if ctx.ln else None), None
+
+
+class _AddNormFn(torch.autograd.Function):
+    """(s, y) = (x + r, norm(x + r)): the residual-stream update and the next sublayer's input in
+    one pass. The backward adds the gradient of s (the stream's own consumers) to the norm's
+    input gradient on the way out: d x = d r = ds + norm_bwd(dy)."""
+
+    @staticmethod
+    def forward(ctx, x, r, w, b, eps):
+        y, s, mean, rstd = lib().norm_fwd(x, r, w, b, eps)
+        ctx.save_for_backward(s, w, mean if b is not None else None, rstd)
+        ctx.ln = b is not None
+        return s, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        s, w, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            return ds, ds, None, None, None
+        dx, dw, db = lib().norm_bwd(dy, ds, s, w, mean, rstd)
+        return dx, dx, dw, (db if ctx.ln else None), None
+
+
+def _norm_ref(x, w, b, eps):
+    xf = x.float()
+    if b is None:
+        y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    else:
+        y = F.layer_norm(xf, (x.shape[-1],), w.float(), b.float(), eps)
+    return y.to(x.dtype)
+
+
+def _norm_ok(x: torch.Tensor, D: int) -> bool:
+    return D % 8 == 0 and D <= 4096 and x.is_contiguous() and x.data_ptr() % 16 == 0
+
+
+def norm(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], eps: float) -> torch.Tensor:
+    """LayerNorm (``b`` given) or RMSNorm (``b is None``) over the last dim."""
+    if _gpu_bf16(x, w, b) and _norm_ok(x, x.shape[-1]):
+        return _NormFn.apply(x, w, b, float(eps))
+    return _norm_ref(x, w, b, eps)
+
+
+def add_norm(x: torch.Tensor, r: Optional[torch.Tensor], w: torch.Tensor,
+             b: Optional[torch.Tensor], eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(s, norm(s)) with s = x + r (r None: s = x)."""
+    if r is None:
+        return x, norm(x, w, b, eps)
+    if _gpu_bf16(x, r, w, b) and _norm_ok(x, x.shape[-1]) and r.is_contiguous() \
+            and r.data_ptr() % 16 == 0 and r.shape == x.shape:
+        return _AddNormFn.apply(x, r, w, b, float(eps))
+    s = x + r
+    return s, _norm_ref(s, w, b, eps)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, d: int, eps: float = 1e-5):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(d))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return norm(x, self.weight, None, self.eps)
+
+
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm whose bf16 GPU forward / backward run the fused HIP kernels."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return norm(x, self.weight, self.bias, self.eps)
+
+
+# ============================================================================ QKV split + RoPE
+class _RopeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, H, KV, hd):
+        q, k, v = lib().rope_fwd(qkv, cos, sin, H, KV, hd)
+        ctx.save_for_backward(cos, sin)
+        ctx.has_rot = cos is not None
+        ctx.shapes = (q.shape, k.shape)
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        cos, sin = ctx.saved_tensors if ctx.has_rot else (None, None)
+        qs, ks = ctx.shapes
+        ref = next(t for t in (dq, dk, dv) if t is not None)
+        dq = dq if dq is not None else ref.new_zeros(qs)
+        dk = dk if dk is not None else ref.new_zeros(ks)
+        dv = dv if dv is not None else ref.new_zeros(ks)
+        return lib().rope_bwd(dq, dk, dv, cos, sin), None, None, None, None, None
+
+
+def rope_tables(S: int, hd: int, theta: float, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp32 (cos, sin) [S, hd/2] for interleaved-pair rotary embeddings."""
+    inv = 1.0 / (theta ** (torch.arange(0, hd, 2, device=device, dtype=torch.float32) / hd))
+    f = torch.outer(torch.arange(S, device=device, dtype=torch.float32), inv)
+    return f.cos().contiguous(), f.sin().contiguous()
+
+
+def _rope_ref(x, cos, sin):
+    """x [B, h, S, hd]; rotate pairs (x[2i], x[2i+1]) by (cos, sin)[s, i]."""
+    xf = x.float()
+    x1, x2 = xf[..., 0::2], xf[..., 1::2]
+    c, s = cos[None, None], sin[None, None]
+    return torch.stack((x1 * c - x2 * s, x1 * s + x2 * c), -1).flatten(-2).to(x.dtype)
+
+
+def qkv_split(qkv: torch.Tensor, H: int, KV: int, hd: int, cos: Optional[torch.Tensor] = None,
+              sin: Optional[torch.Tensor] = None):
+    """Fused projection ``qkv [B, S, (H + 2 KV) hd]`` -> head-major contiguous ``q [B, H, S, hd]``,
+    ``k, v [B, KV, S, hd]``, with RoPE on q / k when (cos, sin) fp32 [S, hd/2] are given."""
+    B, S, _ = qkv.shape
+    if _gpu_bf16(qkv) and hd % 8 == 0 and qkv.is_contiguous() and qkv.data_ptr() % 16 == 0:
+        return _RopeFn.apply(qkv, cos, sin, H, KV, hd)
+    x = qkv.view(B, S, H + 2 * KV, hd).transpose(1, 2)
+    q, k, v = x[:, :H], x[:, H:H + KV], x[:, H + KV:]
+    if cos is not None:
+        q, k = _rope_ref(q, cos, sin), _rope_ref(k, cos, sin)
+    return q.contiguous(), k.contiguous(), v.contiguous()
+
+
+# ============================================================================ SwiGLU
+class _SwiGLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h):
+        ctx.save_for_backward(h)
+        return lib().swiglu_fwd(h)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (h,) = ctx.saved_tensors
+        return lib().swiglu_bwd(dy, h)
+
+
+def swiglu(h: torch.Tensor) -> torch.Tensor:
+    """silu(a) * b for h = [a | b] along the last dim."""
+    F2 = h.shape[-1]
+    if _gpu_bf16(h) and F2 % 16 == 0 and h.is_contiguous() and h.data_ptr() % 16 == 0:
+        return _SwiGLUFn.apply(h)
+    a, b = h.chunk(2, -1)
+    return F.silu(a) * b
+
+
+# ============================================================================ linear (bias grad)
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T + b with the bias gradient from the column-sum kernel (PyTorch's generic column
+    reduction runs these at ~0.4 TB/s: 7 % of the BERT step in profiles/r01_prof13)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ w).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = dy2.t() @ x.reshape(-1, x.shape[-1])
+        if ctx.needs_input_grad[2]:
+            db = lib().colsum(dy2)
+        return dx, dw, db
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if b is not None and _gpu_bf16(x, w, b) and w.shape[0] % 8 == 0:
+        return _LinearFn.apply(x, w, b)
+    return F.linear(x, w, b)
+
+
+class Linear(nn.Linear):
+    """nn.Linear with the fused bias-gradient backward on bf16 GPU tensors."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return linear(x, self.weight, self.bias)

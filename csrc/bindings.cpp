@@ -286,6 +286,211 @@ void fault(Tensor& g, int64_t kind, double scale, double sigma, int64_t seed) {
                                   static_cast<uint64_t>(seed), cur_stream()));
 }
 
+// ---------------------------------------------------------------- transformer ops
+void check_bf16c(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-B aligned");
+}
+
+// logits [R, V] bf16 contiguous, labels [R] int64 -> (lse fp32 [R], loss fp32 [R])
+std::vector<Tensor> ce_fwd(const Tensor& logits, const Tensor& labels, int64_t ignore) {
+  check_bf16c(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2, "logits must be [R, V]");
+  const int64_t R = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(R >= 1 && R <= 2147483647LL && V >= 1 && V <= 2147483647LL, "bad logits shape");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() &&
+                  labels.numel() == R, "labels: contiguous int64 [R] on the GPU");
+  const c10::DeviceGuard guard(logits.device());
+  auto f32 = logits.options().dtype(at::kFloat);
+  Tensor lse = at::empty({R}, f32), loss = at::empty({R}, f32);
+  CML_CHECK_HIP(cml::launch_ce_fwd(logits.data_ptr(), R, static_cast<int>(V),
+                                   labels.data_ptr<int64_t>(), ignore, lse.data_ptr<float>(),
+                                   loss.data_ptr<float>(), cur_stream()));
+  return {lse, loss};
+}
+
+Tensor ce_bwd(const Tensor& logits, const Tensor& labels, const Tensor& lse, const Tensor& scale,
+              int64_t ignore) {
+  check_bf16c(logits, "logits");
+  const int64_t R = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.numel() == R &&
+                  labels.is_contiguous(), "labels: contiguous int64 [R]");
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.numel() == R &&
+                  lse.is_contiguous(), "lse: fp32 [R]");
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() >= 1,
+              "scale: fp32 GPU scalar");
+  const c10::DeviceGuard guard(logits.device());
+  Tensor g = at::empty_like(logits);
+  CML_CHECK_HIP(cml::launch_ce_bwd(logits.data_ptr(), R, static_cast<int>(V),
+                                   labels.data_ptr<int64_t>(), ignore, lse.data_ptr<float>(),
+                                   scale.data_ptr<float>(), g.data_ptr(), cur_stream()));
+  return g;
+}
+
+// x (and res) [.., D] bf16 contiguous; w (and b) [D] bf16. Returns (y, sum|undef, mean|undef, rstd).
+std::vector<Tensor> norm_fwd(const Tensor& x, const optional<Tensor>& res, const Tensor& w,
+                             const optional<Tensor>& b, double eps) {
+  check_bf16c(x, "x");
+  const int64_t D = x.size(-1);
+  const int64_t M = x.numel() / D;
+  check_bf16c(w, "w");
+  TORCH_CHECK(w.numel() == D, "w must be [D]");
+  const bool ln = b.has_value() && b->defined();
+  if (ln) {
+    check_bf16c(*b, "b");
+    TORCH_CHECK(b->numel() == D, "b must be [D]");
+  }
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) {
+    check_bf16c(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "res shape mismatch");
+  }
+  TORCH_CHECK(D % 8 == 0 && D <= 4096, "norm: D % 8 == 0 and D <= 4096");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor y = at::empty_like(x);
+  Tensor sum = has_res ? at::empty_like(x) : Tensor();
+  Tensor mean = ln ? at::empty({M}, f32) : Tensor();
+  Tensor rstd = at::empty({M}, f32);
+  CML_CHECK_HIP(cml::launch_norm_fwd(ln ? 1 : 0, x.data_ptr(), has_res ? res->data_ptr() : nullptr,
+                                     w.data_ptr(), ln ? b->data_ptr() : nullptr, y.data_ptr(),
+                                     has_res ? sum.data_ptr() : nullptr,
+                                     ln ? mean.data_ptr<float>() : nullptr, rstd.data_ptr<float>(),
+                                     M, static_cast<int>(D), static_cast<float>(eps),
+                                     cur_stream()));
+  return {y, sum, mean, rstd};
+}
+
+// Returns (dx, dw, db|undef). dres (optional) is added to dx.
+std::vector<Tensor> norm_bwd(const Tensor& dy_in, const optional<Tensor>& dres_in, const Tensor& x,
+                             const Tensor& w, const optional<Tensor>& mean, const Tensor& rstd) {
+  check_bf16c(x, "x");
+  const int64_t D = x.size(-1);
+  const int64_t M = x.numel() / D;
+  Tensor dy = dy_in.contiguous();
+  check_bf16c(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "dy shape mismatch");
+  Tensor dres;
+  if (dres_in.has_value() && dres_in->defined()) {
+    dres = dres_in->contiguous();
+    check_bf16c(dres, "dres");
+    TORCH_CHECK(dres.sizes() == x.sizes(), "dres shape mismatch");
+  }
+  check_bf16c(w, "w");
+  const bool ln = mean.has_value() && mean->defined();
+  TORCH_CHECK(rstd.is_cuda() && rstd.scalar_type() == at::kFloat && rstd.numel() == M, "rstd: fp32 [M]");
+  if (ln) TORCH_CHECK(mean->scalar_type() == at::kFloat && mean->numel() == M, "mean: fp32 [M]");
+  TORCH_CHECK(D % 8 == 0 && D <= 4096, "norm: D % 8 == 0 and D <= 4096");
+  const c10::DeviceGuard guard(x.device());
+  Tensor dx = at::empty_like(x);
+  Tensor dw = at::empty_like(w);
+  Tensor db = ln ? at::empty_like(w) : Tensor();
+  Tensor work = at::empty({static_cast<int64_t>(cml::norm_workspace_bytes(M, static_cast<int>(D)) / 4 + 1)},
+                          x.options().dtype(at::kFloat));
+  CML_CHECK_HIP(cml::launch_norm_bwd(ln ? 1 : 0, dy.data_ptr(), dres.defined() ? dres.data_ptr() : nullptr,
+                                     x.data_ptr(), w.data_ptr(), ln ? mean->data_ptr<float>() : nullptr,
+                                     rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr(),
+                                     ln ? db.data_ptr() : nullptr, M, static_cast<int>(D),
+                                     work.data_ptr(), cur_stream()));
+  return {dx, dw, db};
+}
+
+void check_rope_tables(const optional<Tensor>& c, const optional<Tensor>& s, int64_t S, int64_t hd) {
+  if (!(c.has_value() && c->defined())) return;
+  TORCH_CHECK(s.has_value() && s->defined(), "rope: cos without sin");
+  for (const Tensor* t : {&*c, &*s}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                    t->numel() >= S * (hd / 2), "rope tables: contiguous fp32 [S, hd/2]");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "rope tables must be 16-B aligned");
+  }
+}
+
+std::vector<Tensor> rope_fwd(const Tensor& qkv, const optional<Tensor>& cosb,
+                             const optional<Tensor>& sinb, int64_t H, int64_t KV, int64_t hd) {
+  check_bf16c(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == (H + 2 * KV) * hd && hd % 8 == 0,
+              "qkv must be [B, S, (H + 2 KV) hd] with hd % 8 == 0");
+  const int64_t B = qkv.size(0), S = qkv.size(1);
+  check_rope_tables(cosb, sinb, S, hd);
+  const c10::DeviceGuard guard(qkv.device());
+  Tensor q = at::empty({B, H, S, hd}, qkv.options());
+  Tensor k = at::empty({B, KV, S, hd}, qkv.options());
+  Tensor v = at::empty({B, KV, S, hd}, qkv.options());
+  const bool rot = cosb.has_value() && cosb->defined();
+  CML_CHECK_HIP(cml::launch_rope_fwd(qkv.data_ptr(), rot ? cosb->data_ptr<float>() : nullptr,
+                                     rot ? sinb->data_ptr<float>() : nullptr, q.data_ptr(),
+                                     k.data_ptr(), v.data_ptr(), B, S, H, KV, hd, cur_stream()));
+  return {q, k, v};
+}
+
+Tensor rope_bwd(const Tensor& dq_in, const Tensor& dk_in, const Tensor& dv_in,
+                const optional<Tensor>& cosb, const optional<Tensor>& sinb) {
+  Tensor dq = dq_in.contiguous(), dk = dk_in.contiguous(), dv = dv_in.contiguous();
+  check_bf16c(dq, "dq");
+  check_bf16c(dk, "dk");
+  check_bf16c(dv, "dv");
+  TORCH_CHECK(dq.dim() == 4 && dk.dim() == 4 && dk.sizes() == dv.sizes() &&
+                  dq.size(0) == dk.size(0) && dq.size(2) == dk.size(2) && dq.size(3) == dk.size(3),
+              "dq [B, H, S, hd], dk / dv [B, KV, S, hd]");
+  const int64_t B = dq.size(0), H = dq.size(1), S = dq.size(2), hd = dq.size(3), KV = dk.size(1);
+  TORCH_CHECK(hd % 8 == 0, "hd % 8 == 0");
+  check_rope_tables(cosb, sinb, S, hd);
+  const c10::DeviceGuard guard(dq.device());
+  Tensor dqkv = at::empty({B, S, (H + 2 * KV) * hd}, dq.options());
+  const bool rot = cosb.has_value() && cosb->defined();
+  CML_CHECK_HIP(cml::launch_rope_bwd(dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                                     rot ? cosb->data_ptr<float>() : nullptr,
+                                     rot ? sinb->data_ptr<float>() : nullptr, dqkv.data_ptr(), B,
+                                     S, H, KV, hd, cur_stream()));
+  return dqkv;
+}
+
+Tensor swiglu_fwd(const Tensor& h) {
+  check_bf16c(h, "h");
+  const int64_t F2 = h.size(-1);
+  TORCH_CHECK(F2 % 16 == 0, "swiglu: last dim must be 2F with F % 8 == 0");
+  const int64_t M = h.numel() / F2;
+  const c10::DeviceGuard guard(h.device());
+  auto sizes = h.sizes().vec();
+  sizes.back() = F2 / 2;
+  Tensor y = at::empty(sizes, h.options());
+  CML_CHECK_HIP(cml::launch_swiglu_fwd(h.data_ptr(), y.data_ptr(), M, static_cast<int>(F2 / 2),
+                                       cur_stream()));
+  return y;
+}
+
+Tensor swiglu_bwd(const Tensor& dy_in, const Tensor& h) {
+  check_bf16c(h, "h");
+  Tensor dy = dy_in.contiguous();
+  check_bf16c(dy, "dy");
+  const int64_t F2 = h.size(-1);
+  const int64_t M = h.numel() / F2;
+  TORCH_CHECK(F2 % 16 == 0 && dy.numel() == M * (F2 / 2), "swiglu_bwd shape mismatch");
+  const c10::DeviceGuard guard(h.device());
+  Tensor dh = at::empty_like(h);
+  CML_CHECK_HIP(cml::launch_swiglu_bwd(dy.data_ptr(), h.data_ptr(), dh.data_ptr(), M,
+                                       static_cast<int>(F2 / 2), cur_stream()));
+  return dh;
+}
+
+// column sums of x viewed as [M, N] (N = last dim) -> bf16 [N]
+Tensor colsum(const Tensor& x_in) {
+  Tensor x = x_in.contiguous();
+  check_bf16c(x, "x");
+  const int64_t N = x.size(-1);
+  const int64_t M = x.numel() / N;
+  TORCH_CHECK(N % 8 == 0 && M >= 1 && (M + 63) / 64 <= 65535, "colsum: N % 8 == 0, M <= 4M rows");
+  const c10::DeviceGuard guard(x.device());
+  Tensor out = at::empty({N}, x.options());
+  Tensor work = at::empty({static_cast<int64_t>(cml::colsum_workspace_bytes(M, static_cast<int>(N)) / 4 + 1)},
+                          x.options().dtype(at::kFloat));
+  CML_CHECK_HIP(cml::launch_colsum(x.data_ptr(), M, static_cast<int>(N), out.data_ptr(),
+                                   work.data_ptr(), cur_stream()));
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -301,6 +506,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd, "fused NHWC BatchNorm(+res)(+ReLU) backward");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
+  m.def("ce_fwd", &ce_fwd, "fused cross-entropy forward over bf16 logits (lse, per-row loss)");
+  m.def("ce_bwd", &ce_bwd, "fused cross-entropy backward (bf16 logits gradient)");
+  m.def("norm_fwd", &norm_fwd, "LayerNorm / RMSNorm (+ residual add) forward");
+  m.def("norm_bwd", &norm_bwd, "LayerNorm / RMSNorm backward (+ residual gradient)");
+  m.def("rope_fwd", &rope_fwd, "QKV split + RoPE into head-major q / k / v");
+  m.def("rope_bwd", &rope_bwd, "inverse of rope_fwd");
+  m.def("swiglu_fwd", &swiglu_fwd, "silu(a) * b over [a | b]");
+  m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
+  m.def("colsum", &colsum, "column sums of a bf16 matrix (bias gradient)");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);
   m.attr("OPT_NONE") = static_cast<int>(cml::OPT_NONE);

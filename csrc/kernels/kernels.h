@@ -99,4 +99,39 @@ hipError_t launch_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, 
 hipError_t launch_fault(int dtype, void* g, int64_t D, int kind, float scale, float sigma,
                         uint64_t seed, hipStream_t stream);
 
+// ---- transformer ops (transformer.hip); bf16 activations, fp32 statistics.
+// Cross-entropy over contiguous bf16 logits [R, V] (16-B aligned base): forward writes the
+// per-row logsumexp and loss (0 for ignored rows); backward writes
+// grad = (*scale) * (softmax - onehot) (0 rows for ignored labels), scale = dloss / n_valid.
+hipError_t launch_ce_fwd(const void* logits, int64_t R, int V, const int64_t* labels,
+                         int64_t ignore, float* lse, float* loss, hipStream_t stream);
+hipError_t launch_ce_bwd(const void* logits, int64_t R, int V, const int64_t* labels,
+                         int64_t ignore, const float* lse, const float* scale, void* grad,
+                         hipStream_t stream);
+// LayerNorm (ln = 1, with bias b and mean) or RMSNorm (ln = 0) over rows of D (D % 8 == 0,
+// D <= 4096). res != null: normalise x + res and write the bf16 sum to `sum`.
+// Backward: dx (+ dres if given) and dw (+ db) via norm_workspace_bytes of partials.
+size_t norm_workspace_bytes(int64_t M, int D);
+hipError_t launch_norm_fwd(int ln, const void* x, const void* res, const void* w, const void* b,
+                           void* y, void* sum, float* mean, float* rstd, int64_t M, int D,
+                           float eps, hipStream_t stream);
+hipError_t launch_norm_bwd(int ln, const void* dy, const void* dres, const void* x,
+                           const void* w, const float* mean, const float* rstd, void* dx,
+                           void* dw, void* db, int64_t M, int D, void* work, hipStream_t stream);
+// qkv [B, S, (H + 2 KV) hd] -> q [B, H, S, hd], k / v [B, KV, S, hd] with interleaved-pair RoPE
+// on q / k from fp32 cos / sin [S, hd / 2] (null: no rotation); backward is the inverse.
+hipError_t launch_rope_fwd(const void* qkv, const float* cosb, const float* sinb, void* q, void* k,
+                           void* v, int B, int S, int H, int KV, int hd, hipStream_t stream);
+hipError_t launch_rope_bwd(const void* dq, const void* dk, const void* dv, const float* cosb,
+                           const float* sinb, void* dqkv, int B, int S, int H, int KV, int hd,
+                           hipStream_t stream);
+// SwiGLU over h = [a | b] ([M, 2F]): y = silu(a) * b; backward writes dh [M, 2F].
+hipError_t launch_swiglu_fwd(const void* h, void* y, int64_t M, int F, hipStream_t stream);
+hipError_t launch_swiglu_bwd(const void* dy, const void* h, void* dh, int64_t M, int F,
+                             hipStream_t stream);
+// Column sums of a bf16 [M, N] matrix (bias gradients), fp32 accumulation, bf16 out.
+size_t colsum_workspace_bytes(int64_t M, int N);
+hipError_t launch_colsum(const void* x, int64_t M, int N, void* out, void* work,
+                         hipStream_t stream);
+
 }  // namespace cml
