@@ -46,8 +46,9 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", action="store_true", help="(reserved) capture step in a hipGraph")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--conv1x1", choices=["gemm", "miopen"], default="miopen",
-                    help="1x1 stride-1 convs as MIOpen convolutions (default) or hipBLASLt GEMMs")
+    ap.add_argument("--conv1x1", choices=["auto", "gemm", "miopen"], default="auto",
+                    help="1x1 stride-1 conv forward / data gradient as hipBLASLt GEMMs: per-shape "
+                         "measured choice (auto), always, or never (MIOpen)")
     ap.add_argument("--profile-marker", action="store_true",
                     help="launch a spin_kernel between warmup and timed steps (prof_summary --after)")
     ap.add_argument("--no-miopen-find", action="store_true",
@@ -128,7 +129,7 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info):
 def main():
     args = parse()
     from consensusml_amd.models import resnet as _resnet
-    _resnet.CONV1X1_GEMM = args.conv1x1 == "gemm"
+    _resnet.CONV1X1_GEMM = args.conv1x1
     if not args.no_miopen_find:
         from consensusml_amd.utils.tuning import configure_miopen
         configure_miopen()

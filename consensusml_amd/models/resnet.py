@@ -18,65 +18,103 @@ import torch.nn.functional as F
 from ..ops.bn import BatchNormAct2d, ResidualLink, fused_ok
 from ..ops.pool import max_pool2d
 
-# 1x1 stride-1 convolutions as plain GEMMs (see Conv1x1); toggled by bench.py --conv1x1.
-# Off by default: measured on MI355X at batch 512 the hipBLASLt kernels chosen for these
-# tall-skinny shapes (e.g. dW with K = N*H*W = 1.6M and a 64x64 output tile grid of 4) made the
-# step 77 ms vs 55 ms with MIOpen's 1x1 solvers (profiles/r01_bench8_conv1x1_gemm_kernels.md).
-CONV1X1_GEMM = os.environ.get("CML_CONV1X1_GEMM", "0") == "1"
+# 1x1 stride-1 convolutions: which passes run as plain GEMMs (hipBLASLt) instead of MIOpen.
+#   "auto"   per-shape choice measured on MI355X at batch 512 (bench/conv_shapes.py,
+#            profiles/r01_conv_shapes9.jsonl): hipBLASLt wins the data gradient dX = dY W whenever
+#            the conv reduces channels (Cout < Cin: every bottleneck conv1, 1.3-1.4x) or the
+#            spatial size is small (H*W <= 196: layer3/4 conv3, 1.7x), and the forward for
+#            Cin >= 1024 (1.4x); MIOpen keeps everything else and every weight gradient (its
+#            wrw kernels are 2-12x faster than a GEMM with K = N*H*W).
+#   "gemm"   forward and data gradient always GEMMs;  "miopen"  never.
+# True / False (older callers) mean "gemm" / "miopen".
+CONV1X1_GEMM = os.environ.get("CML_CONV1X1_GEMM", "auto")
 # identity blocks fuse the residual-gradient add into conv1's dX GEMM (see ops.bn.ResidualLink)
 RESIDUAL_LINK = True
 
 
+def conv1x1_policy(cin: int, cout: int, hw: int):
+    """(forward as GEMM, data gradient as GEMM) for a 1x1 stride-1 conv."""
+    mode = CONV1X1_GEMM
+    if mode is True or mode == "gemm":
+        return True, True
+    if mode is False or mode == "miopen":
+        return False, False
+    return cin >= 1024, (cout < cin) or hw <= 196
+
+
 class _Conv1x1Fn(torch.autograd.Function):
-    """y = x W^T on [M, Cin] rows; backward dX = dY W accumulated into a linked residual
-    gradient when one is parked (ResidualLink), dW = dY^T X."""
+    """1x1 stride-1 conv on a channels_last tensor x [N, C, H, W] (= row-major [M, C] rows).
+
+    forward: y = x W^T as one GEMM (fwd_gemm) or MIOpen. backward: dX = dY W as a GEMM
+    (dgrad_gemm; accumulated in place into a residual gradient parked on ``link`` — the GEMM's
+    beta = 1 epilogue replaces an elementwise add) or MIOpen; dW always MIOpen's backward-weight
+    (``aten.convolution_backward`` with only the weight output requested)."""
 
     @staticmethod
-    def forward(ctx, x2d, w2d, link):
-        ctx.save_for_backward(x2d, w2d)
+    def forward(ctx, x, w, link, fwd_gemm, dgrad_gemm):
+        ctx.save_for_backward(x, w)
         ctx.link = link
-        return torch.mm(x2d, w2d.t())
+        ctx.dgrad_gemm = dgrad_gemm
+        N, C, H, W = x.shape
+        if fwd_gemm:
+            y = torch.mm(x.permute(0, 2, 3, 1).reshape(N * H * W, C), w.reshape(w.shape[0], C).t())
+            return y.view(N, H, W, w.shape[0]).permute(0, 3, 1, 2)
+        return F.conv2d(x, w)
 
     @staticmethod
     def backward(ctx, dy):
-        x2d, w2d = ctx.saved_tensors
-        dx = None
-        if ctx.needs_input_grad[0]:
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        N, C, H, W = x.shape
+        Co = w.shape[0]
+        need_dx = ctx.needs_input_grad[0]
+        mio_dx = need_dx and not ctx.dgrad_gemm
+        dx_m, dw, _ = torch.ops.aten.convolution_backward(
+            dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+            [mio_dx, ctx.needs_input_grad[1], False])
+        dx = dx_m if mio_dx else None
+        if need_dx and ctx.dgrad_gemm:
+            dy2 = dy.permute(0, 2, 3, 1).reshape(N * H * W, Co)
+            w2 = w.reshape(Co, C)
             link = ctx.link
-            if link is not None and link.grad is not None:
-                g = link.grad
-                link.grad = None
-                dres = g.permute(0, 2, 3, 1).reshape(dy.shape[0], -1) if g.dim() == 4 else g
+            g = link.take() if link is not None else None
+            if g is not None:
+                dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
                 if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
-                    dx = dres.addmm_(dy, w2d)          # beta = 1 GEMM epilogue, in place
+                    d2 = dres.addmm_(dy2, w2)          # beta = 1 GEMM epilogue, in place
                 else:
-                    dx = torch.addmm(dres, dy, w2d)
+                    d2 = torch.addmm(dres, dy2, w2)
             else:
-                dx = torch.mm(dy, w2d)
-        dw = torch.mm(dy.t(), x2d) if ctx.needs_input_grad[1] else None
-        return dx, dw, None
+                d2 = torch.mm(dy2, w2)
+            dx = d2.view(N, H, W, C).permute(0, 3, 1, 2)
+        return dx, dw, None, None, None
 
 
 class Conv1x1(nn.Conv2d):
-    """1x1 convolution. With stride 1 on a channels_last GPU tensor, the NHWC activation IS a
-    row-major [N*H*W, C] matrix, so the conv is one GEMM (``F.linear`` -> hipBLASLt) and its
-    backward two more (dX = dY W, dW = dY^T X) — no im2col, no layout change, output already
-    channels_last. These are 8/17 of a bottleneck's FLOPs. Strided 1x1 (downsample) convs and CPU
-    tensors use the regular MIOpen / ATen convolution. Same parameter as nn.Conv2d."""
+    """1x1 convolution. With stride 1 on a channels_last GPU tensor the NHWC activation IS a
+    row-major [N*H*W, C] matrix, so the forward and the data gradient can be single GEMMs (no
+    im2col, no layout change) — chosen per shape by ``conv1x1_policy``. Strided 1x1 (downsample)
+    convs and CPU tensors use the regular MIOpen / ATen convolution. Same parameter as
+    nn.Conv2d."""
 
     def __init__(self, cin: int, cout: int, stride: int = 1):
         super().__init__(cin, cout, 1, stride=stride, bias=False)
 
-    def gemm_ok(self, x: torch.Tensor) -> bool:
-        return (CONV1X1_GEMM and self.stride == (1, 1) and x.is_cuda
-                and x.is_contiguous(memory_format=torch.channels_last))
+    def _policy(self, x: torch.Tensor):
+        if not (self.stride == (1, 1) and x.is_cuda and x.dim() == 4
+                and x.is_contiguous(memory_format=torch.channels_last)):
+            return False, False
+        return conv1x1_policy(self.in_channels, self.out_channels, x.shape[2] * x.shape[3])
+
+    def link_ok(self, x: torch.Tensor) -> bool:
+        """True when the data gradient is a GEMM that can absorb a parked residual gradient."""
+        return self._policy(x)[1]
 
     def forward(self, x: torch.Tensor, res_link: Optional[ResidualLink] = None) -> torch.Tensor:
-        if self.gemm_ok(x):
-            N, C, H, W = x.shape
-            y = _Conv1x1Fn.apply(x.permute(0, 2, 3, 1).reshape(N * H * W, C),
-                                 self.weight.reshape(self.out_channels, C), res_link)
-            return y.view(N, H, W, self.out_channels).permute(0, 3, 1, 2)
+        fwd_gemm, dgrad_gemm = self._policy(x)
+        if fwd_gemm or dgrad_gemm:
+            return _Conv1x1Fn.apply(x, self.weight, res_link if dgrad_gemm else None, fwd_gemm,
+                                    dgrad_gemm)
         return super().forward(x)
 
 
@@ -104,7 +142,7 @@ class Bottleneck(nn.Module):
             # the producing block); conv1's GEMM backward (if used) or the producer's BN backward
             # consumes it (see ops.bn.ResidualLink)
             link = getattr(x, "_cml_link", None) if use_links else None
-            out = self.bn1(self.conv1(x, res_link=link if self.conv1.gemm_ok(x) else None))
+            out = self.bn1(self.conv1(x, res_link=link if self.conv1.link_ok(x) else None))
             out = self.bn2(self.conv2(out))
             z = self.conv3(out)
             fused = fused_ok(z, self.bn3.weight)

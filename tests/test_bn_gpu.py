@@ -116,14 +116,19 @@ def test_maxpool_nhwc(cuda, shape, ksp):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("cin,cout", [(64, 256), (256, 64), (24, 40)])
-def test_conv1x1_gemm_matches_conv(cuda, cin, cout):
+@pytest.mark.parametrize("mode", ["auto", "gemm", "miopen"])
+@pytest.mark.parametrize("cin,cout", [(64, 256), (256, 64), (24, 40), (1024, 256)])
+def test_conv1x1_gemm_matches_conv(cuda, cin, cout, mode):
     from consensusml_amd.models import resnet as R
     torch.manual_seed(0)
     m = R.Conv1x1(cin, cout).to(cuda, torch.bfloat16).to(memory_format=torch.channels_last)
     x = torch.randn(4, cin, 9, 7, device=cuda, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
     x.requires_grad_(True)
-    y = m(x)
+    R.CONV1X1_GEMM = mode
+    try:
+        y = m(x)
+    finally:
+        R.CONV1X1_GEMM = "auto"
     assert y.is_contiguous(memory_format=torch.channels_last)
     g = torch.randn_like(y)
     y.backward(g)
@@ -136,7 +141,7 @@ def test_conv1x1_gemm_matches_conv(cuda, cin, cout):
     torch.testing.assert_close(m.weight.grad.float(), wr.grad, rtol=2e-2, atol=1e-1)
 
 
-@pytest.mark.parametrize("gemm", [False, True])
+@pytest.mark.parametrize("gemm", [False, True, "auto"])
 def test_residual_link_matches_autograd_add(cuda, gemm):
     """Downsample block + 3 identity blocks: with the residual gradient parked on the producer's
     link (consumed as dy2 by the producer's BN backward, or by conv1's GEMM epilogue) and the
@@ -161,7 +166,7 @@ def test_residual_link_matches_autograd_add(cuda, gemm):
             res.append((x.grad.clone(), [p.grad.clone() for p in net.parameters()]))
     finally:
         R.RESIDUAL_LINK = True
-        R.CONV1X1_GEMM = False
+        R.CONV1X1_GEMM = "auto"
     # fp32 reference: same weights, composition path (no fused kernels, no links)
     ref = copy.deepcopy(net).float().to(memory_format=torch.contiguous_format)
     xr = x0.float().contiguous().requires_grad_(True)
