@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.bn import BatchNormAct2d, ResidualLink, fused_ok
+from ..ops.bn import BatchNormAct2d, ResidualLink, fused_ok, link_tap
 from ..ops.pool import max_pool2d
 
 # 1x1 stride-1 convolutions: which passes run as plain GEMMs (hipBLASLt) instead of MIOpen.
@@ -30,6 +30,8 @@ from ..ops.pool import max_pool2d
 CONV1X1_GEMM = os.environ.get("CML_CONV1X1_GEMM", "auto")
 # identity blocks fuse the residual-gradient add into conv1's dX GEMM (see ops.bn.ResidualLink)
 RESIDUAL_LINK = True
+# stem input channels zero-padded 3 -> 4 on the GPU (see ResNet.stem)
+STEM_PAD4 = os.environ.get("CML_STEM_PAD4", "1") == "1"
 
 
 def conv1x1_policy(cin: int, cout: int, hw: int):
@@ -149,10 +151,16 @@ class Bottleneck(nn.Module):
             out_link = ResidualLink() if use_links and fused else None
             y = self.bn3(z, residual=x, res_link=link if fused else None, out_link=out_link)
         else:
-            idt = self.down_bn(self.down_conv(x))
-            out = self.bn1(self.conv1(x))
+            # x feeds conv1 and down_conv. When conv1's data gradient is a GEMM, down_conv's dX is
+            # parked on a link (link_tap) and absorbed by that GEMM's beta = 1 epilogue instead of
+            # an elementwise add. The downsample branch is built after the main branch so that
+            # autograd (ready nodes in reverse creation order) runs its backward first; the link
+            # falls back to a normal add if that order ever changes.
+            dlink = ResidualLink() if use_links and self.conv1.link_ok(x) else None
+            out = self.bn1(self.conv1(x, res_link=dlink))
             out = self.bn2(self.conv2(out))
             z = self.conv3(out)
+            idt = self.down_bn(self.down_conv(link_tap(x, dlink) if dlink is not None else x))
             out_link = ResidualLink() if use_links and fused_ok(z, self.bn3.weight) else None
             y = self.bn3(z, residual=idt, out_link=out_link)
         if out_link is not None:
@@ -178,6 +186,19 @@ class ResNet(nn.Module):
             if isinstance(m, Bottleneck):
                 nn.init.zeros_(m.bn3.weight)
 
+    def stem(self, x: torch.Tensor) -> torch.Tensor:
+        """7x7/2 conv. bf16 NHWC GPU images with 3 channels are zero-padded to 4 (one HIP pass)
+        and the weight likewise (a view-sized pad), so MIOpen runs its vectorised NHWC kernels:
+        1.4x faster forward and weight gradient (bench/stem_pad.py). Same math, same parameter."""
+        w = self.conv1.weight
+        if (STEM_PAD4 and x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] == 3
+                and x.is_contiguous(memory_format=torch.channels_last) and not x.requires_grad):
+            from ..ops.native import lib
+            x4 = lib().pad_c4(x)
+            w4 = F.pad(w, (0, 0, 0, 0, 0, 1)).contiguous(memory_format=torch.channels_last)
+            return F.conv2d(x4, w4, stride=2, padding=3)
+        return self.conv1(x)
+
     def _make(self, planes: int, blocks: int, stride: int) -> nn.Sequential:
         down = stride != 1 or self.inplanes != planes * 4
         mods = [Bottleneck(self.inplanes, planes, stride, down)]
@@ -186,7 +207,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.bn1(self.conv1(x))
+        x = self.bn1(self.stem(x))
         x = max_pool2d(x, 3, 2, 1)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -30,14 +30,48 @@ class ResidualLink:
         sums it on load (``bn_bwd`` with dy2) — the add pass disappears.
     bn3's backward always runs before conv1's and before the previous block's BN backward (both
     depend on it through the graph), so the hand-off is ordered by the graph itself."""
-    __slots__ = ("grad",)
+    __slots__ = ("grad", "closed")
 
     def __init__(self):
         self.grad = None
+        self.closed = False
 
     def take(self):
+        """Consumer side: the parked gradient (or None); later producers keep their own."""
         g, self.grad = self.grad, None
+        self.closed = True
         return g
+
+
+# how often link_tap parked its gradient vs fell back to a normal add (tests pin the order)
+TAP_STATS = {"parked": 0, "fallback": 0}
+
+
+class _LinkTapFn(torch.autograd.Function):
+    """Identity whose backward parks the incoming gradient on a ResidualLink instead of
+    returning it, so a GEMM consumer on a parallel branch can absorb it with its beta = 1
+    epilogue (a downsample block's input feeds both down_conv and conv1: their two data
+    gradients would otherwise meet in an elementwise add). If the consumer already ran, the
+    gradient flows normally and autograd adds it."""
+
+    @staticmethod
+    def forward(ctx, x, link):
+        ctx.link = link
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        link = ctx.link
+        if link.closed or link.grad is not None:
+            TAP_STATS["fallback"] += 1
+            return g, None
+        TAP_STATS["parked"] += 1
+        link.grad = g.contiguous(memory_format=torch.channels_last) if g.dim() == 4 else g.contiguous()
+        return None, None
+
+
+def link_tap(x: torch.Tensor, link: "ResidualLink") -> torch.Tensor:
+    return _LinkTapFn.apply(x, link)
 
 
 class _BNActFn(torch.autograd.Function):

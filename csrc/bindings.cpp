@@ -277,6 +277,18 @@ Tensor maxpool_bwd(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W,
   return dx;
 }
 
+// x [N, C, H, W] channels_last bf16, C <= 4 -> [N, 4, H, W] channels_last, zero channels C..3
+Tensor pad_c4(const Tensor& x) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(1) >= 1 && x.size(1) <= 4, "pad_c4: 4-D NHWC with C <= 4");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const c10::DeviceGuard guard(x.device());
+  Tensor y = at::empty({N, 4, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  CML_CHECK_HIP(cml::launch_pad_c4(x.data_ptr(), y.data_ptr(), N * H * W, static_cast<int>(C),
+                                   cur_stream()));
+  return y;
+}
+
 void fault(Tensor& g, int64_t kind, double scale, double sigma, int64_t seed) {
   check_dev(g, "g");
   TORCH_CHECK(g.is_contiguous(), "g must be contiguous");
@@ -506,6 +518,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd, "fused NHWC BatchNorm(+res)(+ReLU) backward");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
+  m.def("pad_c4", &pad_c4, "NHWC bf16 channel zero-padding to 4");
   m.def("ce_fwd", &ce_fwd, "fused cross-entropy forward over bf16 logits (lse, per-row loss)");
   m.def("ce_bwd", &ce_bwd, "fused cross-entropy backward (bf16 logits gradient)");
   m.def("norm_fwd", &norm_fwd, "LayerNorm / RMSNorm (+ residual add) forward");

@@ -94,38 +94,47 @@ __global__ __launch_bounds__(kBT) void bn_stats_kernel(const bf16* __restrict__ 
   block_partial(s, q, tpr, C, part);
 }
 
-// Fold the [nb][2][C] slab for 32 channels per workgroup: 8 slices of the partial blocks per
-// channel, 4 independent fp64 accumulators per thread (loads stay in flight), then a fixed-order
-// LDS combine -> deterministic (s, q) per channel in the first 32 threads.
-constexpr int kFC = 32;               // channels per finalize workgroup
+// Fold the [nb][2][C] slab for 8 channels per workgroup: 32 slices of the partial blocks per
+// channel, 8 partials (16 loads) in flight per thread, fp64 accumulation, then a fixed-order LDS
+// combine -> deterministic (s, q) per channel in the first 8 threads. The fold is latency-bound
+// (nb <= 1024 partials, L2-resident), so the slices keep every thread's chain of dependent load
+// rounds at nb / 256 (4 for nb = 1024); 32 channels x 8 slices took ~13 us per BN layer.
+constexpr int kFC = 8;                // channels per finalize workgroup
 constexpr int kFS = kBT / kFC;        // partial-block slices
 __device__ __forceinline__ bool fold_partials(const float* __restrict__ part, int nb, int C,
                                               double& s_out, double& q_out, int& c_out) {
   __shared__ double ls[kFS][kFC], lq[kFS][kFC];
   const int cl = threadIdx.x % kFC, sl = threadIdx.x / kFC;
   const int c = blockIdx.x * kFC + cl;
-  double s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+  double S = 0.0, Q = 0.0;
   if (c < C) {
     int b = sl;
-    for (; b + 3 * kFS < nb; b += 4 * kFS) {
+    for (; b + 7 * kFS < nb; b += 8 * kFS) {
+      float s[8], q[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const float* p = part + static_cast<int64_t>(b + u * kFS) * 2 * C;
-        s[u] += p[c];
-        q[u] += p[C + c];
+        s[u] = p[c];
+        q[u] = p[C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        S += s[u];
+        Q += q[u];
       }
     }
     for (; b < nb; b += kFS) {
       const float* p = part + static_cast<int64_t>(b) * 2 * C;
-      s[0] += p[c];
-      q[0] += p[C + c];
+      S += p[c];
+      Q += p[C + c];
     }
   }
-  ls[sl][cl] = (s[0] + s[1]) + (s[2] + s[3]);
-  lq[sl][cl] = (q[0] + q[1]) + (q[2] + q[3]);
+  ls[sl][cl] = S;
+  lq[sl][cl] = Q;
   __syncthreads();
   if (sl != 0 || c >= C) return false;
-  double S = 0.0, Q = 0.0;
+  S = 0.0;
+  Q = 0.0;
 #pragma unroll
   for (int k = 0; k < kFS; ++k) {
     S += ls[k][cl];

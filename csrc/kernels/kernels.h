@@ -95,6 +95,9 @@ hipError_t launch_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, i
 hipError_t launch_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W,
                               int C, int OH, int OW, int k, int s, int p, hipStream_t stream);
 
+// NHWC bf16 channel zero-padding C (<= 4) -> 4 over npix pixels (y 8-B aligned).
+hipError_t launch_pad_c4(const void* x, void* y, int64_t npix, int C, hipStream_t stream);
+
 // Elementwise fault injection on a local gradient (Byzantine simulation, N10).
 hipError_t launch_fault(int dtype, void* g, int64_t D, int kind, float scale, float sigma,
                         uint64_t seed, hipStream_t stream);

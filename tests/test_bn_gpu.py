@@ -156,6 +156,8 @@ def test_residual_link_matches_autograd_add(cuda, gemm):
     x0 = torch.randn(4, 32, 10, 10, device=cuda).to(torch.bfloat16).to(memory_format=torch.channels_last)
     res = []
     R.CONV1X1_GEMM = gemm
+    from consensusml_amd.ops.bn import TAP_STATS
+    TAP_STATS.update(parked=0, fallback=0)
     try:
         for link in (True, False):
             R.RESIDUAL_LINK = link
@@ -167,6 +169,9 @@ def test_residual_link_matches_autograd_add(cuda, gemm):
     finally:
         R.RESIDUAL_LINK = True
         R.CONV1X1_GEMM = "auto"
+    # the downsample branch's backward runs before conv1's: the tap always parks
+    assert TAP_STATS["fallback"] == 0
+    assert TAP_STATS["parked"] == (0 if gemm is False else 1)
     # fp32 reference: same weights, composition path (no fused kernels, no links)
     ref = copy.deepcopy(net).float().to(memory_format=torch.contiguous_format)
     xr = x0.float().contiguous().requires_grad_(True)
@@ -212,3 +217,22 @@ def test_bn_act_two_part_output_grad(cuda, mode):
     torch.testing.assert_close(x.grad.float(), x2.grad.float(), rtol=2e-2, atol=3e-2)
     if res is not None:
         torch.testing.assert_close(res.grad.float(), r2.grad.float(), rtol=2e-2, atol=3e-2)
+
+
+def test_stem_pad4_matches_conv(cuda):
+    """3 -> 4 channel zero-padded stem (HIP pad kernel + padded weight view) == the plain conv."""
+    from consensusml_amd.models import resnet as R
+    torch.manual_seed(5)
+    m = R.resnet_tiny().to(cuda, torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(3, 3, 33, 31, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for pad in (True, False):
+        R.STEM_PAD4 = pad
+        m.zero_grad(set_to_none=True)
+        y = m.stem(x)
+        y.float().square().sum().backward()
+        outs.append((y.float(), m.conv1.weight.grad.float().clone()))
+    R.STEM_PAD4 = True
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=2e-2, atol=0.5)
+    assert m.conv1.weight.grad.shape == (8, 3, 7, 7)
