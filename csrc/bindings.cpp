@@ -277,6 +277,46 @@ Tensor maxpool_bwd(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W,
   return dx;
 }
 
+// dsts[i].copy_(srcs[i]) for same-dtype, same-numel contiguous 16-B aligned tensors, in launches of
+// up to kMaxCopy entries. Returns the indices that did not qualify (the caller copies those).
+std::vector<int64_t> multi_copy(const std::vector<Tensor>& dsts, const std::vector<Tensor>& srcs) {
+  TORCH_CHECK(dsts.size() == srcs.size(), "multi_copy: list length mismatch");
+  std::vector<int64_t> rest;
+  cml::MultiCopyArgs a{};
+  int64_t nv = 0;
+  auto flush = [&]() {
+    if (a.n == 0) return;
+    a.vpre[a.n] = nv;
+    CML_CHECK_HIP(cml::launch_multi_copy(a, cur_stream()));
+    a = cml::MultiCopyArgs{};
+    nv = 0;
+  };
+  c10::optional<c10::DeviceGuard> guard;
+  for (size_t i = 0; i < dsts.size(); ++i) {
+    const Tensor& d = dsts[i];
+    const Tensor& s = srcs[i];
+    const bool ok = d.is_cuda() && s.is_cuda() && d.device() == s.device() &&
+                    d.scalar_type() == s.scalar_type() && d.numel() == s.numel() &&
+                    d.is_contiguous() && s.is_contiguous() && d.element_size() % 2 == 0 &&
+                    (reinterpret_cast<uintptr_t>(d.data_ptr()) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(s.data_ptr()) & 15) == 0;
+    if (!ok) {
+      rest.push_back(static_cast<int64_t>(i));
+      continue;
+    }
+    if (!guard) guard.emplace(d.device());
+    const int64_t bytes = d.numel() * d.element_size();
+    a.src[a.n] = s.data_ptr();
+    a.dst[a.n] = d.data_ptr();
+    a.bytes[a.n] = bytes;
+    a.vpre[a.n] = nv;
+    nv += bytes / 16;
+    if (++a.n == cml::kMaxCopy) flush();
+  }
+  flush();
+  return rest;
+}
+
 // x [N, C, H, W] channels_last bf16, C <= 4 -> [N, 4, H, W] channels_last, zero channels C..3
 Tensor pad_c4(const Tensor& x) {
   check_nhwc(x, "x");
@@ -518,6 +558,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd, "fused NHWC BatchNorm(+res)(+ReLU) backward");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
+  m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");
   m.def("pad_c4", &pad_c4, "NHWC bf16 channel zero-padding to 4");
   m.def("ce_fwd", &ce_fwd, "fused cross-entropy forward over bf16 logits (lse, per-row loss)");
   m.def("ce_bwd", &ce_bwd, "fused cross-entropy backward (bf16 logits gradient)");

@@ -95,6 +95,18 @@ hipError_t launch_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, i
 hipError_t launch_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, int H, int W,
                               int C, int OH, int OW, int k, int s, int p, hipStream_t stream);
 
+// Multi-tensor copy of up to kMaxCopy (src -> dst, bytes) entries in one launch (16-B aligned
+// pointers, even byte counts). vpre[e] = number of whole 16-B vectors before entry e.
+constexpr int kMaxCopy = 32;
+struct MultiCopyArgs {
+  const void* src[kMaxCopy];
+  void* dst[kMaxCopy];
+  int64_t bytes[kMaxCopy];
+  int64_t vpre[kMaxCopy + 1];
+  int n;
+};
+hipError_t launch_multi_copy(const MultiCopyArgs& args, hipStream_t stream);
+
 // NHWC bf16 channel zero-padding C (<= 4) -> 4 over npix pixels (y 8-B aligned).
 hipError_t launch_pad_c4(const void* x, void* y, int64_t npix, int C, hipStream_t stream);
 

@@ -213,3 +213,25 @@ def test_deterministic_bitwise(cuda):
     m1 = K.aggregate(X, "trimmed_mean", trim=2)
     m2 = K.aggregate(X, "trimmed_mean", trim=2)
     assert torch.equal(m1, m2)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_multi_copy(cuda, dtype):
+    """Gradient capture copy: many tensors (odd sizes, > 32 entries -> several launches), with
+    non-qualifying (misaligned / non-contiguous) entries reported back to the caller."""
+    from consensusml_amd.ops.native import lib
+    torch.manual_seed(0)
+    sizes = [1, 7, 8, 9, 64, 1000, 4099, 123457] * 5
+    buf = torch.zeros(sum(s + 128 for s in sizes), device=cuda, dtype=dtype)
+    dst, src, off = [], [], 0
+    for s in sizes:
+        dst.append(buf[off:off + s])
+        src.append(torch.randn(s, device=cuda).to(dtype))
+        off += (s + 63) // 64 * 64 + 64
+    bad_src = torch.randn(10, device=cuda).to(dtype)[1:]          # misaligned view
+    bad_dst = torch.zeros(9, device=cuda, dtype=dtype)
+    rest = lib().multi_copy(dst + [bad_dst], src + [bad_src])
+    assert rest == [len(dst)]
+    torch.cuda.synchronize()
+    for d, s in zip(dst, src):
+        assert torch.equal(d, s)
