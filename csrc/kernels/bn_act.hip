@@ -81,7 +81,23 @@ __global__ __launch_bounds__(kBT) void bn_stats_kernel(const bf16* __restrict__ 
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t lo = static_cast<int64_t>(blockIdx.x) * rpb;
   const int64_t hi = lo + rpb < M ? lo + rpb : M;
-  for (int64_t r = lo + r0; r < hi; r += rpi) {
+  // 4 rows (4 x 16-B loads) in flight per lane: one load per iteration left the stats pass
+  // latency-bound at ~4.3 TB/s (profiles/r01_prof17_*)
+  int64_t r = lo + r0;
+  for (; r + 3 * rpi < hi; r += 4 * rpi) {
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ld8(x + (r + u * rpi) * C + 8 * g, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = v[u][k] - sh[k];
+        s[k] += d;
+        q[k] = fmaf(d, d, q[k]);
+      }
+  }
+  for (; r < hi; r += rpi) {
     float v[8];
     ld8(x + r * C + 8 * g, v);
 #pragma unroll
@@ -199,22 +215,33 @@ __global__ __launch_bounds__(kBT) void bn_apply_kernel(const bf16* __restrict__ 
   float sc[8], bi[8];
   chan_affine(g, mean, invstd, gamma, beta, sc, bi);
   const int64_t rstride = static_cast<int64_t>(gridDim.x) * (kBT / tpr);
-  for (int64_t r = static_cast<int64_t>(blockIdx.x) * (kBT / tpr) + threadIdx.x / tpr; r < M; r += rstride) {
-    float v[8];
-    ld8(x + r * C + 8 * g, v);
-    float rv[8];
-    if constexpr (RES) ld8(res + r * C + 8 * g, rv);
-    uint32_t bits = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float z = fmaf(v[k], sc[k], bi[k]);
-      if constexpr (RES) z += rv[k];
-      if constexpr (MASK) bits |= (z > 0.f ? 1u : 0u) << k;
-      if constexpr (RELU) z = fmaxf(z, 0.f);
-      v[k] = z;
+  // two rows per iteration: both rows' loads are issued before either is used
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * (kBT / tpr) + threadIdx.x / tpr; r < M;
+       r += 2 * rstride) {
+    const bool two = r + rstride < M;
+    float v[2][8], rv[2][8];
+    ld8(x + r * C + 8 * g, v[0]);
+    if constexpr (RES) ld8(res + r * C + 8 * g, rv[0]);
+    if (two) {
+      ld8(x + (r + rstride) * C + 8 * g, v[1]);
+      if constexpr (RES) ld8(res + (r + rstride) * C + 8 * g, rv[1]);
     }
-    store_bf16<8>(y + r * C + 8 * g, v);
-    if constexpr (MASK) mask[r * tpr + g] = static_cast<uint8_t>(bits);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      const int64_t ru = r + u * rstride;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float z = fmaf(v[u][k], sc[k], bi[k]);
+        if constexpr (RES) z += rv[u][k];
+        if constexpr (MASK) bits |= (z > 0.f ? 1u : 0u) << k;
+        if constexpr (RELU) z = fmaxf(z, 0.f);
+        v[u][k] = z;
+      }
+      store_bf16<8>(y + ru * C + 8 * g, v[u]);
+      if constexpr (MASK) mask[ru * tpr + g] = static_cast<uint8_t>(bits);
+    }
   }
 }
 
@@ -271,7 +298,22 @@ __global__ __launch_bounds__(kBT) void bn_bwd_reduce_kernel(const bf16* __restri
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t lo = static_cast<int64_t>(blockIdx.x) * rpb;
   const int64_t hi = lo + rpb < M ? lo + rpb : M;
-  for (int64_t r = lo + threadIdx.x / tpr; r < hi; r += rpi) {
+  int64_t r = lo + threadIdx.x / tpr;
+  for (; r + rpi < hi; r += 2 * rpi) {   // two rows' loads in flight
+    float v[2][8], dz[2][8];
+    ld8(x + r * C + 8 * g, v[0]);
+    ld8(x + (r + rpi) * C + 8 * g, v[1]);
+    load_dz<RM, DY2>(dy, dy2, mask, r, C, g, v[0], sc, bi, dz[0]);
+    load_dz<RM, DY2>(dy, dy2, mask, r + rpi, C, g, v[1], sc, bi, dz[1]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += dz[u][k];
+        q[k] = fmaf(dz[u][k], (v[u][k] - mu[k]) * is[k], q[k]);
+      }
+  }
+  for (; r < hi; r += rpi) {
     float v[8], dz[8];
     ld8(x + r * C + 8 * g, v);
     load_dz<RM, DY2>(dy, dy2, mask, r, C, g, v, sc, bi, dz);
@@ -325,17 +367,27 @@ __global__ __launch_bounds__(kBT) void bn_bwd_apply_kernel(const bf16* __restric
     b[k] = sdzx[8 * g + k] * invM;
   }
   const int64_t rstride = static_cast<int64_t>(gridDim.x) * (kBT / tpr);
-  for (int64_t r = static_cast<int64_t>(blockIdx.x) * (kBT / tpr) + threadIdx.x / tpr; r < M; r += rstride) {
-    float v[8], dz[8], o[8];
-    ld8(x + r * C + 8 * g, v);
-    load_dz<RM, DY2>(dy, dy2, mask, r, C, g, v, sc, bi, dz);
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * (kBT / tpr) + threadIdx.x / tpr; r < M;
+       r += 2 * rstride) {   // two rows' loads in flight
+    const bool two = r + rstride < M;
+    float v[2][8], dz[2][8];
+    ld8(x + r * C + 8 * g, v[0]);
+    if (two) ld8(x + (r + rstride) * C + 8 * g, v[1]);
+    load_dz<RM, DY2>(dy, dy2, mask, r, C, g, v[0], sc, bi, dz[0]);
+    if (two) load_dz<RM, DY2>(dy, dy2, mask, r + rstride, C, g, v[1], sc, bi, dz[1]);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float xh = (v[k] - mu[k]) * is[k];
-      o[k] = sc[k] * (dz[k] - a[k] - xh * b[k]);
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      const int64_t ru = r + u * rstride;
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xh = (v[u][k] - mu[k]) * is[k];
+        o[k] = sc[k] * (dz[u][k] - a[k] - xh * b[k]);
+      }
+      store_bf16<8>(dx + ru * C + 8 * g, o);
+      if constexpr (DRES) store_bf16<8>(dres + ru * C + 8 * g, dz[u]);
     }
-    store_bf16<8>(dx + r * C + 8 * g, o);
-    if constexpr (DRES) store_bf16<8>(dres + r * C + 8 * g, dz);
   }
 }
 
