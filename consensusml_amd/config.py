@@ -76,6 +76,7 @@ class TopologyConfig:
     gossip_weights: tuple = (1 / 3, 1 / 3, 1 / 3)   # self, left, right
     gossip_clip: float = 0.0     # 0 disables neighbour-delta clipping
     gossip_async: bool = False   # delayed gossip: exchange overlaps the next step's compute
+    early_update: bool = True    # gossip, 1 local worker: per-bucket optimizer step in backward
 
     def validate(self) -> None:
         if self.kind not in TOPOLOGIES:

@@ -122,6 +122,17 @@ class ConsensusEngine:
         for i, p in enumerate(fl.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
         self.timings: Dict[str, float] = {}
+        # Gossip with one local worker: the local optimizer step needs nothing from other ranks,
+        # so each bucket's fused AdamW / SGD runs on a side stream as soon as backward has
+        # produced that bucket's gradients (the memory-bound update overlaps the rest of the
+        # backward's GEMMs); step() then only waits for it and does the neighbour exchange. A
+        # parameter's value is not read again once its gradient exists (its last use in backward
+        # produced that gradient), so updating it early is exact.
+        self.early_update = (self.topo == "gossip" and self.V == 1 and dev.type == "cuda"
+                             and cfg.fault.kind not in COLLUSION
+                             and cfg.topology.early_update)
+        self._updated: set = set()
+        self._opt_stream = torch.cuda.Stream(device=dev) if self.early_update else None
 
     # ================================================================ public API
     @property
@@ -149,7 +160,16 @@ class ConsensusEngine:
         """Exchange, aggregate and update (call after all backward passes of the step)."""
         fl = self.flat
         self._flush_row()
-        if not self.overlap or self.cfg.fault.kind in COLLUSION:
+        if self.early_update:
+            for b in fl.buckets:       # buckets whose gradients were never all produced
+                if b.index not in self._updated:
+                    if self.cfg.fault.kind != "none":
+                        apply_faults(fl.flat_grad, self.cfg.fault, self.rank, self.step_count,
+                                     self.group_active, self.cfg.seed + self.step_count,
+                                     cols=slice(b.offset, b.offset + b.length))
+                    self._bucket_update(b)
+            torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
+        elif not self.overlap or self.cfg.fault.kind in COLLUSION:
             apply_faults(fl.flat_grad, self.cfg.fault, self.rank, self.step_count,
                          self.group_active, self.cfg.seed + self.step_count)
         for b in fl.buckets:
@@ -165,6 +185,7 @@ class ConsensusEngine:
             self._step_gossip()
         self._pending.clear()
         self._flushed.clear()
+        self._updated.clear()
         self.step_count += 1
 
     # ================================================================ hooks / launches
@@ -205,6 +226,28 @@ class ConsensusEngine:
         self._flushed.add(b.index)
         if self.overlap and b.index not in self._pending:
             self._launch_bucket(b, inject=True)
+        if self.early_update and complete:
+            self._early_update(b)
+
+    def _early_update(self, b: Bucket) -> None:
+        """Gossip, V == 1: this bucket's local optimizer step on the side stream."""
+        fl = self.flat
+        if self.cfg.fault.kind != "none":
+            apply_faults(fl.flat_grad, self.cfg.fault, self.rank, self.step_count,
+                         self.group_active, self.cfg.seed + self.step_count,
+                         cols=slice(b.offset, b.offset + b.length))
+        st = self._opt_stream
+        st.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(st):
+            self._bucket_update(b)
+        self._updated.add(b.index)
+
+    def _bucket_update(self, b: Bucket) -> None:
+        fl = self.flat
+        m, s1, s2 = self._state(b.offset, b.length)
+        K.agg_update(fl.flat_grad[:, b.offset:b.offset + b.length], combine="weighted", n=self.V,
+                     opt=self._opt_args(gscale=1.0 / self.V), master=m, s1=s1, s2=s2,
+                     param_out=fl.flat_param[b.offset:b.offset + b.length])
 
     def _flush_row(self) -> None:
         for b in self.flat.buckets:
@@ -390,10 +433,11 @@ class ConsensusEngine:
 
     def _step_gossip(self) -> None:
         fl = self.flat
-        opt = self._opt_args(gscale=1.0 / self.V)
-        m, s1, s2 = self._state(0, fl.total)
-        K.agg_update(fl.flat_grad, combine="weighted", n=self.V, opt=opt, master=m, s1=s1, s2=s2,
-                     param_out=fl.flat_param)
+        if not self.early_update:
+            opt = self._opt_args(gscale=1.0 / self.V)
+            m, s1, s2 = self._state(0, fl.total)
+            K.agg_update(fl.flat_grad, combine="weighted", n=self.V, opt=opt, master=m, s1=s1,
+                         s2=s2, param_out=fl.flat_param)
         if not self.group_active or self.N == 1:
             return
         w0, w1, w2 = self.cfg.topology.gossip_weights

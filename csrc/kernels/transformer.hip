@@ -338,17 +338,19 @@ __global__ __launch_bounds__(kTB) void norm_bwd_kernel(const bf16* __restrict__ 
   const float invD = 1.f / static_cast<float>(D);
   // rows r = grp, grp + ngrp, ... (WPR > 1: one row per workgroup, uniform trip counts); the next
   // row's x / dy loads are issued before the current row's reductions
-  float xv[NV][8], dv[NV][8];
+  float xv[NV][8], dv[NV][8], ev[NV][8];
   if (grp < M) {
     row_load<NV, WPR>(x + static_cast<int64_t>(grp) * D, D, sub, lane, xv);
     row_load<NV, WPR>(dy + static_cast<int64_t>(grp) * D, D, sub, lane, dv);
+    if constexpr (DR) row_load<NV, WPR>(dres + static_cast<int64_t>(grp) * D, D, sub, lane, ev);
   }
   for (int64_t r = grp; r < M; r += ngrp) {
-    float xn[NV][8], dn[NV][8];
+    float xn[NV][8], dn[NV][8], en[NV][8];
     const int64_t rn = r + ngrp;
     if (rn < M) {
       row_load<NV, WPR>(x + rn * D, D, sub, lane, xn);
       row_load<NV, WPR>(dy + rn * D, D, sub, lane, dn);
+      if constexpr (DR) row_load<NV, WPR>(dres + rn * D, D, sub, lane, en);
     }
     const float rs = rstd[r];
     const float mu = LN ? mean[r] : 0.f;
@@ -373,12 +375,10 @@ __global__ __launch_bounds__(kTB) void norm_bwd_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int k = 0; k < 8; ++k) dv[i][k] = rs * (dv[i][k] * wt[i][k] - mg - xv[i][k] * mgx);
     if constexpr (DR) {
-      float e[NV][8];
-      row_load<NV, WPR>(dres + r * D, D, sub, lane, e);
 #pragma unroll
       for (int i = 0; i < NV; ++i)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) dv[i][k] += e[i][k];
+        for (int k = 0; k < 8; ++k) dv[i][k] += ev[i][k];
     }
     row_store<NV, WPR>(dx + r * D, D, sub, lane, dv);
 #pragma unroll
@@ -387,6 +387,7 @@ __global__ __launch_bounds__(kTB) void norm_bwd_kernel(const bf16* __restrict__ 
       for (int k = 0; k < 8; ++k) {
         xv[i][k] = xn[i][k];
         dv[i][k] = dn[i][k];
+        if constexpr (DR) ev[i][k] = en[i][k];
       }
   }
   // one partial row pair per workgroup: part[blockIdx.x][2][D]

@@ -106,3 +106,32 @@ def test_gpu_checkpoint_roundtrip(cuda, tmp_path):
     b.fit(8, log_every=0)
     for x, y in zip(a.model.parameters(), b.model.parameters()):
         torch.testing.assert_close(x, y)
+
+
+@pytest.mark.parametrize("optim", ["adamw", "sgd"])
+def test_gossip_early_update_matches_step_update(cuda, optim):
+    """Gossip with one local worker: per-bucket optimizer steps launched from the backward hooks
+    on a side stream give the same parameters as the single update in step()."""
+    from consensusml_amd import TrainConfig
+    from consensusml_amd.parallel.dist import DistInfo
+    from consensusml_amd.trainer.trainer import ConsensusTrainer
+    res = []
+    for early in (True, False):
+        cfg = TrainConfig()
+        cfg.model.name = "llama_tiny"
+        cfg.model.seq_len = 32
+        cfg.batch_per_worker = 2
+        cfg.agg.rule = "mean"
+        cfg.topology.kind = "gossip"
+        cfg.topology.bucket_mb = 0.05      # several buckets
+        cfg.topology.early_update = early
+        cfg.optim.name = optim
+        cfg.optim.lr = 1e-3
+        tr = ConsensusTrainer(cfg, info=DistInfo(0, 1, 0, cuda, "none"))
+        assert tr.engine.early_update == early
+        for _ in range(3):
+            tr.train_step()
+        torch.cuda.synchronize()
+        res.append(torch.cat([p.detach().float().flatten() for p in tr.model.parameters()]))
+        tr.close()
+    torch.testing.assert_close(res[0], res[1], rtol=0, atol=0)
