@@ -221,3 +221,30 @@ def synthetic_cohort(n_genes: int = 2000, n_samples: int = 145, n_signal: int = 
     row = pd.DataFrame({"true_lfc": lfc, "signal": np.isin(np.arange(n_genes), sig)},
                        index=genes)
     return ExpressionSet({"counts": torch.from_numpy(counts)}, genes, samples, row, col)
+
+
+def target_aml_cohort(clinical_csv: str, train_csv: str, test_csv: str) -> pd.DataFrame:
+    """The reference's TARGET-AML analysis cohort from its own files (C08/C12/C30).
+
+    Patients of the seeded 2/3 split (``JSmith_code/TARGET_AML_{Training,Testing}_Samples.csv``,
+    `Differential_Expression_and_Lasso.Rmd:158-187`) joined to the clinical table
+    (``Clinical_Data/AML_dataframe.csv``), first occurrence per USI (`scripts/README.md:6`), with
+    the reference's binarised risk label ``deg_risk`` (Low = 0; Standard / High = 1; Unknown =
+    NA, `cml_targetaml_seanalysis.Rmd:435-436`) and ``exptset`` = train | test
+    (`make_seobj_targetaml.R:81-82`). Columns are renamed to snake case: gender, age_days,
+    risk_group."""
+    clin = pd.read_csv(clinical_csv)
+    train = pd.read_csv(train_csv)["x"].tolist()
+    test = pd.read_csv(test_csv)["x"].tolist()
+    split = {u: "train" for u in train}
+    split.update({u: "test" for u in test})
+    sub = clin[clin["TARGET USI"].isin(split)].drop_duplicates("TARGET USI")
+    out = pd.DataFrame({
+        "usi": sub["TARGET USI"].values,
+        "gender": sub["Gender"].values,
+        "age_days": sub["Age at Diagnosis in Days"].values,
+        "risk_group": sub["Risk group"].values,
+    })
+    out["deg_risk"] = out["risk_group"].map({"Low": 0, "Standard": 1, "High": 1})
+    out["exptset"] = out["usi"].map(split)
+    return out.set_index("usi")

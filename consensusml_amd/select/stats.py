@@ -235,8 +235,9 @@ def cohort_summary(col_data, label: str = "low_risk", covariates=("gender", "age
             continue
         v = col_data[cov]
         if np.issubdtype(v.dtype, np.number):
+            # R: ifelse(age >= median(age), "old", "young")  (SEA:463)
             cut = age_cut if age_cut is not None else float(v.median())
-            v = (v > cut).map({True: f">{cut:g}", False: f"<={cut:g}"})
+            v = (v >= cut).map({True: f">={cut:g}", False: f"<{cut:g}"})
         tab = pd.crosstab(v, col_data[label])
         out[cov] = {"table": tab.to_dict(), **chisq_test(tab.to_numpy())}
     return out
