@@ -3,8 +3,10 @@
 Attention is ``F.scaled_dot_product_attention`` (ROCm flash kernels); the GEMMs are hipBLASLt via
 ``F.linear``. Everything between them runs the hand-written HIP kernels of
 ``csrc/kernels/transformer.hip`` (``ops.transformer``) on bf16 GPU tensors:
-  * the q / k / v projections are ONE fused GEMM whose output is split (and, for Llama, rotated)
-    straight into SDPA's head-major layout by one kernel (backward: one kernel back);
+  * the q / k / v projections are ONE fused GEMM. BERT's attention (S <= 128, head dim 64) runs
+    the MFMA kernel of ``csrc/kernels/attention.hip`` straight from that fused output to the
+    output projection's input layout; Llama's output is split and rotated into SDPA's head-major
+    layout by one kernel (backward: one kernel back);
   * every residual add is fused with the following norm (``add_norm``: the residual stream and the
     normalised sublayer input come out of one pass, and the backward adds the stream's gradient
     on the way out);
@@ -26,8 +28,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, linear, qkv_split,
-                               rope_tables, swiglu)
+from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, fused_qkv_attention,
+                               linear, qkv_split, rope_tables, swiglu)
 
 
 # =============================================================================== BERT
@@ -55,8 +57,7 @@ class BertLayer(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, S, D = x.shape
-        q, k, v = qkv_split(self.qkv(x), self.h, self.h, D // self.h)
-        a = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, S, D)
+        a = fused_qkv_attention(self.qkv(x), self.h, D // self.h)
         _, x = add_norm(x, self.o(a), self.ln1.weight, self.ln1.bias, self.ln1.eps)   # post-LN
         _, x = add_norm(x, self.fc2(F.gelu(self.fc1(x))), self.ln2.weight, self.ln2.bias,
                         self.ln2.eps)

@@ -9,6 +9,8 @@ tests, fp32) runs the equivalent PyTorch composition, which is also the numerics
 """
 from __future__ import annotations
 
+import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -193,6 +195,43 @@ def qkv_split(qkv: torch.Tensor, H: int, KV: int, hd: int, cos: Optional[torch.T
     if cos is not None:
         q, k = _rope_ref(q, cos, sin), _rope_ref(k, cos, sin)
     return q.contiguous(), k.contiguous(), v.contiguous()
+
+
+# ============================================================================ attention
+class _AttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, H, scale):
+        out, lse = lib().attn_fwd(qkv, H, scale)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.H, ctx.scale = H, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        return lib().attn_bwd(qkv, out, dout, lse, ctx.H, ctx.scale), None, None
+
+
+def _attn_ok(qkv: torch.Tensor, H: int, hd: int) -> bool:
+    S = qkv.shape[1]
+    return (_gpu_bf16(qkv) and hd == 64 and S % 32 == 0 and 32 <= S <= 128
+            and qkv.is_contiguous() and qkv.data_ptr() % 16 == 0 and ATTN_KERNEL)
+
+
+# short-sequence MFMA attention for BERT-shaped problems (CML_ATTN_KERNEL=0: SDPA)
+ATTN_KERNEL = os.environ.get("CML_ATTN_KERNEL", "1") == "1"
+
+
+def fused_qkv_attention(qkv: torch.Tensor, H: int, hd: int) -> torch.Tensor:
+    """Non-causal multi-head attention straight from the fused projection ``qkv [B, S, 3 H hd]``
+    to ``[B, S, H hd]`` (the output projection's input layout). S <= 128, hd = 64 bf16 GPU
+    tensors run csrc/kernels/attention.hip (one workgroup per (batch, head), MFMA, exact
+    softmax); anything else splits the heads and runs SDPA."""
+    B, S, _ = qkv.shape
+    if _attn_ok(qkv, H, hd):
+        return _AttnFn.apply(qkv, H, 1.0 / math.sqrt(hd))
+    q, k, v = qkv_split(qkv, H, H, hd)
+    return F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, S, H * hd)
 
 
 # ============================================================================ SwiGLU

@@ -527,6 +527,43 @@ Tensor swiglu_bwd(const Tensor& dy_in, const Tensor& h) {
   return dh;
 }
 
+// qkv [B, S, 3 H 64] bf16 contiguous -> (O [B, S, H 64], lse fp32 [B, H, S])
+std::vector<Tensor> attn_fwd(const Tensor& qkv, int64_t H, double scale) {
+  check_bf16c(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == 3 * H * 64, "attn: qkv must be [B, S, 3 H 64]");
+  const int64_t B = qkv.size(0), S = qkv.size(1);
+  TORCH_CHECK(S % 32 == 0 && S >= 32 && S <= 128, "attn: S % 32 == 0 and S <= 128");
+  const c10::DeviceGuard guard(qkv.device());
+  Tensor out = at::empty({B, S, H * 64}, qkv.options());
+  Tensor lse = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
+  CML_CHECK_HIP(cml::launch_attn_fwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
+                                     static_cast<int>(B), static_cast<int>(S), static_cast<int>(H),
+                                     static_cast<float>(scale), cur_stream()));
+  return {out, lse};
+}
+
+Tensor attn_bwd(const Tensor& qkv, const Tensor& out, const Tensor& dout_in, const Tensor& lse,
+                int64_t H, double scale) {
+  check_bf16c(qkv, "qkv");
+  check_bf16c(out, "out");
+  Tensor dout = dout_in.contiguous();
+  check_bf16c(dout, "dout");
+  const int64_t B = qkv.size(0), S = qkv.size(1);
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) == 3 * H * 64 && S % 32 == 0 && S <= 128,
+              "attn_bwd: qkv must be [B, S, 3 H 64], S % 32 == 0, S <= 128");
+  TORCH_CHECK(out.sizes() == dout.sizes() && out.dim() == 3 && out.size(0) == B && out.size(1) == S &&
+                  out.size(2) == H * 64, "attn_bwd: out / dout must be [B, S, H 64]");
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.is_contiguous() &&
+                  lse.numel() == B * H * S, "attn_bwd: lse fp32 [B, H, S]");
+  const c10::DeviceGuard guard(qkv.device());
+  Tensor dqkv = at::empty_like(qkv);
+  CML_CHECK_HIP(cml::launch_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(),
+                                     lse.data_ptr<float>(), dqkv.data_ptr(), static_cast<int>(B),
+                                     static_cast<int>(S), static_cast<int>(H),
+                                     static_cast<float>(scale), cur_stream()));
+  return dqkv;
+}
+
 // column sums of x viewed as [M, N] (N = last dim) -> bf16 [N]
 Tensor colsum(const Tensor& x_in) {
   Tensor x = x_in.contiguous();
@@ -568,6 +605,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_bwd", &rope_bwd, "inverse of rope_fwd");
   m.def("swiglu_fwd", &swiglu_fwd, "silu(a) * b over [a | b]");
   m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
+  m.def("attn_fwd", &attn_fwd, "short-sequence MFMA attention forward (fused qkv in)");
+  m.def("attn_bwd", &attn_bwd, "short-sequence MFMA attention backward (fused dqkv out)");
   m.def("colsum", &colsum, "column sums of a bf16 matrix (bias gradient)");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);

@@ -144,6 +144,13 @@ hipError_t launch_rope_bwd(const void* dq, const void* dk, const void* dv, const
 hipError_t launch_swiglu_fwd(const void* h, void* y, int64_t M, int F, hipStream_t stream);
 hipError_t launch_swiglu_bwd(const void* dy, const void* h, void* dh, int64_t M, int F,
                              hipStream_t stream);
+// Short-sequence attention (S % 32 == 0, S <= 128, head dim 64, no mask) on MFMA: reads the
+// fused projection qkv [B, S, 3, H, 64], writes O [B, S, H * 64] and lse fp32 [B, H, S];
+// backward writes dqkv in the fused layout.
+hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int S, int H,
+                           float scale, hipStream_t stream);
+hipError_t launch_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
+                           void* dqkv, int B, int S, int H, float scale, hipStream_t stream);
 // Column sums of a bf16 [M, N] matrix (bias gradients), fp32 accumulation, bf16 out.
 size_t colsum_workspace_bytes(int64_t M, int N);
 hipError_t launch_colsum(const void* x, int64_t M, int N, void* out, void* work,
