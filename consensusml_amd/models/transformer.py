@@ -28,6 +28,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.bn import ResidualLink
 from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, fused_qkv_attention,
                                linear, qkv_split, rope_tables, swiglu)
 
@@ -57,10 +58,13 @@ class BertLayer(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, S, D = x.shape
-        a = fused_qkv_attention(self.qkv(x), self.h, D // self.h)
-        _, x = add_norm(x, self.o(a), self.ln1.weight, self.ln1.bias, self.ln1.eps)   # post-LN
-        _, x = add_norm(x, self.fc2(F.gelu(self.fc1(x))), self.ln2.weight, self.ln2.bias,
-                        self.ln2.eps)
+        # x feeds both the QKV GEMM and the residual add of ln1 (likewise fc1 / ln2): the norm's
+        # backward parks x's residual gradient on a link and the GEMM's data gradient absorbs it
+        l1, l2 = ResidualLink(), ResidualLink()
+        a = fused_qkv_attention(self.qkv(x, l1), self.h, D // self.h)
+        _, x = add_norm(x, self.o(a), self.ln1.weight, self.ln1.bias, self.ln1.eps, l1)  # post-LN
+        _, x = add_norm(x, self.fc2(F.gelu(self.fc1(x, l2))), self.ln2.weight, self.ln2.bias,
+                        self.ln2.eps, l2)
         return x
 
 

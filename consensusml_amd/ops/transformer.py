@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .bn import ResidualLink
 from .native import lib
 
 
@@ -83,19 +84,30 @@ class _AddNormFn(torch.autograd.Function):
     input gradient on the way out: d x = d r = ds + norm_bwd(dy)."""
 
     @staticmethod
-    def forward(ctx, x, r, w, b, eps):
+    def forward(ctx, x, r, w, b, eps, x_link):
         y, s, mean, rstd = lib().norm_fwd(x, r, w, b, eps)
         ctx.save_for_backward(s, w, mean if b is not None else None, rstd)
         ctx.ln = b is not None
+        ctx.x_link = x_link
+        # an unused s (post-LN BERT) must arrive as None, not as a zero-filled tensor that the
+        # backward would then read
+        ctx.set_materialize_grads(False)
         return s, y
 
     @staticmethod
     def backward(ctx, ds, dy):
         s, w, mean, rstd = ctx.saved_tensors
         if dy is None:
-            return ds, ds, None, None, None
+            return ds, ds, None, None, None, None
         dx, dw, db = lib().norm_bwd(dy, ds, s, w, mean, rstd)
-        return dx, dx, dw, (db if ctx.ln else None), None
+        gx = dx
+        link = ctx.x_link
+        if link is not None and not link.closed and link.grad is None:
+            # x's other consumer (the next sublayer's input GEMM, see linear(link=...)) runs its
+            # backward later and absorbs this gradient in its beta = 1 epilogue
+            link.grad = dx
+            gx = None
+        return gx, dx, dw, (db if ctx.ln else None), None, None
 
 
 def _norm_ref(x, w, b, eps):
@@ -119,13 +131,16 @@ def norm(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], eps: float
 
 
 def add_norm(x: torch.Tensor, r: Optional[torch.Tensor], w: torch.Tensor,
-             b: Optional[torch.Tensor], eps: float) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(s, norm(s)) with s = x + r (r None: s = x)."""
+             b: Optional[torch.Tensor], eps: float,
+             x_link: Optional[ResidualLink] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(s, norm(s)) with s = x + r (r None: s = x). ``x_link``: x also feeds a ``linear(...,
+    link=x_link)`` whose backward runs after this op's (x's gradient is then added inside that
+    GEMM instead of by autograd)."""
     if r is None:
         return x, norm(x, w, b, eps)
     if _gpu_bf16(x, r, w, b) and _norm_ok(x, x.shape[-1]) and r.is_contiguous() \
             and r.data_ptr() % 16 == 0 and r.shape == x.shape:
-        return _AddNormFn.apply(x, r, w, b, float(eps))
+        return _AddNormFn.apply(x, r, w, b, float(eps), x_link)
     s = x + r
     return s, _norm_ref(s, w, b, eps)
 
@@ -151,6 +166,7 @@ class LayerNorm(nn.LayerNorm):
 class _RopeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, cos, sin, H, KV, hd):
+        ctx.set_materialize_grads(False)
         q, k, v = lib().rope_fwd(qkv, cos, sin, H, KV, hd)
         ctx.save_for_backward(cos, sin)
         ctx.has_rot = cos is not None
@@ -262,8 +278,9 @@ class _LinearFn(torch.autograd.Function):
     reduction runs these at ~0.4 TB/s: 7 % of the BERT step in profiles/r01_prof13)."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, link):
         ctx.save_for_backward(x, w)
+        ctx.link = link
         return F.linear(x, w, b)
 
     @staticmethod
@@ -272,22 +289,31 @@ class _LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = (dy2 @ w).view(x.shape)
+            g = ctx.link.take() if ctx.link is not None else None
+            if g is not None and g.is_contiguous() and g.shape == x.shape:
+                dx = g.view(-1, x.shape[-1]).addmm_(dy2, w).view(x.shape)   # beta = 1 epilogue
+            elif g is not None:
+                dx = (g.reshape(-1, x.shape[-1]) + dy2 @ w).view(x.shape)
+            else:
+                dx = (dy2 @ w).view(x.shape)
         if ctx.needs_input_grad[1]:
             dw = dy2.t() @ x.reshape(-1, x.shape[-1])
         if ctx.needs_input_grad[2]:
             db = lib().colsum(dy2)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
+           link: Optional[ResidualLink] = None) -> torch.Tensor:
+    """``link``: a ResidualLink on which a later-in-forward op (``add_norm(x_link=...)``) parks
+    another gradient of x; this GEMM's data-gradient absorbs it (beta = 1)."""
     if b is not None and _gpu_bf16(x, w, b) and w.shape[0] % 8 == 0:
-        return _LinearFn.apply(x, w, b)
+        return _LinearFn.apply(x, w, b, link)
     return F.linear(x, w, b)
 
 
 class Linear(nn.Linear):
     """nn.Linear with the fused bias-gradient backward on bf16 GPU tensors."""
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return linear(x, self.weight, self.bias)
+    def forward(self, x: torch.Tensor, link: Optional[ResidualLink] = None) -> torch.Tensor:
+        return linear(x, self.weight, self.bias, link)
