@@ -121,35 +121,18 @@ def grow(Xb: torch.Tensor, stat: torch.Tensor, depth: int, k: int, n_bins: int, 
                 r = torch.where(feat_mask[:, None, :], r, torch.full_like(r, -1.0))
             kk = min(k, p) if feat_mask is None else min(k, int(feat_mask.sum(1).min()))
             feats = r.topk(kk, dim=2).indices                     # [T, L, kk]
-        # histograms: H[t, node, j, bin, 2]
-        fsel = torch.gather(feats, 1, local[..., None].expand(T, n, kk))   # [T, n, kk]
-        bins = torch.gather(Xb.long()[None].expand(T, n, p), 2, fsel)      # [T, n, kk]
-        hidx = ((tt[:, None, None] * L + local[..., None]) * kk +
-                torch.arange(kk, device=dev)[None, None]) * n_bins + bins
-        H = torch.zeros(T * L * kk * n_bins, 2, device=dev)
-        am = alive[..., None].expand(T, n, kk).reshape(-1)
-        sv = stat[:, :, None, :].expand(T, n, kk, 2).reshape(-1, 2).float()
-        H.index_add_(0, hidx.view(-1)[am], sv[am])
-        H = H.view(T, L, kk, n_bins, 2)
-        C = torch.cumsum(H, 3)[:, :, :, :-1]                   # left stats for thr = 0..B-2
-        Tt = tot[:, :, None, None, :]
-        R = Tt - C
-        if crit == "gini":
-            def gw(s):   # w * gini = w - (wy^2 + (w-wy)^2)/w
-                w, wy = s[..., 0], s[..., 1]
-                return w - (wy * wy + (w - wy) * (w - wy)) / w.clamp_min(1e-12)
-            gain = gw(Tt) - gw(C) - gw(R)
-            ok = (C[..., 0] >= 1) & (R[..., 0] >= 1)
+        if dev.type == "cuda" and n_bins <= 64:
+            # csrc/kernels/tree_hist.hip: per-(tree, node) LDS histograms, in-order sums,
+            # threshold scan and argmax in one launch
+            from ..ops.native import lib
+            nl = torch.where(alive, node_of - base, torch.full_like(node_of, -1)).int()
+            gbest, jb, bbest = lib().split_search(
+                Xb.contiguous(), nl.contiguous(), stat.float().contiguous(), feats.int().contiguous(),
+                tot.contiguous(), n_bins, 0 if crit == "gini" else 1, float(lam), float(min_child))
+            best, j, b = gbest, jb.long(), bbest.long()
         else:
-            def sc(s):
-                return s[..., 0] * s[..., 0] / (s[..., 1] + lam)
-            gain = 0.5 * (sc(C) + sc(R) - sc(Tt))
-            ok = (C[..., 1] >= min_child) & (R[..., 1] >= min_child)
-        gain = torch.where(ok, gain, torch.full_like(gain, -float("inf")))
-        flat = gain.view(T, L, -1)
-        best, arg = flat.max(2)
-        j = arg // (n_bins - 1)
-        b = arg % (n_bins - 1)
+            best, j, b = _split_search_torch(Xb, stat, feats, local, alive, tot, tt, L, kk,
+                                             n_bins, crit, lam, min_child)
         split = torch.isfinite(best) & (best > 1e-12)
         fbest = torch.gather(feats, 2, j[..., None]).squeeze(2)
         feature[:, base:base + L] = torch.where(split, fbest, torch.full_like(fbest, -1))
@@ -167,6 +150,44 @@ def grow(Xb: torch.Tensor, stat: torch.Tensor, depth: int, k: int, n_bins: int, 
         node_of = torch.where(at_level & (nf >= 0), child, node_of)
         alive = alive & (nf >= 0) & at_level if crit == "gini" else (at_level & (nf >= 0))
     return TreeBatch(feature, thr, value, depth)
+
+
+def _split_search_torch(Xb, stat, feats, local, alive, tot, tt, L, kk, n_bins, crit, lam,
+                        min_child):
+    """Reference formulation of the split search (CPU path; oracle of tree_hist.hip)."""
+    dev = Xb.device
+    T, n, _ = stat.shape
+    p = Xb.shape[1]
+    # histograms: H[t, node, j, bin, 2]
+    fsel = torch.gather(feats, 1, local[..., None].expand(T, n, kk))   # [T, n, kk]
+    bins = torch.gather(Xb.long()[None].expand(T, n, p), 2, fsel)      # [T, n, kk]
+    hidx = ((tt[:, None, None] * L + local[..., None]) * kk +
+            torch.arange(kk, device=dev)[None, None]) * n_bins + bins
+    H = torch.zeros(T * L * kk * n_bins, 2, device=dev)
+    am = alive[..., None].expand(T, n, kk).reshape(-1)
+    sv = stat[:, :, None, :].expand(T, n, kk, 2).reshape(-1, 2).float()
+    H.index_add_(0, hidx.view(-1)[am], sv[am])
+    H = H.view(T, L, kk, n_bins, 2)
+    C = torch.cumsum(H, 3)[:, :, :, :-1]                   # left stats for thr = 0..B-2
+    Tt = tot[:, :, None, None, :]
+    R = Tt - C
+    if crit == "gini":
+        def gw(s):   # w * gini = w - (wy^2 + (w-wy)^2)/w
+            w, wy = s[..., 0], s[..., 1]
+            return w - (wy * wy + (w - wy) * (w - wy)) / w.clamp_min(1e-12)
+        gain = gw(Tt) - gw(C) - gw(R)
+        ok = (C[..., 0] >= 1) & (R[..., 0] >= 1)
+    else:
+        def sc(s):
+            return s[..., 0] * s[..., 0] / (s[..., 1] + lam)
+        gain = 0.5 * (sc(C) + sc(R) - sc(Tt))
+        ok = (C[..., 1] >= min_child) & (R[..., 1] >= min_child)
+    gain = torch.where(ok, gain, torch.full_like(gain, -float("inf")))
+    flat = gain.view(T, L, -1)
+    best, arg = flat.max(2)
+    j = arg // (n_bins - 1)
+    b = arg % (n_bins - 1)
+    return best, j, b
 
 
 class HistForest:
@@ -267,6 +288,9 @@ class HistBoost:
             m = m + self.lr * tb.predict(Xb)[0]
         p1 = torch.sigmoid(m)
         return torch.stack([1 - p1, p1], 1)
+
+    def predict(self, X: torch.Tensor) -> torch.Tensor:
+        return (self.predict_proba(X)[:, 1] > 0.5).long()
 
     @property
     def feature_importances_(self) -> torch.Tensor:

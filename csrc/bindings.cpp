@@ -564,6 +564,40 @@ Tensor attn_bwd(const Tensor& qkv, const Tensor& out, const Tensor& dout_in, con
   return dqkv;
 }
 
+std::vector<Tensor> split_search(const Tensor& Xb, const Tensor& node_local, const Tensor& stat,
+                                 const Tensor& feats, const Tensor& tot, int64_t n_bins,
+                                 int64_t crit, double lam, double min_child) {
+  check_dev(Xb, "Xb");
+  TORCH_CHECK(Xb.scalar_type() == at::kByte && Xb.dim() == 2 && Xb.is_contiguous(), "Xb: uint8 [n, p]");
+  const int64_t n = Xb.size(0), p = Xb.size(1);
+  TORCH_CHECK(node_local.is_cuda() && node_local.scalar_type() == at::kInt && node_local.dim() == 2 &&
+                  node_local.size(1) == n && node_local.is_contiguous(), "node_local: int32 [T, n]");
+  const int64_t T = node_local.size(0);
+  TORCH_CHECK(stat.is_cuda() && stat.scalar_type() == at::kFloat && stat.is_contiguous() &&
+                  stat.numel() == T * n * 2, "stat: fp32 [T, n, 2]");
+  TORCH_CHECK(feats.is_cuda() && feats.scalar_type() == at::kInt && feats.dim() == 3 &&
+                  feats.size(0) == T && feats.is_contiguous(), "feats: int32 [T, L, kk]");
+  const int64_t L = feats.size(1), kk = feats.size(2);
+  TORCH_CHECK(tot.is_cuda() && tot.scalar_type() == at::kFloat && tot.is_contiguous() &&
+                  tot.numel() == T * L * 2, "tot: fp32 [T, L, 2]");
+  TORCH_CHECK(n_bins >= 2 && n_bins <= 64, "split_search: 2 <= n_bins <= 64");
+  TORCH_CHECK(Xb.device() == stat.device() && Xb.device() == feats.device(), "device mismatch");
+  const c10::DeviceGuard guard(Xb.device());
+  Tensor gain = at::empty({T, L}, stat.options());
+  Tensor slot = at::empty({T, L}, feats.options());
+  Tensor bin = at::empty({T, L}, feats.options());
+  CML_CHECK_HIP(cml::launch_split_search(Xb.data_ptr<uint8_t>(), node_local.data_ptr<int>(),
+                                         stat.data_ptr<float>(), feats.data_ptr<int>(),
+                                         tot.data_ptr<float>(), static_cast<int>(T),
+                                         static_cast<int>(L), static_cast<int>(n),
+                                         static_cast<int>(p), static_cast<int>(kk),
+                                         static_cast<int>(n_bins), static_cast<int>(crit),
+                                         static_cast<float>(lam), static_cast<float>(min_child),
+                                         gain.data_ptr<float>(), slot.data_ptr<int>(),
+                                         bin.data_ptr<int>(), cur_stream()));
+  return {gain, slot, bin};
+}
+
 // column sums of x viewed as [M, N] (N = last dim) -> bf16 [N]
 Tensor colsum(const Tensor& x_in) {
   Tensor x = x_in.contiguous();
@@ -607,6 +641,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
   m.def("attn_fwd", &attn_fwd, "short-sequence MFMA attention forward (fused qkv in)");
   m.def("attn_bwd", &attn_bwd, "short-sequence MFMA attention backward (fused dqkv out)");
+  m.def("split_search", &split_search, "tree-ensemble histogram split search (one level)");
   m.def("colsum", &colsum, "column sums of a bf16 matrix (bias gradient)");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);

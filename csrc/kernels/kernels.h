@@ -151,6 +151,14 @@ hipError_t launch_attn_fwd(const void* qkv, void* out, float* lse, int B, int S,
                            float scale, hipStream_t stream);
 hipError_t launch_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse,
                            void* dqkv, int B, int S, int H, float scale, hipStream_t stream);
+// Tree-ensemble split search, one level of T trees x L nodes: per (tree, node) the best
+// (gain, candidate slot, bin) over its kk candidate features (feats [T, L, kk]) from the binned
+// samples Xb [n, p] (uint8, B <= 64 bins) of that node (node_local [T, n], -1 = not in the level),
+// with split statistics stat [T, n, 2] and node totals tot [T, L, 2]; crit 0 Gini, 1 XGBoost.
+hipError_t launch_split_search(const uint8_t* Xb, const int* node_local, const float* stat,
+                               const int* feats, const float* tot, int T, int L, int n, int p,
+                               int kk, int B, int crit, float lam, float min_child,
+                               float* out_gain, int* out_slot, int* out_bin, hipStream_t stream);
 // Column sums of a bf16 [M, N] matrix (bias gradients), fp32 accumulation, bf16 out.
 size_t colsum_workspace_bytes(int64_t M, int N);
 hipError_t launch_colsum(const void* x, int64_t M, int N, void* out, void* work,
