@@ -598,6 +598,48 @@ std::vector<Tensor> split_search(const Tensor& Xb, const Tensor& node_local, con
   return {gain, slot, bin};
 }
 
+float* f32p(const Tensor& t, const char* name, int64_t numel) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == numel,
+              name, ": contiguous fp32 GPU tensor with ", numel, " elements");
+  return t.data_ptr<float>();
+}
+float* f32opt(const optional<Tensor>& t, const char* name, int64_t numel) {
+  return (t.has_value() && t->defined()) ? f32p(*t, name, numel) : nullptr;
+}
+
+void lasso_resid(const Tensor& z, const optional<Tensor>& v0, const Tensor& y, const Tensor& M,
+                 const Tensor& nb, Tensor& r, const optional<Tensor>& rsum) {
+  TORCH_CHECK(z.dim() == 2, "z: [n, B]");
+  const int64_t n = z.size(0), B = z.size(1);
+  const c10::DeviceGuard guard(z.device());
+  CML_CHECK_HIP(cml::launch_lasso_resid(f32p(z, "z", n * B), f32opt(v0, "v0", B), f32p(y, "y", n),
+                                        f32p(M, "M", n * B), f32p(nb, "nb", B), f32p(r, "r", n * B),
+                                        f32opt(rsum, "rsum", B), static_cast<int>(n),
+                                        static_cast<int>(B), cur_stream()));
+}
+
+void lasso_step(Tensor& v, Tensor& beta, const Tensor& g, const Tensor& step, const Tensor& lam,
+                double alpha, Tensor& tk, const optional<Tensor>& rsum, const optional<Tensor>& v0,
+                const optional<Tensor>& b0, Tensor& nbeta, Tensor& mom, Tensor& part,
+                const optional<Tensor>& conv_part) {
+  TORCH_CHECK(v.dim() == 2, "v: [p, B]");
+  const int64_t p = v.size(0), B = v.size(1);
+  const int64_t ns = cml::lasso_slices(static_cast<int>(p));
+  const bool icpt = v0.has_value() && v0->defined();
+  TORCH_CHECK(!icpt || (rsum.has_value() && rsum->defined() && b0.has_value() && b0->defined()),
+              "lasso_step: the intercept needs rsum, v0 and b0");
+  const c10::DeviceGuard guard(v.device());
+  CML_CHECK_HIP(cml::launch_lasso_step(
+      f32p(v, "v", p * B), f32p(beta, "beta", p * B), f32p(g, "g", p * B), f32p(step, "step", B),
+      f32p(lam, "lam", B), static_cast<float>(alpha), f32p(tk, "tk", B),
+      icpt ? f32opt(rsum, "rsum", B) : nullptr, icpt ? f32opt(v0, "v0", B) : nullptr,
+      icpt ? f32opt(b0, "b0", B) : nullptr, f32p(nbeta, "nbeta", p * B), f32p(mom, "mom", B),
+      f32p(part, "part", ns * B), f32opt(conv_part, "conv_part", ns * 2 * B), static_cast<int>(p),
+      static_cast<int>(B), cur_stream()));
+}
+
+int64_t lasso_slices(int64_t p) { return cml::lasso_slices(static_cast<int>(p)); }
+
 // column sums of x viewed as [M, N] (N = last dim) -> bf16 [N]
 Tensor colsum(const Tensor& x_in) {
   Tensor x = x_in.contiguous();
@@ -642,6 +684,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd, "short-sequence MFMA attention forward (fused qkv in)");
   m.def("attn_bwd", &attn_bwd, "short-sequence MFMA attention backward (fused dqkv out)");
   m.def("split_search", &split_search, "tree-ensemble histogram split search (one level)");
+  m.def("lasso_resid", &lasso_resid, "batched logistic-lasso residual (+ intercept gradient)");
+  m.def("lasso_step", &lasso_step, "batched FISTA prox / restart / momentum step");
+  m.def("lasso_slices", &lasso_slices);
   m.def("colsum", &colsum, "column sums of a bf16 matrix (bias gradient)");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);

@@ -159,6 +159,19 @@ hipError_t launch_split_search(const uint8_t* Xb, const int* node_local, const f
                                const int* feats, const float* tot, int T, int L, int n, int p,
                                int kk, int B, int crit, float lam, float min_child,
                                float* out_gain, int* out_slot, int* out_bin, hipStream_t stream);
+// Batched FISTA logistic lasso (lasso_prox.hip), problems along columns (B contiguous):
+// r = (sigmoid(z + v0) - y) M / nb [n, B] (+ rsum = column sums of r), then the prox / restart /
+// momentum step in place on v, beta [p, B] (tk, mom [B]; v0, b0 [B] when fitting an intercept).
+// part: lasso_slices(p) x B floats; conv_part (optional): lasso_slices(p) x 2 x B (max |d|,
+// max |beta| per row slice for the convergence test).
+int lasso_slices(int p);
+hipError_t launch_lasso_resid(const float* z, const float* v0, const float* y, const float* M,
+                              const float* nb, float* r, float* rsum, int n, int B,
+                              hipStream_t stream);
+hipError_t launch_lasso_step(float* v, float* beta, const float* g, const float* step,
+                             const float* lam, float alpha, float* tk, const float* rsum,
+                             float* v0, float* b0, float* nbeta, float* mom, float* part,
+                             float* conv_part, int p, int B, hipStream_t stream);
 // Column sums of a bf16 [M, N] matrix (bias gradients), fp32 accumulation, bf16 out.
 size_t colsum_workspace_bytes(int64_t M, int N);
 hipError_t launch_colsum(const void* x, int64_t M, int N, void* out, void* work,

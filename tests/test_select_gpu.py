@@ -68,3 +68,28 @@ def test_hist_ensemble_gpu_matches_cpu(cuda, kind):
     assert torch.corrcoef(torch.stack([ic, ig]))[0, 1].item() > 0.9
     acc = (gpu.predict(X.to(cuda)).cpu() == y).float().mean().item()
     assert acc > 0.85
+
+
+@pytest.mark.parametrize("intercept", [False, True])
+@pytest.mark.parametrize("alpha", [1.0, 0.5])
+def test_fista_gpu_kernels_match_cpu(cuda, intercept, alpha):
+    """csrc/kernels/lasso_prox.hip (residual, prox / restart / momentum) reproduces the CPU
+    FISTA path: same problems (LOOCV-style masks x lambda grid), same optimum."""
+    from consensusml_amd.select.lasso import fista_logistic
+    g = torch.Generator().manual_seed(2)
+    n, p = 40, 300
+    X = torch.randn(n, p, generator=g)
+    y = (X[:, :5].sum(1) + 0.3 * torch.randn(n, generator=g) > 0).float()
+    lams = torch.tensor([0.2, 0.05, 0.02, 0.005]).repeat(3)
+    masks = torch.ones(n, lams.numel())
+    for k in range(3):                      # three held-out samples
+        masks[k, 4 * k:4 * k + 4] = 0
+    bc, b0c, itc, _ = fista_logistic(X, y, lams, masks, intercept=intercept, alpha=alpha,
+                                     max_iter=2000, tol=1e-7)
+    bg, b0g, itg, _ = fista_logistic(X.to(cuda), y.to(cuda), lams, masks.to(cuda),
+                                     intercept=intercept, alpha=alpha, max_iter=2000, tol=1e-7)
+    torch.testing.assert_close(bg.cpu(), bc, rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(b0g.cpu(), b0c, rtol=2e-3, atol=2e-3)
+    # identical support on clearly nonzero coefficients
+    sig = bc.abs() > 1e-2
+    assert torch.equal(sig, bg.cpu().abs() > 1e-2) or (sig ^ (bg.cpu().abs() > 1e-2)).sum() <= 2
