@@ -49,3 +49,43 @@ def test_train_cli_resume(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(l) for l in (tmp_path / "log.jsonl").read_text().splitlines()]
     assert lines[-1]["step"] == 9
+
+
+def test_select_cli_synthetic(tmp_path):
+    """python -m consensusml_amd.select --synthetic: reference-layout standard table + summary."""
+    from consensusml_amd.select.__main__ import main
+    out = tmp_path / "sel"
+    assert main(["--synthetic", "--genes", "300", "--samples", "48", "--rf-trees", "30",
+                 "--lasso-reps", "1", "--device", "cpu", "--out", str(out)]) == 0
+    assert (out / "standouttable.csv").exists() and (out / "summary.json").exists()
+
+
+def test_select_cli_counts_with_reference_cohort(tmp_path):
+    """--counts path: count columns matched to the reference's own clinical table and split files
+    by TARGET USI (synthetic counts, real cohort metadata)."""
+    import os
+    import numpy as np
+    import pandas as pd
+    ref = "/root/reference"
+    clin = os.path.join(ref, "Clinical_Data", "AML_dataframe.csv")
+    if not os.path.exists(clin):
+        import pytest
+        pytest.skip("reference files not present")
+    from consensusml_amd.select.__main__ import main
+    from consensusml_amd.select.data import target_aml_cohort
+    tr = os.path.join(ref, "JSmith_code", "TARGET_AML_Training_Samples.csv")
+    te = os.path.join(ref, "JSmith_code", "TARGET_AML_Testing_Samples.csv")
+    co = target_aml_cohort(clin, tr, te)
+    usis = list(co.index)
+    g = np.random.default_rng(0)
+    mat = g.negative_binomial(5, 0.05, size=(250, len(usis))).astype(float)
+    low = (co["deg_risk"] == 0).to_numpy()
+    mat[:25, low] *= 6.0                     # 25 genes up in Low-risk patients (learnable signal)
+    counts = pd.DataFrame(mat.round(), index=[f"ENSG{i:011d}.1" for i in range(250)],
+                          columns=[u + "-09A-01R" for u in usis])
+    cpath = tmp_path / "counts.csv"
+    counts.to_csv(cpath)
+    out = tmp_path / "sel"
+    assert main(["--counts", str(cpath), "--clinical", clin, "--train-ids", tr, "--test-ids", te,
+                 "--rf-trees", "20", "--lasso-reps", "1", "--device", "cpu", "--out", str(out)]) == 0
+    assert (out / "standouttable.csv").exists()
