@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.bn import BatchNormAct2d, ResidualLink, fused_ok, link_tap
+from ..ops.bn import BatchNormAct2d, ResidualLink, bn_add_bn_relu, fused_ok, link_tap
 from ..ops.pool import max_pool2d
 
 # 1x1 stride-1 convolutions: which passes run as plain GEMMs (hipBLASLt) instead of MIOpen.
@@ -30,6 +30,8 @@ from ..ops.pool import max_pool2d
 CONV1X1_GEMM = os.environ.get("CML_CONV1X1_GEMM", "auto")
 # identity blocks fuse the residual-gradient add into conv1's dX GEMM (see ops.bn.ResidualLink)
 RESIDUAL_LINK = True
+# downsample-block tail relu(bn3(z) + down_bn(zd)) as one fused op (ops.bn.bn_add_bn_relu)
+FUSE_DOWN_BN = os.environ.get("CML_FUSE_DOWN_BN", "1") == "1"
 # stem input channels zero-padded 3 -> 4 on the GPU (see ResNet.stem)
 STEM_PAD4 = os.environ.get("CML_STEM_PAD4", "1") == "1"
 
@@ -160,9 +162,11 @@ class Bottleneck(nn.Module):
             out = self.bn1(self.conv1(x, res_link=dlink))
             out = self.bn2(self.conv2(out))
             z = self.conv3(out)
-            idt = self.down_bn(self.down_conv(link_tap(x, dlink) if dlink is not None else x))
+            zd = self.down_conv(link_tap(x, dlink) if dlink is not None else x)
             out_link = ResidualLink() if use_links and fused_ok(z, self.bn3.weight) else None
-            y = self.bn3(z, residual=idt, out_link=out_link)
+            # relu(bn3(z) + down_bn(zd)) in one op: the shortcut BN output is never stored
+            y = bn_add_bn_relu(z, self.bn3, zd, self.down_bn, out_link) if FUSE_DOWN_BN \
+                else self.bn3(z, residual=self.down_bn(zd), out_link=out_link)
         if out_link is not None:
             y._cml_link = out_link      # our consumer (an identity block) parks dres here
         return y

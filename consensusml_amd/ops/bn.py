@@ -103,6 +103,50 @@ class _BNActFn(torch.autograd.Function):
                 None, None, None, None)
 
 
+class _BNAddBNActFn(torch.autograd.Function):
+    """y = relu(bn_a(x1) + bn_b(x2)) for a downsample block's tail (bn3 of the main branch plus
+    the shortcut BN) without materialising the shortcut BN's output or its gradient."""
+
+    @staticmethod
+    def forward(ctx, x1, g1, b1, x2, g2, b2, rm1, rv1, rm2, rv2, stats_in, eps, momentum,
+                training, out_link):
+        want_mask = any(ctx.needs_input_grad[:6])
+        m1 = i1 = m2 = i2 = None
+        if not training:
+            m1, i1, m2, i2 = stats_in
+        y, m1, i1, m2, i2, mask = lib().bn_fwd2(x1, x2, g1, b1, g2, b2, rm1, rv1, rm2, rv2, m1,
+                                                i1, m2, i2, eps, momentum, training, want_mask)
+        ctx.save_for_backward(x1, x2, mask if want_mask else None, g1, g2, m1, i1, m2, i2)
+        ctx.out_link = out_link
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x1, x2, mask, g1, g2, m1, i1, m2, i2 = ctx.saved_tensors
+        dy2 = ctx.out_link.take() if ctx.out_link is not None else None
+        dx1, dg1, db1, dx2, dg2, db2 = lib().bn_bwd2(dy, dy2, x1, x2, mask, g1, g2, m1, i1, m2, i2)
+        return (dx1, dg1, db1, dx2, dg2, db2) + (None,) * 9
+
+
+def bn_add_bn_relu(x1: torch.Tensor, bn1: "BatchNormAct2d", x2: torch.Tensor,
+                   bn2: "BatchNormAct2d", out_link: Optional[ResidualLink] = None) -> torch.Tensor:
+    """relu(bn1(x1) + bn2(x2)) with bn1 / bn2 training-mode BatchNorms (bn1.relu applies to the
+    sum, bn2 has no ReLU). Fused path: bf16 channels_last GPU tensors of equal shape."""
+    if (_fused_ok(x1, bn1.weight) and _fused_ok(x2, bn2.weight) and x1.shape == x2.shape
+            and not bn2.relu and bn1.relu and bn1.eps == bn2.eps and bn1.momentum == bn2.momentum):
+        stats = None
+        if not bn1.training:
+            stats = (bn1.running_mean.float(), torch.rsqrt(bn1.running_var.float() + bn1.eps),
+                     bn2.running_mean.float(), torch.rsqrt(bn2.running_var.float() + bn2.eps))
+        return _BNAddBNActFn.apply(x1, bn1.weight, bn1.bias, x2, bn2.weight, bn2.bias,
+                                   bn1.running_mean if bn1.training else None,
+                                   bn1.running_var if bn1.training else None,
+                                   bn2.running_mean if bn2.training else None,
+                                   bn2.running_var if bn2.training else None, stats, bn1.eps,
+                                   bn1.momentum, bn1.training, out_link)
+    return bn1(x1, residual=bn2(x2), out_link=out_link)
+
+
 def fused_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
     return _fused_ok(x, gamma)
 

@@ -252,6 +252,85 @@ std::vector<Tensor> bn_bwd(const Tensor& dy_in, const optional<Tensor>& dy2_in, 
   return {dx, dgamma, dbeta, dres};
 }
 
+// y = relu(bn1(x1) + bn2(x2)); returns (y, mean1, invstd1, mean2, invstd2, mask)
+std::vector<Tensor> bn_fwd2(const Tensor& x1, const Tensor& x2, const Tensor& g1, const Tensor& b1,
+                            const Tensor& g2, const Tensor& b2, const optional<Tensor>& rm1,
+                            const optional<Tensor>& rv1, const optional<Tensor>& rm2,
+                            const optional<Tensor>& rv2, const optional<Tensor>& mean1_in,
+                            const optional<Tensor>& invstd1_in, const optional<Tensor>& mean2_in,
+                            const optional<Tensor>& invstd2_in, double eps, double momentum,
+                            bool training, bool want_mask) {
+  check_nhwc(x1, "x1");
+  check_nhwc(x2, "x2");
+  TORCH_CHECK(x1.sizes() == x2.sizes() && x1.dim() == 4, "bn_fwd2: x1 / x2 same 4-D shape");
+  const int64_t C = x1.size(1);
+  const int64_t M = x1.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "bn: C must be 8 * (power of 2) <= 2048");
+  for (const Tensor* t : {&g1, &b1, &g2, &b2})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->numel() == C,
+                "gamma/beta: contiguous bf16 [C]");
+  const c10::DeviceGuard guard(x1.device());
+  auto f32 = x1.options().dtype(at::kFloat);
+  Tensor y = at::empty_like(x1);
+  Tensor m1, i1, m2, i2;
+  if (training) {
+    m1 = at::empty({C}, f32); i1 = at::empty({C}, f32); m2 = at::empty({C}, f32); i2 = at::empty({C}, f32);
+  } else {
+    TORCH_CHECK(mean1_in.has_value() && invstd1_in.has_value() && mean2_in.has_value() &&
+                    invstd2_in.has_value(), "eval bn_fwd2 needs both means / invstds");
+    m1 = mean1_in->contiguous(); i1 = invstd1_in->contiguous();
+    m2 = mean2_in->contiguous(); i2 = invstd2_in->contiguous();
+  }
+  Tensor mask = want_mask ? at::empty({M, C / 8}, x1.options().dtype(at::kByte)) : Tensor();
+  Tensor work = at::empty({static_cast<int64_t>(cml::bn_workspace_bytes(M, static_cast<int>(C)) / 4 + 1)}, f32);
+  CML_CHECK_HIP(cml::launch_bn_fwd2(
+      x1.data_ptr(), x2.data_ptr(), y.data_ptr(), want_mask ? mask.data_ptr() : nullptr, M,
+      static_cast<int>(C), g1.data_ptr(), b1.data_ptr(), g2.data_ptr(), b2.data_ptr(),
+      m1.data_ptr<float>(), i1.data_ptr<float>(), m2.data_ptr<float>(), i2.data_ptr<float>(),
+      opt_ptr<float>(rm1, at::kFloat, "running_mean1", C), opt_ptr<float>(rv1, at::kFloat, "running_var1", C),
+      opt_ptr<float>(rm2, at::kFloat, "running_mean2", C), opt_ptr<float>(rv2, at::kFloat, "running_var2", C),
+      static_cast<float>(eps), static_cast<float>(momentum), training ? 1 : 0, work.data_ptr(),
+      cur_stream()));
+  return {y, m1, i1, m2, i2, mask};
+}
+
+// returns (dx1, dgamma1, dbeta1, dx2, dgamma2, dbeta2)
+std::vector<Tensor> bn_bwd2(const Tensor& dy_in, const optional<Tensor>& dy2_in, const Tensor& x1,
+                            const Tensor& x2, const Tensor& mask, const Tensor& g1,
+                            const Tensor& g2, const Tensor& mean1, const Tensor& invstd1,
+                            const Tensor& mean2, const Tensor& invstd2) {
+  check_nhwc(x1, "x1");
+  check_nhwc(x2, "x2");
+  Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x1.sizes() && x2.sizes() == x1.sizes(), "bn_bwd2 shape mismatch");
+  Tensor dy2;
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = dy2_in->contiguous(at::MemoryFormat::ChannelsLast);
+    check_nhwc(dy2, "dy2");
+    TORCH_CHECK(dy2.sizes() == x1.sizes(), "dy2 shape mismatch");
+  }
+  const int64_t C = x1.size(1);
+  const int64_t M = x1.numel() / C;
+  TORCH_CHECK(mask.scalar_type() == at::kByte && mask.is_contiguous() && mask.numel() == M * (C / 8),
+              "mask: contiguous uint8 [M, C/8]");
+  const c10::DeviceGuard guard(x1.device());
+  auto f32 = x1.options().dtype(at::kFloat);
+  Tensor dx1 = at::empty_like(x1), dx2 = at::empty_like(x2);
+  Tensor dg1 = at::empty({C}, g1.options()), db1 = at::empty({C}, g1.options());
+  Tensor dg2 = at::empty({C}, g2.options()), db2 = at::empty({C}, g2.options());
+  Tensor sums = at::empty({4, C}, f32);
+  Tensor work = at::empty({static_cast<int64_t>(cml::bn2_workspace_bytes(M, static_cast<int>(C)) / 4 + 1)}, f32);
+  CML_CHECK_HIP(cml::launch_bn_bwd2(
+      dy.data_ptr(), dy2.defined() ? dy2.data_ptr() : nullptr, x1.data_ptr(), x2.data_ptr(),
+      mask.data_ptr(), dx1.data_ptr(), dx2.data_ptr(), M, static_cast<int>(C), g1.data_ptr(),
+      g2.data_ptr(), mean1.data_ptr<float>(), invstd1.data_ptr<float>(), mean2.data_ptr<float>(),
+      invstd2.data_ptr<float>(), dg1.data_ptr(), db1.data_ptr(), dg2.data_ptr(), db2.data_ptr(),
+      sums.data_ptr<float>(), sums.data_ptr<float>() + C, sums.data_ptr<float>() + 2 * C,
+      sums.data_ptr<float>() + 3 * C, work.data_ptr(), cur_stream()));
+  return {dx1, dg1, db1, dx2, dg2, db2};
+}
+
 std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p) {
   check_nhwc(x, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(1) % 8 == 0, "maxpool: 4-D NHWC with C % 8 == 0");
@@ -669,6 +748,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fault", &fault, "Byzantine fault injection");
   m.def("bn_fwd", &bn_fwd, "fused NHWC BatchNorm(+res)(+ReLU) forward");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BatchNorm(+res)(+ReLU) backward");
+  m.def("bn_fwd2", &bn_fwd2, "relu(BN(x1) + BN(x2)) forward (downsample-block tail)");
+  m.def("bn_bwd2", &bn_bwd2, "relu(BN(x1) + BN(x2)) backward");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
   m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");

@@ -89,6 +89,25 @@ hipError_t launch_bn_bwd(const void* dy, const void* dy2, const void* x, const v
                          void* dbeta, float* sdz, float* sdzx, int relu, void* work,
                          hipStream_t stream);
 
+// Downsample-block tail y = relu(bn1(x1) + bn2(x2)) (two training BNs of the same shape, one
+// ReLU, optional 1-bit mask). Forward work: bn_workspace_bytes; backward: bn2_workspace_bytes.
+// Backward writes dx1, dx2, both BNs' dgamma / dbeta and their per-channel sums (sdz, sdzx1) and
+// (sdz_b, sdzx2).
+hipError_t launch_bn_fwd2(const void* x1, const void* x2, void* y, void* mask, int64_t M, int C,
+                          const void* gamma1, const void* beta1, const void* gamma2,
+                          const void* beta2, float* mean1, float* invstd1, float* mean2,
+                          float* invstd2, float* rmean1, float* rvar1, float* rmean2,
+                          float* rvar2, float eps, float momentum, int training, void* work,
+                          hipStream_t stream);
+size_t bn2_workspace_bytes(int64_t M, int C);
+hipError_t launch_bn_bwd2(const void* dy, const void* dy2, const void* x1, const void* x2,
+                          const void* mask, void* dx1, void* dx2, int64_t M, int C,
+                          const void* gamma1, const void* gamma2, const float* mean1,
+                          const float* invstd1, const float* mean2, const float* invstd2,
+                          void* dgamma1, void* dbeta1, void* dgamma2, void* dbeta2, float* sdz,
+                          float* sdzx1, float* sdz_b, float* sdzx2, void* work,
+                          hipStream_t stream);
+
 // NHWC bf16 max-pool with a one-byte argmax per output element; backward is a gather.
 hipError_t launch_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C,
                               int OH, int OW, int k, int s, int p, hipStream_t stream);

@@ -236,3 +236,58 @@ def test_stem_pad4_matches_conv(cuda):
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(outs[0][1], outs[1][1], rtol=2e-2, atol=0.5)
     assert m.conv1.weight.grad.shape == (8, 3, 7, 7)
+
+
+@pytest.mark.parametrize("C", [64, 256, 2048])
+@pytest.mark.parametrize("with_dy2", [False, True])
+def test_bn_add_bn_relu_matches_composition(cuda, C, with_dy2):
+    """Fused relu(bn3(x1) + bn_d(x2)) (one apply, one dual reduce, one dual apply) vs the two
+    separate fused BN ops + residual add, both against an fp32 reference of the same math on the
+    same bf16 inputs: the fused path must be at least as accurate (it adds the shortcut BN output
+    in fp32 instead of rounding it to bf16 first). Running stats and eval mode included."""
+    from consensusml_amd.ops.bn import BatchNormAct2d, ResidualLink, bn_add_bn_relu
+    torch.manual_seed(C)
+    shp = (4, C, 6, 5)
+    mk = lambda s, o: ((torch.randn(*shp, device=cuda) * s + o).to(torch.bfloat16)
+                       .contiguous(memory_format=torch.channels_last))
+    x1, x2 = mk(2.0, 0.5), mk(1.5, -0.3)
+    dy = torch.randn(*shp, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy2 = torch.randn(*shp, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.empty(4, C, device=cuda).uniform_(0.5, 1.5)
+    bb = torch.empty(4, C, device=cuda).uniform_(-0.5, 0.5)
+    res = []
+    for fused in (True, False):
+        bn1 = BatchNormAct2d(C, relu=True).to(cuda, torch.bfloat16)
+        bn2 = BatchNormAct2d(C, relu=False).to(cuda, torch.bfloat16)
+        with torch.no_grad():
+            bn1.weight.copy_(g[0]); bn1.bias.copy_(bb[0]); bn2.weight.copy_(g[1]); bn2.bias.copy_(bb[1])
+        a, c = x1.clone().requires_grad_(True), x2.clone().requires_grad_(True)
+        link = ResidualLink() if with_dy2 else None
+        y = bn_add_bn_relu(a, bn1, c, bn2, link) if fused else bn1(a, residual=bn2(c), out_link=link)
+        if with_dy2:
+            link.grad = dy2.clone()
+        y.backward(dy)
+        bn1.eval()
+        bn2.eval()
+        ye = bn_add_bn_relu(x1, bn1, x2, bn2) if fused else bn1(x1, residual=bn2(x2))
+        res.append([y, a.grad, c.grad, bn1.weight.grad, bn1.bias.grad, bn2.weight.grad,
+                    bn2.bias.grad, bn1.running_mean, bn1.running_var, bn2.running_mean,
+                    bn2.running_var, ye])
+    # fp32 reference
+    a, c = x1.float().requires_grad_(True), x2.float().requires_grad_(True)
+    ps = [t.clone().requires_grad_(True) for t in (g[0], bb[0], g[1], bb[1])]
+    rms = [torch.zeros(C, device=cuda), torch.ones(C, device=cuda), torch.zeros(C, device=cuda),
+           torch.ones(C, device=cuda)]
+    yr = torch.relu(F.batch_norm(a, rms[0], rms[1], ps[0], ps[1], True, 0.1, 1e-5)
+                    + F.batch_norm(c, rms[2], rms[3], ps[2], ps[3], True, 0.1, 1e-5))
+    yr.backward(dy.float() + (dy2.float() if with_dy2 else 0))
+    yre = torch.relu(F.batch_norm(x1.float(), rms[0], rms[1], ps[0], ps[1], False, 0.1, 1e-5)
+                     + F.batch_norm(x2.float(), rms[2], rms[3], ps[2], ps[3], False, 0.1, 1e-5))
+    ref = [yr, a.grad, c.grad, ps[0].grad, ps[1].grad, ps[2].grad, ps[3].grad] + rms + [yre]
+
+    def rel(p, q):
+        p, q = p.float(), q.float()
+        return ((p - q).norm() / q.norm().clamp_min(1e-6)).item()
+    for i, (f, u, r) in enumerate(zip(res[0], res[1], ref)):
+        ef, eu = rel(f, r), rel(u, r)
+        assert ef <= max(2 * eu, 0.05), (i, ef, eu)   # bf16 noise: ~2-4 % on both paths
