@@ -344,6 +344,48 @@ std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p
   return {y, idx};
 }
 
+// maxpool(relu(bn(x))): returns (y_pool, idx, mean, invstd); training -> batch stats (running
+// stats updated), else mean_in / invstd_in
+std::vector<Tensor> bn_relu_maxpool_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta,
+                                        const optional<Tensor>& rmean, const optional<Tensor>& rvar,
+                                        const optional<Tensor>& mean_in,
+                                        const optional<Tensor>& invstd_in, double eps,
+                                        double momentum, bool training, int64_t k, int64_t s,
+                                        int64_t p) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4, "bn_relu_maxpool: 4-D NHWC input");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "bn: C must be 8 * (power of 2) <= 2048");
+  TORCH_CHECK(gamma.scalar_type() == at::kBFloat16 && beta.scalar_type() == at::kBFloat16 &&
+                  gamma.is_contiguous() && beta.is_contiguous() && gamma.numel() == C, "gamma/beta");
+  const int64_t OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor mean, invstd;
+  if (training) {
+    mean = at::empty({C}, f32);
+    invstd = at::empty({C}, f32);
+    Tensor work = at::empty({static_cast<int64_t>(cml::bn_workspace_bytes(N * H * W, static_cast<int>(C)) / 4 + 1)}, f32);
+    CML_CHECK_HIP(cml::launch_bn_stats(x.data_ptr(), N * H * W, static_cast<int>(C),
+                                       mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                       opt_ptr<float>(rmean, at::kFloat, "running_mean", C),
+                                       opt_ptr<float>(rvar, at::kFloat, "running_var", C),
+                                       static_cast<float>(eps), static_cast<float>(momentum),
+                                       work.data_ptr(), cur_stream()));
+  } else {
+    TORCH_CHECK(mean_in.has_value() && invstd_in.has_value(), "eval needs mean / invstd");
+    mean = mean_in->contiguous();
+    invstd = invstd_in->contiguous();
+  }
+  Tensor y = at::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor idx = at::empty({N, OH, OW, C}, x.options().dtype(at::kByte));
+  CML_CHECK_HIP(cml::launch_bn_relu_maxpool_fwd(x.data_ptr(), mean.data_ptr<float>(),
+                                                invstd.data_ptr<float>(), gamma.data_ptr(),
+                                                beta.data_ptr(), y.data_ptr(), idx.data_ptr(), N,
+                                                H, W, C, OH, OW, k, s, p, cur_stream()));
+  return {y, idx, mean, invstd};
+}
+
 Tensor maxpool_bwd(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W, int64_t k,
                    int64_t s, int64_t p) {
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
@@ -750,6 +792,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd, "fused NHWC BatchNorm(+res)(+ReLU) backward");
   m.def("bn_fwd2", &bn_fwd2, "relu(BN(x1) + BN(x2)) forward (downsample-block tail)");
   m.def("bn_bwd2", &bn_bwd2, "relu(BN(x1) + BN(x2)) backward");
+  m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd, "maxpool(relu(BN(x))) forward (stem)");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
   m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");

@@ -712,4 +712,18 @@ hipError_t launch_bn_bwd2(const void* dy, const void* dy2, const void* x1, const
   return hipGetLastError();
 }
 
+// Training statistics only (stats + finalize), for consumers that apply the affine themselves.
+hipError_t launch_bn_stats(const void* x, int64_t M, int C, float* mean, float* invstd,
+                           float* rmean, float* rvar, float eps, float momentum, void* work,
+                           hipStream_t st) {
+  if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1) return hipErrorInvalidValue;
+  const bf16* xb = reinterpret_cast<const bf16*>(x);
+  const BNGeom g = geom(M, C);
+  float* part = reinterpret_cast<float*>(work);
+  bn_stats_kernel<<<g.nb, kBT, 0, st>>>(xb, M, C, g.rpb, part);
+  bn_finalize_kernel<<<(C + kFC - 1) / kFC, kBT, 0, st>>>(part, g.nb, xb, M, C, eps, momentum,
+                                                          mean, invstd, rmean, rvar);
+  return hipGetLastError();
+}
+
 }  // namespace cml

@@ -126,6 +126,16 @@ struct MultiCopyArgs {
 };
 hipError_t launch_multi_copy(const MultiCopyArgs& args, hipStream_t stream);
 
+// Stem: y = maxpool(relu(bn(x))) with the BN affine (training statistics from launch_bn_stats,
+// or running statistics) applied to every window tap; idx as launch_maxpool_fwd.
+hipError_t launch_bn_stats(const void* x, int64_t M, int C, float* mean, float* invstd,
+                           float* rmean, float* rvar, float eps, float momentum, void* work,
+                           hipStream_t stream);
+hipError_t launch_bn_relu_maxpool_fwd(const void* x, const float* mean, const float* invstd,
+                                      const void* gamma, const void* beta, void* y, void* idx,
+                                      int N, int H, int W, int C, int OH, int OW, int k, int s,
+                                      int p, hipStream_t stream);
+
 // NHWC bf16 channel zero-padding C (<= 4) -> 4 over npix pixels (y 8-B aligned).
 hipError_t launch_pad_c4(const void* x, void* y, int64_t npix, int C, hipStream_t stream);
 

@@ -20,18 +20,36 @@ constexpr int kPB = 256;
 // Forward. KK = compile-time window size (3 for the stem; 0 = runtime k): with KK fixed the
 // KK*KK 16-byte loads of a window are all in flight before the max (out-of-image taps load a
 // clamped in-image address and are masked).
-template <int KK>
+// AFF: the input is a pre-BatchNorm tensor; every tap is mapped through the BN affine and ReLU
+// (max(x * sc + bi, 0), sc = gamma * invstd, bi = beta - mean * sc) before the max, so the stem's
+// BN+ReLU output never exists in memory (the backward recomputes its ReLU mask from x).
+template <int KK, bool AFF>
 __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict__ x,
                                                          bf16* __restrict__ y,
                                                          uint8_t* __restrict__ idx, int N, int H,
                                                          int W, int C, int OH, int OW, int k_rt,
-                                                         int s, int p) {
+                                                         int s, int p,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd,
+                                                         const bf16* __restrict__ gamma,
+                                                         const bf16* __restrict__ beta) {
   const int k = KK > 0 ? KK : k_rt;
   const int cg = C / 8;
   const int i = blockIdx.x * kPB + threadIdx.x;
   if (i >= OW * cg) return;
   const int ow = i / cg;
   const int g = i - ow * cg;
+  float sc[8], bi[8];
+  if constexpr (AFF) {
+    float ga[8], be[8];
+    load_vec<bf16, 8>(gamma + 8 * g, ga);
+    load_vec<bf16, 8>(beta + 8 * g, be);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      sc[v] = invstd[8 * g + v] * ga[v];
+      bi[v] = be[v] - mean[8 * g + v] * sc[v];
+    }
+  }
   for (int row = blockIdx.y; row < N * OH; row += gridDim.y) {
     const int n = row / OH;
     const int oh = row - n * OH;
@@ -53,6 +71,10 @@ __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict
           in[a][b] = h >= 0 && h < H && w >= 0 && w < W;
           const int hh = in[a][b] ? h : 0, ww = in[a][b] ? w : 0;
           load_vec<bf16, 8>(x + ((static_cast<int64_t>(n) * H + hh) * W + ww) * C + 8 * g, t[a][b]);
+          if constexpr (AFF) {
+#pragma unroll
+            for (int v = 0; v < 8; ++v) t[a][b][v] = fmaxf(fmaf(t[a][b][v], sc[v], bi[v]), 0.f);
+          }
         }
 #pragma unroll
       for (int a = 0; a < KK; ++a)
@@ -75,6 +97,10 @@ __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict
           if (w < 0 || w >= W) continue;
           float v8[8];
           load_vec<bf16, 8>(xrow + static_cast<int64_t>(w) * C, v8);
+          if constexpr (AFF) {
+#pragma unroll
+            for (int v = 0; v < 8; ++v) v8[v] = fmaxf(fmaf(v8[v], sc[v], bi[v]), 0.f);
+          }
 #pragma unroll
           for (int v = 0; v < 8; ++v) {
             const bool take = v8[v] > best[v] || (v8[v] != v8[v]);
@@ -233,14 +259,29 @@ __global__ __launch_bounds__(256) void pad_c4_kernel(const uint16_t* __restrict_
 
 hipError_t launch_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C,
                               int OH, int OW, int k, int s, int p, hipStream_t st) {
+  return launch_bn_relu_maxpool_fwd(x, nullptr, nullptr, nullptr, nullptr, y, idx, N, H, W, C, OH,
+                                    OW, k, s, p, st);
+}
+
+hipError_t launch_bn_relu_maxpool_fwd(const void* x, const float* mean, const float* invstd,
+                                      const void* gamma, const void* beta, void* y, void* idx,
+                                      int N, int H, int W, int C, int OH, int OW, int k, int s,
+                                      int p, hipStream_t st) {
   if (C % 8 || k * k > 255) return hipErrorInvalidValue;
   if (N * OH < 1) return hipErrorInvalidValue;
   const dim3 grid = pgrid(OW * (C / 8), N * OH);
   const bf16* xp = reinterpret_cast<const bf16*>(x);
   bf16* yp = reinterpret_cast<bf16*>(y);
   uint8_t* ip = reinterpret_cast<uint8_t*>(idx);
-  if (k == 3) maxpool_fwd_kernel<3><<<grid, kPB, 0, st>>>(xp, yp, ip, N, H, W, C, OH, OW, k, s, p);
-  else maxpool_fwd_kernel<0><<<grid, kPB, 0, st>>>(xp, yp, ip, N, H, W, C, OH, OW, k, s, p);
+  const bf16* gp = reinterpret_cast<const bf16*>(gamma);
+  const bf16* bp = reinterpret_cast<const bf16*>(beta);
+  const bool aff = mean != nullptr;
+#define CML_MP(KK, A) maxpool_fwd_kernel<KK, A><<<grid, kPB, 0, st>>>(xp, yp, ip, N, H, W, C, OH, OW, k, s, p, mean, invstd, gp, bp)
+  if (k == 3 && aff) CML_MP(3, true);
+  else if (k == 3) CML_MP(3, false);
+  else if (aff) CML_MP(0, true);
+  else CML_MP(0, false);
+#undef CML_MP
   return hipGetLastError();
 }
 

@@ -291,3 +291,41 @@ def test_bn_add_bn_relu_matches_composition(cuda, C, with_dy2):
     for i, (f, u, r) in enumerate(zip(res[0], res[1], ref)):
         ef, eu = rel(f, r), rel(u, r)
         assert ef <= max(2 * eu, 0.05), (i, ef, eu)   # bf16 noise: ~2-4 % on both paths
+
+
+def test_stem_bn_relu_maxpool_fused(cuda):
+    """maxpool(relu(bn(x))) fused (BN output never stored) vs BN then pool, against fp32."""
+    from consensusml_amd.ops.bn import BatchNormAct2d
+    from consensusml_amd.ops.pool import bn_relu_max_pool2d, max_pool2d
+    torch.manual_seed(9)
+    C = 64
+    x0 = (torch.randn(4, C, 17, 15, device=cuda) * 2 + 0.3).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    dyp = torch.randn(4, C, 9, 8, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.empty(C, device=cuda).uniform_(-1.0, 1.5)     # some negative gammas: affine flips
+    b = torch.empty(C, device=cuda).uniform_(-0.5, 0.5)
+    res = []
+    for fused in (True, False):
+        bn = BatchNormAct2d(C, relu=True).to(cuda, torch.bfloat16)
+        with torch.no_grad():
+            bn.weight.copy_(g)
+            bn.bias.copy_(b)
+        x = x0.clone().requires_grad_(True)
+        y = bn_relu_max_pool2d(x, bn) if fused else max_pool2d(bn(x))
+        y.backward(dyp)
+        bn.eval()
+        ye = bn_relu_max_pool2d(x0, bn) if fused else max_pool2d(bn(x0))
+        res.append([y, x.grad, bn.weight.grad, bn.bias.grad, bn.running_mean, bn.running_var, ye])
+    xr = x0.float().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    yr = F.max_pool2d(torch.relu(F.batch_norm(xr, rm, rv, gr, br, True, 0.1, 1e-5)), 3, 2, 1)
+    yr.backward(dyp.float())
+    yre = F.max_pool2d(torch.relu(F.batch_norm(x0.float(), rm, rv, gr, br, False, 0.1, 1e-5)), 3, 2, 1)
+    ref = [yr, xr.grad, gr.grad, br.grad, rm, rv, yre]
+
+    def rel(p, q):
+        return ((p.float() - q.float()).norm() / q.float().norm().clamp_min(1e-6)).item()
+    for i, (f, u, r) in enumerate(zip(res[0], res[1], ref)):
+        ef, eu = rel(f, r), rel(u, r)
+        assert ef <= max(2 * eu, 0.03), (i, ef, eu)
