@@ -17,6 +17,7 @@ import torch.nn.functional as F
 
 from ..ops.bn import BatchNormAct2d, ResidualLink, bn_add_bn_relu, fused_ok, link_tap
 from ..ops.pool import bn_relu_max_pool2d, max_pool2d
+from ..ops.stem import stem_conv_bn_relu_pool, stem_ok
 
 # 1x1 stride-1 convolutions: which passes run as plain GEMMs (hipBLASLt) instead of MIOpen.
 #   "auto"   per-shape choice measured on MI355X at batch 512 (bench/conv_shapes.py,
@@ -32,6 +33,9 @@ CONV1X1_GEMM = os.environ.get("CML_CONV1X1_GEMM", "auto")
 RESIDUAL_LINK = True
 # downsample-block tail relu(bn3(z) + down_bn(zd)) as one fused op (ops.bn.bn_add_bn_relu)
 FUSE_DOWN_BN = os.environ.get("CML_FUSE_DOWN_BN", "1") == "1"
+# whole stem (conv + BN statistics, BN + ReLU + pool; backward in one weight-gradient pass) on
+# the HIP kernels of csrc/kernels/stem_conv.hip (ops.stem)
+FUSE_STEM_CONV = os.environ.get("CML_FUSE_STEM_CONV", "1") == "1"
 # stem BN + ReLU + max-pool in one pass (ops.pool.bn_relu_max_pool2d)
 FUSE_STEM_POOL = os.environ.get("CML_FUSE_STEM_POOL", "1") == "1"
 # stem input channels zero-padded 3 -> 4 on the GPU (see ResNet.stem)
@@ -213,8 +217,12 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = bn_relu_max_pool2d(self.stem(x), self.bn1, 3, 2, 1) if FUSE_STEM_POOL \
-            else max_pool2d(self.bn1(self.stem(x)), 3, 2, 1)
+        if FUSE_STEM_CONV and stem_ok(x, self.conv1, self.bn1):
+            x = stem_conv_bn_relu_pool(x, self.conv1, self.bn1)
+        elif FUSE_STEM_POOL:
+            x = bn_relu_max_pool2d(self.stem(x), self.bn1, 3, 2, 1)
+        else:
+            x = max_pool2d(self.bn1(self.stem(x)), 3, 2, 1)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

@@ -41,8 +41,8 @@ def _pool_ok(x: torch.Tensor, k: int, s: int) -> bool:
 class _BNReluPoolFn(torch.autograd.Function):
     """maxpool(relu(bn(x))): forward = BN statistics + ONE pass that applies the affine and ReLU
     to every window tap and keeps the max (the 112x112 BN output is never written); backward =
-    the pool's gather into the BN-output gradient, then the fused BN backward with the ReLU mask
-    recomputed from x."""
+    the pool's gather into the BN-output gradient (ReLU-masked by the forward's argmax 255 for
+    windows whose max is <= 0), then the fused BN backward."""
 
     @staticmethod
     def forward(ctx, x, gamma, beta, rmean, rvar, stats, eps, momentum, training, k, s, p):
@@ -58,7 +58,8 @@ class _BNReluPoolFn(torch.autograd.Function):
         x, idx, gamma, beta, mean, invstd = ctx.saved_tensors
         k, s, p = ctx.geom
         dz = lib().maxpool_bwd(dy, idx, x.shape[2], x.shape[3], k, s, p)
-        dx, dg, db, _ = lib().bn_bwd(dz, None, x, None, gamma, beta, mean, invstd, True, False)
+        # the forward marked windows with max <= 0 (argmax 255): dz is already ReLU-masked
+        dx, dg, db, _ = lib().bn_bwd(dz, None, x, None, gamma, beta, mean, invstd, False, False)
         return dx, dg, db, None, None, None, None, None, None, None, None, None
 
 

@@ -386,6 +386,73 @@ std::vector<Tensor> bn_relu_maxpool_fwd(const Tensor& x, const Tensor& gamma, co
   return {y, idx, mean, invstd};
 }
 
+// ResNet stem conv (7x7/s2/p3, C_in 3 or 4 -> 64) with the BatchNorm statistics in its epilogue.
+// x: NHWC bf16 [N, C, H, W] channels_last; wpk: packed bf16 [64, 224]. Returns {z, mean, invstd}
+// (mean / invstd undefined when !training).
+std::vector<Tensor> stem_conv_fwd(const Tensor& x, const Tensor& wpk, const optional<Tensor>& rmean,
+                                  const optional<Tensor>& rvar, double eps, double momentum,
+                                  bool training) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4, "stem_conv: 4-D input");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C == 3 || C == 4, "stem_conv: 3 or 4 input channels");
+  TORCH_CHECK(wpk.scalar_type() == at::kBFloat16 && wpk.is_contiguous() && wpk.numel() == 64 * 224 &&
+                  wpk.device() == x.device(), "stem_conv: packed bf16 weights [64, 224]");
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  const int grid = cml::stem_fwd_grid(N, OH, OW, C);
+  Tensor part = at::empty({grid, 2, 64}, f32);
+  Tensor z = at::empty({N, 64, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor mean, invstd;
+  if (training) {
+    mean = at::empty({64}, f32);
+    invstd = at::empty({64}, f32);
+  }
+  CML_CHECK_HIP(cml::launch_stem_conv_fwd(
+      x.data_ptr(), wpk.data_ptr(), z.data_ptr(), part.data_ptr<float>(), grid,
+      training ? mean.data_ptr<float>() : nullptr, training ? invstd.data_ptr<float>() : nullptr,
+      training ? opt_ptr<float>(rmean, at::kFloat, "running_mean", 64) : nullptr,
+      training ? opt_ptr<float>(rvar, at::kFloat, "running_var", 64) : nullptr,
+      static_cast<float>(eps), static_cast<float>(momentum), N, H, W, C, OH, OW, cur_stream()));
+  return {z, mean, invstd};
+}
+
+// Stem backward through BN: g = ReLU-masked pool gradient (NHWC [N, 64, OH, OW]), z = conv output,
+// x = conv input. Returns {dw [64, C, 7, 7] fp32, dgamma fp32 [64], dbeta fp32 [64]}.
+std::vector<Tensor> stem_wgrad(const Tensor& g_in, const Tensor& z, const Tensor& x,
+                               const Tensor& mean, const Tensor& invstd, const Tensor& gamma) {
+  check_nhwc(x, "x");
+  check_nhwc(z, "z");
+  Tensor g = g_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(g, "g");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  TORCH_CHECK(C == 3 || C == 4, "stem_wgrad: 3 or 4 input channels");
+  TORCH_CHECK(z.size(0) == N && z.size(1) == 64 && z.size(2) == OH && z.size(3) == OW &&
+                  g.sizes() == z.sizes(), "stem_wgrad: g / z shape");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && invstd.scalar_type() == at::kFloat &&
+                  mean.numel() == 64 && invstd.numel() == 64 && mean.is_contiguous() &&
+                  invstd.is_contiguous(), "stem_wgrad: fp32 mean / invstd [64]");
+  TORCH_CHECK(gamma.scalar_type() == at::kBFloat16 && gamma.is_contiguous() && gamma.numel() == 64,
+              "stem_wgrad: bf16 gamma [64]");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  const int grid = cml::stem_bwd_grid(N, OH, OW, C);
+  const int64_t pw = static_cast<int64_t>(cml::stem_wgrad_part_floats());
+  Tensor part = at::empty({grid, pw}, f32);
+  Tensor tot = at::empty({pw}, x.options().dtype(at::kDouble));
+  Tensor dw = at::empty({64, C, 7, 7}, f32);
+  Tensor dg = at::empty({64}, f32), db = at::empty({64}, f32);
+  CML_CHECK_HIP(cml::launch_stem_wgrad(g.data_ptr(), z.data_ptr(), x.data_ptr(),
+                                       mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                       gamma.data_ptr(), part.data_ptr<float>(), grid,
+                                       tot.data_ptr<double>(), dw.data_ptr<float>(),
+                                       dg.data_ptr<float>(), db.data_ptr<float>(), N, H, W, C, OH,
+                                       OW, cur_stream()));
+  return {dw, dg, db};
+}
+
 Tensor maxpool_bwd(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W, int64_t k,
                    int64_t s, int64_t p) {
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
@@ -793,6 +860,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd2", &bn_fwd2, "relu(BN(x1) + BN(x2)) forward (downsample-block tail)");
   m.def("bn_bwd2", &bn_bwd2, "relu(BN(x1) + BN(x2)) backward");
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd, "maxpool(relu(BN(x))) forward (stem)");
+  m.def("stem_conv_fwd", &stem_conv_fwd, "ResNet stem 7x7/s2 conv + BN statistics (MFMA)");
+  m.def("stem_wgrad", &stem_wgrad, "ResNet stem weight gradient through BN (MFMA, one pass)");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
   m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");

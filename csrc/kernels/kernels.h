@@ -206,4 +206,23 @@ size_t colsum_workspace_bytes(int64_t M, int N);
 hipError_t launch_colsum(const void* x, int64_t M, int N, void* out, void* work,
                          hipStream_t stream);
 
+// ResNet stem 7x7/s2/p3 convolution, C_in 3 or 4 -> 64, NHWC bf16 (stem_conv.hip).
+// Forward: z = conv(x, wpk) with wpk the packed weights [64][224] (k = (ky*8 + kx)*4 + c, zero for
+// kx = 7 / c >= C_in); part [grid][2][64] receives per-workgroup channel sums and sums of squares
+// and, when mean != nullptr, mean / invstd (and running stats) are finalized from them.
+// Backward: from g (ReLU-masked max-pool gradient), z, x and the forward mean / invstd, the weight
+// gradient of the conv THROUGH the BatchNorm (dw [64][C][7][7] fp32) and dgamma / dbeta (fp32);
+// part: grid x stem_wgrad_part_floats() floats, tot: stem_wgrad_part_floats() doubles.
+int stem_fwd_grid(int N, int OH, int OW, int C);
+int stem_bwd_grid(int N, int OH, int OW, int C);
+size_t stem_wgrad_part_floats();
+hipError_t launch_stem_conv_fwd(const void* x, const void* wpk, void* z, float* part, int grid,
+                                float* mean, float* invstd, float* rmean, float* rvar, float eps,
+                                float momentum, int N, int H, int W, int C, int OH, int OW,
+                                hipStream_t stream);
+hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const float* mean,
+                             const float* invstd, const void* gamma, float* part, int grid,
+                             double* tot, float* dw, float* dgamma, float* dbeta, int N, int H,
+                             int W, int C, int OH, int OW, hipStream_t stream);
+
 }  // namespace cml

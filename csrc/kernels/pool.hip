@@ -20,9 +20,11 @@ constexpr int kPB = 256;
 // Forward. KK = compile-time window size (3 for the stem; 0 = runtime k): with KK fixed the
 // KK*KK 16-byte loads of a window are all in flight before the max (out-of-image taps load a
 // clamped in-image address and are masked).
-// AFF: the input is a pre-BatchNorm tensor; every tap is mapped through the BN affine and ReLU
-// (max(x * sc + bi, 0), sc = gamma * invstd, bi = beta - mean * sc) before the max, so the stem's
-// BN+ReLU output never exists in memory (the backward recomputes its ReLU mask from x).
+// AFF: the input is a pre-BatchNorm tensor; every tap is mapped through the BN affine
+// (x * sc + bi, sc = gamma * invstd, bi = beta - mean * sc), the max taken, then the ReLU
+// (max(relu(u)) = relu(max(u))), so the stem's BN+ReLU output never exists in memory. A window
+// whose max is <= 0 gets argmax 255: its gradient is the ReLU's zero, and the backward gather
+// routes it nowhere, i.e. the pool gradient comes out already masked by the ReLU.
 template <int KK, bool AFF>
 __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict__ x,
                                                          bf16* __restrict__ y,
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict
           load_vec<bf16, 8>(x + ((static_cast<int64_t>(n) * H + hh) * W + ww) * C + 8 * g, t[a][b]);
           if constexpr (AFF) {
 #pragma unroll
-            for (int v = 0; v < 8; ++v) t[a][b][v] = fmaxf(fmaf(t[a][b][v], sc[v], bi[v]), 0.f);
+            for (int v = 0; v < 8; ++v) t[a][b][v] = fmaf(t[a][b][v], sc[v], bi[v]);
           }
         }
 #pragma unroll
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict
           load_vec<bf16, 8>(xrow + static_cast<int64_t>(w) * C, v8);
           if constexpr (AFF) {
 #pragma unroll
-            for (int v = 0; v < 8; ++v) v8[v] = fmaxf(fmaf(v8[v], sc[v], bi[v]), 0.f);
+            for (int v = 0; v < 8; ++v) v8[v] = fmaf(v8[v], sc[v], bi[v]);
           }
 #pragma unroll
           for (int v = 0; v < 8; ++v) {
@@ -108,6 +110,13 @@ __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict
             arg[v] = take ? static_cast<uint8_t>(a * k + b) : arg[v];
           }
         }
+      }
+    }
+    if constexpr (AFF) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        arg[v] = best[v] > 0.f || best[v] != best[v] ? arg[v] : static_cast<uint8_t>(255);
+        best[v] = best[v] > 0.f || best[v] != best[v] ? best[v] : 0.f;
       }
     }
     const int64_t o = (static_cast<int64_t>(row) * OW + ow) * C + 8 * g;

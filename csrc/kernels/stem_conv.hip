@@ -1,0 +1,606 @@
+// ResNet stem: 7x7 / stride 2 / pad 3 convolution (C_in <= 4 -> 64 channels) on MFMA, with the
+// BatchNorm that follows it folded into the two passes.
+//
+// forward  stem_conv_fwd: implicit GEMM z[pix][co] = sum_k im2col[pix][k] W[co][k] on
+//          v_mfma_f32_32x32x16_bf16. A band of kTY output rows is one tile: its input rows are
+//          staged once in LDS (4 channels = 8 B per pixel, zero padding, C_in = 3 read directly, so
+//          no channel-padding pass), the packed weights live in registers for the workgroup's
+//          lifetime (persistent grid), and the epilogue stores z and accumulates the BatchNorm
+//          statistics (per-channel sum and sum of squares) -> no separate statistics pass over the
+//          822 MB stem output. K order: (ky 0..6)(kx 0..7, 7 = zero tap)(c 0..3) = 224, so every
+//          MFMA k-step is one input row x 4 taps x 4 channels = two 16-B LDS reads per lane.
+//
+// backward stem_wgrad: the BatchNorm backward and the weight gradient in ONE pass over
+//          (g, z, x), g = the max-pool gradient, already masked by the ReLU (the fused pool forward
+//          marks windows whose max is <= 0 with argmax 255, so they route no gradient).
+//          With xhat = (z - mean) invstd the BN backward is
+//            dz = gamma invstd (g - mean(g) - xhat mean(g xhat)),
+//          and dW = sum_p dz[p] (x) im2col[p] is linear in dz, so the kernel accumulates
+//            G = sum_p g (x) im2col,  X = sum_p xhat (x) im2col,  colA = sum_p im2col,
+//            s1 = sum_p g,  s2 = sum_p g xhat
+//          and stem_wgrad_finalize forms dW = gamma invstd (G - s1/M colA - s2/M X),
+//          dgamma = s2, dbeta = s1. dz never exists: the BN backward reduce and apply passes
+//          (2.5 GB of traffic at batch 512) and the library weight-gradient kernel become this
+//          one pass. The products sum over pixels, so both MFMA operands come out of LDS through
+//          ds_read_b64_tr_b16 (the gfx950 transpose read): the g / xhat chunk is stored
+//          [pixel][channel] as loaded and the input tile is the same one the forward uses; no
+//          im2col or transposed copy is materialised anywhere. One wave per kernel row ky
+//          (7 waves) owns the five 32 x 32 accumulators (g, xhat) x (channel blocks 0, 1) + ones.
+#include <math.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace cml {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kCo = 64;                 // output channels
+constexpr int kKP = 224;                // packed K
+constexpr int kSteps = kKP / 16;        // 14 MFMA k-steps, step s = (ky = s / 2, kx = 4 (s & 1) ..)
+constexpr int kTY = 8;                  // forward: output rows per tile
+constexpr int kTYB = 16;                // backward: output rows per tile (fewer tile-load bubbles)
+constexpr int kFT = 256;                // forward workgroup: 4 waves
+constexpr int kBT = 512;                // backward workgroup: 8 waves
+constexpr int kCh = 64;                 // backward pixel chunk (4 MFMA k-steps)
+constexpr int kPartW = 2 * kCo * kKP + kKP + 2 * kCo;   // floats per backward partial
+
+__host__ __device__ constexpr int tile_cols(int OW) { return 2 * OW + 6; }   // ix = -3 .. 2 OW + 2
+__host__ __device__ constexpr int tile_rows(int TY) { return 2 * TY + 5; }
+
+__device__ __forceinline__ f32x16 mfma(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8_t ld_frag(const uint16_t* p) {   // 16-B aligned
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p));
+}
+// transposed LDS read (T10): lane 4q + p of each 16-lane group gives the address of row q,
+// columns 4p..4p+3 of a 4 x 16 block; lane i receives column i, row q in element q
+__device__ __forceinline__ s16x4 ld_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+__device__ __forceinline__ bf16x8_t cat(s16x4 a, s16x4 b) {
+  return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// exact row of pixel index p < 2^20 in a band of width OW (float reciprocal, no integer divide)
+__device__ __forceinline__ int row_of(int p, float inv_ow) {
+  return __float2int_rz((static_cast<float>(p) + 0.5f) * inv_ow);
+}
+
+// Input rows 2 oy0 - 3 .. 2 oy0 + 2 TY + 1 of image n -> LDS [tile_rows][WT] x 8 B (zero outside
+// the image; channels C..3 zero). VEC (C = 3, W % 4 == 0, 8-B aligned rows): a thread moves 4
+// pixels = 24 B as three 8-B loads, up to 4 groups in flight, so a tile costs about one memory
+// round trip instead of one per input row.
+template <int C, int TY, bool VEC>
+__device__ __forceinline__ void stage_input(const uint16_t* __restrict__ x, uint2* __restrict__ tile,
+                                            int n, int oy0, int H, int W, int WT, int tid,
+                                            int nthr) {
+  const int iy0 = 2 * oy0 - 3;
+  if constexpr (VEC) {
+    const int t0 = iy0 < 0 ? -iy0 : 0;                          // first in-image tile row
+    const int t1 = min(tile_rows(TY), H - iy0);                 // one past the last
+    // zero: rows outside the image and the pad columns (u < 3, u >= W + 3) of the others
+    const int npad = WT - W;                                    // u < 3 and u >= W + 3
+    for (int t = 0; t < tile_rows(TY); ++t) {
+      if (t < t0 || t >= t1) {
+        for (int u = tid; u < WT; u += nthr) tile[t * WT + u] = make_uint2(0u, 0u);
+      } else if (tid < npad) {
+        tile[t * WT + (tid < 3 ? tid : W + tid)] = make_uint2(0u, 0u);
+      }
+    }
+    const int G = W / 4;
+    const int total = (t1 > t0 ? t1 - t0 : 0) * G;
+    const float inv_g = 1.f / static_cast<float>(G);
+    const uint16_t* xb = x + (static_cast<int64_t>(n) * H + iy0) * W * 3;
+    for (int e0 = tid; e0 < total; e0 += 4 * nthr) {
+      uint2 v[4][3];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = e0 + k * nthr;
+        const int ec = e < total ? e : 0;
+        const int tr = __float2int_rz((static_cast<float>(ec) + 0.5f) * inv_g);
+        const int g = ec - tr * G;
+        const uint2* src = reinterpret_cast<const uint2*>(xb + (static_cast<int64_t>(t0 + tr) * W + 4 * g) * 3);
+        v[k][0] = src[0];
+        v[k][1] = src[1];
+        v[k][2] = src[2];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = e0 + k * nthr;
+        if (e >= total) break;
+        const int tr = __float2int_rz((static_cast<float>(e) + 0.5f) * inv_g);
+        const int g = e - tr * G;
+        // 12 bf16 = pixels 4g..4g+3 x channels 0..2 -> four 8-B LDS pixels (channel 3 = 0)
+        const uint32_t w0 = v[k][0].x, w1 = v[k][0].y, w2 = v[k][1].x, w3 = v[k][1].y,
+                       w4 = v[k][2].x, w5 = v[k][2].y;
+        uint2* dst = tile + (t0 + tr) * WT + 3 + 4 * g;
+        dst[0] = make_uint2(w0, w1 & 0xffffu);
+        dst[1] = make_uint2((w1 >> 16) | (w2 << 16), w2 >> 16);
+        dst[2] = make_uint2(w3, w4 & 0xffffu);
+        dst[3] = make_uint2((w4 >> 16) | (w5 << 16), w5 >> 16);
+      }
+    }
+  } else {
+#pragma unroll 3
+    for (int t = 0; t < tile_rows(TY); ++t) {
+      const int iy = iy0 + t;
+      const bool rok = iy >= 0 && iy < H;
+      const uint16_t* xr = x + (static_cast<int64_t>(n) * H + (rok ? iy : 0)) * W * C;
+      for (int u = tid; u < WT; u += nthr) {
+        const int ix = u - 3;
+        uint2 v = make_uint2(0u, 0u);
+        if (rok && ix >= 0 && ix < W) {
+          if constexpr (C == 4) {
+            v = *reinterpret_cast<const uint2*>(xr + static_cast<int64_t>(ix) * 4);
+          } else {
+            const uint16_t* q = xr + static_cast<int64_t>(ix) * C;
+            const uint32_t c0 = q[0];
+            const uint32_t c1 = C > 1 ? q[1] : 0u;
+            const uint32_t c2 = C > 2 ? q[2] : 0u;
+            v = make_uint2(c0 | (c1 << 16), c2);
+          }
+        }
+        tile[t * WT + u] = v;
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------- forward
+template <int C, bool VEC>
+__global__ __launch_bounds__(kFT) void stem_conv_fwd_kernel(const uint16_t* __restrict__ x,
+                                                           const uint16_t* __restrict__ wpk,
+                                                           uint16_t* __restrict__ z,
+                                                           float* __restrict__ part, int N,
+                                                           int H, int W, int OH, int OW) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint2* tile = reinterpret_cast<uint2*>(smem);
+  const int WT = tile_cols(OW);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const float inv_ow = 1.f / static_cast<float>(OW);
+  // B operand of step s, channel block b: lane (r, h) holds W[32 b + r][16 s + 8 h .. + 7]
+  bf16x8_t wf[kSteps][2];
+#pragma unroll
+  for (int s = 0; s < kSteps; ++s)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) wf[s][b] = ld_frag(wpk + (32 * b + r) * kKP + 16 * s + 8 * h);
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+  const int bands = (OH + kTY - 1) / kTY;
+  const int ntiles = N * bands;
+  const int nblk = (kTY * OW + 31) / 32;
+  for (int tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+    const int n = tl / bands;
+    const int oy0 = (tl - n * bands) * kTY;
+    const int pv = min(kTY, OH - oy0) * OW;            // valid pixels of the band
+    __syncthreads();                                   // previous tile's LDS readers are done
+    stage_input<C, kTY, VEC>(x, tile, n, oy0, H, W, WT, threadIdx.x, kFT);
+    __syncthreads();
+    uint16_t* zt = z + ((static_cast<int64_t>(n) * OH + oy0) * OW) * kCo;
+    for (int blk = wave; blk < nblk; blk += kFT / 64) {
+      const int p = 32 * blk + r;
+      const int pc = p < pv ? p : 0;                   // rows past the band: read pixel 0, drop
+      const int oyl = row_of(pc, inv_ow);
+      const int ox = pc - oyl * OW;
+      // A operand: lane (r = pixel, h) holds taps kx0 + 2h, kx0 + 2h + 1 x 4 channels of row ky
+      const uint16_t* a0 = reinterpret_cast<const uint16_t*>(tile + 2 * oyl * WT + 2 * ox + 2 * h);
+      f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+      for (int s = 0; s < kSteps; ++s) {
+        const bf16x8_t a = ld_frag(a0 + 4 * ((s >> 1) * WT + 4 * (s & 1)));
+        acc0 = mfma(a, wf[s][0], acc0);
+        acc1 = mfma(a, wf[s][1], acc1);
+      }
+      // register i: pixel 32 blk + (i & 3) + 8 (i >> 2) + 4 h, channel 32 b + r
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int pp = 32 * blk + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (pp < pv) {
+          const float v0 = acc0[i], v1 = acc1[i];
+          uint16_t* zo = zt + static_cast<int64_t>(pp) * kCo + r;
+          zo[0] = f2bf(v0);
+          zo[32] = f2bf(v1);
+          s1[0] += v0;
+          s2[0] = fmaf(v0, v0, s2[0]);
+          s1[1] += v1;
+          s2[1] = fmaf(v1, v1, s2[1]);
+        }
+      }
+    }
+  }
+  // workgroup partial [2][64] in a fixed order: (wave, half) slots summed by 128 threads
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);         // [4 waves][2 h][2 stat][64]
+  const int slot = wave * 2 + h;
+  red[(slot * 2 + 0) * kCo + r] = s1[0];
+  red[(slot * 2 + 0) * kCo + 32 + r] = s1[1];
+  red[(slot * 2 + 1) * kCo + r] = s2[0];
+  red[(slot * 2 + 1) * kCo + 32 + r] = s2[1];
+  __syncthreads();
+  if (threadIdx.x < 2 * kCo) {
+    const int st = threadIdx.x / kCo, c = threadIdx.x % kCo;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 2 * (kFT / 64); ++k) acc += red[(k * 2 + st) * kCo + c];
+    part[static_cast<int64_t>(blockIdx.x) * 2 * kCo + st * kCo + c] = acc;
+  }
+}
+
+// mean / invstd from the [nb][2][64] sums (fp64 fold, 16 slices x 64 channels, fixed order);
+// running statistics update with the unbiased variance.
+__global__ __launch_bounds__(1024) void stem_stats_finalize_kernel(const float* __restrict__ part,
+                                                                  int nb, double M, float eps,
+                                                                  float momentum,
+                                                                  float* __restrict__ mean,
+                                                                  float* __restrict__ invstd,
+                                                                  float* __restrict__ rmean,
+                                                                  float* __restrict__ rvar) {
+  __shared__ double ls[16][kCo], lq[16][kCo];
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  double S = 0.0, Q = 0.0;
+  for (int b = sl; b < nb; b += 16) {
+    S += part[static_cast<int64_t>(b) * 2 * kCo + c];
+    Q += part[static_cast<int64_t>(b) * 2 * kCo + kCo + c];
+  }
+  ls[sl][c] = S;
+  lq[sl][c] = Q;
+  __syncthreads();
+  if (sl != 0) return;
+  S = 0.0;
+  Q = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    S += ls[k][c];
+    Q += lq[k][c];
+  }
+  const double mu = S / M;
+  double var = Q / M - mu * mu;
+  if (var < 0.0) var = 0.0;
+  mean[c] = static_cast<float>(mu);
+  invstd[c] = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+  if (rmean) {
+    const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
+    rmean[c] = static_cast<float>((1.0 - momentum) * rmean[c] + momentum * mu);
+    rvar[c] = static_cast<float>((1.0 - momentum) * rvar[c] + momentum * unb);
+  }
+}
+
+// ---------------------------------------------------------------------------------- backward
+// byte offset of 16-B chunk ch (8 channels) of pixel row rho in a [64 pixels][64 channels] image:
+// chunks 0-3 / 4-7 swap on rows with bit 1 set, so the 4 rows of a transposed read hit 4 distinct
+// 16-bank groups (no conflicts with 128-B rows)
+__device__ __forceinline__ int chunk_off(int rho, int ch) {
+  return rho * 128 + ((ch ^ (((rho >> 1) & 1) << 2)) << 4);
+}
+
+template <int C, bool VEC>
+__global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restrict__ g,
+                                                        const uint16_t* __restrict__ z,
+                                                        const uint16_t* __restrict__ x,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd,
+                                                        float* __restrict__ part, int N, int H,
+                                                        int W, int OH, int OW) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* gbuf = smem;                                   // [64 px][64 ch] bf16, swizzled
+  char* xbuf = smem + kCh * 128;
+  uint2* tile = reinterpret_cast<uint2*>(smem + 2 * kCh * 128);
+  const int WT = tile_cols(OW);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, r = lane & 31;
+  const int gi = lane & 15, grp = lane >> 4;           // 16-lane group of the transposed reads
+  const int q = gi >> 2, pq = gi & 3;
+  // wave -> M block mb (0, 1: g channels 0-31 / 32-63; 2, 3: xhat) x kernel rows ky0 .. +nky-1;
+  // waves w and w + 4 share a SIMD, so every SIMD owns 4 + 3 = 7 accumulators
+  const int mb = wave & 3;
+  const int ky0 = wave < 4 ? 0 : 4;
+  const int nky = wave < 4 ? 4 : 3;
+  const char* abuf = mb < 2 ? gbuf : xbuf;
+  const int chn0 = 4 * (mb & 1) + 2 * (grp & 1) + (pq >> 1);
+  const float inv_ow = 1.f / static_cast<float>(OW);
+  // staging role: pixel tid >> 3 of the chunk, channels 8 cc .. 8 cc + 7
+  const int cc = tid & 7, prow = tid >> 3;
+  float mu[8], is[8], s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mu[k] = mean[8 * cc + k];
+    is[k] = invstd[8 * cc + k];
+    s1[k] = 0.f;
+    s2[k] = 0.f;
+  }
+  f32x16 acc[4] = {};
+  float ca[4] = {0.f, 0.f, 0.f, 0.f};                  // colA share: column (ky0 + kk) 32 + r
+  const int bands = (OH + kTYB - 1) / kTYB;
+  const int ntiles = N * bands;
+  auto band_pv = [&](int tl) {
+    const int n = tl / bands;
+    return min(kTYB, OH - (tl - n * bands) * kTYB) * OW;
+  };
+  auto band_base = [&](int tl) {
+    const int n = tl / bands;
+    return (static_cast<int64_t>(n) * OH + (tl - n * bands) * kTYB) * OW;
+  };
+  // one-chunk register prefetch of (g, z) across the flattened (tile, chunk) sequence
+  uint4 gv = make_uint4(0u, 0u, 0u, 0u), zv = gv;
+  bool okv = false;
+  auto fetch = [&](int tl, int ch) {
+    const int pp = kCh * ch + prow;
+    okv = tl < ntiles && pp < band_pv(tl);
+    if (okv) {
+      const int64_t o = (band_base(tl) + pp) * kCo + 8 * cc;
+      gv = *reinterpret_cast<const uint4*>(g + o);
+      zv = *reinterpret_cast<const uint4*>(z + o);
+    } else {
+      gv = make_uint4(0u, 0u, 0u, 0u);
+      zv = gv;
+    }
+  };
+  fetch(blockIdx.x, 0);
+  for (int tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+    const int n = tl / bands;
+    const int oy0 = (tl - n * bands) * kTYB;
+    const int pv = band_pv(tl);
+    const int nch = (pv + kCh - 1) / kCh;
+    for (int ch = 0; ch < nch; ++ch) {
+      __syncthreads();                                 // previous chunk's / tile's readers done
+      if (ch == 0) stage_input<C, kTYB, VEC>(x, tile, n, oy0, H, W, WT, tid, kBT);
+      {
+        // ---- g / xhat of the prefetched pixel -> LDS; BN-backward sums
+        const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
+        const uint32_t zw[4] = {zv.x, zv.y, zv.z, zv.w};
+        uint32_t xw[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float g0 = __uint_as_float(gw[k] << 16), g1 = __uint_as_float(gw[k] & 0xffff0000u);
+          float x0 = (__uint_as_float(zw[k] << 16) - mu[2 * k]) * is[2 * k];
+          float x1 = (__uint_as_float(zw[k] & 0xffff0000u) - mu[2 * k + 1]) * is[2 * k + 1];
+          x0 = okv ? x0 : 0.f;
+          x1 = okv ? x1 : 0.f;
+          s1[2 * k] += g0;
+          s1[2 * k + 1] += g1;
+          s2[2 * k] = fmaf(g0, x0, s2[2 * k]);
+          s2[2 * k + 1] = fmaf(g1, x1, s2[2 * k + 1]);
+          xw[k] = static_cast<uint32_t>(f2bf(x0)) | (static_cast<uint32_t>(f2bf(x1)) << 16);
+        }
+        *reinterpret_cast<uint4*>(gbuf + chunk_off(prow, cc)) = gv;
+        *reinterpret_cast<uint4*>(xbuf + chunk_off(prow, cc)) = make_uint4(xw[0], xw[1], xw[2], xw[3]);
+      }
+      if (ch + 1 < nch) fetch(tl, ch + 1);
+      else fetch(tl + gridDim.x, 0);
+      __syncthreads();
+      const bool full = kCh * (ch + 1) <= pv;
+      // ---- 4 k-steps of 16 pixels
+#pragma unroll
+      for (int ks = 0; ks < kCh / 16; ++ks) {
+        s16x4 a[2];
+        int tb[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int rho = 16 * ks + 8 * h + 4 * e + q;  // this lane's address row
+          a[e] = ld_tr(abuf + chunk_off(rho, chn0) + 8 * (pq & 1));
+          int pp = kCh * ch + rho;
+          pp = pp < pv ? pp : 0;
+          const int oyl = row_of(pp, inv_ow);
+          const int ox = pp - oyl * OW;
+          tb[e] = (2 * oyl + ky0) * WT + 2 * ox + 4 * (grp & 1) + pq;
+        }
+        const bf16x8_t A = cat(a[0], a[1]);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          if (kk < nky) {
+            const s16x4 b0 = ld_tr(reinterpret_cast<const char*>(tile + tb[0] + kk * WT));
+            const s16x4 b1 = ld_tr(reinterpret_cast<const char*>(tile + tb[1] + kk * WT));
+            acc[kk] = mfma(A, cat(b0, b1), acc[kk]);
+            if (ks == mb) {                            // colA: each k-step summed by one wave
+              const int pj = kCh * ch + 16 * ks + 8 * h;
+              float sum = 0.f;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const uint32_t w2 = static_cast<uint32_t>(static_cast<uint16_t>(b0[j]));
+                sum += (full || pj + j < pv) ? __uint_as_float(w2 << 16) : 0.f;
+                const uint32_t w3 = static_cast<uint32_t>(static_cast<uint16_t>(b1[j]));
+                sum += (full || pj + 4 + j < pv) ? __uint_as_float(w3 << 16) : 0.f;
+              }
+              ca[kk] += sum;
+            }
+          }
+        }
+      }
+    }
+  }
+  // ---- partials: G [64][224], X [64][224], colA [224], s1 [64], s2 [64]
+  float* pw = part + static_cast<int64_t>(blockIdx.x) * kPartW;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    if (kk < nky) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int co = 32 * (mb & 1) + (i & 3) + 8 * (i >> 2) + 4 * h;
+        pw[(mb >> 1) * kCo * kKP + co * kKP + (ky0 + kk) * 32 + r] = acc[kk][i];
+      }
+    }
+  }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);         // [64 rows][2 stat][64]
+  float* redc = red + kCh * 2 * kCo;                   // [8 waves][2 h][4 kk][32]
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[(prow * 2 + 0) * kCo + 8 * cc + k] = s1[k];
+    red[(prow * 2 + 1) * kCo + 8 * cc + k] = s2[k];
+  }
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) redc[((wave * 2 + h) * 4 + kk) * 32 + r] = ca[kk];
+  __syncthreads();
+  if (tid < 2 * kCo) {
+    const int st = tid / kCo, c = tid % kCo;
+    float s = 0.f;
+    for (int k = 0; k < kCh; ++k) s += red[(k * 2 + st) * kCo + c];
+    pw[2 * kCo * kKP + kKP + st * kCo + c] = s;
+  } else if (tid < 2 * kCo + kKP) {
+    const int kc = tid - 2 * kCo;
+    const int ky = kc >> 5, rr = kc & 31;
+    const int w0 = ky < 4 ? 0 : 4, kk = ky - w0;
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) s += redc[(((w0 + m) * 2 + hh) * 4 + kk) * 32 + rr];
+    pw[2 * kCo * kKP + kc] = s;
+  }
+}
+
+// fold the [nb][kPartW] partials (fp64, fixed order; 4 in flight per thread)
+__global__ __launch_bounds__(256) void stem_wgrad_fold_kernel(const float* __restrict__ part, int nb,
+                                                             double* __restrict__ tot) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= kPartW) return;
+  double S = 0.0;
+  int b = 0;
+  for (; b + 3 < nb; b += 4) {
+    const float v0 = part[static_cast<int64_t>(b) * kPartW + e];
+    const float v1 = part[static_cast<int64_t>(b + 1) * kPartW + e];
+    const float v2 = part[static_cast<int64_t>(b + 2) * kPartW + e];
+    const float v3 = part[static_cast<int64_t>(b + 3) * kPartW + e];
+    S += v0;
+    S += v1;
+    S += v2;
+    S += v3;
+  }
+  for (; b < nb; ++b) S += part[static_cast<int64_t>(b) * kPartW + e];
+  tot[e] = S;
+}
+
+// dW[co][c][ky][kx] = gamma invstd (G - s1/M colA - s2/M X); dgamma = s2, dbeta = s1 (fp32)
+__global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __restrict__ tot,
+                                                              const uint16_t* __restrict__ gamma,
+                                                              const float* __restrict__ invstd,
+                                                              double M, int C,
+                                                              float* __restrict__ dw,
+                                                              float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const double* G = tot;
+  const double* X = tot + kCo * kKP;
+  const double* A = tot + 2 * kCo * kKP;
+  const double* S1 = A + kKP;
+  const double* S2 = S1 + kCo;
+  if (e < kCo * C * 49) {
+    const int co = e / (C * 49);
+    const int rem = e - co * C * 49;
+    const int c = rem / 49, t = rem - (rem / 49) * 49;
+    const int ky = t / 7, kx = t - ky * 7;
+    const int kc = (ky * 8 + kx) * 4 + c;
+    const double a = static_cast<double>(bf2f(gamma[co])) * invstd[co];
+    const double v = a * (G[co * kKP + kc] - S1[co] / M * A[kc] - S2[co] / M * X[co * kKP + kc]);
+    dw[e] = static_cast<float>(v);
+  }
+  if (e < kCo) {
+    dgamma[e] = static_cast<float>(S2[e]);
+    dbeta[e] = static_cast<float>(S1[e]);
+  }
+}
+
+size_t fwd_lds(int OW) {   // input tile; the final reduction reuses it
+  const size_t need = static_cast<size_t>(tile_rows(kTY)) * tile_cols(OW) * 8;
+  const size_t red = static_cast<size_t>(kFT / 64) * 2 * 2 * kCo * sizeof(float);
+  return need > red ? need : red;
+}
+size_t bwd_lds(int OW) {   // chunk images + input tile; the final reduction reuses it
+  const size_t need = 2 * kCh * 128 + static_cast<size_t>(tile_rows(kTYB)) * tile_cols(OW) * 8;
+  const size_t red = (static_cast<size_t>(kCh) * 2 * kCo + 8 * 2 * 4 * 32) * sizeof(float);
+  return need > red ? need : red;
+}
+
+int persistent_grid(const void* fn, int threads, size_t lds, int ntiles) {
+  int dev = 0, cus = 256, occ = 1;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, lds) != hipSuccess || occ < 1) occ = 1;
+  const int g = cus * occ;
+  return g < ntiles ? g : ntiles;
+}
+
+// the backward tile needs > 64 KiB of dynamic LDS: opt in once per kernel instance
+void wgrad_lds_optin() {
+  static const bool done = [] {
+    const void* fns[3] = {reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, false>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false>)};
+    for (const void* f : fns)
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+    return true;
+  }();
+  (void)done;
+}
+
+}  // namespace
+
+int stem_fwd_grid(int N, int OH, int OW, int C) {
+  const int ntiles = N * ((OH + kTY - 1) / kTY);
+  const void* fn = C == 4 ? reinterpret_cast<const void*>(&stem_conv_fwd_kernel<4, false>)
+                          : reinterpret_cast<const void*>(&stem_conv_fwd_kernel<3, true>);
+  return persistent_grid(fn, kFT, fwd_lds(OW), ntiles);
+}
+
+int stem_bwd_grid(int N, int OH, int OW, int C) {
+  wgrad_lds_optin();
+  const int ntiles = N * ((OH + kTYB - 1) / kTYB);
+  const void* fn = C == 4 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false>)
+                          : reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true>);
+  return persistent_grid(fn, kBT, bwd_lds(OW), ntiles);
+}
+
+size_t stem_wgrad_part_floats() { return kPartW; }
+
+hipError_t launch_stem_conv_fwd(const void* x, const void* wpk, void* z, float* part, int grid,
+                                float* mean, float* invstd, float* rmean, float* rvar, float eps,
+                                float momentum, int N, int H, int W, int C, int OH, int OW,
+                                hipStream_t st) {
+  if ((C != 3 && C != 4) || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1 || N < 1 || grid < 1)
+    return hipErrorInvalidValue;
+  if (fwd_lds(OW) > 64 * 1024 || OH * OW >= (1 << 20)) return hipErrorInvalidValue;
+  const size_t lds = fwd_lds(OW);
+  const auto* xp = reinterpret_cast<const uint16_t*>(x);
+  const auto* wp = reinterpret_cast<const uint16_t*>(wpk);
+  auto* zp = reinterpret_cast<uint16_t*>(z);
+  const bool vec = C == 3 && W % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
+  if (C == 4) stem_conv_fwd_kernel<4, false><<<grid, kFT, lds, st>>>(xp, wp, zp, part, N, H, W, OH, OW);
+  else if (vec) stem_conv_fwd_kernel<3, true><<<grid, kFT, lds, st>>>(xp, wp, zp, part, N, H, W, OH, OW);
+  else stem_conv_fwd_kernel<3, false><<<grid, kFT, lds, st>>>(xp, wp, zp, part, N, H, W, OH, OW);
+  if (mean != nullptr)
+    stem_stats_finalize_kernel<<<1, 1024, 0, st>>>(part, grid, static_cast<double>(N) * OH * OW,
+                                                   eps, momentum, mean, invstd, rmean, rvar);
+  return hipGetLastError();
+}
+
+hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const float* mean,
+                             const float* invstd, const void* gamma, float* part, int grid,
+                             double* tot, float* dw, float* dgamma, float* dbeta, int N, int H,
+                             int W, int C, int OH, int OW, hipStream_t st) {
+  if ((C != 3 && C != 4) || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1 || N < 1 || grid < 1)
+    return hipErrorInvalidValue;
+  if (bwd_lds(OW) > 120 * 1024 || OH * OW >= (1 << 20)) return hipErrorInvalidValue;
+  const size_t lds = bwd_lds(OW);
+  wgrad_lds_optin();
+  const auto* gp = reinterpret_cast<const uint16_t*>(g);
+  const auto* zp = reinterpret_cast<const uint16_t*>(z);
+  const auto* xp = reinterpret_cast<const uint16_t*>(x);
+  const bool vec = C == 3 && W % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
+  if (C == 4) stem_wgrad_kernel<4, false><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, part, N, H, W, OH, OW);
+  else if (vec) stem_wgrad_kernel<3, true><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, part, N, H, W, OH, OW);
+  else stem_wgrad_kernel<3, false><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, part, N, H, W, OH, OW);
+  stem_wgrad_fold_kernel<<<(kPartW + 255) / 256, 256, 0, st>>>(part, grid, tot);
+  stem_wgrad_final_kernel<<<(kCo * C * 49 + 255) / 256, 256, 0, st>>>(
+      tot, reinterpret_cast<const uint16_t*>(gamma), invstd, static_cast<double>(N) * OH * OW, C,
+      dw, dgamma, dbeta);
+  return hipGetLastError();
+}
+
+}  // namespace cml

@@ -1,0 +1,146 @@
+"""ResNet stem on the HIP kernels of csrc/kernels/stem_conv.hip (MFMA conv with the BN statistics in
+its epilogue; one-pass weight gradient through BN + ReLU + max-pool) vs an fp32 PyTorch reference,
+with the library path (bf16 conv + fused BN-pool) as the yardstick for bf16 error."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from consensusml_amd.ops.bn import BatchNormAct2d
+from consensusml_amd.ops.pool import bn_relu_max_pool2d
+from consensusml_amd.ops.stem import pack_stem_weight, stem_conv_bn_relu_pool, stem_ok
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(p, q):
+    return ((p.float() - q.float()).norm() / q.float().norm().clamp_min(1e-6)).item()
+
+
+@pytest.mark.parametrize("N,C,H,W", [(4, 3, 64, 64), (3, 3, 50, 46), (2, 4, 40, 40),
+                                     (600, 3, 16, 16)])
+def test_stem_fused_vs_fp32(cuda, N, C, H, W):
+    torch.manual_seed(N * 100 + H)
+    x = torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w0 = (torch.randn(64, C, 7, 7, device=cuda) * 0.1).to(torch.bfloat16)
+    gam = torch.empty(64, device=cuda).uniform_(-0.5, 1.5)
+    bet = torch.empty(64, device=cuda).uniform_(-0.5, 0.5)
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    PH, PW = (OH - 1) // 2 + 1, (OW - 1) // 2 + 1
+    dy = torch.randn(N, 64, PH, PW, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    res = []
+    for fused in (True, False):
+        conv = nn.Conv2d(C, 64, 7, 2, 3, bias=False).to(cuda, torch.bfloat16)
+        bn = BatchNormAct2d(64, relu=True).to(cuda, torch.bfloat16)
+        with torch.no_grad():
+            conv.weight.copy_(w0)
+            bn.weight.copy_(gam)
+            bn.bias.copy_(bet)
+        if fused:
+            assert stem_ok(x, conv, bn)
+            y = stem_conv_bn_relu_pool(x, conv, bn)
+        else:
+            y = bn_relu_max_pool2d(conv(x), bn)
+        y.backward(dy)
+        bn.eval()
+        with torch.no_grad():
+            ye = stem_conv_bn_relu_pool(x, conv, bn) if fused else bn_relu_max_pool2d(conv(x), bn)
+        res.append([y, conv.weight.grad, bn.weight.grad, bn.bias.grad, bn.running_mean,
+                    bn.running_var, ye])
+    wr = w0.float().requires_grad_(True)
+    gr, br = gam.clone().to(torch.bfloat16).float().requires_grad_(True), \
+        bet.clone().to(torch.bfloat16).float().requires_grad_(True)
+    rm, rv = torch.zeros(64, device=cuda), torch.ones(64, device=cuda)
+    zr = F.conv2d(x.float(), wr, stride=2, padding=3)
+    yr = F.max_pool2d(torch.relu(F.batch_norm(zr, rm, rv, gr, br, True, 0.1, 1e-5)), 3, 2, 1)
+    yr.backward(dy.float())
+    with torch.no_grad():
+        yre = F.max_pool2d(torch.relu(F.batch_norm(F.conv2d(x.float(), w0.float(), stride=2,
+                                                            padding=3),
+                                                   rm, rv, gr, br, False, 0.1, 1e-5)), 3, 2, 1)
+    ref = [yr, wr.grad, gr.grad, br.grad, rm, rv, yre]
+    names = ["y", "dW", "dgamma", "dbeta", "running_mean", "running_var", "y_eval"]
+    for name, f, u, r in zip(names, res[0], res[1], ref):
+        ef, eu = _rel(f, r), _rel(u, r)
+        # the floor covers ReLU-mask / argmax flips of near-tie windows (a few per channel at
+        # these sizes); the kernels themselves are checked exactly in test_stem_kernels_exact
+        assert ef <= max(2 * eu, 0.05), (name, ef, eu)
+
+
+def test_stem_pack_layout(cuda):
+    w = torch.arange(64 * 3 * 49, dtype=torch.float32).reshape(64, 3, 7, 7)
+    p = pack_stem_weight(w.to(torch.bfloat16)).float().view(64, 7, 8, 4)
+    assert torch.equal(p[:, :, :7, :3], w.to(torch.bfloat16).float().permute(0, 2, 3, 1))
+    assert p[:, :, 7].abs().sum() == 0 and p[..., 3].abs().sum() == 0
+
+
+def test_stem_model_path_matches_unfused(cuda):
+    """ResNet-50 forward/backward with the fused stem vs the library stem, both against the same
+    model in fp32: the stem weight gradient sits under 50 bf16 layers, so the yardstick is the
+    library path's own distance to fp32."""
+    import copy
+
+    import consensusml_amd.models.resnet as R
+    torch.manual_seed(0)
+    m32 = R.resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    m = copy.deepcopy(m32).to(torch.bfloat16)
+    x = torch.randn(8, 3, 96, 96, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device=cuda)
+    loss32 = F.cross_entropy(m32(x.float()), y)
+    loss32.backward()
+    g32 = m32.conv1.weight.grad.float()
+    out = {}
+    for fused in (True, False):
+        R.FUSE_STEM_CONV = fused
+        try:
+            m.zero_grad(set_to_none=True)
+            loss = F.cross_entropy(m(x).float(), y)
+            loss.backward()
+            out[fused] = (loss.item(), m.conv1.weight.grad.float().clone())
+        finally:
+            R.FUSE_STEM_CONV = True
+    assert abs(out[True][0] - loss32.item()) < 0.05 * max(1.0, abs(loss32.item()))
+    ef, eu = _rel(out[True][1], g32), _rel(out[False][1], g32)
+    assert ef <= max(1.5 * eu, 0.1), (ef, eu)
+
+
+@pytest.mark.parametrize("N,C,H,W", [(4, 3, 64, 64), (3, 4, 50, 46)])
+def test_stem_kernels_exact(cuda, N, C, H, W):
+    """Each kernel against a float64 evaluation on ITS OWN inputs (no bf16 re-rounding noise)."""
+    from consensusml_amd.ops.native import lib
+    torch.manual_seed(1)
+    x = torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(64, C, 7, 7, device=cuda) * 0.1).to(torch.bfloat16)
+    gam = torch.empty(64, device=cuda).uniform_(-0.5, 1.5).to(torch.bfloat16)
+    bet = torch.empty(64, device=cuda).uniform_(-0.5, 0.5).to(torch.bfloat16)
+    z, mean, invstd = lib().stem_conv_fwd(x, pack_stem_weight(w), None, None, 1e-5, 0.1, True)
+    zr = F.conv2d(x.double(), w.double(), stride=2, padding=3)
+    assert _rel(z.double(), zr) < 4e-3                       # bf16 output rounding
+    mr, vr = zr.mean((0, 2, 3)), zr.var((0, 2, 3), unbiased=False)
+    assert (mean.double() - mr).abs().max().item() < 1e-5 * max(1.0, mr.abs().max().item())
+    assert ((invstd.double() * (vr + 1e-5).sqrt()) - 1).abs().max().item() < 1e-5
+    y, idx, _, _ = lib().bn_relu_maxpool_fwd(z, gam, bet, None, None, mean, invstd, 1e-5, 0.1,
+                                             False, 3, 2, 1)
+    dy = torch.randn_like(y)
+    g = lib().maxpool_bwd(dy, idx, z.shape[2], z.shape[3], 3, 2, 1)
+    sc = (invstd.double() * gam.double()).view(1, -1, 1, 1)
+    u = (z.double() - mean.double().view(1, -1, 1, 1)) * sc + bet.double().view(1, -1, 1, 1)
+    ud = u.requires_grad_(True)
+    F.max_pool2d(torch.relu(ud), 3, 2, 1).backward(dy.double())
+    assert _rel(g.double(), ud.grad) < 4e-3                  # bf16 output rounding
+    dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gam)
+    gd = g.double()
+    xh = (z.double() - mean.double().view(1, -1, 1, 1)) * invstd.double().view(1, -1, 1, 1)
+    s1, s2 = gd.sum((0, 2, 3)), (gd * xh).sum((0, 2, 3))
+    assert _rel(db.double(), s1) < 1e-5
+    assert _rel(dg.double(), s2) < 1e-5
+    M = gd.numel() / 64
+    dz = (gam.double() * invstd.double()).view(1, -1, 1, 1) * (
+        gd - s1.view(1, -1, 1, 1) / M - xh * (s2.view(1, -1, 1, 1) / M))
+    wq = w.double().requires_grad_(True)
+    F.conv2d(x.double(), wq, stride=2, padding=3).backward(dz)
+    assert _rel(dw.double(), wq.grad) < 2e-3                 # xhat staged as bf16
