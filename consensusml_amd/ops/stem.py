@@ -4,9 +4,9 @@
 forward : MFMA implicit-GEMM conv that also accumulates the BN statistics (no statistics pass,
           no channel-padding pass for 3-channel images), then the pool that applies BN + ReLU to
           every window tap (the BN output is never stored).
-backward: the pool gather (already ReLU-masked), then ONE MFMA pass that produces the conv weight
-          gradient through the BatchNorm plus dgamma / dbeta: the BN input gradient is never formed
-          (see the kernel header for the algebra).
+backward: the pool gather (already ReLU-masked, with its channel sums = dbeta), then ONE MFMA pass
+          that produces the conv weight gradient through the BatchNorm plus dgamma: the BN input
+          gradient is never formed (see the kernel header for the algebra).
 
 Other inputs (CPU, fp32, other stem shapes, images that need an input gradient, eval-mode
 backward) take the module path.
@@ -44,8 +44,8 @@ class _StemFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, z, idx, gamma, mean, invstd = ctx.saved_tensors
-        g = lib().maxpool_bwd(dy, idx, z.shape[2], z.shape[3], 3, 2, 1)
-        dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gamma)
+        g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3])
+        dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gamma, gsum)
         wt, gt, bt = ctx.dtypes
         return None, dw.to(wt), dg.to(gt), db.to(bt), None, None, None, None, None
 

@@ -418,10 +418,12 @@ std::vector<Tensor> stem_conv_fwd(const Tensor& x, const Tensor& wpk, const opti
   return {z, mean, invstd};
 }
 
-// Stem backward through BN: g = ReLU-masked pool gradient (NHWC [N, 64, OH, OW]), z = conv output,
-// x = conv input. Returns {dw [64, C, 7, 7] fp32, dgamma fp32 [64], dbeta fp32 [64]}.
+// Stem backward through BN: g = ReLU-masked pool gradient (NHWC [N, 64, OH, OW]) with its channel
+// sums gsum (maxpool_bwd_sum), z = conv output, x = conv input.
+// Returns {dw [64, C, 7, 7] fp32, dgamma fp32 [64], dbeta fp32 [64]}.
 std::vector<Tensor> stem_wgrad(const Tensor& g_in, const Tensor& z, const Tensor& x,
-                               const Tensor& mean, const Tensor& invstd, const Tensor& gamma) {
+                               const Tensor& mean, const Tensor& invstd, const Tensor& gamma,
+                               const Tensor& gsum) {
   check_nhwc(x, "x");
   check_nhwc(z, "z");
   Tensor g = g_in.contiguous(at::MemoryFormat::ChannelsLast);
@@ -436,6 +438,8 @@ std::vector<Tensor> stem_wgrad(const Tensor& g_in, const Tensor& z, const Tensor
                   invstd.is_contiguous(), "stem_wgrad: fp32 mean / invstd [64]");
   TORCH_CHECK(gamma.scalar_type() == at::kBFloat16 && gamma.is_contiguous() && gamma.numel() == 64,
               "stem_wgrad: bf16 gamma [64]");
+  TORCH_CHECK(gsum.scalar_type() == at::kFloat && gsum.is_contiguous() && gsum.numel() == 64 &&
+                  gsum.device() == x.device(), "stem_wgrad: fp32 channel sums of g [64]");
   const c10::DeviceGuard guard(x.device());
   auto f32 = x.options().dtype(at::kFloat);
   const int grid = cml::stem_bwd_grid(N, OH, OW, C);
@@ -446,7 +450,8 @@ std::vector<Tensor> stem_wgrad(const Tensor& g_in, const Tensor& z, const Tensor
   Tensor dg = at::empty({64}, f32), db = at::empty({64}, f32);
   CML_CHECK_HIP(cml::launch_stem_wgrad(g.data_ptr(), z.data_ptr(), x.data_ptr(),
                                        mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                                       gamma.data_ptr(), part.data_ptr<float>(), grid,
+                                       gamma.data_ptr(), gsum.data_ptr<float>(),
+                                       part.data_ptr<float>(), grid,
                                        tot.data_ptr<double>(), dw.data_ptr<float>(),
                                        dg.data_ptr<float>(), db.data_ptr<float>(), N, H, W, C, OH,
                                        OW, cur_stream()));
@@ -463,6 +468,24 @@ Tensor maxpool_bwd(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W,
   CML_CHECK_HIP(cml::launch_maxpool_bwd(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(), N, H, W, C,
                                         OH, OW, k, s, p, cur_stream()));
   return dx;
+}
+
+// 3x3/s2/p1 max-pool backward + per-channel sums of the result: {dx, sums fp32 [C]}.
+std::vector<Tensor> maxpool_bwd_sum(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W) {
+  Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(dy, "dy");
+  const int64_t N = dy.size(0), C = dy.size(1), OH = dy.size(2), OW = dy.size(3);
+  TORCH_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "maxpool_bwd_sum: 3x3/s2/p1 shapes");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == dy.numel(), "maxpool_bwd_sum: idx");
+  const c10::DeviceGuard guard(dy.device());
+  Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor sums = at::empty({C}, dy.options().dtype(at::kFloat));
+  const size_t wb = cml::maxpool_bwd_sum_workspace_bytes(N, H, W, C);
+  Tensor work = at::empty({static_cast<int64_t>(wb / 4 + 1)}, dy.options().dtype(at::kFloat));
+  CML_CHECK_HIP(cml::launch_maxpool_bwd_sum(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(),
+                                            sums.data_ptr<float>(), work.data_ptr(), N, H, W, C,
+                                            OH, OW, cur_stream()));
+  return {dx, sums};
 }
 
 // dsts[i].copy_(srcs[i]) for same-dtype, same-numel contiguous 16-B aligned tensors, in launches of
@@ -864,6 +887,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_wgrad", &stem_wgrad, "ResNet stem weight gradient through BN (MFMA, one pass)");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
+  m.def("maxpool_bwd_sum", &maxpool_bwd_sum, "3x3/s2 max-pool backward + channel sums of dx");
   m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");
   m.def("pad_c4", &pad_c4, "NHWC bf16 channel zero-padding to 4");
   m.def("ce_fwd", &ce_fwd, "fused cross-entropy forward over bf16 logits (lse, per-row loss)");

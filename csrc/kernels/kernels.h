@@ -126,6 +126,12 @@ struct MultiCopyArgs {
 };
 hipError_t launch_multi_copy(const MultiCopyArgs& args, hipStream_t stream);
 
+// 3x3/s2/p1 max-pool backward that also returns the channel sums of dx (fp32 [C]; the stem BN's
+// dbeta). work: maxpool_bwd_sum_workspace_bytes.
+size_t maxpool_bwd_sum_workspace_bytes(int N, int H, int W, int C);
+hipError_t launch_maxpool_bwd_sum(const void* dy, const void* idx, void* dx, float* sums,
+                                  void* work, int N, int H, int W, int C, int OH, int OW,
+                                  hipStream_t stream);
 // Stem: y = maxpool(relu(bn(x))) with the BN affine (training statistics from launch_bn_stats,
 // or running statistics) applied to every window tap; idx as launch_maxpool_fwd.
 hipError_t launch_bn_stats(const void* x, int64_t M, int C, float* mean, float* invstd,
@@ -210,8 +216,9 @@ hipError_t launch_colsum(const void* x, int64_t M, int N, void* out, void* work,
 // Forward: z = conv(x, wpk) with wpk the packed weights [64][224] (k = (ky*8 + kx)*4 + c, zero for
 // kx = 7 / c >= C_in); part [grid][2][64] receives per-workgroup channel sums and sums of squares
 // and, when mean != nullptr, mean / invstd (and running stats) are finalized from them.
-// Backward: from g (ReLU-masked max-pool gradient), z, x and the forward mean / invstd, the weight
-// gradient of the conv THROUGH the BatchNorm (dw [64][C][7][7] fp32) and dgamma / dbeta (fp32);
+// Backward: from g (ReLU-masked max-pool gradient) and its channel sums gsum, z, x and the forward
+// mean / invstd, the weight gradient of the conv THROUGH the BatchNorm (dw [64][C][7][7] fp32) and
+// dgamma / dbeta (fp32);
 // part: grid x stem_wgrad_part_floats() floats, tot: stem_wgrad_part_floats() doubles.
 int stem_fwd_grid(int N, int OH, int OW, int C);
 int stem_bwd_grid(int N, int OH, int OW, int C);
@@ -221,7 +228,8 @@ hipError_t launch_stem_conv_fwd(const void* x, const void* wpk, void* z, float* 
                                 float momentum, int N, int H, int W, int C, int OH, int OW,
                                 hipStream_t stream);
 hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const float* mean,
-                             const float* invstd, const void* gamma, float* part, int grid,
+                             const float* invstd, const void* gamma, const float* gsum,
+                             float* part, int grid,
                              double* tot, float* dw, float* dgamma, float* dbeta, int N, int H,
                              int W, int C, int OH, int OW, hipStream_t stream);
 

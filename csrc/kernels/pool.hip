@@ -190,17 +190,21 @@ __global__ __launch_bounds__(kPB) void maxpool_bwd_kernel(const bf16* __restrict
 // {j, j+1} x {i, i+1} can cover that block, so each window's (argmax, dy) is read once per 4
 // pixels instead of once per pixel: the generic gather above moves ~6 bytes through L2 per byte of
 // dx it writes, this one ~1.5.
+// part (optional): per-workgroup channel sums of dx, [gridDim.y * gridDim.x][C] (the stem's
+// BatchNorm dbeta, so its backward needs no separate reduction pass).
 __global__ __launch_bounds__(kPB) void maxpool_bwd_k3s2_kernel(const bf16* __restrict__ dy,
                                                               const uint8_t* __restrict__ idx,
                                                               bf16* __restrict__ dx, int N, int H,
-                                                              int W, int C, int OH, int OW) {
+                                                              int W, int C, int OH, int OW,
+                                                              float* __restrict__ part) {
   const int cg = C / 8;
   const int HB = (H + 1) / 2, WB = (W + 1) / 2;
   const int t = blockIdx.x * kPB + threadIdx.x;
-  if (t >= WB * cg) return;
-  const int i = t / cg;
-  const int g = t - i * cg;
-  for (int band = blockIdx.y; band < N * HB; band += gridDim.y) {
+  const bool active = t < WB * cg;
+  const int i = active ? t / cg : 0;
+  const int g = t - (t / cg) * cg;
+  float tsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int band = active ? blockIdx.y : N * HB; band < N * HB; band += gridDim.y) {
     const int n = band / HB;
     const int j = band - n * HB;
     uint2 m[2][2];
@@ -241,8 +245,80 @@ __global__ __launch_bounds__(kPB) void maxpool_bwd_k3s2_kernel(const bf16* __res
             }
           }
         store_bf16<8>(dx + ((static_cast<int64_t>(n) * H + h) * W + w) * C + 8 * g, acc);
+        if (part) {
+#pragma unroll
+          for (int v = 0; v < 8; ++v) tsum[v] += acc[v];
+        }
       }
     }
+  }
+  if (part == nullptr) return;
+  // fixed-order workgroup reduction: channel group g's threads are t = g, g + cg, ...
+  __shared__ float red[kPB][9];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) red[threadIdx.x][v] = tsum[v];
+  __syncthreads();
+  float* pb = part + (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * C;
+  for (int c = threadIdx.x; c < C; c += kPB) {
+    const int gc = c >> 3, v = c & 7;
+    // thread-index offset of this block's first thread with channel group gc
+    const int first = (gc - (blockIdx.x * kPB) % cg + cg) % cg;
+    float acc = 0.f;
+    for (int k = first; k < kPB; k += cg) acc += red[k][v];
+    pb[c] = acc;
+  }
+}
+
+// first fold level: workgroup b sums rows [b nb / G, (b + 1) nb / G) of [nb][C] into out[b][C]
+// (kPB / C slices per channel, fixed order)
+__global__ __launch_bounds__(kPB) void colsum_fold_rows_kernel(const float* __restrict__ part,
+                                                               int nb, int C,
+                                                               float* __restrict__ out) {
+  __shared__ float ls[kPB];
+  const int G = gridDim.x;
+  const int lo = static_cast<int>(static_cast<int64_t>(blockIdx.x) * nb / G);
+  const int hi = static_cast<int>(static_cast<int64_t>(blockIdx.x + 1) * nb / G);
+  const int nsl = kPB / C;
+  const int c = threadIdx.x % C, sl = threadIdx.x / C;
+  float acc = 0.f;
+  if (sl < nsl) {
+    int b = lo + sl;
+    for (; b + 3 * nsl < hi; b += 4 * nsl) {
+      const float v0 = part[static_cast<int64_t>(b) * C + c];
+      const float v1 = part[static_cast<int64_t>(b + nsl) * C + c];
+      const float v2 = part[static_cast<int64_t>(b + 2 * nsl) * C + c];
+      const float v3 = part[static_cast<int64_t>(b + 3 * nsl) * C + c];
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
+    }
+    for (; b < hi; b += nsl) acc += part[static_cast<int64_t>(b) * C + c];
+  }
+  ls[threadIdx.x] = acc;
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < C; cc += kPB) {
+    float s = 0.f;
+    for (int k = 0; k < nsl; ++k) s += ls[k * C + cc];
+    out[static_cast<int64_t>(blockIdx.x) * C + cc] = s;
+  }
+}
+
+// out[c] = sum over nb partial rows [nb][C] (fp64, 1024 threads = slices x channels, fixed order)
+__global__ __launch_bounds__(1024) void colsum_fold_kernel(const float* __restrict__ part, int nb,
+                                                           int C, float* __restrict__ out) {
+  __shared__ double ls[1024];
+  const int nsl = 1024 / C;
+  const int c = threadIdx.x % C, sl = threadIdx.x / C;
+  double acc = 0.0;
+  if (sl < nsl)
+    for (int b = sl; b < nb; b += nsl) acc += part[static_cast<int64_t>(b) * C + c];
+  ls[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x < C) {
+    double s = 0.0;
+    for (int k = 0; k < nsl; ++k) s += ls[k * C + threadIdx.x];
+    out[threadIdx.x] = static_cast<float>(s);
   }
 }
 
@@ -301,7 +377,7 @@ hipError_t launch_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, 
   if (k == 3 && s == 2 && p == 1) {
     maxpool_bwd_k3s2_kernel<<<pgrid(((W + 1) / 2) * (C / 8), N * ((H + 1) / 2)), kPB, 0, st>>>(
         reinterpret_cast<const bf16*>(dy), reinterpret_cast<const uint8_t*>(idx),
-        reinterpret_cast<bf16*>(dx), N, H, W, C, OH, OW);
+        reinterpret_cast<bf16*>(dx), N, H, W, C, OH, OW, nullptr);
     return hipGetLastError();
   }
   const int ks = (k + s - 1) / s;
@@ -324,6 +400,35 @@ hipError_t launch_pad_c4(const void* x, void* y, int64_t npix, int C, hipStream_
   if (b > 16384) b = 16384;
   pad_c4_kernel<<<static_cast<unsigned>(b), 256, 0, st>>>(reinterpret_cast<const uint16_t*>(x),
                                                           reinterpret_cast<uint2*>(y), npix, C);
+  return hipGetLastError();
+}
+
+// grid.y of the summing backward: one band per workgroup row like the plain kernel (a capped grid
+// that loops over bands is latency-bound: +35 % time), the partial rows folded in two levels
+constexpr int kSumRows = 65535;
+constexpr int kFold1 = 256;
+
+size_t maxpool_bwd_sum_workspace_bytes(int N, int H, int W, int C) {
+  const int gx = ((((W + 1) / 2) * (C / 8)) + kPB - 1) / kPB;
+  const int rows = N * ((H + 1) / 2);
+  const int gy = rows < kSumRows ? rows : kSumRows;
+  return (static_cast<size_t>(gx) * gy + kFold1) * C * sizeof(float);
+}
+
+hipError_t launch_maxpool_bwd_sum(const void* dy, const void* idx, void* dx, float* sums,
+                                  void* work, int N, int H, int W, int C, int OH, int OW,
+                                  hipStream_t st) {
+  if (C % 8 || C > kPB || kPB % C || N * H < 1) return hipErrorInvalidValue;
+  const int gx = ((((W + 1) / 2) * (C / 8)) + kPB - 1) / kPB;
+  const int rows = N * ((H + 1) / 2);
+  const int gy = rows < kSumRows ? rows : kSumRows;
+  float* part = reinterpret_cast<float*>(work);
+  maxpool_bwd_k3s2_kernel<<<dim3(gx, gy), kPB, 0, st>>>(
+      reinterpret_cast<const bf16*>(dy), reinterpret_cast<const uint8_t*>(idx),
+      reinterpret_cast<bf16*>(dx), N, H, W, C, OH, OW, part);
+  float* part2 = part + static_cast<int64_t>(gx) * gy * C;
+  colsum_fold_rows_kernel<<<kFold1, kPB, 0, st>>>(part, gx * gy, C, part2);
+  colsum_fold_kernel<<<1, 1024, 0, st>>>(part2, kFold1, C, sums);
   return hipGetLastError();
 }
 

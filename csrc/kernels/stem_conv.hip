@@ -15,18 +15,20 @@
 //          marks windows whose max is <= 0 with argmax 255, so they route no gradient).
 //          With xhat = (z - mean) invstd the BN backward is
 //            dz = gamma invstd (g - mean(g) - xhat mean(g xhat)),
-//          and dW = sum_p dz[p] (x) im2col[p] is linear in dz, so the kernel accumulates
-//            G = sum_p g (x) im2col,  X = sum_p xhat (x) im2col,  colA = sum_p im2col,
-//            s1 = sum_p g,  s2 = sum_p g xhat
-//          and stem_wgrad_finalize forms dW = gamma invstd (G - s1/M colA - s2/M X),
-//          dgamma = s2, dbeta = s1. dz never exists: the BN backward reduce and apply passes
+//          and dW = sum_p dz[p] (x) im2col[p] is linear in dz. mean(g) comes with g (the pool
+//          backward sums its output per channel), so the kernel stages g - mean(g) and accumulates
+//            G = sum_p (g - mean(g)) (x) im2col,  X = sum_p xhat (x) im2col,  s2 = sum_p g xhat
+//          and stem_wgrad_finalize forms dW = gamma invstd (G - s2/M X), dgamma = s2,
+//          dbeta = sum_p g. dz never exists: the BN backward reduce and apply passes
 //          (2.5 GB of traffic at batch 512) and the library weight-gradient kernel become this
 //          one pass. The products sum over pixels, so both MFMA operands come out of LDS through
 //          ds_read_b64_tr_b16 (the gfx950 transpose read): the g / xhat chunk is stored
 //          [pixel][channel] as loaded and the input tile is the same one the forward uses; no
-//          im2col or transposed copy is materialised anywhere. One wave per kernel row ky
-//          (7 waves) owns the five 32 x 32 accumulators (g, xhat) x (channel blocks 0, 1) + ones.
+//          im2col or transposed copy is materialised anywhere. 8 waves: (g, xhat) x (channel
+//          blocks 0, 1) x (kernel rows 0-3 | 4-6), 7 accumulators per SIMD.
 #include <math.h>
+
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -46,8 +48,8 @@ constexpr int kTY = 8;                  // forward: output rows per tile
 constexpr int kTYB = 16;                // backward: output rows per tile (fewer tile-load bubbles)
 constexpr int kFT = 256;                // forward workgroup: 4 waves
 constexpr int kBT = 512;                // backward workgroup: 8 waves
-constexpr int kCh = 64;                 // backward pixel chunk (4 MFMA k-steps)
-constexpr int kPartW = 2 * kCo * kKP + kKP + 2 * kCo;   // floats per backward partial
+constexpr int kCh = 128;                // backward pixel chunk: 8 x 16 pixels, 8 MFMA k-steps
+constexpr int kPartW = 2 * kCo * kKP + kCo;   // floats per backward partial: G, X, s2
 
 __host__ __device__ constexpr int tile_cols(int OW) { return 2 * OW + 6; }   // ix = -3 .. 2 OW + 2
 __host__ __device__ constexpr int tile_rows(int TY) { return 2 * TY + 5; }
@@ -161,7 +163,8 @@ __global__ __launch_bounds__(kFT) void stem_conv_fwd_kernel(const uint16_t* __re
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint2* tile = reinterpret_cast<uint2*>(smem);
   const int WT = tile_cols(OW);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, h = lane >> 5;
   const float inv_ow = 1.f / static_cast<float>(OW);
   // B operand of step s, channel block b: lane (r, h) holds W[32 b + r][16 s + 8 h .. + 7]
@@ -196,19 +199,36 @@ __global__ __launch_bounds__(kFT) void stem_conv_fwd_kernel(const uint16_t* __re
         acc0 = mfma(a, wf[s][0], acc0);
         acc1 = mfma(a, wf[s][1], acc1);
       }
-      // register i: pixel 32 blk + (i & 3) + 8 (i >> 2) + 4 h, channel 32 b + r
+      // register i: pixel 32 blk + (i & 3) + 8 (i >> 2) + 4 h, channel 32 b + r. One cvt_pk per
+      // channel pair (r, r + 32) of a pixel, stored as its low and high halves.
+      uint16_t* zb = zt + static_cast<int64_t>(32 * blk + 4 * h) * kCo + r;
+      if (32 * (blk + 1) <= pv) {                      // whole block inside the band
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int pp = 32 * blk + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (pp < pv) {
+        for (int i = 0; i < 16; ++i) {
           const float v0 = acc0[i], v1 = acc1[i];
-          uint16_t* zo = zt + static_cast<int64_t>(pp) * kCo + r;
-          zo[0] = f2bf(v0);
-          zo[32] = f2bf(v1);
+          const uint32_t pk = static_cast<uint32_t>(f2bf(v0)) | (static_cast<uint32_t>(f2bf(v1)) << 16);
+          uint16_t* zo = zb + ((i & 3) + 8 * (i >> 2)) * kCo;
+          zo[0] = static_cast<uint16_t>(pk);
+          zo[32] = static_cast<uint16_t>(pk >> 16);
           s1[0] += v0;
           s2[0] = fmaf(v0, v0, s2[0]);
           s1[1] += v1;
           s2[1] = fmaf(v1, v1, s2[1]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int pp = 32 * blk + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (pp < pv) {
+            const float v0 = acc0[i], v1 = acc1[i];
+            uint16_t* zo = zb + ((i & 3) + 8 * (i >> 2)) * kCo;
+            zo[0] = f2bf(v0);
+            zo[32] = f2bf(v1);
+            s1[0] += v0;
+            s2[0] = fmaf(v0, v0, s2[0]);
+            s1[1] += v1;
+            s2[1] = fmaf(v1, v1, s2[1]);
+          }
         }
       }
     }
@@ -278,21 +298,26 @@ __device__ __forceinline__ int chunk_off(int rho, int ch) {
   return rho * 128 + ((ch ^ (((rho >> 1) & 1) << 2)) << 4);
 }
 
-template <int C, bool VEC>
+template <int C, bool VEC, int OWC>
 __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restrict__ g,
                                                         const uint16_t* __restrict__ z,
                                                         const uint16_t* __restrict__ x,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ invstd,
+                                                        const float* __restrict__ gsum,
                                                         float* __restrict__ part, int N, int H,
-                                                        int W, int OH, int OW) {
+                                                        int W, int OH, int OW_) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* gbuf = smem;                                   // [64 px][64 ch] bf16, swizzled
+  char* gbuf = smem;                                   // [128 px][64 ch] bf16, swizzled
   char* xbuf = smem + kCh * 128;
   uint2* tile = reinterpret_cast<uint2*>(smem + 2 * kCh * 128);
+  // OWC > 0: the width is a compile-time constant (the 224-px ResNet input) and every chunk is
+  // full, so the transposed reads of a chunk use one base address and immediate offsets
+  const int OW = OWC > 0 ? OWC : OW_;
   const int WT = tile_cols(OW);
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar: uniform branches below
   const int h = lane >> 5, r = lane & 31;
   const int gi = lane & 15, grp = lane >> 4;           // 16-lane group of the transposed reads
   const int q = gi >> 2, pq = gi & 3;
@@ -301,116 +326,147 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
   const int mb = wave & 3;
   const int ky0 = wave < 4 ? 0 : 4;
   const int nky = wave < 4 ? 4 : 3;
-  const char* abuf = mb < 2 ? gbuf : xbuf;
+  const char* abuf = (mb < 2 ? gbuf : xbuf) + 8 * (pq & 1);
   const int chn0 = 4 * (mb & 1) + 2 * (grp & 1) + (pq >> 1);
-  const float inv_ow = 1.f / static_cast<float>(OW);
-  // staging role: pixel tid >> 3 of the chunk, channels 8 cc .. 8 cc + 7
-  const int cc = tid & 7, prow = tid >> 3;
-  float mu[8], is[8], s1[8], s2[8];
+  // a chunk is an 8 x 16 block of output pixels, pixel rho = 16 row + col: the pixel rows of
+  // k-step ks's transposed reads, rho = 16 ks + 8 h + 4 e + q, are row ks, col 8 h + 4 e + q
+  const int cc = tid & 7, srho = tid >> 3;             // staging: pixels srho, srho + 64
+  float mu[8], is[8], mg[8], s2[8];
+  const float inv_m = 1.f / (static_cast<float>(N) * OH * OW);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    mu[k] = mean[8 * cc + k];
     is[k] = invstd[8 * cc + k];
-    s1[k] = 0.f;
+    mu[k] = -mean[8 * cc + k] * is[k];                 // xhat = z * is + mu
+    mg[k] = gsum[8 * cc + k] * inv_m;                  // mean(g)
     s2[k] = 0.f;
   }
   f32x16 acc[4] = {};
-  float ca[4] = {0.f, 0.f, 0.f, 0.f};                  // colA share: column (ky0 + kk) 32 + r
   const int bands = (OH + kTYB - 1) / kTYB;
   const int ntiles = N * bands;
-  auto band_pv = [&](int tl) {
-    const int n = tl / bands;
-    return min(kTYB, OH - (tl - n * bands) * kTYB) * OW;
-  };
-  auto band_base = [&](int tl) {
-    const int n = tl / bands;
-    return (static_cast<int64_t>(n) * OH + (tl - n * bands) * kTYB) * OW;
-  };
-  // one-chunk register prefetch of (g, z) across the flattened (tile, chunk) sequence
-  uint4 gv = make_uint4(0u, 0u, 0u, 0u), zv = gv;
-  bool okv = false;
+  const int ncx = (OW + 15) / 16;
+  const int nch = 2 * ncx;                             // chunks per tile (cy 0..1, cx)
+  // one-chunk register prefetch of (g, z) across the flattened (tile, chunk) sequence. Loads are
+  // unconditional (clamped address) and invalid pixels are zeroed at use: a branch around the
+  // loads makes the compiler wait for them at the join, i.e. no prefetch at all
+  uint4 gv[2], zv[2];
+  bool okv[2];
   auto fetch = [&](int tl, int ch) {
-    const int pp = kCh * ch + prow;
-    okv = tl < ntiles && pp < band_pv(tl);
-    if (okv) {
-      const int64_t o = (band_base(tl) + pp) * kCo + 8 * cc;
-      gv = *reinterpret_cast<const uint4*>(g + o);
-      zv = *reinterpret_cast<const uint4*>(z + o);
-    } else {
-      gv = make_uint4(0u, 0u, 0u, 0u);
-      zv = gv;
+    const int n = tl / bands;
+    const int oy0 = (tl - n * bands) * kTYB;
+    const int cy = ch >= ncx ? 1 : 0, cx = ch - cy * ncx;
+    const int oyend = min(OH, oy0 + kTYB);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rho = srho + 64 * j;
+      const int oy = oy0 + 8 * cy + (rho >> 4), ox = 16 * cx + (rho & 15);
+      okv[j] = tl < ntiles && oy < oyend && ox < OW;
+      const int pix = okv[j] ? (n * OH + oy) * OW + ox : 0;
+      const int64_t o = static_cast<int64_t>(pix) * kCo + 8 * cc;
+      gv[j] = *reinterpret_cast<const uint4*>(g + o);
+      zv[j] = *reinterpret_cast<const uint4*>(z + o);
     }
   };
   fetch(blockIdx.x, 0);
   for (int tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
     const int n = tl / bands;
     const int oy0 = (tl - n * bands) * kTYB;
-    const int pv = band_pv(tl);
-    const int nch = (pv + kCh - 1) / kCh;
+    const int rows = min(kTYB, OH - oy0);              // valid rows of the band
     for (int ch = 0; ch < nch; ++ch) {
+      const int cy = ch >= ncx ? 1 : 0, cx = ch - cy * ncx;
+      const int r0 = 8 * cy, c0 = 16 * cx;             // chunk origin inside the band
       __syncthreads();                                 // previous chunk's / tile's readers done
       if (ch == 0) stage_input<C, kTYB, VEC>(x, tile, n, oy0, H, W, WT, tid, kBT);
-      {
-        // ---- g / xhat of the prefetched pixel -> LDS; BN-backward sums
-        const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
-        const uint32_t zw[4] = {zv.x, zv.y, zv.z, zv.w};
-        uint32_t xw[4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        // ---- g / xhat of the prefetched pixels -> LDS; BN-backward sums
+        const bool ok = OWC > 0 || okv[j];             // fixed-width instance: always valid
+        const uint32_t gw[4] = {gv[j].x, gv[j].y, gv[j].z, gv[j].w};
+        const uint32_t zw[4] = {zv[j].x, zv[j].y, zv[j].z, zv[j].w};
+        uint32_t xw[4], cw[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float g0 = __uint_as_float(gw[k] << 16), g1 = __uint_as_float(gw[k] & 0xffff0000u);
-          float x0 = (__uint_as_float(zw[k] << 16) - mu[2 * k]) * is[2 * k];
-          float x1 = (__uint_as_float(zw[k] & 0xffff0000u) - mu[2 * k + 1]) * is[2 * k + 1];
-          x0 = okv ? x0 : 0.f;
-          x1 = okv ? x1 : 0.f;
-          s1[2 * k] += g0;
-          s1[2 * k + 1] += g1;
+          float x0 = fmaf(__uint_as_float(zw[k] << 16), is[2 * k], mu[2 * k]);
+          float x1 = fmaf(__uint_as_float(zw[k] & 0xffff0000u), is[2 * k + 1], mu[2 * k + 1]);
+          float c0 = g0 - mg[2 * k], c1 = g1 - mg[2 * k + 1];
+          x0 = ok ? x0 : 0.f;
+          x1 = ok ? x1 : 0.f;
+          c0 = ok ? c0 : 0.f;
+          c1 = ok ? c1 : 0.f;
           s2[2 * k] = fmaf(g0, x0, s2[2 * k]);
           s2[2 * k + 1] = fmaf(g1, x1, s2[2 * k + 1]);
           xw[k] = static_cast<uint32_t>(f2bf(x0)) | (static_cast<uint32_t>(f2bf(x1)) << 16);
+          cw[k] = static_cast<uint32_t>(f2bf(c0)) | (static_cast<uint32_t>(f2bf(c1)) << 16);
         }
-        *reinterpret_cast<uint4*>(gbuf + chunk_off(prow, cc)) = gv;
-        *reinterpret_cast<uint4*>(xbuf + chunk_off(prow, cc)) = make_uint4(xw[0], xw[1], xw[2], xw[3]);
+        const int rho = srho + 64 * j;
+        *reinterpret_cast<uint4*>(gbuf + chunk_off(rho, cc)) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+        *reinterpret_cast<uint4*>(xbuf + chunk_off(rho, cc)) = make_uint4(xw[0], xw[1], xw[2], xw[3]);
       }
       if (ch + 1 < nch) fetch(tl, ch + 1);
       else fetch(tl + gridDim.x, 0);
       __syncthreads();
-      const bool full = kCh * (ch + 1) <= pv;
-      // ---- 4 k-steps of 16 pixels
+      if (r0 >= rows) continue;                        // chunk row entirely past the band
+      auto run = [&](auto full_c) {
+        constexpr bool FULL = decltype(full_c)::value;
+        // B (input tile) address of k-step ks, half e: pixel (r0 + ks, c0 + 8 h + 4 e + q).
+        // Partial chunks clamp the pixel into the band / image so every lane reads inside the
+        // tile (invalid pixels have zero g / xhat rows); full chunks are one base + constant
+        // offsets.
+        auto baddr = [&](int ks, int e) {
+          if constexpr (FULL) {
+            return (2 * r0 + ky0) * WT + 2 * (c0 + 8 * h + q) + 4 * (grp & 1) + pq +
+                   2 * ks * WT + 8 * e;
+          } else {
+            const int oyl = min(r0 + ks, rows - 1);
+            const int oxl = min(c0 + 8 * h + 4 * e + q, OW - 1);
+            return (2 * oyl + ky0) * WT + 2 * oxl + 4 * (grp & 1) + pq;
+          }
+        };
+        // software pipeline: the fragments of k-step ks + 1 are read while ks's MFMAs run
+        s16x4 fa[2][2], fb[2][4][2];
+        auto load = [&](int ks, int buf) {
+          const int rho0 = 16 * ks + 8 * h + q;
+          fa[buf][0] = ld_tr(abuf + chunk_off(rho0, chn0));
+          fa[buf][1] = ld_tr(abuf + chunk_off(rho0 + 4, chn0));
+          const int b0 = baddr(ks, 0), b1 = baddr(ks, 1);
 #pragma unroll
-      for (int ks = 0; ks < kCh / 16; ++ks) {
-        s16x4 a[2];
-        int tb[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int rho = 16 * ks + 8 * h + 4 * e + q;  // this lane's address row
-          a[e] = ld_tr(abuf + chunk_off(rho, chn0) + 8 * (pq & 1));
-          int pp = kCh * ch + rho;
-          pp = pp < pv ? pp : 0;
-          const int oyl = row_of(pp, inv_ow);
-          const int ox = pp - oyl * OW;
-          tb[e] = (2 * oyl + ky0) * WT + 2 * ox + 4 * (grp & 1) + pq;
-        }
-        const bf16x8_t A = cat(a[0], a[1]);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          if (kk < nky) {
-            const s16x4 b0 = ld_tr(reinterpret_cast<const char*>(tile + tb[0] + kk * WT));
-            const s16x4 b1 = ld_tr(reinterpret_cast<const char*>(tile + tb[1] + kk * WT));
-            acc[kk] = mfma(A, cat(b0, b1), acc[kk]);
-            if (ks == mb) {                            // colA: each k-step summed by one wave
-              const int pj = kCh * ch + 16 * ks + 8 * h;
-              float sum = 0.f;
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const uint32_t w2 = static_cast<uint32_t>(static_cast<uint16_t>(b0[j]));
-                sum += (full || pj + j < pv) ? __uint_as_float(w2 << 16) : 0.f;
-                const uint32_t w3 = static_cast<uint32_t>(static_cast<uint16_t>(b1[j]));
-                sum += (full || pj + 4 + j < pv) ? __uint_as_float(w3 << 16) : 0.f;
-              }
-              ca[kk] += sum;
+          for (int kk = 0; kk < 4; ++kk) {
+            if (kk < nky) {
+              fb[buf][kk][0] = ld_tr(reinterpret_cast<const char*>(tile + b0 + kk * WT));
+              fb[buf][kk][1] = ld_tr(reinterpret_cast<const char*>(tile + b1 + kk * WT));
             }
           }
+        };
+        auto step = [&](int ks, int buf) {
+          (void)ks;
+          const bf16x8_t A = cat(fa[buf][0], fa[buf][1]);
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            if (kk < nky) acc[kk] = mfma(A, cat(fb[buf][kk][0], fb[buf][kk][1]), acc[kk]);
+        };
+        if constexpr (FULL) {
+          // software pipeline over k-step pairs (rolled, so the scheduler cannot hoist every
+          // fragment read of the chunk): k-step ks + 1's fragments load while ks's MFMAs run
+          load(0, 0);
+#pragma unroll 1
+          for (int ks = 0; ks < kCh / 16; ks += 2) {
+            load(ks + 1, 1);
+            step(ks, 0);
+            if (ks + 2 < kCh / 16) load(ks + 2, 0);
+            step(ks + 1, 1);
+          }
+        } else {
+#pragma unroll 1
+          for (int ks = 0; ks < kCh / 16; ++ks) {
+            load(ks, 0);
+            step(ks, 0);
+          }
         }
+      };
+      if constexpr (OWC > 0) {
+        run(std::true_type{});                         // host guarantees OW == OWC, OH % kTYB == 0
+      } else {
+        run(std::false_type{});                        // generic shapes: clamped + masked path
       }
     }
   }
@@ -427,31 +483,14 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
     }
   }
   __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);         // [64 rows][2 stat][64]
-  float* redc = red + kCh * 2 * kCo;                   // [8 waves][2 h][4 kk][32]
+  float* red = reinterpret_cast<float*>(smem);         // [64 staging rows][64]
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    red[(prow * 2 + 0) * kCo + 8 * cc + k] = s1[k];
-    red[(prow * 2 + 1) * kCo + 8 * cc + k] = s2[k];
-  }
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) redc[((wave * 2 + h) * 4 + kk) * 32 + r] = ca[kk];
+  for (int k = 0; k < 8; ++k) red[srho * kCo + 8 * cc + k] = s2[k];
   __syncthreads();
-  if (tid < 2 * kCo) {
-    const int st = tid / kCo, c = tid % kCo;
+  if (tid < kCo) {
     float s = 0.f;
-    for (int k = 0; k < kCh; ++k) s += red[(k * 2 + st) * kCo + c];
-    pw[2 * kCo * kKP + kKP + st * kCo + c] = s;
-  } else if (tid < 2 * kCo + kKP) {
-    const int kc = tid - 2 * kCo;
-    const int ky = kc >> 5, rr = kc & 31;
-    const int w0 = ky < 4 ? 0 : 4, kk = ky - w0;
-    float s = 0.f;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) s += redc[(((w0 + m) * 2 + hh) * 4 + kk) * 32 + rr];
-    pw[2 * kCo * kKP + kc] = s;
+    for (int k = 0; k < kBT / 8; ++k) s += red[k * kCo + tid];
+    pw[2 * kCo * kKP + tid] = s;
   }
 }
 
@@ -476,10 +515,11 @@ __global__ __launch_bounds__(256) void stem_wgrad_fold_kernel(const float* __res
   tot[e] = S;
 }
 
-// dW[co][c][ky][kx] = gamma invstd (G - s1/M colA - s2/M X); dgamma = s2, dbeta = s1 (fp32)
+// dW[co][c][ky][kx] = gamma invstd (G - s2/M X); dgamma = s2, dbeta = sum g (fp32)
 __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __restrict__ tot,
                                                               const uint16_t* __restrict__ gamma,
                                                               const float* __restrict__ invstd,
+                                                              const float* __restrict__ gsum,
                                                               double M, int C,
                                                               float* __restrict__ dw,
                                                               float* __restrict__ dgamma,
@@ -487,9 +527,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __r
   const int e = blockIdx.x * 256 + threadIdx.x;
   const double* G = tot;
   const double* X = tot + kCo * kKP;
-  const double* A = tot + 2 * kCo * kKP;
-  const double* S1 = A + kKP;
-  const double* S2 = S1 + kCo;
+  const double* S2 = tot + 2 * kCo * kKP;
   if (e < kCo * C * 49) {
     const int co = e / (C * 49);
     const int rem = e - co * C * 49;
@@ -497,12 +535,11 @@ __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __r
     const int ky = t / 7, kx = t - ky * 7;
     const int kc = (ky * 8 + kx) * 4 + c;
     const double a = static_cast<double>(bf2f(gamma[co])) * invstd[co];
-    const double v = a * (G[co * kKP + kc] - S1[co] / M * A[kc] - S2[co] / M * X[co * kKP + kc]);
-    dw[e] = static_cast<float>(v);
+    dw[e] = static_cast<float>(a * (G[co * kKP + kc] - S2[co] / M * X[co * kKP + kc]));
   }
   if (e < kCo) {
     dgamma[e] = static_cast<float>(S2[e]);
-    dbeta[e] = static_cast<float>(S1[e]);
+    dbeta[e] = gsum[e];
   }
 }
 
@@ -513,7 +550,7 @@ size_t fwd_lds(int OW) {   // input tile; the final reduction reuses it
 }
 size_t bwd_lds(int OW) {   // chunk images + input tile; the final reduction reuses it
   const size_t need = 2 * kCh * 128 + static_cast<size_t>(tile_rows(kTYB)) * tile_cols(OW) * 8;
-  const size_t red = (static_cast<size_t>(kCh) * 2 * kCo + 8 * 2 * 4 * 32) * sizeof(float);
+  const size_t red = static_cast<size_t>(kBT / 8) * kCo * sizeof(float);
   return need > red ? need : red;
 }
 
@@ -530,9 +567,10 @@ int persistent_grid(const void* fn, int threads, size_t lds, int ntiles) {
 // the backward tile needs > 64 KiB of dynamic LDS: opt in once per kernel instance
 void wgrad_lds_optin() {
   static const bool done = [] {
-    const void* fns[3] = {reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true>),
-                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, false>),
-                          reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false>)};
+    const void* fns[4] = {reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 112>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 0>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, false, 0>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false, 0>)};
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
     return true;
@@ -552,8 +590,8 @@ int stem_fwd_grid(int N, int OH, int OW, int C) {
 int stem_bwd_grid(int N, int OH, int OW, int C) {
   wgrad_lds_optin();
   const int ntiles = N * ((OH + kTYB - 1) / kTYB);
-  const void* fn = C == 4 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false>)
-                          : reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true>);
+  const void* fn = C == 4 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false, 0>)
+                          : reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 112>);
   return persistent_grid(fn, kBT, bwd_lds(OW), ntiles);
 }
 
@@ -581,25 +619,30 @@ hipError_t launch_stem_conv_fwd(const void* x, const void* wpk, void* z, float* 
 }
 
 hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const float* mean,
-                             const float* invstd, const void* gamma, float* part, int grid,
-                             double* tot, float* dw, float* dgamma, float* dbeta, int N, int H,
-                             int W, int C, int OH, int OW, hipStream_t st) {
+                             const float* invstd, const void* gamma, const float* gsum,
+                             float* part, int grid, double* tot, float* dw, float* dgamma,
+                             float* dbeta, int N, int H, int W, int C, int OH, int OW,
+                             hipStream_t st) {
   if ((C != 3 && C != 4) || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1 || N < 1 || grid < 1)
     return hipErrorInvalidValue;
-  if (bwd_lds(OW) > 120 * 1024 || OH * OW >= (1 << 20)) return hipErrorInvalidValue;
+  if (bwd_lds(OW) > 120 * 1024 || static_cast<int64_t>(N) * OH * OW >= (1ll << 31) / kCo)
+    return hipErrorInvalidValue;
   const size_t lds = bwd_lds(OW);
   wgrad_lds_optin();
   const auto* gp = reinterpret_cast<const uint16_t*>(g);
   const auto* zp = reinterpret_cast<const uint16_t*>(z);
   const auto* xp = reinterpret_cast<const uint16_t*>(x);
   const bool vec = C == 3 && W % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
-  if (C == 4) stem_wgrad_kernel<4, false><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, part, N, H, W, OH, OW);
-  else if (vec) stem_wgrad_kernel<3, true><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, part, N, H, W, OH, OW);
-  else stem_wgrad_kernel<3, false><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, part, N, H, W, OH, OW);
+#define CML_WG(CC, V, OWC) stem_wgrad_kernel<CC, V, OWC><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, gsum, part, N, H, W, OH, OW)
+  if (C == 4) CML_WG(4, false, 0);
+  else if (vec && OW == 112 && OH % kTYB == 0) CML_WG(3, true, 112);
+  else if (vec) CML_WG(3, true, 0);
+  else CML_WG(3, false, 0);
+#undef CML_WG
   stem_wgrad_fold_kernel<<<(kPartW + 255) / 256, 256, 0, st>>>(part, grid, tot);
   stem_wgrad_final_kernel<<<(kCo * C * 49 + 255) / 256, 256, 0, st>>>(
-      tot, reinterpret_cast<const uint16_t*>(gamma), invstd, static_cast<double>(N) * OH * OW, C,
-      dw, dgamma, dbeta);
+      tot, reinterpret_cast<const uint16_t*>(gamma), invstd, gsum,
+      static_cast<double>(N) * OH * OW, C, dw, dgamma, dbeta);
   return hipGetLastError();
 }
 

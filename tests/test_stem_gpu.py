@@ -126,21 +126,24 @@ def test_stem_kernels_exact(cuda, N, C, H, W):
     y, idx, _, _ = lib().bn_relu_maxpool_fwd(z, gam, bet, None, None, mean, invstd, 1e-5, 0.1,
                                              False, 3, 2, 1)
     dy = torch.randn_like(y)
-    g = lib().maxpool_bwd(dy, idx, z.shape[2], z.shape[3], 3, 2, 1)
+    g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3])
     sc = (invstd.double() * gam.double()).view(1, -1, 1, 1)
     u = (z.double() - mean.double().view(1, -1, 1, 1)) * sc + bet.double().view(1, -1, 1, 1)
     ud = u.requires_grad_(True)
     F.max_pool2d(torch.relu(ud), 3, 2, 1).backward(dy.double())
     assert _rel(g.double(), ud.grad) < 4e-3                  # bf16 output rounding
-    dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gam)
+    # gsum adds the unrounded fp32 gradients: compare on the scale of sum |g|
+    gabs = g.double().abs().sum((0, 2, 3)).clamp_min(1e-6)
+    assert ((gsum.double() - g.double().sum((0, 2, 3))).abs() / gabs).max().item() < 2e-3
+    dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gam, gsum)
     gd = g.double()
     xh = (z.double() - mean.double().view(1, -1, 1, 1)) * invstd.double().view(1, -1, 1, 1)
     s1, s2 = gd.sum((0, 2, 3)), (gd * xh).sum((0, 2, 3))
-    assert _rel(db.double(), s1) < 1e-5
+    assert ((db.double() - s1).abs() / gabs).max().item() < 2e-3
     assert _rel(dg.double(), s2) < 1e-5
     M = gd.numel() / 64
     dz = (gam.double() * invstd.double()).view(1, -1, 1, 1) * (
         gd - s1.view(1, -1, 1, 1) / M - xh * (s2.view(1, -1, 1, 1) / M))
     wq = w.double().requires_grad_(True)
     F.conv2d(x.double(), wq, stride=2, padding=3).backward(dz)
-    assert _rel(dw.double(), wq.grad) < 2e-3                 # xhat staged as bf16
+    assert _rel(dw.double(), wq.grad) < 5e-3                 # g - mean(g) and xhat staged as bf16

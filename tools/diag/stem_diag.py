@@ -20,7 +20,7 @@ vr = zr.var((0, 2, 3), unbiased=False)
 print("mean abs err", (mean.double() - mr).abs().max().item(), "invstd rel", ((invstd.double() - (vr + 1e-5).rsqrt()) / (vr + 1e-5).rsqrt()).abs().max().item())
 y, idx, _, _ = lib().bn_relu_maxpool_fwd(z, gam, bet, None, None, mean, invstd, 1e-5, 0.1, False, 3, 2, 1)
 dy = torch.randn_like(y)
-g = lib().maxpool_bwd(dy, idx, z.shape[2], z.shape[3], 3, 2, 1)
+g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3])
 # torch: masked gradient
 u = (z.double() - mean.double().view(1, -1, 1, 1)) * invstd.double().view(1, -1, 1, 1) * gam.double().view(1, -1, 1, 1) + bet.double().view(1, -1, 1, 1)
 ud = u.detach().requires_grad_(True)
@@ -28,7 +28,7 @@ yp = F.max_pool2d(torch.relu(ud), 3, 2, 1)
 yp.backward(dy.double())
 gr = ud.grad
 print("g rel", ((g.double() - gr).norm() / gr.norm()).item(), "frac idx255", (idx == 255).float().mean().item())
-dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gam)
+dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gam, gsum)
 gd = g.double()
 xh = (z.double() - mean.double().view(1, -1, 1, 1)) * invstd.double().view(1, -1, 1, 1)
 s1 = gd.sum((0, 2, 3))
