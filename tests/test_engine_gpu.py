@@ -83,7 +83,10 @@ def test_gpu_topologies_match_cpu_reference(cuda, topo):
     ("llama_tiny", "mean", "gossip", "adamw"),
 ])
 def test_gpu_model_families(cuda, model, rule, topo, opt):
-    cfg = _cfg(rule, topo, V=4, f=1, model=model, opt=opt, lr=1e-3 if opt == "adamw" else 0.05)
+    # resnet_tiny (width 8) in bf16 has ~33 % gradient error vs fp32 on PyTorch's own bf16 ops
+    # too (tools/diag/tiny_grad.py), so SGD at lr 0.05 / batch 4 follows a noise-driven path: the
+    # check is that every family trains through the engine without diverging
+    cfg = _cfg(rule, topo, V=4, f=1, model=model, opt=opt, lr=1e-3 if opt == "adamw" else 0.01)
     cfg.model.num_classes = 10
     cfg.model.image_size = 32
     cfg.model.seq_len = 32
