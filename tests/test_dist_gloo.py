@@ -1,4 +1,4 @@
-"""Multi-process tests on gloo, world_size 2 and 3 (BASELINE config 1: 2-layer MLP, coordinate-wise
+"""Multi-process tests on gloo, world_size 2, 3, 4 and 8 (BASELINE config 1: 2-layer MLP, coordinate-wise
 median) — the "multi-node without a cluster" fixture of SURVEY.md §4.4 item 3.
 
 A run with R ranks x 1 worker must produce bit-for-bit (fp32) the same parameters as 1 rank x R
@@ -94,6 +94,8 @@ def _single(world, rule, topo, f, steps, fault="none", byz=()):
     ("sharded", "geomed", 3, 0),
     ("allgather", "multi_krum", 3, 1),
     ("sharded", "trimmed_mean", 3, 1),
+    ("sharded", "multi_krum", 4, 1),
+    ("sharded", "krum", 8, 1),            # the bench's topology / rule at the node's 8 ranks
 ])
 def test_distributed_equals_virtual(tmp_path, topo, rule, world, f):
     res = _run_world(world, rule, topo, f, 6, tmp_path)
