@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Exhaustive MIOpen tuning (MIOPEN_FIND_ENFORCE=SEARCH_DB_UPDATE) of every ResNet-50 convolution
-that MIOpen runs in the benchmark step (batch 512, bf16 NHWC): forward, data gradient and weight
-gradient of each unique shape, biggest first. The user db is copied to --out after every shape,
-so a run cut short keeps what it tuned; --db seeds the run with an earlier partial result.
+"""MIOpen tuning of every ResNet-50 convolution that MIOpen runs in the benchmark step (bf16 NHWC):
+forward, data gradient and weight gradient of each unique shape, biggest first. --mode search is
+exhaustive (MIOPEN_FIND_ENFORCE=SEARCH_DB_UPDATE); --mode find records MIOpen's normal find (what
+`torch.backends.cudnn.benchmark` does on first use) for a new batch size. The user db is copied
+to --out after every shape, so a run cut short keeps what it tuned; --db seeds the run with an
+earlier (partial) db.
 
   python tools/miopen_tune.py --out gpurun_out/miopen_search [--db tuning/miopen_search] \\
       [--budget 1000]
@@ -46,14 +48,17 @@ def main():
     ap.add_argument("--db", default=None, help="seed user-db directory")
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--budget", type=float, default=1000.0, help="seconds; stop starting shapes after")
+    ap.add_argument("--mode", choices=["search", "find"], default="search",
+                    help="search: exhaustive (SEARCH_DB_UPDATE); find: MIOpen's normal find only")
     a = ap.parse_args()
     work = tempfile.mkdtemp(prefix="cml_miopen_search_")
     if a.db and os.path.isdir(a.db):
         for f in os.listdir(a.db):
             shutil.copy(os.path.join(a.db, f), work)
     os.environ["MIOPEN_USER_DB_PATH"] = work
-    os.environ["MIOPEN_FIND_ENFORCE"] = "SEARCH_DB_UPDATE"
-    os.environ["MIOPEN_FIND_MODE"] = "NORMAL"
+    if a.mode == "search":
+        os.environ["MIOPEN_FIND_ENFORCE"] = "SEARCH_DB_UPDATE"
+        os.environ["MIOPEN_FIND_MODE"] = "NORMAL"
     for v in ("FWD", "BWD", "WRW"):
         os.environ[f"MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_{v}"] = "0"
     import torch
@@ -64,6 +69,7 @@ def main():
     shapes.sort(key=lambda s: -(s[0] * s[3] * s[4] * s[4] * s[1] * s[2] / s[5] ** 2))
     done = set(open(os.path.join(a.db, "done.txt")).read().split()) if a.db and os.path.exists(
         os.path.join(a.db, "done.txt")) else set()
+    done = {d for d in done if d.startswith(f"b{a.batch}:")}
     t0 = time.time()
     alive = [True]
 
@@ -74,7 +80,7 @@ def main():
     threading.Thread(target=beat, daemon=True).start()
     os.makedirs(a.out, exist_ok=True)
     for s in shapes:
-        key = "x".join(map(str, s))
+        key = f"b{a.batch}:" + "x".join(map(str, s))
         if key in done:
             continue
         if time.time() - t0 > a.budget:
