@@ -69,13 +69,6 @@ def test_stem_fused_vs_fp32(cuda, N, C, H, W):
         assert ef <= max(2 * eu, 0.05), (name, ef, eu)
 
 
-def test_stem_pack_layout(cuda):
-    w = torch.arange(64 * 3 * 49, dtype=torch.float32).reshape(64, 3, 7, 7)
-    p = pack_stem_weight(w.to(torch.bfloat16)).float().view(64, 7, 8, 4)
-    assert torch.equal(p[:, :, :7, :3], w.to(torch.bfloat16).float().permute(0, 2, 3, 1))
-    assert p[:, :, 7].abs().sum() == 0 and p[..., 3].abs().sum() == 0
-
-
 def test_stem_model_path_matches_unfused(cuda):
     """ResNet-50 forward/backward with the fused stem vs the library stem, both against the same
     model in fp32: the stem weight gradient sits under 50 bf16 layers, so the yardstick is the
