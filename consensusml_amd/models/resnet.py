@@ -33,6 +33,8 @@ CONV1X1_GEMM = os.environ.get("CML_CONV1X1_GEMM", "auto")
 RESIDUAL_LINK = True
 # downsample-block tail relu(bn3(z) + down_bn(zd)) as one fused op (ops.bn.bn_add_bn_relu)
 FUSE_DOWN_BN = os.environ.get("CML_FUSE_DOWN_BN", "1") == "1"
+# weight gradient of the deeper stride-1 1x1 convs on csrc/kernels/wgrad1x1.hip
+OWN_WGRAD1X1 = os.environ.get("CML_WGRAD1X1", "1") == "1"
 # whole stem (conv + BN statistics, BN + ReLU + pool; backward in one weight-gradient pass) on
 # the HIP kernels of csrc/kernels/stem_conv.hip (ops.stem)
 FUSE_STEM_CONV = os.environ.get("CML_FUSE_STEM_CONV", "1") == "1"
@@ -57,14 +59,16 @@ class _Conv1x1Fn(torch.autograd.Function):
 
     forward: y = x W^T as one GEMM (fwd_gemm) or MIOpen. backward: dX = dY W as a GEMM
     (dgrad_gemm; accumulated in place into a residual gradient parked on ``link`` — the GEMM's
-    beta = 1 epilogue replaces an elementwise add) or MIOpen; dW always MIOpen's backward-weight
-    (``aten.convolution_backward`` with only the weight output requested)."""
+    beta = 1 epilogue replaces an elementwise add) or MIOpen; dW from ``csrc/kernels/wgrad1x1.hip``
+    (own_wgrad: split-K MFMA over the pixels, both operands through transposed LDS reads) or
+    MIOpen's backward-weight (``aten.convolution_backward`` with only the weight output)."""
 
     @staticmethod
-    def forward(ctx, x, w, link, fwd_gemm, dgrad_gemm):
+    def forward(ctx, x, w, link, fwd_gemm, dgrad_gemm, own_wgrad=False):
         ctx.save_for_backward(x, w)
         ctx.link = link
         ctx.dgrad_gemm = dgrad_gemm
+        ctx.own_wgrad = own_wgrad
         N, C, H, W = x.shape
         if fwd_gemm:
             y = torch.mm(x.permute(0, 2, 3, 1).reshape(N * H * W, C), w.reshape(w.shape[0], C).t())
@@ -79,9 +83,16 @@ class _Conv1x1Fn(torch.autograd.Function):
         Co = w.shape[0]
         need_dx = ctx.needs_input_grad[0]
         mio_dx = need_dx and not ctx.dgrad_gemm
-        dx_m, dw, _ = torch.ops.aten.convolution_backward(
-            dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-            [mio_dx, ctx.needs_input_grad[1], False])
+        own_dw = ctx.own_wgrad and ctx.needs_input_grad[1]
+        mio_dw = ctx.needs_input_grad[1] and not own_dw
+        dx_m, dw = None, None
+        if mio_dx or mio_dw:
+            dx_m, dw, _ = torch.ops.aten.convolution_backward(
+                dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                [mio_dx, mio_dw, False])
+        if own_dw:
+            from ..ops.native import lib
+            dw = lib().wgrad1x1(dy, x, w.dtype).view_as(w)
         dx = dx_m if mio_dx else None
         if need_dx and ctx.dgrad_gemm:
             dy2 = dy.permute(0, 2, 3, 1).reshape(N * H * W, Co)
@@ -97,7 +108,18 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 d2 = torch.mm(dy2, w2)
             dx = d2.view(N, H, W, C).permute(0, 3, 1, 2)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
+
+
+# (cin, cout) of the stride-1 1x1 convs whose weight gradient runs faster on wgrad1x1.hip than on
+# MIOpen's kernels, measured per shape at batch 1024 (tools/diag/wgrad1x1_bench.py, us own / MIOpen):
+# 128->512 227/236, 512->128 236/261, 256->1024 187/222, 512->2048 148/188, 2048->512 133/183.
+# Layer-1 shapes are at the HBM floor on MIOpen already; 512->256, 1024->256, 1024->512 tie or lose.
+OWN_WGRAD_SHAPES = {(128, 512), (512, 128), (256, 1024), (512, 2048), (2048, 512)}
+
+
+def own_wgrad_ok(cin: int, cout: int) -> bool:
+    return OWN_WGRAD1X1 and (cin, cout) in OWN_WGRAD_SHAPES
 
 
 class Conv1x1(nn.Conv2d):
@@ -122,9 +144,13 @@ class Conv1x1(nn.Conv2d):
 
     def forward(self, x: torch.Tensor, res_link: Optional[ResidualLink] = None) -> torch.Tensor:
         fwd_gemm, dgrad_gemm = self._policy(x)
-        if fwd_gemm or dgrad_gemm:
+        own = (self.stride == (1, 1) and x.is_cuda and x.dtype == torch.bfloat16
+               and self.weight.dtype in (torch.bfloat16, torch.float32)
+               and x.is_contiguous(memory_format=torch.channels_last)
+               and own_wgrad_ok(self.in_channels, self.out_channels))
+        if fwd_gemm or dgrad_gemm or own:
             return _Conv1x1Fn.apply(x, self.weight, res_link if dgrad_gemm else None, fwd_gemm,
-                                    dgrad_gemm)
+                                    dgrad_gemm, own)
         return super().forward(x)
 
 

@@ -470,6 +470,29 @@ Tensor maxpool_bwd(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W,
   return dx;
 }
 
+// dW of a stride-1 1x1 conv: dy [N, Co, H, W], x [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 1, 1]
+// in `dtype` (bf16 or fp32).
+Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype) {
+  check_nhwc(x, "x");
+  Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(0) == x.size(0) && dy.size(2) == x.size(2) &&
+                  dy.size(3) == x.size(3), "wgrad1x1: dy / x shapes");
+  TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "wgrad1x1: bf16 or fp32 output");
+  const int64_t Co = dy.size(1), Ci = x.size(1);
+  const int64_t P = x.numel() / Ci;
+  TORCH_CHECK(Co % 128 == 0 && Ci % 128 == 0, "wgrad1x1: channels must be multiples of 128");
+  const c10::DeviceGuard guard(x.device());
+  int S = 1, cps = 1;
+  cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps);
+  Tensor part = at::empty({S, Co, Ci}, x.options().dtype(at::kFloat));
+  Tensor dw = at::empty({Co, Ci, 1, 1}, x.options().dtype(dtype));
+  CML_CHECK_HIP(cml::launch_wgrad1x1(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(),
+                                     dw.data_ptr(), dtype == at::kBFloat16, P,
+                                     static_cast<int>(Co), static_cast<int>(Ci), cur_stream()));
+  return dw;
+}
+
 // 3x3/s2/p1 max-pool backward + per-channel sums of the result: {dx, sums fp32 [C]}.
 std::vector<Tensor> maxpool_bwd_sum(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W) {
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
@@ -887,6 +910,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_wgrad", &stem_wgrad, "ResNet stem weight gradient through BN (MFMA, one pass)");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
+  m.def("wgrad1x1", &wgrad1x1, "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
   m.def("maxpool_bwd_sum", &maxpool_bwd_sum, "3x3/s2 max-pool backward + channel sums of dx");
   m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");
   m.def("pad_c4", &pad_c4, "NHWC bf16 channel zero-padding to 4");

@@ -233,4 +233,11 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
                              double* tot, float* dw, float* dgamma, float* dbeta, int N, int H,
                              int W, int C, int OH, int OW, hipStream_t stream);
 
+// Weight gradient of a stride-1 1x1 conv, NHWC bf16: dW[co][ci] = sum_p dy[p][co] x[p][ci]
+// (wgrad1x1.hip). Co, Ci multiples of 128. part: splits x Co x Ci floats (wgrad1x1_plan);
+// dw: bf16 (dw_bf16) or fp32 [Co][Ci].
+void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps);
+hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
+                           int64_t P, int Co, int Ci, hipStream_t stream);
+
 }  // namespace cml

@@ -1,0 +1,230 @@
+// Weight gradient of a stride-1 1x1 convolution on NHWC bf16 activations:
+//   dW[co][ci] = sum_p dy[p][co] x[p][ci]      (p over N*H*W pixels)
+// i.e. a GEMM whose reduction runs over the pixel dimension, which both operands store
+// contiguously per pixel. ResNet-50's deeper 1x1 convs (128..2048 channels, 25k..800k pixels at
+// batch 1024) are where MIOpen's weight-gradient kernels run at 1.4-3.7 TB/s and 0.5-0.6
+// PFLOP/s (tools/diag/wgrad1x1_bench.py).
+//
+// Layout: a workgroup owns a 128 (co) x 128 (ci) tile of dW over a contiguous range of pixels
+// (split-K; fp32 partials folded in a fixed order by wgrad1x1_fold_kernel). Per 64-pixel chunk
+// the dy and x slices are staged as [pixel][channel] 256-B rows (XOR-swizzled so the transposed
+// reads are bank-conflict free) and both MFMA operands come out through ds_read_b64_tr_b16 (the
+// gfx950 transpose read: k = pixel runs down the rows). 4 waves = 2 (co) x 2 (ci) halves of
+// 64 x 64, four v_mfma_f32_32x32x16_bf16 accumulators each. The next chunk is prefetched into
+// registers with unconditional (clamped) loads while the current one is multiplied.
+#include "common.h"
+#include "kernels.h"
+
+namespace cml {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+
+__device__ __forceinline__ f32x16 mfma(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ s16x4 ld_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+__device__ __forceinline__ bf16x8_t cat(s16x4 a, s16x4 b) {
+  return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// component-wise select: a select of whole uint4 values becomes a select of their addresses and
+// pushes the prefetch registers into scratch memory
+__device__ __forceinline__ uint4 keep_if(bool ok, uint4 v) {
+  return make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
+}
+// byte offset of 16-B chunk ch (0..15) of row `row` in a [rows][256 B] image; the XOR spreads
+// the 4 rows x 64 B of each transposed read over all 64 banks
+template <int ROWB>
+__device__ __forceinline__ int img_off(int row, int ch) {
+  return ROWB * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+// TM (co) x TN (ci) tile, (TM / 64) x (TN / 64) waves of 64 x 64 (four 32 x 32 accumulators)
+template <int TM, int TN, int KC>
+__global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, float* __restrict__ part,
+    int P, int Co, int Ci, int tiles_n, int cps) {
+  constexpr int kKC = KC;                              // pixels per chunk
+  constexpr int NT = (TM / 64) * (TN / 64) * 64;
+  constexpr int CA = TM / 8, CB = TN / 8;            // 16-B chunks per staged row
+  constexpr int IA = kKC * CA / NT, IB = kKC * CB / NT;   // staged items per thread
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* abuf = smem;                                   // dy chunk [64 px][TM co]
+  char* bbuf = smem + kKC * TM * 2;                    // x chunk  [64 px][TN ci]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / (TN / 64), wn = wave % (TN / 64);
+  const int h = lane >> 5, r = lane & 31;
+  const int gi = lane & 15, grp = lane >> 4, q = gi >> 2, pq = gi & 3;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
+  const int co0 = tm * TM, ci0 = tn * TN;
+  const int nchunk = (P + kKC - 1) / kKC;
+  const int c_lo = blockIdx.y * cps;
+  const int c_hi = min(nchunk, c_lo + cps);
+  // prefetch registers; loads are unconditional (clamped pixel, zeroed at use) and selects are
+  // component-wise: a branch around the loads makes hipcc wait at the join, and a select of
+  // whole uint4 values became a select of addresses that put these registers in scratch
+  uint4 av[IA], bv[IB];
+  auto fetch = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < IA; ++j) {
+      const int e = tid + NT * j, row = e / CA, ch = e % CA;
+      const int p = min(c * kKC + row, P - 1);
+      av[j] = *reinterpret_cast<const uint4*>(dy + static_cast<int64_t>(p) * Co + co0 + 8 * ch);
+    }
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      const int e = tid + NT * j, row = e / CB, ch = e % CB;
+      const int p = min(c * kKC + row, P - 1);
+      bv[j] = *reinterpret_cast<const uint4*>(x + static_cast<int64_t>(p) * Ci + ci0 + 8 * ch);
+    }
+  };
+  f32x16 acc[2][2] = {};
+  if (c_lo < c_hi) fetch(c_lo);
+  for (int c = c_lo; c < c_hi; ++c) {
+    __syncthreads();                                   // previous chunk's readers are done
+#pragma unroll
+    for (int j = 0; j < IA; ++j) {
+      const int e = tid + NT * j, row = e / CA, ch = e % CA;
+      *reinterpret_cast<uint4*>(abuf + img_off<TM * 2>(row, ch)) = keep_if(c * kKC + row < P, av[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      const int e = tid + NT * j, row = e / CB, ch = e % CB;
+      *reinterpret_cast<uint4*>(bbuf + img_off<TN * 2>(row, ch)) = keep_if(c * kKC + row < P, bv[j]);
+    }
+    fetch(c + 1 < c_hi ? c + 1 : c);                   // the last iteration reloads its chunk
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < kKC / 16; ++ks) {
+      bf16x8_t A[2], B[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int r0 = 16 * ks + 8 * h + q;
+        const int cha = 8 * wm + 4 * b + 2 * (grp & 1) + (pq >> 1);   // co chunk in the tile
+        const int chb = 8 * wn + 4 * b + 2 * (grp & 1) + (pq >> 1);   // ci chunk in the tile
+        A[b] = cat(ld_tr(abuf + img_off<TM * 2>(r0, cha) + 8 * (pq & 1)),
+                   ld_tr(abuf + img_off<TM * 2>(r0 + 4, cha) + 8 * (pq & 1)));
+        B[b] = cat(ld_tr(bbuf + img_off<TN * 2>(r0, chb) + 8 * (pq & 1)),
+                   ld_tr(bbuf + img_off<TN * 2>(r0 + 4, chb) + 8 * (pq & 1)));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(A[i], B[j], acc[i][j]);
+    }
+  }
+  // partial [split][Co][Ci]: lane r = ci column, register k = co row (k&3) + 8 (k>>2) + 4 h
+  float* pw = part + static_cast<int64_t>(blockIdx.y) * Co * Ci;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int co = co0 + 64 * wm + 32 * i + (k & 3) + 8 * (k >> 2) + 4 * h;
+        const int ci = ci0 + 64 * wn + 32 * j + r;
+        pw[static_cast<int64_t>(co) * Ci + ci] = acc[i][j][k];
+      }
+}
+
+// dW = sum over S splits (fixed order), 4 elements per thread, bf16 or fp32 out
+template <bool BF16>
+__global__ __launch_bounds__(256) void wgrad1x1_fold_kernel(const float* __restrict__ part, int S,
+                                                           int64_t n, void* __restrict__ out) {
+  const int64_t e = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
+  if (e >= n) return;
+  float4 s = *reinterpret_cast<const float4*>(part + e);
+  for (int k = 1; k < S; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k) * n + e);
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  if constexpr (BF16) {
+    uint2 o;
+    o.x = static_cast<uint32_t>(f2bf(s.x)) | (static_cast<uint32_t>(f2bf(s.y)) << 16);
+    o.y = static_cast<uint32_t>(f2bf(s.z)) | (static_cast<uint32_t>(f2bf(s.w)) << 16);
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + e) = o;
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + e) = s;
+  }
+}
+
+}  // namespace
+
+namespace {
+// tile choice: cover as much of the smaller channel dimension as possible so the larger operand
+// is streamed once (x is re-read Co / TM times, dy Ci / TN times)
+// (memory-bound shapes, Co * Ci <= 128K); shapes with more MACs per byte take 128 x 128 tiles
+// for more workgroups (tools/diag/wgrad1x1_bench.py)
+void pick_tile(int Co, int Ci, int* TM, int* TN) {
+  if (static_cast<int64_t>(Co) * Ci >= 256 * 1024) {
+    *TM = 128;
+    *TN = 128;
+    return;
+  }
+  *TM = Co % 256 == 0 ? 256 : 128;
+  *TN = Ci % 256 == 0 ? 256 : 128;
+}
+}  // namespace
+
+// pixels per chunk (128-pixel chunks for the 128 x 128 tile measured 5-15 % slower: more
+// registers, fewer chunks per workgroup)
+int chunk_of(int, int) { return 64; }
+
+void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps) {
+  int TM, TN;
+  pick_tile(Co, Ci, &TM, &TN);
+  const int KC = chunk_of(TM, TN);
+  const int tiles = (Co / TM) * (Ci / TN);
+  const int waves = (TM / 64) * (TN / 64);
+  const int nchunk = static_cast<int>((P + KC - 1) / KC);
+  const int target = 256 * 8 / waves;                  // ~8 waves per CU in flight
+  int s = (target + tiles - 1) / tiles;
+  s = s < 1 ? 1 : (s > nchunk ? nchunk : s);
+  const int c = (nchunk + s - 1) / s;
+  *cps = c;
+  *splits = (nchunk + c - 1) / c;
+}
+
+hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
+                           int64_t P, int Co, int Ci, hipStream_t st) {
+  if (Co % 128 || Ci % 128 || P < 1 || P >= (1ll << 31)) return hipErrorInvalidValue;
+  int S, cps, TM, TN;
+  wgrad1x1_plan(P, Co, Ci, &S, &cps);
+  pick_tile(Co, Ci, &TM, &TN);
+  const int KC = chunk_of(TM, TN);
+  const int tiles_n = Ci / TN;
+  const dim3 grid((Co / TM) * tiles_n, S);
+  const auto* dp = reinterpret_cast<const uint16_t*>(dy);
+  const auto* xp = reinterpret_cast<const uint16_t*>(x);
+  const size_t lds = static_cast<size_t>(KC) * (TM + TN) * 2;
+  const int Pi = static_cast<int>(P);
+  if (TM == 256 && TN == 256) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad1x1_kernel<256, 256, 64>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    wgrad1x1_kernel<256, 256, 64><<<grid, 1024, lds, st>>>(dp, xp, part, Pi, Co, Ci, tiles_n, cps);
+  } else if (TM == 256) {
+    wgrad1x1_kernel<256, 128, 64><<<grid, 512, lds, st>>>(dp, xp, part, Pi, Co, Ci, tiles_n, cps);
+  } else if (TN == 256) {
+    wgrad1x1_kernel<128, 256, 64><<<grid, 512, lds, st>>>(dp, xp, part, Pi, Co, Ci, tiles_n, cps);
+  } else {
+    wgrad1x1_kernel<128, 128, 64><<<grid, 256, lds, st>>>(dp, xp, part, Pi, Co, Ci, tiles_n, cps);
+  }
+  const int64_t n = static_cast<int64_t>(Co) * Ci;
+  const int fb = static_cast<int>((n / 4 + 255) / 256);
+  if (dw_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, dw);
+  else wgrad1x1_fold_kernel<false><<<fb, 256, 0, st>>>(part, S, n, dw);
+  return hipGetLastError();
+}
+
+}  // namespace cml
