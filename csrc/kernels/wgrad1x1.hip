@@ -7,6 +7,7 @@
 //
 // Layout: a workgroup owns a 128 (co) x 128 (ci) tile of dW over a contiguous range of pixels
 // (split-K; fp32 partials folded in a fixed order by wgrad1x1_fold_kernel). Per 64-pixel chunk
+// (two LDS stages, one barrier per chunk)
 // the dy and x slices are staged as [pixel][channel] 256-B rows (XOR-swizzled so the transposed
 // reads are bank-conflict free) and both MFMA operands come out through ds_read_b64_tr_b16 (the
 // gfx950 transpose read: k = pixel runs down the rows). 4 waves = 2 (co) x 2 (ci) halves of
@@ -54,9 +55,7 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
   constexpr int NT = (TM / 64) * (TN / 64) * 64;
   constexpr int CA = TM / 8, CB = TN / 8;            // 16-B chunks per staged row
   constexpr int IA = kKC * CA / NT, IB = kKC * CB / NT;   // staged items per thread
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* abuf = smem;                                   // dy chunk [64 px][TM co]
-  char* bbuf = smem + kKC * TM * 2;                    // x chunk  [64 px][TN ci]
+  extern __shared__ __attribute__((aligned(16))) char smem[];   // 2 x {dy [KC][TM], x [KC][TN]}
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -87,21 +86,33 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     }
   };
   f32x16 acc[2][2] = {};
-  if (c_lo < c_hi) fetch(c_lo);
-  for (int c = c_lo; c < c_hi; ++c) {
-    __syncthreads();                                   // previous chunk's readers are done
+  // two LDS stages: chunk c is multiplied out of stage c & 1 while chunk c + 1 is written into the
+  // other stage from registers and chunk c + 2 is in flight -> one barrier per chunk
+  constexpr int STG = kKC * (TM + TN) * 2;
+  auto stage = [&](int c, int sb) {
+    char* ab = smem + sb * STG;
+    char* bb = ab + kKC * TM * 2;
 #pragma unroll
     for (int j = 0; j < IA; ++j) {
       const int e = tid + NT * j, row = e / CA, ch = e % CA;
-      *reinterpret_cast<uint4*>(abuf + img_off<TM * 2>(row, ch)) = keep_if(c * kKC + row < P, av[j]);
+      *reinterpret_cast<uint4*>(ab + img_off<TM * 2>(row, ch)) = keep_if(c * kKC + row < P, av[j]);
     }
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
       const int e = tid + NT * j, row = e / CB, ch = e % CB;
-      *reinterpret_cast<uint4*>(bbuf + img_off<TN * 2>(row, ch)) = keep_if(c * kKC + row < P, bv[j]);
+      *reinterpret_cast<uint4*>(bb + img_off<TN * 2>(row, ch)) = keep_if(c * kKC + row < P, bv[j]);
     }
-    fetch(c + 1 < c_hi ? c + 1 : c);                   // the last iteration reloads its chunk
-    __syncthreads();
+  };
+  if (c_lo < c_hi) {
+    fetch(c_lo);
+    stage(c_lo, 0);
+    fetch(c_lo + 1 < c_hi ? c_lo + 1 : c_lo);
+  }
+  __syncthreads();
+  for (int c = c_lo; c < c_hi; ++c) {
+    const int sb = (c - c_lo) & 1;
+    const char* ab = smem + sb * STG;
+    const char* bb = ab + kKC * TM * 2;
 #pragma unroll
     for (int ks = 0; ks < kKC / 16; ++ks) {
       bf16x8_t A[2], B[2];
@@ -110,16 +121,21 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
         const int r0 = 16 * ks + 8 * h + q;
         const int cha = 8 * wm + 4 * b + 2 * (grp & 1) + (pq >> 1);   // co chunk in the tile
         const int chb = 8 * wn + 4 * b + 2 * (grp & 1) + (pq >> 1);   // ci chunk in the tile
-        A[b] = cat(ld_tr(abuf + img_off<TM * 2>(r0, cha) + 8 * (pq & 1)),
-                   ld_tr(abuf + img_off<TM * 2>(r0 + 4, cha) + 8 * (pq & 1)));
-        B[b] = cat(ld_tr(bbuf + img_off<TN * 2>(r0, chb) + 8 * (pq & 1)),
-                   ld_tr(bbuf + img_off<TN * 2>(r0 + 4, chb) + 8 * (pq & 1)));
+        A[b] = cat(ld_tr(ab + img_off<TM * 2>(r0, cha) + 8 * (pq & 1)),
+                   ld_tr(ab + img_off<TM * 2>(r0 + 4, cha) + 8 * (pq & 1)));
+        B[b] = cat(ld_tr(bb + img_off<TN * 2>(r0, chb) + 8 * (pq & 1)),
+                   ld_tr(bb + img_off<TN * 2>(r0 + 4, chb) + 8 * (pq & 1)));
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma(A[i], B[j], acc[i][j]);
     }
+    if (c + 1 < c_hi) {                                // uniform branch; loads stay unconditional
+      stage(c + 1, sb ^ 1);
+    }
+    fetch(c + 2 < c_hi ? c + 2 : c);                   // past the end: reload a valid chunk
+    __syncthreads();
   }
   // partial [split][Co][Ci]: lane r = ci column, register k = co row (k&3) + 8 (k>>2) + 4 h
   float* pw = part + static_cast<int64_t>(blockIdx.y) * Co * Ci;
@@ -207,11 +223,11 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
   const dim3 grid((Co / TM) * tiles_n, S);
   const auto* dp = reinterpret_cast<const uint16_t*>(dy);
   const auto* xp = reinterpret_cast<const uint16_t*>(x);
-  const size_t lds = static_cast<size_t>(KC) * (TM + TN) * 2;
+  const size_t lds = 2 * static_cast<size_t>(KC) * (TM + TN) * 2;   // two stages
   const int Pi = static_cast<int>(P);
   if (TM == 256 && TN == 256) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad1x1_kernel<256, 256, 64>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
     wgrad1x1_kernel<256, 256, 64><<<grid, 1024, lds, st>>>(dp, xp, part, Pi, Co, Ci, tiles_n, cps);
   } else if (TM == 256) {
     wgrad1x1_kernel<256, 128, 64><<<grid, 512, lds, st>>>(dp, xp, part, Pi, Co, Ci, tiles_n, cps);
