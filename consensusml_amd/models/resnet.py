@@ -111,11 +111,14 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, dw, None, None, None, None
 
 
-# (cin, cout) of the stride-1 1x1 convs whose weight gradient runs faster on wgrad1x1.hip than on
-# MIOpen's kernels, measured per shape at batch 1024 (tools/diag/wgrad1x1_bench.py, us own / MIOpen):
-# 128->512 227/236, 512->128 236/261, 256->1024 187/222, 512->2048 148/188, 2048->512 133/183.
-# Layer-1 shapes are at the HBM floor on MIOpen already; 512->256, 1024->256, 1024->512 tie or lose.
-OWN_WGRAD_SHAPES = {(128, 512), (512, 128), (256, 1024), (512, 2048), (2048, 512)}
+# (cin, cout) of the stride-1 1x1 convs whose weight gradient runs on wgrad1x1.hip. In isolation the
+# kernel beats MIOpen on all nine >= 128-channel shapes at batch 1024 (tools/diag/wgrad1x1_bench.py,
+# profiles/r01_wgrad1x1_60.txt); in the training step the five with the largest margins are the best
+# set: 12,011 img/s vs 11,991 for all nine and 11,929-11,958 for none (profiles/r01_bench62_*.json,
+# same box). The 64-channel layer-1 shapes are at the HBM floor on MIOpen.
+_CORE = {(128, 512), (512, 128), (256, 1024), (512, 2048), (2048, 512)}
+_ALL = _CORE | {(256, 128), (512, 256), (1024, 256), (1024, 512)}
+OWN_WGRAD_SHAPES = _ALL if os.environ.get("CML_WGRAD1X1_SET", "core") == "all" else _CORE
 
 
 def own_wgrad_ok(cin: int, cout: int) -> bool:
