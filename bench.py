@@ -180,6 +180,8 @@ def main():
             "allreduce_ms_per_step": None if base_ms is None else round(base_ms, 3),
             "agg_overhead_vs_allreduce": None if overhead is None else round(overhead, 4),
             "loss_finite": main_res["finite"],
+            "peak_mem_gib": (round(torch.cuda.max_memory_allocated() / 2**30, 1)
+                             if torch.cuda.is_available() else None),
         }
         line = json.dumps(out)
         print(line, flush=True)
