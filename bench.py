@@ -13,9 +13,9 @@ and ``agg_overhead_vs_allreduce`` = (t_krum - t_allreduce) / t_allreduce is repo
 
 Data: synthetic ImageNet-shaped batches (random bf16 images, random labels) generated on
 device; random-init weights. Every timed step runs the full forward, backward, exchange,
-aggregation and optimizer update. Per-GPU batch 1536 by default: 288 GB of HBM holds it, and it
-runs 2-3 % more samples/s than 1024 and 6 % more than 512 (larger GEMM / conv problems, fewer
-fixed per-step costs).
+aggregation and optimizer update. Per-GPU batch 2048 by default: 288 GB of HBM holds it many times
+over (peak ~81 GiB), and throughput still rises with batch (512 ~11.5k, 1024 ~12.0k, 1536
+~12.1-12.4k, 2048 ~12.3k samples/s: larger conv / GEMM problems, fewer fixed per-step costs).
 """
 from __future__ import annotations
 
@@ -36,10 +36,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=1536,
-                    help="per-GPU batch (1536: +2-3 %% samples/s over 1024 and +6 %% over 512 on "
-                         "MI355X, profiles/r01_bench55_b*.json, r01_bench66_b*.json; the shipped "
-                         "MIOpen find-db covers 512 / 1024 / 1536)")
+    ap.add_argument("--batch", type=int, default=2048,
+                    help="per-GPU batch (samples/s on MI355X: 512 ~11.5k, 1024 ~12.0k, 1536 "
+                         "~12.1-12.4k, 2048 ~12.3k, profiles/r01_bench55/66/69_b*.json; peak memory "
+                         "~81 GiB at 2048 of 288; the shipped MIOpen find-db covers all four)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--rule", default="krum")
     ap.add_argument("--f", type=int, default=-1, help="Byzantine tolerance (-1: (n-3)//2)")
