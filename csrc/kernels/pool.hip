@@ -5,6 +5,8 @@
 // byte per output element, and the backward is a GATHER: each input pixel visits the <= ceil(k/s)^2
 // windows that cover it and sums the gradients whose argmax is that pixel — no atomics, bitwise
 // deterministic, every access a 16-byte vector of 8 channels.
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -125,6 +127,109 @@ __global__ __launch_bounds__(kPB) void maxpool_fwd_kernel(const bf16* __restrict
     m.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (static_cast<uint32_t>(arg[3]) << 24);
     m.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (static_cast<uint32_t>(arg[7]) << 24);
     *reinterpret_cast<uint2*>(idx + o) = m;
+  }
+}
+
+// Stem forward (k = 3, s = 2, p = 1, BN affine): one thread owns a 2 x 2 block of outputs x 8
+// channels, whose windows cover a 5 x 5 block of input taps. The taps are loaded one input row at
+// a time (5 x 16 B in flight), mapped through the affine once, and fed to every output window
+// that contains them: 25 loads + 25 affine FMAs per 4 outputs instead of 36 + 36. Tie and NaN
+// rules as maxpool_fwd_kernel (first max in window order, NaN propagates; max <= 0 -> argmax 255).
+__global__ __launch_bounds__(kPB) void maxpool_fwd_k3s2_aff_kernel(
+    const bf16* __restrict__ x, bf16* __restrict__ y, uint8_t* __restrict__ idx, int N, int H,
+    int W, int C, int OH, int OW, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const bf16* __restrict__ gamma,
+    const bf16* __restrict__ beta) {
+  const int cg = C / 8;
+  const int OWB = (OW + 1) / 2, OHB = (OH + 1) / 2;
+  const int t = blockIdx.x * kPB + threadIdx.x;
+  if (t >= OWB * cg) return;
+  const int i = t / cg;
+  const int g = t - i * cg;
+  float sc[8], bi[8];
+  {
+    float ga[8], be[8];
+    load_vec<bf16, 8>(gamma + 8 * g, ga);
+    load_vec<bf16, 8>(beta + 8 * g, be);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      sc[v] = invstd[8 * g + v] * ga[v];
+      bi[v] = be[v] - mean[8 * g + v] * sc[v];
+    }
+  }
+  for (int band = blockIdx.y; band < N * OHB; band += gridDim.y) {
+    const int n = band / OHB;
+    const int j = band - n * OHB;
+    float best[2][2][8];
+    uint8_t arg[2][2][8];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          best[a][b][v] = -__builtin_inff();
+          arg[a][b][v] = 0;
+        }
+#pragma unroll
+    for (int tr = 0; tr < 5; ++tr) {                  // input row 4j - 1 + tr
+      const int h = 4 * j - 1 + tr;
+      const bool hok = h >= 0 && h < H;
+      float tap[5][8];
+      bool wok[5];
+#pragma unroll
+      for (int u = 0; u < 5; ++u) {
+        const int w = 4 * i - 1 + u;
+        wok[u] = hok && w >= 0 && w < W;
+        const int hh = wok[u] ? h : 0, ww = wok[u] ? w : 0;
+        load_vec<bf16, 8>(x + ((static_cast<int64_t>(n) * H + hh) * W + ww) * C + 8 * g, tap[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 5; ++u)
+#pragma unroll
+        for (int v = 0; v < 8; ++v) tap[u][v] = fmaf(tap[u][v], sc[v], bi[v]);
+      // output (a, b) window row = tr - 2a, column = u - 2b, both in 0..2; taps in window order
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int wr = tr - 2 * a;
+        if (wr < 0 || wr > 2) continue;               // compile-time after unrolling
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int wc = 0; wc < 3; ++wc) {
+            const int u = wc + 2 * b;
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+              const float val = tap[u][v];
+              const bool take = wok[u] && (val > best[a][b][v] || (val != val));
+              best[a][b][v] = take ? val : best[a][b][v];
+              arg[a][b][v] = take ? static_cast<uint8_t>(wr * 3 + wc) : arg[a][b][v];
+            }
+          }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = 2 * j + a, ow = 2 * i + b;
+        if (oh >= OH || ow >= OW) continue;
+        float o[8];
+        uint8_t m[8];
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          const float bv = best[a][b][v];
+          const bool pos = bv > 0.f || bv != bv;
+          o[v] = pos ? bv : 0.f;
+          m[v] = pos ? arg[a][b][v] : static_cast<uint8_t>(255);
+        }
+        const int64_t off = ((static_cast<int64_t>(n) * OH + oh) * OW + ow) * C + 8 * g;
+        store_bf16<8>(y + off, o);
+        uint2 mm;
+        mm.x = m[0] | (m[1] << 8) | (m[2] << 16) | (static_cast<uint32_t>(m[3]) << 24);
+        mm.y = m[4] | (m[5] << 8) | (m[6] << 16) | (static_cast<uint32_t>(m[7]) << 24);
+        *reinterpret_cast<uint2*>(idx + off) = mm;
+      }
   }
 }
 
@@ -342,6 +447,15 @@ __global__ __launch_bounds__(256) void pad_c4_kernel(const uint16_t* __restrict_
 
 }  // namespace
 
+// CML_POOL_BLOCKS=0 selects the one-output-per-thread forward for the stem (A/B)
+static bool k3s2_blocks() {
+  static const bool on = [] {
+    const char* e = getenv("CML_POOL_BLOCKS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C,
                               int OH, int OW, int k, int s, int p, hipStream_t st) {
   return launch_bn_relu_maxpool_fwd(x, nullptr, nullptr, nullptr, nullptr, y, idx, N, H, W, C, OH,
@@ -362,7 +476,10 @@ hipError_t launch_bn_relu_maxpool_fwd(const void* x, const float* mean, const fl
   const bf16* bp = reinterpret_cast<const bf16*>(beta);
   const bool aff = mean != nullptr;
 #define CML_MP(KK, A) maxpool_fwd_kernel<KK, A><<<grid, kPB, 0, st>>>(xp, yp, ip, N, H, W, C, OH, OW, k, s, p, mean, invstd, gp, bp)
-  if (k == 3 && aff) CML_MP(3, true);
+  if (k == 3 && s == 2 && p == 1 && aff && k3s2_blocks()) {
+    maxpool_fwd_k3s2_aff_kernel<<<pgrid(((OW + 1) / 2) * (C / 8), N * ((OH + 1) / 2)), kPB, 0, st>>>(
+        xp, yp, ip, N, H, W, C, OH, OW, mean, invstd, gp, bp);
+  } else if (k == 3 && aff) CML_MP(3, true);
   else if (k == 3) CML_MP(3, false);
   else if (aff) CML_MP(0, true);
   else CML_MP(0, false);
