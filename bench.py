@@ -49,7 +49,9 @@ def parse():
     ap.add_argument("--no-baseline", action="store_true")
     ap.add_argument("--baseline-steps", type=int, default=-1)
     ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--graph", action="store_true", help="(reserved) capture step in a hipGraph")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse "
+                         "several ranks sharing one GPU)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--conv1x1", choices=["auto", "gemm", "miopen"], default="auto",
                     help="1x1 stride-1 conv forward / data gradient as hipBLASLt GEMMs: per-shape "
@@ -62,6 +64,7 @@ def parse():
 
 
 def run(args, rule: str, topology: str, steps: int, warmup: int, info):
+    from consensusml_amd.parallel.dist import barrier
     from consensusml_amd import TrainConfig
     from consensusml_amd.trainer.trainer import ConsensusTrainer
     n = info.world
@@ -107,15 +110,13 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info):
               flush=True)
     if args.profile_marker:
         torch.cuda._sleep(1000)
-    if info.distributed:
-        dist.barrier(device_ids=[dev.index])
+    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
         loss = step(i)
     torch.cuda.synchronize()
-    if info.distributed:
-        dist.barrier(device_ids=[dev.index])
+    barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if info.distributed:
@@ -142,7 +143,8 @@ def main():
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
-    info = init_distributed("nccl" if world_env > 1 else "auto")
+    info = init_distributed(args.dist_backend if world_env > 1 else "auto",
+                            device="cuda:0" if args.dist_backend == "gloo" else None)
     # MIOpen find mode: conv solvers are benchmarked on first use of each shape (untimed: the
     # warmup steps, plus one tuning step when --warmup 0) and cached for the run.
     torch.backends.cudnn.benchmark = not args.no_miopen_find

@@ -80,7 +80,7 @@ def set_info(info: DistInfo) -> None:
 
 def barrier() -> None:
     if dist.is_available() and dist.is_initialized():
-        if get_info().device.type == "cuda":
+        if get_info().device.type == "cuda" and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[get_info().device.index])
         else:
             dist.barrier()
