@@ -40,6 +40,8 @@ def _worker(rank, world, port, rule, topo, f, steps, out_dir):
     ("sharded", "krum", 2, 0),          # the bench's topology / rule
     ("sharded", "median", 2, 0),
     ("allgather", "multi_krum", 3, 0),
+    ("sharded", "trimmed_mean", 3, 1),
+    ("allreduce", "mean", 2, 0),        # the bench's all-reduce reference run
 ])
 def test_gpu_ranks_equal_virtual_workers(cuda, tmp_path, topo, rule, world, f):
     from consensusml_amd.parallel.dist import DistInfo
