@@ -16,6 +16,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--keys", default="fill,zero,SubTensor,Memset,memset",
+                    help="comma-separated substrings of the op names to attribute")
     a = ap.parse_args()
     from consensusml_amd import TrainConfig
     from consensusml_amd.parallel.dist import DistInfo
@@ -44,15 +46,19 @@ def main():
         step()
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True,
+                 record_shapes=True) as prof:
         step()
         torch.cuda.synchronize()
-    keys = ("fill", "zero", "SubTensor", "Memset", "memset")
+    keys = tuple(a.keys.split(","))
     print(prof.key_averages(group_by_stack_n=6).table(sort_by="self_device_time_total",
                                                       row_limit=60, max_name_column_width=60))
-    print("=== ops containing fill / zero ===")
+    print("=== ops containing", keys, "===")
+    for e in prof.key_averages(group_by_input_shape=True):
+        if any(k in e.key for k in keys) and e.self_device_time_total > 0:
+            print(e.key, e.count, round(e.self_device_time_total / 1e3, 3), "ms", e.input_shapes)
     for e in prof.key_averages(group_by_stack_n=8):
-        if any(k in e.key for k in keys):
+        if any(k in e.key for k in keys) and e.self_device_time_total > 0:
             print(e.key, e.count, round(e.self_device_time_total / 1e3, 3), "ms")
             for fr in e.stack[:8]:
                 print("     ", fr)
