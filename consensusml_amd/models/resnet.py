@@ -40,6 +40,8 @@ OWN_WGRAD1X1 = os.environ.get("CML_WGRAD1X1", "1") == "1"
 FUSE_STEM_CONV = os.environ.get("CML_FUSE_STEM_CONV", "1") == "1"
 # stem BN + ReLU + max-pool in one pass (ops.pool.bn_relu_max_pool2d)
 FUSE_STEM_POOL = os.environ.get("CML_FUSE_STEM_POOL", "1") == "1"
+# the stem's pool backward sums layer1.0's downsample data gradient on load
+POOL_LINK = os.environ.get("CML_POOL_LINK", "1") == "1"
 # global average pool whose backward writes the NHWC gradient directly
 NHWC_AVGPOOL = os.environ.get("CML_NHWC_AVGPOOL", "1") == "1"
 # stem input channels zero-padded 3 -> 4 on the GPU (see ResNet.stem)
@@ -223,10 +225,14 @@ class Bottleneck(nn.Module):
             # autograd (ready nodes in reverse creation order) runs its backward first; the link
             # falls back to a normal add if that order ever changes.
             dlink = ResidualLink() if use_links and self.conv1.link_ok(x) else None
+            # otherwise, when x is the fused stem's output, its pool backward takes the parked
+            # gradient as a second input (ops.stem._StemFn)
+            tlink = dlink if dlink is not None else \
+                (getattr(x, "_cml_pool_link", None) if use_links else None)
             out = self.bn1(self.conv1(x, res_link=dlink))
             out = self.bn2(self.conv2(out))
             z = self.conv3(out)
-            zd = self.down_conv(link_tap(x, dlink) if dlink is not None else x)
+            zd = self.down_conv(link_tap(x, tlink) if tlink is not None else x)
             out_link = ResidualLink() if use_links and fused_ok(z, self.bn3.weight) else None
             # relu(bn3(z) + down_bn(zd)) in one op: the shortcut BN output is never stored
             y = bn_add_bn_relu(z, self.bn3, zd, self.down_bn, out_link) if FUSE_DOWN_BN \
@@ -276,7 +282,11 @@ class ResNet(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if FUSE_STEM_CONV and stem_ok(x, self.conv1, self.bn1):
-            x = stem_conv_bn_relu_pool(x, self.conv1, self.bn1)
+            plink = ResidualLink() if (POOL_LINK and RESIDUAL_LINK and self.training
+                                       and torch.is_grad_enabled()) else None
+            x = stem_conv_bn_relu_pool(x, self.conv1, self.bn1, plink)
+            if plink is not None:
+                x._cml_pool_link = plink    # layer1.0's downsample conv parks its dX here
         elif FUSE_STEM_POOL:
             x = bn_relu_max_pool2d(self.stem(x), self.bn1, 3, 2, 1)
         else:

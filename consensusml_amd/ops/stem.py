@@ -28,7 +28,7 @@ def pack_stem_weight(w: torch.Tensor) -> torch.Tensor:
 
 class _StemFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, gamma, beta, rmean, rvar, eps, momentum, training):
+    def forward(ctx, x, weight, gamma, beta, rmean, rvar, eps, momentum, training, link=None):
         wpk = pack_stem_weight(weight)
         z, mean, invstd = lib().stem_conv_fwd(x, wpk, rmean if training else None,
                                               rvar if training else None, eps, momentum, training)
@@ -39,15 +39,21 @@ class _StemFn(torch.autograd.Function):
                                                  momentum, False, 3, 2, 1)
         ctx.save_for_backward(x, z, idx, gamma, mean, invstd)
         ctx.dtypes = (weight.dtype, gamma.dtype, beta.dtype)
+        ctx.link = link
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, z, idx, gamma, mean, invstd = ctx.saved_tensors
-        g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3])
+        # a second gradient of y parked by a link_tap consumer (layer1.0's downsample conv) is
+        # summed inside the pool backward instead of by an autograd add
+        dy2 = ctx.link.take() if ctx.link is not None else None
+        if dy2 is not None and dy2.shape != dy.shape:
+            dy, dy2 = dy + dy2, None
+        g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3], dy2)
         dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gamma, gsum)
         wt, gt, bt = ctx.dtypes
-        return None, dw.to(wt), dg.to(gt), db.to(bt), None, None, None, None, None
+        return None, dw.to(wt), dg.to(gt), db.to(bt), None, None, None, None, None, None
 
 
 def stem_ok(x: torch.Tensor, conv, bn) -> bool:
@@ -63,7 +69,9 @@ def stem_ok(x: torch.Tensor, conv, bn) -> bool:
             and (bn.training or not (torch.is_grad_enabled() and w.requires_grad)))
 
 
-def stem_conv_bn_relu_pool(x: torch.Tensor, conv, bn) -> torch.Tensor:
-    """``max_pool2d(bn(conv(x)), 3, 2, 1)`` for the ResNet stem (``bn`` a ReLU BatchNormAct2d)."""
+def stem_conv_bn_relu_pool(x: torch.Tensor, conv, bn, link=None) -> torch.Tensor:
+    """``max_pool2d(bn(conv(x)), 3, 2, 1)`` for the ResNet stem (``bn`` a ReLU BatchNormAct2d).
+    ``link`` (ops.bn.ResidualLink): a consumer of the output may park a second output gradient
+    there (ops.bn.link_tap); the backward sums it on load."""
     return _StemFn.apply(x, conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                         bn.eps, bn.momentum, bn.training)
+                         bn.eps, bn.momentum, bn.training, link)

@@ -493,10 +493,18 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype) {
   return dw;
 }
 
-// 3x3/s2/p1 max-pool backward + per-channel sums of the result: {dx, sums fp32 [C]}.
-std::vector<Tensor> maxpool_bwd_sum(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W) {
+// 3x3/s2/p1 max-pool backward + per-channel sums of the result: {dx, sums fp32 [C]}. dy2: an
+// optional second output gradient of dy's shape, summed on load.
+std::vector<Tensor> maxpool_bwd_sum(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W,
+                                    const optional<Tensor>& dy2_in) {
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc(dy, "dy");
+  Tensor dy2;
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = dy2_in->contiguous(at::MemoryFormat::ChannelsLast);
+    check_nhwc(dy2, "dy2");
+    TORCH_CHECK(dy2.sizes() == dy.sizes() && dy2.device() == dy.device(), "maxpool_bwd_sum: dy2");
+  }
   const int64_t N = dy.size(0), C = dy.size(1), OH = dy.size(2), OW = dy.size(3);
   TORCH_CHECK(OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1, "maxpool_bwd_sum: 3x3/s2/p1 shapes");
   TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == dy.numel(), "maxpool_bwd_sum: idx");
@@ -505,7 +513,9 @@ std::vector<Tensor> maxpool_bwd_sum(const Tensor& dy_in, const Tensor& idx, int6
   Tensor sums = at::empty({C}, dy.options().dtype(at::kFloat));
   const size_t wb = cml::maxpool_bwd_sum_workspace_bytes(N, H, W, C);
   Tensor work = at::empty({static_cast<int64_t>(wb / 4 + 1)}, dy.options().dtype(at::kFloat));
-  CML_CHECK_HIP(cml::launch_maxpool_bwd_sum(dy.data_ptr(), idx.data_ptr(), dx.data_ptr(),
+  CML_CHECK_HIP(cml::launch_maxpool_bwd_sum(dy.data_ptr(),
+                                            dy2.defined() ? dy2.data_ptr() : nullptr,
+                                            idx.data_ptr(), dx.data_ptr(),
                                             sums.data_ptr<float>(), work.data_ptr(), N, H, W, C,
                                             OH, OW, cur_stream()));
   return {dx, sums};
@@ -911,7 +921,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
   m.def("wgrad1x1", &wgrad1x1, "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
-  m.def("maxpool_bwd_sum", &maxpool_bwd_sum, "3x3/s2 max-pool backward + channel sums of dx");
+  m.def("maxpool_bwd_sum", &maxpool_bwd_sum, "3x3/s2 max-pool backward + channel sums of dx",
+        py::arg("dy"), py::arg("idx"), py::arg("H"), py::arg("W"), py::arg("dy2") = py::none());
   m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");
   m.def("pad_c4", &pad_c4, "NHWC bf16 channel zero-padding to 4");
   m.def("ce_fwd", &ce_fwd, "fused cross-entropy forward over bf16 logits (lse, per-row loss)");

@@ -127,11 +127,12 @@ struct MultiCopyArgs {
 hipError_t launch_multi_copy(const MultiCopyArgs& args, hipStream_t stream);
 
 // 3x3/s2/p1 max-pool backward that also returns the channel sums of dx (fp32 [C]; the stem BN's
-// dbeta). work: maxpool_bwd_sum_workspace_bytes.
+// dbeta). dy2 (nullable): a second output gradient, summed on load. work:
+// maxpool_bwd_sum_workspace_bytes.
 size_t maxpool_bwd_sum_workspace_bytes(int N, int H, int W, int C);
-hipError_t launch_maxpool_bwd_sum(const void* dy, const void* idx, void* dx, float* sums,
-                                  void* work, int N, int H, int W, int C, int OH, int OW,
-                                  hipStream_t stream);
+hipError_t launch_maxpool_bwd_sum(const void* dy, const void* dy2, const void* idx, void* dx,
+                                  float* sums, void* work, int N, int H, int W, int C, int OH,
+                                  int OW, hipStream_t stream);
 // Stem: y = maxpool(relu(bn(x))) with the BN affine (training statistics from launch_bn_stats,
 // or running statistics) applied to every window tap; idx as launch_maxpool_fwd.
 hipError_t launch_bn_stats(const void* x, int64_t M, int C, float* mean, float* invstd,

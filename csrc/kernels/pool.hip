@@ -297,7 +297,11 @@ __global__ __launch_bounds__(kPB) void maxpool_bwd_kernel(const bf16* __restrict
 // dx it writes, this one ~1.5.
 // part (optional): per-workgroup channel sums of dx, [gridDim.y * gridDim.x][C] (the stem's
 // BatchNorm dbeta, so its backward needs no separate reduction pass).
+// dy2 (optional): a second gradient of the pool output, summed on load (ResNet layer1.0's
+// downsample conv reads the pool output too; its data gradient arrives here instead of through
+// an elementwise add pass).
 __global__ __launch_bounds__(kPB) void maxpool_bwd_k3s2_kernel(const bf16* __restrict__ dy,
+                                                              const bf16* __restrict__ dy2,
                                                               const uint8_t* __restrict__ idx,
                                                               bf16* __restrict__ dx, int N, int H,
                                                               int W, int C, int OH, int OW,
@@ -325,6 +329,12 @@ __global__ __launch_bounds__(kPB) void maxpool_bwd_k3s2_kernel(const bf16* __res
                            (ok[a][b] ? ow : 0)) * C + 8 * g;
         m[a][b] = *reinterpret_cast<const uint2*>(idx + o);
         load_vec<bf16, 8>(dy + o, d[a][b]);
+        if (dy2) {
+          float e[8];
+          load_vec<bf16, 8>(dy2 + o, e);
+#pragma unroll
+          for (int v = 0; v < 8; ++v) d[a][b][v] += e[v];
+        }
       }
 #pragma unroll
     for (int dh = 0; dh < 2; ++dh) {
@@ -493,7 +503,7 @@ hipError_t launch_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, 
   if (N * H < 1) return hipErrorInvalidValue;
   if (k == 3 && s == 2 && p == 1) {
     maxpool_bwd_k3s2_kernel<<<pgrid(((W + 1) / 2) * (C / 8), N * ((H + 1) / 2)), kPB, 0, st>>>(
-        reinterpret_cast<const bf16*>(dy), reinterpret_cast<const uint8_t*>(idx),
+        reinterpret_cast<const bf16*>(dy), nullptr, reinterpret_cast<const uint8_t*>(idx),
         reinterpret_cast<bf16*>(dx), N, H, W, C, OH, OW, nullptr);
     return hipGetLastError();
   }
@@ -532,16 +542,17 @@ size_t maxpool_bwd_sum_workspace_bytes(int N, int H, int W, int C) {
   return (static_cast<size_t>(gx) * gy + kFold1) * C * sizeof(float);
 }
 
-hipError_t launch_maxpool_bwd_sum(const void* dy, const void* idx, void* dx, float* sums,
-                                  void* work, int N, int H, int W, int C, int OH, int OW,
-                                  hipStream_t st) {
+hipError_t launch_maxpool_bwd_sum(const void* dy, const void* dy2, const void* idx, void* dx,
+                                  float* sums, void* work, int N, int H, int W, int C, int OH,
+                                  int OW, hipStream_t st) {
   if (C % 8 || C > kPB || kPB % C || N * H < 1) return hipErrorInvalidValue;
   const int gx = ((((W + 1) / 2) * (C / 8)) + kPB - 1) / kPB;
   const int rows = N * ((H + 1) / 2);
   const int gy = rows < kSumRows ? rows : kSumRows;
   float* part = reinterpret_cast<float*>(work);
   maxpool_bwd_k3s2_kernel<<<dim3(gx, gy), kPB, 0, st>>>(
-      reinterpret_cast<const bf16*>(dy), reinterpret_cast<const uint8_t*>(idx),
+      reinterpret_cast<const bf16*>(dy), reinterpret_cast<const bf16*>(dy2),
+      reinterpret_cast<const uint8_t*>(idx),
       reinterpret_cast<bf16*>(dx), N, H, W, C, OH, OW, part);
   float* part2 = part + static_cast<int64_t>(gx) * gy * C;
   colsum_fold_rows_kernel<<<kFold1, kPB, 0, st>>>(part, gx * gy, C, part2);

@@ -140,3 +140,41 @@ def test_stem_kernels_exact(cuda, N, C, H, W):
     wq = w.double().requires_grad_(True)
     F.conv2d(x.double(), wq, stride=2, padding=3).backward(dz)
     assert _rel(dw.double(), wq.grad) < 5e-3                 # g - mean(g) and xhat staged as bf16
+
+
+def test_stem_pool_link_second_gradient(cuda):
+    """layer1.0's downsample data gradient parked on the stem's pool link and summed inside the
+    pool backward (kernel dy2) instead of by an autograd add of the two bf16 gradients: both
+    paths measured against the same model in fp32 (the stem gradients sit under 50 bf16 layers,
+    so the yardstick is the add path's own distance to fp32)."""
+    import copy
+
+    import consensusml_amd.models.resnet as R
+    from consensusml_amd.ops.bn import TAP_STATS
+    torch.manual_seed(0)
+    m32 = R.resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    m = copy.deepcopy(m32).to(torch.bfloat16)
+    x = torch.randn(8, 3, 96, 96, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device=cuda)
+    F.cross_entropy(m32(x.float()), y).backward()
+    ref = [m32.conv1.weight.grad, m32.bn1.weight.grad, m32.bn1.bias.grad]
+    out = {}
+    for on in (True, False):
+        R.POOL_LINK = on
+        TAP_STATS.update(parked=0, fallback=0)
+        try:
+            m.zero_grad(set_to_none=True)
+            F.cross_entropy(m(x).float(), y).backward()
+            out[on] = [m.conv1.weight.grad.float().clone(), m.bn1.weight.grad.float().clone(),
+                       m.bn1.bias.grad.float().clone()]
+            stats = dict(TAP_STATS)
+        finally:
+            R.POOL_LINK = True
+        assert stats["fallback"] == 0
+        if on:
+            assert stats["parked"] >= 1
+    for a, b, r in zip(out[True], out[False], ref):
+        e_on, e_off = _rel(a, r), _rel(b, r)
+        print(f"rel err vs fp32: link {e_on:.4f}, add {e_off:.4f}, link vs add {_rel(a, b):.4f}")
+        assert e_on <= max(1.5 * e_off, 0.1), (e_on, e_off)
