@@ -13,9 +13,19 @@ and ``agg_overhead_vs_allreduce`` = (t_krum - t_allreduce) / t_allreduce is repo
 
 Data: synthetic ImageNet-shaped batches (random bf16 images, random labels) generated on
 device; random-init weights. Every timed step runs the full forward, backward, exchange,
-aggregation and optimizer update. Per-GPU batch 2048 by default: 288 GB of HBM holds it many times
-over (peak ~81 GiB), and throughput still rises with batch (512 ~11.5k, 1024 ~12.0k, 1536
-~12.1-12.4k, 2048 ~12.3k samples/s: larger conv / GEMM problems, fewer fixed per-step costs).
+aggregation and optimizer update. Per-GPU batch 2048 by default: 288 GB of HBM holds it many
+times over (peak ~81 GiB), and throughput still rises with batch (larger conv / GEMM problems,
+fewer fixed per-step costs).
+
+Robust aggregation at one GPU. With one rank there is one worker, so the dp line's Krum is
+vacuous there (n = 1, f = 0, nothing exchanged). At N = 1 the bench therefore also runs a
+*virtual-worker* block: 8 workers x 256 images on the one GPU (each worker's gradient kept in its
+own row, n = 8, f = 2): real Krum (MFMA Gram -> scores -> selection -> fused weighted update)
+against the plain mean of the same 8 micro-batch gradients at the same global batch, reported
+as ``krum_n8_virtual_*`` keys. At N > 1 the JSON carries ``dist_backend``, ``world_size_seen``,
+the exchange + aggregation + update time per step that is NOT hidden behind backward (HIP
+events around ``engine.step()``) and a cross-rank bitwise parameter-checksum check
+(``replicas_identical``).
 """
 from __future__ import annotations
 
@@ -37,17 +47,25 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=2048,
-                    help="per-GPU batch (samples/s on MI355X: 512 ~11.5k, 1024 ~12.0k, 1536 "
-                         "~12.1-12.4k, 2048 ~12.3k, profiles/r01_bench55/66/69_b*.json; peak memory "
-                         "~81 GiB at 2048 of 288; the shipped MIOpen find-db covers all four)")
+                    help="per-GPU batch (samples/s on MI355X rise with batch, see README; peak "
+                         "memory ~81 GiB at 2048 of 288; the shipped MIOpen find-db covers "
+                         "256 / 512 / 1024 / 1536 / 2048)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--rule", default="krum")
-    ap.add_argument("--f", type=int, default=-1, help="Byzantine tolerance (-1: (n-3)//2)")
+    ap.add_argument("--f", type=int, default=-1,
+                    help="Byzantine tolerance of the dp run (-1: the largest f with n >= 2f+3, "
+                         "at least 1 once n >= 4)")
     ap.add_argument("--topology", default="sharded")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--no-baseline", action="store_true")
     ap.add_argument("--baseline-steps", type=int, default=-1)
+    ap.add_argument("--virtual-workers", type=int, default=-1,
+                    help="workers of the virtual-worker Krum block (-1: 8 at N = 1, off at N > 1; "
+                         "0: off)")
+    ap.add_argument("--virtual-batch", type=int, default=256, help="images per virtual worker")
+    ap.add_argument("--virtual-f", type=int, default=2)
+    ap.add_argument("--virtual-steps", type=int, default=-1, help="-1: same as --steps")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse "
@@ -63,18 +81,39 @@ def parse():
     return ap.parse_args()
 
 
-def run(args, rule: str, topology: str, steps: int, warmup: int, info):
+def default_f(n: int) -> int:
+    """Largest f with Krum's n >= 2f + 3, but at least 1 once n >= 4 (n > 2f + 1 keeps one
+    nearest neighbour in every score)."""
+    if n < 4:
+        return 0
+    return max(1, (n - 3) // 2)
+
+
+def param_checksum(flat_param: torch.Tensor) -> torch.Tensor:
+    """Exact position-weighted int64 checksum of the parameter bits (equal iff bit-identical,
+    up to a negligible collision chance)."""
+    bits = flat_param.view(torch.int16).to(torch.int64)
+    idx = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 65521 + 1
+    return torch.stack([(bits * idx).sum(), bits.sum()])
+
+
+def run(args, rule: str, topology: str, steps: int, warmup: int, info, *, V: int = 1,
+        batch: int = 0, f: int = -1):
     from consensusml_amd.parallel.dist import barrier
     from consensusml_amd import TrainConfig
     from consensusml_amd.trainer.trainer import ConsensusTrainer
-    n = info.world
+    batch = batch or args.batch
+    n = info.world * V
     cfg = TrainConfig()
     cfg.model.name = args.model
     cfg.model.image_size = args.image_size
-    cfg.batch_per_worker = args.batch
+    cfg.batch_per_worker = batch
+    cfg.virtual_workers = V
     cfg.dtype = "bf16"
     cfg.agg.rule = rule
-    cfg.agg.f = args.f if args.f >= 0 else max(0, (n - 3) // 2)
+    cfg.agg.f = f if f >= 0 else (args.f if args.f >= 0 else default_f(n))
+    if rule == "mean":
+        cfg.agg.f = 0
     cfg.topology.kind = topology
     cfg.topology.bucket_mb = args.bucket_mb
     cfg.topology.overlap = not args.no_overlap
@@ -84,29 +123,44 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info):
     cfg.optim.weight_decay = 5e-5
     tr = ConsensusTrainer(cfg, info=info)
     dev = info.device
-    # pre-generate a few synthetic batches (data generation is not part of the step)
+    # pre-generate a few synthetic batches per worker (data generation is not part of the step)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + info.rank)
-    batches = [tr.task.make_batch(args.batch, gen) for _ in range(2)]
+    batches = [[tr.task.make_batch(batch, gen) for _ in range(V)] for _ in range(2)]
     model, eng = tr.model, tr.engine
+    tag = f"{rule}/{topology}" + (f" V={V}x{batch}" if V > 1 else "")
+    ev = []
 
-    def step(i):
+    def step(i, timed=False):
         eng.zero_grad()
-        loss = tr.task.loss_fn(model, batches[i % len(batches)])
-        loss.backward()
-        eng.step()
-        return loss
+        loss = None
+        for v in range(V):
+            if V > 1:
+                eng.bind_worker(v)
+            lv = tr.task.loss_fn(model, batches[i % len(batches)][v])
+            lv.backward()
+            loss = lv.detach() if loss is None else loss + lv.detach()
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            eng.step()
+            e1.record()
+            ev.append((e0, e1))
+        else:
+            eng.step()
+        return loss / V
 
     tw = time.perf_counter()
     for i in range(max(warmup, 1 if torch.backends.cudnn.benchmark else 0)):
         step(i)
         if info.rank == 0:   # progress: a cold MIOpen find for new conv shapes can take minutes
             torch.cuda.synchronize()
-            print(f"[bench] {rule}/{topology}: warmup step {i} done at {time.perf_counter() - tw:.1f}s",
+            print(f"[bench] {tag}: warmup step {i} done at {time.perf_counter() - tw:.1f}s",
                   file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if info.rank == 0:
-        print(f"[bench] {rule}/{topology}: warmup {time.perf_counter() - tw:.1f}s", file=sys.stderr,
+        print(f"[bench] {tag}: warmup {time.perf_counter() - tw:.1f}s", file=sys.stderr,
               flush=True)
     if args.profile_marker:
         torch.cuda._sleep(1000)
@@ -114,18 +168,31 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        loss = step(i)
+        loss = step(i, timed=True)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    step_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
     if info.distributed:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt, step_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt, step_ms = float(t[0].item()), float(t[1].item())
     finite = bool(torch.isfinite(loss).item())
-    res = {"dt": dt, "f": cfg.agg.f, "loss": float(loss.item()), "finite": finite,
-           "params": eng.flat.real_numel, "buckets": len(eng.flat.buckets)}
+    res = {"dt": dt, "f": cfg.agg.f, "n": n, "loss": float(loss.item()), "finite": finite,
+           "params": eng.flat.real_numel, "buckets": len(eng.flat.buckets),
+           "engine_step_ms": step_ms,
+           "selected": int((eng.w[: eng.n] > 0).sum().item()),
+           "sel_counts": [int(c) for c in eng.sel_counts.tolist()]}
+    if info.distributed:
+        # cross-rank check: every replica must hold bit-identical parameters after the run
+        cs = param_checksum(eng.flat.flat_param)
+        hi, lo = cs.clone(), cs.clone()
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        res["replicas_identical"] = bool(torch.equal(hi, lo))
+        res["world_size_seen"] = dist.get_world_size()
+        res["dist_backend"] = dist.get_backend()
     tr.close()
     del tr, eng, model, batches
     torch.cuda.empty_cache()
@@ -153,12 +220,38 @@ def main():
     ms = main_res["dt"] / args.steps * 1e3
     value = n * args.batch * args.steps / main_res["dt"]
     overhead = None
-    base_ms = None
+    base = None
     if not args.no_baseline:
         bsteps = args.baseline_steps if args.baseline_steps > 0 else args.steps
         base = run(args, "mean", "allreduce", bsteps, args.warmup, info)
-        base_ms = base["dt"] / bsteps * 1e3
-        overhead = (ms - base_ms) / base_ms
+        base["ms"] = base["dt"] / bsteps * 1e3
+        overhead = (ms - base["ms"]) / base["ms"]
+    V = args.virtual_workers if args.virtual_workers >= 0 else (8 if n == 1 else 0)
+    virt = {}
+    if V > 1:
+        vsteps = args.virtual_steps if args.virtual_steps > 0 else args.steps
+        vb = args.virtual_batch
+        kr = run(args, "krum", "sharded", vsteps, args.warmup, info, V=V, batch=vb,
+                 f=args.virtual_f)
+        mn = run(args, "mean", "sharded", vsteps, args.warmup, info, V=V, batch=vb, f=0)
+        k_ms = kr["dt"] / vsteps * 1e3
+        m_ms = mn["dt"] / vsteps * 1e3
+        tag = f"krum_n{kr['n']}_virtual"
+        virt = {
+            f"{tag}_samples_per_s": round(n * V * vb * vsteps / kr["dt"], 2),
+            f"{tag}_ms_per_step": round(k_ms, 3),
+            f"{tag}_mean_ms_per_step": round(m_ms, 3),
+            f"{tag}_overhead": round((k_ms - m_ms) / m_ms, 4),
+            f"{tag}_engine_step_ms": round(kr["engine_step_ms"], 3),
+            f"{tag}_mean_engine_step_ms": round(mn["engine_step_ms"], 3),
+            f"{tag}_config": {"workers": kr["n"], "f": kr["f"], "per_worker_batch": vb,
+                              "global_batch": n * V * vb, "rule": "krum",
+                              "baseline": "mean of the same worker rows (same engine, same "
+                                          "fused SGD)",
+                              "selected_last_step": kr["selected"],
+                              "selection_counts": kr["sel_counts"]},
+            f"{tag}_loss_finite": kr["finite"] and mn["finite"],
+        }
     if info.rank == 0:
         out = {
             "metric": METRIC,
@@ -179,12 +272,20 @@ def main():
                        "topology": args.topology, "optimizer": "sgd-momentum (fused HIP)",
                        "conv1x1": args.conv1x1,
                        "params": main_res["params"], "buckets": main_res["buckets"]},
-            "allreduce_ms_per_step": None if base_ms is None else round(base_ms, 3),
+            "allreduce_ms_per_step": None if base is None else round(base["ms"], 3),
             "agg_overhead_vs_allreduce": None if overhead is None else round(overhead, 4),
+            "engine_step_ms": round(main_res["engine_step_ms"], 3),
+            "allreduce_engine_step_ms": None if base is None else round(base["engine_step_ms"], 3),
             "loss_finite": main_res["finite"],
             "peak_mem_gib": (round(torch.cuda.max_memory_allocated() / 2**30, 1)
                              if torch.cuda.is_available() else None),
         }
+        if info.distributed:
+            out["dist_backend"] = main_res["dist_backend"]
+            out["world_size_seen"] = main_res["world_size_seen"]
+            out["replicas_identical"] = main_res["replicas_identical"] and (
+                base is None or base["replicas_identical"])
+        out.update(virt)
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

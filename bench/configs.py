@@ -44,6 +44,21 @@ CONFIGS = {
 }
 
 
+def default_f(rule: str, n: int) -> int:
+    """Byzantine tolerance used when --f is not given: never 0 once the rule can tolerate a
+    fault (a robust rule at f = 0 is plain averaging, e.g. Multi-Krum at m = n).
+      trimmed_mean   trim (n - 1) // 2 - 1, at least 1 for n >= 3 (n > 2 trim)
+      krum / multi_krum / bulyan / others   largest f with n >= 2f + 3, at least 1 for n >= 4
+    """
+    if rule in ("mean", "median", "geomed"):
+        return 0
+    if rule == "trimmed_mean":
+        return max(1, (n - 1) // 2 - 1) if n >= 3 else 0
+    if rule == "bulyan":
+        return max(0, (n - 3) // 4)
+    return max(1, (n - 3) // 2) if n >= 4 else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", choices=sorted(CONFIGS), required=True)
@@ -78,8 +93,7 @@ def main():
     cfg.virtual_workers = a.virtual_workers
     n = info.world * a.virtual_workers
     cfg.agg.rule = c["rule"]
-    cfg.agg.f = a.f if a.f >= 0 else (max(0, (n - 1) // 2 - 1) if c["rule"] == "trimmed_mean"
-                                     else max(0, (n - 3) // 2))
+    cfg.agg.f = a.f if a.f >= 0 else default_f(c["rule"], n)
     cfg.topology.kind = c["topology"]
     cfg.topology.bucket_mb = c.get("bucket_mb", 64)
     cfg.topology.gossip_async = c.get("gossip_async", False)

@@ -45,6 +45,11 @@ class AggConfig:
     def validate(self, n: int) -> None:
         if self.rule not in RULES:
             raise ValueError(f"unknown aggregation rule {self.rule!r}; choose from {RULES}")
+        # the HIP kernels keep one worker row per lane of a 64-wide wave; centered clipping adds
+        # the previous aggregate as row n
+        limit = 63 if self.rule == "centered_clip" else 64
+        if n > limit:
+            raise ValueError(f"{self.rule} supports at most {limit} workers (n={n})")
         if self.rule in ("krum", "multi_krum") and n > 1 and n <= 2 * self.f:
             # Krum's guarantee needs n >= 2f+3; smaller n runs (nearest-neighbour scoring) but
             # f < n/2 is the hard floor.

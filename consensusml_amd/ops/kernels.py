@@ -38,7 +38,7 @@ def sorted_range(rule: str, n: int, trim: int = 0) -> Tuple[int, int]:
 @dataclass
 class OptArgs:
     """Hyper-parameters of one fused optimizer step (SGD or Adam/AdamW)."""
-    kind: str = "sgd"            # none | sgd | adam
+    kind: str = "sgd"            # none | sgd | adam (L2 weight decay) | adamw (decoupled)
     lr: float = 0.1
     momentum: float = 0.0
     weight_decay: float = 0.0
@@ -51,7 +51,7 @@ class OptArgs:
     gscale: float = 1.0
 
     def opt_id(self) -> int:
-        return {"none": 0, "sgd": 1, "adam": 2, "adamw": 2}[self.kind]
+        return {"none": 0, "sgd": 1, "adamw": 2, "adam": 3 if self.weight_decay else 2}[self.kind]
 
 
 def _as2d(X: torch.Tensor) -> torch.Tensor:
@@ -109,7 +109,7 @@ def agg_update(X: torch.Tensor, *, combine: str, lo: int = 0, cnt: int = 1,
             s1[:D].copy_(b)
     else:
         p, m, v = ref.adam_update(master[:D], g, s1[:D], s2[:D], opt.step, opt.lr, opt.beta1,
-                                  opt.beta2, opt.eps, opt.weight_decay, decoupled=True)
+                                  opt.beta2, opt.eps, opt.weight_decay, decoupled=(k == 2))
         master[:D].copy_(p)
         s1[:D].copy_(m)
         s2[:D].copy_(v)

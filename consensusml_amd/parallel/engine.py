@@ -93,6 +93,7 @@ class ConsensusEngine:
             self.nb_right = torch.empty_like(fl.flat_param)
         self._gossip_reqs = None
         self._send_buf = None
+        self._gossip_restored = False   # neighbour buffers restored from a checkpoint
         # -------------------------------------------------- rule buffers
         self.G = torch.zeros(self.rows_total, self.rows_total, dtype=torch.float64, device=dev)
         self.w = torch.full((self.rows_total,), 1.0 / self.n, dtype=torch.float32, device=dev)
@@ -292,8 +293,9 @@ class ConsensusEngine:
     # ================================================================ optimizer args
     def _opt_args(self, gscale: float = 1.0) -> K.OptArgs:
         o = self.cfg.optim
-        kind = "sgd" if o.name == "sgd" else "adam"
+        kind = o.name if o.name in ("sgd", "adam", "adamw") else "adamw"
         wd = o.weight_decay
+        # 'adam' = torch.optim.Adam (L2 term in the gradient), 'adamw' = decoupled decay
         return K.OptArgs(kind=kind, lr=o.lr, momentum=o.momentum if kind == "sgd" else 0.0,
                          weight_decay=wd, nesterov=o.nesterov, first=self.step_count == 0,
                          beta1=o.betas[0], beta2=o.betas[1], eps=o.eps,
@@ -461,10 +463,9 @@ class ConsensusEngine:
             # Delayed gossip: mix with the neighbour parameters that arrived during THIS step's
             # compute (sent at the end of the previous step), then snapshot the new local
             # parameters and start the next exchange, which overlaps the next forward/backward.
-            if self._gossip_reqs is not None:
-                for rq in self._gossip_reqs:
-                    for w in rq:
-                        w.wait()
+            if self._gossip_reqs is not None or self._gossip_restored:
+                self._drain_gossip()
+                self._gossip_restored = False
                 K.gossip_mix(self.master, self.nb_left, self.nb_right, w0, w1, w2, clip,
                              param_out=fl.flat_param)
             if self._send_buf is None:
@@ -492,10 +493,25 @@ class ConsensusEngine:
                          clip, param_out=fl.flat_param[s:e])
             reqs = nxt
 
+    def _drain_gossip(self) -> None:
+        if self._gossip_reqs is not None:
+            for rq in self._gossip_reqs:
+                for w in rq:
+                    w.wait()
+            self._gossip_reqs = None
+
     # ================================================================ state
     def state_dict(self) -> dict:
         sd = {"master": self.master, "step": self.step_count, "sel_counts": self.sel_counts,
               "rank": self.rank, "world": self.N, "topology": self.topo}
+        if self.topo == "gossip" and self.cfg.topology.gossip_async and \
+                (self._gossip_reqs is not None or self._gossip_restored):
+            # delayed gossip: the exchange started at the end of the last step is part of the
+            # state (the next step mixes with it); finish it and save what arrived
+            self._drain_gossip()
+            self._gossip_restored = True
+            sd["gossip_left"] = self.nb_left
+            sd["gossip_right"] = self.nb_right
         if self.s1 is not None:
             sd["s1"] = self.s1
         if self.s2 is not None:
@@ -516,6 +532,11 @@ class ConsensusEngine:
         self.sel_counts.copy_(sd["sel_counts"])
         if "v0" in sd and self.gout is not None:
             self.gout.copy_(sd["v0"])
+        if "gossip_left" in sd and self.topo == "gossip":
+            self._drain_gossip()
+            self.nb_left.copy_(sd["gossip_left"])
+            self.nb_right.copy_(sd["gossip_right"])
+            self._gossip_restored = True
         self.sync_params_from_master()
 
     def sync_params_from_master(self) -> None:
@@ -532,11 +553,7 @@ class ConsensusEngine:
             fl.flat_param.copy_(self.master.to(fl.dtype))
 
     def close(self) -> None:
-        if self._gossip_reqs is not None:     # drain the in-flight delayed-gossip exchange
-            for rq in self._gossip_reqs:
-                for w in rq:
-                    w.wait()
-            self._gossip_reqs = None
+        self._drain_gossip()     # the in-flight delayed-gossip exchange
         for h in self._hooks:
             h.remove()
         self._hooks = []

@@ -43,14 +43,18 @@ def apply_faults(G: torch.Tensor, cfg: FaultConfig, rank: int, step: int,
         return
     sl = cols if cols is not None else slice(None)
     if cfg.kind in ELEMENTWISE:
+        # bucket-wise injection (overlap / early update): the column offset enters the seed so
+        # every bucket gets its own noise stream instead of a repeat of the first one
+        col0 = (cols.start or 0) if cols is not None else 0
         for r in bad:
             g = G[r, sl]
+            sd = seed * 1000003 + rank * 131 + r + col0 * 7919
             if not g.is_contiguous():
                 tmp = g.contiguous()
-                inject_fault(tmp, cfg.kind, cfg.scale, cfg.sigma, seed * 1000003 + rank * 131 + r)
+                inject_fault(tmp, cfg.kind, cfg.scale, cfg.sigma, sd)
                 g.copy_(tmp)
             else:
-                inject_fault(g, cfg.kind, cfg.scale, cfg.sigma, seed * 1000003 + rank * 131 + r)
+                inject_fault(g, cfg.kind, cfg.scale, cfg.sigma, sd)
         return
     if cfg.kind in COLLUSION:
         honest = [r for r in range(rows) if r not in bad]

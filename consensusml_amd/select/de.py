@@ -178,7 +178,8 @@ def top_table(eb, genes: Sequence[str], p_cut: float = 0.05, lfc: float = 1.0,
 def voom_de(counts: torch.Tensor, groups: Sequence[int], genes: Sequence[str],
             min_frac: float = 0.05, p_cut: float = 0.05, lfc: float = 1.0) -> pd.DataFrame:
     """CPM filter (> 5 % of samples) -> TMM -> voom -> WLS -> contrast (group1 - group0) ->
-    eBayes -> topTable(BH, p < 0.05, |lfc| > 1)."""
+    eBayes -> topTable(BH, p < 0.05, |lfc| > 1, sort.by = "P") as in
+    JSmith_code/Limma_Voom_DE_Function.R:27-42."""
     keep = filter_by_cpm(counts, 1.0, None, min_frac)
     cnt = counts[keep]
     g = [x for x, k in zip(genes, keep.tolist()) if k]
@@ -189,4 +190,4 @@ def voom_de(counts: torch.Tensor, groups: Sequence[int], genes: Sequence[str],
     v = voom(cnt, design, lib)
     fit = lm_fit(v["E"], design, v["weights"])
     fit = contrast(fit, [-1.0, 1.0])
-    return top_table(e_bayes(fit), g, p_cut, lfc)
+    return top_table(e_bayes(fit), g, p_cut, lfc, sort_by="P.Value")

@@ -101,13 +101,23 @@ def effective_lib_sizes(counts: torch.Tensor, factors: Optional[torch.Tensor] = 
 
 def filter_by_cpm(counts: torch.Tensor, min_cpm: float = 1.0, min_samples: Optional[int] = 5,
                   min_frac: Optional[float] = None) -> torch.Tensor:
-    """Boolean gene mask: CPM >= min_cpm in >= max(min_samples, min_frac * n) samples."""
+    """Boolean gene mask on the number k of samples with CPM >= min_cpm.
+
+    * ``min_samples`` only: k >= min_samples (make_seobj_targetaml.R:88-91, "in >= 5 samples").
+    * ``min_frac`` only: k > min_frac * n, a strict comparison against the non-integer bound,
+      exactly ``rowSums(cpm(dge) >= 1) > (0.05*ncol(counts.df))`` of
+      JSmith_code/Limma_Voom_DE_Function.R:27 (n = 100 needs 6 samples, not 5).
+    * both: both conditions.
+    """
     c = cpm(counts)
     n = counts.shape[1]
-    need = min_samples or 0
+    k = (c >= min_cpm).sum(1)
+    keep = torch.ones_like(k, dtype=torch.bool)
+    if min_samples:
+        keep &= k >= min_samples
     if min_frac is not None:
-        need = max(need, int(min_frac * n))
-    return (c >= min_cpm).sum(1) >= need
+        keep &= k.double() > min_frac * n
+    return keep
 
 
 def normalize(es, min_cpm: float = 1.0, min_samples: int = 5, prior_count: float = 1.0):

@@ -52,6 +52,9 @@ void agg_update(const Tensor& X, int64_t n, int64_t D, const optional<Tensor>& r
   check_dev(X, "X");
   TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "X must be 2-D with unit column stride");
   TORCH_CHECK(n >= 1 && n <= 64, "1 <= n <= 64 workers supported, got ", n);
+  // opt 3 = Adam with the L2 term added to the gradient (torch.optim.Adam semantics)
+  const int adam_l2 = opt == 3 ? 1 : 0;
+  if (adam_l2) opt = cml::OPT_ADAM;
   TORCH_CHECK(D >= 0 && D <= X.size(1), "D out of range");
   const c10::DeviceGuard guard(X.device());
   cml::SrcArgs s{};
@@ -87,6 +90,7 @@ void agg_update(const Tensor& X, int64_t n, int64_t D, const optional<Tensor>& r
   u.gscale = static_cast<float>(gscale);
   u.nesterov = nesterov ? 1 : 0;
   u.first = first ? 1 : 0;
+  u.adam_l2 = adam_l2;
   CML_CHECK_HIP(cml::launch_agg_update(dtype_of(X), static_cast<int>(combine), static_cast<int>(opt),
                                        s, u, D, cur_stream()));
 }

@@ -77,10 +77,15 @@ __device__ __forceinline__ void update_and_store(const UpdArgs& u, int opt, int6
     }
 #pragma unroll
     for (int v = 0; v < VEC; ++v) p[v] = fmaf(-u.lr, g[v], p[v]);
-  } else {  // OPT_ADAM (decoupled weight decay when weight_decay != 0)
+  } else {  // OPT_ADAM: decoupled weight decay (AdamW), or the L2 term of Adam (adam_l2)
     float (&m)[VEC] = st.a;
     float (&s)[VEC] = st.b;
-    const float decay = 1.0f - u.lr * u.weight_decay;
+    float decay = 1.0f - u.lr * u.weight_decay;
+    if (u.adam_l2) {   // wave-uniform kernel argument
+      decay = 1.0f;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) g[v] = fmaf(u.weight_decay, p[v], g[v]);
+    }
 #pragma unroll
     for (int v = 0; v < VEC; ++v) {
       m[v] = fmaf(u.beta1, m[v], (1.0f - u.beta1) * g[v]);

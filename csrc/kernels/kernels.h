@@ -41,6 +41,7 @@ struct UpdArgs {
   float lr, momentum, weight_decay, beta1, beta2, eps, step_size, inv_sqrt_bc2, gscale;
   int nesterov, first;
   int param_f32;
+  int adam_l2;       // Adam: torch.optim.Adam's L2 term (g += wd p) instead of AdamW's decay
 };
 
 // Aggregate n worker vectors of length D and apply the optimizer in the same pass.

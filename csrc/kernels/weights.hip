@@ -176,8 +176,11 @@ __global__ __launch_bounds__(64) void robust_weights_kernel(int rule, const doub
     if (i <= n) a[i] = (i == n) ? 1.0 : 0.0;
     __syncthreads();
     for (int it = 0; it < iters; ++it) {
+      // a non-finite worker row contributes nothing (its a[i] stays 0); its NaN / inf Gram row
+      // must not reach gc either, or 0 * NaN poisons c^T G c for every lane (ops/reference.py
+      // centered_clip_weights zeroes the bad rows and columns the same way)
       double gc = 0.0;
-      if (i <= n)
+      if (i <= n && (i == n || !bad[i]))
         for (int j = 0; j <= n; ++j)
           if (!bad[j] || j == n) gc += G[i * N1 + j] * a[j];
       const double cgc = wave_sum(i <= n ? a[i] * gc : 0.0);
@@ -208,6 +211,7 @@ hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m,
                                  double eps, double tol, double tau, float* w, double* scores,
                                  int* sel, hipStream_t stream) {
   if (n < 1 || n > 64) return hipErrorInvalidValue;
+  if (rule == RULE_CCLIP && n > 63) return hipErrorInvalidValue;   // n + 1 rows, one per lane
   if (rule == RULE_BULYAN_SELECT && sel == nullptr) return hipErrorInvalidValue;
   robust_weights_kernel<<<1, 64, 0, stream>>>(rule, G, n, f, m, iters, eps, tol, tau, w, scores, sel);
   return hipGetLastError();

@@ -147,3 +147,25 @@ def test_channels_last_resnet_flat_views():
     lo, hi = fp.data_ptr(), fp.data_ptr() + fp.numel() * fp.element_size()
     for p in tr.model.parameters():
         assert lo <= p.data_ptr() < hi
+
+
+def test_adam_l2_vs_adamw_cpu():
+    """'adam' with weight decay is torch.optim.Adam (L2 term in the gradient), 'adamw' the
+    decoupled form; both match torch.optim on the CPU path of the fused kernel."""
+    from consensusml_amd.ops import kernels as K
+    torch.manual_seed(0)
+    D = 257
+    for kind, topt in (("adam", torch.optim.Adam), ("adamw", torch.optim.AdamW)):
+        p0 = torch.randn(D)
+        master = p0.clone()
+        s1, s2 = torch.zeros(D), torch.zeros(D)
+        ref = torch.nn.Parameter(p0.clone())
+        o = topt([ref], lr=1e-2, weight_decay=0.1, eps=1e-8)
+        for step in range(1, 4):
+            g = torch.randn(D)
+            K.agg_update(g[None], combine="weighted", n=1,
+                         opt=K.OptArgs(kind=kind, lr=1e-2, weight_decay=0.1, step=step),
+                         master=master, s1=s1, s2=s2)
+            ref.grad = g.clone()
+            o.step()
+        torch.testing.assert_close(master, ref.detach(), rtol=1e-5, atol=1e-6)

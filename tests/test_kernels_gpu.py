@@ -137,6 +137,30 @@ def test_weights_nonfinite_worker(cuda):
     assert w[2].item() == 0.0 and abs(w.sum().item() - 1.0) < 1e-6
 
 
+@pytest.mark.parametrize("bad", ["nan", "inf"])
+def test_weights_nonfinite_cclip_bulyan(cuda, bad):
+    """Centered clipping and Bulyan with a NaN / overflowed worker match the CPU oracle
+    (which zeroes the bad rows and columns) and stay finite: clipping must stay ON for the
+    honest workers."""
+    n, D = 7, 2048
+    X = _x(n, D, torch.float32, cuda, 3)
+    X[4, 17] = float(bad)
+    v0 = torch.randn(D, device=cuda) * 0.1
+    Xa = torch.cat([X, v0[None]], 0)
+    G = K.gram(Xa)
+    w = K.robust_weights(G, "centered_clip", n, tau=0.5, iters=3)
+    ref = R.centered_clip_weights(G.cpu().double(), tau=0.5, iters=3).float()
+    assert torch.isfinite(w).all()
+    assert w[4].item() == 0.0
+    torch.testing.assert_close(w.cpu(), ref, rtol=1e-5, atol=1e-6)
+    # clipping is active: weights are not the unclipped 1/n mean
+    assert (w[:n].sum() - 1.0).abs().item() > 1e-3 or w[n].abs().item() > 1e-3
+    out = K.aggregate(X, "bulyan", f=1)
+    assert torch.isfinite(out).all()
+    Xh = torch.cat([X[:4], X[5:]], 0)
+    assert (out.cpu() - Xh.cpu().median(0).values).abs().max() < (Xh.cpu().abs().max() + 1)
+
+
 def test_geomed_gram_vs_direct(cuda):
     X = _x(9, 4096, torch.float32, cuda, 5)
     X[:2] += 20.0

@@ -262,3 +262,15 @@ def test_plots(tmp_path):
     P.rep_performance({"tpr": [0.9, 0.8], "tnr": [0.8, 0.7]}, str(tmp_path / "r.png"), dpi=50)
     P.correlation_density(np.corrcoef(g.random((10, 30))), str(tmp_path / "c.png"), dpi=50)
     assert all((tmp_path / f).stat().st_size > 0 for f in ["v.png", "h.png", "b.png", "r.png", "c.png"])
+
+
+def test_cpm_filter_strict_fraction_boundary():
+    """Limma_Voom_DE_Function.R:27 keeps a gene when rowSums(cpm >= 1) > 0.05 * ncol: at n = 100
+    a gene needs 6 expressing samples (5 is not enough); at n = 90 (4.5) 5 suffice."""
+    for n, need in ((100, 6), (90, 5), (40, 3)):
+        cnt = torch.zeros(3, n, dtype=torch.float64)
+        cnt[2, :] = 1e6           # gene 2: every sample (sets library sizes ~1e6)
+        cnt[0, :need] = 100.0     # gene 0: exactly `need` samples with CPM >= 1 (~100)
+        cnt[1, :need - 1] = 100.0  # gene 1: one fewer
+        keep = N.filter_by_cpm(cnt, 1.0, None, 0.05)
+        assert keep.tolist() == [True, False, True], (n, keep.tolist())
