@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import conv as fconv
 from ..ops.bn import BatchNormAct2d, ResidualLink, bn_add_bn_relu, fused_ok, link_tap
 from ..ops.pool import bn_relu_max_pool2d, max_pool2d
 from ..ops.stem import stem_conv_bn_relu_pool, stem_ok
@@ -46,6 +47,24 @@ POOL_LINK = os.environ.get("CML_POOL_LINK", "1") == "1"
 NHWC_AVGPOOL = os.environ.get("CML_NHWC_AVGPOOL", "1") == "1"
 # stem input channels zero-padded 3 -> 4 on the GPU (see ResNet.stem)
 STEM_PAD4 = os.environ.get("CML_STEM_PAD4", "1") == "1"
+# 1x1 convs fused with their BatchNorms (ops.conv, csrc/kernels/conv1x1.hip): BN statistics in the
+# conv epilogue; conv3 applies bn2 + ReLU in its prologue (y2 never stored). Per shape, see
+# fused_conv1x1_policy.
+FUSED_CONV1X1 = os.environ.get("CML_FUSED_CONV1X1", "1") == "1"
+
+
+def fused_conv1x1_policy(cin: int, cout: int, hw_out: int, stride: int, prologue: bool) -> bool:
+    """Whether a 1x1 conv + BN runs as the fused kernel. Measured per shape at batch 2048
+    (bench/conv1x1_fused.py, profiles/r02_conv1x1_04.jsonl): the fused kernel streams x / y at
+    ~5 TB/s, so it wins wherever the conv is memory-bound (28 x 28 and larger outputs: 0.07-0.83
+    ms saved per call) and whenever it also removes bn2's apply pass (every conv3); on the
+    14 x 14 / 7 x 7 shapes with 1024+ input channels the library GEMMs (0.7-1 PFLOP/s) beat it
+    by more than the statistics pass it saves (0.03-0.14 ms)."""
+    if not FUSED_CONV1X1:
+        return False
+    if prologue:
+        return True
+    return hw_out >= 784
 
 
 def conv1x1_policy(cin: int, cout: int, hw: int):
@@ -205,8 +224,72 @@ class Bottleneck(nn.Module):
         else:
             self.down_conv = None
 
+    def _fused_ok(self, x: torch.Tensor) -> bool:
+        return (FUSED_CONV1X1 and self.training and torch.is_grad_enabled()
+                and fconv.fused_conv_ok(x, self.conv1.weight)
+                and fused_ok(x, self.bn3.weight))
+
+    def _conv_bn(self, x, conv: "Conv1x1", bn, link=None):
+        """(z, stats) of a 1x1 conv followed by a BN: fused kernel when the policy picks it, else
+        the library conv (stats None: the BN computes them)."""
+        st = conv.stride[0]
+        hw = (x.shape[2] // st) * (x.shape[3] // st)
+        if fused_conv1x1_policy(conv.in_channels, conv.out_channels, hw, st, False):
+            dg = st == 1 and conv1x1_policy(conv.in_channels, conv.out_channels, hw)[1]
+            own = st == 1 and own_wgrad_ok(conv.in_channels, conv.out_channels)
+            z, m, i = fconv.conv1x1_bn_stats(x, conv, bn, st, dg, own, link if dg else None)
+            return z, (m, i)
+        if st == 1:
+            return conv(x, res_link=link if conv.link_ok(x) else None), None
+        return conv(x), None
+
+    def _forward_fused(self, x: torch.Tensor, use_links: bool) -> torch.Tensor:
+        """Training forward with the fused conv + BN kernels (ops.conv): bn1 / bn3 / down_bn get
+        their statistics from the conv epilogues, bn2 + ReLU is applied inside conv3."""
+        if self.down_conv is None:
+            link = getattr(x, "_cml_link", None) if use_links else None
+            z1, st1 = self._conv_bn(x, self.conv1, self.bn1, link)
+            dlink = None
+        else:
+            link = None
+            dlink = ResidualLink() if use_links and self.conv1.link_ok(x) else None
+            z1, st1 = self._conv_bn(x, self.conv1, self.bn1, dlink)
+        out = self.bn1(z1, stats=st1)
+        z2 = self.conv2(out)
+        planes = self.conv3.in_channels
+        hw2 = z2.shape[2] * z2.shape[3]
+        if fused_conv1x1_policy(planes, planes * 4, hw2, 1, True):
+            st2 = fconv.bn_stats(z2, self.bn2)
+            dg = conv1x1_policy(planes, planes * 4, hw2)[1]
+            z, m3, i3 = fconv.bnrelu_conv1x1_bn_stats(z2, self.bn2, st2, self.conv3, self.bn3, dg,
+                                                      own_wgrad_ok(planes, planes * 4)
+                                                      or planes == 64)
+            st3 = (m3, i3)
+        else:
+            z, st3 = self.conv3(self.bn2(z2)), None
+        out_link = ResidualLink() if use_links else None
+        if self.down_conv is None:
+            y = self.bn3(z, residual=x, res_link=link, out_link=out_link, stats=st3)
+        else:
+            tlink = dlink if dlink is not None else \
+                (getattr(x, "_cml_pool_link", None) if use_links else None)
+            xin = link_tap(x, tlink) if tlink is not None else x
+            zd, std = self._conv_bn(xin, self.down_conv, self.down_bn)
+            stats = None if (st3 is None or std is None) else st3 + std
+            if stats is None and (st3 is not None or std is not None):
+                # one side fused, the other not: let the unfused side compute its statistics
+                y = self.bn3(z, residual=self.down_bn(zd, stats=std), out_link=out_link,
+                             stats=st3)
+            else:
+                y = bn_add_bn_relu(z, self.bn3, zd, self.down_bn, out_link, stats=stats)
+        if out_link is not None:
+            y._cml_link = out_link
+        return y
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         use_links = RESIDUAL_LINK and torch.is_grad_enabled() and self.training
+        if self._fused_ok(x):
+            return self._forward_fused(x, use_links)
         if self.down_conv is None:
             # identity block: bn3's residual gradient is parked on the link of our input (made by
             # the producing block); conv1's GEMM backward (if used) or the producer's BN backward

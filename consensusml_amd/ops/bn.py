@@ -129,11 +129,18 @@ class _BNAddBNActFn(torch.autograd.Function):
 
 
 def bn_add_bn_relu(x1: torch.Tensor, bn1: "BatchNormAct2d", x2: torch.Tensor,
-                   bn2: "BatchNormAct2d", out_link: Optional[ResidualLink] = None) -> torch.Tensor:
+                   bn2: "BatchNormAct2d", out_link: Optional[ResidualLink] = None,
+                   stats: Optional[tuple] = None) -> torch.Tensor:
     """relu(bn1(x1) + bn2(x2)) with bn1 / bn2 training-mode BatchNorms (bn1.relu applies to the
-    sum, bn2 has no ReLU). Fused path: bf16 channels_last GPU tensors of equal shape."""
+    sum, bn2 has no ReLU). Fused path: bf16 channels_last GPU tensors of equal shape. ``stats`` =
+    (mean1, invstd1, mean2, invstd2): batch statistics already computed by the producing convs
+    (training only; running statistics already updated)."""
     if (_fused_ok(x1, bn1.weight) and _fused_ok(x2, bn2.weight) and x1.shape == x2.shape
             and not bn2.relu and bn1.relu and bn1.eps == bn2.eps and bn1.momentum == bn2.momentum):
+        if stats is not None and bn1.training:
+            return _BNAddBNActFn.apply(x1, bn1.weight, bn1.bias, x2, bn2.weight, bn2.bias, None,
+                                       None, None, None, tuple(stats), bn1.eps, bn1.momentum,
+                                       False, out_link)
         stats = None
         if not bn1.training:
             stats = (bn1.running_mean.float(), torch.rsqrt(bn1.running_var.float() + bn1.eps),
@@ -165,11 +172,17 @@ def bn_act(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor,
            residual: Optional[torch.Tensor] = None, relu: bool = True, training: bool = True,
            momentum: float = 0.1, eps: float = 1e-5,
            res_link: Optional[ResidualLink] = None,
-           out_link: Optional[ResidualLink] = None) -> torch.Tensor:
+           out_link: Optional[ResidualLink] = None,
+           stats: Optional[tuple] = None) -> torch.Tensor:
     """``res_link`` / ``out_link``: see ResidualLink; only honoured on the fused path (callers
-    check ``fused_ok`` before creating links)."""
+    check ``fused_ok`` before creating links). ``stats`` = (mean, invstd): the training batch
+    statistics of x, already computed by its producer (``ops.conv``: the conv epilogue, which also
+    updated the running statistics) — only the apply pass runs."""
     if _fused_ok(x, gamma) and (residual is None or residual.is_contiguous(
             memory_format=torch.channels_last)):
+        if training and stats is not None:
+            return _BNActFn.apply(x, gamma, beta, residual, None, None, stats[0], stats[1], eps,
+                                  momentum, relu, False, res_link, out_link)
         if training:
             return _BNActFn.apply(x, gamma, beta, residual, running_mean, running_var, None, None,
                                   eps, momentum, relu, True, res_link, out_link)
@@ -216,9 +229,11 @@ class BatchNormAct2d(nn.Module):
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                 res_link: Optional[ResidualLink] = None,
-                out_link: Optional[ResidualLink] = None) -> torch.Tensor:
+                out_link: Optional[ResidualLink] = None,
+                stats: Optional[tuple] = None) -> torch.Tensor:
         return bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual,
-                      self.relu, self.training, self.momentum, self.eps, res_link, out_link)
+                      self.relu, self.training, self.momentum, self.eps, res_link, out_link,
+                      stats)
 
     def extra_repr(self) -> str:
         return f"{self.num_features}, relu={self.relu}"

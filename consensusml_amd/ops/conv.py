@@ -1,0 +1,153 @@
+"""1x1 convolutions fused with the BatchNorm around them (``csrc/kernels/conv1x1.hip``).
+
+A ResNet bottleneck is conv1 (1x1) -> bn1 + ReLU -> conv2 (3x3) -> bn2 + ReLU -> conv3 (1x1) ->
+bn3 (+ residual) + ReLU. Unfused, every training BN first re-reads its input for the batch
+statistics, and bn2's output y2 is written only to be read back by conv3. Here:
+
+* ``conv1x1_bn_stats``: the 1x1 conv (stride 1 or 2) emits the BN statistics of its output from
+  the MFMA accumulators (its BN then runs only the apply pass);
+* ``bnrelu_conv1x1_bn_stats``: conv3 reads bn2's *input* z2 and applies bn2 + ReLU while staging
+  its operand (y2 is never written or read), and emits bn3's statistics. Its backward recomputes
+  y2 on the fly inside the MFMA weight-gradient kernel (``wgrad1x1.hip`` prologue) and runs bn2's
+  backward on the data gradient.
+
+The statistics are the exact batch statistics of the bf16 conv output (sums of the rounded
+values, shifted by the running mean, folded in fp64), so the BatchNorm forward and backward are
+the ordinary training ones; running statistics are updated by the finalize kernel.
+Gradients: data gradient as a hipBLASLt GEMM (stride 1, per-shape policy of
+``models.resnet.conv1x1_policy``) or MIOpen; weight gradient on ``wgrad1x1.hip`` or MIOpen.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .native import lib
+
+
+def fused_conv_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes / layouts the fused kernel takes (else callers use the unfused path)."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 64 == 0
+            and w.shape[0] % 64 == 0 and w.shape[2] == 1 and w.shape[3] == 1)
+
+
+def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm: bool,
+           link) -> torch.Tensor:
+    """dX of a 1x1 conv (x only supplies the shape for MIOpen). GEMM path: dX = dY W, with a
+    residual gradient parked on ``link`` absorbed by the beta = 1 epilogue."""
+    N, C, H, W = x.shape
+    Co = w.shape[0]
+    if gemm and stride == 1:
+        dy2 = dy.permute(0, 2, 3, 1).reshape(N * H * W, Co)
+        w2 = w.reshape(Co, C)
+        g = link.take() if link is not None else None
+        if g is not None:
+            dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
+            if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
+                d2 = dres.addmm_(dy2, w2)
+            else:
+                d2 = torch.addmm(dres, dy2, w2)
+        else:
+            d2 = torch.mm(dy2, w2)
+        return d2.view(N, H, W, C).permute(0, 3, 1, 2)
+    dx, _, _ = torch.ops.aten.convolution_backward(
+        dy, x, w, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])
+    return dx
+
+
+def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, own: bool,
+           pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+    """dW of a 1x1 conv. ``pro`` = (sc, bi): the conv's real input is max(x * sc + bi, 0)."""
+    if own and stride == 1:
+        sc, bi = pro if pro is not None else (None, None)
+        return lib().wgrad1x1(dy, x, w.dtype, sc, bi).view_as(w)
+    if pro is not None:   # library weight gradient needs the materialised input
+        sc, bi = pro
+        x = torch.relu(x.float() * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)).to(x.dtype)
+        x = x.contiguous(memory_format=torch.channels_last)
+    _, dw, _ = torch.ops.aten.convolution_backward(
+        dy, x, w, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])
+    return dw
+
+
+class _Conv1x1BNStatsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, rmean, rvar, stride, eps, momentum, dgrad_gemm, own_wgrad, link):
+        y, mean, invstd = lib().conv1x1_bn_fwd(x, w, None, None, rmean, rmean, rvar, stride, True,
+                                               eps, momentum)
+        ctx.save_for_backward(x, w)
+        ctx.stride, ctx.dgrad_gemm, ctx.own_wgrad, ctx.link = stride, dgrad_gemm, own_wgrad, link
+        ctx.mark_non_differentiable(mean, invstd)
+        return y, mean, invstd
+
+    @staticmethod
+    def backward(ctx, dy, _dm, _di):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = _dgrad(dy, x, w, ctx.stride, ctx.dgrad_gemm, ctx.link) \
+            if ctx.needs_input_grad[0] else None
+        dw = _wgrad(dy, x, w, ctx.stride, ctx.own_wgrad) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None, None, None, None, None, None, None
+
+
+class _BNReLUConv1x1BNStatsFn(torch.autograd.Function):
+    """z3 = conv1x1(relu(bn_a(z)), w) with bn_a's batch statistics given (mean, invstd), plus the
+    statistics of z3 for the next BN. Gradients for z, bn_a's gamma / beta and w."""
+
+    @staticmethod
+    def forward(ctx, z, gamma, beta, mean, invstd, w, rmean, rvar, eps, momentum, dgrad_gemm,
+                own_wgrad):
+        sc = gamma.float() * invstd
+        bi = beta.float() - mean * sc
+        y, m3, i3 = lib().conv1x1_bn_fwd(z, w, sc, bi, rmean, rmean, rvar, 1, True, eps, momentum)
+        ctx.save_for_backward(z, gamma, beta, mean, invstd, w, sc, bi)
+        ctx.dgrad_gemm, ctx.own_wgrad = dgrad_gemm, own_wgrad
+        ctx.mark_non_differentiable(m3, i3)
+        return y, m3, i3
+
+    @staticmethod
+    def backward(ctx, dz3, _dm, _di):
+        z, gamma, beta, mean, invstd, w, sc, bi = ctx.saved_tensors
+        dz3 = dz3.contiguous(memory_format=torch.channels_last)
+        dw = _wgrad(dz3, z, w, 1, ctx.own_wgrad, (sc, bi)) if ctx.needs_input_grad[5] else None
+        dy2 = _dgrad(dz3, z, w, 1, ctx.dgrad_gemm, None)
+        dz, dg, db, _ = lib().bn_bwd(dy2, None, z, None, gamma, beta, mean, invstd, True, False)
+        return dz, dg, db, None, None, dw, None, None, None, None, None, None
+
+
+def conv1x1_bn_stats(x: torch.Tensor, conv, bn, stride: int = 1, dgrad_gemm: bool = False,
+                     own_wgrad: bool = False, link=None):
+    """(z, mean, invstd): 1x1 conv output and its training BN statistics (bn's running stats are
+    updated). ``conv`` / ``bn``: nn.Conv2d-like (weight) and BatchNormAct2d modules."""
+    return _Conv1x1BNStatsFn.apply(x, conv.weight, bn.running_mean, bn.running_var, stride,
+                                   bn.eps, bn.momentum, dgrad_gemm, own_wgrad, link)
+
+
+def bnrelu_conv1x1_bn_stats(z: torch.Tensor, bn_a, stats_a, conv, bn_b, dgrad_gemm: bool = False,
+                            own_wgrad: bool = True):
+    """(z3, mean3, invstd3) = conv(relu(bn_a(z))) + bn_b's statistics; bn_a's batch statistics
+    ``stats_a`` = (mean, invstd) from ``bn_stats``."""
+    mean, invstd = stats_a
+    return _BNReLUConv1x1BNStatsFn.apply(z, bn_a.weight, bn_a.bias, mean, invstd, conv.weight,
+                                         bn_b.running_mean, bn_b.running_var, bn_b.eps,
+                                         bn_b.momentum, dgrad_gemm, own_wgrad)
+
+
+def bn_stats(z: torch.Tensor, bn) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Training batch statistics (mean, invstd) of z; bn's running statistics are updated."""
+    return tuple(lib().bn_stats(z, bn.running_mean, bn.running_var, bn.eps, bn.momentum))
+
+
+def reference_conv1x1_bn(x: torch.Tensor, w: torch.Tensor, stride: int = 1,
+                         pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+    """fp32 PyTorch oracle: (y, mean, biased var) of y = conv1x1(f(x)) (tests)."""
+    xf = x.float()
+    if pro is not None:
+        xf = torch.relu(xf * pro[0].view(1, -1, 1, 1) + pro[1].view(1, -1, 1, 1))
+        xf = xf.to(torch.bfloat16).float()   # the kernel stages the transformed input in bf16
+    y = F.conv2d(xf, w.float(), stride=stride)
+    yb = y.to(torch.bfloat16).float()
+    return y, yb.mean((0, 2, 3)), yb.var((0, 2, 3), unbiased=False)

@@ -476,7 +476,8 @@ Tensor maxpool_bwd(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W,
 
 // dW of a stride-1 1x1 conv: dy [N, Co, H, W], x [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 1, 1]
 // in `dtype` (bf16 or fp32).
-Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype) {
+Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
+                const optional<Tensor>& pro_sc, const optional<Tensor>& pro_bi) {
   check_nhwc(x, "x");
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc(dy, "dy");
@@ -485,7 +486,11 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype) {
   TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "wgrad1x1: bf16 or fp32 output");
   const int64_t Co = dy.size(1), Ci = x.size(1);
   const int64_t P = x.numel() / Ci;
-  TORCH_CHECK(Co % 128 == 0 && Ci % 128 == 0, "wgrad1x1: channels must be multiples of 128");
+  TORCH_CHECK(Ci == 64 ? Co % 256 == 0 : (Co % 128 == 0 && Ci % 128 == 0),
+              "wgrad1x1: channels must be multiples of 128 (or Ci 64 with Co % 256 == 0)");
+  const float* sc = opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", Ci);
+  const float* bi = opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", Ci);
+  TORCH_CHECK((sc == nullptr) == (bi == nullptr), "wgrad1x1: pro_sc and pro_bi together");
   const c10::DeviceGuard guard(x.device());
   int S = 1, cps = 1;
   cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps);
@@ -493,8 +498,74 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype) {
   Tensor dw = at::empty({Co, Ci, 1, 1}, x.options().dtype(dtype));
   CML_CHECK_HIP(cml::launch_wgrad1x1(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(),
                                      dw.data_ptr(), dtype == at::kBFloat16, P,
-                                     static_cast<int>(Co), static_cast<int>(Ci), cur_stream()));
+                                     static_cast<int>(Co), static_cast<int>(Ci), sc, bi,
+                                     cur_stream()));
   return dw;
+}
+
+// Fused 1x1 conv forward (conv1x1.hip): x [N, K, H, W] NHWC bf16, w [Cout, K, 1, 1] bf16 ->
+// {y [N, Cout, OH, OW] NHWC, mean, invstd} (mean / invstd: training BN statistics of y, undefined
+// when !stats). pro_sc / pro_bi (fp32 [K]): apply max(x * sc + bi, 0) to the input on load.
+// shift / rmean / rvar: fp32 [Cout] (statistics shift, running statistics updated in place).
+std::vector<Tensor> conv1x1_bn_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& pro_sc,
+                                   const optional<Tensor>& pro_bi, const optional<Tensor>& shift,
+                                   const optional<Tensor>& rmean, const optional<Tensor>& rvar,
+                                   int64_t stride, bool stats, double eps, double momentum) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4, "conv1x1_bn_fwd: 4-D NHWC input");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 &&
+                  w.size(1) == x.size(1), "conv1x1_bn_fwd: w must be bf16 [Cout, Cin, 1, 1]");
+  TORCH_CHECK(w.is_contiguous() || w.is_contiguous(at::MemoryFormat::ChannelsLast), "w layout");
+  TORCH_CHECK(stride == 1 || stride == 2, "stride 1 or 2");
+  const int64_t N = x.size(0), K = x.size(1), H = x.size(2), W = x.size(3), Co = w.size(0);
+  TORCH_CHECK(K % 64 == 0 && Co % 64 == 0, "conv1x1_bn_fwd: channels must be multiples of 64");
+  TORCH_CHECK(stride == 1 || (H % 2 == 0 && W % 2 == 0), "stride 2 needs even H, W");
+  const int64_t OH = H / stride, OW = W / stride;
+  const int64_t M = N * OH * OW;
+  const bool pro = pro_sc.has_value() && pro_sc->defined();
+  const float* sc = opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", K);
+  const float* bi = opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", K);
+  TORCH_CHECK(!pro || bi, "pro_bi needed with pro_sc");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor y = at::empty({N, Co, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor mean, invstd, part;
+  if (stats) {
+    mean = at::empty({Co}, f32);
+    invstd = at::empty({Co}, f32);
+    part = at::empty({static_cast<int64_t>(cml::conv1x1_bn_part_floats(M, static_cast<int>(K),
+                                                                     static_cast<int>(Co), pro))}, f32);
+  }
+  CML_CHECK_HIP(cml::launch_conv1x1_bn_fwd(
+      x.data_ptr(), w.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, sc, bi,
+      opt_ptr<const float>(shift, at::kFloat, "shift", Co), M, static_cast<int>(K),
+      static_cast<int>(Co), static_cast<int>(stride), static_cast<int>(H), static_cast<int>(W),
+      stats ? mean.data_ptr<float>() : nullptr, stats ? invstd.data_ptr<float>() : nullptr,
+      stats ? opt_ptr<float>(rmean, at::kFloat, "running_mean", Co) : nullptr,
+      stats ? opt_ptr<float>(rvar, at::kFloat, "running_var", Co) : nullptr,
+      static_cast<float>(eps), static_cast<float>(momentum), cur_stream()));
+  return {y, mean, invstd};
+}
+
+// BatchNorm training statistics only: x NHWC bf16 -> {mean, invstd} (fp32 [C]); running stats
+// updated in place when given.
+std::vector<Tensor> bn_stats(const Tensor& x, const optional<Tensor>& rmean,
+                             const optional<Tensor>& rvar, double eps, double momentum) {
+  check_nhwc(x, "x");
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "bn: C must be 8 * (power of 2) <= 2048");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32);
+  Tensor work = at::empty({static_cast<int64_t>(cml::bn_workspace_bytes(M, static_cast<int>(C)) / 4 + 1)}, f32);
+  CML_CHECK_HIP(cml::launch_bn_stats(x.data_ptr(), M, static_cast<int>(C), mean.data_ptr<float>(),
+                                     invstd.data_ptr<float>(),
+                                     opt_ptr<float>(rmean, at::kFloat, "running_mean", C),
+                                     opt_ptr<float>(rvar, at::kFloat, "running_var", C),
+                                     static_cast<float>(eps), static_cast<float>(momentum),
+                                     work.data_ptr(), cur_stream()));
+  return {mean, invstd};
 }
 
 // 3x3/s2/p1 max-pool backward + per-channel sums of the result: {dx, sums fp32 [C]}. dy2: an
@@ -924,7 +995,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_wgrad", &stem_wgrad, "ResNet stem weight gradient through BN (MFMA, one pass)");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
-  m.def("wgrad1x1", &wgrad1x1, "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
+  m.def("conv1x1_bn_fwd", &conv1x1_bn_fwd,
+        "fused 1x1 conv forward (MFMA) + BN statistics epilogue + optional BN-ReLU prologue");
+  m.def("bn_stats", &bn_stats, "training BatchNorm statistics (mean, invstd) only");
+  m.def("wgrad1x1", &wgrad1x1, py::arg("dy"), py::arg("x"), py::arg("dtype"),
+        py::arg("pro_sc") = py::none(), py::arg("pro_bi") = py::none(), "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
   m.def("maxpool_bwd_sum", &maxpool_bwd_sum, "3x3/s2 max-pool backward + channel sums of dx",
         py::arg("dy"), py::arg("idx"), py::arg("H"), py::arg("W"), py::arg("dy2") = py::none());
   m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");

@@ -1,0 +1,475 @@
+// Fused 1x1 convolution forward for NHWC bf16 activations, with the BatchNorm statistics of its
+// output in the epilogue and (optionally) the producer's BatchNorm + ReLU in its prologue.
+//
+//   y[m][n] = sum_k W[n][k] * f(x[src(m)][k])         m = output pixel, n = output channel
+//   f(v)    = v                                     (plain)
+//           = max(v * sc[k] + bi[k], 0)             (PRO: the previous BN + ReLU, applied on load)
+//   src(m)  = m, or the stride-2 input pixel of m   (S2: ResNet downsample convs)
+//   part    = per-workgroup (sum, sum of squares) of (y_bf16 - shift[n]) for the BN finalize
+//
+// Why: in ResNet-50 every 1x1 conv feeds a training BatchNorm, whose statistics pass re-reads the
+// whole conv output (~2 B/elem, 8 ms of a 166 ms batch-2048 step over all BNs), and the 3x3
+// conv's BN-ReLU output y2 is written only to be read back by conv3 (4 B/elem). Here conv3 reads
+// z2 and applies bn2 + ReLU while staging, and every 1x1 conv emits its BN sums while its output
+// is still in registers; the apply pass then needs no statistics pass of its own.
+//
+// Tiling (gfx950, wave64): a 256-thread workgroup = WN x WM waves, each wave a 64 (n) x 64 (m)
+// output block = 2 x 2 v_mfma_f32_32x32x16_bf16 accumulators. The products are C^T = W * X^T so
+// the accumulator's lane index is the pixel and its 16 registers are output channels: the store is
+// four 8-B chunks per lane, and the per-channel statistics accumulate in registers across every
+// tile the workgroup visits (one cross-lane reduction per workgroup at the end). K runs in 64-wide
+// steps through 128-B LDS rows (XOR-swizzled: every ds_read_b128 lane group hits 16 distinct bank
+// slots); the next step is prefetched into registers while the current one is multiplied. W is
+// kept resident in LDS for the whole launch when it fits (its n-tile is fixed per workgroup).
+//
+// Work split: workgroups are persistent; each owns one n-tile and every wgpn-th m-tile. The
+// workgroups that share an m-tile (one per n-tile) get equal blockIdx % 8, i.e. run on one XCD
+// under round-robin placement, so x is read from HBM once and re-read from that XCD's L2 (speed
+// only: any placement is correct).
+#include "common.h"
+#include "kernels.h"
+
+namespace cml {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kBK = 64;          // K per step: one 128-B LDS row per output channel / pixel
+constexpr int kThreads = 256;    // 4 waves
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// byte offset of 16-B chunk c (0..7) of row `row` in a [rows][128 B] image. Row parity picks the
+// half of the 256-B bank row, and the XOR with row bits 1..3 spreads the 16 rows of each
+// ds_read_b128 lane group ({0-3,12-15,20-27}, ...) over 16 distinct 16-B bank slots.
+__device__ __forceinline__ int swz(int row, int c) { return row * 128 + 16 * (c ^ ((row >> 1) & 7)); }
+
+struct C1Args {
+  const uint16_t* x;      // [rows_in][K]
+  const uint16_t* w;      // [N][K]
+  uint16_t* y;            // [M][N]
+  float* part;            // [ntn][wgpn * WM][2][BN] or null
+  const float* pro_sc;    // PRO: [K]
+  const float* pro_bi;    // PRO: [K]
+  const float* shift;     // [N] or null (statistics shift, e.g. the BN running mean)
+  int M, K, N;
+  int ntn, wgpn, mtiles;
+  int H, W, OW, OHW;      // S2: input H, W; output W and H*W
+};
+
+__device__ __forceinline__ int64_t src_row(const C1Args& a, int m, bool s2) {
+  m = m < a.M ? m : a.M - 1;                                    // clamped: loads stay in bounds
+  if (s2) {
+    const int img = m / a.OHW;
+    const int rem = m - img * a.OHW;
+    const int oh = rem / a.OW;
+    const int ow = rem - oh * a.OW;
+    return static_cast<int64_t>(img) * a.H * a.W + 2 * oh * a.W + 2 * ow;
+  }
+  return m;
+}
+
+// W k-step ks of rows [n0, n0 + 32 CA) into LDS block `dst`. W is small and L2-resident, so it is
+// loaded at staging time rather than prefetched across the MFMA phase.
+template <int CA>
+__device__ __forceinline__ void stage_w(const C1Args& a, char* dst, int n0, int srow, int ch, int ks) {
+  uint4 tw[CA];
+#pragma unroll
+  for (int j = 0; j < CA; ++j)
+    tw[j] = *reinterpret_cast<const uint4*>(a.w + static_cast<int64_t>(n0 + srow + 32 * j) * a.K + ks * kBK + 8 * ch);
+#pragma unroll
+  for (int j = 0; j < CA; ++j) *reinterpret_cast<uint4*>(dst + swz(srow + 32 * j, ch)) = tw[j];
+}
+
+template <int CB, int BM, bool S2>
+__device__ __forceinline__ void load_x(const C1Args& a, uint4 (&pb)[CB], int t, int ks, int srow,
+                                       int ch) {
+#pragma unroll
+  for (int j = 0; j < CB; ++j)
+    pb[j] = *reinterpret_cast<const uint4*>(a.x + src_row(a, t * BM + srow + 32 * j, S2) * a.K + ks * kBK + 8 * ch);
+}
+
+template <int CB, bool PRO>
+__device__ __forceinline__ void store_x(const uint4 (&pb)[CB], char* sx, const float* s_aff, int K,
+                                        int ks, int srow, int ch) {
+  float sc[8], bi[8];
+  if constexpr (PRO) {
+    const float4* ps = reinterpret_cast<const float4*>(s_aff + ks * kBK + 8 * ch);
+    const float4* pq = reinterpret_cast<const float4*>(s_aff + K + ks * kBK + 8 * ch);
+    const float4 s0 = ps[0], s1 = ps[1], b0 = pq[0], b1 = pq[1];
+    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+    sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    bi[0] = b0.x; bi[1] = b0.y; bi[2] = b0.z; bi[3] = b0.w;
+    bi[4] = b1.x; bi[5] = b1.y; bi[6] = b1.z; bi[7] = b1.w;
+  }
+#pragma unroll
+  for (int j = 0; j < CB; ++j) {
+    uint4 v = pb[j];
+    if constexpr (PRO) {
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float lo = fmaxf(fmaf(__uint_as_float(w4[i] << 16), sc[2 * i], bi[2 * i]), 0.f);
+        const float hi = fmaxf(fmaf(__uint_as_float(w4[i] & 0xffff0000u), sc[2 * i + 1], bi[2 * i + 1]), 0.f);
+        w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+      }
+      v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    *reinterpret_cast<uint4*>(sx + swz(srow + 32 * j, ch)) = v;
+  }
+}
+
+// Round the wave's 64 (n) x 64 (m) block to bf16 and store it, adding the stored values (minus the
+// shift) to the statistics. The accumulator layout (lane = pixel, 4 consecutive channels per
+// register group) would make every global store instruction touch 32 lines with 16 B each (the
+// kernel then wrote at ~3 TB/s); instead the block goes through the wave's own 8 KB LDS image
+// [pixel][128 B] (XOR-swizzled like the operand images) and comes back as 16-B pieces, 8 lanes per
+// 128-B pixel row: every store instruction writes whole lines. The read-back also gives each lane
+// a fixed group of 8 channels (lane & 7), so the statistics need 16 registers (sum and sum of
+// squares of 8 channels) instead of 64. Only this wave touches its image: no workgroup barrier.
+__device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], float (&ss)[8],
+                                         float (&sq)[8], const float (&sh)[8], char* simg, int m0,
+                                         int ncol0, int n0, int lane) {
+  const int h = lane >> 5, r32 = lane & 31;
+#pragma unroll
+  for (int jm = 0; jm < 2; ++jm) {
+    const int p = 32 * jm + r32;                       // pixel row of the wave block
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t b0 = f2bf(acc[i][jm][4 * g + 0]), b1 = f2bf(acc[i][jm][4 * g + 1]);
+        const uint32_t b2 = f2bf(acc[i][jm][4 * g + 2]), b3 = f2bf(acc[i][jm][4 * g + 3]);
+        // channels 32 i + 8 g + 4 h .. +3 = half h of 16-B chunk 4 i + g of the pixel row
+        *reinterpret_cast<uint2*>(simg + swz(p, 4 * i + g) + 8 * h) =
+            make_uint2(b0 | (b1 << 16), b2 | (b3 << 16));
+      }
+    }
+  }
+  // the wave's own LDS writes complete before its reads
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const int c = lane & 7;
+#pragma unroll 2
+  for (int k = 0; k < 8; ++k) {
+    const int p = 8 * k + (lane >> 3);
+    const uint4 v = *reinterpret_cast<const uint4*>(simg + swz(p, c));
+    if (m0 + p < a.M) {
+      *reinterpret_cast<uint4*>(a.y + static_cast<int64_t>(m0 + p) * a.N + n0 + ncol0 + 8 * c) = v;
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float lo = __uint_as_float(w4[q] << 16) - sh[2 * q];
+        const float hi = __uint_as_float(w4[q] & 0xffff0000u) - sh[2 * q + 1];
+        ss[2 * q] += lo;
+        ss[2 * q + 1] += hi;
+        sq[2 * q] = fmaf(lo, lo, sq[2 * q]);
+        sq[2 * q + 1] = fmaf(hi, hi, sq[2 * q + 1]);
+      }
+    }
+  }
+  // the image is rewritten by the next tile's epilogue only after these reads have returned
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jm = 0; jm < 2; ++jm)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[i][jm][k] = 0.f;
+}
+
+template <int WN, int WM, bool PRO, bool WRES, bool S2>
+__global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
+  constexpr int BN = 64 * WN, BM = 64 * WM;
+  constexpr int CA = BN / 32, CB = BM / 32;     // 16-B staging chunks per thread and step
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int KS = a.K / kBK;
+  char* sw = smem;                                              // W: (WRES ? KS : 1) x [BN][128 B]
+  char* sx = smem + (WRES ? KS : 1) * BN * 128;                 // x: [BM][128 B]
+  float* s_aff = reinterpret_cast<float*>(sx + BM * 128);       // PRO: sc[K], bi[K]
+  float* s_sh = s_aff + (PRO ? 2 * a.K : 0);                    // statistics shift [BN]
+  char* s_img = reinterpret_cast<char*>(s_sh + BN);             // epilogue images: 4 x 8 KB
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave / WM, wm = wave % WM;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+  const int nt = slot % a.ntn;
+  const int j0 = (slot / a.ntn) * 8 + xcd;                     // first m-tile of this workgroup
+  const int n0 = nt * BN;
+  const int ch = tid & 7;                                       // 16-B chunk of every staged row
+  const int srow = tid >> 3;                                    // first staged row (+32 per item)
+
+  for (int c = tid; c < BN; c += kThreads) s_sh[c] = a.shift ? a.shift[n0 + c] : 0.f;
+  if constexpr (PRO) {
+    for (int k = tid; k < a.K; k += kThreads) {
+      s_aff[k] = a.pro_sc[k];
+      s_aff[a.K + k] = a.pro_bi[k];
+    }
+  }
+  if constexpr (WRES) {   // the whole W slice of this n-tile, once
+    for (int ks = 0; ks < KS; ++ks) stage_w<CA>(a, sw + ks * BN * 128, n0, srow, ch, ks);
+  }
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      acc[i][0][k] = 0.f;
+      acc[i][1][k] = 0.f;
+    }
+  // statistics: lane owns channels n0 + wn*64 + 8 (lane & 7) + q, q < 8 (see epilogue)
+  float ss[8], sq[8], sh[8];
+
+  uint4 pb[CB];
+  int t = j0, ks = 0;
+  if (t < a.mtiles) {
+    load_x<CB, BM, S2>(a, pb, t, 0, srow, ch);
+    __syncthreads();                 // s_aff / s_sh / resident W visible
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      sh[q] = s_sh[wn * 64 + 8 * (lane & 7) + q];
+      ss[q] = 0.f;
+      sq[q] = 0.f;
+    }
+    store_x<CB, PRO>(pb, sx, s_aff, a.K, 0, srow, ch);
+    if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, 0);
+    __syncthreads();
+    for (;;) {
+      int tn = t, ksn = ks + 1;
+      if (ksn == KS) {
+        ksn = 0;
+        tn = t + a.wgpn;
+      }
+      const bool more = tn < a.mtiles;
+      // prefetch the next step's x into registers; past the end, reload the current (valid) step
+      // instead of branching around the loads (hipcc would wait for them at the join)
+      load_x<CB, BM, S2>(a, pb, more ? tn : t, more ? ksn : ks, srow, ch);
+      const char* wa = sw + (WRES ? ks : 0) * BN * 128;
+#pragma unroll
+      for (int kk = 0; kk < kBK / 16; ++kk) {
+        bf16x8_t A[2], B[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          A[i] = *reinterpret_cast<const bf16x8_t*>(wa + swz(wn * 64 + 32 * i + r32, 2 * kk + h));
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          B[j] = *reinterpret_cast<const bf16x8_t*>(sx + swz(wm * 64 + 32 * j + r32, 2 * kk + h));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(A[i], B[j], acc[i][j]);
+      }
+      if (ks == KS - 1)
+        epilogue(a, acc, ss, sq, sh, s_img + wave * 8192, t * BM + wm * 64, wn * 64, n0, lane);
+      if (!more) break;
+      __syncthreads();               // every wave is done reading this step's LDS
+      store_x<CB, PRO>(pb, sx, s_aff, a.K, ksn, srow, ch);
+      if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, ksn);
+      __syncthreads();
+      t = tn;
+      ks = ksn;
+    }
+  }
+  if (!a.part) return;
+  if (t >= a.mtiles) {   // no tile: zero partials
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      ss[q] = 0.f;
+      sq[q] = 0.f;
+    }
+  }
+  // per-wave channel totals: reduce over the 8 lanes that share a channel group (lane >> 3)
+  float* pp = a.part + (static_cast<int64_t>(nt) * a.wgpn * WM + j0 * WM + wm) * 2 * BN;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float s = ss[q], v = sq[q];
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      s += __shfl_xor(s, o, 64);
+      v += __shfl_xor(v, o, 64);
+    }
+    if (lane < 8) {
+      const int c = wn * 64 + 8 * lane + q;
+      pp[c] = s;
+      pp[BN + c] = v;
+    }
+  }
+}
+
+// BN statistics from the conv's partial slab: 8 channels per workgroup, 32 row slices each, fp64,
+// fixed fold order (deterministic). mean = shift + S / M, var = Q / M - (S / M)^2.
+__global__ __launch_bounds__(256) void conv1x1_bn_finalize_kernel(
+    const float* __restrict__ part, int R, int BN, int N, int64_t M, const float* shift,
+    float eps, float momentum, float* __restrict__ mean, float* __restrict__ invstd,
+    float* __restrict__ rmean, float* __restrict__ rvar) {
+  __shared__ double ls[32][8], lq[32][8];
+  const int cl = threadIdx.x & 7, sl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  double S = 0.0, Q = 0.0;
+  if (c < N) {
+    const int nt = c / BN, cc = c - nt * BN;
+    const float* base = part + static_cast<int64_t>(nt) * R * 2 * BN + cc;
+    int r = sl;
+    for (; r + 3 * 32 < R; r += 4 * 32) {
+      float s[4], q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s[u] = base[static_cast<int64_t>(r + 32 * u) * 2 * BN];
+        q[u] = base[static_cast<int64_t>(r + 32 * u) * 2 * BN + BN];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        S += s[u];
+        Q += q[u];
+      }
+    }
+    for (; r < R; r += 32) {
+      S += base[static_cast<int64_t>(r) * 2 * BN];
+      Q += base[static_cast<int64_t>(r) * 2 * BN + BN];
+    }
+  }
+  ls[sl][cl] = S;
+  lq[sl][cl] = Q;
+  __syncthreads();
+  if (sl != 0 || c >= N) return;
+  S = 0.0;
+  Q = 0.0;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    S += ls[k][cl];
+    Q += lq[k][cl];
+  }
+  const double ms = S / static_cast<double>(M);
+  double var = Q / static_cast<double>(M) - ms * ms;
+  if (var < 0.0) var = 0.0;
+  const double mu = (shift ? static_cast<double>(shift[c]) : 0.0) + ms;
+  mean[c] = static_cast<float>(mu);
+  invstd[c] = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+  if (rmean) {
+    const double unb = M > 1 ? var * static_cast<double>(M) / static_cast<double>(M - 1) : var;
+    rmean[c] = static_cast<float>((1.0 - momentum) * rmean[c] + momentum * mu);
+    rvar[c] = static_cast<float>((1.0 - momentum) * rvar[c] + momentum * unb);
+  }
+}
+
+struct Plan {
+  int WN, WM, BN, BM, ntn, wgpn, mtiles, G;
+  bool wres;
+  size_t lds;
+};
+
+Plan plan_for(int WN, int64_t M, int K, int N, bool pro) {
+  Plan p{};
+  p.WN = WN;
+  p.WM = 4 / p.WN;
+  p.BN = 64 * p.WN;
+  p.BM = 64 * p.WM;
+  p.ntn = N / p.BN;
+  p.mtiles = static_cast<int>((M + p.BM - 1) / p.BM);
+  const int target = 512;                                     // 2 workgroups per CU
+  int w = (target + p.ntn - 1) / p.ntn;
+  const int mt8 = (p.mtiles + 7) / 8 * 8;
+  w = (w + 7) / 8 * 8;
+  p.wgpn = w < mt8 ? w : mt8;
+  p.G = p.ntn * p.wgpn;
+  const size_t wbytes = static_cast<size_t>(K) * p.BN * 2;
+  const size_t xbytes = static_cast<size_t>(p.BM) * 128;
+  const size_t aff = (pro ? static_cast<size_t>(K) * 8 : 0) + static_cast<size_t>(p.BN) * 4 +
+                     4 * 8192;                                 // + the per-wave epilogue images
+  p.wres = wbytes + xbytes + aff <= 80 * 1024;
+  p.lds = (p.wres ? wbytes : static_cast<size_t>(p.BN) * 128) + xbytes + aff;
+  return p;
+}
+
+// Widest n-tile that covers N, except that a 256-channel tile whose W slice cannot stay resident
+// (K > 64) re-stages 32 KB of W per 64 pixels: there 128 x 128 tiles are ~2x faster
+// (bench/conv1x1_fused.py, profiles/r02_conv1x1_*.jsonl).
+Plan make_plan(int64_t M, int K, int N, bool pro) {
+  const int WN = N % 256 == 0 ? 4 : (N % 128 == 0 ? 2 : 1);
+  Plan p = plan_for(WN, M, K, N, pro);
+  if (WN == 4 && !p.wres) p = plan_for(2, M, K, N, pro);
+  return p;
+}
+
+template <int WN, int WM, bool PRO, bool WRES, bool S2>
+hipError_t launch_t(const C1Args& a, const Plan& p, hipStream_t st) {
+  auto k = &conv1x1_bn_fwd_kernel<WN, WM, PRO, WRES, S2>;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+  k<<<p.G, kThreads, p.lds, st>>>(a);
+  return hipGetLastError();
+}
+
+template <int WN, int WM>
+hipError_t launch_w(const C1Args& a, const Plan& p, bool pro, bool s2, hipStream_t st) {
+  if (s2) {
+    if (pro) return hipErrorInvalidValue;   // strided convs read a materialised block input
+    return p.wres ? launch_t<WN, WM, false, true, true>(a, p, st)
+                  : launch_t<WN, WM, false, false, true>(a, p, st);
+  }
+  if (pro)
+    return p.wres ? launch_t<WN, WM, true, true, false>(a, p, st)
+                  : launch_t<WN, WM, true, false, false>(a, p, st);
+  return p.wres ? launch_t<WN, WM, false, true, false>(a, p, st)
+                : launch_t<WN, WM, false, false, false>(a, p, st);
+}
+
+}  // namespace
+
+size_t conv1x1_bn_part_floats(int64_t M, int K, int N, bool pro) {
+  const Plan p = make_plan(M, K, N, pro);
+  return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
+}
+
+hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* part,
+                                 const float* pro_sc, const float* pro_bi, const float* shift,
+                                 int64_t M, int K, int N, int stride, int H, int W, float* mean,
+                                 float* invstd, float* rmean, float* rvar, float eps,
+                                 float momentum, hipStream_t st) {
+  if (K % kBK || N % 64 || M < 1 || M >= (1ll << 31) || K > 4096 || N > 4096)
+    return hipErrorInvalidValue;
+  if (stride != 1 && stride != 2) return hipErrorInvalidValue;
+  const bool pro = pro_sc != nullptr;
+  const Plan p = make_plan(M, K, N, pro);
+  C1Args a{};
+  a.x = reinterpret_cast<const uint16_t*>(x);
+  a.w = reinterpret_cast<const uint16_t*>(w);
+  a.y = reinterpret_cast<uint16_t*>(y);
+  a.part = part;
+  a.pro_sc = pro_sc;
+  a.pro_bi = pro_bi;
+  a.shift = shift;
+  a.M = static_cast<int>(M);
+  a.K = K;
+  a.N = N;
+  a.ntn = p.ntn;
+  a.wgpn = p.wgpn;
+  a.mtiles = p.mtiles;
+  if (stride == 2) {
+    if (H % 2 || W % 2) return hipErrorInvalidValue;
+    a.H = H;
+    a.W = W;
+    a.OW = W / 2;
+    a.OHW = (H / 2) * (W / 2);
+  }
+  const bool s2 = stride == 2;
+  hipError_t e;
+  if (p.WN == 4) e = launch_w<4, 1>(a, p, pro, s2, st);
+  else if (p.WN == 2) e = launch_w<2, 2>(a, p, pro, s2, st);
+  else e = launch_w<1, 4>(a, p, pro, s2, st);
+  if (e != hipSuccess || !part || !mean) return e;
+  const int R = p.wgpn * p.WM;
+  conv1x1_bn_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, R, p.BN, N, M, shift, eps,
+                                                          momentum, mean, invstd, rmean, rvar);
+  return hipGetLastError();
+}
+
+}  // namespace cml

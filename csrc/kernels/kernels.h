@@ -236,10 +236,24 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
                              int W, int C, int OH, int OW, hipStream_t stream);
 
 // Weight gradient of a stride-1 1x1 conv, NHWC bf16: dW[co][ci] = sum_p dy[p][co] x[p][ci]
-// (wgrad1x1.hip). Co, Ci multiples of 128. part: splits x Co x Ci floats (wgrad1x1_plan);
-// dw: bf16 (dw_bf16) or fp32 [Co][Ci].
+// (wgrad1x1.hip). Co, Ci multiples of 128, or Ci == 64 with Co a multiple of 256. part: splits x
+// Co x Ci floats (wgrad1x1_plan); dw: bf16 (dw_bf16) or fp32 [Co][Ci]. pro_sc / pro_bi (fp32
+// [Ci], both or neither): x is replaced by max(x * sc + bi, 0) (a BN + ReLU never materialised).
 void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps);
 hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
-                           int64_t P, int Co, int Ci, hipStream_t stream);
+                           int64_t P, int Co, int Ci, const float* pro_sc, const float* pro_bi,
+                           hipStream_t stream);
+
+// Fused 1x1 convolution forward (conv1x1.hip): y[M][N] = f(x)[src(m)][K] W[N][K]^T on NHWC bf16,
+// f = identity or max(x * pro_sc + pro_bi, 0) per input channel (pro_sc != null), src(m) = m
+// (stride 1) or the stride-2 pixel of an [*, H, W] input. With part / mean non-null also the
+// training BatchNorm statistics of y (shifted by `shift`, e.g. the running mean; finalize updates
+// rmean / rvar when non-null). K % 64 == 0, N % 64 == 0. part: conv1x1_bn_part_floats floats.
+size_t conv1x1_bn_part_floats(int64_t M, int K, int N, bool pro);
+hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* part,
+                                 const float* pro_sc, const float* pro_bi, const float* shift,
+                                 int64_t M, int K, int N, int stride, int H, int W, float* mean,
+                                 float* invstd, float* rmean, float* rvar, float eps,
+                                 float momentum, hipStream_t st);
 
 }  // namespace cml

@@ -39,18 +39,25 @@ __device__ __forceinline__ bf16x8_t cat(s16x4 a, s16x4 b) {
 __device__ __forceinline__ uint4 keep_if(bool ok, uint4 v) {
   return make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
 }
-// byte offset of 16-B chunk ch (0..15) of row `row` in a [rows][256 B] image; the XOR spreads
-// the 4 rows x 64 B of each transposed read over all 64 banks
+// byte offset of 16-B chunk ch of row `row` in a [rows][ROWB] image; the XOR spreads the 4 rows x
+// 64 B of each transposed read over all 64 banks. 256-B (and 512-B) rows: every row starts on the
+// same bank, so chunk bits 0..3 are permuted by the row. 128-B rows (64 channels): row parity
+// already selects the bank half, and rows 2-3 of each group of 4 take the other 64 B of it.
 template <int ROWB>
 __device__ __forceinline__ int img_off(int row, int ch) {
+  if constexpr (ROWB == 128) return ROWB * row + 16 * (ch ^ (((row >> 1) & 1) << 2));
   return ROWB * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
 
-// TM (co) x TN (ci) tile, (TM / 64) x (TN / 64) waves of 64 x 64 (four 32 x 32 accumulators)
-template <int TM, int TN, int KC>
+// TM (co) x TN (ci) tile, (TM / 64) x (TN / 64) waves of 64 x 64 (four 32 x 32 accumulators).
+// PRO: x is the pre-BN activation z of a BN + ReLU whose output the conv consumed; the staging
+// applies max(z * sc[ci] + bi[ci], 0) (bf16-rounded, as the forward's prologue did), so the
+// BN-ReLU output is never materialised (conv1x1.hip's prologue is the forward counterpart).
+template <int TM, int TN, int KC, bool PRO>
 __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, float* __restrict__ part,
-    int P, int Co, int Ci, int tiles_n, int cps) {
+    int P, int Co, int Ci, int tiles_n, int cps, const float* __restrict__ pro_sc,
+    const float* __restrict__ pro_bi) {
   constexpr int kKC = KC;                              // pixels per chunk
   constexpr int NT = (TM / 64) * (TN / 64) * 64;
   constexpr int CA = TM / 8, CB = TN / 8;            // 16-B chunks per staged row
@@ -67,6 +74,29 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
   const int nchunk = (P + kKC - 1) / kKC;
   const int c_lo = blockIdx.y * cps;
   const int c_hi = min(nchunk, c_lo + cps);
+  // every staged x item of this thread covers the same 8 channels (NT is a multiple of CB)
+  float psc[8], pbi[8];
+  if constexpr (PRO) {
+    const int cb = ci0 + 8 * (tid % CB);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      psc[q] = pro_sc[cb + q];
+      pbi[q] = pro_bi[cb + q];
+    }
+  }
+  auto pro = [&](uint4 v) {
+    if constexpr (PRO) {
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float lo = fmaxf(fmaf(__uint_as_float(w4[i] << 16), psc[2 * i], pbi[2 * i]), 0.f);
+        const float hi = fmaxf(fmaf(__uint_as_float(w4[i] & 0xffff0000u), psc[2 * i + 1], pbi[2 * i + 1]), 0.f);
+        w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+      }
+      return make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    return v;
+  };
   // prefetch registers; loads are unconditional (clamped pixel, zeroed at use) and selects are
   // component-wise: a branch around the loads makes hipcc wait at the join, and a select of
   // whole uint4 values became a select of addresses that put these registers in scratch
@@ -100,7 +130,7 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
       const int e = tid + NT * j, row = e / CB, ch = e % CB;
-      *reinterpret_cast<uint4*>(bb + img_off<TN * 2>(row, ch)) = keep_if(c * kKC + row < P, bv[j]);
+      *reinterpret_cast<uint4*>(bb + img_off<TN * 2>(row, ch)) = keep_if(c * kKC + row < P, pro(bv[j]));
     }
   };
   if (c_lo < c_hi) {
@@ -205,9 +235,37 @@ void pick_tile(int Co, int Ci, int* TM, int* TN) {
     return;
   }
   *TM = Co % 256 == 0 ? 256 : 128;
-  *TN = Ci % 256 == 0 ? 256 : 128;
+  *TN = Ci == 64 ? 64 : (Ci % 256 == 0 ? 256 : 128);
+  if (*TN == 64) *TM = 256;   // 4 waves
 }
 }  // namespace
+
+template <int TM, int TN, bool PRO>
+void launch_one(dim3 grid, size_t lds, hipStream_t st, const uint16_t* dp, const uint16_t* xp,
+                float* part, int P, int Co, int Ci, int tiles_n, int cps, const float* sc,
+                const float* bi) {
+  auto k = &wgrad1x1_kernel<TM, TN, 64, PRO>;
+  if (lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+  k<<<grid, (TM / 64) * (TN / 64) * 64, lds, st>>>(dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
+}
+
+template <bool PRO>
+bool launch_tile(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, const uint16_t* dp,
+                 const uint16_t* xp, float* part, int P, int Co, int Ci, int tiles_n, int cps,
+                 const float* sc, const float* bi) {
+  // (no PRO variant of the 1024-thread 256 x 256 tile: it spills, and no ResNet shape needs it)
+  if (TM == 256 && TN == 256) {
+    if constexpr (PRO) return false;
+    else launch_one<256, 256, PRO>(grid, lds, st, dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
+  } else if (TM == 256 && TN == 128) launch_one<256, 128, PRO>(grid, lds, st, dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
+  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO>(grid, lds, st, dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
+  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO>(grid, lds, st, dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
+  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO>(grid, lds, st, dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
+  else return false;
+  return true;
+}
 
 // pixels per chunk (128-pixel chunks for the 128 x 128 tile measured 5-15 % slower: more
 // registers, fewer chunks per workgroup)
@@ -229,8 +287,11 @@ void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps) {
 }
 
 hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
-                           int64_t P, int Co, int Ci, hipStream_t st) {
-  if (Co % 128 || Ci % 128 || P < 1 || P >= (1ll << 31)) return hipErrorInvalidValue;
+                           int64_t P, int Co, int Ci, const float* pro_sc, const float* pro_bi,
+                           hipStream_t st) {
+  if (Ci == 64 ? Co % 256 != 0 : (Co % 128 || Ci % 128)) return hipErrorInvalidValue;
+  if (P < 1 || P >= (1ll << 31)) return hipErrorInvalidValue;
+  if ((pro_sc == nullptr) != (pro_bi == nullptr)) return hipErrorInvalidValue;
   int S, cps, TM, TN;
   wgrad1x1_plan(P, Co, Ci, &S, &cps);
   pick_tile(Co, Ci, &TM, &TN);
@@ -241,16 +302,12 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
   const auto* xp = reinterpret_cast<const uint16_t*>(x);
   const size_t lds = 2 * static_cast<size_t>(KC) * (TM + TN) * 2;   // two stages
   const int Pi = static_cast<int>(P);
-  if (TM == 256 && TN == 256) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad1x1_kernel<256, 256, 64>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-    wgrad1x1_kernel<256, 256, 64><<<grid, 1024, lds, st>>>(dp, xp, part, Pi, Co, Ci, tiles_n, cps);
-  } else if (TM == 256) {
-    wgrad1x1_kernel<256, 128, 64><<<grid, 512, lds, st>>>(dp, xp, part, Pi, Co, Ci, tiles_n, cps);
-  } else if (TN == 256) {
-    wgrad1x1_kernel<128, 256, 64><<<grid, 512, lds, st>>>(dp, xp, part, Pi, Co, Ci, tiles_n, cps);
-  } else {
-    wgrad1x1_kernel<128, 128, 64><<<grid, 256, lds, st>>>(dp, xp, part, Pi, Co, Ci, tiles_n, cps);
+  if (pro_sc) {
+    if (!launch_tile<true>(TM, TN, grid, lds, st, dp, xp, part, Pi, Co, Ci, tiles_n, cps, pro_sc, pro_bi))
+      return hipErrorInvalidValue;
+  } else if (!launch_tile<false>(TM, TN, grid, lds, st, dp, xp, part, Pi, Co, Ci, tiles_n, cps,
+                                 nullptr, nullptr)) {
+    return hipErrorInvalidValue;
   }
   const int64_t n = static_cast<int64_t>(Co) * Ci;
   const int fb = static_cast<int>((n / 4 + 255) / 256);

@@ -169,14 +169,14 @@ def test_geomed_gram_vs_direct(cuda):
     torch.testing.assert_close(got.cpu(), ref, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("kind", ["sgd", "adam"])
+@pytest.mark.parametrize("kind", ["sgd", "adam", "adamw"])
 @pytest.mark.parametrize("combine", ["sorted", "weighted"])
 def test_fused_update(cuda, kind, combine):
     n, D = 5, 10007
     X = _x(n, D, torch.bfloat16, cuda, 1)
     master = torch.randn(D, device=cuda)
     s1 = torch.randn(D, device=cuda).abs() if kind == "sgd" else torch.zeros(D, device=cuda)
-    s2 = torch.zeros(D, device=cuda) if kind == "adam" else None
+    s2 = torch.zeros(D, device=cuda) if kind != "sgd" else None
     p = torch.empty(D, dtype=torch.bfloat16, device=cuda)
     opt = K.OptArgs(kind=kind, lr=0.05, momentum=0.9 if kind == "sgd" else 0.0,
                     weight_decay=0.01, nesterov=kind == "sgd", step=3)
@@ -197,7 +197,9 @@ def test_fused_update(cuda, kind, combine):
         pr, br = R.sgd_update(m0, g, s10, 0.05, 0.9, 0.01, True, False)
         torch.testing.assert_close(s1, br, rtol=1e-5, atol=1e-5)
     else:
-        pr, mr, vr = R.adam_update(m0, g, s10, s20, 3, 0.05, 0.9, 0.999, 1e-8, 0.01)
+        # adam: L2 term in the gradient (torch.optim.Adam); adamw: decoupled decay
+        pr, mr, vr = R.adam_update(m0, g, s10, s20, 3, 0.05, 0.9, 0.999, 1e-8, 0.01,
+                                   decoupled=kind == "adamw")
         # fp32 fma-order differences: relative error ~1e-5 on g^2 terms
         torch.testing.assert_close(s1, mr, rtol=1e-4, atol=1e-6)
         torch.testing.assert_close(s2, vr, rtol=1e-4, atol=1e-7)
