@@ -169,6 +169,23 @@ class ExpressionSet:
         self.col_data.to_csv(os.path.join(path, "col_data.csv"))
 
     @classmethod
+    def from_rdata(cls, path: str, name: Optional[str] = None,
+                   assay_name: str = "logcpm") -> "ExpressionSet":
+        """A SummarizedExperiment saved by the reference (e.g.
+        ``composite_code/rnotebook/data/sesetfilt_degseahack_targetaml.rda``, the 1984 x 137 DEG
+        container loaded at `cml_targetaml_seanalysis.Rmd:409-415`), through the data-only reader
+        ``select.rdata``. The first assay is stored as ``assay_name`` (the reference's analysis
+        assay is TMM log-CPM); row_data holds the DE statistics of its rowRanges."""
+        from .rdata import read_rdata, summarized_experiment
+        objs = read_rdata(path)
+        obj = objs[name] if name else next(iter(objs.values()))
+        se = summarized_experiment(obj)
+        assays = {}
+        for i, (k, v) in enumerate(se["assays"].items()):
+            assays[assay_name if i == 0 else k] = torch.as_tensor(v, dtype=torch.float32)
+        return cls(assays, list(se["genes"]), list(se["samples"]), se["row_data"], se["col_data"])
+
+    @classmethod
     def load(cls, path: str) -> "ExpressionSet":
         from safetensors.torch import load_file
         assays = load_file(os.path.join(path, "assays.safetensors"))

@@ -657,3 +657,79 @@ def walk_types(x, depth: int = 0, max_depth: int = 6, out: Optional[list] = None
     else:
         out.append(f"{pad}{x!r}"[:120])
     return out
+
+
+# ----------------------------------------------------------------------------- Bioconductor
+def _assay_list(se: RS4) -> "RList":
+    """The assays of a SummarizedExperiment: a SimpleList held directly (``SimpleAssays``) or in
+    the reference-class environment of ``ShallowSimpleListAssays`` (field ``data``, stored as
+    ``.->data`` behind the active binding)."""
+    a = se.attrs.get("assays")
+    cur = a
+    for _ in range(4):
+        if isinstance(cur, RS4) and "listData" in cur.attrs:
+            return cur.attrs["listData"]
+        if isinstance(cur, RS4) and "data" in cur.attrs:
+            cur = cur.attrs["data"]
+            continue
+        if isinstance(cur, RS4) and ".xData" in cur.attrs:
+            env = cur.attrs[".xData"]
+            cur = env.frame.get(".->data", env.frame.get("data")) if isinstance(env, REnvironment) \
+                else None
+            continue
+        break
+    raise RDataError("could not locate the assay list of the SummarizedExperiment")
+
+
+def summarized_experiment(se: RS4) -> Dict[str, Any]:
+    """Decode a (Ranged)SummarizedExperiment into plain parts:
+    {assays: {name: np.ndarray [genes, samples]}, genes, samples, row_data (DataFrame: the
+    rowRanges' mcols, e.g. the DE statistics, plus seqnames / start / end / strand), col_data
+    (DataFrame), metadata (dict of str)}."""
+    import pandas as pd
+    if not isinstance(se, RS4) or not any("SummarizedExperiment" in c for c in se.rclass):
+        raise RDataError(f"not a SummarizedExperiment: {se!r}")
+    al = _assay_list(se)
+    assays, genes, samples = {}, None, None
+    for i, (nm, m) in enumerate(zip(names(al) or [None] * len(al), al.items)):
+        arr = as_array(m)
+        dn = dimnames(m)
+        if dn:
+            genes = genes or dn[0]
+            samples = samples or dn[1]
+        assays[nm or f"assay{i + 1}"] = arr
+    col = as_frame(se.attrs["colData"]) if "colData" in se.attrs else pd.DataFrame()
+    rd = pd.DataFrame()
+    rr = se.attrs.get("rowRanges")
+    if isinstance(rr, RS4):
+        em = rr.attrs.get("elementMetadata")
+        if isinstance(em, RS4):
+            rd = as_frame(em)
+        rg = rr.attrs.get("ranges")
+        if isinstance(rg, RS4):
+            start = rg.attrs["start"].values
+            rd["start"] = start
+            rd["end"] = start + rg.attrs["width"].values - 1
+            nm = rg.attrs.get("NAMES")
+            if genes is None and isinstance(nm, RVector):
+                genes = list(nm.values)
+        for slot, col_name in (("seqnames", "seqnames"), ("strand", "strand")):
+            rle = rr.attrs.get(slot)
+            if isinstance(rle, RS4) and "values" in rle.attrs:
+                vals = factor_labels(rle.attrs["values"])
+                rd[col_name] = np.repeat(np.array(vals, dtype=object),
+                                         rle.attrs["lengths"].values.astype(np.int64))
+    elif "elementMetadata" in se.attrs:
+        rd = as_frame(se.attrs["elementMetadata"])
+    if genes is not None and len(rd) == len(genes):
+        rd.index = genes
+    if samples is None and len(col):
+        samples = list(col.index)
+    meta = {}
+    md = se.attrs.get("metadata")
+    if isinstance(md, RList):
+        for k, v in zip(names(md) or [], md.items):
+            if isinstance(v, RVector) and v.rtype == STRSXP and len(v) == 1:
+                meta[k] = v.values[0]
+    return {"assays": assays, "genes": genes, "samples": samples, "row_data": rd,
+            "col_data": col, "metadata": meta}
