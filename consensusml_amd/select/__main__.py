@@ -1,6 +1,14 @@
 """Command line for the feature-selection consensus pipeline (the reference's notebook run,
 `composite_code/rnotebook/cml_targetaml_seanalysis.Rmd`, as one command).
 
+  # the reference's own analysis input: the DEG SummarizedExperiment it saved (1984 x 137
+  # log-CPM; read by the data-only R reader) with its train/test split and risk labels —
+  # the full reference run (4 SVMs, 15 lasso reps, RF 2k/5k/10k, 5 XGB configs) by default
+  python -m consensusml_amd.select \
+      --rdata composite_code/rnotebook/data/sesetfilt_degseahack_targetaml.rda --out out/
+  # ... interrupted? continue from the last finished stage
+  python -m consensusml_amd.select --rdata ... --out out/ --resume
+
   # TARGET-AML-shaped synthetic cohort (no data offline)
   python -m consensusml_amd.select --synthetic --out out/
 
@@ -15,8 +23,10 @@
   torchrun --nproc-per-node 4 --master-addr 127.0.0.1 -m consensusml_amd.select --synthetic
 
 Count columns are matched to patients by their TARGET USI prefix (first 16 characters of the
-sample id, `scripts/clean.py:1-18`). Output: ``standouttable.csv`` (reference layout) + a JSON
-summary, in ``--out``.
+sample id, `scripts/clean.py:1-18`). Output in ``--out``: ``standouttable.csv`` (reference
+24-column layout), ``standouttable_extended.csv``, ``results/<family>_resultslist`` per stage
+(JSON + safetensors), the incrementally saved ``standardtable_mloutputs_summary.csv`` and a JSON
+summary.
 """
 from __future__ import annotations
 
@@ -50,14 +60,24 @@ def main(argv=None) -> int:
     src = ap.add_mutually_exclusive_group(required=True)
     src.add_argument("--synthetic", action="store_true", help="TARGET-AML-shaped synthetic cohort")
     src.add_argument("--counts", help="genes x samples raw count CSV")
+    src.add_argument("--rdata", help="the reference's DEG SummarizedExperiment (.rda)")
+    ap.add_argument("--label-col", default=None, help="label column (default: deg.risk for "
+                    "--rdata, low_risk otherwise)")
+    ap.add_argument("--split-col", default=None, help="train/test column (default: "
+                    "exptset.seahack for --rdata, exptset otherwise)")
+    ap.add_argument("--resume", action="store_true", help="skip stages whose results exist")
+    ap.add_argument("--tree-method", choices=["exact", "hist"], default="exact")
+    ap.add_argument("--xgb-configs", default=None,
+                    help='JSON list of {"max_depth", "n_estimators"} (default: the reference 5)')
+    ap.add_argument("--no-proximity", action="store_true", help="skip RF proximity matrices")
     ap.add_argument("--clinical", help="clinical CSV (Clinical_Data/AML_dataframe.csv layout)")
     ap.add_argument("--train-ids", help="training USIs CSV (reference split file)")
     ap.add_argument("--test-ids", help="testing USIs CSV (reference split file)")
     ap.add_argument("--genes", type=int, default=2000, help="synthetic: number of genes")
     ap.add_argument("--samples", type=int, default=145, help="synthetic: number of samples")
     ap.add_argument("--max-genes", type=int, default=None, help="cap on DE genes carried forward")
-    ap.add_argument("--lasso-reps", type=int, default=3)
-    ap.add_argument("--rf-trees", type=int, nargs="+", default=[200, 500])
+    ap.add_argument("--lasso-reps", type=int, default=15)
+    ap.add_argument("--rf-trees", type=int, nargs="+", default=[2000, 5000, 10000])
     ap.add_argument("--seed", type=int, default=2019)
     ap.add_argument("--device", default="auto", help="cuda | cpu | auto")
     ap.add_argument("--out", default="consensus_out")
@@ -71,11 +91,24 @@ def main(argv=None) -> int:
         init_distributed("gloo" if a.device == "cpu" else "auto")
     dev = torch.device("cuda" if (a.device == "auto" and torch.cuda.is_available())
                        else ("cpu" if a.device == "auto" else a.device))
-    es = synthetic_cohort(a.genes, a.samples, seed=a.seed) if a.synthetic else _load_counts(a)
-    res = consensus_pipeline(es, out_dir=a.out, seed=a.seed, lasso_reps=a.lasso_reps,
-                             rf_trees=tuple(a.rf_trees), device=dev, max_genes=a.max_genes)
+    from .pipeline import REF_XGB
+    xgb = tuple(json.loads(a.xgb_configs)) if a.xgb_configs else REF_XGB
+    kw = dict(out_dir=a.out, seed=a.seed, lasso_reps=a.lasso_reps, rf_trees=tuple(a.rf_trees),
+              device=dev, max_genes=a.max_genes, xgb_configs=xgb, resume=a.resume,
+              tree_method=a.tree_method, rf_proximity=not a.no_proximity)
+    if a.rdata:
+        from .data import ExpressionSet
+        es = ExpressionSet.from_rdata(a.rdata)
+        res = consensus_pipeline(es, label_col=a.label_col or "deg.risk",
+                                 split_col=a.split_col or "exptset.seahack",
+                                 deg_from_container=True, **kw)
+    else:
+        es = synthetic_cohort(a.genes, a.samples, seed=a.seed) if a.synthetic else _load_counts(a)
+        res = consensus_pipeline(es, label_col=a.label_col or "low_risk",
+                                 split_col=a.split_col or "exptset", **kw)
     inter = res.get("intersections", {})
     print(json.dumps({"out": a.out, "samples": len(es.samples), "genes": len(es.genes),
+                      "resumed_stages": res.get("resumed_stages", []),
                       "intersection_sizes": {k: len(v) for k, v in inter.items()}}))
     return 0
 

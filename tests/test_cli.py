@@ -56,7 +56,8 @@ def test_select_cli_synthetic(tmp_path):
     from consensusml_amd.select.__main__ import main
     out = tmp_path / "sel"
     assert main(["--synthetic", "--genes", "300", "--samples", "48", "--rf-trees", "30",
-                 "--lasso-reps", "1", "--device", "cpu", "--out", str(out)]) == 0
+                 "--lasso-reps", "1", "--device", "cpu", "--out", str(out),
+                 "--xgb-configs", '[{"max_depth": 2, "n_estimators": 2}]']) == 0
     assert (out / "standouttable.csv").exists() and (out / "summary.json").exists()
 
 
@@ -87,5 +88,6 @@ def test_select_cli_counts_with_reference_cohort(tmp_path):
     counts.to_csv(cpath)
     out = tmp_path / "sel"
     assert main(["--counts", str(cpath), "--clinical", clin, "--train-ids", tr, "--test-ids", te,
-                 "--rf-trees", "20", "--lasso-reps", "1", "--device", "cpu", "--out", str(out)]) == 0
+                 "--rf-trees", "20", "--lasso-reps", "1", "--device", "cpu", "--out", str(out),
+                 "--xgb-configs", '[{"max_depth": 2, "n_estimators": 2}]']) == 0
     assert (out / "standouttable.csv").exists()

@@ -124,3 +124,44 @@ def test_rf_importance_parity(ref):
     assert spearmanr(ours, imp2k).correlation > 0.55
     top = lambda v: set(np.argsort(-v)[:50])   # noqa: E731
     assert len(top(ours) & top(imp2k)) >= 25
+
+
+def test_pipeline_on_reference_container_with_resume(tmp_path, monkeypatch):
+    """The reference analysis run from its own DEG container, interrupted after the SVM stage
+    and resumed: the finished stage is not recomputed (its result list and table columns are
+    reloaded), and the outputs keep the reference's standard-table layout."""
+    from consensusml_amd.select import pipeline as P
+    from consensusml_amd.select import results as RS
+    from consensusml_amd.select.data import ExpressionSet
+    es = ExpressionSet.from_rdata(SE)
+    kw = dict(label_col="deg.risk", split_col="exptset.seahack", deg_from_container=True,
+              out_dir=str(tmp_path), lasso_reps=3, rf_trees=(100,), max_genes=400,
+              xgb_configs=P.REF_XGB[:2])
+
+    def boom(*a, **k):
+        raise RuntimeError("killed")
+    monkeypatch.setattr(P, "iterative_exclusion", boom)
+    with pytest.raises(RuntimeError, match="killed"):
+        P.consensus_pipeline(es, **kw)
+    assert RS.exists(str(tmp_path / "results" / "svm4reps_resultslist"))
+    saved = pd.read_csv(tmp_path / P.TABLE_FILE, index_col=0)
+    assert "svm1_weights" in saved.columns and "lasso_coef_rep1" not in saved.columns
+    monkeypatch.undo()
+    monkeypatch.setattr(P, "run_svm", boom)          # must not run again
+    out = P.consensus_pipeline(es, resume=True, **kw)
+    assert out["resumed_stages"] == ["svm4reps_resultslist"]
+    np.testing.assert_allclose(out["table"].df["svm1_weights"].to_numpy(),
+                               saved["svm1_weights"].to_numpy())
+    svm = RS.load_results(str(tmp_path / "results" / "svm4reps_resultslist"))
+    assert set(svm) == {"svm1", "svm2", "svm3", "svm4"}
+    assert svm["svm1"]["weightsvect"].shape == (400,) and svm["svm3"]["weightsvect"] is None
+    lasso = RS.load_results(str(tmp_path / "results" / "lasso_resultslist"))
+    assert set(lasso["rep1"]) >= {"training.set", "testing.set", "cv.fit", "confusionMatrix",
+                                  "test.error", "nonzero.coef", "seed"}
+    assert len(lasso["rep1"]["training.set"]) == 93
+    rf = RS.load_results(str(tmp_path / "results" / "rf_noboost_resultslist"))
+    assert rf["rf100.results"]["proximity"].shape == (93, 93)
+    header = pd.read_csv(tmp_path / "standouttable.csv", index_col=0, nrows=1).columns.tolist()
+    assert header == P.DE_COLUMNS + ["lasso_coef_rep1", "lasso_coef_rep2", "lasso_coef_rep3",
+                                     "rfnb_100_MeanDecNodeImp", "svm1_weights", "svm2_weights",
+                                     "svm3_weights", "svm4_weights", "xg1_imp", "xg2_imp"]

@@ -241,10 +241,11 @@ def test_pipeline_end_to_end(tmp_path):
     from consensusml_amd.select.pipeline import consensus_pipeline
     es = D.synthetic_cohort(n_genes=600, n_samples=60, n_signal=30, effect=1.2, seed=5)
     out = consensus_pipeline(es, out_dir=str(tmp_path), lasso_reps=2, rf_trees=(20,),
-                             max_genes=120)
+                             max_genes=120, xgb_configs=({"max_depth": 2, "n_estimators": 2},
+                                                         {"max_depth": 6, "n_estimators": 10}))
     assert (tmp_path / "standouttable.csv").exists()
     df = out["table"].df
-    for col in ["logFC", "p.adj.bh", "svm1_weights", "lasso_coef_rep1", "rfnb_20_MeanDecGini",
+    for col in ["logFC", "p.adj.bh", "svm1_weights", "lasso_coef_rep1", "rfnb_20_MeanDecNodeImp",
                 "xg1_imp", "consensus_votes"]:
         assert col in df.columns
     assert out["performance"]["test_error"].max() < 0.5
