@@ -26,6 +26,8 @@ from __future__ import annotations
 
 import math
 import os
+
+import numpy as np
 from typing import Dict, List, Optional
 
 import torch
@@ -134,6 +136,10 @@ class ConsensusEngine:
                              and cfg.topology.early_update)
         self._updated: set = set()
         self._opt_stream = torch.cuda.Stream(device=dev) if self.early_update else None
+        # training-side consensus table (SURVEY.md §5.4 b): when set, the next step() records
+        # per-worker / per-parameter gradient statistics (consensus_table())
+        self.record_stats = False
+        self.last_stats: Optional[dict] = None
 
     # ================================================================ public API
     @property
@@ -399,6 +405,8 @@ class ConsensusEngine:
         cols = self._bucket_cols()
         if self.rule in GRAM_RULES:
             self._compute_weights(cols)
+        if self.record_stats:
+            self._record_stats(cols)
         opt = self._opt_args()
         for b, X, length in cols:
             gout = self.gout[b.offset:b.offset + b.length] if self.gout is not None else None
@@ -414,6 +422,8 @@ class ConsensusEngine:
         cols = self._bucket_cols()
         if self.rule in GRAM_RULES:
             self._compute_weights(cols)
+        if self.record_stats:
+            self._record_stats(cols)
         opt = self._opt_args()
         works = []
         for b, X, length in cols:
@@ -492,6 +502,99 @@ class ConsensusEngine:
             K.gossip_mix(self.master[s:e], self.nb_left[s:e], self.nb_right[s:e], w0, w1, w2,
                          clip, param_out=fl.flat_param[s:e])
             reqs = nxt
+
+    # ================================================================ consensus table
+    def _local_range(self, b: Bucket, length: int):
+        """Flat-coordinate column range [lo, hi) of bucket b held in this rank's worker rows."""
+        if self.topo == "sharded" and self.group_active:
+            lo = b.offset + self.rank * b.shard
+        else:
+            lo = b.offset
+        return lo, lo + length
+
+    def _aggregate_only(self, b: Bucket, X: torch.Tensor, length: int) -> torch.Tensor:
+        """The rule's aggregate of bucket b's local columns (fp32), without an update."""
+        cfg = self.cfg.agg
+        out = torch.empty(length, dtype=torch.float32, device=X.device)
+        none = K.OptArgs(kind="none")
+        if self.rule in ("median", "trimmed_mean"):
+            trim = cfg.trim if cfg.trim is not None else cfg.f
+            lo, cnt = K.sorted_range(self.rule, self.n, trim)
+            K.agg_update(X, combine="sorted", lo=lo, cnt=cnt, n=self.n, D=length, opt=none,
+                         gout=out)
+        elif self.rule == "bulyan":
+            theta = self.n - 2 * cfg.f
+            lo, cnt = K.sorted_range("trimmed_mean", theta, cfg.f)
+            K.agg_update(X, combine="sorted", lo=lo, cnt=cnt, rows=self.sel[:theta], n=theta,
+                         D=length, opt=none, gout=out)
+        else:
+            K.agg_update(X, combine="weighted", w=self.w, n=self.rows_total, D=length, opt=none,
+                         gout=out)
+        return out
+
+    def _record_stats(self, cols) -> None:
+        """Per (parameter tensor, worker): squared gradient norm and squared distance to the
+        aggregate, from the worker rows this rank holds; shard partial sums are all-reduced."""
+        segs = self.flat.segments()
+        n = self.n
+        dev = self.device
+        sq = torch.zeros(len(segs), n, dtype=torch.float64, device=dev)
+        dd = torch.zeros(len(segs), n, dtype=torch.float64, device=dev)
+        ag = torch.zeros(len(segs), dtype=torch.float64, device=dev)
+        for b, X, length in cols:
+            lo, hi = self._local_range(b, length)
+            agg = self._aggregate_only(b, X, length)
+            for k, (_, off, numel) in enumerate(segs):
+                a, e = max(off, lo), min(off + numel, hi)
+                if a >= e:
+                    continue
+                Xs = X[:n, a - lo:e - lo].double()
+                gs = agg[a - lo:e - lo].double()
+                sq[k] += (Xs * Xs).sum(1)
+                dd[k] += ((Xs - gs[None]) ** 2).sum(1)
+                ag[k] += (gs * gs).sum()
+        if self.group_active and self.topo == "sharded":
+            for t in (sq, dd, ag):
+                dist.all_reduce(t)
+        self.last_stats = {"names": [s[0] for s in segs], "sqnorm": sq.cpu(), "dist2": dd.cpu(),
+                           "agg_sqnorm": ag.cpu(), "step": self.step_count,
+                           "weights": self.w[:n].double().cpu(),
+                           "scores": self.scores[:n].cpu() if self.rule in GRAM_RULES else None,
+                           "sel_counts": self.sel_counts.cpu().clone()}
+        self.record_stats = False
+
+    def consensus_table(self):
+        """The training-side analogue of the reference's standard output table
+        (`composite_code/rnotebook/cml_targetaml_seanalysis.Rmd:627-633`, `:1297-1298`): one row
+        per parameter tensor, one column per worker for its gradient norm and its distance to the
+        robust aggregate, plus aggregate columns (aggregate norm, median worker norm, the worker
+        farthest from the aggregate). Two trailing rows carry the per-worker Krum score and
+        selection count / weight. Needs a step taken with ``record_stats = True``."""
+        import pandas as pd
+        st = self.last_stats
+        if st is None:
+            raise RuntimeError("no recorded step: set engine.record_stats = True before step()")
+        n = self.n
+        norm = st["sqnorm"].clamp_min(0).sqrt().numpy()
+        d = st["dist2"].clamp_min(0).sqrt().numpy()
+        df = pd.DataFrame(index=st["names"])
+        for i in range(n):
+            df[f"grad_norm_w{i}"] = norm[:, i]
+        for i in range(n):
+            df[f"dist_to_agg_w{i}"] = d[:, i]
+        df["agg_norm"] = st["agg_sqnorm"].clamp_min(0).sqrt().numpy()
+        df["median_worker_norm"] = np.median(norm, axis=1)
+        df["farthest_worker"] = d.argmax(1)
+        extra = pd.DataFrame(index=["(krum_score)", "(selection_count)", "(weight)"],
+                             columns=df.columns, dtype=float)
+        for i in range(n):
+            if st["scores"] is not None:
+                extra.loc["(krum_score)", f"grad_norm_w{i}"] = float(st["scores"][i])
+            extra.loc["(selection_count)", f"grad_norm_w{i}"] = float(st["sel_counts"][i])
+            extra.loc["(weight)", f"grad_norm_w{i}"] = float(st["weights"][i])
+        out = pd.concat([df, extra])
+        out.attrs["step"] = st["step"]
+        return out
 
     def _drain_gossip(self) -> None:
         if self._gossip_reqs is not None:

@@ -93,13 +93,18 @@ class ConsensusTrainer:
         t0 = time.perf_counter()
         losses = []
         for s in range(start, steps):
+            ckpt_now = bool(self.cfg.ckpt_every and self.cfg.ckpt_dir
+                            and (s + 1) % self.cfg.ckpt_every == 0)
+            if ckpt_now and self.engine.topo in ("sharded", "allgather"):
+                self.engine.record_stats = True      # consensus table of this step
             loss = self.train_step()
             losses.append(loss)
             if log_every and (s + 1) % log_every == 0:
                 lv = float(loss)
                 self.logger.log(step=s + 1, loss=lv, phases=self.timer.summary())
-            if self.cfg.ckpt_every and self.cfg.ckpt_dir and (s + 1) % self.cfg.ckpt_every == 0:
-                save_checkpoint(self.cfg.ckpt_dir, self.engine, self.cfg, gens=self.gens)
+            if ckpt_now:
+                save_checkpoint(self.cfg.ckpt_dir, self.engine, self.cfg, gens=self.gens,
+                                table=self._consensus_table())
         if self.info.device.type == "cuda":
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
@@ -149,8 +154,17 @@ class ConsensusTrainer:
         return res
 
     # ------------------------------------------------------------------ checkpoint
+    def _consensus_table(self):
+        return self.engine.consensus_table() if self.engine.last_stats is not None else None
+
+    def consensus_table(self):
+        """Per-parameter x per-worker gradient table of the last recorded step (run a step with
+        ``engine.record_stats = True`` first; checkpoints record it automatically)."""
+        return self.engine.consensus_table()
+
     def save(self, root: Optional[str] = None) -> str:
-        return save_checkpoint(root or self.cfg.ckpt_dir, self.engine, self.cfg, gens=self.gens)
+        return save_checkpoint(root or self.cfg.ckpt_dir, self.engine, self.cfg, gens=self.gens,
+                               table=self._consensus_table())
 
     def load(self, path: str) -> dict:
         return load_checkpoint(path, self.engine, self.gens)

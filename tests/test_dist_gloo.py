@@ -129,3 +129,79 @@ def test_checkpoint_resume_gloo(tmp_path):
     single = _single(2, "median", "sharded", 0, 6)
     for a, b in zip(res[0]["params"], single):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def _save_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from consensusml_amd.parallel import dist as D
+    from consensusml_amd.trainer.trainer import ConsensusTrainer
+    D._INFO = None
+    info = D.init_distributed("gloo")
+    cfg = _cfg("krum", "sharded", 1, 0, 3)
+    cfg.optim.momentum = 0.9
+    cfg.ckpt_dir = os.path.join(out_dir, "ckpt")
+    cfg.ckpt_every = 3
+    tr = ConsensusTrainer(cfg, info=info)
+    tr.fit(3, log_every=0)
+    torch.save({"params": [p.detach().clone() for p in tr.model.parameters()],
+                "master": tr.engine.master.clone()}, os.path.join(out_dir, f"saved{rank}.pt"))
+    D.monitored_barrier(30)
+    dist.destroy_process_group()
+
+
+def _load_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from consensusml_amd.parallel import dist as D
+    from consensusml_amd.trainer.trainer import ConsensusTrainer
+    D._INFO = None
+    info = D.init_distributed("gloo")
+    cfg = _cfg("krum", "sharded", 1, 0, 3)
+    cfg.optim.momentum = 0.9
+    tr = ConsensusTrainer(cfg, info=info)
+    r = tr.load(os.path.join(out_dir, "ckpt"))
+    assert r["resharded"]
+    saved = torch.load(os.path.join(out_dir, "saved0.pt"), weights_only=True)
+    for a, b in zip(tr.model.parameters(), saved["params"]):
+        assert torch.equal(a.detach(), b)
+    tr.fit(5, log_every=0)     # keeps training after the re-shard
+    torch.save({"params": [p.detach().clone() for p in tr.model.parameters()],
+                "step": tr.engine.step_count}, os.path.join(out_dir, f"w{world}_{rank}.pt"))
+    D.monitored_barrier(30)
+    dist.destroy_process_group()
+
+
+def test_checkpoint_reshard_world2_to_1_and_4(tmp_path):
+    """A sharded checkpoint written by 2 ranks loads at world 1 (this process) and world 4 with
+    the parameters and fp32 master unchanged; the consensus table is written next to it."""
+    import pandas as pd
+    from consensusml_amd.parallel.dist import DistInfo
+    from consensusml_amd.trainer.trainer import ConsensusTrainer
+    mp.spawn(_save_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    saved = torch.load(tmp_path / "saved0.pt", weights_only=True)
+    # consensus table of the checkpoint step: one row per parameter tensor + per-worker rows
+    tab = pd.read_csv(tmp_path / "ckpt" / "step_3" / "consensus_table.csv", index_col=0)
+    assert {"grad_norm_w0", "grad_norm_w1", "dist_to_agg_w0", "agg_norm"} <= set(tab.columns)
+    assert "(selection_count)" in tab.index and len(tab) == len(saved["params"]) + 3
+    # world 1
+    from consensusml_amd.parallel import dist as D
+    D._INFO = None
+    cfg = _cfg("krum", "sharded", 1, 0, 3)
+    cfg.optim.momentum = 0.9
+    tr = ConsensusTrainer(cfg, info=DistInfo(0, 1, 0, torch.device("cpu"), "none"))
+    r = tr.load(str(tmp_path / "ckpt"))
+    assert r["resharded"] and tr.engine.step_count == 3
+    for a, b in zip(tr.model.parameters(), saved["params"]):
+        torch.testing.assert_close(a.detach(), b, rtol=0, atol=0)
+    # the world-1 master is the full vector: its parameter values equal the saved params
+    for p, (n, o, k) in zip(tr.model.parameters(), tr.engine.flat.segments()):
+        torch.testing.assert_close(tr.engine.master[o:o + k].view_as(p), p.detach().float())
+    # world 4
+    mp.spawn(_load_worker, args=(4, _free_port(), str(tmp_path)), nprocs=4, join=True)
+    for rk in range(4):
+        got = torch.load(tmp_path / f"w4_{rk}.pt", weights_only=True)
+        assert got["step"] == 5
+        assert all(torch.isfinite(p).all() for p in got["params"])
