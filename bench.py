@@ -169,6 +169,7 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info, *, V: int
     t0 = time.perf_counter()
     for i in range(steps):
         loss = step(i, timed=True)
+    eng.wait_params()             # the last step's overlapped parameter all-gather
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

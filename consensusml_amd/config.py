@@ -82,6 +82,7 @@ class TopologyConfig:
     gossip_clip: float = 0.0     # 0 disables neighbour-delta clipping
     gossip_async: bool = False   # delayed gossip: exchange overlaps the next step's compute
     early_update: bool = True    # gossip, 1 local worker: per-bucket optimizer step in backward
+    param_prefetch: bool = True  # sharded: bf16 parameter all-gather overlaps the next forward
 
     def validate(self) -> None:
         if self.kind not in TOPOLOGIES:

@@ -136,6 +136,18 @@ class ConsensusEngine:
                              and cfg.topology.early_update)
         self._updated: set = set()
         self._opt_stream = torch.cuda.Stream(device=dev) if self.early_update else None
+        # Sharded topology: the bf16 parameter all-gather of each bucket is not waited for at the
+        # end of step(); the next forward waits per top-level module (forward pre-hooks) for the
+        # buckets holding that module's parameters, so the all-gathers of later layers overlap
+        # the forward of earlier ones. The all-gathers are launched earliest-layers-first. Which
+        # top-level children are actually called as modules (their params are only read inside
+        # their own forward) is learned on the first step, which waits for everything up front.
+        self._ag_works: Dict[int, object] = {}
+        self.param_prefetch = bool(cfg.topology.param_prefetch and self.topo == "sharded"
+                                   and self.group_active)
+        self._prefetch_hooks = []
+        if self.param_prefetch:
+            self._setup_prefetch()
         # training-side consensus table (SURVEY.md §5.4 b): when set, the next step() records
         # per-worker / per-parameter gradient statistics (consensus_table())
         self.record_stats = False
@@ -163,9 +175,62 @@ class ConsensusEngine:
             self._flush_row()
         self.flat.grad_row = v
 
+    # ================================================================ parameter prefetch
+    def _setup_prefetch(self) -> None:
+        fl = self.flat
+        root = fl.model
+        pid = {id(p): i for i, p in enumerate(fl.params)}
+        self._root_buckets = {fl.bucket_of[pid[id(p)]] for p in root.parameters(recurse=False)
+                              if id(p) in pid}
+        self._child_buckets: Dict[str, set] = {}
+        for name, child in root.named_children():
+            self._child_buckets[name] = {fl.bucket_of[pid[id(p)]] for p in child.parameters()
+                                         if id(p) in pid}
+            self._prefetch_hooks.append(child.register_forward_pre_hook(
+                self._make_child_pre(name)))
+        self._prefetch_hooks.append(root.register_forward_pre_hook(self._root_pre))
+        self._invoked: set = set()
+        self._learned = False
+
+    def _wait_ag(self, bi: int) -> None:
+        w = self._ag_works.pop(bi, None)
+        if w is not None:
+            w.wait()
+
+    def wait_params(self) -> None:
+        """Complete every in-flight parameter all-gather (before reading parameters outside a
+        forward, e.g. a checkpoint or an evaluation of submodules)."""
+        for bi in list(self._ag_works):
+            self._wait_ag(bi)
+
+    def _root_pre(self, _mod, _inp):
+        if not self._ag_works:
+            return
+        if not self._learned:
+            self.wait_params()
+            return
+        need = set(self._root_buckets)
+        for name, bks in self._child_buckets.items():
+            if name not in self._invoked:
+                need |= bks
+        for bi in need:
+            self._wait_ag(bi)
+
+    def _make_child_pre(self, name: str):
+        def pre(_mod, _inp):
+            if not self._learned:
+                self._invoked.add(name)
+            for bi in self._child_buckets[name]:
+                self._wait_ag(bi)
+        return pre
+
     def step(self) -> None:
         """Exchange, aggregate and update (call after all backward passes of the step)."""
         fl = self.flat
+        if self.param_prefetch:
+            self.wait_params()          # params no forward touched
+            if self._invoked:
+                self._learned = True
         self._flush_row()
         if self.early_update:
             for b in fl.buckets:       # buckets whose gradients were never all produced
@@ -426,7 +491,8 @@ class ConsensusEngine:
             self._record_stats(cols)
         opt = self._opt_args()
         works = []
-        for b, X, length in cols:
+        # earliest layers (highest bucket index) first: the next forward needs them first
+        for b, X, length in (reversed(cols) if self.param_prefetch else cols):
             if self.group_active:
                 pout = fl.my_shard(fl.flat_param, b, self.rank)
                 soff = b.shard_offset
@@ -439,7 +505,11 @@ class ConsensusEngine:
                 X[self.n, :length].copy_(gout.to(X.dtype))
             if self.group_active:
                 full = fl.flat_param[b.offset:b.offset + b.length]
-                works.append(dist.all_gather_into_tensor(full, pout, async_op=True))
+                work = dist.all_gather_into_tensor(full, pout, async_op=True)
+                if self.param_prefetch:
+                    self._ag_works[b.index] = work
+                else:
+                    works.append(work)
         for w in works:
             w.wait()
 
@@ -605,6 +675,7 @@ class ConsensusEngine:
 
     # ================================================================ state
     def state_dict(self) -> dict:
+        self.wait_params()
         sd = {"master": self.master, "step": self.step_count, "sel_counts": self.sel_counts,
               "rank": self.rank, "world": self.N, "topology": self.topo}
         if self.topo == "gossip" and self.cfg.topology.gossip_async and \
@@ -644,6 +715,7 @@ class ConsensusEngine:
 
     def sync_params_from_master(self) -> None:
         """Rewrite the bf16 parameters from the fp32 master (after a checkpoint load)."""
+        self.wait_params()
         fl = self.flat
         if self.topo == "sharded" and self.group_active:
             for b in fl.buckets:
@@ -657,6 +729,10 @@ class ConsensusEngine:
 
     def close(self) -> None:
         self._drain_gossip()     # the in-flight delayed-gossip exchange
+        self.wait_params()
+        for h in self._prefetch_hooks:
+            h.remove()
+        self._prefetch_hooks = []
         for h in self._hooks:
             h.remove()
         self._hooks = []

@@ -105,6 +105,7 @@ class ConsensusTrainer:
             if ckpt_now:
                 save_checkpoint(self.cfg.ckpt_dir, self.engine, self.cfg, gens=self.gens,
                                 table=self._consensus_table())
+        self.engine.wait_params()      # the last step's overlapped parameter all-gather
         if self.info.device.type == "cuda":
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
@@ -130,6 +131,7 @@ class ConsensusTrainer:
     def evaluate(self, batches: int = 4, batch_size: Optional[int] = None) -> Dict[str, object]:
         """Loss / accuracy / confusion-derived metrics on fresh synthetic batches."""
         from ..select.metrics import binary_metrics, confusion_matrix
+        self.engine.wait_params()
         self.model.eval()
         gen = torch.Generator(device=self.info.device)
         gen.manual_seed(self.cfg.seed + 99991)

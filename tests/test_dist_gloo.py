@@ -42,7 +42,7 @@ def _cfg(rule, topo, V, f, steps, fault="none", byz=()):
     return cfg
 
 
-def _worker(rank, world, port, rule, topo, f, steps, out_dir, fault, byz, ckpt):
+def _worker(rank, world, port, rule, topo, f, steps, out_dir, fault, byz, ckpt, prefetch=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch.distributed as dist
@@ -51,6 +51,7 @@ def _worker(rank, world, port, rule, topo, f, steps, out_dir, fault, byz, ckpt):
     D._INFO = None
     info = D.init_distributed("gloo")
     cfg = _cfg(rule, topo, 1, f, steps, fault, byz)
+    cfg.topology.param_prefetch = prefetch
     if ckpt:
         cfg.ckpt_dir = os.path.join(out_dir, "ckpt")
     tr = ConsensusTrainer(cfg, info=info)
@@ -70,10 +71,11 @@ def _worker(rank, world, port, rule, topo, f, steps, out_dir, fault, byz, ckpt):
     dist.destroy_process_group()
 
 
-def _run_world(world, rule, topo, f, steps, tmp, fault="none", byz=(), ckpt=False):
+def _run_world(world, rule, topo, f, steps, tmp, fault="none", byz=(), ckpt=False,
+               prefetch=True):
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, rule, topo, f, steps, str(tmp), fault, list(byz), ckpt),
-             nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, rule, topo, f, steps, str(tmp), fault, list(byz), ckpt,
+                            prefetch), nprocs=world, join=True)
     return [torch.load(os.path.join(tmp, f"r{r}.pt"), weights_only=True) for r in range(world)]
 
 
@@ -205,3 +207,15 @@ def test_checkpoint_reshard_world2_to_1_and_4(tmp_path):
         got = torch.load(tmp_path / f"w4_{rk}.pt", weights_only=True)
         assert got["step"] == 5
         assert all(torch.isfinite(p).all() for p in got["params"])
+
+
+def test_param_prefetch_bit_identical(tmp_path):
+    """Overlapping the sharded parameter all-gather with the next forward (per-module waits)
+    gives bit-identical parameters to waiting for it at the end of the step."""
+    (tmp_path / "on").mkdir()
+    (tmp_path / "off").mkdir()
+    a = _run_world(3, "krum", "sharded", 0, 5, tmp_path / "on", prefetch=True)
+    b = _run_world(3, "krum", "sharded", 0, 5, tmp_path / "off", prefetch=False)
+    for r in range(3):
+        for x, y in zip(a[r]["params"], b[r]["params"]):
+            assert torch.equal(x, y)
