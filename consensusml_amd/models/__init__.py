@@ -54,6 +54,20 @@ def build_task(cfg: ModelConfig, device: torch.device, dtype: torch.dtype = torc
         model = resnet50(cfg.num_classes) if name == "resnet50" else resnet_tiny(cfg.num_classes)
         model = model.to(device=device, dtype=dtype, memory_format=torch.channels_last)
         S = cfg.image_size
+        if cfg.extra.get("synthetic") == "templates":
+            # learnable images (robustness benchmark): one fixed smooth template per class
+            # (4x4 noise upsampled to SxS) plus pixel noise of the same scale
+            g0 = torch.Generator().manual_seed(4321)
+            low = torch.randn(cfg.num_classes, 3, 4, 4, generator=g0)
+            tmpl = torch.nn.functional.interpolate(low, size=(S, S), mode="bilinear",
+                                                   align_corners=False).to(device)
+            noise = float(cfg.extra.get("noise", 1.0))
+
+            def make(b, gen):
+                y = torch.randint(0, cfg.num_classes, (b,), generator=gen, device=device)
+                x = tmpl[y] + noise * torch.randn(b, 3, S, S, generator=gen, device=device)
+                return x.to(dtype).contiguous(memory_format=torch.channels_last), y
+            return Task(name, model, make, _ce)
 
         def make(b, gen):
             x = torch.randn(b, 3, S, S, generator=gen, device=device)
