@@ -7,8 +7,9 @@
                            `BuieRProj/KM_WHATEVER.Rmd:151-187`).
 * ``glmboost``             component-wise L2 boosting regression (C32, mlr ``regr.glmboost``,
                            `Ryan/Feature_selection_GLMTrain_WT_TARGET.R:56-64`).
-* ``DLDA`` / ``NSC`` / ``PLDA``  diagonal LDA, nearest shrunken centroids and Poisson LDA
-                           (C31, MLSeq ``voomDLDA`` / ``pam`` / ``PLDA`` at `VikasP/AML.R:174-264`).
+* ``DLDA`` / ``NSC``        diagonal LDA and nearest shrunken centroids: the base estimators of
+                           the MLSeq wrappers in ``select/mlseq.py`` (C31, ``voomDLDA`` / ``pam``
+                           / ``voomNSC`` at `VikasP/AML.R:174-264`; Poisson LDA lives there too).
 """
 from __future__ import annotations
 
@@ -160,66 +161,12 @@ class NSC(DLDA):
         return self
 
 
-class PLDA:
-    """Poisson linear discriminant analysis (Witten 2011) on counts with size factors."""
-
-    def __init__(self, rho: float = 0.0):
-        self.rho = rho
-
-    def fit(self, counts, y):
-        X = counts.double()
-        self.classes = torch.unique(y)
-        s = X.sum(1) / X.sum()                                     # sample size factors
-        self.gene_tot = X.sum(0)
-        N = torch.outer(s, self.gene_tot)
-        self.d = []
-        for c in self.classes:
-            m = y == c
-            num = X[m].sum(0) + 1
-            den = N[m].sum(0) + 1
-            d = num / den
-            if self.rho > 0:   # soft-threshold toward 1 (feature selection)
-                d = 1 + torch.sign(d - 1) * ((d - 1).abs() - self.rho / torch.sqrt(den)).clamp_min(0)
-            self.d.append(d)
-        self.d = torch.stack(self.d)
-        self.prior = torch.stack([(y == c).double().mean() for c in self.classes])
-        self.total = X.sum()
-        return self
-
-    def predict(self, counts):
-        X = counts.double()
-        s = X.sum(1) / self.total
-        N = torch.outer(s, self.gene_tot)
-        sc = X @ torch.log(self.d).t() - N @ self.d.t() + torch.log(self.prior)
-        return self.classes[sc.argmax(1)]
-
-
 def voom_transform(counts: torch.Tensor) -> torch.Tensor:
     """log2-CPM with 0.5 offsets (the voom expression scale used by MLSeq's voomDLDA / voomNSC),
     samples x genes counts in, samples x genes out."""
     x = counts.double()
     lib = x.sum(1, keepdim=True)
     return torch.log2((x + 0.5) / (lib + 1.0) * 1e6)
-
-
-class VoomDLDA(DLDA):
-    """MLSeq ``voomDLDA``: diagonal LDA on voom-transformed counts."""
-
-    def fit(self, counts, y):
-        return super().fit(voom_transform(counts), y)
-
-    def predict(self, counts):
-        return super().predict(voom_transform(counts))
-
-
-class VoomNSC(NSC):
-    """MLSeq ``voomNSC``: nearest shrunken centroids on voom-transformed counts."""
-
-    def fit(self, counts, y):
-        return super().fit(voom_transform(counts), y)
-
-    def predict(self, counts):
-        return super().predict(voom_transform(counts))
 
 
 def cohort_summary(col_data, label: str = "low_risk", covariates=("gender", "age"),

@@ -2,7 +2,8 @@
 import torch
 
 from consensusml_amd.select.data import synthetic_cohort
-from consensusml_amd.select.stats import PLDA, VoomDLDA, VoomNSC, cohort_summary
+from consensusml_amd.select.mlseq import PLDA, VoomDLDA, VoomNSC
+from consensusml_amd.select.stats import cohort_summary
 
 
 def test_cohort_summary_chisq():
@@ -20,4 +21,4 @@ def test_voom_classifiers_separate_strong_signal():
         m.fit(X[:60], y[:60])
         assert (m.predict(X[60:]) == y[60:]).float().mean() > 0.85, type(m).__name__
     nsc = VoomNSC(2.0).fit(X[:60], y[:60])
-    assert 0 < nsc.selected.numel() < 400
+    assert 0 < nsc.selected_genes().numel() < 400
