@@ -32,17 +32,13 @@ def quantile_bins(X: torch.Tensor, n_bins: int = 64):
     lo = S[idx]                                   # [n_bins-1, p]
     hi = S[(idx + 1).clamp_max(n - 1)]
     edges = ((lo + hi) / 2).t().contiguous()      # [p, n_bins-1]
-    Xb = torch.zeros(n, p, dtype=torch.uint8, device=X.device)
-    for j in range(edges.shape[1]):               # bin = #edges strictly below x
-        Xb += (X > edges[:, j][None]).to(torch.uint8)
-    return Xb, edges
+    return bin_with(X, edges), edges
 
 
 def bin_with(X: torch.Tensor, edges: torch.Tensor) -> torch.Tensor:
-    Xb = torch.zeros(X.shape, dtype=torch.uint8, device=X.device)
-    for j in range(edges.shape[1]):
-        Xb += (X.float() > edges[:, j][None]).to(torch.uint8)
-    return Xb
+    """bin = number of edges strictly below x (one searchsorted over the sorted edge rows)."""
+    Xt = X.float().t().contiguous()                                  # [p, n]
+    return torch.searchsorted(edges, Xt, right=False).to(torch.uint8).t().contiguous()
 
 
 @dataclass
@@ -116,7 +112,14 @@ def grow(Xb: torch.Tensor, stat: torch.Tensor, depth: int, k: int, n_bins: int, 
             feats = torch.arange(p, device=dev).expand(T, L, p)
             kk = p
         else:
-            r = torch.rand(T, L, p, generator=gen, device="cpu").to(dev)
+            if dev.type == "cuda":
+                # candidate draws on the device (a host draw of T x L x p keys, 22M at p = 21k,
+                # used to dominate the fit); the device stream is seeded from the host generator
+                dgen = torch.Generator(device=dev)
+                dgen.manual_seed(int(torch.randint(0, 2 ** 62, (1,), generator=gen)))
+                r = torch.rand(T, L, p, generator=dgen, device=dev)
+            else:
+                r = torch.rand(T, L, p, generator=gen, device="cpu").to(dev)
             if feat_mask is not None:
                 r = torch.where(feat_mask[:, None, :], r, torch.full_like(r, -1.0))
             kk = min(k, p) if feat_mask is None else min(k, int(feat_mask.sum(1).min()))
@@ -144,7 +147,7 @@ def grow(Xb: torch.Tensor, stat: torch.Tensor, depth: int, k: int, n_bins: int, 
         # route samples
         nf = torch.gather(feature[:, base:base + L], 1, local)
         nb = torch.gather(thr[:, base:base + L], 1, local)
-        xb = torch.gather(Xb.long()[None].expand(T, n, p), 2, nf.clamp_min(0)[..., None]).squeeze(2)
+        xb = Xb[torch.arange(n, device=dev)[None].expand(T, n), nf.clamp_min(0)].long()
         child = 2 * node_of + 1 + (xb > nb).long()
         at_level = (node_of >= base) & (node_of < base + L)
         node_of = torch.where(at_level & (nf >= 0), child, node_of)

@@ -7,12 +7,15 @@ Reference: ``runSVM`` (`composite_code/rnotebook/cml_targetaml_seanalysis.Rmd:12
 (SURVEY.md §4.3); here the weights always come from the model that is returned, and radial
 models report ``weights=None``.
 
-The Gram / kernel matrix (n x n, n ~ 100) is one GEMM on the device; SMO itself is a few hundred
-O(n) vector steps with libsvm's second-order working-set selection.
+The Gram / kernel matrix (n x n, n ~ 100) is one GEMM on the device; SMO (a few hundred O(n)
+steps with libsvm's second-order working-set selection) runs on the device too, one wave64 per
+problem (``csrc/kernels/svm_smo.hip``), so independent fits (CV folds x cost grid, the four
+runSVM configurations) are solved in ONE launch by ``smo_batched`` / ``fit_svcs``. CPU tensors
+use the numpy oracle ``smo`` with the same selection order.
 """
 from __future__ import annotations
 
-from typing import Dict, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -31,9 +34,11 @@ def kernel_matrix(A: torch.Tensor, B: torch.Tensor, kind: str, gamma: float) -> 
     raise ValueError(kind)
 
 
-def smo(K: np.ndarray, y: np.ndarray, C: float = 1.0, tol: float = 1e-3, max_iter: int = 100000):
+def smo(K: np.ndarray, y: np.ndarray, C: float = 1.0, tol: float = 1e-3, max_iter: int = 100000,
+        return_grad: bool = False):
     """Dual C-SVC: min 1/2 a^T Q a - e^T a, 0 <= a <= C, y^T a = 0 (Q = y y^T * K).
-    Returns (alpha, b) with the decision function sum_i a_i y_i K(x_i, x) + b."""
+    Returns (alpha, b) with the decision function sum_i a_i y_i K(x_i, x) + b. Host oracle of the
+    batched GPU solver ``smo_batched`` (csrc/kernels/svm_smo.hip), same selection order."""
     n = y.size
     Q = K * np.outer(y, y)
     a = np.zeros(n)
@@ -50,9 +55,10 @@ def smo(K: np.ndarray, y: np.ndarray, C: float = 1.0, tol: float = 1e-3, max_ite
         gmin = np.where(lo, v, np.inf).min()
         if gmax - gmin < tol:
             break
-        # second-order working set selection (libsvm WSS2)
+        # second-order working set selection (libsvm WSS2): a_it = Q_ii + Q_tt - 2 y_i y_t Q_it
+        #                                                        = K_ii + K_tt - 2 K_it
         b_ = gmax - v
-        a_ = K[i, i] + np.diag(K) - 2 * y[i] * y * Q[i] * y
+        a_ = K[i, i] + np.diag(K) - 2 * K[i]
         a_ = np.where(a_ > 0, a_, tau)
         cand = lo & (v < gmax)
         obj = np.where(cand, -(b_ * b_) / a_, np.inf)
@@ -89,7 +95,14 @@ def smo(K: np.ndarray, y: np.ndarray, C: float = 1.0, tol: float = 1e-3, max_ite
         dai, daj = ai - a[i], aj - a[j]
         a[i], a[j] = ai, aj
         G += Q[:, i] * dai + Q[:, j] * daj
-    # bias: average over free SVs (libsvm's rho)
+    if return_grad:
+        return a, G
+    return a, _bias(a, G, y, C)
+
+
+def _bias(a, G, y, C) -> float:
+    """-rho of libsvm: mean of y G over free SVs, else the middle of the feasible interval."""
+    a, G, y = (np.asarray(v) for v in (a, G, y))
     free = (a > 1e-12) & (a < C - 1e-12)
     yG = y * G
     if free.any():
@@ -100,7 +113,42 @@ def smo(K: np.ndarray, y: np.ndarray, C: float = 1.0, tol: float = 1e-3, max_ite
         ub = yG[lo].min() if lo.any() else 0.0
         lb = yG[up].max() if up.any() else 0.0
         rho = (ub + lb) / 2
-    return a, -rho
+    return float(-rho)
+
+
+def smo_batched(Ks, ys, C=1.0, tol: float = 1e-3, max_iter: int = 100000):
+    """Solve several dual C-SVC problems at once: one wave64 per problem on the GPU
+    (``svm_smo.hip``), the host oracle per problem on CPU. ``Ks``: list of [n_b, n_b] kernel
+    matrices (or one [B, n, n] tensor), ``ys``: labels (> 0 -> +1), ``C``: scalar or per problem.
+    Returns a list of (alpha [n_b] fp64 tensor, b float, iterations)."""
+    Ks = list(Ks)
+    ys = list(ys)
+    B = len(Ks)
+    Cs = [float(C)] * B if np.isscalar(C) else [float(c) for c in C]
+    dev = Ks[0].device if torch.is_tensor(Ks[0]) else torch.device("cpu")
+    if dev.type == "cuda":
+        from ..ops.native import lib
+        ns = [int(k.shape[0]) for k in Ks]
+        nmax = max(ns)
+        if nmax <= lib().smo_max_n():
+            Kb = torch.zeros(B, nmax, nmax, dtype=torch.float64, device=dev)
+            Yb = torch.ones(B, nmax, dtype=torch.float64, device=dev)
+            for b, (k, yv) in enumerate(zip(Ks, ys)):
+                Kb[b, :ns[b], :ns[b]] = k.double()
+                Yb[b, :ns[b]] = torch.where(yv.to(dev) > 0, 1.0, -1.0).double()
+            Cd = torch.tensor(Cs, dtype=torch.float64, device=dev)
+            A, G, it = lib().svm_smo(Kb, Yb, ns, Cd, float(tol), int(max_iter))
+            A, G, it, Yh = A.cpu().numpy(), G.cpu().numpy(), it.cpu().tolist(), Yb.cpu().numpy()
+            return [(torch.as_tensor(A[b, :ns[b]], device=dev),
+                     _bias(A[b, :ns[b]], G[b, :ns[b]], Yh[b, :ns[b]], Cs[b]), it[b])
+                    for b in range(B)]
+    out = []
+    for k, yv, c in zip(Ks, ys, Cs):
+        kk = k.double().cpu().numpy() if torch.is_tensor(k) else np.asarray(k, dtype=np.float64)
+        yy = np.where(np.asarray(yv.cpu() if torch.is_tensor(yv) else yv) > 0, 1.0, -1.0)
+        a, G = smo(kk, yy, c, tol, max_iter, return_grad=True)
+        out.append((torch.as_tensor(a, device=dev), _bias(a, G, yy, c), -1))
+    return out
 
 
 class SVC:
@@ -108,7 +156,8 @@ class SVC:
                  scale: bool = True, tol: float = 1e-3):
         self.kernel, self.C, self.gamma, self.scale, self.tol = kernel, C, gamma, scale, tol
 
-    def fit(self, X: torch.Tensor, y: torch.Tensor) -> "SVC":
+    def _problem(self, X: torch.Tensor, y: torch.Tensor):
+        """Scaled training data, +-1 labels and the kernel matrix of one fit."""
         X = X.double()
         if self.scale:
             self.mu = X.mean(0)
@@ -117,12 +166,18 @@ class SVC:
             X = (X - self.mu) / self.sd
         self.gamma_ = self.gamma if self.gamma is not None else 1.0 / X.shape[1]
         yy = torch.where(y.to(X.device) > 0, 1.0, -1.0).double()
-        K = kernel_matrix(X, X, self.kernel, self.gamma_).cpu().numpy()
-        a, b = smo(K, yy.cpu().numpy(), self.C, self.tol)
-        sv = np.nonzero(a > 1e-12)[0]
-        self.support_ = torch.as_tensor(sv, device=X.device)
-        self.SV = X[self.support_]
-        self.coefs = torch.as_tensor(a[sv] * yy.cpu().numpy()[sv], device=X.device)   # a_i y_i
+        return X, yy, kernel_matrix(X, X, self.kernel, self.gamma_)
+
+    def fit(self, X: torch.Tensor, y: torch.Tensor) -> "SVC":
+        X, yy, K = self._problem(X, y)
+        ((a, b, self.n_iter_),) = smo_batched([K], [yy], self.C, self.tol)
+        return self._set_solution(X, yy, a, b)
+
+    def _set_solution(self, X, yy, a, b) -> "SVC":
+        sv = torch.nonzero(a > 1e-12).flatten()
+        self.support_ = sv
+        self.SV = X[sv]
+        self.coefs = (a[sv] * yy[sv]).to(X.device)          # a_i y_i
         self.b = float(b)
         return self
 
@@ -143,6 +198,20 @@ class SVC:
         if self.kernel != "linear":
             return None
         return self.coefs @ self.SV
+
+
+def fit_svcs(Xs: Sequence[torch.Tensor], ys: Sequence[torch.Tensor], kernel: str = "linear",
+             C=1.0, gamma: Optional[float] = None, scale: bool = True,
+             tol: float = 1e-3) -> List[SVC]:
+    """Fit independent SVMs (CV folds, cost grids) with ONE batched SMO launch on the GPU."""
+    Cs = [C] * len(Xs) if np.isscalar(C) else list(C)
+    models = [SVC(kernel, c, gamma, scale, tol) for c in Cs]
+    probs = [m._problem(X, y) for m, X, y in zip(models, Xs, ys)]
+    sols = smo_batched([p[2] for p in probs], [p[1] for p in probs], Cs, tol)
+    for m, (X, yy, _), (a, b, it) in zip(models, probs, sols):
+        m.n_iter_ = it
+        m._set_solution(X, yy, a, b)
+    return models
 
 
 def run_svm(seed: int, kernel: str, X_train: torch.Tensor, y_train: torch.Tensor,

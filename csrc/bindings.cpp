@@ -2,6 +2,7 @@
 // kernels stay torch-free; every launch goes on the caller's current HIP stream and none of them
 // synchronises, so the whole aggregation step can be captured in a hipGraph.
 #include <torch/extension.h>
+#include <climits>
 #include <ATen/hip/HIPContext.h>
 #include <c10/core/DeviceGuard.h>
 
@@ -926,6 +927,34 @@ float* f32opt(const optional<Tensor>& t, const char* name, int64_t numel) {
   return (t.has_value() && t->defined()) ? f32p(*t, name, numel) : nullptr;
 }
 
+std::vector<Tensor> svm_smo(const Tensor& K, const Tensor& y, const std::vector<int64_t>& ns,
+                            const Tensor& C, double tol, int64_t max_iter) {
+  TORCH_CHECK(K.is_cuda() && K.scalar_type() == at::kDouble && K.is_contiguous() && K.dim() == 3 &&
+                  K.size(1) == K.size(2),
+              "svm_smo: K must be a contiguous fp64 GPU tensor [B, n, n]");
+  const int64_t B = K.size(0), nmax = K.size(1);
+  TORCH_CHECK(nmax >= 1 && nmax <= cml::smo_max_n(), "svm_smo: n must be in [1, ",
+              cml::smo_max_n(), "]");
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kDouble && y.is_contiguous() &&
+                  y.numel() == B * nmax, "svm_smo: y must be fp64 [B, n]");
+  TORCH_CHECK(C.is_cuda() && C.scalar_type() == at::kDouble && C.is_contiguous() &&
+                  C.numel() == B, "svm_smo: C must be fp64 [B]");
+  TORCH_CHECK(static_cast<int64_t>(ns.size()) == B, "svm_smo: one size per problem");
+  for (int64_t v : ns) TORCH_CHECK(v >= 1 && v <= nmax, "svm_smo: problem size out of range");
+  TORCH_CHECK(max_iter >= 0 && max_iter <= INT_MAX, "svm_smo: max_iter");
+  const c10::DeviceGuard guard(K.device());
+  std::vector<int> ns32(ns.begin(), ns.end());
+  Tensor nsd = at::from_blob(ns32.data(), {B}, at::TensorOptions().dtype(at::kInt)).to(K.device());
+  Tensor alpha = at::zeros({B, nmax}, K.options());
+  Tensor grad = at::zeros({B, nmax}, K.options());
+  Tensor iters = at::zeros({B}, nsd.options());
+  CML_CHECK_HIP(cml::launch_smo(K.data_ptr<double>(), y.data_ptr<double>(), nsd.data_ptr<int>(),
+                                static_cast<int>(B), static_cast<int>(nmax), C.data_ptr<double>(),
+                                tol, static_cast<int>(max_iter), alpha.data_ptr<double>(),
+                                grad.data_ptr<double>(), iters.data_ptr<int>(), cur_stream()));
+  return {alpha, grad, iters};
+}
+
 void lasso_resid(const Tensor& z, const optional<Tensor>& v0, const Tensor& y, const Tensor& M,
                  const Tensor& nb, Tensor& r, const optional<Tensor>& rsum) {
   TORCH_CHECK(z.dim() == 2, "z: [n, B]");
@@ -1015,6 +1044,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd, "short-sequence MFMA attention forward (fused qkv in)");
   m.def("attn_bwd", &attn_bwd, "short-sequence MFMA attention backward (fused dqkv out)");
   m.def("split_search", &split_search, "tree-ensemble histogram split search (one level)");
+  m.def("svm_smo", &svm_smo, "batched dual C-SVC SMO (one wave per problem)");
+  m.def("smo_max_n", &cml::smo_max_n);
   m.def("lasso_resid", &lasso_resid, "batched logistic-lasso residual (+ intercept gradient)");
   m.def("lasso_step", &lasso_step, "batched FISTA prox / restart / momentum step");
   m.def("lasso_slices", &lasso_slices);

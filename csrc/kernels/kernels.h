@@ -256,4 +256,13 @@ hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* p
                                  float* invstd, float* rmean, float* rvar, float eps,
                                  float momentum, hipStream_t st);
 
+// Batched dual C-SVC (svm_smo.hip): one wave per problem b, SMO with second-order working-set
+// selection on K [B][nmax][nmax] fp64 (problem b uses its leading ns[b] x ns[b] block), labels y
+// [B][nmax] (> 0 -> +1), box C [B]; alpha / grad (dual gradient) [B][nmax], iters [B].
+// nmax <= smo_max_n().
+int smo_max_n();
+hipError_t launch_smo(const double* K, const double* y, const int* ns, int B, int nmax,
+                      const double* C, double tol, int max_iter, double* alpha, double* grad,
+                      int* iters, hipStream_t stream);
+
 }  // namespace cml
