@@ -36,7 +36,7 @@ import numpy as np
 import torch
 
 from .stats import DLDA, NSC, voom_transform
-from .svm import SVC
+from .svm import SVC, fit_svcs
 from .trees import grow_tree
 
 # ============================================================================ preprocessing
@@ -175,6 +175,34 @@ class SVMRadial(_Transformed):
 
     def predict(self, counts):
         return self.svc.predict(self._tx(counts, False))
+
+    @classmethod
+    def cv_accuracy(cls, counts, y, folds, grid, preprocessing: str = "deseq-vst",
+                    sigma=None) -> Dict[float, float]:
+        """Mean CV accuracy per cost in ``grid``: the per-fold transform and sigma are computed
+        once per fold, and every (fold, cost) dual problem is solved in ONE batched SMO launch."""
+        Xs, ys, Cs, gs, tests = [], [], [], [], []
+        for rep in folds:
+            for tr, te in rep:
+                tr_t = torch.as_tensor(tr, device=counts.device)
+                te_t = torch.as_tensor(te, device=counts.device)
+                m = cls(1.0, preprocessing, sigma)
+                X = m._tx(counts[tr_t], True)
+                mu, sd = X.mean(0), X.std(0)
+                sd = torch.where(sd > 0, sd, torch.ones_like(sd))
+                gamma = sigma if sigma is not None else cls.sigest((X - mu) / sd)
+                Xte = m._tx(counts[te_t], False)
+                for c in grid:
+                    Xs.append(X)
+                    ys.append(y[tr_t])
+                    Cs.append(c)
+                    gs.append(gamma)
+                    tests.append((Xte, y[te]))
+        models = fit_svcs(Xs, ys, "radial", C=Cs, gamma=gs)
+        acc: Dict[float, List[float]] = {c: [] for c in grid}
+        for mdl, c, (Xte, yte) in zip(models, Cs, tests):
+            acc[c].append(float((mdl.predict(Xte).cpu() == yte.cpu()).float().mean()))
+        return {c: float(np.mean(v)) for c, v in acc.items()}
 
 
 class PAM(_Transformed):
@@ -603,7 +631,10 @@ def classify(counts: torch.Tensor, y: torch.Tensor, method: str, number: int = 5
     tuning: Dict[object, float] = {}
     if len(grid) > 1:
         folds = repeated_stratified_folds(y, number, repeats, seed)
-        for g in grid:
+        if method == "svmRadial":
+            tuning = SVMRadial.cv_accuracy(counts, y, folds, grid,
+                                           kw.get("preprocessing", "deseq-vst"), kw.get("sigma"))
+        for g in (grid if method != "svmRadial" else []):
             accs = []
             for rep in folds:
                 for tr, te in rep:

@@ -201,11 +201,12 @@ class SVC:
 
 
 def fit_svcs(Xs: Sequence[torch.Tensor], ys: Sequence[torch.Tensor], kernel: str = "linear",
-             C=1.0, gamma: Optional[float] = None, scale: bool = True,
-             tol: float = 1e-3) -> List[SVC]:
-    """Fit independent SVMs (CV folds, cost grids) with ONE batched SMO launch on the GPU."""
+             C=1.0, gamma=None, scale: bool = True, tol: float = 1e-3) -> List[SVC]:
+    """Fit independent SVMs (CV folds, cost grids) with ONE batched SMO launch on the GPU.
+    ``C`` and ``gamma``: one value, or one per problem."""
     Cs = [C] * len(Xs) if np.isscalar(C) else list(C)
-    models = [SVC(kernel, c, gamma, scale, tol) for c in Cs]
+    gs = list(gamma) if isinstance(gamma, (list, tuple)) else [gamma] * len(Xs)
+    models = [SVC(kernel, c, g, scale, tol) for c, g in zip(Cs, gs)]
     probs = [m._problem(X, y) for m, X, y in zip(models, Xs, ys)]
     sols = smo_batched([p[2] for p in probs], [p[1] for p in probs], Cs, tol)
     for m, (X, yy, _), (a, b, it) in zip(models, probs, sols):
