@@ -51,6 +51,19 @@ STEM_PAD4 = os.environ.get("CML_STEM_PAD4", "1") == "1"
 # conv epilogue; conv3 applies bn2 + ReLU in its prologue (y2 never stored). Per shape, see
 # fused_conv1x1_policy.
 FUSED_CONV1X1 = os.environ.get("CML_FUSED_CONV1X1", "1") == "1"
+# identity-block tails whose bn3 backward runs inside conv3's gradient kernels and the next
+# conv1's data-gradient epilogue (ops.conv.bnrelu_conv1x1_bn_res)
+FUSED_BN3_BWD = os.environ.get("CML_FUSED_BN3_BWD", "1") == "1"
+FUSED_BN3_BWD_MAX_PLANES = int(os.environ.get("CML_FUSED_BN3_BWD_MAX_PLANES", "128"))
+
+
+def fused_bn3_bwd_policy(planes: int) -> bool:
+    """Whether an identity block uses the fused tail backward. Measured per stage at batch 2048
+    (bench/bwd_fusion.py, profiles/r02_bwd_fusion15.jsonl): layers 1-2 are bandwidth-bound and
+    gain 1.28 / 0.34 ms per block; on layers 3-4 (14 x 14, 7 x 7) the library GEMMs the fusion
+    replaces are faster than the fused kernels (-0.31 / -0.73 ms per block)."""
+    from ..ops import conv as _c
+    return FUSED_BN3_BWD and planes <= FUSED_BN3_BWD_MAX_PLANES and _c.res_tail_ok(planes)
 
 
 def fused_conv1x1_policy(cin: int, cout: int, hw_out: int, stride: int, prologue: bool) -> bool:
@@ -122,6 +135,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             w2 = w.reshape(Co, C)
             link = ctx.link
             g = link.take() if link is not None else None
+            if isinstance(g, fconv.MaskedGrad):
+                return fconv.masked_link_dgrad(dy, w, g, link), dw, None, None, None, None
             if g is not None:
                 dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
                 if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
@@ -260,6 +275,13 @@ class Bottleneck(nn.Module):
         hw2 = z2.shape[2] * z2.shape[3]
         if fused_conv1x1_policy(planes, planes * 4, hw2, 1, True):
             st2 = fconv.bn_stats(z2, self.bn2)
+            if self.down_conv is None and fused_bn3_bwd_policy(planes):
+                out_link = ResidualLink() if use_links else None
+                y = fconv.bnrelu_conv1x1_bn_res(z2, self.bn2, st2, self.conv3, self.bn3, x,
+                                                link, out_link)
+                if out_link is not None:
+                    y._cml_link = out_link
+                return y
             dg = conv1x1_policy(planes, planes * 4, hw2)[1]
             z, m3, i3 = fconv.bnrelu_conv1x1_bn_stats(z2, self.bn2, st2, self.conv3, self.bn3, dg,
                                                       own_wgrad_ok(planes, planes * 4)

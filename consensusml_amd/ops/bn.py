@@ -30,17 +30,48 @@ class ResidualLink:
         sums it on load (``bn_bwd`` with dy2) — the add pass disappears.
     bn3's backward always runs before conv1's and before the previous block's BN backward (both
     depend on it through the graph), so the hand-off is ordered by the graph itself."""
-    __slots__ = ("grad", "closed")
+    __slots__ = ("grad", "closed", "bn_ctx", "sums")
 
     def __init__(self):
         self.grad = None
         self.closed = False
+        # set by a producer tail that applies its BN backward inside its convs (ops.conv
+        # bnrelu_conv1x1_bn_res): (z, mask, mean, invstd) of that BN, so the consumer's conv1
+        # data-gradient kernel can also emit the BN's backward sums -> sums = (sdz, sdzx, ptr)
+        self.bn_ctx = None
+        self.sums = None
 
     def take(self):
-        """Consumer side: the parked gradient (or None); later producers keep their own."""
+        """Consumer side: the parked gradient (a tensor, a ``MaskedGrad`` or None); later
+        producers keep their own."""
         g, self.grad = self.grad, None
         self.closed = True
         return g
+
+    def take_tensor(self):
+        """``take`` with a ``MaskedGrad`` materialised (consumers without a masked epilogue)."""
+        g = self.take()
+        return g.materialize() if isinstance(g, MaskedGrad) else g
+
+
+class MaskedGrad:
+    """A residual gradient m * g left unmaterialised: g is the block-output gradient (NHWC bf16)
+    and m the forward's ReLU bit mask ([M, C/8] bytes, bit k of byte j = channel 8 j + k). The
+    1x1 data-gradient kernel adds it in its epilogue (``lib().conv1x1_link``); anything else calls
+    ``materialize``."""
+    __slots__ = ("g", "mask")
+
+    def __init__(self, g: torch.Tensor, mask: torch.Tensor):
+        self.g = g
+        self.mask = mask
+
+    def materialize(self) -> torch.Tensor:
+        g = self.g
+        N, C, H, W = g.shape
+        shifts = torch.arange(8, device=g.device, dtype=torch.uint8)
+        bits = (self.mask.view(-1, C // 8, 1) >> shifts) & 1
+        rows = g.permute(0, 2, 3, 1).reshape(-1, C) * bits.view(-1, C).to(g.dtype)
+        return rows.view(N, H, W, C).permute(0, 3, 1, 2)
 
 
 # how often link_tap parked its gradient vs fell back to a normal add (tests pin the order)
@@ -93,7 +124,7 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, mask, gamma, beta, mean, invstd = ctx.saved_tensors
-        dy2 = ctx.out_link.take() if ctx.out_link is not None else None
+        dy2 = ctx.out_link.take_tensor() if ctx.out_link is not None else None
         dx, dg, db, dres = lib().bn_bwd(dy, dy2, x, mask, gamma, beta, mean, invstd, ctx.relu,
                                         ctx.has_res)
         if ctx.has_res and ctx.res_link is not None:
@@ -123,7 +154,7 @@ class _BNAddBNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x1, x2, mask, g1, g2, m1, i1, m2, i2 = ctx.saved_tensors
-        dy2 = ctx.out_link.take() if ctx.out_link is not None else None
+        dy2 = ctx.out_link.take_tensor() if ctx.out_link is not None else None
         dx1, dg1, db1, dx2, dg2, db2 = lib().bn_bwd2(dy, dy2, x1, x2, mask, g1, g2, m1, i1, m2, i2)
         return (dx1, dg1, db1, dx2, dg2, db2) + (None,) * 9
 

@@ -16,6 +16,10 @@ values, shifted by the running mean, folded in fp64), so the BatchNorm forward a
 the ordinary training ones; running statistics are updated by the finalize kernel.
 Gradients: data gradient as a hipBLASLt GEMM (stride 1, per-shape policy of
 ``models.resnet.conv1x1_policy``) or MIOpen; weight gradient on ``wgrad1x1.hip`` or MIOpen.
+
+* ``bnrelu_conv1x1_bn_res``: the identity-block tail, whose backward never materialises bn3's
+  input gradient or the residual gradient (bn3's backward runs inside conv3's gradient kernels and
+  the next conv1 data-gradient epilogue; see _BNReLUConv1x1BNResFn and ``masked_link_dgrad``).
 """
 from __future__ import annotations
 
@@ -24,6 +28,7 @@ from typing import Optional, Tuple
 import torch
 import torch.nn.functional as F
 
+from .bn import MaskedGrad
 from .native import lib
 
 
@@ -44,6 +49,8 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm
         dy2 = dy.permute(0, 2, 3, 1).reshape(N * H * W, Co)
         w2 = w.reshape(Co, C)
         g = link.take() if link is not None else None
+        if isinstance(g, MaskedGrad):
+            return masked_link_dgrad(dy, w, g, link)
         if g is not None:
             dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
             if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
@@ -56,6 +63,22 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm
     dx, _, _ = torch.ops.aten.convolution_backward(
         dy, x, w, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])
     return dx
+
+
+def masked_link_dgrad(dy: torch.Tensor, w: torch.Tensor, mg: MaskedGrad, link) -> torch.Tensor:
+    """dX = dY W + m * g of a stride-1 1x1 conv in one kernel (``conv1x1_link``: the masked
+    residual gradient is added in the epilogue, never materialised). If the link carries the
+    producer's BN context (its bn3 applies its backward in its own convs), the same epilogue
+    emits that BN's backward sums over dX and leaves them on the link."""
+    Co, Ci = w.shape[0], w.shape[1]
+    wt = w.reshape(Co, Ci).t().contiguous()
+    bctx = link.bn_ctx if link is not None else None
+    if bctx is not None:
+        z, mask, mean, invstd = bctx
+        dx, sdz, sdzx = lib().conv1x1_link(dy, wt, mg.g, mg.mask, z, mask, mean, invstd)
+        link.sums = (sdz, sdzx, dx.data_ptr())
+        return dx
+    return lib().conv1x1_link(dy, wt, mg.g, mg.mask)[0]
 
 
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, own: bool,
@@ -116,6 +139,82 @@ class _BNReLUConv1x1BNStatsFn(torch.autograd.Function):
         dy2 = _dgrad(dz3, z, w, 1, ctx.dgrad_gemm, None)
         dz, dg, db, _ = lib().bn_bwd(dy2, None, z, None, gamma, beta, mean, invstd, True, False)
         return dz, dg, db, None, None, dw, None, None, None, None, None, None
+
+
+class _BNReLUConv1x1BNResFn(torch.autograd.Function):
+    """Identity-block tail y = relu(bn3(conv3(relu(bn2(z2)))) + res) with bn3's backward applied
+    inside conv3's gradient kernels.
+
+    Forward: the fused conv (bn2 + ReLU prologue, bn3 statistics epilogue) and bn3's apply with
+    the residual, keeping bn3's ReLU as a bit mask. Backward: bn3's two sums (from the consumer
+    block's conv1 data-gradient epilogue when it left them on ``out_link``, else one reduction
+    pass) give per-channel coefficients of dz3 = a (m ? g : 0) + b z3 + c; conv3's data gradient
+    (``conv1x1_bnbwd``) and weight gradient (``wgrad1x1`` dz_*) form dz3 while staging, so neither
+    dz3 nor the residual gradient is written: the residual gradient m * g is parked on ``res_link``
+    as a ``MaskedGrad`` for this block's conv1 data-gradient epilogue."""
+
+    @staticmethod
+    def forward(ctx, z, g2, b2, mean2, invstd2, w, g3, b3, res, rmean3, rvar3, eps, momentum,
+                res_link, out_link):
+        sc = g2.float() * invstd2
+        bi = b2.float() - mean2 * sc
+        z3, m3, i3 = lib().conv1x1_bn_fwd(z, w, sc, bi, rmean3, rmean3, rvar3, 1, True, eps,
+                                          momentum)
+        y, _, _, mask = lib().bn_fwd(z3, res, g3, b3, None, None, m3, i3, eps, momentum, True,
+                                     False, True)
+        ctx.save_for_backward(z, g2, b2, mean2, invstd2, w, sc, bi, z3, mask, g3, b3, m3, i3)
+        ctx.res_link, ctx.out_link = res_link, out_link
+        if out_link is not None:
+            out_link.bn_ctx = (z3, mask, m3, i3)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        z, g2, b2, mean2, invstd2, w, sc, bi, z3, mask, g3, b3, m3, i3 = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        sums, ol = None, ctx.out_link
+        if ol is not None:
+            extra = ol.take_tensor()
+            if ol.sums is not None and extra is None and ol.sums[2] == gy.data_ptr():
+                sums = ol.sums
+            ol.sums = ol.bn_ctx = None
+            if extra is not None:
+                gy = (gy + extra).contiguous(memory_format=torch.channels_last)
+        M = gy.numel() // gy.shape[1]
+        if sums is None:
+            sums = lib().bn_bwd_sums(gy, None, z3, mask, g3, b3, m3, i3, True)
+        ca, cb, cc, dg3, db3 = lib().bn_bwd_coeffs(sums[0], sums[1], g3, m3, i3, M)
+        Co, Ci = w.shape[0], w.shape[1]
+        dw = None
+        if ctx.needs_input_grad[5]:
+            dw = lib().wgrad1x1(gy, z, w.dtype, sc, bi, z3, mask, ca, cb, cc).view_as(w)
+        dy2 = lib().conv1x1_bnbwd(gy, z3, mask, ca, cb, cc, w.reshape(Co, Ci).t().contiguous())
+        dz, dg2, db2, _ = lib().bn_bwd(dy2, None, z, None, g2, b2, mean2, invstd2, True, False)
+        dres = None
+        if ctx.needs_input_grad[8]:
+            mg = MaskedGrad(gy, mask)
+            if ctx.res_link is not None and not ctx.res_link.closed and ctx.res_link.grad is None:
+                ctx.res_link.grad = mg
+            else:
+                dres = mg.materialize()
+        return (dz, dg2, db2, None, None, dw, dg3, db3, dres) + (None,) * 6
+
+
+def res_tail_ok(planes: int) -> bool:
+    """Channel counts the fused identity tail's kernels take (every ResNet-50 stage)."""
+    return planes % 64 == 0 and planes * 4 <= 2048
+
+
+def bnrelu_conv1x1_bn_res(z: torch.Tensor, bn_a, stats_a, conv, bn_b, res: torch.Tensor,
+                          res_link=None, out_link=None) -> torch.Tensor:
+    """y = relu(bn_b(conv(relu(bn_a(z)))) + res) for an identity block (training, GPU bf16);
+    bn_a's batch statistics ``stats_a`` from ``bn_stats``; bn_b's running statistics are
+    updated. See _BNReLUConv1x1BNResFn for the backward."""
+    mean, invstd = stats_a
+    return _BNReLUConv1x1BNResFn.apply(z, bn_a.weight, bn_a.bias, mean, invstd, conv.weight,
+                                       bn_b.weight, bn_b.bias, res, bn_b.running_mean,
+                                       bn_b.running_var, bn_b.eps, bn_b.momentum, res_link,
+                                       out_link)
 
 
 def conv1x1_bn_stats(x: torch.Tensor, conv, bn, stride: int = 1, dgrad_gemm: bool = False,

@@ -47,7 +47,7 @@ class _StemFn(torch.autograd.Function):
         x, z, idx, gamma, mean, invstd = ctx.saved_tensors
         # a second gradient of y parked by a link_tap consumer (layer1.0's downsample conv) is
         # summed inside the pool backward instead of by an autograd add
-        dy2 = ctx.link.take() if ctx.link is not None else None
+        dy2 = ctx.link.take_tensor() if ctx.link is not None else None
         if dy2 is not None and dy2.shape != dy.shape:
             dy, dy2 = dy + dy2, None
         g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3], dy2)

@@ -213,6 +213,39 @@ std::vector<Tensor> bn_fwd(const Tensor& x, const optional<Tensor>& res, const T
 // dy2 (optional): second part of the output gradient, summed on load. mask (optional): the
 // forward's ReLU bit mask (required for relu with a residual). want_dres: also return the
 // residual gradient.
+// Reduction half of a training BN (+ ReLU) backward: {sdz, sdzx} fp32 [C] (sum dy', sum dy' xhat)
+// for consumers that fold the apply into their own prologue (conv1x1_bnbwd, wgrad1x1 dz_*).
+std::vector<Tensor> bn_bwd_sums(const Tensor& dy_in, const optional<Tensor>& dy2_in,
+                                const Tensor& x, const optional<Tensor>& mask, const Tensor& gamma,
+                                const Tensor& beta, const Tensor& mean, const Tensor& invstd,
+                                bool relu) {
+  check_nhwc(x, "x");
+  Tensor dy = x.dim() == 4 ? dy_in.contiguous(at::MemoryFormat::ChannelsLast) : dy_in.contiguous();
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "dy shape mismatch");
+  Tensor dy2;
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = x.dim() == 4 ? dy2_in->contiguous(at::MemoryFormat::ChannelsLast) : dy2_in->contiguous();
+    check_nhwc(dy2, "dy2");
+    TORCH_CHECK(dy2.sizes() == x.sizes(), "dy2 shape mismatch");
+  }
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  const uint8_t* mp = opt_ptr<const uint8_t>(mask, at::kByte, "mask", M * (C / 8));
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor dgamma = at::empty({C}, gamma.options()), dbeta = at::empty({C}, beta.options());
+  Tensor sdz = at::empty({C}, f32), sdzx = at::empty({C}, f32);
+  Tensor work = at::empty({static_cast<int64_t>(cml::bn_workspace_bytes(M, static_cast<int>(C)) / 4 + 1)}, f32);
+  CML_CHECK_HIP(cml::launch_bn_bwd(dy.data_ptr(), dy2.defined() ? dy2.data_ptr() : nullptr,
+                                   x.data_ptr(), mp, nullptr, nullptr, M, static_cast<int>(C),
+                                   gamma.data_ptr(), beta.data_ptr(), mean.data_ptr<float>(),
+                                   invstd.data_ptr<float>(), dgamma.data_ptr(), dbeta.data_ptr(),
+                                   sdz.data_ptr<float>(), sdzx.data_ptr<float>(), relu ? 1 : 0,
+                                   work.data_ptr(), cur_stream()));
+  return {sdz, sdzx};
+}
+
 std::vector<Tensor> bn_bwd(const Tensor& dy_in, const optional<Tensor>& dy2_in, const Tensor& x,
                            const optional<Tensor>& mask, const Tensor& gamma, const Tensor& beta,
                            const Tensor& mean, const Tensor& invstd, bool relu, bool want_dres) {
@@ -478,7 +511,10 @@ Tensor maxpool_bwd(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W,
 // dW of a stride-1 1x1 conv: dy [N, Co, H, W], x [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 1, 1]
 // in `dtype` (bf16 or fp32).
 Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
-                const optional<Tensor>& pro_sc, const optional<Tensor>& pro_bi) {
+                const optional<Tensor>& pro_sc, const optional<Tensor>& pro_bi,
+                const optional<Tensor>& dz_z, const optional<Tensor>& dz_mask,
+                const optional<Tensor>& dz_a, const optional<Tensor>& dz_b,
+                const optional<Tensor>& dz_c) {
   check_nhwc(x, "x");
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc(dy, "dy");
@@ -492,6 +528,19 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
   const float* sc = opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", Ci);
   const float* bi = opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", Ci);
   TORCH_CHECK((sc == nullptr) == (bi == nullptr), "wgrad1x1: pro_sc and pro_bi together");
+  const void* zp = nullptr;
+  if (dz_z.has_value() && dz_z->defined()) {
+    check_nhwc(*dz_z, "dz_z");
+    TORCH_CHECK(dz_z->sizes() == dy.sizes(), "wgrad1x1: dz_z must have dy's shape");
+    zp = dz_z->data_ptr();
+  }
+  const uint8_t* zm = opt_ptr<const uint8_t>(dz_mask, at::kByte, "dz_mask", P * Co / 8);
+  const float* za = opt_ptr<const float>(dz_a, at::kFloat, "dz_a", Co);
+  const float* zb = opt_ptr<const float>(dz_b, at::kFloat, "dz_b", Co);
+  const float* zc = opt_ptr<const float>(dz_c, at::kFloat, "dz_c", Co);
+  TORCH_CHECK((zp == nullptr) == (zm == nullptr) && (zp == nullptr) == (za == nullptr) &&
+                  (zp == nullptr) == (zb == nullptr) && (zp == nullptr) == (zc == nullptr),
+              "wgrad1x1: dz_z, dz_mask, dz_a, dz_b, dz_c together");
   const c10::DeviceGuard guard(x.device());
   int S = 1, cps = 1;
   cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps);
@@ -500,8 +549,108 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
   CML_CHECK_HIP(cml::launch_wgrad1x1(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(),
                                      dw.data_ptr(), dtype == at::kBFloat16, P,
                                      static_cast<int>(Co), static_cast<int>(Ci), sc, bi,
-                                     cur_stream()));
+                                     cur_stream(), zp, zm, za, zb, zc));
   return dw;
+}
+
+namespace {
+// [Cout, Cin] bf16 weight given for a backward GEMM (already transposed by the caller)
+void check_w2(const Tensor& w, int64_t K, const char* fn) {
+  check_dev(w, "w");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 &&
+                  w.size(1) == K && w.size(0) % 64 == 0 && K % 64 == 0,
+              fn, ": w must be contiguous bf16 [N, K] with N, K multiples of 64");
+}
+}  // namespace
+
+// Data gradient through a BN + ReLU backward prologue (conv1x1.hip PM_BNBWD): g, z [N, K, H, W]
+// NHWC bf16 (output gradient and input of the BN), mask [M, K/8] (the BN's ReLU bits), ca / cb /
+// cc fp32 [K] (bn_bwd_coeffs), w [Nout, K] -> y [N, Nout, H, W] = (ca (m ? g : 0) + cb z + cc) w^T.
+Tensor conv1x1_bnbwd(const Tensor& g, const Tensor& z, const Tensor& mask, const Tensor& ca,
+                     const Tensor& cb, const Tensor& cc, const Tensor& w) {
+  check_nhwc(g, "g");
+  check_nhwc(z, "z");
+  TORCH_CHECK(g.dim() == 4 && z.sizes() == g.sizes(), "conv1x1_bnbwd: g / z shapes");
+  const int64_t N = g.size(0), K = g.size(1), H = g.size(2), W = g.size(3), M = N * H * W;
+  check_w2(w, K, "conv1x1_bnbwd");
+  const int64_t No = w.size(0);
+  const uint8_t* mp = opt_ptr<const uint8_t>(mask, at::kByte, "mask", M * K / 8);
+  const float* pa = opt_ptr<const float>(ca, at::kFloat, "ca", K);
+  const float* pb = opt_ptr<const float>(cb, at::kFloat, "cb", K);
+  const float* pc = opt_ptr<const float>(cc, at::kFloat, "cc", K);
+  const c10::DeviceGuard guard(g.device());
+  Tensor y = at::empty({N, No, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  CML_CHECK_HIP(cml::launch_conv1x1_bnbwd(g.data_ptr(), z.data_ptr(), mp, pa, pb, pc, w.data_ptr(),
+                                          y.data_ptr(), M, static_cast<int>(K),
+                                          static_cast<int>(No), cur_stream()));
+  return y;
+}
+
+// Data gradient with the masked residual gradient added in the epilogue: x [N, K, H, W] NHWC bf16,
+// w [Nout, K], link [N, Nout, H, W] + lmask [M, Nout/8] -> y = x w^T + (lmask ? link : 0). With sz /
+// smask / mean / invstd (the BN + ReLU that consumes y): also {sdz, sdzx} = its backward sums.
+std::vector<Tensor> conv1x1_link(const Tensor& x, const Tensor& w, const Tensor& link,
+                                 const Tensor& lmask, const optional<Tensor>& sz,
+                                 const optional<Tensor>& smask, const optional<Tensor>& mean,
+                                 const optional<Tensor>& invstd) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4, "conv1x1_link: 4-D NHWC input");
+  const int64_t N = x.size(0), K = x.size(1), H = x.size(2), W = x.size(3), M = N * H * W;
+  check_w2(w, K, "conv1x1_link");
+  const int64_t No = w.size(0);
+  check_nhwc(link, "link");
+  TORCH_CHECK(link.dim() == 4 && link.size(0) == N && link.size(1) == No && link.size(2) == H &&
+                  link.size(3) == W, "conv1x1_link: link shape");
+  const uint8_t* lm = opt_ptr<const uint8_t>(lmask, at::kByte, "lmask", M * No / 8);
+  const bool sums = sz.has_value() && sz->defined();
+  const void* szp = nullptr;
+  if (sums) {
+    check_nhwc(*sz, "sz");
+    TORCH_CHECK(sz->sizes() == link.sizes(), "conv1x1_link: sz shape");
+    szp = sz->data_ptr();
+  }
+  const uint8_t* sm = opt_ptr<const uint8_t>(smask, at::kByte, "smask", M * No / 8);
+  const float* mu = opt_ptr<const float>(mean, at::kFloat, "mean", No);
+  const float* is = opt_ptr<const float>(invstd, at::kFloat, "invstd", No);
+  TORCH_CHECK(!sums || (sm && mu && is), "conv1x1_link: sz needs smask, mean, invstd");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor y = at::empty({N, No, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor part, sdz, sdzx;
+  if (sums) {
+    part = at::empty({static_cast<int64_t>(cml::conv1x1_link_part_floats(M, static_cast<int>(K),
+                                                                       static_cast<int>(No)))}, f32);
+    sdz = at::empty({No}, f32);
+    sdzx = at::empty({No}, f32);
+  }
+  CML_CHECK_HIP(cml::launch_conv1x1_link(
+      x.data_ptr(), w.data_ptr(), y.data_ptr(), link.data_ptr(), lm, szp, sums ? sm : nullptr,
+      sums ? mu : nullptr, sums ? is : nullptr, sums ? part.data_ptr<float>() : nullptr,
+      sums ? sdz.data_ptr<float>() : nullptr, sums ? sdzx.data_ptr<float>() : nullptr, M,
+      static_cast<int>(K), static_cast<int>(No), cur_stream()));
+  return {y, sdz, sdzx};
+}
+
+// BN + ReLU backward coefficients from its sums: {ca, cb, cc} fp32 [C] with dz = ca (m ? dy : 0) +
+// cb z + cc, and {dgamma, dbeta} in gamma's dtype (bf16).
+std::vector<Tensor> bn_bwd_coeffs(const Tensor& sdz, const Tensor& sdzx, const Tensor& gamma,
+                                  const Tensor& mean, const Tensor& invstd, int64_t M) {
+  const int64_t C = gamma.numel();
+  TORCH_CHECK(gamma.scalar_type() == at::kBFloat16 && gamma.is_contiguous() && gamma.is_cuda(),
+              "bn_bwd_coeffs: bf16 gamma");
+  const float* s = opt_ptr<const float>(sdz, at::kFloat, "sdz", C);
+  const float* q = opt_ptr<const float>(sdzx, at::kFloat, "sdzx", C);
+  const float* mu = opt_ptr<const float>(mean, at::kFloat, "mean", C);
+  const float* is = opt_ptr<const float>(invstd, at::kFloat, "invstd", C);
+  const c10::DeviceGuard guard(gamma.device());
+  auto f32 = gamma.options().dtype(at::kFloat);
+  Tensor ca = at::empty({C}, f32), cb = at::empty({C}, f32), cc = at::empty({C}, f32);
+  Tensor dg = at::empty_like(gamma), db = at::empty_like(gamma);
+  CML_CHECK_HIP(cml::launch_bn_bwd_coeffs(s, q, gamma.data_ptr(), mu, is, static_cast<int>(C), M,
+                                          ca.data_ptr<float>(), cb.data_ptr<float>(),
+                                          cc.data_ptr<float>(), dg.data_ptr(), db.data_ptr(),
+                                          cur_stream()));
+  return {ca, cb, cc, dg, db};
 }
 
 // Fused 1x1 conv forward (conv1x1.hip): x [N, K, H, W] NHWC bf16, w [Cout, K, 1, 1] bf16 ->
@@ -1028,7 +1177,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "fused 1x1 conv forward (MFMA) + BN statistics epilogue + optional BN-ReLU prologue");
   m.def("bn_stats", &bn_stats, "training BatchNorm statistics (mean, invstd) only");
   m.def("wgrad1x1", &wgrad1x1, py::arg("dy"), py::arg("x"), py::arg("dtype"),
-        py::arg("pro_sc") = py::none(), py::arg("pro_bi") = py::none(), "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
+        py::arg("pro_sc") = py::none(), py::arg("pro_bi") = py::none(),
+        py::arg("dz_z") = py::none(), py::arg("dz_mask") = py::none(), py::arg("dz_a") = py::none(),
+        py::arg("dz_b") = py::none(), py::arg("dz_c") = py::none(),
+        "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
+  m.def("conv1x1_bnbwd", &conv1x1_bnbwd, "1x1 data gradient through a BN + ReLU backward prologue");
+  m.def("conv1x1_link", &conv1x1_link, py::arg("x"), py::arg("w"), py::arg("link"),
+        py::arg("lmask"), py::arg("sz") = py::none(), py::arg("smask") = py::none(),
+        py::arg("mean") = py::none(), py::arg("invstd") = py::none(),
+        "1x1 data gradient + masked residual gradient (+ the consumer BN's backward sums)");
+  m.def("bn_bwd_coeffs", &bn_bwd_coeffs, "BN + ReLU backward coefficients from its sums");
+  m.def("bn_bwd_sums", &bn_bwd_sums, "reduction half of a BN (+ ReLU) backward");
   m.def("maxpool_bwd_sum", &maxpool_bwd_sum, "3x3/s2 max-pool backward + channel sums of dx",
         py::arg("dy"), py::arg("idx"), py::arg("H"), py::arg("W"), py::arg("dy2") = py::none());
   m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");

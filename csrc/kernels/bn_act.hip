@@ -599,6 +599,7 @@ void bwd_t(const bf16* d, const bf16* d2, const bf16* xb, const uint8_t* mk, bf1
                                                        bt, part);
   bn_bwd_finalize_kernel<<<(C + kFC - 1) / kFC, kBT, 0, st>>>(part, g.nb, C, sdz, sdzx, dgamma,
                                                               dbeta);
+  if (dxb == nullptr) return;          // sums only (the consumer applies the backward itself)
   bn_bwd_apply_kernel<RM, DRES, DY2><<<apply_grid(M, C), kBT, 0, st>>>(
       d, d2, xb, mk, dxb, drb, M, C, mean, invstd, gm, bt, sdz, sdzx);
 }

@@ -3,7 +3,9 @@
 //
 //   y[m][n] = sum_k W[n][k] * f(x[src(m)][k])         m = output pixel, n = output channel
 //   f(v)    = v                                     (plain)
-//           = max(v * sc[k] + bi[k], 0)             (PRO: the previous BN + ReLU, applied on load)
+//           = max(v * sc[k] + bi[k], 0)             (PM_BNRELU: the previous BN + ReLU, applied on load)
+//           = a (mask ? v : 0) + b z + c            (PM_BNBWD: a BN + ReLU backward on load; data
+//                                                    gradient of a conv whose output fed that BN)
 //   src(m)  = m, or the stride-2 input pixel of m   (S2: ResNet downsample convs)
 //   part    = per-workgroup (sum, sum of squares) of (y_bf16 - shift[n]) for the BN finalize
 //
@@ -47,14 +49,25 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
 // ds_read_b128 lane group ({0-3,12-15,20-27}, ...) over 16 distinct 16-B bank slots.
 __device__ __forceinline__ int swz(int row, int c) { return row * 128 + 16 * (c ^ ((row >> 1) & 7)); }
 
+// Prologue modes (f applied to x while staging) and statistics modes (epilogue sums).
+enum { PM_NONE = 0, PM_BNRELU = 1, PM_BNBWD = 2 };
+enum { SM_BN = 0, SM_BNBWD = 1, SM_OFF = 2 };
+
 struct C1Args {
   const uint16_t* x;      // [rows_in][K]
   const uint16_t* w;      // [N][K]
   uint16_t* y;            // [M][N]
   float* part;            // [ntn][wgpn * WM][2][BN] or null
-  const float* pro_sc;    // PRO: [K]
-  const float* pro_bi;    // PRO: [K]
-  const float* shift;     // [N] or null (statistics shift, e.g. the BN running mean)
+  const float* pro_sc;    // PM_BNRELU: sc[K]; PM_BNBWD: a[K]
+  const float* pro_bi;    // PM_BNRELU: bi[K]; PM_BNBWD: b[K]
+  const float* pro_c;     // PM_BNBWD: c[K]
+  const uint16_t* x2;     // PM_BNBWD: z [rows_in][K] (the BN input)
+  const uint8_t* xm;      // PM_BNBWD: ReLU bit mask of the BN output [rows_in][K / 8]
+  const uint16_t* link;   // EL: [M][N] added to the product where lm's bit is set
+  const uint8_t* lm;      // EL: [M][N / 8]
+  const uint16_t* sz;     // SM_BNBWD: z of the BN whose backward sums are taken [M][N]
+  const uint8_t* sm;      // SM_BNBWD: its ReLU bit mask [M][N / 8]
+  const float* shift;     // [N] or null (SM_BN: statistics shift; SM_BNBWD: the BN's mean)
   int M, K, N;
   int ntn, wgpn, mtiles;
   int H, W, OW, OHW;      // S2: input H, W; output W and H*W
@@ -84,36 +97,65 @@ __device__ __forceinline__ void stage_w(const C1Args& a, char* dst, int n0, int 
   for (int j = 0; j < CA; ++j) *reinterpret_cast<uint4*>(dst + swz(srow + 32 * j, ch)) = tw[j];
 }
 
-template <int CB, int BM, bool S2>
-__device__ __forceinline__ void load_x(const C1Args& a, uint4 (&pb)[CB], int t, int ks, int srow,
-                                       int ch) {
+// x step ks (and, for PM_BNBWD, the matching z chunks and mask bytes) into prefetch registers
+template <int CB, int BM, bool S2, int PM>
+__device__ __forceinline__ void load_x(const C1Args& a, uint4 (&pb)[CB], uint4 (&pz)[CB],
+                                       uint32_t (&pm)[CB], int t, int ks, int srow, int ch) {
 #pragma unroll
-  for (int j = 0; j < CB; ++j)
-    pb[j] = *reinterpret_cast<const uint4*>(a.x + src_row(a, t * BM + srow + 32 * j, S2) * a.K + ks * kBK + 8 * ch);
+  for (int j = 0; j < CB; ++j) {
+    const int64_t r = src_row(a, t * BM + srow + 32 * j, S2);
+    pb[j] = *reinterpret_cast<const uint4*>(a.x + r * a.K + ks * kBK + 8 * ch);
+    if constexpr (PM == PM_BNBWD) {
+      pz[j] = *reinterpret_cast<const uint4*>(a.x2 + r * a.K + ks * kBK + 8 * ch);
+      pm[j] = a.xm[r * (a.K / 8) + ks * (kBK / 8) + ch];
+    }
+  }
 }
 
-template <int CB, bool PRO>
-__device__ __forceinline__ void store_x(const uint4 (&pb)[CB], char* sx, const float* s_aff, int K,
-                                        int ks, int srow, int ch) {
-  float sc[8], bi[8];
-  if constexpr (PRO) {
-    const float4* ps = reinterpret_cast<const float4*>(s_aff + ks * kBK + 8 * ch);
-    const float4* pq = reinterpret_cast<const float4*>(s_aff + K + ks * kBK + 8 * ch);
-    const float4 s0 = ps[0], s1 = ps[1], b0 = pq[0], b1 = pq[1];
-    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
-    sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
-    bi[0] = b0.x; bi[1] = b0.y; bi[2] = b0.z; bi[3] = b0.w;
-    bi[4] = b1.x; bi[5] = b1.y; bi[6] = b1.z; bi[7] = b1.w;
+__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
+  const float4 u0 = reinterpret_cast<const float4*>(p)[0], u1 = reinterpret_cast<const float4*>(p)[1];
+  v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w;
+  v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
+}
+
+// f(x) into the LDS image:
+//   PM_BNRELU  max(x sc + bi, 0)                        (the producer's BN + ReLU)
+//   PM_BNBWD   a (mask ? x : 0) + b z + c               (a BN + ReLU backward: x = dL/d(output),
+//              z = the BN input; a = gamma invstd, b = -gamma invstd^2 q / M,
+//              c = -gamma invstd s / M - b mean, with s, q the BN's backward sums)
+template <int CB, int PM>
+__device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)[CB],
+                                        const uint32_t (&pm)[CB], char* sx, const float* s_aff,
+                                        int K, int ks, int srow, int ch) {
+  float sc[8], bi[8], cc[8];
+  if constexpr (PM != PM_NONE) {
+    ld8f(s_aff + ks * kBK + 8 * ch, sc);
+    ld8f(s_aff + K + ks * kBK + 8 * ch, bi);
   }
+  if constexpr (PM == PM_BNBWD) ld8f(s_aff + 2 * K + ks * kBK + 8 * ch, cc);
 #pragma unroll
   for (int j = 0; j < CB; ++j) {
     uint4 v = pb[j];
-    if constexpr (PRO) {
+    if constexpr (PM == PM_BNRELU) {
       uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float lo = fmaxf(fmaf(__uint_as_float(w4[i] << 16), sc[2 * i], bi[2 * i]), 0.f);
         const float hi = fmaxf(fmaf(__uint_as_float(w4[i] & 0xffff0000u), sc[2 * i + 1], bi[2 * i + 1]), 0.f);
+        w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+      }
+      v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    } else if constexpr (PM == PM_BNBWD) {
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t z4[4] = {pz[j].x, pz[j].y, pz[j].z, pz[j].w};
+      const uint32_t bits = pm[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float glo = ((bits >> (2 * i)) & 1u) ? __uint_as_float(w4[i] << 16) : 0.f;
+        const float ghi = ((bits >> (2 * i + 1)) & 1u) ? __uint_as_float(w4[i] & 0xffff0000u) : 0.f;
+        const float lo = fmaf(sc[2 * i], glo, fmaf(bi[2 * i], __uint_as_float(z4[i] << 16), cc[2 * i]));
+        const float hi = fmaf(sc[2 * i + 1], ghi,
+                              fmaf(bi[2 * i + 1], __uint_as_float(z4[i] & 0xffff0000u), cc[2 * i + 1]));
         w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
       }
       v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
@@ -130,6 +172,12 @@ __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], char* sx, const f
 // 128-B pixel row: every store instruction writes whole lines. The read-back also gives each lane
 // a fixed group of 8 channels (lane & 7), so the statistics need 16 registers (sum and sum of
 // squares of 8 channels) instead of 64. Only this wave touches its image: no workgroup barrier.
+//
+// EL: the stored value is bf16(bf16(acc) + (lm bit ? link : 0)) (a data gradient plus the masked
+// residual gradient of the same tensor). SM_BNBWD: the sums are s = sum (sm bit ? v : 0) and
+// q = sum (sm bit ? v : 0) (sz - shift) -- the backward reduction of the BN + ReLU whose output
+// gradient v is (the consumer BN's mean in shift) -- instead of the BN statistics of v.
+template <bool EL, int SM>
 __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], float (&ss)[8],
                                          float (&sq)[8], const float (&sh)[8], char* simg, int m0,
                                          int ncol0, int n0, int lane) {
@@ -156,18 +204,50 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
 #pragma unroll 2
   for (int k = 0; k < 8; ++k) {
     const int p = 8 * k + (lane >> 3);
-    const uint4 v = *reinterpret_cast<const uint4*>(simg + swz(p, c));
+    uint4 v = *reinterpret_cast<const uint4*>(simg + swz(p, c));
     if (m0 + p < a.M) {
-      *reinterpret_cast<uint4*>(a.y + static_cast<int64_t>(m0 + p) * a.N + n0 + ncol0 + 8 * c) = v;
-      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      const int64_t e0 = static_cast<int64_t>(m0 + p) * a.N + n0 + ncol0 + 8 * c;
+      const int64_t b0 = e0 >> 3;                          // mask byte of these 8 channels
+      if constexpr (EL) {
+        const uint4 l = *reinterpret_cast<const uint4*>(a.link + e0);
+        const uint32_t lb = a.lm[b0];
+        const uint32_t l4[4] = {l.x, l.y, l.z, l.w};
+        uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float lo = __uint_as_float(w4[q] << 16) - sh[2 * q];
-        const float hi = __uint_as_float(w4[q] & 0xffff0000u) - sh[2 * q + 1];
-        ss[2 * q] += lo;
-        ss[2 * q + 1] += hi;
-        sq[2 * q] = fmaf(lo, lo, sq[2 * q]);
-        sq[2 * q + 1] = fmaf(hi, hi, sq[2 * q + 1]);
+        for (int q = 0; q < 4; ++q) {
+          const float lo = __uint_as_float(w4[q] << 16) +
+                           (((lb >> (2 * q)) & 1u) ? __uint_as_float(l4[q] << 16) : 0.f);
+          const float hi = __uint_as_float(w4[q] & 0xffff0000u) +
+                           (((lb >> (2 * q + 1)) & 1u) ? __uint_as_float(l4[q] & 0xffff0000u) : 0.f);
+          w4[q] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+        }
+        v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+      *reinterpret_cast<uint4*>(a.y + e0) = v;
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      if constexpr (SM == SM_BN) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float lo = __uint_as_float(w4[q] << 16) - sh[2 * q];
+          const float hi = __uint_as_float(w4[q] & 0xffff0000u) - sh[2 * q + 1];
+          ss[2 * q] += lo;
+          ss[2 * q + 1] += hi;
+          sq[2 * q] = fmaf(lo, lo, sq[2 * q]);
+          sq[2 * q + 1] = fmaf(hi, hi, sq[2 * q + 1]);
+        }
+      } else if constexpr (SM == SM_BNBWD) {
+        const uint4 z = *reinterpret_cast<const uint4*>(a.sz + e0);
+        const uint32_t zb = a.sm[b0];
+        const uint32_t z4[4] = {z.x, z.y, z.z, z.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float lo = ((zb >> (2 * q)) & 1u) ? __uint_as_float(w4[q] << 16) : 0.f;
+          const float hi = ((zb >> (2 * q + 1)) & 1u) ? __uint_as_float(w4[q] & 0xffff0000u) : 0.f;
+          ss[2 * q] += lo;
+          ss[2 * q + 1] += hi;
+          sq[2 * q] = fmaf(lo, __uint_as_float(z4[q] << 16) - sh[2 * q], sq[2 * q]);
+          sq[2 * q + 1] = fmaf(hi, __uint_as_float(z4[q] & 0xffff0000u) - sh[2 * q + 1], sq[2 * q + 1]);
+        }
       }
     }
   }
@@ -182,16 +262,17 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
       for (int k = 0; k < 16; ++k) acc[i][jm][k] = 0.f;
 }
 
-template <int WN, int WM, bool PRO, bool WRES, bool S2>
+template <int WN, int WM, int PM, bool WRES, bool S2, bool EL, int SM>
 __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
+  constexpr int NAFF = PM == PM_BNBWD ? 3 : (PM == PM_BNRELU ? 2 : 0);
   constexpr int BN = 64 * WN, BM = 64 * WM;
   constexpr int CA = BN / 32, CB = BM / 32;     // 16-B staging chunks per thread and step
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KS = a.K / kBK;
   char* sw = smem;                                              // W: (WRES ? KS : 1) x [BN][128 B]
   char* sx = smem + (WRES ? KS : 1) * BN * 128;                 // x: [BM][128 B]
-  float* s_aff = reinterpret_cast<float*>(sx + BM * 128);       // PRO: sc[K], bi[K]
-  float* s_sh = s_aff + (PRO ? 2 * a.K : 0);                    // statistics shift [BN]
+  float* s_aff = reinterpret_cast<float*>(sx + BM * 128);       // prologue coefficients [NAFF][K]
+  float* s_sh = s_aff + NAFF * a.K;                             // statistics shift [BN]
   char* s_img = reinterpret_cast<char*>(s_sh + BN);             // epilogue images: 4 x 8 KB
 
   const int tid = threadIdx.x;
@@ -207,10 +288,11 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
   const int srow = tid >> 3;                                    // first staged row (+32 per item)
 
   for (int c = tid; c < BN; c += kThreads) s_sh[c] = a.shift ? a.shift[n0 + c] : 0.f;
-  if constexpr (PRO) {
+  if constexpr (NAFF > 0) {
     for (int k = tid; k < a.K; k += kThreads) {
       s_aff[k] = a.pro_sc[k];
       s_aff[a.K + k] = a.pro_bi[k];
+      if constexpr (NAFF > 2) s_aff[2 * a.K + k] = a.pro_c[k];
     }
   }
   if constexpr (WRES) {   // the whole W slice of this n-tile, once
@@ -228,10 +310,11 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
   // statistics: lane owns channels n0 + wn*64 + 8 (lane & 7) + q, q < 8 (see epilogue)
   float ss[8], sq[8], sh[8];
 
-  uint4 pb[CB];
+  uint4 pb[CB], pz[CB];
+  uint32_t pm[CB];
   int t = j0, ks = 0;
   if (t < a.mtiles) {
-    load_x<CB, BM, S2>(a, pb, t, 0, srow, ch);
+    load_x<CB, BM, S2, PM>(a, pb, pz, pm, t, 0, srow, ch);
     __syncthreads();                 // s_aff / s_sh / resident W visible
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -239,7 +322,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       ss[q] = 0.f;
       sq[q] = 0.f;
     }
-    store_x<CB, PRO>(pb, sx, s_aff, a.K, 0, srow, ch);
+    store_x<CB, PM>(pb, pz, pm, sx, s_aff, a.K, 0, srow, ch);
     if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, 0);
     __syncthreads();
     for (;;) {
@@ -251,7 +334,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       const bool more = tn < a.mtiles;
       // prefetch the next step's x into registers; past the end, reload the current (valid) step
       // instead of branching around the loads (hipcc would wait for them at the join)
-      load_x<CB, BM, S2>(a, pb, more ? tn : t, more ? ksn : ks, srow, ch);
+      load_x<CB, BM, S2, PM>(a, pb, pz, pm, more ? tn : t, more ? ksn : ks, srow, ch);
       const char* wa = sw + (WRES ? ks : 0) * BN * 128;
 #pragma unroll
       for (int kk = 0; kk < kBK / 16; ++kk) {
@@ -268,17 +351,18 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
           for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(A[i], B[j], acc[i][j]);
       }
       if (ks == KS - 1)
-        epilogue(a, acc, ss, sq, sh, s_img + wave * 8192, t * BM + wm * 64, wn * 64, n0, lane);
+        epilogue<EL, SM>(a, acc, ss, sq, sh, s_img + wave * 8192, t * BM + wm * 64, wn * 64, n0,
+                         lane);
       if (!more) break;
       __syncthreads();               // every wave is done reading this step's LDS
-      store_x<CB, PRO>(pb, sx, s_aff, a.K, ksn, srow, ch);
+      store_x<CB, PM>(pb, pz, pm, sx, s_aff, a.K, ksn, srow, ch);
       if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, ksn);
       __syncthreads();
       t = tn;
       ks = ksn;
     }
   }
-  if (!a.part) return;
+  if (SM == SM_OFF || !a.part) return;
   if (t >= a.mtiles) {   // no tile: zero partials
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -360,13 +444,64 @@ __global__ __launch_bounds__(256) void conv1x1_bn_finalize_kernel(
   }
 }
 
+// BN-backward sums from the partial slab (SM_BNBWD): sdz = S, sdzx = Q * invstd (same fixed fold
+// order as the statistics finalize).
+__global__ __launch_bounds__(256) void conv1x1_bnbwd_finalize_kernel(
+    const float* __restrict__ part, int R, int BN, int N, const float* __restrict__ invstd,
+    float* __restrict__ sdz, float* __restrict__ sdzx) {
+  __shared__ double ls[32][8], lq[32][8];
+  const int cl = threadIdx.x & 7, sl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  double S = 0.0, Q = 0.0;
+  if (c < N) {
+    const int nt = c / BN, cc = c - nt * BN;
+    const float* base = part + static_cast<int64_t>(nt) * R * 2 * BN + cc;
+    for (int r = sl; r < R; r += 32) {
+      S += base[static_cast<int64_t>(r) * 2 * BN];
+      Q += base[static_cast<int64_t>(r) * 2 * BN + BN];
+    }
+  }
+  ls[sl][cl] = S;
+  lq[sl][cl] = Q;
+  __syncthreads();
+  if (sl != 0 || c >= N) return;
+  S = 0.0;
+  Q = 0.0;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    S += ls[k][cl];
+    Q += lq[k][cl];
+  }
+  sdz[c] = static_cast<float>(S);
+  sdzx[c] = static_cast<float>(Q * static_cast<double>(invstd[c]));
+}
+
+// Per-channel coefficients of a training BN + ReLU backward, dz = a (mask ? dy : 0) + b z + c,
+// from its sums s = sum dy', q = sum dy' xhat (dy' = masked dy); also dgamma = q, dbeta = s.
+__global__ __launch_bounds__(256) void bn_bwd_coeffs_kernel(
+    const float* __restrict__ sdz, const float* __restrict__ sdzx, const uint16_t* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int C, float invM,
+    float* __restrict__ ca, float* __restrict__ cb, float* __restrict__ cc,
+    uint16_t* __restrict__ dgamma, uint16_t* __restrict__ dbeta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float is = invstd[c];
+  const float sc = is * __uint_as_float(static_cast<uint32_t>(gamma[c]) << 16);
+  const float b = -sc * is * sdzx[c] * invM;
+  ca[c] = sc;
+  cb[c] = b;
+  cc[c] = -sc * sdz[c] * invM - b * mean[c];
+  dgamma[c] = f2bf(sdzx[c]);
+  dbeta[c] = f2bf(sdz[c]);
+}
+
 struct Plan {
   int WN, WM, BN, BM, ntn, wgpn, mtiles, G;
   bool wres;
   size_t lds;
 };
 
-Plan plan_for(int WN, int64_t M, int K, int N, bool pro) {
+Plan plan_for(int WN, int64_t M, int K, int N, int naff) {
   Plan p{};
   p.WN = WN;
   p.WM = 4 / p.WN;
@@ -382,7 +517,7 @@ Plan plan_for(int WN, int64_t M, int K, int N, bool pro) {
   p.G = p.ntn * p.wgpn;
   const size_t wbytes = static_cast<size_t>(K) * p.BN * 2;
   const size_t xbytes = static_cast<size_t>(p.BM) * 128;
-  const size_t aff = (pro ? static_cast<size_t>(K) * 8 : 0) + static_cast<size_t>(p.BN) * 4 +
+  const size_t aff = static_cast<size_t>(naff) * K * 4 + static_cast<size_t>(p.BN) * 4 +
                      4 * 8192;                                 // + the per-wave epilogue images
   p.wres = wbytes + xbytes + aff <= 80 * 1024;
   p.lds = (p.wres ? wbytes : static_cast<size_t>(p.BN) * 128) + xbytes + aff;
@@ -392,16 +527,16 @@ Plan plan_for(int WN, int64_t M, int K, int N, bool pro) {
 // Widest n-tile that covers N, except that a 256-channel tile whose W slice cannot stay resident
 // (K > 64) re-stages 32 KB of W per 64 pixels: there 128 x 128 tiles are ~2x faster
 // (bench/conv1x1_fused.py, profiles/r02_conv1x1_*.jsonl).
-Plan make_plan(int64_t M, int K, int N, bool pro) {
+Plan make_plan(int64_t M, int K, int N, int naff) {
   const int WN = N % 256 == 0 ? 4 : (N % 128 == 0 ? 2 : 1);
-  Plan p = plan_for(WN, M, K, N, pro);
-  if (WN == 4 && !p.wres) p = plan_for(2, M, K, N, pro);
+  Plan p = plan_for(WN, M, K, N, naff);
+  if (WN == 4 && !p.wres) p = plan_for(2, M, K, N, naff);
   return p;
 }
 
-template <int WN, int WM, bool PRO, bool WRES, bool S2>
+template <int WN, int WM, int PM, bool WRES, bool S2, bool EL = false, int SM = SM_BN>
 hipError_t launch_t(const C1Args& a, const Plan& p, hipStream_t st) {
-  auto k = &conv1x1_bn_fwd_kernel<WN, WM, PRO, WRES, S2>;
+  auto k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM>;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
   k<<<p.G, kThreads, p.lds, st>>>(a);
@@ -412,21 +547,113 @@ template <int WN, int WM>
 hipError_t launch_w(const C1Args& a, const Plan& p, bool pro, bool s2, hipStream_t st) {
   if (s2) {
     if (pro) return hipErrorInvalidValue;   // strided convs read a materialised block input
-    return p.wres ? launch_t<WN, WM, false, true, true>(a, p, st)
-                  : launch_t<WN, WM, false, false, true>(a, p, st);
+    return p.wres ? launch_t<WN, WM, PM_NONE, true, true>(a, p, st)
+                  : launch_t<WN, WM, PM_NONE, false, true>(a, p, st);
   }
   if (pro)
-    return p.wres ? launch_t<WN, WM, true, true, false>(a, p, st)
-                  : launch_t<WN, WM, true, false, false>(a, p, st);
-  return p.wres ? launch_t<WN, WM, false, true, false>(a, p, st)
-                : launch_t<WN, WM, false, false, false>(a, p, st);
+    return p.wres ? launch_t<WN, WM, PM_BNRELU, true, false>(a, p, st)
+                  : launch_t<WN, WM, PM_BNRELU, false, false>(a, p, st);
+  return p.wres ? launch_t<WN, WM, PM_NONE, true, false>(a, p, st)
+                : launch_t<WN, WM, PM_NONE, false, false>(a, p, st);
+}
+
+// backward variants (stride 1): mode 0 = BN-backward prologue, no statistics; 1 = masked link
+// epilogue; 2 = masked link epilogue + BN-backward sums
+template <int WN, int WM>
+hipError_t launch_bwd_w(const C1Args& a, const Plan& p, int mode, hipStream_t st) {
+  if (mode == 0)
+    return p.wres ? launch_t<WN, WM, PM_BNBWD, true, false, false, SM_OFF>(a, p, st)
+                  : launch_t<WN, WM, PM_BNBWD, false, false, false, SM_OFF>(a, p, st);
+  if (mode == 1)
+    return p.wres ? launch_t<WN, WM, PM_NONE, true, false, true, SM_OFF>(a, p, st)
+                  : launch_t<WN, WM, PM_NONE, false, false, true, SM_OFF>(a, p, st);
+  return p.wres ? launch_t<WN, WM, PM_NONE, true, false, true, SM_BNBWD>(a, p, st)
+                : launch_t<WN, WM, PM_NONE, false, false, true, SM_BNBWD>(a, p, st);
+}
+
+hipError_t launch_bwd(const C1Args& a, const Plan& p, int mode, hipStream_t st) {
+  if (p.WN == 4) return launch_bwd_w<4, 1>(a, p, mode, st);
+  if (p.WN == 2) return launch_bwd_w<2, 2>(a, p, mode, st);
+  return launch_bwd_w<1, 4>(a, p, mode, st);
+}
+
+C1Args base_args(const void* x, const void* w, void* y, int64_t M, int K, int N, const Plan& p) {
+  C1Args a{};
+  a.x = reinterpret_cast<const uint16_t*>(x);
+  a.w = reinterpret_cast<const uint16_t*>(w);
+  a.y = reinterpret_cast<uint16_t*>(y);
+  a.M = static_cast<int>(M);
+  a.K = K;
+  a.N = N;
+  a.ntn = p.ntn;
+  a.wgpn = p.wgpn;
+  a.mtiles = p.mtiles;
+  return a;
+}
+
+bool bad_shape(int64_t M, int K, int N) {
+  return K % kBK || N % 64 || M < 1 || M >= (1ll << 31) || K > 4096 || N > 4096;
 }
 
 }  // namespace
 
 size_t conv1x1_bn_part_floats(int64_t M, int K, int N, bool pro) {
-  const Plan p = make_plan(M, K, N, pro);
+  const Plan p = make_plan(M, K, N, pro ? 2 : 0);
   return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
+}
+
+size_t conv1x1_link_part_floats(int64_t M, int K, int N) {
+  const Plan p = make_plan(M, K, N, 0);
+  return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
+}
+
+hipError_t launch_conv1x1_bnbwd(const void* g, const void* z, const uint8_t* mask, const float* ca,
+                                const float* cb, const float* cc, const void* w, void* y,
+                                int64_t M, int K, int N, hipStream_t st) {
+  if (bad_shape(M, K, N)) return hipErrorInvalidValue;
+  const Plan p = make_plan(M, K, N, 3);
+  C1Args a = base_args(g, w, y, M, K, N, p);
+  a.x2 = reinterpret_cast<const uint16_t*>(z);
+  a.xm = mask;
+  a.pro_sc = ca;
+  a.pro_bi = cb;
+  a.pro_c = cc;
+  return launch_bwd(a, p, 0, st);
+}
+
+hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void* link,
+                               const uint8_t* lm, const void* sz, const uint8_t* sm,
+                               const float* mean, const float* invstd, float* part, float* sdz,
+                               float* sdzx, int64_t M, int K, int N, hipStream_t st) {
+  if (bad_shape(M, K, N)) return hipErrorInvalidValue;
+  const bool sums = sz != nullptr;
+  if (sums && (!sm || !mean || !invstd || !part || !sdz || !sdzx)) return hipErrorInvalidValue;
+  const Plan p = make_plan(M, K, N, 0);
+  C1Args a = base_args(x, w, y, M, K, N, p);
+  a.link = reinterpret_cast<const uint16_t*>(link);
+  a.lm = lm;
+  if (sums) {
+    a.sz = reinterpret_cast<const uint16_t*>(sz);
+    a.sm = sm;
+    a.shift = mean;
+    a.part = part;
+  }
+  hipError_t e = launch_bwd(a, p, sums ? 2 : 1, st);
+  if (e != hipSuccess || !sums) return e;
+  conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N,
+                                                             invstd, sdz, sdzx);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_bwd_coeffs(const float* sdz, const float* sdzx, const void* gamma,
+                                const float* mean, const float* invstd, int C, int64_t M,
+                                float* ca, float* cb, float* cc, void* dgamma, void* dbeta,
+                                hipStream_t st) {
+  bn_bwd_coeffs_kernel<<<(C + 255) / 256, 256, 0, st>>>(
+      sdz, sdzx, reinterpret_cast<const uint16_t*>(gamma), mean, invstd, C,
+      1.0f / static_cast<float>(M), ca, cb, cc, reinterpret_cast<uint16_t*>(dgamma),
+      reinterpret_cast<uint16_t*>(dbeta));
+  return hipGetLastError();
 }
 
 hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* part,
@@ -438,7 +665,7 @@ hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* p
     return hipErrorInvalidValue;
   if (stride != 1 && stride != 2) return hipErrorInvalidValue;
   const bool pro = pro_sc != nullptr;
-  const Plan p = make_plan(M, K, N, pro);
+  const Plan p = make_plan(M, K, N, pro ? 2 : 0);
   C1Args a{};
   a.x = reinterpret_cast<const uint16_t*>(x);
   a.w = reinterpret_cast<const uint16_t*>(w);

@@ -83,7 +83,8 @@ hipError_t launch_bn_fwd(const void* x, const void* res, void* y, void* mask, in
                          int training, void* work, hipStream_t stream);
 // Backward: output gradient dy (+ dy2 if non-null); ReLU from the forward's bit mask when given,
 // else recomputed from x (only valid without a residual); dres (optional) receives the masked
-// output gradient (the residual input's gradient).
+// output gradient (the residual input's gradient). dx == null: the reduction only (sums, dgamma,
+// dbeta), for consumers that apply the backward in their own prologue.
 hipError_t launch_bn_bwd(const void* dy, const void* dy2, const void* x, const void* mask,
                          void* dx, void* dres, int64_t M, int C, const void* gamma,
                          const void* beta, const float* mean, const float* invstd, void* dgamma,
@@ -240,9 +241,13 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
 // Co x Ci floats (wgrad1x1_plan); dw: bf16 (dw_bf16) or fp32 [Co][Ci]. pro_sc / pro_bi (fp32
 // [Ci], both or neither): x is replaced by max(x * sc + bi, 0) (a BN + ReLU never materialised).
 void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps);
+// dz_z / dz_mask / dz_a / dz_b / dz_c (all or none): dy is the output gradient of a BN + ReLU that
+// consumed the conv output z = dz_z; the staging uses dz = a (mask ? dy : 0) + b z + c instead.
 hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
                            int64_t P, int Co, int Ci, const float* pro_sc, const float* pro_bi,
-                           hipStream_t stream);
+                           hipStream_t stream, const void* dz_z = nullptr,
+                           const uint8_t* dz_mask = nullptr, const float* dz_a = nullptr,
+                           const float* dz_b = nullptr, const float* dz_c = nullptr);
 
 // Fused 1x1 convolution forward (conv1x1.hip): y[M][N] = f(x)[src(m)][K] W[N][K]^T on NHWC bf16,
 // f = identity or max(x * pro_sc + pro_bi, 0) per input channel (pro_sc != null), src(m) = m
@@ -255,6 +260,28 @@ hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* p
                                  int64_t M, int K, int N, int stride, int H, int W, float* mean,
                                  float* invstd, float* rmean, float* rvar, float eps,
                                  float momentum, hipStream_t st);
+
+// Backward variants of the fused 1x1 conv (conv1x1.hip), stride 1, W given as [N][K] (for a data
+// gradient: the forward weight transposed).
+//   bnbwd: y = f(g) W^T with f = ca (mask ? g : 0) + cb z + cc per input channel (a BN + ReLU
+//          backward applied while staging: dz never materialised).
+//   link:  y = bf16(x W^T) + (lm ? link : 0) (masked residual gradient added in the epilogue); with
+//          sz non-null also the backward sums of the BN + ReLU that consumes y: sdz = sum m y,
+//          sdzx = sum m y (sz - mean) invstd (m = sm's bit). part: conv1x1_link_part_floats.
+size_t conv1x1_link_part_floats(int64_t M, int K, int N);
+hipError_t launch_conv1x1_bnbwd(const void* g, const void* z, const uint8_t* mask, const float* ca,
+                                const float* cb, const float* cc, const void* w, void* y,
+                                int64_t M, int K, int N, hipStream_t st);
+hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void* link,
+                               const uint8_t* lm, const void* sz, const uint8_t* sm,
+                               const float* mean, const float* invstd, float* part, float* sdz,
+                               float* sdzx, int64_t M, int K, int N, hipStream_t st);
+// dz = ca (mask ? dy : 0) + cb z + cc coefficients of a training BN + ReLU backward from its sums
+// (sdz, sdzx); dgamma = sdzx, dbeta = sdz (bf16).
+hipError_t launch_bn_bwd_coeffs(const float* sdz, const float* sdzx, const void* gamma,
+                                const float* mean, const float* invstd, int C, int64_t M,
+                                float* ca, float* cb, float* cc, void* dgamma, void* dbeta,
+                                hipStream_t st);
 
 // Batched dual C-SVC (svm_smo.hip): one wave per problem b, SMO with second-order working-set
 // selection on K [B][nmax][nmax] fp64 (problem b uses its leading ns[b] x ns[b] block), labels y

@@ -53,11 +53,23 @@ __device__ __forceinline__ int img_off(int row, int ch) {
 // PRO: x is the pre-BN activation z of a BN + ReLU whose output the conv consumed; the staging
 // applies max(z * sc[ci] + bi[ci], 0) (bf16-rounded, as the forward's prologue did), so the
 // BN-ReLU output is never materialised (conv1x1.hip's prologue is the forward counterpart).
-template <int TM, int TN, int KC, bool PRO>
+//
+// DPRO: dy is the output gradient g of a BN + ReLU that consumed the conv's output z; the staging
+// forms the conv's output gradient dz = da (mask ? g : 0) + db z + dc per output channel
+// (conv1x1.hip's PM_BNBWD), so dz is never materialised either.
+struct DPro {
+  const uint16_t* z;      // [P][Co]
+  const uint8_t* mask;    // [P][Co / 8]
+  const float* a;         // [Co]
+  const float* b;
+  const float* c;
+};
+
+template <int TM, int TN, int KC, bool PRO, bool DPRO>
 __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, float* __restrict__ part,
     int P, int Co, int Ci, int tiles_n, int cps, const float* __restrict__ pro_sc,
-    const float* __restrict__ pro_bi) {
+    const float* __restrict__ pro_bi, DPro dp) {
   constexpr int kKC = KC;                              // pixels per chunk
   constexpr int NT = (TM / 64) * (TN / 64) * 64;
   constexpr int CA = TM / 8, CB = TN / 8;            // 16-B chunks per staged row
@@ -84,6 +96,34 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
       pbi[q] = pro_bi[cb + q];
     }
   }
+  // likewise every staged dy item covers the same 8 output channels (NT is a multiple of CA)
+  float da[8], db[8], dc[8];
+  if constexpr (DPRO) {
+    const int cb = co0 + 8 * (tid % CA);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      da[q] = dp.a[cb + q];
+      db[q] = dp.b[cb + q];
+      dc[q] = dp.c[cb + q];
+    }
+  }
+  auto dpro = [&](uint4 v, uint4 zv, uint32_t bits) {
+    if constexpr (DPRO) {
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t z4[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float glo = ((bits >> (2 * i)) & 1u) ? __uint_as_float(w4[i] << 16) : 0.f;
+        const float ghi = ((bits >> (2 * i + 1)) & 1u) ? __uint_as_float(w4[i] & 0xffff0000u) : 0.f;
+        const float lo = fmaf(da[2 * i], glo, fmaf(db[2 * i], __uint_as_float(z4[i] << 16), dc[2 * i]));
+        const float hi = fmaf(da[2 * i + 1], ghi,
+                              fmaf(db[2 * i + 1], __uint_as_float(z4[i] & 0xffff0000u), dc[2 * i + 1]));
+        w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+      }
+      return make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    return v;
+  };
   auto pro = [&](uint4 v) {
     if constexpr (PRO) {
       uint32_t w4[4] = {v.x, v.y, v.z, v.w};
@@ -100,13 +140,18 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
   // prefetch registers; loads are unconditional (clamped pixel, zeroed at use) and selects are
   // component-wise: a branch around the loads makes hipcc wait at the join, and a select of
   // whole uint4 values became a select of addresses that put these registers in scratch
-  uint4 av[IA], bv[IB];
+  uint4 av[IA], bv[IB], zv[DPRO ? IA : 1];
+  uint32_t mv[DPRO ? IA : 1];
   auto fetch = [&](int c) {
 #pragma unroll
     for (int j = 0; j < IA; ++j) {
       const int e = tid + NT * j, row = e / CA, ch = e % CA;
       const int p = min(c * kKC + row, P - 1);
       av[j] = *reinterpret_cast<const uint4*>(dy + static_cast<int64_t>(p) * Co + co0 + 8 * ch);
+      if constexpr (DPRO) {
+        zv[j] = *reinterpret_cast<const uint4*>(dp.z + static_cast<int64_t>(p) * Co + co0 + 8 * ch);
+        mv[j] = dp.mask[static_cast<int64_t>(p) * (Co / 8) + co0 / 8 + ch];
+      }
     }
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
@@ -125,7 +170,9 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
 #pragma unroll
     for (int j = 0; j < IA; ++j) {
       const int e = tid + NT * j, row = e / CA, ch = e % CA;
-      *reinterpret_cast<uint4*>(ab + img_off<TM * 2>(row, ch)) = keep_if(c * kKC + row < P, av[j]);
+      uint4 v = av[j];
+      if constexpr (DPRO) v = dpro(v, zv[j], mv[j]);
+      *reinterpret_cast<uint4*>(ab + img_off<TM * 2>(row, ch)) = keep_if(c * kKC + row < P, v);
     }
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
@@ -240,29 +287,31 @@ void pick_tile(int Co, int Ci, int* TM, int* TN) {
 }
 }  // namespace
 
-template <int TM, int TN, bool PRO>
-void launch_one(dim3 grid, size_t lds, hipStream_t st, const uint16_t* dp, const uint16_t* xp,
+template <int TM, int TN, bool PRO, bool DPRO>
+void launch_one(dim3 grid, size_t lds, hipStream_t st, const uint16_t* dyp, const uint16_t* xp,
                 float* part, int P, int Co, int Ci, int tiles_n, int cps, const float* sc,
-                const float* bi) {
-  auto k = &wgrad1x1_kernel<TM, TN, 64, PRO>;
+                const float* bi, const DPro& dp) {
+  auto k = &wgrad1x1_kernel<TM, TN, 64, PRO, DPRO>;
   if (lds > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-  k<<<grid, (TM / 64) * (TN / 64) * 64, lds, st>>>(dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
+  k<<<grid, (TM / 64) * (TN / 64) * 64, lds, st>>>(dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi,
+                                                    dp);
 }
 
-template <bool PRO>
-bool launch_tile(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, const uint16_t* dp,
+template <bool PRO, bool DPRO>
+bool launch_tile(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, const uint16_t* dyp,
                  const uint16_t* xp, float* part, int P, int Co, int Ci, int tiles_n, int cps,
-                 const float* sc, const float* bi) {
-  // (no PRO variant of the 1024-thread 256 x 256 tile: it spills, and no ResNet shape needs it)
+                 const float* sc, const float* bi, const DPro& dp) {
+  // (no prologue variant of the 1024-thread 256 x 256 tile: it spills, and no ResNet shape needs
+  // it)
   if (TM == 256 && TN == 256) {
-    if constexpr (PRO) return false;
-    else launch_one<256, 256, PRO>(grid, lds, st, dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
-  } else if (TM == 256 && TN == 128) launch_one<256, 128, PRO>(grid, lds, st, dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
-  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO>(grid, lds, st, dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
-  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO>(grid, lds, st, dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
-  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO>(grid, lds, st, dp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi);
+    if constexpr (PRO || DPRO) return false;
+    else launch_one<256, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
+  } else if (TM == 256 && TN == 128) launch_one<256, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
+  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
+  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
+  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
   else return false;
   return true;
 }
@@ -288,7 +337,11 @@ void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps) {
 
 hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
                            int64_t P, int Co, int Ci, const float* pro_sc, const float* pro_bi,
-                           hipStream_t st) {
+                           hipStream_t st, const void* dz_z, const uint8_t* dz_mask,
+                           const float* dz_a, const float* dz_b, const float* dz_c) {
+  const bool dpro = dz_z != nullptr;
+  if (dpro && (!dz_mask || !dz_a || !dz_b || !dz_c)) return hipErrorInvalidValue;
+  DPro dp{reinterpret_cast<const uint16_t*>(dz_z), dz_mask, dz_a, dz_b, dz_c};
   if (Ci == 64 ? Co % 256 != 0 : (Co % 128 || Ci % 128)) return hipErrorInvalidValue;
   if (P < 1 || P >= (1ll << 31)) return hipErrorInvalidValue;
   if ((pro_sc == nullptr) != (pro_bi == nullptr)) return hipErrorInvalidValue;
@@ -298,17 +351,20 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
   const int KC = chunk_of(TM, TN);
   const int tiles_n = Ci / TN;
   const dim3 grid((Co / TM) * tiles_n, S);
-  const auto* dp = reinterpret_cast<const uint16_t*>(dy);
+  const auto* dyp = reinterpret_cast<const uint16_t*>(dy);
   const auto* xp = reinterpret_cast<const uint16_t*>(x);
   const size_t lds = 2 * static_cast<size_t>(KC) * (TM + TN) * 2;   // two stages
   const int Pi = static_cast<int>(P);
-  if (pro_sc) {
-    if (!launch_tile<true>(TM, TN, grid, lds, st, dp, xp, part, Pi, Co, Ci, tiles_n, cps, pro_sc, pro_bi))
-      return hipErrorInvalidValue;
-  } else if (!launch_tile<false>(TM, TN, grid, lds, st, dp, xp, part, Pi, Co, Ci, tiles_n, cps,
-                                 nullptr, nullptr)) {
-    return hipErrorInvalidValue;
-  }
+  bool ok;
+  if (pro_sc && dpro)
+    ok = launch_tile<true, true>(TM, TN, grid, lds, st, dyp, xp, part, Pi, Co, Ci, tiles_n, cps, pro_sc, pro_bi, dp);
+  else if (pro_sc)
+    ok = launch_tile<true, false>(TM, TN, grid, lds, st, dyp, xp, part, Pi, Co, Ci, tiles_n, cps, pro_sc, pro_bi, dp);
+  else if (dpro)
+    ok = launch_tile<false, true>(TM, TN, grid, lds, st, dyp, xp, part, Pi, Co, Ci, tiles_n, cps, nullptr, nullptr, dp);
+  else
+    ok = launch_tile<false, false>(TM, TN, grid, lds, st, dyp, xp, part, Pi, Co, Ci, tiles_n, cps, nullptr, nullptr, dp);
+  if (!ok) return hipErrorInvalidValue;
   const int64_t n = static_cast<int64_t>(Co) * Ci;
   const int fb = static_cast<int>((n / 4 + 255) / 256);
   if (dw_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, dw);

@@ -1,0 +1,174 @@
+"""Backward fusion of the identity-block tail (ops.conv.bnrelu_conv1x1_bn_res): the BN-backward
+prologue of the 1x1 data-gradient kernel, the masked-link epilogue (+ BN-backward sums), the
+coefficient kernel and the weight-gradient dz prologue, each against an fp32 PyTorch oracle; and
+whole blocks with the fusion on vs off."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from consensusml_amd.ops.native import lib
+    return lib()
+
+
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _bits(mask, C):
+    sh = torch.arange(8, device=mask.device, dtype=torch.uint8)
+    return ((mask.view(-1, C // 8, 1) >> sh) & 1).view(-1, C).float()
+
+
+def _rows(t):
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1]).float()
+
+
+def _rand_mask(M, C, dev, gen):
+    return torch.randint(0, 256, (M, C // 8), generator=gen, device=dev, dtype=torch.uint8)
+
+
+def _close(a, b, tol):
+    err = (a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)
+    assert err < tol, f"relative error {err:.3e} >= {tol}"
+
+
+@pytest.mark.parametrize("N,K,No,H", [(2, 256, 64, 28), (3, 512, 128, 14), (2, 1024, 256, 7),
+                                      (1, 2048, 512, 7)])
+def test_conv1x1_bnbwd(cuda, N, K, No, H):
+    g0 = torch.Generator(device=cuda).manual_seed(0)
+    g = _nhwc(torch.randn(N, K, H, H, device=cuda, generator=g0).bfloat16())
+    z = _nhwc(torch.randn(N, K, H, H, device=cuda, generator=g0).bfloat16())
+    M = N * H * H
+    mask = _rand_mask(M, K, cuda, g0)
+    ca, cb, cc = (torch.randn(K, device=cuda, generator=g0) for _ in range(3))
+    w = (torch.randn(No, K, device=cuda, generator=g0) * K ** -0.5).bfloat16()
+    y = _lib().conv1x1_bnbwd(g, z, mask, ca, cb, cc, w)
+    dz = (ca * (_bits(mask, K) * _rows(g)) + cb * _rows(z) + cc).bfloat16().float()
+    ref = dz @ w.float().t()
+    _close(_rows(y), ref, 1e-2)
+
+
+@pytest.mark.parametrize("sums", [False, True])
+@pytest.mark.parametrize("N,K,No,H", [(2, 64, 256, 28), (2, 128, 512, 14), (3, 256, 1024, 7),
+                                      (2, 512, 2048, 7)])
+def test_conv1x1_link(cuda, sums, N, K, No, H):
+    g0 = torch.Generator(device=cuda).manual_seed(1)
+    x = _nhwc(torch.randn(N, K, H, H, device=cuda, generator=g0).bfloat16())
+    w = (torch.randn(No, K, device=cuda, generator=g0) * K ** -0.5).bfloat16()
+    link = _nhwc(torch.randn(N, No, H, H, device=cuda, generator=g0).bfloat16())
+    M = N * H * H
+    lm = _rand_mask(M, No, cuda, g0)
+    ref = (_rows(x) @ w.float().t()).bfloat16().float() + _bits(lm, No) * _rows(link)
+    if not sums:
+        y, _, _ = _lib().conv1x1_link(x, w, link, lm)
+        _close(_rows(y), ref, 1e-2)
+        return
+    sz = _nhwc(torch.randn(N, No, H, H, device=cuda, generator=g0).bfloat16())
+    sm = _rand_mask(M, No, cuda, g0)
+    mean = torch.randn(No, device=cuda, generator=g0) * 0.1
+    invstd = torch.rand(No, device=cuda, generator=g0) + 0.5
+    y, sdz, sdzx = _lib().conv1x1_link(x, w, link, lm, sz, sm, mean, invstd)
+    _close(_rows(y), ref, 1e-2)
+    yv = _rows(y) * _bits(sm, No)
+    torch.testing.assert_close(sdz, yv.sum(0), rtol=1e-3, atol=1e-2 * M ** 0.5)
+    q = (yv * (_rows(sz) - mean) * invstd).sum(0)
+    torch.testing.assert_close(sdzx, q, rtol=1e-3, atol=1e-2 * M ** 0.5)
+
+
+def test_coeffs_reproduce_bn_backward(cuda):
+    """a (m ? g : 0) + b z + c from bn_bwd_sums / bn_bwd_coeffs == the BN backward's dx."""
+    g0 = torch.Generator(device=cuda).manual_seed(2)
+    N, C, H = 4, 256, 14
+    z = _nhwc((torch.randn(N, C, H, H, device=cuda, generator=g0) * 2 + 0.5).bfloat16())
+    res = _nhwc(torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16())
+    gamma = (torch.rand(C, device=cuda, generator=g0) + 0.5).bfloat16()
+    beta = (torch.randn(C, device=cuda, generator=g0) * 0.1).bfloat16()
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y, mean, invstd, mask = _lib().bn_fwd(z, res, gamma, beta, rm, rv, None, None, 1e-5, 0.1,
+                                          True, True, True)
+    gy = _nhwc(torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16())
+    dx, dg, db, dres = _lib().bn_bwd(gy, None, z, mask, gamma, beta, mean, invstd, True, True)
+    sdz, sdzx = _lib().bn_bwd_sums(gy, None, z, mask, gamma, beta, mean, invstd, True)
+    M = N * H * H
+    ca, cb, cc, dg2, db2 = _lib().bn_bwd_coeffs(sdz, sdzx, gamma, mean, invstd, M)
+    dz = ca * (_bits(mask, C) * _rows(gy)) + cb * _rows(z) + cc
+    _close(dz, _rows(dx), 2e-2)
+    torch.testing.assert_close(dg2.float(), dg.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(db2.float(), db.float(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(_bits(mask, C) * _rows(gy), _rows(dres))
+
+
+@pytest.mark.parametrize("Co,Ci,H", [(256, 64, 28), (512, 128, 14), (1024, 256, 14),
+                                     (2048, 512, 7)])
+def test_wgrad_dz_prologue(cuda, Co, Ci, H):
+    g0 = torch.Generator(device=cuda).manual_seed(3)
+    N = 4
+    gy = _nhwc(torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16())
+    z3 = _nhwc(torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16())
+    z2 = _nhwc(torch.randn(N, Ci, H, H, device=cuda, generator=g0).bfloat16())
+    M = N * H * H
+    mask = _rand_mask(M, Co, cuda, g0)
+    ca, cb, cc = (torch.randn(Co, device=cuda, generator=g0) for _ in range(3))
+    sc = torch.rand(Ci, device=cuda, generator=g0) + 0.5
+    bi = torch.randn(Ci, device=cuda, generator=g0) * 0.1
+    dw = _lib().wgrad1x1(gy, z2, torch.float32, sc, bi, z3, mask, ca, cb, cc)
+    dz = (ca * (_bits(mask, Co) * _rows(gy)) + cb * _rows(z3) + cc).bfloat16().float()
+    x = torch.relu(_rows(z2) * sc + bi).bfloat16().float()
+    ref = dz.t() @ x
+    _close(dw.view(Co, Ci), ref, 1e-2)
+
+
+def _chain(cuda, planes, blocks, seed=0):
+    from consensusml_amd.models.resnet import Bottleneck
+    torch.manual_seed(seed)
+    m = torch.nn.Sequential(*[Bottleneck(planes * 4, planes) for _ in range(blocks)])
+    for mod in m.modules():
+        if hasattr(mod, "bias") and isinstance(mod.bias, torch.nn.Parameter) \
+                and mod.__class__.__name__ == "BatchNormAct2d":
+            with torch.no_grad():
+                mod.weight.uniform_(0.5, 1.5)
+                mod.bias.uniform_(-0.1, 0.1)
+    return m.to(device=cuda, dtype=torch.bfloat16, memory_format=torch.channels_last).train()
+
+
+def _err(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("planes,H", [(64, 28), (256, 14), (512, 7)])
+def test_identity_chain_fused_vs_unfused(cuda, planes, H):
+    """Three identity blocks (links between them: phase-2 sums in the conv1 epilogue). Both bf16
+    backwards -- fusion on and off -- are compared with an fp32 run of the same weights: the fused
+    one must be as accurate as the unfused one (BN backward amplifies bf16 rounding, so the
+    absolute error level depends on the shape)."""
+    from consensusml_amd.models import resnet
+    m_on = _chain(cuda, planes, 3)
+    m_off = copy.deepcopy(m_on)
+    m32 = copy.deepcopy(m_on).float()
+    g0 = torch.Generator(device=cuda).manual_seed(5)
+    x = _nhwc(torch.randn(8, planes * 4, H, H, device=cuda, generator=g0).bfloat16())
+    gy = _nhwc(torch.randn(8, planes * 4, H, H, device=cuda, generator=g0).bfloat16())
+    outs = {}
+    for key, m, dt in (("on", m_on, torch.bfloat16), ("off", m_off, torch.bfloat16),
+                       ("fp32", m32, torch.float32)):
+        old = resnet.FUSED_BN3_BWD, resnet.FUSED_BN3_BWD_MAX_PLANES
+        resnet.FUSED_BN3_BWD, resnet.FUSED_BN3_BWD_MAX_PLANES = key == "on", 4096
+        try:
+            xi = x.to(dt).clone().requires_grad_(True)
+            y = m(xi)
+            y.backward(gy.to(dt))
+        finally:
+            resnet.FUSED_BN3_BWD, resnet.FUSED_BN3_BWD_MAX_PLANES = old
+        outs[key] = (y.detach().float(), xi.grad.float(), [p.grad.float() for p in m.parameters()])
+    ref = outs["fp32"]
+    for k in (0, 1):
+        e_on, e_off = _err(outs["on"][k], ref[k]), _err(outs["off"][k], ref[k])
+        assert e_on <= 1.5 * e_off + 1e-2, (k, e_on, e_off)
+    for a, b, r in zip(outs["on"][2], outs["off"][2], ref[2]):
+        e_on, e_off = _err(a, r), _err(b, r)
+        assert e_on <= 1.5 * e_off + 2e-2, (e_on, e_off)
