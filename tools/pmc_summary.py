@@ -8,9 +8,12 @@ Per kernel: dispatches, mean duration (from the counter run's own timestamps), m
 values, and derived HBM-side rates: FETCH_SIZE / WRITE_SIZE are KiB per dispatch -> GB/s over the
 dispatch duration; SQ_INSTS_VALU_MFMA_MOPS_BF16 counts 512-FLOP units -> TFLOP/s.
 
-Calibration on this MI355X image: for the fp32->bf16 copy kernel of the same run (reads exactly
-2x the bytes it writes), FETCH_SIZE reports HALF the bytes read while WRITE_SIZE is exact, so
-``--fetch-scale 2`` (default) is applied to the fetch rate; the raw counter column is unscaled.
+Calibration on this MI355X image (tools/diag/fetch_calibration.py, profiles/
+r02_fetch_size_calibration.md): on kernels with exactly known traffic -- a bf16 copy, a bf16 sum
+and an fp32->bf16 cast at 64 MiB (inside the 256 MiB MALL), 1 GiB and 2000 MiB working sets --
+FETCH_SIZE x 1 KiB is 0.500 of the true bytes read in every case (not a cache effect) and
+WRITE_SIZE is exact, so ``--fetch-scale 2`` (default) is applied to the fetch rate; the raw
+counter column is unscaled.
 """
 import collections
 import csv
