@@ -61,7 +61,8 @@ def fused_bn3_bwd_policy(planes: int) -> bool:
     """Whether an identity block uses the fused tail backward. Measured per stage at batch 2048
     (bench/bwd_fusion.py, profiles/r02_bwd_fusion15.jsonl): layers 1-2 are bandwidth-bound and
     gain 1.28 / 0.34 ms per block; on layers 3-4 (14 x 14, 7 x 7) the library GEMMs the fusion
-    replaces are faster than the fused kernels (-0.31 / -0.73 ms per block)."""
+    replaces are faster than the fused kernels (-0.31 / -0.73 ms per block; -0.12 / -0.51 with
+    the MT = 2 tiles, profiles/r02_19_mt2/r02_19_bwdfusion.jsonl)."""
     from ..ops import conv as _c
     return FUSED_BN3_BWD and planes <= FUSED_BN3_BWD_MAX_PLANES and _c.res_tail_ok(planes)
 

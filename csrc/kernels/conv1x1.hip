@@ -28,6 +28,8 @@
 // workgroups that share an m-tile (one per n-tile) get equal blockIdx % 8, i.e. run on one XCD
 // under round-robin placement, so x is read from HBM once and re-read from that XCD's L2 (speed
 // only: any placement is correct).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -262,18 +264,24 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
       for (int k = 0; k < 16; ++k) acc[i][jm][k] = 0.f;
 }
 
-template <int WN, int WM, int PM, bool WRES, bool S2, bool EL, int SM>
+// MT: 64-pixel sub-blocks per wave (wave tile 64 (n) x 64 MT (m)). MT = 2 halves the LDS operand
+// reads per MFMA (2 A + 4 B fragments feed 8 MFMAs instead of 2 + 2 for 4) and the W re-staging
+// per output pixel; its epilogue images then alias the x staging buffer (BM = 256 rows = 32 KB,
+// behind one extra barrier per tile) to stay inside 80 KB of LDS.
+template <int WN, int WM, int PM, bool WRES, bool S2, bool EL, int SM, int MT = 1>
 __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
   constexpr int NAFF = PM == PM_BNBWD ? 3 : (PM == PM_BNRELU ? 2 : 0);
-  constexpr int BN = 64 * WN, BM = 64 * WM;
+  constexpr int BN = 64 * WN, BM = 64 * WM * MT;
   constexpr int CA = BN / 32, CB = BM / 32;     // 16-B staging chunks per thread and step
+  constexpr bool ALIAS = MT > 1;
+  static_assert(!ALIAS || BM * 128 == 4 * 8192, "aliased epilogue images need a 32 KB x buffer");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int KS = a.K / kBK;
   char* sw = smem;                                              // W: (WRES ? KS : 1) x [BN][128 B]
   char* sx = smem + (WRES ? KS : 1) * BN * 128;                 // x: [BM][128 B]
   float* s_aff = reinterpret_cast<float*>(sx + BM * 128);       // prologue coefficients [NAFF][K]
   float* s_sh = s_aff + NAFF * a.K;                             // statistics shift [BN]
-  char* s_img = reinterpret_cast<char*>(s_sh + BN);             // epilogue images: 4 x 8 KB
+  char* s_img = ALIAS ? sx : reinterpret_cast<char*>(s_sh + BN);   // epilogue images: 4 x 8 KB
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -299,14 +307,16 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
     for (int ks = 0; ks < KS; ++ks) stage_w<CA>(a, sw + ks * BN * 128, n0, srow, ch, ks);
   }
 
-  f32x16 acc[2][2];
+  f32x16 acc[MT][2][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int u = 0; u < MT; ++u)
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      acc[i][0][k] = 0.f;
-      acc[i][1][k] = 0.f;
-    }
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        acc[u][i][0][k] = 0.f;
+        acc[u][i][1][k] = 0.f;
+      }
   // statistics: lane owns channels n0 + wn*64 + 8 (lane & 7) + q, q < 8 (see epilogue)
   float ss[8], sq[8], sh[8];
 
@@ -338,21 +348,30 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       const char* wa = sw + (WRES ? ks : 0) * BN * 128;
 #pragma unroll
       for (int kk = 0; kk < kBK / 16; ++kk) {
-        bf16x8_t A[2], B[2];
+        bf16x8_t A[2], B[MT][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
           A[i] = *reinterpret_cast<const bf16x8_t*>(wa + swz(wn * 64 + 32 * i + r32, 2 * kk + h));
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          B[j] = *reinterpret_cast<const bf16x8_t*>(sx + swz(wm * 64 + 32 * j + r32, 2 * kk + h));
+        for (int u = 0; u < MT; ++u)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+          for (int j = 0; j < 2; ++j)
+            B[u][j] = *reinterpret_cast<const bf16x8_t*>(
+                sx + swz(wm * 64 * MT + 64 * u + 32 * j + r32, 2 * kk + h));
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(A[i], B[j], acc[i][j]);
+        for (int u = 0; u < MT; ++u)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[u][i][j] = mfma32(A[i], B[u][j], acc[u][i][j]);
       }
-      if (ks == KS - 1)
-        epilogue<EL, SM>(a, acc, ss, sq, sh, s_img + wave * 8192, t * BM + wm * 64, wn * 64, n0,
-                         lane);
+      if (ks == KS - 1) {
+        if constexpr (ALIAS) __syncthreads();   // every wave is done reading x before the images
+#pragma unroll
+        for (int u = 0; u < MT; ++u)
+          epilogue<EL, SM>(a, acc[u], ss, sq, sh, s_img + wave * 8192,
+                           t * BM + wm * 64 * MT + 64 * u, wn * 64, n0, lane);
+      }
       if (!more) break;
       __syncthreads();               // every wave is done reading this step's LDS
       store_x<CB, PM>(pb, pz, pm, sx, s_aff, a.K, ksn, srow, ch);
@@ -496,17 +515,18 @@ __global__ __launch_bounds__(256) void bn_bwd_coeffs_kernel(
 }
 
 struct Plan {
-  int WN, WM, BN, BM, ntn, wgpn, mtiles, G;
+  int WN, WM, MT, BN, BM, ntn, wgpn, mtiles, G;
   bool wres;
   size_t lds;
 };
 
-Plan plan_for(int WN, int64_t M, int K, int N, int naff) {
+Plan plan_for(int WN, int64_t M, int K, int N, int naff, int mt = 1) {
   Plan p{};
   p.WN = WN;
   p.WM = 4 / p.WN;
+  p.MT = mt;
   p.BN = 64 * p.WN;
-  p.BM = 64 * p.WM;
+  p.BM = 64 * p.WM * mt;
   p.ntn = N / p.BN;
   p.mtiles = static_cast<int>((M + p.BM - 1) / p.BM);
   const int target = 512;                                     // 2 workgroups per CU
@@ -518,7 +538,7 @@ Plan plan_for(int WN, int64_t M, int K, int N, int naff) {
   const size_t wbytes = static_cast<size_t>(K) * p.BN * 2;
   const size_t xbytes = static_cast<size_t>(p.BM) * 128;
   const size_t aff = static_cast<size_t>(naff) * K * 4 + static_cast<size_t>(p.BN) * 4 +
-                     4 * 8192;                                 // + the per-wave epilogue images
+                     (mt > 1 ? 0 : 4 * 8192);   // + the per-wave epilogue images (aliased at MT 2)
   p.wres = wbytes + xbytes + aff <= 80 * 1024;
   p.lds = (p.wres ? wbytes : static_cast<size_t>(p.BN) * 128) + xbytes + aff;
   return p;
@@ -527,16 +547,34 @@ Plan plan_for(int WN, int64_t M, int K, int N, int naff) {
 // Widest n-tile that covers N, except that a 256-channel tile whose W slice cannot stay resident
 // (K > 64) re-stages 32 KB of W per 64 pixels: there 128 x 128 tiles are ~2x faster
 // (bench/conv1x1_fused.py, profiles/r02_conv1x1_*.jsonl).
+// CML_C1_MT2=0 disables the MT = 2 tiles (A/B)
+bool mt2_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CML_C1_MT2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 Plan make_plan(int64_t M, int K, int N, int naff) {
   const int WN = N % 256 == 0 ? 4 : (N % 128 == 0 ? 2 : 1);
   Plan p = plan_for(WN, M, K, N, naff);
   if (WN == 4 && !p.wres) p = plan_for(2, M, K, N, naff);
+  // non-resident 128 x 128 tiles: two 64-pixel sub-blocks per wave (see the kernel)
+  // (not with the BN-backward prologue: its extra z / mask prefetch registers would spill)
+  if (p.WN == 2 && !p.wres && naff < 3 && mt2_enabled()) {
+    const Plan q = plan_for(2, M, K, N, naff, 2);
+    if (!q.wres && q.lds <= 80 * 1024) p = q;
+  }
   return p;
 }
 
 template <int WN, int WM, int PM, bool WRES, bool S2, bool EL = false, int SM = SM_BN>
 hipError_t launch_t(const C1Args& a, const Plan& p, hipStream_t st) {
-  auto k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM>;
+  auto k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 1>;
+  if constexpr (WN == 2 && !WRES && PM != PM_BNBWD) {
+    if (p.MT == 2) k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 2>;
+  }
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
   k<<<p.G, kThreads, p.lds, st>>>(a);
