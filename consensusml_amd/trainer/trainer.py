@@ -92,16 +92,19 @@ class ConsensusTrainer:
         start = self.engine.step_count
         t0 = time.perf_counter()
         losses = []
+        stats_ok = self.engine.topo in ("sharded", "allgather")
         for s in range(start, steps):
             ckpt_now = bool(self.cfg.ckpt_every and self.cfg.ckpt_dir
                             and (s + 1) % self.cfg.ckpt_every == 0)
-            if ckpt_now and self.engine.topo in ("sharded", "allgather"):
-                self.engine.record_stats = True      # consensus table of this step
+            log_now = bool(log_every and (s + 1) % log_every == 0)
+            if stats_ok and (ckpt_now or (log_now and self.logger.enabled)):
+                self.engine.record_stats = True      # consensus table / log stats of this step
             loss = self.train_step()
             losses.append(loss)
-            if log_every and (s + 1) % log_every == 0:
+            if log_now:
                 lv = float(loss)
-                self.logger.log(step=s + 1, loss=lv, phases=self.timer.summary())
+                self.logger.log(step=s + 1, loss=lv, phases=self.timer.summary(),
+                                **self._log_stats())
             if ckpt_now:
                 save_checkpoint(self.cfg.ckpt_dir, self.engine, self.cfg, gens=self.gens,
                                 table=self._consensus_table())
@@ -125,6 +128,22 @@ class ConsensusTrainer:
             "samples_per_sec": samples / dt if dt > 0 else float("nan"),
             "wall_s": dt,
         }
+
+    def _log_stats(self) -> Dict[str, object]:
+        """Observability fields of a JSONL step record: selection counts and
+        aggregation weights of the rule, and -- when the step was recorded -- per-worker gradient
+        norms, distances to the aggregate and Krum scores (whole model)."""
+        e = self.engine
+        out: Dict[str, object] = {"selection_counts": e.sel_counts.cpu().tolist(),
+                                  "weights": e.w[: e.n].float().cpu().tolist()}
+        st = e.last_stats
+        if st is not None and st.get("step") == e.step_count - 1:   # recorded by the last step
+            out["worker_grad_norm"] = st["sqnorm"].sum(0).sqrt().tolist()
+            out["worker_dist_to_aggregate"] = st["dist2"].sum(0).sqrt().tolist()
+            out["aggregate_grad_norm"] = float(st["agg_sqnorm"].sum().sqrt())
+            if st.get("scores") is not None:
+                out["krum_scores"] = st["scores"].tolist()
+        return out
 
     # ------------------------------------------------------------------ evaluation
     @torch.no_grad()

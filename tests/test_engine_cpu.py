@@ -169,3 +169,23 @@ def test_adam_l2_vs_adamw_cpu():
             ref.grad = g.clone()
             o.step()
         torch.testing.assert_close(master, ref.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_jsonl_step_log_has_consensus_stats(tmp_path):
+    """JSONL step records carry selection counts, weights, per-worker gradient norms,
+    distances to the aggregate and Krum scores."""
+    import json
+    cfg = make_cfg("krum", "sharded", V=5, f=1, fault="sign_flip", byz=[2])
+    cfg.log_path = str(tmp_path / "log.jsonl")
+    tr = ConsensusTrainer(cfg, info=CPU)
+    tr.fit(4, log_every=2)
+    tr.close()
+    recs = [json.loads(l) for l in open(cfg.log_path)]
+    assert [r["step"] for r in recs] == [2, 4]
+    for r in recs:
+        assert len(r["selection_counts"]) == 5 and len(r["weights"]) == 5
+        assert len(r["worker_grad_norm"]) == 5 and len(r["worker_dist_to_aggregate"]) == 5
+        assert len(r["krum_scores"]) == 5 and r["aggregate_grad_norm"] > 0
+        # the sign-flipped worker (x10) has the largest gradient norm and is never selected
+        assert max(range(5), key=lambda i: r["worker_grad_norm"][i]) == 2
+        assert r["weights"][2] == 0.0
