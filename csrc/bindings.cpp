@@ -697,6 +697,46 @@ std::vector<Tensor> conv1x1_bn_fwd(const Tensor& x, const Tensor& w, const optio
   return {y, mean, invstd};
 }
 
+// 3x3 / stride 1 / padding 1 conv as an implicit GEMM on the fused 1x1 kernel (conv1x1.hip TAP):
+// x [N, C, H, W] NHWC bf16, w [Cout, C, 3, 3] bf16 (made channels_last: [Cout][3][3][C]) ->
+// {y NHWC, mean, invstd}; pro_sc / pro_bi (fp32 [C]): max(x sc + bi, 0) applied on load.
+std::vector<Tensor> conv3x3_bn_fwd(const Tensor& x, const Tensor& w_in, const optional<Tensor>& pro_sc,
+                                   const optional<Tensor>& pro_bi, const optional<Tensor>& shift,
+                                   const optional<Tensor>& rmean, const optional<Tensor>& rvar,
+                                   bool stats, double eps, double momentum) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4, "conv3x3_bn_fwd: 4-D NHWC input");
+  TORCH_CHECK(w_in.scalar_type() == at::kBFloat16 && w_in.dim() == 4 && w_in.size(1) == x.size(1) &&
+                  w_in.size(2) == 3 && w_in.size(3) == 3, "conv3x3_bn_fwd: w must be bf16 [Cout, C, 3, 3]");
+  Tensor w = w_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), Co = w.size(0);
+  TORCH_CHECK(C % 64 == 0 && Co % 64 == 0, "conv3x3_bn_fwd: channels must be multiples of 64");
+  const int64_t M = N * H * W;
+  const bool pro = pro_sc.has_value() && pro_sc->defined();
+  const float* sc = opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", C);
+  const float* bi = opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", C);
+  TORCH_CHECK(!pro || bi, "pro_bi needed with pro_sc");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor mean, invstd, part;
+  if (stats) {
+    mean = at::empty({Co}, f32);
+    invstd = at::empty({Co}, f32);
+    part = at::empty({static_cast<int64_t>(cml::conv3x3_bn_part_floats(M, static_cast<int>(C),
+                                                                     static_cast<int>(Co), pro))}, f32);
+  }
+  CML_CHECK_HIP(cml::launch_conv3x3_bn_fwd(
+      x.data_ptr(), w.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, sc, bi,
+      opt_ptr<const float>(shift, at::kFloat, "shift", Co), static_cast<int>(N),
+      static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(Co),
+      stats ? mean.data_ptr<float>() : nullptr, stats ? invstd.data_ptr<float>() : nullptr,
+      stats ? opt_ptr<float>(rmean, at::kFloat, "running_mean", Co) : nullptr,
+      stats ? opt_ptr<float>(rvar, at::kFloat, "running_var", Co) : nullptr,
+      static_cast<float>(eps), static_cast<float>(momentum), cur_stream()));
+  return {y, mean, invstd};
+}
+
 // BatchNorm training statistics only: x NHWC bf16 -> {mean, invstd} (fp32 [C]); running stats
 // updated in place when given.
 std::vector<Tensor> bn_stats(const Tensor& x, const optional<Tensor>& rmean,
@@ -1181,6 +1221,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dz_z") = py::none(), py::arg("dz_mask") = py::none(), py::arg("dz_a") = py::none(),
         py::arg("dz_b") = py::none(), py::arg("dz_c") = py::none(),
         "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
+  m.def("conv3x3_bn_fwd", &conv3x3_bn_fwd, "3x3/s1/p1 conv (implicit GEMM) + BN statistics");
   m.def("conv1x1_bnbwd", &conv1x1_bnbwd, "1x1 data gradient through a BN + ReLU backward prologue");
   m.def("conv1x1_link", &conv1x1_link, py::arg("x"), py::arg("w"), py::arg("link"),
         py::arg("lmask"), py::arg("sz") = py::none(), py::arg("smask") = py::none(),

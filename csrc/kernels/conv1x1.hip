@@ -72,7 +72,8 @@ struct C1Args {
   const float* shift;     // [N] or null (SM_BN: statistics shift; SM_BNBWD: the BN's mean)
   int M, K, N;
   int ntn, wgpn, mtiles;
-  int H, W, OW, OHW;      // S2: input H, W; output W and H*W
+  int H, W, OW, OHW;      // S2: input H, W; output W and H*W.  TAP: H, W (in = out) and OHW = H W
+  int C;                  // TAP: input channels (K = 9 C, k = tap C + c, tap = 3 (dy + 1) + dx + 1)
 };
 
 __device__ __forceinline__ int64_t src_row(const C1Args& a, int m, bool s2) {
@@ -100,9 +101,34 @@ __device__ __forceinline__ void stage_w(const C1Args& a, char* dst, int n0, int 
 }
 
 // x step ks (and, for PM_BNBWD, the matching z chunks and mask bytes) into prefetch registers
-template <int CB, int BM, bool S2, int PM>
+// TAP (3x3, stride 1, padding 1 implicit GEMM): k-step ks is 64 channels of one tap; rows whose
+// tap falls into the padding load a valid row and are zeroed at staging (bit j of vm).
+template <int CB, int BM, bool S2, int PM, bool TAP = false>
 __device__ __forceinline__ void load_x(const C1Args& a, uint4 (&pb)[CB], uint4 (&pz)[CB],
-                                       uint32_t (&pm)[CB], int t, int ks, int srow, int ch) {
+                                       uint32_t (&pm)[CB], int t, int ks, int srow, int ch,
+                                       uint32_t& vm) {
+  if constexpr (TAP) {
+    const int CS = a.C >> 6;
+    const int tap = ks / CS, cc = ks - tap * CS;
+    const int ty = tap / 3 - 1, tx = tap - 3 * (tap / 3) - 1;
+    vm = 0;
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      const int m = t * BM + srow + 32 * j;
+      const int mc = m < a.M ? m : a.M - 1;
+      const int img = mc / a.OHW;
+      const int rem = mc - img * a.OHW;
+      const int oh = rem / a.W;
+      const int ow = rem - oh * a.W;
+      const int ih = oh + ty, iw = ow + tx;
+      const bool ok = m < a.M && static_cast<unsigned>(ih) < static_cast<unsigned>(a.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(a.W);
+      const int64_t r = ok ? static_cast<int64_t>(img) * a.OHW + ih * a.W + iw : mc;
+      vm |= (ok ? 1u : 0u) << j;
+      pb[j] = *reinterpret_cast<const uint4*>(a.x + r * a.C + cc * kBK + 8 * ch);
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < CB; ++j) {
     const int64_t r = src_row(a, t * BM + srow + 32 * j, S2);
@@ -125,16 +151,18 @@ __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
 //   PM_BNBWD   a (mask ? x : 0) + b z + c               (a BN + ReLU backward: x = dL/d(output),
 //              z = the BN input; a = gamma invstd, b = -gamma invstd^2 q / M,
 //              c = -gamma invstd s / M - b mean, with s, q the BN's backward sums)
-template <int CB, int PM>
+// kofs: first input channel of this k-step (ks * 64, or the tap's channel chunk); KA: entries per
+// coefficient row of s_aff; TAP: rows with a clear bit in vm are zeroed (padding).
+template <int CB, int PM, bool TAP = false>
 __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)[CB],
                                         const uint32_t (&pm)[CB], char* sx, const float* s_aff,
-                                        int K, int ks, int srow, int ch) {
+                                        int KA, int kofs, int srow, int ch, uint32_t vm = ~0u) {
   float sc[8], bi[8], cc[8];
   if constexpr (PM != PM_NONE) {
-    ld8f(s_aff + ks * kBK + 8 * ch, sc);
-    ld8f(s_aff + K + ks * kBK + 8 * ch, bi);
+    ld8f(s_aff + kofs + 8 * ch, sc);
+    ld8f(s_aff + KA + kofs + 8 * ch, bi);
   }
-  if constexpr (PM == PM_BNBWD) ld8f(s_aff + 2 * K + ks * kBK + 8 * ch, cc);
+  if constexpr (PM == PM_BNBWD) ld8f(s_aff + 2 * KA + kofs + 8 * ch, cc);
 #pragma unroll
   for (int j = 0; j < CB; ++j) {
     uint4 v = pb[j];
@@ -161,6 +189,10 @@ __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)
         w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
       }
       v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    if constexpr (TAP) {
+      const bool ok = (vm >> j) & 1u;
+      v = make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
     }
     *reinterpret_cast<uint4*>(sx + swz(srow + 32 * j, ch)) = v;
   }
@@ -268,9 +300,11 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
 // reads per MFMA (2 A + 4 B fragments feed 8 MFMAs instead of 2 + 2 for 4) and the W re-staging
 // per output pixel; its epilogue images then alias the x staging buffer (BM = 256 rows = 32 KB,
 // behind one extra barrier per tile) to stay inside 80 KB of LDS.
-template <int WN, int WM, int PM, bool WRES, bool S2, bool EL, int SM, int MT = 1>
+template <int WN, int WM, int PM, bool WRES, bool S2, bool EL, int SM, int MT = 1,
+          bool TAP = false>
 __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
   constexpr int NAFF = PM == PM_BNBWD ? 3 : (PM == PM_BNRELU ? 2 : 0);
+  const int KA = TAP ? a.C : a.K;                               // prologue coefficients per row
   constexpr int BN = 64 * WN, BM = 64 * WM * MT;
   constexpr int CA = BN / 32, CB = BM / 32;     // 16-B staging chunks per thread and step
   constexpr bool ALIAS = MT > 1;
@@ -280,7 +314,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
   char* sw = smem;                                              // W: (WRES ? KS : 1) x [BN][128 B]
   char* sx = smem + (WRES ? KS : 1) * BN * 128;                 // x: [BM][128 B]
   float* s_aff = reinterpret_cast<float*>(sx + BM * 128);       // prologue coefficients [NAFF][K]
-  float* s_sh = s_aff + NAFF * a.K;                             // statistics shift [BN]
+  float* s_sh = s_aff + NAFF * KA;                              // statistics shift [BN]
   char* s_img = ALIAS ? sx : reinterpret_cast<char*>(s_sh + BN);   // epilogue images: 4 x 8 KB
 
   const int tid = threadIdx.x;
@@ -297,12 +331,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
 
   for (int c = tid; c < BN; c += kThreads) s_sh[c] = a.shift ? a.shift[n0 + c] : 0.f;
   if constexpr (NAFF > 0) {
-    for (int k = tid; k < a.K; k += kThreads) {
+    for (int k = tid; k < KA; k += kThreads) {
       s_aff[k] = a.pro_sc[k];
-      s_aff[a.K + k] = a.pro_bi[k];
-      if constexpr (NAFF > 2) s_aff[2 * a.K + k] = a.pro_c[k];
+      s_aff[KA + k] = a.pro_bi[k];
+      if constexpr (NAFF > 2) s_aff[2 * KA + k] = a.pro_c[k];
     }
   }
+  // first input channel of k-step ks (TAP: the channel chunk within the tap)
+  auto kofs = [&](int ks_) { return TAP ? (ks_ % (a.C >> 6)) * kBK : ks_ * kBK; };
   if constexpr (WRES) {   // the whole W slice of this n-tile, once
     for (int ks = 0; ks < KS; ++ks) stage_w<CA>(a, sw + ks * BN * 128, n0, srow, ch, ks);
   }
@@ -322,9 +358,10 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
 
   uint4 pb[CB], pz[CB];
   uint32_t pm[CB];
+  uint32_t vm = ~0u;
   int t = j0, ks = 0;
   if (t < a.mtiles) {
-    load_x<CB, BM, S2, PM>(a, pb, pz, pm, t, 0, srow, ch);
+    load_x<CB, BM, S2, PM, TAP>(a, pb, pz, pm, t, 0, srow, ch, vm);
     __syncthreads();                 // s_aff / s_sh / resident W visible
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -332,7 +369,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       ss[q] = 0.f;
       sq[q] = 0.f;
     }
-    store_x<CB, PM>(pb, pz, pm, sx, s_aff, a.K, 0, srow, ch);
+    store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, 0, srow, ch, vm);
     if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, 0);
     __syncthreads();
     for (;;) {
@@ -344,7 +381,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       const bool more = tn < a.mtiles;
       // prefetch the next step's x into registers; past the end, reload the current (valid) step
       // instead of branching around the loads (hipcc would wait for them at the join)
-      load_x<CB, BM, S2, PM>(a, pb, pz, pm, more ? tn : t, more ? ksn : ks, srow, ch);
+      load_x<CB, BM, S2, PM, TAP>(a, pb, pz, pm, more ? tn : t, more ? ksn : ks, srow, ch, vm);
       const char* wa = sw + (WRES ? ks : 0) * BN * 128;
 #pragma unroll
       for (int kk = 0; kk < kBK / 16; ++kk) {
@@ -374,7 +411,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       }
       if (!more) break;
       __syncthreads();               // every wave is done reading this step's LDS
-      store_x<CB, PM>(pb, pz, pm, sx, s_aff, a.K, ksn, srow, ch);
+      store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, kofs(ksn), srow, ch, vm);
       if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, ksn);
       __syncthreads();
       t = tn;
@@ -520,7 +557,8 @@ struct Plan {
   size_t lds;
 };
 
-Plan plan_for(int WN, int64_t M, int K, int N, int naff, int mt = 1) {
+Plan plan_for(int WN, int64_t M, int K, int N, int naff, int mt = 1, int kaff = -1) {
+  if (kaff < 0) kaff = K;
   Plan p{};
   p.WN = WN;
   p.WM = 4 / p.WN;
@@ -537,7 +575,7 @@ Plan plan_for(int WN, int64_t M, int K, int N, int naff, int mt = 1) {
   p.G = p.ntn * p.wgpn;
   const size_t wbytes = static_cast<size_t>(K) * p.BN * 2;
   const size_t xbytes = static_cast<size_t>(p.BM) * 128;
-  const size_t aff = static_cast<size_t>(naff) * K * 4 + static_cast<size_t>(p.BN) * 4 +
+  const size_t aff = static_cast<size_t>(naff) * kaff * 4 + static_cast<size_t>(p.BN) * 4 +
                      (mt > 1 ? 0 : 4 * 8192);   // + the per-wave epilogue images (aliased at MT 2)
   p.wres = wbytes + xbytes + aff <= 80 * 1024;
   p.lds = (p.wres ? wbytes : static_cast<size_t>(p.BN) * 128) + xbytes + aff;
@@ -556,24 +594,25 @@ bool mt2_enabled() {
   return on;
 }
 
-Plan make_plan(int64_t M, int K, int N, int naff) {
+Plan make_plan(int64_t M, int K, int N, int naff, int kaff = -1) {
   const int WN = N % 256 == 0 ? 4 : (N % 128 == 0 ? 2 : 1);
-  Plan p = plan_for(WN, M, K, N, naff);
-  if (WN == 4 && !p.wres) p = plan_for(2, M, K, N, naff);
+  Plan p = plan_for(WN, M, K, N, naff, 1, kaff);
+  if (WN == 4 && !p.wres) p = plan_for(2, M, K, N, naff, 1, kaff);
   // non-resident 128 x 128 tiles: two 64-pixel sub-blocks per wave (see the kernel)
   // (not with the BN-backward prologue: its extra z / mask prefetch registers would spill)
   if (p.WN == 2 && !p.wres && naff < 3 && mt2_enabled()) {
-    const Plan q = plan_for(2, M, K, N, naff, 2);
+    const Plan q = plan_for(2, M, K, N, naff, 2, kaff);
     if (!q.wres && q.lds <= 80 * 1024) p = q;
   }
   return p;
 }
 
-template <int WN, int WM, int PM, bool WRES, bool S2, bool EL = false, int SM = SM_BN>
+template <int WN, int WM, int PM, bool WRES, bool S2, bool EL = false, int SM = SM_BN,
+          bool TAP = false>
 hipError_t launch_t(const C1Args& a, const Plan& p, hipStream_t st) {
-  auto k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 1>;
+  auto k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 1, TAP>;
   if constexpr (WN == 2 && !WRES && PM != PM_BNBWD) {
-    if (p.MT == 2) k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 2>;
+    if (p.MT == 2) k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 2, TAP>;
   }
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
@@ -593,6 +632,16 @@ hipError_t launch_w(const C1Args& a, const Plan& p, bool pro, bool s2, hipStream
                   : launch_t<WN, WM, PM_BNRELU, false, false>(a, p, st);
   return p.wres ? launch_t<WN, WM, PM_NONE, true, false>(a, p, st)
                 : launch_t<WN, WM, PM_NONE, false, false>(a, p, st);
+}
+
+// 3x3 / stride 1 / padding 1 forward (TAP), optional BN + ReLU prologue, BN statistics epilogue
+template <int WN, int WM>
+hipError_t launch_tap_w(const C1Args& a, const Plan& p, bool pro, hipStream_t st) {
+  if (pro)
+    return p.wres ? launch_t<WN, WM, PM_BNRELU, true, false, false, SM_BN, true>(a, p, st)
+                  : launch_t<WN, WM, PM_BNRELU, false, false, false, SM_BN, true>(a, p, st);
+  return p.wres ? launch_t<WN, WM, PM_NONE, true, false, false, SM_BN, true>(a, p, st)
+                : launch_t<WN, WM, PM_NONE, false, false, false, SM_BN, true>(a, p, st);
 }
 
 // backward variants (stride 1): mode 0 = BN-backward prologue, no statistics; 1 = masked link
@@ -643,6 +692,41 @@ size_t conv1x1_bn_part_floats(int64_t M, int K, int N, bool pro) {
 size_t conv1x1_link_part_floats(int64_t M, int K, int N) {
   const Plan p = make_plan(M, K, N, 0);
   return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
+}
+
+size_t conv3x3_bn_part_floats(int64_t M, int C, int N, bool pro) {
+  const Plan p = make_plan(M, 9 * C, N, pro ? 2 : 0, C);
+  return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
+}
+
+hipError_t launch_conv3x3_bn_fwd(const void* x, const void* w, void* y, float* part,
+                                 const float* pro_sc, const float* pro_bi, const float* shift,
+                                 int Nimg, int H, int W, int C, int N, float* mean, float* invstd,
+                                 float* rmean, float* rvar, float eps, float momentum,
+                                 hipStream_t st) {
+  const int64_t M = static_cast<int64_t>(Nimg) * H * W;
+  if (C % kBK || N % 64 || C > 2048 || N > 4096 || M < 1 || M >= (1ll << 31) || H < 1 || W < 1)
+    return hipErrorInvalidValue;
+  const bool pro = pro_sc != nullptr;
+  const int K = 9 * C;
+  const Plan p = make_plan(M, K, N, pro ? 2 : 0, C);
+  C1Args a = base_args(x, w, y, M, K, N, p);
+  a.part = part;
+  a.pro_sc = pro_sc;
+  a.pro_bi = pro_bi;
+  a.shift = shift;
+  a.H = H;
+  a.W = W;
+  a.OHW = H * W;
+  a.C = C;
+  hipError_t e;
+  if (p.WN == 4) e = launch_tap_w<4, 1>(a, p, pro, st);
+  else if (p.WN == 2) e = launch_tap_w<2, 2>(a, p, pro, st);
+  else e = launch_tap_w<1, 4>(a, p, pro, st);
+  if (e != hipSuccess || !part || !mean) return e;
+  conv1x1_bn_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N, M, shift,
+                                                          eps, momentum, mean, invstd, rmean, rvar);
+  return hipGetLastError();
 }
 
 hipError_t launch_conv1x1_bnbwd(const void* g, const void* z, const uint8_t* mask, const float* ca,

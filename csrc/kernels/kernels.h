@@ -261,6 +261,16 @@ hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* p
                                  float* invstd, float* rmean, float* rvar, float eps,
                                  float momentum, hipStream_t st);
 
+// 3x3 / stride 1 / padding 1 convolution as an implicit GEMM in the same kernel (conv1x1.hip TAP):
+// x [Nimg][H][W][C] NHWC bf16, w [N][3][3][C] (channels_last weight), y [Nimg][H][W][N]; optional
+// BN + ReLU prologue on x (pro_sc / pro_bi [C]) and BN statistics of y (as conv1x1_bn_fwd).
+size_t conv3x3_bn_part_floats(int64_t M, int C, int N, bool pro);
+hipError_t launch_conv3x3_bn_fwd(const void* x, const void* w, void* y, float* part,
+                                 const float* pro_sc, const float* pro_bi, const float* shift,
+                                 int Nimg, int H, int W, int C, int N, float* mean, float* invstd,
+                                 float* rmean, float* rvar, float eps, float momentum,
+                                 hipStream_t st);
+
 // Backward variants of the fused 1x1 conv (conv1x1.hip), stride 1, W given as [N][K] (for a data
 // gradient: the forward weight transposed).
 //   bnbwd: y = f(g) W^T with f = ca (mask ? g : 0) + cb z + cc per input channel (a BN + ReLU

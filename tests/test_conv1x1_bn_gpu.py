@@ -189,3 +189,31 @@ def test_resnet50_fused_conv_bn_matches_unfused(cuda):
         if "running" in k:
             torch.testing.assert_close(out["fused"][2][k], out["unfused"][2][k], rtol=2e-2,
                                        atol=2e-3)
+
+
+@pytest.mark.parametrize("N,C,Co,H", [(2, 64, 64, 9), (3, 128, 128, 7), (2, 256, 256, 5),
+                                      (1, 512, 512, 4), (2, 64, 128, 6)])
+@pytest.mark.parametrize("pro", [False, True])
+def test_conv3x3_tap_vs_fp32(cuda, N, C, Co, H, pro):
+    """3x3 / stride 1 / padding 1 implicit GEMM (conv1x1.hip TAP mode): output vs an fp32 conv of
+    the (BN + ReLU'd, bf16-rounded) input; BN statistics of the bf16 output."""
+    import torch.nn.functional as F
+    from consensusml_amd.ops.native import lib
+    g0 = torch.Generator(device=cuda).manual_seed(7)
+    x = torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, 3, 3, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
+    sc = torch.rand(C, device=cuda, generator=g0) + 0.5 if pro else None
+    bi = torch.randn(C, device=cuda, generator=g0) * 0.2 if pro else None
+    rm, rv = torch.zeros(Co, device=cuda), torch.ones(Co, device=cuda)
+    y, mean, invstd = lib().conv3x3_bn_fwd(x, w, sc, bi, rm, rm, rv, True, 1e-5, 0.1)
+    xf = x.float()
+    if pro:
+        xf = torch.relu(xf * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)).bfloat16().float()
+    ref = F.conv2d(xf, w.float(), padding=1)
+    err = (y.float() - ref).norm() / ref.norm()
+    assert err < 5e-3, float(err)
+    yb = y.float()
+    torch.testing.assert_close(mean, yb.mean((0, 2, 3)), rtol=1e-3, atol=1e-3)
+    var = yb.var((0, 2, 3), unbiased=False)
+    torch.testing.assert_close(invstd, torch.rsqrt(var + 1e-5), rtol=2e-3, atol=1e-3)
