@@ -47,6 +47,29 @@ def main():
         rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
         flops = 2 * batch * H * H * 9 * C * C
         t_lib = _t(lambda: F.conv2d(x, w, padding=1))
+        gy = torch.randn_like(x)
+        t_dg = _t(lambda: torch.ops.aten.convolution_backward(
+            gy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]))
+        t_wg = _t(lambda: torch.ops.aten.convolution_backward(
+            gy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
+        # data gradient = the forward TAP conv of gy with the rotated, transposed weights
+        wr = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+        t_own_dg = _t(lambda: L.conv3x3_bn_fwd(gy, wr, None, None, None, None, None, False, 1e-5, 0.1))
+        dref = torch.ops.aten.convolution_backward(gy[:4].float(), x[:4].float(), w.float(), None,
+                                                   [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                   [True, False, False])[0]
+        down, _, _ = L.conv3x3_bn_fwd(gy[:4].contiguous(memory_format=torch.channels_last), wr,
+                                      None, None, None, None, None, False, 1e-5, 0.1)
+        dg_err = float((down.float() - dref).norm() / dref.norm())
+        w2 = w.permute(0, 2, 3, 1).reshape(C, 9 * C).contiguous()
+        wr2 = wr.permute(0, 2, 3, 1).reshape(C, 9 * C).contiguous()
+        t_g = _t(lambda: L.conv_gemm(x, w2, 9))
+        t_gdg = _t(lambda: L.conv_gemm(gy, wr2, 9))
+        yg = L.conv_gemm(x[:4].contiguous(memory_format=torch.channels_last), w2, 9)
+        g_ref = F.conv2d(x[:4].float(), w.float(), padding=1)
+        g_err = float((yg.float() - g_ref).norm() / g_ref.norm())
+        dgg = L.conv_gemm(gy[:4].contiguous(memory_format=torch.channels_last), wr2, 9)
+        gdg_err = float((dgg.float() - dref).norm() / dref.norm())
         t_own = _t(lambda: L.conv3x3_bn_fwd(x, w, None, None, None, None, None, False, 1e-5, 0.1))
         t_own_st = _t(lambda: L.conv3x3_bn_fwd(x, w, sc, bi, rm, rm, rv, True, 1e-5, 0.1))
         # numerics on the first 4 images
@@ -58,7 +81,12 @@ def main():
         print(json.dumps({"C": C, "H": H, "batch": batch, "miopen_ms": round(t_lib, 4),
                           "own_ms": round(t_own, 4), "own_bnrelu_stats_ms": round(t_own_st, 4),
                           "miopen_tflops": round(flops / t_lib / 1e9, 1),
-                          "own_tflops": round(flops / t_own / 1e9, 1), "rel_err": err}), flush=True)
+                          "own_tflops": round(flops / t_own / 1e9, 1), "rel_err": err,
+                          "miopen_dgrad_ms": round(t_dg, 4), "own_dgrad_ms": round(t_own_dg, 4),
+                          "miopen_wgrad_ms": round(t_wg, 4), "dgrad_rel_err": dg_err,
+                          "glds_fwd_ms": round(t_g, 4), "glds_dgrad_ms": round(t_gdg, 4),
+                          "glds_tflops": round(flops / t_g / 1e9, 1),
+                          "glds_fwd_err": g_err, "glds_dgrad_err": gdg_err}), flush=True)
         del x, w
         torch.cuda.empty_cache()
 

@@ -55,6 +55,8 @@ FUSED_CONV1X1 = os.environ.get("CML_FUSED_CONV1X1", "1") == "1"
 # conv1's data-gradient epilogue (ops.conv.bnrelu_conv1x1_bn_res)
 FUSED_BN3_BWD = os.environ.get("CML_FUSED_BN3_BWD", "1") == "1"
 FUSED_BN3_BWD_MAX_PLANES = int(os.environ.get("CML_FUSED_BN3_BWD_MAX_PLANES", "128"))
+# stride-1 3x3 convs: data gradient on csrc/kernels/conv_gemm.hip (ops.conv.conv3x3)
+OWN_DGRAD3X3 = os.environ.get("CML_DGRAD3X3", "1") == "1"
 
 
 def fused_bn3_bwd_policy(planes: int) -> bool:
@@ -240,6 +242,11 @@ class Bottleneck(nn.Module):
         else:
             self.down_conv = None
 
+    def _conv2(self, x: torch.Tensor) -> torch.Tensor:
+        if OWN_DGRAD3X3 and self.training:
+            return fconv.conv3x3(x, self.conv2)
+        return self.conv2(x)
+
     def _fused_ok(self, x: torch.Tensor) -> bool:
         return (FUSED_CONV1X1 and self.training and torch.is_grad_enabled()
                 and fconv.fused_conv_ok(x, self.conv1.weight)
@@ -271,7 +278,7 @@ class Bottleneck(nn.Module):
             dlink = ResidualLink() if use_links and self.conv1.link_ok(x) else None
             z1, st1 = self._conv_bn(x, self.conv1, self.bn1, dlink)
         out = self.bn1(z1, stats=st1)
-        z2 = self.conv2(out)
+        z2 = self._conv2(out)
         planes = self.conv3.in_channels
         hw2 = z2.shape[2] * z2.shape[3]
         if fused_conv1x1_policy(planes, planes * 4, hw2, 1, True):
@@ -319,7 +326,7 @@ class Bottleneck(nn.Module):
             # consumes it (see ops.bn.ResidualLink)
             link = getattr(x, "_cml_link", None) if use_links else None
             out = self.bn1(self.conv1(x, res_link=link if self.conv1.link_ok(x) else None))
-            out = self.bn2(self.conv2(out))
+            out = self.bn2(self._conv2(out))
             z = self.conv3(out)
             fused = fused_ok(z, self.bn3.weight)
             out_link = ResidualLink() if use_links and fused else None
@@ -336,7 +343,7 @@ class Bottleneck(nn.Module):
             tlink = dlink if dlink is not None else \
                 (getattr(x, "_cml_pool_link", None) if use_links else None)
             out = self.bn1(self.conv1(x, res_link=dlink))
-            out = self.bn2(self.conv2(out))
+            out = self.bn2(self._conv2(out))
             z = self.conv3(out)
             zd = self.down_conv(link_tap(x, tlink) if tlink is not None else x)
             out_link = ResidualLink() if use_links and fused_ok(z, self.bn3.weight) else None

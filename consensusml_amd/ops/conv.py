@@ -217,6 +217,48 @@ def bnrelu_conv1x1_bn_res(z: torch.Tensor, bn_a, stats_a, conv, bn_b, res: torch
                                        out_link)
 
 
+class _Conv3x3Fn(torch.autograd.Function):
+    """3x3 / stride 1 / padding 1 conv: forward and weight gradient on MIOpen, data gradient on
+    ``conv_gemm.hip`` (the forward implicit GEMM of dy with the rotated, transposed weights; 15-27 %
+    faster than MIOpen's backward-data at the ResNet-50 shapes, profiles/r02_conv_gemm24/)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return F.conv2d(x, w, padding=1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            Co, Ci = w.shape[0], w.shape[1]
+            # w_rot[ci][ky][kx][co] = w[co][ci][2 - ky][2 - kx], flattened k = tap Co + co
+            wr = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co).contiguous()
+            dx = lib().conv_gemm(dy, wr, 9)
+        if ctx.needs_input_grad[1]:
+            _, dw, _ = torch.ops.aten.convolution_backward(
+                dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
+        return dx, dw
+
+
+def conv3x3_ok(x: torch.Tensor, conv) -> bool:
+    """Stride-1 padding-1 3x3 convs on NHWC bf16 GPU tensors with 64-multiple channels."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
+            and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+            and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
+
+
+def conv3x3(x: torch.Tensor, conv) -> torch.Tensor:
+    """``conv(x)`` with the data gradient on the HIP implicit GEMM where eligible."""
+    if conv3x3_ok(x, conv) and torch.is_grad_enabled():
+        return _Conv3x3Fn.apply(x, conv.weight)
+    return conv(x)
+
+
 def conv1x1_bn_stats(x: torch.Tensor, conv, bn, stride: int = 1, dgrad_gemm: bool = False,
                      own_wgrad: bool = False, link=None):
     """(z, mean, invstd): 1x1 conv output and its training BN statistics (bn's running stats are

@@ -737,6 +737,27 @@ std::vector<Tensor> conv3x3_bn_fwd(const Tensor& x, const Tensor& w_in, const op
   return {y, mean, invstd};
 }
 
+// Implicit-GEMM conv (conv_gemm.hip): x [N, C, H, W] NHWC bf16, w [Cout, taps * C] contiguous
+// bf16 (k = tap C + c), taps 1 or 9 (3x3, padding 1) -> y [N, Cout, H, W] NHWC.
+Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4, "conv_gemm: 4-D NHWC input");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(taps == 1 || taps == 9, "conv_gemm: taps 1 or 9");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 &&
+                  w.size(1) == taps * C && w.size(0) % 64 == 0 && C % 64 == 0,
+              "conv_gemm: w must be contiguous bf16 [Cout, taps * C], channels multiples of 64");
+  const int64_t Co = w.size(0);
+  const c10::DeviceGuard guard(x.device());
+  Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor zero = at::zeros({64}, x.options());
+  CML_CHECK_HIP(cml::launch_conv_gemm(x.data_ptr(), w.data_ptr(), y.data_ptr(), zero.data_ptr(),
+                                      static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
+                                      static_cast<int>(C), static_cast<int>(Co),
+                                      static_cast<int>(taps), cur_stream()));
+  return y;
+}
+
 // BatchNorm training statistics only: x NHWC bf16 -> {mean, invstd} (fp32 [C]); running stats
 // updated in place when given.
 std::vector<Tensor> bn_stats(const Tensor& x, const optional<Tensor>& rmean,
@@ -1221,6 +1242,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dz_z") = py::none(), py::arg("dz_mask") = py::none(), py::arg("dz_a") = py::none(),
         py::arg("dz_b") = py::none(), py::arg("dz_c") = py::none(),
         "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
+  m.def("conv_gemm", &conv_gemm, "implicit-GEMM NHWC conv (1x1 / 3x3 stride 1), glds staging");
   m.def("conv3x3_bn_fwd", &conv3x3_bn_fwd, "3x3/s1/p1 conv (implicit GEMM) + BN statistics");
   m.def("conv1x1_bnbwd", &conv1x1_bnbwd, "1x1 data gradient through a BN + ReLU backward prologue");
   m.def("conv1x1_link", &conv1x1_link, py::arg("x"), py::arg("w"), py::arg("link"),

@@ -1,0 +1,266 @@
+// Implicit-GEMM NHWC convolution, stride 1, 1x1 or 3x3 (padding 1), on MFMA with both operands
+// staged by global_load_lds into two LDS buffers:
+//
+//   y[m][n] = sum_{tap, c} x[src(m, tap)][c] * w[n][tap * C + c]
+//
+// (a 3x3 data gradient is this with dy as x and the rotated, transposed weights). Design
+// (gfx950): a workgroup of BM BN / 4096 waves owns a BM (pixels) x BN (channels) tile, every wave a 64 x 64
+// block = 2 x 2 v_mfma_f32_32x32x16_bf16 accumulators; one k-step = 64 input channels of one
+// tap. The k-step ks + 1 is copied global -> LDS by the DMA path (global_load_lds_dwordx4: 8 rows
+// x 128 B per wave instruction, no VGPR staging) while step ks is multiplied, and retired by one
+// vmcnt(0) + barrier per step. Rows are gathered per lane (the global source address is per
+// lane): padded taps and rows past M read a zero row. The LDS image is lane-linear, so the bank
+// swizzle lives in the SOURCE address: lane p of a row loads chunk p ^ ((row >> 1) & 7), and the
+// fragment reads use the same involution (conv1x1.hip's swz). The fp32 accumulators go out through
+// a per-wave LDS image as whole-line 16-B stores. Tiles are mapped XCD-aware (the n-tiles of one
+// m-tile are consecutive on one XCD: x comes from HBM once and from that XCD's L2 after).
+#include <cstdlib>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace cml {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void g_void;
+
+constexpr int kBK = 64;
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int swz(int row, int c) { return row * 128 + 16 * (c ^ ((row >> 1) & 7)); }
+
+struct GArgs {
+  const uint16_t* x;      // [rows][C]
+  const uint16_t* w;      // [N][TAPS * C]
+  uint16_t* y;            // [M][N]
+  const uint16_t* zero;   // >= 64 zero elements
+  int M, C, N, H, W, HW;
+  int KS;                 // TAPS * C / 64
+  int ntn, tiles;
+};
+
+// NBUF = 2: the DMA of step ks + 1 overlaps step ks, retired by vmcnt(0) + barrier per step.
+// NBUF = 3: steps ks + 1 and ks + 2 in flight; a counted vmcnt (this wave's instructions of one
+// step) + a raw s_barrier retires only step ks + 1 (a __syncthreads() would drain the queue).
+template <int BM, int BN, int TAPS, int NBUF = 2>
+__global__ __launch_bounds__(BM * BN / 64, 1) void conv_gemm_kernel(GArgs a) {
+  constexpr int WN = BN / 64, WM = BM / 64, NW = WN * WM;
+  constexpr int QA = BM / (8 * NW), QB = BN / (8 * NW);   // glds instructions per wave per step
+  static_assert(QA * 8 * NW == BM && QB * 8 * NW == BN, "rows split evenly over the waves");
+  constexpr int SB = (BM + BN) * 128;           // one LDS buffer: x tile then w tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave / WM, wm = wave % WM;
+  const int h = lane >> 5, r32 = lane & 31;
+  // bijective XCD remap: consecutive tile ids share an XCD
+  const int G = a.tiles, b = blockIdx.x, xcd = b & 7, q8 = G >> 3, r8 = G & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int mt = t / a.ntn, nt = t - mt * a.ntn;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  // this lane's staged rows: x rows wave * (BM / NW) + 8 i + lane / 8, w rows likewise
+  const int p = lane & 7, lrow = lane >> 3;
+  int pimg[QA], poh[QA], pow_[QA];
+#pragma unroll
+  for (int i = 0; i < QA; ++i) {
+    const int m = m0 + wave * (BM / NW) + 8 * i + lrow;
+    if (m < a.M) {
+      const int img = m / a.HW, rem = m - img * a.HW;
+      pimg[i] = img * a.HW;
+      poh[i] = rem / a.W;
+      pow_[i] = rem - poh[i] * a.W;
+    } else {
+      pimg[i] = -1;
+      poh[i] = 0;
+      pow_[i] = 0;
+    }
+  }
+
+  auto issue = [&](int ks, int buf) {
+    const int CS = a.C >> 6;
+    const int tap = TAPS == 1 ? 0 : ks / CS;
+    const int cc = ks - tap * CS;
+    const int dy = TAPS == 1 ? 0 : tap / 3 - 1, dx = TAPS == 1 ? 0 : tap - 3 * (tap / 3) - 1;
+    char* base = smem + buf * SB;
+#pragma unroll
+    for (int i = 0; i < QA; ++i) {
+      const int row = wave * (BM / NW) + 8 * i + lrow;
+      const int ih = poh[i] + dy, iw = pow_[i] + dx;
+      const bool ok = pimg[i] >= 0 && static_cast<unsigned>(ih) < static_cast<unsigned>(a.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(a.W);
+      const int c = p ^ ((row >> 1) & 7);
+      const uint16_t* src = ok ? a.x + (static_cast<int64_t>(pimg[i]) + ih * a.W + iw) * a.C +
+                                     cc * kBK + 8 * c
+                               : a.zero;
+      __builtin_amdgcn_global_load_lds((g_void*)src,
+                                       (lds_void*)(base + (wave * (BM / NW) + 8 * i) * 128), 16, 0,
+                                       0);
+    }
+    char* wb = base + BM * 128;
+#pragma unroll
+    for (int i = 0; i < QB; ++i) {
+      const int row = wave * (BN / NW) + 8 * i + lrow;
+      const int c = p ^ ((row >> 1) & 7);
+      const uint16_t* src = a.w + static_cast<int64_t>(n0 + row) * (a.KS * kBK) + ks * kBK + 8 * c;
+      __builtin_amdgcn_global_load_lds((g_void*)src,
+                                       (lds_void*)(wb + (wave * (BN / NW) + 8 * i) * 128), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      acc[i][0][k] = 0.f;
+      acc[i][1][k] = 0.f;
+    }
+
+  issue(0, 0);
+  if constexpr (NBUF == 3) {
+    if (a.KS > 1) {
+      issue(1, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QA + QB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int ks = 0; ks < a.KS; ++ks) {
+    const int buf = NBUF == 3 ? ks % 3 : (ks & 1);
+    if constexpr (NBUF == 3) {
+      if (ks + 2 < a.KS) issue(ks + 2, (ks + 2) % 3);
+    } else {
+      if (ks + 1 < a.KS) issue(ks + 1, buf ^ 1);
+    }
+    const char* sx = smem + buf * SB;
+    const char* sw = sx + BM * 128;
+#pragma unroll
+    for (int kk = 0; kk < kBK / 16; ++kk) {
+      bf16x8_t A[2], B[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        A[i] = *reinterpret_cast<const bf16x8_t*>(sw + swz(wn * 64 + 32 * i + r32, 2 * kk + h));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        B[j] = *reinterpret_cast<const bf16x8_t*>(sx + swz(wm * 64 + 32 * j + r32, 2 * kk + h));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(A[i], B[j], acc[i][j]);
+    }
+    if constexpr (NBUF == 3) {
+      // retire step ks + 1 (this wave's loads of step ks + 2 may stay in flight); the barrier also
+      // ends every wave's reads of buffer ks % 3 before step ks + 1 re-issues into it
+      if (ks + 2 < a.KS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(QA + QB) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+
+  // epilogue: the wave's 64 (n) x 64 (m) block via its own 8 KB LDS image (buffers are free now)
+  char* simg = smem + wave * 8192;
+#pragma unroll
+  for (int jm = 0; jm < 2; ++jm) {
+    const int pr = 32 * jm + r32;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t b0 = f2bf(acc[i][jm][4 * g + 0]), b1 = f2bf(acc[i][jm][4 * g + 1]);
+        const uint32_t b2 = f2bf(acc[i][jm][4 * g + 2]), b3 = f2bf(acc[i][jm][4 * g + 3]);
+        *reinterpret_cast<uint2*>(simg + swz(pr, 4 * i + g) + 8 * h) =
+            make_uint2(b0 | (b1 << 16), b2 | (b3 << 16));
+      }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const int c = lane & 7;
+  const int mb = m0 + wm * 64;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int pr = 8 * k + (lane >> 3);
+    const uint4 v = *reinterpret_cast<const uint4*>(simg + swz(pr, c));
+    if (mb + pr < a.M)
+      *reinterpret_cast<uint4*>(a.y + static_cast<int64_t>(mb + pr) * a.N + n0 + wn * 64 + 8 * c) = v;
+  }
+}
+
+template <int BM, int BN, int TAPS, int NBUF>
+hipError_t launch_g(const GArgs& a, hipStream_t st) {
+  auto k = &conv_gemm_kernel<BM, BN, TAPS, NBUF>;
+  const size_t lds = NBUF * static_cast<size_t>(BM + BN) * 128;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  k<<<a.tiles, BM * BN / 64, lds, st>>>(a);
+  return hipGetLastError();
+}
+
+// CML_CONV_GEMM_VARIANT (A/B): 0 = 128 x 128, 2 buffers; 1 = 128 x 128, 3 buffers;
+// 2 = 256 x 128 (8 waves), 2 buffers (default); 3 = 256 x 128, 3 buffers. N % 128 != 0: 256 x 64.
+// Measured on the ResNet-50 3x3 shapes at batch 2048 (bench/conv3x3.py, profiles/r02_conv_gemm24/):
+// variant 2 is the fastest or within 3 % everywhere; the third buffer does not pay here.
+int gemm_variant() {
+  static const int v = [] {
+    const char* e = getenv("CML_CONV_GEMM_VARIANT");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
+template <int TAPS>
+hipError_t launch_v(GArgs& a, int64_t M, hipStream_t st) {
+  const bool wide = a.N % 128 == 0;
+  const int v = wide ? gemm_variant() : 0;
+  const int BM = !wide ? 256 : (v >= 2 ? 256 : 128), BN = wide ? 128 : 64;
+  a.ntn = a.N / BN;
+  const int64_t tiles = (M + BM - 1) / BM * a.ntn;
+  if (tiles >= (1ll << 31)) return hipErrorInvalidValue;
+  a.tiles = static_cast<int>(tiles);
+  if (!wide) return launch_g<256, 64, TAPS, 2>(a, st);
+  switch (v) {
+    case 1: return launch_g<128, 128, TAPS, 3>(a, st);
+    case 2: return launch_g<256, 128, TAPS, 2>(a, st);
+    case 3: return launch_g<256, 128, TAPS, 3>(a, st);
+    default: return launch_g<128, 128, TAPS, 2>(a, st);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* zero, int Nimg,
+                            int H, int W, int C, int N, int taps, hipStream_t st) {
+  const int64_t M = static_cast<int64_t>(Nimg) * H * W;
+  if (C % kBK || N % 64 || (taps != 1 && taps != 9) || M < 1 || M >= (1ll << 31) ||
+      static_cast<int64_t>(taps) * C > 65536)
+    return hipErrorInvalidValue;
+  GArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(x);
+  a.w = reinterpret_cast<const uint16_t*>(w);
+  a.y = reinterpret_cast<uint16_t*>(y);
+  a.zero = reinterpret_cast<const uint16_t*>(zero);
+  a.M = static_cast<int>(M);
+  a.C = C;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.HW = H * W;
+  a.KS = taps * C / kBK;
+  return taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
+}
+
+}  // namespace cml

@@ -271,6 +271,12 @@ hipError_t launch_conv3x3_bn_fwd(const void* x, const void* w, void* y, float* p
                                  float* rmean, float* rvar, float eps, float momentum,
                                  hipStream_t st);
 
+// Implicit-GEMM NHWC conv, stride 1, 1x1 (taps 1) or 3x3 padding 1 (taps 9), global_load_lds
+// double-buffered (conv_gemm.hip): x [Nimg][H][W][C], w [N][taps][C], y [Nimg][H][W][N]; zero:
+// >= 64 zero bf16 (padding rows).
+hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* zero, int Nimg,
+                            int H, int W, int C, int N, int taps, hipStream_t st);
+
 // Backward variants of the fused 1x1 conv (conv1x1.hip), stride 1, W given as [N][K] (for a data
 // gradient: the forward weight transposed).
 //   bnbwd: y = f(g) W^T with f = ca (mask ? g : 0) + cb z + cc per input channel (a BN + ReLU

@@ -217,3 +217,37 @@ def test_conv3x3_tap_vs_fp32(cuda, N, C, Co, H, pro):
     torch.testing.assert_close(mean, yb.mean((0, 2, 3)), rtol=1e-3, atol=1e-3)
     var = yb.var((0, 2, 3), unbiased=False)
     torch.testing.assert_close(invstd, torch.rsqrt(var + 1e-5), rtol=2e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("C,Co,H", [(64, 64, 9), (128, 128, 7), (256, 256, 5), (512, 512, 4),
+                                    (64, 128, 6), (128, 64, 5)])
+def test_conv_gemm_and_3x3_dgrad(cuda, C, Co, H):
+    """conv_gemm.hip: forward 3x3 / 1x1 implicit GEMM vs fp32, and the 3x3 data gradient of
+    ops.conv.conv3x3 vs the fp32 autograd gradient."""
+    import torch.nn.functional as F
+    from consensusml_amd.ops import conv as fconv
+    from consensusml_amd.ops.native import lib
+    g0 = torch.Generator(device=cuda).manual_seed(9)
+    N = 3
+    x = torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, 3, 3, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
+    y = lib().conv_gemm(x, w.permute(0, 2, 3, 1).reshape(Co, 9 * C).contiguous(), 9)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    assert float((y.float() - ref).norm() / ref.norm()) < 5e-3
+    y1 = lib().conv_gemm(x, w[:, :, 1, 1].contiguous(), 1)
+    ref1 = F.conv2d(x.float(), w[:, :, 1:2, 1:2].float())
+    assert float((y1.float() - ref1).norm() / ref1.norm()) < 5e-3
+    conv = torch.nn.Conv2d(C, Co, 3, padding=1, bias=False).to(cuda, torch.bfloat16)
+    with torch.no_grad():
+        conv.weight.copy_(w)
+    xi = x.clone().requires_grad_(True)
+    out = fconv.conv3x3(xi, conv)
+    gy = torch.randn(out.shape, device=cuda, generator=g0).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    out.backward(gy)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    F.conv2d(xr, wr, padding=1).backward(gy.float())
+    assert float((xi.grad.float() - xr.grad).norm() / xr.grad.norm()) < 5e-3
+    assert float((conv.weight.grad.float() - wr.grad).norm() / wr.grad.norm()) < 1e-2
