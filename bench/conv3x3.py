@@ -68,6 +68,14 @@ def main():
         yg = L.conv_gemm(x[:4].contiguous(memory_format=torch.channels_last), w2, 9)
         g_ref = F.conv2d(x[:4].float(), w.float(), padding=1)
         g_err = float((yg.float() - g_ref).norm() / g_ref.norm())
+        t_owg = _t(lambda: L.wgrad3x3(gy, x, torch.float32))
+        t_owg_pro = _t(lambda: L.wgrad3x3(gy, x, torch.float32, sc, bi))
+        wref = torch.ops.aten.convolution_backward(gy[:8].float(), x[:8].float(), w.float(), None,
+                                                   [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                   [False, True, False])[1]
+        wo = L.wgrad3x3(gy[:8].contiguous(memory_format=torch.channels_last),
+                        x[:8].contiguous(memory_format=torch.channels_last), torch.float32)
+        wg_err = float((wo.float() - wref).norm() / wref.norm())
         dgg = L.conv_gemm(gy[:4].contiguous(memory_format=torch.channels_last), wr2, 9)
         gdg_err = float((dgg.float() - dref).norm() / dref.norm())
         t_own = _t(lambda: L.conv3x3_bn_fwd(x, w, None, None, None, None, None, False, 1e-5, 0.1))
@@ -86,7 +94,9 @@ def main():
                           "miopen_wgrad_ms": round(t_wg, 4), "dgrad_rel_err": dg_err,
                           "glds_fwd_ms": round(t_g, 4), "glds_dgrad_ms": round(t_gdg, 4),
                           "glds_tflops": round(flops / t_g / 1e9, 1),
-                          "glds_fwd_err": g_err, "glds_dgrad_err": gdg_err}), flush=True)
+                          "glds_fwd_err": g_err, "glds_dgrad_err": gdg_err,
+                          "own_wgrad_ms": round(t_owg, 4), "own_wgrad_pro_ms": round(t_owg_pro, 4),
+                          "own_wgrad_err": wg_err}), flush=True)
         del x, w
         torch.cuda.empty_cache()
 

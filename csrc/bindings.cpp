@@ -737,6 +737,35 @@ std::vector<Tensor> conv3x3_bn_fwd(const Tensor& x, const Tensor& w_in, const op
   return {y, mean, invstd};
 }
 
+// Weight gradient of a 3x3 / stride 1 / padding 1 conv (wgrad1x1.hip TAP): dy [N, Co, H, W],
+// x [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 3, 3] in `dtype` (channels_last memory); pro_sc / pro_bi
+// (fp32 [Ci]): x replaced by max(x sc + bi, 0) (zero padding after the transform).
+Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
+                const optional<Tensor>& pro_sc, const optional<Tensor>& pro_bi) {
+  check_nhwc(x, "x");
+  Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(0) == x.size(0) && dy.size(2) == x.size(2) &&
+                  dy.size(3) == x.size(3), "wgrad3x3: dy / x shapes");
+  TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "wgrad3x3: bf16 or fp32 output");
+  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1);
+  TORCH_CHECK(Ci == 64 ? (Co == 64 || Co % 256 == 0) : (Co % 128 == 0 && Ci % 128 == 0),
+              "wgrad3x3: unsupported channel counts");
+  const float* sc = opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", Ci);
+  const float* bi = opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", Ci);
+  TORCH_CHECK((sc == nullptr) == (bi == nullptr), "wgrad3x3: pro_sc and pro_bi together");
+  const c10::DeviceGuard guard(x.device());
+  int TM, TN, S = 1, cps = 1;
+  cml::wgrad3x3_plan(N * H * W, static_cast<int>(Co), static_cast<int>(Ci), &TM, &TN, &S, &cps);
+  Tensor part = at::empty({S, 9, Co, Ci}, x.options().dtype(at::kFloat));
+  Tensor dw = at::empty({3, 3, Co, Ci}, x.options().dtype(dtype));
+  CML_CHECK_HIP(cml::launch_wgrad3x3(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(),
+                                     dw.data_ptr(), dtype == at::kBFloat16, static_cast<int>(N),
+                                     static_cast<int>(H), static_cast<int>(W), static_cast<int>(Co),
+                                     static_cast<int>(Ci), sc, bi, cur_stream()));
+  return dw.permute({2, 3, 0, 1});   // [Co, Ci, 3, 3] view of the tap-major result
+}
+
 // Implicit-GEMM conv (conv_gemm.hip): x [N, C, H, W] NHWC bf16, w [Cout, taps * C] contiguous
 // bf16 (k = tap C + c), taps 1 or 9 (3x3, padding 1) -> y [N, Cout, H, W] NHWC.
 Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps) {
@@ -1242,6 +1271,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dz_z") = py::none(), py::arg("dz_mask") = py::none(), py::arg("dz_a") = py::none(),
         py::arg("dz_b") = py::none(), py::arg("dz_c") = py::none(),
         "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
+  m.def("wgrad3x3", &wgrad3x3, py::arg("dy"), py::arg("x"), py::arg("dtype"),
+        py::arg("pro_sc") = py::none(), py::arg("pro_bi") = py::none(),
+        "weight gradient of a 3x3 stride-1 conv (MFMA, split-K, one tap per grid z)");
   m.def("conv_gemm", &conv_gemm, "implicit-GEMM NHWC conv (1x1 / 3x3 stride 1), glds staging");
   m.def("conv3x3_bn_fwd", &conv3x3_bn_fwd, "3x3/s1/p1 conv (implicit GEMM) + BN statistics");
   m.def("conv1x1_bnbwd", &conv1x1_bnbwd, "1x1 data gradient through a BN + ReLU backward prologue");

@@ -249,6 +249,14 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
                            const uint8_t* dz_mask = nullptr, const float* dz_a = nullptr,
                            const float* dz_b = nullptr, const float* dz_c = nullptr);
 
+// 3x3 / stride 1 / padding 1 weight gradient on the same kernel (one tap per grid z): dy [P][Co],
+// x [P][Ci] NHWC with P = Nimg H W -> dw [9][Co][Ci] (tap = 3 (dy + 1) + dx + 1), optional BN +
+// ReLU prologue on x. Co % 128 == 0 and Ci % 128 == 0, or Ci == 64 with Co == 64 or Co % 256 == 0.
+void wgrad3x3_plan(int64_t P, int Co, int Ci, int* TM, int* TN, int* splits, int* cps);
+hipError_t launch_wgrad3x3(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
+                           int Nimg, int H, int W, int Co, int Ci, const float* pro_sc,
+                           const float* pro_bi, hipStream_t st);
+
 // Fused 1x1 convolution forward (conv1x1.hip): y[M][N] = f(x)[src(m)][K] W[N][K]^T on NHWC bf16,
 // f = identity or max(x * pro_sc + pro_bi, 0) per input channel (pro_sc != null), src(m) = m
 // (stride 1) or the stride-2 pixel of an [*, H, W] input. With part / mean non-null also the

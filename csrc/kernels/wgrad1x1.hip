@@ -65,11 +65,20 @@ struct DPro {
   const float* c;
 };
 
-template <int TM, int TN, int KC, bool PRO, bool DPRO>
+// TAP: weight gradient of a 3x3 / stride 1 / padding 1 conv, one tap per blockIdx.z: x rows are
+// gathered at the tap's shifted pixel (zero in the padding, after the prologue) and the partials
+// go to part[split][tap][Co][Ci].
+struct TapGeo {
+  int H, W, HW;
+};
+
+template <int TM, int TN, int KC, bool PRO, bool DPRO, bool TAP = false>
 __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, float* __restrict__ part,
     int P, int Co, int Ci, int tiles_n, int cps, const float* __restrict__ pro_sc,
-    const float* __restrict__ pro_bi, DPro dp) {
+    const float* __restrict__ pro_bi, DPro dp, TapGeo tg) {
+  const int tap = TAP ? static_cast<int>(blockIdx.z) : 0;
+  const int tdy = TAP ? tap / 3 - 1 : 0, tdx = TAP ? tap - 3 * (tap / 3) - 1 : 0;
   constexpr int kKC = KC;                              // pixels per chunk
   constexpr int NT = (TM / 64) * (TN / 64) * 64;
   constexpr int CA = TM / 8, CB = TN / 8;            // 16-B chunks per staged row
@@ -142,6 +151,7 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
   // whole uint4 values became a select of addresses that put these registers in scratch
   uint4 av[IA], bv[IB], zv[DPRO ? IA : 1];
   uint32_t mv[DPRO ? IA : 1];
+  uint32_t xok = ~0u;                                  // TAP: bit j = x item j inside the image
   auto fetch = [&](int c) {
 #pragma unroll
     for (int j = 0; j < IA; ++j) {
@@ -153,10 +163,20 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
         mv[j] = dp.mask[static_cast<int64_t>(p) * (Co / 8) + co0 / 8 + ch];
       }
     }
+    if constexpr (TAP) xok = 0;
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
       const int e = tid + NT * j, row = e / CB, ch = e % CB;
-      const int p = min(c * kKC + row, P - 1);
+      int p = min(c * kKC + row, P - 1);
+      if constexpr (TAP) {
+        const int img = p / tg.HW, rem = p - img * tg.HW;
+        const int oh = rem / tg.W, ow = rem - oh * tg.W;
+        const int ih = oh + tdy, iw = ow + tdx;
+        const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(tg.H) &&
+                        static_cast<unsigned>(iw) < static_cast<unsigned>(tg.W);
+        xok |= (ok ? 1u : 0u) << j;
+        if (ok) p = img * tg.HW + ih * tg.W + iw;
+      }
       bv[j] = *reinterpret_cast<const uint4*>(x + static_cast<int64_t>(p) * Ci + ci0 + 8 * ch);
     }
   };
@@ -177,7 +197,8 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
       const int e = tid + NT * j, row = e / CB, ch = e % CB;
-      *reinterpret_cast<uint4*>(bb + img_off<TN * 2>(row, ch)) = keep_if(c * kKC + row < P, pro(bv[j]));
+      *reinterpret_cast<uint4*>(bb + img_off<TN * 2>(row, ch)) =
+          keep_if(c * kKC + row < P && ((xok >> j) & 1u), pro(bv[j]));
     }
   };
   if (c_lo < c_hi) {
@@ -215,7 +236,7 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     __syncthreads();
   }
   // partial [split][Co][Ci]: lane r = ci column, register k = co row (k&3) + 8 (k>>2) + 4 h
-  float* pw = part + static_cast<int64_t>(blockIdx.y) * Co * Ci;
+  float* pw = part + (static_cast<int64_t>(blockIdx.y) * (TAP ? 9 : 1) + tap) * Co * Ci;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -287,16 +308,16 @@ void pick_tile(int Co, int Ci, int* TM, int* TN) {
 }
 }  // namespace
 
-template <int TM, int TN, bool PRO, bool DPRO>
+template <int TM, int TN, bool PRO, bool DPRO, bool TAP = false>
 void launch_one(dim3 grid, size_t lds, hipStream_t st, const uint16_t* dyp, const uint16_t* xp,
                 float* part, int P, int Co, int Ci, int tiles_n, int cps, const float* sc,
-                const float* bi, const DPro& dp) {
-  auto k = &wgrad1x1_kernel<TM, TN, 64, PRO, DPRO>;
+                const float* bi, const DPro& dp, const TapGeo& tg = TapGeo{1, 1, 1}) {
+  auto k = &wgrad1x1_kernel<TM, TN, 64, PRO, DPRO, TAP>;
   if (lds > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
   k<<<grid, (TM / 64) * (TN / 64) * 64, lds, st>>>(dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi,
-                                                    dp);
+                                                    dp, tg);
 }
 
 template <bool PRO, bool DPRO>
@@ -312,6 +333,20 @@ bool launch_tile(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, const ui
   else if (TM == 128 && TN == 256) launch_one<128, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
   else if (TM == 128 && TN == 128) launch_one<128, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
   else if (TM == 256 && TN == 64) launch_one<256, 64, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
+  else return false;
+  return true;
+}
+
+template <bool PRO>
+bool launch_tile_tap(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, const uint16_t* dyp,
+                     const uint16_t* xp, float* part, int P, int Co, int Ci, int tiles_n, int cps,
+                     const float* sc, const float* bi, const TapGeo& tg) {
+  const DPro dp{};
+  if (TM == 256 && TN == 128) launch_one<256, 128, PRO, false, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
+  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO, false, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
+  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO, false, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
+  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO, false, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
+  else if (TM == 64 && TN == 64) launch_one<64, 64, PRO, false, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
   else return false;
   return true;
 }
@@ -366,6 +401,49 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
     ok = launch_tile<false, false>(TM, TN, grid, lds, st, dyp, xp, part, Pi, Co, Ci, tiles_n, cps, nullptr, nullptr, dp);
   if (!ok) return hipErrorInvalidValue;
   const int64_t n = static_cast<int64_t>(Co) * Ci;
+  const int fb = static_cast<int>((n / 4 + 255) / 256);
+  if (dw_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, dw);
+  else wgrad1x1_fold_kernel<false><<<fb, 256, 0, st>>>(part, S, n, dw);
+  return hipGetLastError();
+}
+
+// 3x3 / stride 1 / padding 1 weight gradient: dy [P][Co], x [P][Ci] (same H x W), dw [9][Co][Ci]
+// (tap-major). Tiles as the 1x1 kernel with Co x Ci; 128 x 128 tiles when Co and Ci allow (the 9
+// taps already multiply the workgroup count).
+void wgrad3x3_plan(int64_t P, int Co, int Ci, int* TM, int* TN, int* splits, int* cps) {
+  *TM = Co % 256 == 0 && Ci <= 128 ? 256 : 128;
+  *TN = Ci == 64 ? 64 : 128;
+  if (*TN == 64) *TM = Co % 256 == 0 ? 256 : 64;   // 64 x 64: one wave (ResNet layer 1, 64 -> 64)
+  const int tiles = (Co / *TM) * (Ci / *TN) * 9;
+  const int waves = (*TM / 64) * (*TN / 64);
+  const int nchunk = static_cast<int>((P + 63) / 64);
+  const int target = 256 * 8 / waves;
+  int s = (target + tiles - 1) / tiles;
+  s = s < 1 ? 1 : (s > nchunk ? nchunk : s);
+  const int c = (nchunk + s - 1) / s;
+  *cps = c;
+  *splits = (nchunk + c - 1) / c;
+}
+
+hipError_t launch_wgrad3x3(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
+                           int Nimg, int H, int W, int Co, int Ci, const float* pro_sc,
+                           const float* pro_bi, hipStream_t st) {
+  const int64_t P = static_cast<int64_t>(Nimg) * H * W;
+  if (Ci == 64 ? (Co != 64 && Co % 256) : (Co % 128 || Ci % 128)) return hipErrorInvalidValue;
+  if (P < 1 || P >= (1ll << 31)) return hipErrorInvalidValue;
+  if ((pro_sc == nullptr) != (pro_bi == nullptr)) return hipErrorInvalidValue;
+  int TM, TN, S, cps;
+  wgrad3x3_plan(P, Co, Ci, &TM, &TN, &S, &cps);
+  const int tiles_n = Ci / TN;
+  const dim3 grid((Co / TM) * tiles_n, S, 9);
+  const size_t lds = 2 * static_cast<size_t>(64) * (TM + TN) * 2;
+  const TapGeo tg{H, W, H * W};
+  const auto* dyp = reinterpret_cast<const uint16_t*>(dy);
+  const auto* xp = reinterpret_cast<const uint16_t*>(x);
+  const bool ok = pro_sc ? launch_tile_tap<true>(TM, TN, grid, lds, st, dyp, xp, part, static_cast<int>(P), Co, Ci, tiles_n, cps, pro_sc, pro_bi, tg)
+                         : launch_tile_tap<false>(TM, TN, grid, lds, st, dyp, xp, part, static_cast<int>(P), Co, Ci, tiles_n, cps, nullptr, nullptr, tg);
+  if (!ok) return hipErrorInvalidValue;
+  const int64_t n = 9ll * Co * Ci;
   const int fb = static_cast<int>((n / 4 + 255) / 256);
   if (dw_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, dw);
   else wgrad1x1_fold_kernel<false><<<fb, 256, 0, st>>>(part, S, n, dw);

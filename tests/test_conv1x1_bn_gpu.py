@@ -251,3 +251,27 @@ def test_conv_gemm_and_3x3_dgrad(cuda, C, Co, H):
     F.conv2d(xr, wr, padding=1).backward(gy.float())
     assert float((xi.grad.float() - xr.grad).norm() / xr.grad.norm()) < 5e-3
     assert float((conv.weight.grad.float() - wr.grad).norm() / wr.grad.norm()) < 1e-2
+
+
+@pytest.mark.parametrize("C,Co,H", [(64, 64, 9), (128, 128, 6), (256, 256, 5), (64, 256, 5)])
+@pytest.mark.parametrize("pro", [False, True])
+def test_wgrad3x3_tap_vs_fp32(cuda, C, Co, H, pro):
+    """3x3 weight gradient (wgrad1x1.hip TAP mode) vs the fp32 convolution weight gradient, with
+    the optional BN + ReLU prologue on x (padding stays zero after the transform)."""
+    from consensusml_amd.ops.native import lib
+    g0 = torch.Generator(device=cuda).manual_seed(11)
+    N = 4
+    x = torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    gy = torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    sc = torch.rand(C, device=cuda, generator=g0) + 0.5 if pro else None
+    bi = torch.randn(C, device=cuda, generator=g0) * 0.2 if pro else None
+    dw = lib().wgrad3x3(gy, x, torch.float32, sc, bi)
+    xf = x.float()
+    if pro:
+        xf = torch.relu(xf * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)).bfloat16().float()
+    w = torch.zeros(Co, C, 3, 3, device=cuda)
+    ref = torch.ops.aten.convolution_backward(gy.float(), xf, w, None, [1, 1], [1, 1], [1, 1],
+                                              False, [0, 0], 1, [False, True, False])[1]
+    assert float((dw.float() - ref).norm() / ref.norm()) < 5e-3
