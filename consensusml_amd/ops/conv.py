@@ -217,6 +217,17 @@ def bnrelu_conv1x1_bn_res(z: torch.Tensor, bn_a, stats_a, conv, bn_b, res: torch
                                        out_link)
 
 
+_ZERO_ROWS = {}
+
+
+def _zero_row(device: torch.device) -> torch.Tensor:
+    """A cached row of zeros (padding source of conv_gemm's gathered loads)."""
+    z = _ZERO_ROWS.get(device)
+    if z is None:
+        z = _ZERO_ROWS[device] = torch.zeros(64, dtype=torch.bfloat16, device=device)
+    return z
+
+
 class _Conv3x3Fn(torch.autograd.Function):
     """3x3 / stride 1 / padding 1 conv: forward and weight gradient on MIOpen, data gradient on
     ``conv_gemm.hip`` (the forward implicit GEMM of dy with the rotated, transposed weights; 15-27 %
@@ -236,7 +247,7 @@ class _Conv3x3Fn(torch.autograd.Function):
             Co, Ci = w.shape[0], w.shape[1]
             # w_rot[ci][ky][kx][co] = w[co][ci][2 - ky][2 - kx], flattened k = tap Co + co
             wr = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co).contiguous()
-            dx = lib().conv_gemm(dy, wr, 9)
+            dx = lib().conv_gemm(dy, wr, 9, _zero_row(dy.device))
         if ctx.needs_input_grad[1]:
             _, dw, _ = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])

@@ -768,7 +768,7 @@ Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
 
 // Implicit-GEMM conv (conv_gemm.hip): x [N, C, H, W] NHWC bf16, w [Cout, taps * C] contiguous
 // bf16 (k = tap C + c), taps 1 or 9 (3x3, padding 1) -> y [N, Cout, H, W] NHWC.
-Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps) {
+Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps, const optional<Tensor>& zero_in) {
   check_nhwc(x, "x");
   TORCH_CHECK(x.dim() == 4, "conv_gemm: 4-D NHWC input");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -779,7 +779,15 @@ Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps) {
   const int64_t Co = w.size(0);
   const c10::DeviceGuard guard(x.device());
   Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  Tensor zero = at::zeros({64}, x.options());
+  // zero row for padded taps: pass a cached >= 64-element zero bf16 tensor to skip the per-call fill
+  Tensor zero;
+  if (zero_in.has_value() && zero_in->defined()) {
+    zero = *zero_in;
+    TORCH_CHECK(zero.is_cuda() && zero.device() == x.device() && zero.scalar_type() == at::kBFloat16 &&
+                    zero.is_contiguous() && zero.numel() >= 64, "conv_gemm: zero must be >= 64 bf16");
+  } else {
+    zero = at::zeros({64}, x.options());
+  }
   CML_CHECK_HIP(cml::launch_conv_gemm(x.data_ptr(), w.data_ptr(), y.data_ptr(), zero.data_ptr(),
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
                                       static_cast<int>(C), static_cast<int>(Co),
@@ -1274,7 +1282,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad3x3", &wgrad3x3, py::arg("dy"), py::arg("x"), py::arg("dtype"),
         py::arg("pro_sc") = py::none(), py::arg("pro_bi") = py::none(),
         "weight gradient of a 3x3 stride-1 conv (MFMA, split-K, one tap per grid z)");
-  m.def("conv_gemm", &conv_gemm, "implicit-GEMM NHWC conv (1x1 / 3x3 stride 1), glds staging");
+  m.def("conv_gemm", &conv_gemm, py::arg("x"), py::arg("w"), py::arg("taps"),
+        py::arg("zero") = py::none(), "implicit-GEMM NHWC conv (1x1 / 3x3 stride 1), glds staging");
   m.def("conv3x3_bn_fwd", &conv3x3_bn_fwd, "3x3/s1/p1 conv (implicit GEMM) + BN statistics");
   m.def("conv1x1_bnbwd", &conv1x1_bnbwd, "1x1 data gradient through a BN + ReLU backward prologue");
   m.def("conv1x1_link", &conv1x1_link, py::arg("x"), py::arg("w"), py::arg("link"),
