@@ -47,9 +47,12 @@ struct GArgs {
 // NBUF = 2: the DMA of step ks + 1 overlaps step ks, retired by vmcnt(0) + barrier per step.
 // NBUF = 3: steps ks + 1 and ks + 2 in flight; a counted vmcnt (this wave's instructions of one
 // step) + a raw s_barrier retires only step ks + 1 (a __syncthreads() would drain the queue).
-template <int BM, int BN, int TAPS, int NBUF = 2>
-__global__ __launch_bounds__(BM * BN / 64, 1) void conv_gemm_kernel(GArgs a) {
-  constexpr int WN = BN / 64, WM = BM / 64, NW = WN * WM;
+// WTN: output channels per wave (64: 2 x 2 accumulators; 128: 4 x 2, half the x-fragment reads
+// per MFMA).
+template <int BM, int BN, int TAPS, int NBUF = 2, int WTN = 64>
+__global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
+  constexpr int WN = BN / WTN, WM = BM / 64, NW = WN * WM;
+  constexpr int NI = WTN / 32;                  // accumulator rows (n) per wave
   constexpr int QA = BM / (8 * NW), QB = BN / (8 * NW);   // glds instructions per wave per step
   static_assert(QA * 8 * NW == BM && QB * 8 * NW == BN, "rows split evenly over the waves");
   constexpr int SB = (BM + BN) * 128;           // one LDS buffer: x tile then w tile
@@ -114,9 +117,9 @@ __global__ __launch_bounds__(BM * BN / 64, 1) void conv_gemm_kernel(GArgs a) {
     }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[NI][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       acc[i][0][k] = 0.f;
@@ -147,15 +150,15 @@ __global__ __launch_bounds__(BM * BN / 64, 1) void conv_gemm_kernel(GArgs a) {
     const char* sw = sx + BM * 128;
 #pragma unroll
     for (int kk = 0; kk < kBK / 16; ++kk) {
-      bf16x8_t A[2], B[2];
+      bf16x8_t A[NI], B[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        A[i] = *reinterpret_cast<const bf16x8_t*>(sw + swz(wn * 64 + 32 * i + r32, 2 * kk + h));
+      for (int i = 0; i < NI; ++i)
+        A[i] = *reinterpret_cast<const bf16x8_t*>(sw + swz(wn * WTN + 32 * i + r32, 2 * kk + h));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         B[j] = *reinterpret_cast<const bf16x8_t*>(sx + swz(wm * 64 + 32 * j + r32, 2 * kk + h));
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(A[i], B[j], acc[i][j]);
     }
@@ -172,52 +175,62 @@ __global__ __launch_bounds__(BM * BN / 64, 1) void conv_gemm_kernel(GArgs a) {
     }
   }
 
-  // epilogue: the wave's 64 (n) x 64 (m) block via its own 8 KB LDS image (buffers are free now)
+  // epilogue: the wave's WTN (n) x 64 (m) block, 64 channels at a time, via its own 8 KB LDS image
+  // (the staging buffers are free now)
   char* simg = smem + wave * 8192;
-#pragma unroll
-  for (int jm = 0; jm < 2; ++jm) {
-    const int pr = 32 * jm + r32;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t b0 = f2bf(acc[i][jm][4 * g + 0]), b1 = f2bf(acc[i][jm][4 * g + 1]);
-        const uint32_t b2 = f2bf(acc[i][jm][4 * g + 2]), b3 = f2bf(acc[i][jm][4 * g + 3]);
-        *reinterpret_cast<uint2*>(simg + swz(pr, 4 * i + g) + 8 * h) =
-            make_uint2(b0 | (b1 << 16), b2 | (b3 << 16));
-      }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
   const int c = lane & 7;
   const int mb = m0 + wm * 64;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int pr = 8 * k + (lane >> 3);
-    const uint4 v = *reinterpret_cast<const uint4*>(simg + swz(pr, c));
-    if (mb + pr < a.M)
-      *reinterpret_cast<uint4*>(a.y + static_cast<int64_t>(mb + pr) * a.N + n0 + wn * 64 + 8 * c) = v;
+  for (int sb = 0; sb < WTN / 64; ++sb) {
+#pragma unroll
+    for (int jm = 0; jm < 2; ++jm) {
+      const int pr = 32 * jm + r32;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x16& v = acc[2 * sb + i][jm];
+          const uint32_t b0 = f2bf(v[4 * g + 0]), b1 = f2bf(v[4 * g + 1]);
+          const uint32_t b2 = f2bf(v[4 * g + 2]), b3 = f2bf(v[4 * g + 3]);
+          *reinterpret_cast<uint2*>(simg + swz(pr, 4 * i + g) + 8 * h) =
+              make_uint2(b0 | (b1 << 16), b2 | (b3 << 16));
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int pr = 8 * k + (lane >> 3);
+      const uint4 v = *reinterpret_cast<const uint4*>(simg + swz(pr, c));
+      if (mb + pr < a.M)
+        *reinterpret_cast<uint4*>(a.y + static_cast<int64_t>(mb + pr) * a.N + n0 + wn * WTN +
+                                  64 * sb + 8 * c) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
-template <int BM, int BN, int TAPS, int NBUF>
+template <int BM, int BN, int TAPS, int NBUF, int WTN = 64>
 hipError_t launch_g(const GArgs& a, hipStream_t st) {
-  auto k = &conv_gemm_kernel<BM, BN, TAPS, NBUF>;
+  auto k = &conv_gemm_kernel<BM, BN, TAPS, NBUF, WTN>;
   const size_t lds = NBUF * static_cast<size_t>(BM + BN) * 128;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-  k<<<a.tiles, BM * BN / 64, lds, st>>>(a);
+  k<<<a.tiles, BM * BN / WTN, lds, st>>>(a);
   return hipGetLastError();
 }
 
 // CML_CONV_GEMM_VARIANT (A/B): 0 = 128 x 128, 2 buffers; 1 = 128 x 128, 3 buffers;
-// 2 = 256 x 128 (8 waves), 2 buffers (default); 3 = 256 x 128, 3 buffers. N % 128 != 0: 256 x 64.
-// Measured on the ResNet-50 3x3 shapes at batch 2048 (bench/conv3x3.py, profiles/r02_conv_gemm24/):
-// variant 2 is the fastest or within 3 % everywhere; the third buffer does not pay here.
+// 2 = 256 x 128 (8 waves), 2 buffers; 3 = 256 x 128, 3 buffers; 4 (default) = 256 x 256, 8 waves
+// of 64 x 128 (N % 256 == 0, else 2). N % 128 != 0: 256 x 64.
+// Measured on the ResNet-50 3x3 shapes at batch 2048 (bench/conv3x3.py, profiles/r02_conv_gemm24/,
+// r02_conv_gemm30/): 2 beats 0, 1, 3 (the third buffer does not pay here); 4 is 13-17 % faster
+// than 2 on the 256 / 512-channel layers (3x3 data gradient 0.52 ms vs MIOpen 0.71-0.74).
 int gemm_variant() {
   static const int v = [] {
     const char* e = getenv("CML_CONV_GEMM_VARIANT");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 4;
   }();
   return v;
 }
@@ -225,8 +238,9 @@ int gemm_variant() {
 template <int TAPS>
 hipError_t launch_v(GArgs& a, int64_t M, hipStream_t st) {
   const bool wide = a.N % 128 == 0;
-  const int v = wide ? gemm_variant() : 0;
-  const int BM = !wide ? 256 : (v >= 2 ? 256 : 128), BN = wide ? 128 : 64;
+  int v = wide ? gemm_variant() : 0;
+  if (v == 4 && a.N % 256) v = 2;                 // 256 x 256 tiles need N % 256 == 0
+  const int BM = !wide ? 256 : (v >= 2 ? 256 : 128), BN = v == 4 ? 256 : (wide ? 128 : 64);
   a.ntn = a.N / BN;
   const int64_t tiles = (M + BM - 1) / BM * a.ntn;
   if (tiles >= (1ll << 31)) return hipErrorInvalidValue;
@@ -236,6 +250,7 @@ hipError_t launch_v(GArgs& a, int64_t M, hipStream_t st) {
     case 1: return launch_g<128, 128, TAPS, 3>(a, st);
     case 2: return launch_g<256, 128, TAPS, 2>(a, st);
     case 3: return launch_g<256, 128, TAPS, 3>(a, st);
+    case 4: return launch_g<256, 256, TAPS, 2, 128>(a, st);
     default: return launch_g<128, 128, TAPS, 2>(a, st);
   }
 }
