@@ -64,6 +64,11 @@ def main():
         w2 = w.permute(0, 2, 3, 1).reshape(C, 9 * C).contiguous()
         wr2 = wr.permute(0, 2, 3, 1).reshape(C, 9 * C).contiguous()
         t_g = _t(lambda: L.conv_gemm(x, w2, 9))
+        zr = torch.zeros(64, dtype=torch.bfloat16, device=dev)
+        t_gst = _t(lambda: L.conv_gemm_bn(x, w2, 9, zr, rm, rm, rv, 1e-5, 0.1))
+        y_lib = F.conv2d(x, w, padding=1)
+        t_st = _t(lambda: L.bn_stats(y_lib, rm, rv, 1e-5, 0.1))
+        del y_lib
         t_gdg = _t(lambda: L.conv_gemm(gy, wr2, 9))
         yg = L.conv_gemm(x[:4].contiguous(memory_format=torch.channels_last), w2, 9)
         g_ref = F.conv2d(x[:4].float(), w.float(), padding=1)
@@ -93,6 +98,7 @@ def main():
                           "miopen_dgrad_ms": round(t_dg, 4), "own_dgrad_ms": round(t_own_dg, 4),
                           "miopen_wgrad_ms": round(t_wg, 4), "dgrad_rel_err": dg_err,
                           "glds_fwd_ms": round(t_g, 4), "glds_dgrad_ms": round(t_gdg, 4),
+                          "glds_fwd_stats_ms": round(t_gst, 4), "bn_stats_ms": round(t_st, 4),
                           "glds_tflops": round(flops / t_g / 1e9, 1),
                           "glds_fwd_err": g_err, "glds_dgrad_err": gdg_err,
                           "own_wgrad_ms": round(t_owg, 4), "own_wgrad_pro_ms": round(t_owg_pro, 4),

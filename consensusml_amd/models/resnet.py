@@ -57,6 +57,9 @@ FUSED_BN3_BWD = os.environ.get("CML_FUSED_BN3_BWD", "1") == "1"
 FUSED_BN3_BWD_MAX_PLANES = int(os.environ.get("CML_FUSED_BN3_BWD_MAX_PLANES", "128"))
 # stride-1 3x3 convs: data gradient on csrc/kernels/conv_gemm.hip (ops.conv.conv3x3)
 OWN_DGRAD3X3 = os.environ.get("CML_DGRAD3X3", "1") == "1"
+# ... and their forward on conv_gemm too, with bn2's statistics in the epilogue
+# (ops.conv.conv3x3_bn_stats) instead of a separate statistics pass over z2
+CONV3X3_BN_STATS = os.environ.get("CML_CONV3X3_BN_STATS", "1") == "1"
 
 
 def fused_bn3_bwd_policy(planes: int) -> bool:
@@ -278,11 +281,15 @@ class Bottleneck(nn.Module):
             dlink = ResidualLink() if use_links and self.conv1.link_ok(x) else None
             z1, st1 = self._conv_bn(x, self.conv1, self.bn1, dlink)
         out = self.bn1(z1, stats=st1)
-        z2 = self._conv2(out)
         planes = self.conv3.in_channels
-        hw2 = z2.shape[2] * z2.shape[3]
-        if fused_conv1x1_policy(planes, planes * 4, hw2, 1, True):
-            st2 = fconv.bn_stats(z2, self.bn2)
+        hw2 = (out.shape[2] // self.conv2.stride[0]) * (out.shape[3] // self.conv2.stride[0])
+        fuse3 = fused_conv1x1_policy(planes, planes * 4, hw2, 1, True)
+        if fuse3 and CONV3X3_BN_STATS and OWN_DGRAD3X3 and fconv.conv3x3_ok(out, self.conv2):
+            z2, st2 = fconv.conv3x3_bn_stats(out, self.conv2, self.bn2)
+        else:
+            z2 = self._conv2(out)
+            st2 = fconv.bn_stats(z2, self.bn2) if fuse3 else None
+        if fuse3:
             if self.down_conv is None and fused_bn3_bwd_policy(planes):
                 out_link = ResidualLink() if use_links else None
                 y = fconv.bnrelu_conv1x1_bn_res(z2, self.bn2, st2, self.conv3, self.bn3, x,

@@ -254,6 +254,35 @@ class _Conv3x3Fn(torch.autograd.Function):
         return dx, dw
 
 
+class _Conv3x3BNStatsFn(torch.autograd.Function):
+    """(z, mean, invstd): 3x3 / stride 1 / padding 1 conv on ``conv_gemm.hip`` with the next BN's
+    training statistics accumulated in its epilogue (no separate statistics pass over z); backward
+    as ``_Conv3x3Fn``."""
+
+    @staticmethod
+    def forward(ctx, x, w, rmean, rvar, eps, momentum):
+        Co, Ci = w.shape[0], w.shape[1]
+        wf = w.permute(0, 2, 3, 1).reshape(Co, 9 * Ci).contiguous()   # k = (3 ky + kx) Ci + ci
+        y, mean, invstd = lib().conv_gemm_bn(x, wf, 9, _zero_row(x.device), rmean, rmean, rvar,
+                                             eps, momentum)
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(mean, invstd)
+        return y, mean, invstd
+
+    @staticmethod
+    def backward(ctx, dy, _dm, _di):
+        dx, dw = _Conv3x3Fn.backward(ctx, dy)
+        return dx, dw, None, None, None, None
+
+
+def conv3x3_bn_stats(x: torch.Tensor, conv, bn):
+    """(z, (mean, invstd)) of ``conv(x)`` and bn's training statistics (running stats updated),
+    from one implicit-GEMM kernel; callers check ``conv3x3_ok`` first."""
+    z, m, i = _Conv3x3BNStatsFn.apply(x, conv.weight, bn.running_mean, bn.running_var, bn.eps,
+                                      bn.momentum)
+    return z, (m, i)
+
+
 def conv3x3_ok(x: torch.Tensor, conv) -> bool:
     """Stride-1 padding-1 3x3 convs on NHWC bf16 GPU tensors with 64-multiple channels."""
     return (x.is_cuda and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16

@@ -795,6 +795,44 @@ Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps, const optional<
   return y;
 }
 
+// conv_gemm + the training BatchNorm statistics of its bf16 output (shifted by `shift`, e.g. the
+// running mean) in the epilogue -> {y, mean, invstd}; running stats updated in place when given.
+std::vector<Tensor> conv_gemm_bn(const Tensor& x, const Tensor& w, int64_t taps,
+                                 const optional<Tensor>& zero_in, const optional<Tensor>& shift,
+                                 const optional<Tensor>& rmean, const optional<Tensor>& rvar,
+                                 double eps, double momentum) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4, "conv_gemm_bn: 4-D NHWC input");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(taps == 1 || taps == 9, "conv_gemm_bn: taps 1 or 9");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 &&
+                  w.size(1) == taps * C && w.size(0) % 64 == 0 && C % 64 == 0,
+              "conv_gemm_bn: w must be contiguous bf16 [Cout, taps * C], channels multiples of 64");
+  const int64_t Co = w.size(0), M = N * H * W;
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor zero;
+  if (zero_in.has_value() && zero_in->defined()) {
+    zero = *zero_in;
+    TORCH_CHECK(zero.is_cuda() && zero.device() == x.device() && zero.scalar_type() == at::kBFloat16 &&
+                    zero.is_contiguous() && zero.numel() >= 64, "conv_gemm_bn: zero must be >= 64 bf16");
+  } else {
+    zero = at::zeros({64}, x.options());
+  }
+  Tensor mean = at::empty({Co}, f32), invstd = at::empty({Co}, f32);
+  Tensor part = at::empty({static_cast<int64_t>(cml::conv_gemm_part_floats(M, static_cast<int>(Co)))}, f32);
+  CML_CHECK_HIP(cml::launch_conv_gemm(
+      x.data_ptr(), w.data_ptr(), y.data_ptr(), zero.data_ptr(), static_cast<int>(N),
+      static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(Co),
+      static_cast<int>(taps), cur_stream(), part.data_ptr<float>(),
+      opt_ptr<const float>(shift, at::kFloat, "shift", Co), mean.data_ptr<float>(),
+      invstd.data_ptr<float>(), opt_ptr<float>(rmean, at::kFloat, "running_mean", Co),
+      opt_ptr<float>(rvar, at::kFloat, "running_var", Co), static_cast<float>(eps),
+      static_cast<float>(momentum)));
+  return {y, mean, invstd};
+}
+
 // BatchNorm training statistics only: x NHWC bf16 -> {mean, invstd} (fp32 [C]); running stats
 // updated in place when given.
 std::vector<Tensor> bn_stats(const Tensor& x, const optional<Tensor>& rmean,
@@ -1284,6 +1322,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "weight gradient of a 3x3 stride-1 conv (MFMA, split-K, one tap per grid z)");
   m.def("conv_gemm", &conv_gemm, py::arg("x"), py::arg("w"), py::arg("taps"),
         py::arg("zero") = py::none(), "implicit-GEMM NHWC conv (1x1 / 3x3 stride 1), glds staging");
+  m.def("conv_gemm_bn", &conv_gemm_bn, py::arg("x"), py::arg("w"), py::arg("taps"),
+        py::arg("zero") = py::none(), py::arg("shift") = py::none(),
+        py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
+        py::arg("eps") = 1e-5, py::arg("momentum") = 0.1,
+        "implicit-GEMM conv + BN statistics of the output in the epilogue -> {y, mean, invstd}");
   m.def("conv3x3_bn_fwd", &conv3x3_bn_fwd, "3x3/s1/p1 conv (implicit GEMM) + BN statistics");
   m.def("conv1x1_bnbwd", &conv1x1_bnbwd, "1x1 data gradient through a BN + ReLU backward prologue");
   m.def("conv1x1_link", &conv1x1_link, py::arg("x"), py::arg("w"), py::arg("link"),

@@ -28,6 +28,7 @@
 // workgroups that share an m-tile (one per n-tile) get equal blockIdx % 8, i.e. run on one XCD
 // under round-robin placement, so x is read from HBM once and re-read from that XCD's L2 (speed
 // only: any placement is correct).
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -500,6 +501,38 @@ __global__ __launch_bounds__(256) void conv1x1_bn_finalize_kernel(
   }
 }
 
+// First level of a two-level fold of a tall [ntn][R][2][BN] partial slab (one row per output tile
+// of a non-persistent GEMM): block (s, nt) sums rows [s rp, (s + 1) rp) into out row s of
+// [ntn][S][2][BN], so the per-channel finalize reads S << R rows (fixed order: deterministic).
+__global__ __launch_bounds__(256) void part_fold_kernel(const float* __restrict__ part, int R,
+                                                        int BN, int rp, int S,
+                                                        float* __restrict__ out) {
+  __shared__ float red[256];
+  const int cols = 2 * BN, nt = blockIdx.y, s = blockIdx.x;
+  const int RL = cols >= 256 ? 1 : 256 / cols;
+  const int t = threadIdx.x, rl = t / (cols >= 256 ? 256 : cols);
+  const int r0 = s * rp, r1 = min(R, r0 + rp);
+  const float* base = part + static_cast<int64_t>(nt) * R * cols;
+  float* ob = out + (static_cast<int64_t>(nt) * S + s) * cols;
+  if (RL == 1) {
+    for (int col = t; col < cols; col += 256) {
+      float acc = 0.f;
+      for (int r = r0; r < r1; ++r) acc += base[static_cast<int64_t>(r) * cols + col];
+      ob[col] = acc;
+    }
+    return;
+  }
+  const int col = t - rl * cols;
+  float acc = 0.f;
+  for (int r = r0 + rl; r < r1; r += RL) acc += base[static_cast<int64_t>(r) * cols + col];
+  red[t] = acc;
+  __syncthreads();
+  if (rl == 0) {
+    for (int k = 1; k < RL; ++k) acc += red[k * cols + col];
+    ob[col] = acc;
+  }
+}
+
 // BN-backward sums from the partial slab (SM_BNBWD): sdz = S, sdzx = Q * invstd (same fixed fold
 // order as the statistics finalize).
 __global__ __launch_bounds__(256) void conv1x1_bnbwd_finalize_kernel(
@@ -687,6 +720,29 @@ bool bad_shape(int64_t M, int K, int N) {
 size_t conv1x1_bn_part_floats(int64_t M, int K, int N, bool pro) {
   const Plan p = make_plan(M, K, N, pro ? 2 : 0);
   return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
+}
+
+int bn_part_fold_slices(int R, int ntn) {
+  if (R <= 256) return 0;
+  const int want = std::max(256, (2048 + ntn - 1) / ntn);
+  return std::min((R + 15) / 16, want);
+}
+
+hipError_t launch_bn_stats_finalize(const float* part, int R, int BN, int N, int64_t M,
+                                   const float* shift, float eps, float momentum, float* mean,
+                                   float* invstd, float* rmean, float* rvar, hipStream_t st,
+                                   float* fold) {
+  const int S = fold ? bn_part_fold_slices(R, N / BN) : 0;
+  if (S > 0) {
+    const int rp = (R + S - 1) / S;
+    const int S2 = (R + rp - 1) / rp;
+    part_fold_kernel<<<dim3(S2, N / BN), 256, 0, st>>>(part, R, BN, rp, S2, fold);
+    part = fold;
+    R = S2;
+  }
+  conv1x1_bn_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, R, BN, N, M, shift, eps, momentum,
+                                                          mean, invstd, rmean, rvar);
+  return hipGetLastError();
 }
 
 size_t conv1x1_link_part_floats(int64_t M, int K, int N) {

@@ -39,6 +39,8 @@ struct GArgs {
   const uint16_t* w;      // [N][TAPS * C]
   uint16_t* y;            // [M][N]
   const uint16_t* zero;   // >= 64 zero elements
+  float* part;            // ST: [ntn][mtiles * WM][2][BN] shifted sums of the bf16 output
+  const float* shift;     // ST: [N] statistics shift (the BN running mean) or null
   int M, C, N, H, W, HW;
   int KS;                 // TAPS * C / 64
   int ntn, tiles;
@@ -49,7 +51,9 @@ struct GArgs {
 // step) + a raw s_barrier retires only step ks + 1 (a __syncthreads() would drain the queue).
 // WTN: output channels per wave (64: 2 x 2 accumulators; 128: 4 x 2, half the x-fragment reads
 // per MFMA).
-template <int BM, int BN, int TAPS, int NBUF = 2, int WTN = 64>
+// ST: the epilogue also accumulates the BN statistics (sum, sum of squares of y_bf16 - shift) of
+// the stored values per channel and writes one partial row per (m-tile, wave row).
+template <int BM, int BN, int TAPS, int NBUF = 2, int WTN = 64, bool ST = false>
 __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
   constexpr int WN = BN / WTN, WM = BM / 64, NW = WN * WM;
   constexpr int NI = WTN / 32;                  // accumulator rows (n) per wave
@@ -198,13 +202,53 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+    const int cb = n0 + wn * WTN + 64 * sb + 8 * c;   // this lane's 8 channels
+    float sh[8], ss[8], sq[8];
+    if constexpr (ST) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        sh[q] = a.shift ? a.shift[cb + q] : 0.f;
+        ss[q] = 0.f;
+        sq[q] = 0.f;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int pr = 8 * k + (lane >> 3);
       const uint4 v = *reinterpret_cast<const uint4*>(simg + swz(pr, c));
-      if (mb + pr < a.M)
-        *reinterpret_cast<uint4*>(a.y + static_cast<int64_t>(mb + pr) * a.N + n0 + wn * WTN +
-                                  64 * sb + 8 * c) = v;
+      if (mb + pr < a.M) {
+        *reinterpret_cast<uint4*>(a.y + static_cast<int64_t>(mb + pr) * a.N + cb) = v;
+        if constexpr (ST) {
+          const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float lo = __uint_as_float(w4[q] << 16) - sh[2 * q];
+            const float hi = __uint_as_float(w4[q] & 0xffff0000u) - sh[2 * q + 1];
+            ss[2 * q] += lo;
+            ss[2 * q + 1] += hi;
+            sq[2 * q] = fmaf(lo, lo, sq[2 * q]);
+            sq[2 * q + 1] = fmaf(hi, hi, sq[2 * q + 1]);
+          }
+        }
+      }
+    }
+    if constexpr (ST) {
+      // fold the 8 lanes sharing a channel group (lane & 7), one partial row per (m-tile, wm)
+      float* pp = a.part + (static_cast<int64_t>(nt) * (a.tiles / a.ntn) * WM + mt * WM + wm) * 2 * BN;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float sv = ss[q], qv = sq[q];
+#pragma unroll
+        for (int o = 8; o < 64; o <<= 1) {
+          sv += __shfl_xor(sv, o, 64);
+          qv += __shfl_xor(qv, o, 64);
+        }
+        if (lane < 8) {
+          const int col = wn * WTN + 64 * sb + 8 * lane + q;
+          pp[col] = sv;
+          pp[BN + col] = qv;
+        }
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -213,7 +257,8 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
 
 template <int BM, int BN, int TAPS, int NBUF, int WTN = 64>
 hipError_t launch_g(const GArgs& a, hipStream_t st) {
-  auto k = &conv_gemm_kernel<BM, BN, TAPS, NBUF, WTN>;
+  auto k = a.part ? &conv_gemm_kernel<BM, BN, TAPS, NBUF, WTN, true>
+                  : &conv_gemm_kernel<BM, BN, TAPS, NBUF, WTN, false>;
   const size_t lds = NBUF * static_cast<size_t>(BM + BN) * 128;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
@@ -257,8 +302,31 @@ hipError_t launch_v(GArgs& a, int64_t M, hipStream_t st) {
 
 }  // namespace
 
+namespace {
+// the tile (BM, BN) launch_v picks for N
+void tile_of(int N, int* BM, int* BN) {
+  const bool wide = N % 128 == 0;
+  int v = wide ? gemm_variant() : 0;
+  if (v == 4 && N % 256) v = 2;
+  *BM = !wide ? 256 : (v >= 2 ? 256 : 128);
+  *BN = v == 4 ? 256 : (wide ? 128 : 64);
+}
+}  // namespace
+
+size_t conv_gemm_part_floats(int64_t M, int N) {
+  int BM, BN;
+  tile_of(N, &BM, &BN);
+  const int64_t mtiles = (M + BM - 1) / BM;
+  const int R = static_cast<int>(mtiles * (BM / 64));
+  // the slab, then the fold area of launch_bn_stats_finalize
+  return static_cast<size_t>(N / BN) * (static_cast<size_t>(R) + bn_part_fold_slices(R, N / BN)) *
+         2 * BN;
+}
+
 hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* zero, int Nimg,
-                            int H, int W, int C, int N, int taps, hipStream_t st) {
+                            int H, int W, int C, int N, int taps, hipStream_t st, float* part,
+                            const float* shift, float* mean, float* invstd, float* rmean,
+                            float* rvar, float eps, float momentum) {
   const int64_t M = static_cast<int64_t>(Nimg) * H * W;
   if (C % kBK || N % 64 || (taps != 1 && taps != 9) || M < 1 || M >= (1ll << 31) ||
       static_cast<int64_t>(taps) * C > 65536)
@@ -275,7 +343,15 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
   a.W = W;
   a.HW = H * W;
   a.KS = taps * C / kBK;
-  return taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
+  a.part = part;
+  a.shift = shift;
+  hipError_t e = taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
+  if (e != hipSuccess || !part || !mean) return e;
+  int BM, BN;
+  tile_of(N, &BM, &BN);
+  const int R = static_cast<int>((M + BM - 1) / BM) * (BM / 64);
+  return launch_bn_stats_finalize(part, R, BN, N, M, shift, eps, momentum, mean, invstd, rmean,
+                                  rvar, st, part + static_cast<size_t>(N / BN) * R * 2 * BN);
 }
 
 }  // namespace cml

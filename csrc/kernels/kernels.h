@@ -282,8 +282,24 @@ hipError_t launch_conv3x3_bn_fwd(const void* x, const void* w, void* y, float* p
 // Implicit-GEMM NHWC conv, stride 1, 1x1 (taps 1) or 3x3 padding 1 (taps 9), global_load_lds
 // double-buffered (conv_gemm.hip): x [Nimg][H][W][C], w [N][taps][C], y [Nimg][H][W][N]; zero:
 // >= 64 zero bf16 (padding rows).
+// With part / mean non-null also the training BatchNorm statistics of y (shifted by `shift`),
+// finalized like conv1x1_bn_fwd (running stats updated when rmean / rvar are non-null); part:
+// conv_gemm_part_floats floats.
+size_t conv_gemm_part_floats(int64_t M, int N);
 hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* zero, int Nimg,
-                            int H, int W, int C, int N, int taps, hipStream_t st);
+                            int H, int W, int C, int N, int taps, hipStream_t st,
+                            float* part = nullptr, const float* shift = nullptr,
+                            float* mean = nullptr, float* invstd = nullptr,
+                            float* rmean = nullptr, float* rvar = nullptr, float eps = 1e-5f,
+                            float momentum = 0.1f);
+// BN statistics from a [ntn][R][2][BN] partial slab of shifted sums (conv1x1.hip's finalize).
+// With `fold` (>= ntn * bn_part_fold_slices(R, ntn) * 2 * BN floats) a tall slab is first folded
+// to bn_part_fold_slices rows per column tile by a wide kernel.
+int bn_part_fold_slices(int R, int ntn);
+hipError_t launch_bn_stats_finalize(const float* part, int R, int BN, int N, int64_t M,
+                                   const float* shift, float eps, float momentum, float* mean,
+                                   float* invstd, float* rmean, float* rvar, hipStream_t st,
+                                   float* fold = nullptr);
 
 // Backward variants of the fused 1x1 conv (conv1x1.hip), stride 1, W given as [N][K] (for a data
 // gradient: the forward weight transposed).

@@ -253,6 +253,48 @@ def test_conv_gemm_and_3x3_dgrad(cuda, C, Co, H):
     assert float((conv.weight.grad.float() - wr.grad).norm() / wr.grad.norm()) < 1e-2
 
 
+@pytest.mark.parametrize("C,Co,H,N", [(64, 64, 9, 3), (128, 128, 7, 3), (256, 256, 5, 3),
+                                      (512, 512, 4, 5), (64, 192, 6, 2), (128, 512, 14, 4),
+                                      (64, 64, 66, 4), (128, 128, 40, 12)])
+def test_conv3x3_bn_stats_vs_fp32(cuda, C, Co, H, N):
+    """conv_gemm_bn (ops.conv.conv3x3_bn_stats): the output, the BN batch statistics of the bf16
+    output (epilogue partial sums, shifted by the running mean), the running-stat update and the
+    gradients vs fp32 PyTorch. Odd M exercises partial tiles, the two largest M the two-level
+    fold of the partial slab."""
+    import torch.nn.functional as F
+    from consensusml_amd.ops import conv as fconv
+    g0 = torch.Generator(device=cuda).manual_seed(12)
+    x = (torch.randn(N, C, H, H, device=cuda, generator=g0) + 0.3).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(Co, C, 3, 3, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
+    conv = torch.nn.Conv2d(C, Co, 3, padding=1, bias=False).to(cuda, torch.bfloat16)
+    bn = torch.nn.BatchNorm2d(Co).to(cuda)
+    with torch.no_grad():
+        conv.weight.copy_(w)
+        bn.running_mean.copy_(torch.randn(Co, device=cuda, generator=g0) * 0.1)
+    rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+    xi = x.clone().requires_grad_(True)
+    z, (mean, invstd) = fconv.conv3x3_bn_stats(xi, conv, bn)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    assert float((z.float() - ref).norm() / ref.norm()) < 5e-3
+    zb = z.float()
+    M = N * H * H
+    m_ref, v_ref = zb.mean((0, 2, 3)), zb.var((0, 2, 3), unbiased=False)
+    torch.testing.assert_close(mean, m_ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(invstd, (v_ref + bn.eps).rsqrt(), rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(bn.running_mean, 0.9 * rm0 + 0.1 * m_ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, 0.9 * rv0 + 0.1 * v_ref * M / (M - 1),
+                               rtol=1e-3, atol=1e-4)
+    gy = torch.randn(z.shape, device=cuda, generator=g0).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    z.backward(gy)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    F.conv2d(xr, wr, padding=1).backward(gy.float())
+    assert float((xi.grad.float() - xr.grad).norm() / xr.grad.norm()) < 5e-3
+    assert float((conv.weight.grad.float() - wr.grad).norm() / wr.grad.norm()) < 1e-2
+
+
 @pytest.mark.parametrize("C,Co,H", [(64, 64, 9), (128, 128, 6), (256, 256, 5), (64, 256, 5)])
 @pytest.mark.parametrize("pro", [False, True])
 def test_wgrad3x3_tap_vs_fp32(cuda, C, Co, H, pro):

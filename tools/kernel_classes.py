@@ -10,7 +10,7 @@ CLASSES = [
     ("BatchNorm passes (bn_act.hip)", r"cml::.*bn_(apply|stats|bwd|finalize|apply2|bwd_apply2|bwd_reduce2)"),
     ("fused 1x1 conv + BN (conv1x1.hip)", r"cml::.*(conv1x1_bn|conv1x1_bnbwd|bn_bwd_coeffs)"),
     ("1x1 weight gradient (wgrad1x1.hip)", r"cml::.*wgrad1x1"),
-    ("3x3 data gradient (conv_gemm.hip)", r"cml::.*conv_gemm"),
+    ("3x3 conv fwd + data gradient (conv_gemm.hip)", r"cml::.*conv_gemm"),
     ("stem / pool (stem_conv.hip, pool.hip)", r"cml::.*(stem_|maxpool|bn_relu_max)"),
     ("aggregation + optimizer (agg_update, gram, weights)", r"cml::.*(agg_|gram|robust_weights|weights_kernel|fault)"),
     ("conv fwd (MIOpen / CK)", r"(grouped_conv_fwd|igemm_fwd|conv_fwd)"),
