@@ -212,11 +212,44 @@ __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)
 // residual gradient of the same tensor). SM_BNBWD: the sums are s = sum (sm bit ? v : 0) and
 // q = sum (sm bit ? v : 0) (sz - shift) -- the backward reduction of the BN + ReLU whose output
 // gradient v is (the consumer BN's mean in shift) -- instead of the BN statistics of v.
-template <bool EL, int SM>
+template <bool EL, int SM, int MT>
 __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], float (&ss)[8],
                                          float (&sq)[8], const float (&sh)[8], char* simg, int m0,
                                          int ncol0, int n0, int lane) {
   const int h = lane >> 5, r32 = lane & 31;
+  const int c = lane & 7;
+  // EL / SM_BNBWD operands of the read-back rows are issued as one batch before they are needed
+  // (a 1-2 k-step GEMM was otherwise bound by these dependent loads, one latency per row pair):
+  // all 8 rows at once with one operand (EL), in batches of 4 with two, halved again at MT = 2
+  // (more registers would spill). Rows past M re-read row m0.
+  constexpr bool LD = EL || SM == SM_BNBWD;
+  constexpr int RB = ((EL && SM == SM_BNBWD) ? 4 : 8) / MT;   // rows per batch
+  uint4 lv[RB], zv[RB];
+  uint32_t lbv[RB], zbv[RB];
+  if constexpr (!(EL && SM == SM_BNBWD)) {   // one operand: keep the row body's arguments defined
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      if constexpr (!EL) { lv[k] = make_uint4(0u, 0u, 0u, 0u); lbv[k] = 0u; }
+      if constexpr (SM != SM_BNBWD) { zv[k] = make_uint4(0u, 0u, 0u, 0u); zbv[k] = 0u; }
+    }
+  }
+  auto issue = [&](int k0) {
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const int p = 8 * (k0 + k) + (lane >> 3);
+      const int64_t row = m0 + p < a.M ? m0 + p : m0;
+      const int64_t e0 = row * a.N + n0 + ncol0 + 8 * c;
+      if constexpr (EL) {
+        lv[k] = *reinterpret_cast<const uint4*>(a.link + e0);
+        lbv[k] = a.lm[e0 >> 3];
+      }
+      if constexpr (SM == SM_BNBWD) {
+        zv[k] = *reinterpret_cast<const uint4*>(a.sz + e0);
+        zbv[k] = a.sm[e0 >> 3];
+      }
+    }
+  };
+  if constexpr (LD) issue(0);
 #pragma unroll
   for (int jm = 0; jm < 2; ++jm) {
     const int p = 32 * jm + r32;                       // pixel row of the wave block
@@ -235,56 +268,61 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
   // the wave's own LDS writes complete before its reads
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  const int c = lane & 7;
-#pragma unroll 2
-  for (int k = 0; k < 8; ++k) {
+  // one read-back row: 8 channels (lane & 7) of pixel 8 k + lane / 8
+  auto row = [&](int k, const uint4& l, uint32_t lb, const uint4& z, uint32_t zb) {
     const int p = 8 * k + (lane >> 3);
     uint4 v = *reinterpret_cast<const uint4*>(simg + swz(p, c));
-    if (m0 + p < a.M) {
-      const int64_t e0 = static_cast<int64_t>(m0 + p) * a.N + n0 + ncol0 + 8 * c;
-      const int64_t b0 = e0 >> 3;                          // mask byte of these 8 channels
-      if constexpr (EL) {
-        const uint4 l = *reinterpret_cast<const uint4*>(a.link + e0);
-        const uint32_t lb = a.lm[b0];
-        const uint32_t l4[4] = {l.x, l.y, l.z, l.w};
-        uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    if (m0 + p >= a.M) return;
+    const int64_t e0 = static_cast<int64_t>(m0 + p) * a.N + n0 + ncol0 + 8 * c;
+    if constexpr (EL) {
+      const uint32_t l4[4] = {l.x, l.y, l.z, l.w};
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float lo = __uint_as_float(w4[q] << 16) +
-                           (((lb >> (2 * q)) & 1u) ? __uint_as_float(l4[q] << 16) : 0.f);
-          const float hi = __uint_as_float(w4[q] & 0xffff0000u) +
-                           (((lb >> (2 * q + 1)) & 1u) ? __uint_as_float(l4[q] & 0xffff0000u) : 0.f);
-          w4[q] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
-        }
-        v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      for (int q = 0; q < 4; ++q) {
+        const float lo = __uint_as_float(w4[q] << 16) +
+                         (((lb >> (2 * q)) & 1u) ? __uint_as_float(l4[q] << 16) : 0.f);
+        const float hi = __uint_as_float(w4[q] & 0xffff0000u) +
+                         (((lb >> (2 * q + 1)) & 1u) ? __uint_as_float(l4[q] & 0xffff0000u) : 0.f);
+        w4[q] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
       }
-      *reinterpret_cast<uint4*>(a.y + e0) = v;
-      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-      if constexpr (SM == SM_BN) {
+      v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+    *reinterpret_cast<uint4*>(a.y + e0) = v;
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    if constexpr (SM == SM_BN) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float lo = __uint_as_float(w4[q] << 16) - sh[2 * q];
-          const float hi = __uint_as_float(w4[q] & 0xffff0000u) - sh[2 * q + 1];
-          ss[2 * q] += lo;
-          ss[2 * q + 1] += hi;
-          sq[2 * q] = fmaf(lo, lo, sq[2 * q]);
-          sq[2 * q + 1] = fmaf(hi, hi, sq[2 * q + 1]);
-        }
-      } else if constexpr (SM == SM_BNBWD) {
-        const uint4 z = *reinterpret_cast<const uint4*>(a.sz + e0);
-        const uint32_t zb = a.sm[b0];
-        const uint32_t z4[4] = {z.x, z.y, z.z, z.w};
+      for (int q = 0; q < 4; ++q) {
+        const float lo = __uint_as_float(w4[q] << 16) - sh[2 * q];
+        const float hi = __uint_as_float(w4[q] & 0xffff0000u) - sh[2 * q + 1];
+        ss[2 * q] += lo;
+        ss[2 * q + 1] += hi;
+        sq[2 * q] = fmaf(lo, lo, sq[2 * q]);
+        sq[2 * q + 1] = fmaf(hi, hi, sq[2 * q + 1]);
+      }
+    } else if constexpr (SM == SM_BNBWD) {
+      const uint32_t z4[4] = {z.x, z.y, z.z, z.w};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float lo = ((zb >> (2 * q)) & 1u) ? __uint_as_float(w4[q] << 16) : 0.f;
-          const float hi = ((zb >> (2 * q + 1)) & 1u) ? __uint_as_float(w4[q] & 0xffff0000u) : 0.f;
-          ss[2 * q] += lo;
-          ss[2 * q + 1] += hi;
-          sq[2 * q] = fmaf(lo, __uint_as_float(z4[q] << 16) - sh[2 * q], sq[2 * q]);
-          sq[2 * q + 1] = fmaf(hi, __uint_as_float(z4[q] & 0xffff0000u) - sh[2 * q + 1], sq[2 * q + 1]);
-        }
+      for (int q = 0; q < 4; ++q) {
+        const float lo = ((zb >> (2 * q)) & 1u) ? __uint_as_float(w4[q] << 16) : 0.f;
+        const float hi = ((zb >> (2 * q + 1)) & 1u) ? __uint_as_float(w4[q] & 0xffff0000u) : 0.f;
+        ss[2 * q] += lo;
+        ss[2 * q + 1] += hi;
+        sq[2 * q] = fmaf(lo, __uint_as_float(z4[q] << 16) - sh[2 * q], sq[2 * q]);
+        sq[2 * q + 1] = fmaf(hi, __uint_as_float(z4[q] & 0xffff0000u) - sh[2 * q + 1], sq[2 * q + 1]);
       }
     }
+  };
+  if constexpr (LD) {
+#pragma unroll
+    for (int kb = 0; kb < 8; kb += RB) {
+      if (kb > 0) issue(kb);
+#pragma unroll
+      for (int k = 0; k < RB; ++k) row(kb + k, lv[k], lbv[k], zv[k], zbv[k]);
+    }
+  } else {
+    const uint4 none = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll 2
+    for (int k = 0; k < 8; ++k) row(k, none, 0u, none, 0u);
   }
   // the image is rewritten by the next tile's epilogue only after these reads have returned
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -407,7 +445,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
         if constexpr (ALIAS) __syncthreads();   // every wave is done reading x before the images
 #pragma unroll
         for (int u = 0; u < MT; ++u)
-          epilogue<EL, SM>(a, acc[u], ss, sq, sh, s_img + wave * 8192,
+          epilogue<EL, SM, MT>(a, acc[u], ss, sq, sh, s_img + wave * 8192,
                            t * BM + wm * 64 * MT + 64 * u, wn * 64, n0, lane);
       }
       if (!more) break;
@@ -627,13 +665,13 @@ bool mt2_enabled() {
   return on;
 }
 
-Plan make_plan(int64_t M, int K, int N, int naff, int kaff = -1) {
+Plan make_plan(int64_t M, int K, int N, int naff, int kaff = -1, bool mt2_ok = true) {
   const int WN = N % 256 == 0 ? 4 : (N % 128 == 0 ? 2 : 1);
   Plan p = plan_for(WN, M, K, N, naff, 1, kaff);
   if (WN == 4 && !p.wres) p = plan_for(2, M, K, N, naff, 1, kaff);
   // non-resident 128 x 128 tiles: two 64-pixel sub-blocks per wave (see the kernel)
   // (not with the BN-backward prologue: its extra z / mask prefetch registers would spill)
-  if (p.WN == 2 && !p.wres && naff < 3 && mt2_enabled()) {
+  if (p.WN == 2 && !p.wres && naff < 3 && mt2_ok && mt2_enabled()) {
     const Plan q = plan_for(2, M, K, N, naff, 2, kaff);
     if (!q.wres && q.lds <= 80 * 1024) p = q;
   }
@@ -644,7 +682,7 @@ template <int WN, int WM, int PM, bool WRES, bool S2, bool EL = false, int SM = 
           bool TAP = false>
 hipError_t launch_t(const C1Args& a, const Plan& p, hipStream_t st) {
   auto k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 1, TAP>;
-  if constexpr (WN == 2 && !WRES && PM != PM_BNBWD) {
+  if constexpr (WN == 2 && !WRES && PM != PM_BNBWD && SM != SM_BNBWD) {
     if (p.MT == 2) k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 2, TAP>;
   }
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
@@ -745,8 +783,9 @@ hipError_t launch_bn_stats_finalize(const float* part, int R, int BN, int N, int
   return hipGetLastError();
 }
 
+// the link + BN-backward-sums kernel runs MT = 1 tiles (at MT = 2 its epilogue operands spill)
 size_t conv1x1_link_part_floats(int64_t M, int K, int N) {
-  const Plan p = make_plan(M, K, N, 0);
+  const Plan p = make_plan(M, K, N, 0, -1, false);
   return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
 }
 
@@ -806,7 +845,7 @@ hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void
   if (bad_shape(M, K, N)) return hipErrorInvalidValue;
   const bool sums = sz != nullptr;
   if (sums && (!sm || !mean || !invstd || !part || !sdz || !sdzx)) return hipErrorInvalidValue;
-  const Plan p = make_plan(M, K, N, 0);
+  const Plan p = make_plan(M, K, N, 0, -1, !sums);
   C1Args a = base_args(x, w, y, M, K, N, p);
   a.link = reinterpret_cast<const uint16_t*>(link);
   a.lm = lm;
