@@ -55,6 +55,8 @@ FUSED_CONV1X1 = os.environ.get("CML_FUSED_CONV1X1", "1") == "1"
 # conv1's data-gradient epilogue (ops.conv.bnrelu_conv1x1_bn_res)
 FUSED_BN3_BWD = os.environ.get("CML_FUSED_BN3_BWD", "1") == "1"
 FUSED_BN3_BWD_MAX_PLANES = int(os.environ.get("CML_FUSED_BN3_BWD_MAX_PLANES", "128"))
+# fused identity tails of planes 64 / 128 without a stored z3 (ops.conv._RecomputeTailFn)
+RECOMPUTE_TAIL = os.environ.get("CML_RECOMPUTE_TAIL", "1") == "1"
 # stride-1 3x3 convs: data gradient on csrc/kernels/conv_gemm.hip (ops.conv.conv3x3)
 OWN_DGRAD3X3 = os.environ.get("CML_DGRAD3X3", "1") == "1"
 # ... and their forward on conv_gemm too, with bn2's statistics in the epilogue
@@ -292,8 +294,10 @@ class Bottleneck(nn.Module):
         if fuse3:
             if self.down_conv is None and fused_bn3_bwd_policy(planes):
                 out_link = ResidualLink() if use_links else None
-                y = fconv.bnrelu_conv1x1_bn_res(z2, self.bn2, st2, self.conv3, self.bn3, x,
-                                                link, out_link)
+                tail = fconv.bnrelu_conv1x1_bn_res_recompute \
+                    if RECOMPUTE_TAIL and fconv.recompute_tail_ok(planes) \
+                    else fconv.bnrelu_conv1x1_bn_res
+                y = tail(z2, self.bn2, st2, self.conv3, self.bn3, x, link, out_link)
                 if out_link is not None:
                     y._cml_link = out_link
                 return y

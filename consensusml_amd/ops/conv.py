@@ -200,6 +200,110 @@ class _BNReLUConv1x1BNResFn(torch.autograd.Function):
         return (dz, dg2, db2, None, None, dw, dg3, db3, dres) + (None,) * 6
 
 
+_CONST = {}
+
+
+def _const(n: int, v: float, device) -> torch.Tensor:
+    key = (n, v, device)
+    t = _CONST.get(key)
+    if t is None:
+        t = _CONST[key] = torch.full((n,), v, dtype=torch.float32, device=device)
+    return t
+
+
+class _RecomputeTailFn(torch.autograd.Function):
+    """Identity-block tail y = relu(bn3(conv3(relu(bn2(z2)))) + res) that never stores z3.
+
+    z3 = conv3(y2) (y2 = relu(bn2(z2)), p channels) has 4p channels, so in the layer-1/2 blocks
+    writing it and reading it back (forward apply, bn3's backward sums, conv3's two gradient
+    GEMMs) is most of the tail's HBM traffic. Here:
+
+    Forward: a statistics-only pass of the fused conv (bn2 + ReLU prologue, bn3 statistics from
+    the bf16 products, nothing stored), then the same GEMM again (same plan: the same bf16 z3)
+    with bn3 + residual + ReLU applied in its epilogue (``conv1x1_bnres``, y and its bit mask).
+
+    Backward, with u = m * g (g the block-output gradient, m bn3's ReLU mask) and
+    dz3 = a u + b z3 + c (bn3's backward: a = gamma invstd, b, c from its sums):
+      P = u^T y2 and s = sum u           one weight-gradient pass (``wgrad1x1_ex`` mode 2 + column
+                                         sums), reading g, m and z2 -- not z3
+      Gram = y2^T y2, sum y2             one small pass over z2 (mode 3)
+      q = sum u (z3 - mean) invstd = invstd (rowsum(W3 * P) - mean s)    (z3 = y2 W3^T)
+      dW3 = diag(a) P + diag(b) W3 Gram + c (sum y2)^T
+      dy2 = (a u + c) W3 + y2 (W3^T diag(b) W3)     one two-source GEMM (``conv1x1_cat``, K = 5p)
+    All exact identities of the unfused computation (z3 in fp32 instead of its bf16 rounding).
+    The residual gradient m * g is parked on ``res_link`` as a ``MaskedGrad`` as in
+    ``_BNReLUConv1x1BNResFn``."""
+
+    @staticmethod
+    def forward(ctx, z, g2, b2, mean2, invstd2, w, g3, b3, res, rmean3, rvar3, eps, momentum,
+                res_link, out_link):
+        sc = g2.float() * invstd2
+        bi = b2.float() - mean2 * sc
+        wc = w.contiguous()
+        m3, i3 = lib().conv1x1_bn_stats_only(z, wc, sc, bi, rmean3, rmean3, rvar3, eps, momentum)
+        sc3 = g3.float() * i3
+        bi3 = b3.float() - m3 * sc3
+        y, mask = lib().conv1x1_bnres(z, wc, sc, bi, sc3, bi3, res)
+        ctx.save_for_backward(z, g2, b2, mean2, invstd2, w, sc, bi, mask, g3, m3, i3)
+        ctx.res_link, ctx.out_link = res_link, out_link
+        if out_link is not None:
+            out_link.bn_ctx = None   # the consumer's conv1 epilogue owes this tail no sums
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        z, g2, b2, mean2, invstd2, w, sc, bi, mask, g3, m3, i3 = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        ol = ctx.out_link
+        if ol is not None:
+            extra = ol.take_tensor()
+            ol.sums = ol.bn_ctx = None
+            if extra is not None:
+                gy = (gy + extra).contiguous(memory_format=torch.channels_last)
+        M = gy.numel() // gy.shape[1]
+        Co, Ci = w.shape[0], w.shape[1]
+        dev = gy.device
+        L = lib()
+        P, s = L.wgrad1x1_ex(gy, z, sc, bi, 2, mask, _const(Co, 1.0, dev), None,
+                             _const(Co, 0.0, dev), True)
+        gram, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
+        W3 = w.reshape(Co, Ci).float()
+        q = i3 * ((W3 * P).sum(1) - m3 * s)
+        ca, cb, cc, dg3, db3 = L.bn_bwd_coeffs(s, q, g3, m3, i3, M)
+        dw = None
+        if ctx.needs_input_grad[5]:
+            dw = (ca[:, None] * P + cb[:, None] * (W3 @ gram) + cc[:, None] * cy[None, :])
+            dw = dw.to(w.dtype).view_as(w)
+        G = W3.t() @ (cb[:, None] * W3)
+        w_cat = torch.cat([W3.t(), G.t()], 1).to(torch.bfloat16).contiguous()
+        dy2 = L.conv1x1_cat(gy, mask, z, torch.cat([ca, sc]), torch.cat([cc, bi]), w_cat)
+        dz, dg2, db2, _ = L.bn_bwd(dy2, None, z, None, g2, b2, mean2, invstd2, True, False)
+        dres = None
+        if ctx.needs_input_grad[8]:
+            mg = MaskedGrad(gy, mask)
+            if ctx.res_link is not None and not ctx.res_link.closed and ctx.res_link.grad is None:
+                ctx.res_link.grad = mg
+            else:
+                dres = mg.materialize()
+        return (dz, dg2, db2, None, None, dw, dg3, db3, dres) + (None,) * 6
+
+
+def recompute_tail_ok(planes: int) -> bool:
+    """Channel counts of the recompute tail's kernels (the Gram pass's column sums need a tile of
+    at most 512 threads: planes 64 and 128, ResNet-50 layers 1-2)."""
+    return planes in (64, 128)
+
+
+def bnrelu_conv1x1_bn_res_recompute(z: torch.Tensor, bn_a, stats_a, conv, bn_b,
+                                    res: torch.Tensor, res_link=None,
+                                    out_link=None) -> torch.Tensor:
+    """``bnrelu_conv1x1_bn_res`` without a stored z3 (see _RecomputeTailFn)."""
+    mean, invstd = stats_a
+    return _RecomputeTailFn.apply(z, bn_a.weight, bn_a.bias, mean, invstd, conv.weight,
+                                  bn_b.weight, bn_b.bias, res, bn_b.running_mean,
+                                  bn_b.running_var, bn_b.eps, bn_b.momentum, res_link, out_link)
+
+
 def res_tail_ok(planes: int) -> bool:
     """Channel counts the fused identity tail's kernels take (every ResNet-50 stage)."""
     return planes % 64 == 0 and planes * 4 <= 2048

@@ -553,6 +553,45 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
   return dw;
 }
 
+// wgrad1x1 with a general dy prologue (dmode: 0 none, 2 dz_a (mask ? dy : 0) + dz_c,
+// 3 max(dy dz_a + dz_b, 0)) and optional column sums of the staged dz -> {dw fp32 [Co, Ci], cs [Co]}.
+std::vector<Tensor> wgrad1x1_ex(const Tensor& dy_in, const Tensor& x, const optional<Tensor>& pro_sc,
+                                const optional<Tensor>& pro_bi, int64_t dmode,
+                                const optional<Tensor>& dz_mask, const optional<Tensor>& dz_a,
+                                const optional<Tensor>& dz_b, const optional<Tensor>& dz_c,
+                                bool colsum) {
+  check_nhwc(x, "x");
+  Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(0) == x.size(0) && dy.size(2) == x.size(2) &&
+                  dy.size(3) == x.size(3), "wgrad1x1_ex: dy / x shapes");
+  TORCH_CHECK(dmode == 0 || dmode == 2 || dmode == 3, "wgrad1x1_ex: dmode 0, 2 or 3");
+  const int64_t Co = dy.size(1), Ci = x.size(1), P = x.numel() / Ci;
+  const float* sc = opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", Ci);
+  const float* bi = opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", Ci);
+  TORCH_CHECK((sc == nullptr) == (bi == nullptr), "wgrad1x1_ex: pro_sc and pro_bi together");
+  const c10::DeviceGuard guard(x.device());
+  int S = 1, cps = 1;
+  cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps);
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor part = at::empty({S, Co, Ci}, f32);
+  Tensor dw = at::empty({Co, Ci}, f32);
+  Tensor cs, cs_part;
+  if (colsum) {
+    cs = at::empty({Co}, f32);
+    cs_part = at::empty({S, Co}, f32);
+  }
+  CML_CHECK_HIP(cml::launch_wgrad1x1_ex(
+      dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), dw.data_ptr(), false, P,
+      static_cast<int>(Co), static_cast<int>(Ci), sc, bi, cur_stream(), static_cast<int>(dmode),
+      nullptr, opt_ptr<const uint8_t>(dz_mask, at::kByte, "dz_mask", P * Co / 8),
+      opt_ptr<const float>(dz_a, at::kFloat, "dz_a", Co),
+      opt_ptr<const float>(dz_b, at::kFloat, "dz_b", Co),
+      opt_ptr<const float>(dz_c, at::kFloat, "dz_c", Co),
+      colsum ? cs_part.data_ptr<float>() : nullptr, colsum ? cs.data_ptr<float>() : nullptr));
+  return {dw, cs};
+}
+
 namespace {
 // [Cout, Cin] bf16 weight given for a backward GEMM (already transposed by the caller)
 void check_w2(const Tensor& w, int64_t K, const char* fn) {
@@ -695,6 +734,89 @@ std::vector<Tensor> conv1x1_bn_fwd(const Tensor& x, const Tensor& w, const optio
       stats ? opt_ptr<float>(rvar, at::kFloat, "running_var", Co) : nullptr,
       static_cast<float>(eps), static_cast<float>(momentum), cur_stream()));
   return {y, mean, invstd};
+}
+
+// Statistics-only pass of a stride-1 1x1 conv with the BN + ReLU prologue (the product is not
+// stored): {mean, invstd} of bf16(conv1x1(max(x sc + bi, 0))), running stats updated when given.
+std::vector<Tensor> conv1x1_bn_stats_only(const Tensor& x, const Tensor& w, const Tensor& pro_sc,
+                                          const Tensor& pro_bi, const optional<Tensor>& shift,
+                                          const optional<Tensor>& rmean,
+                                          const optional<Tensor>& rvar, double eps, double momentum) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4 && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 1 &&
+                  w.size(3) == 1 && w.size(1) == x.size(1) && w.is_contiguous(),
+              "conv1x1_bn_stats_only: x NHWC, w contiguous bf16 [Cout, Cin, 1, 1]");
+  const int64_t K = x.size(1), Co = w.size(0), M = x.numel() / K;
+  TORCH_CHECK(K % 64 == 0 && Co % 64 == 0, "conv1x1_bn_stats_only: channels multiples of 64");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({Co}, f32), invstd = at::empty({Co}, f32);
+  Tensor part = at::empty({static_cast<int64_t>(cml::conv1x1_bn_part_floats(
+                              M, static_cast<int>(K), static_cast<int>(Co), true))}, f32);
+  CML_CHECK_HIP(cml::launch_conv1x1_bn_fwd(
+      x.data_ptr(), w.data_ptr(), nullptr, part.data_ptr<float>(),
+      opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", K),
+      opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", K),
+      opt_ptr<const float>(shift, at::kFloat, "shift", Co), M, static_cast<int>(K),
+      static_cast<int>(Co), 1, 0, 0, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+      opt_ptr<float>(rmean, at::kFloat, "running_mean", Co),
+      opt_ptr<float>(rvar, at::kFloat, "running_var", Co), static_cast<float>(eps),
+      static_cast<float>(momentum), cur_stream()));
+  return {mean, invstd};
+}
+
+// y = max(bf16(conv1x1(max(x sc + bi, 0))) ep_sc + ep_bi + res, 0) and its ReLU bit mask
+// [M, Cout / 8] (uint8) -- the apply pass of a BN whose statistics came from
+// conv1x1_bn_stats_only, recomputing the product instead of reading it.
+std::vector<Tensor> conv1x1_bnres(const Tensor& x, const Tensor& w, const Tensor& pro_sc,
+                                  const Tensor& pro_bi, const Tensor& ep_sc, const Tensor& ep_bi,
+                                  const Tensor& res) {
+  check_nhwc(x, "x");
+  check_nhwc(res, "res");
+  TORCH_CHECK(x.dim() == 4 && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 1 &&
+                  w.size(3) == 1 && w.size(1) == x.size(1) && w.is_contiguous(),
+              "conv1x1_bnres: x NHWC, w contiguous bf16 [Cout, Cin, 1, 1]");
+  const int64_t N = x.size(0), K = x.size(1), H = x.size(2), W = x.size(3), Co = w.size(0);
+  const int64_t M = N * H * W;
+  TORCH_CHECK(res.dim() == 4 && res.size(0) == N && res.size(1) == Co && res.size(2) == H &&
+                  res.size(3) == W, "conv1x1_bnres: res shape");
+  TORCH_CHECK(K % 64 == 0 && Co % 64 == 0, "conv1x1_bnres: channels multiples of 64");
+  const c10::DeviceGuard guard(x.device());
+  Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor mask = at::empty({M, Co / 8}, x.options().dtype(at::kByte));
+  CML_CHECK_HIP(cml::launch_conv1x1_bnres(
+      x.data_ptr(), w.data_ptr(), y.data_ptr(), mask.data_ptr<uint8_t>(),
+      opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", K),
+      opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", K),
+      opt_ptr<const float>(ep_sc, at::kFloat, "ep_sc", Co),
+      opt_ptr<const float>(ep_bi, at::kFloat, "ep_bi", Co), res.data_ptr(), M,
+      static_cast<int>(K), static_cast<int>(Co), cur_stream()));
+  return {y, mask};
+}
+
+// y = [a (mask ? g : 0) + c | max(x2 sc + bi, 0)] w^T (two sources concatenated along K):
+// g [N, K1, H, W], mask [M, K1 / 8], x2 [N, K2, H, W] NHWC bf16; a_cat = [a | sc], c_cat = [c | bi]
+// fp32 [K1 + K2]; w [Cout, K1 + K2] contiguous bf16 -> y [N, Cout, H, W] NHWC.
+Tensor conv1x1_cat(const Tensor& g, const Tensor& mask, const Tensor& x2, const Tensor& a_cat,
+                   const Tensor& c_cat, const Tensor& w) {
+  check_nhwc(g, "g");
+  check_nhwc(x2, "x2");
+  const int64_t N = g.size(0), K1 = g.size(1), H = g.size(2), W = g.size(3), K2 = x2.size(1);
+  const int64_t M = N * H * W, K = K1 + K2;
+  TORCH_CHECK(x2.dim() == 4 && x2.size(0) == N && x2.size(2) == H && x2.size(3) == W,
+              "conv1x1_cat: x2 shape");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.size(1) == K &&
+                  w.is_contiguous() && w.size(0) % 64 == 0 && K1 % 64 == 0 && K2 % 64 == 0,
+              "conv1x1_cat: w contiguous bf16 [Cout, K1 + K2], channels multiples of 64");
+  const int64_t Co = w.size(0);
+  const c10::DeviceGuard guard(g.device());
+  Tensor y = at::empty({N, Co, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  CML_CHECK_HIP(cml::launch_conv1x1_cat(
+      g.data_ptr(), opt_ptr<const uint8_t>(mask, at::kByte, "mask", M * K1 / 8), x2.data_ptr(),
+      opt_ptr<const float>(a_cat, at::kFloat, "a_cat", K),
+      opt_ptr<const float>(c_cat, at::kFloat, "c_cat", K), w.data_ptr(), y.data_ptr(), M,
+      static_cast<int>(K1), static_cast<int>(K), static_cast<int>(Co), cur_stream()));
+  return y;
 }
 
 // 3x3 / stride 1 / padding 1 conv as an implicit GEMM on the fused 1x1 kernel (conv1x1.hip TAP):
@@ -1322,6 +1444,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "weight gradient of a 3x3 stride-1 conv (MFMA, split-K, one tap per grid z)");
   m.def("conv_gemm", &conv_gemm, py::arg("x"), py::arg("w"), py::arg("taps"),
         py::arg("zero") = py::none(), "implicit-GEMM NHWC conv (1x1 / 3x3 stride 1), glds staging");
+  m.def("conv1x1_bn_stats_only", &conv1x1_bn_stats_only, py::arg("x"), py::arg("w"),
+        py::arg("pro_sc"), py::arg("pro_bi"), py::arg("shift") = py::none(),
+        py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
+        py::arg("eps") = 1e-5, py::arg("momentum") = 0.1,
+        "BN statistics of conv1x1(bnrelu(x)) without storing the product");
+  m.def("conv1x1_bnres", &conv1x1_bnres, "recomputed conv1x1 + BN apply + residual + ReLU -> {y, mask}");
+  m.def("conv1x1_cat", &conv1x1_cat, "two-source (masked affine | BN-ReLU) 1x1 conv along K");
+  m.def("wgrad1x1_ex", &wgrad1x1_ex, py::arg("dy"), py::arg("x"), py::arg("pro_sc") = py::none(),
+        py::arg("pro_bi") = py::none(), py::arg("dmode") = 0, py::arg("dz_mask") = py::none(),
+        py::arg("dz_a") = py::none(), py::arg("dz_b") = py::none(), py::arg("dz_c") = py::none(),
+        py::arg("colsum") = false, "1x1 weight gradient with dy prologue modes and column sums");
   m.def("conv_gemm_bn", &conv_gemm_bn, py::arg("x"), py::arg("w"), py::arg("taps"),
         py::arg("zero") = py::none(), py::arg("shift") = py::none(),
         py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),

@@ -53,8 +53,8 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
 __device__ __forceinline__ int swz(int row, int c) { return row * 128 + 16 * (c ^ ((row >> 1) & 7)); }
 
 // Prologue modes (f applied to x while staging) and statistics modes (epilogue sums).
-enum { PM_NONE = 0, PM_BNRELU = 1, PM_BNBWD = 2 };
-enum { SM_BN = 0, SM_BNBWD = 1, SM_OFF = 2 };
+enum { PM_NONE = 0, PM_BNRELU = 1, PM_BNBWD = 2, PM_CAT = 3 };
+enum { SM_BN = 0, SM_BNBWD = 1, SM_OFF = 2, SM_BNRES = 3 };
 
 struct C1Args {
   const uint16_t* x;      // [rows_in][K]
@@ -71,6 +71,10 @@ struct C1Args {
   const uint16_t* sz;     // SM_BNBWD: z of the BN whose backward sums are taken [M][N]
   const uint8_t* sm;      // SM_BNBWD: its ReLU bit mask [M][N / 8]
   const float* shift;     // [N] or null (SM_BN: statistics shift; SM_BNBWD: the BN's mean)
+  const float* ep_sc;     // SM_BNRES: y = max(v ep_sc + ep_bi + link, 0) per output channel [N]
+  const float* ep_bi;
+  uint8_t* ymask;         // SM_BNRES: bit mask of y > 0 [M][N / 8]
+  int K1;                 // PM_CAT: channels of the first source (x, with mask xm); x2 has K - K1
   int M, K, N;
   int ntn, wgpn, mtiles;
   int H, W, OW, OHW;      // S2: input H, W; output W and H*W.  TAP: H, W (in = out) and OHW = H W
@@ -130,6 +134,22 @@ __device__ __forceinline__ void load_x(const C1Args& a, uint4 (&pb)[CB], uint4 (
     }
     return;
   }
+  if constexpr (PM == PM_CAT) {
+    const int k0 = ks * kBK;
+    const bool first = k0 < a.K1;
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      const int64_t r = src_row(a, t * BM + srow + 32 * j, false);
+      if (first) {
+        pb[j] = *reinterpret_cast<const uint4*>(a.x + r * a.K1 + k0 + 8 * ch);
+        pm[j] = a.xm[r * (a.K1 / 8) + k0 / 8 + ch];
+      } else {
+        pb[j] = *reinterpret_cast<const uint4*>(a.x2 + r * (a.K - a.K1) + (k0 - a.K1) + 8 * ch);
+        pm[j] = 0u;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < CB; ++j) {
     const int64_t r = src_row(a, t * BM + srow + 32 * j, S2);
@@ -154,10 +174,14 @@ __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
 //              c = -gamma invstd s / M - b mean, with s, q the BN's backward sums)
 // kofs: first input channel of this k-step (ks * 64, or the tap's channel chunk); KA: entries per
 // coefficient row of s_aff; TAP: rows with a clear bit in vm are zeroed (padding).
+//   PM_CAT     a (mask ? x : 0) + c  for k < K1 (x = a BN + ReLU output gradient, no z term),
+//              max(x2 sc + bi, 0)   for k >= K1 (a BN + ReLU output, recomputed): one GEMM over two
+//              sources concatenated along K
 template <int CB, int PM, bool TAP = false>
 __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)[CB],
                                         const uint32_t (&pm)[CB], char* sx, const float* s_aff,
-                                        int KA, int kofs, int srow, int ch, uint32_t vm = ~0u) {
+                                        int KA, int kofs, int srow, int ch, uint32_t vm = ~0u,
+                                        int K1 = 0) {
   float sc[8], bi[8], cc[8];
   if constexpr (PM != PM_NONE) {
     ld8f(s_aff + kofs + 8 * ch, sc);
@@ -188,6 +212,27 @@ __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)
         const float hi = fmaf(sc[2 * i + 1], ghi,
                               fmaf(bi[2 * i + 1], __uint_as_float(z4[i] & 0xffff0000u), cc[2 * i + 1]));
         w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+      }
+      v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    } else if constexpr (PM == PM_CAT) {
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t bits = pm[j];
+      if (kofs < K1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float glo = ((bits >> (2 * i)) & 1u) ? __uint_as_float(w4[i] << 16) : 0.f;
+          const float ghi = ((bits >> (2 * i + 1)) & 1u) ? __uint_as_float(w4[i] & 0xffff0000u) : 0.f;
+          const float lo = fmaf(sc[2 * i], glo, bi[2 * i]);
+          const float hi = fmaf(sc[2 * i + 1], ghi, bi[2 * i + 1]);
+          w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float lo = fmaxf(fmaf(__uint_as_float(w4[i] << 16), sc[2 * i], bi[2 * i]), 0.f);
+          const float hi = fmaxf(fmaf(__uint_as_float(w4[i] & 0xffff0000u), sc[2 * i + 1], bi[2 * i + 1]), 0.f);
+          w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+        }
       }
       v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
@@ -222,16 +267,23 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
   // (a 1-2 k-step GEMM was otherwise bound by these dependent loads, one latency per row pair):
   // all 8 rows at once with one operand (EL), in batches of 4 with two, halved again at MT = 2
   // (more registers would spill). Rows past M re-read row m0.
-  constexpr bool LD = EL || SM == SM_BNBWD;
+  constexpr bool LD = EL || SM == SM_BNBWD || SM == SM_BNRES;
   constexpr int RB = ((EL && SM == SM_BNBWD) ? 4 : 8) / MT;   // rows per batch
   uint4 lv[RB], zv[RB];
   uint32_t lbv[RB], zbv[RB];
   if constexpr (!(EL && SM == SM_BNBWD)) {   // one operand: keep the row body's arguments defined
 #pragma unroll
     for (int k = 0; k < RB; ++k) {
-      if constexpr (!EL) { lv[k] = make_uint4(0u, 0u, 0u, 0u); lbv[k] = 0u; }
+      if constexpr (!EL) lbv[k] = 0u;
+      if constexpr (!EL && SM != SM_BNRES) lv[k] = make_uint4(0u, 0u, 0u, 0u);
       if constexpr (SM != SM_BNBWD) { zv[k] = make_uint4(0u, 0u, 0u, 0u); zbv[k] = 0u; }
     }
+  }
+  // SM_BNRES: the lane's 8 output channels' BN coefficients
+  float esc[8], ebi[8];
+  if constexpr (SM == SM_BNRES) {
+    ld8f(a.ep_sc + n0 + ncol0 + 8 * c, esc);
+    ld8f(a.ep_bi + n0 + ncol0 + 8 * c, ebi);
   }
   auto issue = [&](int k0) {
 #pragma unroll
@@ -243,6 +295,7 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
         lv[k] = *reinterpret_cast<const uint4*>(a.link + e0);
         lbv[k] = a.lm[e0 >> 3];
       }
+      if constexpr (SM == SM_BNRES) lv[k] = *reinterpret_cast<const uint4*>(a.link + e0);
       if constexpr (SM == SM_BNBWD) {
         zv[k] = *reinterpret_cast<const uint4*>(a.sz + e0);
         zbv[k] = a.sm[e0 >> 3];
@@ -287,7 +340,26 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
       }
       v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
-    *reinterpret_cast<uint4*>(a.y + e0) = v;
+    if constexpr (SM == SM_BNRES) {   // y = max(bn(v) + res, 0) and its bit mask; no statistics
+      const uint32_t r4[4] = {l.x, l.y, l.z, l.w};
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      uint32_t bits = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float lo = fmaf(__uint_as_float(w4[q] << 16), esc[2 * q], ebi[2 * q]) +
+                         __uint_as_float(r4[q] << 16);
+        const float hi = fmaf(__uint_as_float(w4[q] & 0xffff0000u), esc[2 * q + 1], ebi[2 * q + 1]) +
+                         __uint_as_float(r4[q] & 0xffff0000u);
+        bits |= (lo > 0.f ? 1u : 0u) << (2 * q);
+        bits |= (hi > 0.f ? 1u : 0u) << (2 * q + 1);
+        w4[q] = static_cast<uint32_t>(f2bf(fmaxf(lo, 0.f))) |
+                (static_cast<uint32_t>(f2bf(fmaxf(hi, 0.f))) << 16);
+      }
+      *reinterpret_cast<uint4*>(a.y + e0) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      a.ymask[e0 >> 3] = static_cast<uint8_t>(bits);
+      return;
+    }
+    if (SM != SM_BN || a.y) *reinterpret_cast<uint4*>(a.y + e0) = v;   // SM_BN, y null: stats only
     const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
     if constexpr (SM == SM_BN) {
 #pragma unroll
@@ -342,7 +414,7 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
 template <int WN, int WM, int PM, bool WRES, bool S2, bool EL, int SM, int MT = 1,
           bool TAP = false>
 __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
-  constexpr int NAFF = PM == PM_BNBWD ? 3 : (PM == PM_BNRELU ? 2 : 0);
+  constexpr int NAFF = PM == PM_BNBWD ? 3 : ((PM == PM_BNRELU || PM == PM_CAT) ? 2 : 0);
   const int KA = TAP ? a.C : a.K;                               // prologue coefficients per row
   constexpr int BN = 64 * WN, BM = 64 * WM * MT;
   constexpr int CA = BN / 32, CB = BM / 32;     // 16-B staging chunks per thread and step
@@ -408,7 +480,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       ss[q] = 0.f;
       sq[q] = 0.f;
     }
-    store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, 0, srow, ch, vm);
+    store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, 0, srow, ch, vm, a.K1);
     if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, 0);
     __syncthreads();
     for (;;) {
@@ -450,7 +522,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       }
       if (!more) break;
       __syncthreads();               // every wave is done reading this step's LDS
-      store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, kofs(ksn), srow, ch, vm);
+      store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, kofs(ksn), srow, ch, vm, a.K1);
       if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, ksn);
       __syncthreads();
       t = tn;
@@ -735,6 +807,22 @@ hipError_t launch_bwd(const C1Args& a, const Plan& p, int mode, hipStream_t st) 
   return launch_bwd_w<1, 4>(a, p, mode, st);
 }
 
+// recompute tail (fused BN + residual + ReLU epilogue) and two-source (PM_CAT) data gradient
+template <int WN, int WM>
+hipError_t launch_tail_w(const C1Args& a, const Plan& p, bool cat, hipStream_t st) {
+  if (cat)
+    return p.wres ? launch_t<WN, WM, PM_CAT, true, false, false, SM_OFF>(a, p, st)
+                  : launch_t<WN, WM, PM_CAT, false, false, false, SM_OFF>(a, p, st);
+  return p.wres ? launch_t<WN, WM, PM_BNRELU, true, false, false, SM_BNRES>(a, p, st)
+                : launch_t<WN, WM, PM_BNRELU, false, false, false, SM_BNRES>(a, p, st);
+}
+
+hipError_t launch_tail(const C1Args& a, const Plan& p, bool cat, hipStream_t st) {
+  if (p.WN == 4) return launch_tail_w<4, 1>(a, p, cat, st);
+  if (p.WN == 2) return launch_tail_w<2, 2>(a, p, cat, st);
+  return launch_tail_w<1, 4>(a, p, cat, st);
+}
+
 C1Args base_args(const void* x, const void* w, void* y, int64_t M, int K, int N, const Plan& p) {
   C1Args a{};
   a.x = reinterpret_cast<const uint16_t*>(x);
@@ -871,6 +959,38 @@ hipError_t launch_bn_bwd_coeffs(const float* sdz, const float* sdzx, const void*
       1.0f / static_cast<float>(M), ca, cb, cc, reinterpret_cast<uint16_t*>(dgamma),
       reinterpret_cast<uint16_t*>(dbeta));
   return hipGetLastError();
+}
+
+hipError_t launch_conv1x1_bnres(const void* x, const void* w, void* y, uint8_t* ymask,
+                                const float* pro_sc, const float* pro_bi, const float* ep_sc,
+                                const float* ep_bi, const void* res, int64_t M, int K, int N,
+                                hipStream_t st) {
+  if (bad_shape(M, K, N) || !pro_sc || !pro_bi || !ep_sc || !ep_bi || !res || !ymask)
+    return hipErrorInvalidValue;
+  const Plan p = make_plan(M, K, N, 2);   // the plan of the statistics pass (same z rounding)
+  C1Args a = base_args(x, w, y, M, K, N, p);
+  a.pro_sc = pro_sc;
+  a.pro_bi = pro_bi;
+  a.ep_sc = ep_sc;
+  a.ep_bi = ep_bi;
+  a.link = reinterpret_cast<const uint16_t*>(res);
+  a.ymask = ymask;
+  return launch_tail(a, p, false, st);
+}
+
+hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2, const float* a_cat,
+                              const float* c_cat, const void* w, void* y, int64_t M, int K1, int K,
+                              int N, hipStream_t st) {
+  if (bad_shape(M, K, N) || K1 % kBK || K1 <= 0 || K1 >= K || !mask || !a_cat || !c_cat)
+    return hipErrorInvalidValue;
+  const Plan p = make_plan(M, K, N, 2);
+  C1Args a = base_args(g, w, y, M, K, N, p);
+  a.xm = mask;
+  a.x2 = reinterpret_cast<const uint16_t*>(x2);
+  a.pro_sc = a_cat;
+  a.pro_bi = c_cat;
+  a.K1 = K1;
+  return launch_tail(a, p, true, st);
 }
 
 hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* part,

@@ -243,6 +243,14 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
 void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps);
 // dz_z / dz_mask / dz_a / dz_b / dz_c (all or none): dy is the output gradient of a BN + ReLU that
 // consumed the conv output z = dz_z; the staging uses dz = a (mask ? dy : 0) + b z + c instead.
+// General form: dmode 0 none, 1 the dz_* BN-backward prologue above, 2 dz = dz_a (mask ? dy : 0)
+// + dz_c (no z), 3 dz = max(dy dz_a + dz_b, 0); Co = Ci = 64 also allowed. cs_part (splits x Co
+// floats) / cs: column sums of the staged dz over the pixels -> cs [Co] (fp32).
+hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
+                              int64_t P, int Co, int Ci, const float* pro_sc, const float* pro_bi,
+                              hipStream_t st, int dmode, const void* dz_z, const uint8_t* dz_mask,
+                              const float* dz_a, const float* dz_b, const float* dz_c,
+                              float* cs_part, float* cs);
 hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
                            int64_t P, int Co, int Ci, const float* pro_sc, const float* pro_bi,
                            hipStream_t stream, const void* dz_z = nullptr,
@@ -309,6 +317,20 @@ hipError_t launch_bn_stats_finalize(const float* part, int R, int BN, int N, int
 //          sz non-null also the backward sums of the BN + ReLU that consumes y: sdz = sum m y,
 //          sdzx = sum m y (sz - mean) invstd (m = sm's bit). part: conv1x1_link_part_floats.
 size_t conv1x1_link_part_floats(int64_t M, int K, int N);
+
+// Identity-block tail without a stored z3 (ops.conv._RecomputeTailFn):
+// y = max(conv1x1(max(x sc + bi, 0)) ep_sc + ep_bi + res, 0) with its ReLU bit mask ymask
+// [M][N / 8]; the product is rounded to bf16 exactly as conv1x1_bn_fwd's statistics pass (same
+// plan) rounded it, so the statistics describe the values normalised here.
+hipError_t launch_conv1x1_bnres(const void* x, const void* w, void* y, uint8_t* ymask,
+                                const float* pro_sc, const float* pro_bi, const float* ep_sc,
+                                const float* ep_bi, const void* res, int64_t M, int K, int N,
+                                hipStream_t st);
+// y = [a (mask ? g : 0) + c | max(x2 sc + bi, 0)] W^T: K = K1 + K2 channels from two sources
+// (g, mask: [M][K1]; x2: [M][K2]); a_cat = [a | sc], c_cat = [c | bi] (fp32 [K]); w [N][K].
+hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2, const float* a_cat,
+                              const float* c_cat, const void* w, void* y, int64_t M, int K1, int K,
+                              int N, hipStream_t st);
 hipError_t launch_conv1x1_bnbwd(const void* g, const void* z, const uint8_t* mask, const float* ca,
                                 const float* cb, const float* cc, const void* w, void* y,
                                 int64_t M, int K, int N, hipStream_t st);

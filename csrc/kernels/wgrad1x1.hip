@@ -57,12 +57,19 @@ __device__ __forceinline__ int img_off(int row, int ch) {
 // DPRO: dy is the output gradient g of a BN + ReLU that consumed the conv's output z; the staging
 // forms the conv's output gradient dz = da (mask ? g : 0) + db z + dc per output channel
 // (conv1x1.hip's PM_BNBWD), so dz is never materialised either.
+//   DP_MASK   dz = da (mask ? g : 0) + dc   (no z term: the tail recompute path supplies it
+//             algebraically, ops.conv._RecomputeTailFn)
+//   DP_BNRELU dz = max(g da + db, 0)        (dy is itself the input of a BN + ReLU: Gram matrices
+//             of a BN-ReLU output that is never stored)
+// CS (runtime, cs_part non-null, non-TAP): per-split column sums of the staged dz over the pixels
+// (bf16 values as multiplied), taken by the workgroups of the first ci tile.
+enum { DP_NONE = 0, DP_FULL = 1, DP_MASK = 2, DP_BNRELU = 3 };
 struct DPro {
-  const uint16_t* z;      // [P][Co]
-  const uint8_t* mask;    // [P][Co / 8]
+  const uint16_t* z;      // [P][Co]   (DP_FULL)
+  const uint8_t* mask;    // [P][Co / 8] (DP_FULL, DP_MASK)
   const float* a;         // [Co]
-  const float* b;
-  const float* c;
+  const float* b;         //           (DP_FULL, DP_BNRELU)
+  const float* c;         //           (DP_FULL, DP_MASK)
 };
 
 // TAP: weight gradient of a 3x3 / stride 1 / padding 1 conv, one tap per blockIdx.z: x rows are
@@ -72,11 +79,11 @@ struct TapGeo {
   int H, W, HW;
 };
 
-template <int TM, int TN, int KC, bool PRO, bool DPRO, bool TAP = false>
+template <int TM, int TN, int KC, bool PRO, int DPRO, bool TAP = false>
 __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, float* __restrict__ part,
     int P, int Co, int Ci, int tiles_n, int cps, const float* __restrict__ pro_sc,
-    const float* __restrict__ pro_bi, DPro dp, TapGeo tg) {
+    const float* __restrict__ pro_bi, DPro dp, TapGeo tg, float* __restrict__ cs_part) {
   const int tap = TAP ? static_cast<int>(blockIdx.z) : 0;
   const int tdy = TAP ? tap / 3 - 1 : 0, tdx = TAP ? tap - 3 * (tap / 3) - 1 : 0;
   constexpr int kKC = KC;                              // pixels per chunk
@@ -107,17 +114,34 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
   }
   // likewise every staged dy item covers the same 8 output channels (NT is a multiple of CA)
   float da[8], db[8], dc[8];
-  if constexpr (DPRO) {
+  if constexpr (DPRO != DP_NONE) {
     const int cb = co0 + 8 * (tid % CA);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       da[q] = dp.a[cb + q];
-      db[q] = dp.b[cb + q];
-      dc[q] = dp.c[cb + q];
+      db[q] = DPRO == DP_MASK ? 0.f : dp.b[cb + q];
+      dc[q] = DPRO == DP_BNRELU ? 0.f : dp.c[cb + q];
     }
   }
   auto dpro = [&](uint4 v, uint4 zv, uint32_t bits) {
-    if constexpr (DPRO) {
+    if constexpr (DPRO == DP_MASK || DPRO == DP_BNRELU) {
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float lo, hi;
+        if constexpr (DPRO == DP_MASK) {
+          const float glo = ((bits >> (2 * i)) & 1u) ? __uint_as_float(w4[i] << 16) : 0.f;
+          const float ghi = ((bits >> (2 * i + 1)) & 1u) ? __uint_as_float(w4[i] & 0xffff0000u) : 0.f;
+          lo = fmaf(da[2 * i], glo, dc[2 * i]);
+          hi = fmaf(da[2 * i + 1], ghi, dc[2 * i + 1]);
+        } else {
+          lo = fmaxf(fmaf(__uint_as_float(w4[i] << 16), da[2 * i], db[2 * i]), 0.f);
+          hi = fmaxf(fmaf(__uint_as_float(w4[i] & 0xffff0000u), da[2 * i + 1], db[2 * i + 1]), 0.f);
+        }
+        w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+      }
+      return make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    } else if constexpr (DPRO == DP_FULL) {
       uint32_t w4[4] = {v.x, v.y, v.z, v.w};
       const uint32_t z4[4] = {zv.x, zv.y, zv.z, zv.w};
 #pragma unroll
@@ -149,8 +173,11 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
   // prefetch registers; loads are unconditional (clamped pixel, zeroed at use) and selects are
   // component-wise: a branch around the loads makes hipcc wait at the join, and a select of
   // whole uint4 values became a select of addresses that put these registers in scratch
-  uint4 av[IA], bv[IB], zv[DPRO ? IA : 1];
-  uint32_t mv[DPRO ? IA : 1];
+  constexpr bool HZ = DPRO == DP_FULL, HM = DPRO == DP_FULL || DPRO == DP_MASK;
+  uint4 av[IA], bv[IB], zv[HZ ? IA : 1];
+  uint32_t mv[HM ? IA : 1];
+  if constexpr (!HZ) zv[0] = make_uint4(0u, 0u, 0u, 0u);
+  if constexpr (!HM) mv[0] = 0u;
   uint32_t xok = ~0u;                                  // TAP: bit j = x item j inside the image
   auto fetch = [&](int c) {
 #pragma unroll
@@ -158,10 +185,9 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
       const int e = tid + NT * j, row = e / CA, ch = e % CA;
       const int p = min(c * kKC + row, P - 1);
       av[j] = *reinterpret_cast<const uint4*>(dy + static_cast<int64_t>(p) * Co + co0 + 8 * ch);
-      if constexpr (DPRO) {
+      if constexpr (HZ)
         zv[j] = *reinterpret_cast<const uint4*>(dp.z + static_cast<int64_t>(p) * Co + co0 + 8 * ch);
-        mv[j] = dp.mask[static_cast<int64_t>(p) * (Co / 8) + co0 / 8 + ch];
-      }
+      if constexpr (HM) mv[j] = dp.mask[static_cast<int64_t>(p) * (Co / 8) + co0 / 8 + ch];
     }
     if constexpr (TAP) xok = 0;
 #pragma unroll
@@ -184,6 +210,12 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
   // two LDS stages: chunk c is multiplied out of stage c & 1 while chunk c + 1 is written into the
   // other stage from registers and chunk c + 2 is in flight -> one barrier per chunk
   constexpr int STG = kKC * (TM + TN) * 2;
+  // (not in the 1024-thread tile: its 128 registers have no room for the sums)
+  constexpr bool CSOK = !TAP && NT <= 512;
+  const bool csum = CSOK && cs_part != nullptr && tn == 0;   // uniform per workgroup
+  float cs[CSOK ? 8 : 1];
+#pragma unroll
+  for (int q = 0; q < (CSOK ? 8 : 1); ++q) cs[q] = 0.f;
   auto stage = [&](int c, int sb) {
     char* ab = smem + sb * STG;
     char* bb = ab + kKC * TM * 2;
@@ -191,8 +223,17 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     for (int j = 0; j < IA; ++j) {
       const int e = tid + NT * j, row = e / CA, ch = e % CA;
       uint4 v = av[j];
-      if constexpr (DPRO) v = dpro(v, zv[j], mv[j]);
-      *reinterpret_cast<uint4*>(ab + img_off<TM * 2>(row, ch)) = keep_if(c * kKC + row < P, v);
+      if constexpr (DPRO != DP_NONE) v = dpro(v, zv[HZ ? j : 0], mv[HM ? j : 0]);
+      v = keep_if(c * kKC + row < P, v);
+      *reinterpret_cast<uint4*>(ab + img_off<TM * 2>(row, ch)) = v;
+      if constexpr (CSOK) if (csum) {
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          cs[2 * i] += __uint_as_float(w4[i] << 16);
+          cs[2 * i + 1] += __uint_as_float(w4[i] & 0xffff0000u);
+        }
+      }
     }
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
@@ -234,6 +275,20 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     }
     fetch(c + 2 < c_hi ? c + 2 : c);                   // past the end: reload a valid chunk
     __syncthreads();
+  }
+  if constexpr (CSOK) if (csum) {   // fold the threads of each 8-channel group (tid % CA)
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[tid * 8 + q] = cs[q];
+    __syncthreads();
+    if (tid < CA) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float v = 0.f;
+        for (int k = tid; k < NT; k += CA) v += red[k * 8 + q];
+        cs_part[static_cast<int64_t>(blockIdx.y) * Co + co0 + 8 * tid + q] = v;
+      }
+    }
   }
   // partial [split][Co][Ci]: lane r = ci column, register k = co row (k&3) + 8 (k>>2) + 4 h
   float* pw = part + (static_cast<int64_t>(blockIdx.y) * (TAP ? 9 : 1) + tap) * Co * Ci;
@@ -297,6 +352,11 @@ namespace {
 // (memory-bound shapes, Co * Ci <= 128K); shapes with more MACs per byte take 128 x 128 tiles
 // for more workgroups (tools/diag/wgrad1x1_bench.py)
 void pick_tile(int Co, int Ci, int* TM, int* TN) {
+  if (Co == 64 && Ci == 64) {   // Gram matrix of a 64-channel activation: one wave per tile
+    *TM = 64;
+    *TN = 64;
+    return;
+  }
   if (static_cast<int64_t>(Co) * Ci >= 256 * 1024) {
     *TM = 128;
     *TN = 128;
@@ -308,31 +368,34 @@ void pick_tile(int Co, int Ci, int* TM, int* TN) {
 }
 }  // namespace
 
-template <int TM, int TN, bool PRO, bool DPRO, bool TAP = false>
+template <int TM, int TN, bool PRO, int DPRO, bool TAP = false>
 void launch_one(dim3 grid, size_t lds, hipStream_t st, const uint16_t* dyp, const uint16_t* xp,
                 float* part, int P, int Co, int Ci, int tiles_n, int cps, const float* sc,
-                const float* bi, const DPro& dp, const TapGeo& tg = TapGeo{1, 1, 1}) {
+                const float* bi, const DPro& dp, const TapGeo& tg = TapGeo{1, 1, 1},
+                float* cs_part = nullptr) {
   auto k = &wgrad1x1_kernel<TM, TN, 64, PRO, DPRO, TAP>;
   if (lds > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
   k<<<grid, (TM / 64) * (TN / 64) * 64, lds, st>>>(dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi,
-                                                    dp, tg);
+                                                    dp, tg, cs_part);
 }
 
-template <bool PRO, bool DPRO>
+template <bool PRO, int DPRO>
 bool launch_tile(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, const uint16_t* dyp,
                  const uint16_t* xp, float* part, int P, int Co, int Ci, int tiles_n, int cps,
-                 const float* sc, const float* bi, const DPro& dp) {
+                 const float* sc, const float* bi, const DPro& dp, float* cs_part) {
+  const TapGeo tg{1, 1, 1};
   // (no prologue variant of the 1024-thread 256 x 256 tile: it spills, and no ResNet shape needs
   // it)
   if (TM == 256 && TN == 256) {
-    if constexpr (PRO || DPRO) return false;
-    else launch_one<256, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
-  } else if (TM == 256 && TN == 128) launch_one<256, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
-  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
-  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
-  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp);
+    if constexpr (PRO || DPRO != DP_NONE) return false;
+    else launch_one<256, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
+  } else if (TM == 256 && TN == 128) launch_one<256, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
+  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
+  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
+  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
+  else if (TM == 64 && TN == 64) launch_one<64, 64, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
   else return false;
   return true;
 }
@@ -342,11 +405,11 @@ bool launch_tile_tap(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, cons
                      const uint16_t* xp, float* part, int P, int Co, int Ci, int tiles_n, int cps,
                      const float* sc, const float* bi, const TapGeo& tg) {
   const DPro dp{};
-  if (TM == 256 && TN == 128) launch_one<256, 128, PRO, false, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
-  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO, false, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
-  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO, false, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
-  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO, false, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
-  else if (TM == 64 && TN == 64) launch_one<64, 64, PRO, false, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
+  if (TM == 256 && TN == 128) launch_one<256, 128, PRO, DP_NONE, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
+  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO, DP_NONE, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
+  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO, DP_NONE, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
+  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO, DP_NONE, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
+  else if (TM == 64 && TN == 64) launch_one<64, 64, PRO, DP_NONE, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
   else return false;
   return true;
 }
@@ -374,10 +437,29 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
                            int64_t P, int Co, int Ci, const float* pro_sc, const float* pro_bi,
                            hipStream_t st, const void* dz_z, const uint8_t* dz_mask,
                            const float* dz_a, const float* dz_b, const float* dz_c) {
-  const bool dpro = dz_z != nullptr;
-  if (dpro && (!dz_mask || !dz_a || !dz_b || !dz_c)) return hipErrorInvalidValue;
+  return launch_wgrad1x1_ex(dy, x, part, dw, dw_bf16, P, Co, Ci, pro_sc, pro_bi, st,
+                            dz_z ? DP_FULL : DP_NONE, dz_z, dz_mask, dz_a, dz_b, dz_c, nullptr,
+                            nullptr);
+}
+
+hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
+                              int64_t P, int Co, int Ci, const float* pro_sc, const float* pro_bi,
+                              hipStream_t st, int dmode, const void* dz_z, const uint8_t* dz_mask,
+                              const float* dz_a, const float* dz_b, const float* dz_c,
+                              float* cs_part, float* cs) {
+  if (dmode == DP_FULL && (!dz_z || !dz_mask || !dz_a || !dz_b || !dz_c)) return hipErrorInvalidValue;
+  if (dmode == DP_MASK && (!dz_mask || !dz_a || !dz_c)) return hipErrorInvalidValue;
+  if (dmode == DP_BNRELU && (!dz_a || !dz_b)) return hipErrorInvalidValue;
+  if (dmode < DP_NONE || dmode > DP_BNRELU || ((cs_part == nullptr) != (cs == nullptr)))
+    return hipErrorInvalidValue;
+  {
+    int tm, tn;
+    pick_tile(Co, Ci, &tm, &tn);
+    if (cs && tm * tn > 32768) return hipErrorInvalidValue;   // no column sums in that tile
+  }
   DPro dp{reinterpret_cast<const uint16_t*>(dz_z), dz_mask, dz_a, dz_b, dz_c};
-  if (Ci == 64 ? Co % 256 != 0 : (Co % 128 || Ci % 128)) return hipErrorInvalidValue;
+  if (!(Co == 64 && Ci == 64) && (Ci == 64 ? Co % 256 != 0 : (Co % 128 || Ci % 128)))
+    return hipErrorInvalidValue;
   if (P < 1 || P >= (1ll << 31)) return hipErrorInvalidValue;
   if ((pro_sc == nullptr) != (pro_bi == nullptr)) return hipErrorInvalidValue;
   int S, cps, TM, TN;
@@ -391,15 +473,31 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
   const size_t lds = 2 * static_cast<size_t>(KC) * (TM + TN) * 2;   // two stages
   const int Pi = static_cast<int>(P);
   bool ok;
-  if (pro_sc && dpro)
-    ok = launch_tile<true, true>(TM, TN, grid, lds, st, dyp, xp, part, Pi, Co, Ci, tiles_n, cps, pro_sc, pro_bi, dp);
-  else if (pro_sc)
-    ok = launch_tile<true, false>(TM, TN, grid, lds, st, dyp, xp, part, Pi, Co, Ci, tiles_n, cps, pro_sc, pro_bi, dp);
-  else if (dpro)
-    ok = launch_tile<false, true>(TM, TN, grid, lds, st, dyp, xp, part, Pi, Co, Ci, tiles_n, cps, nullptr, nullptr, dp);
-  else
-    ok = launch_tile<false, false>(TM, TN, grid, lds, st, dyp, xp, part, Pi, Co, Ci, tiles_n, cps, nullptr, nullptr, dp);
+  const float* sc = pro_sc;
+  const float* bi = pro_bi;
+#define CML_WG_TILE(P_, D_) \
+  launch_tile<P_, D_>(TM, TN, grid, lds, st, dyp, xp, part, Pi, Co, Ci, tiles_n, cps, sc, bi, dp, cs_part)
+  if (pro_sc) {
+    switch (dmode) {
+      case DP_FULL: ok = CML_WG_TILE(true, DP_FULL); break;
+      case DP_MASK: ok = CML_WG_TILE(true, DP_MASK); break;
+      case DP_BNRELU: ok = CML_WG_TILE(true, DP_BNRELU); break;
+      default: ok = CML_WG_TILE(true, DP_NONE);
+    }
+  } else {
+    switch (dmode) {
+      case DP_FULL: ok = CML_WG_TILE(false, DP_FULL); break;
+      case DP_MASK: ok = CML_WG_TILE(false, DP_MASK); break;
+      case DP_BNRELU: ok = CML_WG_TILE(false, DP_BNRELU); break;
+      default: ok = CML_WG_TILE(false, DP_NONE);
+    }
+  }
+#undef CML_WG_TILE
   if (!ok) return hipErrorInvalidValue;
+  if (cs) {
+    const int cb = (Co / 4 + 255) / 256;
+    wgrad1x1_fold_kernel<false><<<cb, 256, 0, st>>>(cs_part, S, Co, cs);
+  }
   const int64_t n = static_cast<int64_t>(Co) * Ci;
   const int fb = static_cast<int>((n / 4 + 255) / 256);
   if (dw_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, dw);

@@ -172,3 +172,113 @@ def test_identity_chain_fused_vs_unfused(cuda, planes, H):
     for a, b, r in zip(outs["on"][2], outs["off"][2], ref[2]):
         e_on, e_off = _err(a, r), _err(b, r)
         assert e_on <= 1.5 * e_off + 2e-2, (e_on, e_off)
+
+
+# ---- recompute tail (ops.conv._RecomputeTailFn): kernels and the whole chain ----
+
+@pytest.mark.parametrize("N,K,H", [(2, 64, 28), (3, 128, 14), (2, 128, 9)])
+def test_stats_only_and_bnres_match_stored_path(cuda, N, K, H):
+    """The statistics-only pass gives conv1x1_bn_fwd's statistics bit for bit, and the recompute
+    apply gives bn_fwd(z3, res)'s output and mask (same bf16 z3, same plan)."""
+    g0 = torch.Generator(device=cuda).manual_seed(21)
+    Co = 4 * K
+    z = _nhwc(torch.randn(N, K, H, H, device=cuda, generator=g0).bfloat16())
+    w = (torch.randn(Co, K, 1, 1, device=cuda, generator=g0) * K ** -0.5).bfloat16()
+    sc = torch.rand(K, device=cuda, generator=g0) + 0.5
+    bi = torch.randn(K, device=cuda, generator=g0) * 0.1
+    res = _nhwc(torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16())
+    rm = torch.randn(Co, device=cuda, generator=g0) * 0.1
+    z3, m_ref, i_ref = _lib().conv1x1_bn_fwd(z, w, sc, bi, rm.clone(), None, None, 1, True, 1e-5,
+                                             0.1)
+    m, i = _lib().conv1x1_bn_stats_only(z, w, sc, bi, rm.clone(), None, None, 1e-5, 0.1)
+    assert torch.equal(m, m_ref) and torch.equal(i, i_ref)
+    g3 = (torch.rand(Co, device=cuda, generator=g0) + 0.5).bfloat16()
+    b3 = (torch.randn(Co, device=cuda, generator=g0) * 0.1).bfloat16()
+    sc3 = g3.float() * i
+    bi3 = b3.float() - m * sc3
+    y, mask = _lib().conv1x1_bnres(z, w, sc, bi, sc3, bi3, res)
+    t = _rows(z3) * sc3 + bi3 + _rows(res)
+    _close(_rows(y), torch.relu(t), 1e-2)
+    agree = (_bits(mask, Co) == (t > 0).float()).float().mean().item()
+    assert agree > 0.999, agree
+
+
+@pytest.mark.parametrize("N,K1,K2,No,H", [(2, 256, 64, 64, 28), (3, 512, 128, 128, 14),
+                                          (2, 512, 128, 128, 9)])
+def test_conv1x1_cat(cuda, N, K1, K2, No, H):
+    g0 = torch.Generator(device=cuda).manual_seed(22)
+    g = _nhwc(torch.randn(N, K1, H, H, device=cuda, generator=g0).bfloat16())
+    x2 = _nhwc(torch.randn(N, K2, H, H, device=cuda, generator=g0).bfloat16())
+    M = N * H * H
+    mask = _rand_mask(M, K1, cuda, g0)
+    a = torch.randn(K1, device=cuda, generator=g0)
+    c = torch.randn(K1, device=cuda, generator=g0) * 0.1
+    sc = torch.rand(K2, device=cuda, generator=g0) + 0.5
+    bi = torch.randn(K2, device=cuda, generator=g0) * 0.1
+    w = (torch.randn(No, K1 + K2, device=cuda, generator=g0) * (K1 + K2) ** -0.5).bfloat16()
+    y = _lib().conv1x1_cat(g, mask, x2, torch.cat([a, sc]), torch.cat([c, bi]), w)
+    u = (a * (_bits(mask, K1) * _rows(g)) + c).bfloat16().float()
+    v = torch.relu(_rows(x2) * sc + bi).bfloat16().float()
+    ref = torch.cat([u, v], 1) @ w.float().t()
+    _close(_rows(y), ref, 1e-2)
+
+
+@pytest.mark.parametrize("Co,Ci,H", [(256, 64, 28), (512, 128, 14), (64, 64, 20), (128, 128, 9)])
+def test_wgrad1x1_ex_modes(cuda, Co, Ci, H):
+    """Mode 2 (masked affine dy) and mode 3 (BN-ReLU dy), each with the column sums."""
+    g0 = torch.Generator(device=cuda).manual_seed(23)
+    N = 3
+    dy = _nhwc(torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16())
+    x = _nhwc(torch.randn(N, Ci, H, H, device=cuda, generator=g0).bfloat16())
+    M = N * H * H
+    sc = torch.rand(Ci, device=cuda, generator=g0) + 0.5
+    bi = torch.randn(Ci, device=cuda, generator=g0) * 0.1
+    X = torch.relu(_rows(x) * sc + bi).bfloat16().float()
+    mask = _rand_mask(M, Co, cuda, g0)
+    a = torch.randn(Co, device=cuda, generator=g0)
+    c = torch.randn(Co, device=cuda, generator=g0) * 0.1
+    dw, cs = _lib().wgrad1x1_ex(dy, x, sc, bi, 2, mask, a, None, c, True)
+    D = (a * (_bits(mask, Co) * _rows(dy)) + c).bfloat16().float()
+    _close(dw, D.t() @ X, 1e-3)
+    torch.testing.assert_close(cs, D.sum(0), rtol=1e-3, atol=1e-2 * M ** 0.5)
+    da = torch.rand(Co, device=cuda, generator=g0) + 0.5
+    db = torch.randn(Co, device=cuda, generator=g0) * 0.1
+    dw3, cs3 = _lib().wgrad1x1_ex(dy, x, sc, bi, 3, None, da, db, None, True)
+    D3 = torch.relu(_rows(dy) * da + db).bfloat16().float()
+    _close(dw3, D3.t() @ X, 1e-3)
+    torch.testing.assert_close(cs3, D3.sum(0), rtol=1e-3, atol=1e-2 * M ** 0.5)
+
+
+@pytest.mark.parametrize("planes,H", [(64, 28), (128, 14)])
+def test_identity_chain_recompute_tail(cuda, planes, H):
+    """Three identity blocks with the recompute tail vs the stored-z3 fused tail, both against an
+    fp32 run of the same weights (output, input gradient and every parameter gradient)."""
+    from consensusml_amd.models import resnet
+    m_on = _chain(cuda, planes, 3, seed=1)
+    m_off = copy.deepcopy(m_on)
+    m32 = copy.deepcopy(m_on).float()
+    g0 = torch.Generator(device=cuda).manual_seed(6)
+    x = _nhwc(torch.randn(8, planes * 4, H, H, device=cuda, generator=g0).bfloat16())
+    gy = _nhwc(torch.randn(8, planes * 4, H, H, device=cuda, generator=g0).bfloat16())
+    outs = {}
+    for key, m, dt in (("on", m_on, torch.bfloat16), ("off", m_off, torch.bfloat16),
+                       ("fp32", m32, torch.float32)):
+        old = resnet.RECOMPUTE_TAIL
+        resnet.RECOMPUTE_TAIL = key == "on"
+        try:
+            xi = x.to(dt).clone().requires_grad_(True)
+            y = m(xi)
+            y.backward(gy.to(dt))
+        finally:
+            resnet.RECOMPUTE_TAIL = old
+        outs[key] = (y.detach().float(), xi.grad.float(), [p.grad.float() for p in m.parameters()],
+                     [b.float().clone() for b in m.buffers()])
+    ref = outs["fp32"]
+    for k in (0, 1):
+        e_on, e_off = _err(outs["on"][k], ref[k]), _err(outs["off"][k], ref[k])
+        assert e_on <= 1.5 * e_off + 1e-2, (k, e_on, e_off)
+    for a, b, r in zip(outs["on"][2], outs["off"][2], ref[2]):
+        e_on, e_off = _err(a, r), _err(b, r)
+        assert e_on <= 1.5 * e_off + 2e-2, (e_on, e_off)
+    for a, b in zip(outs["on"][3], outs["off"][3]):   # running statistics
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
