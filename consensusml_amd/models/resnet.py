@@ -55,8 +55,16 @@ FUSED_CONV1X1 = os.environ.get("CML_FUSED_CONV1X1", "1") == "1"
 # conv1's data-gradient epilogue (ops.conv.bnrelu_conv1x1_bn_res)
 FUSED_BN3_BWD = os.environ.get("CML_FUSED_BN3_BWD", "1") == "1"
 FUSED_BN3_BWD_MAX_PLANES = int(os.environ.get("CML_FUSED_BN3_BWD_MAX_PLANES", "128"))
-# fused identity tails of planes 64 / 128 without a stored z3 (ops.conv._RecomputeTailFn)
+# fused identity tails without a stored z3 (ops.conv._RecomputeTailFn), up to this many planes
 RECOMPUTE_TAIL = os.environ.get("CML_RECOMPUTE_TAIL", "1") == "1"
+RECOMPUTE_TAIL_MAX_PLANES = int(os.environ.get("CML_RECOMPUTE_TAIL_MAX_PLANES", "256"))
+
+
+def recompute_tail_policy(planes: int) -> bool:
+    """Measured at batch 2048 (profiles/r02_recompute_tail35/): up to 128 planes 152.1 -> 145.2
+    ms / step; adding layer 3 (256) another -1.1 ms; layer 4 (512) +0.4-0.6 ms back."""
+    return (RECOMPUTE_TAIL and planes <= RECOMPUTE_TAIL_MAX_PLANES
+            and fconv.recompute_tail_ok(planes))
 # stride-1 3x3 convs: data gradient on csrc/kernels/conv_gemm.hip (ops.conv.conv3x3)
 OWN_DGRAD3X3 = os.environ.get("CML_DGRAD3X3", "1") == "1"
 # ... and their forward on conv_gemm too, with bn2's statistics in the epilogue
@@ -292,10 +300,10 @@ class Bottleneck(nn.Module):
             z2 = self._conv2(out)
             st2 = fconv.bn_stats(z2, self.bn2) if fuse3 else None
         if fuse3:
-            if self.down_conv is None and fused_bn3_bwd_policy(planes):
+            rec = self.down_conv is None and recompute_tail_policy(planes)
+            if rec or (self.down_conv is None and fused_bn3_bwd_policy(planes)):
                 out_link = ResidualLink() if use_links else None
-                tail = fconv.bnrelu_conv1x1_bn_res_recompute \
-                    if RECOMPUTE_TAIL and fconv.recompute_tail_ok(planes) \
+                tail = fconv.bnrelu_conv1x1_bn_res_recompute if rec \
                     else fconv.bnrelu_conv1x1_bn_res
                 y = tail(z2, self.bn2, st2, self.conv3, self.bn3, x, link, out_link)
                 if out_link is not None:

@@ -289,9 +289,8 @@ class _RecomputeTailFn(torch.autograd.Function):
 
 
 def recompute_tail_ok(planes: int) -> bool:
-    """Channel counts of the recompute tail's kernels (the Gram pass's column sums need a tile of
-    at most 512 threads: planes 64 and 128, ResNet-50 layers 1-2)."""
-    return planes in (64, 128)
+    """Channel counts of the recompute tail's kernels (every ResNet-50 stage)."""
+    return planes in (64, 128, 256, 512)
 
 
 def bnrelu_conv1x1_bn_res_recompute(z: torch.Tensor, bn_a, stats_a, conv, bn_b,

@@ -543,7 +543,8 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
               "wgrad1x1: dz_z, dz_mask, dz_a, dz_b, dz_c together");
   const c10::DeviceGuard guard(x.device());
   int S = 1, cps = 1;
-  cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps);
+  cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps,
+                     sc != nullptr || zp != nullptr);
   Tensor part = at::empty({S, Co, Ci}, x.options().dtype(at::kFloat));
   Tensor dw = at::empty({Co, Ci, 1, 1}, x.options().dtype(dtype));
   CML_CHECK_HIP(cml::launch_wgrad1x1(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(),
@@ -572,7 +573,8 @@ std::vector<Tensor> wgrad1x1_ex(const Tensor& dy_in, const Tensor& x, const opti
   TORCH_CHECK((sc == nullptr) == (bi == nullptr), "wgrad1x1_ex: pro_sc and pro_bi together");
   const c10::DeviceGuard guard(x.device());
   int S = 1, cps = 1;
-  cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps);
+  cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps,
+                     sc != nullptr || dmode != 0);
   auto f32 = x.options().dtype(at::kFloat);
   Tensor part = at::empty({S, Co, Ci}, f32);
   Tensor dw = at::empty({Co, Ci}, f32);
@@ -738,8 +740,9 @@ std::vector<Tensor> conv1x1_bn_fwd(const Tensor& x, const Tensor& w, const optio
 
 // Statistics-only pass of a stride-1 1x1 conv with the BN + ReLU prologue (the product is not
 // stored): {mean, invstd} of bf16(conv1x1(max(x sc + bi, 0))), running stats updated when given.
-std::vector<Tensor> conv1x1_bn_stats_only(const Tensor& x, const Tensor& w, const Tensor& pro_sc,
-                                          const Tensor& pro_bi, const optional<Tensor>& shift,
+std::vector<Tensor> conv1x1_bn_stats_only(const Tensor& x, const Tensor& w,
+                                          const optional<Tensor>& pro_sc,
+                                          const optional<Tensor>& pro_bi, const optional<Tensor>& shift,
                                           const optional<Tensor>& rmean,
                                           const optional<Tensor>& rvar, double eps, double momentum) {
   check_nhwc(x, "x");
@@ -751,8 +754,10 @@ std::vector<Tensor> conv1x1_bn_stats_only(const Tensor& x, const Tensor& w, cons
   const c10::DeviceGuard guard(x.device());
   auto f32 = x.options().dtype(at::kFloat);
   Tensor mean = at::empty({Co}, f32), invstd = at::empty({Co}, f32);
+  const bool pro = pro_sc.has_value() && pro_sc->defined();
+  TORCH_CHECK(pro == (pro_bi.has_value() && pro_bi->defined()), "pro_sc and pro_bi together");
   Tensor part = at::empty({static_cast<int64_t>(cml::conv1x1_bn_part_floats(
-                              M, static_cast<int>(K), static_cast<int>(Co), true))}, f32);
+                              M, static_cast<int>(K), static_cast<int>(Co), pro))}, f32);
   CML_CHECK_HIP(cml::launch_conv1x1_bn_fwd(
       x.data_ptr(), w.data_ptr(), nullptr, part.data_ptr<float>(),
       opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", K),
@@ -791,6 +796,34 @@ std::vector<Tensor> conv1x1_bnres(const Tensor& x, const Tensor& w, const Tensor
       opt_ptr<const float>(ep_sc, at::kFloat, "ep_sc", Co),
       opt_ptr<const float>(ep_bi, at::kFloat, "ep_bi", Co), res.data_ptr(), M,
       static_cast<int>(K), static_cast<int>(Co), cur_stream()));
+  return {y, mask};
+}
+
+// Downsample tail in one GEMM: y = max(bf16([max(x1 sc + bi, 0) | max(x2 sc + bi, 0)] w^T) ep_sc
+// + ep_bi, 0) and its ReLU bit mask; sc_cat / bi_cat fp32 [K1 + K2], w [Cout, K1 + K2] bf16.
+std::vector<Tensor> conv1x1_cat_bnres(const Tensor& x1, const Tensor& x2, const Tensor& sc_cat,
+                                      const Tensor& bi_cat, const Tensor& w, const Tensor& ep_sc,
+                                      const Tensor& ep_bi) {
+  check_nhwc(x1, "x1");
+  check_nhwc(x2, "x2");
+  const int64_t N = x1.size(0), K1 = x1.size(1), H = x1.size(2), W = x1.size(3), K2 = x2.size(1);
+  const int64_t M = N * H * W, K = K1 + K2;
+  TORCH_CHECK(x2.dim() == 4 && x2.size(0) == N && x2.size(2) == H && x2.size(3) == W,
+              "conv1x1_cat_bnres: x2 shape");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.size(1) == K &&
+                  w.is_contiguous() && w.size(0) % 64 == 0 && K1 % 64 == 0 && K2 % 64 == 0,
+              "conv1x1_cat_bnres: w contiguous bf16 [Cout, K1 + K2], channels multiples of 64");
+  const int64_t Co = w.size(0);
+  const c10::DeviceGuard guard(x1.device());
+  Tensor y = at::empty({N, Co, H, W}, x1.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor mask = at::empty({M, Co / 8}, x1.options().dtype(at::kByte));
+  CML_CHECK_HIP(cml::launch_conv1x1_cat_bnres(
+      x1.data_ptr(), x2.data_ptr(), opt_ptr<const float>(sc_cat, at::kFloat, "sc_cat", K),
+      opt_ptr<const float>(bi_cat, at::kFloat, "bi_cat", K), w.data_ptr(),
+      opt_ptr<const float>(ep_sc, at::kFloat, "ep_sc", Co),
+      opt_ptr<const float>(ep_bi, at::kFloat, "ep_bi", Co), nullptr, y.data_ptr(),
+      mask.data_ptr<uint8_t>(), M, static_cast<int>(K1), static_cast<int>(K),
+      static_cast<int>(Co), cur_stream()));
   return {y, mask};
 }
 
@@ -1450,6 +1483,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps") = 1e-5, py::arg("momentum") = 0.1,
         "BN statistics of conv1x1(bnrelu(x)) without storing the product");
   m.def("conv1x1_bnres", &conv1x1_bnres, "recomputed conv1x1 + BN apply + residual + ReLU -> {y, mask}");
+  m.def("conv1x1_cat_bnres", &conv1x1_cat_bnres,
+        "two BN'd 1x1 convs summed + ReLU in one K-concatenated GEMM -> {y, mask}");
   m.def("conv1x1_cat", &conv1x1_cat, "two-source (masked affine | BN-ReLU) 1x1 conv along K");
   m.def("wgrad1x1_ex", &wgrad1x1_ex, py::arg("dy"), py::arg("x"), py::arg("pro_sc") = py::none(),
         py::arg("pro_bi") = py::none(), py::arg("dmode") = 0, py::arg("dz_mask") = py::none(),

@@ -75,6 +75,7 @@ struct C1Args {
   const float* ep_bi;
   uint8_t* ymask;         // SM_BNRES: bit mask of y > 0 [M][N / 8]
   int K1;                 // PM_CAT: channels of the first source (x, with mask xm); x2 has K - K1
+  int cat_bnrelu;         // PM_CAT: 1 = the first source is max(x sc + bi, 0) too (no mask)
   int M, K, N;
   int ntn, wgpn, mtiles;
   int H, W, OW, OHW;      // S2: input H, W; output W and H*W.  TAP: H, W (in = out) and OHW = H W
@@ -142,7 +143,7 @@ __device__ __forceinline__ void load_x(const C1Args& a, uint4 (&pb)[CB], uint4 (
       const int64_t r = src_row(a, t * BM + srow + 32 * j, false);
       if (first) {
         pb[j] = *reinterpret_cast<const uint4*>(a.x + r * a.K1 + k0 + 8 * ch);
-        pm[j] = a.xm[r * (a.K1 / 8) + k0 / 8 + ch];
+        pm[j] = a.cat_bnrelu ? 0u : a.xm[r * (a.K1 / 8) + k0 / 8 + ch];
       } else {
         pb[j] = *reinterpret_cast<const uint4*>(a.x2 + r * (a.K - a.K1) + (k0 - a.K1) + 8 * ch);
         pm[j] = 0u;
@@ -181,7 +182,7 @@ template <int CB, int PM, bool TAP = false>
 __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)[CB],
                                         const uint32_t (&pm)[CB], char* sx, const float* s_aff,
                                         int KA, int kofs, int srow, int ch, uint32_t vm = ~0u,
-                                        int K1 = 0) {
+                                        int K1 = 0, int cat_bnrelu = 0) {
   float sc[8], bi[8], cc[8];
   if constexpr (PM != PM_NONE) {
     ld8f(s_aff + kofs + 8 * ch, sc);
@@ -217,7 +218,7 @@ __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)
     } else if constexpr (PM == PM_CAT) {
       uint32_t w4[4] = {v.x, v.y, v.z, v.w};
       const uint32_t bits = pm[j];
-      if (kofs < K1) {
+      if (kofs < K1 && !cat_bnrelu) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float glo = ((bits >> (2 * i)) & 1u) ? __uint_as_float(w4[i] << 16) : 0.f;
@@ -268,7 +269,8 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
   // all 8 rows at once with one operand (EL), in batches of 4 with two, halved again at MT = 2
   // (more registers would spill). Rows past M re-read row m0.
   constexpr bool LD = EL || SM == SM_BNBWD || SM == SM_BNRES;
-  constexpr int RB = ((EL && SM == SM_BNBWD) ? 4 : 8) / MT;   // rows per batch
+  constexpr int RB = ((EL && SM == SM_BNBWD) ? 4 : 8) / MT /   // rows per batch
+                     ((SM == SM_BNRES && MT == 2) ? 2 : 1);
   uint4 lv[RB], zv[RB];
   uint32_t lbv[RB], zbv[RB];
   if constexpr (!(EL && SM == SM_BNBWD)) {   // one operand: keep the row body's arguments defined
@@ -295,7 +297,8 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
         lv[k] = *reinterpret_cast<const uint4*>(a.link + e0);
         lbv[k] = a.lm[e0 >> 3];
       }
-      if constexpr (SM == SM_BNRES) lv[k] = *reinterpret_cast<const uint4*>(a.link + e0);
+      if constexpr (SM == SM_BNRES)   // (no residual: link null)
+        lv[k] = a.link ? *reinterpret_cast<const uint4*>(a.link + e0) : make_uint4(0u, 0u, 0u, 0u);
       if constexpr (SM == SM_BNBWD) {
         zv[k] = *reinterpret_cast<const uint4*>(a.sz + e0);
         zbv[k] = a.sm[e0 >> 3];
@@ -480,7 +483,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       ss[q] = 0.f;
       sq[q] = 0.f;
     }
-    store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, 0, srow, ch, vm, a.K1);
+    store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, 0, srow, ch, vm, a.K1, a.cat_bnrelu);
     if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, 0);
     __syncthreads();
     for (;;) {
@@ -522,7 +525,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       }
       if (!more) break;
       __syncthreads();               // every wave is done reading this step's LDS
-      store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, kofs(ksn), srow, ch, vm, a.K1);
+      store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, kofs(ksn), srow, ch, vm, a.K1,
+                           a.cat_bnrelu);
       if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, ksn);
       __syncthreads();
       t = tn;
@@ -754,7 +758,8 @@ template <int WN, int WM, int PM, bool WRES, bool S2, bool EL = false, int SM = 
           bool TAP = false>
 hipError_t launch_t(const C1Args& a, const Plan& p, hipStream_t st) {
   auto k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 1, TAP>;
-  if constexpr (WN == 2 && !WRES && PM != PM_BNBWD && SM != SM_BNBWD) {
+  if constexpr (WN == 2 && !WRES && PM != PM_BNBWD && SM != SM_BNBWD &&
+                !(PM == PM_CAT && SM == SM_BNRES)) {
     if (p.MT == 2) k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 2, TAP>;
   }
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
@@ -810,6 +815,9 @@ hipError_t launch_bwd(const C1Args& a, const Plan& p, int mode, hipStream_t st) 
 // recompute tail (fused BN + residual + ReLU epilogue) and two-source (PM_CAT) data gradient
 template <int WN, int WM>
 hipError_t launch_tail_w(const C1Args& a, const Plan& p, bool cat, hipStream_t st) {
+  if (cat && a.ymask)
+    return p.wres ? launch_t<WN, WM, PM_CAT, true, false, false, SM_BNRES>(a, p, st)
+                  : launch_t<WN, WM, PM_CAT, false, false, false, SM_BNRES>(a, p, st);
   if (cat)
     return p.wres ? launch_t<WN, WM, PM_CAT, true, false, false, SM_OFF>(a, p, st)
                   : launch_t<WN, WM, PM_CAT, false, false, false, SM_OFF>(a, p, st);
@@ -990,6 +998,27 @@ hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2
   a.pro_sc = a_cat;
   a.pro_bi = c_cat;
   a.K1 = K1;
+  return launch_tail(a, p, true, st);
+}
+
+hipError_t launch_conv1x1_cat_bnres(const void* x1, const void* x2, const float* sc_cat,
+                                    const float* bi_cat, const void* w, const float* ep_sc,
+                                    const float* ep_bi, const void* res, void* y, uint8_t* ymask,
+                                    int64_t M, int K1, int K, int N, hipStream_t st) {
+  if (bad_shape(M, K, N) || K1 % kBK || K1 <= 0 || K1 >= K || !sc_cat || !bi_cat || !ep_sc ||
+      !ep_bi || !ymask)
+    return hipErrorInvalidValue;
+  const Plan p = make_plan(M, K, N, 2, -1, false);   // (its MT = 2 tile spills)
+  C1Args a = base_args(x1, w, y, M, K, N, p);
+  a.x2 = reinterpret_cast<const uint16_t*>(x2);
+  a.pro_sc = sc_cat;
+  a.pro_bi = bi_cat;
+  a.K1 = K1;
+  a.cat_bnrelu = 1;
+  a.ep_sc = ep_sc;
+  a.ep_bi = ep_bi;
+  a.link = reinterpret_cast<const uint16_t*>(res);
+  a.ymask = ymask;
   return launch_tail(a, p, true, st);
 }
 

@@ -240,7 +240,8 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
 // (wgrad1x1.hip). Co, Ci multiples of 128, or Ci == 64 with Co a multiple of 256. part: splits x
 // Co x Ci floats (wgrad1x1_plan); dw: bf16 (dw_bf16) or fp32 [Co][Ci]. pro_sc / pro_bi (fp32
 // [Ci], both or neither): x is replaced by max(x * sc + bi, 0) (a BN + ReLU never materialised).
-void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps);
+// pro: a dy or x prologue is applied (the plan then avoids the 1024-thread tile)
+void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro = false);
 // dz_z / dz_mask / dz_a / dz_b / dz_c (all or none): dy is the output gradient of a BN + ReLU that
 // consumed the conv output z = dz_z; the staging uses dz = a (mask ? dy : 0) + b z + c instead.
 // General form: dmode 0 none, 1 the dz_* BN-backward prologue above, 2 dz = dz_a (mask ? dy : 0)
@@ -328,6 +329,12 @@ hipError_t launch_conv1x1_bnres(const void* x, const void* w, void* y, uint8_t* 
                                 hipStream_t st);
 // y = [a (mask ? g : 0) + c | max(x2 sc + bi, 0)] W^T: K = K1 + K2 channels from two sources
 // (g, mask: [M][K1]; x2: [M][K2]); a_cat = [a | sc], c_cat = [c | bi] (fp32 [K]); w [N][K].
+// y = max(bf16([max(x1 sc + bi, 0) | max(x2 sc + bi, 0)] W^T) ep_sc + ep_bi (+ res), 0) and its
+// ReLU bit mask: two BN'd convs summed before a ReLU (a downsample block's tail) in one GEMM.
+hipError_t launch_conv1x1_cat_bnres(const void* x1, const void* x2, const float* sc_cat,
+                                    const float* bi_cat, const void* w, const float* ep_sc,
+                                    const float* ep_bi, const void* res, void* y, uint8_t* ymask,
+                                    int64_t M, int K1, int K, int N, hipStream_t st);
 hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2, const float* a_cat,
                               const float* c_cat, const void* w, void* y, int64_t M, int K1, int K,
                               int N, hipStream_t st);

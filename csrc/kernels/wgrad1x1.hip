@@ -351,7 +351,7 @@ namespace {
 // is streamed once (x is re-read Co / TM times, dy Ci / TN times)
 // (memory-bound shapes, Co * Ci <= 128K); shapes with more MACs per byte take 128 x 128 tiles
 // for more workgroups (tools/diag/wgrad1x1_bench.py)
-void pick_tile(int Co, int Ci, int* TM, int* TN) {
+void pick_tile(int Co, int Ci, int* TM, int* TN, bool pro = false) {
   if (Co == 64 && Ci == 64) {   // Gram matrix of a 64-channel activation: one wave per tile
     *TM = 64;
     *TN = 64;
@@ -365,6 +365,7 @@ void pick_tile(int Co, int Ci, int* TM, int* TN) {
   *TM = Co % 256 == 0 ? 256 : 128;
   *TN = Ci == 64 ? 64 : (Ci % 256 == 0 ? 256 : 128);
   if (*TN == 64) *TM = 256;   // 4 waves
+  if (pro && *TM == 256 && *TN == 256) *TN = 128;   // the 1024-thread tile has no prologue variant
 }
 }  // namespace
 
@@ -418,9 +419,9 @@ bool launch_tile_tap(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, cons
 // registers, fewer chunks per workgroup)
 int chunk_of(int, int) { return 64; }
 
-void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps) {
+void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro) {
   int TM, TN;
-  pick_tile(Co, Ci, &TM, &TN);
+  pick_tile(Co, Ci, &TM, &TN, pro);
   const int KC = chunk_of(TM, TN);
   const int tiles = (Co / TM) * (Ci / TN);
   const int waves = (TM / 64) * (TN / 64);
@@ -454,7 +455,7 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
     return hipErrorInvalidValue;
   {
     int tm, tn;
-    pick_tile(Co, Ci, &tm, &tn);
+    pick_tile(Co, Ci, &tm, &tn, pro_sc != nullptr || dmode != DP_NONE);
     if (cs && tm * tn > 32768) return hipErrorInvalidValue;   // no column sums in that tile
   }
   DPro dp{reinterpret_cast<const uint16_t*>(dz_z), dz_mask, dz_a, dz_b, dz_c};
@@ -463,8 +464,9 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
   if (P < 1 || P >= (1ll << 31)) return hipErrorInvalidValue;
   if ((pro_sc == nullptr) != (pro_bi == nullptr)) return hipErrorInvalidValue;
   int S, cps, TM, TN;
-  wgrad1x1_plan(P, Co, Ci, &S, &cps);
-  pick_tile(Co, Ci, &TM, &TN);
+  const bool anypro = pro_sc != nullptr || dmode != DP_NONE;
+  wgrad1x1_plan(P, Co, Ci, &S, &cps, anypro);
+  pick_tile(Co, Ci, &TM, &TN, anypro);
   const int KC = chunk_of(TM, TN);
   const int tiles_n = Ci / TN;
   const dim3 grid((Co / TM) * tiles_n, S);

@@ -223,7 +223,8 @@ def test_conv1x1_cat(cuda, N, K1, K2, No, H):
     _close(_rows(y), ref, 1e-2)
 
 
-@pytest.mark.parametrize("Co,Ci,H", [(256, 64, 28), (512, 128, 14), (64, 64, 20), (128, 128, 9)])
+@pytest.mark.parametrize("Co,Ci,H", [(256, 64, 28), (512, 128, 14), (64, 64, 20), (128, 128, 9),
+                                    (1024, 256, 7), (256, 256, 7), (512, 512, 5)])
 def test_wgrad1x1_ex_modes(cuda, Co, Ci, H):
     """Mode 2 (masked affine dy) and mode 3 (BN-ReLU dy), each with the column sums."""
     g0 = torch.Generator(device=cuda).manual_seed(23)
@@ -249,7 +250,7 @@ def test_wgrad1x1_ex_modes(cuda, Co, Ci, H):
     torch.testing.assert_close(cs3, D3.sum(0), rtol=1e-3, atol=1e-2 * M ** 0.5)
 
 
-@pytest.mark.parametrize("planes,H", [(64, 28), (128, 14)])
+@pytest.mark.parametrize("planes,H", [(64, 28), (128, 14), (256, 14), (512, 7)])
 def test_identity_chain_recompute_tail(cuda, planes, H):
     """Three identity blocks with the recompute tail vs the stored-z3 fused tail, both against an
     fp32 run of the same weights (output, input gradient and every parameter gradient)."""
@@ -263,14 +264,14 @@ def test_identity_chain_recompute_tail(cuda, planes, H):
     outs = {}
     for key, m, dt in (("on", m_on, torch.bfloat16), ("off", m_off, torch.bfloat16),
                        ("fp32", m32, torch.float32)):
-        old = resnet.RECOMPUTE_TAIL
-        resnet.RECOMPUTE_TAIL = key == "on"
+        old = resnet.RECOMPUTE_TAIL, resnet.RECOMPUTE_TAIL_MAX_PLANES
+        resnet.RECOMPUTE_TAIL, resnet.RECOMPUTE_TAIL_MAX_PLANES = key == "on", 4096
         try:
             xi = x.to(dt).clone().requires_grad_(True)
             y = m(xi)
             y.backward(gy.to(dt))
         finally:
-            resnet.RECOMPUTE_TAIL = old
+            resnet.RECOMPUTE_TAIL, resnet.RECOMPUTE_TAIL_MAX_PLANES = old
         outs[key] = (y.detach().float(), xi.grad.float(), [p.grad.float() for p in m.parameters()],
                      [b.float().clone() for b in m.buffers()])
     ref = outs["fp32"]
