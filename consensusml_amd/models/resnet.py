@@ -58,6 +58,8 @@ FUSED_BN3_BWD_MAX_PLANES = int(os.environ.get("CML_FUSED_BN3_BWD_MAX_PLANES", "1
 # fused identity tails without a stored z3 (ops.conv._RecomputeTailFn), up to this many planes
 RECOMPUTE_TAIL = os.environ.get("CML_RECOMPUTE_TAIL", "1") == "1"
 RECOMPUTE_TAIL_MAX_PLANES = int(os.environ.get("CML_RECOMPUTE_TAIL_MAX_PLANES", "256"))
+# ... and the stride-1 downsample tail (layer 1) without z3 / zd (ops.conv._RecomputeDownTailFn)
+RECOMPUTE_DOWN_TAIL = os.environ.get("CML_RECOMPUTE_DOWN_TAIL", "1") == "1"
 
 
 def recompute_tail_policy(planes: int) -> bool:
@@ -306,6 +308,17 @@ class Bottleneck(nn.Module):
                 tail = fconv.bnrelu_conv1x1_bn_res_recompute if rec \
                     else fconv.bnrelu_conv1x1_bn_res
                 y = tail(z2, self.bn2, st2, self.conv3, self.bn3, x, link, out_link)
+                if out_link is not None:
+                    y._cml_link = out_link
+                return y
+            if (self.down_conv is not None and RECOMPUTE_DOWN_TAIL and self.bn3.eps ==
+                    self.down_bn.eps and fconv.down_tail_recompute_ok(x, planes, self.down_conv)):
+                out_link = ResidualLink() if use_links else None
+                tlink = dlink if dlink is not None else \
+                    (getattr(x, "_cml_pool_link", None) if use_links else None)
+                xin = link_tap(x, tlink) if tlink is not None else x
+                y = fconv.down_tail_recompute(z2, self.bn2, st2, self.conv3, self.bn3, xin,
+                                              self.down_conv, self.down_bn, out_link)
                 if out_link is not None:
                     y._cml_link = out_link
                 return y

@@ -288,6 +288,109 @@ class _RecomputeTailFn(torch.autograd.Function):
         return (dz, dg2, db2, None, None, dw, dg3, db3, dres) + (None,) * 6
 
 
+class _RecomputeDownTailFn(torch.autograd.Function):
+    """Downsample-block tail y = relu(bn3(conv3(relu(bn2(z2)))) + bnd(convd(x))) with stride-1
+    convd, storing neither z3 nor zd (both 4p channels; ResNet-50 layer 1: 3.3 GB each at batch
+    2048).
+
+    Forward: statistics-only passes of both convs, then one GEMM over [y2 | x] (K = p + Cin)
+    with the BN scales folded into the weights, + both BN shifts, ReLU and its mask
+    (``conv1x1_cat_bnres``). Backward as ``_RecomputeTailFn`` for each branch -- both BNs see the
+    same u = m * g -- with dx = (ad u + cd) Wd + x (Wd^T diag(bd) Wd) from ``conv1x1_cat`` (its
+    second source passes x through max(x * 1 + 0, 0): x must be a ReLU output, as every block
+    input is). x's gradient goes back through autograd (callers wrap x in ``link_tap`` to hand it
+    to conv1's data-gradient GEMM)."""
+
+    @staticmethod
+    def forward(ctx, z, g2, b2, mean2, invstd2, w3, g3, b3, rm3, rv3, x, wd, gd, bd, rmd, rvd,
+                eps, momentum, out_link):
+        sc = g2.float() * invstd2
+        bi = b2.float() - mean2 * sc
+        L = lib()
+        w3c, wdc = w3.contiguous(), wd.contiguous()
+        m3, i3 = L.conv1x1_bn_stats_only(z, w3c, sc, bi, rm3, rm3, rv3, eps, momentum)
+        md, idd = L.conv1x1_bn_stats_only(x, wdc, None, None, rmd, rmd, rvd, eps, momentum)
+        Co, P_, Cin = w3.shape[0], w3.shape[1], wd.shape[1]
+        sc3 = g3.float() * i3
+        scd = gd.float() * idd
+        bias = (b3.float() - m3 * sc3) + (bd.float() - md * scd)
+        w_cat = torch.cat([w3c.view(Co, P_).float() * sc3[:, None],
+                           wdc.view(Co, Cin).float() * scd[:, None]], 1).to(torch.bfloat16)
+        dev = z.device
+        y, mask = L.conv1x1_cat_bnres(z, x, torch.cat([sc, _const(Cin, 1.0, dev)]),
+                                      torch.cat([bi, _const(Cin, 0.0, dev)]), w_cat.contiguous(),
+                                      _const(Co, 1.0, dev), bias)
+        ctx.save_for_backward(z, g2, b2, mean2, invstd2, w3, sc, bi, mask, g3, m3, i3, x, wd, gd,
+                              md, idd)
+        ctx.out_link = out_link
+        if out_link is not None:
+            out_link.bn_ctx = None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (z, g2, b2, mean2, invstd2, w3, sc, bi, mask, g3, m3, i3, x, wd, gd, md,
+         idd) = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        ol = ctx.out_link
+        if ol is not None:
+            extra = ol.take_tensor()
+            ol.sums = ol.bn_ctx = None
+            if extra is not None:
+                gy = (gy + extra).contiguous(memory_format=torch.channels_last)
+        M = gy.numel() // gy.shape[1]
+        Co, P_, Cin = w3.shape[0], w3.shape[1], wd.shape[1]
+        dev = gy.device
+        L = lib()
+        one, zero = _const(Co, 1.0, dev), _const(Co, 0.0, dev)
+        P3, s = L.wgrad1x1_ex(gy, z, sc, bi, 2, mask, one, None, zero, True)
+        Pd, _ = L.wgrad1x1_ex(gy, x, None, None, 2, mask, one, None, zero, False)
+        gram3, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
+        gramd, cx = L.wgrad1x1_ex(x, x, None, None, 0, None, None, None, None, True)
+        W3 = w3.reshape(Co, P_).float()
+        Wd = wd.reshape(Co, Cin).float()
+        q3 = i3 * ((W3 * P3).sum(1) - m3 * s)
+        qd = idd * ((Wd * Pd).sum(1) - md * s)
+        a3, b3c, c3, dg3, db3 = L.bn_bwd_coeffs(s, q3, g3, m3, i3, M)
+        ad, bdc, cd, dgd, dbd = L.bn_bwd_coeffs(s, qd, gd, md, idd, M)
+        dw3 = dwd = None
+        if ctx.needs_input_grad[5]:
+            dw3 = (a3[:, None] * P3 + b3c[:, None] * (W3 @ gram3) + c3[:, None] * cy[None, :])
+            dw3 = dw3.to(w3.dtype).view_as(w3)
+        if ctx.needs_input_grad[11]:
+            dwd = (ad[:, None] * Pd + bdc[:, None] * (Wd @ gramd) + cd[:, None] * cx[None, :])
+            dwd = dwd.to(wd.dtype).view_as(wd)
+        G3 = W3.t() @ (b3c[:, None] * W3)
+        dy2 = L.conv1x1_cat(gy, mask, z, torch.cat([a3, sc]), torch.cat([c3, bi]),
+                            torch.cat([W3.t(), G3.t()], 1).to(torch.bfloat16).contiguous())
+        dz, dg2, db2, _ = L.bn_bwd(dy2, None, z, None, g2, b2, mean2, invstd2, True, False)
+        dx = None
+        if ctx.needs_input_grad[10]:
+            Gd = Wd.t() @ (bdc[:, None] * Wd)
+            dx = L.conv1x1_cat(gy, mask, x, torch.cat([ad, _const(Cin, 1.0, dev)]),
+                               torch.cat([cd, _const(Cin, 0.0, dev)]),
+                               torch.cat([Wd.t(), Gd.t()], 1).to(torch.bfloat16).contiguous())
+        return (dz, dg2, db2, None, None, dw3, dg3, db3, None, None, dx, dwd, dgd, dbd) + \
+            (None,) * 5
+
+
+def down_tail_recompute_ok(x: torch.Tensor, planes: int, down_conv) -> bool:
+    """Stride-1 downsample convs (ResNet-50 layer 1) with the recompute kernels' channel counts."""
+    return (down_conv.stride[0] == 1 and planes in (64, 128) and x.shape[1] % 64 == 0
+            and x.shape[1] <= 256)
+
+
+def down_tail_recompute(z: torch.Tensor, bn_a, stats_a, conv, bn_b, x: torch.Tensor, down_conv,
+                        down_bn, out_link=None) -> torch.Tensor:
+    """y = relu(bn_b(conv(relu(bn_a(z)))) + down_bn(down_conv(x))) (see _RecomputeDownTailFn)."""
+    mean, invstd = stats_a
+    return _RecomputeDownTailFn.apply(z, bn_a.weight, bn_a.bias, mean, invstd, conv.weight,
+                                      bn_b.weight, bn_b.bias, bn_b.running_mean,
+                                      bn_b.running_var, x, down_conv.weight, down_bn.weight,
+                                      down_bn.bias, down_bn.running_mean, down_bn.running_var,
+                                      bn_b.eps, bn_b.momentum, out_link)
+
+
 def recompute_tail_ok(planes: int) -> bool:
     """Channel counts of the recompute tail's kernels (every ResNet-50 stage)."""
     return planes in (64, 128, 256, 512)

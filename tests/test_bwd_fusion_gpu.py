@@ -283,3 +283,46 @@ def test_identity_chain_recompute_tail(cuda, planes, H):
         assert e_on <= 1.5 * e_off + 2e-2, (e_on, e_off)
     for a, b in zip(outs["on"][3], outs["off"][3]):   # running statistics
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("cin,planes,H", [(64, 64, 28), (128, 128, 14)])
+def test_downsample_recompute_tail(cuda, cin, planes, H):
+    """Stride-1 downsample block with the recompute tail (no z3 / zd) vs the stored path, both
+    against an fp32 copy: output, input gradient, parameter gradients, running statistics."""
+    from consensusml_amd.models import resnet
+    from consensusml_amd.models.resnet import Bottleneck
+    torch.manual_seed(3)
+    m_on = Bottleneck(cin, planes, 1, downsample=True)
+    for mod in m_on.modules():
+        if mod.__class__.__name__ == "BatchNormAct2d":
+            with torch.no_grad():
+                mod.weight.uniform_(0.5, 1.5)
+                mod.bias.uniform_(-0.1, 0.1)
+    m_on = m_on.to(device=cuda, dtype=torch.bfloat16, memory_format=torch.channels_last).train()
+    m_off = copy.deepcopy(m_on)
+    m32 = copy.deepcopy(m_on).float()
+    g0 = torch.Generator(device=cuda).manual_seed(7)
+    x = _nhwc(torch.relu(torch.randn(8, cin, H, H, device=cuda, generator=g0)).bfloat16())
+    gy = _nhwc(torch.randn(8, planes * 4, H, H, device=cuda, generator=g0).bfloat16())
+    outs = {}
+    for key, m, dt in (("on", m_on, torch.bfloat16), ("off", m_off, torch.bfloat16),
+                       ("fp32", m32, torch.float32)):
+        old = resnet.RECOMPUTE_DOWN_TAIL
+        resnet.RECOMPUTE_DOWN_TAIL = key == "on"
+        try:
+            xi = x.to(dt).clone().requires_grad_(True)
+            y = m(xi)
+            y.backward(gy.to(dt))
+        finally:
+            resnet.RECOMPUTE_DOWN_TAIL = old
+        outs[key] = (y.detach().float(), xi.grad.float(), [p.grad.float() for p in m.parameters()],
+                     [b.float().clone() for b in m.buffers()])
+    ref = outs["fp32"]
+    for k in (0, 1):
+        e_on, e_off = _err(outs["on"][k], ref[k]), _err(outs["off"][k], ref[k])
+        assert e_on <= 1.5 * e_off + 1e-2, (k, e_on, e_off)
+    for a, b, r in zip(outs["on"][2], outs["off"][2], ref[2]):
+        e_on, e_off = _err(a, r), _err(b, r)
+        assert e_on <= 1.5 * e_off + 2e-2, (e_on, e_off)
+    for a, b in zip(outs["on"][3], outs["off"][3]):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
