@@ -16,7 +16,8 @@ using c10::optional;
 #define CML_CHECK_HIP(expr)                                                               \
   do {                                                                                    \
     hipError_t _e = (expr);                                                               \
-    TORCH_CHECK(_e == hipSuccess, "consensusml_amd HIP error: ", hipGetErrorString(_e)); \
+    TORCH_CHECK(_e == hipSuccess, "consensusml_amd HIP error: ", hipGetErrorString(_e), " at " \
+                #expr " (bindings.cpp:", __LINE__, ")");                                  \
   } while (0)
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
@@ -896,7 +897,8 @@ std::vector<Tensor> conv3x3_bn_fwd(const Tensor& x, const Tensor& w_in, const op
 // x [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 3, 3] in `dtype` (channels_last memory); pro_sc / pro_bi
 // (fp32 [Ci]): x replaced by max(x sc + bi, 0) (zero padding after the transform).
 Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
-                const optional<Tensor>& pro_sc, const optional<Tensor>& pro_bi) {
+                const optional<Tensor>& pro_sc, const optional<Tensor>& pro_bi,
+                const optional<Tensor>& zero_in, bool tap_mode) {
   check_nhwc(x, "x");
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc(dy, "dy");
@@ -904,13 +906,36 @@ Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
                   dy.size(3) == x.size(3), "wgrad3x3: dy / x shapes");
   TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "wgrad3x3: bf16 or fp32 output");
   const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1);
-  TORCH_CHECK(Ci == 64 ? (Co == 64 || Co % 256 == 0) : (Co % 128 == 0 && Ci % 128 == 0),
-              "wgrad3x3: unsupported channel counts");
   const float* sc = opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", Ci);
   const float* bi = opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", Ci);
   TORCH_CHECK((sc == nullptr) == (bi == nullptr), "wgrad3x3: pro_sc and pro_bi together");
   const c10::DeviceGuard guard(x.device());
-  int TM, TN, S = 1, cps = 1;
+  int S = 1, T = 0;
+  if (!sc && !tap_mode &&
+      cml::wgrad3x3_direct_plan(static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
+                                static_cast<int>(Co), static_cast<int>(Ci), &S, &T)) {
+    // all nine taps per workgroup (wgrad3x3.hip); dW in the channels_last order of [Co, Ci, 3, 3]
+    Tensor zero;
+    if (zero_in.has_value() && zero_in->defined()) {
+      zero = *zero_in;
+      TORCH_CHECK(zero.is_cuda() && zero.device() == x.device() && zero.scalar_type() == at::kBFloat16 &&
+                      zero.is_contiguous() && zero.numel() >= 8, "wgrad3x3: zero must be >= 8 bf16");
+    } else {
+      zero = at::zeros({64}, x.options());
+    }
+    Tensor part = at::empty({S, Co, 9, Ci}, x.options().dtype(at::kFloat));
+    Tensor dw = at::empty({Co, 3, 3, Ci}, x.options().dtype(dtype));
+    CML_CHECK_HIP(cml::launch_wgrad3x3_direct(dy.data_ptr(), x.data_ptr(), zero.data_ptr(),
+                                              part.data_ptr<float>(), dw.data_ptr(),
+                                              dtype == at::kBFloat16, static_cast<int>(N),
+                                              static_cast<int>(H), static_cast<int>(W),
+                                              static_cast<int>(Co), static_cast<int>(Ci),
+                                              cur_stream()));
+    return dw.permute({0, 3, 1, 2});
+  }
+  TORCH_CHECK(Ci == 64 ? (Co == 64 || Co % 256 == 0) : (Co % 128 == 0 && Ci % 128 == 0),
+              "wgrad3x3: unsupported channel counts");
+  int TM, TN, cps = 1;
   cml::wgrad3x3_plan(N * H * W, static_cast<int>(Co), static_cast<int>(Ci), &TM, &TN, &S, &cps);
   Tensor part = at::empty({S, 9, Co, Ci}, x.options().dtype(at::kFloat));
   Tensor dw = at::empty({3, 3, Co, Ci}, x.options().dtype(dtype));
@@ -1474,7 +1499,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
   m.def("wgrad3x3", &wgrad3x3, py::arg("dy"), py::arg("x"), py::arg("dtype"),
         py::arg("pro_sc") = py::none(), py::arg("pro_bi") = py::none(),
-        "weight gradient of a 3x3 stride-1 conv (MFMA, split-K, one tap per grid z)");
+        py::arg("zero") = py::none(), py::arg("tap_mode") = false,
+        "weight gradient of a 3x3 stride-1 conv (MFMA, split-K): all nine taps per workgroup "
+        "(wgrad3x3.hip) where the plan fits, else / with a prologue / tap_mode one tap per grid z");
+  m.def("wgrad3x3_direct_ok", [](int64_t B, int64_t H, int64_t W, int64_t Co, int64_t Ci) {
+    int S, T;
+    return cml::wgrad3x3_direct_plan(static_cast<int>(B), static_cast<int>(H), static_cast<int>(W),
+                                     static_cast<int>(Co), static_cast<int>(Ci), &S, &T);
+  }, "whether wgrad3x3 takes the nine-tap kernel for this shape");
   m.def("conv_gemm", &conv_gemm, py::arg("x"), py::arg("w"), py::arg("taps"),
         py::arg("zero") = py::none(), "implicit-GEMM NHWC conv (1x1 / 3x3 stride 1), glds staging");
   m.def("conv1x1_bn_stats_only", &conv1x1_bn_stats_only, py::arg("x"), py::arg("w"),

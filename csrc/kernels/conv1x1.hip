@@ -267,7 +267,8 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
   // EL / SM_BNBWD operands of the read-back rows are issued as one batch before they are needed
   // (a 1-2 k-step GEMM was otherwise bound by these dependent loads, one latency per row pair):
   // all 8 rows at once with one operand (EL), in batches of 4 with two, halved again at MT = 2
-  // (more registers would spill). Rows past M re-read row m0.
+  // (more registers would spill). Rows past M re-read row M - 1 (a wave block of a partial tile
+  // can start past M).
   constexpr bool LD = EL || SM == SM_BNBWD || SM == SM_BNRES;
   constexpr int RB = ((EL && SM == SM_BNBWD) ? 4 : 8) / MT /   // rows per batch
                      ((SM == SM_BNRES && MT == 2) ? 2 : 1);
@@ -291,7 +292,7 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
 #pragma unroll
     for (int k = 0; k < RB; ++k) {
       const int p = 8 * (k0 + k) + (lane >> 3);
-      const int64_t row = m0 + p < a.M ? m0 + p : m0;
+      const int64_t row = m0 + p < a.M ? m0 + p : a.M - 1;
       const int64_t e0 = row * a.N + n0 + ncol0 + 8 * c;
       if constexpr (EL) {
         lv[k] = *reinterpret_cast<const uint4*>(a.link + e0);

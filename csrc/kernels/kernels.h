@@ -261,6 +261,17 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
 // 3x3 / stride 1 / padding 1 weight gradient on the same kernel (one tap per grid z): dy [P][Co],
 // x [P][Ci] NHWC with P = Nimg H W -> dw [9][Co][Ci] (tap = 3 (dy + 1) + dx + 1), optional BN +
 // ReLU prologue on x. Co % 128 == 0 and Ci % 128 == 0, or Ci == 64 with Co == 64 or Co % 256 == 0.
+// dW = sum of S fp32 partial slabs of n floats (n % 4 == 0), fixed order, bf16 or fp32 out.
+hipError_t launch_wgrad_fold(const float* part, int S, int64_t n, void* out, bool out_bf16,
+                             hipStream_t st);
+// 3x3 / stride 1 / padding 1 weight gradient with all nine taps per workgroup (wgrad3x3.hip):
+// dy [B][H][W][Co], x [B][H][W][Ci] bf16, zero: >= 8 zero bf16, part: splits x Co x 9 x Ci floats,
+// dw [Co][3][3][Ci] (bf16 or fp32). Co % 64 == 0, Ci == 64 or Ci % 128 == 0; the plan also needs a
+// chunk geometry that fits LDS (false: use wgrad3x3 / the library).
+bool wgrad3x3_direct_plan(int B, int H, int W, int Co, int Ci, int* splits, int* tci);
+hipError_t launch_wgrad3x3_direct(const void* dy, const void* x, const void* zero, float* part,
+                                  void* dw, bool dw_bf16, int B, int H, int W, int Co, int Ci,
+                                  hipStream_t st);
 void wgrad3x3_plan(int64_t P, int Co, int Ci, int* TM, int* TN, int* splits, int* cps);
 hipError_t launch_wgrad3x3(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
                            int Nimg, int H, int W, int Co, int Ci, const float* pro_sc,

@@ -507,6 +507,15 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
   return hipGetLastError();
 }
 
+hipError_t launch_wgrad_fold(const float* part, int S, int64_t n, void* out, bool out_bf16,
+                             hipStream_t st) {
+  if (S < 1 || n % 4) return hipErrorInvalidValue;
+  const int fb = static_cast<int>((n / 4 + 255) / 256);
+  if (out_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, out);
+  else wgrad1x1_fold_kernel<false><<<fb, 256, 0, st>>>(part, S, n, out);
+  return hipGetLastError();
+}
+
 // 3x3 / stride 1 / padding 1 weight gradient: dy [P][Co], x [P][Ci] (same H x W), dw [9][Co][Ci]
 // (tap-major). Tiles as the 1x1 kernel with Co x Ci; 128 x 128 tiles when Co and Ci allow (the 9
 // taps already multiply the workgroup count).

@@ -55,7 +55,7 @@ def test_conv1x1_bnbwd(cuda, N, K, No, H):
 
 @pytest.mark.parametrize("sums", [False, True])
 @pytest.mark.parametrize("N,K,No,H", [(2, 64, 256, 28), (2, 128, 512, 14), (3, 256, 1024, 7),
-                                      (2, 512, 2048, 7)])
+                                      (2, 512, 2048, 7), (1, 128, 512, 2)])
 def test_conv1x1_link(cuda, sums, N, K, No, H):
     g0 = torch.Generator(device=cuda).manual_seed(1)
     x = _nhwc(torch.randn(N, K, H, H, device=cuda, generator=g0).bfloat16())
@@ -176,7 +176,9 @@ def test_identity_chain_fused_vs_unfused(cuda, planes, H):
 
 # ---- recompute tail (ops.conv._RecomputeTailFn): kernels and the whole chain ----
 
-@pytest.mark.parametrize("N,K,H", [(2, 64, 28), (3, 128, 14), (2, 128, 9)])
+# (1, 128, 3): M = 9 pixels, so whole wave blocks of the tile start past M (their epilogue operand
+# loads must stay inside the tensors)
+@pytest.mark.parametrize("N,K,H", [(2, 64, 28), (3, 128, 14), (2, 128, 9), (1, 128, 3)])
 def test_stats_only_and_bnres_match_stored_path(cuda, N, K, H):
     """The statistics-only pass gives conv1x1_bn_fwd's statistics bit for bit, and the recompute
     apply gives bn_fwd(z3, res)'s output and mask (same bf16 z3, same plan)."""

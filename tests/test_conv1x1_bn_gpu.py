@@ -295,6 +295,39 @@ def test_conv3x3_bn_stats_vs_fp32(cuda, C, Co, H, N):
     assert float((conv.weight.grad.float() - wr.grad).norm() / wr.grad.norm()) < 1e-2
 
 
+@pytest.mark.parametrize("C,Co,H,N", [(64, 64, 9, 4), (128, 128, 6, 4), (256, 256, 5, 4),
+                                      (64, 256, 5, 4), (64, 64, 56, 2), (128, 128, 28, 2),
+                                      (256, 256, 14, 3), (512, 512, 7, 4), (64, 128, 16, 3),
+                                      (128, 256, 20, 2), (256, 128, 30, 1), (128, 64, 7, 3)])
+@pytest.mark.parametrize("mode", ["direct", "tap"])
+def test_wgrad3x3_vs_fp32(cuda, C, Co, H, N, mode):
+    """3x3 weight gradient, nine taps per workgroup (wgrad3x3.hip: single-row to multi-image
+    chunks, halo rows at image edges, channel tiles) or one tap per grid z (wgrad1x1.hip TAP), vs
+    the fp32 convolution weight gradient."""
+    from consensusml_amd.ops.native import lib
+    L = lib()
+    direct = L.wgrad3x3_direct_ok(N, H, H, Co, C)
+    if mode == "tap" and not (C == 64 and (Co == 64 or Co % 256 == 0) or
+                              (C % 128 == 0 and Co % 128 == 0)):
+        pytest.skip("channel counts of the TAP kernel")
+    if mode == "direct":
+        assert direct, (N, H, Co, C)
+    g0 = torch.Generator(device=cuda).manual_seed(12)
+    x = torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    gy = torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    zero = torch.zeros(64, dtype=torch.bfloat16, device=cuda)
+    dw = L.wgrad3x3(gy, x, torch.float32, None, None, zero, mode == "tap")
+    w = torch.zeros(Co, C, 3, 3, device=cuda)
+    ref = torch.ops.aten.convolution_backward(gy.float(), x.float(), w, None, [1, 1], [1, 1],
+                                              [1, 1], False, [0, 0], 1, [False, True, False])[1]
+    assert float((dw.float() - ref).norm() / ref.norm()) < 1e-5 * (N * H * H) ** 0.5 + 1e-4
+    dwb = L.wgrad3x3(gy, x, torch.bfloat16, None, None, zero, mode == "tap")
+    assert dwb.dtype == torch.bfloat16
+    assert float((dwb.float() - ref).norm() / ref.norm()) < 5e-3
+
+
 @pytest.mark.parametrize("C,Co,H", [(64, 64, 9), (128, 128, 6), (256, 256, 5), (64, 256, 5)])
 @pytest.mark.parametrize("pro", [False, True])
 def test_wgrad3x3_tap_vs_fp32(cuda, C, Co, H, pro):

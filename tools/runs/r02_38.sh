@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 2, GPU pass 38 (epilogue row clamp fix): full GPU suite, default bench (driver contract), step profile.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+O=$R/gpurun_out
+rm -rf $O/r02_38_* $O/raw38
+AMD_SERIALIZE_KERNEL=3 timeout -k 10 300 python -u -m pytest tests/test_bench_contract_gpu.py tests/test_bwd_fusion_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/r02_38_contract.txt 2>&1 || { tail -40 $O/r02_38_contract.txt; exit 1; }
+tail -1 $O/r02_38_contract.txt
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/r02_38_gputests.txt 2>&1 || { tail -40 $O/r02_38_gputests.txt; exit 1; }
+tail -1 $O/r02_38_gputests.txt
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/r02_38_smoke.log 2>&1 || { tail -20 $O/r02_38_smoke.log; exit 1; }
+tail -1 $O/r02_38_smoke.log
+timeout -k 10 500 python -u bench.py > $O/r02_38_bench.log 2>&1 || { tail -20 $O/r02_38_bench.log; exit 1; }
+grep '^{' $O/r02_38_bench.log > $O/r02_38_bench.json
+cut -c1-300 $O/r02_38_bench.json
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace -d $O/raw38 -o run -- python3 $R/bench.py --steps 6 --warmup 2 --no-baseline --virtual-workers 0 --profile-marker > $O/r02_38_prof.log 2>&1 || { tail -20 $O/r02_38_prof.log; exit 1; }
+db=$(find $O/raw38 -name '*.db' -print -quit)
+python3 $R/tools/prof_summary.py "$db" --after spin_kernel --steps 6 --top 90 --out $O/r02_38_kernels.md
+rm -rf $O/raw38
+python3 $R/tools/kernel_classes.py $O/r02_38_kernels.md
