@@ -23,6 +23,7 @@ Gradients: data gradient as a hipBLASLt GEMM (stride 1, per-shape policy of
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -434,10 +435,25 @@ def _zero_row(device: torch.device) -> torch.Tensor:
     return z
 
 
+# 3x3 weight gradients on csrc/kernels/wgrad3x3.hip (nine taps per workgroup): 1.4-2.0x faster
+# than MIOpen's at the ResNet-50 shapes (profiles/r02_wgrad3x3_39.jsonl)
+OWN_WGRAD3X3 = os.environ.get("CML_WGRAD3X3", "1") == "1"
+
+
+def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    N, Ci, H, W = x.shape
+    Co = dy.shape[1]
+    if OWN_WGRAD3X3 and lib().wgrad3x3_direct_ok(N, H, W, Co, Ci):
+        return lib().wgrad3x3(dy, x, w.dtype, None, None, _zero_row(dy.device), False)
+    return torch.ops.aten.convolution_backward(
+        dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+
+
 class _Conv3x3Fn(torch.autograd.Function):
-    """3x3 / stride 1 / padding 1 conv: forward and weight gradient on MIOpen, data gradient on
-    ``conv_gemm.hip`` (the forward implicit GEMM of dy with the rotated, transposed weights; 15-27 %
-    faster than MIOpen's backward-data at the ResNet-50 shapes, profiles/r02_conv_gemm24/)."""
+    """3x3 / stride 1 / padding 1 conv: forward on MIOpen, data gradient on ``conv_gemm.hip`` (the
+    forward implicit GEMM of dy with the rotated, transposed weights; 15-27 % faster than MIOpen's
+    backward-data at the ResNet-50 shapes, profiles/r02_conv_gemm24/), weight gradient on
+    ``wgrad3x3.hip``."""
 
     @staticmethod
     def forward(ctx, x, w):
@@ -455,8 +471,7 @@ class _Conv3x3Fn(torch.autograd.Function):
             wr = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co).contiguous()
             dx = lib().conv_gemm(dy, wr, 9, _zero_row(dy.device))
         if ctx.needs_input_grad[1]:
-            _, dw, _ = torch.ops.aten.convolution_backward(
-                dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])
+            dw = _wgrad3x3(dy, x, w)
         return dx, dw
 
 
