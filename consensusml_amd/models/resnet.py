@@ -210,7 +210,27 @@ class Conv1x1(nn.Conv2d):
         if fwd_gemm or dgrad_gemm or own:
             return _Conv1x1Fn.apply(x, self.weight, res_link if dgrad_gemm else None, fwd_gemm,
                                     dgrad_gemm, own)
+        if self.stride == (2, 2) and torch.is_grad_enabled() and fconv.wgrad1x1_s2_ok(x, self.weight):
+            return _Conv1x1S2Fn.apply(x, self.weight)
         return super().forward(x)
+
+
+class _Conv1x1S2Fn(torch.autograd.Function):
+    """Stride-2 1x1 (downsample) conv: forward and data gradient on MIOpen, weight gradient on
+    ``wgrad1x1.hip`` (x gathered at the even pixels, ``ops.conv._wgrad``)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return F.conv2d(x, w, stride=2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = fconv._dgrad(dy, x, w, 2, False, None) if ctx.needs_input_grad[0] else None
+        dw = fconv._wgrad(dy, x, w, 2, False) if ctx.needs_input_grad[1] else None
+        return dx, dw
 
 
 class _GlobalAvgPoolFn(torch.autograd.Function):
@@ -298,6 +318,8 @@ class Bottleneck(nn.Module):
         fuse3 = fused_conv1x1_policy(planes, planes * 4, hw2, 1, True)
         if fuse3 and CONV3X3_BN_STATS and OWN_DGRAD3X3 and fconv.conv3x3_ok(out, self.conv2):
             z2, st2 = fconv.conv3x3_bn_stats(out, self.conv2, self.bn2)
+        elif fuse3 and fconv.conv3x3_s2_ok(out, self.conv2):
+            z2, st2 = fconv.conv3x3_s2_bn_stats(out, self.conv2, self.bn2)
         else:
             z2 = self._conv2(out)
             st2 = fconv.bn_stats(z2, self.bn2) if fuse3 else None

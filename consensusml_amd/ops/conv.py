@@ -82,12 +82,28 @@ def masked_link_dgrad(dy: torch.Tensor, w: torch.Tensor, mg: MaskedGrad, link) -
     return lib().conv1x1_link(dy, wt, mg.g, mg.mask)[0]
 
 
+# stride-2 1x1 (downsample) weight gradients on wgrad1x1.hip (x gathered at the even pixels).
+# Off by default: 0.78-0.80 ms vs MIOpen's 0.63-0.74 at the three ResNet-50 shapes, step within
+# noise (profiles/r02_stride2_43.jsonl, profiles/r02_stride2_42.txt)
+OWN_WGRAD1X1_S2 = os.environ.get("CML_WGRAD1X1_S2", "0") == "1"
+
+
+def wgrad1x1_s2_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    Co, Ci = w.shape[0], w.shape[1]
+    return (OWN_WGRAD1X1_S2 and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and ((Co == 64 and Ci == 64) or (Ci == 64 and Co % 256 == 0)
+                 or (Co % 128 == 0 and Ci % 128 == 0)))
+
+
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, own: bool,
            pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """dW of a 1x1 conv. ``pro`` = (sc, bi): the conv's real input is max(x * sc + bi, 0)."""
     if own and stride == 1:
         sc, bi = pro if pro is not None else (None, None)
         return lib().wgrad1x1(dy, x, w.dtype, sc, bi).view_as(w)
+    if stride == 2 and pro is None and wgrad1x1_s2_ok(x, w):
+        return lib().wgrad1x1_s2(dy, x, w.dtype)
     if pro is not None:   # library weight gradient needs the materialised input
         sc, bi = pro
         x = torch.relu(x.float() * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)).to(x.dtype)
@@ -494,6 +510,52 @@ class _Conv3x3BNStatsFn(torch.autograd.Function):
     def backward(ctx, dy, _dm, _di):
         dx, dw = _Conv3x3Fn.backward(ctx, dy)
         return dx, dw, None, None, None, None
+
+
+class _Conv3x3S2BNStatsFn(torch.autograd.Function):
+    """(z, mean, invstd) of a stride-2 3x3 conv (ResNet-50 v1.5 downsampling blocks) on
+    ``conv_gemm.hip`` with the next BN's statistics in its epilogue; backward on MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w, rmean, rvar, eps, momentum):
+        Co, Ci = w.shape[0], w.shape[1]
+        wf = w.permute(0, 2, 3, 1).reshape(Co, 9 * Ci).contiguous()
+        y, mean, invstd = lib().conv_gemm_bn(x, wf, 9, _zero_row(x.device), rmean, rmean, rvar,
+                                             eps, momentum, 2)
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(mean, invstd)
+        return y, mean, invstd
+
+    @staticmethod
+    def backward(ctx, dy, _dm, _di):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx, dw, _ = torch.ops.aten.convolution_backward(
+            dy, x, w, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
+            [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        return dx, dw, None, None, None, None
+
+
+# stride-2 3x3 forward on conv_gemm with the BN statistics epilogue instead of MIOpen + a
+# statistics pass. Off by default: 0.85 / 0.59 / 0.57 ms vs 0.83 / 0.65 / 0.58 (layers 2 / 3 / 4),
+# step within noise (profiles/r02_stride2_43.jsonl)
+OWN_CONV3X3_S2 = os.environ.get("CML_CONV3X3_S2", "0") == "1"
+
+
+def conv3x3_s2_ok(x: torch.Tensor, conv) -> bool:
+    return (OWN_CONV3X3_S2 and x.is_cuda and x.dtype == torch.bfloat16
+            and conv.weight.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and conv.kernel_size == (3, 3)
+            and conv.stride == (2, 2) and conv.padding == (1, 1) and conv.dilation == (1, 1)
+            and conv.groups == 1 and conv.bias is None and conv.in_channels % 64 == 0
+            and conv.out_channels % 64 == 0)
+
+
+def conv3x3_s2_bn_stats(x: torch.Tensor, conv, bn):
+    """(z, (mean, invstd)) of a stride-2 3x3 ``conv(x)`` and bn's training statistics."""
+    z, m, i = _Conv3x3S2BNStatsFn.apply(x, conv.weight, bn.running_mean, bn.running_var, bn.eps,
+                                        bn.momentum)
+    return z, (m, i)
 
 
 def conv3x3_bn_stats(x: torch.Tensor, conv, bn):

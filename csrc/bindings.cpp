@@ -893,6 +893,31 @@ std::vector<Tensor> conv3x3_bn_fwd(const Tensor& x, const Tensor& w_in, const op
   return {y, mean, invstd};
 }
 
+// Weight gradient of a stride-2 1x1 conv (downsample): dy [N, Co, ceil(H/2), ceil(W/2)], x
+// [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 1, 1] in `dtype`.
+Tensor wgrad1x1_s2(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype) {
+  check_nhwc(x, "x");
+  Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(dy, "dy");
+  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1);
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(0) == N && dy.size(2) == (H + 1) / 2 &&
+                  dy.size(3) == (W + 1) / 2, "wgrad1x1_s2: dy / x shapes");
+  TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "wgrad1x1_s2: bf16 or fp32 output");
+  TORCH_CHECK((Co == 64 && Ci == 64) || (Ci == 64 ? Co % 256 == 0 : (Co % 128 == 0 && Ci % 128 == 0)),
+              "wgrad1x1_s2: unsupported channel counts");
+  const c10::DeviceGuard guard(x.device());
+  const int S = cml::wgrad1x1_s2_splits(static_cast<int>(N), static_cast<int>(H),
+                                        static_cast<int>(W), static_cast<int>(Co),
+                                        static_cast<int>(Ci));
+  Tensor part = at::empty({S, Co, Ci}, x.options().dtype(at::kFloat));
+  Tensor dw = at::empty({Co, Ci, 1, 1}, x.options().dtype(dtype));
+  CML_CHECK_HIP(cml::launch_wgrad1x1_s2(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(),
+                                        dw.data_ptr(), dtype == at::kBFloat16, static_cast<int>(N),
+                                        static_cast<int>(H), static_cast<int>(W),
+                                        static_cast<int>(Co), static_cast<int>(Ci), cur_stream()));
+  return dw;
+}
+
 // Weight gradient of a 3x3 / stride 1 / padding 1 conv (wgrad1x1.hip TAP): dy [N, Co, H, W],
 // x [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 3, 3] in `dtype` (channels_last memory); pro_sc / pro_bi
 // (fp32 [Ci]): x replaced by max(x sc + bi, 0) (zero padding after the transform).
@@ -948,7 +973,8 @@ Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
 
 // Implicit-GEMM conv (conv_gemm.hip): x [N, C, H, W] NHWC bf16, w [Cout, taps * C] contiguous
 // bf16 (k = tap C + c), taps 1 or 9 (3x3, padding 1) -> y [N, Cout, H, W] NHWC.
-Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps, const optional<Tensor>& zero_in) {
+Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps, const optional<Tensor>& zero_in,
+                 int64_t stride) {
   check_nhwc(x, "x");
   TORCH_CHECK(x.dim() == 4, "conv_gemm: 4-D NHWC input");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -956,9 +982,11 @@ Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps, const optional<
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 &&
                   w.size(1) == taps * C && w.size(0) % 64 == 0 && C % 64 == 0,
               "conv_gemm: w must be contiguous bf16 [Cout, taps * C], channels multiples of 64");
+  TORCH_CHECK(stride == 1 || stride == 2, "conv_gemm: stride 1 or 2");
   const int64_t Co = w.size(0);
   const c10::DeviceGuard guard(x.device());
-  Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor y = at::empty({N, Co, (H - 1) / stride + 1, (W - 1) / stride + 1},
+                       x.options().memory_format(at::MemoryFormat::ChannelsLast));
   // zero row for padded taps: pass a cached >= 64-element zero bf16 tensor to skip the per-call fill
   Tensor zero;
   if (zero_in.has_value() && zero_in->defined()) {
@@ -971,7 +999,9 @@ Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps, const optional<
   CML_CHECK_HIP(cml::launch_conv_gemm(x.data_ptr(), w.data_ptr(), y.data_ptr(), zero.data_ptr(),
                                       static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
                                       static_cast<int>(C), static_cast<int>(Co),
-                                      static_cast<int>(taps), cur_stream()));
+                                      static_cast<int>(taps), cur_stream(), nullptr, nullptr,
+                                      nullptr, nullptr, nullptr, nullptr, 1e-5f, 0.1f,
+                                      static_cast<int>(stride)));
   return y;
 }
 
@@ -980,7 +1010,7 @@ Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps, const optional<
 std::vector<Tensor> conv_gemm_bn(const Tensor& x, const Tensor& w, int64_t taps,
                                  const optional<Tensor>& zero_in, const optional<Tensor>& shift,
                                  const optional<Tensor>& rmean, const optional<Tensor>& rvar,
-                                 double eps, double momentum) {
+                                 double eps, double momentum, int64_t stride) {
   check_nhwc(x, "x");
   TORCH_CHECK(x.dim() == 4, "conv_gemm_bn: 4-D NHWC input");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -988,10 +1018,12 @@ std::vector<Tensor> conv_gemm_bn(const Tensor& x, const Tensor& w, int64_t taps,
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 &&
                   w.size(1) == taps * C && w.size(0) % 64 == 0 && C % 64 == 0,
               "conv_gemm_bn: w must be contiguous bf16 [Cout, taps * C], channels multiples of 64");
-  const int64_t Co = w.size(0), M = N * H * W;
+  TORCH_CHECK(stride == 1 || stride == 2, "conv_gemm_bn: stride 1 or 2");
+  const int64_t OH = (H - 1) / stride + 1, OW = (W - 1) / stride + 1;
+  const int64_t Co = w.size(0), M = N * OH * OW;
   const c10::DeviceGuard guard(x.device());
   auto f32 = x.options().dtype(at::kFloat);
-  Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor y = at::empty({N, Co, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor zero;
   if (zero_in.has_value() && zero_in->defined()) {
     zero = *zero_in;
@@ -1009,7 +1041,7 @@ std::vector<Tensor> conv_gemm_bn(const Tensor& x, const Tensor& w, int64_t taps,
       opt_ptr<const float>(shift, at::kFloat, "shift", Co), mean.data_ptr<float>(),
       invstd.data_ptr<float>(), opt_ptr<float>(rmean, at::kFloat, "running_mean", Co),
       opt_ptr<float>(rvar, at::kFloat, "running_var", Co), static_cast<float>(eps),
-      static_cast<float>(momentum)));
+      static_cast<float>(momentum), static_cast<int>(stride)));
   return {y, mean, invstd};
 }
 
@@ -1502,13 +1534,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("zero") = py::none(), py::arg("tap_mode") = false,
         "weight gradient of a 3x3 stride-1 conv (MFMA, split-K): all nine taps per workgroup "
         "(wgrad3x3.hip) where the plan fits, else / with a prologue / tap_mode one tap per grid z");
+  m.def("wgrad1x1_s2", &wgrad1x1_s2, py::arg("dy"), py::arg("x"), py::arg("dtype"),
+        "weight gradient of a stride-2 1x1 conv (MFMA, split-K, x gathered at even pixels)");
   m.def("wgrad3x3_direct_ok", [](int64_t B, int64_t H, int64_t W, int64_t Co, int64_t Ci) {
     int S, T;
     return cml::wgrad3x3_direct_plan(static_cast<int>(B), static_cast<int>(H), static_cast<int>(W),
                                      static_cast<int>(Co), static_cast<int>(Ci), &S, &T);
   }, "whether wgrad3x3 takes the nine-tap kernel for this shape");
   m.def("conv_gemm", &conv_gemm, py::arg("x"), py::arg("w"), py::arg("taps"),
-        py::arg("zero") = py::none(), "implicit-GEMM NHWC conv (1x1 / 3x3 stride 1), glds staging");
+        py::arg("zero") = py::none(), py::arg("stride") = 1,
+        "implicit-GEMM NHWC conv (1x1 / 3x3 padding 1, stride 1 or 2), glds staging");
   m.def("conv1x1_bn_stats_only", &conv1x1_bn_stats_only, py::arg("x"), py::arg("w"),
         py::arg("pro_sc"), py::arg("pro_bi"), py::arg("shift") = py::none(),
         py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
@@ -1525,7 +1560,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_gemm_bn", &conv_gemm_bn, py::arg("x"), py::arg("w"), py::arg("taps"),
         py::arg("zero") = py::none(), py::arg("shift") = py::none(),
         py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
-        py::arg("eps") = 1e-5, py::arg("momentum") = 0.1,
+        py::arg("eps") = 1e-5, py::arg("momentum") = 0.1, py::arg("stride") = 1,
         "implicit-GEMM conv + BN statistics of the output in the epilogue -> {y, mean, invstd}");
   m.def("conv3x3_bn_fwd", &conv3x3_bn_fwd, "3x3/s1/p1 conv (implicit GEMM) + BN statistics");
   m.def("conv1x1_bnbwd", &conv1x1_bnbwd, "1x1 data gradient through a BN + ReLU backward prologue");

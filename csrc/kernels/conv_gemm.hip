@@ -1,4 +1,4 @@
-// Implicit-GEMM NHWC convolution, stride 1, 1x1 or 3x3 (padding 1), on MFMA with both operands
+// Implicit-GEMM NHWC convolution, stride 1 or 2, 1x1 or 3x3 (padding 1), on MFMA with both operands
 // staged by global_load_lds into two LDS buffers:
 //
 //   y[m][n] = sum_{tap, c} x[src(m, tap)][c] * w[n][tap * C + c]
@@ -41,7 +41,8 @@ struct GArgs {
   const uint16_t* zero;   // >= 64 zero elements
   float* part;            // ST: [ntn][mtiles * WM][2][BN] shifted sums of the bf16 output
   const float* shift;     // ST: [N] statistics shift (the BN running mean) or null
-  int M, C, N, H, W, HW;
+  int M, C, N, H, W, HW;   // H, W: output
+  int S, IH, IW, IHW;     // stride; input height, width and pixels per image
   int KS;                 // TAPS * C / 64
   int ntn, tiles;
 };
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
     const int m = m0 + wave * (BM / NW) + 8 * i + lrow;
     if (m < a.M) {
       const int img = m / a.HW, rem = m - img * a.HW;
-      pimg[i] = img * a.HW;
+      pimg[i] = img * a.IHW;
       poh[i] = rem / a.W;
       pow_[i] = rem - poh[i] * a.W;
     } else {
@@ -99,11 +100,11 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
 #pragma unroll
     for (int i = 0; i < QA; ++i) {
       const int row = wave * (BM / NW) + 8 * i + lrow;
-      const int ih = poh[i] + dy, iw = pow_[i] + dx;
-      const bool ok = pimg[i] >= 0 && static_cast<unsigned>(ih) < static_cast<unsigned>(a.H) &&
-                      static_cast<unsigned>(iw) < static_cast<unsigned>(a.W);
+      const int ih = a.S * poh[i] + dy, iw = a.S * pow_[i] + dx;
+      const bool ok = pimg[i] >= 0 && static_cast<unsigned>(ih) < static_cast<unsigned>(a.IH) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(a.IW);
       const int c = p ^ ((row >> 1) & 7);
-      const uint16_t* src = ok ? a.x + (static_cast<int64_t>(pimg[i]) + ih * a.W + iw) * a.C +
+      const uint16_t* src = ok ? a.x + (static_cast<int64_t>(pimg[i]) + ih * a.IW + iw) * a.C +
                                      cc * kBK + 8 * c
                                : a.zero;
       __builtin_amdgcn_global_load_lds((g_void*)src,
@@ -326,10 +327,12 @@ size_t conv_gemm_part_floats(int64_t M, int N) {
 hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* zero, int Nimg,
                             int H, int W, int C, int N, int taps, hipStream_t st, float* part,
                             const float* shift, float* mean, float* invstd, float* rmean,
-                            float* rvar, float eps, float momentum) {
-  const int64_t M = static_cast<int64_t>(Nimg) * H * W;
+                            float* rvar, float eps, float momentum, int stride) {
+  if (stride != 1 && stride != 2) return hipErrorInvalidValue;
+  const int OH = (H - 1) / stride + 1, OW = (W - 1) / stride + 1;
+  const int64_t M = static_cast<int64_t>(Nimg) * OH * OW;
   if (C % kBK || N % 64 || (taps != 1 && taps != 9) || M < 1 || M >= (1ll << 31) ||
-      static_cast<int64_t>(taps) * C > 65536)
+      static_cast<int64_t>(Nimg) * H * W >= (1ll << 31) || static_cast<int64_t>(taps) * C > 65536)
     return hipErrorInvalidValue;
   GArgs a{};
   a.x = reinterpret_cast<const uint16_t*>(x);
@@ -339,9 +342,13 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
   a.M = static_cast<int>(M);
   a.C = C;
   a.N = N;
-  a.H = H;
-  a.W = W;
-  a.HW = H * W;
+  a.H = OH;
+  a.W = OW;
+  a.HW = OH * OW;
+  a.S = stride;
+  a.IH = H;
+  a.IW = W;
+  a.IHW = H * W;
   a.KS = taps * C / kBK;
   a.part = part;
   a.shift = shift;

@@ -261,6 +261,11 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
 // 3x3 / stride 1 / padding 1 weight gradient on the same kernel (one tap per grid z): dy [P][Co],
 // x [P][Ci] NHWC with P = Nimg H W -> dw [9][Co][Ci] (tap = 3 (dy + 1) + dx + 1), optional BN +
 // ReLU prologue on x. Co % 128 == 0 and Ci % 128 == 0, or Ci == 64 with Co == 64 or Co % 256 == 0.
+// Weight gradient of a stride-2 1x1 conv: dy [Nimg][ceil(IH/2)][ceil(IW/2)][Co], x
+// [Nimg][IH][IW][Ci] bf16; part: wgrad1x1_s2_splits() x Co x Ci floats; dw [Co][Ci].
+int wgrad1x1_s2_splits(int Nimg, int IH, int IW, int Co, int Ci);
+hipError_t launch_wgrad1x1_s2(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
+                              int Nimg, int IH, int IW, int Co, int Ci, hipStream_t st);
 // dW = sum of S fp32 partial slabs of n floats (n % 4 == 0), fixed order, bf16 or fp32 out.
 hipError_t launch_wgrad_fold(const float* part, int S, int64_t n, void* out, bool out_bf16,
                              hipStream_t st);
@@ -311,7 +316,7 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
                             float* part = nullptr, const float* shift = nullptr,
                             float* mean = nullptr, float* invstd = nullptr,
                             float* rmean = nullptr, float* rvar = nullptr, float eps = 1e-5f,
-                            float momentum = 0.1f);
+                            float momentum = 0.1f, int stride = 1);
 // BN statistics from a [ntn][R][2][BN] partial slab of shifted sums (conv1x1.hip's finalize).
 // With `fold` (>= ntn * bn_part_fold_slices(R, ntn) * 2 * BN floats) a tall slab is first folded
 // to bn_part_fold_slices rows per column tile by a wide kernel.

@@ -76,7 +76,9 @@ struct DPro {
 // gathered at the tap's shifted pixel (zero in the padding, after the prologue) and the partials
 // go to part[split][tap][Co][Ci].
 struct TapGeo {
-  int H, W, HW;
+  int H, W, HW;       // output geometry (TAP: = input)
+  int S = 1;          // 2: a stride-2 1x1 conv (downsample) instead of the 3x3 taps: x pixel of
+  int IW = 0, IHW = 0;  //    output (oh, ow) is (2 oh, 2 ow) of the IH x IW input
 };
 
 template <int TM, int TN, int KC, bool PRO, int DPRO, bool TAP = false>
@@ -85,7 +87,8 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     int P, int Co, int Ci, int tiles_n, int cps, const float* __restrict__ pro_sc,
     const float* __restrict__ pro_bi, DPro dp, TapGeo tg, float* __restrict__ cs_part) {
   const int tap = TAP ? static_cast<int>(blockIdx.z) : 0;
-  const int tdy = TAP ? tap / 3 - 1 : 0, tdx = TAP ? tap - 3 * (tap / 3) - 1 : 0;
+  const int tdy = TAP && tg.S == 1 ? tap / 3 - 1 : 0;
+  const int tdx = TAP && tg.S == 1 ? tap - 3 * (tap / 3) - 1 : 0;
   constexpr int kKC = KC;                              // pixels per chunk
   constexpr int NT = (TM / 64) * (TN / 64) * 64;
   constexpr int CA = TM / 8, CB = TN / 8;            // 16-B chunks per staged row
@@ -197,6 +200,12 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
       if constexpr (TAP) {
         const int img = p / tg.HW, rem = p - img * tg.HW;
         const int oh = rem / tg.W, ow = rem - oh * tg.W;
+        if (tg.S == 2) {   // stride-2 1x1: always inside the input
+          p = img * tg.IHW + 2 * oh * tg.IW + 2 * ow;
+          bv[j] = *reinterpret_cast<const uint4*>(x + static_cast<int64_t>(p) * Ci + ci0 + 8 * ch);
+          xok |= 1u << j;
+          continue;
+        }
         const int ih = oh + tdy, iw = ow + tdx;
         const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(tg.H) &&
                         static_cast<unsigned>(iw) < static_cast<unsigned>(tg.W);
@@ -291,7 +300,7 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     }
   }
   // partial [split][Co][Ci]: lane r = ci column, register k = co row (k&3) + 8 (k>>2) + 4 h
-  float* pw = part + (static_cast<int64_t>(blockIdx.y) * (TAP ? 9 : 1) + tap) * Co * Ci;
+  float* pw = part + (static_cast<int64_t>(blockIdx.y) * gridDim.z + tap) * Co * Ci;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -514,6 +523,58 @@ hipError_t launch_wgrad_fold(const float* part, int S, int64_t n, void* out, boo
   if (out_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, out);
   else wgrad1x1_fold_kernel<false><<<fb, 256, 0, st>>>(part, S, n, out);
   return hipGetLastError();
+}
+
+// Weight gradient of a stride-2 1x1 conv (ResNet downsample): dy [Nimg][OH][OW][Co], x
+// [Nimg][IH][IW][Ci] with OH = ceil(IH / 2), OW = ceil(IW / 2); the TAP kernel with one "tap" that
+// gathers x at (2 oh, 2 ow). Same channel counts and tiles as launch_wgrad1x1.
+hipError_t launch_wgrad1x1_s2(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
+                              int Nimg, int IH, int IW, int Co, int Ci, hipStream_t st) {
+  const int OH = (IH + 1) / 2, OW = (IW + 1) / 2;
+  const int64_t P = static_cast<int64_t>(Nimg) * OH * OW;
+  if (!(Co == 64 && Ci == 64) && (Ci == 64 ? Co % 256 != 0 : (Co % 128 || Ci % 128)))
+    return hipErrorInvalidValue;
+  if (P < 1 || static_cast<int64_t>(Nimg) * IH * IW >= (1ll << 31)) return hipErrorInvalidValue;
+  int S, cps, TM, TN;
+  wgrad1x1_plan(P, Co, Ci, &S, &cps, false);
+  pick_tile(Co, Ci, &TM, &TN, false);
+  if (TM == 256 && TN == 256) TN = 128;   // (no TAP instantiation of the 1024-thread tile)
+  const int KC = chunk_of(TM, TN);
+  const int nchunk = static_cast<int>((P + KC - 1) / KC);
+  const int tiles = (Co / TM) * (Ci / TN);
+  const int waves = (TM / 64) * (TN / 64);
+  int s = (256 * 8 / waves + tiles - 1) / tiles;
+  s = s < 1 ? 1 : (s > nchunk ? nchunk : s);
+  cps = (nchunk + s - 1) / s;
+  S = (nchunk + cps - 1) / cps;
+  const int tiles_n = Ci / TN;
+  const dim3 grid((Co / TM) * tiles_n, S, 1);
+  const size_t lds = 2 * static_cast<size_t>(KC) * (TM + TN) * 2;
+  TapGeo tg{OH, OW, OH * OW};
+  tg.S = 2;
+  tg.IW = IW;
+  tg.IHW = IH * IW;
+  if (!launch_tile_tap<false>(TM, TN, grid, lds, st, reinterpret_cast<const uint16_t*>(dy),
+                              reinterpret_cast<const uint16_t*>(x), part, static_cast<int>(P), Co,
+                              Ci, tiles_n, cps, nullptr, nullptr, tg))
+    return hipErrorInvalidValue;
+  return launch_wgrad_fold(part, S, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, st);
+}
+
+// splits of launch_wgrad1x1_s2 (its partial buffer: splits x Co x Ci floats)
+int wgrad1x1_s2_splits(int Nimg, int IH, int IW, int Co, int Ci) {
+  const int64_t P = static_cast<int64_t>(Nimg) * ((IH + 1) / 2) * ((IW + 1) / 2);
+  int TM, TN;
+  pick_tile(Co, Ci, &TM, &TN, false);
+  if (TM == 256 && TN == 256) TN = 128;
+  const int KC = chunk_of(TM, TN);
+  const int nchunk = static_cast<int>((P + KC - 1) / KC);
+  const int tiles = (Co / TM) * (Ci / TN);
+  const int waves = (TM / 64) * (TN / 64);
+  int s = (256 * 8 / waves + tiles - 1) / tiles;
+  s = s < 1 ? 1 : (s > nchunk ? nchunk : s);
+  const int cps = (nchunk + s - 1) / s;
+  return (nchunk + cps - 1) / cps;
 }
 
 // 3x3 / stride 1 / padding 1 weight gradient: dy [P][Co], x [P][Ci] (same H x W), dw [9][Co][Ci]
