@@ -281,17 +281,35 @@ int gemm_variant() {
   return v;
 }
 
+// CML_CONV_GEMM_NARROW (A/B, N % 128 != 0): 0 (default) = 256 x 64, 2 buffers; 1 = 256 x 64,
+// 3 buffers; 2 = 128 x 64, 2 buffers; 3 = 128 x 64, 3 buffers
+int narrow_variant() {
+  static const int v = [] {
+    const char* e = getenv("CML_CONV_GEMM_NARROW");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <int TAPS>
 hipError_t launch_v(GArgs& a, int64_t M, hipStream_t st) {
   const bool wide = a.N % 128 == 0;
   int v = wide ? gemm_variant() : 0;
   if (v == 4 && a.N % 256) v = 2;                 // 256 x 256 tiles need N % 256 == 0
-  const int BM = !wide ? 256 : (v >= 2 ? 256 : 128), BN = v == 4 ? 256 : (wide ? 128 : 64);
+  const int BM = !wide ? (narrow_variant() >= 2 ? 128 : 256) : (v >= 2 ? 256 : 128);
+  const int BN = v == 4 ? 256 : (wide ? 128 : 64);
   a.ntn = a.N / BN;
   const int64_t tiles = (M + BM - 1) / BM * a.ntn;
   if (tiles >= (1ll << 31)) return hipErrorInvalidValue;
   a.tiles = static_cast<int>(tiles);
-  if (!wide) return launch_g<256, 64, TAPS, 2>(a, st);
+  if (!wide) {
+    switch (narrow_variant()) {
+      case 1: return launch_g<256, 64, TAPS, 3>(a, st);
+      case 2: return launch_g<128, 64, TAPS, 2>(a, st);
+      case 3: return launch_g<128, 64, TAPS, 3>(a, st);
+      default: return launch_g<256, 64, TAPS, 2>(a, st);
+    }
+  }
   switch (v) {
     case 1: return launch_g<128, 128, TAPS, 3>(a, st);
     case 2: return launch_g<256, 128, TAPS, 2>(a, st);
@@ -309,7 +327,7 @@ void tile_of(int N, int* BM, int* BN) {
   const bool wide = N % 128 == 0;
   int v = wide ? gemm_variant() : 0;
   if (v == 4 && N % 256) v = 2;
-  *BM = !wide ? 256 : (v >= 2 ? 256 : 128);
+  *BM = !wide ? (narrow_variant() >= 2 ? 128 : 256) : (v >= 2 ? 256 : 128);
   *BN = v == 4 ? 256 : (wide ? 128 : 64);
 }
 }  // namespace
