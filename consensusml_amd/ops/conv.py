@@ -228,6 +228,11 @@ def _const(n: int, v: float, device) -> torch.Tensor:
     return t
 
 
+# recompute tails: the tail BN's statistics from the Gram matrix of the conv input (computed once,
+# reused by the backward) instead of a statistics-only pass of the conv (CML_GRAM_STATS=0)
+GRAM_STATS = os.environ.get("CML_GRAM_STATS", "1") == "1"
+
+
 class _RecomputeTailFn(torch.autograd.Function):
     """Identity-block tail y = relu(bn3(conv3(relu(bn2(z2)))) + res) that never stores z3.
 
@@ -235,9 +240,12 @@ class _RecomputeTailFn(torch.autograd.Function):
     writing it and reading it back (forward apply, bn3's backward sums, conv3's two gradient
     GEMMs) is most of the tail's HBM traffic. Here:
 
-    Forward: a statistics-only pass of the fused conv (bn2 + ReLU prologue, bn3 statistics from
-    the bf16 products, nothing stored), then the same GEMM again (same plan: the same bf16 z3)
-    with bn3 + residual + ReLU applied in its epilogue (``conv1x1_bnres``, y and its bit mask).
+    Forward: bn3's statistics from y2's Gram matrix: mean = W3 sum(y2) / M, var = w^T (y2^T y2)
+    w / M - mean^2 per output channel (``wgrad1x1_ex`` mode 3 + ``bn_stats_gram``; p x p instead
+    of the 4p-channel conv, and the Gram is the one the backward needs anyway), then the GEMM with
+    bn3 + residual + ReLU applied in its epilogue (``conv1x1_bnres``, y and its bit mask).
+    CML_GRAM_STATS=0: a statistics-only pass of the conv instead (bn3 statistics of the bf16
+    products).
 
     Backward, with u = m * g (g the block-output gradient, m bn3's ReLU mask) and
     dz3 = a u + b z3 + c (bn3's backward: a = gamma invstd, b, c from its sums):
@@ -257,10 +265,19 @@ class _RecomputeTailFn(torch.autograd.Function):
         sc = g2.float() * invstd2
         bi = b2.float() - mean2 * sc
         wc = w.contiguous()
-        m3, i3 = lib().conv1x1_bn_stats_only(z, wc, sc, bi, rmean3, rmean3, rvar3, eps, momentum)
+        L = lib()
+        gram = cy = None
+        if GRAM_STATS:
+            # bn3's statistics from y2's Gram matrix (also the backward's), not a conv pass
+            gram, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
+            m3, i3 = L.bn_stats_gram(gram, cy, wc, z.numel() // z.shape[1], rmean3, rvar3, eps,
+                                     momentum)
+        else:
+            m3, i3 = L.conv1x1_bn_stats_only(z, wc, sc, bi, rmean3, rmean3, rvar3, eps, momentum)
         sc3 = g3.float() * i3
         bi3 = b3.float() - m3 * sc3
-        y, mask = lib().conv1x1_bnres(z, wc, sc, bi, sc3, bi3, res)
+        y, mask = L.conv1x1_bnres(z, wc, sc, bi, sc3, bi3, res)
+        ctx.gram = (gram, cy)
         ctx.save_for_backward(z, g2, b2, mean2, invstd2, w, sc, bi, mask, g3, m3, i3)
         ctx.res_link, ctx.out_link = res_link, out_link
         if out_link is not None:
@@ -283,7 +300,10 @@ class _RecomputeTailFn(torch.autograd.Function):
         L = lib()
         P, s = L.wgrad1x1_ex(gy, z, sc, bi, 2, mask, _const(Co, 1.0, dev), None,
                              _const(Co, 0.0, dev), True)
-        gram, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
+        gram, cy = ctx.gram
+        ctx.gram = None
+        if gram is None:
+            gram, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
         W3 = w.reshape(Co, Ci).float()
         q = i3 * ((W3 * P).sum(1) - m3 * s)
         ca, cb, cc, dg3, db3 = L.bn_bwd_coeffs(s, q, g3, m3, i3, M)
@@ -325,8 +345,18 @@ class _RecomputeDownTailFn(torch.autograd.Function):
         bi = b2.float() - mean2 * sc
         L = lib()
         w3c, wdc = w3.contiguous(), wd.contiguous()
-        m3, i3 = L.conv1x1_bn_stats_only(z, w3c, sc, bi, rm3, rm3, rv3, eps, momentum)
-        md, idd = L.conv1x1_bn_stats_only(x, wdc, None, None, rmd, rmd, rvd, eps, momentum)
+        grams = (None, None, None, None)
+        if GRAM_STATS:
+            M_ = z.numel() // z.shape[1]
+            gram3, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
+            gramd, cx = L.wgrad1x1_ex(x, x, None, None, 0, None, None, None, None, True)
+            m3, i3 = L.bn_stats_gram(gram3, cy, w3c, M_, rm3, rv3, eps, momentum)
+            md, idd = L.bn_stats_gram(gramd, cx, wdc, M_, rmd, rvd, eps, momentum)
+            grams = (gram3, cy, gramd, cx)
+        else:
+            m3, i3 = L.conv1x1_bn_stats_only(z, w3c, sc, bi, rm3, rm3, rv3, eps, momentum)
+            md, idd = L.conv1x1_bn_stats_only(x, wdc, None, None, rmd, rmd, rvd, eps, momentum)
+        ctx.grams = grams
         Co, P_, Cin = w3.shape[0], w3.shape[1], wd.shape[1]
         sc3 = g3.float() * i3
         scd = gd.float() * idd
@@ -362,8 +392,11 @@ class _RecomputeDownTailFn(torch.autograd.Function):
         one, zero = _const(Co, 1.0, dev), _const(Co, 0.0, dev)
         P3, s = L.wgrad1x1_ex(gy, z, sc, bi, 2, mask, one, None, zero, True)
         Pd, _ = L.wgrad1x1_ex(gy, x, None, None, 2, mask, one, None, zero, False)
-        gram3, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
-        gramd, cx = L.wgrad1x1_ex(x, x, None, None, 0, None, None, None, None, True)
+        gram3, cy, gramd, cx = ctx.grams
+        ctx.grams = None
+        if gram3 is None:
+            gram3, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
+            gramd, cx = L.wgrad1x1_ex(x, x, None, None, 0, None, None, None, None, True)
         W3 = w3.reshape(Co, P_).float()
         Wd = wd.reshape(Co, Cin).float()
         q3 = i3 * ((W3 * P3).sum(1) - m3 * s)

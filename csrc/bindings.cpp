@@ -675,6 +675,32 @@ std::vector<Tensor> conv1x1_link(const Tensor& x, const Tensor& w, const Tensor&
 
 // BN + ReLU backward coefficients from its sums: {ca, cb, cc} fp32 [C] with dz = ca (m ? dy : 0) +
 // cb z + cc, and {dgamma, dbeta} in gamma's dtype (bf16).
+// BN training statistics of z = y W^T (1x1 conv, W [Co, P(, 1, 1)] bf16) from y's Gram matrix G
+// [P, P] and column sums cy [P] over M rows (fp32, e.g. wgrad1x1_ex mode 3 / 0 with sums)
+// -> {mean, invstd}; running stats updated in place when given.
+std::vector<Tensor> bn_stats_gram(const Tensor& G, const Tensor& cy, const Tensor& w, int64_t M,
+                                  const optional<Tensor>& rmean, const optional<Tensor>& rvar,
+                                  double eps, double momentum) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() > 0,
+              "bn_stats_gram: contiguous bf16 weights");
+  const int64_t Co = w.size(0), P = w.numel() / Co;
+  TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kFloat && G.is_contiguous() && G.numel() == P * P,
+              "bn_stats_gram: G fp32 [P, P]");
+  const float* cp = opt_ptr<const float>(cy, at::kFloat, "cy", P);
+  TORCH_CHECK(M >= 1, "bn_stats_gram: M >= 1");
+  const c10::DeviceGuard guard(w.device());
+  auto f32 = w.options().dtype(at::kFloat);
+  Tensor mean = at::empty({Co}, f32), invstd = at::empty({Co}, f32);
+  CML_CHECK_HIP(cml::launch_bn_stats_gram(G.data_ptr<float>(), cp, w.data_ptr(), static_cast<int>(P),
+                                          static_cast<int>(Co), M, static_cast<float>(eps),
+                                          static_cast<float>(momentum), mean.data_ptr<float>(),
+                                          invstd.data_ptr<float>(),
+                                          opt_ptr<float>(rmean, at::kFloat, "running_mean", Co),
+                                          opt_ptr<float>(rvar, at::kFloat, "running_var", Co),
+                                          cur_stream()));
+  return {mean, invstd};
+}
+
 std::vector<Tensor> bn_bwd_coeffs(const Tensor& sdz, const Tensor& sdzx, const Tensor& gamma,
                                   const Tensor& mean, const Tensor& invstd, int64_t M) {
   const int64_t C = gamma.numel();
@@ -1568,6 +1594,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lmask"), py::arg("sz") = py::none(), py::arg("smask") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(),
         "1x1 data gradient + masked residual gradient (+ the consumer BN's backward sums)");
+  m.def("bn_stats_gram", &bn_stats_gram, py::arg("G"), py::arg("cy"), py::arg("w"), py::arg("M"),
+        py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
+        py::arg("eps") = 1e-5, py::arg("momentum") = 0.1,
+        "BN statistics of a 1x1 conv's output from its input's Gram matrix and column sums");
   m.def("bn_bwd_coeffs", &bn_bwd_coeffs, "BN + ReLU backward coefficients from its sums");
   m.def("bn_bwd_sums", &bn_bwd_sums, "reduction half of a BN (+ ReLU) backward");
   m.def("maxpool_bwd_sum", &maxpool_bwd_sum, "3x3/s2 max-pool backward + channel sums of dx",

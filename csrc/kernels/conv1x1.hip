@@ -680,6 +680,80 @@ __global__ __launch_bounds__(256) void conv1x1_bnbwd_finalize_kernel(
   sdzx[c] = static_cast<float>(Q * static_cast<double>(invstd[c]));
 }
 
+// BN training statistics of z = y W^T (W [Co][P] bf16: the 1x1 conv's weights) from the Gram matrix
+// G = y^T y [P][P] and the column sums cy of y over M rows (fp32: wgrad1x1_ex's products of the
+// same bf16 y the conv multiplies): mean = W cy / M, var = w^T G w / M - mean^2, in fp64. These are
+// the statistics of the fp32-accumulated products; the statistics-only conv pass they replace saw
+// the same products rounded to bf16. 8 output channels per workgroup; running statistics updated
+// as conv1x1_bn_finalize_kernel does.
+__global__ __launch_bounds__(256) void bn_stats_gram_kernel(
+    const float* __restrict__ G, const float* __restrict__ cy, const uint16_t* __restrict__ W, int P,
+    int Co, int64_t M, float eps, float momentum, float* __restrict__ mean,
+    float* __restrict__ invstd, float* __restrict__ rmean, float* __restrict__ rvar) {
+  extern __shared__ float ws[];            // [8][P] weights of this workgroup's channels
+  __shared__ double red[4][16];
+  const int n0 = blockIdx.x * 8, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int e = tid; e < 8 * P; e += 256) {
+    const int c = e / P, j = e - c * P;
+    ws[e] = n0 + c < Co ? bf2f(W[static_cast<int64_t>(n0 + c) * P + j]) : 0.f;
+  }
+  __syncthreads();
+  double q[8], sm[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    q[c] = 0.0;
+    sm[c] = 0.0;
+  }
+  for (int i = tid; i < P; i += 256) {
+    double t[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) t[c] = 0.0;
+    const float* gr = G + static_cast<int64_t>(i) * P;
+    for (int j = 0; j < P; ++j) {
+      const double g = gr[j];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) t[c] = fma(g, static_cast<double>(ws[c * P + j]), t[c]);
+    }
+    const double yi = cy[i];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const double wi = ws[c * P + i];
+      q[c] = fma(wi, t[c], q[c]);
+      sm[c] = fma(wi, yi, sm[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      q[c] += __shfl_xor(q[c], o, 64);
+      sm[c] += __shfl_xor(sm[c], o, 64);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      red[wv][c] = q[c];
+      red[wv][8 + c] = sm[c];
+    }
+  }
+  __syncthreads();
+  if (tid >= 8 || n0 + tid >= Co) return;
+  const int n = n0 + tid;
+  const double Q = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+  const double S = red[0][8 + tid] + red[1][8 + tid] + red[2][8 + tid] + red[3][8 + tid];
+  const double mu = S / static_cast<double>(M);
+  double var = Q / static_cast<double>(M) - mu * mu;
+  if (var < 0.0) var = 0.0;
+  mean[n] = static_cast<float>(mu);
+  invstd[n] = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+  if (rmean) {
+    const double unb = M > 1 ? var * static_cast<double>(M) / static_cast<double>(M - 1) : var;
+    rmean[n] = static_cast<float>((1.0 - momentum) * rmean[n] + momentum * mu);
+    rvar[n] = static_cast<float>((1.0 - momentum) * rvar[n] + momentum * unb);
+  }
+}
+
 // Per-channel coefficients of a training BN + ReLU backward, dz = a (mask ? dy : 0) + b z + c,
 // from its sums s = sum dy', q = sum dy' xhat (dy' = masked dy); also dgamma = q, dbeta = s.
 __global__ __launch_bounds__(256) void bn_bwd_coeffs_kernel(
@@ -956,6 +1030,16 @@ hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void
   if (e != hipSuccess || !sums) return e;
   conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N,
                                                              invstd, sdz, sdzx);
+  return hipGetLastError();
+}
+
+hipError_t launch_bn_stats_gram(const float* G, const float* cy, const void* w, int P, int Co,
+                                int64_t M, float eps, float momentum, float* mean, float* invstd,
+                                float* rmean, float* rvar, hipStream_t st) {
+  if (P < 1 || P > 1024 || Co < 1 || M < 1) return hipErrorInvalidValue;
+  bn_stats_gram_kernel<<<(Co + 7) / 8, 256, 8 * P * sizeof(float), st>>>(
+      G, cy, reinterpret_cast<const uint16_t*>(w), P, Co, M, eps, momentum, mean, invstd, rmean,
+      rvar);
   return hipGetLastError();
 }
 

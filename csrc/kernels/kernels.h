@@ -363,6 +363,11 @@ hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void
                                float* sdzx, int64_t M, int K, int N, hipStream_t st);
 // dz = ca (mask ? dy : 0) + cb z + cc coefficients of a training BN + ReLU backward from its sums
 // (sdz, sdzx); dgamma = sdzx, dbeta = sdz (bf16).
+// BN training statistics (mean, invstd; running stats updated when given) of z = y W^T from the
+// Gram matrix G = y^T y [P][P] and column sums cy [P] of y over M rows; W [Co][P] bf16 (conv1x1.hip).
+hipError_t launch_bn_stats_gram(const float* G, const float* cy, const void* w, int P, int Co,
+                                int64_t M, float eps, float momentum, float* mean, float* invstd,
+                                float* rmean, float* rvar, hipStream_t st);
 hipError_t launch_bn_bwd_coeffs(const float* sdz, const float* sdzx, const void* gamma,
                                 const float* mean, const float* invstd, int C, int64_t M,
                                 float* ca, float* cb, float* cc, void* dgamma, void* dbeta,

@@ -328,3 +328,31 @@ def test_downsample_recompute_tail(cuda, cin, planes, H):
         assert e_on <= 1.5 * e_off + 2e-2, (e_on, e_off)
     for a, b in zip(outs["on"][3], outs["off"][3]):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("N,K,H", [(2, 64, 28), (3, 128, 14), (2, 256, 9), (1, 128, 3)])
+def test_bn_stats_gram_vs_fp64(cuda, N, K, H):
+    """bn3's statistics from y2's Gram matrix (wgrad1x1_ex mode 3 + bn_stats_gram) equal the fp64
+    statistics of z3 = y2 W^T (y2 = relu(z sc + bi) in bf16), running stats included."""
+    g0 = torch.Generator(device=cuda).manual_seed(24)
+    Co = 4 * K
+    z = _nhwc(torch.randn(N, K, H, H, device=cuda, generator=g0).bfloat16())
+    w = (torch.randn(Co, K, 1, 1, device=cuda, generator=g0) * K ** -0.5).bfloat16()
+    sc = torch.rand(K, device=cuda, generator=g0) + 0.5
+    bi = torch.randn(K, device=cuda, generator=g0) * 0.1 + 0.2
+    gram, cy = _lib().wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
+    y2 = torch.relu(_rows(z) * sc + bi).bfloat16().double()
+    M = y2.shape[0]
+    torch.testing.assert_close(gram.double(), y2.t() @ y2, rtol=1e-5, atol=1e-3)
+    rm = torch.randn(Co, device=cuda, generator=g0) * 0.1
+    rv = torch.rand(Co, device=cuda, generator=g0) + 0.5
+    rm0, rv0 = rm.clone(), rv.clone()
+    mean, invstd = _lib().bn_stats_gram(gram, cy, w, M, rm, rv, 1e-5, 0.1)
+    z3 = y2 @ w.view(Co, K).double().t()
+    m_ref = z3.mean(0)
+    v_ref = z3.var(0, unbiased=False)
+    torch.testing.assert_close(mean.double(), m_ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(invstd.double(), torch.rsqrt(v_ref + 1e-5), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rm.double(), 0.9 * rm0.double() + 0.1 * m_ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv.double(), 0.9 * rv0.double() + 0.1 * z3.var(0, unbiased=True),
+                               rtol=1e-4, atol=1e-5)
