@@ -684,46 +684,48 @@ __global__ __launch_bounds__(256) void conv1x1_bnbwd_finalize_kernel(
 // G = y^T y [P][P] and the column sums cy of y over M rows (fp32: wgrad1x1_ex's products of the
 // same bf16 y the conv multiplies): mean = W cy / M, var = w^T G w / M - mean^2, in fp64. These are
 // the statistics of the fp32-accumulated products; the statistics-only conv pass they replace saw
-// the same products rounded to bf16. 8 output channels per workgroup; running statistics updated
+// the same products rounded to bf16. 16 output channels per workgroup; running statistics updated
 // as conv1x1_bn_finalize_kernel does.
 __global__ __launch_bounds__(256) void bn_stats_gram_kernel(
     const float* __restrict__ G, const float* __restrict__ cy, const uint16_t* __restrict__ W, int P,
     int Co, int64_t M, float eps, float momentum, float* __restrict__ mean,
     float* __restrict__ invstd, float* __restrict__ rmean, float* __restrict__ rvar) {
-  extern __shared__ float ws[];            // [8][P] weights of this workgroup's channels
-  __shared__ double red[4][16];
-  const int n0 = blockIdx.x * 8, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int e = tid; e < 8 * P; e += 256) {
+  constexpr int NC = 16;                   // output channels per workgroup
+  extern __shared__ float ws[];            // [NC][P] weights of this workgroup's channels
+  __shared__ double red[4][2 * NC];
+  const int n0 = blockIdx.x * NC, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int e = tid; e < NC * P; e += 256) {
     const int c = e / P, j = e - c * P;
     ws[e] = n0 + c < Co ? bf2f(W[static_cast<int64_t>(n0 + c) * P + j]) : 0.f;
   }
   __syncthreads();
-  double q[8], sm[8];
+  double q[NC], sm[NC];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
+  for (int c = 0; c < NC; ++c) {
     q[c] = 0.0;
     sm[c] = 0.0;
   }
+  // row i of G w (fp32 over P <= 1024 terms of one row), then w_i (G w)_i summed in fp64
   for (int i = tid; i < P; i += 256) {
-    double t[8];
+    float t[NC];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) t[c] = 0.0;
+    for (int c = 0; c < NC; ++c) t[c] = 0.f;
     const float* gr = G + static_cast<int64_t>(i) * P;
     for (int j = 0; j < P; ++j) {
-      const double g = gr[j];
+      const float g = gr[j];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) t[c] = fma(g, static_cast<double>(ws[c * P + j]), t[c]);
+      for (int c = 0; c < NC; ++c) t[c] = fmaf(g, ws[c * P + j], t[c]);
     }
     const double yi = cy[i];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < NC; ++c) {
       const double wi = ws[c * P + i];
-      q[c] = fma(wi, t[c], q[c]);
+      q[c] = fma(wi, static_cast<double>(t[c]), q[c]);
       sm[c] = fma(wi, yi, sm[c]);
     }
   }
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
+  for (int c = 0; c < NC; ++c) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
       q[c] += __shfl_xor(q[c], o, 64);
@@ -732,16 +734,16 @@ __global__ __launch_bounds__(256) void bn_stats_gram_kernel(
   }
   if (lane == 0) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < NC; ++c) {
       red[wv][c] = q[c];
-      red[wv][8 + c] = sm[c];
+      red[wv][NC + c] = sm[c];
     }
   }
   __syncthreads();
-  if (tid >= 8 || n0 + tid >= Co) return;
+  if (tid >= NC || n0 + tid >= Co) return;
   const int n = n0 + tid;
   const double Q = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-  const double S = red[0][8 + tid] + red[1][8 + tid] + red[2][8 + tid] + red[3][8 + tid];
+  const double S = red[0][NC + tid] + red[1][NC + tid] + red[2][NC + tid] + red[3][NC + tid];
   const double mu = S / static_cast<double>(M);
   double var = Q / static_cast<double>(M) - mu * mu;
   if (var < 0.0) var = 0.0;
@@ -816,6 +818,17 @@ bool mt2_enabled() {
   return on;
 }
 
+// Also take the MT = 2 tile when it lets W stay resident (without the per-wave epilogue images
+// the MT = 1 plan needs, W fits): the layer-2 recompute apply GEMM (K 128, N 512); step 133.5 ->
+// 133.1 ms (profiles/r02_c1_mt2_wres47.txt). CML_C1_MT2_WRES=0 disables it (A/B).
+bool mt2_wres_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CML_C1_MT2_WRES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 Plan make_plan(int64_t M, int K, int N, int naff, int kaff = -1, bool mt2_ok = true) {
   const int WN = N % 256 == 0 ? 4 : (N % 128 == 0 ? 2 : 1);
   Plan p = plan_for(WN, M, K, N, naff, 1, kaff);
@@ -824,7 +837,7 @@ Plan make_plan(int64_t M, int K, int N, int naff, int kaff = -1, bool mt2_ok = t
   // (not with the BN-backward prologue: its extra z / mask prefetch registers would spill)
   if (p.WN == 2 && !p.wres && naff < 3 && mt2_ok && mt2_enabled()) {
     const Plan q = plan_for(2, M, K, N, naff, 2, kaff);
-    if (!q.wres && q.lds <= 80 * 1024) p = q;
+    if ((!q.wres || mt2_wres_enabled()) && q.lds <= 80 * 1024) p = q;
   }
   return p;
 }
@@ -833,8 +846,7 @@ template <int WN, int WM, int PM, bool WRES, bool S2, bool EL = false, int SM = 
           bool TAP = false>
 hipError_t launch_t(const C1Args& a, const Plan& p, hipStream_t st) {
   auto k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 1, TAP>;
-  if constexpr (WN == 2 && !WRES && PM != PM_BNBWD && SM != SM_BNBWD &&
-                !(PM == PM_CAT && SM == SM_BNRES)) {
+  if constexpr (WN == 2 && PM != PM_BNBWD && SM != SM_BNBWD && !(PM == PM_CAT && SM == SM_BNRES)) {
     if (p.MT == 2) k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 2, TAP>;
   }
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
@@ -1036,8 +1048,11 @@ hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void
 hipError_t launch_bn_stats_gram(const float* G, const float* cy, const void* w, int P, int Co,
                                 int64_t M, float eps, float momentum, float* mean, float* invstd,
                                 float* rmean, float* rvar, hipStream_t st) {
-  if (P < 1 || P > 1024 || Co < 1 || M < 1) return hipErrorInvalidValue;
-  bn_stats_gram_kernel<<<(Co + 7) / 8, 256, 8 * P * sizeof(float), st>>>(
+  if (P < 1 || P > 2048 || Co < 1 || M < 1) return hipErrorInvalidValue;
+  if (16 * P * sizeof(float) > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bn_stats_gram_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 16 * P * 4);
+  bn_stats_gram_kernel<<<(Co + 15) / 16, 256, 16 * P * sizeof(float), st>>>(
       G, cy, reinterpret_cast<const uint16_t*>(w), P, Co, M, eps, momentum, mean, invstd, rmean,
       rvar);
   return hipGetLastError();
