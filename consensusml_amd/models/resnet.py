@@ -334,6 +334,18 @@ class Bottleneck(nn.Module):
                     y._cml_link = out_link
                 return y
             if (self.down_conv is not None and RECOMPUTE_DOWN_TAIL and self.bn3.eps ==
+                    self.down_bn.eps and fconv.down_tail_recompute_s2_ok(x, planes, self.down_conv)):
+                # stride-2 downsample tail: the stride-1 recompute kernels on x[:, :, ::2, ::2];
+                # its gradient (zero-filled full resolution) parks on conv1's link as before
+                out_link = ResidualLink() if use_links else None
+                xin = link_tap(x, dlink) if dlink is not None else x
+                y = fconv.down_tail_recompute(z2, self.bn2, st2, self.conv3, self.bn3,
+                                              fconv.subsample2(xin), self.down_conv, self.down_bn,
+                                              out_link)
+                if out_link is not None:
+                    y._cml_link = out_link
+                return y
+            if (self.down_conv is not None and RECOMPUTE_DOWN_TAIL and self.bn3.eps ==
                     self.down_bn.eps and fconv.down_tail_recompute_ok(x, planes, self.down_conv)):
                 out_link = ResidualLink() if use_links else None
                 tlink = dlink if dlink is not None else \

@@ -424,6 +424,43 @@ class _RecomputeDownTailFn(torch.autograd.Function):
             (None,) * 5
 
 
+class _Subsample2Fn(torch.autograd.Function):
+    """x[:, :, ::2, ::2] as a dense NHWC tensor (the pixels a stride-2 1x1 conv reads); backward
+    scatters the gradient back into a zero-filled full-resolution tensor."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
+            return lib().subsample2(x.contiguous(memory_format=torch.channels_last))
+        return x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
+
+    @staticmethod
+    def backward(ctx, g):
+        N, C, H, W = ctx.shape
+        if g.is_cuda and g.dtype == torch.bfloat16 and C % 8 == 0:
+            return lib().upsample2_scatter(g, H, W)
+        dx = torch.zeros(ctx.shape, dtype=g.dtype, device=g.device).contiguous(
+            memory_format=torch.channels_last)
+        dx[:, :, ::2, ::2] = g
+        return dx
+
+
+def subsample2(x: torch.Tensor) -> torch.Tensor:
+    return _Subsample2Fn.apply(x)
+
+
+def down_tail_recompute_s2_ok(x: torch.Tensor, planes: int, down_conv) -> bool:
+    """Stride-2 downsample tails (ResNet-50 layer 2) on the recompute kernels: the convolution
+    reads x[:, :, ::2, ::2], materialised once (``subsample2``), so the stride-1 kernels apply."""
+    return (RECOMPUTE_DOWN_TAIL_S2 and down_conv.stride[0] == 2 and down_conv.stride[1] == 2
+            and planes in (64, 128) and x.shape[1] % 64 == 0 and x.shape[1] <= 256)
+
+
+# CML_RECOMPUTE_DOWN_TAIL_S2=0: stride-2 downsample tails keep stored z3 / zd (bn_add_bn_relu)
+RECOMPUTE_DOWN_TAIL_S2 = os.environ.get("CML_RECOMPUTE_DOWN_TAIL_S2", "1") == "1"
+
+
 def down_tail_recompute_ok(x: torch.Tensor, planes: int, down_conv) -> bool:
     """Stride-1 downsample convs (ResNet-50 layer 1) with the recompute kernels' channel counts."""
     return (down_conv.stride[0] == 1 and planes in (64, 128) and x.shape[1] % 64 == 0

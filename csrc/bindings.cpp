@@ -575,7 +575,7 @@ std::vector<Tensor> wgrad1x1_ex(const Tensor& dy_in, const Tensor& x, const opti
   const c10::DeviceGuard guard(x.device());
   int S = 1, cps = 1;
   cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps,
-                     sc != nullptr || dmode != 0);
+                     sc != nullptr || dmode != 0 || colsum);
   auto f32 = x.options().dtype(at::kFloat);
   Tensor part = at::empty({S, Co, Ci}, f32);
   Tensor dw = at::empty({Co, Ci}, f32);
@@ -917,6 +917,35 @@ std::vector<Tensor> conv3x3_bn_fwd(const Tensor& x, const Tensor& w_in, const op
       stats ? opt_ptr<float>(rvar, at::kFloat, "running_var", Co) : nullptr,
       static_cast<float>(eps), static_cast<float>(momentum), cur_stream()));
   return {y, mean, invstd};
+}
+
+// x[:, :, ::2, ::2] of an NHWC bf16 tensor as a dense NHWC tensor, and the backward scatter
+// (full resolution, zeros at the odd pixels; H, W: the full-resolution size).
+Tensor subsample2(const Tensor& x) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(1) % 8 == 0, "subsample2: 4-D NHWC, C % 8 == 0");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const c10::DeviceGuard guard(x.device());
+  Tensor y = at::empty({N, C, (H + 1) / 2, (W + 1) / 2},
+                       x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  CML_CHECK_HIP(cml::launch_subsample2(x.data_ptr(), y.data_ptr(), static_cast<int>(N),
+                                       static_cast<int>(H), static_cast<int>(W),
+                                       static_cast<int>(C), cur_stream()));
+  return y;
+}
+
+Tensor upsample2_scatter(const Tensor& g_in, int64_t H, int64_t W) {
+  Tensor g = g_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(g, "g");
+  const int64_t N = g.size(0), C = g.size(1);
+  TORCH_CHECK(g.dim() == 4 && C % 8 == 0 && g.size(2) == (H + 1) / 2 && g.size(3) == (W + 1) / 2,
+              "upsample2_scatter: g [N, C, ceil(H/2), ceil(W/2)], C % 8 == 0");
+  const c10::DeviceGuard guard(g.device());
+  Tensor dx = at::empty({N, C, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  CML_CHECK_HIP(cml::launch_upsample2_scatter(g.data_ptr(), dx.data_ptr(), static_cast<int>(N),
+                                              static_cast<int>(H), static_cast<int>(W),
+                                              static_cast<int>(C), cur_stream()));
+  return dx;
 }
 
 // Weight gradient of a stride-2 1x1 conv (downsample): dy [N, Co, ceil(H/2), ceil(W/2)], x
@@ -1560,6 +1589,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("zero") = py::none(), py::arg("tap_mode") = false,
         "weight gradient of a 3x3 stride-1 conv (MFMA, split-K): all nine taps per workgroup "
         "(wgrad3x3.hip) where the plan fits, else / with a prologue / tap_mode one tap per grid z");
+  m.def("subsample2", &subsample2, "x[:, :, ::2, ::2] of an NHWC bf16 tensor, dense NHWC");
+  m.def("upsample2_scatter", &upsample2_scatter, py::arg("g"), py::arg("H"), py::arg("W"),
+        "full-resolution NHWC tensor with g at the even pixels, zeros elsewhere");
   m.def("wgrad1x1_s2", &wgrad1x1_s2, py::arg("dy"), py::arg("x"), py::arg("dtype"),
         "weight gradient of a stride-2 1x1 conv (MFMA, split-K, x gathered at even pixels)");
   m.def("wgrad3x3_direct_ok", [](int64_t B, int64_t H, int64_t W, int64_t Co, int64_t Ci) {

@@ -110,6 +110,11 @@ hipError_t launch_bn_bwd2(const void* dy, const void* dy2, const void* x1, const
                           float* sdzx1, float* sdz_b, float* sdzx2, void* work,
                           hipStream_t stream);
 
+// y = x[:, ::2, ::2, :] of NHWC bf16 x [N][H][W][C] (y [N][ceil(H/2)][ceil(W/2)][C]); the
+// scatter writes the full-resolution dx with g at the even pixels and zeros elsewhere. C % 8 == 0.
+hipError_t launch_subsample2(const void* x, void* y, int N, int H, int W, int C, hipStream_t st);
+hipError_t launch_upsample2_scatter(const void* g, void* dx, int N, int H, int W, int C,
+                                    hipStream_t st);
 // NHWC bf16 max-pool with a one-byte argmax per output element; backward is a gather.
 hipError_t launch_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C,
                               int OH, int OW, int k, int s, int p, hipStream_t stream);

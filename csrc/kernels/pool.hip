@@ -455,6 +455,38 @@ __global__ __launch_bounds__(256) void pad_c4_kernel(const uint16_t* __restrict_
   }
 }
 
+// Stride-2 pixel subsampling of NHWC bf16 (what a 1x1 stride-2 conv reads), and its backward: a
+// full-resolution gradient with g at the even pixels and zeros elsewhere, written in one pass.
+// 16-B vectors; C % 8 == 0.
+__global__ __launch_bounds__(256) void subsample2_kernel(const uint4* __restrict__ x,
+                                                         uint4* __restrict__ y, int64_t total,
+                                                         int C8, int OH, int OW, int H, int W) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int64_t pix = e / C8;
+  const int c = static_cast<int>(e - pix * C8);
+  const int64_t n = pix / (static_cast<int64_t>(OH) * OW);
+  const int rem = static_cast<int>(pix - n * OH * OW);
+  const int oh = rem / OW, ow = rem - oh * OW;
+  y[e] = x[((n * H + 2 * oh) * W + 2 * ow) * C8 + c];
+}
+
+__global__ __launch_bounds__(256) void upsample2_scatter_kernel(const uint4* __restrict__ g,
+                                                                uint4* __restrict__ dx,
+                                                                int64_t total, int C8, int OH,
+                                                                int OW, int H, int W) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int64_t pix = e / C8;
+  const int c = static_cast<int>(e - pix * C8);
+  const int64_t n = pix / (static_cast<int64_t>(H) * W);
+  const int rem = static_cast<int>(pix - n * H * W);
+  const int h = rem / W, w = rem - h * W;
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (!(h & 1) && !(w & 1)) v = g[((n * OH + (h >> 1)) * OW + (w >> 1)) * C8 + c];
+  dx[e] = v;
+}
+
 }  // namespace
 
 // CML_POOL_BLOCKS=0 selects the one-output-per-thread forward for the stem (A/B)
@@ -464,6 +496,25 @@ static bool k3s2_blocks() {
     return !(e && e[0] == '0');
   }();
   return on;
+}
+
+hipError_t launch_subsample2(const void* x, void* y, int N, int H, int W, int C, hipStream_t st) {
+  if (C % 8 || N < 1 || H < 1 || W < 1) return hipErrorInvalidValue;
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2, C8 = C / 8;
+  const int64_t total = static_cast<int64_t>(N) * OH * OW * C8;
+  subsample2_kernel<<<static_cast<unsigned>((total + 255) / 256), 256, 0, st>>>(
+      reinterpret_cast<const uint4*>(x), reinterpret_cast<uint4*>(y), total, C8, OH, OW, H, W);
+  return hipGetLastError();
+}
+
+hipError_t launch_upsample2_scatter(const void* g, void* dx, int N, int H, int W, int C,
+                                    hipStream_t st) {
+  if (C % 8 || N < 1 || H < 1 || W < 1) return hipErrorInvalidValue;
+  const int OH = (H + 1) / 2, OW = (W + 1) / 2, C8 = C / 8;
+  const int64_t total = static_cast<int64_t>(N) * H * W * C8;
+  upsample2_scatter_kernel<<<static_cast<unsigned>((total + 255) / 256), 256, 0, st>>>(
+      reinterpret_cast<const uint4*>(g), reinterpret_cast<uint4*>(dx), total, C8, OH, OW, H, W);
+  return hipGetLastError();
 }
 
 hipError_t launch_maxpool_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C,

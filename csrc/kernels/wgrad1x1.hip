@@ -464,7 +464,7 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
     return hipErrorInvalidValue;
   {
     int tm, tn;
-    pick_tile(Co, Ci, &tm, &tn, pro_sc != nullptr || dmode != DP_NONE);
+    pick_tile(Co, Ci, &tm, &tn, pro_sc != nullptr || dmode != DP_NONE || cs != nullptr);
     if (cs && tm * tn > 32768) return hipErrorInvalidValue;   // no column sums in that tile
   }
   DPro dp{reinterpret_cast<const uint16_t*>(dz_z), dz_mask, dz_a, dz_b, dz_c};
@@ -473,7 +473,8 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
   if (P < 1 || P >= (1ll << 31)) return hipErrorInvalidValue;
   if ((pro_sc == nullptr) != (pro_bi == nullptr)) return hipErrorInvalidValue;
   int S, cps, TM, TN;
-  const bool anypro = pro_sc != nullptr || dmode != DP_NONE;
+  // (the column sums have no 1024-thread tile either: it takes the prologue tiles)
+  const bool anypro = pro_sc != nullptr || dmode != DP_NONE || cs != nullptr;
   wgrad1x1_plan(P, Co, Ci, &S, &cps, anypro);
   pick_tile(Co, Ci, &TM, &TN, anypro);
   const int KC = chunk_of(TM, TN);

@@ -287,14 +287,16 @@ def test_identity_chain_recompute_tail(cuda, planes, H):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("cin,planes,H", [(64, 64, 28), (128, 128, 14)])
-def test_downsample_recompute_tail(cuda, cin, planes, H):
-    """Stride-1 downsample block with the recompute tail (no z3 / zd) vs the stored path, both
-    against an fp32 copy: output, input gradient, parameter gradients, running statistics."""
+@pytest.mark.parametrize("cin,planes,H,stride", [(64, 64, 28, 1), (128, 128, 14, 1),
+                                                 (256, 128, 28, 2), (128, 64, 14, 2)])
+def test_downsample_recompute_tail(cuda, cin, planes, H, stride):
+    """Downsample block (stride 1, or stride 2 through ops.conv.subsample2) with the recompute
+    tail (no z3 / zd) vs the stored path, both against an fp32 copy: output, input gradient,
+    parameter gradients, running statistics."""
     from consensusml_amd.models import resnet
     from consensusml_amd.models.resnet import Bottleneck
     torch.manual_seed(3)
-    m_on = Bottleneck(cin, planes, 1, downsample=True)
+    m_on = Bottleneck(cin, planes, stride, downsample=True)
     for mod in m_on.modules():
         if mod.__class__.__name__ == "BatchNormAct2d":
             with torch.no_grad():
@@ -305,7 +307,8 @@ def test_downsample_recompute_tail(cuda, cin, planes, H):
     m32 = copy.deepcopy(m_on).float()
     g0 = torch.Generator(device=cuda).manual_seed(7)
     x = _nhwc(torch.relu(torch.randn(8, cin, H, H, device=cuda, generator=g0)).bfloat16())
-    gy = _nhwc(torch.randn(8, planes * 4, H, H, device=cuda, generator=g0).bfloat16())
+    Ho = (H - 1) // stride + 1
+    gy = _nhwc(torch.randn(8, planes * 4, Ho, Ho, device=cuda, generator=g0).bfloat16())
     outs = {}
     for key, m, dt in (("on", m_on, torch.bfloat16), ("off", m_off, torch.bfloat16),
                        ("fp32", m32, torch.float32)):
@@ -356,3 +359,23 @@ def test_bn_stats_gram_vs_fp64(cuda, N, K, H):
     torch.testing.assert_close(rm.double(), 0.9 * rm0.double() + 0.1 * m_ref, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(rv.double(), 0.9 * rv0.double() + 0.1 * z3.var(0, unbiased=True),
                                rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,C,H,W", [(2, 256, 56, 56), (3, 64, 7, 9), (1, 512, 14, 14)])
+def test_subsample2_and_scatter(cuda, N, C, H, W):
+    """subsample2 = x[:, :, ::2, ::2] (dense NHWC) and its backward scatter (zeros at odd pixels),
+    exactly; through ops.conv.subsample2's autograd too."""
+    from consensusml_amd.ops import conv as fconv
+    g0 = torch.Generator(device=cuda).manual_seed(25)
+    x = _nhwc(torch.randn(N, C, H, W, device=cuda, generator=g0).bfloat16())
+    y = _lib().subsample2(x)
+    assert torch.equal(y, x[:, :, ::2, ::2])
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    g = _nhwc(torch.randn(y.shape, device=cuda, generator=g0).bfloat16())
+    dx = _lib().upsample2_scatter(g, H, W)
+    ref = torch.zeros_like(x)
+    ref[:, :, ::2, ::2] = g
+    assert torch.equal(dx, ref)
+    xi = x.clone().requires_grad_(True)
+    fconv.subsample2(xi).backward(g)
+    assert torch.equal(xi.grad, ref)
