@@ -155,6 +155,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             g = link.take() if link is not None else None
             if isinstance(g, fconv.MaskedGrad):
                 return fconv.masked_link_dgrad(dy, w, g, link), dw, None, None, None, None
+            if isinstance(g, fconv.S2Grad):
+                g = g.materialize()
             if g is not None:
                 dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
                 if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
@@ -338,10 +340,9 @@ class Bottleneck(nn.Module):
                 # stride-2 downsample tail: the stride-1 recompute kernels on x[:, :, ::2, ::2];
                 # its gradient (zero-filled full resolution) parks on conv1's link as before
                 out_link = ResidualLink() if use_links else None
-                xin = link_tap(x, dlink) if dlink is not None else x
                 y = fconv.down_tail_recompute(z2, self.bn2, st2, self.conv3, self.bn3,
-                                              fconv.subsample2(xin), self.down_conv, self.down_bn,
-                                              out_link)
+                                              fconv.subsample2_link(x, dlink), self.down_conv,
+                                              self.down_bn, out_link)
                 if out_link is not None:
                     y._cml_link = out_link
                 return y

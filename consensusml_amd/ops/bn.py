@@ -49,9 +49,10 @@ class ResidualLink:
         return g
 
     def take_tensor(self):
-        """``take`` with a ``MaskedGrad`` materialised (consumers without a masked epilogue)."""
+        """``take`` with a ``MaskedGrad`` / ``ops.conv.S2Grad`` materialised (consumers without the
+        matching epilogue)."""
         g = self.take()
-        return g.materialize() if isinstance(g, MaskedGrad) else g
+        return g.materialize() if hasattr(g, "materialize") else g
 
 
 class MaskedGrad:

@@ -52,6 +52,13 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm
         g = link.take() if link is not None else None
         if isinstance(g, MaskedGrad):
             return masked_link_dgrad(dy, w, g, link)
+        if isinstance(g, S2Grad):
+            if (S2_LINK_DGRAD and dy.dtype == torch.bfloat16 and C % 64 == 0 and Co % 64 == 0
+                    and g.H == H and g.W == W):
+                wt = w.reshape(Co, C).t().contiguous()
+                return lib().conv1x1_link_s2(dy.contiguous(memory_format=torch.channels_last), wt,
+                                             g.g)
+            g = g.materialize()
         if g is not None:
             dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
             if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
@@ -450,6 +457,46 @@ def subsample2(x: torch.Tensor) -> torch.Tensor:
     return _Subsample2Fn.apply(x)
 
 
+class S2Grad:
+    """A stride-2 conv's data gradient left compact ([N, C, ceil(H/2), ceil(W/2)]): the parallel
+    1x1 data-gradient kernel adds it at the even pixels (``conv1x1_link_s2``); anything else
+    calls ``materialize`` (zero-filled full resolution)."""
+    __slots__ = ("g", "H", "W")
+
+    def __init__(self, g: torch.Tensor, H: int, W: int):
+        self.g, self.H, self.W = g, H, W
+
+    def materialize(self) -> torch.Tensor:
+        return lib().upsample2_scatter(self.g, self.H, self.W)
+
+
+class _Subsample2LinkFn(torch.autograd.Function):
+    """``subsample2`` whose backward parks the compact gradient on a ResidualLink (for conv1's
+    data-gradient kernel to add at the even pixels) instead of scattering it; if the consumer
+    already ran, the scattered gradient flows normally."""
+
+    @staticmethod
+    def forward(ctx, x, link):
+        ctx.shape, ctx.link = x.shape, link
+        return lib().subsample2(x.contiguous(memory_format=torch.channels_last))
+
+    @staticmethod
+    def backward(ctx, g):
+        link = ctx.link
+        g = g.contiguous(memory_format=torch.channels_last)
+        if link.closed or link.grad is not None:
+            return lib().upsample2_scatter(g, ctx.shape[2], ctx.shape[3]), None
+        link.grad = S2Grad(g, ctx.shape[2], ctx.shape[3])
+        return None, None
+
+
+def subsample2_link(x: torch.Tensor, link) -> torch.Tensor:
+    """``subsample2(x)`` with the backward hand-off of _Subsample2LinkFn (GPU bf16 NHWC)."""
+    if link is None or not (x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0):
+        return subsample2(x)
+    return _Subsample2LinkFn.apply(x, link)
+
+
 def down_tail_recompute_s2_ok(x: torch.Tensor, planes: int, down_conv) -> bool:
     """Stride-2 downsample tails (ResNet-50 layer 2) on the recompute kernels: the convolution
     reads x[:, :, ::2, ::2], materialised once (``subsample2``), so the stride-1 kernels apply."""
@@ -457,6 +504,9 @@ def down_tail_recompute_s2_ok(x: torch.Tensor, planes: int, down_conv) -> bool:
             and planes in (64, 128) and x.shape[1] % 64 == 0 and x.shape[1] <= 256)
 
 
+# stride-2 downsample tails: the compact data gradient is added at the even pixels by conv1's
+# data-gradient kernel (CML_S2_LINK_DGRAD=0: scattered to full resolution, then hipBLASLt addmm_)
+S2_LINK_DGRAD = os.environ.get("CML_S2_LINK_DGRAD", "1") == "1"
 # CML_RECOMPUTE_DOWN_TAIL_S2=0: stride-2 downsample tails keep stored z3 / zd (bn_add_bn_relu)
 RECOMPUTE_DOWN_TAIL_S2 = os.environ.get("CML_RECOMPUTE_DOWN_TAIL_S2", "1") == "1"
 

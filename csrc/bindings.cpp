@@ -919,6 +919,30 @@ std::vector<Tensor> conv3x3_bn_fwd(const Tensor& x, const Tensor& w_in, const op
   return {y, mean, invstd};
 }
 
+// dX = dY W (1x1, stride 1: x = dY [N, K, H, W] NHWC, w [No, K] -- W^T of the conv's weight)
+// plus, at the even pixels, link [N, No, ceil(H/2), ceil(W/2)]: a parallel stride-2 conv's
+// compact data gradient (never scattered to full resolution).
+Tensor conv1x1_link_s2(const Tensor& x, const Tensor& w, const Tensor& link_in) {
+  check_nhwc(x, "x");
+  TORCH_CHECK(x.dim() == 4, "conv1x1_link_s2: 4-D NHWC input");
+  const int64_t N = x.size(0), K = x.size(1), H = x.size(2), W = x.size(3);
+  check_w2(w, K, "conv1x1_link_s2");
+  const int64_t No = w.size(0);
+  Tensor link = link_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(link, "link");
+  TORCH_CHECK(link.dim() == 4 && link.size(0) == N && link.size(1) == No &&
+                  link.size(2) == (H + 1) / 2 && link.size(3) == (W + 1) / 2,
+              "conv1x1_link_s2: link [N, No, ceil(H/2), ceil(W/2)]");
+  const c10::DeviceGuard guard(x.device());
+  Tensor y = at::empty({N, No, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  CML_CHECK_HIP(cml::launch_conv1x1_link_s2(x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                                            link.data_ptr(), static_cast<int>(N),
+                                            static_cast<int>(H), static_cast<int>(W),
+                                            static_cast<int>(K), static_cast<int>(No),
+                                            cur_stream()));
+  return y;
+}
+
 // x[:, :, ::2, ::2] of an NHWC bf16 tensor as a dense NHWC tensor, and the backward scatter
 // (full resolution, zeros at the odd pixels; H, W: the full-resolution size).
 Tensor subsample2(const Tensor& x) {
@@ -1589,6 +1613,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("zero") = py::none(), py::arg("tap_mode") = false,
         "weight gradient of a 3x3 stride-1 conv (MFMA, split-K): all nine taps per workgroup "
         "(wgrad3x3.hip) where the plan fits, else / with a prologue / tap_mode one tap per grid z");
+  m.def("conv1x1_link_s2", &conv1x1_link_s2,
+        "1x1 data gradient + a stride-2 conv's compact data gradient at the even pixels");
   m.def("subsample2", &subsample2, "x[:, :, ::2, ::2] of an NHWC bf16 tensor, dense NHWC");
   m.def("upsample2_scatter", &upsample2_scatter, py::arg("g"), py::arg("H"), py::arg("W"),
         "full-resolution NHWC tensor with g at the even pixels, zeros elsewhere");

@@ -80,6 +80,9 @@ struct C1Args {
   int ntn, wgpn, mtiles;
   int H, W, OW, OHW;      // S2: input H, W; output W and H*W.  TAP: H, W (in = out) and OHW = H W
   int C;                  // TAP: input channels (K = 9 C, k = tap C + c, tap = 3 (dy + 1) + dx + 1)
+  // EL with link_s2: link is [N][ceil(H/2)][ceil(W/2)][N channels] (a stride-2 conv's compact
+  // data gradient), added at the even pixels of this [N][H][W] output (lm unused)
+  int link_s2, lW, lHW, lOW, lOHW;
 };
 
 __device__ __forceinline__ int64_t src_row(const C1Args& a, int m, bool s2) {
@@ -295,8 +298,18 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
       const int64_t row = m0 + p < a.M ? m0 + p : a.M - 1;
       const int64_t e0 = row * a.N + n0 + ncol0 + 8 * c;
       if constexpr (EL) {
-        lv[k] = *reinterpret_cast<const uint4*>(a.link + e0);
-        lbv[k] = a.lm[e0 >> 3];
+        if (a.link_s2) {   // compact stride-2 gradient: only the even pixels get an addend
+          const int img = static_cast<int>(row / a.lHW);
+          const int rem = static_cast<int>(row - static_cast<int64_t>(img) * a.lHW);
+          const int hh = rem / a.lW, ww = rem - hh * a.lW;
+          const bool ev = !((hh | ww) & 1);
+          const int64_t lrow = ev ? static_cast<int64_t>(img) * a.lOHW + (hh >> 1) * a.lOW + (ww >> 1) : 0;
+          lv[k] = *reinterpret_cast<const uint4*>(a.link + lrow * a.N + n0 + ncol0 + 8 * c);
+          lbv[k] = ev ? 0xffu : 0u;
+        } else {
+          lv[k] = *reinterpret_cast<const uint4*>(a.link + e0);
+          lbv[k] = a.lm[e0 >> 3];
+        }
       }
       if constexpr (SM == SM_BNRES)   // (no residual: link null)
         lv[k] = a.link ? *reinterpret_cast<const uint4*>(a.link + e0) : make_uint4(0u, 0u, 0u, 0u);
@@ -1043,6 +1056,21 @@ hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void
   conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N,
                                                              invstd, sdz, sdzx);
   return hipGetLastError();
+}
+
+hipError_t launch_conv1x1_link_s2(const void* x, const void* w, void* y, const void* link,
+                                  int Nimg, int H, int W, int K, int N, hipStream_t st) {
+  const int64_t M = static_cast<int64_t>(Nimg) * H * W;
+  if (bad_shape(M, K, N)) return hipErrorInvalidValue;
+  const Plan p = make_plan(M, K, N, 0, -1, true);
+  C1Args a = base_args(x, w, y, M, K, N, p);
+  a.link = reinterpret_cast<const uint16_t*>(link);
+  a.link_s2 = 1;
+  a.lW = W;
+  a.lHW = H * W;
+  a.lOW = (W + 1) / 2;
+  a.lOHW = ((H + 1) / 2) * a.lOW;
+  return launch_bwd(a, p, 1, st);
 }
 
 hipError_t launch_bn_stats_gram(const float* G, const float* cy, const void* w, int P, int Co,

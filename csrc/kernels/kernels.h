@@ -368,6 +368,10 @@ hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void
                                float* sdzx, int64_t M, int K, int N, hipStream_t st);
 // dz = ca (mask ? dy : 0) + cb z + cc coefficients of a training BN + ReLU backward from its sums
 // (sdz, sdzx); dgamma = sdzx, dbeta = sdz (bf16).
+// 1x1 data gradient y = x w^T (x = dY [Nimg][H][W][K], w [N][K]) plus, at the even pixels, a
+// stride-2 conv's compact data gradient link [Nimg][ceil(H/2)][ceil(W/2)][N] (conv1x1.hip EL).
+hipError_t launch_conv1x1_link_s2(const void* x, const void* w, void* y, const void* link,
+                                  int Nimg, int H, int W, int K, int N, hipStream_t st);
 // BN training statistics (mean, invstd; running stats updated when given) of z = y W^T from the
 // Gram matrix G = y^T y [P][P] and column sums cy [P] of y over M rows; W [Co][P] bf16 (conv1x1.hip).
 hipError_t launch_bn_stats_gram(const float* G, const float* cy, const void* w, int P, int Co,

@@ -379,3 +379,18 @@ def test_subsample2_and_scatter(cuda, N, C, H, W):
     xi = x.clone().requires_grad_(True)
     fconv.subsample2(xi).backward(g)
     assert torch.equal(xi.grad, ref)
+
+
+@pytest.mark.parametrize("N,K,No,H,W", [(2, 128, 256, 56, 56), (3, 64, 128, 7, 9),
+                                        (1, 512, 1024, 14, 14)])
+def test_conv1x1_link_s2(cuda, N, K, No, H, W):
+    """dX = dY W^T plus a stride-2 conv's compact gradient at the even pixels, vs fp32."""
+    g0 = torch.Generator(device=cuda).manual_seed(26)
+    dy = _nhwc(torch.randn(N, K, H, W, device=cuda, generator=g0).bfloat16())
+    w = (torch.randn(No, K, device=cuda, generator=g0) * K ** -0.5).bfloat16()
+    g = _nhwc(torch.randn(N, No, (H + 1) // 2, (W + 1) // 2, device=cuda, generator=g0).bfloat16())
+    y = _lib().conv1x1_link_s2(dy, w.contiguous(), g)
+    full = torch.zeros(N, No, H, W, device=cuda)
+    full[:, :, ::2, ::2] = g.float()
+    ref = _rows(dy) @ w.float().t() + _rows(full)
+    _close(_rows(y), ref, 1e-2)
