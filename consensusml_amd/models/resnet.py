@@ -314,17 +314,22 @@ class Bottleneck(nn.Module):
             link = None
             dlink = ResidualLink() if use_links and self.conv1.link_ok(x) else None
             z1, st1 = self._conv_bn(x, self.conv1, self.bn1, dlink)
-        out = self.bn1(z1, stats=st1)
         planes = self.conv3.in_channels
-        hw2 = (out.shape[2] // self.conv2.stride[0]) * (out.shape[3] // self.conv2.stride[0])
+        hw2 = (z1.shape[2] // self.conv2.stride[0]) * (z1.shape[3] // self.conv2.stride[0])
         fuse3 = fused_conv1x1_policy(planes, planes * 4, hw2, 1, True)
-        if fuse3 and CONV3X3_BN_STATS and OWN_DGRAD3X3 and fconv.conv3x3_ok(out, self.conv2):
-            z2, st2 = fconv.conv3x3_bn_stats(out, self.conv2, self.bn2)
-        elif fuse3 and fconv.conv3x3_s2_ok(out, self.conv2):
-            z2, st2 = fconv.conv3x3_s2_bn_stats(out, self.conv2, self.bn2)
+        own3 = fuse3 and CONV3X3_BN_STATS and OWN_DGRAD3X3 and fconv.conv3x3_ok(z1, self.conv2)
+        if own3 and fconv.BN1_DGRAD_SUMS and st1 is not None and self.bn1.training:
+            # bn1's backward sums come from the 3x3 data gradient's epilogue
+            z2, st2 = fconv.bnrelu_conv3x3_bn_stats(z1, self.bn1, st1, self.conv2, self.bn2)
         else:
-            z2 = self._conv2(out)
-            st2 = fconv.bn_stats(z2, self.bn2) if fuse3 else None
+            out = self.bn1(z1, stats=st1)
+            if own3:
+                z2, st2 = fconv.conv3x3_bn_stats(out, self.conv2, self.bn2)
+            elif fuse3 and fconv.conv3x3_s2_ok(out, self.conv2):
+                z2, st2 = fconv.conv3x3_s2_bn_stats(out, self.conv2, self.bn2)
+            else:
+                z2 = self._conv2(out)
+                st2 = fconv.bn_stats(z2, self.bn2) if fuse3 else None
         if fuse3:
             rec = self.down_conv is None and recompute_tail_policy(planes)
             if rec or (self.down_conv is None and fused_bn3_bwd_policy(planes)):

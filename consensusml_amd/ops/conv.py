@@ -239,6 +239,25 @@ def _const(n: int, v: float, device) -> torch.Tensor:
 # reused by the backward) instead of a statistics-only pass of the conv (CML_GRAM_STATS=0)
 GRAM_STATS = os.environ.get("CML_GRAM_STATS", "1") == "1"
 
+# recompute tails: bn2's backward sums from the epilogue of the GEMM that produces its output
+# gradient dy2 (``conv1x1_cat_bnsums``, ReLU mask recomputed from z2), so only bn2's apply pass
+# remains (CML_CAT_BNSUMS=0: the separate reduction pass)
+CAT_BNSUMS = os.environ.get("CML_CAT_BNSUMS", "1") == "1"
+
+
+def _cat_dgrad_bn2(L, gy, mask, z, a1, c1, sc, bi, w_cat, g2, b2, mean2, invstd2):
+    """dy2 = [a1 (mask ? gy : 0) + c1 | relu(z sc + bi)] w_cat^T, then bn2's (BN + ReLU on z)
+    backward: (dz, dgamma2, dbeta2)."""
+    a_cat, c_cat = torch.cat([a1, sc]), torch.cat([c1, bi])
+    if CAT_BNSUMS:
+        dy2, s2, q2 = L.conv1x1_cat_bnsums(gy, mask, z, a_cat, c_cat, w_cat, mean2, invstd2)
+        M = z.numel() // z.shape[1]
+        _, _, _, dg2, db2 = L.bn_bwd_coeffs(s2, q2, g2, mean2, invstd2, M)
+        return L.bn_bwd_apply(dy2, z, g2, b2, mean2, invstd2, s2, q2), dg2, db2
+    dy2 = L.conv1x1_cat(gy, mask, z, a_cat, c_cat, w_cat)
+    dz, dg2, db2, _ = L.bn_bwd(dy2, None, z, None, g2, b2, mean2, invstd2, True, False)
+    return dz, dg2, db2
+
 
 class _RecomputeTailFn(torch.autograd.Function):
     """Identity-block tail y = relu(bn3(conv3(relu(bn2(z2)))) + res) that never stores z3.
@@ -320,8 +339,8 @@ class _RecomputeTailFn(torch.autograd.Function):
             dw = dw.to(w.dtype).view_as(w)
         G = W3.t() @ (cb[:, None] * W3)
         w_cat = torch.cat([W3.t(), G.t()], 1).to(torch.bfloat16).contiguous()
-        dy2 = L.conv1x1_cat(gy, mask, z, torch.cat([ca, sc]), torch.cat([cc, bi]), w_cat)
-        dz, dg2, db2, _ = L.bn_bwd(dy2, None, z, None, g2, b2, mean2, invstd2, True, False)
+        dz, dg2, db2 = _cat_dgrad_bn2(L, gy, mask, z, ca, cc, sc, bi, w_cat, g2, b2, mean2,
+                                      invstd2)
         dres = None
         if ctx.needs_input_grad[8]:
             mg = MaskedGrad(gy, mask)
@@ -418,9 +437,9 @@ class _RecomputeDownTailFn(torch.autograd.Function):
             dwd = (ad[:, None] * Pd + bdc[:, None] * (Wd @ gramd) + cd[:, None] * cx[None, :])
             dwd = dwd.to(wd.dtype).view_as(wd)
         G3 = W3.t() @ (b3c[:, None] * W3)
-        dy2 = L.conv1x1_cat(gy, mask, z, torch.cat([a3, sc]), torch.cat([c3, bi]),
-                            torch.cat([W3.t(), G3.t()], 1).to(torch.bfloat16).contiguous())
-        dz, dg2, db2, _ = L.bn_bwd(dy2, None, z, None, g2, b2, mean2, invstd2, True, False)
+        dz, dg2, db2 = _cat_dgrad_bn2(
+            L, gy, mask, z, a3, c3, sc, bi,
+            torch.cat([W3.t(), G3.t()], 1).to(torch.bfloat16).contiguous(), g2, b2, mean2, invstd2)
         dx = None
         if ctx.needs_input_grad[10]:
             Gd = Wd.t() @ (bdc[:, None] * Wd)
@@ -630,6 +649,60 @@ class _Conv3x3BNStatsFn(torch.autograd.Function):
     def backward(ctx, dy, _dm, _di):
         dx, dw = _Conv3x3Fn.backward(ctx, dy)
         return dx, dw, None, None, None, None
+
+
+class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
+    """(z2, mean2, invstd2) = conv3x3(relu(bn1(z1))) and bn2's training statistics, with bn1's
+    batch statistics (mean1, invstd1) given by its producer. Forward as ``bn_act`` +
+    ``_Conv3x3BNStatsFn`` (y1 is materialised: the implicit GEMM stages it with global_load_lds).
+    Backward: the 3x3 data-gradient GEMM also takes bn1's BN + ReLU backward sums in its epilogue
+    (``conv_gemm_bnsums``, ReLU bit recomputed from z1), so bn1's backward is its apply pass only
+    (the separate reduction re-read dy1 and z1)."""
+
+    @staticmethod
+    def forward(ctx, z1, g1, b1, mean1, invstd1, eps1, w, rmean, rvar, eps, momentum):
+        L = lib()
+        y1 = L.bn_fwd(z1, None, g1, b1, None, None, mean1, invstd1, eps1, momentum, True, False,
+                      False)[0]
+        Co, Ci = w.shape[0], w.shape[1]
+        wf = w.permute(0, 2, 3, 1).reshape(Co, 9 * Ci).contiguous()   # k = (3 ky + kx) Ci + ci
+        z2, m2, i2 = L.conv_gemm_bn(y1, wf, 9, _zero_row(z1.device), rmean, rmean, rvar, eps,
+                                    momentum)
+        ctx.save_for_backward(z1, g1, b1, mean1, invstd1, y1, w)
+        ctx.mark_non_differentiable(m2, i2)
+        return z2, m2, i2
+
+    @staticmethod
+    def backward(ctx, dz2, _dm, _di):
+        z1, g1, b1, mean1, invstd1, y1, w = ctx.saved_tensors
+        dz2 = dz2.contiguous(memory_format=torch.channels_last)
+        L = lib()
+        Co, Ci = w.shape[0], w.shape[1]
+        # w_rot[ci][ky][kx][co] = w[co][ci][2 - ky][2 - kx], flattened k = tap Co + co
+        wr = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co).contiguous()
+        sc = g1.float() * invstd1
+        bi = b1.float() - mean1 * sc
+        dy1, s1, q1 = L.conv_gemm_bnsums(dz2, wr, 9, _zero_row(dz2.device), z1, sc, bi, mean1,
+                                         invstd1)
+        M = z1.numel() // z1.shape[1]
+        _, _, _, dg1, db1 = L.bn_bwd_coeffs(s1, q1, g1, mean1, invstd1, M)
+        dz1 = L.bn_bwd_apply(dy1, z1, g1, b1, mean1, invstd1, s1, q1)
+        dw = _wgrad3x3(dz2, y1, w) if ctx.needs_input_grad[6] else None
+        return dz1, dg1, db1, None, None, None, dw, None, None, None, None
+
+
+# bn1 + ReLU -> 3x3 conv with bn1's backward sums in the data-gradient epilogue
+# (CML_BN1_DGRAD_SUMS=0: bn_act + conv3x3_bn_stats, bn1's backward with its own reduction pass)
+BN1_DGRAD_SUMS = os.environ.get("CML_BN1_DGRAD_SUMS", "1") == "1"
+
+
+def bnrelu_conv3x3_bn_stats(z1: torch.Tensor, bn_a, stats_a, conv, bn):
+    """(z, (mean, invstd)) of ``conv(relu(bn_a(z1)))`` (bn_a's batch statistics ``stats_a``) and
+    bn's training statistics; callers check ``conv3x3_ok`` on z1 first."""
+    z, m, i = _BNReLUConv3x3BNStatsFn.apply(z1, bn_a.weight, bn_a.bias, stats_a[0], stats_a[1],
+                                            bn_a.eps, conv.weight, bn.running_mean, bn.running_var,
+                                            bn.eps, bn.momentum)
+    return z, (m, i)
 
 
 class _Conv3x3S2BNStatsFn(torch.autograd.Function):

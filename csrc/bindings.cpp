@@ -557,6 +557,20 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
 
 // wgrad1x1 with a general dy prologue (dmode: 0 none, 2 dz_a (mask ? dy : 0) + dz_c,
 // 3 max(dy dz_a + dz_b, 0)) and optional column sums of the staged dz -> {dw fp32 [Co, Ci], cs [Co]}.
+// Fixed-order fold of a split-K partial slab part [S, n] fp32 (n % 4 == 0) -> [n] fp32 / bf16 (the
+// weight-gradient kernels' second stage; exposed for tests and the fold A/B).
+Tensor split_fold(const Tensor& part, bool out_bf16) {
+  check_dev(part, "part");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 2 &&
+                  part.size(1) % 4 == 0 && part.size(0) >= 1 && part.size(0) < (1ll << 31),
+              "split_fold: part must be contiguous fp32 [S, n] with n % 4 == 0");
+  const c10::DeviceGuard guard(part.device());
+  Tensor out = at::empty({part.size(1)}, part.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  CML_CHECK_HIP(cml::launch_wgrad_fold(part.data_ptr<float>(), static_cast<int>(part.size(0)),
+                                       part.size(1), out.data_ptr(), out_bf16, cur_stream()));
+  return out;
+}
+
 std::vector<Tensor> wgrad1x1_ex(const Tensor& dy_in, const Tensor& x, const optional<Tensor>& pro_sc,
                                 const optional<Tensor>& pro_bi, int64_t dmode,
                                 const optional<Tensor>& dz_mask, const optional<Tensor>& dz_a,
@@ -879,6 +893,63 @@ Tensor conv1x1_cat(const Tensor& g, const Tensor& mask, const Tensor& x2, const 
   return y;
 }
 
+// conv1x1_cat whose output dy2 is the gradient of relu(bn(x2)) (Cout = K2): also that BN + ReLU
+// backward's sums {sdz, sdzx} from the epilogue (mask recomputed from x2 with bn's affine, the
+// second halves of a_cat / c_cat), so only bn_bwd_apply remains. mean / invstd fp32 [K2].
+std::vector<Tensor> conv1x1_cat_bnsums(const Tensor& g, const Tensor& mask, const Tensor& x2,
+                                       const Tensor& a_cat, const Tensor& c_cat, const Tensor& w,
+                                       const Tensor& mean, const Tensor& invstd) {
+  check_nhwc(g, "g");
+  check_nhwc(x2, "x2");
+  const int64_t N = g.size(0), K1 = g.size(1), H = g.size(2), W = g.size(3), K2 = x2.size(1);
+  const int64_t M = N * H * W, K = K1 + K2;
+  TORCH_CHECK(x2.dim() == 4 && x2.size(0) == N && x2.size(2) == H && x2.size(3) == W,
+              "conv1x1_cat_bnsums: x2 shape");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.size(1) == K &&
+                  w.is_contiguous() && w.size(0) == K2 && K1 % 64 == 0 && K2 % 64 == 0,
+              "conv1x1_cat_bnsums: w contiguous bf16 [K2, K1 + K2], channels multiples of 64");
+  const int64_t Co = w.size(0);
+  const c10::DeviceGuard guard(g.device());
+  auto f32 = g.options().dtype(at::kFloat);
+  Tensor y = at::empty({N, Co, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor part = at::empty({static_cast<int64_t>(cml::conv1x1_cat_part_floats(M, K, Co))}, f32);
+  Tensor sdz = at::empty({Co}, f32), sdzx = at::empty({Co}, f32);
+  CML_CHECK_HIP(cml::launch_conv1x1_cat(
+      g.data_ptr(), opt_ptr<const uint8_t>(mask, at::kByte, "mask", M * K1 / 8), x2.data_ptr(),
+      opt_ptr<const float>(a_cat, at::kFloat, "a_cat", K),
+      opt_ptr<const float>(c_cat, at::kFloat, "c_cat", K), w.data_ptr(), y.data_ptr(), M,
+      static_cast<int>(K1), static_cast<int>(K), static_cast<int>(Co), cur_stream(),
+      opt_ptr<const float>(mean, at::kFloat, "mean", Co),
+      opt_ptr<const float>(invstd, at::kFloat, "invstd", Co), part.data_ptr<float>(),
+      sdz.data_ptr<float>(), sdzx.data_ptr<float>()));
+  return {y, sdz, sdzx};
+}
+
+// Apply half of a BN + ReLU backward (mask recomputed from x) from its sums: dy, x [N, C, H, W]
+// NHWC bf16 -> dx.
+Tensor bn_bwd_apply(const Tensor& dy_in, const Tensor& x, const Tensor& gamma, const Tensor& beta,
+                    const Tensor& mean, const Tensor& invstd, const Tensor& sdz,
+                    const Tensor& sdzx) {
+  check_nhwc(x, "x");
+  Tensor dy = x.dim() == 4 ? dy_in.contiguous(at::MemoryFormat::ChannelsLast) : dy_in.contiguous();
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "bn_bwd_apply: dy shape mismatch");
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(gamma.scalar_type() == at::kBFloat16 && beta.scalar_type() == at::kBFloat16 &&
+                  gamma.numel() == C && beta.numel() == C,
+              "bn_bwd_apply: bf16 gamma / beta [C]");
+  const c10::DeviceGuard guard(x.device());
+  Tensor dx = at::empty_like(x);
+  CML_CHECK_HIP(cml::launch_bn_bwd_apply(
+      dy.data_ptr(), x.data_ptr(), dx.data_ptr(), M, static_cast<int>(C), gamma.data_ptr(),
+      beta.data_ptr(), opt_ptr<const float>(mean, at::kFloat, "mean", C),
+      opt_ptr<const float>(invstd, at::kFloat, "invstd", C),
+      opt_ptr<const float>(sdz, at::kFloat, "sdz", C),
+      opt_ptr<const float>(sdzx, at::kFloat, "sdzx", C), cur_stream()));
+  return dx;
+}
+
 // 3x3 / stride 1 / padding 1 conv as an implicit GEMM on the fused 1x1 kernel (conv1x1.hip TAP):
 // x [N, C, H, W] NHWC bf16, w [Cout, C, 3, 3] bf16 (made channels_last: [Cout][3][3][C]) ->
 // {y NHWC, mean, invstd}; pro_sc / pro_bi (fp32 [C]): max(x sc + bi, 0) applied on load.
@@ -1052,6 +1123,41 @@ Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
 
 // Implicit-GEMM conv (conv_gemm.hip): x [N, C, H, W] NHWC bf16, w [Cout, taps * C] contiguous
 // bf16 (k = tap C + c), taps 1 or 9 (3x3, padding 1) -> y [N, Cout, H, W] NHWC.
+// Stride-1 conv_gemm whose output is the gradient of relu(bn(z)) (z [N, Cout, H, W] NHWC bf16, sc /
+// bi bn's affine, mean / invstd its batch statistics, fp32 [Cout]): {y, sdz, sdzx} with that BN +
+// ReLU backward's sums from the epilogue (bn_bwd_apply finishes it).
+std::vector<Tensor> conv_gemm_bnsums(const Tensor& x, const Tensor& w, int64_t taps,
+                                     const Tensor& zero, const Tensor& z, const Tensor& sc,
+                                     const Tensor& bi, const Tensor& mean, const Tensor& invstd) {
+  check_nhwc(x, "x");
+  check_nhwc(z, "z");
+  TORCH_CHECK(x.dim() == 4, "conv_gemm_bnsums: 4-D NHWC input");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(taps == 1 || taps == 9, "conv_gemm_bnsums: taps 1 or 9");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.dim() == 2 &&
+                  w.size(1) == taps * C && w.size(0) % 64 == 0 && C % 64 == 0,
+              "conv_gemm_bnsums: w must be contiguous bf16 [Cout, taps * C], channels multiples of 64");
+  const int64_t Co = w.size(0), M = N * H * W;
+  TORCH_CHECK(z.dim() == 4 && z.size(0) == N && z.size(1) == Co && z.size(2) == H && z.size(3) == W,
+              "conv_gemm_bnsums: z must be [N, Cout, H, W]");
+  TORCH_CHECK(zero.is_cuda() && zero.device() == x.device() && zero.scalar_type() == at::kBFloat16 &&
+                  zero.is_contiguous() && zero.numel() >= 64, "conv_gemm_bnsums: zero must be >= 64 bf16");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor part = at::empty({static_cast<int64_t>(cml::conv_gemm_part_floats(M, static_cast<int>(Co)))}, f32);
+  Tensor sdz = at::empty({Co}, f32), sdzx = at::empty({Co}, f32);
+  CML_CHECK_HIP(cml::launch_conv_gemm_bnsums(
+      x.data_ptr(), w.data_ptr(), y.data_ptr(), zero.data_ptr(), static_cast<int>(N),
+      static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(Co),
+      static_cast<int>(taps), z.data_ptr(), opt_ptr<const float>(sc, at::kFloat, "sc", Co),
+      opt_ptr<const float>(bi, at::kFloat, "bi", Co),
+      opt_ptr<const float>(mean, at::kFloat, "mean", Co),
+      opt_ptr<const float>(invstd, at::kFloat, "invstd", Co), part.data_ptr<float>(),
+      sdz.data_ptr<float>(), sdzx.data_ptr<float>(), cur_stream()));
+  return {y, sdz, sdzx};
+}
+
 Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps, const optional<Tensor>& zero_in,
                  int64_t stride) {
   check_nhwc(x, "x");
@@ -1625,6 +1731,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return cml::wgrad3x3_direct_plan(static_cast<int>(B), static_cast<int>(H), static_cast<int>(W),
                                      static_cast<int>(Co), static_cast<int>(Ci), &S, &T);
   }, "whether wgrad3x3 takes the nine-tap kernel for this shape");
+  m.def("conv_gemm_bnsums", &conv_gemm_bnsums,
+        "stride-1 conv_gemm + the sums of the BN + ReLU backward its output feeds");
   m.def("conv_gemm", &conv_gemm, py::arg("x"), py::arg("w"), py::arg("taps"),
         py::arg("zero") = py::none(), py::arg("stride") = 1,
         "implicit-GEMM NHWC conv (1x1 / 3x3 padding 1, stride 1 or 2), glds staging");
@@ -1636,7 +1744,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_bnres", &conv1x1_bnres, "recomputed conv1x1 + BN apply + residual + ReLU -> {y, mask}");
   m.def("conv1x1_cat_bnres", &conv1x1_cat_bnres,
         "two BN'd 1x1 convs summed + ReLU in one K-concatenated GEMM -> {y, mask}");
+  m.def("conv1x1_cat_bnsums", &conv1x1_cat_bnsums,
+        "conv1x1_cat + the sums of the BN + ReLU backward its output feeds");
+  m.def("bn_bwd_apply", &bn_bwd_apply, "apply half of a BN + ReLU backward from its sums");
   m.def("conv1x1_cat", &conv1x1_cat, "two-source (masked affine | BN-ReLU) 1x1 conv along K");
+  m.def("split_fold", &split_fold, "fixed-order fold of a split-K partial slab");
   m.def("wgrad1x1_ex", &wgrad1x1_ex, py::arg("dy"), py::arg("x"), py::arg("pro_sc") = py::none(),
         py::arg("pro_bi") = py::none(), py::arg("dmode") = 0, py::arg("dz_mask") = py::none(),
         py::arg("dz_a") = py::none(), py::arg("dz_b") = py::none(), py::arg("dz_c") = py::none(),

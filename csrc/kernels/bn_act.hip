@@ -647,6 +647,18 @@ hipError_t launch_bn_bwd(const void* dy, const void* dy2, const void* x, const v
   return hipGetLastError();
 }
 
+hipError_t launch_bn_bwd_apply(const void* dy, const void* x, void* dx, int64_t M, int C,
+                               const void* gamma, const void* beta, const float* mean,
+                               const float* invstd, const float* sdz, const float* sdzx,
+                               hipStream_t st) {
+  if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1) return hipErrorInvalidValue;
+  bn_bwd_apply_kernel<RM_RECOMP, false, false><<<apply_grid(M, C), kBT, 0, st>>>(
+      reinterpret_cast<const bf16*>(dy), nullptr, reinterpret_cast<const bf16*>(x), nullptr,
+      reinterpret_cast<bf16*>(dx), nullptr, M, C, mean, invstd,
+      reinterpret_cast<const bf16*>(gamma), reinterpret_cast<const bf16*>(beta), sdz, sdzx);
+  return hipGetLastError();
+}
+
 hipError_t launch_bn_fwd2(const void* x1, const void* x2, void* y, void* mask, int64_t M, int C,
                           const void* gamma1, const void* beta1, const void* gamma2,
                           const void* beta2, float* mean1, float* invstd1, float* mean2,

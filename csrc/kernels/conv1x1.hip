@@ -261,7 +261,10 @@ __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)
 // residual gradient of the same tensor). SM_BNBWD: the sums are s = sum (sm bit ? v : 0) and
 // q = sum (sm bit ? v : 0) (sz - shift) -- the backward reduction of the BN + ReLU whose output
 // gradient v is (the consumer BN's mean in shift) -- instead of the BN statistics of v.
-template <bool EL, int SM, int MT>
+// DM (SM_BNBWD without a stored mask, PM_CAT data gradients of the recompute tails): the ReLU bit
+// is recomputed from the BN input, sz * ep_sc + ep_bi > 0 (the BN's own affine, as its forward
+// prologue applied it), so the BN + ReLU backward that follows needs no reduction pass of its own.
+template <bool EL, int SM, int MT, bool DM = false>
 __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], float (&ss)[8],
                                          float (&sq)[8], const float (&sh)[8], char* simg, int m0,
                                          int ncol0, int n0, int lane) {
@@ -285,9 +288,9 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
       if constexpr (SM != SM_BNBWD) { zv[k] = make_uint4(0u, 0u, 0u, 0u); zbv[k] = 0u; }
     }
   }
-  // SM_BNRES: the lane's 8 output channels' BN coefficients
+  // SM_BNRES / DM: the lane's 8 output channels' BN coefficients
   float esc[8], ebi[8];
-  if constexpr (SM == SM_BNRES) {
+  if constexpr (SM == SM_BNRES || DM) {
     ld8f(a.ep_sc + n0 + ncol0 + 8 * c, esc);
     ld8f(a.ep_bi + n0 + ncol0 + 8 * c, ebi);
   }
@@ -315,7 +318,7 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
         lv[k] = a.link ? *reinterpret_cast<const uint4*>(a.link + e0) : make_uint4(0u, 0u, 0u, 0u);
       if constexpr (SM == SM_BNBWD) {
         zv[k] = *reinterpret_cast<const uint4*>(a.sz + e0);
-        zbv[k] = a.sm[e0 >> 3];
+        zbv[k] = DM ? 0u : a.sm[e0 >> 3];
       }
     }
   };
@@ -390,6 +393,15 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
       }
     } else if constexpr (SM == SM_BNBWD) {
       const uint32_t z4[4] = {z.x, z.y, z.z, z.w};
+      if constexpr (DM) {
+        zb = 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          zb |= (fmaf(__uint_as_float(z4[q] << 16), esc[2 * q], ebi[2 * q]) > 0.f ? 1u : 0u) << (2 * q);
+          zb |= (fmaf(__uint_as_float(z4[q] & 0xffff0000u), esc[2 * q + 1], ebi[2 * q + 1]) > 0.f
+                     ? 1u : 0u) << (2 * q + 1);
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float lo = ((zb >> (2 * q)) & 1u) ? __uint_as_float(w4[q] << 16) : 0.f;
@@ -534,7 +546,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
         if constexpr (ALIAS) __syncthreads();   // every wave is done reading x before the images
 #pragma unroll
         for (int u = 0; u < MT; ++u)
-          epilogue<EL, SM, MT>(a, acc[u], ss, sq, sh, s_img + wave * 8192,
+          epilogue<EL, SM, MT, PM == PM_CAT && SM == SM_BNBWD>(a, acc[u], ss, sq, sh,
+                                                               s_img + wave * 8192,
                            t * BM + wm * 64 * MT + 64 * u, wn * 64, n0, lane);
       }
       if (!more) break;
@@ -918,6 +931,9 @@ hipError_t launch_tail_w(const C1Args& a, const Plan& p, bool cat, hipStream_t s
   if (cat && a.ymask)
     return p.wres ? launch_t<WN, WM, PM_CAT, true, false, false, SM_BNRES>(a, p, st)
                   : launch_t<WN, WM, PM_CAT, false, false, false, SM_BNRES>(a, p, st);
+  if (cat && a.part)   // + the BN + ReLU backward sums of the output (mask recomputed, DM)
+    return p.wres ? launch_t<WN, WM, PM_CAT, true, false, false, SM_BNBWD>(a, p, st)
+                  : launch_t<WN, WM, PM_CAT, false, false, false, SM_BNBWD>(a, p, st);
   if (cat)
     return p.wres ? launch_t<WN, WM, PM_CAT, true, false, false, SM_OFF>(a, p, st)
                   : launch_t<WN, WM, PM_CAT, false, false, false, SM_OFF>(a, p, st);
@@ -976,6 +992,22 @@ hipError_t launch_bn_stats_finalize(const float* part, int R, int BN, int N, int
   }
   conv1x1_bn_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, R, BN, N, M, shift, eps, momentum,
                                                           mean, invstd, rmean, rvar);
+  return hipGetLastError();
+}
+
+// BN + ReLU backward sums {sdz, sdzx} from a GEMM's partial slab [ntn][R][2][BN] (tall slabs folded
+// first, as launch_bn_stats_finalize does)
+hipError_t launch_bnbwd_sums_finalize(const float* part, int R, int BN, int N, const float* invstd,
+                                      float* sdz, float* sdzx, hipStream_t st, float* fold) {
+  const int S = fold ? bn_part_fold_slices(R, N / BN) : 0;
+  if (S > 0) {
+    const int rp = (R + S - 1) / S;
+    const int S2 = (R + rp - 1) / rp;
+    part_fold_kernel<<<dim3(S2, N / BN), 256, 0, st>>>(part, R, BN, rp, S2, fold);
+    part = fold;
+    R = S2;
+  }
+  conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, R, BN, N, invstd, sdz, sdzx);
   return hipGetLastError();
 }
 
@@ -1116,17 +1148,37 @@ hipError_t launch_conv1x1_bnres(const void* x, const void* w, void* y, uint8_t* 
 
 hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2, const float* a_cat,
                               const float* c_cat, const void* w, void* y, int64_t M, int K1, int K,
-                              int N, hipStream_t st) {
+                              int N, hipStream_t st, const float* mean, const float* invstd,
+                              float* part, float* sdz, float* sdzx) {
   if (bad_shape(M, K, N) || K1 % kBK || K1 <= 0 || K1 >= K || !mask || !a_cat || !c_cat)
     return hipErrorInvalidValue;
-  const Plan p = make_plan(M, K, N, 2);
+  const bool sums = mean != nullptr;
+  // sums: the output is the gradient of the BN + ReLU whose input is x2 itself (N = K - K1)
+  if (sums && (!invstd || !part || !sdz || !sdzx || N != K - K1)) return hipErrorInvalidValue;
+  const Plan p = make_plan(M, K, N, 2, -1, !sums);   // (the sums' MT = 2 tile spills)
   C1Args a = base_args(g, w, y, M, K, N, p);
   a.xm = mask;
   a.x2 = reinterpret_cast<const uint16_t*>(x2);
   a.pro_sc = a_cat;
   a.pro_bi = c_cat;
   a.K1 = K1;
-  return launch_tail(a, p, true, st);
+  if (sums) {
+    a.sz = a.x2;
+    a.ep_sc = a_cat + K1;   // the BN's own affine: the second source's prologue coefficients
+    a.ep_bi = c_cat + K1;
+    a.shift = mean;
+    a.part = part;
+  }
+  hipError_t e = launch_tail(a, p, true, st);
+  if (e != hipSuccess || !sums) return e;
+  conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N,
+                                                             invstd, sdz, sdzx);
+  return hipGetLastError();
+}
+
+size_t conv1x1_cat_part_floats(int64_t M, int K, int N) {
+  const Plan p = make_plan(M, K, N, 2, -1, false);
+  return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
 }
 
 hipError_t launch_conv1x1_cat_bnres(const void* x1, const void* x2, const float* sc_cat,

@@ -40,7 +40,10 @@ struct GArgs {
   uint16_t* y;            // [M][N]
   const uint16_t* zero;   // >= 64 zero elements
   float* part;            // ST: [ntn][mtiles * WM][2][BN] shifted sums of the bf16 output
-  const float* shift;     // ST: [N] statistics shift (the BN running mean) or null
+  const float* shift;     // ST: [N] statistics shift (the BN running mean) or null; BB: the BN's mean
+  const uint16_t* sz;     // BB: input z [M][N] of the BN + ReLU whose output gradient y is
+  const float* ep_sc;     // BB: that BN's affine [N] (ReLU bit: z ep_sc + ep_bi > 0)
+  const float* ep_bi;
   int M, C, N, H, W, HW;   // H, W: output
   int S, IH, IW, IHW;     // stride; input height, width and pixels per image
   int KS;                 // TAPS * C / 64
@@ -54,7 +57,10 @@ struct GArgs {
 // per MFMA).
 // ST: the epilogue also accumulates the BN statistics (sum, sum of squares of y_bf16 - shift) of
 // the stored values per channel and writes one partial row per (m-tile, wave row).
-template <int BM, int BN, int TAPS, int NBUF = 2, int WTN = 64, bool ST = false>
+// BB (with ST): instead the sums of the backward of the BN + ReLU whose output gradient y is (a
+// data gradient): s = sum y', q = sum y' (z - mean) with y' = (z ep_sc + ep_bi > 0) ? y : 0, the
+// ReLU bit recomputed from the BN input z -- that BN's backward then needs no reduction pass.
+template <int BM, int BN, int TAPS, int NBUF = 2, int WTN = 64, bool ST = false, bool BB = false>
 __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
   constexpr int WN = BN / WTN, WM = BM / 64, NW = WN * WM;
   constexpr int NI = WTN / 32;                  // accumulator rows (n) per wave
@@ -204,13 +210,27 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     const int cb = n0 + wn * WTN + 64 * sb + 8 * c;   // this lane's 8 channels
-    float sh[8], ss[8], sq[8];
+    float sh[8], ss[8], sq[8], esc[8], ebi[8];
     if constexpr (ST) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         sh[q] = a.shift ? a.shift[cb + q] : 0.f;
         ss[q] = 0.f;
         sq[q] = 0.f;
+        if constexpr (BB) {
+          esc[q] = a.ep_sc[cb + q];
+          ebi[q] = a.ep_bi[cb + q];
+        }
+      }
+    }
+    // BB: the 8 rows' z chunks issued together (rows past M re-read row M - 1)
+    uint4 zr[BB ? 8 : 1];
+    if constexpr (BB) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int m = mb + 8 * k + (lane >> 3);
+        zr[k] = *reinterpret_cast<const uint4*>(
+            a.sz + static_cast<int64_t>(m < a.M ? m : a.M - 1) * a.N + cb);
       }
     }
 #pragma unroll
@@ -219,7 +239,22 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
       const uint4 v = *reinterpret_cast<const uint4*>(simg + swz(pr, c));
       if (mb + pr < a.M) {
         *reinterpret_cast<uint4*>(a.y + static_cast<int64_t>(mb + pr) * a.N + cb) = v;
-        if constexpr (ST) {
+        if constexpr (BB) {
+          const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+          const uint32_t z4[4] = {zr[k].x, zr[k].y, zr[k].z, zr[k].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float zlo = __uint_as_float(z4[q] << 16);
+            const float zhi = __uint_as_float(z4[q] & 0xffff0000u);
+            const float lo = fmaf(zlo, esc[2 * q], ebi[2 * q]) > 0.f ? __uint_as_float(w4[q] << 16) : 0.f;
+            const float hi = fmaf(zhi, esc[2 * q + 1], ebi[2 * q + 1]) > 0.f
+                                 ? __uint_as_float(w4[q] & 0xffff0000u) : 0.f;
+            ss[2 * q] += lo;
+            ss[2 * q + 1] += hi;
+            sq[2 * q] = fmaf(lo, zlo - sh[2 * q], sq[2 * q]);
+            sq[2 * q + 1] = fmaf(hi, zhi - sh[2 * q + 1], sq[2 * q + 1]);
+          }
+        } else if constexpr (ST) {
           const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -258,8 +293,9 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
 
 template <int BM, int BN, int TAPS, int NBUF, int WTN = 64>
 hipError_t launch_g(const GArgs& a, hipStream_t st) {
-  auto k = a.part ? &conv_gemm_kernel<BM, BN, TAPS, NBUF, WTN, true>
-                  : &conv_gemm_kernel<BM, BN, TAPS, NBUF, WTN, false>;
+  auto k = !a.part ? &conv_gemm_kernel<BM, BN, TAPS, NBUF, WTN, false>
+            : (a.sz ? &conv_gemm_kernel<BM, BN, TAPS, NBUF, WTN, true, true>
+                    : &conv_gemm_kernel<BM, BN, TAPS, NBUF, WTN, true>);
   const size_t lds = NBUF * static_cast<size_t>(BM + BN) * 128;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
@@ -377,6 +413,46 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
   const int R = static_cast<int>((M + BM - 1) / BM) * (BM / 64);
   return launch_bn_stats_finalize(part, R, BN, N, M, shift, eps, momentum, mean, invstd, rmean,
                                   rvar, st, part + static_cast<size_t>(N / BN) * R * 2 * BN);
+}
+
+hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const void* zero,
+                                   int Nimg, int H, int W, int C, int N, int taps, const void* z,
+                                   const float* sc, const float* bi, const float* mean,
+                                   const float* invstd, float* part, float* sdz, float* sdzx,
+                                   hipStream_t st) {
+  const int64_t M = static_cast<int64_t>(Nimg) * H * W;
+  if (C % kBK || N % 64 || (taps != 1 && taps != 9) || M < 1 || M >= (1ll << 31) ||
+      static_cast<int64_t>(taps) * C > 65536 || !z || !sc || !bi || !mean || !invstd || !part ||
+      !sdz || !sdzx)
+    return hipErrorInvalidValue;
+  GArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(x);
+  a.w = reinterpret_cast<const uint16_t*>(w);
+  a.y = reinterpret_cast<uint16_t*>(y);
+  a.zero = reinterpret_cast<const uint16_t*>(zero);
+  a.M = static_cast<int>(M);
+  a.C = C;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.HW = H * W;
+  a.S = 1;
+  a.IH = H;
+  a.IW = W;
+  a.IHW = H * W;
+  a.KS = taps * C / kBK;
+  a.part = part;
+  a.shift = mean;
+  a.sz = reinterpret_cast<const uint16_t*>(z);
+  a.ep_sc = sc;
+  a.ep_bi = bi;
+  hipError_t e = taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
+  if (e != hipSuccess) return e;
+  int BM, BN;
+  tile_of(N, &BM, &BN);
+  const int R = static_cast<int>((M + BM - 1) / BM) * (BM / 64);
+  return launch_bnbwd_sums_finalize(part, R, BN, N, invstd, sdz, sdzx, st,
+                                    part + static_cast<size_t>(N / BN) * R * 2 * BN);
 }
 
 }  // namespace cml

@@ -85,6 +85,12 @@ hipError_t launch_bn_fwd(const void* x, const void* res, void* y, void* mask, in
 // else recomputed from x (only valid without a residual); dres (optional) receives the masked
 // output gradient (the residual input's gradient). dx == null: the reduction only (sums, dgamma,
 // dbeta), for consumers that apply the backward in their own prologue.
+// Apply half of a training BN + ReLU backward (ReLU mask recomputed from x) from its sums
+// (sdz = sum dy', sdzx = sum dy' xhat): dx = gamma invstd (dy' - sdz / M - xhat sdzx / M).
+hipError_t launch_bn_bwd_apply(const void* dy, const void* x, void* dx, int64_t M, int C,
+                               const void* gamma, const void* beta, const float* mean,
+                               const float* invstd, const float* sdz, const float* sdzx,
+                               hipStream_t st);
 hipError_t launch_bn_bwd(const void* dy, const void* dy2, const void* x, const void* mask,
                          void* dx, void* dres, int64_t M, int C, const void* gamma,
                          const void* beta, const float* mean, const float* invstd, void* dgamma,
@@ -316,6 +322,16 @@ hipError_t launch_conv3x3_bn_fwd(const void* x, const void* w, void* y, float* p
 // finalized like conv1x1_bn_fwd (running stats updated when rmean / rvar are non-null); part:
 // conv_gemm_part_floats floats.
 size_t conv_gemm_part_floats(int64_t M, int N);
+// 3x3 (or 1x1) stride-1 implicit GEMM whose output y is the gradient of relu(bn(z)) (z [M][N],
+// bn's affine sc / bi and batch statistics mean / invstd): also that backward's sums {sdz, sdzx}
+// (part: conv_gemm_part_floats floats).
+hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const void* zero,
+                                   int Nimg, int H, int W, int C, int N, int taps, const void* z,
+                                   const float* sc, const float* bi, const float* mean,
+                                   const float* invstd, float* part, float* sdz, float* sdzx,
+                                   hipStream_t st);
+hipError_t launch_bnbwd_sums_finalize(const float* part, int R, int BN, int N, const float* invstd,
+                                      float* sdz, float* sdzx, hipStream_t st, float* fold);
 hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* zero, int Nimg,
                             int H, int W, int C, int N, int taps, hipStream_t st,
                             float* part = nullptr, const float* shift = nullptr,
@@ -356,9 +372,14 @@ hipError_t launch_conv1x1_cat_bnres(const void* x1, const void* x2, const float*
                                     const float* bi_cat, const void* w, const float* ep_sc,
                                     const float* ep_bi, const void* res, void* y, uint8_t* ymask,
                                     int64_t M, int K1, int K, int N, hipStream_t st);
+// mean / invstd (optional): also the sums {sdz, sdzx} of the backward of the BN + ReLU whose input
+// is x2 (N = K - K1), ReLU mask recomputed from x2; part: conv1x1_cat_part_floats floats
 hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2, const float* a_cat,
                               const float* c_cat, const void* w, void* y, int64_t M, int K1, int K,
-                              int N, hipStream_t st);
+                              int N, hipStream_t st, const float* mean = nullptr,
+                              const float* invstd = nullptr, float* part = nullptr,
+                              float* sdz = nullptr, float* sdzx = nullptr);
+size_t conv1x1_cat_part_floats(int64_t M, int K, int N);
 hipError_t launch_conv1x1_bnbwd(const void* g, const void* z, const uint8_t* mask, const float* ca,
                                 const float* cb, const float* cc, const void* w, void* y,
                                 int64_t M, int K, int N, hipStream_t st);

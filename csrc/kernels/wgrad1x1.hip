@@ -353,6 +353,86 @@ __global__ __launch_bounds__(256) void wgrad1x1_fold_kernel(const float* __restr
   }
 }
 
+// The same fold for many splits over few outputs (Gram matrices / column sums of 64-channel
+// activations: S up to 2048 over n = 64..4096, where the kernel above runs 1-16 workgroups whose
+// threads each walk all S rows, ~27 us per call). Here 16 split lanes share 64 outputs: lane sl
+// sums splits sl, sl + 16, ... (8 loads in flight; a wave reads 4 split rows x 256 contiguous B),
+// then lane 0 adds the 16 lane sums in lane order. Fixed order: deterministic.
+template <bool BF16>
+__global__ __launch_bounds__(256) void wgrad_fold_wide_kernel(const float* __restrict__ part,
+                                                              int S, int64_t n,
+                                                              void* __restrict__ out) {
+  __shared__ float4 red[16][17];
+  const int cg = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int64_t e = (static_cast<int64_t>(blockIdx.x) * 16 + cg) * 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < n) {
+    int k = sl;
+    for (; k + 7 * 16 < S; k += 8 * 16) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k + 16 * u) * n + e);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s.x += v[u].x;
+        s.y += v[u].y;
+        s.z += v[u].z;
+        s.w += v[u].w;
+      }
+    }
+    for (; k < S; k += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(part + static_cast<int64_t>(k) * n + e);
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+  }
+  red[sl][cg] = s;
+  __syncthreads();
+  if (sl != 0 || e >= n) return;
+#pragma unroll
+  for (int j = 1; j < 16; ++j) {
+    const float4 v = red[j][cg];
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  if constexpr (BF16) {
+    uint2 o;
+    o.x = static_cast<uint32_t>(f2bf(s.x)) | (static_cast<uint32_t>(f2bf(s.y)) << 16);
+    o.y = static_cast<uint32_t>(f2bf(s.z)) | (static_cast<uint32_t>(f2bf(s.w)) << 16);
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + e) = o;
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + e) = s;
+  }
+}
+
+// Splits from which the wide fold is used (CML_FOLD_WIDE_MIN, default 32; 0 disables it: A/B).
+int fold_wide_min() {
+  static const int v = [] {
+    const char* e = getenv("CML_FOLD_WIDE_MIN");
+    return e ? atoi(e) : 32;
+  }();
+  return v;
+}
+
+// out[0:n] = sum over S rows of part [S][n] (n % 4 == 0), fixed order, bf16 or fp32 out.
+void fold_splits(const float* part, int S, int64_t n, void* out, bool out_bf16, hipStream_t st) {
+  const int wmin = fold_wide_min();
+  if (wmin > 0 && S >= wmin) {
+    const int64_t b = (n + 63) / 64;
+    if (out_bf16) wgrad_fold_wide_kernel<true><<<static_cast<unsigned>(b), 256, 0, st>>>(part, S, n, out);
+    else wgrad_fold_wide_kernel<false><<<static_cast<unsigned>(b), 256, 0, st>>>(part, S, n, out);
+    return;
+  }
+  const int fb = static_cast<int>((n / 4 + 255) / 256);
+  if (out_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, out);
+  else wgrad1x1_fold_kernel<false><<<fb, 256, 0, st>>>(part, S, n, out);
+}
+
 }  // namespace
 
 namespace {
@@ -506,23 +586,15 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
   }
 #undef CML_WG_TILE
   if (!ok) return hipErrorInvalidValue;
-  if (cs) {
-    const int cb = (Co / 4 + 255) / 256;
-    wgrad1x1_fold_kernel<false><<<cb, 256, 0, st>>>(cs_part, S, Co, cs);
-  }
-  const int64_t n = static_cast<int64_t>(Co) * Ci;
-  const int fb = static_cast<int>((n / 4 + 255) / 256);
-  if (dw_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, dw);
-  else wgrad1x1_fold_kernel<false><<<fb, 256, 0, st>>>(part, S, n, dw);
+  if (cs) fold_splits(cs_part, S, Co, cs, false, st);
+  fold_splits(part, S, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, st);
   return hipGetLastError();
 }
 
 hipError_t launch_wgrad_fold(const float* part, int S, int64_t n, void* out, bool out_bf16,
                              hipStream_t st) {
   if (S < 1 || n % 4) return hipErrorInvalidValue;
-  const int fb = static_cast<int>((n / 4 + 255) / 256);
-  if (out_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, out);
-  else wgrad1x1_fold_kernel<false><<<fb, 256, 0, st>>>(part, S, n, out);
+  fold_splits(part, S, n, out, out_bf16, st);
   return hipGetLastError();
 }
 
@@ -614,10 +686,7 @@ hipError_t launch_wgrad3x3(const void* dy, const void* x, float* part, void* dw,
   const bool ok = pro_sc ? launch_tile_tap<true>(TM, TN, grid, lds, st, dyp, xp, part, static_cast<int>(P), Co, Ci, tiles_n, cps, pro_sc, pro_bi, tg)
                          : launch_tile_tap<false>(TM, TN, grid, lds, st, dyp, xp, part, static_cast<int>(P), Co, Ci, tiles_n, cps, nullptr, nullptr, tg);
   if (!ok) return hipErrorInvalidValue;
-  const int64_t n = 9ll * Co * Ci;
-  const int fb = static_cast<int>((n / 4 + 255) / 256);
-  if (dw_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, dw);
-  else wgrad1x1_fold_kernel<false><<<fb, 256, 0, st>>>(part, S, n, dw);
+  fold_splits(part, S, 9ll * Co * Ci, dw, dw_bf16, st);
   return hipGetLastError();
 }
 

@@ -225,6 +225,91 @@ def test_conv1x1_cat(cuda, N, K1, K2, No, H):
     _close(_rows(y), ref, 1e-2)
 
 
+@pytest.mark.parametrize("N,K1,K2,H", [(2, 256, 64, 28), (3, 512, 128, 14), (2, 1024, 256, 9),
+                                       (1, 256, 64, 3)])
+def test_conv1x1_cat_bnsums(cuda, N, K1, K2, H):
+    """conv1x1_cat whose output feeds relu(bn(x2))'s backward: the epilogue's sums (ReLU mask
+    recomputed from x2) against fp64 sums of the kernel's own output, and bn_bwd_apply from those
+    sums against the two-pass bn_bwd."""
+    g0 = torch.Generator(device=cuda).manual_seed(24)
+    g = _nhwc(torch.randn(N, K1, H, H, device=cuda, generator=g0).bfloat16())
+    x2 = _nhwc(torch.randn(N, K2, H, H, device=cuda, generator=g0).bfloat16())
+    M = N * H * H
+    mask = _rand_mask(M, K1, cuda, g0)
+    a = torch.randn(K1, device=cuda, generator=g0)
+    c = torch.randn(K1, device=cuda, generator=g0) * 0.1
+    gam = (torch.rand(K2, device=cuda, generator=g0) + 0.5).bfloat16()
+    bet = (torch.randn(K2, device=cuda, generator=g0) * 0.1).bfloat16()
+    X = _rows(x2).double()
+    mean = X.mean(0).float()
+    invstd = (X.var(0, unbiased=False) + 1e-5).rsqrt().float()
+    sc = gam.float() * invstd
+    bi = bet.float() - mean * sc
+    w = (torch.randn(K2, K1 + K2, device=cuda, generator=g0) * (K1 + K2) ** -0.5).bfloat16()
+    a_cat, c_cat = torch.cat([a, sc]), torch.cat([c, bi])
+    y, s, q = _lib().conv1x1_cat_bnsums(g, mask, x2, a_cat, c_cat, w, mean, invstd)
+    _close(_rows(y), _rows(_lib().conv1x1_cat(g, mask, x2, a_cat, c_cat, w)), 1e-2)
+    m = (torch.addcmul(bi, _rows(x2), sc) > 0).double()
+    dyv = _rows(y).double() * m
+    s_ref = dyv.sum(0)
+    q_ref = (dyv * (X - mean.double()) * invstd.double()).sum(0)
+    _close(s, s_ref, 1e-5)
+    _close(q, q_ref, 1e-5)
+    dz = _lib().bn_bwd_apply(y, x2, gam, bet, mean, invstd, s, q)
+    dz_ref, _, _, _ = _lib().bn_bwd(y, None, x2, None, gam, bet, mean, invstd, True, False)
+    _close(_rows(dz), _rows(dz_ref), 1e-2)
+
+
+@pytest.mark.parametrize("N,Cin,Co,H", [(2, 64, 64, 20), (2, 128, 128, 14), (3, 256, 256, 7),
+                                        (2, 512, 512, 5), (1, 64, 128, 3)])
+def test_conv_gemm_bnsums(cuda, N, Cin, Co, H):
+    """3x3 implicit GEMM whose output feeds relu(bn(z))'s backward: dy equal to conv_gemm's, the
+    epilogue sums against fp64 sums of that output, bn_bwd_apply against the two-pass bn_bwd."""
+    g0 = torch.Generator(device=cuda).manual_seed(25)
+    x = _nhwc(torch.randn(N, Cin, H, H, device=cuda, generator=g0).bfloat16())
+    z = _nhwc(torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16())
+    w = (torch.randn(Co, 9 * Cin, device=cuda, generator=g0) * (9 * Cin) ** -0.5).bfloat16()
+    zero = torch.zeros(64, device=cuda, dtype=torch.bfloat16)
+    gam = (torch.rand(Co, device=cuda, generator=g0) + 0.5).bfloat16()
+    bet = (torch.randn(Co, device=cuda, generator=g0) * 0.1).bfloat16()
+    Z = _rows(z).double()
+    mean = Z.mean(0).float()
+    invstd = (Z.var(0, unbiased=False) + 1e-5).rsqrt().float()
+    sc = gam.float() * invstd
+    bi = bet.float() - mean * sc
+    y, s, q = _lib().conv_gemm_bnsums(x, w, 9, zero, z, sc, bi, mean, invstd)
+    assert torch.equal(y, _lib().conv_gemm(x, w, 9, zero))
+    m = (torch.addcmul(bi, _rows(z), sc) > 0).double()
+    dyv = _rows(y).double() * m
+    _close(s, dyv.sum(0), 1e-5)
+    _close(q, (dyv * (Z - mean.double()) * invstd.double()).sum(0), 1e-5)
+    dz = _lib().bn_bwd_apply(y, z, gam, bet, mean, invstd, s, q)
+    dz_ref, _, _, _ = _lib().bn_bwd(y, None, z, None, gam, bet, mean, invstd, True, False)
+    _close(_rows(dz), _rows(dz_ref), 1e-2)
+
+
+def test_bottleneck_bn1_dgrad_sums_matches_unfused(cuda):
+    """A bottleneck block's gradients with bn1's backward sums from the 3x3 data gradient's
+    epilogue equal those of bn_act + its own reduction pass."""
+    import consensusml_amd.models.resnet as R
+    import consensusml_amd.ops.conv as C
+    torch.manual_seed(5)
+    blk = R.Bottleneck(256, 64).to(cuda, torch.bfloat16).to(memory_format=torch.channels_last)
+    blk.train()
+    x0 = _nhwc(torch.randn(4, 256, 14, 14, device=cuda).relu().bfloat16())
+    gy = _nhwc(torch.randn(4, 256, 14, 14, device=cuda).bfloat16())
+    grads = {}
+    for on in (True, False):
+        C.BN1_DGRAD_SUMS = on
+        b = copy.deepcopy(blk)
+        x = x0.clone().requires_grad_(True)
+        b(x).backward(gy)
+        grads[on] = [x.grad] + [p.grad for p in b.parameters()]
+    C.BN1_DGRAD_SUMS = True
+    for a, r in zip(grads[True], grads[False]):
+        _close(a, r, 2e-2)
+
+
 @pytest.mark.parametrize("Co,Ci,H", [(256, 64, 28), (512, 128, 14), (64, 64, 20), (128, 128, 9),
                                     (1024, 256, 7), (256, 256, 7), (512, 512, 5)])
 def test_wgrad1x1_ex_modes(cuda, Co, Ci, H):

@@ -48,3 +48,18 @@ def test_conv1x1_module_own_wgrad_matches_miopen(cuda):
             R.OWN_WGRAD1X1 = True
     assert _rel(out[True][0], out[False][0]) < 1e-2
     assert _rel(out[True][1], out[False][1]) < 1e-2
+
+
+@pytest.mark.parametrize("S,n", [(1, 64), (7, 4096), (31, 256), (32, 256), (100, 4100),
+                                 (2048, 4096), (2048, 64), (129, 65536), (8, 262144)])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_split_fold_vs_fp64(cuda, S, n, bf16):
+    """The split-K fold (narrow kernel below 32 splits, wide 16-lane kernel from 32) against an
+    fp64 sum; bitwise repeatable."""
+    torch.manual_seed(S * 7 + n)
+    part = torch.randn(S, n, device=cuda)
+    out = lib().split_fold(part, bf16)
+    assert out.shape == (n,) and out.dtype == (torch.bfloat16 if bf16 else torch.float32)
+    ref = part.double().sum(0)
+    assert _rel(out, ref) < (6e-3 if bf16 else 1e-6)
+    assert torch.equal(out, lib().split_fold(part, bf16))
