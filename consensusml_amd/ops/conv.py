@@ -241,15 +241,19 @@ GRAM_STATS = os.environ.get("CML_GRAM_STATS", "1") == "1"
 
 # recompute tails: bn2's backward sums from the epilogue of the GEMM that produces its output
 # gradient dy2 (``conv1x1_cat_bnsums``, ReLU mask recomputed from z2), so only bn2's apply pass
-# remains (CML_CAT_BNSUMS=0: the separate reduction pass)
+# remains (CML_CAT_BNSUMS=0: the separate reduction pass). Only up to CML_CAT_BNSUMS_MAXC
+# channels (default 64, layer 1): the sums variant runs MT = 1 tiles (its MT = 2 tile spills), and
+# on the 128 / 256-channel GEMMs that costs about what the reduction pass did
+# (profiles/r02_prof53_*: 722 vs 658 us per layer-2/3 call, 1160 vs 1095 us per layer-1 call).
 CAT_BNSUMS = os.environ.get("CML_CAT_BNSUMS", "1") == "1"
+CAT_BNSUMS_MAXC = int(os.environ.get("CML_CAT_BNSUMS_MAXC", "64"))
 
 
 def _cat_dgrad_bn2(L, gy, mask, z, a1, c1, sc, bi, w_cat, g2, b2, mean2, invstd2):
     """dy2 = [a1 (mask ? gy : 0) + c1 | relu(z sc + bi)] w_cat^T, then bn2's (BN + ReLU on z)
     backward: (dz, dgamma2, dbeta2)."""
     a_cat, c_cat = torch.cat([a1, sc]), torch.cat([c1, bi])
-    if CAT_BNSUMS:
+    if CAT_BNSUMS and z.shape[1] <= CAT_BNSUMS_MAXC:
         dy2, s2, q2 = L.conv1x1_cat_bnsums(gy, mask, z, a_cat, c_cat, w_cat, mean2, invstd2)
         M = z.numel() // z.shape[1]
         _, _, _, dg2, db2 = L.bn_bwd_coeffs(s2, q2, g2, mean2, invstd2, M)
