@@ -335,13 +335,15 @@ class _RecomputeTailFn(torch.autograd.Function):
         if gram is None:
             gram, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
         W3 = w.reshape(Co, Ci).float()
-        q = i3 * ((W3 * P).sum(1) - m3 * s)
+        q = torch.addcmul((W3 * P).sum(1), m3, s, value=-1.0).mul_(i3)
         ca, cb, cc, dg3, db3 = L.bn_bwd_coeffs(s, q, g3, m3, i3, M)
+        cbW3 = cb[:, None] * W3   # diag(b) W3, shared by dW3 and G
         dw = None
         if ctx.needs_input_grad[5]:
-            dw = (ca[:, None] * P + cb[:, None] * (W3 @ gram) + cc[:, None] * cy[None, :])
+            # dW3 = diag(a) P + diag(b) W3 Gram + c cy^T (fewer small launches as addcmul / addmm)
+            dw = torch.addmm(torch.addcmul(torch.outer(cc, cy), ca[:, None], P), cbW3, gram)
             dw = dw.to(w.dtype).view_as(w)
-        G = W3.t() @ (cb[:, None] * W3)
+        G = W3.t() @ cbW3
         w_cat = torch.cat([W3.t(), G.t()], 1).to(torch.bfloat16).contiguous()
         dz, dg2, db2 = _cat_dgrad_bn2(L, gy, mask, z, ca, cc, sc, bi, w_cat, g2, b2, mean2,
                                       invstd2)
@@ -429,24 +431,25 @@ class _RecomputeDownTailFn(torch.autograd.Function):
             gramd, cx = L.wgrad1x1_ex(x, x, None, None, 0, None, None, None, None, True)
         W3 = w3.reshape(Co, P_).float()
         Wd = wd.reshape(Co, Cin).float()
-        q3 = i3 * ((W3 * P3).sum(1) - m3 * s)
-        qd = idd * ((Wd * Pd).sum(1) - md * s)
+        q3 = torch.addcmul((W3 * P3).sum(1), m3, s, value=-1.0).mul_(i3)
+        qd = torch.addcmul((Wd * Pd).sum(1), md, s, value=-1.0).mul_(idd)
         a3, b3c, c3, dg3, db3 = L.bn_bwd_coeffs(s, q3, g3, m3, i3, M)
         ad, bdc, cd, dgd, dbd = L.bn_bwd_coeffs(s, qd, gd, md, idd, M)
+        bW3, bWd = b3c[:, None] * W3, bdc[:, None] * Wd
         dw3 = dwd = None
         if ctx.needs_input_grad[5]:
-            dw3 = (a3[:, None] * P3 + b3c[:, None] * (W3 @ gram3) + c3[:, None] * cy[None, :])
+            dw3 = torch.addmm(torch.addcmul(torch.outer(c3, cy), a3[:, None], P3), bW3, gram3)
             dw3 = dw3.to(w3.dtype).view_as(w3)
         if ctx.needs_input_grad[11]:
-            dwd = (ad[:, None] * Pd + bdc[:, None] * (Wd @ gramd) + cd[:, None] * cx[None, :])
+            dwd = torch.addmm(torch.addcmul(torch.outer(cd, cx), ad[:, None], Pd), bWd, gramd)
             dwd = dwd.to(wd.dtype).view_as(wd)
-        G3 = W3.t() @ (b3c[:, None] * W3)
+        G3 = W3.t() @ bW3
         dz, dg2, db2 = _cat_dgrad_bn2(
             L, gy, mask, z, a3, c3, sc, bi,
             torch.cat([W3.t(), G3.t()], 1).to(torch.bfloat16).contiguous(), g2, b2, mean2, invstd2)
         dx = None
         if ctx.needs_input_grad[10]:
-            Gd = Wd.t() @ (bdc[:, None] * Wd)
+            Gd = Wd.t() @ bWd
             dx = L.conv1x1_cat(gy, mask, x, torch.cat([ad, _const(Cin, 1.0, dev)]),
                                torch.cat([cd, _const(Cin, 0.0, dev)]),
                                torch.cat([Wd.t(), Gd.t()], 1).to(torch.bfloat16).contiguous())
