@@ -527,7 +527,8 @@ def down_tail_recompute_s2_ok(x: torch.Tensor, planes: int, down_conv) -> bool:
     """Stride-2 downsample tails (ResNet-50 layer 2) on the recompute kernels: the convolution
     reads x[:, :, ::2, ::2], materialised once (``subsample2``), so the stride-1 kernels apply."""
     return (RECOMPUTE_DOWN_TAIL_S2 and down_conv.stride[0] == 2 and down_conv.stride[1] == 2
-            and planes in (64, 128) and x.shape[1] % 64 == 0 and x.shape[1] <= 256)
+            and planes in (64, 128, 256, 512) and x.shape[1] % 64 == 0
+            and x.shape[1] <= DOWN_TAIL_S2_MAX_CIN)
 
 
 # stride-2 downsample tails: the compact data gradient is added at the even pixels by conv1's
@@ -535,6 +536,9 @@ def down_tail_recompute_s2_ok(x: torch.Tensor, planes: int, down_conv) -> bool:
 S2_LINK_DGRAD = os.environ.get("CML_S2_LINK_DGRAD", "1") == "1"
 # CML_RECOMPUTE_DOWN_TAIL_S2=0: stride-2 downsample tails keep stored z3 / zd (bn_add_bn_relu)
 RECOMPUTE_DOWN_TAIL_S2 = os.environ.get("CML_RECOMPUTE_DOWN_TAIL_S2", "1") == "1"
+# widest block input of a recompute stride-2 downsample tail (256: layer 2; 512: also layer 3,
+# step 128.9 / 129.2 -> 128.0 / 128.5 ms and -1.1 GiB peak, profiles/r02_down_tail_l3_58/)
+DOWN_TAIL_S2_MAX_CIN = int(os.environ.get("CML_DOWN_TAIL_S2_MAX_CIN", "512"))
 
 
 def down_tail_recompute_ok(x: torch.Tensor, planes: int, down_conv) -> bool:

@@ -373,13 +373,16 @@ def test_identity_chain_recompute_tail(cuda, planes, H):
 
 
 @pytest.mark.parametrize("cin,planes,H,stride", [(64, 64, 28, 1), (128, 128, 14, 1),
-                                                 (256, 128, 28, 2), (128, 64, 14, 2)])
-def test_downsample_recompute_tail(cuda, cin, planes, H, stride):
+                                                 (256, 128, 28, 2), (128, 64, 14, 2),
+                                                 (512, 256, 14, 2), (1024, 512, 8, 2)])
+def test_downsample_recompute_tail(cuda, cin, planes, H, stride, monkeypatch):
     """Downsample block (stride 1, or stride 2 through ops.conv.subsample2) with the recompute
     tail (no z3 / zd) vs the stored path, both against an fp32 copy: output, input gradient,
     parameter gradients, running statistics."""
     from consensusml_amd.models import resnet
     from consensusml_amd.models.resnet import Bottleneck
+    import consensusml_amd.ops.conv as C
+    monkeypatch.setattr(C, "DOWN_TAIL_S2_MAX_CIN", 1024)
     torch.manual_seed(3)
     m_on = Bottleneck(cin, planes, stride, downsample=True)
     for mod in m_on.modules():
