@@ -147,8 +147,7 @@ class _BNReLUConv1x1BNStatsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, gamma, beta, mean, invstd, w, rmean, rvar, eps, momentum, dgrad_gemm,
                 own_wgrad):
-        sc = gamma.float() * invstd
-        bi = beta.float() - mean * sc
+        sc, bi = _affine(gamma, beta, mean, invstd)
         y, m3, i3 = lib().conv1x1_bn_fwd(z, w, sc, bi, rmean, rmean, rvar, 1, True, eps, momentum)
         ctx.save_for_backward(z, gamma, beta, mean, invstd, w, sc, bi)
         ctx.dgrad_gemm, ctx.own_wgrad = dgrad_gemm, own_wgrad
@@ -180,8 +179,7 @@ class _BNReLUConv1x1BNResFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, g2, b2, mean2, invstd2, w, g3, b3, res, rmean3, rvar3, eps, momentum,
                 res_link, out_link):
-        sc = g2.float() * invstd2
-        bi = b2.float() - mean2 * sc
+        sc, bi = _affine(g2, b2, mean2, invstd2)
         z3, m3, i3 = lib().conv1x1_bn_fwd(z, w, sc, bi, rmean3, rmean3, rvar3, 1, True, eps,
                                           momentum)
         y, _, _, mask = lib().bn_fwd(z3, res, g3, b3, None, None, m3, i3, eps, momentum, True,
@@ -222,6 +220,19 @@ class _BNReLUConv1x1BNResFn(torch.autograd.Function):
             else:
                 dres = mg.materialize()
         return (dz, dg2, db2, None, None, dw, dg3, db3, dres) + (None,) * 6
+
+
+def _affine(gamma: torch.Tensor, beta: torch.Tensor, mean: torch.Tensor, invstd: torch.Tensor):
+    """(sc, bi) = (gamma invstd, beta - mean sc) in fp32: one ``bn_affine`` launch (bit-identical to
+    ``gamma.float() * invstd`` and ``beta.float() - mean * sc``, which take five)."""
+    if not BN_AFFINE_KERNEL:
+        sc = gamma.float() * invstd
+        return sc, beta.float() - mean * sc
+    ab = lib().bn_affine(gamma, beta, mean, invstd)
+    return ab[0], ab[1]
+
+
+BN_AFFINE_KERNEL = os.environ.get("CML_BN_AFFINE_KERNEL", "1") == "1"   # 0: PyTorch ops (A/B)
 
 
 _CONST = {}
@@ -292,8 +303,7 @@ class _RecomputeTailFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, g2, b2, mean2, invstd2, w, g3, b3, res, rmean3, rvar3, eps, momentum,
                 res_link, out_link):
-        sc = g2.float() * invstd2
-        bi = b2.float() - mean2 * sc
+        sc, bi = _affine(g2, b2, mean2, invstd2)
         wc = w.contiguous()
         L = lib()
         gram = cy = None
@@ -304,8 +314,7 @@ class _RecomputeTailFn(torch.autograd.Function):
                                      momentum)
         else:
             m3, i3 = L.conv1x1_bn_stats_only(z, wc, sc, bi, rmean3, rmean3, rvar3, eps, momentum)
-        sc3 = g3.float() * i3
-        bi3 = b3.float() - m3 * sc3
+        sc3, bi3 = _affine(g3, b3, m3, i3)
         y, mask = L.conv1x1_bnres(z, wc, sc, bi, sc3, bi3, res)
         ctx.gram = (gram, cy)
         ctx.save_for_backward(z, g2, b2, mean2, invstd2, w, sc, bi, mask, g3, m3, i3)
@@ -373,8 +382,7 @@ class _RecomputeDownTailFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, g2, b2, mean2, invstd2, w3, g3, b3, rm3, rv3, x, wd, gd, bd, rmd, rvd,
                 eps, momentum, out_link):
-        sc = g2.float() * invstd2
-        bi = b2.float() - mean2 * sc
+        sc, bi = _affine(g2, b2, mean2, invstd2)
         L = lib()
         w3c, wdc = w3.contiguous(), wd.contiguous()
         grams = (None, None, None, None)
@@ -390,9 +398,9 @@ class _RecomputeDownTailFn(torch.autograd.Function):
             md, idd = L.conv1x1_bn_stats_only(x, wdc, None, None, rmd, rmd, rvd, eps, momentum)
         ctx.grams = grams
         Co, P_, Cin = w3.shape[0], w3.shape[1], wd.shape[1]
-        sc3 = g3.float() * i3
-        scd = gd.float() * idd
-        bias = (b3.float() - m3 * sc3) + (bd.float() - md * scd)
+        sc3, bi3 = _affine(g3, b3, m3, i3)
+        scd, bid = _affine(gd, bd, md, idd)
+        bias = bi3 + bid
         w_cat = torch.cat([w3c.view(Co, P_).float() * sc3[:, None],
                            wdc.view(Co, Cin).float() * scd[:, None]], 1).to(torch.bfloat16)
         dev = z.device
@@ -691,8 +699,7 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
         Co, Ci = w.shape[0], w.shape[1]
         # w_rot[ci][ky][kx][co] = w[co][ci][2 - ky][2 - kx], flattened k = tap Co + co
         wr = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co).contiguous()
-        sc = g1.float() * invstd1
-        bi = b1.float() - mean1 * sc
+        sc, bi = _affine(g1, b1, mean1, invstd1)
         dy1, s1, q1 = L.conv_gemm_bnsums(dz2, wr, 9, _zero_row(dz2.device), z1, sc, bi, mean1,
                                          invstd1)
         M = z1.numel() // z1.shape[1]

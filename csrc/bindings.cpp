@@ -925,6 +925,24 @@ std::vector<Tensor> conv1x1_cat_bnsums(const Tensor& g, const Tensor& mask, cons
   return {y, sdz, sdzx};
 }
 
+// {sc, bi} fp32 [2, C]: sc = gamma invstd, bi = beta - mean sc (gamma / beta bf16 [C]).
+Tensor bn_affine(const Tensor& gamma, const Tensor& beta, const Tensor& mean, const Tensor& invstd) {
+  const int64_t C = gamma.numel();
+  TORCH_CHECK(gamma.scalar_type() == at::kBFloat16 && beta.scalar_type() == at::kBFloat16 &&
+                  gamma.is_contiguous() && beta.is_contiguous() && beta.numel() == C && C > 0,
+              "bn_affine: contiguous bf16 gamma / beta [C]");
+  check_dev(gamma, "gamma");
+  check_dev(beta, "beta");
+  const c10::DeviceGuard guard(gamma.device());
+  Tensor out = at::empty({2, C}, gamma.options().dtype(at::kFloat));
+  CML_CHECK_HIP(cml::launch_bn_affine(gamma.data_ptr(), beta.data_ptr(),
+                                      opt_ptr<const float>(mean, at::kFloat, "mean", C),
+                                      opt_ptr<const float>(invstd, at::kFloat, "invstd", C),
+                                      static_cast<int>(C), out.data_ptr<float>(),
+                                      out.data_ptr<float>() + C, cur_stream()));
+  return out;
+}
+
 // Apply half of a BN + ReLU backward (mask recomputed from x) from its sums: dy, x [N, C, H, W]
 // NHWC bf16 -> dx.
 Tensor bn_bwd_apply(const Tensor& dy_in, const Tensor& x, const Tensor& gamma, const Tensor& beta,
@@ -1746,6 +1764,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "two BN'd 1x1 convs summed + ReLU in one K-concatenated GEMM -> {y, mask}");
   m.def("conv1x1_cat_bnsums", &conv1x1_cat_bnsums,
         "conv1x1_cat + the sums of the BN + ReLU backward its output feeds");
+  m.def("bn_affine", &bn_affine, "BN affine (gamma invstd, beta - mean sc) of batch statistics");
   m.def("bn_bwd_apply", &bn_bwd_apply, "apply half of a BN + ReLU backward from its sums");
   m.def("conv1x1_cat", &conv1x1_cat, "two-source (masked affine | BN-ReLU) 1x1 conv along K");
   m.def("split_fold", &split_fold, "fixed-order fold of a split-K partial slab");

@@ -647,6 +647,36 @@ hipError_t launch_bn_bwd(const void* dy, const void* dy2, const void* x, const v
   return hipGetLastError();
 }
 
+namespace {
+// sc = gamma invstd, bi = beta - mean sc per channel: the BN affine the fused conv prologues /
+// epilogues take (one launch instead of PyTorch's five small ones; rounded exactly as those:
+// separate fp32 multiply and subtract, no contraction)
+__global__ __launch_bounds__(256) void bn_affine_kernel(const uint16_t* __restrict__ gamma,
+                                                        const uint16_t* __restrict__ beta,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, int C,
+                                                        float* __restrict__ sc,
+                                                        float* __restrict__ bi) {
+#pragma clang fp contract(off)
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  // (plain operators under contract(off): the __f*_rn helpers are inlined with contraction on)
+  const float s = __uint_as_float(static_cast<uint32_t>(gamma[c]) << 16) * invstd[c];
+  sc[c] = s;
+  const float ms = mean[c] * s;
+  bi[c] = __uint_as_float(static_cast<uint32_t>(beta[c]) << 16) - ms;
+}
+}  // namespace
+
+hipError_t launch_bn_affine(const void* gamma, const void* beta, const float* mean,
+                            const float* invstd, int C, float* sc, float* bi, hipStream_t st) {
+  if (C < 1) return hipErrorInvalidValue;
+  bn_affine_kernel<<<(C + 255) / 256, 256, 0, st>>>(reinterpret_cast<const uint16_t*>(gamma),
+                                                   reinterpret_cast<const uint16_t*>(beta), mean,
+                                                   invstd, C, sc, bi);
+  return hipGetLastError();
+}
+
 hipError_t launch_bn_bwd_apply(const void* dy, const void* x, void* dx, int64_t M, int C,
                                const void* gamma, const void* beta, const float* mean,
                                const float* invstd, const float* sdz, const float* sdzx,

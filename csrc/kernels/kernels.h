@@ -87,6 +87,9 @@ hipError_t launch_bn_fwd(const void* x, const void* res, void* y, void* mask, in
 // dbeta), for consumers that apply the backward in their own prologue.
 // Apply half of a training BN + ReLU backward (ReLU mask recomputed from x) from its sums
 // (sdz = sum dy', sdzx = sum dy' xhat): dx = gamma invstd (dy' - sdz / M - xhat sdzx / M).
+// BN affine of batch statistics: sc = gamma invstd, bi = beta - mean sc (fp32 [C]; gamma / beta bf16)
+hipError_t launch_bn_affine(const void* gamma, const void* beta, const float* mean,
+                            const float* invstd, int C, float* sc, float* bi, hipStream_t st);
 hipError_t launch_bn_bwd_apply(const void* dy, const void* x, void* dx, int64_t M, int C,
                                const void* gamma, const void* beta, const float* mean,
                                const float* invstd, const float* sdz, const float* sdzx,

@@ -482,3 +482,18 @@ def test_conv1x1_link_s2(cuda, N, K, No, H, W):
     full[:, :, ::2, ::2] = g.float()
     ref = _rows(dy) @ w.float().t() + _rows(full)
     _close(_rows(y), ref, 1e-2)
+
+
+@pytest.mark.parametrize("C", [64, 256, 2048, 100])
+def test_bn_affine_bit_identical(cuda, C):
+    """bn_affine (one launch) equals gamma.float() * invstd and beta.float() - mean * sc bit for
+    bit."""
+    g0 = torch.Generator(device=cuda).manual_seed(C)
+    gam = (torch.rand(C, device=cuda, generator=g0) + 0.5).bfloat16()
+    bet = torch.randn(C, device=cuda, generator=g0).bfloat16()
+    mean = torch.randn(C, device=cuda, generator=g0)
+    invstd = torch.rand(C, device=cuda, generator=g0) * 3 + 0.1
+    ab = _lib().bn_affine(gam, bet, mean, invstd)
+    sc = gam.float() * invstd
+    assert torch.equal(ab[0], sc)
+    assert torch.equal(ab[1], bet.float() - mean * sc)
