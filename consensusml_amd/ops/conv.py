@@ -128,6 +128,7 @@ class _Conv1x1BNStatsFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.dgrad_gemm, ctx.own_wgrad, ctx.link = stride, dgrad_gemm, own_wgrad, link
         ctx.mark_non_differentiable(mean, invstd)
+        ctx.set_materialize_grads(False)   # no zero-filled grads for the statistics outputs
         return y, mean, invstd
 
     @staticmethod
@@ -152,6 +153,7 @@ class _BNReLUConv1x1BNStatsFn(torch.autograd.Function):
         ctx.save_for_backward(z, gamma, beta, mean, invstd, w, sc, bi)
         ctx.dgrad_gemm, ctx.own_wgrad = dgrad_gemm, own_wgrad
         ctx.mark_non_differentiable(m3, i3)
+        ctx.set_materialize_grads(False)   # no zero-filled grads for the statistics outputs
         return y, m3, i3
 
     @staticmethod
@@ -662,6 +664,7 @@ class _Conv3x3BNStatsFn(torch.autograd.Function):
                                              eps, momentum)
         ctx.save_for_backward(x, w)
         ctx.mark_non_differentiable(mean, invstd)
+        ctx.set_materialize_grads(False)   # no zero-filled grads for the statistics outputs
         return y, mean, invstd
 
     @staticmethod
@@ -689,6 +692,7 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
                                     momentum)
         ctx.save_for_backward(z1, g1, b1, mean1, invstd1, y1, w)
         ctx.mark_non_differentiable(m2, i2)
+        ctx.set_materialize_grads(False)   # no zero-filled grads for the statistics outputs
         return z2, m2, i2
 
     @staticmethod
@@ -735,6 +739,7 @@ class _Conv3x3S2BNStatsFn(torch.autograd.Function):
                                              eps, momentum, 2)
         ctx.save_for_backward(x, w)
         ctx.mark_non_differentiable(mean, invstd)
+        ctx.set_materialize_grads(False)   # no zero-filled grads for the statistics outputs
         return y, mean, invstd
 
     @staticmethod
