@@ -218,7 +218,9 @@ class ConsensusEngine:
 
     def _make_child_pre(self, name: str):
         def pre(_mod, _inp):
-            if not self._learned:
+            # learn only from training forwards (evaluate() / no-grad forwards of a child may
+            # differ from how the training forward reads its parameters)
+            if not self._learned and self.flat.model.training and torch.is_grad_enabled():
                 self._invoked.add(name)
             for bi in self._child_buckets[name]:
                 self._wait_ag(bi)

@@ -102,8 +102,12 @@ class _Stages:
     def _p(self, *parts) -> str:
         return os.path.join(self.out_dir, *parts)
 
-    def done(self, name: str) -> bool:
-        return self.resume and RS.exists(self._p("results", name)) and self.saved is not None
+    def done(self, name: str, columns: Sequence[str] = ()) -> bool:
+        """A stage is finished when its result list (the commit marker, written last) exists
+        and the saved table holds every column the stage would add now (a run with other
+        lasso_reps / svm_runs / tree counts re-runs the stage instead of failing in restore)."""
+        return (self.resume and self.saved is not None and RS.exists(self._p("results", name))
+                and all(c in self.saved.columns for c in columns))
 
     def restore(self, name: str, columns: Sequence[str]) -> Dict[str, object]:
         """Reload a finished stage: its result list and its table columns."""
@@ -116,11 +120,13 @@ class _Stages:
     def finish(self, name: str, resultslist: Dict[str, object]) -> None:
         if self.out_dir is None or not _is_writer():
             return
-        RS.save_results(self._p("results", name), resultslist)
+        # the table first, the result list last: the result list is the stage's commit marker
+        # (done()), so an interruption between the two writes re-runs the stage
         os.makedirs(self.out_dir, exist_ok=True)
         tmp = self._p(TABLE_FILE + ".part")
         self.table.df.to_csv(tmp)
         os.replace(tmp, self._p(TABLE_FILE))
+        RS.save_results(self._p("results", name), resultslist)
 
 
 def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
@@ -173,7 +179,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
 
     # ---------------------------------------------------------------- SVM (svm4reps)
     svm_cols = [f"{n}_weights" for n, _, _ in svm_runs]
-    if st.done("svm4reps_resultslist"):
+    if st.done("svm4reps_resultslist", svm_cols):
         svm_res = st.restore("svm4reps_resultslist", svm_cols)
     else:
         members: List[Member] = []
@@ -206,7 +212,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
 
     # ---------------------------------------------------------------- lasso reps
     lasso_cols = [f"lasso_coef_rep{k + 1}" for k in range(lasso_reps)]
-    if st.done("lasso_resultslist"):
+    if st.done("lasso_resultslist", lasso_cols):
         lasso_res = st.restore("lasso_resultslist", lasso_cols)
     else:
         def lasso_member():
@@ -237,7 +243,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
 
     # ---------------------------------------------------------------- random forests
     rf_cols = [rf_column(n) for n in rf_trees]
-    if st.done("rf_noboost_resultslist"):
+    if st.done("rf_noboost_resultslist", rf_cols):
         rf_res = st.restore("rf_noboost_resultslist", rf_cols)
     else:
         members = []
@@ -268,7 +274,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
 
     # ---------------------------------------------------------------- boosted trees
     xgb_cols = [f"xg{i + 1}_imp" for i in range(len(xgb_configs))]
-    if st.done("xgb_resultslist"):
+    if st.done("xgb_resultslist", xgb_cols):
         xgb_res = st.restore("xgb_resultslist", xgb_cols)
     else:
         members = []

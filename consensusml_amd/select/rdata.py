@@ -196,12 +196,21 @@ def _decompress(raw: bytes) -> bytes:
     return raw
 
 
+# Limits for untrusted input: nesting depth of items (a Python frame chain per level, so a
+# crafted deeply nested stream raises RDataError instead of exhausting the C stack) and the
+# number of elements an ALTREP compact sequence may expand to (its length is file-supplied and
+# costs no stream bytes).
+MAX_DEPTH = 8192     # model formulas nest one call level per term: a 1984-gene terms object ~2000
+MAX_EXPANDED_ELEMENTS = 1 << 27
+
+
 class _Reader:
     def __init__(self, buf: bytes, strict: bool = False):
         self.b = memoryview(buf)
         self.p = 0
         self.refs: List[Any] = []
         self.strict = strict
+        self.depth = 0
 
     def _code(self, what: str) -> None:
         if self.strict:
@@ -259,6 +268,15 @@ class _Reader:
         return {}
 
     def item(self) -> Any:
+        if self.depth >= MAX_DEPTH:
+            raise RDataError(f"items nested deeper than {MAX_DEPTH} levels")
+        self.depth += 1
+        try:
+            return self._item()
+        finally:
+            self.depth -= 1
+
+    def _item(self) -> Any:
         flags = self.int()
         t = flags & 0xFF
         levels = flags >> 12
@@ -429,7 +447,7 @@ class _Reader:
             # CDR: continue the chain without recursion while it is the same pairlist kind
             nf = self.int()
             nt = nf & 0xFF
-            if nt in (LISTSXP, ATTRLISTSXP) and kind == "pairlist":
+            if nt in (LISTSXP, ATTRLISTSXP):   # (a call's arguments are a pairlist too)
                 flags, t = nf, nt
                 continue
             if nt in (NILVALUE_SXP, NILSXP):
@@ -457,13 +475,19 @@ class _Reader:
 
 
 def _expand_altrep(cls: Optional[str], state) -> Optional[RObj]:
+    if cls in ("compact_intseq", "compact_realseq") and isinstance(state, RVector):
+        if len(state.values) < 3:
+            raise RDataError(f"{cls} state has {len(state.values)} values, needs 3")
+        n = state.values[0]
+        if not np.isfinite(n) or not 0 <= n <= MAX_EXPANDED_ELEMENTS:
+            raise RDataError(f"{cls} of length {n}: outside [0, {MAX_EXPANDED_ELEMENTS}]")
+        n = int(n)
     if cls == "compact_intseq" and isinstance(state, RVector):
-        n, start, step = (int(x) for x in state.values[:3])
-        return RVector(np.arange(start, start + n * step, step, dtype=np.int64)[:n].astype(np.int32),
-                       INTSXP)
+        start, step = (int(x) for x in state.values[1:3])
+        return RVector((start + step * np.arange(n, dtype=np.int64)).astype(np.int32), INTSXP)
     if cls == "compact_realseq" and isinstance(state, RVector):
-        n, start, step = state.values[:3]
-        return RVector(start + step * np.arange(int(n), dtype=np.float64), REALSXP)
+        start, step = state.values[1:3]
+        return RVector(start + step * np.arange(n, dtype=np.float64), REALSXP)
     if cls == "deferred_string" and isinstance(state, RPairList) and state.pairs:
         src = state.pairs[0][1]
         if isinstance(src, RVector):
@@ -492,13 +516,33 @@ def _r_num_str(x: float) -> str:
 
 # ----------------------------------------------------------------------------- public API
 def _deep(fn):
+    """Run a parse on a thread with a stack sized for MAX_DEPTH item levels (up to ~4 Python
+    frames each), so the depth counter -- not the C stack -- is what bounds a crafted stream."""
     import sys
-    old = sys.getrecursionlimit()
-    sys.setrecursionlimit(max(old, 20000))
+    import threading
+    out: Dict[str, Any] = {}
+
+    def run():
+        old = sys.getrecursionlimit()
+        sys.setrecursionlimit(max(old, 4 * MAX_DEPTH + 500))
+        try:
+            out["v"] = fn()
+        except BaseException as e:   # re-raised on the caller's thread
+            out["e"] = e
+        finally:
+            sys.setrecursionlimit(old)
+
+    prev = threading.stack_size()
+    threading.stack_size(512 * 1024 * 1024)
     try:
-        return fn()
+        t = threading.Thread(target=run, name="rdata-parse")
+        t.start()
     finally:
-        sys.setrecursionlimit(old)
+        threading.stack_size(prev)
+    t.join()
+    if "e" in out:
+        raise out["e"]
+    return out["v"]
 
 
 def read_rds(path: str, strict: bool = False) -> Any:

@@ -49,13 +49,17 @@ def main(argv=None) -> int:
             tr.load(cfg.ckpt_dir)
     res = {}
     start = tr.engine.step_count
+    stats_ok = tr.engine.topo in ("sharded", "allgather")
     for s in range(start, cfg.steps):
+        ckpt_now = bool(cfg.ckpt_every and cfg.ckpt_dir and (s + 1) % cfg.ckpt_every == 0)
+        if stats_ok and ckpt_now:
+            tr.engine.record_stats = True     # the checkpoint's consensus_table.csv
         loss = tr.train_step()
         if wd is not None:
             wd.beat(s)
         if (s + 1) % 10 == 0 or s + 1 == cfg.steps:
             tr.logger.log(step=s + 1, loss=float(loss), selection=tr.engine.sel_counts.tolist())
-        if cfg.ckpt_every and cfg.ckpt_dir and (s + 1) % cfg.ckpt_every == 0:
+        if ckpt_now:
             tr.save()
     res["final_loss"] = float(loss) if cfg.steps > start else None
     res["eval"] = tr.evaluate(a.eval_batches)

@@ -169,6 +169,13 @@ def _resharded_state(path: str, meta: dict, engine) -> Dict[str, object]:
     sel = torch.zeros(n, dtype=sc.dtype)
     sel[:min(n, sc.numel())] = sc[:min(n, sc.numel())]
     es["sel_counts"] = sel
+    if lay["topology"] == "gossip" and engine.topo == "gossip" and \
+            "gossip_left" in first["engine"]:
+        # delayed gossip: the neighbour parameters that arrived before the save (saved rank
+        # r mod N's). At another world size the neighbours are other ranks, so the first mix
+        # after the load uses these as the nearest available neighbour snapshot.
+        for key in ("gossip_left", "gossip_right"):
+            es[key] = _relayout(first["engine"][key], lay, engine)
     es["world"] = engine.N
     es["topology"] = engine.topo
     mine = states.get(engine.rank % N, first)

@@ -97,8 +97,11 @@ class ConsensusTrainer:
             ckpt_now = bool(self.cfg.ckpt_every and self.cfg.ckpt_dir
                             and (s + 1) % self.cfg.ckpt_every == 0)
             log_now = bool(log_every and (s + 1) % log_every == 0)
-            if stats_ok and (ckpt_now or (log_now and self.logger.enabled)):
-                self.engine.record_stats = True      # consensus table / log stats of this step
+            # consensus table / log stats of this step. The stats all-reduce is collective, so
+            # the decision must be the same on every rank: it depends on the config only, not
+            # on logger.enabled (rank 0 alone logs)
+            if stats_ok and (ckpt_now or (log_now and bool(self.cfg.log_path))):
+                self.engine.record_stats = True
             loss = self.train_step()
             losses.append(loss)
             if log_now:

@@ -219,3 +219,38 @@ def test_param_prefetch_bit_identical(tmp_path):
     for r in range(3):
         for x, y in zip(a[r]["params"], b[r]["params"]):
             assert torch.equal(x, y)
+
+
+def _log_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from consensusml_amd.parallel import dist as D
+    from consensusml_amd.trainer.trainer import ConsensusTrainer
+    D._INFO = None
+    info = D.init_distributed("gloo", timeout_s=60)
+    cfg = _cfg("krum", "sharded", 1, 0, 4)
+    cfg.log_path = os.path.join(out_dir, "log.jsonl")
+    tr = ConsensusTrainer(cfg, info=info)
+    # every step is a log step: the stats all-reduces must run on every rank, not on the
+    # logging rank 0 alone (which would mismatch the collectives and hang)
+    tr.fit(4, log_every=1)
+    tr.close()
+    torch.save({"params": [p.detach().clone() for p in tr.model.parameters()]},
+               os.path.join(out_dir, f"log{rank}.pt"))
+    D.monitored_barrier(30)
+    dist.destroy_process_group()
+
+
+def test_fit_with_log_path_multirank(tmp_path):
+    """fit() with a log path and log_every = 1 on 2 sharded ranks completes, rank 0 writes one
+    record per step with the recorded statistics, and the replicas stay identical."""
+    import json
+    mp.spawn(_log_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    recs = [json.loads(l) for l in open(tmp_path / "log.jsonl")]
+    assert [r["step"] for r in recs] == [1, 2, 3, 4]
+    assert all("worker_grad_norm" in r and len(r["worker_grad_norm"]) == 2 for r in recs)
+    a = torch.load(tmp_path / "log0.pt", weights_only=True)["params"]
+    b = torch.load(tmp_path / "log1.pt", weights_only=True)["params"]
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)

@@ -104,7 +104,11 @@ def test_xgb_importance_parity(ref):
             np.testing.assert_allclose(imp, r, atol=1e-6)
         else:        # deep trees: near-tied gains split differently; most genes agree
             a, b = set(np.nonzero(imp)[0]), set(np.nonzero(r)[0])
-            assert len(a & b) >= len(b) // 2
+            # achieved (profiles/r02_reference_fullrun/parity.md): 4 of 7 and 7 of 13 shared
+            # nonzero genes, top-50 overlap 48 / 42
+            assert len(a & b) >= (4 if i == 1 else 7)
+            top = lambda v: set(np.argsort(-v, kind="stable")[:50])   # noqa: E731
+            assert len(top(imp) & top(r)) >= 40
 
 
 def test_rf_importance_parity(ref):
@@ -119,11 +123,13 @@ def test_rf_importance_parity(ref):
     imp2k = R.as_array(rf["rf2k.results"]["fitmodel"]["importance"]).ravel()
     np.testing.assert_allclose(imp2k, ref["st"]["rfnb_2k_MeanDecNodeImp"].to_numpy(), rtol=1e-9)
     X, y, tr = ref["X"], ref["y"], ref["tr"]
-    m = RandomForest(1000, seed=20).fit(X[tr], y[tr])
+    m = RandomForest(2000, seed=20).fit(X[tr], y[tr])     # the reference's rf2k size
     ours = m.mean_decrease_gini.numpy()
-    assert spearmanr(ours, imp2k).correlation > 0.55
+    # achieved: 0.656 vs rf2k, 0.760 vs rf10k (the reference's own rf2k vs rf10k: 0.77)
+    assert spearmanr(ours, imp2k).correlation > 0.62
+    assert spearmanr(ours, ref["st"]["rfnb_10k_MeanDecNodeImp"].to_numpy()).correlation > 0.72
     top = lambda v: set(np.argsort(-v)[:50])   # noqa: E731
-    assert len(top(ours) & top(imp2k)) >= 25
+    assert len(top(ours) & top(imp2k)) >= 36
 
 
 def test_pipeline_on_reference_container_with_resume(tmp_path, monkeypatch):
