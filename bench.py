@@ -14,8 +14,16 @@ and ``agg_overhead_vs_allreduce`` = (t_krum - t_allreduce) / t_allreduce is repo
 Data: synthetic ImageNet-shaped batches (random bf16 images, random labels) generated on
 device; random-init weights. Every timed step runs the full forward, backward, exchange,
 aggregation and optimizer update. Per-GPU batch 2048 by default: 288 GB of HBM holds it many
-times over (peak ~81 GiB), and throughput still rises with batch (larger conv / GEMM problems,
+times over (peak ~52 GiB), and throughput still rises with batch (larger conv / GEMM problems,
 fewer fixed per-step costs).
+
+Communication-visible block (``b256_*`` keys, every N): at batch 2048 the step is ~127 ms of
+compute, so at N = 8 the exposed exchange is far below 1 % and "agg overhead vs all-reduce" says
+little. The bench therefore also times per-GPU batch 256 (the batch a real 8-GPU DP run uses,
+~22 ms of compute per step) with Krum over the sharded exchange vs the mean all-reduce baseline:
+``b256_agg_overhead_vs_allreduce`` is the robust-aggregation overhead where communication is
+visible. Gradient buckets default to 8 MB (ResNet-50: 7 buckets), so the last all-to-all -- the
+one that cannot hide behind backward -- moves ~8 MB instead of 25.
 
 Robust aggregation at one GPU. With one rank there is one worker, so the dp line's Krum is
 vacuous there (n = 1, f = 0, nothing exchanged). At N = 1 the bench therefore also runs a
@@ -48,7 +56,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=2048,
                     help="per-GPU batch (samples/s on MI355X rise with batch, see README; peak "
-                         "memory ~81 GiB at 2048 of 288; the shipped MIOpen find-db covers "
+                         "memory ~52 GiB at 2048 of 288; the shipped MIOpen find-db covers "
                          "256 / 512 / 1024 / 1536 / 2048)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--rule", default="krum")
@@ -56,7 +64,11 @@ def parse():
                     help="Byzantine tolerance of the dp run (-1: the largest f with n >= 2f+3, "
                          "at least 1 once n >= 4)")
     ap.add_argument("--topology", default="sharded")
-    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--bucket-mb", type=float, default=8.0)
+    ap.add_argument("--b256-batch", type=int, default=256,
+                    help="per-GPU batch of the communication-visible Krum vs all-reduce block "
+                         "(0: off)")
+    ap.add_argument("--b256-steps", type=int, default=30)
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--no-baseline", action="store_true")
     ap.add_argument("--baseline-steps", type=int, default=-1)
@@ -182,7 +194,8 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info, *, V: int
     finite = bool(torch.isfinite(loss).item())
     res = {"dt": dt, "f": cfg.agg.f, "n": n, "loss": float(loss.item()), "finite": finite,
            "params": eng.flat.real_numel, "buckets": len(eng.flat.buckets),
-           "engine_step_ms": step_ms,
+           "engine_step_ms": step_ms, "early_grams": eng.early_grams,
+           "steps_run": eng.step_count,
            "selected": int((eng.w[: eng.n] > 0).sum().item()),
            "sel_counts": [int(c) for c in eng.sel_counts.tolist()]}
     if info.distributed:
@@ -253,6 +266,31 @@ def main():
                               "selection_counts": kr["sel_counts"]},
             f"{tag}_loss_finite": kr["finite"] and mn["finite"],
         }
+    small = {}
+    if args.b256_batch > 0 and args.b256_batch != args.batch:
+        sb = args.b256_batch
+        ks = run(args, args.rule, args.topology, args.b256_steps, args.warmup, info, batch=sb)
+        ar = run(args, "mean", "allreduce", args.b256_steps, args.warmup, info, batch=sb)
+        k_ms = ks["dt"] / args.b256_steps * 1e3
+        a_ms = ar["dt"] / args.b256_steps * 1e3
+        small = {
+            "b256_samples_per_s": round(n * sb * args.b256_steps / ks["dt"], 2),
+            "b256_ms_per_step": round(k_ms, 3),
+            "b256_allreduce_samples_per_s": round(n * sb * args.b256_steps / ar["dt"], 2),
+            "b256_allreduce_ms_per_step": round(a_ms, 3),
+            "b256_agg_overhead_vs_allreduce": round((k_ms - a_ms) / a_ms, 4),
+            "b256_engine_step_ms": round(ks["engine_step_ms"], 3),
+            "b256_allreduce_engine_step_ms": round(ar["engine_step_ms"], 3),
+            "b256_config": {"per_gpu_batch": sb, "global_batch": n * sb, "rule": args.rule,
+                            "f": ks["f"], "topology": args.topology, "buckets": ks["buckets"],
+                            "steps": args.b256_steps,
+                            "early_grams_per_step": round(ks["early_grams"] /
+                                                          max(ks["steps_run"], 1), 2)},
+            "b256_loss_finite": ks["finite"] and ar["finite"],
+        }
+        if info.distributed:
+            small["b256_replicas_identical"] = ks["replicas_identical"] and \
+                ar["replicas_identical"]
     if info.rank == 0:
         out = {
             "metric": METRIC,
@@ -287,6 +325,7 @@ def main():
             out["replicas_identical"] = main_res["replicas_identical"] and (
                 base is None or base["replicas_identical"])
         out.update(virt)
+        out.update(small)
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

@@ -18,6 +18,7 @@ import yaml
 
 RULES = ("mean", "median", "trimmed_mean", "krum", "multi_krum", "geomed", "bulyan", "centered_clip")
 TOPOLOGIES = ("allreduce", "allgather", "sharded", "gossip")
+GOSSIP_GRAPHS = ("ring", "exp", "exp_all")
 FAULTS = ("none", "sign_flip", "gaussian", "scaled", "zero", "nan", "alie", "ipm")
 
 
@@ -78,15 +79,23 @@ class TopologyConfig:
     bucket_mb: float = 64.0      # bucket size in MB of gradient (bf16 on the wire)
     comm_dtype: str = "bf16"     # dtype of exchanged gradients
     overlap: bool = True         # launch bucket collectives during backward
-    gossip_weights: tuple = (1 / 3, 1 / 3, 1 / 3)   # self, left, right
+    gossip_graph: str = "ring"   # ring | exp (one rotating peer 2^(t mod log2 N)) | exp_all
+    gossip_chunk_mb: float = 256.0   # gossip exchange pipeline chunk (MB of bf16)
+    gossip_weights: tuple = (1 / 3, 1 / 3, 1 / 3)   # ring: self, left, right
     gossip_clip: float = 0.0     # 0 disables neighbour-delta clipping
     gossip_async: bool = False   # delayed gossip: exchange overlaps the next step's compute
     early_update: bool = True    # gossip, 1 local worker: per-bucket optimizer step in backward
     param_prefetch: bool = True  # sharded: bf16 parameter all-gather overlaps the next forward
+    early_gram: bool = True      # Gram-space rules: per-bucket Gram as each exchange lands
 
     def validate(self) -> None:
         if self.kind not in TOPOLOGIES:
             raise ValueError(f"unknown topology {self.kind!r}; choose from {TOPOLOGIES}")
+        if self.gossip_graph not in GOSSIP_GRAPHS:
+            raise ValueError(f"unknown gossip graph {self.gossip_graph!r}; choose from "
+                             f"{GOSSIP_GRAPHS}")
+        if self.gossip_chunk_mb <= 0:
+            raise ValueError("gossip_chunk_mb must be positive")
 
 
 @dataclass

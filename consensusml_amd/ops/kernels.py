@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -256,6 +256,23 @@ def gossip_mix(master: torch.Tensor, left: torch.Tensor, right: torch.Tensor, w0
         lib().gossip_mix(master, param_out, left, right, w0, w1, w2, clip, work)
         return
     x = ref.gossip_mix(master, left, right, w0, w1, w2, clip)
+    master.copy_(x)
+    if param_out is not None:
+        param_out.copy_(x.to(param_out.dtype))
+
+
+def gossip_mix_k(master: torch.Tensor, nbrs: List[torch.Tensor], w: List[float], w0: float,
+                 clip: float = 0.0, param_out: Optional[torch.Tensor] = None,
+                 work: Optional[torch.Tensor] = None) -> None:
+    """In-place k-neighbour mixing (1 <= k <= 8) of the fp32 master with the neighbours' bf16
+    parameters: x <- (w0 + sum w_k) x + sum_k w_k clip_k(nb_k - x)."""
+    if master.is_cuda:
+        if work is None:
+            work = torch.empty(lib().gossip_workspace_bytes(master.numel()) // 4,
+                               dtype=torch.float32, device=master.device)
+        lib().gossip_mix_k(master, param_out, list(nbrs), [float(v) for v in w], w0, clip, work)
+        return
+    x = ref.gossip_mix_k(master, nbrs, w, w0, clip)
     master.copy_(x)
     if param_out is not None:
         param_out.copy_(x.to(param_out.dtype))

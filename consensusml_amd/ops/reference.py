@@ -268,6 +268,18 @@ def gossip_mix(x: torch.Tensor, left: torch.Tensor, right: torch.Tensor, w0: flo
     return (w0 + w1 + w2) * x + w1 * dl + w2 * dr
 
 
+def gossip_mix_k(x: torch.Tensor, nbrs, w, w0: float, clip: float = 0.0) -> torch.Tensor:
+    """x <- (w0 + sum w_k) x + sum_k w_k c_k (nb_k - x), c_k = min(1, clip / ||nb_k - x||)."""
+    x = x.float()
+    out = (w0 + sum(w)) * x
+    for nb, wk in zip(nbrs, w):
+        d = nb.float() - x
+        if clip > 0:
+            d = d * min(1.0, clip / max(d.norm().item(), 1e-30))
+        out = out + wk * d
+    return out
+
+
 def ceil_div(a: int, b: int) -> int:
     return -(-a // b)
 

@@ -15,9 +15,14 @@ Topologies:
              clipping, Bulyan's selection) all-reduce the [n, n] fp64 partial Gram (<= 32 KB)
              so every rank derives identical weights. Traffic ~= one ring all-reduce, spread over
              all 7 xGMI links by the all-to-all.
-  gossip     topology C: local fused step, then ring exchange of bf16 parameters with rank +-1
-             (grouped send/recv, chunked so exchange of chunk k+1 overlaps mixing of chunk k) and
-             a fused, optionally clipped, mixing kernel.
+  gossip     topology C: local fused step, then an exchange of bf16 parameters with this step's
+             neighbours (grouped send/recv, chunked so exchange of chunk k+1 overlaps mixing of
+             chunk k) and a fused, optionally clipped, k-neighbour mixing kernel. Graphs
+             (topology.gossip_graph): ring (r +- 1, 2 of the 7 xGMI links); exp (one-peer
+             exponential graph: at step t send to r + 2^(t mod tau), receive from r - 2^(t mod
+             tau), x <- (x + nb) / 2; exact averaging after tau = ceil(log2 N) steps when N is a
+             power of two, half the ring's bytes per step, ONE receive buffer); exp_all (every
+             r +- 2^i at once: 5 distinct peers at N = 8, uniform weights 1 / (k + 1)).
 
 Workers = ranks x virtual_workers (micro-batches whose gradients are kept separately), so the
 robust rules can be exercised at n = 8 on a single GPU.
@@ -90,9 +95,9 @@ class ConsensusEngine:
         elif self.topo == "allgather":
             for b in fl.buckets:
                 self.recv.append(torch.zeros(self.rows_total, b.length, dtype=fl.dtype, device=dev))
-        elif self.topo == "gossip":
-            self.nb_left = torch.empty_like(fl.flat_param)
-            self.nb_right = torch.empty_like(fl.flat_param)
+        self.nb_bufs: List[torch.Tensor] = []
+        if self.topo == "gossip" and self.N > 1:
+            self._setup_gossip()
         self._gossip_reqs = None
         self._send_buf = None
         self._gossip_restored = False   # neighbour buffers restored from a checkpoint
@@ -148,6 +153,18 @@ class ConsensusEngine:
         self._prefetch_hooks = []
         if self.param_prefetch:
             self._setup_prefetch()
+        # Per-bucket Gram partials (Gram-space rules, sharded / allgather across ranks): slot b
+        # holds bucket b's local X X^T. A slot is filled as soon as that bucket's exchange has
+        # landed -- polled from the gradient hooks while backward still runs -- and step() sums
+        # the slots in bucket order, so the result does not depend on when each was computed.
+        self.early_gram = bool(cfg.topology.early_gram and self.rule in GRAM_RULES
+                               and self.group_active
+                               and self.topo in ("sharded", "allgather"))
+        self.Gb = (torch.zeros(len(fl.buckets), self.rows_total, self.rows_total,
+                               dtype=torch.float64, device=dev) if self.early_gram else None)
+        self._gram_done: set = set()
+        self.early_grams = 0       # bucket Grams computed before step() (all steps)
+        self._gram_eager = False   # tests: wait for each exchange in its hook (forces the path)
         # training-side consensus table (SURVEY.md §5.4 b): when set, the next step() records
         # per-worker / per-parameter gradient statistics (consensus_table())
         self.record_stats = False
@@ -167,6 +184,7 @@ class ConsensusEngine:
             v.clear()
         self._flushed.clear()
         self._pending.clear()
+        self._gram_done.clear()
         self.flat.grad_row = 0
 
     def bind_worker(self, v: int) -> None:
@@ -300,6 +318,8 @@ class ConsensusEngine:
         self._flushed.add(b.index)
         if self.overlap and b.index not in self._pending:
             self._launch_bucket(b, inject=True)
+            if self.early_gram:
+                self._poll_grams()
         if self.early_update and complete:
             self._early_update(b)
 
@@ -363,6 +383,25 @@ class ConsensusEngine:
         if w is not None:
             w.wait()
 
+    def _bucket_gram(self, b: Bucket) -> None:
+        """Slot b of the per-bucket Gram partials, once its exchange has landed."""
+        if b.index in self._gram_done:
+            return
+        self._wait(b)
+        X = self._cclip_rows(b) if self.rule == "centered_clip" else self._rows(b)
+        length = b.shard if self.topo == "sharded" else X.shape[1]
+        K.gram(X, n=self.rows_total, D=length, out=self.Gb[b.index])
+        self._gram_done.add(b.index)
+
+    def _poll_grams(self) -> None:
+        """Gram partials of every bucket whose exchange has completed (non-blocking test), so
+        they run during backward instead of after the last all-to-all."""
+        for bi, w in list(self._pending.items()):
+            if bi not in self._gram_done and w is not None and (self._gram_eager
+                                                                or w.is_completed()):
+                self._bucket_gram(self.flat.buckets[bi])
+                self.early_grams += 1
+
     # ================================================================ optimizer args
     def _opt_args(self, gscale: float = 1.0) -> K.OptArgs:
         o = self.cfg.optim
@@ -408,11 +447,21 @@ class ConsensusEngine:
         return R
 
     def _compute_weights(self, cols) -> None:
-        """Gram over every bucket (accumulated), all-reduced across shards, then weights."""
+        """Gram over every bucket (accumulated in bucket order), all-reduced across shards,
+        then weights."""
         cfg = self.cfg.agg
-        self.G.zero_()
-        for b, X, length in cols:
-            K.gram(X, n=self.rows_total, D=length, out=self.G, accumulate=True)
+        if self.early_gram:
+            # per-bucket partials (most computed during backward), summed in bucket order:
+            # G = ((g0 + g1) + g2) ..., the same fp64 adds as accumulating bucket by bucket
+            for b, _, _ in cols:
+                self._bucket_gram(b)
+            self.G.copy_(self.Gb[0])
+            for k in range(1, len(cols)):
+                self.G.add_(self.Gb[k])
+        else:
+            self.G.zero_()
+            for b, X, length in cols:
+                K.gram(X, n=self.rows_total, D=length, out=self.G, accumulate=True)
         if self.group_active and self.topo == "sharded":
             dist.all_reduce(self.G)
         rule = "bulyan_select" if self.rule == "bulyan" else self.rule
@@ -515,6 +564,58 @@ class ConsensusEngine:
         for w in works:
             w.wait()
 
+    def _setup_gossip(self) -> None:
+        """Neighbour receive buffers. ring: left + right (full vectors); exp: ONE full vector
+        (the step's single peer); exp_all: per-peer chunk buffers when synchronous (mixing runs
+        chunk by chunk), full vectors in delayed mode (the exchange lands during the next step)."""
+        fl, tc = self.flat, self.cfg.topology
+        self.gossip_graph = tc.gossip_graph
+        self._tau = max(1, (self.N - 1).bit_length())          # ceil(log2 N)
+        self._chunk = max(int(tc.gossip_chunk_mb * 1024 * 1024 // 2), 64)
+        if self.gossip_graph == "ring":
+            nbuf, full = 2, True
+        elif self.gossip_graph == "exp":
+            nbuf, full = 1, True
+        else:
+            nbuf = len(self._gossip_peers(0)[0])
+            full = tc.gossip_async or tc.gossip_clip > 0
+        size = fl.flat_param.numel() if full else min(self._chunk, fl.flat_param.numel())
+        self.nb_bufs = [torch.empty(size, dtype=fl.flat_param.dtype, device=self.device)
+                        for _ in range(nbuf)]
+        self._nb_full = full
+
+    def _gossip_peers(self, t: int):
+        """(send-to, recv-from, mixing weights, self weight) of gossip step t; recv_from[k] is
+        the rank whose parameters land in nb_bufs[k]."""
+        N, r = self.N, self.rank
+        if self.gossip_graph == "ring":
+            w0, w1, w2 = self.cfg.topology.gossip_weights
+            left, right = (r - 1) % N, (r + 1) % N
+            return [left, right], [left, right], [w1, w2], w0
+        if self.gossip_graph == "exp":
+            s = 1 << (t % self._tau)
+            return [(r + s) % N], [(r - s) % N], [0.5], 0.5
+        peers = []
+        for i in range(self._tau):
+            for q in ((r + (1 << i)) % N, (r - (1 << i)) % N):
+                if q != r and q not in peers:
+                    peers.append(q)
+        w = 1.0 / (len(peers) + 1)
+        return peers, peers, [w] * len(peers), w
+
+    def _gossip_exchange(self, t: int, s: int, e: int, src: torch.Tensor, bufs, off: int):
+        """Grouped send/recv of src[s:e] for step t; neighbour k's slice lands in
+        bufs[k][s - off:e - off]."""
+        send, recv, _, _ = self._gossip_peers(t)
+        ops = [dist.P2POp(dist.isend, src[s:e], q) for q in send]
+        ops += [dist.P2POp(dist.irecv, bufs[k][s - off:e - off], q) for k, q in enumerate(recv)]
+        return dist.batch_isend_irecv(ops)
+
+    def _gossip_mix(self, t: int, s: int, e: int, off: int = 0) -> None:
+        _, _, w, w0 = self._gossip_peers(t)
+        K.gossip_mix_k(self.master[s:e], [b[s - off:e - off] for b in self.nb_bufs], w, w0,
+                       self.cfg.topology.gossip_clip, param_out=self.flat.flat_param[s:e])
+
     def _step_gossip(self) -> None:
         fl = self.flat
         if not self.early_update:
@@ -524,55 +625,57 @@ class ConsensusEngine:
                          s2=s2, param_out=fl.flat_param)
         if not self.group_active or self.N == 1:
             return
-        w0, w1, w2 = self.cfg.topology.gossip_weights
+        t = self.step_count
         clip = self.cfg.topology.gossip_clip
-        left = (self.rank - 1) % self.N
-        right = (self.rank + 1) % self.N
-        chunk = max(int(256 * 1024 * 1024 // 2), 64)   # 256 MB of bf16 per exchange chunk
+        chunk = self._chunk
         total = fl.total
         starts = list(range(0, total, chunk))
 
-        def exchange(s, src=None):
-            src = fl.flat_param if src is None else src
-            e = min(s + chunk, total)
-            ops = [dist.P2POp(dist.isend, src[s:e], left),
-                   dist.P2POp(dist.isend, src[s:e], right),
-                   dist.P2POp(dist.irecv, self.nb_left[s:e], left),
-                   dist.P2POp(dist.irecv, self.nb_right[s:e], right)]
-            return dist.batch_isend_irecv(ops)
+        def wait_all(reqs):
+            for rq in reqs:
+                for w in rq:
+                    w.wait()
 
         if self.cfg.topology.gossip_async:
             # Delayed gossip: mix with the neighbour parameters that arrived during THIS step's
-            # compute (sent at the end of the previous step), then snapshot the new local
-            # parameters and start the next exchange, which overlaps the next forward/backward.
+            # compute (sent at the end of the previous step, graph of step t - 1), then snapshot
+            # the new local parameters and start the next exchange, which overlaps the next
+            # forward/backward.
             if self._gossip_reqs is not None or self._gossip_restored:
                 self._drain_gossip()
                 self._gossip_restored = False
-                K.gossip_mix(self.master, self.nb_left, self.nb_right, w0, w1, w2, clip,
-                             param_out=fl.flat_param)
+                self._gossip_mix(t - 1, 0, total)
             if self._send_buf is None:
                 self._send_buf = torch.empty_like(fl.flat_param)
             self._send_buf.copy_(fl.flat_param)
-            self._gossip_reqs = [exchange(s, self._send_buf) for s in starts]
+            self._gossip_reqs = [self._gossip_exchange(t, s, min(s + chunk, total),
+                                                       self._send_buf, self.nb_bufs, 0)
+                                 for s in starts]
             return
 
         if clip > 0 and len(starts) > 1:
             # clipping needs whole-vector neighbour distances: exchange everything first
-            reqs = [exchange(s) for s in starts]
-            for rq in reqs:
-                for w in rq:
-                    w.wait()
-            K.gossip_mix(self.master, self.nb_left, self.nb_right, w0, w1, w2, clip,
-                         param_out=fl.flat_param)
+            wait_all([self._gossip_exchange(t, s, min(s + chunk, total), fl.flat_param,
+                                            self.nb_bufs, 0) for s in starts])
+            self._gossip_mix(t, 0, total)
             return
-        reqs = exchange(starts[0])
+        if not self._nb_full:
+            # per-peer chunk buffers: exchange chunk k, mix it, reuse the buffers for k + 1
+            for s in starts:
+                e = min(s + chunk, total)
+                wait_all([self._gossip_exchange(t, s, e, fl.flat_param, self.nb_bufs, s)])
+                self._gossip_mix(t, s, e, off=s)
+            return
+        reqs = self._gossip_exchange(t, starts[0], min(starts[0] + chunk, total), fl.flat_param,
+                                     self.nb_bufs, 0)
         for k, s in enumerate(starts):
-            nxt = exchange(starts[k + 1]) if k + 1 < len(starts) else None
+            e = min(s + chunk, total)
+            nxt = (self._gossip_exchange(t, starts[k + 1], min(starts[k + 1] + chunk, total),
+                                         fl.flat_param, self.nb_bufs, 0)
+                   if k + 1 < len(starts) else None)
             for w in reqs:
                 w.wait()
-            e = min(s + chunk, total)
-            K.gossip_mix(self.master[s:e], self.nb_left[s:e], self.nb_right[s:e], w0, w1, w2,
-                         clip, param_out=fl.flat_param[s:e])
+            self._gossip_mix(t, s, e)
             reqs = nxt
 
     # ================================================================ consensus table
@@ -686,8 +789,7 @@ class ConsensusEngine:
             # state (the next step mixes with it); finish it and save what arrived
             self._drain_gossip()
             self._gossip_restored = True
-            sd["gossip_left"] = self.nb_left
-            sd["gossip_right"] = self.nb_right
+            sd["gossip_nb"] = list(self.nb_bufs)
         if self.s1 is not None:
             sd["s1"] = self.s1
         if self.s2 is not None:
@@ -708,10 +810,13 @@ class ConsensusEngine:
         self.sel_counts.copy_(sd["sel_counts"])
         if "v0" in sd and self.gout is not None:
             self.gout.copy_(sd["v0"])
-        if "gossip_left" in sd and self.topo == "gossip":
+        nb = sd.get("gossip_nb")
+        if nb is None and "gossip_left" in sd:          # round-2 checkpoints (ring)
+            nb = [sd["gossip_left"], sd["gossip_right"]]
+        if nb is not None and self.topo == "gossip" and len(nb) == len(self.nb_bufs):
             self._drain_gossip()
-            self.nb_left.copy_(sd["gossip_left"])
-            self.nb_right.copy_(sd["gossip_right"])
+            for dst, src in zip(self.nb_bufs, nb):
+                dst.copy_(src)
             self._gossip_restored = True
         self.sync_params_from_master()
 

@@ -169,13 +169,15 @@ def _resharded_state(path: str, meta: dict, engine) -> Dict[str, object]:
     sel = torch.zeros(n, dtype=sc.dtype)
     sel[:min(n, sc.numel())] = sc[:min(n, sc.numel())]
     es["sel_counts"] = sel
-    if lay["topology"] == "gossip" and engine.topo == "gossip" and \
-            "gossip_left" in first["engine"]:
+    se = first["engine"]
+    nb = se.get("gossip_nb") or ([se["gossip_left"], se["gossip_right"]]
+                                  if "gossip_left" in se else None)
+    if lay["topology"] == "gossip" and engine.topo == "gossip" and nb is not None:
         # delayed gossip: the neighbour parameters that arrived before the save (saved rank
         # r mod N's). At another world size the neighbours are other ranks, so the first mix
-        # after the load uses these as the nearest available neighbour snapshot.
-        for key in ("gossip_left", "gossip_right"):
-            es[key] = _relayout(first["engine"][key], lay, engine)
+        # after the load uses these as the nearest available neighbour snapshot (the engine
+        # takes them when the graph keeps the same number of receive buffers).
+        es["gossip_nb"] = [_relayout(v, lay, engine) for v in nb]
     es["world"] = engine.N
     es["topology"] = engine.topo
     mine = states.get(engine.rank % N, first)

@@ -157,6 +157,30 @@ void gossip_mix(Tensor& master, const optional<Tensor>& param_out, const Tensor&
                                        work.data_ptr(), cur_stream()));
 }
 
+void gossip_mix_k(Tensor& master, const optional<Tensor>& param_out, std::vector<Tensor> nbrs,
+                  std::vector<double> w, double w0, double clip, Tensor& work) {
+  check_dev(master, "master");
+  TORCH_CHECK(master.scalar_type() == at::kFloat && master.is_contiguous(), "master: fp32 contiguous");
+  const int64_t D = master.numel();
+  const int k = static_cast<int>(nbrs.size());
+  TORCH_CHECK(k >= 1 && k <= 8 && w.size() == nbrs.size(), "1..8 neighbours, one weight each");
+  std::vector<const void*> ptr(k);
+  std::vector<float> wf(k);
+  for (int i = 0; i < k; ++i) {
+    TORCH_CHECK(nbrs[i].scalar_type() == nbrs[0].scalar_type() && nbrs[i].is_contiguous() &&
+                    nbrs[i].numel() >= D && nbrs[i].device() == master.device(),
+                "neighbours: contiguous, same dtype and device, master's size");
+    ptr[i] = nbrs[i].data_ptr();
+    wf[i] = static_cast<float>(w[i]);
+  }
+  TORCH_CHECK(work.numel() * work.element_size() >= gossip_workspace_bytes(D), "gossip workspace too small");
+  void* p = opt_ptr<void>(param_out, nbrs[0].scalar_type(), "param_out", D);
+  const c10::DeviceGuard guard(master.device());
+  CML_CHECK_HIP(cml::launch_gossip_mix_k(dtype_of(nbrs[0]), master.data_ptr<float>(), p, ptr.data(),
+                                         wf.data(), k, D, static_cast<float>(w0),
+                                         static_cast<float>(clip), work.data_ptr(), cur_stream()));
+}
+
 // x / res / y: NHWC-contiguous bf16 (4-D channels_last or 2-D [M, C]).
 void check_nhwc(const Tensor& t, const char* name) {
   check_dev(t, name);
@@ -1714,6 +1738,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("robust_weights", &robust_weights, "robust weights from a Gram matrix");
   m.def("gossip_workspace_bytes", &gossip_workspace_bytes);
   m.def("gossip_mix", &gossip_mix, "ring gossip mixing with neighbour clipping");
+  m.def("gossip_mix_k", &gossip_mix_k, "k-neighbour gossip mixing with neighbour clipping");
   m.def("fault", &fault, "Byzantine fault injection");
   m.def("bn_fwd", &bn_fwd, "fused NHWC BatchNorm(+res)(+ReLU) forward");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BatchNorm(+res)(+ReLU) backward");

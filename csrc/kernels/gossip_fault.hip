@@ -1,10 +1,11 @@
 // Decentralized gossip mixing (N09) and Byzantine fault injection (N10).
 //
-// Gossip: after the local step each rank holds its own fp32 master x and has received its ring
-// neighbours' bf16 parameters (RCCL send/recv, both directions at once). The mix
-//   x <- (w0 + w1 + w2) x + w1 * c_l (left - x) + w2 * c_r (right - x)
-// with c = min(1, clip / ||neighbour - x||) (robust gossip: a Byzantine neighbour moves us by at
-// most `clip`) is one streaming pass; the two distances need one reduction pass first. Partial
+// Gossip: after the local step each rank holds its own fp32 master x and has received the bf16
+// parameters of its k neighbours in this step's communication graph (ring: r - 1 and r + 1;
+// exponential graphs: r +- 2^i, RCCL send/recv, all directions at once). The mix
+//   x <- (w0 + sum_k w_k) x + sum_k w_k c_k (nb_k - x)
+// with c_k = min(1, clip / ||nb_k - x||) (robust gossip: a Byzantine neighbour moves us by at
+// most `clip`) is one streaming pass; the k distances need one reduction pass first. Partial
 // sums go to a per-workgroup slab and the mix kernel's workgroups each fold the slab (<= 2048
 // values, L2-resident) in a fixed order, so the result is deterministic and needs no extra
 // launch or host sync.
@@ -16,6 +17,7 @@ namespace {
 
 constexpr int kBlk = 256;
 constexpr int kMaxBlk = 1024;
+constexpr int kMaxNbrs = 8;     // neighbours of one gossip mix (the 7 xGMI peers of an 8-GPU node)
 
 template <typename T>
 __device__ __forceinline__ float ld1(const T* p, int64_t e) {
@@ -23,88 +25,109 @@ __device__ __forceinline__ float ld1(const T* p, int64_t e) {
   else return p[e];
 }
 
+// Neighbour pointers and mixing weights of one gossip step (by value: one kernel argument).
 template <typename T>
-__global__ __launch_bounds__(kBlk) void pair_sqdist_kernel(const float* __restrict__ x,
-                                                          const T* __restrict__ l,
-                                                          const T* __restrict__ r, int64_t D,
-                                                          float* __restrict__ part) {
-  float sl = 0.f, sr = 0.f;
+struct Nbrs {
+  const T* p[kMaxNbrs];
+  float w[kMaxNbrs];
+};
+
+// per-workgroup partial ||nb_k - x||^2 for every neighbour k: part[k * nblk + block]
+template <typename T, int K>
+__global__ __launch_bounds__(kBlk) void nbr_sqdist_kernel(const float* __restrict__ x, Nbrs<T> nb,
+                                                         int64_t D, float* __restrict__ part) {
+  float s[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) s[k] = 0.f;
   const int64_t nv = D / 8;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlk;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlk + threadIdx.x; t < nv; t += stride) {
-    float xv[8], lv[8], rv[8];
+    float xv[8];
     load_vec<float, 8>(x + t * 8, xv);
-    load_vec<T, 8>(l + t * 8, lv);
-    load_vec<T, 8>(r + t * 8, rv);
 #pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      const float a = lv[v] - xv[v], b = rv[v] - xv[v];
-      sl = fmaf(a, a, sl);
-      sr = fmaf(b, b, sr);
+    for (int k = 0; k < K; ++k) {
+      float v[8];
+      load_vec<T, 8>(nb.p[k] + t * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[e] - xv[e];
+        s[k] = fmaf(d, d, s[k]);
+      }
     }
   }
   if (blockIdx.x == 0) {
     for (int64_t e = nv * 8 + threadIdx.x; e < D; e += kBlk) {
-      const float a = ld1(l, e) - x[e];
-      const float b = ld1(r, e) - x[e];
-      sl = fmaf(a, a, sl);
-      sr = fmaf(b, b, sr);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float d = ld1(nb.p[k], e) - x[e];
+        s[k] = fmaf(d, d, s[k]);
+      }
     }
   }
-  __shared__ float red[2][kBlk / kWave];
-  sl = wave_sum(sl);
-  sr = wave_sum(sr);
+  __shared__ float red[K][kBlk / kWave];
   const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    red[0][wv] = sl;
-    red[1][wv] = sr;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const float v = wave_sum(s[k]);
+    if ((threadIdx.x & 63) == 0) red[k][wv] = v;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float a = 0.f, b = 0.f;
-    for (int k = 0; k < kBlk / kWave; ++k) {
-      a += red[0][k];
-      b += red[1][k];
-    }
-    part[2 * blockIdx.x] = a;
-    part[2 * blockIdx.x + 1] = b;
+  if (threadIdx.x < K) {
+    float a = 0.f;
+    for (int w = 0; w < kBlk / kWave; ++w) a += red[threadIdx.x][w];
+    part[static_cast<int64_t>(threadIdx.x) * gridDim.x + blockIdx.x] = a;
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(kBlk) void gossip_mix_kernel(float* __restrict__ x,
-                                                         T* __restrict__ p,
-                                                         const T* __restrict__ l,
-                                                         const T* __restrict__ r, int64_t D,
-                                                         float w0, float w1, float w2, float clip,
-                                                         const float* __restrict__ part, int nblk) {
-  __shared__ float scl[2];
+// x <- (w0 + sum_k w_k) x + sum_k w_k c_k (nb_k - x), c_k = min(1, clip / ||nb_k - x||); the
+// sum is formed from the last neighbour down (for K = 2: fmaf(c0, l - x, c1 (r - x)), the ring
+// kernel's expression). Each workgroup folds the distance slab itself (fixed order).
+template <typename T, int K>
+__global__ __launch_bounds__(kBlk) void gossip_mix_kernel(float* __restrict__ x, T* __restrict__ p,
+                                                         Nbrs<T> nb, int64_t D, float w0,
+                                                         float clip, const float* __restrict__ part,
+                                                         int nblk) {
+  __shared__ float scl[K];
   if (threadIdx.x < 64) {
-    double a = 0.0, b = 0.0;
-    if (clip > 0.f) {
-      for (int k = threadIdx.x; k < nblk; k += 64) {
-        a += part[2 * k];
-        b += part[2 * k + 1];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      double a = 0.0;
+      if (clip > 0.f) {
+        for (int b = threadIdx.x; b < nblk; b += 64) a += part[static_cast<int64_t>(k) * nblk + b];
+        a = wave_sum(a);
       }
-      a = wave_sum(a);
-      b = wave_sum(b);
-    }
-    if (threadIdx.x == 0) {
-      scl[0] = clip > 0.f ? fminf(1.f, clip / fmaxf(sqrtf(static_cast<float>(a)), 1e-30f)) : 1.f;
-      scl[1] = clip > 0.f ? fminf(1.f, clip / fmaxf(sqrtf(static_cast<float>(b)), 1e-30f)) : 1.f;
+      if (threadIdx.x == 0)
+        scl[k] = clip > 0.f ? fminf(1.f, clip / fmaxf(sqrtf(static_cast<float>(a)), 1e-30f)) : 1.f;
     }
   }
   __syncthreads();
-  const float cl = w1 * scl[0], cr = w2 * scl[1], cs = w0 + w1 + w2;
+  float c[K];
+  float cs = w0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    c[k] = nb.w[k] * scl[k];
+    cs += nb.w[k];
+  }
   const int64_t nv = D / 8;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlk;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlk + threadIdx.x; t < nv; t += stride) {
-    float xv[8], lv[8], rv[8];
+    float xv[8], acc[8];
     load_vec<float, 8>(x + t * 8, xv);
-    load_vec<T, 8>(l + t * 8, lv);
-    load_vec<T, 8>(r + t * 8, rv);
+    {
+      float v[8];
+      load_vec<T, 8>(nb.p[K - 1] + t * 8, v);
 #pragma unroll
-    for (int v = 0; v < 8; ++v) xv[v] = fmaf(cs, xv[v], fmaf(cl, lv[v] - xv[v], cr * (rv[v] - xv[v])));
+      for (int e = 0; e < 8; ++e) acc[e] = c[K - 1] * (v[e] - xv[e]);
+    }
+#pragma unroll
+    for (int k = K - 2; k >= 0; --k) {
+      float v[8];
+      load_vec<T, 8>(nb.p[k] + t * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf(c[k], v[e] - xv[e], acc[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xv[e] = fmaf(cs, xv[e], acc[e]);
     store_f32<8>(x + t * 8, xv);
     if (p) {
       if constexpr (sizeof(T) == 2) store_bf16<8>(p + t * 8, xv);
@@ -114,7 +137,10 @@ __global__ __launch_bounds__(kBlk) void gossip_mix_kernel(float* __restrict__ x,
   if (blockIdx.x == 0) {
     for (int64_t e = nv * 8 + threadIdx.x; e < D; e += kBlk) {
       const float xe = x[e];
-      const float v = fmaf(cs, xe, fmaf(cl, ld1(l, e) - xe, cr * (ld1(r, e) - xe)));
+      float acc = c[K - 1] * (ld1(nb.p[K - 1], e) - xe);
+#pragma unroll
+      for (int k = K - 2; k >= 0; --k) acc = fmaf(c[k], ld1(nb.p[k], e) - xe, acc);
+      const float v = fmaf(cs, xe, acc);
       x[e] = v;
       if (p) {
         if constexpr (sizeof(T) == 2) reinterpret_cast<uint16_t*>(p)[e] = f2bf(v);
@@ -168,30 +194,59 @@ int nblocks(int64_t work, int cap) {
 
 }  // namespace
 
-size_t gossip_workspace_bytes(int64_t) { return 2 * kMaxBlk * sizeof(float); }
+size_t gossip_workspace_bytes(int64_t) { return kMaxNbrs * kMaxBlk * sizeof(float); }
+
+namespace {
+template <typename T, int K>
+void gossip_k(float* master, void* param_out, const Nbrs<T>& nb, int64_t D, float w0, float clip,
+              void* work, hipStream_t stream) {
+  float* part = reinterpret_cast<float*>(work);
+  const int nb_blocks = nblocks(D / 8, kMaxBlk);
+  if (clip > 0.f) nbr_sqdist_kernel<T, K><<<nb_blocks, kBlk, 0, stream>>>(master, nb, D, part);
+  gossip_mix_kernel<T, K><<<nblocks(D / 8, 2048), kBlk, 0, stream>>>(
+      master, reinterpret_cast<T*>(param_out), nb, D, w0, clip, part, nb_blocks);
+}
 
 template <typename T>
-void gossip_t(float* master, void* param_out, const void* left, const void* right, int64_t D,
-              float w0, float w1, float w2, float clip, void* work, hipStream_t stream) {
-  float* part = reinterpret_cast<float*>(work);
-  const int nb = nblocks(D / 8, kMaxBlk);
-  if (clip > 0.f)
-    pair_sqdist_kernel<T><<<nb, kBlk, 0, stream>>>(master, reinterpret_cast<const T*>(left),
-                                                   reinterpret_cast<const T*>(right), D, part);
-  gossip_mix_kernel<T><<<nblocks(D / 8, 2048), kBlk, 0, stream>>>(
-      master, reinterpret_cast<T*>(param_out), reinterpret_cast<const T*>(left),
-      reinterpret_cast<const T*>(right), D, w0, w1, w2, clip, part, nb);
+hipError_t gossip_t(float* master, void* param_out, const void* const* nbrs, const float* w,
+                    int k, int64_t D, float w0, float clip, void* work, hipStream_t stream) {
+  Nbrs<T> nb{};
+  for (int i = 0; i < k; ++i) {
+    nb.p[i] = reinterpret_cast<const T*>(nbrs[i]);
+    nb.w[i] = w[i];
+  }
+  switch (k) {
+    case 1: gossip_k<T, 1>(master, param_out, nb, D, w0, clip, work, stream); break;
+    case 2: gossip_k<T, 2>(master, param_out, nb, D, w0, clip, work, stream); break;
+    case 3: gossip_k<T, 3>(master, param_out, nb, D, w0, clip, work, stream); break;
+    case 4: gossip_k<T, 4>(master, param_out, nb, D, w0, clip, work, stream); break;
+    case 5: gossip_k<T, 5>(master, param_out, nb, D, w0, clip, work, stream); break;
+    case 6: gossip_k<T, 6>(master, param_out, nb, D, w0, clip, work, stream); break;
+    case 7: gossip_k<T, 7>(master, param_out, nb, D, w0, clip, work, stream); break;
+    case 8: gossip_k<T, 8>(master, param_out, nb, D, w0, clip, work, stream); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_gossip_mix_k(int dtype, float* master, void* param_out, const void* const* nbrs,
+                               const float* w, int k, int64_t D, float w0, float clip, void* work,
+                               hipStream_t stream) {
+  if (k < 1 || k > kMaxNbrs) return hipErrorInvalidValue;
+  uintptr_t a = reinterpret_cast<uintptr_t>(master) | reinterpret_cast<uintptr_t>(param_out);
+  for (int i = 0; i < k; ++i) a |= reinterpret_cast<uintptr_t>(nbrs[i]);
+  if (a % 16) return hipErrorInvalidValue;
+  return dtype == DT_BF16 ? gossip_t<bf16>(master, param_out, nbrs, w, k, D, w0, clip, work, stream)
+                          : gossip_t<float>(master, param_out, nbrs, w, k, D, w0, clip, work, stream);
 }
 
 hipError_t launch_gossip_mix(int dtype, float* master, void* param_out, const void* left,
                              const void* right, int64_t D, float w0, float w1, float w2,
                              float clip, void* work, hipStream_t stream) {
-  if ((reinterpret_cast<uintptr_t>(master) | reinterpret_cast<uintptr_t>(left) |
-       reinterpret_cast<uintptr_t>(right) | reinterpret_cast<uintptr_t>(param_out)) % 16)
-    return hipErrorInvalidValue;
-  if (dtype == DT_BF16) gossip_t<bf16>(master, param_out, left, right, D, w0, w1, w2, clip, work, stream);
-  else gossip_t<float>(master, param_out, left, right, D, w0, w1, w2, clip, work, stream);
-  return hipGetLastError();
+  const void* nb[2] = {left, right};
+  const float w[2] = {w1, w2};
+  return launch_gossip_mix_k(dtype, master, param_out, nb, w, 2, D, w0, clip, work, stream);
 }
 
 hipError_t launch_fault(int dtype, void* g, int64_t D, int kind, float scale, float sigma,

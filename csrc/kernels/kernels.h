@@ -66,6 +66,10 @@ hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m,
 // Gossip: x <- (w0+w1+w2) x + w1*clip(left-x) + w2*clip(right-x); writes fp32 master and bf16
 // params. clip <= 0 disables clipping. ``work`` must hold gossip_workspace_bytes(D) bytes.
 size_t gossip_workspace_bytes(int64_t D);
+// k-neighbour mix (1 <= k <= 8): x <- (w0 + sum w_k) x + sum_k w_k clip_k(nbrs[k] - x)
+hipError_t launch_gossip_mix_k(int dtype, float* master, void* param_out, const void* const* nbrs,
+                               const float* w, int k, int64_t D, float w0, float clip, void* work,
+                               hipStream_t stream);
 hipError_t launch_gossip_mix(int dtype, float* master, void* param_out, const void* left,
                              const void* right, int64_t D, float w0, float w1, float w2,
                              float clip, void* work, hipStream_t stream);

@@ -16,7 +16,7 @@ KEYS = {"metric": str, "value": float, "unit": str, "n_gpus": int, "steps": int,
         "ms_per_step": float, "higher_is_better": bool, "scaling": str, "dtype": str,
         "data": str, "config": dict}
 SMALL = ["--batch", "16", "--image-size", "64", "--steps", "2", "--warmup", "1",
-         "--no-miopen-find"]
+         "--no-miopen-find", "--b256-batch", "8", "--b256-steps", "2"]
 
 
 def _port():
@@ -40,6 +40,11 @@ def _check(r: dict, n: int):
     for k in ("model", "global_batch", "seq_len", "parallelism"):
         assert k in r["config"]
     assert r["config"]["global_batch"] == 16 * n
+    # the communication-visible small-batch block (here batch 8 per rank)
+    for k in ("b256_samples_per_s", "b256_ms_per_step", "b256_allreduce_ms_per_step",
+              "b256_agg_overhead_vs_allreduce", "b256_engine_step_ms"):
+        assert isinstance(r[k], float), (k, r.get(k))
+    assert r["b256_config"]["global_batch"] == 8 * n and r["b256_loss_finite"] is True
 
 
 def test_bench_single_rank_contract(cuda):
@@ -65,3 +70,4 @@ def test_bench_two_ranks_gloo_contract(cuda):
     _check(r, 2)
     assert r["dist_backend"] == "gloo" and r["world_size_seen"] == 2
     assert r["replicas_identical"] is True and r["engine_step_ms"] >= 0
+    assert r["b256_replicas_identical"] is True

@@ -42,7 +42,8 @@ def _cfg(rule, topo, V, f, steps, fault="none", byz=()):
     return cfg
 
 
-def _worker(rank, world, port, rule, topo, f, steps, out_dir, fault, byz, ckpt, prefetch=True):
+def _worker(rank, world, port, rule, topo, f, steps, out_dir, fault, byz, ckpt, prefetch=True,
+            early_gram=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch.distributed as dist
@@ -52,9 +53,12 @@ def _worker(rank, world, port, rule, topo, f, steps, out_dir, fault, byz, ckpt, 
     info = D.init_distributed("gloo")
     cfg = _cfg(rule, topo, 1, f, steps, fault, byz)
     cfg.topology.param_prefetch = prefetch
+    cfg.topology.early_gram = early_gram
     if ckpt:
         cfg.ckpt_dir = os.path.join(out_dir, "ckpt")
     tr = ConsensusTrainer(cfg, info=info)
+    # early_gram: compute every bucket's Gram in its hook (the timing-dependent path, forced)
+    tr.engine._gram_eager = early_gram
     if ckpt:
         tr.fit(steps // 2, log_every=0)
         tr.save()
@@ -65,17 +69,18 @@ def _worker(rank, world, port, rule, topo, f, steps, out_dir, fault, byz, ckpt, 
     else:
         tr.fit(steps, log_every=0)
     params = [p.detach().clone() for p in tr.model.parameters()]
-    torch.save({"params": params, "sel": tr.engine.sel_counts.clone()},
+    torch.save({"params": params, "sel": tr.engine.sel_counts.clone(),
+                "early_grams": tr.engine.early_grams},
                os.path.join(out_dir, f"r{rank}.pt"))
     D.monitored_barrier(30)
     dist.destroy_process_group()
 
 
 def _run_world(world, rule, topo, f, steps, tmp, fault="none", byz=(), ckpt=False,
-               prefetch=True):
+               prefetch=True, early_gram=True):
     port = _free_port()
     mp.spawn(_worker, args=(world, port, rule, topo, f, steps, str(tmp), fault, list(byz), ckpt,
-                            prefetch), nprocs=world, join=True)
+                            prefetch, early_gram), nprocs=world, join=True)
     return [torch.load(os.path.join(tmp, f"r{r}.pt"), weights_only=True) for r in range(world)]
 
 
@@ -254,3 +259,18 @@ def test_fit_with_log_path_multirank(tmp_path):
     b = torch.load(tmp_path / "log1.pt", weights_only=True)["params"]
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("topo,rule,f", [("sharded", "krum", 0), ("allgather", "multi_krum", 1),
+                                         ("sharded", "centered_clip", 0)])
+def test_early_gram_bit_identical(tmp_path, topo, rule, f):
+    """Per-bucket Gram partials computed as each exchange lands (during backward) and summed in
+    bucket order give bit-identical parameters to the Gram computed after the last exchange."""
+    (tmp_path / "on").mkdir()
+    (tmp_path / "off").mkdir()
+    a = _run_world(3, rule, topo, f, 5, tmp_path / "on", early_gram=True)
+    b = _run_world(3, rule, topo, f, 5, tmp_path / "off", early_gram=False)
+    assert a[0]["early_grams"] > 0 and b[0]["early_grams"] == 0
+    for r in range(3):
+        for x, y in zip(a[r]["params"], b[r]["params"]):
+            assert torch.equal(x, y)
