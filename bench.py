@@ -215,8 +215,8 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info, *, V: int
 
 def main():
     args = parse()
-    from consensusml_amd.models import resnet as _resnet
-    _resnet.CONV1X1_GEMM = args.conv1x1
+    from consensusml_amd import perf
+    perf.set_policy(perf.policy().replace(conv1x1_gemm=args.conv1x1))
     if not args.no_miopen_find:
         from consensusml_amd.utils.tuning import configure_miopen
         configure_miopen()
@@ -318,6 +318,8 @@ def main():
             "loss_finite": main_res["finite"],
             "peak_mem_gib": (round(torch.cuda.max_memory_allocated() / 2**30, 1)
                              if torch.cuda.is_available() else None),
+            # every kernel / fusion switch in force (consensusml_amd.perf.PerfPolicy)
+            "perf_policy": perf.policy().to_dict(),
         }
         if info.distributed:
             out["dist_backend"] = main_res["dist_backend"]

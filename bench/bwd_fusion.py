@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Identity-block backward fusion A/B per ResNet-50 stage (models.resnet.FUSED_BN3_BWD).
+"""Identity-block backward fusion A/B per ResNet-50 stage (PerfPolicy.fused_bn3_bwd).
 
 For each stage shape (planes 64/128/256/512 at 56/28/14/7 px, batch 2048) a chain of three
 identity Bottlenecks runs forward + backward with the fused tail on and off; ms per chain
@@ -25,13 +25,12 @@ def main():
     ap.add_argument("--blocks", type=int, default=3)
     ap.add_argument("--stages", default="64:56,128:28,256:14,512:7")
     a = ap.parse_args()
-    from consensusml_amd.models import resnet
     from consensusml_amd.models.resnet import Bottleneck
     from consensusml_amd.ops.bn import ResidualLink
     from consensusml_amd.utils.tuning import configure_miopen
     configure_miopen()
     dev = torch.device("cuda:0")
-    resnet.FUSED_BN3_BWD_MAX_PLANES = 4096     # the A/B covers every stage
+    from consensusml_amd import perf
     for item in a.stages.split(","):
         planes, H = (int(v) for v in item.split(":"))
         torch.manual_seed(0)
@@ -42,7 +41,9 @@ def main():
         gy = torch.randn_like(x)
         res = {}
         for flag in (False, True, False, True):
-            resnet.FUSED_BN3_BWD = flag
+            # the A/B covers every stage
+            perf.set_policy(perf.policy().replace(fused_bn3_bwd=flag,
+                                                  fused_bn3_bwd_max_planes=4096))
             ts = []
             for it in range(8):
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

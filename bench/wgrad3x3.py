@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """3x3 stride-1 weight gradients of ResNet-50 at batch 2048: MIOpen (aten convolution_backward,
-channels_last bf16) vs csrc/kernels/wgrad3x3.hip (nine taps per workgroup) vs the one-tap-per-grid-z
+channels_last bf16) vs csrc/kernels/wgrad3x3.hip (nine taps per workgroup) (the one-tap-per-grid-z variant was removed in round 3)
 TAP mode of wgrad1x1.hip. One JSON line per shape (ms, PFLOP/s, relative error vs fp32 on a slice).
 
   python bench/wgrad3x3.py [--json-out FILE]
@@ -52,17 +52,16 @@ def main():
         flops = 2 * B * H * H * 9 * C * C
         t_lib = _t(lambda: torch.ops.aten.convolution_backward(
             gy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
-        t_dir = _t(lambda: L.wgrad3x3(gy, x, torch.bfloat16, None, None, zero, False))
-        t_tap = _t(lambda: L.wgrad3x3(gy, x, torch.bfloat16, None, None, zero, True))
+        t_dir = _t(lambda: L.wgrad3x3(gy, x, torch.bfloat16, zero))
         xs, gs = x[:16].contiguous(memory_format=torch.channels_last), \
             gy[:16].contiguous(memory_format=torch.channels_last)
         ref = torch.ops.aten.convolution_backward(gs.float(), xs.float(), w.float(), None, [1, 1],
                                                   [1, 1], [1, 1], False, [0, 0], 1,
                                                   [False, True, False])[1]
-        d = L.wgrad3x3(gs, xs, torch.float32, None, None, zero, False)
+        d = L.wgrad3x3(gs, xs, torch.float32, zero)
         err = float((d.float() - ref).norm() / ref.norm())
         r = {"C": C, "H": H, "batch": B, "miopen_ms": round(t_lib, 4), "direct_ms": round(t_dir, 4),
-             "tap_ms": round(t_tap, 4), "miopen_pflops": round(flops / t_lib / 1e12, 3),
+             "miopen_pflops": round(flops / t_lib / 1e12, 3),
              "direct_pflops": round(flops / t_dir / 1e12, 3),
              "direct_ok": bool(L.wgrad3x3_direct_ok(B, H, H, C, C)), "direct_rel_err": err}
         print(json.dumps(r), flush=True)

@@ -8,7 +8,6 @@ BASELINE.json config: "ResNet-50 bf16 DP=8 with Krum".
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional
 
 import torch
@@ -20,58 +19,18 @@ from ..ops.bn import BatchNormAct2d, ResidualLink, bn_add_bn_relu, fused_ok, lin
 from ..ops.pool import bn_relu_max_pool2d, max_pool2d
 from ..ops.stem import stem_conv_bn_relu_pool, stem_ok
 
-# 1x1 stride-1 convolutions: which passes run as plain GEMMs (hipBLASLt) instead of MIOpen.
-#   "auto"   per-shape choice measured on MI355X at batch 512 (bench/conv_shapes.py,
-#            profiles/r01_conv_shapes9.jsonl): hipBLASLt wins the data gradient dX = dY W whenever
-#            the conv reduces channels (Cout < Cin: every bottleneck conv1, 1.3-1.4x) or the
-#            spatial size is small (H*W <= 196: layer3/4 conv3, 1.7x), and the forward for
-#            Cin >= 1024 (1.4x); MIOpen keeps everything else and every weight gradient (its
-#            wrw kernels are 2-12x faster than a GEMM with K = N*H*W).
-#   "gemm"   forward and data gradient always GEMMs;  "miopen"  never.
-# True / False (older callers) mean "gemm" / "miopen".
-CONV1X1_GEMM = os.environ.get("CML_CONV1X1_GEMM", "auto")
-# identity blocks fuse the residual-gradient add into conv1's dX GEMM (see ops.bn.ResidualLink)
-RESIDUAL_LINK = True
-# downsample-block tail relu(bn3(z) + down_bn(zd)) as one fused op (ops.bn.bn_add_bn_relu)
-FUSE_DOWN_BN = os.environ.get("CML_FUSE_DOWN_BN", "1") == "1"
-# weight gradient of the deeper stride-1 1x1 convs on csrc/kernels/wgrad1x1.hip
-OWN_WGRAD1X1 = os.environ.get("CML_WGRAD1X1", "1") == "1"
-# whole stem (conv + BN statistics, BN + ReLU + pool; backward in one weight-gradient pass) on
-# the HIP kernels of csrc/kernels/stem_conv.hip (ops.stem)
-FUSE_STEM_CONV = os.environ.get("CML_FUSE_STEM_CONV", "1") == "1"
-# stem BN + ReLU + max-pool in one pass (ops.pool.bn_relu_max_pool2d)
-FUSE_STEM_POOL = os.environ.get("CML_FUSE_STEM_POOL", "1") == "1"
-# the stem's pool backward sums layer1.0's downsample data gradient on load
-POOL_LINK = os.environ.get("CML_POOL_LINK", "1") == "1"
-# global average pool whose backward writes the NHWC gradient directly
-NHWC_AVGPOOL = os.environ.get("CML_NHWC_AVGPOOL", "1") == "1"
-# stem input channels zero-padded 3 -> 4 on the GPU (see ResNet.stem)
-STEM_PAD4 = os.environ.get("CML_STEM_PAD4", "1") == "1"
-# 1x1 convs fused with their BatchNorms (ops.conv, csrc/kernels/conv1x1.hip): BN statistics in the
-# conv epilogue; conv3 applies bn2 + ReLU in its prologue (y2 never stored). Per shape, see
-# fused_conv1x1_policy.
-FUSED_CONV1X1 = os.environ.get("CML_FUSED_CONV1X1", "1") == "1"
-# identity-block tails whose bn3 backward runs inside conv3's gradient kernels and the next
-# conv1's data-gradient epilogue (ops.conv.bnrelu_conv1x1_bn_res)
-FUSED_BN3_BWD = os.environ.get("CML_FUSED_BN3_BWD", "1") == "1"
-FUSED_BN3_BWD_MAX_PLANES = int(os.environ.get("CML_FUSED_BN3_BWD_MAX_PLANES", "128"))
-# fused identity tails without a stored z3 (ops.conv._RecomputeTailFn), up to this many planes
-RECOMPUTE_TAIL = os.environ.get("CML_RECOMPUTE_TAIL", "1") == "1"
-RECOMPUTE_TAIL_MAX_PLANES = int(os.environ.get("CML_RECOMPUTE_TAIL_MAX_PLANES", "256"))
-# ... and the stride-1 downsample tail (layer 1) without z3 / zd (ops.conv._RecomputeDownTailFn)
-RECOMPUTE_DOWN_TAIL = os.environ.get("CML_RECOMPUTE_DOWN_TAIL", "1") == "1"
+# Every kernel / fusion choice of this model is a field of the typed PerfPolicy
+# (consensusml_amd.perf), read when the model runs: ``perf.use_policy(...)`` switches paths inside
+# one process, and benchmark lines / checkpoints record the policy in force.
+from ..perf import policy as _P
 
 
 def recompute_tail_policy(planes: int) -> bool:
     """Measured at batch 2048 (profiles/r02_recompute_tail35/): up to 128 planes 152.1 -> 145.2
     ms / step; adding layer 3 (256) another -1.1 ms; layer 4 (512) +0.4-0.6 ms back."""
-    return (RECOMPUTE_TAIL and planes <= RECOMPUTE_TAIL_MAX_PLANES
+    p = _P()
+    return (p.recompute_tail and planes <= p.recompute_tail_max_planes
             and fconv.recompute_tail_ok(planes))
-# stride-1 3x3 convs: data gradient on csrc/kernels/conv_gemm.hip (ops.conv.conv3x3)
-OWN_DGRAD3X3 = os.environ.get("CML_DGRAD3X3", "1") == "1"
-# ... and their forward on conv_gemm too, with bn2's statistics in the epilogue
-# (ops.conv.conv3x3_bn_stats) instead of a separate statistics pass over z2
-CONV3X3_BN_STATS = os.environ.get("CML_CONV3X3_BN_STATS", "1") == "1"
 
 
 def fused_bn3_bwd_policy(planes: int) -> bool:
@@ -81,7 +40,8 @@ def fused_bn3_bwd_policy(planes: int) -> bool:
     replaces are faster than the fused kernels (-0.31 / -0.73 ms per block; -0.12 / -0.51 with
     the MT = 2 tiles, profiles/r02_19_mt2/r02_19_bwdfusion.jsonl)."""
     from ..ops import conv as _c
-    return FUSED_BN3_BWD and planes <= FUSED_BN3_BWD_MAX_PLANES and _c.res_tail_ok(planes)
+    p = _P()
+    return p.fused_bn3_bwd and planes <= p.fused_bn3_bwd_max_planes and _c.res_tail_ok(planes)
 
 
 def fused_conv1x1_policy(cin: int, cout: int, hw_out: int, stride: int, prologue: bool) -> bool:
@@ -91,7 +51,7 @@ def fused_conv1x1_policy(cin: int, cout: int, hw_out: int, stride: int, prologue
     ms saved per call) and whenever it also removes bn2's apply pass (every conv3); on the
     14 x 14 / 7 x 7 shapes with 1024+ input channels the library GEMMs (0.7-1 PFLOP/s) beat it
     by more than the statistics pass it saves (0.03-0.14 ms)."""
-    if not FUSED_CONV1X1:
+    if not _P().fused_conv1x1:
         return False
     if prologue:
         return True
@@ -100,7 +60,7 @@ def fused_conv1x1_policy(cin: int, cout: int, hw_out: int, stride: int, prologue
 
 def conv1x1_policy(cin: int, cout: int, hw: int):
     """(forward as GEMM, data gradient as GEMM) for a 1x1 stride-1 conv."""
-    mode = CONV1X1_GEMM
+    mode = _P().conv1x1_gemm
     if mode is True or mode == "gemm":
         return True, True
     if mode is False or mode == "miopen":
@@ -176,11 +136,11 @@ class _Conv1x1Fn(torch.autograd.Function):
 # same box). The 64-channel layer-1 shapes are at the HBM floor on MIOpen.
 _CORE = {(128, 512), (512, 128), (256, 1024), (512, 2048), (2048, 512)}
 _ALL = _CORE | {(256, 128), (512, 256), (1024, 256), (1024, 512)}
-OWN_WGRAD_SHAPES = _ALL if os.environ.get("CML_WGRAD1X1_SET", "core") == "all" else _CORE
 
 
 def own_wgrad_ok(cin: int, cout: int) -> bool:
-    return OWN_WGRAD1X1 and (cin, cout) in OWN_WGRAD_SHAPES
+    p = _P()
+    return p.own_wgrad1x1 and (cin, cout) in (_ALL if p.wgrad1x1_set == "all" else _CORE)
 
 
 class Conv1x1(nn.Conv2d):
@@ -212,27 +172,7 @@ class Conv1x1(nn.Conv2d):
         if fwd_gemm or dgrad_gemm or own:
             return _Conv1x1Fn.apply(x, self.weight, res_link if dgrad_gemm else None, fwd_gemm,
                                     dgrad_gemm, own)
-        if self.stride == (2, 2) and torch.is_grad_enabled() and fconv.wgrad1x1_s2_ok(x, self.weight):
-            return _Conv1x1S2Fn.apply(x, self.weight)
         return super().forward(x)
-
-
-class _Conv1x1S2Fn(torch.autograd.Function):
-    """Stride-2 1x1 (downsample) conv: forward and data gradient on MIOpen, weight gradient on
-    ``wgrad1x1.hip`` (x gathered at the even pixels, ``ops.conv._wgrad``)."""
-
-    @staticmethod
-    def forward(ctx, x, w):
-        ctx.save_for_backward(x, w)
-        return F.conv2d(x, w, stride=2)
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, w = ctx.saved_tensors
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        dx = fconv._dgrad(dy, x, w, 2, False, None) if ctx.needs_input_grad[0] else None
-        dw = fconv._wgrad(dy, x, w, 2, False) if ctx.needs_input_grad[1] else None
-        return dx, dw
 
 
 class _GlobalAvgPoolFn(torch.autograd.Function):
@@ -256,7 +196,7 @@ class _GlobalAvgPoolFn(torch.autograd.Function):
 
 
 def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
-    if NHWC_AVGPOOL and x.is_cuda and x.dim() == 4 \
+    if _P().nhwc_avgpool and x.is_cuda and x.dim() == 4 \
             and x.is_contiguous(memory_format=torch.channels_last):
         return _GlobalAvgPoolFn.apply(x)
     return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
@@ -280,12 +220,12 @@ class Bottleneck(nn.Module):
             self.down_conv = None
 
     def _conv2(self, x: torch.Tensor) -> torch.Tensor:
-        if OWN_DGRAD3X3 and self.training:
+        if _P().own_dgrad3x3 and self.training:
             return fconv.conv3x3(x, self.conv2)
         return self.conv2(x)
 
     def _fused_ok(self, x: torch.Tensor) -> bool:
-        return (FUSED_CONV1X1 and self.training and torch.is_grad_enabled()
+        return (_P().fused_conv1x1 and self.training and torch.is_grad_enabled()
                 and fconv.fused_conv_ok(x, self.conv1.weight)
                 and fused_ok(x, self.bn3.weight))
 
@@ -317,16 +257,16 @@ class Bottleneck(nn.Module):
         planes = self.conv3.in_channels
         hw2 = (z1.shape[2] // self.conv2.stride[0]) * (z1.shape[3] // self.conv2.stride[0])
         fuse3 = fused_conv1x1_policy(planes, planes * 4, hw2, 1, True)
-        own3 = fuse3 and CONV3X3_BN_STATS and OWN_DGRAD3X3 and fconv.conv3x3_ok(z1, self.conv2)
-        if own3 and fconv.BN1_DGRAD_SUMS and st1 is not None and self.bn1.training:
+        pol = _P()
+        own3 = (fuse3 and pol.conv3x3_bn_stats and pol.own_dgrad3x3
+                and fconv.conv3x3_ok(z1, self.conv2))
+        if own3 and pol.bn1_dgrad_sums and st1 is not None and self.bn1.training:
             # bn1's backward sums come from the 3x3 data gradient's epilogue
             z2, st2 = fconv.bnrelu_conv3x3_bn_stats(z1, self.bn1, st1, self.conv2, self.bn2)
         else:
             out = self.bn1(z1, stats=st1)
             if own3:
                 z2, st2 = fconv.conv3x3_bn_stats(out, self.conv2, self.bn2)
-            elif fuse3 and fconv.conv3x3_s2_ok(out, self.conv2):
-                z2, st2 = fconv.conv3x3_s2_bn_stats(out, self.conv2, self.bn2)
             else:
                 z2 = self._conv2(out)
                 st2 = fconv.bn_stats(z2, self.bn2) if fuse3 else None
@@ -340,7 +280,7 @@ class Bottleneck(nn.Module):
                 if out_link is not None:
                     y._cml_link = out_link
                 return y
-            if (self.down_conv is not None and RECOMPUTE_DOWN_TAIL and self.bn3.eps ==
+            if (self.down_conv is not None and pol.recompute_down_tail and self.bn3.eps ==
                     self.down_bn.eps and fconv.down_tail_recompute_s2_ok(x, planes, self.down_conv)):
                 # stride-2 downsample tail: the stride-1 recompute kernels on x[:, :, ::2, ::2];
                 # its gradient (zero-filled full resolution) parks on conv1's link as before
@@ -351,7 +291,7 @@ class Bottleneck(nn.Module):
                 if out_link is not None:
                     y._cml_link = out_link
                 return y
-            if (self.down_conv is not None and RECOMPUTE_DOWN_TAIL and self.bn3.eps ==
+            if (self.down_conv is not None and pol.recompute_down_tail and self.bn3.eps ==
                     self.down_bn.eps and fconv.down_tail_recompute_ok(x, planes, self.down_conv)):
                 out_link = ResidualLink() if use_links else None
                 tlink = dlink if dlink is not None else \
@@ -389,7 +329,7 @@ class Bottleneck(nn.Module):
         return y
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        use_links = RESIDUAL_LINK and torch.is_grad_enabled() and self.training
+        use_links = _P().residual_link and torch.is_grad_enabled() and self.training
         if self._fused_ok(x):
             return self._forward_fused(x, use_links)
         if self.down_conv is None:
@@ -420,7 +360,7 @@ class Bottleneck(nn.Module):
             zd = self.down_conv(link_tap(x, tlink) if tlink is not None else x)
             out_link = ResidualLink() if use_links and fused_ok(z, self.bn3.weight) else None
             # relu(bn3(z) + down_bn(zd)) in one op: the shortcut BN output is never stored
-            y = bn_add_bn_relu(z, self.bn3, zd, self.down_bn, out_link) if FUSE_DOWN_BN \
+            y = bn_add_bn_relu(z, self.bn3, zd, self.down_bn, out_link) if _P().fuse_down_bn \
                 else self.bn3(z, residual=self.down_bn(zd), out_link=out_link)
         if out_link is not None:
             y._cml_link = out_link      # our consumer (an identity block) parks dres here
@@ -450,7 +390,7 @@ class ResNet(nn.Module):
         and the weight likewise (a view-sized pad), so MIOpen runs its vectorised NHWC kernels:
         1.4x faster forward and weight gradient (bench/stem_pad.py). Same math, same parameter."""
         w = self.conv1.weight
-        if (STEM_PAD4 and x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] == 3
+        if (_P().stem_pad4 and x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] == 3
                 and x.is_contiguous(memory_format=torch.channels_last) and not x.requires_grad):
             from ..ops.native import lib
             x4 = lib().pad_c4(x)
@@ -466,13 +406,14 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if FUSE_STEM_CONV and stem_ok(x, self.conv1, self.bn1):
-            plink = ResidualLink() if (POOL_LINK and RESIDUAL_LINK and self.training
+        pol = _P()
+        if pol.fuse_stem_conv and stem_ok(x, self.conv1, self.bn1):
+            plink = ResidualLink() if (pol.pool_link and pol.residual_link and self.training
                                        and torch.is_grad_enabled()) else None
             x = stem_conv_bn_relu_pool(x, self.conv1, self.bn1, plink)
             if plink is not None:
                 x._cml_pool_link = plink    # layer1.0's downsample conv parks its dX here
-        elif FUSE_STEM_POOL:
+        elif pol.fuse_stem_pool:
             x = bn_relu_max_pool2d(self.stem(x), self.bn1, 3, 2, 1)
         else:
             x = max_pool2d(self.bn1(self.stem(x)), 3, 2, 1)

@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..perf import policy as _P
 from .native import lib
 
 
@@ -192,6 +193,8 @@ def fused_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
 
 def _fused_ok(x: torch.Tensor, gamma: torch.Tensor) -> bool:
     if not (x.is_cuda and x.dtype == torch.bfloat16 and gamma.dtype == torch.bfloat16):
+        return False
+    if not _P().fused_bn:     # PerfPolicy.library(): PyTorch's BatchNorm composition
         return False
     C = x.shape[1]
     if C % 8 or C > 2048 or 256 % (C // 8):

@@ -23,12 +23,12 @@ Gradients: data gradient as a hipBLASLt GEMM (stride 1, per-shape policy of
 """
 from __future__ import annotations
 
-import os
 from typing import Optional, Tuple
 
 import torch
 import torch.nn.functional as F
 
+from ..perf import policy as _P
 from .bn import MaskedGrad
 from .native import lib
 
@@ -53,7 +53,7 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm
         if isinstance(g, MaskedGrad):
             return masked_link_dgrad(dy, w, g, link)
         if isinstance(g, S2Grad):
-            if (S2_LINK_DGRAD and dy.dtype == torch.bfloat16 and C % 64 == 0 and Co % 64 == 0
+            if (_P().s2_link_dgrad and dy.dtype == torch.bfloat16 and C % 64 == 0 and Co % 64 == 0
                     and g.H == H and g.W == W):
                 wt = w.reshape(Co, C).t().contiguous()
                 return lib().conv1x1_link_s2(dy.contiguous(memory_format=torch.channels_last), wt,
@@ -89,28 +89,12 @@ def masked_link_dgrad(dy: torch.Tensor, w: torch.Tensor, mg: MaskedGrad, link) -
     return lib().conv1x1_link(dy, wt, mg.g, mg.mask)[0]
 
 
-# stride-2 1x1 (downsample) weight gradients on wgrad1x1.hip (x gathered at the even pixels).
-# Off by default: 0.78-0.80 ms vs MIOpen's 0.63-0.74 at the three ResNet-50 shapes, step within
-# noise (profiles/r02_stride2_43.jsonl, profiles/r02_stride2_42.txt)
-OWN_WGRAD1X1_S2 = os.environ.get("CML_WGRAD1X1_S2", "0") == "1"
-
-
-def wgrad1x1_s2_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    Co, Ci = w.shape[0], w.shape[1]
-    return (OWN_WGRAD1X1_S2 and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
-            and x.is_contiguous(memory_format=torch.channels_last)
-            and ((Co == 64 and Ci == 64) or (Ci == 64 and Co % 256 == 0)
-                 or (Co % 128 == 0 and Ci % 128 == 0)))
-
-
 def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, own: bool,
            pro: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
     """dW of a 1x1 conv. ``pro`` = (sc, bi): the conv's real input is max(x * sc + bi, 0)."""
     if own and stride == 1:
         sc, bi = pro if pro is not None else (None, None)
         return lib().wgrad1x1(dy, x, w.dtype, sc, bi).view_as(w)
-    if stride == 2 and pro is None and wgrad1x1_s2_ok(x, w):
-        return lib().wgrad1x1_s2(dy, x, w.dtype)
     if pro is not None:   # library weight gradient needs the materialised input
         sc, bi = pro
         x = torch.relu(x.float() * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)).to(x.dtype)
@@ -227,14 +211,12 @@ class _BNReLUConv1x1BNResFn(torch.autograd.Function):
 def _affine(gamma: torch.Tensor, beta: torch.Tensor, mean: torch.Tensor, invstd: torch.Tensor):
     """(sc, bi) = (gamma invstd, beta - mean sc) in fp32: one ``bn_affine`` launch (bit-identical to
     ``gamma.float() * invstd`` and ``beta.float() - mean * sc``, which take five)."""
-    if not BN_AFFINE_KERNEL:
+    if not _P().bn_affine_kernel:
         sc = gamma.float() * invstd
         return sc, beta.float() - mean * sc
     ab = lib().bn_affine(gamma, beta, mean, invstd)
     return ab[0], ab[1]
 
-
-BN_AFFINE_KERNEL = os.environ.get("CML_BN_AFFINE_KERNEL", "1") == "1"   # 0: PyTorch ops (A/B)
 
 
 _CONST = {}
@@ -248,25 +230,21 @@ def _const(n: int, v: float, device) -> torch.Tensor:
     return t
 
 
-# recompute tails: the tail BN's statistics from the Gram matrix of the conv input (computed once,
-# reused by the backward) instead of a statistics-only pass of the conv (CML_GRAM_STATS=0)
-GRAM_STATS = os.environ.get("CML_GRAM_STATS", "1") == "1"
-
-# recompute tails: bn2's backward sums from the epilogue of the GEMM that produces its output
-# gradient dy2 (``conv1x1_cat_bnsums``, ReLU mask recomputed from z2), so only bn2's apply pass
-# remains (CML_CAT_BNSUMS=0: the separate reduction pass). Only up to CML_CAT_BNSUMS_MAXC
-# channels (default 64, layer 1): the sums variant runs MT = 1 tiles (its MT = 2 tile spills), and
-# on the 128 / 256-channel GEMMs that costs about what the reduction pass did
-# (profiles/r02_prof53_*: 722 vs 658 us per layer-2/3 call, 1160 vs 1095 us per layer-1 call).
-CAT_BNSUMS = os.environ.get("CML_CAT_BNSUMS", "1") == "1"
-CAT_BNSUMS_MAXC = int(os.environ.get("CML_CAT_BNSUMS_MAXC", "64"))
+# PerfPolicy.gram_stats -- recompute tails: the tail BN's statistics from the Gram matrix of the
+# conv input (computed once, reused by the backward) instead of a statistics-only pass of the conv.
+# PerfPolicy.cat_bnsums -- recompute tails: bn2's backward sums from the epilogue of the GEMM that
+# produces its output gradient dy2 (``conv1x1_cat_bnsums``, ReLU mask recomputed from z2), so only
+# bn2's apply pass remains; up to cat_bnsums_maxc channels (round 2: the register-staged sums
+# variant ran MT = 1 tiles, which on the 128 / 256-channel GEMMs cost about what the reduction pass
+# did: profiles/r02_prof53_*).
 
 
 def _cat_dgrad_bn2(L, gy, mask, z, a1, c1, sc, bi, w_cat, g2, b2, mean2, invstd2):
     """dy2 = [a1 (mask ? gy : 0) + c1 | relu(z sc + bi)] w_cat^T, then bn2's (BN + ReLU on z)
     backward: (dz, dgamma2, dbeta2)."""
     a_cat, c_cat = torch.cat([a1, sc]), torch.cat([c1, bi])
-    if CAT_BNSUMS and z.shape[1] <= CAT_BNSUMS_MAXC:
+    pol = _P()
+    if pol.cat_bnsums and z.shape[1] <= pol.cat_bnsums_maxc:
         dy2, s2, q2 = L.conv1x1_cat_bnsums(gy, mask, z, a_cat, c_cat, w_cat, mean2, invstd2)
         M = z.numel() // z.shape[1]
         _, _, _, dg2, db2 = L.bn_bwd_coeffs(s2, q2, g2, mean2, invstd2, M)
@@ -287,7 +265,7 @@ class _RecomputeTailFn(torch.autograd.Function):
     w / M - mean^2 per output channel (``wgrad1x1_ex`` mode 3 + ``bn_stats_gram``; p x p instead
     of the 4p-channel conv, and the Gram is the one the backward needs anyway), then the GEMM with
     bn3 + residual + ReLU applied in its epilogue (``conv1x1_bnres``, y and its bit mask).
-    CML_GRAM_STATS=0: a statistics-only pass of the conv instead (bn3 statistics of the bf16
+    PerfPolicy.gram_stats off: a statistics-only pass of the conv instead (bn3 statistics of the bf16
     products).
 
     Backward, with u = m * g (g the block-output gradient, m bn3's ReLU mask) and
@@ -309,7 +287,7 @@ class _RecomputeTailFn(torch.autograd.Function):
         wc = w.contiguous()
         L = lib()
         gram = cy = None
-        if GRAM_STATS:
+        if _P().gram_stats:
             # bn3's statistics from y2's Gram matrix (also the backward's), not a conv pass
             gram, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
             m3, i3 = L.bn_stats_gram(gram, cy, wc, z.numel() // z.shape[1], rmean3, rvar3, eps,
@@ -388,7 +366,7 @@ class _RecomputeDownTailFn(torch.autograd.Function):
         L = lib()
         w3c, wdc = w3.contiguous(), wd.contiguous()
         grams = (None, None, None, None)
-        if GRAM_STATS:
+        if _P().gram_stats:
             M_ = z.numel() // z.shape[1]
             gram3, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
             gramd, cx = L.wgrad1x1_ex(x, x, None, None, 0, None, None, None, None, True)
@@ -536,19 +514,17 @@ def subsample2_link(x: torch.Tensor, link) -> torch.Tensor:
 def down_tail_recompute_s2_ok(x: torch.Tensor, planes: int, down_conv) -> bool:
     """Stride-2 downsample tails (ResNet-50 layer 2) on the recompute kernels: the convolution
     reads x[:, :, ::2, ::2], materialised once (``subsample2``), so the stride-1 kernels apply."""
-    return (RECOMPUTE_DOWN_TAIL_S2 and down_conv.stride[0] == 2 and down_conv.stride[1] == 2
+    pol = _P()
+    return (pol.recompute_down_tail_s2 and down_conv.stride[0] == 2 and down_conv.stride[1] == 2
             and planes in (64, 128, 256, 512) and x.shape[1] % 64 == 0
-            and x.shape[1] <= DOWN_TAIL_S2_MAX_CIN)
+            and x.shape[1] <= pol.down_tail_s2_max_cin)
 
 
-# stride-2 downsample tails: the compact data gradient is added at the even pixels by conv1's
-# data-gradient kernel (CML_S2_LINK_DGRAD=0: scattered to full resolution, then hipBLASLt addmm_)
-S2_LINK_DGRAD = os.environ.get("CML_S2_LINK_DGRAD", "1") == "1"
-# CML_RECOMPUTE_DOWN_TAIL_S2=0: stride-2 downsample tails keep stored z3 / zd (bn_add_bn_relu)
-RECOMPUTE_DOWN_TAIL_S2 = os.environ.get("CML_RECOMPUTE_DOWN_TAIL_S2", "1") == "1"
-# widest block input of a recompute stride-2 downsample tail (256: layer 2; 512: also layer 3,
-# step 128.9 / 129.2 -> 128.0 / 128.5 ms and -1.1 GiB peak, profiles/r02_down_tail_l3_58/)
-DOWN_TAIL_S2_MAX_CIN = int(os.environ.get("CML_DOWN_TAIL_S2_MAX_CIN", "512"))
+# PerfPolicy.s2_link_dgrad -- stride-2 downsample tails: the compact data gradient is added at the
+# even pixels by conv1's data-gradient kernel (off: scattered to full resolution, then addmm_).
+# PerfPolicy.recompute_down_tail_s2 / down_tail_s2_max_cin -- widest block input of a recompute
+# stride-2 downsample tail (256: layer 2; 512: also layer 3, step 128.9 / 129.2 -> 128.0 / 128.5 ms
+# and -1.1 GiB peak, profiles/r02_down_tail_l3_58/).
 
 
 def down_tail_recompute_ok(x: torch.Tensor, planes: int, down_conv) -> bool:
@@ -611,16 +587,15 @@ def _zero_row(device: torch.device) -> torch.Tensor:
     return z
 
 
-# 3x3 weight gradients on csrc/kernels/wgrad3x3.hip (nine taps per workgroup): 1.4-2.0x faster
-# than MIOpen's at the ResNet-50 shapes (profiles/r02_wgrad3x3_39.jsonl)
-OWN_WGRAD3X3 = os.environ.get("CML_WGRAD3X3", "1") == "1"
+# PerfPolicy.own_wgrad3x3 -- 3x3 weight gradients on csrc/kernels/wgrad3x3.hip (nine taps per
+# workgroup): 1.4-2.0x faster than MIOpen's at the ResNet-50 shapes (profiles/r02_wgrad3x3_39.jsonl)
 
 
 def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     N, Ci, H, W = x.shape
     Co = dy.shape[1]
-    if OWN_WGRAD3X3 and lib().wgrad3x3_direct_ok(N, H, W, Co, Ci):
-        return lib().wgrad3x3(dy, x, w.dtype, None, None, _zero_row(dy.device), False)
+    if _P().own_wgrad3x3 and lib().wgrad3x3_direct_ok(N, H, W, Co, Ci):
+        return lib().wgrad3x3(dy, x, w.dtype, _zero_row(dy.device))
     return torch.ops.aten.convolution_backward(
         dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
 
@@ -713,9 +688,8 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
         return dz1, dg1, db1, None, None, None, dw, None, None, None, None
 
 
-# bn1 + ReLU -> 3x3 conv with bn1's backward sums in the data-gradient epilogue
-# (CML_BN1_DGRAD_SUMS=0: bn_act + conv3x3_bn_stats, bn1's backward with its own reduction pass)
-BN1_DGRAD_SUMS = os.environ.get("CML_BN1_DGRAD_SUMS", "1") == "1"
+# PerfPolicy.bn1_dgrad_sums -- bn1 + ReLU -> 3x3 conv with bn1's backward sums in the data-gradient
+# epilogue (off: bn_act + conv3x3_bn_stats, bn1's backward with its own reduction pass)
 
 
 def bnrelu_conv3x3_bn_stats(z1: torch.Tensor, bn_a, stats_a, conv, bn):
@@ -724,53 +698,6 @@ def bnrelu_conv3x3_bn_stats(z1: torch.Tensor, bn_a, stats_a, conv, bn):
     z, m, i = _BNReLUConv3x3BNStatsFn.apply(z1, bn_a.weight, bn_a.bias, stats_a[0], stats_a[1],
                                             bn_a.eps, conv.weight, bn.running_mean, bn.running_var,
                                             bn.eps, bn.momentum)
-    return z, (m, i)
-
-
-class _Conv3x3S2BNStatsFn(torch.autograd.Function):
-    """(z, mean, invstd) of a stride-2 3x3 conv (ResNet-50 v1.5 downsampling blocks) on
-    ``conv_gemm.hip`` with the next BN's statistics in its epilogue; backward on MIOpen."""
-
-    @staticmethod
-    def forward(ctx, x, w, rmean, rvar, eps, momentum):
-        Co, Ci = w.shape[0], w.shape[1]
-        wf = w.permute(0, 2, 3, 1).reshape(Co, 9 * Ci).contiguous()
-        y, mean, invstd = lib().conv_gemm_bn(x, wf, 9, _zero_row(x.device), rmean, rmean, rvar,
-                                             eps, momentum, 2)
-        ctx.save_for_backward(x, w)
-        ctx.mark_non_differentiable(mean, invstd)
-        ctx.set_materialize_grads(False)   # no zero-filled grads for the statistics outputs
-        return y, mean, invstd
-
-    @staticmethod
-    def backward(ctx, dy, _dm, _di):
-        x, w = ctx.saved_tensors
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        dx, dw, _ = torch.ops.aten.convolution_backward(
-            dy, x, w, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
-            [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
-        return dx, dw, None, None, None, None
-
-
-# stride-2 3x3 forward on conv_gemm with the BN statistics epilogue instead of MIOpen + a
-# statistics pass. Off by default: 0.85 / 0.59 / 0.57 ms vs 0.83 / 0.65 / 0.58 (layers 2 / 3 / 4),
-# step within noise (profiles/r02_stride2_43.jsonl)
-OWN_CONV3X3_S2 = os.environ.get("CML_CONV3X3_S2", "0") == "1"
-
-
-def conv3x3_s2_ok(x: torch.Tensor, conv) -> bool:
-    return (OWN_CONV3X3_S2 and x.is_cuda and x.dtype == torch.bfloat16
-            and conv.weight.dtype == torch.bfloat16 and x.dim() == 4
-            and x.is_contiguous(memory_format=torch.channels_last) and conv.kernel_size == (3, 3)
-            and conv.stride == (2, 2) and conv.padding == (1, 1) and conv.dilation == (1, 1)
-            and conv.groups == 1 and conv.bias is None and conv.in_channels % 64 == 0
-            and conv.out_channels % 64 == 0)
-
-
-def conv3x3_s2_bn_stats(x: torch.Tensor, conv, bn):
-    """(z, (mean, invstd)) of a stride-2 3x3 ``conv(x)`` and bn's training statistics."""
-    z, m, i = _Conv3x3S2BNStatsFn.apply(x, conv.weight, bn.running_mean, bn.running_var, bn.eps,
-                                        bn.momentum)
     return z, (m, i)
 
 

@@ -35,6 +35,8 @@ def lib():
                         "consensusml_amd native HIP extension is not built; run "
                         "`python -m consensusml_amd._build`") from e
             _C = mod
+            from .. import perf     # the policy's native-side switches
+            perf.ensure_native_synced()
     return _C
 
 

@@ -10,13 +10,13 @@ tests, fp32) runs the equivalent PyTorch composition, which is also the numerics
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional, Tuple
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..perf import policy as _P
 from .bn import ResidualLink
 from .native import lib
 
@@ -231,11 +231,10 @@ class _AttnFn(torch.autograd.Function):
 def _attn_ok(qkv: torch.Tensor, H: int, hd: int) -> bool:
     S = qkv.shape[1]
     return (_gpu_bf16(qkv) and hd == 64 and S % 32 == 0 and 32 <= S <= 128
-            and qkv.is_contiguous() and qkv.data_ptr() % 16 == 0 and ATTN_KERNEL)
+            and qkv.is_contiguous() and qkv.data_ptr() % 16 == 0 and _P().attn_kernel)
 
 
-# short-sequence MFMA attention for BERT-shaped problems (CML_ATTN_KERNEL=0: SDPA)
-ATTN_KERNEL = os.environ.get("CML_ATTN_KERNEL", "1") == "1"
+# PerfPolicy.attn_kernel: short-sequence MFMA attention for BERT-shaped problems (off: SDPA)
 
 
 def fused_qkv_attention(qkv: torch.Tensor, H: int, hd: int) -> torch.Tensor:

@@ -30,7 +30,6 @@ robust rules can be exercised at n = 8 on a single GPU.
 from __future__ import annotations
 
 import math
-import os
 
 import numpy as np
 from typing import Dict, List, Optional
@@ -40,13 +39,12 @@ import torch.distributed as dist
 
 from ..config import TrainConfig
 from ..ops import kernels as K
+from ..perf import policy as _P
 from ..ops.native import lib
 from .dist import DistInfo
 from .faults import COLLUSION, apply_faults
 from .flat import Bucket, FlatModel
 
-# copy-on-ready capture through the HIP multi-tensor copy (CML_MULTI_COPY=0: torch._foreach_copy_)
-_MULTI_COPY = os.environ.get("CML_MULTI_COPY", "1") == "1"
 
 GRAM_RULES = ("krum", "multi_krum", "geomed", "centered_clip", "bulyan")
 
@@ -300,7 +298,8 @@ class ConsensusEngine:
         if lst:
             dst = [views[i] for i in lst]
             src = [fl.params[i].grad for i in lst]
-            if dst[0].is_cuda and _MULTI_COPY:
+            # copy-on-ready through the HIP multi-tensor copy (PerfPolicy.multi_copy)
+            if dst[0].is_cuda and _P().multi_copy:
                 # one HIP launch per 32 tensors at ~HBM speed (csrc/kernels/multi_copy.hip)
                 rest = lib().multi_copy(dst, src)
                 if rest:

@@ -4,8 +4,9 @@ The reference persists stage results with R ``save()/load()`` of named result li
 append-only standard table (`composite_code/rnotebook/cml_targetaml_seanalysis.Rmd:673`, `:778`,
 `:1069`, `:1239`, `:1298`). Here a training checkpoint is a directory
 
-    <root>/step_<k>/meta.json            config, world size, topology, step, wall time, and the
+    <root>/step_<k>/meta.json            config, world size, topology, step, wall time, the
                                          flat-buffer layout (buckets, shards, parameter offsets)
+                                         and the PerfPolicy (kernel / fusion switches) in force
     <root>/step_<k>/rank<r>.pt           this rank's engine state (fp32 master / optimizer shard),
                                          model buffers (BN statistics), RNG states
     <root>/step_<k>/consensus_table.csv  per-parameter x per-worker gradient statistics of the
@@ -34,6 +35,7 @@ import torch
 import torch.distributed as dist
 
 from ..parallel.dist import barrier
+from ..perf import policy
 
 STATE_KEYS = ("master", "s1", "s2", "v0")
 
@@ -81,7 +83,8 @@ def save_checkpoint(root: str, engine, cfg, extra: Optional[dict] = None,
     if rank == 0:
         meta = {"step": step, "world": engine.N, "topology": engine.topo, "rule": engine.rule,
                 "time": time.time(), "config": json.loads(cfg.to_json()),
-                "params": engine.flat.real_numel, "layout": layout_of(engine)}
+                "params": engine.flat.real_numel, "layout": layout_of(engine),
+                "perf_policy": policy().to_dict()}
         with open(os.path.join(tmp, "meta.json"), "w") as fh:
             json.dump(meta, fh, indent=1)
         if table is not None:

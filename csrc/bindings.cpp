@@ -992,46 +992,6 @@ Tensor bn_bwd_apply(const Tensor& dy_in, const Tensor& x, const Tensor& gamma, c
   return dx;
 }
 
-// 3x3 / stride 1 / padding 1 conv as an implicit GEMM on the fused 1x1 kernel (conv1x1.hip TAP):
-// x [N, C, H, W] NHWC bf16, w [Cout, C, 3, 3] bf16 (made channels_last: [Cout][3][3][C]) ->
-// {y NHWC, mean, invstd}; pro_sc / pro_bi (fp32 [C]): max(x sc + bi, 0) applied on load.
-std::vector<Tensor> conv3x3_bn_fwd(const Tensor& x, const Tensor& w_in, const optional<Tensor>& pro_sc,
-                                   const optional<Tensor>& pro_bi, const optional<Tensor>& shift,
-                                   const optional<Tensor>& rmean, const optional<Tensor>& rvar,
-                                   bool stats, double eps, double momentum) {
-  check_nhwc(x, "x");
-  TORCH_CHECK(x.dim() == 4, "conv3x3_bn_fwd: 4-D NHWC input");
-  TORCH_CHECK(w_in.scalar_type() == at::kBFloat16 && w_in.dim() == 4 && w_in.size(1) == x.size(1) &&
-                  w_in.size(2) == 3 && w_in.size(3) == 3, "conv3x3_bn_fwd: w must be bf16 [Cout, C, 3, 3]");
-  Tensor w = w_in.contiguous(at::MemoryFormat::ChannelsLast);
-  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), Co = w.size(0);
-  TORCH_CHECK(C % 64 == 0 && Co % 64 == 0, "conv3x3_bn_fwd: channels must be multiples of 64");
-  const int64_t M = N * H * W;
-  const bool pro = pro_sc.has_value() && pro_sc->defined();
-  const float* sc = opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", C);
-  const float* bi = opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", C);
-  TORCH_CHECK(!pro || bi, "pro_bi needed with pro_sc");
-  const c10::DeviceGuard guard(x.device());
-  auto f32 = x.options().dtype(at::kFloat);
-  Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  Tensor mean, invstd, part;
-  if (stats) {
-    mean = at::empty({Co}, f32);
-    invstd = at::empty({Co}, f32);
-    part = at::empty({static_cast<int64_t>(cml::conv3x3_bn_part_floats(M, static_cast<int>(C),
-                                                                     static_cast<int>(Co), pro))}, f32);
-  }
-  CML_CHECK_HIP(cml::launch_conv3x3_bn_fwd(
-      x.data_ptr(), w.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, sc, bi,
-      opt_ptr<const float>(shift, at::kFloat, "shift", Co), static_cast<int>(N),
-      static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(Co),
-      stats ? mean.data_ptr<float>() : nullptr, stats ? invstd.data_ptr<float>() : nullptr,
-      stats ? opt_ptr<float>(rmean, at::kFloat, "running_mean", Co) : nullptr,
-      stats ? opt_ptr<float>(rvar, at::kFloat, "running_var", Co) : nullptr,
-      static_cast<float>(eps), static_cast<float>(momentum), cur_stream()));
-  return {y, mean, invstd};
-}
-
 // dX = dY W (1x1, stride 1: x = dY [N, K, H, W] NHWC, w [No, K] -- W^T of the conv's weight)
 // plus, at the even pixels, link [N, No, ceil(H/2), ceil(W/2)]: a parallel stride-2 conv's
 // compact data gradient (never scattered to full resolution).
@@ -1085,37 +1045,11 @@ Tensor upsample2_scatter(const Tensor& g_in, int64_t H, int64_t W) {
   return dx;
 }
 
-// Weight gradient of a stride-2 1x1 conv (downsample): dy [N, Co, ceil(H/2), ceil(W/2)], x
-// [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 1, 1] in `dtype`.
-Tensor wgrad1x1_s2(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype) {
-  check_nhwc(x, "x");
-  Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
-  check_nhwc(dy, "dy");
-  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1);
-  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(0) == N && dy.size(2) == (H + 1) / 2 &&
-                  dy.size(3) == (W + 1) / 2, "wgrad1x1_s2: dy / x shapes");
-  TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "wgrad1x1_s2: bf16 or fp32 output");
-  TORCH_CHECK((Co == 64 && Ci == 64) || (Ci == 64 ? Co % 256 == 0 : (Co % 128 == 0 && Ci % 128 == 0)),
-              "wgrad1x1_s2: unsupported channel counts");
-  const c10::DeviceGuard guard(x.device());
-  const int S = cml::wgrad1x1_s2_splits(static_cast<int>(N), static_cast<int>(H),
-                                        static_cast<int>(W), static_cast<int>(Co),
-                                        static_cast<int>(Ci));
-  Tensor part = at::empty({S, Co, Ci}, x.options().dtype(at::kFloat));
-  Tensor dw = at::empty({Co, Ci, 1, 1}, x.options().dtype(dtype));
-  CML_CHECK_HIP(cml::launch_wgrad1x1_s2(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(),
-                                        dw.data_ptr(), dtype == at::kBFloat16, static_cast<int>(N),
-                                        static_cast<int>(H), static_cast<int>(W),
-                                        static_cast<int>(Co), static_cast<int>(Ci), cur_stream()));
-  return dw;
-}
 
-// Weight gradient of a 3x3 / stride 1 / padding 1 conv (wgrad1x1.hip TAP): dy [N, Co, H, W],
-// x [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 3, 3] in `dtype` (channels_last memory); pro_sc / pro_bi
-// (fp32 [Ci]): x replaced by max(x sc + bi, 0) (zero padding after the transform).
+// Weight gradient of a 3x3 / stride 1 / padding 1 conv (wgrad3x3.hip, nine taps per workgroup):
+// dy [N, Co, H, W], x [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 3, 3] in `dtype` (channels_last memory).
 Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
-                const optional<Tensor>& pro_sc, const optional<Tensor>& pro_bi,
-                const optional<Tensor>& zero_in, bool tap_mode) {
+                const optional<Tensor>& zero_in) {
   check_nhwc(x, "x");
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc(dy, "dy");
@@ -1123,44 +1057,30 @@ Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
                   dy.size(3) == x.size(3), "wgrad3x3: dy / x shapes");
   TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "wgrad3x3: bf16 or fp32 output");
   const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1);
-  const float* sc = opt_ptr<const float>(pro_sc, at::kFloat, "pro_sc", Ci);
-  const float* bi = opt_ptr<const float>(pro_bi, at::kFloat, "pro_bi", Ci);
-  TORCH_CHECK((sc == nullptr) == (bi == nullptr), "wgrad3x3: pro_sc and pro_bi together");
   const c10::DeviceGuard guard(x.device());
   int S = 1, T = 0;
-  if (!sc && !tap_mode &&
-      cml::wgrad3x3_direct_plan(static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
-                                static_cast<int>(Co), static_cast<int>(Ci), &S, &T)) {
-    // all nine taps per workgroup (wgrad3x3.hip); dW in the channels_last order of [Co, Ci, 3, 3]
-    Tensor zero;
-    if (zero_in.has_value() && zero_in->defined()) {
-      zero = *zero_in;
-      TORCH_CHECK(zero.is_cuda() && zero.device() == x.device() && zero.scalar_type() == at::kBFloat16 &&
-                      zero.is_contiguous() && zero.numel() >= 8, "wgrad3x3: zero must be >= 8 bf16");
-    } else {
-      zero = at::zeros({64}, x.options());
-    }
-    Tensor part = at::empty({S, Co, 9, Ci}, x.options().dtype(at::kFloat));
-    Tensor dw = at::empty({Co, 3, 3, Ci}, x.options().dtype(dtype));
-    CML_CHECK_HIP(cml::launch_wgrad3x3_direct(dy.data_ptr(), x.data_ptr(), zero.data_ptr(),
-                                              part.data_ptr<float>(), dw.data_ptr(),
-                                              dtype == at::kBFloat16, static_cast<int>(N),
-                                              static_cast<int>(H), static_cast<int>(W),
-                                              static_cast<int>(Co), static_cast<int>(Ci),
-                                              cur_stream()));
-    return dw.permute({0, 3, 1, 2});
+  TORCH_CHECK(cml::wgrad3x3_direct_plan(static_cast<int>(N), static_cast<int>(H),
+                                        static_cast<int>(W), static_cast<int>(Co),
+                                        static_cast<int>(Ci), &S, &T),
+              "wgrad3x3: no plan for this shape (check wgrad3x3_direct_ok first)");
+  // all nine taps per workgroup (wgrad3x3.hip); dW in the channels_last order of [Co, Ci, 3, 3]
+  Tensor zero;
+  if (zero_in.has_value() && zero_in->defined()) {
+    zero = *zero_in;
+    TORCH_CHECK(zero.is_cuda() && zero.device() == x.device() && zero.scalar_type() == at::kBFloat16 &&
+                    zero.is_contiguous() && zero.numel() >= 8, "wgrad3x3: zero must be >= 8 bf16");
+  } else {
+    zero = at::zeros({64}, x.options());
   }
-  TORCH_CHECK(Ci == 64 ? (Co == 64 || Co % 256 == 0) : (Co % 128 == 0 && Ci % 128 == 0),
-              "wgrad3x3: unsupported channel counts");
-  int TM, TN, cps = 1;
-  cml::wgrad3x3_plan(N * H * W, static_cast<int>(Co), static_cast<int>(Ci), &TM, &TN, &S, &cps);
-  Tensor part = at::empty({S, 9, Co, Ci}, x.options().dtype(at::kFloat));
-  Tensor dw = at::empty({3, 3, Co, Ci}, x.options().dtype(dtype));
-  CML_CHECK_HIP(cml::launch_wgrad3x3(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(),
-                                     dw.data_ptr(), dtype == at::kBFloat16, static_cast<int>(N),
-                                     static_cast<int>(H), static_cast<int>(W), static_cast<int>(Co),
-                                     static_cast<int>(Ci), sc, bi, cur_stream()));
-  return dw.permute({2, 3, 0, 1});   // [Co, Ci, 3, 3] view of the tap-major result
+  Tensor part = at::empty({S, Co, 9, Ci}, x.options().dtype(at::kFloat));
+  Tensor dw = at::empty({Co, 3, 3, Ci}, x.options().dtype(dtype));
+  CML_CHECK_HIP(cml::launch_wgrad3x3_direct(dy.data_ptr(), x.data_ptr(), zero.data_ptr(),
+                                            part.data_ptr<float>(), dw.data_ptr(),
+                                            dtype == at::kBFloat16, static_cast<int>(N),
+                                            static_cast<int>(H), static_cast<int>(W),
+                                            static_cast<int>(Co), static_cast<int>(Ci),
+                                            cur_stream()));
+  return dw.permute({0, 3, 1, 2});
 }
 
 // Implicit-GEMM conv (conv_gemm.hip): x [N, C, H, W] NHWC bf16, w [Cout, taps * C] contiguous
@@ -1739,6 +1659,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gossip_workspace_bytes", &gossip_workspace_bytes);
   m.def("gossip_mix", &gossip_mix, "ring gossip mixing with neighbour clipping");
   m.def("gossip_mix_k", &gossip_mix_k, "k-neighbour gossip mixing with neighbour clipping");
+  m.def("conv1x1g_mode", &cml::conv1x1g_mode, "fused 1x1 kernel family: 0 old, 1 glds, 2 auto");
+  m.def("set_conv1x1g_mode", &cml::set_conv1x1g_mode, "select the fused 1x1 kernel family");
   m.def("fault", &fault, "Byzantine fault injection");
   m.def("bn_fwd", &bn_fwd, "fused NHWC BatchNorm(+res)(+ReLU) forward");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BatchNorm(+res)(+ReLU) backward");
@@ -1758,17 +1680,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dz_b") = py::none(), py::arg("dz_c") = py::none(),
         "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
   m.def("wgrad3x3", &wgrad3x3, py::arg("dy"), py::arg("x"), py::arg("dtype"),
-        py::arg("pro_sc") = py::none(), py::arg("pro_bi") = py::none(),
-        py::arg("zero") = py::none(), py::arg("tap_mode") = false,
-        "weight gradient of a 3x3 stride-1 conv (MFMA, split-K): all nine taps per workgroup "
-        "(wgrad3x3.hip) where the plan fits, else / with a prologue / tap_mode one tap per grid z");
+        py::arg("zero") = py::none(),
+        "weight gradient of a 3x3 stride-1 conv (MFMA, split-K, all nine taps per workgroup: "
+        "wgrad3x3.hip) for shapes with wgrad3x3_direct_ok");
   m.def("conv1x1_link_s2", &conv1x1_link_s2,
         "1x1 data gradient + a stride-2 conv's compact data gradient at the even pixels");
   m.def("subsample2", &subsample2, "x[:, :, ::2, ::2] of an NHWC bf16 tensor, dense NHWC");
   m.def("upsample2_scatter", &upsample2_scatter, py::arg("g"), py::arg("H"), py::arg("W"),
         "full-resolution NHWC tensor with g at the even pixels, zeros elsewhere");
-  m.def("wgrad1x1_s2", &wgrad1x1_s2, py::arg("dy"), py::arg("x"), py::arg("dtype"),
-        "weight gradient of a stride-2 1x1 conv (MFMA, split-K, x gathered at even pixels)");
   m.def("wgrad3x3_direct_ok", [](int64_t B, int64_t H, int64_t W, int64_t Co, int64_t Ci) {
     int S, T;
     return cml::wgrad3x3_direct_plan(static_cast<int>(B), static_cast<int>(H), static_cast<int>(W),
@@ -1802,7 +1721,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
         py::arg("eps") = 1e-5, py::arg("momentum") = 0.1, py::arg("stride") = 1,
         "implicit-GEMM conv + BN statistics of the output in the epilogue -> {y, mean, invstd}");
-  m.def("conv3x3_bn_fwd", &conv3x3_bn_fwd, "3x3/s1/p1 conv (implicit GEMM) + BN statistics");
   m.def("conv1x1_bnbwd", &conv1x1_bnbwd, "1x1 data gradient through a BN + ReLU backward prologue");
   m.def("conv1x1_link", &conv1x1_link, py::arg("x"), py::arg("w"), py::arg("link"),
         py::arg("lmask"), py::arg("sz") = py::none(), py::arg("smask") = py::none(),

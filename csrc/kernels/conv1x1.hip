@@ -32,70 +32,12 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "conv1x1_common.h"
 #include "kernels.h"
 
 namespace cml {
 namespace {
-
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-constexpr int kBK = 64;          // K per step: one 128-B LDS row per output channel / pixel
-constexpr int kThreads = 256;    // 4 waves
-
-__device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// byte offset of 16-B chunk c (0..7) of row `row` in a [rows][128 B] image. Row parity picks the
-// half of the 256-B bank row, and the XOR with row bits 1..3 spreads the 16 rows of each
-// ds_read_b128 lane group ({0-3,12-15,20-27}, ...) over 16 distinct 16-B bank slots.
-__device__ __forceinline__ int swz(int row, int c) { return row * 128 + 16 * (c ^ ((row >> 1) & 7)); }
-
-// Prologue modes (f applied to x while staging) and statistics modes (epilogue sums).
-enum { PM_NONE = 0, PM_BNRELU = 1, PM_BNBWD = 2, PM_CAT = 3 };
-enum { SM_BN = 0, SM_BNBWD = 1, SM_OFF = 2, SM_BNRES = 3 };
-
-struct C1Args {
-  const uint16_t* x;      // [rows_in][K]
-  const uint16_t* w;      // [N][K]
-  uint16_t* y;            // [M][N]
-  float* part;            // [ntn][wgpn * WM][2][BN] or null
-  const float* pro_sc;    // PM_BNRELU: sc[K]; PM_BNBWD: a[K]
-  const float* pro_bi;    // PM_BNRELU: bi[K]; PM_BNBWD: b[K]
-  const float* pro_c;     // PM_BNBWD: c[K]
-  const uint16_t* x2;     // PM_BNBWD: z [rows_in][K] (the BN input)
-  const uint8_t* xm;      // PM_BNBWD: ReLU bit mask of the BN output [rows_in][K / 8]
-  const uint16_t* link;   // EL: [M][N] added to the product where lm's bit is set
-  const uint8_t* lm;      // EL: [M][N / 8]
-  const uint16_t* sz;     // SM_BNBWD: z of the BN whose backward sums are taken [M][N]
-  const uint8_t* sm;      // SM_BNBWD: its ReLU bit mask [M][N / 8]
-  const float* shift;     // [N] or null (SM_BN: statistics shift; SM_BNBWD: the BN's mean)
-  const float* ep_sc;     // SM_BNRES: y = max(v ep_sc + ep_bi + link, 0) per output channel [N]
-  const float* ep_bi;
-  uint8_t* ymask;         // SM_BNRES: bit mask of y > 0 [M][N / 8]
-  int K1;                 // PM_CAT: channels of the first source (x, with mask xm); x2 has K - K1
-  int cat_bnrelu;         // PM_CAT: 1 = the first source is max(x sc + bi, 0) too (no mask)
-  int M, K, N;
-  int ntn, wgpn, mtiles;
-  int H, W, OW, OHW;      // S2: input H, W; output W and H*W.  TAP: H, W (in = out) and OHW = H W
-  int C;                  // TAP: input channels (K = 9 C, k = tap C + c, tap = 3 (dy + 1) + dx + 1)
-  // EL with link_s2: link is [N][ceil(H/2)][ceil(W/2)][N channels] (a stride-2 conv's compact
-  // data gradient), added at the even pixels of this [N][H][W] output (lm unused)
-  int link_s2, lW, lHW, lOW, lOHW;
-};
-
-__device__ __forceinline__ int64_t src_row(const C1Args& a, int m, bool s2) {
-  m = m < a.M ? m : a.M - 1;                                    // clamped: loads stay in bounds
-  if (s2) {
-    const int img = m / a.OHW;
-    const int rem = m - img * a.OHW;
-    const int oh = rem / a.OW;
-    const int ow = rem - oh * a.OW;
-    return static_cast<int64_t>(img) * a.H * a.W + 2 * oh * a.W + 2 * ow;
-  }
-  return m;
-}
+using namespace c1;
 
 // W k-step ks of rows [n0, n0 + 32 CA) into LDS block `dst`. W is small and L2-resident, so it is
 // loaded at staging time rather than prefetched across the MFMA phase.
@@ -110,34 +52,9 @@ __device__ __forceinline__ void stage_w(const C1Args& a, char* dst, int n0, int 
 }
 
 // x step ks (and, for PM_BNBWD, the matching z chunks and mask bytes) into prefetch registers
-// TAP (3x3, stride 1, padding 1 implicit GEMM): k-step ks is 64 channels of one tap; rows whose
-// tap falls into the padding load a valid row and are zeroed at staging (bit j of vm).
-template <int CB, int BM, bool S2, int PM, bool TAP = false>
+template <int CB, int BM, bool S2, int PM>
 __device__ __forceinline__ void load_x(const C1Args& a, uint4 (&pb)[CB], uint4 (&pz)[CB],
-                                       uint32_t (&pm)[CB], int t, int ks, int srow, int ch,
-                                       uint32_t& vm) {
-  if constexpr (TAP) {
-    const int CS = a.C >> 6;
-    const int tap = ks / CS, cc = ks - tap * CS;
-    const int ty = tap / 3 - 1, tx = tap - 3 * (tap / 3) - 1;
-    vm = 0;
-#pragma unroll
-    for (int j = 0; j < CB; ++j) {
-      const int m = t * BM + srow + 32 * j;
-      const int mc = m < a.M ? m : a.M - 1;
-      const int img = mc / a.OHW;
-      const int rem = mc - img * a.OHW;
-      const int oh = rem / a.W;
-      const int ow = rem - oh * a.W;
-      const int ih = oh + ty, iw = ow + tx;
-      const bool ok = m < a.M && static_cast<unsigned>(ih) < static_cast<unsigned>(a.H) &&
-                      static_cast<unsigned>(iw) < static_cast<unsigned>(a.W);
-      const int64_t r = ok ? static_cast<int64_t>(img) * a.OHW + ih * a.W + iw : mc;
-      vm |= (ok ? 1u : 0u) << j;
-      pb[j] = *reinterpret_cast<const uint4*>(a.x + r * a.C + cc * kBK + 8 * ch);
-    }
-    return;
-  }
+                                       uint32_t (&pm)[CB], int t, int ks, int srow, int ch) {
   if constexpr (PM == PM_CAT) {
     const int k0 = ks * kBK;
     const bool first = k0 < a.K1;
@@ -165,27 +82,21 @@ __device__ __forceinline__ void load_x(const C1Args& a, uint4 (&pb)[CB], uint4 (
   }
 }
 
-__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
-  const float4 u0 = reinterpret_cast<const float4*>(p)[0], u1 = reinterpret_cast<const float4*>(p)[1];
-  v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w;
-  v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
-}
 
 // f(x) into the LDS image:
 //   PM_BNRELU  max(x sc + bi, 0)                        (the producer's BN + ReLU)
 //   PM_BNBWD   a (mask ? x : 0) + b z + c               (a BN + ReLU backward: x = dL/d(output),
 //              z = the BN input; a = gamma invstd, b = -gamma invstd^2 q / M,
 //              c = -gamma invstd s / M - b mean, with s, q the BN's backward sums)
-// kofs: first input channel of this k-step (ks * 64, or the tap's channel chunk); KA: entries per
-// coefficient row of s_aff; TAP: rows with a clear bit in vm are zeroed (padding).
+// kofs: first input channel of this k-step (ks * 64); KA: entries per coefficient row of s_aff.
 //   PM_CAT     a (mask ? x : 0) + c  for k < K1 (x = a BN + ReLU output gradient, no z term),
 //              max(x2 sc + bi, 0)   for k >= K1 (a BN + ReLU output, recomputed): one GEMM over two
 //              sources concatenated along K
-template <int CB, int PM, bool TAP = false>
+template <int CB, int PM>
 __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)[CB],
                                         const uint32_t (&pm)[CB], char* sx, const float* s_aff,
-                                        int KA, int kofs, int srow, int ch, uint32_t vm = ~0u,
-                                        int K1 = 0, int cat_bnrelu = 0) {
+                                        int KA, int kofs, int srow, int ch, int K1 = 0,
+                                        int cat_bnrelu = 0) {
   float sc[8], bi[8], cc[8];
   if constexpr (PM != PM_NONE) {
     ld8f(s_aff + kofs + 8 * ch, sc);
@@ -240,211 +151,18 @@ __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)
       }
       v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
-    if constexpr (TAP) {
-      const bool ok = (vm >> j) & 1u;
-      v = make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
-    }
     *reinterpret_cast<uint4*>(sx + swz(srow + 32 * j, ch)) = v;
   }
-}
-
-// Round the wave's 64 (n) x 64 (m) block to bf16 and store it, adding the stored values (minus the
-// shift) to the statistics. The accumulator layout (lane = pixel, 4 consecutive channels per
-// register group) would make every global store instruction touch 32 lines with 16 B each (the
-// kernel then wrote at ~3 TB/s); instead the block goes through the wave's own 8 KB LDS image
-// [pixel][128 B] (XOR-swizzled like the operand images) and comes back as 16-B pieces, 8 lanes per
-// 128-B pixel row: every store instruction writes whole lines. The read-back also gives each lane
-// a fixed group of 8 channels (lane & 7), so the statistics need 16 registers (sum and sum of
-// squares of 8 channels) instead of 64. Only this wave touches its image: no workgroup barrier.
-//
-// EL: the stored value is bf16(bf16(acc) + (lm bit ? link : 0)) (a data gradient plus the masked
-// residual gradient of the same tensor). SM_BNBWD: the sums are s = sum (sm bit ? v : 0) and
-// q = sum (sm bit ? v : 0) (sz - shift) -- the backward reduction of the BN + ReLU whose output
-// gradient v is (the consumer BN's mean in shift) -- instead of the BN statistics of v.
-// DM (SM_BNBWD without a stored mask, PM_CAT data gradients of the recompute tails): the ReLU bit
-// is recomputed from the BN input, sz * ep_sc + ep_bi > 0 (the BN's own affine, as its forward
-// prologue applied it), so the BN + ReLU backward that follows needs no reduction pass of its own.
-template <bool EL, int SM, int MT, bool DM = false>
-__device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], float (&ss)[8],
-                                         float (&sq)[8], const float (&sh)[8], char* simg, int m0,
-                                         int ncol0, int n0, int lane) {
-  const int h = lane >> 5, r32 = lane & 31;
-  const int c = lane & 7;
-  // EL / SM_BNBWD operands of the read-back rows are issued as one batch before they are needed
-  // (a 1-2 k-step GEMM was otherwise bound by these dependent loads, one latency per row pair):
-  // all 8 rows at once with one operand (EL), in batches of 4 with two, halved again at MT = 2
-  // (more registers would spill). Rows past M re-read row M - 1 (a wave block of a partial tile
-  // can start past M).
-  constexpr bool LD = EL || SM == SM_BNBWD || SM == SM_BNRES;
-  constexpr int RB = ((EL && SM == SM_BNBWD) ? 4 : 8) / MT /   // rows per batch
-                     ((SM == SM_BNRES && MT == 2) ? 2 : 1);
-  uint4 lv[RB], zv[RB];
-  uint32_t lbv[RB], zbv[RB];
-  if constexpr (!(EL && SM == SM_BNBWD)) {   // one operand: keep the row body's arguments defined
-#pragma unroll
-    for (int k = 0; k < RB; ++k) {
-      if constexpr (!EL) lbv[k] = 0u;
-      if constexpr (!EL && SM != SM_BNRES) lv[k] = make_uint4(0u, 0u, 0u, 0u);
-      if constexpr (SM != SM_BNBWD) { zv[k] = make_uint4(0u, 0u, 0u, 0u); zbv[k] = 0u; }
-    }
-  }
-  // SM_BNRES / DM: the lane's 8 output channels' BN coefficients
-  float esc[8], ebi[8];
-  if constexpr (SM == SM_BNRES || DM) {
-    ld8f(a.ep_sc + n0 + ncol0 + 8 * c, esc);
-    ld8f(a.ep_bi + n0 + ncol0 + 8 * c, ebi);
-  }
-  auto issue = [&](int k0) {
-#pragma unroll
-    for (int k = 0; k < RB; ++k) {
-      const int p = 8 * (k0 + k) + (lane >> 3);
-      const int64_t row = m0 + p < a.M ? m0 + p : a.M - 1;
-      const int64_t e0 = row * a.N + n0 + ncol0 + 8 * c;
-      if constexpr (EL) {
-        if (a.link_s2) {   // compact stride-2 gradient: only the even pixels get an addend
-          const int img = static_cast<int>(row / a.lHW);
-          const int rem = static_cast<int>(row - static_cast<int64_t>(img) * a.lHW);
-          const int hh = rem / a.lW, ww = rem - hh * a.lW;
-          const bool ev = !((hh | ww) & 1);
-          const int64_t lrow = ev ? static_cast<int64_t>(img) * a.lOHW + (hh >> 1) * a.lOW + (ww >> 1) : 0;
-          lv[k] = *reinterpret_cast<const uint4*>(a.link + lrow * a.N + n0 + ncol0 + 8 * c);
-          lbv[k] = ev ? 0xffu : 0u;
-        } else {
-          lv[k] = *reinterpret_cast<const uint4*>(a.link + e0);
-          lbv[k] = a.lm[e0 >> 3];
-        }
-      }
-      if constexpr (SM == SM_BNRES)   // (no residual: link null)
-        lv[k] = a.link ? *reinterpret_cast<const uint4*>(a.link + e0) : make_uint4(0u, 0u, 0u, 0u);
-      if constexpr (SM == SM_BNBWD) {
-        zv[k] = *reinterpret_cast<const uint4*>(a.sz + e0);
-        zbv[k] = DM ? 0u : a.sm[e0 >> 3];
-      }
-    }
-  };
-  if constexpr (LD) issue(0);
-#pragma unroll
-  for (int jm = 0; jm < 2; ++jm) {
-    const int p = 32 * jm + r32;                       // pixel row of the wave block
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t b0 = f2bf(acc[i][jm][4 * g + 0]), b1 = f2bf(acc[i][jm][4 * g + 1]);
-        const uint32_t b2 = f2bf(acc[i][jm][4 * g + 2]), b3 = f2bf(acc[i][jm][4 * g + 3]);
-        // channels 32 i + 8 g + 4 h .. +3 = half h of 16-B chunk 4 i + g of the pixel row
-        *reinterpret_cast<uint2*>(simg + swz(p, 4 * i + g) + 8 * h) =
-            make_uint2(b0 | (b1 << 16), b2 | (b3 << 16));
-      }
-    }
-  }
-  // the wave's own LDS writes complete before its reads
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  // one read-back row: 8 channels (lane & 7) of pixel 8 k + lane / 8
-  auto row = [&](int k, const uint4& l, uint32_t lb, const uint4& z, uint32_t zb) {
-    const int p = 8 * k + (lane >> 3);
-    uint4 v = *reinterpret_cast<const uint4*>(simg + swz(p, c));
-    if (m0 + p >= a.M) return;
-    const int64_t e0 = static_cast<int64_t>(m0 + p) * a.N + n0 + ncol0 + 8 * c;
-    if constexpr (EL) {
-      const uint32_t l4[4] = {l.x, l.y, l.z, l.w};
-      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float lo = __uint_as_float(w4[q] << 16) +
-                         (((lb >> (2 * q)) & 1u) ? __uint_as_float(l4[q] << 16) : 0.f);
-        const float hi = __uint_as_float(w4[q] & 0xffff0000u) +
-                         (((lb >> (2 * q + 1)) & 1u) ? __uint_as_float(l4[q] & 0xffff0000u) : 0.f);
-        w4[q] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
-      }
-      v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-    }
-    if constexpr (SM == SM_BNRES) {   // y = max(bn(v) + res, 0) and its bit mask; no statistics
-      const uint32_t r4[4] = {l.x, l.y, l.z, l.w};
-      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-      uint32_t bits = 0u;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float lo = fmaf(__uint_as_float(w4[q] << 16), esc[2 * q], ebi[2 * q]) +
-                         __uint_as_float(r4[q] << 16);
-        const float hi = fmaf(__uint_as_float(w4[q] & 0xffff0000u), esc[2 * q + 1], ebi[2 * q + 1]) +
-                         __uint_as_float(r4[q] & 0xffff0000u);
-        bits |= (lo > 0.f ? 1u : 0u) << (2 * q);
-        bits |= (hi > 0.f ? 1u : 0u) << (2 * q + 1);
-        w4[q] = static_cast<uint32_t>(f2bf(fmaxf(lo, 0.f))) |
-                (static_cast<uint32_t>(f2bf(fmaxf(hi, 0.f))) << 16);
-      }
-      *reinterpret_cast<uint4*>(a.y + e0) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-      a.ymask[e0 >> 3] = static_cast<uint8_t>(bits);
-      return;
-    }
-    if (SM != SM_BN || a.y) *reinterpret_cast<uint4*>(a.y + e0) = v;   // SM_BN, y null: stats only
-    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-    if constexpr (SM == SM_BN) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float lo = __uint_as_float(w4[q] << 16) - sh[2 * q];
-        const float hi = __uint_as_float(w4[q] & 0xffff0000u) - sh[2 * q + 1];
-        ss[2 * q] += lo;
-        ss[2 * q + 1] += hi;
-        sq[2 * q] = fmaf(lo, lo, sq[2 * q]);
-        sq[2 * q + 1] = fmaf(hi, hi, sq[2 * q + 1]);
-      }
-    } else if constexpr (SM == SM_BNBWD) {
-      const uint32_t z4[4] = {z.x, z.y, z.z, z.w};
-      if constexpr (DM) {
-        zb = 0u;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          zb |= (fmaf(__uint_as_float(z4[q] << 16), esc[2 * q], ebi[2 * q]) > 0.f ? 1u : 0u) << (2 * q);
-          zb |= (fmaf(__uint_as_float(z4[q] & 0xffff0000u), esc[2 * q + 1], ebi[2 * q + 1]) > 0.f
-                     ? 1u : 0u) << (2 * q + 1);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float lo = ((zb >> (2 * q)) & 1u) ? __uint_as_float(w4[q] << 16) : 0.f;
-        const float hi = ((zb >> (2 * q + 1)) & 1u) ? __uint_as_float(w4[q] & 0xffff0000u) : 0.f;
-        ss[2 * q] += lo;
-        ss[2 * q + 1] += hi;
-        sq[2 * q] = fmaf(lo, __uint_as_float(z4[q] << 16) - sh[2 * q], sq[2 * q]);
-        sq[2 * q + 1] = fmaf(hi, __uint_as_float(z4[q] & 0xffff0000u) - sh[2 * q + 1], sq[2 * q + 1]);
-      }
-    }
-  };
-  if constexpr (LD) {
-#pragma unroll
-    for (int kb = 0; kb < 8; kb += RB) {
-      if (kb > 0) issue(kb);
-#pragma unroll
-      for (int k = 0; k < RB; ++k) row(kb + k, lv[k], lbv[k], zv[k], zbv[k]);
-    }
-  } else {
-    const uint4 none = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll 2
-    for (int k = 0; k < 8; ++k) row(k, none, 0u, none, 0u);
-  }
-  // the image is rewritten by the next tile's epilogue only after these reads have returned
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int jm = 0; jm < 2; ++jm)
-#pragma unroll
-      for (int k = 0; k < 16; ++k) acc[i][jm][k] = 0.f;
 }
 
 // MT: 64-pixel sub-blocks per wave (wave tile 64 (n) x 64 MT (m)). MT = 2 halves the LDS operand
 // reads per MFMA (2 A + 4 B fragments feed 8 MFMAs instead of 2 + 2 for 4) and the W re-staging
 // per output pixel; its epilogue images then alias the x staging buffer (BM = 256 rows = 32 KB,
 // behind one extra barrier per tile) to stay inside 80 KB of LDS.
-template <int WN, int WM, int PM, bool WRES, bool S2, bool EL, int SM, int MT = 1,
-          bool TAP = false>
+template <int WN, int WM, int PM, bool WRES, bool S2, bool EL, int SM, int MT = 1>
 __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
   constexpr int NAFF = PM == PM_BNBWD ? 3 : ((PM == PM_BNRELU || PM == PM_CAT) ? 2 : 0);
-  const int KA = TAP ? a.C : a.K;                               // prologue coefficients per row
+  const int KA = a.K;                                           // prologue coefficients per row
   constexpr int BN = 64 * WN, BM = 64 * WM * MT;
   constexpr int CA = BN / 32, CB = BM / 32;     // 16-B staging chunks per thread and step
   constexpr bool ALIAS = MT > 1;
@@ -477,8 +195,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       if constexpr (NAFF > 2) s_aff[2 * KA + k] = a.pro_c[k];
     }
   }
-  // first input channel of k-step ks (TAP: the channel chunk within the tap)
-  auto kofs = [&](int ks_) { return TAP ? (ks_ % (a.C >> 6)) * kBK : ks_ * kBK; };
+  // first input channel of k-step ks
+  auto kofs = [&](int ks_) { return ks_ * kBK; };
   if constexpr (WRES) {   // the whole W slice of this n-tile, once
     for (int ks = 0; ks < KS; ++ks) stage_w<CA>(a, sw + ks * BN * 128, n0, srow, ch, ks);
   }
@@ -498,10 +216,9 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
 
   uint4 pb[CB], pz[CB];
   uint32_t pm[CB];
-  uint32_t vm = ~0u;
   int t = j0, ks = 0;
   if (t < a.mtiles) {
-    load_x<CB, BM, S2, PM, TAP>(a, pb, pz, pm, t, 0, srow, ch, vm);
+    load_x<CB, BM, S2, PM>(a, pb, pz, pm, t, 0, srow, ch);
     __syncthreads();                 // s_aff / s_sh / resident W visible
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -509,7 +226,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       ss[q] = 0.f;
       sq[q] = 0.f;
     }
-    store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, 0, srow, ch, vm, a.K1, a.cat_bnrelu);
+    store_x<CB, PM>(pb, pz, pm, sx, s_aff, KA, 0, srow, ch, a.K1, a.cat_bnrelu);
     if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, 0);
     __syncthreads();
     for (;;) {
@@ -521,7 +238,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       const bool more = tn < a.mtiles;
       // prefetch the next step's x into registers; past the end, reload the current (valid) step
       // instead of branching around the loads (hipcc would wait for them at the join)
-      load_x<CB, BM, S2, PM, TAP>(a, pb, pz, pm, more ? tn : t, more ? ksn : ks, srow, ch, vm);
+      load_x<CB, BM, S2, PM>(a, pb, pz, pm, more ? tn : t, more ? ksn : ks, srow, ch);
       const char* wa = sw + (WRES ? ks : 0) * BN * 128;
 #pragma unroll
       for (int kk = 0; kk < kBK / 16; ++kk) {
@@ -552,7 +269,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       }
       if (!more) break;
       __syncthreads();               // every wave is done reading this step's LDS
-      store_x<CB, PM, TAP>(pb, pz, pm, sx, s_aff, KA, kofs(ksn), srow, ch, vm, a.K1,
+      store_x<CB, PM>(pb, pz, pm, sx, s_aff, KA, kofs(ksn), srow, ch, a.K1,
                            a.cat_bnrelu);
       if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, ksn);
       __syncthreads();
@@ -868,12 +585,11 @@ Plan make_plan(int64_t M, int K, int N, int naff, int kaff = -1, bool mt2_ok = t
   return p;
 }
 
-template <int WN, int WM, int PM, bool WRES, bool S2, bool EL = false, int SM = SM_BN,
-          bool TAP = false>
+template <int WN, int WM, int PM, bool WRES, bool S2, bool EL = false, int SM = SM_BN>
 hipError_t launch_t(const C1Args& a, const Plan& p, hipStream_t st) {
-  auto k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 1, TAP>;
+  auto k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 1>;
   if constexpr (WN == 2 && PM != PM_BNBWD && SM != SM_BNBWD && !(PM == PM_CAT && SM == SM_BNRES)) {
-    if (p.MT == 2) k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 2, TAP>;
+    if (p.MT == 2) k = &conv1x1_bn_fwd_kernel<WN, WM, PM, WRES, S2, EL, SM, 2>;
   }
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
@@ -893,16 +609,6 @@ hipError_t launch_w(const C1Args& a, const Plan& p, bool pro, bool s2, hipStream
                   : launch_t<WN, WM, PM_BNRELU, false, false>(a, p, st);
   return p.wres ? launch_t<WN, WM, PM_NONE, true, false>(a, p, st)
                 : launch_t<WN, WM, PM_NONE, false, false>(a, p, st);
-}
-
-// 3x3 / stride 1 / padding 1 forward (TAP), optional BN + ReLU prologue, BN statistics epilogue
-template <int WN, int WM>
-hipError_t launch_tap_w(const C1Args& a, const Plan& p, bool pro, hipStream_t st) {
-  if (pro)
-    return p.wres ? launch_t<WN, WM, PM_BNRELU, true, false, false, SM_BN, true>(a, p, st)
-                  : launch_t<WN, WM, PM_BNRELU, false, false, false, SM_BN, true>(a, p, st);
-  return p.wres ? launch_t<WN, WM, PM_NONE, true, false, false, SM_BN, true>(a, p, st)
-                : launch_t<WN, WM, PM_NONE, false, false, false, SM_BN, true>(a, p, st);
 }
 
 // backward variants (stride 1): mode 0 = BN-backward prologue, no statistics; 1 = masked link
@@ -969,7 +675,9 @@ bool bad_shape(int64_t M, int K, int N) {
 
 size_t conv1x1_bn_part_floats(int64_t M, int K, int N, bool pro) {
   const Plan p = make_plan(M, K, N, pro ? 2 : 0);
-  return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
+  const size_t g = conv1x1g_pick(M, K, N, pro ? PM_BNRELU : PM_NONE)
+                       ? conv1x1g_part_floats(M, K, N, pro ? PM_BNRELU : PM_NONE) : 0;
+  return std::max(static_cast<size_t>(p.G) * p.WM * 2 * p.BN, g);
 }
 
 int bn_part_fold_slices(int R, int ntn) {
@@ -1014,42 +722,8 @@ hipError_t launch_bnbwd_sums_finalize(const float* part, int R, int BN, int N, c
 // the link + BN-backward-sums kernel runs MT = 1 tiles (at MT = 2 its epilogue operands spill)
 size_t conv1x1_link_part_floats(int64_t M, int K, int N) {
   const Plan p = make_plan(M, K, N, 0, -1, false);
-  return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
-}
-
-size_t conv3x3_bn_part_floats(int64_t M, int C, int N, bool pro) {
-  const Plan p = make_plan(M, 9 * C, N, pro ? 2 : 0, C);
-  return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
-}
-
-hipError_t launch_conv3x3_bn_fwd(const void* x, const void* w, void* y, float* part,
-                                 const float* pro_sc, const float* pro_bi, const float* shift,
-                                 int Nimg, int H, int W, int C, int N, float* mean, float* invstd,
-                                 float* rmean, float* rvar, float eps, float momentum,
-                                 hipStream_t st) {
-  const int64_t M = static_cast<int64_t>(Nimg) * H * W;
-  if (C % kBK || N % 64 || C > 2048 || N > 4096 || M < 1 || M >= (1ll << 31) || H < 1 || W < 1)
-    return hipErrorInvalidValue;
-  const bool pro = pro_sc != nullptr;
-  const int K = 9 * C;
-  const Plan p = make_plan(M, K, N, pro ? 2 : 0, C);
-  C1Args a = base_args(x, w, y, M, K, N, p);
-  a.part = part;
-  a.pro_sc = pro_sc;
-  a.pro_bi = pro_bi;
-  a.shift = shift;
-  a.H = H;
-  a.W = W;
-  a.OHW = H * W;
-  a.C = C;
-  hipError_t e;
-  if (p.WN == 4) e = launch_tap_w<4, 1>(a, p, pro, st);
-  else if (p.WN == 2) e = launch_tap_w<2, 2>(a, p, pro, st);
-  else e = launch_tap_w<1, 4>(a, p, pro, st);
-  if (e != hipSuccess || !part || !mean) return e;
-  conv1x1_bn_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N, M, shift,
-                                                          eps, momentum, mean, invstd, rmean, rvar);
-  return hipGetLastError();
+  const size_t g = conv1x1g_pick(M, K, N, PM_NONE) ? conv1x1g_part_floats(M, K, N, PM_NONE) : 0;
+  return std::max(static_cast<size_t>(p.G) * p.WM * 2 * p.BN, g);
 }
 
 hipError_t launch_conv1x1_bnbwd(const void* g, const void* z, const uint8_t* mask, const float* ca,
@@ -1083,6 +757,13 @@ hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void
     a.shift = mean;
     a.part = part;
   }
+  if (conv1x1g_pick(M, K, N, PM_NONE)) {
+    int R, BN;
+    hipError_t e = launch_conv1x1g(a, PM_NONE, sums ? SM_BNBWD : SM_OFF, true, st, &R, &BN);
+    if (e != hipSuccess || !sums) return e;
+    return launch_bnbwd_sums_finalize(part, R, BN, N, invstd, sdz, sdzx, st,
+                                      part + static_cast<size_t>(N / BN) * R * 2 * BN);
+  }
   hipError_t e = launch_bwd(a, p, sums ? 2 : 1, st);
   if (e != hipSuccess || !sums) return e;
   conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N,
@@ -1102,6 +783,10 @@ hipError_t launch_conv1x1_link_s2(const void* x, const void* w, void* y, const v
   a.lHW = H * W;
   a.lOW = (W + 1) / 2;
   a.lOHW = ((H + 1) / 2) * a.lOW;
+  if (conv1x1g_pick(M, K, N, PM_NONE)) {
+    int R, BN;
+    return launch_conv1x1g(a, PM_NONE, SM_OFF, true, st, &R, &BN);
+  }
   return launch_bwd(a, p, 1, st);
 }
 
@@ -1143,6 +828,10 @@ hipError_t launch_conv1x1_bnres(const void* x, const void* w, void* y, uint8_t* 
   a.ep_bi = ep_bi;
   a.link = reinterpret_cast<const uint16_t*>(res);
   a.ymask = ymask;
+  if (conv1x1g_pick(M, K, N, PM_BNRELU)) {
+    int R, BN;
+    return launch_conv1x1g(a, PM_BNRELU, SM_BNRES, false, st, &R, &BN);
+  }
   return launch_tail(a, p, false, st);
 }
 
@@ -1169,6 +858,13 @@ hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2
     a.shift = mean;
     a.part = part;
   }
+  if (conv1x1g_pick(M, K, N, PM_CAT)) {
+    int R, BN;
+    hipError_t e = launch_conv1x1g(a, PM_CAT, sums ? SM_BNBWD : SM_OFF, false, st, &R, &BN);
+    if (e != hipSuccess || !sums) return e;
+    return launch_bnbwd_sums_finalize(part, R, BN, N, invstd, sdz, sdzx, st,
+                                      part + static_cast<size_t>(N / BN) * R * 2 * BN);
+  }
   hipError_t e = launch_tail(a, p, true, st);
   if (e != hipSuccess || !sums) return e;
   conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N,
@@ -1178,7 +874,8 @@ hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2
 
 size_t conv1x1_cat_part_floats(int64_t M, int K, int N) {
   const Plan p = make_plan(M, K, N, 2, -1, false);
-  return static_cast<size_t>(p.G) * p.WM * 2 * p.BN;
+  const size_t g = conv1x1g_pick(M, K, N, PM_CAT) ? conv1x1g_part_floats(M, K, N, PM_CAT) : 0;
+  return std::max(static_cast<size_t>(p.G) * p.WM * 2 * p.BN, g);
 }
 
 hipError_t launch_conv1x1_cat_bnres(const void* x1, const void* x2, const float* sc_cat,
@@ -1199,6 +896,10 @@ hipError_t launch_conv1x1_cat_bnres(const void* x1, const void* x2, const float*
   a.ep_bi = ep_bi;
   a.link = reinterpret_cast<const uint16_t*>(res);
   a.ymask = ymask;
+  if (conv1x1g_pick(M, K, N, PM_CAT)) {
+    int R, BN;
+    return launch_conv1x1g(a, PM_CAT, SM_BNRES, false, st, &R, &BN);
+  }
   return launch_tail(a, p, true, st);
 }
 
@@ -1234,6 +935,13 @@ hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* p
     a.OHW = (H / 2) * (W / 2);
   }
   const bool s2 = stride == 2;
+  if (!s2 && conv1x1g_pick(M, K, N, pro ? PM_BNRELU : PM_NONE)) {
+    int R, BN;
+    hipError_t e = launch_conv1x1g(a, pro ? PM_BNRELU : PM_NONE, SM_BN, false, st, &R, &BN);
+    if (e != hipSuccess || !part || !mean) return e;
+    return launch_bn_stats_finalize(part, R, BN, N, M, shift, eps, momentum, mean, invstd, rmean,
+                                    rvar, st, part + static_cast<size_t>(N / BN) * R * 2 * BN);
+  }
   hipError_t e;
   if (p.WN == 4) e = launch_w<4, 1>(a, p, pro, s2, st);
   else if (p.WN == 2) e = launch_w<2, 2>(a, p, pro, s2, st);

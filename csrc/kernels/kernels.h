@@ -65,6 +65,12 @@ hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m,
 
 // Gossip: x <- (w0+w1+w2) x + w1*clip(left-x) + w2*clip(right-x); writes fp32 master and bf16
 // params. clip <= 0 disables clipping. ``work`` must hold gossip_workspace_bytes(D) bytes.
+// The fused 1x1-conv kernel family used by launch_conv1x1_* (conv1x1g.hip policy): 0 = the
+// register-staged conv1x1.hip kernels only, 1 = the global_load_lds kernels wherever eligible,
+// 2 = per-shape auto (default; env CML_C1G = 0 / 1 / auto).
+int conv1x1g_mode();
+void set_conv1x1g_mode(int mode);
+
 size_t gossip_workspace_bytes(int64_t D);
 // k-neighbour mix (1 <= k <= 8): x <- (w0 + sum w_k) x + sum_k w_k clip_k(nbrs[k] - x)
 hipError_t launch_gossip_mix_k(int dtype, float* master, void* param_out, const void* const* nbrs,
@@ -276,29 +282,17 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
                            const uint8_t* dz_mask = nullptr, const float* dz_a = nullptr,
                            const float* dz_b = nullptr, const float* dz_c = nullptr);
 
-// 3x3 / stride 1 / padding 1 weight gradient on the same kernel (one tap per grid z): dy [P][Co],
-// x [P][Ci] NHWC with P = Nimg H W -> dw [9][Co][Ci] (tap = 3 (dy + 1) + dx + 1), optional BN +
-// ReLU prologue on x. Co % 128 == 0 and Ci % 128 == 0, or Ci == 64 with Co == 64 or Co % 256 == 0.
-// Weight gradient of a stride-2 1x1 conv: dy [Nimg][ceil(IH/2)][ceil(IW/2)][Co], x
-// [Nimg][IH][IW][Ci] bf16; part: wgrad1x1_s2_splits() x Co x Ci floats; dw [Co][Ci].
-int wgrad1x1_s2_splits(int Nimg, int IH, int IW, int Co, int Ci);
-hipError_t launch_wgrad1x1_s2(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
-                              int Nimg, int IH, int IW, int Co, int Ci, hipStream_t st);
 // dW = sum of S fp32 partial slabs of n floats (n % 4 == 0), fixed order, bf16 or fp32 out.
 hipError_t launch_wgrad_fold(const float* part, int S, int64_t n, void* out, bool out_bf16,
                              hipStream_t st);
 // 3x3 / stride 1 / padding 1 weight gradient with all nine taps per workgroup (wgrad3x3.hip):
 // dy [B][H][W][Co], x [B][H][W][Ci] bf16, zero: >= 8 zero bf16, part: splits x Co x 9 x Ci floats,
 // dw [Co][3][3][Ci] (bf16 or fp32). Co % 64 == 0, Ci == 64 or Ci % 128 == 0; the plan also needs a
-// chunk geometry that fits LDS (false: use wgrad3x3 / the library).
+// chunk geometry that fits LDS (false: the library's weight gradient).
 bool wgrad3x3_direct_plan(int B, int H, int W, int Co, int Ci, int* splits, int* tci);
 hipError_t launch_wgrad3x3_direct(const void* dy, const void* x, const void* zero, float* part,
                                   void* dw, bool dw_bf16, int B, int H, int W, int Co, int Ci,
                                   hipStream_t st);
-void wgrad3x3_plan(int64_t P, int Co, int Ci, int* TM, int* TN, int* splits, int* cps);
-hipError_t launch_wgrad3x3(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
-                           int Nimg, int H, int W, int Co, int Ci, const float* pro_sc,
-                           const float* pro_bi, hipStream_t st);
 
 // Fused 1x1 convolution forward (conv1x1.hip): y[M][N] = f(x)[src(m)][K] W[N][K]^T on NHWC bf16,
 // f = identity or max(x * pro_sc + pro_bi, 0) per input channel (pro_sc != null), src(m) = m
@@ -311,16 +305,6 @@ hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* p
                                  int64_t M, int K, int N, int stride, int H, int W, float* mean,
                                  float* invstd, float* rmean, float* rvar, float eps,
                                  float momentum, hipStream_t st);
-
-// 3x3 / stride 1 / padding 1 convolution as an implicit GEMM in the same kernel (conv1x1.hip TAP):
-// x [Nimg][H][W][C] NHWC bf16, w [N][3][3][C] (channels_last weight), y [Nimg][H][W][N]; optional
-// BN + ReLU prologue on x (pro_sc / pro_bi [C]) and BN statistics of y (as conv1x1_bn_fwd).
-size_t conv3x3_bn_part_floats(int64_t M, int C, int N, bool pro);
-hipError_t launch_conv3x3_bn_fwd(const void* x, const void* w, void* y, float* part,
-                                 const float* pro_sc, const float* pro_bi, const float* shift,
-                                 int Nimg, int H, int W, int C, int N, float* mean, float* invstd,
-                                 float* rmean, float* rvar, float eps, float momentum,
-                                 hipStream_t st);
 
 // Implicit-GEMM NHWC conv, stride 1, 1x1 (taps 1) or 3x3 padding 1 (taps 9), global_load_lds
 // double-buffered (conv_gemm.hip): x [Nimg][H][W][C], w [N][taps][C], y [Nimg][H][W][N]; zero:

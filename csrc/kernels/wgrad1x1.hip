@@ -61,7 +61,7 @@ __device__ __forceinline__ int img_off(int row, int ch) {
 //             algebraically, ops.conv._RecomputeTailFn)
 //   DP_BNRELU dz = max(g da + db, 0)        (dy is itself the input of a BN + ReLU: Gram matrices
 //             of a BN-ReLU output that is never stored)
-// CS (runtime, cs_part non-null, non-TAP): per-split column sums of the staged dz over the pixels
+// CS (runtime, cs_part non-null): per-split column sums of the staged dz over the pixels
 // (bf16 values as multiplied), taken by the workgroups of the first ci tile.
 enum { DP_NONE = 0, DP_FULL = 1, DP_MASK = 2, DP_BNRELU = 3 };
 struct DPro {
@@ -72,23 +72,11 @@ struct DPro {
   const float* c;         //           (DP_FULL, DP_MASK)
 };
 
-// TAP: weight gradient of a 3x3 / stride 1 / padding 1 conv, one tap per blockIdx.z: x rows are
-// gathered at the tap's shifted pixel (zero in the padding, after the prologue) and the partials
-// go to part[split][tap][Co][Ci].
-struct TapGeo {
-  int H, W, HW;       // output geometry (TAP: = input)
-  int S = 1;          // 2: a stride-2 1x1 conv (downsample) instead of the 3x3 taps: x pixel of
-  int IW = 0, IHW = 0;  //    output (oh, ow) is (2 oh, 2 ow) of the IH x IW input
-};
-
-template <int TM, int TN, int KC, bool PRO, int DPRO, bool TAP = false>
+template <int TM, int TN, int KC, bool PRO, int DPRO>
 __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, float* __restrict__ part,
     int P, int Co, int Ci, int tiles_n, int cps, const float* __restrict__ pro_sc,
-    const float* __restrict__ pro_bi, DPro dp, TapGeo tg, float* __restrict__ cs_part) {
-  const int tap = TAP ? static_cast<int>(blockIdx.z) : 0;
-  const int tdy = TAP && tg.S == 1 ? tap / 3 - 1 : 0;
-  const int tdx = TAP && tg.S == 1 ? tap - 3 * (tap / 3) - 1 : 0;
+    const float* __restrict__ pro_bi, DPro dp, float* __restrict__ cs_part) {
   constexpr int kKC = KC;                              // pixels per chunk
   constexpr int NT = (TM / 64) * (TN / 64) * 64;
   constexpr int CA = TM / 8, CB = TN / 8;            // 16-B chunks per staged row
@@ -181,7 +169,6 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
   uint32_t mv[HM ? IA : 1];
   if constexpr (!HZ) zv[0] = make_uint4(0u, 0u, 0u, 0u);
   if constexpr (!HM) mv[0] = 0u;
-  uint32_t xok = ~0u;                                  // TAP: bit j = x item j inside the image
   auto fetch = [&](int c) {
 #pragma unroll
     for (int j = 0; j < IA; ++j) {
@@ -192,26 +179,10 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
         zv[j] = *reinterpret_cast<const uint4*>(dp.z + static_cast<int64_t>(p) * Co + co0 + 8 * ch);
       if constexpr (HM) mv[j] = dp.mask[static_cast<int64_t>(p) * (Co / 8) + co0 / 8 + ch];
     }
-    if constexpr (TAP) xok = 0;
 #pragma unroll
     for (int j = 0; j < IB; ++j) {
       const int e = tid + NT * j, row = e / CB, ch = e % CB;
-      int p = min(c * kKC + row, P - 1);
-      if constexpr (TAP) {
-        const int img = p / tg.HW, rem = p - img * tg.HW;
-        const int oh = rem / tg.W, ow = rem - oh * tg.W;
-        if (tg.S == 2) {   // stride-2 1x1: always inside the input
-          p = img * tg.IHW + 2 * oh * tg.IW + 2 * ow;
-          bv[j] = *reinterpret_cast<const uint4*>(x + static_cast<int64_t>(p) * Ci + ci0 + 8 * ch);
-          xok |= 1u << j;
-          continue;
-        }
-        const int ih = oh + tdy, iw = ow + tdx;
-        const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(tg.H) &&
-                        static_cast<unsigned>(iw) < static_cast<unsigned>(tg.W);
-        xok |= (ok ? 1u : 0u) << j;
-        if (ok) p = img * tg.HW + ih * tg.W + iw;
-      }
+      const int p = min(c * kKC + row, P - 1);
       bv[j] = *reinterpret_cast<const uint4*>(x + static_cast<int64_t>(p) * Ci + ci0 + 8 * ch);
     }
   };
@@ -220,7 +191,7 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
   // other stage from registers and chunk c + 2 is in flight -> one barrier per chunk
   constexpr int STG = kKC * (TM + TN) * 2;
   // (not in the 1024-thread tile: its 128 registers have no room for the sums)
-  constexpr bool CSOK = !TAP && NT <= 512;
+  constexpr bool CSOK = NT <= 512;
   const bool csum = CSOK && cs_part != nullptr && tn == 0;   // uniform per workgroup
   float cs[CSOK ? 8 : 1];
 #pragma unroll
@@ -248,7 +219,7 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     for (int j = 0; j < IB; ++j) {
       const int e = tid + NT * j, row = e / CB, ch = e % CB;
       *reinterpret_cast<uint4*>(bb + img_off<TN * 2>(row, ch)) =
-          keep_if(c * kKC + row < P && ((xok >> j) & 1u), pro(bv[j]));
+          keep_if(c * kKC + row < P, pro(bv[j]));
     }
   };
   if (c_lo < c_hi) {
@@ -300,7 +271,7 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
     }
   }
   // partial [split][Co][Ci]: lane r = ci column, register k = co row (k&3) + 8 (k>>2) + 4 h
-  float* pw = part + (static_cast<int64_t>(blockIdx.y) * gridDim.z + tap) * Co * Ci;
+  float* pw = part + static_cast<int64_t>(blockIdx.y) * Co * Ci;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -458,48 +429,33 @@ void pick_tile(int Co, int Ci, int* TM, int* TN, bool pro = false) {
 }
 }  // namespace
 
-template <int TM, int TN, bool PRO, int DPRO, bool TAP = false>
+template <int TM, int TN, bool PRO, int DPRO>
 void launch_one(dim3 grid, size_t lds, hipStream_t st, const uint16_t* dyp, const uint16_t* xp,
                 float* part, int P, int Co, int Ci, int tiles_n, int cps, const float* sc,
-                const float* bi, const DPro& dp, const TapGeo& tg = TapGeo{1, 1, 1},
+                const float* bi, const DPro& dp,
                 float* cs_part = nullptr) {
-  auto k = &wgrad1x1_kernel<TM, TN, 64, PRO, DPRO, TAP>;
+  auto k = &wgrad1x1_kernel<TM, TN, 64, PRO, DPRO>;
   if (lds > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
   k<<<grid, (TM / 64) * (TN / 64) * 64, lds, st>>>(dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi,
-                                                    dp, tg, cs_part);
+                                                    dp, cs_part);
 }
 
 template <bool PRO, int DPRO>
 bool launch_tile(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, const uint16_t* dyp,
                  const uint16_t* xp, float* part, int P, int Co, int Ci, int tiles_n, int cps,
                  const float* sc, const float* bi, const DPro& dp, float* cs_part) {
-  const TapGeo tg{1, 1, 1};
   // (no prologue variant of the 1024-thread 256 x 256 tile: it spills, and no ResNet shape needs
   // it)
   if (TM == 256 && TN == 256) {
     if constexpr (PRO || DPRO != DP_NONE) return false;
-    else launch_one<256, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
-  } else if (TM == 256 && TN == 128) launch_one<256, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
-  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
-  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
-  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
-  else if (TM == 64 && TN == 64) launch_one<64, 64, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg, cs_part);
-  else return false;
-  return true;
-}
-
-template <bool PRO>
-bool launch_tile_tap(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, const uint16_t* dyp,
-                     const uint16_t* xp, float* part, int P, int Co, int Ci, int tiles_n, int cps,
-                     const float* sc, const float* bi, const TapGeo& tg) {
-  const DPro dp{};
-  if (TM == 256 && TN == 128) launch_one<256, 128, PRO, DP_NONE, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
-  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO, DP_NONE, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
-  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO, DP_NONE, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
-  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO, DP_NONE, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
-  else if (TM == 64 && TN == 64) launch_one<64, 64, PRO, DP_NONE, true>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, tg);
+    else launch_one<256, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, cs_part);
+  } else if (TM == 256 && TN == 128) launch_one<256, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, cs_part);
+  else if (TM == 128 && TN == 256) launch_one<128, 256, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, cs_part);
+  else if (TM == 128 && TN == 128) launch_one<128, 128, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, cs_part);
+  else if (TM == 256 && TN == 64) launch_one<256, 64, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, cs_part);
+  else if (TM == 64 && TN == 64) launch_one<64, 64, PRO, DPRO>(grid, lds, st, dyp, xp, part, P, Co, Ci, tiles_n, cps, sc, bi, dp, cs_part);
   else return false;
   return true;
 }
@@ -595,98 +551,6 @@ hipError_t launch_wgrad_fold(const float* part, int S, int64_t n, void* out, boo
                              hipStream_t st) {
   if (S < 1 || n % 4) return hipErrorInvalidValue;
   fold_splits(part, S, n, out, out_bf16, st);
-  return hipGetLastError();
-}
-
-// Weight gradient of a stride-2 1x1 conv (ResNet downsample): dy [Nimg][OH][OW][Co], x
-// [Nimg][IH][IW][Ci] with OH = ceil(IH / 2), OW = ceil(IW / 2); the TAP kernel with one "tap" that
-// gathers x at (2 oh, 2 ow). Same channel counts and tiles as launch_wgrad1x1.
-hipError_t launch_wgrad1x1_s2(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
-                              int Nimg, int IH, int IW, int Co, int Ci, hipStream_t st) {
-  const int OH = (IH + 1) / 2, OW = (IW + 1) / 2;
-  const int64_t P = static_cast<int64_t>(Nimg) * OH * OW;
-  if (!(Co == 64 && Ci == 64) && (Ci == 64 ? Co % 256 != 0 : (Co % 128 || Ci % 128)))
-    return hipErrorInvalidValue;
-  if (P < 1 || static_cast<int64_t>(Nimg) * IH * IW >= (1ll << 31)) return hipErrorInvalidValue;
-  int S, cps, TM, TN;
-  wgrad1x1_plan(P, Co, Ci, &S, &cps, false);
-  pick_tile(Co, Ci, &TM, &TN, false);
-  if (TM == 256 && TN == 256) TN = 128;   // (no TAP instantiation of the 1024-thread tile)
-  const int KC = chunk_of(TM, TN);
-  const int nchunk = static_cast<int>((P + KC - 1) / KC);
-  const int tiles = (Co / TM) * (Ci / TN);
-  const int waves = (TM / 64) * (TN / 64);
-  int s = (256 * 8 / waves + tiles - 1) / tiles;
-  s = s < 1 ? 1 : (s > nchunk ? nchunk : s);
-  cps = (nchunk + s - 1) / s;
-  S = (nchunk + cps - 1) / cps;
-  const int tiles_n = Ci / TN;
-  const dim3 grid((Co / TM) * tiles_n, S, 1);
-  const size_t lds = 2 * static_cast<size_t>(KC) * (TM + TN) * 2;
-  TapGeo tg{OH, OW, OH * OW};
-  tg.S = 2;
-  tg.IW = IW;
-  tg.IHW = IH * IW;
-  if (!launch_tile_tap<false>(TM, TN, grid, lds, st, reinterpret_cast<const uint16_t*>(dy),
-                              reinterpret_cast<const uint16_t*>(x), part, static_cast<int>(P), Co,
-                              Ci, tiles_n, cps, nullptr, nullptr, tg))
-    return hipErrorInvalidValue;
-  return launch_wgrad_fold(part, S, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, st);
-}
-
-// splits of launch_wgrad1x1_s2 (its partial buffer: splits x Co x Ci floats)
-int wgrad1x1_s2_splits(int Nimg, int IH, int IW, int Co, int Ci) {
-  const int64_t P = static_cast<int64_t>(Nimg) * ((IH + 1) / 2) * ((IW + 1) / 2);
-  int TM, TN;
-  pick_tile(Co, Ci, &TM, &TN, false);
-  if (TM == 256 && TN == 256) TN = 128;
-  const int KC = chunk_of(TM, TN);
-  const int nchunk = static_cast<int>((P + KC - 1) / KC);
-  const int tiles = (Co / TM) * (Ci / TN);
-  const int waves = (TM / 64) * (TN / 64);
-  int s = (256 * 8 / waves + tiles - 1) / tiles;
-  s = s < 1 ? 1 : (s > nchunk ? nchunk : s);
-  const int cps = (nchunk + s - 1) / s;
-  return (nchunk + cps - 1) / cps;
-}
-
-// 3x3 / stride 1 / padding 1 weight gradient: dy [P][Co], x [P][Ci] (same H x W), dw [9][Co][Ci]
-// (tap-major). Tiles as the 1x1 kernel with Co x Ci; 128 x 128 tiles when Co and Ci allow (the 9
-// taps already multiply the workgroup count).
-void wgrad3x3_plan(int64_t P, int Co, int Ci, int* TM, int* TN, int* splits, int* cps) {
-  *TM = Co % 256 == 0 && Ci <= 128 ? 256 : 128;
-  *TN = Ci == 64 ? 64 : 128;
-  if (*TN == 64) *TM = Co % 256 == 0 ? 256 : 64;   // 64 x 64: one wave (ResNet layer 1, 64 -> 64)
-  const int tiles = (Co / *TM) * (Ci / *TN) * 9;
-  const int waves = (*TM / 64) * (*TN / 64);
-  const int nchunk = static_cast<int>((P + 63) / 64);
-  const int target = 256 * 8 / waves;
-  int s = (target + tiles - 1) / tiles;
-  s = s < 1 ? 1 : (s > nchunk ? nchunk : s);
-  const int c = (nchunk + s - 1) / s;
-  *cps = c;
-  *splits = (nchunk + c - 1) / c;
-}
-
-hipError_t launch_wgrad3x3(const void* dy, const void* x, float* part, void* dw, bool dw_bf16,
-                           int Nimg, int H, int W, int Co, int Ci, const float* pro_sc,
-                           const float* pro_bi, hipStream_t st) {
-  const int64_t P = static_cast<int64_t>(Nimg) * H * W;
-  if (Ci == 64 ? (Co != 64 && Co % 256) : (Co % 128 || Ci % 128)) return hipErrorInvalidValue;
-  if (P < 1 || P >= (1ll << 31)) return hipErrorInvalidValue;
-  if ((pro_sc == nullptr) != (pro_bi == nullptr)) return hipErrorInvalidValue;
-  int TM, TN, S, cps;
-  wgrad3x3_plan(P, Co, Ci, &TM, &TN, &S, &cps);
-  const int tiles_n = Ci / TN;
-  const dim3 grid((Co / TM) * tiles_n, S, 9);
-  const size_t lds = 2 * static_cast<size_t>(64) * (TM + TN) * 2;
-  const TapGeo tg{H, W, H * W};
-  const auto* dyp = reinterpret_cast<const uint16_t*>(dy);
-  const auto* xp = reinterpret_cast<const uint16_t*>(x);
-  const bool ok = pro_sc ? launch_tile_tap<true>(TM, TN, grid, lds, st, dyp, xp, part, static_cast<int>(P), Co, Ci, tiles_n, cps, pro_sc, pro_bi, tg)
-                         : launch_tile_tap<false>(TM, TN, grid, lds, st, dyp, xp, part, static_cast<int>(P), Co, Ci, tiles_n, cps, nullptr, nullptr, tg);
-  if (!ok) return hipErrorInvalidValue;
-  fold_splits(part, S, 9ll * Co * Ci, dw, dw_bf16, st);
   return hipGetLastError();
 }
 

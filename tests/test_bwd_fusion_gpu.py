@@ -7,6 +7,8 @@ import copy
 import pytest
 import torch
 
+from consensusml_amd import perf
+
 pytestmark = pytest.mark.gpu
 
 
@@ -146,7 +148,6 @@ def test_identity_chain_fused_vs_unfused(cuda, planes, H):
     backwards -- fusion on and off -- are compared with an fp32 run of the same weights: the fused
     one must be as accurate as the unfused one (BN backward amplifies bf16 rounding, so the
     absolute error level depends on the shape)."""
-    from consensusml_amd.models import resnet
     m_on = _chain(cuda, planes, 3)
     m_off = copy.deepcopy(m_on)
     m32 = copy.deepcopy(m_on).float()
@@ -156,14 +157,11 @@ def test_identity_chain_fused_vs_unfused(cuda, planes, H):
     outs = {}
     for key, m, dt in (("on", m_on, torch.bfloat16), ("off", m_off, torch.bfloat16),
                        ("fp32", m32, torch.float32)):
-        old = resnet.FUSED_BN3_BWD, resnet.FUSED_BN3_BWD_MAX_PLANES
-        resnet.FUSED_BN3_BWD, resnet.FUSED_BN3_BWD_MAX_PLANES = key == "on", 4096
-        try:
+        with perf.use_policy(perf.policy().replace(fused_bn3_bwd=key == "on",
+                                                   fused_bn3_bwd_max_planes=4096)):
             xi = x.to(dt).clone().requires_grad_(True)
             y = m(xi)
             y.backward(gy.to(dt))
-        finally:
-            resnet.FUSED_BN3_BWD, resnet.FUSED_BN3_BWD_MAX_PLANES = old
         outs[key] = (y.detach().float(), xi.grad.float(), [p.grad.float() for p in m.parameters()])
     ref = outs["fp32"]
     for k in (0, 1):
@@ -292,7 +290,6 @@ def test_bottleneck_bn1_dgrad_sums_matches_unfused(cuda):
     """A bottleneck block's gradients with bn1's backward sums from the 3x3 data gradient's
     epilogue equal those of bn_act + its own reduction pass."""
     import consensusml_amd.models.resnet as R
-    import consensusml_amd.ops.conv as C
     torch.manual_seed(5)
     blk = R.Bottleneck(256, 64).to(cuda, torch.bfloat16).to(memory_format=torch.channels_last)
     blk.train()
@@ -300,12 +297,11 @@ def test_bottleneck_bn1_dgrad_sums_matches_unfused(cuda):
     gy = _nhwc(torch.randn(4, 256, 14, 14, device=cuda).bfloat16())
     grads = {}
     for on in (True, False):
-        C.BN1_DGRAD_SUMS = on
-        b = copy.deepcopy(blk)
-        x = x0.clone().requires_grad_(True)
-        b(x).backward(gy)
+        with perf.use_policy(perf.policy().replace(bn1_dgrad_sums=on)):
+            b = copy.deepcopy(blk)
+            x = x0.clone().requires_grad_(True)
+            b(x).backward(gy)
         grads[on] = [x.grad] + [p.grad for p in b.parameters()]
-    C.BN1_DGRAD_SUMS = True
     for a, r in zip(grads[True], grads[False]):
         _close(a, r, 2e-2)
 
@@ -341,7 +337,6 @@ def test_wgrad1x1_ex_modes(cuda, Co, Ci, H):
 def test_identity_chain_recompute_tail(cuda, planes, H):
     """Three identity blocks with the recompute tail vs the stored-z3 fused tail, both against an
     fp32 run of the same weights (output, input gradient and every parameter gradient)."""
-    from consensusml_amd.models import resnet
     m_on = _chain(cuda, planes, 3, seed=1)
     m_off = copy.deepcopy(m_on)
     m32 = copy.deepcopy(m_on).float()
@@ -351,14 +346,11 @@ def test_identity_chain_recompute_tail(cuda, planes, H):
     outs = {}
     for key, m, dt in (("on", m_on, torch.bfloat16), ("off", m_off, torch.bfloat16),
                        ("fp32", m32, torch.float32)):
-        old = resnet.RECOMPUTE_TAIL, resnet.RECOMPUTE_TAIL_MAX_PLANES
-        resnet.RECOMPUTE_TAIL, resnet.RECOMPUTE_TAIL_MAX_PLANES = key == "on", 4096
-        try:
+        with perf.use_policy(perf.policy().replace(recompute_tail=key == "on",
+                                                   recompute_tail_max_planes=4096)):
             xi = x.to(dt).clone().requires_grad_(True)
             y = m(xi)
             y.backward(gy.to(dt))
-        finally:
-            resnet.RECOMPUTE_TAIL, resnet.RECOMPUTE_TAIL_MAX_PLANES = old
         outs[key] = (y.detach().float(), xi.grad.float(), [p.grad.float() for p in m.parameters()],
                      [b.float().clone() for b in m.buffers()])
     ref = outs["fp32"]
@@ -375,14 +367,11 @@ def test_identity_chain_recompute_tail(cuda, planes, H):
 @pytest.mark.parametrize("cin,planes,H,stride", [(64, 64, 28, 1), (128, 128, 14, 1),
                                                  (256, 128, 28, 2), (128, 64, 14, 2),
                                                  (512, 256, 14, 2), (1024, 512, 8, 2)])
-def test_downsample_recompute_tail(cuda, cin, planes, H, stride, monkeypatch):
+def test_downsample_recompute_tail(cuda, cin, planes, H, stride):
     """Downsample block (stride 1, or stride 2 through ops.conv.subsample2) with the recompute
     tail (no z3 / zd) vs the stored path, both against an fp32 copy: output, input gradient,
     parameter gradients, running statistics."""
-    from consensusml_amd.models import resnet
     from consensusml_amd.models.resnet import Bottleneck
-    import consensusml_amd.ops.conv as C
-    monkeypatch.setattr(C, "DOWN_TAIL_S2_MAX_CIN", 1024)
     torch.manual_seed(3)
     m_on = Bottleneck(cin, planes, stride, downsample=True)
     for mod in m_on.modules():
@@ -400,14 +389,11 @@ def test_downsample_recompute_tail(cuda, cin, planes, H, stride, monkeypatch):
     outs = {}
     for key, m, dt in (("on", m_on, torch.bfloat16), ("off", m_off, torch.bfloat16),
                        ("fp32", m32, torch.float32)):
-        old = resnet.RECOMPUTE_DOWN_TAIL
-        resnet.RECOMPUTE_DOWN_TAIL = key == "on"
-        try:
+        with perf.use_policy(perf.policy().replace(recompute_down_tail=key == "on",
+                                                   down_tail_s2_max_cin=1024)):
             xi = x.to(dt).clone().requires_grad_(True)
             y = m(xi)
             y.backward(gy.to(dt))
-        finally:
-            resnet.RECOMPUTE_DOWN_TAIL = old
         outs[key] = (y.detach().float(), xi.grad.float(), [p.grad.float() for p in m.parameters()],
                      [b.float().clone() for b in m.buffers()])
     ref = outs["fp32"]

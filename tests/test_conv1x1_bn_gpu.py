@@ -191,34 +191,6 @@ def test_resnet50_fused_conv_bn_matches_unfused(cuda):
                                        atol=2e-3)
 
 
-@pytest.mark.parametrize("N,C,Co,H", [(2, 64, 64, 9), (3, 128, 128, 7), (2, 256, 256, 5),
-                                      (1, 512, 512, 4), (2, 64, 128, 6)])
-@pytest.mark.parametrize("pro", [False, True])
-def test_conv3x3_tap_vs_fp32(cuda, N, C, Co, H, pro):
-    """3x3 / stride 1 / padding 1 implicit GEMM (conv1x1.hip TAP mode): output vs an fp32 conv of
-    the (BN + ReLU'd, bf16-rounded) input; BN statistics of the bf16 output."""
-    import torch.nn.functional as F
-    from consensusml_amd.ops.native import lib
-    g0 = torch.Generator(device=cuda).manual_seed(7)
-    x = torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16().contiguous(
-        memory_format=torch.channels_last)
-    w = (torch.randn(Co, C, 3, 3, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
-    sc = torch.rand(C, device=cuda, generator=g0) + 0.5 if pro else None
-    bi = torch.randn(C, device=cuda, generator=g0) * 0.2 if pro else None
-    rm, rv = torch.zeros(Co, device=cuda), torch.ones(Co, device=cuda)
-    y, mean, invstd = lib().conv3x3_bn_fwd(x, w, sc, bi, rm, rm, rv, True, 1e-5, 0.1)
-    xf = x.float()
-    if pro:
-        xf = torch.relu(xf * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)).bfloat16().float()
-    ref = F.conv2d(xf, w.float(), padding=1)
-    err = (y.float() - ref).norm() / ref.norm()
-    assert err < 5e-3, float(err)
-    yb = y.float()
-    torch.testing.assert_close(mean, yb.mean((0, 2, 3)), rtol=1e-3, atol=1e-3)
-    var = yb.var((0, 2, 3), unbiased=False)
-    torch.testing.assert_close(invstd, torch.rsqrt(var + 1e-5), rtol=2e-3, atol=1e-3)
-
-
 @pytest.mark.parametrize("C,Co,H", [(64, 64, 9), (128, 128, 7), (256, 256, 5), (512, 512, 4),
                                     (64, 128, 6), (128, 64, 5)])
 def test_conv_gemm_and_3x3_dgrad(cuda, C, Co, H):
@@ -299,154 +271,24 @@ def test_conv3x3_bn_stats_vs_fp32(cuda, C, Co, H, N):
                                       (64, 256, 5, 4), (64, 64, 56, 2), (128, 128, 28, 2),
                                       (256, 256, 14, 3), (512, 512, 7, 4), (64, 128, 16, 3),
                                       (128, 256, 20, 2), (256, 128, 30, 1), (128, 64, 7, 3)])
-@pytest.mark.parametrize("mode", ["direct", "tap"])
-def test_wgrad3x3_vs_fp32(cuda, C, Co, H, N, mode):
+def test_wgrad3x3_vs_fp32(cuda, C, Co, H, N):
     """3x3 weight gradient, nine taps per workgroup (wgrad3x3.hip: single-row to multi-image
-    chunks, halo rows at image edges, channel tiles) or one tap per grid z (wgrad1x1.hip TAP), vs
-    the fp32 convolution weight gradient."""
+    chunks, halo rows at image edges, channel tiles) vs the fp32 convolution weight gradient."""
     from consensusml_amd.ops.native import lib
     L = lib()
-    direct = L.wgrad3x3_direct_ok(N, H, H, Co, C)
-    if mode == "tap" and not (C == 64 and (Co == 64 or Co % 256 == 0) or
-                              (C % 128 == 0 and Co % 128 == 0)):
-        pytest.skip("channel counts of the TAP kernel")
-    if mode == "direct":
-        assert direct, (N, H, Co, C)
+    assert L.wgrad3x3_direct_ok(N, H, H, Co, C), (N, H, Co, C)
     g0 = torch.Generator(device=cuda).manual_seed(12)
     x = torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16().contiguous(
         memory_format=torch.channels_last)
     gy = torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16().contiguous(
         memory_format=torch.channels_last)
     zero = torch.zeros(64, dtype=torch.bfloat16, device=cuda)
-    dw = L.wgrad3x3(gy, x, torch.float32, None, None, zero, mode == "tap")
+    dw = L.wgrad3x3(gy, x, torch.float32, zero)
     w = torch.zeros(Co, C, 3, 3, device=cuda)
     ref = torch.ops.aten.convolution_backward(gy.float(), x.float(), w, None, [1, 1], [1, 1],
                                               [1, 1], False, [0, 0], 1, [False, True, False])[1]
     assert float((dw.float() - ref).norm() / ref.norm()) < 1e-5 * (N * H * H) ** 0.5 + 1e-4
-    dwb = L.wgrad3x3(gy, x, torch.bfloat16, None, None, zero, mode == "tap")
+    dwb = L.wgrad3x3(gy, x, torch.bfloat16, zero)
     assert dwb.dtype == torch.bfloat16
     assert float((dwb.float() - ref).norm() / ref.norm()) < 5e-3
 
-
-@pytest.mark.parametrize("C,Co,H", [(64, 64, 9), (128, 128, 6), (256, 256, 5), (64, 256, 5)])
-@pytest.mark.parametrize("pro", [False, True])
-def test_wgrad3x3_tap_vs_fp32(cuda, C, Co, H, pro):
-    """3x3 weight gradient (wgrad1x1.hip TAP mode) vs the fp32 convolution weight gradient, with
-    the optional BN + ReLU prologue on x (padding stays zero after the transform)."""
-    from consensusml_amd.ops.native import lib
-    g0 = torch.Generator(device=cuda).manual_seed(11)
-    N = 4
-    x = torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16().contiguous(
-        memory_format=torch.channels_last)
-    gy = torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16().contiguous(
-        memory_format=torch.channels_last)
-    sc = torch.rand(C, device=cuda, generator=g0) + 0.5 if pro else None
-    bi = torch.randn(C, device=cuda, generator=g0) * 0.2 if pro else None
-    dw = lib().wgrad3x3(gy, x, torch.float32, sc, bi)
-    xf = x.float()
-    if pro:
-        xf = torch.relu(xf * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)).bfloat16().float()
-    w = torch.zeros(Co, C, 3, 3, device=cuda)
-    ref = torch.ops.aten.convolution_backward(gy.float(), xf, w, None, [1, 1], [1, 1], [1, 1],
-                                              False, [0, 0], 1, [False, True, False])[1]
-    assert float((dw.float() - ref).norm() / ref.norm()) < 5e-3
-
-
-@pytest.mark.parametrize("Ci,Co,H,N", [(256, 512, 56, 2), (512, 1024, 28, 2), (1024, 2048, 14, 3),
-                                      (64, 256, 9, 3), (128, 128, 7, 5), (64, 64, 10, 2)])
-def test_wgrad1x1_s2_vs_fp32(cuda, Ci, Co, H, N):
-    """Stride-2 1x1 (downsample) weight gradient on wgrad1x1.hip vs the fp32 conv weight gradient
-    (odd input sizes included: the output is ceil(H / 2))."""
-    from consensusml_amd.ops.native import lib
-    g0 = torch.Generator(device=cuda).manual_seed(13)
-    OH = (H + 1) // 2
-    x = torch.randn(N, Ci, H, H, device=cuda, generator=g0).bfloat16().contiguous(
-        memory_format=torch.channels_last)
-    gy = torch.randn(N, Co, OH, OH, device=cuda, generator=g0).bfloat16().contiguous(
-        memory_format=torch.channels_last)
-    w = torch.zeros(Co, Ci, 1, 1, device=cuda)
-    ref = torch.ops.aten.convolution_backward(gy.float(), x.float(), w, None, [2, 2], [0, 0],
-                                              [1, 1], False, [0, 0], 1, [False, True, False])[1]
-    dw = lib().wgrad1x1_s2(gy, x, torch.float32)
-    assert dw.shape == (Co, Ci, 1, 1)
-    assert float((dw - ref).norm() / ref.norm()) < 1e-5 * (N * OH * OH) ** 0.5 + 1e-4
-    dwb = lib().wgrad1x1_s2(gy, x, torch.bfloat16)
-    assert float((dwb.float() - ref).norm() / ref.norm()) < 5e-3
-
-
-def test_downsample_s2_module_grads(cuda):
-    """Conv1x1(stride 2) in training takes the own weight gradient and matches nn.Conv2d's."""
-    from consensusml_amd.models.resnet import Conv1x1, _Conv1x1S2Fn  # noqa: F401
-    from consensusml_amd.ops import conv as fconv
-    torch.manual_seed(4)
-    old, fconv.OWN_WGRAD1X1_S2 = fconv.OWN_WGRAD1X1_S2, True
-    try:
-        _downsample_s2_module_grads(cuda)
-    finally:
-        fconv.OWN_WGRAD1X1_S2 = old
-
-
-def _downsample_s2_module_grads(cuda):
-    from consensusml_amd.models.resnet import Conv1x1
-    m = Conv1x1(512, 1024, stride=2).to(cuda, torch.bfloat16, memory_format=torch.channels_last)
-    ref = torch.nn.Conv2d(512, 1024, 1, stride=2, bias=False).to(cuda, torch.float32)
-    with torch.no_grad():
-        ref.weight.copy_(m.weight.float())
-    x = torch.randn(4, 512, 14, 14, device=cuda).bfloat16().contiguous(
-        memory_format=torch.channels_last)
-    xi = x.clone().requires_grad_(True)
-    y = m(xi)
-    assert y.grad_fn is not None and "Conv1x1S2" in type(y.grad_fn).__name__
-    gy = torch.randn_like(y)
-    y.backward(gy)
-    xr = x.float().requires_grad_(True)
-    ref(xr).backward(gy.float())
-    assert float((m.weight.grad.float() - ref.weight.grad).norm() / ref.weight.grad.norm()) < 1e-2
-    assert float((xi.grad.float() - xr.grad).norm() / xr.grad.norm()) < 1e-2
-
-
-@pytest.mark.parametrize("C,Co,H,N", [(64, 64, 9, 3), (128, 128, 56, 2), (256, 256, 28, 2),
-                                      (512, 512, 14, 3), (128, 256, 7, 5), (64, 128, 10, 4)])
-def test_conv_gemm_stride2_vs_fp32(cuda, C, Co, H, N):
-    """conv_gemm.hip with stride 2: 3x3 / padding 1 and 1x1 forward vs fp32 (odd H included), and
-    the stride-2 3x3 conv + BN statistics of ops.conv.conv3x3_s2_bn_stats (output, statistics,
-    gradients through the MIOpen backward)."""
-    import torch.nn.functional as F
-    from consensusml_amd.ops import conv as fconv
-    from consensusml_amd.ops.native import lib
-    g0 = torch.Generator(device=cuda).manual_seed(14)
-    x = torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16().contiguous(
-        memory_format=torch.channels_last)
-    w = (torch.randn(Co, C, 3, 3, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
-    y = lib().conv_gemm(x, w.permute(0, 2, 3, 1).reshape(Co, 9 * C).contiguous(), 9, None, 2)
-    ref = F.conv2d(x.float(), w.float(), padding=1, stride=2)
-    assert y.shape == ref.shape
-    assert float((y.float() - ref).norm() / ref.norm()) < 5e-3
-    y1 = lib().conv_gemm(x, w[:, :, 1, 1].contiguous(), 1, None, 2)
-    ref1 = F.conv2d(x.float(), w[:, :, 1:2, 1:2].float(), stride=2)
-    assert y1.shape == ref1.shape
-    assert float((y1.float() - ref1).norm() / ref1.norm()) < 5e-3
-    conv = torch.nn.Conv2d(C, Co, 3, stride=2, padding=1, bias=False).to(cuda, torch.bfloat16)
-    with torch.no_grad():
-        conv.weight.copy_(w)
-    bn = torch.nn.BatchNorm2d(Co).to(cuda)
-    old, fconv.OWN_CONV3X3_S2 = fconv.OWN_CONV3X3_S2, True
-    try:
-        assert fconv.conv3x3_s2_ok(x, conv)
-    finally:
-        fconv.OWN_CONV3X3_S2 = old
-    xi = x.clone().requires_grad_(True)
-    z, (mean, invstd) = fconv.conv3x3_s2_bn_stats(xi, conv, bn)
-    assert float((z.float() - ref).norm() / ref.norm()) < 5e-3
-    zb = z.float()
-    torch.testing.assert_close(mean, zb.mean((0, 2, 3)), rtol=1e-3, atol=1e-3)
-    torch.testing.assert_close(invstd, torch.rsqrt(zb.var((0, 2, 3), unbiased=False) + 1e-5),
-                               rtol=2e-3, atol=1e-3)
-    gy = torch.randn(z.shape, device=cuda, generator=g0).bfloat16().contiguous(
-        memory_format=torch.channels_last)
-    z.backward(gy)
-    xr = x.float().requires_grad_(True)
-    wr = w.float().requires_grad_(True)
-    F.conv2d(xr, wr, padding=1, stride=2).backward(gy.float())
-    assert float((xi.grad.float() - xr.grad).norm() / xr.grad.norm()) < 5e-3
-    assert float((conv.weight.grad.float() - wr.grad).norm() / wr.grad.norm()) < 1e-2

@@ -220,6 +220,28 @@ def test_gossip_mix(cuda):
         torch.testing.assert_close(xx, ref, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 7, 8])
+def test_gossip_mix_k(cuda, k):
+    """k-neighbour mixing vs the fp64 reference; k = 2 bit-identical to the ring kernel."""
+    D = 100003
+    g = torch.Generator(device=cuda).manual_seed(k)
+    x = torch.randn(D, device=cuda, generator=g)
+    nbs = [(torch.randn(D, device=cuda, generator=g) * (1 + i)).to(torch.bfloat16)
+           for i in range(k)]
+    w = [0.1 * (i + 1) for i in range(k)]
+    for clip in [0.0, 20.0]:
+        xx = x.clone()
+        p = torch.empty(D, dtype=torch.bfloat16, device=cuda)
+        K.gossip_mix_k(xx, nbs, w, 0.3, clip, param_out=p)
+        ref = R.gossip_mix_k(x, nbs, w, 0.3, clip)
+        torch.testing.assert_close(xx, ref, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(p, xx.to(torch.bfloat16))
+        if k == 2:
+            yy = x.clone()
+            K.gossip_mix(yy, nbs[0], nbs[1], 0.3, w[0], w[1], clip)
+            assert torch.equal(xx, yy)
+
+
 def test_fault_kernel(cuda):
     g = torch.randn(4096, device=cuda).to(torch.bfloat16)
     h = g.clone()
