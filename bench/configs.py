@@ -75,7 +75,7 @@ def main():
     c = dict(CONFIGS[a.config])
     if a.model:
         c["model"] = a.model
-    from consensusml_amd import TrainConfig
+    from consensusml_amd import TrainConfig, perf
     from consensusml_amd.parallel.dist import init_distributed
     from consensusml_amd.trainer.trainer import ConsensusTrainer
     from consensusml_amd.utils.tuning import configure_miopen
@@ -131,7 +131,11 @@ def main():
            "samples_per_s": round(samples / dt, 2),
            "tokens_per_s": round(samples * tr.task.samples_per_item / dt, 1),
            "ms_per_step": round(dt / a.steps * 1e3, 3), "phase_ms_per_step": phases,
-           "loss": float(loss), "data": "synthetic", "steps": a.steps, "warmup": a.warmup}
+           "loss": float(loss), "data": "synthetic", "steps": a.steps, "warmup": a.warmup,
+           "batched_workers": bool(n > info.world and tr.task.batched_workers
+                                   and perf.policy().batched_workers
+                                   and info.device.type == "cuda" and cfg.dtype == "bf16"),
+           "perf_policy": perf.policy().to_dict()}
     if info.device.type == "cuda":
         out["max_mem_gb"] = round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)
     if info.rank == 0:

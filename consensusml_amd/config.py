@@ -32,6 +32,8 @@ class AggConfig:
     m             number of workers averaged by Multi-Krum; ``None`` -> n - f
     iters, eps    Weiszfeld iterations and distance floor (geometric median)
     tau, clip_iters  radius / iterations of centered clipping
+    centered_gram Gram-space rules: second Gram pass relative to the medoid worker row, so
+                  near-duplicate workers' distances do not cancel (ops.kernels.gram)
     """
     rule: str = "mean"
     f: int = 0
@@ -42,6 +44,7 @@ class AggConfig:
     tol: float = 1e-7
     tau: float = 10.0
     clip_iters: int = 3
+    centered_gram: bool = True
 
     def validate(self, n: int) -> None:
         if self.rule not in RULES:

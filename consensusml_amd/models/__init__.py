@@ -26,6 +26,9 @@ class Task:
     make_batch: Callable[[int, torch.Generator], Tuple[torch.Tensor, torch.Tensor]]
     loss_fn: Callable[[nn.Module, Tuple[torch.Tensor, torch.Tensor]], torch.Tensor]
     samples_per_item: int = 1   # tokens/sample accounting (1 = one image / one row)
+    # no cross-sample coupling and every parameter-owning op writes per-worker gradients
+    # (ops.worker_grads): virtual workers may run as one batched forward / backward
+    batched_workers: bool = False
 
 
 def _ce(model, batch):
@@ -83,7 +86,7 @@ def build_task(cfg: ModelConfig, device: torch.device, dtype: torch.dtype = torc
             ids = torch.randint(0, V, (b, S), generator=gen, device=device)
             labels = torch.randint(0, V, (b, S), generator=gen, device=device)
             return ids, labels
-        return Task(name, model, make, _ce, samples_per_item=S)
+        return Task(name, model, make, _ce, samples_per_item=S, batched_workers=True)
     if name in ("llama3_8b", "llama_tiny"):
         model = (llama3_8b() if name == "llama3_8b" else llama_tiny()).to(device, dtype)
         V = model.c.vocab

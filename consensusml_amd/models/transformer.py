@@ -29,8 +29,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.bn import ResidualLink
-from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, fused_qkv_attention,
-                               linear, qkv_split, rope_tables, swiglu)
+from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, bert_embed,
+                               fused_qkv_attention, linear, qkv_split, rope_tables, swiglu)
 
 
 # =============================================================================== BERT
@@ -87,10 +87,7 @@ class BertMLM(nn.Module):
                     nn.init.zeros_(m.bias)
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
-        B, S = ids.shape
-        pos = torch.arange(S, device=ids.device)
-        x = self.tok(ids) + self.pos(pos)[None] + self.typ.weight[0]
-        x = self.ln(x)
+        x = self.ln(bert_embed(ids, self.tok.weight, self.pos.weight, self.typ.weight))
         for l in self.layers:
             x = l(x)
         x = self.head_ln(F.gelu(self.head(x)))

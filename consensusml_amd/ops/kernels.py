@@ -135,8 +135,10 @@ class GramWorkspace:
 
 def gram(X: torch.Tensor, rows: Optional[torch.Tensor] = None, n: Optional[int] = None,
          D: Optional[int] = None, out: Optional[torch.Tensor] = None,
-         accumulate: bool = False) -> torch.Tensor:
-    """G = X X^T in fp64 ([n, n]); MFMA kernel on GPU. ``accumulate``: out += X X^T."""
+         accumulate: bool = False, center: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """G = X X^T in fp64 ([n, n]); MFMA kernel on GPU. ``accumulate``: out += X X^T.
+    ``center`` (int32 [1] on X's device): the Gram of the rows relative to row ``center[0]``
+    (same distances, no cancellation for near-duplicate rows; see ``gram_center``)."""
     X = _as2d(X)
     n = n if n is not None else (rows.numel() if rows is not None else X.shape[0])
     D = D if D is not None else X.shape[1]
@@ -149,10 +151,14 @@ def gram(X: torch.Tensor, rows: Optional[torch.Tensor] = None, n: Optional[int] 
         if accumulate and out is None:
             raise ValueError("accumulate needs out")
         ws = GramWorkspace.get(X.device, n, D)
-        lib().gram(X, n, D, rows, ws, out, accumulate)
+        lib().gram(X, n, D, rows, ws, out, accumulate, center)
         return out
     Xr = X[rows.long()] if rows is not None else X[:n]
-    G = ref.gram(Xr[:, :D])
+    Xr = Xr[:, :D]
+    if center is not None:
+        c = min(max(int(center[0]), 0), n - 1)
+        Xr = Xr.double() - Xr[c].double()
+    G = ref.gram(Xr)
     if out is not None:
         if accumulate:
             out.add_(G)
@@ -160,6 +166,18 @@ def gram(X: torch.Tensor, rows: Optional[torch.Tensor] = None, n: Optional[int] 
             out.copy_(G)
         return out
     return G
+
+
+def gram_center(G: torch.Tensor, n: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """int32 [1]: the medoid of the finite rows of G (least summed squared distance to the
+    other finite rows; ties -> lower index), the center of a second, centered Gram pass."""
+    if out is None:
+        out = torch.zeros(1, dtype=torch.int32, device=G.device)
+    if G.is_cuda:
+        lib().gram_center(G.contiguous(), n, out)
+        return out
+    out.fill_(ref.gram_center(G[:n, :n]))
+    return out
 
 
 def robust_weights(G: torch.Tensor, rule: str, n: int, f: int = 0, m: Optional[int] = None,

@@ -72,6 +72,20 @@ def _bad_rows(G: torch.Tensor) -> torch.Tensor:
     return ~torch.isfinite(torch.diagonal(G))
 
 
+def gram_center(G: torch.Tensor) -> int:
+    """Medoid of the finite rows (csrc/kernels/gram.hip:gram_center_kernel)."""
+    d = torch.diagonal(G)
+    ok = torch.isfinite(d)
+    D = (d[:, None] + d[None, :] - 2.0 * G).clamp_min(0.0)
+    D = torch.where(ok[None, :], D, torch.zeros_like(D))
+    s = D.sum(1)
+    s = torch.where(ok & torch.isfinite(s), s, torch.full_like(s, float("inf")))
+    if not bool(torch.isfinite(s).any()):
+        return 0
+    best = float(s.min())
+    return int(torch.nonzero(s == best)[0, 0])
+
+
 def krum_scores(G: torch.Tensor, f: int) -> torch.Tensor:
     """score_i = sum of the n-f-2 smallest squared distances from i to the others."""
     n = G.shape[0]

@@ -17,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..perf import policy as _P
+from . import worker_grads as WG
 from .bn import ResidualLink
 from .native import lib
 
@@ -69,11 +70,15 @@ class _NormFn(torch.autograd.Function):
         y, _, mean, rstd = lib().norm_fwd(x, None, w, b, eps)
         ctx.save_for_backward(x, w, mean if b is not None else None, rstd)
         ctx.ln = b is not None
+        ctx.params = (w, b)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w, mean, rstd = ctx.saved_tensors
+        seg = _norm_bwd_workers(ctx, dy, None, x, w, mean, rstd)
+        if seg is not None:
+            return seg, None, None, None
         dx, dw, db = lib().norm_bwd(dy, None, x, w, mean, rstd)
         return dx, dw, (db if ctx.ln else None), None
 
@@ -88,6 +93,7 @@ class _AddNormFn(torch.autograd.Function):
         y, s, mean, rstd = lib().norm_fwd(x, r, w, b, eps)
         ctx.save_for_backward(s, w, mean if b is not None else None, rstd)
         ctx.ln = b is not None
+        ctx.params = (w, b)
         ctx.x_link = x_link
         # an unused s (post-LN BERT) must arrive as None, not as a zero-filled tensor that the
         # backward would then read
@@ -99,7 +105,11 @@ class _AddNormFn(torch.autograd.Function):
         s, w, mean, rstd = ctx.saved_tensors
         if dy is None:
             return ds, ds, None, None, None, None
-        dx, dw, db = lib().norm_bwd(dy, ds, s, w, mean, rstd)
+        seg = _norm_bwd_workers(ctx, dy, ds, s, w, mean, rstd)
+        if seg is not None:
+            dx, dw, db = seg, None, None
+        else:
+            dx, dw, db = lib().norm_bwd(dy, ds, s, w, mean, rstd)
         gx = dx
         link = ctx.x_link
         if link is not None and not link.closed and link.grad is None:
@@ -108,6 +118,28 @@ class _AddNormFn(torch.autograd.Function):
             link.grad = dx
             gx = None
         return gx, dx, dw, (db if ctx.ln else None), None, None
+
+
+def _norm_bwd_workers(ctx, dy, ds, x, w, mean, rstd) -> Optional[torch.Tensor]:
+    """Batched virtual workers (ops.worker_grads): dx, with worker v's dgamma / dbeta written to
+    row v of the engine's gradient buffer; None when no per-worker destination is active."""
+    wg = WG.current()
+    pw, pb = ctx.params
+    if wg is None or not wg.has(pw):
+        return None
+    V, D = wg.V, x.shape[-1]
+    dwv, fw = wg.out(pw)
+    dbv, fb = wg.out(pb) if ctx.ln else (None, True)
+    if fw and fb:
+        return lib().norm_bwd_seg(dy, ds, x, w, mean, rstd, V, dwv.view(V, D),
+                                  dbv.view(V, D) if dbv is not None else None)
+    tw = torch.empty(V, D, dtype=dwv.dtype, device=dwv.device)      # (second producer: add)
+    tb = torch.empty_like(tw) if ctx.ln else None
+    dx = lib().norm_bwd_seg(dy, ds, x, w, mean, rstd, V, tw, tb)
+    (dwv.view(V, D).copy_ if fw else dwv.view(V, D).add_)(tw)
+    if ctx.ln:
+        (dbv.view(V, D).copy_ if fb else dbv.view(V, D).add_)(tb)
+    return dx
 
 
 def _norm_ref(x, w, b, eps):
@@ -160,6 +192,62 @@ class LayerNorm(nn.LayerNorm):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return norm(x, self.weight, self.bias, self.eps)
+
+
+# ============================================================================ BERT embedding
+class _BertEmbedFn(torch.autograd.Function):
+    """x = tok[ids] + pos[0:S] + typ[0] (segment 0 everywhere), the same three bf16 ops as the
+    module composition. Its own backward so that batched virtual workers get per-worker
+    embedding gradients (ops.worker_grads); otherwise the dense embedding backward of each
+    table, as autograd would compute it."""
+
+    @staticmethod
+    def forward(ctx, ids, tok, pos, typ):
+        S = ids.shape[1]
+        x = F.embedding(ids, tok) + pos[:S][None] + typ[0]
+        ctx.save_for_backward(ids)
+        ctx.params = (tok, pos, typ)
+        ctx.nums = (tok.shape[0], pos.shape[0])
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        (ids,) = ctx.saved_tensors
+        tok, pos, typ = ctx.params
+        nv, npos = ctx.nums
+        B, S, D = dx.shape
+        emb_bwd = torch.ops.aten.embedding_dense_backward
+
+        def parts(d, i):
+            gt = emb_bwd(d, i, nv, -1, False)
+            gp = torch.zeros(npos, D, dtype=d.dtype, device=d.device)
+            gp[:S] = d.sum(0)
+            gy = torch.zeros(2, D, dtype=d.dtype, device=d.device)
+            gy[0] = d.sum((0, 1))
+            return gt, gp, gy
+
+        wg = WG.current()
+        if wg is not None and wg.has(tok):
+            V = wg.V
+            dv, iv = dx.view(V, B // V, S, D), ids.view(V, B // V, S)
+            for v in range(V):
+                gt, gp, gy = parts(dv[v], iv[v])
+                for p, g in ((tok, gt), (pos, gp), (typ, gy)):
+                    dst, first = wg.views[id(p)], id(p) not in wg.touched
+                    (dst[v].copy_ if first else dst[v].add_)(g)
+            for p in (tok, pos, typ):
+                wg.touched.add(id(p))
+            return None, None, None, None
+        gt, gp, gy = parts(dx, ids)
+        return None, gt, gp, gy
+
+
+def bert_embed(ids: torch.Tensor, tok: torch.Tensor, pos: torch.Tensor,
+               typ: torch.Tensor) -> torch.Tensor:
+    if _gpu_bf16(tok, pos, typ) and ids.is_cuda:
+        return _BertEmbedFn.apply(ids, tok, pos, typ)
+    S = ids.shape[1]
+    return F.embedding(ids, tok) + pos[:S][None] + typ[0]
 
 
 # ============================================================================ QKV split + RoPE
@@ -280,6 +368,7 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b, link):
         ctx.save_for_backward(x, w)
         ctx.link = link
+        ctx.params = (w, b)
         return F.linear(x, w, b)
 
     @staticmethod
@@ -295,10 +384,32 @@ class _LinearFn(torch.autograd.Function):
                 dx = (g.reshape(-1, x.shape[-1]) + dy2 @ w).view(x.shape)
             else:
                 dx = (dy2 @ w).view(x.shape)
+        wg = WG.current()
+        pw, pb = ctx.params
+        if wg is not None and (wg.has(pw) or wg.has(pb)):
+            # batched virtual workers: per-worker dW / db straight into the gradient rows
+            V, N, K = wg.V, dy2.shape[-1], x.shape[-1]
+            T = dy2.shape[0] // V
+            if ctx.needs_input_grad[1] and wg.has(pw):
+                dst, first = wg.out(pw)
+                a = dy2.view(V, T, N).transpose(1, 2)
+                bm = x.reshape(V, T, K)
+                if first:
+                    torch.bmm(a, bm, out=dst.view(V, N, K))
+                else:
+                    dst.view(V, N, K).baddbmm_(a, bm)
+            if ctx.needs_input_grad[2] and wg.has(pb):
+                dst, first = wg.out(pb)
+                if first and N % 8 == 0 and T % 32 == 0 and dy2.is_cuda:
+                    lib().colsum_seg(dy2, V, dst.view(V, N))
+                else:
+                    g = dy2.view(V, T, N).sum(1)
+                    (dst.copy_ if first else dst.add_)(g)
+            return dx, None, None, None
         if ctx.needs_input_grad[1]:
             dw = dy2.t() @ x.reshape(-1, x.shape[-1])
         if ctx.needs_input_grad[2]:
-            db = lib().colsum(dy2)
+            db = lib().colsum(dy2) if dy2.shape[-1] % 8 == 0 else dy2.sum(0)
         return dx, dw, db, None
 
 
@@ -306,7 +417,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
            link: Optional[ResidualLink] = None) -> torch.Tensor:
     """``link``: a ResidualLink on which a later-in-forward op (``add_norm(x_link=...)``) parks
     another gradient of x; this GEMM's data-gradient absorbs it (beta = 1)."""
-    if b is not None and _gpu_bf16(x, w, b) and w.shape[0] % 8 == 0:
+    wg = WG.current()
+    if _gpu_bf16(x, w, b) and ((b is not None and w.shape[0] % 8 == 0)
+                               or (wg is not None and wg.has(w))):
         return _LinearFn.apply(x, w, b, link)
     return F.linear(x, w, b)
 

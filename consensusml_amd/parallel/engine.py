@@ -29,6 +29,7 @@ robust rules can be exercised at n = 8 on a single GPU.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import numpy as np
@@ -39,6 +40,7 @@ import torch.distributed as dist
 
 from ..config import TrainConfig
 from ..ops import kernels as K
+from ..ops import worker_grads as WG
 from ..perf import policy as _P
 from ..ops.native import lib
 from .dist import DistInfo
@@ -107,6 +109,7 @@ class ConsensusEngine:
         self.scores = torch.zeros(self.n, dtype=torch.float64, device=dev)
         self.sel = torch.zeros(self.n + 1, dtype=torch.int32, device=dev)
         self.sel_counts = torch.zeros(self.n, dtype=torch.float64, device=dev)
+        self.center = torch.zeros(1, dtype=torch.int32, device=dev)   # centered-Gram row
         self.gout = None
         if self.rule == "centered_clip":
             self.gout = torch.zeros(self.state_len, dtype=torch.float32, device=dev)
@@ -190,6 +193,31 @@ class ConsensusEngine:
         if v != self.flat.grad_row:
             self._flush_row()
         self.flat.grad_row = v
+
+    @contextlib.contextmanager
+    def worker_batch(self):
+        """Batched virtual workers (ops.worker_grads): run the V micro-batches as ONE forward /
+        backward inside this context. The parameter-owning ops write worker v's gradient into
+        row v of the flat gradient buffer and hand autograd no parameter gradient, so the
+        copy-on-ready hooks stay idle; parameters no op produced a gradient for get zero rows.
+        Only valid for models without cross-sample coupling (Task.batched_workers)."""
+        fl = self.flat
+        views = fl.worker_views()
+        wg = WG.WorkerGrads(self.V, {id(p): views[i] for i, p in enumerate(fl.params)})
+        prev = WG.activate(wg)
+        try:
+            yield wg
+        finally:
+            WG.activate(prev)
+        for i, p in enumerate(fl.params):
+            if p.grad is not None:
+                raise RuntimeError(
+                    f"parameter {fl.param_names()[i]} got an autograd gradient inside "
+                    "worker_batch(): its op has no per-worker gradient path")
+            if id(p) not in wg.touched:
+                views[i].zero_()
+        self._flushed = {b.index for b in fl.buckets}
+        fl.grad_row = self.V - 1
 
     # ================================================================ parameter prefetch
     def _setup_prefetch(self) -> None:
@@ -463,6 +491,16 @@ class ConsensusEngine:
                 K.gram(X, n=self.rows_total, D=length, out=self.G, accumulate=True)
         if self.group_active and self.topo == "sharded":
             dist.all_reduce(self.G)
+        if cfg.centered_gram:
+            # second pass relative to the medoid row: exact distances for near-duplicate
+            # workers (the rules are translation invariant, so only the precision changes)
+            K.gram_center(self.G, self.rows_total, out=self.center)
+            self.G.zero_()
+            for b, X, length in cols:
+                K.gram(X, n=self.rows_total, D=length, out=self.G, accumulate=True,
+                       center=self.center)
+            if self.group_active and self.topo == "sharded":
+                dist.all_reduce(self.G)
         rule = "bulyan_select" if self.rule == "bulyan" else self.rule
         m = cfg.m if cfg.m is not None else self.n - cfg.f
         iters = cfg.clip_iters if rule == "centered_clip" else cfg.iters

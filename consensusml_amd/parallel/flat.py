@@ -135,6 +135,19 @@ class FlatModel:
             cache[row] = [self._view(g, i) for i in range(len(self.params))]
         return cache[row]
 
+    def worker_views(self) -> List[torch.Tensor]:
+        """Per-parameter [grad_rows, *shape] views spanning every gradient row (cached): the
+        destinations of batched virtual workers (ops.worker_grads)."""
+        cache = getattr(self, "_wv", None)
+        if cache is None:
+            g = self.flat_grad
+            cache = self._wv = [
+                torch.as_strided(g, (self.grad_rows,) + tuple(p.shape),
+                                 (g.stride(0),) + tuple(p.stride()),
+                                 g.storage_offset() + self.param_offset[i])
+                for i, p in enumerate(self.params)]
+        return cache
+
     def release_grads(self, row: int) -> None:
         """Switch to copy-on-ready mode: autograd owns fresh .grad tensors, hooks copy them."""
         for p in self.params:

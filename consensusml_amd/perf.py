@@ -71,6 +71,7 @@ class PerfPolicy:
     # ---------------------------------------------------------------- transformers / engine
     attn_kernel: bool = True              # MFMA attention for short sequences (BERT)
     multi_copy: bool = True               # multi-tensor HIP copy for gradient capture
+    batched_workers: bool = True          # virtual workers as one batched fwd/bwd (BERT)
 
     @classmethod
     def from_env(cls) -> "PerfPolicy":
@@ -106,6 +107,7 @@ class PerfPolicy:
             own_wgrad3x3=_env_bool("CML_WGRAD3X3", True),
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),
             multi_copy=_env_bool("CML_MULTI_COPY", True),
+            batched_workers=_env_bool("CML_BATCHED_WORKERS", True),
         )
 
     @classmethod

@@ -28,6 +28,7 @@ process group each rank runs members[rank::world] and the results are all-gather
 from __future__ import annotations
 
 import json
+import time
 import os
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -176,6 +177,15 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
     Xtr, Xte = X[train], X[test]
     ytr, yte = y[train], y[test]
     perf: Dict[str, dict] = {}
+    stage_s: Dict[str, float] = {}     # wall seconds per stage (device-synchronised)
+    clock = [time.perf_counter()]
+
+    def lap(name: str) -> None:
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        now = time.perf_counter()
+        stage_s[name] = round(now - clock[0], 3)
+        clock[0] = now
 
     # ---------------------------------------------------------------- SVM (svm4reps)
     svm_cols = [f"{n}_weights" for n, _, _ in svm_runs]
@@ -209,6 +219,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
         st.finish("svm4reps_resultslist", svm_res)
     for name, _, _ in svm_runs:
         perf[f"{name}_weights"] = svm_res[name]["test_metrics"]
+    lap("svm")
 
     # ---------------------------------------------------------------- lasso reps
     lasso_cols = [f"lasso_coef_rep{k + 1}" for k in range(lasso_reps)]
@@ -240,6 +251,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
         rep = lasso_res.get(f"rep{k + 1}")
         if rep:
             perf[f"lasso_rep{k + 1}"] = rep["test_metrics"]
+    lap("lasso")
 
     # ---------------------------------------------------------------- random forests
     rf_cols = [rf_column(n) for n in rf_trees]
@@ -271,6 +283,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
         st.finish("rf_noboost_resultslist", rf_res)
     for nt, col in zip(rf_trees, rf_cols):
         perf[col] = rf_res[f"rf{nt}.results"]["test_metrics"]
+    lap("random_forest")
 
     # ---------------------------------------------------------------- boosted trees
     xgb_cols = [f"xg{i + 1}_imp" for i in range(len(xgb_configs))]
@@ -312,6 +325,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
         st.finish("xgb_resultslist", xgb_res)
     for i, col in enumerate(xgb_cols):
         perf[col] = xgb_res[f"rep{i + 1}"]["test_metrics"]
+    lap("boosted_trees")
 
     # ---------------------------------------------------------------- consensus
     runs = list(table.runs)
@@ -325,7 +339,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
            "membership": membership_table(sets), "genes": genes,
            "train_idx": train.tolist(), "test_idx": test.tolist(),
            "resultslists": {"svm": svm_res, "lasso": lasso_res, "rf": rf_res, "xgb": xgb_res},
-           "resumed_stages": list(st.skipped)}
+           "resumed_stages": list(st.skipped), "stage_seconds": stage_s}
     if out_dir and _is_writer():
         os.makedirs(out_dir, exist_ok=True)
         ref_cols = [c for c in DE_COLUMNS if c in table.df.columns] + \
@@ -338,6 +352,7 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
         out["membership"].to_csv(os.path.join(out_dir, "membership.csv"))
         with open(os.path.join(out_dir, "summary.json"), "w") as fh:
             json.dump({"n_genes": len(genes), "runs": runs, "resumed_stages": st.skipped,
+                       "device": str(dev), "stage_seconds": stage_s,
                        "consensus_all_models": int((table.df["consensus_votes"] ==
                                                     len(valid)).sum()),
                        "intersections": {k: len(v) for k, v in out["intersections"].items()}},

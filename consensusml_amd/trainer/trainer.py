@@ -19,6 +19,7 @@ from ..config import TrainConfig
 from ..models import Task, build_task
 from ..parallel.dist import DistInfo, init_distributed
 from ..parallel.engine import ConsensusEngine
+from ..perf import policy as _P
 from ..utils.logging import JsonlLogger, PhaseTimer
 from .checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 
@@ -65,17 +66,14 @@ class ConsensusTrainer:
         e, t = self.engine, self.timer
         self.model.train()
         e.zero_grad()
+        if (e.V > 1 and self.task.batched_workers and _P().batched_workers
+                and e.device.type == "cuda" and self.cfg.dtype == "bf16"):
+            return self._batched_step()
         total = None
         for v in range(e.V):
             e.bind_worker(v)
             with t.phase("data"):
-                if self.loaders:
-                    x, yb, _ = self.loaders[v].next()
-                    if x.dim() == 4:
-                        x = x.contiguous(memory_format=torch.channels_last)
-                    batch = (x, yb)
-                else:
-                    batch = self.task.make_batch(self.cfg.batch_per_worker, self.gens[v])
+                batch = self._worker_batch(v)
             with t.phase("fwd_bwd"):
                 loss = self.task.loss_fn(self.model, batch)
                 loss.backward()
@@ -83,6 +81,32 @@ class ConsensusTrainer:
         with t.phase("exchange_aggregate_update"):
             e.step()
         return total / e.V
+
+    def _worker_batch(self, v: int):
+        if self.loaders:
+            x, yb, _ = self.loaders[v].next()
+            if x.dim() == 4:
+                x = x.contiguous(memory_format=torch.channels_last)
+            return x, yb
+        return self.task.make_batch(self.cfg.batch_per_worker, self.gens[v])
+
+    def _batched_step(self) -> torch.Tensor:
+        """Virtual workers as ONE forward / backward over the V micro-batches (same data as
+        the sequential loop: worker v's batch from its own stream), per-worker gradients written
+        to the engine's rows by the ops (ConsensusEngine.worker_batch). The loss is the mean over
+        all V micro-batches; scaling it by V gives every activation exactly worker v's own
+        gradient (equal-sized micro-batches, mean reductions)."""
+        e, t = self.engine, self.timer
+        with t.phase("data"):
+            parts = [self._worker_batch(v) for v in range(e.V)]
+            batch = tuple(torch.cat(z) for z in zip(*parts))
+        with t.phase("fwd_bwd"):
+            with e.worker_batch():
+                loss = self.task.loss_fn(self.model, batch)
+                (loss * e.V).backward()
+        with t.phase("exchange_aggregate_update"):
+            e.step()
+        return loss.detach()
 
     def fit(self, steps: Optional[int] = None, log_every: int = 10,
             resume: bool = False) -> Dict[str, object]:

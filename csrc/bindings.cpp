@@ -102,7 +102,7 @@ int64_t gram_workspace_bytes(int64_t n, int64_t D) {
 }
 
 void gram(const Tensor& X, int64_t n, int64_t D, const optional<Tensor>& rows, Tensor& work,
-          Tensor& G, bool accumulate) {
+          Tensor& G, bool accumulate, const optional<Tensor>& center) {
   check_dev(X, "X");
   TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "X must be 2-D with unit column stride");
   TORCH_CHECK(n >= 1 && n <= 64, "1 <= n <= 64 workers supported");
@@ -114,10 +114,22 @@ void gram(const Tensor& X, int64_t n, int64_t D, const optional<Tensor>& rows, T
               "gram workspace too small");
   TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kDouble && G.is_contiguous() && G.numel() >= n * n,
               "G must be a contiguous fp64 [n, n] GPU tensor");
+  const int* c = opt_ptr<const int>(center, at::kInt, "center", 1);
   const c10::DeviceGuard guard(X.device());
   CML_CHECK_HIP(cml::launch_gram(dtype_of(X), X.data_ptr(), X.stride(0), static_cast<int>(n), r, D,
                                  work.data_ptr(), G.data_ptr<double>(), accumulate ? 1 : 0,
-                                 cur_stream()));
+                                 cur_stream(), c));
+}
+
+// out (int32 [1]) = medoid of the finite rows of G (fp64 [n, n])
+void gram_center(const Tensor& G, int64_t n, Tensor& out) {
+  TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kDouble && G.is_contiguous() && G.numel() >= n * n,
+              "G must be a contiguous fp64 [n, n] GPU tensor");
+  TORCH_CHECK(n >= 1 && n <= 64, "1 <= n <= 64");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kInt && out.numel() >= 1, "out: int32 [1]");
+  const c10::DeviceGuard guard(G.device());
+  CML_CHECK_HIP(cml::launch_gram_center(G.data_ptr<double>(), static_cast<int>(n),
+                                        out.data_ptr<int>(), cur_stream()));
 }
 
 void robust_weights(const Tensor& G, int64_t rule, int64_t n, int64_t f, int64_t m, int64_t iters,
@@ -1648,17 +1660,88 @@ Tensor colsum(const Tensor& x_in) {
   return out;
 }
 
+// Per-segment column sums of x [M, N] (nseg equal row segments) into out [nseg, N] (bf16, any row
+// stride: e.g. the per-worker rows of the engine's flat gradient buffer).
+void colsum_seg(const Tensor& x_in, int64_t nseg, Tensor& out) {
+  Tensor x = x_in.contiguous();
+  check_bf16c(x, "x");
+  const int64_t N = x.size(-1);
+  const int64_t M = x.numel() / N;
+  TORCH_CHECK(out.is_cuda() && out.device() == x.device() && out.scalar_type() == at::kBFloat16 &&
+                  out.dim() == 2 && out.size(0) == nseg && out.size(1) == N && out.stride(1) == 1,
+              "colsum_seg: out must be bf16 [nseg, N] with unit column stride");
+  const c10::DeviceGuard guard(x.device());
+  Tensor work = at::empty({static_cast<int64_t>(cml::colsum_workspace_bytes(M, static_cast<int>(N)) / 4 + 1)},
+                          x.options().dtype(at::kFloat));
+  CML_CHECK_HIP(cml::launch_colsum_seg(x.data_ptr(), M, static_cast<int>(N), static_cast<int>(nseg),
+                                       out.data_ptr(), out.stride(0), work.data_ptr(), cur_stream()));
+}
+
+// Segmented norm backward: dx for all rows; dgamma / dbeta of segment z into dw_out[z] / db_out[z]
+// (bf16 [nseg, D] views with one common row stride).
+Tensor norm_bwd_seg(const Tensor& dy_in, const optional<Tensor>& dres_in, const Tensor& x,
+                    const Tensor& w, const optional<Tensor>& mean, const Tensor& rstd,
+                    int64_t nseg, Tensor& dw_out, const optional<Tensor>& db_out) {
+  check_bf16c(x, "x");
+  const int64_t D = x.size(-1);
+  const int64_t M = x.numel() / D;
+  Tensor dy = dy_in.contiguous();
+  check_bf16c(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "dy shape mismatch");
+  Tensor dres;
+  if (dres_in.has_value() && dres_in->defined()) {
+    dres = dres_in->contiguous();
+    check_bf16c(dres, "dres");
+    TORCH_CHECK(dres.sizes() == x.sizes(), "dres shape mismatch");
+  }
+  check_bf16c(w, "w");
+  const bool ln = mean.has_value() && mean->defined();
+  TORCH_CHECK(rstd.is_cuda() && rstd.scalar_type() == at::kFloat && rstd.numel() == M, "rstd: fp32 [M]");
+  if (ln) TORCH_CHECK(mean->scalar_type() == at::kFloat && mean->numel() == M, "mean: fp32 [M]");
+  TORCH_CHECK(D % 8 == 0 && D <= 4096, "norm: D % 8 == 0 and D <= 4096");
+  TORCH_CHECK(nseg >= 1 && M % nseg == 0, "norm_bwd_seg: rows must split into nseg equal segments");
+  auto chk = [&](const Tensor& o, const char* nm) {
+    TORCH_CHECK(o.is_cuda() && o.device() == x.device() && o.scalar_type() == at::kBFloat16 &&
+                    o.dim() == 2 && o.size(0) == nseg && o.size(1) == D && o.stride(1) == 1,
+                nm, ": bf16 [nseg, D] with unit column stride");
+  };
+  chk(dw_out, "dw_out");
+  void* dbp = nullptr;
+  if (ln) {
+    TORCH_CHECK(db_out.has_value() && db_out->defined(), "norm_bwd_seg: LayerNorm needs db_out");
+    chk(*db_out, "db_out");
+    TORCH_CHECK(db_out->stride(0) == dw_out.stride(0), "dw_out / db_out: one row stride");
+    dbp = db_out->data_ptr();
+  }
+  const c10::DeviceGuard guard(x.device());
+  Tensor dx = at::empty_like(x);
+  Tensor work = at::empty({static_cast<int64_t>(cml::norm_workspace_bytes_seg(M, static_cast<int>(D),
+                                                                              static_cast<int>(nseg)) / 4 + 1)},
+                          x.options().dtype(at::kFloat));
+  CML_CHECK_HIP(cml::launch_norm_bwd_seg(ln ? 1 : 0, dy.data_ptr(), dres.defined() ? dres.data_ptr() : nullptr,
+                                         x.data_ptr(), w.data_ptr(), ln ? mean->data_ptr<float>() : nullptr,
+                                         rstd.data_ptr<float>(), dx.data_ptr(), dw_out.data_ptr(), dbp,
+                                         M, static_cast<int>(D), static_cast<int>(nseg),
+                                         dw_out.stride(0), work.data_ptr(), cur_stream()));
+  return dx;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "consensusml_amd native HIP kernels for gfx950 (MI355X)";
   m.def("agg_update", &agg_update, "fused robust aggregation + optimizer update");
   m.def("gram_workspace_bytes", &gram_workspace_bytes);
-  m.def("gram", &gram, "G = X X^T (fp64) on MFMA");
+  m.def("gram", &gram, "G = X X^T (fp64) on MFMA; center: rows relative to that row",
+        py::arg("X"), py::arg("n"), py::arg("D"), py::arg("rows"), py::arg("work"), py::arg("G"),
+        py::arg("accumulate"), py::arg("center") = py::none());
+  m.def("gram_center", &gram_center, "medoid of the finite rows of a Gram matrix");
   m.def("robust_weights", &robust_weights, "robust weights from a Gram matrix");
   m.def("gossip_workspace_bytes", &gossip_workspace_bytes);
   m.def("gossip_mix", &gossip_mix, "ring gossip mixing with neighbour clipping");
   m.def("gossip_mix_k", &gossip_mix_k, "k-neighbour gossip mixing with neighbour clipping");
+  m.def("colsum_seg", &colsum_seg, "per-segment column sums into strided rows");
+  m.def("norm_bwd_seg", &norm_bwd_seg, "LayerNorm / RMSNorm backward with per-segment dgamma / dbeta");
   m.def("conv1x1g_mode", &cml::conv1x1g_mode, "fused 1x1 kernel family: 0 old, 1 glds, 2 auto");
   m.def("set_conv1x1g_mode", &cml::set_conv1x1g_mode, "select the fused 1x1 kernel family");
   m.def("fault", &fault, "Byzantine fault injection");

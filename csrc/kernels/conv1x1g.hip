@@ -241,7 +241,7 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv1x1g_kernel(C1Args a) {
     }
     f32x16 blk[2][2] = {{acc[2 * sb][0], acc[2 * sb][1]}, {acc[2 * sb + 1][0], acc[2 * sb + 1][1]}};
     epilogue<EL, SM, 2, DM>(a, blk, ss, sq, sh, simg, m0 + wm * 64, ncol0, n0, lane);
-    if constexpr (STATS) {
+    if (STATS && a.part) {   // (SM_BN without a slab: the conv only, no statistics)
       // fold the 8 lanes sharing a channel group (lane & 7): one partial row per (m-tile, wm)
       float* pp = a.part + (static_cast<int64_t>(nt) * a.mtiles * WM + mt * WM + wm) * 2 * BN;
 #pragma unroll

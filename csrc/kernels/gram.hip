@@ -17,6 +17,16 @@
 // blocks gives X X^T. Every lane loads unique bytes, so HBM bytes in flight per wave double
 // (n = 8) or more. Each lane keeps Q 16-byte loads in flight per iteration (Q = 8 for n <= 32).
 //
+// Centered Gram (center != null): every row is taken relative to worker row *center,
+// G'_ij = (x_i - x_c) . (x_j - x_c). Every quantity the Gram-space rules read is translation
+// invariant (pairwise distances; distances to an affine combination sum_j a_j x_j with
+// sum a = 1), so G' gives the same weights -- but without the cancellation of
+// d_ij = G_ii + G_jj - 2 G_ij when the workers are near-duplicates (|x_i - x_j| << |x|): the fp32
+// MFMA partials then carry ~1e-6 of |x|^2, which is all of d_ij for a tight honest cluster. The
+// difference is formed in fp32 (exact for bf16 inputs) and rounded once to the MFMA input type.
+// gram_center_kernel picks the center: the medoid (least summed squared distance to the finite
+// rows) of a first, uncentered G.
+//
 // Stage 1 writes one [P, P] fp32 partial per workgroup (fixed-order LDS reduction of its 4
 // waves, folded over column groups); stage 2 sums the partials in fp64 in block order ->
 // bitwise reproducible G. Rows >= n load a valid duplicate row and are zeroed by a select, so
@@ -81,6 +91,18 @@ template <typename T> struct GramLoad;
 template <> struct GramLoad<bf16> {
   typedef uint4 type;
   static __device__ __forceinline__ uint4 zero() { return make_uint4(0, 0, 0, 0); }
+  // a - c elementwise (fp32 difference of two bf16 values, rounded once to bf16)
+  static __device__ __forceinline__ uint4 sub(uint4 a, uint4 c) {
+    const uint32_t av[4] = {a.x, a.y, a.z, a.w}, cv[4] = {c.x, c.y, c.z, c.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float lo = __uint_as_float(av[i] << 16) - __uint_as_float(cv[i] << 16);
+      const float hi = __uint_as_float(av[i] & 0xffff0000u) - __uint_as_float(cv[i] & 0xffff0000u);
+      o[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+  }
   // guarded load of 8 elements at p[c .. c+8) with columns >= D zero
   static __device__ __forceinline__ uint4 tail(const bf16* p, int64_t c, int64_t D) {
     if (c + 8 <= D) return *reinterpret_cast<const uint4*>(p + c);
@@ -94,6 +116,9 @@ template <> struct GramLoad<bf16> {
 template <> struct GramLoad<float> {
   typedef float4 type;
   static __device__ __forceinline__ float4 zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  static __device__ __forceinline__ float4 sub(float4 a, float4 c) {
+    return make_float4(a.x - c.x, a.y - c.y, a.z - c.z, a.w - c.w);
+  }
   static __device__ __forceinline__ float4 tail(const float* p, int64_t c, int64_t D) {
     if (c + 4 <= D) return *reinterpret_cast<const float4*>(p + c);
     return make_float4(c < D ? p[c] : 0.f, c + 1 < D ? p[c + 1] : 0.f, c + 2 < D ? p[c + 2] : 0.f,
@@ -102,10 +127,12 @@ template <> struct GramLoad<float> {
 };
 
 // G = column-group packing factor (1, or 16/P2 when TT == 1 and n <= 8).
-template <typename T, int TT, int G>
+// CENTER: rows relative to row *center (see the header).
+template <typename T, int TT, int G, bool CENTER>
 __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restrict__ X, int64_t ld,
                                                               int n, const int* __restrict__ rows,
-                                                              int64_t D, float* __restrict__ part) {
+                                                              int64_t D, float* __restrict__ part,
+                                                              const int* __restrict__ center) {
   static_assert(G == 1 || TT == 1, "column-group packing is for a single row tile");
   typedef typename GramLoad<T>::type V;
   constexpr int P = 16 * TT;
@@ -134,6 +161,12 @@ __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restri
     const int rr = valid[t] ? row : (row % n);
     rowp[t] = X + static_cast<int64_t>(rows ? rows[rr] : rr) * ld + grp * GSPAN + VEC * h;
   }
+  const T* cp = nullptr;
+  if constexpr (CENTER) {
+    int c = *center;
+    c = c < 0 ? 0 : (c >= n ? n - 1 : c);
+    cp = X + static_cast<int64_t>(rows ? rows[c] : c) * ld + grp * GSPAN + VEC * h;
+  }
 
   f32x4 acc[NT];
 #pragma unroll
@@ -144,26 +177,34 @@ __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restri
   const int64_t Dmain = (D / COLS) * COLS;
 
   for (int64_t k0 = gw * COLS; k0 < Dmain; k0 += W * COLS) {
-    V u[Q][TT];
+    V u[Q][TT], cu[CENTER ? Q : 1];
 #pragma unroll
     for (int q = 0; q < Q; ++q)
 #pragma unroll
       for (int t = 0; t < TT; ++t) u[q][t] = *reinterpret_cast<const V*>(rowp[t] + k0 + STEP * q);
+    if constexpr (CENTER) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) cu[q] = *reinterpret_cast<const V*>(cp + k0 + STEP * q);
+    }
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
 #pragma unroll
-      for (int t = 0; t < TT; ++t) u[q][t] = valid[t] ? u[q][t] : GramLoad<T>::zero();
+      for (int t = 0; t < TT; ++t) {
+        if constexpr (CENTER) u[q][t] = GramLoad<T>::sub(u[q][t], cu[q]);
+        u[q][t] = valid[t] ? u[q][t] : GramLoad<T>::zero();
+      }
       gram_mfma<TT>(acc, u[q]);
     }
   }
   // Tail [Dmain, D): STEP-column chunks strided over all waves; only column group 0 loads
   // (the other groups' diagonal blocks just add zeros).
   for (int64_t k0 = Dmain + gw * STEP; k0 < D; k0 += W * STEP) {
-    V u[TT];
+    V u[TT], cu = GramLoad<T>::zero();
+    if constexpr (CENTER) cu = GramLoad<T>::tail(cp - grp * GSPAN - VEC * h, k0 + VEC * h, D);
 #pragma unroll
     for (int t = 0; t < TT; ++t) {
       const T* base = rowp[t] - grp * GSPAN - VEC * h;
-      u[t] = (valid[t] && grp == 0) ? GramLoad<T>::tail(base, k0 + VEC * h, D)
+      u[t] = (valid[t] && grp == 0) ? GramLoad<T>::sub(GramLoad<T>::tail(base, k0 + VEC * h, D), cu)
                                     : GramLoad<T>::zero();
     }
     gram_mfma<TT>(acc, u);
@@ -234,6 +275,38 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
   }
 }
 
+// Medoid of the finite rows of G (n <= 64, one wave): score_i = sum over finite rows j of
+// max(G_ii + G_jj - 2 G_ij, 0); non-finite rows / scores never win; ties -> lower index.
+__global__ __launch_bounds__(64) void gram_center_kernel(const double* __restrict__ G, int n,
+                                                         int* __restrict__ out) {
+  const int i = threadIdx.x;
+  double sc = __builtin_inf();
+  if (i < n) {
+    const double gii = G[i * n + i];
+    if (isfinite(gii)) {
+      double s = 0.0;
+      for (int j = 0; j < n; ++j) {
+        const double gjj = G[j * n + j];
+        if (!isfinite(gjj)) continue;
+        const double d = gii + gjj - 2.0 * G[i * n + j];
+        s += d > 0.0 ? d : 0.0;
+      }
+      if (isfinite(s)) sc = s;
+    }
+  }
+  int idx = i;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double s2 = __shfl_xor(sc, o, 64);
+    const int i2 = __shfl_xor(idx, o, 64);
+    if (s2 < sc || (s2 == sc && i2 < idx)) {
+      sc = s2;
+      idx = i2;
+    }
+  }
+  if (i == 0) out[0] = (idx < n && isfinite(sc)) ? idx : 0;
+}
+
 int gram_tiles(int n) { return (n + 15) / 16; }
 
 int gram_blocks(int64_t D, int cols) {
@@ -245,9 +318,12 @@ int gram_blocks(int64_t D, int cols) {
 
 template <typename T, int TT, int G>
 void launch_gram_t(const T* X, int64_t ld, int n, const int* rows, int64_t D, float* part,
-                   double* Gm, int acc, hipStream_t st) {
+                   double* Gm, int acc, const int* center, hipStream_t st) {
   const int nb = gram_blocks(D, gram_cols<T, TT, G>());
-  gram_partial_kernel<T, TT, G><<<nb, kGBlock, 0, st>>>(X, ld, n, rows, D, part);
+  if (center)
+    gram_partial_kernel<T, TT, G, true><<<nb, kGBlock, 0, st>>>(X, ld, n, rows, D, part, center);
+  else
+    gram_partial_kernel<T, TT, G, false><<<nb, kGBlock, 0, st>>>(X, ld, n, rows, D, part, nullptr);
   // (packed launches fold into the top-left block; the reduce skips elements >= n anyway)
   const int P = 16 * TT;
   gram_reduce_kernel<<<P * P, 256, 0, st>>>(part, nb, P, n, Gm, acc);
@@ -255,15 +331,15 @@ void launch_gram_t(const T* X, int64_t ld, int n, const int* rows, int64_t D, fl
 
 template <typename T>
 void launch_gram_dispatch(const T* x, int64_t ld, int n, const int* rows, int64_t D, float* part,
-                          double* G, int acc, hipStream_t st) {
-  if (n == 1) launch_gram_t<T, 1, 16>(x, ld, n, rows, D, part, G, acc, st);
-  else if (n == 2) launch_gram_t<T, 1, 8>(x, ld, n, rows, D, part, G, acc, st);
-  else if (n <= 4) launch_gram_t<T, 1, 4>(x, ld, n, rows, D, part, G, acc, st);
-  else if (n <= 8) launch_gram_t<T, 1, 2>(x, ld, n, rows, D, part, G, acc, st);
-  else if (n <= 16) launch_gram_t<T, 1, 1>(x, ld, n, rows, D, part, G, acc, st);
-  else if (n <= 32) launch_gram_t<T, 2, 1>(x, ld, n, rows, D, part, G, acc, st);
-  else if (n <= 48) launch_gram_t<T, 3, 1>(x, ld, n, rows, D, part, G, acc, st);
-  else launch_gram_t<T, 4, 1>(x, ld, n, rows, D, part, G, acc, st);
+                          double* G, int acc, const int* c, hipStream_t st) {
+  if (n == 1) launch_gram_t<T, 1, 16>(x, ld, n, rows, D, part, G, acc, c, st);
+  else if (n == 2) launch_gram_t<T, 1, 8>(x, ld, n, rows, D, part, G, acc, c, st);
+  else if (n <= 4) launch_gram_t<T, 1, 4>(x, ld, n, rows, D, part, G, acc, c, st);
+  else if (n <= 8) launch_gram_t<T, 1, 2>(x, ld, n, rows, D, part, G, acc, c, st);
+  else if (n <= 16) launch_gram_t<T, 1, 1>(x, ld, n, rows, D, part, G, acc, c, st);
+  else if (n <= 32) launch_gram_t<T, 2, 1>(x, ld, n, rows, D, part, G, acc, c, st);
+  else if (n <= 48) launch_gram_t<T, 3, 1>(x, ld, n, rows, D, part, G, acc, c, st);
+  else launch_gram_t<T, 4, 1>(x, ld, n, rows, D, part, G, acc, c, st);
 }
 }  // namespace
 
@@ -273,7 +349,8 @@ size_t gram_workspace_bytes(int n, int64_t D) {
 }
 
 hipError_t launch_gram(int dtype, const void* X, int64_t ld, int n, const int* rows, int64_t D,
-                       void* work, double* G, int accumulate, hipStream_t stream) {
+                       void* work, double* G, int accumulate, hipStream_t stream,
+                       const int* center) {
   if (n < 1 || n > 64 || D < 1) return hipErrorInvalidValue;
   const int es = dtype == DT_BF16 ? 2 : 4;
   const int vec = 16 / es;
@@ -281,10 +358,16 @@ hipError_t launch_gram(int dtype, const void* X, int64_t ld, int n, const int* r
   float* part = reinterpret_cast<float*>(work);
   if (dtype == DT_BF16)
     launch_gram_dispatch(reinterpret_cast<const bf16*>(X), ld, n, rows, D, part, G, accumulate,
-                         stream);
+                         center, stream);
   else
     launch_gram_dispatch(reinterpret_cast<const float*>(X), ld, n, rows, D, part, G, accumulate,
-                         stream);
+                         center, stream);
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_center(const double* G, int n, int* out, hipStream_t stream) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  gram_center_kernel<<<1, 64, 0, stream>>>(G, n, out);
   return hipGetLastError();
 }
 

@@ -52,8 +52,13 @@ hipError_t launch_agg_update(int dtype, int combine, int opt, const SrcArgs& src
 // Gram matrix G = X X^T (fp64, [n, n], row-major) of n <= 64 worker rows. ``work`` must hold
 // gram_workspace_bytes(n, D) bytes. accumulate != 0: G += X X^T (bucket-by-bucket Gram).
 size_t gram_workspace_bytes(int n, int64_t D);
+// center (device int, may be null): rows relative to worker row *center (centered Gram,
+// translation-invariant for every Gram-space rule, no cancellation for near-duplicate workers).
 hipError_t launch_gram(int dtype, const void* X, int64_t ld, int n, const int* rows, int64_t D,
-                       void* work, double* G, int accumulate, hipStream_t stream);
+                       void* work, double* G, int accumulate, hipStream_t stream,
+                       const int* center = nullptr);
+// out[0] = the medoid of the finite rows of G [n, n] (the centered Gram's center).
+hipError_t launch_gram_center(const double* G, int n, int* out, hipStream_t stream);
 
 // Robust weights from a Gram matrix (single workgroup). Outputs:
 //   w[n_out] fp32 (n_out = n, or n+1 for centered clipping whose last row is the previous
@@ -195,6 +200,13 @@ hipError_t launch_norm_fwd(int ln, const void* x, const void* res, const void* w
 hipError_t launch_norm_bwd(int ln, const void* dy, const void* dres, const void* x,
                            const void* w, const float* mean, const float* rstd, void* dx,
                            void* dw, void* db, int64_t M, int D, void* work, hipStream_t stream);
+// Segmented backward (batched virtual workers): the M rows are nseg equal segments; segment z's
+// dgamma / dbeta go to dw / db + z ostride (bf16). Workspace: norm_workspace_bytes_seg.
+size_t norm_workspace_bytes_seg(int64_t M, int D, int nseg);
+hipError_t launch_norm_bwd_seg(int ln, const void* dy, const void* dres, const void* x,
+                               const void* w, const float* mean, const float* rstd, void* dx,
+                               void* dw, void* db, int64_t M, int D, int nseg, int64_t ostride,
+                               void* work, hipStream_t stream);
 // qkv [B, S, (H + 2 KV) hd] -> q [B, H, S, hd], k / v [B, KV, S, hd] with interleaved-pair RoPE
 // on q / k from fp32 cos / sin [S, hd / 2] (null: no rotation); backward is the inverse.
 hipError_t launch_rope_fwd(const void* qkv, const float* cosb, const float* sinb, void* q, void* k,
@@ -238,6 +250,10 @@ hipError_t launch_lasso_step(float* v, float* beta, const float* g, const float*
 size_t colsum_workspace_bytes(int64_t M, int N);
 hipError_t launch_colsum(const void* x, int64_t M, int N, void* out, void* work,
                          hipStream_t stream);
+// Per-segment column sums (nseg equal row segments, (M / nseg) % 32 == 0): segment z -> out +
+// z ostride. Workspace: colsum_workspace_bytes(M, N).
+hipError_t launch_colsum_seg(const void* x, int64_t M, int N, int nseg, void* out,
+                             int64_t ostride, void* work, hipStream_t stream);
 
 // ResNet stem 7x7/s2/p3 convolution, C_in 3 or 4 -> 64, NHWC bf16 (stem_conv.hip).
 // Forward: z = conv(x, wpk) with wpk the packed weights [64][224] (k = (ky*8 + kx)*4 + c, zero for

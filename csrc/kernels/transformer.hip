@@ -311,6 +311,9 @@ __global__ __launch_bounds__(kTB) void norm_fwd_kernel(const bf16* __restrict__ 
 // their rows; partial rows go to part[group][2][D] for the fixed-order column fold.
 // DR: a second gradient of the normalised input (the residual stream's own gradient, see
 // ops.transformer.add_norm) is added on the way out, replacing an elementwise add pass.
+// Segments (batched virtual workers): the M rows are nseg consecutive segments of Ms rows and
+// every workgroup works inside one segment (nbs workgroups per segment), so the partial rows of
+// segment s are part[s nbs .. (s + 1) nbs) and fold to that worker's own dgamma / dbeta.
 template <int NV, int WPR, bool LN, bool DR>
 __global__ __launch_bounds__(kTB) void norm_bwd_kernel(const bf16* __restrict__ dy,
                                                       const bf16* __restrict__ dres,
@@ -318,16 +321,20 @@ __global__ __launch_bounds__(kTB) void norm_bwd_kernel(const bf16* __restrict__ 
                                                       const bf16* __restrict__ w,
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ rstd,
-                                                      bf16* __restrict__ dx, int64_t M, int D,
-                                                      float* __restrict__ part) {
+                                                      bf16* __restrict__ dx, int64_t Mtot, int D,
+                                                      float* __restrict__ part, int64_t Ms,
+                                                      int nbs) {
   __shared__ float red[2 * kWPB * 2];
   int parity = 0;
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int sub = wv % WPR;
   constexpr int kRPB = kWPB / WPR;
-  const int grp = blockIdx.x * kRPB + wv / WPR;
-  const int ngrp = gridDim.x * kRPB;
+  const int seg = blockIdx.x / nbs;
+  const int64_t r0 = static_cast<int64_t>(seg) * Ms;
+  const int64_t M = r0 + Ms < Mtot ? r0 + Ms : Mtot;          // end of this segment's rows
+  const int64_t grp = r0 + static_cast<int64_t>(blockIdx.x - seg * nbs) * kRPB + wv / WPR;
+  const int ngrp = nbs * kRPB;
   float wt[NV][8];
   row_load<NV, WPR>(w, D, sub, lane, wt);
   float aw[NV][8], ab[NV][8];
@@ -340,9 +347,9 @@ __global__ __launch_bounds__(kTB) void norm_bwd_kernel(const bf16* __restrict__ 
   // row's x / dy loads are issued before the current row's reductions
   float xv[NV][8], dv[NV][8], ev[NV][8];
   if (grp < M) {
-    row_load<NV, WPR>(x + static_cast<int64_t>(grp) * D, D, sub, lane, xv);
-    row_load<NV, WPR>(dy + static_cast<int64_t>(grp) * D, D, sub, lane, dv);
-    if constexpr (DR) row_load<NV, WPR>(dres + static_cast<int64_t>(grp) * D, D, sub, lane, ev);
+    row_load<NV, WPR>(x + grp * D, D, sub, lane, xv);
+    row_load<NV, WPR>(dy + grp * D, D, sub, lane, dv);
+    if constexpr (DR) row_load<NV, WPR>(dres + grp * D, D, sub, lane, ev);
   }
   for (int64_t r = grp; r < M; r += ngrp) {
     float xn[NV][8], dn[NV][8], en[NV][8];
@@ -427,13 +434,15 @@ __global__ __launch_bounds__(kTB) void norm_bwd_kernel(const bf16* __restrict__ 
 // 16 columns x 16 partial slices (every lane has <= ceil(np / 16) loads, 4 in flight); the 16
 // slice sums are combined through LDS in slice order. Latency, not bandwidth, bounds these folds,
 // so they are spread over D / 16 workgroups instead of one thread per column.
+// Segments (blockIdx.z): slices [z np, (z + 1) np) fold into out0 / out1 + z ostride.
 __global__ __launch_bounds__(kTB) void fold_kernel(const float* __restrict__ part, int np,
                                                   int64_t pstride, int D, bf16* __restrict__ out0,
-                                                  bf16* __restrict__ out1) {
+                                                  bf16* __restrict__ out1, int64_t ostride = 0) {
   const int cl = threadIdx.x & 15, sl = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   const int h = blockIdx.y;
-  const float* src = part + static_cast<int64_t>(h) * D + c;
+  const int64_t zs = blockIdx.z;
+  const float* src = part + zs * np * pstride + static_cast<int64_t>(h) * D + c;
   const int per = (np + 15) / 16;
   const int p0 = sl * per;
   const int p1 = p0 + per < np ? p0 + per : np;
@@ -458,7 +467,7 @@ __global__ __launch_bounds__(kTB) void fold_kernel(const float* __restrict__ par
       float t = 0.f;
 #pragma unroll
       for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
-      stbf(h == 0 ? out0 : out1, cc, t);
+      stbf((h == 0 ? out0 : out1) + zs * ostride, cc, t);
     }
   }
 }
@@ -705,9 +714,9 @@ void norm_fwd_t(bool ln, bool resid, const bf16* x, const bf16* res, const bf16*
 template <int NV, int WPR>
 void norm_bwd_t(bool ln, const bf16* dy, const bf16* dr, const bf16* x, const bf16* w,
                 const float* mean, const float* rstd, bf16* dx, int64_t M, int D, float* part,
-                int nblk, hipStream_t st) {
-  const unsigned g = static_cast<unsigned>(nblk);
-#define CML_NB(L, R) norm_bwd_kernel<NV, WPR, L, R><<<g, kTB, 0, st>>>(dy, dr, x, w, mean, rstd, dx, M, D, part)
+                int nblk, hipStream_t st, int64_t Ms, int nseg) {
+  const unsigned g = static_cast<unsigned>(nblk) * nseg;
+#define CML_NB(L, R) norm_bwd_kernel<NV, WPR, L, R><<<g, kTB, 0, st>>>(dy, dr, x, w, mean, rstd, dx, M, D, part, Ms, nblk)
   if (ln && dr) CML_NB(true, true);
   else if (ln) CML_NB(true, false);
   else if (dr) CML_NB(false, true);
@@ -740,26 +749,42 @@ hipError_t launch_norm_fwd(int ln, const void* x, const void* res, const void* w
   return hipGetLastError();
 }
 
-hipError_t launch_norm_bwd(int ln, const void* dy, const void* dres, const void* x,
-                           const void* w, const float* mean, const float* rstd, void* dx,
-                           void* dw, void* db, int64_t M, int D, void* work, hipStream_t st) {
+size_t norm_workspace_bytes_seg(int64_t M, int D, int nseg) {
   const NormGeom g = norm_geom(D);
-  if (M < 1 || D % 8 || g.nv == 0 || (ln && (!db || !mean))) return hipErrorInvalidValue;
-  const int ngrp = norm_bwd_blocks(M, g.wpr);
+  return static_cast<size_t>(nseg) * norm_bwd_blocks(M / nseg, g.wpr < 1 ? 1 : g.wpr) * 2 * D *
+         sizeof(float);
+}
+
+hipError_t launch_norm_bwd_seg(int ln, const void* dy, const void* dres, const void* x,
+                               const void* w, const float* mean, const float* rstd, void* dx,
+                               void* dw, void* db, int64_t M, int D, int nseg, int64_t ostride,
+                               void* work, hipStream_t st) {
+  const NormGeom g = norm_geom(D);
+  if (M < 1 || D % 8 || g.nv == 0 || (ln && (!db || !mean)) || nseg < 1 || M % nseg ||
+      nseg > 65535)
+    return hipErrorInvalidValue;
+  const int64_t Ms = M / nseg;
+  const int ngrp = norm_bwd_blocks(Ms, g.wpr);
   auto* part = reinterpret_cast<float*>(work);
   auto* dyb = reinterpret_cast<const bf16*>(dy);
   auto* drb = reinterpret_cast<const bf16*>(dres);
   auto* xb = reinterpret_cast<const bf16*>(x);
   auto* wb = reinterpret_cast<const bf16*>(w);
   auto* dxb = reinterpret_cast<bf16*>(dx);
-  if (g.wpr == 1 && g.nv == 1) norm_bwd_t<1, 1>(ln, dyb, drb, xb, wb, mean, rstd, dxb, M, D, part, ngrp, st);
-  else if (g.wpr == 1) norm_bwd_t<2, 1>(ln, dyb, drb, xb, wb, mean, rstd, dxb, M, D, part, ngrp, st);
-  else if (g.nv == 1) norm_bwd_t<1, 4>(ln, dyb, drb, xb, wb, mean, rstd, dxb, M, D, part, ngrp, st);
-  else norm_bwd_t<2, 4>(ln, dyb, drb, xb, wb, mean, rstd, dxb, M, D, part, ngrp, st);
-  fold_kernel<<<dim3((D + 15) / 16, ln ? 2 : 1), kTB, 0, st>>>(part, ngrp, 2 * static_cast<int64_t>(D),
-                                                               D, reinterpret_cast<bf16*>(dw),
-                                                               reinterpret_cast<bf16*>(db));
+  if (g.wpr == 1 && g.nv == 1) norm_bwd_t<1, 1>(ln, dyb, drb, xb, wb, mean, rstd, dxb, M, D, part, ngrp, st, Ms, nseg);
+  else if (g.wpr == 1) norm_bwd_t<2, 1>(ln, dyb, drb, xb, wb, mean, rstd, dxb, M, D, part, ngrp, st, Ms, nseg);
+  else if (g.nv == 1) norm_bwd_t<1, 4>(ln, dyb, drb, xb, wb, mean, rstd, dxb, M, D, part, ngrp, st, Ms, nseg);
+  else norm_bwd_t<2, 4>(ln, dyb, drb, xb, wb, mean, rstd, dxb, M, D, part, ngrp, st, Ms, nseg);
+  fold_kernel<<<dim3((D + 15) / 16, ln ? 2 : 1, nseg), kTB, 0, st>>>(
+      part, ngrp, 2 * static_cast<int64_t>(D), D, reinterpret_cast<bf16*>(dw),
+      reinterpret_cast<bf16*>(db), ostride);
   return hipGetLastError();
+}
+
+hipError_t launch_norm_bwd(int ln, const void* dy, const void* dres, const void* x,
+                           const void* w, const float* mean, const float* rstd, void* dx,
+                           void* dw, void* db, int64_t M, int D, void* work, hipStream_t st) {
+  return launch_norm_bwd_seg(ln, dy, dres, x, w, mean, rstd, dx, dw, db, M, D, 1, 0, work, st);
 }
 
 hipError_t launch_rope_fwd(const void* qkv, const float* cosb, const float* sinb, void* q, void* k,
@@ -802,6 +827,24 @@ hipError_t launch_swiglu_bwd(const void* dy, const void* h, void* dh, int64_t M,
 
 size_t colsum_workspace_bytes(int64_t M, int N) {
   return static_cast<size_t>((M + kCSRows - 1) / kCSRows) * N * sizeof(float);
+}
+
+// Column sums of nseg row segments of M / nseg rows each (segment z -> out + z ostride); the
+// 32-row slices never straddle segments when M / nseg is a multiple of 32 (else -> invalid).
+hipError_t launch_colsum_seg(const void* x, int64_t M, int N, int nseg, void* out,
+                             int64_t ostride, void* work, hipStream_t st) {
+  if (M < 1 || N < 8 || N % 8 || (reinterpret_cast<uintptr_t>(x) & 15) || nseg < 1 ||
+      M % nseg || (M / nseg) % kCSRows || nseg > 65535)
+    return hipErrorInvalidValue;
+  const int64_t slices = (M + kCSRows - 1) / kCSRows;
+  if (slices > 65535) return hipErrorInvalidValue;
+  dim3 grid((N / 8 + kWave - 1) / kWave, static_cast<unsigned>(slices));
+  colsum_partial_kernel<<<grid, kTB, 0, st>>>(reinterpret_cast<const bf16*>(x), M, N,
+                                              reinterpret_cast<float*>(work));
+  fold_kernel<<<dim3((N + 15) / 16, 1, nseg), kTB, 0, st>>>(
+      reinterpret_cast<const float*>(work), static_cast<int>(slices / nseg), N, N,
+      reinterpret_cast<bf16*>(out), nullptr, ostride);
+  return hipGetLastError();
 }
 
 hipError_t launch_colsum(const void* x, int64_t M, int N, void* out, void* work, hipStream_t st) {

@@ -67,10 +67,13 @@ def test_bn_fwd_and_stats_only(cuda, pro, N, K, Co, H):
         r1, r2 = rm.clone(), rv.clone()
         y, m, i = L.conv1x1_bn_fwd(x, w, sc, bi, r1, r1, r2, 1, True, 1e-5, 0.1)
         m2, i2 = L.conv1x1_bn_stats_only(x, w, sc, bi, rm.clone(), None, None, 1e-5, 0.1)
-        return y, m, i, r1, r2, m2, i2
+        y0, m0, _ = L.conv1x1_bn_fwd(x, w, sc, bi, None, None, None, 1, False, 1e-5, 0.1)
+        assert m0 is None
+        return y, m, i, r1, r2, m2, i2, y0
 
     a, b = _both(run)
-    assert torch.equal(a[0], b[0])
+    assert torch.equal(a[0], b[0]) and torch.equal(a[7], b[7]) and torch.equal(b[0], b[7])
+    a, b = a[:7], b[:7]
     for u, v in zip(a[1:], b[1:]):
         torch.testing.assert_close(u, v, rtol=2e-5, atol=1e-6)
     xin = _rows(x)

@@ -1,0 +1,117 @@
+"""Krum / Multi-Krum / geometric-median selection among NEAR-DUPLICATE workers against fp64 direct
+pairwise distances.
+
+Gram-space rules read d_ij = G_ii + G_jj - 2 G_ij. For workers that differ by a few percent of their
+norm, d_ij is ~1e-3 of G_ii, and the fp32 MFMA partials of the Gram kernel carry ~1e-6 of G_ii:
+the distances keep only ~3 digits and Krum scores whose true gaps are ~1e-3 can reorder. The
+engine therefore runs a second, centered Gram pass (rows relative to the medoid worker,
+``ops.kernels.gram(center=...)``): every rule is translation invariant and the centered entries
+are of the size of the distances themselves. The test builds a tight honest cluster with slightly
+graded spreads (a unique fp64 Krum winner with a ~1 % margin) plus outliers and checks the centered
+path's selection / distances against fp64 distances computed directly from the bf16 rows."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _direct_sqdist(X: torch.Tensor) -> torch.Tensor:
+    Xd = X.double()
+    n = Xd.shape[0]
+    D = torch.zeros(n, n, dtype=torch.float64, device=X.device)
+    for i in range(n):
+        D[i] = (Xd - Xd[i]).pow(2).sum(1)
+    return D
+
+
+def _krum_from_dist(D: torch.Tensor, f: int, m: int):
+    n = D.shape[0]
+    k = n - f - 2
+    s = torch.stack([torch.cat([D[i, :i], D[i, i + 1:]]).sort().values[:k].sum() for i in range(n)])
+    order = sorted(range(n), key=lambda i: (float(s[i]), i))
+    return s, order[:m]
+
+
+def _workers(n_honest: int, byz: int, Dim: int, sigma: float, seed: int, dev):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    base = torch.randn(Dim, device=dev, generator=g)
+    rows = []
+    for i in range(n_honest):
+        s = sigma * (1.0 + 0.02 * ((i * 5) % n_honest))   # graded spreads: unique winner
+        rows.append(base + s * torch.randn(Dim, device=dev, generator=g))
+    for j in range(byz):
+        rows.append(base + 20 * sigma * torch.randn(Dim, device=dev, generator=g))
+    return torch.stack(rows).bfloat16().contiguous()
+
+
+@pytest.mark.parametrize("sigma", [0.03, 0.01])
+@pytest.mark.parametrize("n_honest,byz,Dim", [(6, 2, 1 << 21), (14, 2, 1 << 20), (30, 4, 1 << 18)])
+def test_near_duplicate_krum_selection(cuda, sigma, n_honest, byz, Dim):
+    from consensusml_amd.ops import kernels as K
+    X = _workers(n_honest, byz, Dim, sigma, 11 + n_honest, cuda)
+    n, f = X.shape[0], byz
+    Dref = _direct_sqdist(X)
+    s_ref, sel_ref = _krum_from_dist(Dref, f, 1)
+    _, msel_ref = _krum_from_dist(Dref, f, n - f)
+
+    G0 = K.gram(X)
+    c = K.gram_center(G0, n)
+    assert int(c) < n_honest, "the medoid of a cluster + outliers is a cluster row"
+    G = K.gram(X, center=c)
+    d = torch.diagonal(G)
+    Dc = (d[:, None] + d[None, :] - 2 * G).clamp_min(0)
+    off = ~torch.eye(n, dtype=torch.bool, device=cuda)
+    rel = ((Dc - Dref).abs()[off] / Dref[off]).max()
+    assert float(rel) < 2e-4, float(rel)
+
+    scores = torch.zeros(n, dtype=torch.float64, device=cuda)
+    sel = torch.zeros(n + 1, dtype=torch.int32, device=cuda)
+    w = K.robust_weights(G, "krum", n, f=f, scores=scores, sel=sel)
+    assert int(w.argmax()) == sel_ref[0]
+    torch.testing.assert_close(scores, s_ref, rtol=2e-4, atol=0)
+    wm = K.robust_weights(G, "multi_krum", n, f=f, m=n - f)
+    assert sorted(torch.nonzero(wm > 0).flatten().tolist()) == sorted(msel_ref)
+
+    # uncentered distances for the record: their error is what the centered pass removes
+    d0 = torch.diagonal(G0)
+    D0 = (d0[:, None] + d0[None, :] - 2 * G0).clamp_min(0)
+    rel0 = float(((D0 - Dref).abs()[off] / Dref[off]).max())
+    print(f"n={n} sigma={sigma} D={Dim}: max rel distance error centered {float(rel):.2e} "
+          f"uncentered {rel0:.2e}")
+
+
+def test_near_duplicate_geomed_weights(cuda):
+    from consensusml_amd.ops import kernels as K
+    from consensusml_amd.ops import reference as R
+    X = _workers(10, 2, 1 << 20, 0.02, 3, cuda)
+    n = X.shape[0]
+    # fp64 reference Gram from centered fp64 rows (exact distances), CPU Weiszfeld
+    Xd = X.double()
+    Gref = ((Xd - Xd[0]) @ (Xd - Xd[0]).t()).cpu()
+    w_ref = R.weiszfeld_weights(Gref, iters=8, eps=1e-6, tol=0.0)
+    G = K.gram(X, center=K.gram_center(K.gram(X), n))
+    w = K.robust_weights(G, "geomed", n, iters=8, eps=1e-6, tol=0.0)
+    torch.testing.assert_close(w.double().cpu(), w_ref, rtol=1e-3, atol=1e-6)
+
+
+def test_engine_centered_gram_matches_direct_krum(cuda):
+    """The engine path (virtual workers, sharded topology, one GPU) selects the fp64 winner."""
+    from consensusml_amd import TrainConfig
+    from consensusml_amd.parallel.dist import DistInfo
+    from consensusml_amd.parallel.engine import ConsensusEngine
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(1024, 1024, bias=False)).to(cuda, torch.bfloat16)
+    cfg = TrainConfig()
+    cfg.virtual_workers = 8
+    cfg.agg.rule = "krum"
+    cfg.agg.f = 2
+    cfg.topology.kind = "sharded"
+    cfg.optim.lr = 0.0
+    e = ConsensusEngine(model, cfg, DistInfo(0, 1, 0, cuda, "none"))
+    X = _workers(6, 2, e.flat.total, 0.02, 9, cuda)
+    e.zero_grad()
+    e.flat.flat_grad.copy_(X)
+    e._flushed = {b.index for b in e.flat.buckets}
+    e.step()
+    _, sel_ref = _krum_from_dist(_direct_sqdist(X), 2, 1)
+    assert int(e.w[:8].argmax()) == sel_ref[0]

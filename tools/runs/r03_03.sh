@@ -17,3 +17,11 @@ timeout -k 10 300 python -u bench.py --no-baseline --virtual-workers 0 --b256-ba
 grep '^{' $O/r03_03_bench_auto.log | cut -c1-300
 CML_C1G=0 timeout -k 10 300 python -u bench.py --no-baseline --virtual-workers 0 --b256-batch 0 > $O/r03_03_bench_old.log 2>&1 || { tail -20 $O/r03_03_bench_old.log; exit 1; }
 grep '^{' $O/r03_03_bench_old.log | cut -c1-300
+timeout -k 10 300 $T tests/test_batched_workers_gpu.py > $O/r03_03_batched.log 2>&1 || { tail -40 $O/r03_03_batched.log; exit 1; }
+tail -3 $O/r03_03_batched.log
+timeout -k 10 300 python -u bench/configs.py --config bert_geomed --virtual-workers 8 --batch 32 --steps 10 --warmup 3 > $O/r03_03_bert_b.log 2>&1 || { tail -20 $O/r03_03_bert_b.log; exit 1; }
+grep '^{' $O/r03_03_bert_b.log | cut -c1-600
+CML_BATCHED_WORKERS=0 timeout -k 10 300 python -u bench/configs.py --config bert_geomed --virtual-workers 8 --batch 32 --steps 10 --warmup 3 > $O/r03_03_bert_s.log 2>&1 || { tail -20 $O/r03_03_bert_s.log; exit 1; }
+grep '^{' $O/r03_03_bert_s.log | cut -c1-600
+timeout -k 10 300 $T -s tests/test_gram_precision_gpu.py > $O/r03_03_gramprec.log 2>&1 || { tail -40 $O/r03_03_gramprec.log; exit 1; }
+grep "rel distance\|passed\|failed" $O/r03_03_gramprec.log
