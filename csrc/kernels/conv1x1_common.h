@@ -89,12 +89,16 @@ __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
 // DM (SM_BNBWD without a stored mask, PM_CAT data gradients of the recompute tails): the ReLU bit
 // is recomputed from the BN input, sz * ep_sc + ep_bi > 0 (the BN's own affine, as its forward
 // prologue applied it), so the BN + ReLU backward that follows needs no reduction pass of its own.
+// mhi: global row of block rows 32..63 (default m0 + 32; the quad-phase kernel's waves own two
+// separate 32-row groups).
 template <bool EL, int SM, int MT, bool DM = false>
 __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], float (&ss)[8],
                                          float (&sq)[8], const float (&sh)[8], char* simg, int m0,
-                                         int ncol0, int n0, int lane) {
+                                         int ncol0, int n0, int lane, int mhi = -1) {
   const int h = lane >> 5, r32 = lane & 31;
   const int c = lane & 7;
+  const int mh = mhi < 0 ? m0 + 32 : mhi;
+  auto grow = [&](int p) { return p < 32 ? m0 + p : mh + (p - 32); };
   // EL / SM_BNBWD operands of the read-back rows are issued as one batch before they are needed
   // (a 1-2 k-step GEMM was otherwise bound by these dependent loads, one latency per row pair):
   // all 8 rows at once with one operand (EL), in batches of 4 with two, halved again at MT = 2
@@ -123,7 +127,8 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
 #pragma unroll
     for (int k = 0; k < RB; ++k) {
       const int p = 8 * (k0 + k) + (lane >> 3);
-      const int64_t row = m0 + p < a.M ? m0 + p : a.M - 1;
+      const int gp = grow(p);
+      const int64_t row = gp < a.M ? gp : a.M - 1;
       const int64_t e0 = row * a.N + n0 + ncol0 + 8 * c;
       if constexpr (EL) {
         if (a.link_s2) {   // compact stride-2 gradient: only the even pixels get an addend
@@ -170,8 +175,9 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
   auto row = [&](int k, const uint4& l, uint32_t lb, const uint4& z, uint32_t zb) {
     const int p = 8 * k + (lane >> 3);
     uint4 v = *reinterpret_cast<const uint4*>(simg + swz(p, c));
-    if (m0 + p >= a.M) return;
-    const int64_t e0 = static_cast<int64_t>(m0 + p) * a.N + n0 + ncol0 + 8 * c;
+    const int gp = grow(p);
+    if (gp >= a.M) return;
+    const int64_t e0 = static_cast<int64_t>(gp) * a.N + n0 + ncol0 + 8 * c;
     if constexpr (EL) {
       const uint32_t l4[4] = {l.x, l.y, l.z, l.w};
       uint32_t w4[4] = {v.x, v.y, v.z, v.w};

@@ -263,6 +263,290 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv1x1g_kernel(C1Args a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Quad-phase ping-pong kernel (conv1x1q): 256 x 256 tiles for the compute-bound shapes (large K).
+//
+// The 2-buffer kernel above waits vmcnt(0) + barrier every k-step, so each step's DMA has one
+// step of MFMA work to land in and every step ends in a drain. Here the 64-deep k-step of a tile
+// is split into four 16 KB "units" -- x rows 0-127 (X0), x rows 128-255 (X1), W rows 0-127 (W0)
+// and W rows 128-255 (W1) -- with two slots each (k-step parity, 128 KB). Each k-step runs four
+// phases; in each phase a wave multiplies one quadrant of its 64 (m) x 128 (n) output (32 pixels
+// x 64 channels: its rows in x half mh, its channels in W half nh) over K = 64:
+//
+//   phase  quadrant   LDS reads (fragments)      DMA issued   wait        prologue (in LDS)
+//     0    X0 x W0    X0 -> xf, W0 -> wc (kept)  X1(s+1)      -           X1(s)
+//     1    X0 x W1    W1 -> wf                   W0(s+2)      -           -
+//     2    X1 x W1    X1 -> xf                   X0(s+2)      X0(s+1)     -
+//     3    X1 x W0    -                          W1(s+2)      X1(s+1)     X0(s+1)
+//
+// (the transforms sit in the phases with the fewest live fragment registers: the accumulators
+// are 128 of the 256 registers a wave has at two waves per SIMD)
+// so one unit is re-staged per phase, each into the slot its previous tile-step left one phase
+// earlier, and 4 units (64 KB) stay in flight across barriers (counted vmcnt, raw s_barrier;
+// a __syncthreads would drain the DMA queue). The prologue (f) is applied once per x unit, in
+// place in LDS, by all threads, one phase after the wait that retired the unit's DMA and one
+// phase before its first fragment read.
+//
+// Ping-pong: waves 4-7 (wn = 1) start one barrier late, so on every SIMD one wave multiplies while
+// its partner reads fragments, issues DMA, transforms and waits. Each phase has two barriers: A
+// (end of the load segment, after lgkmcnt(0): every ds_read / transform write of it has returned)
+// and B (end of the MFMA segment). With the one-barrier stagger, a unit waited in phase p is
+// visible to both groups from phase p + 1, and a slot whose last reads were in phase p may be
+// re-staged from phase p + 1.
+//
+// Same products in the same k order and the same prologue arithmetic as conv1x1.hip: outputs are
+// bit-identical to both other kernel families. Partial statistics rows per (m-tile, wave m-row)
+// as in conv1x1g_kernel (same finalize).
+template <int PM, int SM, bool EL>
+__global__ __launch_bounds__(512, 1) void conv1x1q_kernel(C1Args a) {
+  constexpr int NT = 512, WM = 4, BM = 256, BN = 256;
+  constexpr bool CAT = PM == PM_CAT, PRO = PM != PM_NONE;
+  constexpr int UB = 128 * 128;                   // one unit: 128 rows x 128 B
+  constexpr int GX = CAT ? 3 : 2;                 // DMA instructions per thread of an x unit
+  constexpr int VQ = 4 + 2 * GX;                  // ... of the 4 units issued after a waited one
+  constexpr int MKB = 2048;                       // CAT mask bytes per x slot (two copies)
+  constexpr int SMASK = 8 * UB, SAFF = SMASK + (CAT ? 4 * MKB : 0);
+  constexpr bool DM = CAT && SM == SM_BNBWD;
+  constexpr bool STATS = SM == SM_BN || SM == SM_BNBWD;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* s_aff = reinterpret_cast<float*>(smem + SAFF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 3, wn = wave >> 2;        // wn: the ping-pong group
+  const int h = lane >> 5, r32 = lane & 31;
+  const int G = a.ntn * a.mtiles, b = blockIdx.x, xcd = b & 7, q8 = G >> 3, r8 = G & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int mt = t / a.ntn, nt = t - mt * a.ntn;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int K = a.K, KT = K / kBK;
+  const int K1 = CAT ? a.K1 : K;
+
+  if constexpr (PRO) {
+    for (int k = tid; k < K; k += NT) {
+      s_aff[k] = a.pro_sc[k];
+      s_aff[K + k] = a.pro_bi[k];
+    }
+  }
+  // staged rows of this thread in every unit: wave * 16 + 8 i + lane / 8 (i = 0, 1), 16-B chunk
+  // lane & 7 of the row (source address inverse-swizzled: the DMA writes lane-linear)
+  const int p = lane & 7, lrow = lane >> 3;
+  // (addresses: a block-uniform base plus a 32-bit per-lane element offset, so the loop keeps
+  // one register per DMA row instead of a 64-bit pointer per row and source)
+  int xr[2][2];   // x row relative to m0 (clamped to M - 1: rows past M load a valid row)
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = m0 + 128 * u + wave * 16 + 8 * i + lrow;
+      xr[u][i] = (m < a.M ? m : a.M - 1) - m0;
+    }
+  int mrow[2] = {0, 0};
+  if constexpr (CAT) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int m = m0 + 128 * u + wm * 32 + (lane >> 1);
+      mrow[u] = (m < a.M ? m : a.M - 1) - m0;
+    }
+  }
+  auto slot = [&](int u, int s) { return smem + (((s & 1) << 2) + u) * UB; };
+  auto mslot = [&](int u, int s) { return smem + SMASK + (((s & 1) << 1) + u) * MKB; };
+
+  // unit u (0 X0, 1 X1, 2 W0, 3 W1) of k-step s: 2 DMA instructions per thread (+1 mask, CAT x)
+  auto issue = [&](int u, int s) {
+    char* base = slot(u, s);
+    const int k0 = s * kBK;
+    if (u < 2) {
+      const bool first = !CAT || k0 < K1;
+      const int ld = first ? K1 : K - K1;
+      const uint16_t* xb = first ? a.x + static_cast<int64_t>(m0) * K1 + k0
+                                 : a.x2 + static_cast<int64_t>(m0) * (K - K1) + (k0 - K1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = p ^ ((4 * i + (lrow >> 1)) & 7);   // (row >> 1) & 7 of row wave*16+8i+lrow
+        __builtin_amdgcn_global_load_lds((g_void*)(xb + (xr[u][i] * ld + 8 * c)),
+                                         (lds_void*)(base + (wave * 16 + 8 * i) * 128), 16, 0, 0);
+      }
+      if constexpr (CAT) {
+        // 8 mask bytes per row at [row][8]; waves 4-7 load a second copy (every wave issues the
+        // same DMA count). Second-source steps and cat_bnrelu: a dummy read, never used.
+        const uint8_t* mb = a.cat_bnrelu ? reinterpret_cast<const uint8_t*>(a.x)
+                                         : a.xm + static_cast<int64_t>(m0) * (K1 / 8) +
+                                               (first ? k0 / 8 : 0);
+        const int mo = a.cat_bnrelu ? 0 : mrow[u] * (K1 / 8) + 4 * (lane & 1);
+        __builtin_amdgcn_global_load_lds((g_void*)(mb + mo), (lds_void*)(mslot(u, s) + wave * 256),
+                                         4, 0, 0);
+      }
+    } else {
+      const uint16_t* wb = a.w + static_cast<int64_t>(n0 + 128 * (u - 2)) * K + k0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = p ^ ((4 * i + (lrow >> 1)) & 7);
+        __builtin_amdgcn_global_load_lds((g_void*)(wb + ((wave * 16 + 8 * i + lrow) * K + 8 * c)),
+                                         (lds_void*)(base + (wave * 16 + 8 * i) * 128), 16, 0, 0);
+      }
+    }
+  };
+  // f in place on x unit u of step s: thread = chunk tid & 7 of rows tid / 8 and tid / 8 + 64
+  auto transform = [&](int u, int s) {
+    if constexpr (PRO) {
+      char* sx = slot(u, s);
+      const int k0 = s * kBK;
+      const bool masked = CAT && k0 < K1 && !a.cat_bnrelu;
+      const int c = tid & 7;
+      float sc[8], bi[8];
+      ld8f(s_aff + k0 + 8 * c, sc);
+      ld8f(s_aff + K + k0 + 8 * c, bi);
+      const uint8_t* smk = reinterpret_cast<const uint8_t*>(mslot(u, s));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (tid >> 3) + 64 * i;
+        bf16x8_t* q = reinterpret_cast<bf16x8_t*>(sx + swz(row, c));
+        if (masked) *q = prologue<true>(*q, sc, bi, smk[row * 8 + c]);
+        else *q = prologue<false>(*q, sc, bi, 0u);
+      }
+    }
+  };
+
+  bf16x8_t xf[4], wc[4][2], wf[4][2];
+  auto rd_x = [&](int u, int s) {
+    const char* sx = slot(u, s);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      xf[kk] = *reinterpret_cast<const bf16x8_t*>(sx + swz(wm * 32 + r32, 2 * kk + h));
+  };
+  auto rd_w = [&](bf16x8_t (&dst)[4][2], int u, int s) {
+    const char* sw = slot(u, s);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        dst[kk][i] = *reinterpret_cast<const bf16x8_t*>(sw + swz(wn * 64 + 32 * i + r32, 2 * kk + h));
+  };
+  f32x16 acc[2][2][2];   // [x half][W half][32-channel fragment]
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc[u][v][i][k] = 0.f;
+  auto mma = [&](f32x16 (&ac)[2], const bf16x8_t (&wv)[4][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) ac[i] = mfma32(wv[kk][i], xf[kk], ac[i]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // end of a load segment: this wave's LDS reads / writes returned, then the rendezvous
+  auto bar_a = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto bar_b = [&]() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue: steps 0 and 1 (X1(1) is phase 0's DMA); X0(0) transformed, X1(0) landed
+  // (in every phase the LDS reads and writes come before the DMA issue: hipcc waits vmcnt(0)
+  // before an LDS access that follows a global_load_lds it cannot prove disjoint)
+  issue(2, 0);
+  issue(0, 0);
+  issue(3, 0);
+  issue(1, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // step 0 landed
+  bar_a();                                           // ... in every wave
+  transform(0, 0);
+  issue(2, 1);
+  issue(0, 1);
+  issue(3, 1);
+  bar_a();
+  if (wn == 1) __builtin_amdgcn_s_barrier();   // ping-pong: group 1 one barrier behind
+
+  for (int s = 0; s < KT; ++s) {
+    const bool n1 = s + 1 < KT, n2 = s + 2 < KT;
+    // ---- phase 0: X0 x W0
+    rd_x(0, s);
+    rd_w(wc, 2, s);
+    transform(1, s);
+    if (n1) issue(1, s + 1);
+    bar_a();
+    mma(acc[0][0], wc);
+    bar_b();
+    // ---- phase 1: X0 x W1
+    rd_w(wf, 3, s);
+    if (n2) issue(2, s + 2);
+    bar_a();
+    mma(acc[0][1], wf);
+    bar_b();
+    // ---- phase 2: X1 x W1
+    rd_x(1, s);
+    if (n2) issue(0, s + 2);
+    if (n2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VQ) : "memory");   // X0(s+1), W0(s+1)
+    else if (n1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + GX) : "memory");
+    bar_a();
+    mma(acc[1][1], wf);
+    bar_b();
+    // ---- phase 3: X1 x W0
+    if (n1) transform(0, s + 1);
+    if (n2) issue(3, s + 2);
+    if (n2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + GX) : "memory");   // X1(s+1), W1(s+1)
+    else if (n1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar_a();
+    mma(acc[1][0], wc);
+    bar_b();
+  }
+  if (wn == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();                             // staging area free for the epilogue images
+
+  char* simg = smem + wave * 8192;
+  float ss[8], sq[8], sh[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    ss[q] = 0.f;
+    sq[q] = 0.f;
+    sh[q] = 0.f;
+  }
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {               // W half: channels 128 v + 64 wn .. + 63
+    const int ncol0 = 128 * v + 64 * wn;
+    if constexpr (STATS) {
+      if (a.shift) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sh[q] = a.shift[n0 + ncol0 + 8 * (lane & 7) + q];
+      }
+    }
+    f32x16 blk[2][2] = {{acc[0][v][0], acc[1][v][0]}, {acc[0][v][1], acc[1][v][1]}};
+    epilogue<EL, SM, 2, DM>(a, blk, ss, sq, sh, simg, m0 + wm * 32, ncol0, n0, lane,
+                            m0 + 128 + wm * 32);
+    if (STATS && a.part) {
+      float* pp = a.part + (static_cast<int64_t>(nt) * a.mtiles * WM + mt * WM + wm) * 2 * BN;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float sv = ss[q], qv = sq[q];
+#pragma unroll
+        for (int o = 8; o < 64; o <<= 1) {
+          sv += __shfl_xor(sv, o, 64);
+          qv += __shfl_xor(qv, o, 64);
+        }
+        if (lane < 8) {
+          pp[ncol0 + 8 * lane + q] = sv;
+          pp[BN + ncol0 + 8 * lane + q] = qv;
+        }
+        ss[q] = 0.f;
+        sq[q] = 0.f;
+      }
+    }
+  }
+}
+
 struct GPlan {
   int BM, BN, WTN, ntn, mtiles;
   size_t lds;
@@ -296,8 +580,31 @@ hipError_t launch_k(const C1Args& a, const GPlan& p, hipStream_t st) {
   return hipGetLastError();
 }
 
+size_t quad_lds(int K, int pm) {
+  return static_cast<size_t>(8) * 128 * 128 + (pm == PM_CAT ? 4 * 2048 : 0) +
+         (pm != PM_NONE ? static_cast<size_t>(2) * K * 4 : 0);
+}
+
+bool quad_eligible(int64_t M, int K, int N, int pm) {
+  return N % 256 == 0 && K % kBK == 0 && K >= 2 * kBK && pm != PM_BNBWD &&
+         quad_lds(K, pm) <= 160 * 1024;
+}
+
+template <int PM, int SM, bool EL>
+hipError_t launch_q(const C1Args& a, const GPlan& p, hipStream_t st) {
+  auto k = &conv1x1q_kernel<PM, SM, EL>;
+  const size_t lds = quad_lds(a.K, PM);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  k<<<p.ntn * p.mtiles, 512, lds, st>>>(a);
+  return hipGetLastError();
+}
+
+bool use_quad(int64_t M, int K, int N, int pm);
+
 template <int PM, int SM, bool EL>
 hipError_t launch_m(const C1Args& a, const GPlan& p, hipStream_t st) {
+  if (use_quad(a.M, a.K, a.N, PM)) return launch_q<PM, SM, EL>(a, p, st);
   return p.BN == 256 ? launch_k<256, 128, PM, SM, EL>(a, p, st)
                      : launch_k<128, 64, PM, SM, EL>(a, p, st);
 }
@@ -305,13 +612,22 @@ hipError_t launch_m(const C1Args& a, const GPlan& p, hipStream_t st) {
 }  // namespace
 
 namespace {
-int g_mode = -1;   // 0 off, 1 wherever eligible, 2 auto (the shape policy below)
+// 0 off (conv1x1.hip), 1 the 2-buffer glds kernel wherever eligible, 2 auto (the shape policy
+// below), 3 the quad-phase kernel wherever eligible (else the 2-buffer kernel)
+int g_mode = -1;
+
+bool use_quad(int64_t M, int K, int N, int pm) {
+  const int mode = conv1x1g_mode();
+  if (!quad_eligible(M, K, N, pm)) return false;
+  return mode == 3 || (mode == 2 && K >= 384);
+}
 }  // namespace
 
 int conv1x1g_mode() {
   if (g_mode < 0) {
     const char* e = getenv("CML_C1G");
-    g_mode = (!e || !strcmp(e, "auto")) ? 2 : (atoi(e) ? 1 : 0);
+    g_mode = (!e || !strcmp(e, "auto")) ? 2 : atoi(e);
+    if (g_mode < 0 || g_mode > 3) g_mode = 2;
   }
   return g_mode;
 }
@@ -327,11 +643,11 @@ bool conv1x1g_eligible(int64_t M, int K, int N, int pm) {
 bool conv1x1g_pick(int64_t M, int K, int N, int pm) {
   const int mode = conv1x1g_mode();
   if (mode == 0 || !conv1x1g_eligible(M, K, N, pm)) return false;
-  if (mode == 1) return true;
-  // auto: the GEMMs where conv1x1.hip's register-staged pipeline is compute-limited. The
-  // persistent kernel keeps streaming while it runs epilogues, so it stays on the HBM-bound shapes
-  // (few k-steps per tile).
-  return K >= 256;
+  if (mode == 1 || mode == 3) return true;
+  // auto: the quad-phase kernel on the compute-bound GEMMs (many k-steps per 256 x 256 tile);
+  // the persistent register-staged kernel keeps the HBM-bound shapes (few k-steps per tile: it
+  // overlaps one tile's epilogue with the next tile's loads, two workgroups per CU)
+  return use_quad(M, K, N, pm);
 }
 
 size_t conv1x1g_part_floats(int64_t M, int K, int N, int pm) {

@@ -1,5 +1,7 @@
 """The global_load_lds fused 1x1 kernels (csrc/kernels/conv1x1g.hip) against the register-staged
-kernels of conv1x1.hip (same launchers, ``set_conv1x1g_mode`` 1 vs 0) and against fp32 oracles.
+kernels of conv1x1.hip (same launchers, ``set_conv1x1g_mode`` 1 = the 2-buffer kernel, 3 = the
+quad-phase ping-pong kernel where eligible (N % 256 == 0, K >= 128), vs 0) and against fp32
+oracles.
 
 The two families compute the same bf16 operands (same prologue arithmetic) and the same MFMA
 products in the same k order, so every stored output is compared bit for bit; BN statistics and
@@ -34,14 +36,23 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
 
 
+_MODE = [1]
+
+
+@pytest.fixture(autouse=True, params=[1, 3], ids=["glds2", "quad"])
+def _glds_mode(request):
+    _MODE[0] = request.param
+    yield
+
+
 def _both(fn):
-    """fn() under the old kernels (mode 0) and the glds kernels (mode 1)."""
+    """fn() under the old kernels (mode 0) and the glds kernels (mode 1 or 3)."""
     L = _lib()
     prev = L.conv1x1g_mode()
     try:
         L.set_conv1x1g_mode(0)
         a = fn()
-        L.set_conv1x1g_mode(1)
+        L.set_conv1x1g_mode(_MODE[0])
         b = fn()
     finally:
         L.set_conv1x1g_mode(prev)
