@@ -87,6 +87,8 @@ def run(name: str, pol, cfg, steps: int, eval_batches: int, eval_bs: int) -> dic
         t0 = time.perf_counter()
         for s in range(steps):
             losses.append(float(tr.train_step()))
+            if (s + 1) % 10 == 0:
+                print(f"{name} step {s + 1} loss {losses[-1]:.4f}", flush=True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         acc_train = accuracy(tr, eval_batches, eval_bs, True)

@@ -228,15 +228,29 @@ class _BertEmbedFn(torch.autograd.Function):
 
         wg = WG.current()
         if wg is not None and wg.has(tok):
+            # all workers at once: token ids offset by v * vocab index one [V * vocab, D] table
             V = wg.V
-            dv, iv = dx.view(V, B // V, S, D), ids.view(V, B // V, S)
-            for v in range(V):
-                gt, gp, gy = parts(dv[v], iv[v])
-                for p, g in ((tok, gt), (pos, gp), (typ, gy)):
-                    dst, first = wg.views[id(p)], id(p) not in wg.touched
-                    (dst[v].copy_ if first else dst[v].add_)(g)
-            for p in (tok, pos, typ):
-                wg.touched.add(id(p))
+            b = B // V
+            off = (torch.arange(V, device=ids.device) * nv).view(V, 1, 1)
+            gt = emb_bwd(dx, (ids.view(V, b, S) + off).view(B, S), V * nv, -1, False)
+            gp = dx.view(V, b, S, D).sum(1)                   # [V, S, D]
+            gy = dx.view(V, b * S, D).sum(1)                  # [V, D]
+            for p, g, put in ((tok, gt.view(V, nv, D), None), (pos, gp, S), (typ, gy, 0)):
+                dst, first = wg.out(p)
+                if put is None:
+                    (dst.copy_ if first else dst.add_)(g)
+                elif put == 0:                                # segment 0 only
+                    if first:
+                        dst[:, 1:].zero_()
+                        dst[:, 0].copy_(g)
+                    else:
+                        dst[:, 0].add_(g)
+                else:                                         # positions [0, S)
+                    if first:
+                        dst[:, S:].zero_()
+                        dst[:, :S].copy_(g)
+                    else:
+                        dst[:, :S].add_(g)
             return None, None, None, None
         gt, gp, gy = parts(dx, ids)
         return None, gt, gp, gy

@@ -123,6 +123,7 @@ class ConsensusEngine:
         self._pending: Dict[int, object] = {}
         self._ready: Dict[int, List[int]] = {b.index: [] for b in fl.buckets}
         self._flushed: set = set()
+        self._in_worker_batch = False
         self._hooks = []
         self.overlap = bool(cfg.topology.overlap and self.V == 1 and self.N > 1
                             and self.topo in ("allreduce", "allgather", "sharded")
@@ -205,10 +206,12 @@ class ConsensusEngine:
         views = fl.worker_views()
         wg = WG.WorkerGrads(self.V, {id(p): views[i] for i, p in enumerate(fl.params)})
         prev = WG.activate(wg)
+        self._in_worker_batch = True
         try:
             yield wg
         finally:
             WG.activate(prev)
+            self._in_worker_batch = False
         for i, p in enumerate(fl.params):
             if p.grad is not None:
                 raise RuntimeError(
@@ -312,6 +315,8 @@ class ConsensusEngine:
         need = len(b.params)
 
         def hook(_p):
+            if self._in_worker_batch:   # autograd runs the hook even for a None gradient
+                return
             lst = self._ready[b.index]
             lst.append(i)
             if len(lst) == need:

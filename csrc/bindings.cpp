@@ -1744,6 +1744,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_bwd_seg", &norm_bwd_seg, "LayerNorm / RMSNorm backward with per-segment dgamma / dbeta");
   m.def("conv1x1g_mode", &cml::conv1x1g_mode, "fused 1x1 kernel family: 0 old, 1 glds, 2 auto");
   m.def("set_conv1x1g_mode", &cml::set_conv1x1g_mode, "select the fused 1x1 kernel family");
+  m.def("set_conv1x1g_ablate", &cml::set_conv1x1g_ablate, "diagnostics: quad kernel ablation bits");
   m.def("fault", &fault, "Byzantine fault injection");
   m.def("bn_fwd", &bn_fwd, "fused NHWC BatchNorm(+res)(+ReLU) forward");
   m.def("bn_bwd", &bn_bwd, "fused NHWC BatchNorm(+res)(+ReLU) backward");

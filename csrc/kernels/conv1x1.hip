@@ -448,14 +448,15 @@ __global__ __launch_bounds__(256) void bn_stats_gram_kernel(
     q[c] = 0.0;
     sm[c] = 0.0;
   }
-  // row i of G w (fp32 over P <= 1024 terms of one row), then w_i (G w)_i summed in fp64
+  // (G w)_i (fp32 over P <= 1024 terms), then w_i (G w)_i summed in fp64. G is symmetric, so
+  // (G w)_i = sum_j G[j][i] w_j: for each j the lanes read consecutive floats of row j
+  // (coalesced; reading row i per lane touched 64 cache lines per load)
   for (int i = tid; i < P; i += 256) {
     float t[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) t[c] = 0.f;
-    const float* gr = G + static_cast<int64_t>(i) * P;
     for (int j = 0; j < P; ++j) {
-      const float g = gr[j];
+      const float g = G[static_cast<int64_t>(j) * P + i];
 #pragma unroll
       for (int c = 0; c < NC; ++c) t[c] = fmaf(g, ws[c * P + j], t[c]);
     }

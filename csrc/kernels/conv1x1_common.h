@@ -53,6 +53,9 @@ struct C1Args {
   // EL with link_s2: link is [N][ceil(H/2)][ceil(W/2)][N channels] (a stride-2 conv's compact
   // data gradient), added at the even pixels of this [N][H][W] output (lm unused)
   int link_s2, lW, lHW, lOW, lOHW;
+  // diagnostics only (bench/conv1x1g.py --ablate; 0 in production): quad-phase kernel skips
+  // bit 0 the MFMAs, bit 1 the DMA issue, bit 2 the in-LDS prologue, bit 3 the epilogue
+  int ablate;
 };
 
 __device__ __forceinline__ int64_t src_row(const C1Args& a, int m, bool s2) {

@@ -354,7 +354,9 @@ __global__ __launch_bounds__(512, 1) void conv1x1q_kernel(C1Args a) {
   auto mslot = [&](int u, int s) { return smem + SMASK + (((s & 1) << 1) + u) * MKB; };
 
   // unit u (0 X0, 1 X1, 2 W0, 3 W1) of k-step s: 2 DMA instructions per thread (+1 mask, CAT x)
+  const int ab = a.ablate;
   auto issue = [&](int u, int s) {
+    if (ab & 2) return;
     char* base = slot(u, s);
     const int k0 = s * kBK;
     if (u < 2) {
@@ -390,6 +392,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1q_kernel(C1Args a) {
   };
   // f in place on x unit u of step s: thread = chunk tid & 7 of rows tid / 8 and tid / 8 + 64
   auto transform = [&](int u, int s) {
+    if (ab & 4) return;
     if constexpr (PRO) {
       char* sx = slot(u, s);
       const int k0 = s * kBK;
@@ -434,6 +437,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1q_kernel(C1Args a) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) acc[u][v][i][k] = 0.f;
   auto mma = [&](f32x16 (&ac)[2], const bf16x8_t (&wv)[4][2]) {
+    if (ab & 1) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
@@ -506,6 +510,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1q_kernel(C1Args a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();                             // staging area free for the epilogue images
 
+  if (ab & 8) return;
   char* simg = smem + wave * 8192;
   float ss[8], sq[8], sh[8];
 #pragma unroll
@@ -634,6 +639,11 @@ int conv1x1g_mode() {
 
 void set_conv1x1g_mode(int mode) { g_mode = mode; }
 
+namespace {
+int g_ablate = 0;
+}  // namespace
+void set_conv1x1g_ablate(int bits) { g_ablate = bits; }
+
 bool conv1x1g_eligible(int64_t M, int K, int N, int pm) {
   if (K % kBK || N % 128 || K < kBK || M < 1 || M >= (1ll << 31) || N > 4096) return false;
   const GPlan p = gplan(M, K, N, pm);
@@ -661,6 +671,7 @@ hipError_t launch_conv1x1g(const C1Args& a0, int pm, int sm, bool el, hipStream_
                            int* BN) {
   const GPlan p = gplan(a0.M, a0.K, a0.N, pm);
   C1Args a = a0;
+  a.ablate = g_ablate;
   a.ntn = p.ntn;
   a.mtiles = p.mtiles;
   a.wgpn = 0;

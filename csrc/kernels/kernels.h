@@ -75,6 +75,8 @@ hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m,
 // 2 = per-shape auto (default; env CML_C1G = 0 / 1 / auto).
 int conv1x1g_mode();
 void set_conv1x1g_mode(int mode);
+// diagnostics: ablation bits passed to the quad-phase kernel (see C1Args::ablate)
+void set_conv1x1g_ablate(int bits);
 
 size_t gossip_workspace_bytes(int64_t D);
 // k-neighbour mix (1 <= k <= 8): x <- (w0 + sum w_k) x + sum_k w_k clip_k(nbrs[k] - x)
