@@ -31,13 +31,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def make_cfg(batch: int, image: int, classes: int, lr: float, V: int = 1, rule: str = "mean",
-             f: int = 0, seed: int = 7):
+             f: int = 0, seed: int = 7, noise: float = 1.0):
     from consensusml_amd import TrainConfig
     cfg = TrainConfig()
     cfg.model.name = "resnet50"
     cfg.model.num_classes = classes
     cfg.model.image_size = image
-    cfg.model.extra = {"synthetic": "templates", "noise": 1.0}
+    cfg.model.extra = {"synthetic": "templates", "noise": noise}
     cfg.batch_per_worker = batch // V
     cfg.virtual_workers = V
     cfg.agg.rule = rule
@@ -130,6 +130,9 @@ def main():
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--classes", type=int, default=10)
     ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--noise", type=float, default=1.0,
+                    help="pixel noise over the class templates (higher: a harder task whose loss "
+                         "stays informative for longer)")
     ap.add_argument("--eval-batches", type=int, default=8)
     ap.add_argument("--no-krum", action="store_true")
     ap.add_argument("--out", default=None)
@@ -138,15 +141,16 @@ def main():
     torch.backends.cudnn.benchmark = False     # MIOpen immediate mode: no find for new shapes
     fused_pol = perf.policy()
     runs = {}
-    runs["fused"] = run("fused", fused_pol, make_cfg(a.batch, a.image_size, a.classes, a.lr),
+    runs["fused"] = run("fused", fused_pol,
+                        make_cfg(a.batch, a.image_size, a.classes, a.lr, noise=a.noise),
                         a.steps, a.eval_batches, a.batch)
     runs["library"] = run("library", perf.PerfPolicy.library(),
-                          make_cfg(a.batch, a.image_size, a.classes, a.lr), a.steps,
+                          make_cfg(a.batch, a.image_size, a.classes, a.lr, noise=a.noise), a.steps,
                           a.eval_batches, a.batch)
     if not a.no_krum:
         runs["krum8"] = run("krum8", fused_pol,
                             make_cfg(a.batch, a.image_size, a.classes, a.lr, V=8, rule="krum",
-                                     f=2), a.steps, a.eval_batches, a.batch)
+                                     f=2, noise=a.noise), a.steps, a.eval_batches, a.batch)
     cmp = compare(runs["fused"], runs["library"])
     summary = {"config": vars(a), "fused_vs_library": cmp,
                "runs": {k: {kk: vv for kk, vv in r.items() if kk != "stats"}
