@@ -106,16 +106,19 @@ def main():
             x2 = nh(torch.randn(B, K2, H, H, device=dev, generator=g0).bfloat16())
             w = (torch.randn(N, K, device=dev, generator=g0) * K ** -0.5).bfloat16()
             sc, bi = torch.rand(K, device=dev) + 0.5, torch.randn(K, device=dev) * 0.1
+            # as the model calls them: the downsample GEMMs stage the block input x2 as is
+            sc2, bi2 = (None, None) if kind == "cat_bnres" or "down" in name else (sc[K1:], bi[K1:])
             if kind == "cat_bnres":
                 es, eb = torch.rand(N, device=dev) + 0.5, torch.randn(N, device=dev) * 0.1
-                fn = lambda: L.conv1x1_cat_bnres(x, x2, sc, bi, w, es, eb)  # noqa: E731
+                fn = lambda: L.conv1x1_cat_bnres(x, x2, sc[:K1], bi[:K1], sc2, bi2, w, es, eb)  # noqa
             else:
                 mask = torch.randint(0, 256, (M, K1 // 8), device=dev, dtype=torch.uint8)
+                bias = torch.randn(N, device=dev) * 0.1
                 if kind == "cat":
-                    fn = lambda: L.conv1x1_cat(x, mask, x2, sc, bi, w)  # noqa: E731
+                    fn = lambda: L.conv1x1_cat(x, mask, x2, sc2, bi2, w, bias)  # noqa: E731
                 else:
                     mu, iv = torch.zeros(N, device=dev), torch.ones(N, device=dev)
-                    fn = lambda: L.conv1x1_cat_bnsums(x, mask, x2, sc, bi, w, mu, iv)  # noqa
+                    fn = lambda: L.conv1x1_cat_bnsums(x, mask, x2, sc2, bi2, w, bias, mu, iv)  # noqa
 
         def in_mode(m):
             def f():

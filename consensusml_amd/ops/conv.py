@@ -239,17 +239,26 @@ def _const(n: int, v: float, device) -> torch.Tensor:
 # did: profiles/r02_prof53_*).
 
 
-def _cat_dgrad_bn2(L, gy, mask, z, a1, c1, sc, bi, w_cat, g2, b2, mean2, invstd2):
-    """dy2 = [a1 (mask ? gy : 0) + c1 | relu(z sc + bi)] w_cat^T, then bn2's (BN + ReLU on z)
-    backward: (dz, dgamma2, dbeta2)."""
-    a_cat, c_cat = torch.cat([a1, sc]), torch.cat([c1, bi])
+def fold_cat(w1: torch.Tensor, a: torch.Tensor, c: torch.Tensor, w2: torch.Tensor):
+    """Weights and bias of a two-source GEMM whose first source is a BN + ReLU backward,
+    a (mask ? g : 0) + c (a, c fp32 [K1]; w1 [Co, K1], w2 [Co, K2] fp32): the kernels stage only
+    (mask ? g : 0), so a is folded into w1's columns and c into a per-output bias,
+    [a u + c | x2] [w1 | w2]^T = [u | x2] [w1 diag(a) | w2]^T + w1 c.
+    Returns (w_cat bf16 [Co, K1 + K2] contiguous, bias fp32 [Co])."""
+    w_cat = torch.cat([w1 * a[None, :], w2], 1).to(torch.bfloat16).contiguous()
+    return w_cat, torch.mv(w1, c)
+
+
+def _cat_dgrad_bn2(L, gy, mask, z, sc, bi, w_cat, bias, g2, b2, mean2, invstd2):
+    """dy2 = [(mask ? gy : 0) | relu(z sc + bi)] w_cat^T + bias (``fold_cat``), then bn2's
+    (BN + ReLU on z) backward: (dz, dgamma2, dbeta2)."""
     pol = _P()
     if pol.cat_bnsums and z.shape[1] <= pol.cat_bnsums_maxc:
-        dy2, s2, q2 = L.conv1x1_cat_bnsums(gy, mask, z, a_cat, c_cat, w_cat, mean2, invstd2)
+        dy2, s2, q2 = L.conv1x1_cat_bnsums(gy, mask, z, sc, bi, w_cat, bias, mean2, invstd2)
         M = z.numel() // z.shape[1]
         _, _, _, dg2, db2 = L.bn_bwd_coeffs(s2, q2, g2, mean2, invstd2, M)
         return L.bn_bwd_apply(dy2, z, g2, b2, mean2, invstd2, s2, q2), dg2, db2
-    dy2 = L.conv1x1_cat(gy, mask, z, a_cat, c_cat, w_cat)
+    dy2 = L.conv1x1_cat(gy, mask, z, sc, bi, w_cat, bias)
     dz, dg2, db2, _ = L.bn_bwd(dy2, None, z, None, g2, b2, mean2, invstd2, True, False)
     return dz, dg2, db2
 
@@ -333,9 +342,8 @@ class _RecomputeTailFn(torch.autograd.Function):
             dw = torch.addmm(torch.addcmul(torch.outer(cc, cy), ca[:, None], P), cbW3, gram)
             dw = dw.to(w.dtype).view_as(w)
         G = W3.t() @ cbW3
-        w_cat = torch.cat([W3.t(), G.t()], 1).to(torch.bfloat16).contiguous()
-        dz, dg2, db2 = _cat_dgrad_bn2(L, gy, mask, z, ca, cc, sc, bi, w_cat, g2, b2, mean2,
-                                      invstd2)
+        w_cat, bias = fold_cat(W3.t(), ca, cc, G.t())
+        dz, dg2, db2 = _cat_dgrad_bn2(L, gy, mask, z, sc, bi, w_cat, bias, g2, b2, mean2, invstd2)
         dres = None
         if ctx.needs_input_grad[8]:
             mg = MaskedGrad(gy, mask)
@@ -355,7 +363,7 @@ class _RecomputeDownTailFn(torch.autograd.Function):
     with the BN scales folded into the weights, + both BN shifts, ReLU and its mask
     (``conv1x1_cat_bnres``). Backward as ``_RecomputeTailFn`` for each branch -- both BNs see the
     same u = m * g -- with dx = (ad u + cd) Wd + x (Wd^T diag(bd) Wd) from ``conv1x1_cat`` (its
-    second source passes x through max(x * 1 + 0, 0): x must be a ReLU output, as every block
+    second source stages x as is, as the forward's GEMM does: x is a ReLU output, as every block
     input is). x's gradient goes back through autograd (callers wrap x in ``link_tap`` to hand it
     to conv1's data-gradient GEMM)."""
 
@@ -384,8 +392,8 @@ class _RecomputeDownTailFn(torch.autograd.Function):
         w_cat = torch.cat([w3c.view(Co, P_).float() * sc3[:, None],
                            wdc.view(Co, Cin).float() * scd[:, None]], 1).to(torch.bfloat16)
         dev = z.device
-        y, mask = L.conv1x1_cat_bnres(z, x, torch.cat([sc, _const(Cin, 1.0, dev)]),
-                                      torch.cat([bi, _const(Cin, 0.0, dev)]), w_cat.contiguous(),
+        # x: the block input, a ReLU output, staged as is
+        y, mask = L.conv1x1_cat_bnres(z, x, sc, bi, None, None, w_cat.contiguous(),
                                       _const(Co, 1.0, dev), bias)
         ctx.save_for_backward(z, g2, b2, mean2, invstd2, w3, sc, bi, mask, g3, m3, i3, x, wd, gd,
                               md, idd)
@@ -432,15 +440,14 @@ class _RecomputeDownTailFn(torch.autograd.Function):
             dwd = torch.addmm(torch.addcmul(torch.outer(cd, cx), ad[:, None], Pd), bWd, gramd)
             dwd = dwd.to(wd.dtype).view_as(wd)
         G3 = W3.t() @ bW3
-        dz, dg2, db2 = _cat_dgrad_bn2(
-            L, gy, mask, z, a3, c3, sc, bi,
-            torch.cat([W3.t(), G3.t()], 1).to(torch.bfloat16).contiguous(), g2, b2, mean2, invstd2)
+        w_cat3, bias3 = fold_cat(W3.t(), a3, c3, G3.t())
+        dz, dg2, db2 = _cat_dgrad_bn2(L, gy, mask, z, sc, bi, w_cat3, bias3, g2, b2, mean2,
+                                      invstd2)
         dx = None
         if ctx.needs_input_grad[10]:
             Gd = Wd.t() @ bWd
-            dx = L.conv1x1_cat(gy, mask, x, torch.cat([ad, _const(Cin, 1.0, dev)]),
-                               torch.cat([cd, _const(Cin, 0.0, dev)]),
-                               torch.cat([Wd.t(), Gd.t()], 1).to(torch.bfloat16).contiguous())
+            w_catd, biasd = fold_cat(Wd.t(), ad, cd, Gd.t())
+            dx = L.conv1x1_cat(gy, mask, x, None, None, w_catd, biasd)   # x staged as is
         return (dz, dg2, db2, None, None, dw3, dg3, db3, None, None, dx, dwd, dgd, dbd) + \
             (None,) * 5
 

@@ -2,6 +2,7 @@
 // kernels stay torch-free; every launch goes on the caller's current HIP stream and none of them
 // synchronises, so the whole aggregation step can be captured in a hipGraph.
 #include <torch/extension.h>
+#include <array>
 #include <climits>
 #include <ATen/hip/HIPContext.h>
 #include <c10/core/DeviceGuard.h>
@@ -876,27 +877,39 @@ std::vector<Tensor> conv1x1_bnres(const Tensor& x, const Tensor& w, const Tensor
   return {y, mask};
 }
 
-// Downsample tail in one GEMM: y = max(bf16([max(x1 sc + bi, 0) | max(x2 sc + bi, 0)] w^T) ep_sc
-// + ep_bi, 0) and its ReLU bit mask; sc_cat / bi_cat fp32 [K1 + K2], w [Cout, K1 + K2] bf16.
-std::vector<Tensor> conv1x1_cat_bnres(const Tensor& x1, const Tensor& x2, const Tensor& sc_cat,
-                                      const Tensor& bi_cat, const Tensor& w, const Tensor& ep_sc,
-                                      const Tensor& ep_bi) {
+namespace {
+// shapes of a two-source 1x1 GEMM: {N, K1, H, W, K2, M, K, Co}
+std::array<int64_t, 8> cat_shape(const Tensor& x1, const Tensor& x2, const Tensor& w,
+                                 const char* what) {
   check_nhwc(x1, "x1");
   check_nhwc(x2, "x2");
   const int64_t N = x1.size(0), K1 = x1.size(1), H = x1.size(2), W = x1.size(3), K2 = x2.size(1);
-  const int64_t M = N * H * W, K = K1 + K2;
-  TORCH_CHECK(x2.dim() == 4 && x2.size(0) == N && x2.size(2) == H && x2.size(3) == W,
-              "conv1x1_cat_bnres: x2 shape");
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.size(1) == K &&
-                  w.is_contiguous() && w.size(0) % 64 == 0 && K1 % 64 == 0 && K2 % 64 == 0,
-              "conv1x1_cat_bnres: w contiguous bf16 [Cout, K1 + K2], channels multiples of 64");
-  const int64_t Co = w.size(0);
+  TORCH_CHECK(x2.dim() == 4 && x2.size(0) == N && x2.size(2) == H && x2.size(3) == W, what,
+              ": x2 shape");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 &&
+                  w.size(1) == K1 + K2 && w.is_contiguous() && w.size(0) % 64 == 0 &&
+                  K1 % 64 == 0 && K2 % 64 == 0,
+              what, ": w contiguous bf16 [Cout, K1 + K2], channels multiples of 64");
+  return {N, K1, H, W, K2, N * H * W, K1 + K2, w.size(0)};
+}
+}  // namespace
+
+// Downsample tail in one GEMM: y = max(bf16([max(x1 sc1 + bi1, 0) | f2(x2)] w^T) ep_sc + ep_bi, 0)
+// and its ReLU bit mask; f2 = max(x2 sc2 + bi2, 0), or x2 itself when sc2 / bi2 are None (a ReLU
+// output); sc / bi fp32 [K1] / [K2], w [Cout, K1 + K2] bf16.
+std::vector<Tensor> conv1x1_cat_bnres(const Tensor& x1, const Tensor& x2, const Tensor& sc1,
+                                      const Tensor& bi1, const optional<Tensor>& sc2,
+                                      const optional<Tensor>& bi2, const Tensor& w,
+                                      const Tensor& ep_sc, const Tensor& ep_bi) {
+  const auto [N, K1, H, W, K2, M, K, Co] = cat_shape(x1, x2, w, "conv1x1_cat_bnres");
   const c10::DeviceGuard guard(x1.device());
   Tensor y = at::empty({N, Co, H, W}, x1.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor mask = at::empty({M, Co / 8}, x1.options().dtype(at::kByte));
   CML_CHECK_HIP(cml::launch_conv1x1_cat_bnres(
-      x1.data_ptr(), x2.data_ptr(), opt_ptr<const float>(sc_cat, at::kFloat, "sc_cat", K),
-      opt_ptr<const float>(bi_cat, at::kFloat, "bi_cat", K), w.data_ptr(),
+      x1.data_ptr(), x2.data_ptr(), opt_ptr<const float>(sc1, at::kFloat, "sc1", K1),
+      opt_ptr<const float>(bi1, at::kFloat, "bi1", K1),
+      opt_ptr<const float>(sc2, at::kFloat, "sc2", K2),
+      opt_ptr<const float>(bi2, at::kFloat, "bi2", K2), w.data_ptr(),
       opt_ptr<const float>(ep_sc, at::kFloat, "ep_sc", Co),
       opt_ptr<const float>(ep_bi, at::kFloat, "ep_bi", Co), nullptr, y.data_ptr(),
       mask.data_ptr<uint8_t>(), M, static_cast<int>(K1), static_cast<int>(K),
@@ -904,47 +917,35 @@ std::vector<Tensor> conv1x1_cat_bnres(const Tensor& x1, const Tensor& x2, const 
   return {y, mask};
 }
 
-// y = [a (mask ? g : 0) + c | max(x2 sc + bi, 0)] w^T (two sources concatenated along K):
-// g [N, K1, H, W], mask [M, K1 / 8], x2 [N, K2, H, W] NHWC bf16; a_cat = [a | sc], c_cat = [c | bi]
-// fp32 [K1 + K2]; w [Cout, K1 + K2] contiguous bf16 -> y [N, Cout, H, W] NHWC.
-Tensor conv1x1_cat(const Tensor& g, const Tensor& mask, const Tensor& x2, const Tensor& a_cat,
-                   const Tensor& c_cat, const Tensor& w) {
-  check_nhwc(g, "g");
-  check_nhwc(x2, "x2");
-  const int64_t N = g.size(0), K1 = g.size(1), H = g.size(2), W = g.size(3), K2 = x2.size(1);
-  const int64_t M = N * H * W, K = K1 + K2;
-  TORCH_CHECK(x2.dim() == 4 && x2.size(0) == N && x2.size(2) == H && x2.size(3) == W,
-              "conv1x1_cat: x2 shape");
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.size(1) == K &&
-                  w.is_contiguous() && w.size(0) % 64 == 0 && K1 % 64 == 0 && K2 % 64 == 0,
-              "conv1x1_cat: w contiguous bf16 [Cout, K1 + K2], channels multiples of 64");
-  const int64_t Co = w.size(0);
+// y = [(mask ? g : 0) | f2(x2)] w^T + bias (two sources concatenated along K): g [N, K1, H, W],
+// mask [M, K1 / 8], x2 [N, K2, H, W] NHWC bf16; f2 = max(x2 sc2 + bi2, 0) (fp32 [K2]) or x2 itself
+// (None); bias fp32 [Cout] or None; w [Cout, K1 + K2] contiguous bf16 -> y [N, Cout, H, W] NHWC.
+// A BN + ReLU backward on g (a (mask ? g : 0) + c) is folded by the caller: w[:, :K1] diag(a),
+// bias += w[:, :K1] c (ops.conv.fold_cat).
+Tensor conv1x1_cat(const Tensor& g, const Tensor& mask, const Tensor& x2,
+                   const optional<Tensor>& sc2, const optional<Tensor>& bi2, const Tensor& w,
+                   const optional<Tensor>& bias) {
+  const auto [N, K1, H, W, K2, M, K, Co] = cat_shape(g, x2, w, "conv1x1_cat");
   const c10::DeviceGuard guard(g.device());
   Tensor y = at::empty({N, Co, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
   CML_CHECK_HIP(cml::launch_conv1x1_cat(
       g.data_ptr(), opt_ptr<const uint8_t>(mask, at::kByte, "mask", M * K1 / 8), x2.data_ptr(),
-      opt_ptr<const float>(a_cat, at::kFloat, "a_cat", K),
-      opt_ptr<const float>(c_cat, at::kFloat, "c_cat", K), w.data_ptr(), y.data_ptr(), M,
+      opt_ptr<const float>(sc2, at::kFloat, "sc2", K2),
+      opt_ptr<const float>(bi2, at::kFloat, "bi2", K2),
+      opt_ptr<const float>(bias, at::kFloat, "bias", Co), w.data_ptr(), y.data_ptr(), M,
       static_cast<int>(K1), static_cast<int>(K), static_cast<int>(Co), cur_stream()));
   return y;
 }
 
-// conv1x1_cat whose output dy2 is the gradient of relu(bn(x2)) (Cout = K2): also that BN + ReLU
-// backward's sums {sdz, sdzx} from the epilogue (mask recomputed from x2 with bn's affine, the
-// second halves of a_cat / c_cat), so only bn_bwd_apply remains. mean / invstd fp32 [K2].
+// conv1x1_cat whose output dy2 is the gradient of relu(bn(x2)) (Cout = K2; sc2 / bi2 are that
+// BN's affine): also that BN + ReLU backward's sums {sdz, sdzx} from the epilogue (mask
+// recomputed from x2), so only bn_bwd_apply remains. mean / invstd fp32 [K2].
 std::vector<Tensor> conv1x1_cat_bnsums(const Tensor& g, const Tensor& mask, const Tensor& x2,
-                                       const Tensor& a_cat, const Tensor& c_cat, const Tensor& w,
-                                       const Tensor& mean, const Tensor& invstd) {
-  check_nhwc(g, "g");
-  check_nhwc(x2, "x2");
-  const int64_t N = g.size(0), K1 = g.size(1), H = g.size(2), W = g.size(3), K2 = x2.size(1);
-  const int64_t M = N * H * W, K = K1 + K2;
-  TORCH_CHECK(x2.dim() == 4 && x2.size(0) == N && x2.size(2) == H && x2.size(3) == W,
-              "conv1x1_cat_bnsums: x2 shape");
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.size(1) == K &&
-                  w.is_contiguous() && w.size(0) == K2 && K1 % 64 == 0 && K2 % 64 == 0,
-              "conv1x1_cat_bnsums: w contiguous bf16 [K2, K1 + K2], channels multiples of 64");
-  const int64_t Co = w.size(0);
+                                       const Tensor& sc2, const Tensor& bi2, const Tensor& w,
+                                       const optional<Tensor>& bias, const Tensor& mean,
+                                       const Tensor& invstd) {
+  const auto [N, K1, H, W, K2, M, K, Co] = cat_shape(g, x2, w, "conv1x1_cat_bnsums");
+  TORCH_CHECK(Co == K2, "conv1x1_cat_bnsums: w must be [K2, K1 + K2]");
   const c10::DeviceGuard guard(g.device());
   auto f32 = g.options().dtype(at::kFloat);
   Tensor y = at::empty({N, Co, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -952,8 +953,9 @@ std::vector<Tensor> conv1x1_cat_bnsums(const Tensor& g, const Tensor& mask, cons
   Tensor sdz = at::empty({Co}, f32), sdzx = at::empty({Co}, f32);
   CML_CHECK_HIP(cml::launch_conv1x1_cat(
       g.data_ptr(), opt_ptr<const uint8_t>(mask, at::kByte, "mask", M * K1 / 8), x2.data_ptr(),
-      opt_ptr<const float>(a_cat, at::kFloat, "a_cat", K),
-      opt_ptr<const float>(c_cat, at::kFloat, "c_cat", K), w.data_ptr(), y.data_ptr(), M,
+      opt_ptr<const float>(sc2, at::kFloat, "sc2", K2),
+      opt_ptr<const float>(bi2, at::kFloat, "bi2", K2),
+      opt_ptr<const float>(bias, at::kFloat, "bias", Co), w.data_ptr(), y.data_ptr(), M,
       static_cast<int>(K1), static_cast<int>(K), static_cast<int>(Co), cur_stream(),
       opt_ptr<const float>(mean, at::kFloat, "mean", Co),
       opt_ptr<const float>(invstd, at::kFloat, "invstd", Co), part.data_ptr<float>(),
@@ -1794,7 +1796,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "conv1x1_cat + the sums of the BN + ReLU backward its output feeds");
   m.def("bn_affine", &bn_affine, "BN affine (gamma invstd, beta - mean sc) of batch statistics");
   m.def("bn_bwd_apply", &bn_bwd_apply, "apply half of a BN + ReLU backward from its sums");
-  m.def("conv1x1_cat", &conv1x1_cat, "two-source (masked affine | BN-ReLU) 1x1 conv along K");
+  m.def("conv1x1_cat", &conv1x1_cat, "two-source (masked | BN-ReLU or identity) 1x1 conv along K, + bias");
   m.def("split_fold", &split_fold, "fixed-order fold of a split-K partial slab");
   m.def("wgrad1x1_ex", &wgrad1x1_ex, py::arg("dy"), py::arg("x"), py::arg("pro_sc") = py::none(),
         py::arg("pro_bi") = py::none(), py::arg("dmode") = 0, py::arg("dz_mask") = py::none(),

@@ -56,18 +56,23 @@ template <int CB, int BM, bool S2, int PM>
 __device__ __forceinline__ void load_x(const C1Args& a, uint4 (&pb)[CB], uint4 (&pz)[CB],
                                        uint32_t (&pm)[CB], int t, int ks, int srow, int ch) {
   if constexpr (PM == PM_CAT) {
+    // the source is picked per k-step by address, and every row loads a mask byte (a valid dummy
+    // when the step needs none): hipcc turns per-row conditional loads into branches that wait
+    // vmcnt(0) before re-targeting a register with a load still in flight
     const int k0 = ks * kBK;
     const bool first = k0 < a.K1;
+    const uint16_t* base = first ? a.x : a.x2;
+    const int ld = first ? a.K1 : a.K - a.K1;
+    const int ko = (first ? k0 : k0 - a.K1) + 8 * ch;
+    const bool mk = first && !a.cat_bnrelu;
+    const uint8_t* mb = a.cat_bnrelu ? reinterpret_cast<const uint8_t*>(a.x) : a.xm;
+    const int mld = a.cat_bnrelu ? 0 : a.K1 / 8;
+    const int mo = mk ? k0 / 8 + ch : 0;
 #pragma unroll
     for (int j = 0; j < CB; ++j) {
       const int64_t r = src_row(a, t * BM + srow + 32 * j, false);
-      if (first) {
-        pb[j] = *reinterpret_cast<const uint4*>(a.x + r * a.K1 + k0 + 8 * ch);
-        pm[j] = a.cat_bnrelu ? 0u : a.xm[r * (a.K1 / 8) + k0 / 8 + ch];
-      } else {
-        pb[j] = *reinterpret_cast<const uint4*>(a.x2 + r * (a.K - a.K1) + (k0 - a.K1) + 8 * ch);
-        pm[j] = 0u;
-      }
+      pb[j] = *reinterpret_cast<const uint4*>(base + r * ld + ko);
+      pm[j] = mb[r * mld + mo];
     }
     return;
   }
@@ -83,75 +88,78 @@ __device__ __forceinline__ void load_x(const C1Args& a, uint4 (&pb)[CB], uint4 (
 }
 
 
-// f(x) into the LDS image:
+// f(x) into the LDS image (packed VALU, common.h):
 //   PM_BNRELU  max(x sc + bi, 0)                        (the producer's BN + ReLU)
 //   PM_BNBWD   a (mask ? x : 0) + b z + c               (a BN + ReLU backward: x = dL/d(output),
 //              z = the BN input; a = gamma invstd, b = -gamma invstd^2 q / M,
 //              c = -gamma invstd s / M - b mean, with s, q the BN's backward sums)
+//   PM_CAT     (mask ? x : 0)        for k < K1 (x = a BN + ReLU output gradient; the BN backward's
+//                                    affine is folded into w and the epilogue bias), or
+//              max(x sc + bi, 0)     for k < K1 with cat_bnrelu;
+//              max(x2 sc + bi, 0)    for k >= K1 (a BN + ReLU output, recomputed), or x2 itself
+//                                    (id2: a ReLU output that needs no BN): one GEMM over two
+//                                    sources concatenated along K
 // kofs: first input channel of this k-step (ks * 64); KA: entries per coefficient row of s_aff.
-//   PM_CAT     a (mask ? x : 0) + c  for k < K1 (x = a BN + ReLU output gradient, no z term),
-//              max(x2 sc + bi, 0)   for k >= K1 (a BN + ReLU output, recomputed): one GEMM over two
-//              sources concatenated along K
+// The mode is uniform per k-step, so each is one straight loop over the thread's chunks.
 template <int CB, int PM>
 __device__ __forceinline__ void store_x(const uint4 (&pb)[CB], const uint4 (&pz)[CB],
                                         const uint32_t (&pm)[CB], char* sx, const float* s_aff,
                                         int KA, int kofs, int srow, int ch, int K1 = 0,
-                                        int cat_bnrelu = 0) {
-  float sc[8], bi[8], cc[8];
-  if constexpr (PM != PM_NONE) {
+                                        int cat_bnrelu = 0, bool id2 = false) {
+  auto put = [&](int j, uint4 v) { *reinterpret_cast<uint4*>(sx + swz(srow + 32 * j, ch)) = v; };
+  // 0: as is, 1: BN + ReLU, 2: mask only
+  const int mode = PM == PM_NONE ? 0
+                 : PM == PM_CAT  ? (kofs < K1 ? (cat_bnrelu ? 1 : 2) : (id2 ? 0 : 1))
+                                 : 1;
+  if constexpr (PM == PM_BNBWD) {
+    float sc[8], bi[8], cc[8];
     ld8f(s_aff + kofs + 8 * ch, sc);
     ld8f(s_aff + KA + kofs + 8 * ch, bi);
-  }
-  if constexpr (PM == PM_BNBWD) ld8f(s_aff + 2 * KA + kofs + 8 * ch, cc);
+    ld8f(s_aff + 2 * KA + kofs + 8 * ch, cc);
 #pragma unroll
-  for (int j = 0; j < CB; ++j) {
-    uint4 v = pb[j];
-    if constexpr (PM == PM_BNRELU) {
-      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float lo = fmaxf(fmaf(__uint_as_float(w4[i] << 16), sc[2 * i], bi[2 * i]), 0.f);
-        const float hi = fmaxf(fmaf(__uint_as_float(w4[i] & 0xffff0000u), sc[2 * i + 1], bi[2 * i + 1]), 0.f);
-        w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
-      }
-      v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-    } else if constexpr (PM == PM_BNBWD) {
-      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    for (int j = 0; j < CB; ++j) {
+      const uint32_t bits = pm[j];
+      const uint4 g = make_uint4(mask_pk<0>(pb[j].x, bits), mask_pk<1>(pb[j].y, bits),
+                                 mask_pk<2>(pb[j].z, bits), mask_pk<3>(pb[j].w, bits));
+      const uint32_t g4[4] = {g.x, g.y, g.z, g.w};
       const uint32_t z4[4] = {pz[j].x, pz[j].y, pz[j].z, pz[j].w};
-      const uint32_t bits = pm[j];
+      uint32_t w4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float glo = ((bits >> (2 * i)) & 1u) ? __uint_as_float(w4[i] << 16) : 0.f;
-        const float ghi = ((bits >> (2 * i + 1)) & 1u) ? __uint_as_float(w4[i] & 0xffff0000u) : 0.f;
-        const float lo = fmaf(sc[2 * i], glo, fmaf(bi[2 * i], __uint_as_float(z4[i] << 16), cc[2 * i]));
-        const float hi = fmaf(sc[2 * i + 1], ghi,
-                              fmaf(bi[2 * i + 1], __uint_as_float(z4[i] & 0xffff0000u), cc[2 * i + 1]));
-        w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+        const f32x2 gv = {__uint_as_float(g4[i] << 16), __uint_as_float(g4[i] & 0xffff0000u)};
+        const f32x2 zv = {__uint_as_float(z4[i] << 16), __uint_as_float(z4[i] & 0xffff0000u)};
+        const f32x2 t = __builtin_elementwise_fma(f32x2{bi[2 * i], bi[2 * i + 1]}, zv,
+                                                  f32x2{cc[2 * i], cc[2 * i + 1]});
+        const f32x2 r = __builtin_elementwise_fma(f32x2{sc[2 * i], sc[2 * i + 1]}, gv, t);
+        w4[i] = pk_bf16(r.x, r.y);
       }
-      v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-    } else if constexpr (PM == PM_CAT) {
-      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-      const uint32_t bits = pm[j];
-      if (kofs < K1 && !cat_bnrelu) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float glo = ((bits >> (2 * i)) & 1u) ? __uint_as_float(w4[i] << 16) : 0.f;
-          const float ghi = ((bits >> (2 * i + 1)) & 1u) ? __uint_as_float(w4[i] & 0xffff0000u) : 0.f;
-          const float lo = fmaf(sc[2 * i], glo, bi[2 * i]);
-          const float hi = fmaf(sc[2 * i + 1], ghi, bi[2 * i + 1]);
-          w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float lo = fmaxf(fmaf(__uint_as_float(w4[i] << 16), sc[2 * i], bi[2 * i]), 0.f);
-          const float hi = fmaxf(fmaf(__uint_as_float(w4[i] & 0xffff0000u), sc[2 * i + 1], bi[2 * i + 1]), 0.f);
-          w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
-        }
-      }
-      v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      put(j, make_uint4(w4[0], w4[1], w4[2], w4[3]));
     }
-    *reinterpret_cast<uint4*>(sx + swz(srow + 32 * j, ch)) = v;
+    return;
+  }
+  if (mode == 1) {
+    float sc[8], bi[8];
+    ld8f(s_aff + kofs + 8 * ch, sc);
+    ld8f(s_aff + KA + kofs + 8 * ch, bi);
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      const uint4 v = pb[j];
+      put(j, make_uint4(bnrelu_pk(v.x, f32x2{sc[0], sc[1]}, f32x2{bi[0], bi[1]}),
+                        bnrelu_pk(v.y, f32x2{sc[2], sc[3]}, f32x2{bi[2], bi[3]}),
+                        bnrelu_pk(v.z, f32x2{sc[4], sc[5]}, f32x2{bi[4], bi[5]}),
+                        bnrelu_pk(v.w, f32x2{sc[6], sc[7]}, f32x2{bi[6], bi[7]})));
+    }
+  } else if (mode == 2) {
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      const uint4 v = pb[j];
+      const uint32_t bits = pm[j];
+      put(j, make_uint4(mask_pk<0>(v.x, bits), mask_pk<1>(v.y, bits), mask_pk<2>(v.z, bits),
+                        mask_pk<3>(v.w, bits)));
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < CB; ++j) put(j, pb[j]);
   }
 }
 
@@ -173,7 +181,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
   char* sx = smem + (WRES ? KS : 1) * BN * 128;                 // x: [BM][128 B]
   float* s_aff = reinterpret_cast<float*>(sx + BM * 128);       // prologue coefficients [NAFF][K]
   float* s_sh = s_aff + NAFF * KA;                              // statistics shift [BN]
-  char* s_img = ALIAS ? sx : reinterpret_cast<char*>(s_sh + BN);   // epilogue images: 4 x 8 KB
+  float* s_bias = s_sh + BN;                                    // PM_CAT: epilogue bias [BN]
+  char* s_img = ALIAS ? sx : reinterpret_cast<char*>(s_bias + BN);   // epilogue images: 4 x 8 KB
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -188,13 +197,14 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
   const int srow = tid >> 3;                                    // first staged row (+32 per item)
 
   for (int c = tid; c < BN; c += kThreads) s_sh[c] = a.shift ? a.shift[n0 + c] : 0.f;
-  if constexpr (NAFF > 0) {
-    for (int k = tid; k < KA; k += kThreads) {
-      s_aff[k] = a.pro_sc[k];
-      s_aff[KA + k] = a.pro_bi[k];
-      if constexpr (NAFF > 2) s_aff[2 * KA + k] = a.pro_c[k];
-    }
+  if constexpr (PM == PM_CAT) {   // the bias of the workgroup's n-tile, read by every tile's epilogue
+    for (int c = tid; c < BN; c += kThreads) s_bias[c] = a.bias ? a.bias[n0 + c] : 0.f;
   }
+  if constexpr (NAFF > 0) fill_aff(a, PM == PM_CAT, s_aff, KA, tid, kThreads);
+  if constexpr (NAFF > 2) {
+    for (int k = tid; k < KA; k += kThreads) s_aff[2 * KA + k] = a.pro_c[k];
+  }
+  const bool id2 = PM == PM_CAT && a.pro_sc2 == nullptr;
   // first input channel of k-step ks
   auto kofs = [&](int ks_) { return ks_ * kBK; };
   if constexpr (WRES) {   // the whole W slice of this n-tile, once
@@ -226,7 +236,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
       ss[q] = 0.f;
       sq[q] = 0.f;
     }
-    store_x<CB, PM>(pb, pz, pm, sx, s_aff, KA, 0, srow, ch, a.K1, a.cat_bnrelu);
+    store_x<CB, PM>(pb, pz, pm, sx, s_aff, KA, 0, srow, ch, a.K1, a.cat_bnrelu, id2);
     if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, 0);
     __syncthreads();
     for (;;) {
@@ -263,14 +273,15 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
         if constexpr (ALIAS) __syncthreads();   // every wave is done reading x before the images
 #pragma unroll
         for (int u = 0; u < MT; ++u)
-          epilogue<EL, SM, MT, PM == PM_CAT && SM == SM_BNBWD>(a, acc[u], ss, sq, sh,
+          epilogue<EL, SM, MT, PM == PM_CAT && SM == SM_BNBWD,
+                   PM == PM_CAT && SM != SM_BNRES>(a, acc[u], ss, sq, sh,
                                                                s_img + wave * 8192,
-                           t * BM + wm * 64 * MT + 64 * u, wn * 64, n0, lane);
+                           t * BM + wm * 64 * MT + 64 * u, wn * 64, n0, lane, -1,
+                           a.bias ? s_bias : nullptr);
       }
       if (!more) break;
       __syncthreads();               // every wave is done reading this step's LDS
-      store_x<CB, PM>(pb, pz, pm, sx, s_aff, KA, kofs(ksn), srow, ch, a.K1,
-                           a.cat_bnrelu);
+      store_x<CB, PM>(pb, pz, pm, sx, s_aff, KA, kofs(ksn), srow, ch, a.K1, a.cat_bnrelu, id2);
       if constexpr (!WRES) stage_w<CA>(a, sw, n0, srow, ch, ksn);
       __syncthreads();
       t = tn;
@@ -543,7 +554,7 @@ Plan plan_for(int WN, int64_t M, int K, int N, int naff, int mt = 1, int kaff = 
   p.G = p.ntn * p.wgpn;
   const size_t wbytes = static_cast<size_t>(K) * p.BN * 2;
   const size_t xbytes = static_cast<size_t>(p.BM) * 128;
-  const size_t aff = static_cast<size_t>(naff) * kaff * 4 + static_cast<size_t>(p.BN) * 4 +
+  const size_t aff = static_cast<size_t>(naff) * kaff * 4 + static_cast<size_t>(p.BN) * 8 +
                      (mt > 1 ? 0 : 4 * 8192);   // + the per-wave epilogue images (aliased at MT 2)
   p.wres = wbytes + xbytes + aff <= 80 * 1024;
   p.lds = (p.wres ? wbytes : static_cast<size_t>(p.BN) * 128) + xbytes + aff;
@@ -836,26 +847,27 @@ hipError_t launch_conv1x1_bnres(const void* x, const void* w, void* y, uint8_t* 
   return launch_tail(a, p, false, st);
 }
 
-hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2, const float* a_cat,
-                              const float* c_cat, const void* w, void* y, int64_t M, int K1, int K,
-                              int N, hipStream_t st, const float* mean, const float* invstd,
-                              float* part, float* sdz, float* sdzx) {
-  if (bad_shape(M, K, N) || K1 % kBK || K1 <= 0 || K1 >= K || !mask || !a_cat || !c_cat)
+hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2, const float* sc2,
+                              const float* bi2, const float* bias, const void* w, void* y,
+                              int64_t M, int K1, int K, int N, hipStream_t st, const float* mean,
+                              const float* invstd, float* part, float* sdz, float* sdzx) {
+  if (bad_shape(M, K, N) || K1 % kBK || K1 <= 0 || K1 >= K || !mask || (!sc2 != !bi2))
     return hipErrorInvalidValue;
   const bool sums = mean != nullptr;
   // sums: the output is the gradient of the BN + ReLU whose input is x2 itself (N = K - K1)
-  if (sums && (!invstd || !part || !sdz || !sdzx || N != K - K1)) return hipErrorInvalidValue;
+  if (sums && (!invstd || !part || !sdz || !sdzx || N != K - K1 || !sc2)) return hipErrorInvalidValue;
   const Plan p = make_plan(M, K, N, 2, -1, !sums);   // (the sums' MT = 2 tile spills)
   C1Args a = base_args(g, w, y, M, K, N, p);
   a.xm = mask;
   a.x2 = reinterpret_cast<const uint16_t*>(x2);
-  a.pro_sc = a_cat;
-  a.pro_bi = c_cat;
+  a.pro_sc2 = sc2;
+  a.pro_bi2 = bi2;
+  a.bias = bias;
   a.K1 = K1;
   if (sums) {
     a.sz = a.x2;
-    a.ep_sc = a_cat + K1;   // the BN's own affine: the second source's prologue coefficients
-    a.ep_bi = c_cat + K1;
+    a.ep_sc = sc2;   // the BN's own affine: the second source's prologue coefficients
+    a.ep_bi = bi2;
     a.shift = mean;
     a.part = part;
   }
@@ -879,25 +891,28 @@ size_t conv1x1_cat_part_floats(int64_t M, int K, int N) {
   return std::max(static_cast<size_t>(p.G) * p.WM * 2 * p.BN, g);
 }
 
-hipError_t launch_conv1x1_cat_bnres(const void* x1, const void* x2, const float* sc_cat,
-                                    const float* bi_cat, const void* w, const float* ep_sc,
-                                    const float* ep_bi, const void* res, void* y, uint8_t* ymask,
-                                    int64_t M, int K1, int K, int N, hipStream_t st) {
-  if (bad_shape(M, K, N) || K1 % kBK || K1 <= 0 || K1 >= K || !sc_cat || !bi_cat || !ep_sc ||
-      !ep_bi || !ymask)
+hipError_t launch_conv1x1_cat_bnres(const void* x1, const void* x2, const float* sc1,
+                                    const float* bi1, const float* sc2, const float* bi2,
+                                    const void* w, const float* ep_sc, const float* ep_bi,
+                                    const void* res, void* y, uint8_t* ymask, int64_t M, int K1,
+                                    int K, int N, hipStream_t st) {
+  if (bad_shape(M, K, N) || K1 % kBK || K1 <= 0 || K1 >= K || !sc1 || !bi1 || (!sc2 != !bi2) ||
+      !ep_sc || !ep_bi || !ymask)
     return hipErrorInvalidValue;
   const Plan p = make_plan(M, K, N, 2, -1, false);   // (its MT = 2 tile spills)
   C1Args a = base_args(x1, w, y, M, K, N, p);
   a.x2 = reinterpret_cast<const uint16_t*>(x2);
-  a.pro_sc = sc_cat;
-  a.pro_bi = bi_cat;
+  a.pro_sc = sc1;
+  a.pro_bi = bi1;
+  a.pro_sc2 = sc2;
+  a.pro_bi2 = bi2;
   a.K1 = K1;
   a.cat_bnrelu = 1;
   a.ep_sc = ep_sc;
   a.ep_bi = ep_bi;
   a.link = reinterpret_cast<const uint16_t*>(res);
   a.ymask = ymask;
-  if (conv1x1g_pick(M, K, N, PM_CAT)) {
+  if (conv1x1g_pick(M, K, N, PM_CAT, true)) {
     int R, BN;
     return launch_conv1x1g(a, PM_CAT, SM_BNRES, false, st, &R, &BN);
   }

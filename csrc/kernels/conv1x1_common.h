@@ -45,8 +45,15 @@ struct C1Args {
   const float* ep_sc;     // SM_BNRES: y = max(v ep_sc + ep_bi + link, 0) per output channel [N]
   const float* ep_bi;
   uint8_t* ymask;         // SM_BNRES: bit mask of y > 0 [M][N / 8]
-  int K1;                 // PM_CAT: channels of the first source (x, with mask xm); x2 has K - K1
-  int cat_bnrelu;         // PM_CAT: 1 = the first source is max(x sc + bi, 0) too (no mask)
+  // PM_CAT (two sources concatenated along K): the first source (x, K1 channels) is staged as
+  // (mask xm ? x : 0) -- a BN + ReLU backward's affine a u + c is folded into w and `bias` by the
+  // caller -- or, with cat_bnrelu, as max(x pro_sc + pro_bi, 0) (pro_sc / pro_bi [K1]); the second
+  // (x2, K - K1 channels) as max(x2 pro_sc2 + pro_bi2, 0), or as x2 itself when pro_sc2 is null.
+  const float* pro_sc2;
+  const float* pro_bi2;
+  const float* bias;      // PM_CAT: [N] added to the fp32 products before rounding, or null
+  int K1;
+  int cat_bnrelu;
   int M, K, N;
   int ntn, wgpn, mtiles;
   int H, W, OW, OHW;      // S2: input H, W; output W and H*W
@@ -68,6 +75,28 @@ __device__ __forceinline__ int64_t src_row(const C1Args& a, int m, bool s2) {
     return static_cast<int64_t>(img) * a.H * a.W + 2 * oh * a.W + 2 * ow;
   }
   return m;
+}
+
+// prologue coefficient table s_aff = {sc[K], bi[K]} in LDS. PM_CAT: the first K1 entries are the
+// first source's BN affine (cat_bnrelu; 1 / 0 when it is masked), the rest the second source's
+// (pro_sc2 / pro_bi2; 1 / 0 when it is staged as is).
+__device__ __forceinline__ void fill_aff(const C1Args& a, bool cat, float* s_aff, int K, int tid,
+                                         int nt) {
+  for (int k = tid; k < K; k += nt) {
+    float sc, bi;
+    if (!cat) {
+      sc = a.pro_sc[k];
+      bi = a.pro_bi[k];
+    } else if (k < a.K1) {
+      sc = a.cat_bnrelu ? a.pro_sc[k] : 1.f;
+      bi = a.cat_bnrelu ? a.pro_bi[k] : 0.f;
+    } else {
+      sc = a.pro_sc2 ? a.pro_sc2[k - a.K1] : 1.f;
+      bi = a.pro_sc2 ? a.pro_bi2[k - a.K1] : 0.f;
+    }
+    s_aff[k] = sc;
+    s_aff[K + k] = bi;
+  }
 }
 
 __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
@@ -94,10 +123,13 @@ __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
 // prologue applied it), so the BN + ReLU backward that follows needs no reduction pass of its own.
 // mhi: global row of block rows 32..63 (default m0 + 32; the quad-phase kernel's waves own two
 // separate 32-row groups).
-template <bool EL, int SM, int MT, bool DM = false>
+// BIAS: bsrc[ncol0 + channel] (when bsrc is set: PM_CAT's folded affine, a.bias from the tile's
+// first channel, or its LDS copy) is added to every product before rounding.
+template <bool EL, int SM, int MT, bool DM = false, bool BIAS = false>
 __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], float (&ss)[8],
                                          float (&sq)[8], const float (&sh)[8], char* simg, int m0,
-                                         int ncol0, int n0, int lane, int mhi = -1) {
+                                         int ncol0, int n0, int lane, int mhi = -1,
+                                         const float* bsrc = nullptr) {
   const int h = lane >> 5, r32 = lane & 31;
   const int c = lane & 7;
   const int mh = mhi < 0 ? m0 + 32 : mhi;
@@ -156,18 +188,21 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
     }
   };
   if constexpr (LD) issue(0);
+  const bool bias = BIAS && bsrc != nullptr;
 #pragma unroll
-  for (int jm = 0; jm < 2; ++jm) {
-    const int p = 32 * jm + r32;                       // pixel row of the wave block
+  for (int i = 0; i < 2; ++i) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int g = 0; g < 4; ++g) {
+      // channels 32 i + 8 g + 4 h .. +3 = half h of 16-B chunk 4 i + g of the pixel row
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (bias) bv = *reinterpret_cast<const float4*>(bsrc + ncol0 + 32 * i + 8 * g + 4 * h);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t b0 = f2bf(acc[i][jm][4 * g + 0]), b1 = f2bf(acc[i][jm][4 * g + 1]);
-        const uint32_t b2 = f2bf(acc[i][jm][4 * g + 2]), b3 = f2bf(acc[i][jm][4 * g + 3]);
-        // channels 32 i + 8 g + 4 h .. +3 = half h of 16-B chunk 4 i + g of the pixel row
+      for (int jm = 0; jm < 2; ++jm) {
+        const int p = 32 * jm + r32;                   // pixel row of the wave block
+        const f32x16& v = acc[i][jm];
         *reinterpret_cast<uint2*>(simg + swz(p, 4 * i + g) + 8 * h) =
-            make_uint2(b0 | (b1 << 16), b2 | (b3 << 16));
+            make_uint2(pk_bf16(v[4 * g + 0] + bv.x, v[4 * g + 1] + bv.y),
+                       pk_bf16(v[4 * g + 2] + bv.z, v[4 * g + 3] + bv.w));
       }
     }
   }
@@ -190,7 +225,7 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
                          (((lb >> (2 * q)) & 1u) ? __uint_as_float(l4[q] << 16) : 0.f);
         const float hi = __uint_as_float(w4[q] & 0xffff0000u) +
                          (((lb >> (2 * q + 1)) & 1u) ? __uint_as_float(l4[q] & 0xffff0000u) : 0.f);
-        w4[q] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+        w4[q] = pk_bf16(lo, hi);
       }
       v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
@@ -206,8 +241,7 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
                          __uint_as_float(r4[q] & 0xffff0000u);
         bits |= (lo > 0.f ? 1u : 0u) << (2 * q);
         bits |= (hi > 0.f ? 1u : 0u) << (2 * q + 1);
-        w4[q] = static_cast<uint32_t>(f2bf(fmaxf(lo, 0.f))) |
-                (static_cast<uint32_t>(f2bf(fmaxf(hi, 0.f))) << 16);
+        w4[q] = pk_bf16(fmaxf(lo, 0.f), fmaxf(hi, 0.f));
       }
       *reinterpret_cast<uint4*>(a.y + e0) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
       a.ymask[e0 >> 3] = static_cast<uint8_t>(bits);
@@ -275,7 +309,8 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
 // conv1x1g.hip: the global_load_lds-staged kernel for the same (prologue, epilogue) modes.
 // conv1x1g_pick: policy (CML_C1G = 0 / 1 / auto); part slabs: [ntn][R][2][BN] + fold area.
 bool conv1x1g_eligible(int64_t M, int K, int N, int pm);
-bool conv1x1g_pick(int64_t M, int K, int N, int pm);
+// bnres: the two-source GEMM with the BN + residual + ReLU epilogue (conv1x1_cat_bnres)
+bool conv1x1g_pick(int64_t M, int K, int N, int pm, bool bnres = false);
 size_t conv1x1g_part_floats(int64_t M, int K, int N, int pm);
 hipError_t launch_conv1x1g(const c1::C1Args& a, int pm, int sm, bool el, hipStream_t st, int* R,
                            int* BN);

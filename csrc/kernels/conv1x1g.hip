@@ -41,27 +41,21 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void g_void;
 
 // f of one B fragment (8 channels k0 .. k0 + 7 of one pixel); sc / bi: the channels' coefficients
-// MASKED: a (bit ? x : 0) + c, else max(x sc + bi, 0)
+// MASKED: (bit ? x : 0) (the cat's first source; its BN-backward affine is folded into w and the
+// epilogue bias), else max(x sc + bi, 0). Packed VALU (common.h): 4 / 5 instructions per pair.
 template <bool MASKED>
 __device__ __forceinline__ bf16x8_t prologue(bf16x8_t v, const float (&sc)[8], const float (&bi)[8],
                                              uint32_t bits) {
   uint4 u = *reinterpret_cast<const uint4*>(&v);
-  uint32_t w4[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float lo, hi;
-    if constexpr (MASKED) {
-      const float glo = ((bits >> (2 * i)) & 1u) ? __uint_as_float(w4[i] << 16) : 0.f;
-      const float ghi = ((bits >> (2 * i + 1)) & 1u) ? __uint_as_float(w4[i] & 0xffff0000u) : 0.f;
-      lo = fmaf(sc[2 * i], glo, bi[2 * i]);
-      hi = fmaf(sc[2 * i + 1], ghi, bi[2 * i + 1]);
-    } else {
-      lo = fmaxf(fmaf(__uint_as_float(w4[i] << 16), sc[2 * i], bi[2 * i]), 0.f);
-      hi = fmaxf(fmaf(__uint_as_float(w4[i] & 0xffff0000u), sc[2 * i + 1], bi[2 * i + 1]), 0.f);
-    }
-    w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+  if constexpr (MASKED) {
+    u = make_uint4(mask_pk<0>(u.x, bits), mask_pk<1>(u.y, bits), mask_pk<2>(u.z, bits),
+                   mask_pk<3>(u.w, bits));
+  } else {
+    u = make_uint4(bnrelu_pk(u.x, f32x2{sc[0], sc[1]}, f32x2{bi[0], bi[1]}),
+                   bnrelu_pk(u.y, f32x2{sc[2], sc[3]}, f32x2{bi[2], bi[3]}),
+                   bnrelu_pk(u.z, f32x2{sc[4], sc[5]}, f32x2{bi[4], bi[5]}),
+                   bnrelu_pk(u.w, f32x2{sc[6], sc[7]}, f32x2{bi[6], bi[7]}));
   }
-  u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
   return *reinterpret_cast<const bf16x8_t*>(&u);
 }
 
@@ -97,12 +91,7 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv1x1g_kernel(C1Args a) {
   const int K = a.K, KS = K / kBK;
   const int K1 = CAT ? a.K1 : K;
 
-  if constexpr (PM != PM_NONE) {
-    for (int k = tid; k < K; k += NT) {
-      s_aff[k] = a.pro_sc[k];
-      s_aff[K + k] = a.pro_bi[k];
-    }
-  }
+  if constexpr (PM != PM_NONE) fill_aff(a, CAT, s_aff, K, tid, NT);
   // this lane's staged rows (clamped: rows past M load row M - 1; their products are dropped)
   const int p = lane & 7, lrow = lane >> 3;
   int64_t xr[QA];
@@ -169,7 +158,8 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv1x1g_kernel(C1Args a) {
     const char* sw = sx + SX;
     const uint8_t* smk = reinterpret_cast<const uint8_t*>(sw + SW);
     const bool masked = CAT && ks * kBK < K1 && !a.cat_bnrelu;
-    if constexpr (TL && PM != PM_NONE) {
+    const bool ident = CAT && ks * kBK >= K1 && a.pro_sc2 == nullptr;   // x2 staged as is
+    if (TL && PM != PM_NONE && !ident) {
       // thread: logical 16-B chunk tid & 7 (8 channels) of rows tid / 8 + NT / 8 * i, in place
       char* sxw = smem + buf * SB;
       const int c = tid & 7;
@@ -197,7 +187,7 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv1x1g_kernel(C1Args a) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         B[j] = *reinterpret_cast<const bf16x8_t*>(sx + swz(wm * 64 + 32 * j + r32, 2 * kk + h));
-      if constexpr (PM != PM_NONE && !TL) {
+      if (PM != PM_NONE && !TL && !ident) {
         const int k0 = ks * kBK + 16 * kk + 8 * h;   // this lane's 8 channels
         float sc[8], bi[8];
         ld8f(s_aff + k0, sc);
@@ -240,7 +230,8 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv1x1g_kernel(C1Args a) {
       }
     }
     f32x16 blk[2][2] = {{acc[2 * sb][0], acc[2 * sb][1]}, {acc[2 * sb + 1][0], acc[2 * sb + 1][1]}};
-    epilogue<EL, SM, 2, DM>(a, blk, ss, sq, sh, simg, m0 + wm * 64, ncol0, n0, lane);
+    epilogue<EL, SM, 2, DM, CAT && SM != SM_BNRES>(a, blk, ss, sq, sh, simg, m0 + wm * 64, ncol0,
+                                                  n0, lane, -1, a.bias ? a.bias + n0 : nullptr);
     if (STATS && a.part) {   // (SM_BN without a slab: the conv only, no statistics)
       // fold the 8 lanes sharing a channel group (lane & 7): one partial row per (m-tile, wm)
       float* pp = a.part + (static_cast<int64_t>(nt) * a.mtiles * WM + mt * WM + wm) * 2 * BN;
@@ -323,12 +314,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1q_kernel(C1Args a) {
   const int K = a.K, KT = K / kBK;
   const int K1 = CAT ? a.K1 : K;
 
-  if constexpr (PRO) {
-    for (int k = tid; k < K; k += NT) {
-      s_aff[k] = a.pro_sc[k];
-      s_aff[K + k] = a.pro_bi[k];
-    }
-  }
+  if constexpr (PRO) fill_aff(a, CAT, s_aff, K, tid, NT);
   // staged rows of this thread in every unit: wave * 16 + 8 i + lane / 8 (i = 0, 1), 16-B chunk
   // lane & 7 of the row (source address inverse-swizzled: the DMA writes lane-linear)
   const int p = lane & 7, lrow = lane >> 3;
@@ -397,6 +383,7 @@ __global__ __launch_bounds__(512, 1) void conv1x1q_kernel(C1Args a) {
       char* sx = slot(u, s);
       const int k0 = s * kBK;
       const bool masked = CAT && k0 < K1 && !a.cat_bnrelu;
+      if (CAT && k0 >= K1 && a.pro_sc2 == nullptr) return;   // identity second source
       const int c = tid & 7;
       float sc[8], bi[8];
       ld8f(s_aff + k0 + 8 * c, sc);
@@ -529,8 +516,9 @@ __global__ __launch_bounds__(512, 1) void conv1x1q_kernel(C1Args a) {
       }
     }
     f32x16 blk[2][2] = {{acc[0][v][0], acc[1][v][0]}, {acc[0][v][1], acc[1][v][1]}};
-    epilogue<EL, SM, 2, DM>(a, blk, ss, sq, sh, simg, m0 + wm * 32, ncol0, n0, lane,
-                            m0 + 128 + wm * 32);
+    epilogue<EL, SM, 2, DM, CAT && SM != SM_BNRES>(a, blk, ss, sq, sh, simg, m0 + wm * 32, ncol0,
+                                                  n0, lane, m0 + 128 + wm * 32,
+                                                  a.bias ? a.bias + n0 : nullptr);
     if (STATS && a.part) {
       float* pp = a.part + (static_cast<int64_t>(nt) * a.mtiles * WM + mt * WM + wm) * 2 * BN;
 #pragma unroll
@@ -650,14 +638,14 @@ bool conv1x1g_eligible(int64_t M, int K, int N, int pm) {
   return p.lds <= 160 * 1024 && static_cast<int64_t>(p.ntn) * p.mtiles < (1ll << 31);
 }
 
-bool conv1x1g_pick(int64_t M, int K, int N, int pm) {
+bool conv1x1g_pick(int64_t M, int K, int N, int pm, bool bnres) {
   const int mode = conv1x1g_mode();
   if (mode == 0 || !conv1x1g_eligible(M, K, N, pm)) return false;
   if (mode == 1 || mode == 3) return true;
-  // auto: the quad-phase kernel on the compute-bound GEMMs (many k-steps per 256 x 256 tile);
-  // the persistent register-staged kernel keeps the HBM-bound shapes (few k-steps per tile: it
-  // overlaps one tile's epilogue with the next tile's loads, two workgroups per CU)
-  return use_quad(M, K, N, pm);
+  // auto: since the packed prologues (round 3, profiles/r03_11_families.jsonl) the persistent
+  // register-staged kernel is as fast or faster everywhere except the downsample tails' forward
+  // GEMM (cat_bnres: 256 x 256 tiles, 1.14 / 0.92 vs 1.44 / 1.21 ms at batch 2048)
+  return pm == PM_CAT && bnres && use_quad(M, K, N, pm);
 }
 
 size_t conv1x1g_part_floats(int64_t M, int K, int N, int pm) {

@@ -373,21 +373,25 @@ hipError_t launch_conv1x1_bnres(const void* x, const void* w, void* y, uint8_t* 
                                 const float* pro_sc, const float* pro_bi, const float* ep_sc,
                                 const float* ep_bi, const void* res, int64_t M, int K, int N,
                                 hipStream_t st);
-// y = [a (mask ? g : 0) + c | max(x2 sc + bi, 0)] W^T: K = K1 + K2 channels from two sources
-// (g, mask: [M][K1]; x2: [M][K2]); a_cat = [a | sc], c_cat = [c | bi] (fp32 [K]); w [N][K].
+// Two-source GEMMs (K = K1 + K2 channels from g / x1 [M][K1] and x2 [M][K2]; w [N][K]):
 // y = max(bf16([max(x1 sc + bi, 0) | max(x2 sc + bi, 0)] W^T) ep_sc + ep_bi (+ res), 0) and its
 // ReLU bit mask: two BN'd convs summed before a ReLU (a downsample block's tail) in one GEMM.
-hipError_t launch_conv1x1_cat_bnres(const void* x1, const void* x2, const float* sc_cat,
-                                    const float* bi_cat, const void* w, const float* ep_sc,
-                                    const float* ep_bi, const void* res, void* y, uint8_t* ymask,
-                                    int64_t M, int K1, int K, int N, hipStream_t st);
-// mean / invstd (optional): also the sums {sdz, sdzx} of the backward of the BN + ReLU whose input
-// is x2 (N = K - K1), ReLU mask recomputed from x2; part: conv1x1_cat_part_floats floats
-hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2, const float* a_cat,
-                              const float* c_cat, const void* w, void* y, int64_t M, int K1, int K,
-                              int N, hipStream_t st, const float* mean = nullptr,
-                              const float* invstd = nullptr, float* part = nullptr,
-                              float* sdz = nullptr, float* sdzx = nullptr);
+// x1 staged as max(x1 sc1 + bi1, 0) (sc1 / bi1 [K1]), x2 as max(x2 sc2 + bi2, 0) ([K - K1]) or as
+// is (sc2 / bi2 null)
+hipError_t launch_conv1x1_cat_bnres(const void* x1, const void* x2, const float* sc1,
+                                    const float* bi1, const float* sc2, const float* bi2,
+                                    const void* w, const float* ep_sc, const float* ep_bi,
+                                    const void* res, void* y, uint8_t* ymask, int64_t M, int K1,
+                                    int K, int N, hipStream_t st);
+// y = [(mask ? g : 0) | f2(x2)] w^T + bias: f2 = max(x2 sc2 + bi2, 0) ([K - K1]) or the identity
+// (sc2 / bi2 null); bias [N] or null. mean / invstd (optional): also the sums {sdz, sdzx} of the
+// backward of the BN + ReLU whose input is x2 (N = K - K1, needs sc2 / bi2: its mask is
+// recomputed from x2); part: conv1x1_cat_part_floats floats
+hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2, const float* sc2,
+                              const float* bi2, const float* bias, const void* w, void* y,
+                              int64_t M, int K1, int K, int N, hipStream_t st,
+                              const float* mean = nullptr, const float* invstd = nullptr,
+                              float* part = nullptr, float* sdz = nullptr, float* sdzx = nullptr);
 size_t conv1x1_cat_part_floats(int64_t M, int K, int N);
 hipError_t launch_conv1x1_bnbwd(const void* g, const void* z, const uint8_t* mask, const float* ca,
                                 const float* cb, const float* cc, const void* w, void* y,

@@ -203,23 +203,34 @@ def test_stats_only_and_bnres_match_stored_path(cuda, N, K, H):
     assert agree > 0.999, agree
 
 
+@pytest.mark.parametrize("id2", [False, True])
 @pytest.mark.parametrize("N,K1,K2,No,H", [(2, 256, 64, 64, 28), (3, 512, 128, 128, 14),
                                           (2, 512, 128, 128, 9)])
-def test_conv1x1_cat(cuda, N, K1, K2, No, H):
+def test_conv1x1_cat(cuda, id2, N, K1, K2, No, H):
+    """[a (mask ? g : 0) + c | f2(x2)] w^T with a, c folded into the weights and a bias
+    (ops.conv.fold_cat); f2 = relu(x2 sc + bi), or x2 as is (id2, x2 a ReLU output)."""
+    from consensusml_amd.ops.conv import fold_cat
     g0 = torch.Generator(device=cuda).manual_seed(22)
     g = _nhwc(torch.randn(N, K1, H, H, device=cuda, generator=g0).bfloat16())
     x2 = _nhwc(torch.randn(N, K2, H, H, device=cuda, generator=g0).bfloat16())
+    if id2:
+        x2 = torch.relu(x2)
     M = N * H * H
     mask = _rand_mask(M, K1, cuda, g0)
     a = torch.randn(K1, device=cuda, generator=g0)
     c = torch.randn(K1, device=cuda, generator=g0) * 0.1
     sc = torch.rand(K2, device=cuda, generator=g0) + 0.5
     bi = torch.randn(K2, device=cuda, generator=g0) * 0.1
-    w = (torch.randn(No, K1 + K2, device=cuda, generator=g0) * (K1 + K2) ** -0.5).bfloat16()
-    y = _lib().conv1x1_cat(g, mask, x2, torch.cat([a, sc]), torch.cat([c, bi]), w)
-    u = (a * (_bits(mask, K1) * _rows(g)) + c).bfloat16().float()
-    v = torch.relu(_rows(x2) * sc + bi).bfloat16().float()
-    ref = torch.cat([u, v], 1) @ w.float().t()
+    w = torch.randn(No, K1 + K2, device=cuda, generator=g0) * (K1 + K2) ** -0.5
+    w_cat, bias = fold_cat(w[:, :K1], a, c, w[:, K1:])
+    if id2:
+        y = _lib().conv1x1_cat(g, mask, x2, None, None, w_cat, bias)
+        v = _rows(x2)
+    else:
+        y = _lib().conv1x1_cat(g, mask, x2, sc, bi, w_cat, bias)
+        v = torch.relu(_rows(x2) * sc + bi).bfloat16().float()
+    u = a * (_bits(mask, K1) * _rows(g)) + c
+    ref = torch.cat([u, v], 1) @ w.t()
     _close(_rows(y), ref, 1e-2)
 
 
@@ -243,10 +254,11 @@ def test_conv1x1_cat_bnsums(cuda, N, K1, K2, H):
     invstd = (X.var(0, unbiased=False) + 1e-5).rsqrt().float()
     sc = gam.float() * invstd
     bi = bet.float() - mean * sc
-    w = (torch.randn(K2, K1 + K2, device=cuda, generator=g0) * (K1 + K2) ** -0.5).bfloat16()
-    a_cat, c_cat = torch.cat([a, sc]), torch.cat([c, bi])
-    y, s, q = _lib().conv1x1_cat_bnsums(g, mask, x2, a_cat, c_cat, w, mean, invstd)
-    _close(_rows(y), _rows(_lib().conv1x1_cat(g, mask, x2, a_cat, c_cat, w)), 1e-2)
+    w = torch.randn(K2, K1 + K2, device=cuda, generator=g0) * (K1 + K2) ** -0.5
+    from consensusml_amd.ops.conv import fold_cat
+    w_cat, bias = fold_cat(w[:, :K1], a, c, w[:, K1:])
+    y, s, q = _lib().conv1x1_cat_bnsums(g, mask, x2, sc, bi, w_cat, bias, mean, invstd)
+    _close(_rows(y), _rows(_lib().conv1x1_cat(g, mask, x2, sc, bi, w_cat, bias)), 1e-2)
     m = (torch.addcmul(bi, _rows(x2), sc) > 0).double()
     dyv = _rows(y).double() * m
     s_ref = dyv.sum(0)

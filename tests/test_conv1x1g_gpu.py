@@ -160,20 +160,25 @@ def test_cat(cuda, bnsums, N, K1, K2, H):
     c1 = torch.randn(K1, device=cuda, generator=g0) * 0.1
     sc = torch.rand(K2, device=cuda, generator=g0) + 0.5
     bi = torch.randn(K2, device=cuda, generator=g0) * 0.1
-    w = (torch.randn(K2, K1 + K2, device=cuda, generator=g0) * (K1 + K2) ** -0.5).bfloat16()
-    a_cat, c_cat = torch.cat([a1, sc]), torch.cat([c1, bi])
+    w = torch.randn(K2, K1 + K2, device=cuda, generator=g0) * (K1 + K2) ** -0.5
+    from consensusml_amd.ops.conv import fold_cat
+    w_cat, bias = fold_cat(w[:, :K1], a1, c1, w[:, K1:])
     L = _lib()
     if not bnsums:
-        a, b = _both(lambda: L.conv1x1_cat(g, mask, x2, a_cat, c_cat, w))
+        a, b = _both(lambda: L.conv1x1_cat(g, mask, x2, sc, bi, w_cat, bias))
         assert torch.equal(a, b)
-        u = (a1 * (_bits(mask, K1) * _rows(g)) + c1).bfloat16().float()
+        u = a1 * (_bits(mask, K1) * _rows(g)) + c1
         v = torch.relu(_rows(x2) * sc + bi).bfloat16().float()
-        assert _rel(_rows(b), torch.cat([u, v], 1) @ w.float().t()) < 1e-2
+        assert _rel(_rows(b), torch.cat([u, v], 1) @ w.t()) < 1e-2
+        xr = torch.relu(x2)   # identity second source (a ReLU output staged as is)
+        a, b = _both(lambda: L.conv1x1_cat(g, mask, xr, None, None, w_cat, bias))
+        assert torch.equal(a, b)
+        assert _rel(_rows(b), torch.cat([u, _rows(xr)], 1) @ w.t()) < 1e-2
         return
     X = _rows(x2).double()
     mean = X.mean(0).float()
     invstd = (X.var(0, unbiased=False) + 1e-5).rsqrt().float()
-    a, b = _both(lambda: L.conv1x1_cat_bnsums(g, mask, x2, a_cat, c_cat, w, mean, invstd))
+    a, b = _both(lambda: L.conv1x1_cat_bnsums(g, mask, x2, sc, bi, w_cat, bias, mean, invstd))
     assert torch.equal(a[0], b[0])
     torch.testing.assert_close(a[1], b[1], rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(a[2], b[2], rtol=1e-5, atol=1e-3)
@@ -191,5 +196,13 @@ def test_cat_bnres(cuda, N, K1, K2, Co, H):
     w = (torch.randn(Co, K1 + K2, device=cuda, generator=g0) * (K1 + K2) ** -0.5).bfloat16()
     esc = torch.rand(Co, device=cuda, generator=g0) + 0.5
     ebi = torch.randn(Co, device=cuda, generator=g0) * 0.1
-    a, b = _both(lambda: _lib().conv1x1_cat_bnres(x1, x2, sc, bi, w.contiguous(), esc, ebi))
+    a, b = _both(lambda: _lib().conv1x1_cat_bnres(x1, x2, sc[:K1], bi[:K1], sc[K1:], bi[K1:],
+                                                  w.contiguous(), esc, ebi))
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    xr = torch.relu(x2)   # identity second source == max(x * 1 + 0, 0) of a ReLU output
+    a, b = _both(lambda: _lib().conv1x1_cat_bnres(x1, xr, sc[:K1], bi[:K1], None, None,
+                                                  w.contiguous(), esc, ebi))
+    one, zero = torch.ones(K2, device=cuda), torch.zeros(K2, device=cuda)
+    c = _lib().conv1x1_cat_bnres(x1, xr, sc[:K1], bi[:K1], one, zero, w.contiguous(), esc, ebi)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert torch.equal(a[0], c[0]) and torch.equal(a[1], c[1])

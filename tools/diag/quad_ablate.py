@@ -51,10 +51,10 @@ def build(name, dev):
         g = nh(torch.randn(B, K1, H, H, device=dev, generator=g0).bfloat16())
         x2 = nh(torch.randn(B, K2, H, H, device=dev, generator=g0).bfloat16())
         mask = torch.randint(0, 256, (M, K1 // 8), device=dev, dtype=torch.uint8)
-        a = torch.rand(K1 + K2, device=dev) + 0.5
-        c = torch.randn(K1 + K2, device=dev) * 0.1
+        bias = torch.randn(N, device=dev) * 0.1
         w = (torch.randn(N, K1 + K2, device=dev, generator=g0) * 0.03).bfloat16()
-        return lambda: L.conv1x1_cat(g, mask, x2, a, c, w), 2.0 * M * (K1 + K2) * N
+        # (a downsample data gradient: the block input x2 is staged as is)
+        return lambda: L.conv1x1_cat(g, mask, x2, None, None, w, bias), 2.0 * M * (K1 + K2) * N
     if kind == "cat_bnres":
         x1 = nh(torch.randn(B, K1, H, H, device=dev, generator=g0).bfloat16())
         x2 = nh(torch.randn(B, K2, H, H, device=dev, generator=g0).bfloat16())
@@ -62,7 +62,8 @@ def build(name, dev):
         bi = torch.randn(K1 + K2, device=dev) * 0.1
         w = (torch.randn(N, K1 + K2, device=dev, generator=g0) * 0.03).bfloat16()
         es, eb = torch.rand(N, device=dev) + 0.5, torch.randn(N, device=dev) * 0.1
-        return lambda: L.conv1x1_cat_bnres(x1, x2, sc, bi, w, es, eb), 2.0 * M * (K1 + K2) * N
+        return (lambda: L.conv1x1_cat_bnres(x1, x2, sc[:K1], bi[:K1], None, None, w, es, eb),
+                2.0 * M * (K1 + K2) * N)
     if kind == "link":
         x = nh(torch.randn(B, K1, H, H, device=dev, generator=g0).bfloat16())
         w = (torch.randn(N, K1, device=dev, generator=g0) * 0.03).bfloat16()
