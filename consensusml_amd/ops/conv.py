@@ -323,7 +323,7 @@ class _RecomputeTailFn(torch.autograd.Function):
             if extra is not None:
                 gy = (gy + extra).contiguous(memory_format=torch.channels_last)
         M = gy.numel() // gy.shape[1]
-        Co, Ci = w.shape[0], w.shape[1]
+        Co = w.shape[0]
         dev = gy.device
         L = lib()
         P, s = L.wgrad1x1_ex(gy, z, sc, bi, 2, mask, _const(Co, 1.0, dev), None,
@@ -332,17 +332,12 @@ class _RecomputeTailFn(torch.autograd.Function):
         ctx.gram = None
         if gram is None:
             gram, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
-        W3 = w.reshape(Co, Ci).float()
-        q = torch.addcmul((W3 * P).sum(1), m3, s, value=-1.0).mul_(i3)
-        ca, cb, cc, dg3, db3 = L.bn_bwd_coeffs(s, q, g3, m3, i3, M)
-        cbW3 = cb[:, None] * W3   # diag(b) W3, shared by dW3 and G
-        dw = None
-        if ctx.needs_input_grad[5]:
-            # dW3 = diag(a) P + diag(b) W3 Gram + c cy^T (fewer small launches as addcmul / addmm)
-            dw = torch.addmm(torch.addcmul(torch.outer(cc, cy), ca[:, None], P), cbW3, gram)
-            dw = dw.to(w.dtype).view_as(w)
-        G = W3.t() @ cbW3
-        w_cat, bias = fold_cat(W3.t(), ca, cc, G.t())
+        # q, bn3's coefficients, dW3 = diag(a) P + diag(b) W3 Gram + c cy^T and the folded
+        # w_cat = [W3^T diag(a) | W3^T diag(b) W3], bias = W3^T c: two launches (tail_prep.hip)
+        need_dw = ctx.needs_input_grad[5]
+        w_cat, bias, dw, dg3, db3 = L.tail_bwd_prep(w.contiguous(), P, s, gram, cy, g3, m3, i3, M,
+                                                    need_dw)
+        dw = dw.view_as(w) if need_dw else None
         dz, dg2, db2 = _cat_dgrad_bn2(L, gy, mask, z, sc, bi, w_cat, bias, g2, b2, mean2, invstd2)
         dres = None
         if ctx.needs_input_grad[8]:
@@ -414,7 +409,7 @@ class _RecomputeDownTailFn(torch.autograd.Function):
             if extra is not None:
                 gy = (gy + extra).contiguous(memory_format=torch.channels_last)
         M = gy.numel() // gy.shape[1]
-        Co, P_, Cin = w3.shape[0], w3.shape[1], wd.shape[1]
+        Co = w3.shape[0]
         dev = gy.device
         L = lib()
         one, zero = _const(Co, 1.0, dev), _const(Co, 0.0, dev)
@@ -425,28 +420,18 @@ class _RecomputeDownTailFn(torch.autograd.Function):
         if gram3 is None:
             gram3, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
             gramd, cx = L.wgrad1x1_ex(x, x, None, None, 0, None, None, None, None, True)
-        W3 = w3.reshape(Co, P_).float()
-        Wd = wd.reshape(Co, Cin).float()
-        q3 = torch.addcmul((W3 * P3).sum(1), m3, s, value=-1.0).mul_(i3)
-        qd = torch.addcmul((Wd * Pd).sum(1), md, s, value=-1.0).mul_(idd)
-        a3, b3c, c3, dg3, db3 = L.bn_bwd_coeffs(s, q3, g3, m3, i3, M)
-        ad, bdc, cd, dgd, dbd = L.bn_bwd_coeffs(s, qd, gd, md, idd, M)
-        bW3, bWd = b3c[:, None] * W3, bdc[:, None] * Wd
-        dw3 = dwd = None
-        if ctx.needs_input_grad[5]:
-            dw3 = torch.addmm(torch.addcmul(torch.outer(c3, cy), a3[:, None], P3), bW3, gram3)
-            dw3 = dw3.to(w3.dtype).view_as(w3)
-        if ctx.needs_input_grad[11]:
-            dwd = torch.addmm(torch.addcmul(torch.outer(cd, cx), ad[:, None], Pd), bWd, gramd)
-            dwd = dwd.to(wd.dtype).view_as(wd)
-        G3 = W3.t() @ bW3
-        w_cat3, bias3 = fold_cat(W3.t(), a3, c3, G3.t())
+        # each branch's backward algebra in two launches (tail_prep.hip; see _RecomputeTailFn)
+        nd3, ndd = ctx.needs_input_grad[5], ctx.needs_input_grad[11]
+        w_cat3, bias3, dw3, dg3, db3 = L.tail_bwd_prep(w3.contiguous(), P3, s, gram3, cy, g3, m3,
+                                                       i3, M, nd3)
+        w_catd, biasd, dwd, dgd, dbd = L.tail_bwd_prep(wd.contiguous(), Pd, s, gramd, cx, gd, md,
+                                                       idd, M, ndd)
+        dw3 = dw3.view_as(w3) if nd3 else None
+        dwd = dwd.view_as(wd) if ndd else None
         dz, dg2, db2 = _cat_dgrad_bn2(L, gy, mask, z, sc, bi, w_cat3, bias3, g2, b2, mean2,
                                       invstd2)
         dx = None
         if ctx.needs_input_grad[10]:
-            Gd = Wd.t() @ bWd
-            w_catd, biasd = fold_cat(Wd.t(), ad, cd, Gd.t())
             dx = L.conv1x1_cat(gy, mask, x, None, None, w_catd, biasd)   # x staged as is
         return (dz, dg2, db2, None, None, dw3, dg3, db3, None, None, dx, dwd, dgd, dbd) + \
             (None,) * 5

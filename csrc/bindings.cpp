@@ -741,14 +741,16 @@ std::vector<Tensor> bn_stats_gram(const Tensor& G, const Tensor& cy, const Tenso
   TORCH_CHECK(M >= 1, "bn_stats_gram: M >= 1");
   const c10::DeviceGuard guard(w.device());
   auto f32 = w.options().dtype(at::kFloat);
+  TORCH_CHECK(P % 64 == 0, "bn_stats_gram: P must be a multiple of 64");
   Tensor mean = at::empty({Co}, f32), invstd = at::empty({Co}, f32);
+  Tensor part = at::empty({P / 64, Co}, w.options().dtype(at::kDouble));
   CML_CHECK_HIP(cml::launch_bn_stats_gram(G.data_ptr<float>(), cp, w.data_ptr(), static_cast<int>(P),
                                           static_cast<int>(Co), M, static_cast<float>(eps),
                                           static_cast<float>(momentum), mean.data_ptr<float>(),
                                           invstd.data_ptr<float>(),
                                           opt_ptr<float>(rmean, at::kFloat, "running_mean", Co),
                                           opt_ptr<float>(rvar, at::kFloat, "running_var", Co),
-                                          cur_stream()));
+                                          part.data_ptr<double>(), cur_stream()));
   return {mean, invstd};
 }
 
@@ -770,6 +772,45 @@ std::vector<Tensor> bn_bwd_coeffs(const Tensor& sdz, const Tensor& sdzx, const T
                                           cc.data_ptr<float>(), dg.data_ptr(), db.data_ptr(),
                                           cur_stream()));
   return {ca, cb, cc, dg, db};
+}
+
+// Recompute-tail backward algebra in two launches (tail_prep.hip): W bf16 [Co, p] (any shape with
+// Co * p elements, contiguous), P fp32 [Co, p], s fp32 [Co], gram fp32 [p, p], cy fp32 [p], gamma
+// bf16 [Co], mean / invstd fp32 [Co] -> {w_cat bf16 [p, Co + p], bias fp32 [p], dW bf16 [Co, p]
+// (undefined unless need_dw), dgamma, dbeta bf16 [Co]}.
+std::vector<Tensor> tail_bwd_prep(const Tensor& W, const Tensor& P, const Tensor& s,
+                                  const Tensor& gram, const Tensor& cy, const Tensor& gamma,
+                                  const Tensor& mean, const Tensor& invstd, int64_t M,
+                                  bool need_dw) {
+  TORCH_CHECK(P.dim() == 2, "tail_bwd_prep: P [Co, p]");
+  const int64_t Co = P.size(0), p = P.size(1);
+  TORCH_CHECK(W.is_cuda() && W.scalar_type() == at::kBFloat16 && W.is_contiguous() &&
+                  W.numel() == Co * p, "tail_bwd_prep: W contiguous bf16 with Co * p elements");
+  TORCH_CHECK(gamma.scalar_type() == at::kBFloat16 && gamma.is_contiguous() && gamma.numel() == Co,
+              "tail_bwd_prep: gamma bf16 [Co]");
+  TORCH_CHECK(Co % 64 == 0 && p % 64 == 0, "tail_bwd_prep: Co % 64 == 0 and p % 64 == 0");
+  check_dev(W, "W");
+  check_dev(gamma, "gamma");
+  const float* Pp = opt_ptr<const float>(P, at::kFloat, "P", Co * p);
+  const float* sp = opt_ptr<const float>(s, at::kFloat, "s", Co);
+  const float* gp = opt_ptr<const float>(gram, at::kFloat, "gram", p * p);
+  const float* cp = opt_ptr<const float>(cy, at::kFloat, "cy", p);
+  const float* mp = opt_ptr<const float>(mean, at::kFloat, "mean", Co);
+  const float* ip = opt_ptr<const float>(invstd, at::kFloat, "invstd", Co);
+  const c10::DeviceGuard guard(W.device());
+  auto f32 = P.options();
+  Tensor work = at::empty({static_cast<int64_t>(
+                              cml::tail_bwd_prep_work_floats(static_cast<int>(Co), static_cast<int>(p)))},
+                          f32);
+  Tensor wcat = at::empty({p, Co + p}, W.options());
+  Tensor bias = at::empty({p}, f32);
+  Tensor dW = need_dw ? at::empty({Co, p}, W.options()) : Tensor();
+  Tensor dg = at::empty_like(gamma), db = at::empty_like(gamma);
+  CML_CHECK_HIP(cml::launch_tail_bwd_prep(
+      W.data_ptr(), Pp, sp, gp, cp, gamma.data_ptr(), mp, ip, static_cast<int>(Co),
+      static_cast<int>(p), M, work.data_ptr<float>(), need_dw ? dW.data_ptr() : nullptr,
+      wcat.data_ptr(), bias.data_ptr<float>(), dg.data_ptr(), db.data_ptr(), cur_stream()));
+  return {wcat, bias, dW, dg, db};
 }
 
 // Fused 1x1 conv forward (conv1x1.hip): x [N, K, H, W] NHWC bf16, w [Cout, K, 1, 1] bf16 ->
@@ -1796,6 +1837,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "conv1x1_cat + the sums of the BN + ReLU backward its output feeds");
   m.def("bn_affine", &bn_affine, "BN affine (gamma invstd, beta - mean sc) of batch statistics");
   m.def("bn_bwd_apply", &bn_bwd_apply, "apply half of a BN + ReLU backward from its sums");
+  m.def("tail_bwd_prep", &tail_bwd_prep,
+        "recompute-tail backward algebra: {w_cat, bias, dW, dgamma, dbeta}");
   m.def("conv1x1_cat", &conv1x1_cat, "two-source (masked | BN-ReLU or identity) 1x1 conv along K, + bias");
   m.def("split_fold", &split_fold, "fixed-order fold of a split-K partial slab");
   m.def("wgrad1x1_ex", &wgrad1x1_ex, py::arg("dy"), py::arg("x"), py::arg("pro_sc") = py::none(),

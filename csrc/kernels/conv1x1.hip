@@ -436,69 +436,94 @@ __global__ __launch_bounds__(256) void conv1x1_bnbwd_finalize_kernel(
 
 // BN training statistics of z = y W^T (W [Co][P] bf16: the 1x1 conv's weights) from the Gram matrix
 // G = y^T y [P][P] and the column sums cy of y over M rows (fp32: wgrad1x1_ex's products of the
-// same bf16 y the conv multiplies): mean = W cy / M, var = w^T G w / M - mean^2, in fp64. These are
-// the statistics of the fp32-accumulated products; the statistics-only conv pass they replace saw
-// the same products rounded to bf16. 16 output channels per workgroup; running statistics updated
-// as conv1x1_bn_finalize_kernel does.
+// same bf16 y the conv multiplies): mean = W cy / M, var = w^T G w / M - mean^2, partial inner
+// products (G w)_i in fp32 and everything after in fp64. These are the statistics of the
+// fp32-accumulated products; the statistics-only conv pass they replace saw the same products
+// rounded to bf16.
+// Two launches. bn_stats_gram_kernel: workgroup (channel block of kGramNC, 64-row chunk jc of G)
+// computes q_part = sum_i w_i sum_{j in jc} G[j][i] w_j (each thread 4 consecutive i, one float4
+// of a G row per step) into an fp64 slab [P / 64][Co]; bn_stats_gram_fin_kernel (one wave per
+// channel) sums the chunks in a fixed order (deterministic), adds S = w . cy and writes the
+// statistics. ~0.7 TFLOP-equivalent of fp32 FMA per ResNet-50 step spread over (Co / 8) x (P / 64)
+// workgroups (round 2's kernel read all of G in one workgroup per 16 channels with one float per
+// load: ~45 us per call at any batch, 0.75 ms per step).
+constexpr int kGramNC = 8;
+
 __global__ __launch_bounds__(256) void bn_stats_gram_kernel(
-    const float* __restrict__ G, const float* __restrict__ cy, const uint16_t* __restrict__ W, int P,
-    int Co, int64_t M, float eps, float momentum, float* __restrict__ mean,
-    float* __restrict__ invstd, float* __restrict__ rmean, float* __restrict__ rvar) {
-  constexpr int NC = 16;                   // output channels per workgroup
-  extern __shared__ float ws[];            // [NC][P] weights of this workgroup's channels
-  __shared__ double red[4][2 * NC];
-  const int n0 = blockIdx.x * NC, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const float* __restrict__ G, const uint16_t* __restrict__ W, int P, int Co,
+    double* __restrict__ part) {
+  constexpr int NC = kGramNC;
+  extern __shared__ float ws[];            // [P][NC] weights of this workgroup's channels
+  __shared__ double red[4][NC];
+  const int n0 = blockIdx.x * NC, jc = blockIdx.y * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int Q4 = P / 4;                              // float4 columns of a G row
+  const int TG = Q4 < 256 ? Q4 : 256;                // threads per row subgroup
+  const int JP = 256 / TG, JL = 64 / JP;             // row subgroups, rows per subgroup
+  const int jp = tid / TG, q0 = tid - jp * TG;
   for (int e = tid; e < NC * P; e += 256) {
     const int c = e / P, j = e - c * P;
-    ws[e] = n0 + c < Co ? bf2f(W[static_cast<int64_t>(n0 + c) * P + j]) : 0.f;
+    ws[j * NC + c] = n0 + c < Co ? bf2f(W[static_cast<int64_t>(n0 + c) * P + j]) : 0.f;
   }
   __syncthreads();
-  double q[NC], sm[NC];
+  double q[NC];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    q[c] = 0.0;
-    sm[c] = 0.0;
-  }
-  // (G w)_i (fp32 over P <= 1024 terms), then w_i (G w)_i summed in fp64. G is symmetric, so
-  // (G w)_i = sum_j G[j][i] w_j: for each j the lanes read consecutive floats of row j
-  // (coalesced; reading row i per lane touched 64 cache lines per load)
-  for (int i = tid; i < P; i += 256) {
-    float t[NC];
+  for (int c = 0; c < NC; ++c) q[c] = 0.0;
+  const int j0 = jc + jp * JL;
+  // G is symmetric: (G w)_i = sum_j G[j][i] w_j, the lanes reading consecutive float4 of row j
+  for (int qi = q0; qi < Q4; qi += TG) {
+    const int i = 4 * qi;
+    float t[NC][4];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) t[c] = 0.f;
-    for (int j = 0; j < P; ++j) {
-      const float g = G[static_cast<int64_t>(j) * P + i];
+    for (int c = 0; c < NC; ++c) t[c][0] = t[c][1] = t[c][2] = t[c][3] = 0.f;
+    const float* gp = G + static_cast<int64_t>(j0) * P + i;
+#pragma unroll 8
+    for (int j = 0; j < JL; ++j) {
+      const float4 g = *reinterpret_cast<const float4*>(gp + static_cast<int64_t>(j) * P);
 #pragma unroll
-      for (int c = 0; c < NC; ++c) t[c] = fmaf(g, ws[c * P + j], t[c]);
+      for (int c = 0; c < NC; ++c) {
+        const float w = ws[(j0 + j) * NC + c];
+        t[c][0] = fmaf(g.x, w, t[c][0]);
+        t[c][1] = fmaf(g.y, w, t[c][1]);
+        t[c][2] = fmaf(g.z, w, t[c][2]);
+        t[c][3] = fmaf(g.w, w, t[c][3]);
+      }
     }
-    const double yi = cy[i];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const double wi = ws[c * P + i];
-      q[c] = fma(wi, static_cast<double>(t[c]), q[c]);
-      sm[c] = fma(wi, yi, sm[c]);
-    }
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        q[c] = fma(static_cast<double>(ws[(i + k) * NC + c]), static_cast<double>(t[c][k]), q[c]);
   }
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
+  for (int c = 0; c < NC; ++c)
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      q[c] += __shfl_xor(q[c], o, 64);
-      sm[c] += __shfl_xor(sm[c], o, 64);
-    }
-  }
+    for (int o = 32; o >= 1; o >>= 1) q[c] += __shfl_xor(q[c], o, 64);
   if (lane == 0) {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      red[wv][c] = q[c];
-      red[wv][NC + c] = sm[c];
-    }
+    for (int c = 0; c < NC; ++c) red[wv][c] = q[c];
   }
   __syncthreads();
-  if (tid >= NC || n0 + tid >= Co) return;
-  const int n = n0 + tid;
-  const double Q = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-  const double S = red[0][NC + tid] + red[1][NC + tid] + red[2][NC + tid] + red[3][NC + tid];
+  if (tid < NC && n0 + tid < Co)
+    part[static_cast<int64_t>(blockIdx.y) * Co + n0 + tid] =
+        red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+}
+
+__global__ __launch_bounds__(256) void bn_stats_gram_fin_kernel(
+    const double* __restrict__ part, const float* __restrict__ cy, const uint16_t* __restrict__ W,
+    int P, int Co, int64_t M, float eps, float momentum, float* __restrict__ mean,
+    float* __restrict__ invstd, float* __restrict__ rmean, float* __restrict__ rvar) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= Co) return;
+  double S = 0.0;
+  for (int i = lane; i < P; i += 64)
+    S = fma(static_cast<double>(bf2f(W[static_cast<int64_t>(n) * P + i])), static_cast<double>(cy[i]), S);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) S += __shfl_xor(S, o, 64);
+  if (lane != 0) return;
+  double Q = 0.0;
+  for (int c = 0; c < P / 64; ++c) Q += part[static_cast<int64_t>(c) * Co + n];
   const double mu = S / static_cast<double>(M);
   double var = Q / static_cast<double>(M) - mu * mu;
   if (var < 0.0) var = 0.0;
@@ -804,14 +829,17 @@ hipError_t launch_conv1x1_link_s2(const void* x, const void* w, void* y, const v
 
 hipError_t launch_bn_stats_gram(const float* G, const float* cy, const void* w, int P, int Co,
                                 int64_t M, float eps, float momentum, float* mean, float* invstd,
-                                float* rmean, float* rvar, hipStream_t st) {
-  if (P < 1 || P > 2048 || Co < 1 || M < 1) return hipErrorInvalidValue;
-  if (16 * P * sizeof(float) > 65536)
+                                float* rmean, float* rvar, double* part, hipStream_t st) {
+  if (P < 64 || P % 64 || P > 2048 || Co < 1 || M < 1 || !part) return hipErrorInvalidValue;
+  const size_t lds = static_cast<size_t>(kGramNC) * P * sizeof(float);
+  if (lds > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bn_stats_gram_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 16 * P * 4);
-  bn_stats_gram_kernel<<<(Co + 15) / 16, 256, 16 * P * sizeof(float), st>>>(
-      G, cy, reinterpret_cast<const uint16_t*>(w), P, Co, M, eps, momentum, mean, invstd, rmean,
-      rvar);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  const uint16_t* W = reinterpret_cast<const uint16_t*>(w);
+  bn_stats_gram_kernel<<<dim3((Co + kGramNC - 1) / kGramNC, P / 64), 256, lds, st>>>(G, W, P, Co,
+                                                                                     part);
+  bn_stats_gram_fin_kernel<<<(Co + 3) / 4, 256, 0, st>>>(part, cy, W, P, Co, M, eps, momentum, mean,
+                                                         invstd, rmean, rvar);
   return hipGetLastError();
 }
 

@@ -408,9 +408,21 @@ hipError_t launch_conv1x1_link_s2(const void* x, const void* w, void* y, const v
                                   int Nimg, int H, int W, int K, int N, hipStream_t st);
 // BN training statistics (mean, invstd; running stats updated when given) of z = y W^T from the
 // Gram matrix G = y^T y [P][P] and column sums cy [P] of y over M rows; W [Co][P] bf16 (conv1x1.hip).
+// part: fp64 scratch [P / 64][Co]; P % 64 == 0.
 hipError_t launch_bn_stats_gram(const float* G, const float* cy, const void* w, int P, int Co,
                                 int64_t M, float eps, float momentum, float* mean, float* invstd,
-                                float* rmean, float* rvar, hipStream_t st);
+                                float* rmean, float* rvar, double* part, hipStream_t st);
+// Recompute-tail backward algebra (tail_prep.hip): from conv3's W bf16 [Co][p], P = u^T y2 and
+// s = sum u (fp32), y2's Gram / column sums and bn3's gamma (bf16) / mean / invstd: bn3's backward
+// coefficients, dgamma / dbeta (bf16 [Co]), conv3's weight gradient dW (bf16 [Co][p], skipped when
+// null), w_cat = [W^T diag(a) | W^T diag(b) W] (bf16 [p][Co + p]) and bias = W^T c (fp32 [p]).
+// work: tail_bwd_prep_work_floats(Co, p) fp32 scratch. Co % 64 == 0, p % 64 == 0.
+hipError_t launch_tail_bwd_prep(const void* W, const float* P, const float* s, const float* gram,
+                                const float* cy, const void* gamma, const float* mean,
+                                const float* invstd, int Co, int p, int64_t M, float* work,
+                                void* dW, void* wcat, float* bias, void* dgamma, void* dbeta,
+                                hipStream_t st);
+size_t tail_bwd_prep_work_floats(int Co, int p);
 hipError_t launch_bn_bwd_coeffs(const float* sdz, const float* sdzx, const void* gamma,
                                 const float* mean, const float* invstd, int C, int64_t M,
                                 float* ca, float* cb, float* cc, void* dgamma, void* dbeta,

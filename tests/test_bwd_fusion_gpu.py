@@ -419,7 +419,7 @@ def test_downsample_recompute_tail(cuda, cin, planes, H, stride):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("N,K,H", [(2, 64, 28), (3, 128, 14), (2, 256, 9), (1, 128, 3)])
+@pytest.mark.parametrize("N,K,H", [(2, 64, 28), (3, 128, 14), (2, 256, 9), (1, 128, 3), (1, 512, 5)])
 def test_bn_stats_gram_vs_fp64(cuda, N, K, H):
     """bn3's statistics from y2's Gram matrix (wgrad1x1_ex mode 3 + bn_stats_gram) equal the fp64
     statistics of z3 = y2 W^T (y2 = relu(z sc + bi) in bf16), running stats included."""
@@ -495,3 +495,40 @@ def test_bn_affine_bit_identical(cuda, C):
     sc = gam.float() * invstd
     assert torch.equal(ab[0], sc)
     assert torch.equal(ab[1], bet.float() - mean * sc)
+
+
+@pytest.mark.parametrize("Co,p,need_dw", [(256, 64, True), (1024, 256, True), (512, 128, False),
+                                          (2048, 512, True)])
+def test_tail_bwd_prep_vs_torch(cuda, Co, p, need_dw):
+    """tail_bwd_prep's two launches against the fp64 PyTorch algebra they replace: bn3's backward
+    coefficients / dgamma / dbeta, dW3 = diag(a) P + diag(b) W Gram + c cy^T, and the folded
+    w_cat = [W^T diag(a) | W^T diag(b) W], bias = W^T c."""
+    g0 = torch.Generator(device=cuda).manual_seed(41)
+    M = 4096
+    w = (torch.randn(Co, p, 1, 1, device=cuda, generator=g0) * p ** -0.5).bfloat16()
+    y = torch.relu(torch.randn(M, p, device=cuda, generator=g0)).bfloat16().float()
+    u = torch.randn(M, Co, device=cuda, generator=g0).bfloat16().float()
+    P, s = (u.t() @ y).contiguous(), u.sum(0)
+    gram, cy = (y.t() @ y).contiguous(), y.sum(0)
+    g3 = (torch.rand(Co, device=cuda, generator=g0) + 0.5).bfloat16()
+    m3 = torch.randn(Co, device=cuda, generator=g0) * 0.1
+    i3 = torch.rand(Co, device=cuda, generator=g0) + 0.5
+    w_cat, bias, dw, dg, db = _lib().tail_bwd_prep(w, P, s, gram, cy, g3, m3, i3, M, need_dw)
+    W = w.view(Co, p).double()
+    Pd, sd, Gd, cyd = P.double(), s.double(), gram.double(), cy.double()
+    q = ((W * Pd).sum(1) - m3.double() * sd) * i3.double()
+    a = i3.double() * g3.double()
+    b = -a * i3.double() * q / M
+    c = -a * sd / M - b * m3.double()
+    _close(dg, q, 1e-2)
+    _close(db, sd, 1e-2)
+    if need_dw:
+        dw_ref = a[:, None] * Pd + b[:, None] * (W @ Gd) + c[:, None] * cyd[None, :]
+        _close(dw, dw_ref, 1e-2)
+    else:
+        assert dw is None
+    wc_ref = torch.cat([W.t() * a[None, :], W.t() @ (b[:, None] * W)], 1)
+    assert w_cat.shape == (p, Co + p)
+    _close(w_cat[:, :Co], wc_ref[:, :Co], 1e-2)
+    _close(w_cat[:, Co:], wc_ref[:, Co:], 1e-2)
+    _close(bias, W.t() @ c, 1e-4)
