@@ -60,7 +60,7 @@ class PerfPolicy:
     fuse_down_bn: bool = True             # relu(bn3(z) + bn_d(zd)) as one op
     gram_stats: bool = True               # recompute-tail BN statistics from the Gram matrix
     cat_bnsums: bool = True               # bn2's backward sums in the cat GEMM's epilogue
-    cat_bnsums_maxc: int = 64
+    cat_bnsums_maxc: int = 256
     s2_link_dgrad: bool = True            # compact stride-2 gradient added in conv1's dgrad
     bn_affine_kernel: bool = True         # one-launch BN affine (sc, bi)
     # ---------------------------------------------------------------- 3x3 convolutions
@@ -99,7 +99,7 @@ class PerfPolicy:
             fuse_down_bn=_env_bool("CML_FUSE_DOWN_BN", True),
             gram_stats=_env_bool("CML_GRAM_STATS", True),
             cat_bnsums=_env_bool("CML_CAT_BNSUMS", True),
-            cat_bnsums_maxc=_env_int("CML_CAT_BNSUMS_MAXC", 64),
+            cat_bnsums_maxc=_env_int("CML_CAT_BNSUMS_MAXC", 256),
             s2_link_dgrad=_env_bool("CML_S2_LINK_DGRAD", True),
             bn_affine_kernel=_env_bool("CML_BN_AFFINE_KERNEL", True),
             own_dgrad3x3=_env_bool("CML_DGRAD3X3", True),

@@ -8,7 +8,10 @@ import sys
 
 CLASSES = [
     ("BatchNorm passes (bn_act.hip)", r"cml::.*bn_(apply|stats|bwd|finalize|apply2|bwd_apply2|bwd_reduce2)"),
-    ("fused 1x1 conv + BN (conv1x1.hip)", r"cml::.*(conv1x1_bn|conv1x1_bnbwd|bn_bwd_coeffs)"),
+    ("fused 1x1 conv + BN (conv1x1.hip, conv1x1g.hip)",
+     r"cml::.*(conv1x1_bn|conv1x1_bnbwd|bn_bwd_coeffs|conv1x1g_|conv1x1q_)"),
+    ("3x3 weight gradient (wgrad3x3.hip)", r"cml::.*wgrad3x3"),
+    ("recompute-tail algebra (tail_prep.hip, bn_stats_gram)", r"cml::.*(tail_|bn_stats_gram)"),
     ("1x1 weight gradient (wgrad1x1.hip)", r"cml::.*wgrad1x1"),
     ("3x3 conv fwd + data gradient (conv_gemm.hip)", r"cml::.*conv_gemm"),
     ("stem / pool (stem_conv.hip, pool.hip)", r"cml::.*(stem_|maxpool|bn_relu_max)"),
