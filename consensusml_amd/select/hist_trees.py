@@ -41,6 +41,26 @@ def bin_with(X: torch.Tensor, edges: torch.Tensor) -> torch.Tensor:
     return torch.searchsorted(edges, Xt, right=False).to(torch.uint8).t().contiguous()
 
 
+def exact_bins(X: torch.Tensor, max_bins: int = 128):
+    """Rank bins: every distinct value of a feature gets its own bin, edges at the midpoints
+    between consecutive distinct values (R randomForest's candidate thresholds), padded with
+    +inf. Returns (Xb uint8 [n, p], edges [p, max_bins - 1], B = most distinct values of any
+    feature), or None when some feature has more than ``max_bins`` distinct values."""
+    X = X.float()
+    S, _ = torch.sort(X, 0)
+    mids = (S[1:] + S[:-1]) / 2
+    valid = S[1:] > S[:-1]                                   # [n - 1, p]
+    B = int(valid.sum(0).max().item()) + 1 if X.shape[0] > 1 else 1
+    if B > max_bins:
+        return None
+    keys = torch.where(valid, mids, torch.full_like(mids, float("inf")))
+    keys, _ = torch.sort(keys, 0)                             # valid midpoints first, ascending
+    edges = torch.full((X.shape[1], max_bins - 1), float("inf"), device=X.device)
+    k = min(max_bins - 1, keys.shape[0])
+    edges[:, :k] = keys[:k].t()
+    return bin_with(X, edges), edges, max(B, 2)
+
+
 @dataclass
 class TreeBatch:
     feature: torch.Tensor     # [T, nodes] int64, -1 = leaf
@@ -59,10 +79,10 @@ class TreeBatch:
         node = torch.zeros(T, m, dtype=torch.long, device=Xb.device)
         ar = torch.arange(m, device=Xb.device)
         for _ in range(self.depth):
-            f = torch.gather(self.feature, 1, node)
+            f = torch.gather(self.feature, 1, node).long()
             leaf = f < 0
             b = Xb[ar[None].expand(T, m), f.clamp_min(0)].long()
-            thr = torch.gather(self.thr_bin, 1, node)
+            thr = torch.gather(self.thr_bin, 1, node).long()
             child = 2 * node + 1 + (b > thr).long()
             node = torch.where(leaf, node, child)
         return node
@@ -191,6 +211,129 @@ def _split_search_torch(Xb, stat, feats, local, alive, tot, tt, L, kk, n_bins, c
     j = arg // (n_bins - 1)
     b = arg % (n_bins - 1)
     return best, j, b
+
+
+def grow_sampled(Xb: torch.Tensor, stat: torch.Tensor, depth: int, k: int, n_bins: int,
+                 gen: torch.Generator, importance: Optional[torch.Tensor] = None) -> TreeBatch:
+    """``grow`` (Gini) with the candidate features drawn inside tree_hist.hip's
+    split_search_sampled (k distinct features per node, seeded per level from ``gen``) and up to
+    128 bins; stops at the first level where no node splits. Node arrays are stored compact
+    (int16 features, uint8 thresholds)."""
+    from ..ops.native import lib
+    dev = Xb.device
+    T, n, _ = stat.shape
+    nodes = 2 ** (depth + 1) - 1
+    feature = torch.full((T, nodes), -1, dtype=torch.int16, device=dev)
+    thr = torch.zeros(T, nodes, dtype=torch.uint8, device=dev)
+    value = torch.zeros(T, nodes, device=dev)
+    node_of = torch.zeros(T, n, dtype=torch.long, device=dev)
+    alive = stat[..., 0] != 0
+    tt = torch.arange(T, device=dev)
+    stat = stat.float().contiguous()
+    used = depth
+    for level in range(depth + 1):
+        L = 2 ** level
+        base = L - 1
+        local = (node_of - base).clamp(0, L - 1)
+        key = (tt[:, None] * L + local).view(-1)
+        tot = torch.zeros(T * L, 2, device=dev)
+        m = alive.view(-1)
+        tot.index_add_(0, key[m], stat.view(-1, 2)[m])
+        tot = tot.view(T, L, 2)
+        value[:, base:base + L] = tot[..., 1] / tot[..., 0].clamp_min(1e-12)
+        if level == depth:
+            break
+        nl = torch.where(alive, node_of - base, torch.full_like(node_of, -1)).int().contiguous()
+        seed = int(torch.randint(0, 2 ** 62, (1,), generator=gen))
+        best, fbest, b = lib().split_search_sampled(Xb, nl, stat, tot.contiguous(), L, k, n_bins,
+                                                    0, 1.0, 1.0, seed)
+        split = torch.isfinite(best) & (best > 1e-12)
+        if not bool(split.any()):
+            used = level
+            break
+        fbest = fbest.long()
+        feature[:, base:base + L] = torch.where(split, fbest, torch.full_like(fbest, -1)).to(
+            torch.int16)
+        thr[:, base:base + L] = b.to(torch.uint8)
+        if importance is not None:
+            gsum = torch.where(split, best, torch.zeros_like(best))
+            importance.index_add_(0, fbest.view(-1), gsum.view(-1).double())
+        nf = torch.gather(feature[:, base:base + L], 1, local).long()
+        nb = torch.gather(thr[:, base:base + L], 1, local).long()
+        xb = Xb[torch.arange(n, device=dev)[None].expand(T, n), nf.clamp_min(0)].long()
+        child = 2 * node_of + 1 + (xb > nb).long()
+        at_level = (node_of >= base) & (node_of < base + L)
+        node_of = torch.where(at_level & (nf >= 0), child, node_of)
+        alive = alive & (nf >= 0) & at_level
+    return TreeBatch(feature, thr, value, max(used, 1))
+
+
+class ExactForest:
+    """R randomForest on the device: CART with EXACT thresholds (rank bins -- one bin per distinct
+    training value, edges at the midpoints; ``exact_bins``), bootstrap counts as sample weights,
+    sqrt(p) distinct candidate features per node drawn in the split kernel, grown level by level
+    for a chunk of trees at a time until every node is pure or ``max_depth``. MeanDecreaseGini,
+    predict and proximity as ``HistForest``. Falls back to 128 quantile bins when a feature has
+    more than 128 distinct values (then the thresholds are approximate)."""
+
+    def __init__(self, n_estimators: int = 500, max_depth: int = 13, max_features: str = "sqrt",
+                 seed: int = 8, chunk: int = 512):
+        self.n, self.depth, self.mf, self.seed, self.chunk = \
+            n_estimators, max_depth, max_features, seed, chunk
+
+    def fit(self, X: torch.Tensor, y: torch.Tensor) -> "ExactForest":
+        dev = X.device
+        n, p = X.shape
+        ex = exact_bins(X)
+        if ex is None:
+            Xb, self.edges = quantile_bins(X, 128)
+            B = 128
+            self.exact = False
+        else:
+            Xb, self.edges, B = ex
+            self.exact = True
+        Xb = Xb.contiguous()
+        k = max(1, int(math.sqrt(p))) if self.mf == "sqrt" else (
+            max(1, int(math.log2(p))) if self.mf == "log2" else p)
+        gen = torch.Generator().manual_seed(self.seed)
+        yv = y.float().to(dev)
+        self.importance = torch.zeros(p, dtype=torch.float64, device=dev)
+        self.batches = []
+        self.depth_used = 0
+        for s in range(0, self.n, self.chunk):
+            T = min(self.chunk, self.n - s)
+            draws = torch.randint(0, n, (T, n), generator=gen).to(dev)
+            w = torch.zeros(T, n, device=dev)
+            w.scatter_add_(1, draws, torch.ones(T, n, device=dev))
+            stat = torch.stack([w, w * yv[None]], 2)
+            tb = grow_sampled(Xb, stat, self.depth, k, B, gen, importance=self.importance)
+            self.depth_used = max(self.depth_used, tb.depth)
+            self.batches.append(tb)
+        self.mean_decrease_gini = (self.importance / self.n).cpu()
+        return self
+
+    def predict_proba(self, X: torch.Tensor) -> torch.Tensor:
+        Xb = bin_with(X, self.edges)
+        p1 = torch.cat([tb.predict(Xb) for tb in self.batches]).mean(0)
+        return torch.stack([1 - p1, p1], 1)
+
+    def predict(self, X: torch.Tensor) -> torch.Tensor:
+        return (self.predict_proba(X)[:, 1] > 0.5).long()
+
+    def proximity(self, X: torch.Tensor) -> torch.Tensor:
+        """Fraction of trees in which two rows share a leaf ([m, m]), from the leaf ids."""
+        Xb = bin_with(X, self.edges)
+        m = Xb.shape[0]
+        P = torch.zeros(m, m, device=Xb.device)
+        for tb in self.batches:
+            leaves = tb.apply(Xb)                                      # [T, m]
+            P += (leaves[:, :, None] == leaves[:, None, :]).float().sum(0)
+        return P / self.n
+
+    @property
+    def feature_importances_(self) -> torch.Tensor:
+        imp = self.importance.cpu()
+        return imp / imp.sum() if imp.sum() > 0 else imp
 
 
 class HistForest:

@@ -264,6 +264,10 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
                 if tree_method == "hist":
                     from .hist_trees import HistForest
                     rf = HistForest(nt, max_depth=10, seed=20).fit(Xtr, ytr)
+                elif Xtr.is_cuda:
+                    # exact thresholds, level-synchronous on the device (tree_hist.hip)
+                    from .hist_trees import ExactForest
+                    rf = ExactForest(nt, seed=20).fit(Xtr, ytr)
                 else:
                     from .trees import RandomForest
                     rf = RandomForest(nt, seed=20).fit(Xtr, ytr)

@@ -1617,6 +1617,37 @@ std::vector<Tensor> split_search(const Tensor& Xb, const Tensor& node_local, con
   return {gain, slot, bin};
 }
 
+// split_search with in-kernel candidate sampling (kk distinct features per node from `seed`) and up
+// to 128 bins: {gain [T, L], feature [T, L], bin [T, L]} (select/hist_trees.py ExactForest).
+std::vector<Tensor> split_search_sampled(const Tensor& Xb, const Tensor& node_local,
+                                         const Tensor& stat, const Tensor& tot, int64_t L,
+                                         int64_t kk, int64_t n_bins, int64_t crit, double lam,
+                                         double min_child, int64_t seed) {
+  check_dev(Xb, "Xb");
+  TORCH_CHECK(Xb.scalar_type() == at::kByte && Xb.dim() == 2 && Xb.is_contiguous(), "Xb: uint8 [n, p]");
+  const int64_t n = Xb.size(0), p = Xb.size(1);
+  TORCH_CHECK(node_local.is_cuda() && node_local.scalar_type() == at::kInt && node_local.dim() == 2 &&
+                  node_local.size(1) == n && node_local.is_contiguous(), "node_local: int32 [T, n]");
+  const int64_t T = node_local.size(0);
+  TORCH_CHECK(stat.is_cuda() && stat.scalar_type() == at::kFloat && stat.is_contiguous() &&
+                  stat.numel() == T * n * 2, "stat: fp32 [T, n, 2]");
+  TORCH_CHECK(tot.is_cuda() && tot.scalar_type() == at::kFloat && tot.is_contiguous() &&
+                  tot.numel() == T * L * 2, "tot: fp32 [T, L, 2]");
+  TORCH_CHECK(n_bins >= 2 && n_bins <= 128 && kk >= 1 && kk <= 512 && kk <= p && p <= 65536,
+              "split_search_sampled: 2 <= n_bins <= 128, 1 <= kk <= min(512, p), p <= 65536");
+  const c10::DeviceGuard guard(Xb.device());
+  Tensor gain = at::empty({T, L}, stat.options());
+  Tensor feat = at::empty({T, L}, node_local.options());
+  Tensor bin = at::empty({T, L}, node_local.options());
+  CML_CHECK_HIP(cml::launch_split_search_sampled(
+      Xb.data_ptr<uint8_t>(), node_local.data_ptr<int>(), stat.data_ptr<float>(),
+      tot.data_ptr<float>(), static_cast<int>(T), static_cast<int>(L), static_cast<int>(n),
+      static_cast<int>(p), static_cast<int>(kk), static_cast<int>(n_bins), static_cast<int>(crit),
+      static_cast<float>(lam), static_cast<float>(min_child), static_cast<uint64_t>(seed),
+      gain.data_ptr<float>(), feat.data_ptr<int>(), bin.data_ptr<int>(), cur_stream()));
+  return {gain, feat, bin};
+}
+
 float* f32p(const Tensor& t, const char* name, int64_t numel) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == numel,
               name, ": contiguous fp32 GPU tensor with ", numel, " elements");
@@ -1837,6 +1868,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "conv1x1_cat + the sums of the BN + ReLU backward its output feeds");
   m.def("bn_affine", &bn_affine, "BN affine (gamma invstd, beta - mean sc) of batch statistics");
   m.def("bn_bwd_apply", &bn_bwd_apply, "apply half of a BN + ReLU backward from its sums");
+  m.def("split_search_sampled", &split_search_sampled,
+        "tree split search with in-kernel candidate sampling, <= 128 bins -> {gain, feature, bin}");
   m.def("tail_bwd_prep", &tail_bwd_prep,
         "recompute-tail backward algebra: {w_cat, bias, dW, dgamma, dbeta}");
   m.def("conv1x1_cat", &conv1x1_cat, "two-source (masked | BN-ReLU or identity) 1x1 conv along K, + bias");

@@ -235,6 +235,13 @@ hipError_t launch_split_search(const uint8_t* Xb, const int* node_local, const f
                                const int* feats, const float* tot, int T, int L, int n, int p,
                                int kk, int B, int crit, float lam, float min_child,
                                float* out_gain, int* out_slot, int* out_bin, hipStream_t stream);
+// Exact-threshold variant: B <= 128 rank bins, kk distinct candidate features per (tree, node)
+// drawn in the kernel from `seed` (no feats tensor); returns the winning feature id.
+hipError_t launch_split_search_sampled(const uint8_t* Xb, const int* node_local,
+                                       const float* stat, const float* tot, int T, int L, int n,
+                                       int p, int kk, int B, int crit, float lam, float min_child,
+                                       uint64_t seed, float* out_gain, int* out_feat, int* out_bin,
+                                       hipStream_t stream);
 // Batched FISTA logistic lasso (lasso_prox.hip), problems along columns (B contiguous):
 // r = (sigmoid(z + v0) - y) M / nb [n, B] (+ rsum = column sums of r), then the prox / restart /
 // momentum step in place on v, beta [p, B] (tk, mom [B]; v0, b0 [B] when fitting an intercept).

@@ -70,3 +70,27 @@ def test_rf_and_xgb_resultslists():
         perf = xg[f"rep{i}"]["performance_testset"]
         assert abs(perf["mean_err"] - df.loc[f"rep{i}", "mean_err"]) < 1e-12
         assert int(perf["confusion_matrix"].sum()) == 20
+
+
+def test_exact_bins_are_distinct_value_ranks():
+    """exact_bins: one bin per distinct value (its rank), edges at the midpoints between
+    consecutive distinct values, +inf padding; x <= edge_b <=> bin <= b for any x."""
+    from consensusml_amd.select.hist_trees import exact_bins
+    g = torch.Generator().manual_seed(3)
+    X = torch.randint(0, 7, (40, 5), generator=g).float() * 0.5
+    X[:, 4] = torch.randn(40, generator=g)          # 40 distinct values
+    Xb, edges, B = exact_bins(X)
+    for f in range(5):
+        u = torch.unique(X[:, f])
+        rank = torch.searchsorted(u, X[:, f])
+        assert torch.equal(Xb[:, f].long(), rank)
+        k = u.numel()
+        torch.testing.assert_close(edges[f, :k - 1], (u[1:] + u[:-1]) / 2)
+        assert torch.isinf(edges[f, k - 1:]).all()
+    assert B == 40
+    t = torch.randn(100, 5, generator=g)
+    tb = bin_with(t, edges)
+    for f in range(5):
+        for b in range(3):
+            assert torch.equal(t[:, f] <= edges[f, b], tb[:, f].long() <= b)
+    assert exact_bins(torch.randn(300, 2, generator=g), max_bins=128) is None

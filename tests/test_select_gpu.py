@@ -93,3 +93,27 @@ def test_fista_gpu_kernels_match_cpu(cuda, intercept, alpha):
     # identical support on clearly nonzero coefficients
     sig = bc.abs() > 1e-2
     assert torch.equal(sig, bg.cpu().abs() > 1e-2) or (sig ^ (bg.cpu().abs() > 1e-2)).sum() <= 2
+
+
+def test_exact_forest_gpu(cuda):
+    """ExactForest (exact thresholds, in-kernel candidate sampling): fits the training rows,
+    ranks the informative features first like the CPU exact RandomForest, the same total
+    MeanDecreaseGini per tree, and a symmetric proximity matrix with a unit diagonal."""
+    from consensusml_amd.select.hist_trees import ExactForest
+    from consensusml_amd.select.trees import RandomForest
+    g = torch.Generator().manual_seed(5)
+    n, p = 93, 400
+    X = torch.randn(n, p, generator=g)
+    y = (X[:, :3].sum(1) > 0).long()
+    ef = ExactForest(400, seed=2).fit(X.to(cuda), y.to(cuda))
+    assert ef.exact
+    assert (ef.predict(X.to(cuda)).cpu() == y).float().mean() > 0.95
+    imp = ef.mean_decrease_gini
+    assert {0, 1, 2} <= set(torch.topk(imp, 6).indices.tolist())
+    rf = RandomForest(100, seed=2).fit(X, y)
+    assert {0, 1, 2} <= set(torch.topk(rf.mean_decrease_gini, 6).indices.tolist())
+    # fully grown trees on the same rows: the Gini decreases add up to about the same per tree
+    ratio = float(imp.sum() / rf.mean_decrease_gini.sum())
+    assert 0.8 < ratio < 1.25, ratio
+    P = ef.proximity(X.to(cuda)).cpu()
+    assert torch.allclose(P, P.t()) and torch.allclose(P.diag(), torch.ones(n))

@@ -47,6 +47,21 @@ def main():
     K = max(a.steps, 0)
     if K:
         lines.append(f"per step (over {K} steps): {total/1e3/K:.2f} ms kernel time")
+    if rows:
+        # busy time = union of the dispatch intervals (overlapping kernels counted once); the rest
+        # of the window's span is idle GPU time (launch gaps, host waits)
+        iv = sorted((s_, e_) for _, s_, e_ in rows)
+        busy, cs, ce = 0, iv[0][0], iv[0][1]
+        for s_, e_ in iv[1:]:
+            if s_ > ce:
+                busy += ce - cs
+                cs, ce = s_, e_
+            else:
+                ce = max(ce, e_)
+        busy += ce - cs
+        span = max(e_ for _, e_ in iv) - iv[0][0]
+        lines.append(f"GPU busy {busy/1e6:.2f} ms of a {span/1e6:.2f} ms window "
+                     f"({100 * busy / max(span, 1):.1f} %)")
     lines += ["", "| kernel | calls | total ms | avg us | % |" + (" ms/step |" if K else ""),
               "|---|---|---|---|---|" + ("---|" if K else "")]
     for name, (n, t) in items[: a.top]:

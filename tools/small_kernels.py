@@ -61,8 +61,19 @@ def main():
     for e in events:
         if e.device_type.name != "CPU" or not getattr(e, "kernels", None):
             continue
-        fr = [s for s in (e.stack or []) if "consensusml_amd" in s]
-        where = fr[0].split("consensusml_amd/")[-1] if fr else "(no package frame)"
+        # innermost package frame on this op's or an enclosing op's stack; backward ops run on the
+        # autograd thread (no Python stack): name the enclosing autograd Function / op chain
+        where, p, chain = None, e, []
+        while p is not None and where is None:
+            fr = [s for s in (p.stack or []) if "consensusml_amd" in s]
+            if fr:
+                where = fr[0].split("consensusml_amd/")[-1]
+            else:
+                chain.append(p.name)
+                p = getattr(p, "cpu_parent", None)
+        if where is None:
+            fn = [n for n in chain if "Backward" in n or n.startswith("_")]
+            where = fn[0] if fn else " < ".join(chain[:3])
         for k in e.kernels:
             kernels += 1
             total_us += k.duration
