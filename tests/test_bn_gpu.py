@@ -124,11 +124,9 @@ def test_conv1x1_gemm_matches_conv(cuda, cin, cout, mode):
     m = R.Conv1x1(cin, cout).to(cuda, torch.bfloat16).to(memory_format=torch.channels_last)
     x = torch.randn(4, cin, 9, 7, device=cuda, dtype=torch.bfloat16).to(memory_format=torch.channels_last)
     x.requires_grad_(True)
-    R.CONV1X1_GEMM = mode
-    try:
+    from consensusml_amd import perf
+    with perf.use_policy(perf.policy().replace(conv1x1_gemm=mode)):
         y = m(x)
-    finally:
-        R.CONV1X1_GEMM = "auto"
     assert y.is_contiguous(memory_format=torch.channels_last)
     g = torch.randn_like(y)
     y.backward(g)
@@ -155,20 +153,17 @@ def test_residual_link_matches_autograd_add(cuda, gemm):
         torch.nn.init.normal_(m.bn3.weight, 1.0, 0.1)
     x0 = torch.randn(4, 32, 10, 10, device=cuda).to(torch.bfloat16).to(memory_format=torch.channels_last)
     res = []
-    R.CONV1X1_GEMM = gemm
+    from consensusml_amd import perf
     from consensusml_amd.ops.bn import TAP_STATS
     TAP_STATS.update(parked=0, fallback=0)
-    try:
-        for link in (True, False):
-            R.RESIDUAL_LINK = link
+    mode = {False: "miopen", True: "gemm"}.get(gemm, gemm)
+    for link in (True, False):
+        with perf.use_policy(perf.policy().replace(conv1x1_gemm=mode, residual_link=link)):
             net.zero_grad(set_to_none=True)
             x = x0.clone().requires_grad_(True)
             y = net(x)
             y.float().square().sum().backward()
             res.append((x.grad.clone(), [p.grad.clone() for p in net.parameters()]))
-    finally:
-        R.RESIDUAL_LINK = True
-        R.CONV1X1_GEMM = "auto"
     # the downsample branch's backward runs before conv1's: the tap always parks
     assert TAP_STATS["fallback"] == 0
     assert TAP_STATS["parked"] == (0 if gemm is False else 1)
@@ -226,13 +221,13 @@ def test_stem_pad4_matches_conv(cuda):
     m = R.resnet_tiny().to(cuda, torch.bfloat16).to(memory_format=torch.channels_last)
     x = torch.randn(3, 3, 33, 31, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     outs = []
+    from consensusml_amd import perf
     for pad in (True, False):
-        R.STEM_PAD4 = pad
-        m.zero_grad(set_to_none=True)
-        y = m.stem(x)
-        y.float().square().sum().backward()
-        outs.append((y.float(), m.conv1.weight.grad.float().clone()))
-    R.STEM_PAD4 = True
+        with perf.use_policy(perf.policy().replace(stem_pad4=pad)):
+            m.zero_grad(set_to_none=True)
+            y = m.stem(x)
+            y.float().square().sum().backward()
+            outs.append((y.float(), m.conv1.weight.grad.float().clone()))
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(outs[0][1], outs[1][1], rtol=2e-2, atol=0.5)
     assert m.conv1.weight.grad.shape == (8, 3, 7, 7)

@@ -173,12 +173,10 @@ def test_resnet50_fused_conv_bn_matches_unfused(cuda):
         if name != "fp32":
             m = m.to(torch.bfloat16).to(memory_format=torch.channels_last)
             xx = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        R.FUSED_CONV1X1 = name == "fused"
-        try:
+        from consensusml_amd import perf
+        with perf.use_policy(perf.policy().replace(fused_conv1x1=name == "fused")):
             loss = F.cross_entropy(m(xx).float(), y)
             loss.backward()
-        finally:
-            R.FUSED_CONV1X1 = True
         out[name] = (loss.item(), torch.cat([p.grad.float().flatten() for p in m.parameters()]),
                      {k: b.float().clone() for k, b in m.named_buffers()})
     cf = F.cosine_similarity(out["fused"][1], out["fp32"][1], dim=0).item()

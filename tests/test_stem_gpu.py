@@ -87,14 +87,12 @@ def test_stem_model_path_matches_unfused(cuda):
     g32 = m32.conv1.weight.grad.float()
     out = {}
     for fused in (True, False):
-        R.FUSE_STEM_CONV = fused
-        try:
+        from consensusml_amd import perf
+        with perf.use_policy(perf.policy().replace(fuse_stem_conv=fused)):
             m.zero_grad(set_to_none=True)
             loss = F.cross_entropy(m(x).float(), y)
             loss.backward()
             out[fused] = (loss.item(), m.conv1.weight.grad.float().clone())
-        finally:
-            R.FUSE_STEM_CONV = True
     assert abs(out[True][0] - loss32.item()) < 0.05 * max(1.0, abs(loss32.item()))
     ef, eu = _rel(out[True][1], g32), _rel(out[False][1], g32)
     assert ef <= max(1.5 * eu, 0.1), (ef, eu)
@@ -161,16 +159,14 @@ def test_stem_pool_link_second_gradient(cuda):
     ref = [m32.conv1.weight.grad, m32.bn1.weight.grad, m32.bn1.bias.grad]
     out = {}
     for on in (True, False):
-        R.POOL_LINK = on
+        from consensusml_amd import perf
         TAP_STATS.update(parked=0, fallback=0)
-        try:
+        with perf.use_policy(perf.policy().replace(pool_link=on)):
             m.zero_grad(set_to_none=True)
             F.cross_entropy(m(x).float(), y).backward()
             out[on] = [m.conv1.weight.grad.float().clone(), m.bn1.weight.grad.float().clone(),
                        m.bn1.bias.grad.float().clone()]
             stats = dict(TAP_STATS)
-        finally:
-            R.POOL_LINK = True
         assert stats["fallback"] == 0
         if on:
             assert stats["parked"] >= 1

@@ -197,9 +197,7 @@ def test_mfma_attention_matches_sdpa_path(cuda):
     torch.manual_seed(11)
     qkv = torch.randn(4, 128, 3 * 12 * 64, device=cuda).to(torch.bfloat16)
     a = T.fused_qkv_attention(qkv, 12, 64)
-    T.ATTN_KERNEL = False
-    try:
+    from consensusml_amd import perf
+    with perf.use_policy(perf.policy().replace(attn_kernel=False)):
         b = T.fused_qkv_attention(qkv, 12, 64)
-    finally:
-        T.ATTN_KERNEL = True
     torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2)

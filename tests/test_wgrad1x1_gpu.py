@@ -38,14 +38,12 @@ def test_conv1x1_module_own_wgrad_matches_miopen(cuda):
         memory_format=torch.channels_last)
     out = {}
     for own in (True, False):
-        R.OWN_WGRAD1X1 = own
-        try:
+        from consensusml_amd import perf
+        with perf.use_policy(perf.policy().replace(own_wgrad1x1=own)):
             conv.weight.grad = None
             x.grad = None
             conv(x).backward(dy)
             out[own] = (conv.weight.grad.float().clone(), x.grad.float().clone())
-        finally:
-            R.OWN_WGRAD1X1 = True
     assert _rel(out[True][0], out[False][0]) < 1e-2
     assert _rel(out[True][1], out[False][1]) < 1e-2
 
