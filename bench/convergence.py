@@ -76,13 +76,23 @@ def accuracy(tr, batches: int, bs: int, train_mode: bool) -> float:
     return hit / tot
 
 
-def run(name: str, pol, cfg, steps: int, eval_batches: int, eval_bs: int) -> dict:
+def run(name: str, pol, cfg, steps: int, eval_batches: int, eval_bs: int,
+        perturb: float = 0.0) -> dict:
+    """``perturb`` > 0: multiply every initial master weight by (1 + perturb N(0, 1)) (a fixed
+    generator) -- the same model up to rounding-level noise, to measure how far two runs drift
+    apart from numerics alone (the noise floor a fused-vs-library difference is judged against)."""
     from consensusml_amd import perf
     from consensusml_amd.parallel.dist import DistInfo
     from consensusml_amd.trainer.trainer import ConsensusTrainer
     dev = torch.device("cuda", 0)
     with perf.use_policy(pol):
         tr = ConsensusTrainer(cfg, info=DistInfo(0, 1, 0, dev, "none"))
+        if perturb > 0:
+            gen = torch.Generator(device=dev)
+            gen.manual_seed(4242)
+            m = tr.engine.master
+            m.mul_(1 + perturb * torch.randn(m.shape, generator=gen, device=dev))
+            tr.engine.sync_params_from_master()
         losses = []
         t0 = time.perf_counter()
         for s in range(steps):
@@ -111,7 +121,7 @@ def compare(a: dict, b: dict, every: int = 10) -> dict:
     rel = [abs(la[i] - lb[i]) / max(abs(lb[i]), 1e-12) for i in idx]
     # once both runs fit the task the losses are ~1e-3 and their ratio is noise: the tolerance
     # used by the tests is |la - lb| <= 0.1 * max(la, lb) + 0.05 nats
-    excess = [abs(la[i] - lb[i]) - (0.1 * max(abs(la[i]), abs(lb[i])) + 0.05) for i in idx]
+    absd = [abs(la[i] - lb[i]) for i in idx]
     stat_rel = {}
     for k, v in b["stats"].items():
         u = a["stats"][k]
@@ -119,7 +129,7 @@ def compare(a: dict, b: dict, every: int = 10) -> dict:
     return {"steps": [i + 1 for i in idx], "loss_a": [la[i] for i in idx],
             "loss_b": [lb[i] for i in idx], "loss_rel_diff": rel,
             "max_loss_rel_diff": max(rel) if rel else None,
-            "max_loss_tol_excess": max(excess) if excess else None,
+            "mean_loss_abs_diff": sum(absd) / len(absd) if absd else None,
             "acc_train_mode_diff_points": 100 * (a["acc_train_mode"] - b["acc_train_mode"]),
             "acc_eval_mode_diff_points": 100 * (a["acc_eval_mode"] - b["acc_eval_mode"]),
             "bn_stats_max_rel_diff": max(stat_rel.values()),

@@ -23,15 +23,21 @@ def test_fused_step_trains_like_library(cuda):
     fused = C.run("fused", perf.policy(), C.make_cfg(batch, 224, 10, 0.05), steps, 4, batch)
     lib = C.run("library", perf.PerfPolicy.library(), C.make_cfg(batch, 224, 10, 0.05), steps, 4,
                 batch)
+    # noise floor: the library path again from weights perturbed at bf16-rounding level
+    libp = C.run("library_perturbed", perf.PerfPolicy.library(), C.make_cfg(batch, 224, 10, 0.05),
+                 steps, 4, batch, perturb=2.0 ** -8)
     cmp = C.compare(fused, lib)
+    noise = C.compare(libp, lib)
+    print("fused vs library:", cmp, "\nperturbed library vs library:", noise, flush=True)
     # both learn the 10-class template task (chance: 2.3 nats, 10 %)
     for r in (fused, lib):
         assert sum(r["losses"][-5:]) / 5 < 0.5 * r["losses"][0], r["losses"]
         assert r["acc_train_mode"] > 0.8, r["acc_train_mode"]
-    # the two paths reduce in different orders, so after tens of SGD steps their trajectories
-    # drift apart chaotically; losses agree within 10 % + 0.05 nats (near-zero late losses make a
-    # pure ratio meaningless), BN running statistics agree to 5 % on the median layer
-    assert cmp["max_loss_tol_excess"] <= 0.0, cmp
-    assert abs(cmp["acc_train_mode_diff_points"]) <= 5.0, cmp
-    assert cmp["bn_stats_median_rel_diff"] < 0.05, cmp
-    assert cmp["bn_stats_max_rel_diff"] < 0.25, cmp
+    # SGD at this batch amplifies any rounding difference, so after the first steps the fused path
+    # is judged against that noise floor: early losses agree closely, later losses, accuracies and
+    # BN running statistics within a small multiple of the floor
+    assert cmp["loss_rel_diff"][0] < 0.05, (cmp, noise)
+    assert cmp["mean_loss_abs_diff"] <= 3 * noise["mean_loss_abs_diff"] + 0.02, (cmp, noise)
+    assert abs(cmp["acc_train_mode_diff_points"]) <= 5.0, (cmp, noise)
+    assert cmp["bn_stats_median_rel_diff"] <= 3 * noise["bn_stats_median_rel_diff"] + 0.01, \
+        (cmp, noise)
