@@ -592,6 +592,19 @@ def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tenso
         dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
 
 
+def _w3x3_layouts(w: torch.Tensor, want_wf: bool):
+    """(wf or None, wr): the implicit-GEMM forward layout wf [Co, 9 Ci] (k = (3 ky + kx) Ci + ci)
+    and the data-gradient layout wr [Ci, 9 Co] (rotated, transposed: wr[ci][(3 ky + kx) Co + co] =
+    w[co][ci][2 - ky][2 - kx]) of a 3x3 weight, in one launch (``conv3x3_wlayouts``) instead of a
+    permute copy, a flip and another permute copy per conv and step."""
+    if w.is_cuda and w.dtype == torch.bfloat16:
+        wf, wr = lib().conv3x3_wlayouts(w, want_wf)
+        return wf, wr
+    Co, Ci = w.shape[0], w.shape[1]
+    wf = w.permute(0, 2, 3, 1).reshape(Co, 9 * Ci).contiguous() if want_wf else None
+    return wf, w.flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co).contiguous()
+
+
 class _Conv3x3Fn(torch.autograd.Function):
     """3x3 / stride 1 / padding 1 conv: forward on MIOpen, data gradient on ``conv_gemm.hip`` (the
     forward implicit GEMM of dy with the rotated, transposed weights; 15-27 % faster than MIOpen's
@@ -609,9 +622,10 @@ class _Conv3x3Fn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            Co, Ci = w.shape[0], w.shape[1]
             # w_rot[ci][ky][kx][co] = w[co][ci][2 - ky][2 - kx], flattened k = tap Co + co
-            wr = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co).contiguous()
+            wr = getattr(ctx, "wr", None)
+            if wr is None:
+                wr = _w3x3_layouts(w, False)[1]
             dx = lib().conv_gemm(dy, wr, 9, _zero_row(dy.device))
         if ctx.needs_input_grad[1]:
             dw = _wgrad3x3(dy, x, w)
@@ -625,11 +639,11 @@ class _Conv3x3BNStatsFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, rmean, rvar, eps, momentum):
-        Co, Ci = w.shape[0], w.shape[1]
-        wf = w.permute(0, 2, 3, 1).reshape(Co, 9 * Ci).contiguous()   # k = (3 ky + kx) Ci + ci
+        wf, wr = _w3x3_layouts(w, True)   # both layouts now: the backward reuses wr
         y, mean, invstd = lib().conv_gemm_bn(x, wf, 9, _zero_row(x.device), rmean, rmean, rvar,
                                              eps, momentum)
         ctx.save_for_backward(x, w)
+        ctx.wr = wr
         ctx.mark_non_differentiable(mean, invstd)
         ctx.set_materialize_grads(False)   # no zero-filled grads for the statistics outputs
         return y, mean, invstd
@@ -653,11 +667,11 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
         L = lib()
         y1 = L.bn_fwd(z1, None, g1, b1, None, None, mean1, invstd1, eps1, momentum, True, False,
                       False)[0]
-        Co, Ci = w.shape[0], w.shape[1]
-        wf = w.permute(0, 2, 3, 1).reshape(Co, 9 * Ci).contiguous()   # k = (3 ky + kx) Ci + ci
+        wf, wr = _w3x3_layouts(w, True)   # both layouts now: the backward reuses wr
         z2, m2, i2 = L.conv_gemm_bn(y1, wf, 9, _zero_row(z1.device), rmean, rmean, rvar, eps,
                                     momentum)
         ctx.save_for_backward(z1, g1, b1, mean1, invstd1, y1, w)
+        ctx.wr = wr
         ctx.mark_non_differentiable(m2, i2)
         ctx.set_materialize_grads(False)   # no zero-filled grads for the statistics outputs
         return z2, m2, i2
@@ -667,9 +681,7 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
         z1, g1, b1, mean1, invstd1, y1, w = ctx.saved_tensors
         dz2 = dz2.contiguous(memory_format=torch.channels_last)
         L = lib()
-        Co, Ci = w.shape[0], w.shape[1]
-        # w_rot[ci][ky][kx][co] = w[co][ci][2 - ky][2 - kx], flattened k = tap Co + co
-        wr = w.flip(2, 3).permute(1, 2, 3, 0).reshape(Ci, 9 * Co).contiguous()
+        wr = ctx.wr   # rotated / transposed layout, made by the forward
         sc, bi = _affine(g1, b1, mean1, invstd1)
         dy1, s1, q1 = L.conv_gemm_bnsums(dz2, wr, 9, _zero_row(dz2.device), z1, sc, bi, mean1,
                                          invstd1)

@@ -4,9 +4,13 @@
 forward : MFMA implicit-GEMM conv that also accumulates the BN statistics (no statistics pass,
           no channel-padding pass for 3-channel images), then the pool that applies BN + ReLU to
           every window tap (the BN output is never stored).
-backward: the pool gather (already ReLU-masked, with its channel sums = dbeta), then ONE MFMA pass
-          that produces the conv weight gradient through the BatchNorm plus dgamma: the BN input
-          gradient is never formed (see the kernel header for the algebra).
+backward: ONE MFMA pass that produces the conv weight gradient through the BatchNorm plus dgamma
+          (the BN input gradient is never formed; see the kernel header for the algebra), reading
+          the pool's OUTPUT gradient: each pixel's pool input gradient (ReLU-masked by the
+          forward's argmax) is gathered from the windows that contain it while staging, after a
+          small pass for its channel sums (= dbeta). PerfPolicy.stem_pool_gather off: the pool
+          backward writes the full-resolution gradient (4x the pooled size) and the MFMA pass
+          reads it back.
 
 Other inputs (CPU, fp32, other stem shapes, images that need an input gradient, eval-mode
 backward) take the module path.
@@ -16,6 +20,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ..perf import policy as _P
 from .native import lib
 
 
@@ -50,8 +55,11 @@ class _StemFn(torch.autograd.Function):
         dy2 = ctx.link.take_tensor() if ctx.link is not None else None
         if dy2 is not None and dy2.shape != dy.shape:
             dy, dy2 = dy + dy2, None
-        g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3], dy2)
-        dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gamma, gsum)
+        if _P().stem_pool_gather:
+            dw, dg, db = lib().stem_wgrad_pool(dy, idx, dy2, z, x, mean, invstd, gamma)
+        else:
+            g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3], dy2)
+            dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gamma, gsum)
         wt, gt, bt = ctx.dtypes
         return None, dw.to(wt), dg.to(gt), db.to(bt), None, None, None, None, None, None
 

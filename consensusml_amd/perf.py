@@ -42,6 +42,7 @@ class PerfPolicy:
     fuse_stem_conv: bool = True           # stem_conv.hip conv + BN stats, one-pass weight grad
     fuse_stem_pool: bool = True           # BN + ReLU + max-pool in one pass
     pool_link: bool = True                # pool backward sums layer1.0's downsample gradient
+    stem_pool_gather: bool = True         # stem wgrad gathers the pool input gradient itself
     stem_pad4: bool = True                # 3 -> 4 input channels for MIOpen's NHWC kernels
     nhwc_avgpool: bool = True             # global average pool with an NHWC backward
     # ---------------------------------------------------------------- 1x1 convolutions
@@ -81,6 +82,7 @@ class PerfPolicy:
             fuse_stem_conv=_env_bool("CML_FUSE_STEM_CONV", True),
             fuse_stem_pool=_env_bool("CML_FUSE_STEM_POOL", True),
             pool_link=_env_bool("CML_POOL_LINK", True),
+            stem_pool_gather=_env_bool("CML_STEM_POOL_GATHER", True),
             stem_pad4=_env_bool("CML_STEM_PAD4", True),
             nhwc_avgpool=_env_bool("CML_NHWC_AVGPOOL", True),
             conv1x1_gemm=_env_str("CML_CONV1X1_GEMM", "auto"),

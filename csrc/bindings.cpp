@@ -534,6 +534,69 @@ std::vector<Tensor> stem_wgrad(const Tensor& g_in, const Tensor& z, const Tensor
   return {dw, dg, db};
 }
 
+// Stem backward straight from the max-pool's OUTPUT gradient dy [N, 64, PH, PW] (+ an optional
+// second gradient dy2 of the same shape) and the pool's argmax bytes idx: the routed channel sums
+// (launch_pool_gsum), then stem_wgrad gathering each pixel's pool input gradient from its windows
+// (the full-resolution pool gradient is never written). Same outputs as stem_wgrad.
+std::vector<Tensor> stem_wgrad_pool(const Tensor& dy_in, const Tensor& idx,
+                                    const optional<Tensor>& dy2_in, const Tensor& z,
+                                    const Tensor& x, const Tensor& mean, const Tensor& invstd,
+                                    const Tensor& gamma) {
+  check_nhwc(x, "x");
+  check_nhwc(z, "z");
+  Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc(dy, "dy");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const int64_t PH = (OH - 1) / 2 + 1, PW = (OW - 1) / 2 + 1;
+  TORCH_CHECK(C == 3 || C == 4, "stem_wgrad_pool: 3 or 4 input channels");
+  TORCH_CHECK(z.size(0) == N && z.size(1) == 64 && z.size(2) == OH && z.size(3) == OW,
+              "stem_wgrad_pool: z shape");
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == 64 && dy.size(2) == PH && dy.size(3) == PW,
+              "stem_wgrad_pool: dy must be the 3x3 / s2 / p1 pool output gradient of z");
+  // idx: the pool forward's argmax bytes, [N, PH, PW, 64] contiguous (bn_relu_maxpool_fwd)
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == dy.numel() && idx.is_contiguous() &&
+                  idx.device() == dy.device(),
+              "stem_wgrad_pool: idx");
+  Tensor dy2;
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = dy2_in->contiguous(at::MemoryFormat::ChannelsLast);
+    check_nhwc(dy2, "dy2");
+    TORCH_CHECK(dy2.sizes() == dy.sizes() && dy2.device() == dy.device(), "stem_wgrad_pool: dy2");
+  }
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && invstd.scalar_type() == at::kFloat &&
+                  mean.numel() == 64 && invstd.numel() == 64 && mean.is_contiguous() &&
+                  invstd.is_contiguous(), "stem_wgrad_pool: fp32 mean / invstd [64]");
+  TORCH_CHECK(gamma.scalar_type() == at::kBFloat16 && gamma.is_contiguous() && gamma.numel() == 64,
+              "stem_wgrad_pool: bf16 gamma [64]");
+  const c10::DeviceGuard guard(x.device());
+  auto f32 = x.options().dtype(at::kFloat);
+  const int64_t P = N * PH * PW;
+  Tensor gsum = at::empty({64}, f32);
+  Tensor work = at::empty({static_cast<int64_t>(cml::pool_gsum_workspace_floats(P, 64))}, f32);
+  Tensor dsum;
+  if (dy2.defined()) dsum = at::empty_like(dy);
+  CML_CHECK_HIP(cml::launch_pool_gsum(dy.data_ptr(), dy2.defined() ? dy2.data_ptr() : nullptr,
+                                      idx.data_ptr(), dsum.defined() ? dsum.data_ptr() : nullptr,
+                                      gsum.data_ptr<float>(), work.data_ptr<float>(), P, 64,
+                                      cur_stream()));
+  const Tensor& pg = dsum.defined() ? dsum : dy;
+  const int grid = cml::stem_bwd_grid(N, OH, OW, C);
+  const int64_t pw = static_cast<int64_t>(cml::stem_wgrad_part_floats());
+  Tensor part = at::empty({grid, pw}, f32);
+  Tensor tot = at::empty({pw}, x.options().dtype(at::kDouble));
+  Tensor dw = at::empty({64, C, 7, 7}, f32);
+  Tensor dg = at::empty({64}, f32), db = at::empty({64}, f32);
+  CML_CHECK_HIP(cml::launch_stem_wgrad(pg.data_ptr(), z.data_ptr(), x.data_ptr(),
+                                       mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                       gamma.data_ptr(), gsum.data_ptr<float>(),
+                                       part.data_ptr<float>(), grid,
+                                       tot.data_ptr<double>(), dw.data_ptr<float>(),
+                                       dg.data_ptr<float>(), db.data_ptr<float>(), N, H, W, C, OH,
+                                       OW, cur_stream(), idx.data_ptr<uint8_t>()));
+  return {dw, dg, db};
+}
+
 Tensor maxpool_bwd(const Tensor& dy_in, const Tensor& idx, int64_t H, int64_t W, int64_t k,
                    int64_t s, int64_t p) {
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
@@ -1143,6 +1206,24 @@ Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
 // Stride-1 conv_gemm whose output is the gradient of relu(bn(z)) (z [N, Cout, H, W] NHWC bf16, sc /
 // bi bn's affine, mean / invstd its batch statistics, fp32 [Cout]): {y, sdz, sdzx} with that BN +
 // ReLU backward's sums from the epilogue (bn_bwd_apply finishes it).
+// {wf or None, wr}: the GEMM layouts of a bf16 [Co, Ci, 3, 3] conv weight (any strides) for the
+// implicit-GEMM forward (wf [Co, 9 Ci]) and data gradient (wr [Ci, 9 Co], rotated / transposed).
+std::vector<Tensor> conv3x3_wlayouts(const Tensor& w, bool want_wf) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 3 &&
+                  w.size(3) == 3, "conv3x3_wlayouts: bf16 [Co, Ci, 3, 3] CUDA weight");
+  const int64_t Co = w.size(0), Ci = w.size(1);
+  const c10::DeviceGuard guard(w.device());
+  Tensor wr = at::empty({Ci, 9 * Co}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  Tensor wf;
+  if (want_wf) wf = at::empty({Co, 9 * Ci}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  CML_CHECK_HIP(cml::launch_conv3x3_wlayouts(w.data_ptr(), static_cast<int>(Co),
+                                             static_cast<int>(Ci), w.stride(0), w.stride(1),
+                                             w.stride(2), w.stride(3),
+                                             want_wf ? wf.data_ptr() : nullptr, wr.data_ptr(),
+                                             cur_stream()));
+  return {wf, wr};   // wf undefined (None) unless asked for
+}
+
 std::vector<Tensor> conv_gemm_bnsums(const Tensor& x, const Tensor& w, int64_t taps,
                                      const Tensor& zero, const Tensor& z, const Tensor& sc,
                                      const Tensor& bi, const Tensor& mean, const Tensor& invstd) {
@@ -1894,6 +1975,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "BN statistics of a 1x1 conv's output from its input's Gram matrix and column sums");
   m.def("bn_bwd_coeffs", &bn_bwd_coeffs, "BN + ReLU backward coefficients from its sums");
   m.def("bn_bwd_sums", &bn_bwd_sums, "reduction half of a BN (+ ReLU) backward");
+  m.def("stem_wgrad_pool", &stem_wgrad_pool, py::arg("dy"), py::arg("idx"), py::arg("dy2"),
+        py::arg("z"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"),
+        "stem backward (conv weight gradient through BN, dgamma, dbeta) from the pool output "
+        "gradient, the pool input gradient gathered inside the kernel");
+  m.def("conv3x3_wlayouts", &conv3x3_wlayouts, py::arg("w"), py::arg("want_wf"),
+        "forward / data-gradient GEMM layouts of a 3x3 conv weight in one launch");
   m.def("maxpool_bwd_sum", &maxpool_bwd_sum, "3x3/s2 max-pool backward + channel sums of dx",
         py::arg("dy"), py::arg("idx"), py::arg("H"), py::arg("W"), py::arg("dy2") = py::none());
   m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");

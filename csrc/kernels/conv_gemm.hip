@@ -455,4 +455,38 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
                                     part + static_cast<size_t>(N / BN) * R * 2 * BN);
 }
 
+namespace {
+// The two GEMM layouts of a 3x3 conv weight w[co][ci][ky][kx] (any strides, bf16) in one pass:
+//   wf[co][(3 ky + kx) Ci + ci]        = w[co][ci][ky][kx]          (forward implicit GEMM)
+//   wr[ci][(3 ky + kx) Co + co]        = w[co][ci][2 - ky][2 - kx]  (data gradient: rotated,
+//                                                                     transposed)
+// One thread per weight element (replaces a permute copy, a flip and a second permute copy).
+__global__ __launch_bounds__(256) void conv3x3_wlayouts_kernel(const uint16_t* __restrict__ w,
+                                                              int Co, int Ci, int64_t s0,
+                                                              int64_t s1, int64_t s2, int64_t s3,
+                                                              uint16_t* __restrict__ wf,
+                                                              uint16_t* __restrict__ wr) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= static_cast<int64_t>(Co) * Ci * 9) return;
+  // e enumerates (co, tap, ci) so the wf writes are contiguous
+  const int ci = static_cast<int>(e % Ci);
+  const int t = static_cast<int>((e / Ci) % 9);
+  const int co = static_cast<int>(e / (static_cast<int64_t>(Ci) * 9));
+  const int ky = t / 3, kx = t - 3 * (t / 3);
+  const uint16_t v = w[co * s0 + ci * s1 + ky * s2 + kx * s3];
+  if (wf) wf[e] = v;
+  wr[(static_cast<int64_t>(ci) * 9 + (8 - t)) * Co + co] = v;
+}
+}  // namespace
+
+hipError_t launch_conv3x3_wlayouts(const void* w, int Co, int Ci, int64_t s0, int64_t s1,
+                                   int64_t s2, int64_t s3, void* wf, void* wr, hipStream_t st) {
+  if (Co < 1 || Ci < 1 || !wr) return hipErrorInvalidValue;
+  const int64_t n = static_cast<int64_t>(Co) * Ci * 9;
+  conv3x3_wlayouts_kernel<<<static_cast<unsigned>((n + 255) / 256), 256, 0, st>>>(
+      reinterpret_cast<const uint16_t*>(w), Co, Ci, s0, s1, s2, s3,
+      reinterpret_cast<uint16_t*>(wf), reinterpret_cast<uint16_t*>(wr));
+  return hipGetLastError();
+}
+
 }  // namespace cml

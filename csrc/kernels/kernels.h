@@ -163,6 +163,13 @@ hipError_t launch_multi_copy(const MultiCopyArgs& args, hipStream_t stream);
 // dbeta). dy2 (nullable): a second output gradient, summed on load. work:
 // maxpool_bwd_sum_workspace_bytes.
 size_t maxpool_bwd_sum_workspace_bytes(int N, int H, int W, int C);
+// Channel sums of a max-pool's routed output gradient: sums[c] = sum over pooled pixels whose
+// argmax byte is not 255 of dy (+ dy2) (= the channel sums of the pool's input gradient, which is
+// never formed); with dy2, dsum = bf16(dy + dy2) as well. P pooled pixels, C channels (C / 8
+// divides 256); work: pool_gsum_workspace_floats(P, C) floats.
+size_t pool_gsum_workspace_floats(int64_t P, int C);
+hipError_t launch_pool_gsum(const void* dy, const void* dy2, const void* idx, void* dsum,
+                            float* sums, float* work, int64_t P, int C, hipStream_t st);
 hipError_t launch_maxpool_bwd_sum(const void* dy, const void* dy2, const void* idx, void* dx,
                                   float* sums, void* work, int N, int H, int W, int C, int OH,
                                   int OW, hipStream_t stream);
@@ -283,7 +290,11 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
                              const float* invstd, const void* gamma, const float* gsum,
                              float* part, int grid,
                              double* tot, float* dw, float* dgamma, float* dbeta, int N, int H,
-                             int W, int C, int OH, int OW, hipStream_t stream);
+                             int W, int C, int OH, int OW, hipStream_t stream,
+                             const uint8_t* pidx = nullptr);
+// pidx != nullptr: g is the 3x3 / s2 / p1 max-pool's output gradient [N][PH][PW][64] and pidx its
+// forward argmax bytes; the kernel gathers the pool's input gradient itself (gsum from
+// launch_pool_gsum).
 
 // Weight gradient of a stride-1 1x1 conv, NHWC bf16: dW[co][ci] = sum_p dy[p][co] x[p][ci]
 // (wgrad1x1.hip). Co, Ci multiples of 128, or Ci == 64 with Co a multiple of 256. part: splits x
@@ -348,6 +359,11 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
                                    hipStream_t st);
 hipError_t launch_bnbwd_sums_finalize(const float* part, int R, int BN, int N, const float* invstd,
                                       float* sdz, float* sdzx, hipStream_t st, float* fold);
+// The forward (wf [Co][9 Ci], k = (3 ky + kx) Ci + ci) and data-gradient (wr [Ci][9 Co], rotated
+// and transposed: wr[ci][(3 ky + kx) Co + co] = w[co][ci][2 - ky][2 - kx]) GEMM layouts of a bf16
+// 3x3 conv weight with strides s0..s3 (elements), in one launch; wf may be null.
+hipError_t launch_conv3x3_wlayouts(const void* w, int Co, int Ci, int64_t s0, int64_t s1,
+                                   int64_t s2, int64_t s3, void* wf, void* wr, hipStream_t st);
 hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* zero, int Nimg,
                             int H, int W, int C, int N, int taps, hipStream_t st,
                             float* part = nullptr, const float* shift = nullptr,

@@ -437,6 +437,61 @@ __global__ __launch_bounds__(1024) void colsum_fold_kernel(const float* __restri
   }
 }
 
+// Routed channel sums of a max-pool output gradient (the stem backward's dbeta and mean(g) when
+// stem_wgrad gathers the pool's input gradient itself): a window whose argmax byte is 255 (max <= 0,
+// ReLU-masked) routes nothing, every other window routes its gradient to exactly one input pixel.
+// Thread = 8 channels of one pooled pixel row per iteration (4 rows in flight), per-workgroup
+// partials [nb][C] in a fixed order. DY2: dsum = bf16(dy + dy2) for the gather.
+template <bool DY2>
+__global__ __launch_bounds__(kPB) void pool_gsum_kernel(const bf16* __restrict__ dy,
+                                                       const bf16* __restrict__ dy2,
+                                                       const uint8_t* __restrict__ idx,
+                                                       bf16* __restrict__ dsum, int64_t P, int C,
+                                                       int64_t ppb, float* __restrict__ part) {
+  const int cg = C / 8, rpi = kPB / cg;
+  const int g = threadIdx.x % cg;
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * ppb;
+  const int64_t hi = lo + ppb < P ? lo + ppb : P;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t r0 = lo + threadIdx.x / cg; r0 < hi; r0 += 4 * rpi) {
+    float d[4][8];
+    uint2 m[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {   // clamped unconditional loads, zeroed past the range
+      const int64_t r = r0 + u * rpi < hi ? r0 + u * rpi : hi - 1;
+      load_vec<bf16, 8>(dy + r * C + 8 * g, d[u]);
+      m[u] = *reinterpret_cast<const uint2*>(idx + r * C + 8 * g);
+      if constexpr (DY2) {
+        float e[8];
+        load_vec<bf16, 8>(dy2 + r * C + 8 * g, e);
+#pragma unroll
+        for (int v = 0; v < 8; ++v) d[u][v] += e[v];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t r = r0 + u * rpi;
+      if (r >= hi) break;
+      if constexpr (DY2) store_bf16<8>(dsum + r * C + 8 * g, d[u]);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const uint32_t b = ((v < 4 ? m[u].x : m[u].y) >> (8 * (v & 3))) & 0xffu;
+        s[v] += b != 0xffu ? d[u][v] : 0.f;
+      }
+    }
+  }
+  __shared__ float red[kPB][9];
+#pragma unroll
+  for (int v = 0; v < 8; ++v) red[threadIdx.x][v] = s[v];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kPB) {
+    const int gc = c >> 3, v = c & 7;
+    float acc = 0.f;
+    for (int k = gc; k < kPB; k += cg) acc += red[k][v];
+    part[static_cast<int64_t>(blockIdx.x) * C + c] = acc;
+  }
+}
+
 dim3 pgrid(int inner, int rows) {
   return dim3((inner + kPB - 1) / kPB, rows < 65535 ? rows : 65535);
 }
@@ -608,6 +663,28 @@ hipError_t launch_maxpool_bwd_sum(const void* dy, const void* dy2, const void* i
   float* part2 = part + static_cast<int64_t>(gx) * gy * C;
   colsum_fold_rows_kernel<<<kFold1, kPB, 0, st>>>(part, gx * gy, C, part2);
   colsum_fold_kernel<<<1, 1024, 0, st>>>(part2, kFold1, C, sums);
+  return hipGetLastError();
+}
+
+constexpr int kGsumBlocks = 1024;
+
+size_t pool_gsum_workspace_floats(int64_t, int C) { return static_cast<size_t>(kGsumBlocks) * C; }
+
+hipError_t launch_pool_gsum(const void* dy, const void* dy2, const void* idx, void* dsum,
+                            float* sums, float* work, int64_t P, int C, hipStream_t st) {
+  if (C % 8 || C > kPB || kPB % C || P < 1 || (dy2 && !dsum)) return hipErrorInvalidValue;
+  const int rpi = kPB / (C / 8);
+  int64_t nb = (P + 16 * rpi - 1) / (16 * rpi);   // >= 16 row iterations per workgroup
+  if (nb > kGsumBlocks) nb = kGsumBlocks;
+  const int64_t ppb = ((P + nb - 1) / nb + rpi - 1) / rpi * rpi;
+  nb = (P + ppb - 1) / ppb;
+  const auto* d = reinterpret_cast<const bf16*>(dy);
+  const auto* d2 = reinterpret_cast<const bf16*>(dy2);
+  const auto* ix = reinterpret_cast<const uint8_t*>(idx);
+  auto* ds = reinterpret_cast<bf16*>(dsum);
+  if (dy2) pool_gsum_kernel<true><<<static_cast<unsigned>(nb), kPB, 0, st>>>(d, d2, ix, ds, P, C, ppb, work);
+  else pool_gsum_kernel<false><<<static_cast<unsigned>(nb), kPB, 0, st>>>(d, d2, ix, ds, P, C, ppb, work);
+  colsum_fold_kernel<<<1, 1024, 0, st>>>(work, static_cast<int>(nb), C, sums);
   return hipGetLastError();
 }
 

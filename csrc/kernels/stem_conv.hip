@@ -298,7 +298,16 @@ __device__ __forceinline__ int chunk_off(int rho, int ch) {
   return rho * 128 + ((ch ^ (((rho >> 1) & 1) << 2)) << 4);
 }
 
-template <int C, bool VEC, int OWC>
+// GATHER: g is the max-pool's OUTPUT gradient [N][PH][PW][64] with the forward's argmax bytes pidx
+// (3x3 / stride 2 / pad 1, window (j, i) covers rows 2j - 1 .. 2j + 1, tap = 3 row + col inside
+// it, 255 = ReLU-masked window), so the full-resolution pool gradient (4x the pooled size) is never
+// written or read. A chunk's 8 x 16 pixels lie in the 6 x 10 pooled windows from (oyc / 2 - 1,
+// oxc / 2 - 1): that tile (7.5 KB of gradient + 3.75 KB of argmax bytes, one 16-B + 8-B item per
+// thread) is prefetched like z, put in LDS, and every pixel sums the (up to) 2 x 2 windows that
+// route to it. (Per-pixel window loads straight to registers needed 4 x 24 B per pixel and spilled.)
+constexpr int kPR = 6, kPC = 10;                      // pooled rows / cols of a chunk's windows
+constexpr int kPoolLds = kPR * kPC * (kCo * 2 + kCo);  // gradient [60][64] bf16 + argmax [60][64] B
+template <int C, bool VEC, int OWC, bool GATHER>
 __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restrict__ g,
                                                         const uint16_t* __restrict__ z,
                                                         const uint16_t* __restrict__ x,
@@ -306,11 +315,16 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
                                                         const float* __restrict__ invstd,
                                                         const float* __restrict__ gsum,
                                                         float* __restrict__ part, int N, int H,
-                                                        int W, int OH, int OW_) {
+                                                        int W, int OH, int OW_,
+                                                        const uint8_t* __restrict__ pidx, int PH,
+                                                        int PW) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* gbuf = smem;                                   // [128 px][64 ch] bf16, swizzled
   char* xbuf = smem + kCh * 128;
   uint2* tile = reinterpret_cast<uint2*>(smem + 2 * kCh * 128);
+  // GATHER: the chunk's pooled tile after the input tile
+  char* pgbuf = smem + 2 * kCh * 128 + ((tile_rows(kTYB) * tile_cols(OWC > 0 ? OWC : OW_) * 8 + 15) & ~15);
+  char* pibuf = pgbuf + kPR * kPC * 128;
   // OWC > 0: the width is a compile-time constant (the 224-px ResNet input) and every chunk is
   // full, so the transposed reads of a chunk use one base address and immediate offsets
   const int OW = OWC > 0 ? OWC : OW_;
@@ -348,8 +362,14 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
   // one-chunk register prefetch of (g, z) across the flattened (tile, chunk) sequence. Loads are
   // unconditional (clamped address) and invalid pixels are zeroed at use: a branch around the
   // loads makes the compiler wait for them at the join, i.e. no prefetch at all
-  uint4 gv[2], zv[2];
+  uint4 gv[GATHER ? 1 : 2], zv[2];
   bool okv[2];
+  // GATHER: this thread's item of the chunk's pooled tile (pixel e / 8 of the 6 x 10 windows,
+  // channels 8 (e % 8) ..; items >= 480 idle) and whether it lies inside the pooled image
+  uint4 pv;
+  uint2 iv;
+  bool pok;
+  const int pe = tid >> 3;
   auto fetch = [&](int tl, int ch) {
     const int n = tl / bands;
     const int oy0 = (tl - n * bands) * kTYB;
@@ -362,8 +382,17 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
       okv[j] = tl < ntiles && oy < oyend && ox < OW;
       const int pix = okv[j] ? (n * OH + oy) * OW + ox : 0;
       const int64_t o = static_cast<int64_t>(pix) * kCo + 8 * cc;
-      gv[j] = *reinterpret_cast<const uint4*>(g + o);
+      if constexpr (!GATHER) gv[j] = *reinterpret_cast<const uint4*>(g + o);
       zv[j] = *reinterpret_cast<const uint4*>(z + o);
+    }
+    if constexpr (GATHER) {
+      const int pj = (oy0 + 8 * cy) / 2 - 1 + pe / kPC, pi = 8 * cx - 1 + pe % kPC;
+      pok = tl < ntiles && pe < kPR * kPC && pj >= 0 && pj < PH && pi >= 0 && pi < PW;
+      const int64_t po =
+          ((static_cast<int64_t>(pok ? n : 0) * PH + (pok ? pj : 0)) * PW + (pok ? pi : 0)) * kCo +
+          8 * cc;
+      pv = *reinterpret_cast<const uint4*>(g + po);
+      iv = *reinterpret_cast<const uint2*>(pidx + po);
     }
   };
   fetch(blockIdx.x, 0);
@@ -376,16 +405,58 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
       const int r0 = 8 * cy, c0 = 16 * cx;             // chunk origin inside the band
       __syncthreads();                                 // previous chunk's / tile's readers done
       if (ch == 0) stage_input<C, kTYB, VEC>(x, tile, n, oy0, H, W, WT, tid, kBT);
+      if constexpr (GATHER) {
+        if (pe < kPR * kPC) {   // windows outside the pooled image route nothing (argmax 0xff)
+          *reinterpret_cast<uint4*>(pgbuf + pe * 128 + 16 * cc) = pok ? pv : make_uint4(0u, 0u, 0u, 0u);
+          *reinterpret_cast<uint2*>(pibuf + pe * 64 + 8 * cc) =
+              pok ? iv : make_uint2(0xffffffffu, 0xffffffffu);
+        }
+        __syncthreads();
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         // ---- g / xhat of the prefetched pixels -> LDS; BN-backward sums
         const bool ok = OWC > 0 || okv[j];             // fixed-width instance: always valid
-        const uint32_t gw[4] = {gv[j].x, gv[j].y, gv[j].z, gv[j].w};
+        float gf[8];
+        if constexpr (GATHER) {
+          // pixel (r, c) of the chunk (oyc, oxc even): windows (r + 1) / 2 + 1 - a, (c + 1) / 2 +
+          // 1 - b of the tile, tap (ta + 2a, tb + 2b) with ta = (r + 1) & 1, tb = (c + 1) & 1
+          const int rr = (srho + 64 * j) >> 4, rc = (srho + 64 * j) & 15;
+          const int lr = ((rr + 1) >> 1) + 1, lc = ((rc + 1) >> 1) + 1;
+          const int ta = (rr + 1) & 1, tb = (rc + 1) & 1;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) gf[k] = 0.f;
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              const int tta = ta + 2 * a, ttb = tb + 2 * b;
+              const uint32_t me = tta <= 2 && ttb <= 2 ? static_cast<uint32_t>(3 * tta + ttb) : 0x100u;
+              const int w = (lr - a) * kPC + (lc - b);
+              const uint4 pw = *reinterpret_cast<const uint4*>(pgbuf + w * 128 + 16 * cc);
+              const uint2 iw = *reinterpret_cast<const uint2*>(pibuf + w * 64 + 8 * cc);
+              const uint32_t pw4[4] = {pw.x, pw.y, pw.z, pw.w};
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const uint32_t byte = ((k < 4 ? iw.x : iw.y) >> (8 * (k & 3))) & 0xffu;
+                const float d = (k & 1) ? __uint_as_float(pw4[k >> 1] & 0xffff0000u)
+                                        : __uint_as_float(pw4[k >> 1] << 16);
+                gf[k] += byte == me ? d : 0.f;
+              }
+            }
+        } else {
+          const uint32_t gw[4] = {gv[j].x, gv[j].y, gv[j].z, gv[j].w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            gf[2 * k] = __uint_as_float(gw[k] << 16);
+            gf[2 * k + 1] = __uint_as_float(gw[k] & 0xffff0000u);
+          }
+        }
         const uint32_t zw[4] = {zv[j].x, zv[j].y, zv[j].z, zv[j].w};
         uint32_t xw[4], cw[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float g0 = __uint_as_float(gw[k] << 16), g1 = __uint_as_float(gw[k] & 0xffff0000u);
+          const float g0 = gf[2 * k], g1 = gf[2 * k + 1];
           float x0 = fmaf(__uint_as_float(zw[k] << 16), is[2 * k], mu[2 * k]);
           float x1 = fmaf(__uint_as_float(zw[k] & 0xffff0000u), is[2 * k + 1], mu[2 * k + 1]);
           float c0 = g0 - mg[2 * k], c1 = g1 - mg[2 * k + 1];
@@ -548,8 +619,11 @@ size_t fwd_lds(int OW) {   // input tile; the final reduction reuses it
   const size_t red = static_cast<size_t>(kFT / 64) * 2 * 2 * kCo * sizeof(float);
   return need > red ? need : red;
 }
-size_t bwd_lds(int OW) {   // chunk images + input tile; the final reduction reuses it
-  const size_t need = 2 * kCh * 128 + static_cast<size_t>(tile_rows(kTYB)) * tile_cols(OW) * 8;
+size_t bwd_lds(int OW, bool gather = true) {   // chunk images + input tile (+ pooled tile); the
+                                                 // final reduction reuses it
+  const size_t need = 2 * kCh * 128 +
+                      ((static_cast<size_t>(tile_rows(kTYB)) * tile_cols(OW) * 8 + 15) & ~static_cast<size_t>(15)) +
+                      (gather ? kPoolLds : 0);
   const size_t red = static_cast<size_t>(kBT / 8) * kCo * sizeof(float);
   return need > red ? need : red;
 }
@@ -567,10 +641,14 @@ int persistent_grid(const void* fn, int threads, size_t lds, int ntiles) {
 // the backward tile needs > 64 KiB of dynamic LDS: opt in once per kernel instance
 void wgrad_lds_optin() {
   static const bool done = [] {
-    const void* fns[4] = {reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 112>),
-                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 0>),
-                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, false, 0>),
-                          reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false, 0>)};
+    const void* fns[8] = {reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 112, false>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 0, false>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, false, 0, false>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false, 0, false>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 112, true>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 0, true>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, false, 0, true>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false, 0, true>)};
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
     return true;
@@ -590,8 +668,8 @@ int stem_fwd_grid(int N, int OH, int OW, int C) {
 int stem_bwd_grid(int N, int OH, int OW, int C) {
   wgrad_lds_optin();
   const int ntiles = N * ((OH + kTYB - 1) / kTYB);
-  const void* fn = C == 4 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false, 0>)
-                          : reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 112>);
+  const void* fn = C == 4 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false, 0, true>)
+                          : reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 112, true>);
   return persistent_grid(fn, kBT, bwd_lds(OW), ntiles);
 }
 
@@ -622,22 +700,31 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
                              const float* invstd, const void* gamma, const float* gsum,
                              float* part, int grid, double* tot, float* dw, float* dgamma,
                              float* dbeta, int N, int H, int W, int C, int OH, int OW,
-                             hipStream_t st) {
+                             hipStream_t st, const uint8_t* pidx) {
   if ((C != 3 && C != 4) || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1 || N < 1 || grid < 1)
     return hipErrorInvalidValue;
-  if (bwd_lds(OW) > 120 * 1024 || static_cast<int64_t>(N) * OH * OW >= (1ll << 31) / kCo)
+  if (bwd_lds(OW, pidx != nullptr) > 120 * 1024 ||
+      static_cast<int64_t>(N) * OH * OW >= (1ll << 31) / kCo)
     return hipErrorInvalidValue;
-  const size_t lds = bwd_lds(OW);
+  const size_t lds = bwd_lds(OW, pidx != nullptr);
   wgrad_lds_optin();
   const auto* gp = reinterpret_cast<const uint16_t*>(g);
   const auto* zp = reinterpret_cast<const uint16_t*>(z);
   const auto* xp = reinterpret_cast<const uint16_t*>(x);
+  const int PH = (OH - 1) / 2 + 1, PW = (OW - 1) / 2 + 1;   // the 3x3 / s2 / p1 pool's output
   const bool vec = C == 3 && W % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
-#define CML_WG(CC, V, OWC) stem_wgrad_kernel<CC, V, OWC><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, gsum, part, N, H, W, OH, OW)
-  if (C == 4) CML_WG(4, false, 0);
-  else if (vec && OW == 112 && OH % kTYB == 0) CML_WG(3, true, 112);
-  else if (vec) CML_WG(3, true, 0);
-  else CML_WG(3, false, 0);
+#define CML_WG(CC, V, OWC, G) stem_wgrad_kernel<CC, V, OWC, G><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, gsum, part, N, H, W, OH, OW, pidx, PH, PW)
+#define CML_WG_ALL(G)                                       \
+  if (C == 4) CML_WG(4, false, 0, G);                        \
+  else if (vec && OW == 112 && OH % kTYB == 0) CML_WG(3, true, 112, G); \
+  else if (vec) CML_WG(3, true, 0, G);                       \
+  else CML_WG(3, false, 0, G);
+  if (pidx) {
+    CML_WG_ALL(true)
+  } else {
+    CML_WG_ALL(false)
+  }
+#undef CML_WG_ALL
 #undef CML_WG
   stem_wgrad_fold_kernel<<<(kPartW + 255) / 256, 256, 0, st>>>(part, grid, tot);
   stem_wgrad_final_kernel<<<(kCo * C * 49 + 255) / 256, 256, 0, st>>>(

@@ -174,3 +174,52 @@ def test_stem_pool_link_second_gradient(cuda):
         e_on, e_off = _rel(a, r), _rel(b, r)
         print(f"rel err vs fp32: link {e_on:.4f}, add {e_off:.4f}, link vs add {_rel(a, b):.4f}")
         assert e_on <= max(1.5 * e_off, 0.1), (e_on, e_off)
+
+
+@pytest.mark.parametrize("N,C,H,W,two", [(4, 3, 64, 64, False), (3, 4, 50, 46, True),
+                                         (2, 3, 224, 224, False), (2, 3, 224, 224, True),
+                                         (5, 3, 30, 62, False)])
+def test_stem_wgrad_pool_gather(cuda, N, C, H, W, two):
+    """stem_wgrad_pool (the pool's input gradient gathered from the pooled gradient inside the
+    weight-gradient kernel, after a routed channel-sum pass) vs the two-pass path (maxpool_bwd_sum
+    writes the full-resolution gradient, stem_wgrad reads it) and vs float64. 224 x 224 runs the
+    fixed-width (OW = 112) instance of the bench; (5, 3, 30, 62) has partial bands and chunks."""
+    from consensusml_amd.ops.native import lib
+    torch.manual_seed(N + H + int(two))
+    x = torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(64, C, 7, 7, device=cuda) * 0.1).to(torch.bfloat16)
+    gam = torch.empty(64, device=cuda).uniform_(-0.5, 1.5).to(torch.bfloat16)
+    bet = torch.empty(64, device=cuda).uniform_(-0.5, 0.5).to(torch.bfloat16)
+    z, mean, invstd = lib().stem_conv_fwd(x, pack_stem_weight(w), None, None, 1e-5, 0.1, True)
+    y, idx, _, _ = lib().bn_relu_maxpool_fwd(z, gam, bet, None, None, mean, invstd, 1e-5, 0.1,
+                                             False, 3, 2, 1)
+    assert (idx == 255).any()                                 # some ReLU-masked windows
+    dy = torch.randn_like(y)
+    dy2 = torch.randn_like(y) if two else None
+    dw, dg, db = lib().stem_wgrad_pool(dy, idx, dy2, z, x, mean, invstd, gam)
+    g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3], dy2)
+    dw2, dg2, db2 = lib().stem_wgrad(g, z, x, mean, invstd, gam, gsum)
+    gabs = g.double().abs().sum((0, 2, 3)).clamp_min(1e-6)
+    assert ((db.double() - db2.double()).abs() / gabs).max().item() < 1e-3
+    assert _rel(dg, dg2) < 2e-3
+    # float64 on the pool gradient the kernels route (dy + dy2 rounded to bf16 when two)
+    dyt = (dy.float() + dy2.float()).to(torch.bfloat16) if two else dy
+    sc = (invstd.double() * gam.double()).view(1, -1, 1, 1)
+    u = ((z.double() - mean.double().view(1, -1, 1, 1)) * sc +
+         bet.double().view(1, -1, 1, 1)).requires_grad_(True)
+    F.max_pool2d(torch.relu(u), 3, 2, 1).backward(dyt.double())
+    gd = u.grad
+    xh = (z.double() - mean.double().view(1, -1, 1, 1)) * invstd.double().view(1, -1, 1, 1)
+    s1, s2 = gd.sum((0, 2, 3)), (gd * xh).sum((0, 2, 3))
+    assert ((db.double() - s1).abs() / gabs).max().item() < 2e-3
+    assert _rel(dg.double(), s2) < 1e-4
+    M = gd.numel() / 64
+    dz = sc * (gd - s1.view(1, -1, 1, 1) / M - xh * (s2.view(1, -1, 1, 1) / M))
+    wq = w.double().requires_grad_(True)
+    F.conv2d(x.double(), wq, stride=2, padding=3).backward(dz)
+    # g - mean(g) and xhat are staged as bf16 on both paths (the two-pass path rounds g first):
+    # each is ~2-4e-3 from float64 and they differ from each other by as much
+    e_gather, e_two = _rel(dw.double(), wq.grad), _rel(dw2.double(), wq.grad)
+    assert e_gather < 5e-3, (e_gather, e_two)
+    assert e_gather <= 1.25 * e_two + 5e-4, (e_gather, e_two)
