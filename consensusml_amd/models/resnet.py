@@ -260,6 +260,12 @@ class Bottleneck(nn.Module):
         pol = _P()
         own3 = (fuse3 and pol.conv3x3_bn_stats and pol.own_dgrad3x3
                 and fconv.conv3x3_ok(z1, self.conv2))
+        if (own3 and pol.bn1_dgrad_sums and st1 is None and pol.bn1_sums_lib_conv1
+                and self.bn1.training and fused_ok(z1, self.bn1.weight)):
+            # conv1 ran on the library (layers 3-4, 14 x 14 / 7 x 7): one statistics pass here
+            # (the module BN would make the same one), so that bn1's backward also takes its sums
+            # from the 3x3 data gradient's epilogue instead of a reduction pass over dy1 and z1
+            st1 = fconv.bn_stats(z1, self.bn1)
         if own3 and pol.bn1_dgrad_sums and st1 is not None and self.bn1.training:
             # bn1's backward sums come from the 3x3 data gradient's epilogue
             z2, st2 = fconv.bnrelu_conv3x3_bn_stats(z1, self.bn1, st1, self.conv2, self.bn2)

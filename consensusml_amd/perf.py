@@ -68,6 +68,8 @@ class PerfPolicy:
     own_dgrad3x3: bool = True             # conv_gemm.hip data gradient
     conv3x3_bn_stats: bool = True         # conv_gemm.hip forward + BN statistics epilogue
     bn1_dgrad_sums: bool = True           # bn1's backward sums in the 3x3 dgrad epilogue
+    bn1_sums_lib_conv1: bool = False      # ... also behind a library conv1 (layers 3-4): 0.4-0.6
+                                          # ms/step SLOWER (pass 26, profiles/r03_26/)
     own_wgrad3x3: bool = True             # wgrad3x3.hip weight gradient
     # ---------------------------------------------------------------- transformers / engine
     attn_kernel: bool = True              # MFMA attention for short sequences (BERT)
@@ -107,6 +109,7 @@ class PerfPolicy:
             own_dgrad3x3=_env_bool("CML_DGRAD3X3", True),
             conv3x3_bn_stats=_env_bool("CML_CONV3X3_BN_STATS", True),
             bn1_dgrad_sums=_env_bool("CML_BN1_DGRAD_SUMS", True),
+            bn1_sums_lib_conv1=_env_bool("CML_BN1_SUMS_LIB_CONV1", False),
             own_wgrad3x3=_env_bool("CML_WGRAD3X3", True),
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),
             multi_copy=_env_bool("CML_MULTI_COPY", True),

@@ -521,23 +521,26 @@ std::vector<Tensor> stem_wgrad(const Tensor& g_in, const Tensor& z, const Tensor
   const int grid = cml::stem_bwd_grid(N, OH, OW, C);
   const int64_t pw = static_cast<int64_t>(cml::stem_wgrad_part_floats());
   Tensor part = at::empty({grid, pw}, f32);
-  Tensor tot = at::empty({pw}, x.options().dtype(at::kDouble));
+  Tensor tot = at::empty({static_cast<int64_t>(cml::stem_wgrad_tot_doubles())},
+                         x.options().dtype(at::kDouble));
   Tensor dw = at::empty({64, C, 7, 7}, f32);
   Tensor dg = at::empty({64}, f32), db = at::empty({64}, f32);
+  Tensor cwork = at::empty({static_cast<int64_t>(cml::stem_cola_work_floats(N, H, W, C))}, f32);
   CML_CHECK_HIP(cml::launch_stem_wgrad(g.data_ptr(), z.data_ptr(), x.data_ptr(),
                                        mean.data_ptr<float>(), invstd.data_ptr<float>(),
                                        gamma.data_ptr(), gsum.data_ptr<float>(),
                                        part.data_ptr<float>(), grid,
                                        tot.data_ptr<double>(), dw.data_ptr<float>(),
                                        dg.data_ptr<float>(), db.data_ptr<float>(), N, H, W, C, OH,
-                                       OW, cur_stream()));
+                                       OW, cur_stream(), nullptr, cwork.data_ptr<float>()));
   return {dw, dg, db};
 }
 
 // Stem backward straight from the max-pool's OUTPUT gradient dy [N, 64, PH, PW] (+ an optional
-// second gradient dy2 of the same shape) and the pool's argmax bytes idx: the routed channel sums
-// (launch_pool_gsum), then stem_wgrad gathering each pixel's pool input gradient from its windows
-// (the full-resolution pool gradient is never written). Same outputs as stem_wgrad.
+// second gradient dy2 of the same shape, summed into one pooled gradient first) and the pool's
+// argmax bytes idx: stem_wgrad gathering each pixel's pool input gradient from its windows (the
+// full-resolution pool gradient is never written), its mean handled through the column sums of
+// the input patches. Same outputs as stem_wgrad.
 std::vector<Tensor> stem_wgrad_pool(const Tensor& dy_in, const Tensor& idx,
                                     const optional<Tensor>& dy2_in, const Tensor& z,
                                     const Tensor& x, const Tensor& mean, const Tensor& invstd,
@@ -572,28 +575,31 @@ std::vector<Tensor> stem_wgrad_pool(const Tensor& dy_in, const Tensor& idx,
   const c10::DeviceGuard guard(x.device());
   auto f32 = x.options().dtype(at::kFloat);
   const int64_t P = N * PH * PW;
-  Tensor gsum = at::empty({64}, f32);
-  Tensor work = at::empty({static_cast<int64_t>(cml::pool_gsum_workspace_floats(P, 64))}, f32);
   Tensor dsum;
-  if (dy2.defined()) dsum = at::empty_like(dy);
-  CML_CHECK_HIP(cml::launch_pool_gsum(dy.data_ptr(), dy2.defined() ? dy2.data_ptr() : nullptr,
-                                      idx.data_ptr(), dsum.defined() ? dsum.data_ptr() : nullptr,
-                                      gsum.data_ptr<float>(), work.data_ptr<float>(), P, 64,
-                                      cur_stream()));
+  if (dy2.defined()) {   // one pooled gradient for the gather: dsum = bf16(dy + dy2)
+    dsum = at::empty_like(dy);
+    Tensor gs = at::empty({64}, f32);
+    Tensor work = at::empty({static_cast<int64_t>(cml::pool_gsum_workspace_floats(P, 64))}, f32);
+    CML_CHECK_HIP(cml::launch_pool_gsum(dy.data_ptr(), dy2.data_ptr(), idx.data_ptr(),
+                                        dsum.data_ptr(), gs.data_ptr<float>(),
+                                        work.data_ptr<float>(), P, 64, cur_stream()));
+  }
   const Tensor& pg = dsum.defined() ? dsum : dy;
+  Tensor cwork = at::empty({static_cast<int64_t>(cml::stem_cola_work_floats(N, H, W, C))}, f32);
   const int grid = cml::stem_bwd_grid(N, OH, OW, C);
   const int64_t pw = static_cast<int64_t>(cml::stem_wgrad_part_floats());
   Tensor part = at::empty({grid, pw}, f32);
-  Tensor tot = at::empty({pw}, x.options().dtype(at::kDouble));
+  Tensor tot = at::empty({static_cast<int64_t>(cml::stem_wgrad_tot_doubles())},
+                         x.options().dtype(at::kDouble));
   Tensor dw = at::empty({64, C, 7, 7}, f32);
   Tensor dg = at::empty({64}, f32), db = at::empty({64}, f32);
   CML_CHECK_HIP(cml::launch_stem_wgrad(pg.data_ptr(), z.data_ptr(), x.data_ptr(),
                                        mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                                       gamma.data_ptr(), gsum.data_ptr<float>(),
-                                       part.data_ptr<float>(), grid,
+                                       gamma.data_ptr(), nullptr, part.data_ptr<float>(), grid,
                                        tot.data_ptr<double>(), dw.data_ptr<float>(),
                                        dg.data_ptr<float>(), db.data_ptr<float>(), N, H, W, C, OH,
-                                       OW, cur_stream(), idx.data_ptr<uint8_t>()));
+                                       OW, cur_stream(), idx.data_ptr<uint8_t>(),
+                                       cwork.data_ptr<float>()));
   return {dw, dg, db};
 }
 

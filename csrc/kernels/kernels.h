@@ -291,10 +291,13 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
                              float* part, int grid,
                              double* tot, float* dw, float* dgamma, float* dbeta, int N, int H,
                              int W, int C, int OH, int OW, hipStream_t stream,
-                             const uint8_t* pidx = nullptr);
+                             const uint8_t* pidx = nullptr, float* cola_work = nullptr);
 // pidx != nullptr: g is the 3x3 / s2 / p1 max-pool's output gradient [N][PH][PW][64] and pidx its
-// forward argmax bytes; the kernel gathers the pool's input gradient itself (gsum from
-// launch_pool_gsum).
+// forward argmax bytes; the kernel gathers the pool's input gradient itself and takes dbeta and
+// mean(g) from its own sums (gsum unused). cola_work (always): stem_cola_work_floats floats.
+// tot: stem_wgrad_tot_doubles() doubles.
+size_t stem_wgrad_tot_doubles();
+size_t stem_cola_work_floats(int N, int H, int W, int C);
 
 // Weight gradient of a stride-1 1x1 conv, NHWC bf16: dW[co][ci] = sum_p dy[p][co] x[p][ci]
 // (wgrad1x1.hip). Co, Ci multiples of 128, or Ci == 64 with Co a multiple of 256. part: splits x

@@ -49,7 +49,7 @@ constexpr int kTYB = 16;                // backward: output rows per tile (fewer
 constexpr int kFT = 256;                // forward workgroup: 4 waves
 constexpr int kBT = 512;                // backward workgroup: 8 waves
 constexpr int kCh = 128;                // backward pixel chunk: 8 x 16 pixels, 8 MFMA k-steps
-constexpr int kPartW = 2 * kCo * kKP + kCo;   // floats per backward partial: G, X, s2
+constexpr int kPartW = 2 * kCo * kKP + 2 * kCo;   // floats per backward partial: G, X, s2, s1
 
 __host__ __device__ constexpr int tile_cols(int OW) { return 2 * OW + 6; }   // ix = -3 .. 2 OW + 2
 __host__ __device__ constexpr int tile_rows(int TY) { return 2 * TY + 5; }
@@ -345,15 +345,18 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
   // a chunk is an 8 x 16 block of output pixels, pixel rho = 16 row + col: the pixel rows of
   // k-step ks's transposed reads, rho = 16 ks + 8 h + 4 e + q, are row ks, col 8 h + 4 e + q
   const int cc = tid & 7, srho = tid >> 3;             // staging: pixels srho, srho + 64
-  float mu[8], is[8], mg[8], s2[8];
-  const float inv_m = 1.f / (static_cast<float>(N) * OH * OW);
+  // g is staged as it is and mean(g) enters the finalize through the column sums of the input
+  // patches (colA): staging g - mean(g) rounded every unrouted pixel's 0 - mean(g) to the same
+  // bf16 value, a per-channel bias whose share of dW grew with the batch (profiles/r03_26/)
+  float mu[8], is[8], s2[8], s1[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     is[k] = invstd[8 * cc + k];
     mu[k] = -mean[8 * cc + k] * is[k];                 // xhat = z * is + mu
-    mg[k] = gsum[8 * cc + k] * inv_m;                  // mean(g)
     s2[k] = 0.f;
+    s1[k] = 0.f;
   }
+  (void)gsum;
   f32x16 acc[4] = {};
   const int bands = (OH + kTYB - 1) / kTYB;
   const int ntiles = N * bands;
@@ -459,13 +462,17 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
           const float g0 = gf[2 * k], g1 = gf[2 * k + 1];
           float x0 = fmaf(__uint_as_float(zw[k] << 16), is[2 * k], mu[2 * k]);
           float x1 = fmaf(__uint_as_float(zw[k] & 0xffff0000u), is[2 * k + 1], mu[2 * k + 1]);
-          float c0 = g0 - mg[2 * k], c1 = g1 - mg[2 * k + 1];
+          float c0 = g0, c1 = g1;
           x0 = ok ? x0 : 0.f;
           x1 = ok ? x1 : 0.f;
           c0 = ok ? c0 : 0.f;
           c1 = ok ? c1 : 0.f;
           s2[2 * k] = fmaf(g0, x0, s2[2 * k]);
           s2[2 * k + 1] = fmaf(g1, x1, s2[2 * k + 1]);
+          if constexpr (GATHER) {   // dbeta = sum g (fp32 gathered values, before rounding)
+            s1[2 * k] += ok ? g0 : 0.f;
+            s1[2 * k + 1] += ok ? g1 : 0.f;
+          }
           xw[k] = static_cast<uint32_t>(f2bf(x0)) | (static_cast<uint32_t>(f2bf(x1)) << 16);
           cw[k] = static_cast<uint32_t>(f2bf(c0)) | (static_cast<uint32_t>(f2bf(c1)) << 16);
         }
@@ -563,6 +570,17 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
     for (int k = 0; k < kBT / 8; ++k) s += red[k * kCo + tid];
     pw[2 * kCo * kKP + tid] = s;
   }
+  if constexpr (GATHER) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[srho * kCo + 8 * cc + k] = s1[k];
+    __syncthreads();
+    if (tid < kCo) {
+      float s = 0.f;
+      for (int k = 0; k < kBT / 8; ++k) s += red[k * kCo + tid];
+      pw[2 * kCo * kKP + kCo + tid] = s;
+    }
+  }
 }
 
 // fold the [nb][kPartW] partials (fp64, fixed order; 4 in flight per thread)
@@ -586,11 +604,15 @@ __global__ __launch_bounds__(256) void stem_wgrad_fold_kernel(const float* __res
   tot[e] = S;
 }
 
-// dW[co][c][ky][kx] = gamma invstd (G - s2/M X); dgamma = s2, dbeta = sum g (fp32)
+// dW[co][c][ky][kx] = gamma invstd (G - s1/M colA - s2/M X) with G = sum g (x) im2col,
+// X = sum xhat (x) im2col, colA[k] = sum over pixels of im2col[.][k] (stem_cola); dgamma = s2,
+// dbeta = s1 = sum g: the channel sums of the pool backward (gsum) or, without them (GATHER), the
+// kernel's own partials.
 __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __restrict__ tot,
                                                               const uint16_t* __restrict__ gamma,
                                                               const float* __restrict__ invstd,
                                                               const float* __restrict__ gsum,
+                                                              const double* __restrict__ cola,
                                                               double M, int C,
                                                               float* __restrict__ dw,
                                                               float* __restrict__ dgamma,
@@ -599,6 +621,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __r
   const double* G = tot;
   const double* X = tot + kCo * kKP;
   const double* S2 = tot + 2 * kCo * kKP;
+  const double* S1 = S2 + kCo;
   if (e < kCo * C * 49) {
     const int co = e / (C * 49);
     const int rem = e - co * C * 49;
@@ -606,11 +629,117 @@ __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __r
     const int ky = t / 7, kx = t - ky * 7;
     const int kc = (ky * 8 + kx) * 4 + c;
     const double a = static_cast<double>(bf2f(gamma[co])) * invstd[co];
-    dw[e] = static_cast<float>(a * (G[co * kKP + kc] - S2[co] / M * X[co * kKP + kc]));
+    const double s1 = gsum ? static_cast<double>(gsum[co]) : S1[co];
+    dw[e] = static_cast<float>(
+        a * (G[co * kKP + kc] - s1 / M * cola[kc] - S2[co] / M * X[co * kKP + kc]));
   }
   if (e < kCo) {
     dgamma[e] = static_cast<float>(S2[e]);
-    dbeta[e] = gsum[e];
+    dbeta[e] = gsum ? gsum[e] : static_cast<float>(S1[e]);
+  }
+}
+
+// colA[k], k = (ky * 8 + kx) * 4 + c: the sum over every output pixel (n, oy, ox) of the input
+// patch value x[n][2 oy + ky - 3][2 ox + kx - 3][c] (0 outside the image). Pass 1 sums x over
+// chunks of kColaChunk images per input pixel (grid = input rows x image chunks, a thread per
+// (column, channel), images in order, 8 loads in flight) into fp32 partials [chunk][H][W][C];
+// pass 2 (one workgroup per tap) adds, in fp64 and a fixed order, the partials of the pixels that
+// tap (ky, kx) reaches: rows ky - 3 + 2 oy and columns kx - 3 + 2 ox inside the image.
+constexpr int kColaChunk = 128;   // images per partial
+// V: 16-B loads (W C a multiple of 8): thread = 8 consecutive (column, channel) values of the row
+// x one of 256 / (W C / 8) image slices (fixed-order LDS combine of the slices)
+template <bool V>
+__global__ __launch_bounds__(256) void stem_cola_rows_kernel(const uint16_t* __restrict__ x, int N,
+                                                            int H, int W, int C,
+                                                            float* __restrict__ part) {
+  const int iy = blockIdx.x;
+  const int n0 = blockIdx.y * kColaChunk, n1 = min(N, n0 + kColaChunk);
+  const int64_t img = static_cast<int64_t>(H) * W * C;
+  const int WC = W * C;
+  float* out = part + (static_cast<int64_t>(blockIdx.y) * H + iy) * WC;
+  if constexpr (V) {
+    __shared__ float red[256][9];
+    const int G8 = WC / 8;
+    const int nsl = G8 >= 256 ? 1 : 256 / G8;
+    for (int gb = 0; gb < G8; gb += 256 / nsl) {
+      const int grp = gb + threadIdx.x % (256 / nsl), sl = threadIdx.x / (256 / nsl);
+      float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (grp < G8 && sl < nsl) {
+        const uint16_t* px = x + static_cast<int64_t>(iy) * WC + 8 * grp;
+        int n = n0 + sl;
+        for (; n + 3 * nsl < n1; n += 4 * nsl) {
+          float v[4][8];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) load_vec<bf16, 8>(reinterpret_cast<const bf16*>(px + (n + u * nsl) * img), v[u]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a[k] += v[u][k];
+        }
+        for (; n < n1; n += nsl) {
+          float v[8];
+          load_vec<bf16, 8>(reinterpret_cast<const bf16*>(px + n * img), v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) a[k] += v[k];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[threadIdx.x][k] = a[k];
+      __syncthreads();
+      const int per = 256 / nsl;
+      if (threadIdx.x < per && gb + threadIdx.x < G8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float s = 0.f;
+          for (int q = 0; q < nsl; ++q) s += red[q * per + threadIdx.x][k];
+          out[8 * (gb + threadIdx.x) + k] = s;
+        }
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < WC; e += 256) {
+      const uint16_t* px = x + static_cast<int64_t>(iy) * WC + e;
+      float a = 0.f;
+      int n = n0;
+      for (; n + 8 <= n1; n += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = bf2f(px[(n + u) * img]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += v[u];
+      }
+      for (; n < n1; ++n) a += bf2f(px[n * img]);
+      out[e] = a;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void stem_cola_kernel(const float* __restrict__ part, int nchunk,
+                                                       int H, int W, int C, int OH, int OW,
+                                                       double* __restrict__ cola) {
+  __shared__ double red[256][4];
+  const int t = blockIdx.x;                 // tap ky * 8 + kx (kx = 7: the zero tap)
+  const int ky = t / 8, kx = t - 8 * (t / 8);
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  if (kx < 7) {
+    const int64_t plane = static_cast<int64_t>(H) * W * C;
+    for (int q = threadIdx.x; q < OH * OW; q += 256) {
+      const int oy = q / OW, ox = q - oy * OW;
+      const int iy = ky - 3 + 2 * oy, ix = kx - 3 + 2 * ox;
+      if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
+      const float* d = part + (static_cast<int64_t>(iy) * W + ix) * C;
+      for (int k = 0; k < nchunk; ++k)
+        for (int c = 0; c < C; ++c) acc[c] += d[k * plane + c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) red[threadIdx.x][c] = acc[c];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double s = 0.0;
+    for (int k = 0; k < 256; ++k) s += red[k][threadIdx.x];
+    cola[t * 4 + threadIdx.x] = threadIdx.x < C ? s : 0.0;
   }
 }
 
@@ -674,6 +803,10 @@ int stem_bwd_grid(int N, int OH, int OW, int C) {
 }
 
 size_t stem_wgrad_part_floats() { return kPartW; }
+size_t stem_wgrad_tot_doubles() { return kPartW + kKP; }   // partial totals + colA
+size_t stem_cola_work_floats(int N, int H, int W, int C) {
+  return static_cast<size_t>((N + kColaChunk - 1) / kColaChunk) * H * W * C;
+}
 
 hipError_t launch_stem_conv_fwd(const void* x, const void* wpk, void* z, float* part, int grid,
                                 float* mean, float* invstd, float* rmean, float* rvar, float eps,
@@ -700,7 +833,8 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
                              const float* invstd, const void* gamma, const float* gsum,
                              float* part, int grid, double* tot, float* dw, float* dgamma,
                              float* dbeta, int N, int H, int W, int C, int OH, int OW,
-                             hipStream_t st, const uint8_t* pidx) {
+                             hipStream_t st, const uint8_t* pidx, float* cola_work) {
+  if (!cola_work || (!pidx && !gsum)) return hipErrorInvalidValue;
   if ((C != 3 && C != 4) || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1 || N < 1 || grid < 1)
     return hipErrorInvalidValue;
   if (bwd_lds(OW, pidx != nullptr) > 120 * 1024 ||
@@ -727,8 +861,14 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
 #undef CML_WG_ALL
 #undef CML_WG
   stem_wgrad_fold_kernel<<<(kPartW + 255) / 256, 256, 0, st>>>(part, grid, tot);
+  double* cola = tot + kPartW;   // tot has room for the column sums after the partial totals
+  const int nchunk = (N + kColaChunk - 1) / kColaChunk;
+  const bool v16 = (W * C) % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  if (v16) stem_cola_rows_kernel<true><<<dim3(H, nchunk), 256, 0, st>>>(xp, N, H, W, C, cola_work);
+  else stem_cola_rows_kernel<false><<<dim3(H, nchunk), 256, 0, st>>>(xp, N, H, W, C, cola_work);
+  stem_cola_kernel<<<kKP / 4, 256, 0, st>>>(cola_work, nchunk, H, W, C, OH, OW, cola);
   stem_wgrad_final_kernel<<<(kCo * C * 49 + 255) / 256, 256, 0, st>>>(
-      tot, reinterpret_cast<const uint16_t*>(gamma), invstd, gsum,
+      tot, reinterpret_cast<const uint16_t*>(gamma), invstd, pidx ? nullptr : gsum, cola,
       static_cast<double>(N) * OH * OW, C, dw, dgamma, dbeta);
   return hipGetLastError();
 }

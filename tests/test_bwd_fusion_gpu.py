@@ -298,18 +298,21 @@ def test_conv_gemm_bnsums(cuda, N, Cin, Co, H):
     _close(_rows(dz), _rows(dz_ref), 1e-2)
 
 
-def test_bottleneck_bn1_dgrad_sums_matches_unfused(cuda):
+@pytest.mark.parametrize("H", [14, 28])
+def test_bottleneck_bn1_dgrad_sums_matches_unfused(cuda, H):
     """A bottleneck block's gradients with bn1's backward sums from the 3x3 data gradient's
-    epilogue equal those of bn_act + its own reduction pass."""
+    epilogue equal those of bn_act + its own reduction pass. H = 14: conv1 on the library (its
+    output under 784 pixels), bn1's statistics from a separate pass (bn1_sums_lib_conv1); H = 28:
+    the statistics from the fused conv1's epilogue."""
     import consensusml_amd.models.resnet as R
     torch.manual_seed(5)
     blk = R.Bottleneck(256, 64).to(cuda, torch.bfloat16).to(memory_format=torch.channels_last)
     blk.train()
-    x0 = _nhwc(torch.randn(4, 256, 14, 14, device=cuda).relu().bfloat16())
-    gy = _nhwc(torch.randn(4, 256, 14, 14, device=cuda).bfloat16())
+    x0 = _nhwc(torch.randn(4, 256, H, H, device=cuda).relu().bfloat16())
+    gy = _nhwc(torch.randn(4, 256, H, H, device=cuda).bfloat16())
     grads = {}
     for on in (True, False):
-        with perf.use_policy(perf.policy().replace(bn1_dgrad_sums=on)):
+        with perf.use_policy(perf.policy().replace(bn1_dgrad_sums=on, bn1_sums_lib_conv1=on)):
             b = copy.deepcopy(blk)
             x = x0.clone().requires_grad_(True)
             b(x).backward(gy)
