@@ -266,9 +266,17 @@ class Bottleneck(nn.Module):
             # (the module BN would make the same one), so that bn1's backward also takes its sums
             # from the 3x3 data gradient's epilogue instead of a reduction pass over dy1 and z1
             st1 = fconv.bn_stats(z1, self.bn1)
+        own3s2 = (fuse3 and not own3 and pol.own_conv3x3_s2
+                  and fconv.conv3x3_s2_ok(z1, self.conv2))
         if own3 and pol.bn1_dgrad_sums and st1 is not None and self.bn1.training:
             # bn1's backward sums come from the 3x3 data gradient's epilogue
             z2, st2 = fconv.bnrelu_conv3x3_bn_stats(z1, self.bn1, st1, self.conv2, self.bn2)
+        elif (own3s2 and pol.bn1_dgrad_sums and st1 is not None and self.bn1.training
+                and fused_ok(z1, self.bn1.weight)):
+            # stride-2 conv of a downsample block: the same, with the parity-class data gradient
+            z2, st2 = fconv.bnrelu_conv3x3_s2_bn_stats(z1, self.bn1, st1, self.conv2, self.bn2)
+        elif own3s2:
+            z2, st2 = fconv.conv3x3_s2_bn_stats(self.bn1(z1, stats=st1), self.conv2, self.bn2)
         else:
             out = self.bn1(z1, stats=st1)
             if own3:

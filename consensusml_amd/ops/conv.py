@@ -692,6 +692,101 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
         return dz1, dg1, db1, None, None, None, dw, None, None, None, None
 
 
+def _wgrad3x3_s2(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """Weight gradient of a stride-2 / padding-1 3x3 conv (MIOpen)."""
+    return torch.ops.aten.convolution_backward(
+        dy, x, w, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+
+
+class _Conv3x3S2BNStatsFn(torch.autograd.Function):
+    """(z, mean, invstd): stride-2 / padding-1 3x3 conv on ``conv_gemm.hip`` (stride-2 gather)
+    with the next BN's statistics in the epilogue. Backward: the data gradient as four
+    output-parity-class implicit GEMMs of 4 / 2 / 2 / 1 taps (``conv_gemm_s2dgrad``: no multiply
+    by the structural zeros of a stride-2 transposed conv, every dx pixel written once, no fill);
+    weight gradient on MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w, rmean, rvar, eps, momentum):
+        wf, wr = _w3x3_layouts(w, True)
+        y, mean, invstd = lib().conv_gemm_bn(x, wf, 9, _zero_row(x.device), rmean, rmean, rvar,
+                                             eps, momentum, 2)
+        ctx.save_for_backward(x, w)
+        ctx.wr = wr
+        ctx.mark_non_differentiable(mean, invstd)
+        ctx.set_materialize_grads(False)
+        return y, mean, invstd
+
+    @staticmethod
+    def backward(ctx, dy, _dm, _di):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = lib().conv_gemm_s2dgrad(dy, ctx.wr, _zero_row(dy.device))[0] \
+            if ctx.needs_input_grad[0] else None
+        dw = _wgrad3x3_s2(dy, x, w) if ctx.needs_input_grad[1] else None
+        return dx, dw, None, None, None, None
+
+
+class _BNReLUConv3x3S2BNStatsFn(torch.autograd.Function):
+    """``_BNReLUConv3x3BNStatsFn`` for the stride-2 3x3 conv of a downsample block: the
+    parity-class data gradient also takes bn1's BN + ReLU backward sums in its epilogue, so bn1's
+    backward is its apply pass only."""
+
+    @staticmethod
+    def forward(ctx, z1, g1, b1, mean1, invstd1, eps1, w, rmean, rvar, eps, momentum):
+        L = lib()
+        y1 = L.bn_fwd(z1, None, g1, b1, None, None, mean1, invstd1, eps1, momentum, True, False,
+                      False)[0]
+        wf, wr = _w3x3_layouts(w, True)
+        z2, m2, i2 = L.conv_gemm_bn(y1, wf, 9, _zero_row(z1.device), rmean, rmean, rvar, eps,
+                                    momentum, 2)
+        ctx.save_for_backward(z1, g1, b1, mean1, invstd1, y1, w)
+        ctx.wr = wr
+        ctx.mark_non_differentiable(m2, i2)
+        ctx.set_materialize_grads(False)
+        return z2, m2, i2
+
+    @staticmethod
+    def backward(ctx, dz2, _dm, _di):
+        z1, g1, b1, mean1, invstd1, y1, w = ctx.saved_tensors
+        dz2 = dz2.contiguous(memory_format=torch.channels_last)
+        L = lib()
+        sc, bi = _affine(g1, b1, mean1, invstd1)
+        dy1, s1, q1 = L.conv_gemm_s2dgrad(dz2, ctx.wr, _zero_row(dz2.device), z1, sc, bi, mean1,
+                                          invstd1)
+        M = z1.numel() // z1.shape[1]
+        _, _, _, dg1, db1 = L.bn_bwd_coeffs(s1, q1, g1, mean1, invstd1, M)
+        dz1 = L.bn_bwd_apply(dy1, z1, g1, b1, mean1, invstd1, s1, q1)
+        dw = _wgrad3x3_s2(dz2, y1, w) if ctx.needs_input_grad[6] else None
+        return dz1, dg1, db1, None, None, None, dw, None, None, None, None
+
+
+def conv3x3_s2_ok(x: torch.Tensor, conv) -> bool:
+    """Stride-2 padding-1 3x3 convs on NHWC bf16 GPU tensors with 64-multiple channels and an even
+    input (every dx pixel then belongs to exactly one parity class)."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
+            and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
+            and conv.kernel_size == (3, 3) and conv.stride == (2, 2) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
+
+
+def conv3x3_s2_bn_stats(x: torch.Tensor, conv, bn):
+    """(z, (mean, invstd)) of a stride-2 ``conv(x)`` and bn's training statistics; callers check
+    ``conv3x3_s2_ok``."""
+    z, m, i = _Conv3x3S2BNStatsFn.apply(x, conv.weight, bn.running_mean, bn.running_var, bn.eps,
+                                        bn.momentum)
+    return z, (m, i)
+
+
+def bnrelu_conv3x3_s2_bn_stats(z1: torch.Tensor, bn_a, stats_a, conv, bn):
+    """``bnrelu_conv3x3_bn_stats`` for a stride-2 conv; callers check ``conv3x3_s2_ok`` on z1."""
+    z, m, i = _BNReLUConv3x3S2BNStatsFn.apply(z1, bn_a.weight, bn_a.bias, stats_a[0], stats_a[1],
+                                              bn_a.eps, conv.weight, bn.running_mean,
+                                              bn.running_var, bn.eps, bn.momentum)
+    return z, (m, i)
+
+
 # PerfPolicy.bn1_dgrad_sums -- bn1 + ReLU -> 3x3 conv with bn1's backward sums in the data-gradient
 # epilogue (off: bn_act + conv3x3_bn_stats, bn1's backward with its own reduction pass)
 

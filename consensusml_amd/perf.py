@@ -71,6 +71,8 @@ class PerfPolicy:
     bn1_sums_lib_conv1: bool = False      # ... also behind a library conv1 (layers 3-4): 0.4-0.6
                                           # ms/step SLOWER (pass 26, profiles/r03_26/)
     own_wgrad3x3: bool = True             # wgrad3x3.hip weight gradient
+    own_conv3x3_s2: bool = True           # stride-2 3x3: conv_gemm forward + BN stats, parity-class
+                                          # data gradient (+ bn1 backward sums)
     # ---------------------------------------------------------------- transformers / engine
     attn_kernel: bool = True              # MFMA attention for short sequences (BERT)
     multi_copy: bool = True               # multi-tensor HIP copy for gradient capture
@@ -111,6 +113,7 @@ class PerfPolicy:
             bn1_dgrad_sums=_env_bool("CML_BN1_DGRAD_SUMS", True),
             bn1_sums_lib_conv1=_env_bool("CML_BN1_SUMS_LIB_CONV1", False),
             own_wgrad3x3=_env_bool("CML_WGRAD3X3", True),
+            own_conv3x3_s2=_env_bool("CML_CONV3X3_S2", True),
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),
             multi_copy=_env_bool("CML_MULTI_COPY", True),
             batched_workers=_env_bool("CML_BATCHED_WORKERS", True),

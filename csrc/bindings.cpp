@@ -1262,6 +1262,53 @@ std::vector<Tensor> conv_gemm_bnsums(const Tensor& x, const Tensor& w, int64_t t
   return {y, sdz, sdzx};
 }
 
+// Data gradient of a stride-2 / padding-1 3x3 conv with an even [2 Ho, 2 Wo] input: dy [N, Co, Ho,
+// Wo] NHWC bf16, wr [Ci, 9 Co] (conv3x3_wlayouts) -> {dx [N, Ci, 2 Ho, 2 Wo] NHWC, sdz, sdzx}; with
+// z (+ sc, bi, mean, invstd as conv_gemm_bnsums) the BN + ReLU backward sums dx feeds, else
+// sdz / sdzx are undefined.
+std::vector<Tensor> conv_gemm_s2dgrad(const Tensor& dy, const Tensor& wr, const Tensor& zero,
+                                      const optional<Tensor>& z, const optional<Tensor>& sc,
+                                      const optional<Tensor>& bi, const optional<Tensor>& mean,
+                                      const optional<Tensor>& invstd) {
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(dy.dim() == 4, "conv_gemm_s2dgrad: 4-D NHWC dy");
+  const int64_t N = dy.size(0), Co = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(wr.is_cuda() && wr.scalar_type() == at::kBFloat16 && wr.is_contiguous() &&
+                  wr.dim() == 2 && wr.size(1) == 9 * Co && wr.size(0) % 64 == 0 && Co % 64 == 0,
+              "conv_gemm_s2dgrad: wr must be contiguous bf16 [Ci, 9 Co], channels multiples of 64");
+  TORCH_CHECK(zero.is_cuda() && zero.device() == dy.device() && zero.scalar_type() == at::kBFloat16 &&
+                  zero.is_contiguous() && zero.numel() >= 64, "conv_gemm_s2dgrad: zero must be >= 64 bf16");
+  const int64_t Ci = wr.size(0);
+  const bool sums = z.has_value() && z->defined();
+  if (sums) {
+    check_nhwc(*z, "z");
+    TORCH_CHECK(z->dim() == 4 && z->size(0) == N && z->size(1) == Ci && z->size(2) == 2 * Ho &&
+                    z->size(3) == 2 * Wo, "conv_gemm_s2dgrad: z must be [N, Ci, 2 Ho, 2 Wo]");
+  }
+  const c10::DeviceGuard guard(dy.device());
+  auto f32 = dy.options().dtype(at::kFloat);
+  Tensor dx = at::empty({N, Ci, 2 * Ho, 2 * Wo},
+                        dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor part, sdz, sdzx;
+  if (sums) {
+    part = at::empty({static_cast<int64_t>(cml::conv_gemm_s2dgrad_part_floats(N * Ho * Wo,
+                                                                              static_cast<int>(Ci)))}, f32);
+    sdz = at::empty({Ci}, f32);
+    sdzx = at::empty({Ci}, f32);
+  }
+  CML_CHECK_HIP(cml::launch_conv_gemm_s2dgrad(
+      dy.data_ptr(), wr.data_ptr(), dx.data_ptr(), zero.data_ptr(), static_cast<int>(N),
+      static_cast<int>(Ho), static_cast<int>(Wo), static_cast<int>(Co), static_cast<int>(Ci),
+      sums ? z->data_ptr() : nullptr,
+      sums ? opt_ptr<const float>(sc, at::kFloat, "sc", Ci) : nullptr,
+      sums ? opt_ptr<const float>(bi, at::kFloat, "bi", Ci) : nullptr,
+      sums ? opt_ptr<const float>(mean, at::kFloat, "mean", Ci) : nullptr,
+      sums ? opt_ptr<const float>(invstd, at::kFloat, "invstd", Ci) : nullptr,
+      sums ? part.data_ptr<float>() : nullptr, sums ? sdz.data_ptr<float>() : nullptr,
+      sums ? sdzx.data_ptr<float>() : nullptr, cur_stream()));
+  return {dx, sdz, sdzx};
+}
+
 Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps, const optional<Tensor>& zero_in,
                  int64_t stride) {
   check_nhwc(x, "x");
@@ -1940,6 +1987,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "whether wgrad3x3 takes the nine-tap kernel for this shape");
   m.def("conv_gemm_bnsums", &conv_gemm_bnsums,
         "stride-1 conv_gemm + the sums of the BN + ReLU backward its output feeds");
+  m.def("conv_gemm_s2dgrad", &conv_gemm_s2dgrad, py::arg("dy"), py::arg("wr"), py::arg("zero"),
+        py::arg("z") = py::none(), py::arg("sc") = py::none(), py::arg("bi") = py::none(),
+        py::arg("mean") = py::none(), py::arg("invstd") = py::none(),
+        "stride-2 3x3 data gradient as four parity-class implicit GEMMs (+ BN + ReLU backward sums)");
   m.def("conv_gemm", &conv_gemm, py::arg("x"), py::arg("w"), py::arg("taps"),
         py::arg("zero") = py::none(), py::arg("stride") = 1,
         "implicit-GEMM NHWC conv (1x1 / 3x3 padding 1, stride 1 or 2), glds staging");

@@ -48,6 +48,10 @@ struct GArgs {
   int S, IH, IW, IHW;     // stride; input height, width and pixels per image
   int KS;                 // TAPS * C / 64
   int ntn, tiles;
+  // PAR (stride-2 3x3 data gradient, one output parity class per launch): the class (py, px), the
+  // weight row stride (9 C), and this class's rows of the statistics slab (total rows per n-tile,
+  // first row)
+  int py, px, wld, prt, prb;
 };
 
 // NBUF = 2: the DMA of step ks + 1 overlaps step ks, retired by vmcnt(0) + barrier per step.
@@ -60,7 +64,14 @@ struct GArgs {
 // BB (with ST): instead the sums of the backward of the BN + ReLU whose output gradient y is (a
 // data gradient): s = sum y', q = sum y' (z - mean) with y' = (z ep_sc + ep_bi > 0) ? y : 0, the
 // ReLU bit recomputed from the BN input z -- that BN's backward then needs no reduction pass.
-template <int BM, int BN, int TAPS, int NBUF = 2, int WTN = 64, bool ST = false, bool BB = false>
+// PAR: the data gradient of a stride-2 / padding-1 3x3 conv with an even input, one output parity
+// class (py, px) per launch. dx[2 m + py][2 l + px] gathers dy only through the taps of matching
+// parity: along an axis, parity 0 takes ky = 1 from dy row m, parity 1 takes ky = 0 from row m + 1
+// and ky = 2 from row m; so the classes run 1 / 2 / 2 / 4 taps (9 in total, no multiply by a
+// structural zero). x = dy (C = its channels, output grid = dy's grid), w = the rotated,
+// transposed layout wr [N][9 C] of the data gradient; output rows go to dx's pixels of the class.
+template <int BM, int BN, int TAPS, int NBUF = 2, int WTN = 64, bool ST = false, bool BB = false,
+          bool PAR = false>
 __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
   constexpr int WN = BN / WTN, WM = BM / 64, NW = WN * WM;
   constexpr int NI = WTN / 32;                  // accumulator rows (n) per wave
@@ -97,11 +108,20 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
     }
   }
 
+  const int wld = PAR ? a.wld : a.KS * kBK;
   auto issue = [&](int ks, int buf) {
     const int CS = a.C >> 6;
     const int tap = TAPS == 1 ? 0 : ks / CS;
     const int cc = ks - tap * CS;
-    const int dy = TAPS == 1 ? 0 : tap / 3 - 1, dx = TAPS == 1 ? 0 : tap - 3 * (tap / 3) - 1;
+    int dy = TAPS == 1 ? 0 : tap / 3 - 1, dx = TAPS == 1 ? 0 : tap - 3 * (tap / 3) - 1;
+    int wcol = ks * kBK;
+    if constexpr (PAR) {
+      const int tyi = a.px ? (tap >> 1) : tap, txi = a.px ? (tap & 1) : 0;
+      const int ky = a.py ? (tyi ? 2 : 0) : 1, kx = a.px ? (txi ? 2 : 0) : 1;
+      dy = (a.py && tyi == 0) ? 1 : 0;
+      dx = (a.px && txi == 0) ? 1 : 0;
+      wcol = (3 * (2 - ky) + (2 - kx)) * a.C + cc * kBK;   // wr's tap (2 - ky, 2 - kx)
+    }
     char* base = smem + buf * SB;
 #pragma unroll
     for (int i = 0; i < QA; ++i) {
@@ -122,7 +142,7 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
     for (int i = 0; i < QB; ++i) {
       const int row = wave * (BN / NW) + 8 * i + lrow;
       const int c = p ^ ((row >> 1) & 7);
-      const uint16_t* src = a.w + static_cast<int64_t>(n0 + row) * (a.KS * kBK) + ks * kBK + 8 * c;
+      const uint16_t* src = a.w + static_cast<int64_t>(n0 + row) * wld + wcol + 8 * c;
       __builtin_amdgcn_global_load_lds((g_void*)src,
                                        (lds_void*)(wb + (wave * (BN / NW) + 8 * i) * 128), 16, 0, 0);
     }
@@ -191,6 +211,16 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
   char* simg = smem + wave * 8192;
   const int c = lane & 7;
   const int mb = m0 + wm * 64;
+  // output row of GEMM row m (PAR: the class pixel of dx, a 2H x 2W image)
+  auto orow = [&](int m) -> int64_t {
+    if constexpr (PAR) {
+      const int img = m / a.HW, rem = m - img * a.HW;
+      const int oh = rem / a.W, ow = rem - oh * a.W;
+      return static_cast<int64_t>(img) * 4 * a.HW + (2 * oh + a.py) * (2 * a.W) + 2 * ow + a.px;
+    } else {
+      return m;
+    }
+  };
 #pragma unroll
   for (int sb = 0; sb < WTN / 64; ++sb) {
 #pragma unroll
@@ -229,8 +259,7 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int m = mb + 8 * k + (lane >> 3);
-        zr[k] = *reinterpret_cast<const uint4*>(
-            a.sz + static_cast<int64_t>(m < a.M ? m : a.M - 1) * a.N + cb);
+        zr[k] = *reinterpret_cast<const uint4*>(a.sz + orow(m < a.M ? m : a.M - 1) * a.N + cb);
       }
     }
 #pragma unroll
@@ -238,7 +267,7 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
       const int pr = 8 * k + (lane >> 3);
       const uint4 v = *reinterpret_cast<const uint4*>(simg + swz(pr, c));
       if (mb + pr < a.M) {
-        *reinterpret_cast<uint4*>(a.y + static_cast<int64_t>(mb + pr) * a.N + cb) = v;
+        *reinterpret_cast<uint4*>(a.y + orow(mb + pr) * a.N + cb) = v;
         if constexpr (BB) {
           const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
           const uint32_t z4[4] = {zr[k].x, zr[k].y, zr[k].z, zr[k].w};
@@ -270,7 +299,8 @@ __global__ __launch_bounds__(BM * BN / WTN, 1) void conv_gemm_kernel(GArgs a) {
     }
     if constexpr (ST) {
       // fold the 8 lanes sharing a channel group (lane & 7), one partial row per (m-tile, wm)
-      float* pp = a.part + (static_cast<int64_t>(nt) * (a.tiles / a.ntn) * WM + mt * WM + wm) * 2 * BN;
+      const int prt = PAR ? a.prt : (a.tiles / a.ntn) * WM, prb = PAR ? a.prb : 0;
+      float* pp = a.part + (static_cast<int64_t>(nt) * prt + prb + mt * WM + wm) * 2 * BN;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         float sv = ss[q], qv = sq[q];
@@ -327,13 +357,41 @@ int narrow_variant() {
   return v;
 }
 
+// Small-M shapes (the layer-3 / 4 convs at batch 256: 98-196 tiles of 256 x 256 for 256 CUs) take
+// smaller tiles when the 256 x 256 grid has fewer than CML_CONV_GEMM_SMALLM tiles (default 512;
+// 0 disables): variant CML_CONV_GEMM_SMALLV (default 0 = 128 x 128, 2 workgroups per CU).
+int smallm_tiles() {
+  static const int v = [] {
+    const char* e = getenv("CML_CONV_GEMM_SMALLM");
+    return e ? atoi(e) : 512;
+  }();
+  return v;
+}
+int smallm_variant() {
+  static const int v = [] {
+    const char* e = getenv("CML_CONV_GEMM_SMALLV");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+// the variant and tile (BM, BN) for an M x N output
+int pick_variant(int64_t M, int N, int* BM, int* BN) {
+  const bool wide = N % 128 == 0;
+  int v = wide ? gemm_variant() : 0;
+  if (v == 4 && N % 256) v = 2;                   // 256 x 256 tiles need N % 256 == 0
+  if (v == 4 && smallm_tiles() > 0 && (M + 255) / 256 * (N / 256) < smallm_tiles())
+    v = smallm_variant();
+  *BM = !wide ? (narrow_variant() >= 2 ? 128 : 256) : (v >= 2 ? 256 : 128);
+  *BN = v == 4 ? 256 : (wide ? 128 : 64);
+  return v;
+}
+
 template <int TAPS>
 hipError_t launch_v(GArgs& a, int64_t M, hipStream_t st) {
   const bool wide = a.N % 128 == 0;
-  int v = wide ? gemm_variant() : 0;
-  if (v == 4 && a.N % 256) v = 2;                 // 256 x 256 tiles need N % 256 == 0
-  const int BM = !wide ? (narrow_variant() >= 2 ? 128 : 256) : (v >= 2 ? 256 : 128);
-  const int BN = v == 4 ? 256 : (wide ? 128 : 64);
+  int BM, BN;
+  const int v = pick_variant(M, a.N, &BM, &BN);
   a.ntn = a.N / BN;
   const int64_t tiles = (M + BM - 1) / BM * a.ntn;
   if (tiles >= (1ll << 31)) return hipErrorInvalidValue;
@@ -358,19 +416,13 @@ hipError_t launch_v(GArgs& a, int64_t M, hipStream_t st) {
 }  // namespace
 
 namespace {
-// the tile (BM, BN) launch_v picks for N
-void tile_of(int N, int* BM, int* BN) {
-  const bool wide = N % 128 == 0;
-  int v = wide ? gemm_variant() : 0;
-  if (v == 4 && N % 256) v = 2;
-  *BM = !wide ? (narrow_variant() >= 2 ? 128 : 256) : (v >= 2 ? 256 : 128);
-  *BN = v == 4 ? 256 : (wide ? 128 : 64);
-}
+// the tile (BM, BN) launch_v picks for M x N
+void tile_of(int64_t M, int N, int* BM, int* BN) { (void)pick_variant(M, N, BM, BN); }
 }  // namespace
 
 size_t conv_gemm_part_floats(int64_t M, int N) {
   int BM, BN;
-  tile_of(N, &BM, &BN);
+  tile_of(M, N, &BM, &BN);
   const int64_t mtiles = (M + BM - 1) / BM;
   const int R = static_cast<int>(mtiles * (BM / 64));
   // the slab, then the fold area of launch_bn_stats_finalize
@@ -409,7 +461,7 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
   hipError_t e = taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
   if (e != hipSuccess || !part || !mean) return e;
   int BM, BN;
-  tile_of(N, &BM, &BN);
+  tile_of(M, N, &BM, &BN);
   const int R = static_cast<int>((M + BM - 1) / BM) * (BM / 64);
   return launch_bn_stats_finalize(part, R, BN, N, M, shift, eps, momentum, mean, invstd, rmean,
                                   rvar, st, part + static_cast<size_t>(N / BN) * R * 2 * BN);
@@ -449,10 +501,108 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
   hipError_t e = taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
   if (e != hipSuccess) return e;
   int BM, BN;
-  tile_of(N, &BM, &BN);
+  tile_of(M, N, &BM, &BN);
   const int R = static_cast<int>((M + BM - 1) / BM) * (BM / 64);
   return launch_bnbwd_sums_finalize(part, R, BN, N, invstd, sdz, sdzx, st,
                                     part + static_cast<size_t>(N / BN) * R * 2 * BN);
+}
+
+namespace {
+// the tile of the stride-2 data gradient for N = Ci output channels
+// (small grids -- fewer than smallm_tiles() 256 x 256 tiles per class, e.g. batch 256 -- take
+// 128 x 128 tiles, two workgroups per CU)
+void tile_par(int64_t Mc, int N, int* BM, int* BN, int* WTN) {
+  *BM = 256;
+  *BN = N % 256 == 0 ? 256 : (N % 128 == 0 ? 128 : 64);
+  *WTN = *BN == 256 ? 128 : 64;
+  if (*BN >= 128 && smallm_tiles() > 0 && (Mc + 255) / 256 * (N / 256 > 0 ? N / 256 : 1) <
+                                               smallm_tiles()) {
+    *BM = 128;
+    *BN = 128;
+    *WTN = 64;
+  }
+}
+
+template <int BM, int BN, int WTN>
+hipError_t launch_par(GArgs a, hipStream_t st) {
+  auto k = a.sz ? &conv_gemm_kernel<BM, BN, 9, 2, WTN, true, true, true>
+                : &conv_gemm_kernel<BM, BN, 9, 2, WTN, false, false, true>;
+  const size_t lds = 2 * static_cast<size_t>(BM + BN) * 128;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  a.ntn = a.N / BN;
+  const int64_t mt = (static_cast<int64_t>(a.M) + BM - 1) / BM;
+  if (mt * a.ntn >= (1ll << 31)) return hipErrorInvalidValue;
+  a.tiles = static_cast<int>(mt * a.ntn);
+  a.prt = static_cast<int>(4 * mt * (BM / 64));
+  // the 4-tap class first, the 1-tap class last (its short k loop fills the others' tails)
+  static const int order[4][2] = {{1, 1}, {1, 0}, {0, 1}, {0, 0}};
+  for (int i = 0; i < 4; ++i) {
+    a.py = order[i][0];
+    a.px = order[i][1];
+    a.KS = (a.py + 1) * (a.px + 1) * (a.C / kBK);
+    a.prb = static_cast<int>(i * mt * (BM / 64));
+    k<<<a.tiles, BM * BN / WTN, lds, st>>>(a);
+  }
+  return hipGetLastError();
+}
+}  // namespace
+
+size_t conv_gemm_s2dgrad_part_floats(int64_t Mc, int N) {
+  int BM, BN, WTN;
+  tile_par(Mc, N, &BM, &BN, &WTN);
+  const int R = static_cast<int>(4 * ((Mc + BM - 1) / BM) * (BM / 64));
+  return static_cast<size_t>(N / BN) * (static_cast<size_t>(R) + bn_part_fold_slices(R, N / BN)) *
+         2 * BN;
+}
+
+// dx [Nimg, 2 Ho, 2 Wo, Ci] of a stride-2 / padding-1 3x3 conv from dy [Nimg, Ho, Wo, Co] and
+// the rotated, transposed weights wr [Ci][9 Co] (conv3x3_wlayouts), four parity-class launches
+// that together write every pixel once. With z: also the sums of the BN + ReLU backward dx feeds
+// (as launch_conv_gemm_bnsums).
+hipError_t launch_conv_gemm_s2dgrad(const void* dy, const void* wr, void* dx, const void* zero,
+                                    int Nimg, int Ho, int Wo, int Co, int Ci, const void* z,
+                                    const float* sc, const float* bi, const float* mean,
+                                    const float* invstd, float* part, float* sdz, float* sdzx,
+                                    hipStream_t st) {
+  const int64_t Mc = static_cast<int64_t>(Nimg) * Ho * Wo;
+  if (Co % kBK || Ci % 64 || Mc < 1 || 4 * Mc >= (1ll << 31) || 9ll * Co > 65536 || !zero)
+    return hipErrorInvalidValue;
+  if (z && (!sc || !bi || !mean || !invstd || !part || !sdz || !sdzx)) return hipErrorInvalidValue;
+  GArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(dy);
+  a.w = reinterpret_cast<const uint16_t*>(wr);
+  a.y = reinterpret_cast<uint16_t*>(dx);
+  a.zero = reinterpret_cast<const uint16_t*>(zero);
+  a.M = static_cast<int>(Mc);
+  a.C = Co;
+  a.N = Ci;
+  a.H = Ho;
+  a.W = Wo;
+  a.HW = Ho * Wo;
+  a.S = 1;
+  a.IH = Ho;
+  a.IW = Wo;
+  a.IHW = Ho * Wo;
+  a.wld = 9 * Co;
+  if (z) {
+    a.part = part;
+    a.shift = mean;
+    a.sz = reinterpret_cast<const uint16_t*>(z);
+    a.ep_sc = sc;
+    a.ep_bi = bi;
+  }
+  int BM, BN, WTN;
+  tile_par(Mc, Ci, &BM, &BN, &WTN);
+  hipError_t e;
+  if (BM == 128) e = launch_par<128, 128, 64>(a, st);
+  else if (BN == 256) e = launch_par<256, 256, 128>(a, st);
+  else if (BN == 128) e = launch_par<256, 128, 64>(a, st);
+  else e = launch_par<256, 64, 64>(a, st);
+  if (e != hipSuccess || !z) return e;
+  const int R = static_cast<int>(4 * ((Mc + BM - 1) / BM) * (BM / 64));
+  return launch_bnbwd_sums_finalize(part, R, BN, Ci, invstd, sdz, sdzx, st,
+                                    part + static_cast<size_t>(Ci / BN) * R * 2 * BN);
 }
 
 namespace {

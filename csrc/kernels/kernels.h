@@ -362,6 +362,16 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
                                    hipStream_t st);
 hipError_t launch_bnbwd_sums_finalize(const float* part, int R, int BN, int N, const float* invstd,
                                       float* sdz, float* sdzx, hipStream_t st, float* fold);
+// Data gradient dx [Nimg][2 Ho][2 Wo][Ci] of a stride-2 / padding-1 3x3 conv (even input) from dy
+// [Nimg][Ho][Wo][Co] and wr [Ci][9 Co] (launch_conv3x3_wlayouts), as four output-parity-class
+// implicit GEMMs of 4 / 2 / 2 / 1 taps. With z non-null also the sums of the BN + ReLU backward
+// dx feeds, as launch_conv_gemm_bnsums (part: conv_gemm_s2dgrad_part_floats(Nimg Ho Wo, Ci)).
+size_t conv_gemm_s2dgrad_part_floats(int64_t Mc, int N);
+hipError_t launch_conv_gemm_s2dgrad(const void* dy, const void* wr, void* dx, const void* zero,
+                                    int Nimg, int Ho, int Wo, int Co, int Ci, const void* z,
+                                    const float* sc, const float* bi, const float* mean,
+                                    const float* invstd, float* part, float* sdz, float* sdzx,
+                                    hipStream_t st);
 // The forward (wf [Co][9 Ci], k = (3 ky + kx) Ci + ci) and data-gradient (wr [Ci][9 Co], rotated
 // and transposed: wr[ci][(3 ky + kx) Co + co] = w[co][ci][2 - ky][2 - kx]) GEMM layouts of a bf16
 // 3x3 conv weight with strides s0..s3 (elements), in one launch; wf may be null.
