@@ -224,6 +224,25 @@ class Bottleneck(nn.Module):
             return fconv.conv3x3(x, self.conv2)
         return self.conv2(x)
 
+    def _down_s2_compact_ok(self, x: torch.Tensor, dlink) -> bool:
+        c = self.down_conv
+        return (dlink is not None and _P().down_s2_compact and c.stride == (2, 2)
+                and x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0
+                and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
+                and x.is_contiguous(memory_format=torch.channels_last))
+
+    def _down_conv_s2_compact(self, x: torch.Tensor, dlink) -> torch.Tensor:
+        """The stride-2 downsample conv as a stride-1 1x1 conv of x[:, :, ::2, ::2] (one subsample
+        pass): forward / data gradient as plain GEMMs at the compact resolution, and the compact
+        data gradient parked on conv1's link (``subsample2_link``) for conv1's data-gradient GEMM to
+        take -- instead of MIOpen's stride-2 backward-data, which zero-fills and writes a
+        full-resolution gradient (layer 4: 1024 -> 2048 at 14 x 14 -> 7 x 7)."""
+        c = self.down_conv
+        xs = fconv.subsample2_link(x, dlink)
+        fwd, dg = conv1x1_policy(c.in_channels, c.out_channels, xs.shape[2] * xs.shape[3])
+        return _Conv1x1Fn.apply(xs, c.weight, None, fwd, dg,
+                                own_wgrad_ok(c.in_channels, c.out_channels))
+
     def _fused_ok(self, x: torch.Tensor) -> bool:
         return (_P().fused_conv1x1 and self.training and torch.is_grad_enabled()
                 and fconv.fused_conv_ok(x, self.conv1.weight)
@@ -329,8 +348,11 @@ class Bottleneck(nn.Module):
         else:
             tlink = dlink if dlink is not None else \
                 (getattr(x, "_cml_pool_link", None) if use_links else None)
-            xin = link_tap(x, tlink) if tlink is not None else x
-            zd, std = self._conv_bn(xin, self.down_conv, self.down_bn)
+            if self._down_s2_compact_ok(x, dlink):
+                zd, std = self._down_conv_s2_compact(x, dlink), None
+            else:
+                xin = link_tap(x, tlink) if tlink is not None else x
+                zd, std = self._conv_bn(xin, self.down_conv, self.down_bn)
             stats = None if (st3 is None or std is None) else st3 + std
             if stats is None and (st3 is not None or std is not None):
                 # one side fused, the other not: let the unfused side compute its statistics

@@ -63,6 +63,8 @@ class PerfPolicy:
     cat_bnsums: bool = True               # bn2's backward sums in the cat GEMM's epilogue
     cat_bnsums_maxc: int = 256
     s2_link_dgrad: bool = True            # compact stride-2 gradient added in conv1's dgrad
+    down_s2_compact: bool = True          # non-recompute stride-2 downsample (layer 4) as a
+                                          # stride-1 GEMM of x[:, :, ::2, ::2], compact gradient
     bn_affine_kernel: bool = True         # one-launch BN affine (sc, bi)
     # ---------------------------------------------------------------- 3x3 convolutions
     own_dgrad3x3: bool = True             # conv_gemm.hip data gradient
@@ -107,6 +109,7 @@ class PerfPolicy:
             cat_bnsums=_env_bool("CML_CAT_BNSUMS", True),
             cat_bnsums_maxc=_env_int("CML_CAT_BNSUMS_MAXC", 256),
             s2_link_dgrad=_env_bool("CML_S2_LINK_DGRAD", True),
+            down_s2_compact=_env_bool("CML_DOWN_S2_COMPACT", True),
             bn_affine_kernel=_env_bool("CML_BN_AFFINE_KERNEL", True),
             own_dgrad3x3=_env_bool("CML_DGRAD3X3", True),
             conv3x3_bn_stats=_env_bool("CML_CONV3X3_BN_STATS", True),

@@ -98,3 +98,32 @@ def test_downsample_block_s2_matches_library_conv(cuda, monkeypatch, inplanes, p
     assert _rel(outs[True].float(), outs[False].float()) < 2e-2
     for a, r in zip(grads[True], grads[False]):
         assert _rel(a.float(), r.float()) < 3e-2
+
+
+def test_layer4_downsample_compact_matches_strided(cuda, monkeypatch):
+    """Layer-4 downsample block (1024 -> 2048, 14 x 14 -> 7 x 7): the downsample conv as a stride-1
+    GEMM of x[:, :, ::2, ::2] with its compact data gradient handed to conv1's data-gradient GEMM
+    (PerfPolicy.down_s2_compact) vs MIOpen's stride-2 conv; output and every gradient."""
+    import consensusml_amd.models.resnet as R
+    calls = []
+    orig = R.Bottleneck._down_conv_s2_compact
+    monkeypatch.setattr(R.Bottleneck, "_down_conv_s2_compact",
+                        lambda self, *a: (calls.append(1), orig(self, *a))[1])
+    torch.manual_seed(8)
+    blk = R.Bottleneck(1024, 512, stride=2, downsample=True).to(cuda, torch.bfloat16)
+    blk = blk.to(memory_format=torch.channels_last).train()
+    x0 = _nhwc(torch.randn(4, 1024, 14, 14, device=cuda).relu().bfloat16())
+    gy = _nhwc(torch.randn(4, 2048, 7, 7, device=cuda).bfloat16())
+    outs, grads = {}, {}
+    for on in (True, False):
+        with perf.use_policy(perf.policy().replace(down_s2_compact=on)):
+            b = copy.deepcopy(blk)
+            x = x0.clone().requires_grad_(True)
+            y = b(x)
+            y.backward(gy)
+        outs[on] = y.detach()
+        grads[on] = [x.grad] + [p.grad for p in b.parameters()]
+    assert len(calls) == 1, "the compact downsample path did not run exactly once"
+    assert _rel(outs[True].float(), outs[False].float()) < 2e-2
+    for a, r in zip(grads[True], grads[False]):
+        assert _rel(a.float(), r.float()) < 3e-2

@@ -14,7 +14,7 @@ grep '^{' $O/r03_32_shapes.jsonl
 timeout -k 10 300 python -u tools/small_kernels.py --batch 256 --top 60 > $O/r03_32_small256.txt 2>&1 || { tail -30 $O/r03_32_small256.txt; exit 1; }
 head -5 $O/r03_32_small256.txt
 for rep in 1 2; do
-  for arm in default nosmallm nos2; do
+  for arm in default nosmallm; do
     case $arm in
       default) envs="";;
       nosmallm) envs="CML_CONV_GEMM_SMALLM=0";;
