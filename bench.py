@@ -82,6 +82,12 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse "
                          "several ranks sharing one GPU)")
+    ap.add_argument("--loopback", choices=["auto", "on", "off"], default="auto",
+                    help="N = 1: run the engine's distributed code path on a 1-rank process group "
+                         "(every all-to-all / all-gather / all-reduce goes through RCCL, to this "
+                         "rank itself). auto: on with nccl on a GPU")
+    ap.add_argument("--timeout", type=float, default=900.0,
+                    help="seconds any collective may block before the run fails (non-zero exit)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--conv1x1", choices=["auto", "gemm", "miopen"], default="auto",
                     help="1x1 stride-1 conv forward / data gradient as hipBLASLt GEMMs: per-shape "
@@ -107,6 +113,24 @@ def param_checksum(flat_param: torch.Tensor) -> torch.Tensor:
     bits = flat_param.view(torch.int16).to(torch.int64)
     idx = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 65521 + 1
     return torch.stack([(bits * idx).sum(), bits.sum()])
+
+
+def _sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+class _HostEvent:
+    """CPU stand-in for torch.cuda.Event (CPU rehearsals of the launcher / contract)."""
+
+    def __init__(self, **_):
+        self.t = 0.0
+
+    def record(self):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other) -> float:
+        return (other.t - self.t) * 1e3
 
 
 def run(args, rule: str, topology: str, steps: int, warmup: int, info, *, V: int = 1,
@@ -153,8 +177,9 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info, *, V: int
             lv.backward()
             loss = lv.detach() if loss is None else loss + lv.detach()
         if timed:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
+            Ev = torch.cuda.Event if dev.type == "cuda" else _HostEvent
+            e0 = Ev(enable_timing=True)
+            e1 = Ev(enable_timing=True)
             e0.record()
             eng.step()
             e1.record()
@@ -167,24 +192,24 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info, *, V: int
     for i in range(max(warmup, 1 if torch.backends.cudnn.benchmark else 0)):
         step(i)
         if info.rank == 0:   # progress: a cold MIOpen find for new conv shapes can take minutes
-            torch.cuda.synchronize()
+            _sync()
             print(f"[bench] {tag}: warmup step {i} done at {time.perf_counter() - tw:.1f}s",
                   file=sys.stderr, flush=True)
-    torch.cuda.synchronize()
+    _sync()
     if info.rank == 0:
         print(f"[bench] {tag}: warmup {time.perf_counter() - tw:.1f}s", file=sys.stderr,
               flush=True)
     if args.profile_marker:
         torch.cuda._sleep(1000)
     barrier()
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     for i in range(steps):
         loss = step(i, timed=True)
     eng.wait_params()             # the last step's overlapped parameter all-gather
-    torch.cuda.synchronize()
+    _sync()
     barrier()
-    torch.cuda.synchronize()
+    _sync()
     dt = time.perf_counter() - t0
     step_ms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
     if info.distributed:
@@ -213,19 +238,88 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info, *, V: int
     return res
 
 
+def self_launch(n: int) -> int:
+    """``--gpus N`` without a launcher: start N ranks of this script (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* on 127.0.0.1), one process per GPU. The parent never touches the GPU
+    (nothing here initialises HIP), waits for every rank, and returns the first non-zero exit
+    code; once one rank has failed the others get 60 s to fail on their own (a collective
+    timeout) and are then killed, so a broken rank can never leave the run hanging."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                   CML_BENCH_SELF_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=env, start_new_session=True))
+    print(f"[bench] self-launched {n} ranks (pids {[p.pid for p in procs]}, port {port})",
+          file=sys.stderr, flush=True)
+    rc, failed_at = 0, None
+    grace = float(os.environ.get("CML_BENCH_KILL_GRACE_S", "60"))
+    alive = set(range(n))
+    try:
+        while alive:
+            for r in sorted(alive):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                alive.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    failed_at = time.monotonic()
+                    print(f"[bench] rank {r} exited with {c}", file=sys.stderr, flush=True)
+            if alive and failed_at is not None and time.monotonic() - failed_at > grace:
+                for r in alive:
+                    print(f"[bench] killing rank {r} (pid {procs[r].pid})", file=sys.stderr,
+                          flush=True)
+                    os.killpg(procs[r].pid, signal.SIGKILL)
+                for r in alive:
+                    procs[r].wait()
+                alive.clear()
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+        raise
+    return rc
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
+    world_env = int(world_env or "1")
+    if world_env != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        sys.exit(2)
     from consensusml_amd import perf
     perf.set_policy(perf.policy().replace(conv1x1_gemm=args.conv1x1))
     if not args.no_miopen_find:
         from consensusml_amd.utils.tuning import configure_miopen
         configure_miopen()
     from consensusml_amd.parallel.dist import init_distributed
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if world_env != args.gpus:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
-    info = init_distributed(args.dist_backend if world_env > 1 else "auto",
-                            device="cuda:0" if args.dist_backend == "gloo" else None)
+    loopback = world_env == 1 and (args.loopback == "on" or (
+        args.loopback == "auto" and args.dist_backend == "nccl" and torch.cuda.is_available()))
+    backend = args.dist_backend if (world_env > 1 or loopback) else "auto"
+    share = args.dist_backend == "gloo" and torch.cuda.is_available()
+    info = init_distributed(backend, device="cuda:0" if share else None,
+                            timeout_s=args.timeout, loopback=loopback)
+    seen = dist.get_world_size() if dist.is_initialized() else 1
+    if seen != args.gpus or info.world != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but the process group has {seen} rank(s)",
+              file=sys.stderr)
+        sys.exit(2)
+    if os.environ.get("CML_BENCH_FAIL_RANK") == str(info.rank):   # launcher tests
+        print(f"[bench] rank {info.rank}: injected failure", file=sys.stderr, flush=True)
+        os._exit(7)
     # MIOpen find mode: conv solvers are benchmarked on first use of each shape (untimed: the
     # warmup steps, plus one tuning step when --warmup 0) and cached for the run.
     torch.backends.cudnn.benchmark = not args.no_miopen_find
@@ -305,7 +399,7 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (random bf16 224x224 images + labels on device; random-init weights)",
-            "config": {"model": "resnet50", "global_batch": n * args.batch, "seq_len": None,
+            "config": {"model": args.model, "global_batch": n * args.batch, "seq_len": None,
                        "image_size": args.image_size, "per_gpu_batch": args.batch,
                        "parallelism": f"dp{n}", "rule": args.rule, "f": main_res["f"],
                        "topology": args.topology, "optimizer": "sgd-momentum (fused HIP)",
@@ -326,6 +420,15 @@ def main():
             out["world_size_seen"] = main_res["world_size_seen"]
             out["replicas_identical"] = main_res["replicas_identical"] and (
                 base is None or base["replicas_identical"])
+        else:
+            out["dist_backend"] = None
+            out["world_size_seen"] = 1
+        out["selection"] = {"n": main_res["n"], "f": main_res["f"],
+                            "selected_last_step": main_res["selected"],
+                            "selection_counts": main_res["sel_counts"]}
+        out["loopback"] = info.loopback
+        out["launcher"] = ("self" if os.environ.get("CML_BENCH_SELF_LAUNCHED") else
+                           "external" if "WORLD_SIZE" in os.environ else "none")
         out.update(virt)
         out.update(small)
         line = json.dumps(out)

@@ -20,6 +20,7 @@ RULE_IDS = {"mean": 0, "krum": 1, "multi_krum": 2, "geomed": 3, "centered_clip":
             "bulyan_select": 5}
 COORD_RULES = ("median", "trimmed_mean")
 GRAM_RULES = ("krum", "multi_krum", "geomed", "centered_clip")
+GOSSIP_MAX_NBRS = 8   # neighbour buffers one gossip_mix_k launch reads (kMaxNbrs, gossip_fault.hip)
 
 
 def sorted_range(rule: str, n: int, trim: int = 0) -> Tuple[int, int]:

@@ -23,6 +23,10 @@ class DistInfo:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str = "none"
+    # a 1-rank process group that the engine drives exactly like a multi-rank one (every
+    # all-to-all / all-gather / all-reduce / send-recv is issued, to this rank itself): the RCCL
+    # code path of the N > 1 engine, runnable on a single GPU
+    loopback: bool = False
 
     @property
     def is_master(self) -> bool:
@@ -30,15 +34,21 @@ class DistInfo:
 
     @property
     def distributed(self) -> bool:
-        return self.world > 1 and dist.is_available() and dist.is_initialized()
+        return (self.world > 1 or self.loopback) and dist.is_available() and \
+            dist.is_initialized()
 
 
 _INFO: Optional[DistInfo] = None
 
 
 def init_distributed(backend: str = "auto", device: Optional[str] = None,
-                     timeout_s: float = 1800.0) -> DistInfo:
-    """Initialise (once) and return this process's DistInfo."""
+                     timeout_s: float = 1800.0, loopback: bool = False) -> DistInfo:
+    """Initialise (once) and return this process's DistInfo.
+
+    ``loopback``: with WORLD_SIZE 1, still create a (1-rank, in-process store) process group so
+    the engine issues its collectives -- over RCCL when the backend is nccl -- to itself.
+    ``timeout_s`` bounds every collective: a rank that stops answering ends the run with an
+    error (RCCL: the watchdog aborts the communicator and the process) instead of a hang."""
     global _INFO
     if _INFO is not None:
         return _INFO
@@ -56,15 +66,25 @@ def init_distributed(backend: str = "auto", device: Optional[str] = None,
         torch.cuda.set_device(dev)
     if backend == "auto":
         backend = "nccl" if dev.type == "cuda" else "gloo"
-    if world > 1 and not dist.is_initialized():
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29500")
+    if backend == "nccl" and dev.type == "cuda" and local >= torch.cuda.device_count():
+        raise RuntimeError(f"nccl (RCCL) needs one GPU per rank: local rank {local} of "
+                           f"{world} but {torch.cuda.device_count()} visible GPU(s)")
+    loop = bool(loopback and world == 1)
+    if (world > 1 or loop) and not dist.is_initialized():
+        # surface collective failures as errors (the default already does on recent torch)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         kw = dict(backend=backend, rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
+        if loop:
+            kw["store"] = dist.HashStore()
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29500")
         if backend == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
-    _INFO = DistInfo(rank, world, local, dev, backend if world > 1 else "none")
+    active = world > 1 or loop
+    _INFO = DistInfo(rank, world, local, dev, backend if active else "none", loopback=loop)
     return _INFO
 
 

@@ -51,6 +51,38 @@ from .flat import Bucket, FlatModel
 GRAM_RULES = ("krum", "multi_krum", "geomed", "centered_clip", "bulyan")
 
 
+def gossip_peers(graph: str, N: int, r: int, t: int, ring_weights=(1 / 3, 1 / 3, 1 / 3)):
+    """(send-to, recv-from, mixing weights, self weight) of rank r at gossip step t.
+
+    ring     r -+ 1 with ``ring_weights`` = (self, left, right)
+    exp      one rotating peer: send to r + 2^(t mod tau), receive from r - 2^(t mod tau),
+             x <- (x + nb) / 2, tau = ceil(log2 N)
+    exp_all  every distinct r +- 2^i (i < tau) at once, uniform weights 1 / (k + 1)
+    """
+    tau = max(1, (N - 1).bit_length())          # ceil(log2 N)
+    if graph == "ring":
+        w0, w1, w2 = ring_weights
+        left, right = (r - 1) % N, (r + 1) % N
+        return [left, right], [left, right], [w1, w2], w0
+    if graph == "exp":
+        s = 1 << (t % tau)
+        return [(r + s) % N], [(r - s) % N], [0.5], 0.5
+    peers = []
+    for i in range(tau):
+        for q in ((r + (1 << i)) % N, (r - (1 << i)) % N):
+            if q != r and q not in peers:
+                peers.append(q)
+    w = 1.0 / (len(peers) + 1)
+    return peers, peers, [w] * len(peers), w
+
+
+def max_gossip_peers(graph: str, N: int) -> int:
+    """Largest number of neighbour buffers one mixing step reads, over every rank and step
+    (exp_all: 2 ceil(log2 N) - 1 at N = 2^k, e.g. 5 at N = 8 and 9 at N = 32)."""
+    tau = max(1, (N - 1).bit_length())
+    return max(len(gossip_peers(graph, N, r, t)[1]) for r in range(N) for t in range(tau))
+
+
 class ConsensusEngine:
     def __init__(self, model: torch.nn.Module, cfg: TrainConfig, info: DistInfo):
         self.cfg = cfg
@@ -96,7 +128,7 @@ class ConsensusEngine:
             for b in fl.buckets:
                 self.recv.append(torch.zeros(self.rows_total, b.length, dtype=fl.dtype, device=dev))
         self.nb_bufs: List[torch.Tensor] = []
-        if self.topo == "gossip" and self.N > 1:
+        if self.topo == "gossip" and self.group_active:
             self._setup_gossip()
         self._gossip_reqs = None
         self._send_buf = None
@@ -125,7 +157,7 @@ class ConsensusEngine:
         self._flushed: set = set()
         self._in_worker_batch = False
         self._hooks = []
-        self.overlap = bool(cfg.topology.overlap and self.V == 1 and self.N > 1
+        self.overlap = bool(cfg.topology.overlap and self.V == 1 and self.group_active
                             and self.topo in ("allreduce", "allgather", "sharded")
                             and cfg.fault.kind not in COLLUSION)
         fl.release_grads(0)
@@ -612,8 +644,14 @@ class ConsensusEngine:
         chunk by chunk), full vectors in delayed mode (the exchange lands during the next step)."""
         fl, tc = self.flat, self.cfg.topology
         self.gossip_graph = tc.gossip_graph
-        self._tau = max(1, (self.N - 1).bit_length())          # ceil(log2 N)
-        self._chunk = max(int(tc.gossip_chunk_mb * 1024 * 1024 // 2), 64)
+        k = max_gossip_peers(self.gossip_graph, self.N)
+        if k > K.GOSSIP_MAX_NBRS:
+            raise ValueError(
+                f"gossip graph {self.gossip_graph!r} at N={self.N} mixes {k} neighbours per step; "
+                f"the mixing kernel takes at most {K.GOSSIP_MAX_NBRS} (use 'exp' or 'ring')")
+        self._self_copy = self.N == 1 and dist.get_backend() != "nccl"
+        # whole 128-byte lines per chunk: the mixing kernel reads 16-byte aligned vectors
+        self._chunk = max(int(tc.gossip_chunk_mb * 1024 * 1024 // 2) // 64 * 64, 64)
         if self.gossip_graph == "ring":
             nbuf, full = 2, True
         elif self.gossip_graph == "exp":
@@ -629,29 +667,26 @@ class ConsensusEngine:
     def _gossip_peers(self, t: int):
         """(send-to, recv-from, mixing weights, self weight) of gossip step t; recv_from[k] is
         the rank whose parameters land in nb_bufs[k]."""
-        N, r = self.N, self.rank
-        if self.gossip_graph == "ring":
-            w0, w1, w2 = self.cfg.topology.gossip_weights
-            left, right = (r - 1) % N, (r + 1) % N
-            return [left, right], [left, right], [w1, w2], w0
-        if self.gossip_graph == "exp":
-            s = 1 << (t % self._tau)
-            return [(r + s) % N], [(r - s) % N], [0.5], 0.5
-        peers = []
-        for i in range(self._tau):
-            for q in ((r + (1 << i)) % N, (r - (1 << i)) % N):
-                if q != r and q not in peers:
-                    peers.append(q)
-        w = 1.0 / (len(peers) + 1)
-        return peers, peers, [w] * len(peers), w
+        return gossip_peers(self.gossip_graph, self.N, self.rank, t,
+                            self.cfg.topology.gossip_weights)
 
     def _gossip_exchange(self, t: int, s: int, e: int, src: torch.Tensor, bufs, off: int):
         """Grouped send/recv of src[s:e] for step t; neighbour k's slice lands in
         bufs[k][s - off:e - off]."""
         send, recv, _, _ = self._gossip_peers(t)
+        if self._self_copy:
+            # 1-rank loopback group on gloo (no self pairs): the "received" slice is a copy;
+            # RCCL sends to itself for real
+            for k, q in enumerate(recv):
+                if q == self.rank:
+                    bufs[k][s - off:e - off].copy_(src[s:e])
+            send = [q for q in send if q != self.rank]
+            recv = [(k, q) for k, q in enumerate(recv) if q != self.rank]
+        else:
+            recv = list(enumerate(recv))
         ops = [dist.P2POp(dist.isend, src[s:e], q) for q in send]
-        ops += [dist.P2POp(dist.irecv, bufs[k][s - off:e - off], q) for k, q in enumerate(recv)]
-        return dist.batch_isend_irecv(ops)
+        ops += [dist.P2POp(dist.irecv, bufs[k][s - off:e - off], q) for k, q in recv]
+        return dist.batch_isend_irecv(ops) if ops else []
 
     def _gossip_mix(self, t: int, s: int, e: int, off: int = 0) -> None:
         _, _, w, w0 = self._gossip_peers(t)
@@ -665,7 +700,7 @@ class ConsensusEngine:
             m, s1, s2 = self._state(0, fl.total)
             K.agg_update(fl.flat_grad, combine="weighted", n=self.V, opt=opt, master=m, s1=s1,
                          s2=s2, param_out=fl.flat_param)
-        if not self.group_active or self.N == 1:
+        if not self.group_active or not self._gossip_peers(self.step_count)[0]:
             return
         t = self.step_count
         clip = self.cfg.topology.gossip_clip
