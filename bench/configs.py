@@ -38,9 +38,12 @@ CONFIGS = {
                         seq_len=128, dtype="bf16", optim="adamw", lr=1e-4),
     # per-GPU batch 4 x 2048 tokens: ~190 GB at world 1 (+16 GB async send buffer at world > 1)
     # of the 288 GB HBM3E; 18.2k tokens/s vs 12.9k at batch 1 (profiles/r01_configs22_llama.jsonl)
+    # graph "exp": one peer per step (r + 2^(t mod 3) at N = 8): exact averaging after 3 steps
+    # (tests/test_gossip_graphs.py), half the ring's bytes, and ONE 16 GB receive buffer instead
+    # of the ring's two (exp_all would need 5 x 16 GB in delayed mode)
     "llama_gossip": dict(model="llama3_8b", rule="mean", topology="gossip", batch=4,
                          seq_len=2048, dtype="bf16", optim="adamw", lr=1e-5, bucket_mb=512,
-                         gossip_async=True),
+                         gossip_async=True, gossip_graph="exp"),
 }
 
 
@@ -68,6 +71,10 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--model", default=None, help="override the model (e.g. llama_tiny)")
     ap.add_argument("--f", type=int, default=-1)
+    ap.add_argument("--loopback", action="store_true",
+                    help="world 1: run the distributed exchange on a 1-rank process group (RCCL "
+                         "send/recv / all-to-all to this rank itself)")
+    ap.add_argument("--gossip-graph", default=None, choices=["ring", "exp", "exp_all"])
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--profile-marker", action="store_true",
                     help="launch a spin_kernel between warmup and timed steps (prof_summary --after)")
@@ -83,7 +90,7 @@ def main():
     backend = c.get("backend", "auto")
     if backend == "gloo" and torch.cuda.is_available() and os.environ.get("CML_MLP_GPU") == "1":
         backend = "auto"
-    info = init_distributed(backend)
+    info = init_distributed(backend, loopback=a.loopback)
     torch.backends.cudnn.benchmark = info.device.type == "cuda"
     cfg = TrainConfig()
     cfg.model.name = c["model"]
@@ -97,6 +104,7 @@ def main():
     cfg.topology.kind = c["topology"]
     cfg.topology.bucket_mb = c.get("bucket_mb", 64)
     cfg.topology.gossip_async = c.get("gossip_async", False)
+    cfg.topology.gossip_graph = a.gossip_graph or c.get("gossip_graph", "ring")
     cfg.dtype = c["dtype"]
     cfg.optim.name = c["optim"]
     cfg.optim.lr = c["lr"]
@@ -138,6 +146,20 @@ def main():
            "perf_policy": perf.policy().to_dict()}
     if info.device.type == "cuda":
         out["max_mem_gb"] = round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)
+    out["loopback"] = info.loopback
+    if cfg.topology.kind == "gossip":
+        e = tr.engine
+        out["gossip_graph"] = cfg.topology.gossip_graph
+        out["gossip_async"] = cfg.topology.gossip_async
+        out["gossip_exchanged"] = bool(e.nb_bufs)
+        gb = lambda t: round(t.numel() * t.element_size() / 2 ** 30, 2)   # noqa: E731
+        out["memory_plan_gib"] = {
+            "params_bf16": gb(e.flat.flat_param), "grads": gb(e.flat.flat_grad),
+            "master_fp32": gb(e.master),
+            "optimizer_state": round(sum(gb(t) for t in (e.s1, e.s2) if t is not None), 2),
+            "neighbour_buffers": round(sum(gb(t) for t in e.nb_bufs), 2),
+            "send_buffer": gb(e._send_buf) if e._send_buf is not None else 0.0,
+            "n_neighbour_buffers": len(e.nb_bufs)}
     if info.rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -32,8 +32,13 @@ class AggConfig:
     m             number of workers averaged by Multi-Krum; ``None`` -> n - f
     iters, eps    Weiszfeld iterations and distance floor (geometric median)
     tau, clip_iters  radius / iterations of centered clipping
-    centered_gram Gram-space rules: second Gram pass relative to the medoid worker row, so
-                  near-duplicate workers' distances do not cancel (ops.kernels.gram)
+    centered_gram Gram-space rules: the Gram of the rows relative to a medoid worker row, so
+                  near-duplicate workers' distances do not cancel (ops.kernels.gram). ONE pass
+                  per step, centered at the medoid picked from the previous step's Gram; the
+                  first step (and a restore from a checkpoint that has no center) runs an
+                  uncentered pass first to pick it
+    gram_two_pass every step: uncentered pass -> medoid -> centered pass (+ a second Gram
+                  all-reduce in the sharded topology); the round-3 scheme
     """
     rule: str = "mean"
     f: int = 0
@@ -45,6 +50,7 @@ class AggConfig:
     tau: float = 10.0
     clip_iters: int = 3
     centered_gram: bool = True
+    gram_two_pass: bool = False
 
     def validate(self, n: int) -> None:
         if self.rule not in RULES:

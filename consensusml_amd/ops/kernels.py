@@ -158,7 +158,8 @@ def gram(X: torch.Tensor, rows: Optional[torch.Tensor] = None, n: Optional[int] 
     Xr = Xr[:, :D]
     if center is not None:
         c = min(max(int(center[0]), 0), n - 1)
-        Xr = Xr.double() - Xr[c].double()
+        xc = Xr[c].double()
+        Xr = Xr.double() - torch.where(torch.isfinite(xc), xc, torch.zeros_like(xc))
     G = ref.gram(Xr)
     if out is not None:
         if accumulate:

@@ -142,6 +142,7 @@ class ConsensusEngine:
         self.sel = torch.zeros(self.n + 1, dtype=torch.int32, device=dev)
         self.sel_counts = torch.zeros(self.n, dtype=torch.float64, device=dev)
         self.center = torch.zeros(1, dtype=torch.int32, device=dev)   # centered-Gram row
+        self.have_center = False    # self.center holds a medoid from an earlier step
         self.gout = None
         if self.rule == "centered_clip":
             self.gout = torch.zeros(self.state_len, dtype=torch.float32, device=dev)
@@ -454,7 +455,7 @@ class ConsensusEngine:
         self._wait(b)
         X = self._cclip_rows(b) if self.rule == "centered_clip" else self._rows(b)
         length = b.shard if self.topo == "sharded" else X.shape[1]
-        K.gram(X, n=self.rows_total, D=length, out=self.Gb[b.index])
+        K.gram(X, n=self.rows_total, D=length, out=self.Gb[b.index], center=self._pass_center())
         self._gram_done.add(b.index)
 
     def _poll_grams(self) -> None:
@@ -510,10 +511,20 @@ class ConsensusEngine:
         R[: self.n].copy_(X)
         return R
 
+    def _pass_center(self) -> Optional[torch.Tensor]:
+        """Center row of this step's (first) Gram pass: the previous step's medoid (one centered
+        pass per step), or None (uncentered) when no medoid is known yet or two passes are
+        configured."""
+        cfg = self.cfg.agg
+        if cfg.centered_gram and self.have_center and not cfg.gram_two_pass:
+            return self.center
+        return None
+
     def _compute_weights(self, cols) -> None:
         """Gram over every bucket (accumulated in bucket order), all-reduced across shards,
         then weights."""
         cfg = self.cfg.agg
+        center = self._pass_center()
         if self.early_gram:
             # per-bucket partials (most computed during backward), summed in bucket order:
             # G = ((g0 + g1) + g2) ..., the same fp64 adds as accumulating bucket by bucket
@@ -525,12 +536,13 @@ class ConsensusEngine:
         else:
             self.G.zero_()
             for b, X, length in cols:
-                K.gram(X, n=self.rows_total, D=length, out=self.G, accumulate=True)
+                K.gram(X, n=self.rows_total, D=length, out=self.G, accumulate=True, center=center)
         if self.group_active and self.topo == "sharded":
             dist.all_reduce(self.G)
-        if cfg.centered_gram:
-            # second pass relative to the medoid row: exact distances for near-duplicate
-            # workers (the rules are translation invariant, so only the precision changes)
+        if cfg.centered_gram and center is None:
+            # no medoid yet (first step) or the two-pass scheme: a second pass relative to the
+            # medoid of the uncentered G -- exact distances for near-duplicate workers (the rules
+            # are translation invariant, so only the precision changes)
             K.gram_center(self.G, self.rows_total, out=self.center)
             self.G.zero_()
             for b, X, length in cols:
@@ -538,6 +550,11 @@ class ConsensusEngine:
                        center=self.center)
             if self.group_active and self.topo == "sharded":
                 dist.all_reduce(self.G)
+        if cfg.centered_gram:
+            # the medoid of this step's (precise) G centers the next step's single pass; it is
+            # computed on the device from the all-reduced G, so every rank holds the same row
+            K.gram_center(self.G, self.rows_total, out=self.center)
+            self.have_center = True
         rule = "bulyan_select" if self.rule == "bulyan" else self.rule
         m = cfg.m if cfg.m is not None else self.n - cfg.f
         iters = cfg.clip_iters if rule == "centered_clip" else cfg.iters
@@ -860,6 +877,8 @@ class ConsensusEngine:
         self.wait_params()
         sd = {"master": self.master, "step": self.step_count, "sel_counts": self.sel_counts,
               "rank": self.rank, "world": self.N, "topology": self.topo}
+        if self.have_center:
+            sd["gram_center"] = self.center
         if self.topo == "gossip" and self.cfg.topology.gossip_async and \
                 (self._gossip_reqs is not None or self._gossip_restored):
             # delayed gossip: the exchange started at the end of the last step is part of the
@@ -885,6 +904,9 @@ class ConsensusEngine:
             self.s2.copy_(sd["s2"])
         self.step_count = int(sd["step"])
         self.sel_counts.copy_(sd["sel_counts"])
+        if "gram_center" in sd:
+            self.center.copy_(sd["gram_center"])
+            self.have_center = True
         if "v0" in sd and self.gout is not None:
             self.gout.copy_(sd["v0"])
         nb = sd.get("gossip_nb")

@@ -20,12 +20,16 @@
 // Centered Gram (center != null): every row is taken relative to worker row *center,
 // G'_ij = (x_i - x_c) . (x_j - x_c). Every quantity the Gram-space rules read is translation
 // invariant (pairwise distances; distances to an affine combination sum_j a_j x_j with
-// sum a = 1), so G' gives the same weights -- but without the cancellation of
+// sum a = 1) -- and that holds coordinate by coordinate, so the center may be ANY vector: a
+// non-finite element of row c is replaced by 0, which keeps every finite row finite when the
+// center worker has turned non-finite. G' gives the same weights -- but without the
+// cancellation of
 // d_ij = G_ii + G_jj - 2 G_ij when the workers are near-duplicates (|x_i - x_j| << |x|): the fp32
 // MFMA partials then carry ~1e-6 of |x|^2, which is all of d_ij for a tight honest cluster. The
 // difference is formed in fp32 (exact for bf16 inputs) and rounded once to the MFMA input type.
 // gram_center_kernel picks the center: the medoid (least summed squared distance to the finite
-// rows) of a first, uncentered G.
+// rows) of a G; the engine uses the medoid of step t - 1 as step t's center, so one centered pass
+// per step suffices (the medoid of an honest cluster stays inside it from step to step).
 //
 // Stage 1 writes one [P, P] fp32 partial per workgroup (fixed-order LDS reduction of its 4
 // waves, folded over column groups); stage 2 sums the partials in fp64 in block order ->
@@ -91,14 +95,17 @@ template <typename T> struct GramLoad;
 template <> struct GramLoad<bf16> {
   typedef uint4 type;
   static __device__ __forceinline__ uint4 zero() { return make_uint4(0, 0, 0, 0); }
-  // a - c elementwise (fp32 difference of two bf16 values, rounded once to bf16)
+  // a - c elementwise (fp32 difference of two bf16 values, rounded once to bf16); a non-finite
+  // center element counts as 0 (the center may be any vector, see the header)
   static __device__ __forceinline__ uint4 sub(uint4 a, uint4 c) {
     const uint32_t av[4] = {a.x, a.y, a.z, a.w}, cv[4] = {c.x, c.y, c.z, c.w};
     uint32_t o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float lo = __uint_as_float(av[i] << 16) - __uint_as_float(cv[i] << 16);
-      const float hi = __uint_as_float(av[i] & 0xffff0000u) - __uint_as_float(cv[i] & 0xffff0000u);
+      const uint32_t clo = (cv[i] & 0x7f80u) == 0x7f80u ? 0u : (cv[i] << 16);
+      const uint32_t chi = (cv[i] & 0x7f800000u) == 0x7f800000u ? 0u : (cv[i] & 0xffff0000u);
+      const float lo = __uint_as_float(av[i] << 16) - __uint_as_float(clo);
+      const float hi = __uint_as_float(av[i] & 0xffff0000u) - __uint_as_float(chi);
       o[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
     }
     return make_uint4(o[0], o[1], o[2], o[3]);
@@ -116,8 +123,9 @@ template <> struct GramLoad<bf16> {
 template <> struct GramLoad<float> {
   typedef float4 type;
   static __device__ __forceinline__ float4 zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  static __device__ __forceinline__ float fin(float c) { return isfinite(c) ? c : 0.f; }
   static __device__ __forceinline__ float4 sub(float4 a, float4 c) {
-    return make_float4(a.x - c.x, a.y - c.y, a.z - c.z, a.w - c.w);
+    return make_float4(a.x - fin(c.x), a.y - fin(c.y), a.z - fin(c.z), a.w - fin(c.w));
   }
   static __device__ __forceinline__ float4 tail(const float* p, int64_t c, int64_t D) {
     if (c + 4 <= D) return *reinterpret_cast<const float4*>(p + c);

@@ -189,3 +189,40 @@ def test_jsonl_step_log_has_consensus_stats(tmp_path):
         # the sign-flipped worker (x10) has the largest gradient norm and is never selected
         assert max(range(5), key=lambda i: r["worker_grad_norm"][i]) == 2
         assert r["weights"][2] == 0.0
+
+
+def test_single_pass_center_equals_two_pass_cpu():
+    """One Gram pass centered at the previous step's medoid selects what the two-pass scheme
+    selects (CPU reference path), including after the center row turns non-finite."""
+    import torch
+    from consensusml_amd import TrainConfig
+    from consensusml_amd.parallel.dist import DistInfo
+    from consensusml_amd.parallel.engine import ConsensusEngine
+
+    def eng(two):
+        torch.manual_seed(0)
+        cfg = TrainConfig()
+        cfg.virtual_workers = 8
+        cfg.agg.rule = "multi_krum"
+        cfg.agg.f = 2
+        cfg.agg.gram_two_pass = two
+        cfg.topology.kind = "sharded"
+        cfg.topology.bucket_mb = 0.01
+        cfg.optim.lr = 0.0
+        return ConsensusEngine(torch.nn.Linear(64, 64), cfg, DistInfo())
+
+    one, two = eng(False), eng(True)
+    g = torch.Generator().manual_seed(5)
+    for step in range(4):
+        base = torch.randn(one.flat.total, generator=g)
+        X = base + 0.01 * torch.randn(8, one.flat.total, generator=g)
+        X[6:] = base + 0.5 * torch.randn(2, one.flat.total, generator=g)
+        if step == 3:
+            X[int(one.center)] = float("nan")
+        for e in (one, two):
+            e.zero_grad()
+            e.flat.flat_grad.copy_(X.to(e.flat.flat_grad.dtype))
+            e._flushed = {b.index for b in e.flat.buckets}
+            e.step()
+        assert torch.equal(one.w, two.w), step
+        assert one.have_center
