@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.bn import ResidualLink
-from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, bert_embed,
+from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, bert_embed, ffn_gelu,
                                fused_qkv_attention, linear, qkv_split, rope_tables, swiglu)
 
 
@@ -63,7 +63,7 @@ class BertLayer(nn.Module):
         l1, l2 = ResidualLink(), ResidualLink()
         a = fused_qkv_attention(self.qkv(x, l1), self.h, D // self.h)
         _, x = add_norm(x, self.o(a), self.ln1.weight, self.ln1.bias, self.ln1.eps, l1)  # post-LN
-        _, x = add_norm(x, self.fc2(F.gelu(self.fc1(x, l2))), self.ln2.weight, self.ln2.bias,
+        _, x = add_norm(x, ffn_gelu(x, self.fc1, self.fc2, l2), self.ln2.weight, self.ln2.bias,
                         self.ln2.eps, l2)
         return x
 

@@ -443,3 +443,112 @@ class Linear(nn.Linear):
 
     def forward(self, x: torch.Tensor, link: Optional[ResidualLink] = None) -> torch.Tensor:
         return linear(x, self.weight, self.bias, link)
+
+
+# ============================================================================ fused GELU FFN
+def _gemm_ok(M: int, N: int, K: int) -> bool:
+    try:
+        return bool(lib().gemm_nt_ok(M, N, K))
+    except Exception:
+        return False
+
+
+def _bias_grad_rows(b: torch.Tensor, V: int):
+    """(destination [V, N] of the bias gradient, scatter-back or None): the engine's per-worker
+    rows when batched workers own b, else a fresh [1, N] tensor."""
+    wg = WG.current()
+    if wg is not None and wg.has(b):
+        dst, first = wg.out(b)
+        dst = dst.view(V, -1)
+        if first:
+            return dst, None
+        tmp = torch.empty_like(dst)
+        return tmp, (lambda: dst.add_(tmp))
+    return torch.empty(1, b.shape[0], dtype=b.dtype, device=b.device), None
+
+
+class _FFNGeluFn(torch.autograd.Function):
+    """y = fc2(gelu(fc1(x))) with the elementwise work in GEMM epilogues (csrc/kernels/gemm.hip):
+
+    forward   fc1 on gemm.hip, epilogue h = x W1^T + b1 (kept for the backward) and a = gelu(h);
+              fc2 = a W2^T + b2 (hipBLASLt)
+    backward  dh = (dy W2) * gelu'(h) as ONE gemm.hip launch (dy against the transposed W2), with
+              the fc1 bias gradient as column sums in the same epilogue (per worker segment for
+              batched virtual workers); weight gradients and dx on hipBLASLt
+    The unfused composition rounds h, a, da and dh to bf16 at the same points."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, link):
+        x2 = x.reshape(-1, x.shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        M, F1 = x2.shape[0], w1.shape[0]
+        h = torch.empty(M, F1, dtype=x.dtype, device=x.device)
+        a = lib().gemm_nt(x2, w1, 1, bias=b1, aux=h)
+        y = F.linear(a, w2, b2)
+        ctx.save_for_backward(x2, w1, w2, h, a)
+        ctx.link = link
+        ctx.params = (w1, b1, w2, b2)
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1, w2, h, a = ctx.saved_tensors
+        pw1, pb1, pw2, pb2 = ctx.params
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        wg = WG.current()
+        V = wg.V if wg is not None and (wg.has(pb1) or wg.has(pw1)) else 1
+        cs, post = _bias_grad_rows(pb1, V)
+        dh = lib().gemm_nt(dy2, w2.t().contiguous(), 2, aux=h, colsum_out=cs)
+        if post is not None:
+            post()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            g = ctx.link.take() if ctx.link is not None else None
+            if g is not None and g.is_contiguous() and g.shape == ctx.xshape:
+                dx = g.view(-1, x2.shape[-1]).addmm_(dh, w1).view(ctx.xshape)
+            elif g is not None:
+                dx = (g.reshape(-1, x2.shape[-1]) + dh @ w1).view(ctx.xshape)
+            else:
+                dx = (dh @ w1).view(ctx.xshape)
+        if wg is not None and (wg.has(pw1) or wg.has(pw2)):
+            T = dy2.shape[0] // wg.V
+            for pw, gout, gin in ((pw1, dh, x2), (pw2, dy2, a)):
+                dst, first = wg.out(pw)
+                A = gout.view(wg.V, T, -1).transpose(1, 2)
+                Bm = gin.view(wg.V, T, -1)
+                if first:
+                    torch.bmm(A, Bm, out=dst.view(wg.V, pw.shape[0], pw.shape[1]))
+                else:
+                    dst.view(wg.V, pw.shape[0], pw.shape[1]).baddbmm_(A, Bm)
+            if wg.has(pb2):
+                dst, first = wg.out(pb2)
+                if first:
+                    lib().colsum_seg(dy2, wg.V, dst.view(wg.V, -1))
+                else:
+                    dst.view(wg.V, -1).add_(dy2.view(wg.V, T, -1).sum(1))
+            return dx, None, None, None, None, None
+        dw1 = dh.t() @ x2 if ctx.needs_input_grad[1] else None
+        db1 = cs.view(-1) if ctx.needs_input_grad[2] else None
+        dw2 = dy2.t() @ a if ctx.needs_input_grad[3] else None
+        db2 = lib().colsum(dy2) if ctx.needs_input_grad[4] else None
+        return dx, dw1, db1, dw2, db2, None
+
+
+def ffn_gelu(x: torch.Tensor, fc1: nn.Linear, fc2: nn.Linear,
+             link: Optional[ResidualLink] = None) -> torch.Tensor:
+    """fc2(gelu(fc1(x))) (erf GELU). bf16 GPU tensors of gemm.hip-eligible shapes (tokens and FFN
+    width multiples of 256) run the fused epilogue path; everything else the composition."""
+    w1, b1, w2, b2 = fc1.weight, fc1.bias, fc2.weight, fc2.bias
+    M = x.numel() // x.shape[-1]
+    wg = WG.current()
+    ok = (_P().fused_ffn and _gpu_bf16(x, w1, b1, w2, b2) and b1 is not None
+          and b2 is not None and _gemm_ok(M, w1.shape[0], w1.shape[1])
+          and _gemm_ok(M, w1.shape[0], w2.shape[0]) and w2.shape[0] % 8 == 0
+          and (wg is None or M % (128 * wg.V) == 0))
+    if ok:
+        return _FFNGeluFn.apply(x, w1, b1, w2, b2, link)
+    return fc2(F.gelu(fc1(x, link)))

@@ -1852,6 +1852,67 @@ void lasso_step(Tensor& v, Tensor& beta, const Tensor& g, const Tensor& step, co
 
 int64_t lasso_slices(int64_t p) { return cml::lasso_slices(static_cast<int>(p)); }
 
+// Dense NT GEMM with fused epilogues (gemm.hip). y = epi(a [M, K] @ b [N, K]^T).
+// ep 0: + bias; ep 1: aux <- h = a b^T + bias, y = gelu(h); ep 2: y = (a b^T) * gelu'(aux) and,
+// with colsum_out, its column sums per row segment (colsum_out [nseg, N], bf16 or fp32, unit
+// column stride, any row stride).
+Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tensor>& bias,
+               const optional<Tensor>& aux, const optional<Tensor>& out,
+               const optional<Tensor>& colsum_out) {
+  check_dev(a, "a");
+  check_dev(b, "b");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm_nt: bf16");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1,
+              "gemm_nt: 2-D operands with unit column stride");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "gemm_nt: K mismatch");
+  TORCH_CHECK(cml::gemm_nt_eligible(M, N, K), "gemm_nt: needs M % 256 == 0, N % 256 == 0, K % 64 == 0");
+  const c10::DeviceGuard guard(a.device());
+  Tensor y;
+  if (out.has_value() && out->defined()) {
+    y = *out;
+    TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 2 && y.size(0) == M &&
+                y.size(1) == N && y.stride(1) == 1, "gemm_nt: out must be bf16 [M, N]");
+  } else {
+    y = at::empty({M, N}, a.options());
+  }
+  cml::GemmArgs g{};
+  g.a = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  g.b = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  g.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  g.M = M; g.N = N; g.K = K;
+  g.lda = a.stride(0); g.ldb = b.stride(0); g.ldy = y.stride(0);
+  g.bias = opt_ptr<const uint16_t>(bias, at::kBFloat16, "bias", N);
+  if (ep == cml::EP_GELU || ep == cml::EP_DGELU) {
+    TORCH_CHECK(aux.has_value() && aux->defined(), "gemm_nt: ep ", ep, " needs aux");
+    TORCH_CHECK(aux->scalar_type() == at::kBFloat16 && aux->dim() == 2 && aux->size(0) == M &&
+                aux->size(1) == N && aux->stride(1) == 1 && aux->stride(0) == y.stride(0),
+                "gemm_nt: aux must be bf16 [M, N] with out's row stride");
+    g.aux = reinterpret_cast<uint16_t*>(aux->data_ptr());
+  }
+  Tensor part;
+  const bool cs = colsum_out.has_value() && colsum_out->defined();
+  if (cs) {
+    TORCH_CHECK(ep == cml::EP_DGELU, "gemm_nt: column sums only with ep 2");
+    TORCH_CHECK(colsum_out->dim() == 2 && colsum_out->size(1) == N && colsum_out->stride(1) == 1,
+                "gemm_nt: colsum_out must be [nseg, N]");
+    part = at::empty({M / 128, N}, a.options().dtype(at::kFloat));
+    g.part = part.data_ptr<float>();
+  }
+  CML_CHECK_HIP(cml::launch_gemm_nt(g, static_cast<int>(ep), cur_stream()));
+  if (cs) {
+    const bool f32 = colsum_out->scalar_type() == at::kFloat;
+    TORCH_CHECK(f32 || colsum_out->scalar_type() == at::kBFloat16, "colsum_out: bf16 or fp32");
+    CML_CHECK_HIP(cml::launch_colsum_fold(part.data_ptr<float>(), M, static_cast<int>(N),
+                                          static_cast<int>(colsum_out->size(0)),
+                                          colsum_out->data_ptr(), colsum_out->stride(0),
+                                          f32 ? 1 : 0, cur_stream()));
+  }
+  return y;
+}
+
+bool gemm_nt_ok(int64_t M, int64_t N, int64_t K) { return cml::gemm_nt_eligible(M, N, K); }
+
 // column sums of x viewed as [M, N] (N = last dim) -> bf16 [N]
 Tensor colsum(const Tensor& x_in) {
   Tensor x = x_in.contiguous();
@@ -2059,6 +2120,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lasso_step", &lasso_step, "batched FISTA prox / restart / momentum step");
   m.def("lasso_slices", &lasso_slices);
   m.def("colsum", &colsum, "column sums of a bf16 matrix (bias gradient)");
+  m.def("gemm_nt", &gemm_nt, "NT GEMM with fused epilogues (bias / bias+GELU / GELU backward + "
+        "column sums)", py::arg("a"), py::arg("b"), py::arg("ep"), py::arg("bias") = py::none(),
+        py::arg("aux") = py::none(), py::arg("out") = py::none(),
+        py::arg("colsum_out") = py::none());
+  m.def("gemm_nt_ok", &gemm_nt_ok, "shape eligibility of gemm_nt");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);
   m.attr("OPT_NONE") = static_cast<int>(cml::OPT_NONE);

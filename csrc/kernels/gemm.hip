@@ -1,0 +1,370 @@
+// Dense bf16 GEMM with fused epilogues for the transformer FFN (BERT: bias + GELU forward, GELU
+// backward + bias-gradient column sums), gfx950 / CDNA4:
+//
+//   y[m][n] = epi( sum_k A[m][k] B[n][k] )           A [M][K], B [N][K]: both K-contiguous ("NT",
+//                                                     nn.Linear's x W^T)
+//   EP_STORE   y = bf16(acc + bias[n])                (bias optional)
+//   EP_GELU    h = bf16(acc + bias[n]) -> aux,  y = bf16(gelu(h))   (erf GELU, from the bf16 h)
+//   EP_DGELU   g = bf16(acc);  y = bf16(g * gelu'(aux[m][n])),  part[m / 128][n] = column sums of y
+//
+// The rounding points are those of the unfused PyTorch composition (GEMM output rounded to bf16,
+// then the elementwise op in fp32 on the bf16 values), so the fused path changes only the GEMM's
+// summation order.
+//
+// Tile and schedule (one 512-thread workgroup = 8 waves per 256 x 256 output tile, 1 per CU):
+//   * waves as 2 (m) x 4 (n); each owns 128 x 64 outputs = 8 x 4 accumulators of
+//     v_mfma_f32_16x16x32_bf16, computed transposed (C^T = B A^T) so that a lane holds 4
+//     consecutive output channels of one row -- 8-B packed bf16 writes into the epilogue image;
+//   * K in 64-deep tiles through two LDS buffers (2 x 64 KB: A then B image, 128-B rows,
+//     XOR-swizzled so every ds_read_b128 lane group hits 16 distinct bank slots; the swizzle lives
+//     in the per-lane SOURCE address since global_load_lds writes lane-linear);
+//   * each K-tile is computed in 4 phases, one output quadrant (64 m x 32 n, 16 MFMAs) each; a
+//     phase is a read section (fragment ds_reads, one staging issue, a counted vmcnt) and an
+//     MFMA section, each closed by a raw s_barrier. The waves of m-row 1 (the second wave on
+//     every SIMD) run one section behind m-row 0 (one extra barrier up front, one at the end for
+//     m-row 0), so every SIMD alternates one wave's MFMAs with its partner's LDS reads.
+//     Fragments read per phase: 1 = the wave's first 64 A rows + first 32 B rows, 2 = the second
+//     32 B rows, 3 = the second 64 A rows, 4 = none. A tile is staged as 4 units matching that
+//     order (U1 = A rows 0-63 of each 128-row half, U2 = B rows 0-31 of each 64-row group,
+//     U3 = the other B rows, U4 = the other A rows), one unit (2 global_load_lds dwordx4 per
+//     lane) per phase: U3, U4 of tile t+1 in phases 1, 2 and U1, U2 of tile t+2 in phases 3, 4.
+//     With the one-section stagger a region may be restaged only 2 phases after its last read
+//     (WAR: the lagging group retires its reads one barrier later), which this order meets
+//     (U1: 2 phases, U2-U4: 3). Each read section ends with `s_waitcnt vmcnt(8)` (4 newer units
+//     may stay in flight) before its barrier: that retires exactly the unit(s) the NEXT phase
+//     reads, early enough for the lagging group (RAW); every unit has 4 phases of flight and the
+//     queue never drains in the loop. Past the last K-tile the issues repeat the last tile into
+//     dead buffers, so the counts stay uniform.
+//   * epilogue: each wave rounds its 128 x 64 block into its own 16 KB LDS image and reads it
+//     back as 16-B row pieces (8 lanes per 128-B row): whole-line global stores, 8 fixed
+//     channels per lane for the column sums.
+//   * tiles are mapped XCD-aware: the n-tiles of one m-tile get consecutive ids, and
+//     consecutive ids share an XCD under round-robin placement (A read from HBM once).
+// Requirements (checked by the launcher): M % 256 == 0, N % 256 == 0, K % 64 == 0, 16-B aligned
+// rows. Other shapes go to hipBLASLt (ops/transformer.py).
+#include "common.h"
+#include "kernels.h"
+
+namespace cml {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void g_void;
+
+constexpr int kT = 256;                 // tile edge
+constexpr int kBK = 64;                 // K per tile step
+constexpr int kThreads = 512;
+constexpr int kImg = kT * 128;          // one operand image (256 rows x 128 B)
+constexpr int kBuf = 2 * kImg;          // A image + B image
+constexpr int kLds = 2 * kBuf;          // 128 KB
+
+__device__ __forceinline__ int swz(int row, int c) { return row * 128 + 16 * (c ^ ((row >> 1) & 7)); }
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8_t a, bf16x8_t b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// erf-GELU and its derivative. erf by Abramowitz-Stegun 7.1.26 (|error| < 1.5e-7, far below the
+// bf16 output's resolution) instead of ocml's erff: 2 transcendentals (rcp, exp), and the
+// exp(-x^2 / 2) term is shared with the derivative's density.
+__device__ __forceinline__ float erf_as(float z, float e) {   // e = exp(-z^2)
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  const float r = fmaf(-p * t, e, 1.f);
+  return copysignf(r, z);
+}
+__device__ __forceinline__ float gelu_f(float x) {
+  const float z = x * 0.70710678118654752f;
+  const float e = __expf(-z * z);
+  return 0.5f * x * (1.f + erf_as(z, e));
+}
+// d gelu / dx = Phi(x) + x phi(x)
+__device__ __forceinline__ float dgelu_f(float x) {
+  const float z = x * 0.70710678118654752f;
+  const float e = __expf(-z * z);
+  return fmaf(0.5f, erf_as(z, e), 0.5f) + x * 0.3989422804014327f * e;
+}
+
+template <int EP>
+__global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // ---- tile (bijective XCD remap: consecutive ids share an XCD; n fastest)
+  const int ntn = a.N / kT;
+  const int G = (a.M / kT) * ntn, b = blockIdx.x, xcd = b & 7, q8 = G >> 3, r8 = G & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int mtile = t / ntn, ntile = t - mtile * ntn;
+  const int m0 = mtile * kT, n0 = ntile * kT;
+  const int nk = a.K / kBK;
+
+  // ---- staging: unit u (0..3 = U1..U4) of K-tile kt into buffer buf; this wave's 2 of the
+  // unit's 16 wave-instructions (8 rows x 128 B each)
+  const int lrow = lane >> 3, lp = lane & 7;
+  auto stage = [&](int u, int kt, int buf) {
+    kt = kt < nk ? kt : nk - 1;                 // past the end: a harmless repeat (dead buffer)
+    const int64_t kofs = static_cast<int64_t>(kt) * kBK;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = wave + 8 * s;               // wave-instruction of the unit
+      int row0;
+      if (u == 0 || u == 3) row0 = (i >> 3) * 128 + (u == 3 ? 64 : 0) + (i & 7) * 8;   // A
+      else row0 = (i >> 2) * 64 + (u == 2 ? 32 : 0) + (i & 3) * 8;                  // B
+      const int row = row0 + lrow;
+      const int c = lp ^ ((row >> 1) & 7);
+      const bool isA = (u == 0 || u == 3);
+      const uint16_t* src = isA ? a.a + static_cast<int64_t>(m0 + row) * a.lda + kofs + 8 * c
+                                : a.b + static_cast<int64_t>(n0 + row) * a.ldb + kofs + 8 * c;
+      char* dst = smem + buf * kBuf + (isA ? 0 : kImg) + row0 * 128;
+      __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
+    }
+  };
+
+  // ---- fragments: lane row lane & 15, 16-B chunk (lane >> 4) + 4 ks
+  const int fr = lane & 15, fc = lane >> 4;
+  bf16x8_t aF[2][4][2], bF[2][2][2];
+  auto readA = [&](bf16x8_t (&f)[4][2], int mh, int buf) {
+    const char* img = smem + buf * kBuf;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        f[mt][ks] = *reinterpret_cast<const bf16x8_t*>(
+            img + swz(wm * 128 + mh * 64 + mt * 16 + fr, fc + 4 * ks));
+  };
+  auto readB = [&](bf16x8_t (&f)[2][2], int nh, int buf) {
+    const char* img = smem + buf * kBuf + kImg;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        f[nt][ks] = *reinterpret_cast<const bf16x8_t*>(
+            img + swz(wn * 64 + nh * 32 + nt * 16 + fr, fc + 4 * ks));
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto quad = [&](int mh, int nh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          acc[mh * 4 + mt][nh * 2 + nt] =
+              mfma16(bF[nh][nt][ks], aF[mh][mt][ks], acc[mh * 4 + mt][nh * 2 + nt]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto wait8 = [] { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // ---- prologue: tile 0 whole, U1 + U2 of tile 1; retire U1, U2 of tile 0
+  stage(0, 0, 0); stage(1, 0, 0); stage(2, 0, 0); stage(3, 0, 0);
+  stage(0, 1, 1); stage(1, 1, 1);
+  wait8();
+  bar();
+  // stagger: the m-row-1 waves (the second wave of every SIMD) run one section behind, so each
+  // SIMD alternates one wave's MFMA section with its partner's read / issue section
+  if (wm) bar();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    // phase 1: quadrant (0, 0)
+    stage(2, kt + 1, buf ^ 1);
+    readA(aF[0], 0, buf);
+    readB(bF[0], 0, buf);
+    wait8();                  // retires U3 of tile kt (read in phase 2)
+    bar();
+    quad(0, 0);
+    bar();
+    // phase 2: quadrant (0, 1)
+    stage(3, kt + 1, buf ^ 1);
+    readB(bF[1], 1, buf);
+    wait8();                  // retires U4 of tile kt (phase 3)
+    bar();
+    quad(0, 1);
+    bar();
+    // phase 3: quadrant (1, 1)
+    stage(0, kt + 2, buf);
+    readA(aF[1], 1, buf);
+    wait8();
+    bar();
+    quad(1, 1);
+    bar();
+    // phase 4: quadrant (1, 0), no fragment reads
+    stage(1, kt + 2, buf);
+    wait8();                  // retires U1, U2 of tile kt + 1 (next phase 1)
+    bar();
+    quad(1, 0);
+    bar();
+  }
+  if (!wm) bar();             // balance the stagger barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+
+  // ---- epilogue: bf16 image of the wave's 128 (m) x 64 (n) block, [m][128 B] swizzled
+  char* img = smem + wave * (128 * 128);
+  // lane's 16 output channels (4 per accumulator column group): n = ni 16 + 4 fc + j
+  float bias[4][4];
+  if (a.bias) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const uint2 bv = *reinterpret_cast<const uint2*>(a.bias + n0 + wn * 64 + ni * 16 + 4 * fc);
+      bias[ni][0] = __uint_as_float(bv.x << 16);
+      bias[ni][1] = __uint_as_float(bv.x & 0xffff0000u);
+      bias[ni][2] = __uint_as_float(bv.y << 16);
+      bias[ni][3] = __uint_as_float(bv.y & 0xffff0000u);
+    }
+  } else {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bias[ni][j] = 0.f;
+  }
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const f32x4 v = acc[mi][ni];
+      const uint2 w = make_uint2(pk_bf16(v[0] + bias[ni][0], v[1] + bias[ni][1]),
+                                 pk_bf16(v[2] + bias[ni][2], v[3] + bias[ni][3]));
+      const int row = mi * 16 + fr;
+      const int ch = ni * 2 + (fc >> 1);
+      *reinterpret_cast<uint2*>(img + swz(row, ch) + 8 * (fc & 1)) = w;
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+
+  const int c8 = lane & 7;
+  const int ncol = n0 + wn * 64 + 8 * c8;
+  float cs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const int row = 8 * it + lrow;
+    const uint4 v = *reinterpret_cast<const uint4*>(img + swz(row, c8));
+    const int64_t m = m0 + wm * 128 + row;
+    uint16_t* yp = a.y + m * a.ldy + ncol;
+    if constexpr (EP == EP_STORE) {
+      *reinterpret_cast<uint4*>(yp) = v;
+    } else if constexpr (EP == EP_GELU) {
+      *reinterpret_cast<uint4*>(a.aux + m * a.ldy + ncol) = v;
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        o[q] = pk_bf16(gelu_f(__uint_as_float(w4[q] << 16)),
+                       gelu_f(__uint_as_float(w4[q] & 0xffff0000u)));
+      *reinterpret_cast<uint4*>(yp) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {   // EP_DGELU
+      const uint4 hv = *reinterpret_cast<const uint4*>(a.aux + m * a.ldy + ncol);
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, h4[4] = {hv.x, hv.y, hv.z, hv.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        o[q] = pk_bf16(__uint_as_float(w4[q] << 16) * dgelu_f(__uint_as_float(h4[q] << 16)),
+                       __uint_as_float(w4[q] & 0xffff0000u) *
+                           dgelu_f(__uint_as_float(h4[q] & 0xffff0000u)));
+        cs[2 * q] += __uint_as_float(o[q] << 16);
+        cs[2 * q + 1] += __uint_as_float(o[q] & 0xffff0000u);
+      }
+      *reinterpret_cast<uint4*>(yp) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  if constexpr (EP == EP_DGELU) {
+    if (a.part) {
+      // lanes with equal lane & 7 hold the same 8 channels: fixed-order xor tree over lane >> 3
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float s = cs[e];
+        s += __shfl_xor(s, 8, 64);
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        cs[e] = s;
+      }
+      if (lane < 8) {
+        float* p = a.part + static_cast<int64_t>(mtile * 2 + wm) * a.N + ncol;
+        reinterpret_cast<float4*>(p)[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+        reinterpret_cast<float4*>(p)[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
+      }
+    }
+  }
+}
+
+// out[s][n] = sum over the 128-row blocks r of segment s (rows_per_seg / 128 of them, in order)
+// of part[r][n]; bf16 or fp32 output
+__global__ __launch_bounds__(256) void colsum_fold_kernel(const float* __restrict__ part, int nblk_seg,
+                                                         int N, int64_t ldo, void* out, int out_f32) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int s = blockIdx.y;
+  if (n >= N) return;
+  const float* p = part + static_cast<int64_t>(s) * nblk_seg * N + n;
+  float v = 0.f;
+  for (int r = 0; r < nblk_seg; ++r) v += p[static_cast<int64_t>(r) * N];
+  if (out_f32) reinterpret_cast<float*>(out)[static_cast<int64_t>(s) * ldo + n] = v;
+  else reinterpret_cast<uint16_t*>(out)[static_cast<int64_t>(s) * ldo + n] = f2bf(v);
+}
+
+}  // namespace
+
+bool gemm_nt_eligible(int64_t M, int64_t N, int64_t K) {
+  return M > 0 && N > 0 && K > 0 && M % kT == 0 && N % kT == 0 && K % kBK == 0 &&
+         (M / kT) * (N / kT) < (1LL << 31);
+}
+
+hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st) {
+  if (!gemm_nt_eligible(a.M, a.N, a.K)) return hipErrorInvalidValue;
+  if ((a.lda % 8) || (a.ldb % 8) || (a.ldy % 8)) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(a.a) | reinterpret_cast<uintptr_t>(a.b) |
+       reinterpret_cast<uintptr_t>(a.y)) % 16)
+    return hipErrorInvalidValue;
+  if ((ep == EP_GELU || ep == EP_DGELU) && (a.aux == nullptr || reinterpret_cast<uintptr_t>(a.aux) % 16))
+    return hipErrorInvalidValue;
+  const int tiles = (a.M / kT) * (a.N / kT);
+  switch (ep) {
+    case EP_STORE:
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<EP_STORE>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+      gemm_nt_kernel<EP_STORE><<<tiles, kThreads, kLds, st>>>(a);
+      break;
+    case EP_GELU:
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<EP_GELU>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+      gemm_nt_kernel<EP_GELU><<<tiles, kThreads, kLds, st>>>(a);
+      break;
+    case EP_DGELU:
+      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<EP_DGELU>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+      gemm_nt_kernel<EP_DGELU><<<tiles, kThreads, kLds, st>>>(a);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_colsum_fold(const float* part, int64_t M, int N, int nseg, void* out, int64_t ldo,
+                              int out_f32, hipStream_t st) {
+  if (nseg < 1 || M % (128LL * nseg) != 0 || N % 8 != 0) return hipErrorInvalidValue;
+  const int nblk_seg = static_cast<int>(M / 128 / nseg);
+  dim3 grid((N + 255) / 256, nseg);
+  colsum_fold_kernel<<<grid, 256, 0, st>>>(part, nblk_seg, N, ldo, out, out_f32);
+  return hipGetLastError();
+}
+
+}  // namespace cml

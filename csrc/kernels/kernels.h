@@ -473,4 +473,27 @@ hipError_t launch_smo(const double* K, const double* y, const int* ns, int B, in
                       const double* C, double tol, int max_iter, double* alpha, double* grad,
                       int* iters, hipStream_t stream);
 
+// Dense NT GEMM with fused epilogues (gemm.hip): y[M][N] = epi(A[M][K] B[N][K]^T), bf16 in/out,
+// fp32 accumulation. EP_STORE: + bias[N] (bf16, optional); EP_GELU: aux = h = bf16(acc + bias),
+// y = bf16(gelu(h)); EP_DGELU: y = bf16(bf16(acc) * gelu'(aux)) and, when part is set, fp32
+// column sums of y per 128-row block into part [M / 128][N]. M % 256 == 0, N % 256 == 0,
+// K % 64 == 0, leading dimensions % 8 == 0, 16-B aligned bases.
+enum { EP_STORE = 0, EP_GELU = 1, EP_DGELU = 2 };
+struct GemmArgs {
+  const uint16_t* a;
+  const uint16_t* b;
+  uint16_t* y;
+  uint16_t* aux;
+  const uint16_t* bias;
+  float* part;
+  int64_t M, N, K;
+  int64_t lda, ldb, ldy;
+};
+bool gemm_nt_eligible(int64_t M, int64_t N, int64_t K);
+hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st);
+// out[s][n] = sum of the 128-row partial column sums of segment s of M rows (nseg equal
+// segments, fixed order); out bf16 [nseg][ldo] or fp32 when out_f32
+hipError_t launch_colsum_fold(const float* part, int64_t M, int N, int nseg, void* out, int64_t ldo,
+                              int out_f32, hipStream_t st);
+
 }  // namespace cml
