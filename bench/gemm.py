@@ -66,6 +66,17 @@ def main():
         if name.startswith("fc1") and not name.endswith("dgrad"):
             r["own_gelu_ms"] = timeit(lambda: lib().gemm_nt(x, w, 1, bias=bias, aux=h, out=y), a.reps)
             r["blas_gelu_ms"] = timeit(lambda: F.gelu(F.linear(x, w, bias)), a.reps)
+        if name == "fc2_dgrad":
+            cs = torch.empty(8, N, dtype=torch.bfloat16, device=dev)
+            h.copy_(y)
+            r["own_dgelu_ms"] = timeit(lambda: lib().gemm_nt(x, w, 2, aux=h, out=y, colsum_out=cs),
+                                       a.reps)
+
+            def blas_dgelu():
+                g = torch.matmul(x, w.t())
+                d = torch.ops.aten.gelu_backward(g, h)
+                return lib().colsum_seg(d, 8, cs)
+            r["blas_dgelu_ms"] = timeit(blas_dgelu, a.reps)
         for k in list(r):
             if k.endswith("_ms"):
                 r[k] = round(r[k], 4)

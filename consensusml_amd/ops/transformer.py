@@ -374,6 +374,17 @@ def swiglu(h: torch.Tensor) -> torch.Tensor:
 
 
 # ============================================================================ linear (bias grad)
+def _own_gemm(M: int, N: int, K: int) -> bool:
+    """gemm.hip for a bf16 GEMM of this shape: eligible (256-multiples) and enough 256 x 256
+    tiles to fill the chip (>= 128; below that hipBLASLt's smaller tiles win, bench/gemm.py)."""
+    if not _P().own_gemm:
+        return False
+    try:
+        return bool(lib().gemm_nt_ok(M, N, K)) and (M // 256) * (N // 256) >= 128
+    except Exception:
+        return False
+
+
 class _LinearFn(torch.autograd.Function):
     """y = x W^T + b with the bias gradient from the column-sum kernel (PyTorch's generic column
     reduction runs these at ~0.4 TB/s: 7 % of the BERT step in profiles/r01_prof13)."""
@@ -383,6 +394,9 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.link = link
         ctx.params = (w, b)
+        x2 = x.reshape(-1, x.shape[-1])
+        if _own_gemm(x2.shape[0], w.shape[0], w.shape[1]) and x2.is_contiguous():
+            return lib().gemm_nt(x2, w, 0, bias=b).view(*x.shape[:-1], w.shape[0])
         return F.linear(x, w, b)
 
     @staticmethod
@@ -392,7 +406,18 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             g = ctx.link.take() if ctx.link is not None else None
-            if g is not None and g.is_contiguous() and g.shape == x.shape:
+            K = x.shape[-1]
+            own = _own_gemm(dy2.shape[0], K, w.shape[0]) and dy2.is_contiguous()
+            if own and (g is None or (g.is_contiguous() and g.shape == x.shape)):
+                # data gradient on gemm.hip against the transposed weight, the parked residual
+                # gradient added in the epilogue (in place)
+                wt = w.t().contiguous()
+                if g is not None:
+                    g2 = g.view(-1, K)
+                    dx = lib().gemm_nt(dy2, wt, 0, out=g2, cin=g2).view(x.shape)
+                else:
+                    dx = lib().gemm_nt(dy2, wt, 0).view(x.shape)
+            elif g is not None and g.is_contiguous() and g.shape == x.shape:
                 dx = g.view(-1, x.shape[-1]).addmm_(dy2, w).view(x.shape)   # beta = 1 epilogue
             elif g is not None:
                 dx = (g.reshape(-1, x.shape[-1]) + dy2 @ w).view(x.shape)
@@ -485,7 +510,8 @@ class _FFNGeluFn(torch.autograd.Function):
         M, F1 = x2.shape[0], w1.shape[0]
         h = torch.empty(M, F1, dtype=x.dtype, device=x.device)
         a = lib().gemm_nt(x2, w1, 1, bias=b1, aux=h)
-        y = F.linear(a, w2, b2)
+        y = (lib().gemm_nt(a, w2, 0, bias=b2) if _own_gemm(M, w2.shape[0], F1)
+             else F.linear(a, w2, b2))
         ctx.save_for_backward(x2, w1, w2, h, a)
         ctx.link = link
         ctx.params = (w1, b1, w2, b2)
@@ -508,7 +534,16 @@ class _FFNGeluFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             g = ctx.link.take() if ctx.link is not None else None
-            if g is not None and g.is_contiguous() and g.shape == ctx.xshape:
+            K = x2.shape[-1]
+            if _own_gemm(dh.shape[0], K, dh.shape[1]) and (
+                    g is None or (g.is_contiguous() and g.shape == ctx.xshape)):
+                w1t = w1.t().contiguous()
+                if g is not None:
+                    g2 = g.view(-1, K)
+                    dx = lib().gemm_nt(dh, w1t, 0, out=g2, cin=g2).view(ctx.xshape)
+                else:
+                    dx = lib().gemm_nt(dh, w1t, 0).view(ctx.xshape)
+            elif g is not None and g.is_contiguous() and g.shape == ctx.xshape:
                 dx = g.view(-1, x2.shape[-1]).addmm_(dh, w1).view(ctx.xshape)
             elif g is not None:
                 dx = (g.reshape(-1, x2.shape[-1]) + dh @ w1).view(ctx.xshape)

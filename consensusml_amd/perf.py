@@ -79,6 +79,7 @@ class PerfPolicy:
     attn_kernel: bool = True              # MFMA attention for short sequences (BERT)
     multi_copy: bool = True               # multi-tensor HIP copy for gradient capture
     batched_workers: bool = True          # virtual workers as one batched fwd/bwd (BERT)
+    own_gemm: bool = True                 # gemm.hip for transformer linears with >= 128 tiles
     fused_ffn: bool = True                # BERT FFN on gemm.hip: bias + GELU in fc1's epilogue,
                                           # GELU backward + bias gradient in the dgrad epilogue
 
@@ -122,6 +123,7 @@ class PerfPolicy:
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),
             multi_copy=_env_bool("CML_MULTI_COPY", True),
             batched_workers=_env_bool("CML_BATCHED_WORKERS", True),
+            own_gemm=_env_bool("CML_OWN_GEMM", True),
             fused_ffn=_env_bool("CML_FUSED_FFN", True),
         )
 

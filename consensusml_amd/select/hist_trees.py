@@ -286,12 +286,17 @@ class ExactForest:
         n, p = X.shape
         ex = exact_bins(X)
         if ex is None:
+            import warnings
+            warnings.warn(f"ExactForest: a feature has more than 128 distinct training values "
+                          f"(n = {n}); using 128 quantile bins (approximate thresholds)",
+                          RuntimeWarning, stacklevel=2)
             Xb, self.edges = quantile_bins(X, 128)
             B = 128
             self.exact = False
         else:
             Xb, self.edges, B = ex
             self.exact = True
+        self.n_bins = B
         Xb = Xb.contiguous()
         k = max(1, int(math.sqrt(p))) if self.mf == "sqrt" else (
             max(1, int(math.log2(p))) if self.mf == "log2" else p)

@@ -275,7 +275,12 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
                 out = {"importance": rf.mean_decrease_gini.numpy(),
                        "predicted_test": pred.numpy(),
                        "conf.matrix": confusion_matrix(yte.cpu(), pred, 2).numpy(),
-                       "ntree": nt, "test_metrics": binary_metrics(yte.cpu(), pred)}
+                       "ntree": nt, "test_metrics": binary_metrics(yte.cpu(), pred),
+                       # which split finder ran (ExactForest falls back to 128 quantile bins
+                       # past 128 distinct training values per feature)
+                       "split_method": {"exact": bool(getattr(rf, "exact", tree_method != "hist")),
+                                        "bins": int(getattr(rf, "n_bins", 0) or 0),
+                                        "impl": type(rf).__name__}}
                 if rf_proximity:
                     out["proximity"] = rf.proximity(Xtr).cpu().numpy()
                 return out
@@ -356,6 +361,8 @@ def consensus_pipeline(es: ExpressionSet, label_col: str = "low_risk",
         out["membership"].to_csv(os.path.join(out_dir, "membership.csv"))
         with open(os.path.join(out_dir, "summary.json"), "w") as fh:
             json.dump({"n_genes": len(genes), "runs": runs, "resumed_stages": st.skipped,
+                       "rf_split_method": {f"rf{nt}": rf_res[f"rf{nt}.results"].get("split_method")
+                                           for nt in rf_trees},
                        "device": str(dev), "stage_seconds": stage_s,
                        "consensus_all_models": int((table.df["consensus_votes"] ==
                                                     len(valid)).sum()),

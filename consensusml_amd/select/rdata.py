@@ -53,6 +53,11 @@ ATTRLANGSXP, ATTRLISTSXP, ALTREP_SXP, BCREPREF = 240, 239, 238, 243
 UTF8_MASK, LATIN1_MASK, BYTES_MASK, ASCII_MASK = 1 << 3, 1 << 2, 1 << 1, 1 << 6
 
 
+import threading as _threading
+
+_STACK_LOCK = _threading.Lock()
+
+
 class RDataError(ValueError):
     pass
 
@@ -532,13 +537,21 @@ def _deep(fn):
         finally:
             sys.setrecursionlimit(old)
 
-    prev = threading.stack_size()
-    threading.stack_size(512 * 1024 * 1024)
-    try:
-        t = threading.Thread(target=run, name="rdata-parse")
-        t.start()
-    finally:
-        threading.stack_size(prev)
+    # the parse thread's stack, sized from the depth bound: ~4 interpreter frames per nesting
+    # level at a few KB each, with headroom (64 MB at MAX_DEPTH 8192). stack_size() is
+    # process-wide, so it is set and restored under a lock: a thread another thread starts
+    # meanwhile never inherits it by accident
+    size = max(32 << 20, 4 * MAX_DEPTH * 2048)
+    with _STACK_LOCK:
+        prev = threading.stack_size()
+        try:
+            threading.stack_size(size)
+            t = threading.Thread(target=run, name="rdata-parse")
+            t.start()
+        except (RuntimeError, ValueError, MemoryError) as e:
+            raise RDataError(f"cannot start the parse thread with a {size >> 20} MB stack: {e}")
+        finally:
+            threading.stack_size(prev)
     t.join()
     if "e" in out:
         raise out["e"]

@@ -1858,7 +1858,7 @@ int64_t lasso_slices(int64_t p) { return cml::lasso_slices(static_cast<int>(p));
 // column stride, any row stride).
 Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tensor>& bias,
                const optional<Tensor>& aux, const optional<Tensor>& out,
-               const optional<Tensor>& colsum_out) {
+               const optional<Tensor>& colsum_out, const optional<Tensor>& cin) {
   check_dev(a, "a");
   check_dev(b, "b");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm_nt: bf16");
@@ -1883,6 +1883,13 @@ Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tens
   g.M = M; g.N = N; g.K = K;
   g.lda = a.stride(0); g.ldb = b.stride(0); g.ldy = y.stride(0);
   g.bias = opt_ptr<const uint16_t>(bias, at::kBFloat16, "bias", N);
+  if (cin.has_value() && cin->defined()) {
+    TORCH_CHECK(ep == cml::EP_STORE, "gemm_nt: cin only with ep 0");
+    TORCH_CHECK(cin->scalar_type() == at::kBFloat16 && cin->dim() == 2 && cin->size(0) == M &&
+                cin->size(1) == N && cin->stride(1) == 1 && cin->stride(0) == y.stride(0),
+                "gemm_nt: cin must be bf16 [M, N] with out's row stride");
+    g.cin = reinterpret_cast<const uint16_t*>(cin->data_ptr());
+  }
   if (ep == cml::EP_GELU || ep == cml::EP_DGELU) {
     TORCH_CHECK(aux.has_value() && aux->defined(), "gemm_nt: ep ", ep, " needs aux");
     TORCH_CHECK(aux->scalar_type() == at::kBFloat16 && aux->dim() == 2 && aux->size(0) == M &&
@@ -2123,7 +2130,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, "NT GEMM with fused epilogues (bias / bias+GELU / GELU backward + "
         "column sums)", py::arg("a"), py::arg("b"), py::arg("ep"), py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("out") = py::none(),
-        py::arg("colsum_out") = py::none());
+        py::arg("colsum_out") = py::none(), py::arg("cin") = py::none());
   m.def("gemm_nt_ok", &gemm_nt_ok, "shape eligibility of gemm_nt");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);

@@ -3,7 +3,8 @@
 //
 //   y[m][n] = epi( sum_k A[m][k] B[n][k] )           A [M][K], B [N][K]: both K-contiguous ("NT",
 //                                                     nn.Linear's x W^T)
-//   EP_STORE   y = bf16(acc + bias[n])                (bias optional)
+//   EP_STORE   y = bf16(acc + bias[n]) [+ cin[m][n]]  (bias, cin optional; cin may alias y: the
+//                                                     residual-gradient add of a data gradient)
 //   EP_GELU    h = bf16(acc + bias[n]) -> aux,  y = bf16(gelu(h))   (erf GELU, from the bf16 h)
 //   EP_DGELU   g = bf16(acc);  y = bf16(g * gelu'(aux[m][n])),  part[m / 128][n] = column sums of y
 //
@@ -217,6 +218,20 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   bar();
 
   // ---- epilogue: bf16 image of the wave's 128 (m) x 64 (n) block, [m][128 B] swizzled
+  // The second operand of the read-back (DGELU: h; STORE with cin: the residual gradient) is
+  // loaded for all 16 read-back rows up front, so its latency overlaps the image writes instead
+  // of stalling every row (a dependent load per row cost ~13 us per tile).
+  const int c8 = lane & 7;
+  const int ncol = n0 + wn * 64 + 8 * c8;
+  constexpr bool kPre = EP == EP_DGELU || EP == EP_STORE;
+  const uint16_t* psrc = EP == EP_DGELU ? a.aux : a.cin;
+  uint4 pre[kPre ? 16 : 1];
+  if (kPre && psrc) {
+#pragma unroll
+    for (int it = 0; it < 16; ++it)
+      pre[it] = *reinterpret_cast<const uint4*>(
+          psrc + static_cast<int64_t>(m0 + wm * 128 + 8 * it + lrow) * a.ldy + ncol);
+  }
   char* img = smem + wave * (128 * 128);
   // lane's 16 output channels (4 per accumulator column group): n = ni 16 + 4 fc + j
   float bias[4][4];
@@ -249,19 +264,28 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 
-  const int c8 = lane & 7;
-  const int ncol = n0 + wn * 64 + 8 * c8;
   float cs[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) cs[e] = 0.f;
-#pragma unroll 4
+#pragma unroll
   for (int it = 0; it < 16; ++it) {
     const int row = 8 * it + lrow;
     const uint4 v = *reinterpret_cast<const uint4*>(img + swz(row, c8));
     const int64_t m = m0 + wm * 128 + row;
     uint16_t* yp = a.y + m * a.ldy + ncol;
     if constexpr (EP == EP_STORE) {
-      *reinterpret_cast<uint4*>(yp) = v;
+      if (a.cin) {   // y = bf16(bf16(acc + bias) + cin): a residual gradient added on the way out
+        const uint4 cv = pre[it];
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, c4[4] = {cv.x, cv.y, cv.z, cv.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[q] = pk_bf16(__uint_as_float(w4[q] << 16) + __uint_as_float(c4[q] << 16),
+                         __uint_as_float(w4[q] & 0xffff0000u) + __uint_as_float(c4[q] & 0xffff0000u));
+        *reinterpret_cast<uint4*>(yp) = make_uint4(o[0], o[1], o[2], o[3]);
+      } else {
+        *reinterpret_cast<uint4*>(yp) = v;
+      }
     } else if constexpr (EP == EP_GELU) {
       *reinterpret_cast<uint4*>(a.aux + m * a.ldy + ncol) = v;
       const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
@@ -272,7 +296,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
                        gelu_f(__uint_as_float(w4[q] & 0xffff0000u)));
       *reinterpret_cast<uint4*>(yp) = make_uint4(o[0], o[1], o[2], o[3]);
     } else {   // EP_DGELU
-      const uint4 hv = *reinterpret_cast<const uint4*>(a.aux + m * a.ldy + ncol);
+      const uint4 hv = pre[it];
       const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, h4[4] = {hv.x, hv.y, hv.z, hv.w};
       uint32_t o[4];
 #pragma unroll

@@ -486,6 +486,7 @@ struct GemmArgs {
   uint16_t* aux;
   const uint16_t* bias;
   float* part;
+  const uint16_t* cin;    // EP_STORE: y = bf16(bf16(acc + bias) + cin), cin [M][ldy] (may be y)
   int64_t M, N, K;
   int64_t lda, ldb, ldy;
 };

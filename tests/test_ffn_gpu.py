@@ -65,3 +65,29 @@ def test_ffn_gelu_matches_unfused_bf16(cuda):
                            fc2.weight.grad.clone(), fc2.bias.grad.clone()]
     for a, b in zip(outs[True], outs[False]):
         assert _rel(a, b) < 6e-3
+
+
+def test_linear_own_gemm_with_link(cuda):
+    """ops.transformer.linear on gemm.hip (>= 128 tiles): forward with bias, data gradient against
+    the transposed weight with the parked residual gradient added in place (ResidualLink)."""
+    from consensusml_amd.ops.bn import ResidualLink
+    from consensusml_amd.ops.transformer import _own_gemm, linear
+    M, N, K = 16384, 3072, 768
+    assert _own_gemm(M, N, K) and _own_gemm(M, K, N)
+    torch.manual_seed(1)
+    x = torch.randn(M, K, device=cuda).bfloat16().requires_grad_(True)
+    w = (torch.randn(N, K, device=cuda) * 0.05).bfloat16().requires_grad_(True)
+    b = torch.randn(N, device=cuda).bfloat16().requires_grad_(True)
+    link = ResidualLink()
+    y = linear(x, w, b, link)
+    g_res = torch.randn(M, K, device=cuda).bfloat16()
+    link.grad = g_res.clone()
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xf, wf, bf = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yf = F.linear(xf, wf, bf)
+    yf.backward(dy.float())
+    assert _rel(y, yf) < 4e-3
+    assert _rel(x.grad, xf.grad + g_res.float()) < 6e-3
+    assert _rel(w.grad, wf.grad) < 6e-3
+    assert _rel(b.grad, bf.grad) < 1e-2

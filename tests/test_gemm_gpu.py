@@ -95,3 +95,14 @@ def test_gemm_deterministic(cuda):
     y1 = lib().gemm_nt(a, b, 0)
     y2 = lib().gemm_nt(a, b, 0)
     assert torch.equal(y1, y2)
+
+
+def test_gemm_cin_inplace(cuda):
+    """y = a b^T + cin written over cin (the parked residual gradient of a data gradient)."""
+    from consensusml_amd.ops.native import lib
+    a, b = _rand(512, 768, dev=cuda, seed=14), _rand(256, 768, dev=cuda, seed=15)
+    c = _rand(512, 256, dev=cuda, seed=16)
+    ref = a.float() @ b.float().t() + c.float()
+    y = lib().gemm_nt(a, b, 0, out=c, cin=c)
+    assert y.data_ptr() == c.data_ptr()
+    assert _rel(c, ref) < 4e-3

@@ -98,10 +98,17 @@ def test_lasso_rep1_parity(ref):
     assert abs(res["cv_fit"]["lambda_min"] - lmin_ref) / lmin_ref < 1e-6       # 0.1630
     assert abs(res["test_error"] - float(rl["test.error"].values[0])) < 1e-6   # 3 / 44
     ours = res["nonzero_coef"]
-    assert set(ref_coef) <= set(ours)                                          # 13 genes
+    assert set(ref_coef) == set(ours)                                          # 13 genes
     a = np.array([ours[g] for g in ref_coef])
     b = np.array(list(ref_coef.values()))
-    assert np.corrcoef(a, b)[0, 1] > 0.99
+    assert np.corrcoef(a, b)[0, 1] > 0.9999
+    # per coefficient vs glmnet's refit (`...seanalysis.Rmd:110-115`): ours is the exact optimum
+    # (objective 0.32552073 vs glmnet's 0.32552075, glmnet stops at thresh = 1e-7), so the
+    # tolerance is glmnet's own convergence error: < 1 % relative on every coefficient above
+    # 1e-3, and < 5e-5 absolute on the one at the selection boundary (2.75e-4)
+    big = np.abs(b) > 1e-3
+    np.testing.assert_allclose(a[big], b[big], rtol=1e-2)
+    np.testing.assert_allclose(a[~big], b[~big], atol=5e-5)
 
 
 def test_xgb_importance_parity(ref):
