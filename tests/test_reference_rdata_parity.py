@@ -33,23 +33,51 @@ def _ref_dir() -> str:
 REF = _ref_dir()
 SE = os.path.join(REF, "sesetfilt_degseahack_targetaml.rda")
 STAND = os.path.join(REF, "standouttable.csv")
+# derived, data-only subset (tools/make_ref_fixture.py): what the model-parity tests need, so they
+# also run on GPU boxes without /root/reference
+FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures",
+                       "reference_subset.npz")
+HAVE_RDA = os.path.exists(SE)
 
-pytestmark = pytest.mark.skipif(not os.path.exists(SE), reason="reference files not present")
+pytestmark = pytest.mark.skipif(not (HAVE_RDA or os.path.exists(FIXTURE)),
+                                reason="reference files not present")
+needs_rda = pytest.mark.skipif(not HAVE_RDA, reason="needs the reference's .rda files")
 
 
 @pytest.fixture(scope="module")
 def ref():
+    if HAVE_RDA:
+        from consensusml_amd.select.data import ExpressionSet
+        es = ExpressionSet.from_rdata(SE)
+        cd = es.col_data
+        tr = np.where(cd["exptset.seahack"].to_numpy() == "train")[0]
+        te = np.where(cd["exptset.seahack"].to_numpy() == "test")[0]
+        y = torch.tensor(pd.to_numeric(cd["deg.risk"]).to_numpy(), dtype=torch.long)
+        X = es.assays["logcpm"].t().contiguous()
+        st = pd.read_csv(STAND, index_col=0).loc[es.genes]
+        return {"es": es, "X": X, "y": y, "tr": tr, "te": te, "st": st, "genes": list(es.genes),
+                "source": "rda"}
+    z = np.load(FIXTURE)                        # allow_pickle=False (default): arrays only
+    genes = [str(g) for g in z["genes"]]
+    st = pd.DataFrame(z["st"], index=genes, columns=[str(c) for c in z["st_cols"]])
+    return {"es": None, "X": torch.from_numpy(z["X"]), "y": torch.from_numpy(z["y"]),
+            "tr": z["train"], "te": z["test"], "st": st, "genes": genes, "fixture": z,
+            "source": "fixture"}
+
+
+def test_fixture_matches_rda():
+    """The committed fixture is exactly what the data-only reader extracts from the reference."""
+    if not (HAVE_RDA and os.path.exists(FIXTURE)):
+        pytest.skip("needs both the .rda files and the fixture")
     from consensusml_amd.select.data import ExpressionSet
     es = ExpressionSet.from_rdata(SE)
-    cd = es.col_data
-    tr = np.where(cd["exptset.seahack"].to_numpy() == "train")[0]
-    te = np.where(cd["exptset.seahack"].to_numpy() == "test")[0]
-    y = torch.tensor(pd.to_numeric(cd["deg.risk"]).to_numpy(), dtype=torch.long)
-    X = es.assays["logcpm"].t().contiguous()
-    st = pd.read_csv(STAND, index_col=0).loc[es.genes]
-    return {"es": es, "X": X, "y": y, "tr": tr, "te": te, "st": st}
+    z = np.load(FIXTURE)
+    np.testing.assert_array_equal(z["X"], es.assays["logcpm"].t().contiguous().numpy()
+                                  .astype(np.float32))
+    assert [str(g) for g in z["genes"]] == list(es.genes)
 
 
+@needs_rda
 def test_rdata_container_matches_reference(ref):
     es, st = ref["es"], ref["st"]
     assert es.shape == (1984, 137)                                  # SEA:454 "1984 137"
@@ -60,6 +88,7 @@ def test_rdata_container_matches_reference(ref):
     assert list(es.row_data["hgnc_symbol"].fillna("")) == list(st["hgnc_symbol"].fillna(""))
 
 
+@needs_rda
 def test_rdata_reader_objects():
     from consensusml_amd.select import rdata as R
     ann = R.read_rdata(os.path.join(REF, "dfens_v95hg38_bmart.rda"))["dfens"]
@@ -78,7 +107,7 @@ def test_rdata_reader_objects():
 def test_svm1_weights_parity(ref):
     from consensusml_amd.select.svm import run_svm
     X, y, tr, te = ref["X"], ref["y"], ref["tr"], ref["te"]
-    r = run_svm(50, "linear", X[tr], y[tr], X[te], y[te], None, ref["es"].genes)
+    r = run_svm(50, "linear", X[tr], y[tr], X[te], y[te], None, ref["genes"])
     w = r["weightsvect"].numpy()
     w_ref = ref["st"]["svm1_weights"].to_numpy()
     assert np.corrcoef(w, w_ref)[0, 1] > 0.9999
@@ -88,15 +117,21 @@ def test_svm1_weights_parity(ref):
 
 
 def test_lasso_rep1_parity(ref):
-    from consensusml_amd.select import rdata as R
     from consensusml_amd.select.lasso import run_lasso
-    rl = R.read_rdata(os.path.join(REF, "lasso_resultslist.rda"))["lasso.resultslist"][0]
-    lmin_ref = float(rl["cv.fit"]["lambda.min"].values[0])
-    nz = rl["nonzero.coef"]
-    ref_coef = dict(zip(R.names(nz), nz.values))
-    res = run_lasso(ref["X"].float(), ref["y"], ref["es"].genes, ref["tr"], ref["te"], seed=2019)
+    if ref["source"] == "rda":
+        from consensusml_amd.select import rdata as R
+        rl = R.read_rdata(os.path.join(REF, "lasso_resultslist.rda"))["lasso.resultslist"][0]
+        lmin_ref = float(rl["cv.fit"]["lambda.min"].values[0])
+        terr_ref = float(rl["test.error"].values[0])
+        nz = rl["nonzero.coef"]
+        ref_coef = dict(zip(R.names(nz), nz.values))
+    else:
+        z = ref["fixture"]
+        lmin_ref, terr_ref = float(z["lasso_lambda_min"]), float(z["lasso_test_error"])
+        ref_coef = dict(zip([str(g) for g in z["lasso_genes"]], z["lasso_coef"]))
+    res = run_lasso(ref["X"].float(), ref["y"], ref["genes"], ref["tr"], ref["te"], seed=2019)
     assert abs(res["cv_fit"]["lambda_min"] - lmin_ref) / lmin_ref < 1e-6       # 0.1630
-    assert abs(res["test_error"] - float(rl["test.error"].values[0])) < 1e-6   # 3 / 44
+    assert abs(res["test_error"] - terr_ref) < 1e-6                            # 3 / 44
     ours = res["nonzero_coef"]
     assert set(ref_coef) == set(ours)                                          # 13 genes
     a = np.array([ours[g] for g in ref_coef])
@@ -135,12 +170,14 @@ def test_rf_importance_parity(ref):
     reference's 2k-tree run about as well as the reference's own 10k-tree run does (Spearman
     0.77, top-50 overlap 43 between rf2k and rf10k)."""
     from scipy.stats import spearmanr
-    from consensusml_amd.select import rdata as R
     from consensusml_amd.select.trees import RandomForest
-    RF = R.read_rdata(os.path.join(REF, "rf_noboost_2k5k10ktrees_allresultslist.rda"))
-    rf = RF["rf.returnlist"]
-    imp2k = R.as_array(rf["rf2k.results"]["fitmodel"]["importance"]).ravel()
-    np.testing.assert_allclose(imp2k, ref["st"]["rfnb_2k_MeanDecNodeImp"].to_numpy(), rtol=1e-9)
+    imp2k = ref["st"]["rfnb_2k_MeanDecNodeImp"].to_numpy()
+    if ref["source"] == "rda":
+        from consensusml_amd.select import rdata as R
+        RF = R.read_rdata(os.path.join(REF, "rf_noboost_2k5k10ktrees_allresultslist.rda"))
+        rf = RF["rf.returnlist"]
+        imp_rda = R.as_array(rf["rf2k.results"]["fitmodel"]["importance"]).ravel()
+        np.testing.assert_allclose(imp_rda, imp2k, rtol=1e-9)
     X, y, tr = ref["X"], ref["y"], ref["tr"]
     m = RandomForest(2000, seed=20).fit(X[tr], y[tr])     # the reference's rf2k size
     ours = m.mean_decrease_gini.numpy()
@@ -151,6 +188,7 @@ def test_rf_importance_parity(ref):
     assert len(top(ours) & top(imp2k)) >= 36
 
 
+@needs_rda
 def test_pipeline_on_reference_container_with_resume(tmp_path, monkeypatch):
     """The reference analysis run from its own DEG container, interrupted after the SVM stage
     and resumed: the finished stage is not recomputed (its result list and table columns are
