@@ -85,7 +85,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         ctx.own_wgrad = own_wgrad
         N, C, H, W = x.shape
         if fwd_gemm:
-            y = torch.mm(x.permute(0, 2, 3, 1).reshape(N * H * W, C), w.reshape(w.shape[0], C).t())
+            y = fconv.conv_mm(x.permute(0, 2, 3, 1).reshape(N * H * W, C), w.reshape(w.shape[0], C))
             return y.view(N, H, W, w.shape[0]).permute(0, 3, 1, 2)
         return F.conv2d(x, w)
 
@@ -120,11 +120,11 @@ class _Conv1x1Fn(torch.autograd.Function):
             if g is not None:
                 dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
                 if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
-                    d2 = dres.addmm_(dy2, w2)          # beta = 1 GEMM epilogue, in place
+                    d2 = fconv.conv_mm(dy2, w2.t(), acc=dres)   # beta = 1 epilogue, in place
                 else:
                     d2 = torch.addmm(dres, dy2, w2)
             else:
-                d2 = torch.mm(dy2, w2)
+                d2 = fconv.conv_mm(dy2, w2.t())
             dx = d2.view(N, H, W, C).permute(0, 3, 1, 2)
         return dx, dw, None, None, None, None
 

@@ -30,7 +30,8 @@ import torch.nn.functional as F
 
 from ..ops.bn import ResidualLink
 from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, bert_embed, ffn_gelu,
-                               fused_qkv_attention, linear, qkv_split, rope_tables, swiglu)
+                               fused_qkv_attention, linear, linear_gelu, qkv_split, rope_tables,
+                               swiglu)
 
 
 # =============================================================================== BERT
@@ -90,7 +91,7 @@ class BertMLM(nn.Module):
         x = self.ln(bert_embed(ids, self.tok.weight, self.pos.weight, self.typ.weight))
         for l in self.layers:
             x = l(x)
-        x = self.head_ln(F.gelu(self.head(x)))
+        x = self.head_ln(linear_gelu(x, self.head))
         return linear(x, self.tok.weight, self.bias)
 
 
@@ -99,7 +100,8 @@ def bert_base() -> BertMLM:
 
 
 def bert_tiny() -> BertMLM:
-    return BertMLM(BertConfig(vocab=512, d=64, layers=2, heads=4, ffn=128, max_pos=128))
+    # vocab not a multiple of 8 (like BERT-base's 30522): tests cover the padded-logits head
+    return BertMLM(BertConfig(vocab=510, d=64, layers=2, heads=4, ffn=128, max_pos=128))
 
 
 # =============================================================================== Llama

@@ -40,6 +40,41 @@ def fused_conv_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and w.shape[0] % 64 == 0 and w.shape[2] == 1 and w.shape[3] == 1)
 
 
+def _nt_ok(a: torch.Tensor, M: int, N: int, K: int) -> bool:
+    """gemm.hip takes this 1x1-conv GEMM: policy on, bf16 GPU operands, 256-multiple M and N,
+    64-multiple K, enough 256 x 256 tiles to fill the chip."""
+    if not (_P().own_gemm_conv1x1 and a.is_cuda and a.dtype == torch.bfloat16):
+        return False
+    try:
+        return bool(lib().gemm_nt_ok(M, N, K)) and (M // 256) * (N // 256) >= 128
+    except Exception:
+        return False
+
+
+CONV_MM_STATS = {"own": 0, "blas": 0}   # which path conv_mm took (tests)
+
+
+def conv_mm(a: torch.Tensor, w_nk: torch.Tensor, acc: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a [M, K] @ w_nk^T (+ acc, in place) for a 1x1 conv as a plain GEMM: the forward (w_nk = W
+    [Co, C]) or the data gradient (w_nk = W^T [C, Co]; acc = a parked residual gradient). On
+    ``gemm.hip`` (NT, acc added in its epilogue: bf16(bf16(a w^T) + acc)) when eligible, else
+    hipBLASLt (mm / addmm_ beta = 1). Replaces the layer-3/4 hipBLASLt GEMMs of the ResNet step
+    (4.8 ms/step in profiles/r04_07/)."""
+    M, K = a.shape
+    N = w_nk.shape[0]
+    if (_nt_ok(a, M, N, K) and a.is_contiguous() and a.data_ptr() % 16 == 0
+            and (acc is None or (acc.is_contiguous() and acc.data_ptr() % 16 == 0))):
+        w = w_nk.contiguous()
+        CONV_MM_STATS["own"] += 1
+        if acc is not None:
+            return lib().gemm_nt(a, w, 0, out=acc, cin=acc)
+        return lib().gemm_nt(a, w, 0)
+    CONV_MM_STATS["blas"] += 1
+    if acc is not None:
+        return acc.addmm_(a, w_nk.t()) if acc.is_contiguous() else torch.addmm(acc, a, w_nk.t())
+    return torch.mm(a, w_nk.t())
+
+
 def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm: bool,
            link) -> torch.Tensor:
     """dX of a 1x1 conv (x only supplies the shape for MIOpen). GEMM path: dX = dY W, with a
@@ -62,11 +97,11 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm
         if g is not None:
             dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
             if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
-                d2 = dres.addmm_(dy2, w2)
+                d2 = conv_mm(dy2, w2.t(), acc=dres)
             else:
                 d2 = torch.addmm(dres, dy2, w2)
         else:
-            d2 = torch.mm(dy2, w2)
+            d2 = conv_mm(dy2, w2.t())
         return d2.view(N, H, W, C).permute(0, 3, 1, 2)
     dx, _, _ = torch.ops.aten.convolution_backward(
         dy, x, w, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])

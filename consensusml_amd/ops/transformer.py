@@ -27,6 +27,19 @@ def _gpu_bf16(*ts: Optional[torch.Tensor]) -> bool:
 
 
 # ============================================================================ cross-entropy
+# logits-bias gradients produced by the cross-entropy backward, keyed by the data pointer of the
+# logits gradient it returned: the producing linear (``_LinearFn`` with a padded output) takes the
+# fold instead of re-reading the R x V gradient for its column sums (same hand-off pattern as the
+# ResidualLink sums of ops.conv)
+_LOGIT_BIAS_PARTS = {}
+
+
+def _row_strided(x: torch.Tensor) -> bool:
+    """[R, V] with unit column stride and 16-B aligned padded rows (ld % 8 == 0, ld > V)."""
+    return (x.dim() == 2 and x.stride(1) == 1 and x.stride(0) > x.shape[1]
+            and x.stride(0) % 8 == 0)
+
+
 class _CEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, ignore_index):
@@ -40,6 +53,13 @@ class _CEFn(torch.autograd.Function):
     def backward(ctx, go):
         logits, labels, lse, count = ctx.saved_tensors
         scale = (go.float() / count).reshape(1)
+        if _row_strided(logits) and logits.shape[0] % 64 == 0:
+            # padded logits of a biased linear: gradient rows with the same stride, and the bias
+            # gradient's column partials from the same pass
+            g, part = lib().ce_bwd_cs(logits, labels, lse, scale, ctx.ignore)
+            _LOGIT_BIAS_PARTS.clear()
+            _LOGIT_BIAS_PARTS[g.data_ptr()] = (part, g.shape)
+            return g, None, None
         return lib().ce_bwd(logits, labels, lse, scale, ctx.ignore), None, None
 
 
@@ -48,17 +68,27 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor,
     """Mean cross-entropy of ``logits [..., V]`` against integer ``labels [...]``.
 
     bf16 GPU logits never get an fp32 copy: one read for the loss, one read + one bf16 write for
-    the gradient (fp32 math inside). Other inputs use ``F.cross_entropy`` in fp32."""
+    the gradient (fp32 math inside). Row-strided logits (the padded output of a linear whose V is
+    not a multiple of 8, ``linear``) are read in place, and their backward also emits the bias
+    gradient's column sums. Other inputs use ``F.cross_entropy`` in fp32."""
     V = logits.shape[-1]
     if _gpu_bf16(logits) and labels.is_cuda:
         x = logits.reshape(-1, V)
-        if not x.is_contiguous():
+        if not (x.is_contiguous() or _row_strided(x)):
             x = x.contiguous()
         if x.data_ptr() % 16:   # misaligned view (the kernel reads 16-B vectors)
             x = x.clone()
         return _CEFn.apply(x, labels.reshape(-1).long().contiguous(), int(ignore_index))
     return F.cross_entropy(logits.float().reshape(-1, V), labels.reshape(-1),
                            ignore_index=ignore_index)
+
+
+def _take_bias_parts(dy2: torch.Tensor):
+    """The cross-entropy's column partials for this logits gradient, if it left them."""
+    hit = _LOGIT_BIAS_PARTS.pop(dy2.data_ptr(), None)
+    if hit is not None and tuple(hit[1]) == tuple(dy2.shape):
+        return hit[0]
+    return None
 
 
 # ============================================================================ norms
@@ -395,61 +425,130 @@ class _LinearFn(torch.autograd.Function):
         ctx.link = link
         ctx.params = (w, b)
         x2 = x.reshape(-1, x.shape[-1])
-        if _own_gemm(x2.shape[0], w.shape[0], w.shape[1]) and x2.is_contiguous():
-            return lib().gemm_nt(x2, w, 0, bias=b).view(*x.shape[:-1], w.shape[0])
+        N = w.shape[0]
+        if _own_gemm(x2.shape[0], N, w.shape[1]) and x2.is_contiguous():
+            return lib().gemm_nt(x2, w, 0, bias=b).view(*x.shape[:-1], N)
+        if b is not None and N % 8 and x2.shape[0] % 64 == 0 and _P().padded_logits:
+            # N not a multiple of 8 (BERT's MLM head, V = 30522): the GEMM writes rows padded to
+            # Np (zero weight rows / bias), the output is the [.., N] view -- 16-B aligned rows
+            # for the cross-entropy kernels, whose backward then also emits the bias gradient
+            Np = (N + 7) // 8 * 8
+            wp = w.new_zeros(Np, w.shape[1])
+            wp[:N].copy_(w)
+            bp = b.new_zeros(Np)
+            bp[:N].copy_(b)
+            y = F.linear(x2, wp, bp)
+            return y.view(*x.shape[:-1], Np)[..., :N]
         return F.linear(x, w, b)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            g = ctx.link.take() if ctx.link is not None else None
-            K = x.shape[-1]
-            own = _own_gemm(dy2.shape[0], K, w.shape[0]) and dy2.is_contiguous()
-            if own and (g is None or (g.is_contiguous() and g.shape == x.shape)):
-                # data gradient on gemm.hip against the transposed weight, the parked residual
-                # gradient added in the epilogue (in place)
-                wt = w.t().contiguous()
-                if g is not None:
-                    g2 = g.view(-1, K)
-                    dx = lib().gemm_nt(dy2, wt, 0, out=g2, cin=g2).view(x.shape)
-                else:
-                    dx = lib().gemm_nt(dy2, wt, 0).view(x.shape)
-            elif g is not None and g.is_contiguous() and g.shape == x.shape:
-                dx = g.view(-1, x.shape[-1]).addmm_(dy2, w).view(x.shape)   # beta = 1 epilogue
-            elif g is not None:
-                dx = (g.reshape(-1, x.shape[-1]) + dy2 @ w).view(x.shape)
+        return _linear_grads(ctx, dy.reshape(-1, dy.shape[-1]), x, w) + (None,)
+
+
+def _linear_grads(ctx, dy2: torch.Tensor, x: torch.Tensor, w: torch.Tensor):
+    """(dx, dw, db) of y = x W^T + b from the output gradient rows dy2 [M, N] (ctx: needs_input_grad
+    over (x, w, b), ``link``, ``params`` = (w, b) modules' tensors). Batched virtual workers write
+    per-worker dW / db straight into their gradient rows and return dw = db = None."""
+    dx = dw = db = None
+    # bias-gradient column partials left by the cross-entropy backward (padded logits)
+    parts = _take_bias_parts(dy2) if ctx.needs_input_grad[2] and dy2.is_cuda else None
+    if ctx.needs_input_grad[0]:
+        g = ctx.link.take() if ctx.link is not None else None
+        K = x.shape[-1]
+        own = _own_gemm(dy2.shape[0], K, w.shape[0]) and dy2.is_contiguous()
+        if own and (g is None or (g.is_contiguous() and g.shape == x.shape)):
+            # data gradient on gemm.hip against the transposed weight, the parked residual
+            # gradient added in the epilogue (in place)
+            wt = w.t().contiguous()
+            if g is not None:
+                g2 = g.view(-1, K)
+                dx = lib().gemm_nt(dy2, wt, 0, out=g2, cin=g2).view(x.shape)
             else:
-                dx = (dy2 @ w).view(x.shape)
-        wg = WG.current()
-        pw, pb = ctx.params
-        if wg is not None and (wg.has(pw) or wg.has(pb)):
-            # batched virtual workers: per-worker dW / db straight into the gradient rows
-            V, N, K = wg.V, dy2.shape[-1], x.shape[-1]
-            T = dy2.shape[0] // V
-            if ctx.needs_input_grad[1] and wg.has(pw):
-                dst, first = wg.out(pw)
-                a = dy2.view(V, T, N).transpose(1, 2)
-                bm = x.reshape(V, T, K)
-                if first:
-                    torch.bmm(a, bm, out=dst.view(V, N, K))
-                else:
-                    dst.view(V, N, K).baddbmm_(a, bm)
-            if ctx.needs_input_grad[2] and wg.has(pb):
-                dst, first = wg.out(pb)
-                if first and N % 8 == 0 and T % 32 == 0 and dy2.is_cuda:
-                    lib().colsum_seg(dy2, V, dst.view(V, N))
-                else:
-                    g = dy2.view(V, T, N).sum(1)
-                    (dst.copy_ if first else dst.add_)(g)
-            return dx, None, None, None
-        if ctx.needs_input_grad[1]:
-            dw = dy2.t() @ x.reshape(-1, x.shape[-1])
-        if ctx.needs_input_grad[2]:
-            db = lib().colsum(dy2) if dy2.shape[-1] % 8 == 0 else dy2.sum(0)
-        return dx, dw, db, None
+                dx = lib().gemm_nt(dy2, wt, 0).view(x.shape)
+        elif g is not None and g.is_contiguous() and g.shape == x.shape:
+            dx = g.view(-1, x.shape[-1]).addmm_(dy2, w).view(x.shape)   # beta = 1 epilogue
+        elif g is not None:
+            dx = (g.reshape(-1, x.shape[-1]) + dy2 @ w).view(x.shape)
+        else:
+            dx = (dy2 @ w).view(x.shape)
+    wg = WG.current()
+    pw, pb = ctx.params
+    if wg is not None and (wg.has(pw) or (pb is not None and wg.has(pb))):
+        # batched virtual workers: per-worker dW / db straight into the gradient rows
+        V, N, K = wg.V, dy2.shape[-1], x.shape[-1]
+        T = dy2.shape[0] // V
+        if ctx.needs_input_grad[1] and wg.has(pw):
+            dst, first = wg.out(pw)
+            a = dy2.view(V, T, N).transpose(1, 2)
+            bm = x.reshape(V, T, K)
+            if first:
+                torch.bmm(a, bm, out=dst.view(V, N, K))
+            else:
+                dst.view(V, N, K).baddbmm_(a, bm)
+        if ctx.needs_input_grad[2] and pb is not None and wg.has(pb):
+            dst, first = wg.out(pb)
+            if parts is not None and T % 64 == 0:
+                tgt = dst.view(V, N) if first else torch.empty(V, N, dtype=dst.dtype,
+                                                               device=dst.device)
+                lib().ce_part_fold(parts, N, V, tgt)
+                if not first:
+                    dst.view(V, N).add_(tgt)
+            elif first and N % 8 == 0 and T % 32 == 0 and dy2.is_cuda and dy2.is_contiguous():
+                lib().colsum_seg(dy2, V, dst.view(V, N))
+            else:
+                g = dy2.view(V, T, N).sum(1)
+                (dst.copy_ if first else dst.add_)(g)
+        return dx, None, None
+    if ctx.needs_input_grad[1]:
+        dw = dy2.t() @ x.reshape(-1, x.shape[-1])
+    if ctx.needs_input_grad[2]:
+        if parts is not None:
+            db = torch.empty(1, dy2.shape[-1], dtype=dy2.dtype, device=dy2.device)
+            lib().ce_part_fold(parts, dy2.shape[-1], 1, db)
+            db = db.view(-1)
+        else:
+            db = lib().colsum(dy2) if (dy2.shape[-1] % 8 == 0 and dy2.is_contiguous()) \
+                else dy2.sum(0)
+    return dx, dw, db
+
+
+class _LinearGeluFn(torch.autograd.Function):
+    """a = gelu(x W^T + b) (erf GELU) on gemm.hip with bias + GELU in the epilogue (h kept for the
+    backward), backward dh = da * gelu'(h) in one elementwise pass (``gelu_bwd``), then the linear's
+    gradients as ``_LinearFn`` (BERT's MLM-head transform; the PyTorch GELU kernels it replaces:
+    profiles/r04_06/bert_kernels.md)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        h = torch.empty(x2.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+        a = lib().gemm_nt(x2, w, 1, bias=b, aux=h)
+        ctx.save_for_backward(x2, w, h)
+        ctx.link = None
+        ctx.params = (w, b)
+        ctx.xshape = x.shape
+        return a.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, da):
+        x2, w, h = ctx.saved_tensors
+        dh = lib().gelu_bwd(da.reshape(-1, da.shape[-1]).contiguous(), h)
+        dx, dw, db = _linear_grads(ctx, dh, x2, w)
+        return (dx.view(ctx.xshape) if dx is not None else None), dw, db
+
+
+def linear_gelu(x: torch.Tensor, lin: nn.Linear) -> torch.Tensor:
+    """gelu(lin(x)) (erf GELU); gemm.hip-eligible bf16 GPU shapes run the fused-epilogue path."""
+    w, b = lin.weight, lin.bias
+    M = x.numel() // x.shape[-1]
+    if (_P().fused_ffn and _gpu_bf16(x, w, b) and b is not None
+            and _gemm_ok(M, w.shape[0], w.shape[1])):
+        return _LinearGeluFn.apply(x, w, b)
+    return F.gelu(lin(x))
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
@@ -457,7 +556,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
     """``link``: a ResidualLink on which a later-in-forward op (``add_norm(x_link=...)``) parks
     another gradient of x; this GEMM's data-gradient absorbs it (beta = 1)."""
     wg = WG.current()
-    if _gpu_bf16(x, w, b) and ((b is not None and w.shape[0] % 8 == 0)
+    if _gpu_bf16(x, w, b) and ((b is not None and (w.shape[0] % 8 == 0 or _P().padded_logits))
                                or (wg is not None and wg.has(w))):
         return _LinearFn.apply(x, w, b, link)
     return F.linear(x, w, b)

@@ -82,6 +82,11 @@ class PerfPolicy:
     own_gemm: bool = True                 # gemm.hip for transformer linears with >= 128 tiles
     fused_ffn: bool = True                # BERT FFN on gemm.hip: bias + GELU in fc1's epilogue,
                                           # GELU backward + bias gradient in the dgrad epilogue
+    padded_logits: bool = True            # biased linears with N % 8 != 0 (BERT MLM head) write
+                                          # 16-B aligned padded rows; the CE backward emits the
+                                          # bias gradient (no column-sum pass over R x V)
+    own_gemm_conv1x1: bool = True         # ResNet 1x1 convs that run as plain GEMMs (layers 3-4
+                                          # forward / data gradient) on gemm.hip, not hipBLASLt
 
     @classmethod
     def from_env(cls) -> "PerfPolicy":
@@ -125,6 +130,8 @@ class PerfPolicy:
             batched_workers=_env_bool("CML_BATCHED_WORKERS", True),
             own_gemm=_env_bool("CML_OWN_GEMM", True),
             fused_ffn=_env_bool("CML_FUSED_FFN", True),
+            own_gemm_conv1x1=_env_bool("CML_OWN_GEMM_CONV1X1", True),
+            padded_logits=_env_bool("CML_PADDED_LOGITS", True),
         )
 
     @classmethod

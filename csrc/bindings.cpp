@@ -1500,9 +1500,21 @@ void check_bf16c(const Tensor& t, const char* name) {
 }
 
 // logits [R, V] bf16 contiguous, labels [R] int64 -> (lse fp32 [R], loss fp32 [R])
+// logits [R, V] with unit column stride; rows contiguous (ld = V) or row-strided (ld % 8 == 0,
+// a padded logits buffer)
+int64_t ce_row_stride(const Tensor& logits) {
+  check_dev(logits, "logits");
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16, "logits must be bf16");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [R, V] with unit column stride");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(logits.data_ptr()) & 15) == 0, "logits must be 16-B aligned");
+  const int64_t V = logits.size(1), ld = logits.stride(0);
+  TORCH_CHECK(ld == V || (ld >= V && ld % 8 == 0) || logits.size(0) == 1,
+              "logits rows must be contiguous or 16-B aligned (row stride % 8 == 0)");
+  return logits.size(0) == 1 ? V : ld;
+}
+
 std::vector<Tensor> ce_fwd(const Tensor& logits, const Tensor& labels, int64_t ignore) {
-  check_bf16c(logits, "logits");
-  TORCH_CHECK(logits.dim() == 2, "logits must be [R, V]");
+  const int64_t ld = ce_row_stride(logits);
   const int64_t R = logits.size(0), V = logits.size(1);
   TORCH_CHECK(R >= 1 && R <= 2147483647LL && V >= 1 && V <= 2147483647LL, "bad logits shape");
   TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() &&
@@ -1510,10 +1522,59 @@ std::vector<Tensor> ce_fwd(const Tensor& logits, const Tensor& labels, int64_t i
   const c10::DeviceGuard guard(logits.device());
   auto f32 = logits.options().dtype(at::kFloat);
   Tensor lse = at::empty({R}, f32), loss = at::empty({R}, f32);
-  CML_CHECK_HIP(cml::launch_ce_fwd(logits.data_ptr(), R, static_cast<int>(V),
+  CML_CHECK_HIP(cml::launch_ce_fwd(logits.data_ptr(), R, static_cast<int>(V), ld,
                                    labels.data_ptr<int64_t>(), ignore, lse.data_ptr<float>(),
                                    loss.data_ptr<float>(), cur_stream()));
   return {lse, loss};
+}
+
+// Fused backward over row-strided logits (ld % 8 == 0, R % 64 == 0): (grad [R, V] view of an
+// [R, ld] buffer, part [R / 64, ld] fp32 column sums per 64-row block) -- ce_part_fold turns part
+// into the logits bias gradient.
+std::vector<Tensor> ce_bwd_cs(const Tensor& logits, const Tensor& labels, const Tensor& lse,
+                              const Tensor& scale, int64_t ignore) {
+  const int64_t ld = ce_row_stride(logits);
+  const int64_t R = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(ld % 8 == 0 && R % 64 == 0, "ce_bwd_cs: needs a row stride % 8 == 0 and R % 64 == 0");
+  TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.numel() == R &&
+                  labels.is_contiguous(), "labels: contiguous int64 [R]");
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.numel() == R &&
+                  lse.is_contiguous(), "lse: fp32 [R]");
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() >= 1,
+              "scale: fp32 GPU scalar");
+  const c10::DeviceGuard guard(logits.device());
+  Tensor gbuf = at::empty({R, ld}, logits.options());
+  Tensor part = at::empty({R / 64, ld}, logits.options().dtype(at::kFloat));
+  CML_CHECK_HIP(cml::launch_ce_bwd_cs(logits.data_ptr(), R, static_cast<int>(V), ld,
+                                      labels.data_ptr<int64_t>(), ignore, lse.data_ptr<float>(),
+                                      scale.data_ptr<float>(), gbuf.data_ptr(),
+                                      part.data_ptr<float>(), cur_stream()));
+  return {gbuf.narrow(1, 0, V), part};
+}
+
+Tensor gelu_bwd(const Tensor& da, const Tensor& h) {
+  check_bf16c(da, "da");
+  check_bf16c(h, "h");
+  TORCH_CHECK(da.numel() == h.numel() && da.numel() % 8 == 0, "gelu_bwd: same size, % 8 == 0");
+  const c10::DeviceGuard guard(da.device());
+  Tensor dh = at::empty_like(h);
+  CML_CHECK_HIP(cml::launch_gelu_bwd(da.data_ptr(), h.data_ptr(), dh.data_ptr(), da.numel(),
+                                     cur_stream()));
+  return dh;
+}
+
+// out [nseg, V] (bf16 or fp32, unit column stride) = per-segment sums of ce_bwd_cs's partials
+void ce_part_fold(const Tensor& part, int64_t V, int64_t nseg, Tensor& out) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() == 2 &&
+                  part.is_contiguous(), "part: fp32 [R / 64, ld]");
+  TORCH_CHECK(out.is_cuda() && (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat) &&
+                  out.dim() == 2 && out.size(0) == nseg && out.size(1) == V && out.stride(1) == 1,
+              "out must be [nseg, V] bf16 / fp32");
+  const c10::DeviceGuard guard(part.device());
+  CML_CHECK_HIP(cml::launch_ce_part_fold(part.data_ptr<float>(), part.size(0) * 64,
+                                         static_cast<int>(V), part.size(1), static_cast<int>(nseg),
+                                         out.data_ptr(), out.stride(0),
+                                         out.scalar_type() == at::kFloat ? 1 : 0, cur_stream()));
 }
 
 Tensor ce_bwd(const Tensor& logits, const Tensor& labels, const Tensor& lse, const Tensor& scale,
@@ -2112,6 +2173,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pad_c4", &pad_c4, "NHWC bf16 channel zero-padding to 4");
   m.def("ce_fwd", &ce_fwd, "fused cross-entropy forward over bf16 logits (lse, per-row loss)");
   m.def("ce_bwd", &ce_bwd, "fused cross-entropy backward (bf16 logits gradient)");
+  m.def("ce_bwd_cs", &ce_bwd_cs, "cross-entropy backward over row-strided logits + bias-gradient "
+        "column partials");
+  m.def("gelu_bwd", &gelu_bwd, "dh = da * gelu'(h) (erf GELU), bf16");
+  m.def("ce_part_fold", &ce_part_fold, "per-segment fold of ce_bwd_cs's column partials");
   m.def("norm_fwd", &norm_fwd, "LayerNorm / RMSNorm (+ residual add) forward");
   m.def("norm_bwd", &norm_bwd, "LayerNorm / RMSNorm backward (+ residual gradient)");
   m.def("rope_fwd", &rope_fwd, "QKV split + RoPE into head-major q / k / v");

@@ -240,4 +240,30 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// ---------------------------------------------------------------- erf GELU
+// erf by Abramowitz-Stegun 7.1.26 (|error| < 1.5e-7, far below bf16 resolution) instead of ocml's
+// erff: 2 transcendentals (rcp, exp), and the exp(-x^2 / 2) term is shared with the derivative's
+// density. Used by the GEMM epilogues (gemm.hip) and the standalone GELU backward (transformer.hip).
+__device__ __forceinline__ float erf_as(float z, float e) {   // e = exp(-z^2)
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  const float r = fmaf(-p * t, e, 1.f);
+  return copysignf(r, z);
+}
+__device__ __forceinline__ float gelu_f(float x) {
+  const float z = x * 0.70710678118654752f;
+  const float e = __expf(-z * z);
+  return 0.5f * x * (1.f + erf_as(z, e));
+}
+// d gelu / dx = Phi(x) + x phi(x)
+__device__ __forceinline__ float dgelu_f(float x) {
+  const float z = x * 0.70710678118654752f;
+  const float e = __expf(-z * z);
+  return fmaf(0.5f, erf_as(z, e), 0.5f) + x * 0.3989422804014327f * e;
+}
+
 }  // namespace cml

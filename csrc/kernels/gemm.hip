@@ -66,31 +66,6 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_t a, bf16x8_t b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// erf-GELU and its derivative. erf by Abramowitz-Stegun 7.1.26 (|error| < 1.5e-7, far below the
-// bf16 output's resolution) instead of ocml's erff: 2 transcendentals (rcp, exp), and the
-// exp(-x^2 / 2) term is shared with the derivative's density.
-__device__ __forceinline__ float erf_as(float z, float e) {   // e = exp(-z^2)
-  const float az = fabsf(z);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.f));
-  float p = fmaf(t, 1.061405429f, -1.453152027f);
-  p = fmaf(t, p, 1.421413741f);
-  p = fmaf(t, p, -0.284496736f);
-  p = fmaf(t, p, 0.254829592f);
-  const float r = fmaf(-p * t, e, 1.f);
-  return copysignf(r, z);
-}
-__device__ __forceinline__ float gelu_f(float x) {
-  const float z = x * 0.70710678118654752f;
-  const float e = __expf(-z * z);
-  return 0.5f * x * (1.f + erf_as(z, e));
-}
-// d gelu / dx = Phi(x) + x phi(x)
-__device__ __forceinline__ float dgelu_f(float x) {
-  const float z = x * 0.70710678118654752f;
-  const float e = __expf(-z * z);
-  return fmaf(0.5f, erf_as(z, e), 0.5f) + x * 0.3989422804014327f * e;
-}
-
 template <int EP>
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];

@@ -194,11 +194,21 @@ hipError_t launch_fault(int dtype, void* g, int64_t D, int kind, float scale, fl
 // Cross-entropy over contiguous bf16 logits [R, V] (16-B aligned base): forward writes the
 // per-row logsumexp and loss (0 for ignored rows); backward writes
 // grad = (*scale) * (softmax - onehot) (0 rows for ignored labels), scale = dloss / n_valid.
-hipError_t launch_ce_fwd(const void* logits, int64_t R, int V, const int64_t* labels,
+hipError_t launch_ce_fwd(const void* logits, int64_t R, int V, int64_t ld, const int64_t* labels,
                          int64_t ignore, float* lse, float* loss, hipStream_t stream);
 hipError_t launch_ce_bwd(const void* logits, int64_t R, int V, const int64_t* labels,
                          int64_t ignore, const float* lse, const float* scale, void* grad,
                          hipStream_t stream);
+// Row-strided form (ld % 8 == 0, R % 64 == 0): grad gets the same stride (columns [V, ld) = 0),
+// and part [R / 64][ld] fp32 the column sums of each 64-row block of the stored gradient;
+// launch_ce_part_fold sums them per segment of R / nseg rows into out [nseg][ldo] (bf16 / fp32).
+hipError_t launch_ce_bwd_cs(const void* logits, int64_t R, int V, int64_t ld,
+                            const int64_t* labels, int64_t ignore, const float* lse,
+                            const float* scale, void* grad, float* part, hipStream_t stream);
+hipError_t launch_ce_part_fold(const float* part, int64_t R, int V, int64_t ld, int nseg, void* out,
+                               int64_t ldo, int out_f32, hipStream_t stream);
+// dh = bf16(da * gelu'(h)) (erf GELU), n % 8 == 0, 16-B aligned
+hipError_t launch_gelu_bwd(const void* da, const void* h, void* dh, int64_t n, hipStream_t stream);
 // LayerNorm (ln = 1, with bias b and mean) or RMSNorm (ln = 0) over rows of D (D % 8 == 0,
 // D <= 4096). res != null: normalise x + res and write the bf16 sum to `sum`.
 // Backward: dx (+ dres if given) and dw (+ db) via norm_workspace_bytes of partials.

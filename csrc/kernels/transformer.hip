@@ -55,12 +55,13 @@ __device__ __forceinline__ void online_add(float& m, float& s, float v) {
 }
 
 __global__ __launch_bounds__(kTB) void ce_fwd_kernel(const bf16* __restrict__ x, int V,
+                                                    int64_t ld,
                                                     const int64_t* __restrict__ labels,
                                                     int64_t ignore, float* __restrict__ lse,
                                                     float* __restrict__ loss) {
   const int64_t r = blockIdx.x;
   const int t = threadIdx.x;
-  const int64_t e0 = r * static_cast<int64_t>(V);
+  const int64_t e0 = r * ld;   // row stride ld >= V (a padded logits buffer: ld % 8 == 0)
   const int64_t end = e0 + V;
   int64_t ci0 = (e0 + 7) & ~int64_t(7);
   int64_t ci1 = end & ~int64_t(7);
@@ -165,6 +166,102 @@ __global__ __launch_bounds__(kTB) void ce_bwd_kernel(const bf16* __restrict__ x,
       }
     }
   }
+}
+
+// Backward over row-strided logits (ld % 8 == 0, so every row is 16-B aligned) into a gradient
+// buffer of the same stride, plus the column sums of the gradient (the logits bias gradient, no
+// second read of the R x V gradient): workgroup b owns rows [64 b, 64 b + 64) and sweeps the row
+// block column chunk by column chunk (lane: 8 columns), 8 rows of loads in flight, so its 8 column
+// sums per chunk accumulate in registers; part[b][c] = sum over its 64 rows (fixed order). Columns
+// in [V, ld) of the gradient are written as 0 and contribute 0.
+constexpr int kCeRows = 64;
+__global__ __launch_bounds__(kTB) void ce_bwd_cs_kernel(const bf16* __restrict__ x, int V, int64_t ld,
+                                                       const int64_t* __restrict__ labels,
+                                                       int64_t ignore, const float* __restrict__ lse,
+                                                       const float* __restrict__ scale_ptr,
+                                                       bf16* __restrict__ g, float* __restrict__ part) {
+  __shared__ float sL[kCeRows], sS[kCeRows];
+  __shared__ int sLab[kCeRows];
+  const int t = threadIdx.x;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kCeRows;
+  if (t < kCeRows) {
+    const int64_t lab = labels[r0 + t];
+    const bool valid = lab != ignore && lab >= 0 && lab < V;
+    sL[t] = lse[r0 + t];
+    sS[t] = valid ? *scale_ptr : 0.f;
+    sLab[t] = valid ? static_cast<int>(lab) : -1;
+  }
+  __syncthreads();
+  const uint16_t* xr = reinterpret_cast<const uint16_t*>(x) + r0 * ld;
+  uint16_t* gr = reinterpret_cast<uint16_t*>(g) + r0 * ld;
+  for (int c = 8 * t; c < V; c += 8 * kTB) {
+    float cs[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cs[k] = 0.f;
+    const int nv = V - c < 8 ? V - c : 8;   // valid columns of this chunk
+    for (int rb = 0; rb < kCeRows; rb += 8) {
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const uint4*>(xr + (rb + u) * ld + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rr = rb + u;
+        const float L = sL[rr], sc = sS[rr];
+        const int lc = sLab[rr] - c;   // label column within the chunk (0..7) or outside
+        const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        uint32_t o4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float lo = sc * __expf(__uint_as_float(w4[q] << 16) - L) - (lc == 2 * q ? sc : 0.f);
+          float hi = sc * __expf(__uint_as_float(w4[q] & 0xffff0000u) - L) - (lc == 2 * q + 1 ? sc : 0.f);
+          if (2 * q >= nv) lo = 0.f;
+          if (2 * q + 1 >= nv) hi = 0.f;
+          o4[q] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+          cs[2 * q] += __uint_as_float(o4[q] << 16);   // the stored (bf16) values are summed
+          cs[2 * q + 1] += __uint_as_float(o4[q] & 0xffff0000u);
+        }
+        *reinterpret_cast<uint4*>(gr + (rb + u) * ld + c) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+      }
+    }
+    float* pp = part + static_cast<int64_t>(blockIdx.x) * ld + c;
+    reinterpret_cast<float4*>(pp)[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+    reinterpret_cast<float4*>(pp)[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
+  }
+}
+
+// dh = bf16(da * gelu'(h)) over n elements (n % 8 == 0): the backward of a GELU applied in a GEMM
+// epilogue (gemm.hip EP_GELU) whose consumer is not a GEMM (BERT's MLM-head transform -> LayerNorm)
+__global__ __launch_bounds__(kTB) void gelu_bwd_kernel(const bf16* __restrict__ da,
+                                                      const bf16* __restrict__ h,
+                                                      bf16* __restrict__ dh, int64_t n8) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kTB + threadIdx.x; i < n8;
+       i += static_cast<int64_t>(gridDim.x) * kTB) {
+    const uint4 av = reinterpret_cast<const uint4*>(da)[i];
+    const uint4 hv = reinterpret_cast<const uint4*>(h)[i];
+    const uint32_t a4[4] = {av.x, av.y, av.z, av.w}, h4[4] = {hv.x, hv.y, hv.z, hv.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float lo = __uint_as_float(a4[q] << 16) * dgelu_f(__uint_as_float(h4[q] << 16));
+      const float hi = __uint_as_float(a4[q] & 0xffff0000u) * dgelu_f(__uint_as_float(h4[q] & 0xffff0000u));
+      o[q] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+    }
+    reinterpret_cast<uint4*>(dh)[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// out[s][c] = sum over the nb partial rows of segment s (in order) of part[.][c], c < V
+__global__ __launch_bounds__(kTB) void ce_part_fold_kernel(const float* __restrict__ part, int nb,
+                                                          int V, int64_t ld, void* __restrict__ out,
+                                                          int64_t ldo, int out_f32) {
+  const int c = blockIdx.x * kTB + threadIdx.x;
+  const int s = blockIdx.y;
+  if (c >= V) return;
+  const float* p = part + static_cast<int64_t>(s) * nb * ld + c;
+  float v = 0.f;
+  for (int b = 0; b < nb; ++b) v += p[static_cast<int64_t>(b) * ld];
+  if (out_f32) reinterpret_cast<float*>(out)[static_cast<int64_t>(s) * ldo + c] = v;
+  else reinterpret_cast<uint16_t*>(out)[static_cast<int64_t>(s) * ldo + c] = f2bf(v);
 }
 
 // ============================================================================ RMSNorm / LayerNorm
@@ -676,11 +773,11 @@ int stream_grid(int64_t work_items) {
 }  // namespace
 
 // ---------------------------------------------------------------------------- host launchers
-hipError_t launch_ce_fwd(const void* logits, int64_t R, int V, const int64_t* labels,
+hipError_t launch_ce_fwd(const void* logits, int64_t R, int V, int64_t ld, const int64_t* labels,
                          int64_t ignore, float* lse, float* loss, hipStream_t st) {
-  if (R < 1 || V < 1 || (reinterpret_cast<uintptr_t>(logits) & 15)) return hipErrorInvalidValue;
+  if (R < 1 || V < 1 || ld < V || (reinterpret_cast<uintptr_t>(logits) & 15)) return hipErrorInvalidValue;
   ce_fwd_kernel<<<static_cast<unsigned>(R), kTB, 0, st>>>(reinterpret_cast<const bf16*>(logits), V,
-                                                          labels, ignore, lse, loss);
+                                                          ld, labels, ignore, lse, loss);
   return hipGetLastError();
 }
 
@@ -693,6 +790,38 @@ hipError_t launch_ce_bwd(const void* logits, int64_t R, int V, const int64_t* la
   ce_bwd_kernel<<<static_cast<unsigned>(R), kTB, 0, st>>>(reinterpret_cast<const bf16*>(logits), V,
                                                           labels, ignore, lse, scale,
                                                           reinterpret_cast<bf16*>(grad));
+  return hipGetLastError();
+}
+
+hipError_t launch_ce_bwd_cs(const void* logits, int64_t R, int V, int64_t ld,
+                            const int64_t* labels, int64_t ignore, const float* lse,
+                            const float* scale, void* grad, float* part, hipStream_t st) {
+  if (R < kCeRows || R % kCeRows || V < 1 || ld < V || ld % 8 ||
+      ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(grad) |
+        reinterpret_cast<uintptr_t>(part)) & 15))
+    return hipErrorInvalidValue;
+  ce_bwd_cs_kernel<<<static_cast<unsigned>(R / kCeRows), kTB, 0, st>>>(
+      reinterpret_cast<const bf16*>(logits), V, ld, labels, ignore, lse, scale,
+      reinterpret_cast<bf16*>(grad), part);
+  return hipGetLastError();
+}
+
+hipError_t launch_gelu_bwd(const void* da, const void* h, void* dh, int64_t n, hipStream_t st) {
+  if (n < 1 || n % 8 || ((reinterpret_cast<uintptr_t>(da) | reinterpret_cast<uintptr_t>(h) |
+                          reinterpret_cast<uintptr_t>(dh)) & 15))
+    return hipErrorInvalidValue;
+  gelu_bwd_kernel<<<stream_grid(n / 8), kTB, 0, st>>>(reinterpret_cast<const bf16*>(da),
+                                                      reinterpret_cast<const bf16*>(h),
+                                                      reinterpret_cast<bf16*>(dh), n / 8);
+  return hipGetLastError();
+}
+
+hipError_t launch_ce_part_fold(const float* part, int64_t R, int V, int64_t ld, int nseg, void* out,
+                               int64_t ldo, int out_f32, hipStream_t st) {
+  if (nseg < 1 || R % (static_cast<int64_t>(kCeRows) * nseg) || V < 1 || ld < V) return hipErrorInvalidValue;
+  const dim3 grid((V + kTB - 1) / kTB, nseg);
+  ce_part_fold_kernel<<<grid, kTB, 0, st>>>(part, static_cast<int>(R / kCeRows / nseg), V, ld, out,
+                                            ldo, out_f32);
   return hipGetLastError();
 }
 
