@@ -16,6 +16,9 @@ eval-mode running statistics on fresh batches), and every BN running statistic. 
 relative difference of the running statistics per BN layer.
 
   python bench/convergence.py [--steps 100] [--batch 128] [--image-size 224] [--out DIR]
+  python bench/convergence.py --steps 30 --batch 2048 --no-krum --noise 2 --noise-floor 0.004
+      (the batch-2048 check: the bench's own kernel choices -- M-aware tiles, quad family,
+       256 x 256 tiles -- which differ from the small-batch test's)
 """
 from __future__ import annotations
 
@@ -149,6 +152,10 @@ def main():
                          "stays informative for longer)")
     ap.add_argument("--eval-batches", type=int, default=8)
     ap.add_argument("--no-krum", action="store_true")
+    ap.add_argument("--noise-floor", type=float, default=0.0,
+                    help="> 0: also a library run from weights perturbed by this relative amount; "
+                         "library vs perturbed-library is the numerics noise floor that the "
+                         "fused-vs-library difference is judged against")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from consensusml_amd import perf
@@ -161,17 +168,25 @@ def main():
     runs["library"] = run("library", perf.PerfPolicy.library(),
                           make_cfg(a.batch, a.image_size, a.classes, a.lr, noise=a.noise), a.steps,
                           a.eval_batches, a.batch)
+    if a.noise_floor > 0:
+        runs["library_perturbed"] = run("library_perturbed", perf.PerfPolicy.library(),
+                                        make_cfg(a.batch, a.image_size, a.classes, a.lr,
+                                                 noise=a.noise), a.steps, a.eval_batches,
+                                        a.batch, perturb=a.noise_floor)
     if not a.no_krum:
         runs["krum8"] = run("krum8", fused_pol,
                             make_cfg(a.batch, a.image_size, a.classes, a.lr, V=8, rule="krum",
                                      f=2, noise=a.noise), a.steps, a.eval_batches, a.batch)
     cmp = compare(runs["fused"], runs["library"])
-    summary = {"config": vars(a), "fused_vs_library": cmp,
+    floor = compare(runs["library_perturbed"], runs["library"]) if a.noise_floor > 0 else None
+    summary = {"config": vars(a), "fused_vs_library": cmp, "noise_floor": floor,
                "runs": {k: {kk: vv for kk, vv in r.items() if kk != "stats"}
                         for k, r in runs.items()}}
     line = json.dumps(summary)
     print(json.dumps({"fused_vs_library": {k: v for k, v in cmp.items()
                                             if not isinstance(v, list)},
+                      "noise_floor": ({k: v for k, v in floor.items() if not isinstance(v, list)}
+                                      if floor else None),
                       "final_loss": {k: r["losses"][-1] for k, r in runs.items()},
                       "acc_eval_mode": {k: r["acc_eval_mode"] for k, r in runs.items()},
                       "acc_train_mode": {k: r["acc_train_mode"] for k, r in runs.items()},

@@ -48,7 +48,7 @@ class PerfPolicy:
     # ---------------------------------------------------------------- 1x1 convolutions
     conv1x1_gemm: str = "auto"            # auto | gemm | miopen (library fwd / dgrad choice)
     fused_conv1x1: bool = True            # conv1x1 + BN statistics / bn2 prologue kernels
-    conv1x1g: str = "auto"                # fused-kernel family: auto | quad | glds | regstage
+    conv1x1g: str = "auto"                # fused-kernel family: auto | quad | regstage
     own_wgrad1x1: bool = True             # wgrad1x1.hip for the OWN_WGRAD_SHAPES set
     wgrad1x1_set: str = "core"            # core (5 shapes) | all (9)
     fused_bn3_bwd: bool = True            # identity-tail backward inside conv3's kernels
@@ -101,8 +101,7 @@ class PerfPolicy:
             nhwc_avgpool=_env_bool("CML_NHWC_AVGPOOL", True),
             conv1x1_gemm=_env_str("CML_CONV1X1_GEMM", "auto"),
             fused_conv1x1=_env_bool("CML_FUSED_CONV1X1", True),
-            conv1x1g={"0": "regstage", "1": "glds", "3": "quad"}.get(os.environ.get("CML_C1G", ""),
-                                                                   "auto"),
+            conv1x1g={"0": "regstage", "3": "quad"}.get(os.environ.get("CML_C1G", ""), "auto"),
             own_wgrad1x1=_env_bool("CML_WGRAD1X1", True),
             wgrad1x1_set=_env_str("CML_WGRAD1X1_SET", "core"),
             fused_bn3_bwd=_env_bool("CML_FUSED_BN3_BWD", True),
@@ -153,8 +152,8 @@ class PerfPolicy:
     def validate(self) -> "PerfPolicy":
         if self.conv1x1_gemm not in ("auto", "gemm", "miopen"):
             raise ValueError(f"conv1x1_gemm must be auto | gemm | miopen, not {self.conv1x1_gemm!r}")
-        if self.conv1x1g not in ("auto", "quad", "glds", "regstage"):
-            raise ValueError(f"conv1x1g must be auto | quad | glds | regstage, not "
+        if self.conv1x1g not in ("auto", "quad", "regstage"):
+            raise ValueError(f"conv1x1g must be auto | quad | regstage, not "
                              f"{self.conv1x1g!r}")
         if self.wgrad1x1_set not in ("core", "all"):
             raise ValueError(f"wgrad1x1_set must be core | all, not {self.wgrad1x1_set!r}")
@@ -173,7 +172,7 @@ def policy() -> PerfPolicy:
 def _sync_native(p: PerfPolicy) -> None:
     """Push the native-side switches (kernel-family choice inside the C++ launchers)."""
     global _NATIVE_SYNCED
-    mode = {"regstage": 0, "glds": 1, "auto": 2, "quad": 3}[p.conv1x1g]
+    mode = {"regstage": 0, "auto": 2, "quad": 3}[p.conv1x1g]
     if _NATIVE_SYNCED == mode:
         return
     try:

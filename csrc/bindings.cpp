@@ -1919,14 +1919,14 @@ int64_t lasso_slices(int64_t p) { return cml::lasso_slices(static_cast<int>(p));
 // column stride, any row stride).
 Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tensor>& bias,
                const optional<Tensor>& aux, const optional<Tensor>& out,
-               const optional<Tensor>& colsum_out, const optional<Tensor>& cin) {
+               const optional<Tensor>& colsum_out, const optional<Tensor>& cin, bool b_kn) {
   check_dev(a, "a");
   check_dev(b, "b");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm_nt: bf16");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1,
               "gemm_nt: 2-D operands with unit column stride");
-  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-  TORCH_CHECK(b.size(1) == K, "gemm_nt: K mismatch");
+  const int64_t M = a.size(0), K = a.size(1), N = b_kn ? b.size(1) : b.size(0);
+  TORCH_CHECK((b_kn ? b.size(0) : b.size(1)) == K, "gemm_nt: K mismatch");
   TORCH_CHECK(cml::gemm_nt_eligible(M, N, K), "gemm_nt: needs M % 256 == 0, N % 256 == 0, K % 64 == 0");
   const c10::DeviceGuard guard(a.device());
   Tensor y;
@@ -1967,7 +1967,7 @@ Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tens
     part = at::empty({M / 128, N}, a.options().dtype(at::kFloat));
     g.part = part.data_ptr<float>();
   }
-  CML_CHECK_HIP(cml::launch_gemm_nt(g, static_cast<int>(ep), cur_stream()));
+  CML_CHECK_HIP(cml::launch_gemm_nt(g, static_cast<int>(ep), cur_stream(), b_kn));
   if (cs) {
     const bool f32 = colsum_out->scalar_type() == at::kFloat;
     TORCH_CHECK(f32 || colsum_out->scalar_type() == at::kBFloat16, "colsum_out: bf16 or fp32");
@@ -2195,7 +2195,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, "NT GEMM with fused epilogues (bias / bias+GELU / GELU backward + "
         "column sums)", py::arg("a"), py::arg("b"), py::arg("ep"), py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("out") = py::none(),
-        py::arg("colsum_out") = py::none(), py::arg("cin") = py::none());
+        py::arg("colsum_out") = py::none(), py::arg("cin") = py::none(),
+        py::arg("b_kn") = false);
   m.def("gemm_nt_ok", &gemm_nt_ok, "shape eligibility of gemm_nt");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);

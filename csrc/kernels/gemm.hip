@@ -2,7 +2,8 @@
 // backward + bias-gradient column sums), gfx950 / CDNA4:
 //
 //   y[m][n] = epi( sum_k A[m][k] B[n][k] )           A [M][K], B [N][K]: both K-contiguous ("NT",
-//                                                     nn.Linear's x W^T)
+//                                                     nn.Linear's x W^T), or B given as [K][N]
+//                                                     (b_kn: a data gradient dy W, no W^T copy)
 //   EP_STORE   y = bf16(acc + bias[n]) [+ cin[m][n]]  (bias, cin optional; cin may alias y: the
 //                                                     residual-gradient add of a data gradient)
 //   EP_GELU    h = bf16(acc + bias[n]) -> aux,  y = bf16(gelu(h))   (erf GELU, from the bf16 h)
@@ -66,7 +67,21 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_t a, bf16x8_t b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int EP>
+// BKN: B given as [K][N] (row-major, contraction-major: a weight W [out][in] used as the B of a data
+// gradient dx = dy W), staged without a transposed copy. Its K-tile is two sub-images, one per
+// 32-column half of every 64-column wave group (units U2 / U3), each [64 k][128 n] with 256-B rows;
+// 32-B slot t of row r holds columns 16 (t ^ kn_s(r)) .. +15 (the XOR lives in the per-lane DMA
+// source address), and the fragments are read with ds_read_b64_tr_b16: lane group fc takes k rows
+// 8 (fc + 4 ks) + 0..3 and + 4..7 of 16 columns, so a 32-lane half reads 8 rows whose kn_s values
+// are distinct: conflict-free.
+__device__ __forceinline__ int kn_s(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+__device__ __forceinline__ uint2 tr_rd(const char* p) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p)));
+}
+
+template <int EP, bool BKN>
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -93,9 +108,19 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
       int row0;
       if (u == 0 || u == 3) row0 = (i >> 3) * 128 + (u == 3 ? 64 : 0) + (i & 7) * 8;   // A
       else row0 = (i >> 2) * 64 + (u == 2 ? 32 : 0) + (i & 3) * 8;                  // B
+      const bool isA = (u == 0 || u == 3);
+      if (BKN && !isA) {
+        // sub-image u - 1, rows 4 i .. 4 i + 3 (1 KB); lane: row 4 i + lane / 16, 16-B piece lane & 15
+        const int r = 4 * i + (lane >> 4);
+        const int np = 16 * (((lane & 15) >> 1) ^ kn_s(r)) + 8 * (lane & 1);   // column in sub-image
+        const int n = n0 + (np >> 5) * 64 + (u - 1) * 32 + (np & 31);
+        const uint16_t* src = a.b + (kofs + r) * a.ldb + n;
+        char* dst = smem + buf * kBuf + kImg + (u - 1) * (kImg / 2) + i * 1024;
+        __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
+        continue;
+      }
       const int row = row0 + lrow;
       const int c = lp ^ ((row >> 1) & 7);
-      const bool isA = (u == 0 || u == 3);
       const uint16_t* src = isA ? a.a + static_cast<int64_t>(m0 + row) * a.lda + kofs + 8 * c
                                 : a.b + static_cast<int64_t>(n0 + row) * a.ldb + kofs + 8 * c;
       char* dst = smem + buf * kBuf + (isA ? 0 : kImg) + row0 * 128;
@@ -116,6 +141,20 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
             img + swz(wm * 128 + mh * 64 + mt * 16 + fr, fc + 4 * ks));
   };
   auto readB = [&](bf16x8_t (&f)[2][2], int nh, int buf) {
+    if constexpr (BKN) {
+      const char* img = smem + buf * kBuf + kImg + nh * (kImg / 2);
+      const int q = (lane >> 2) & 3, p8 = 8 * (lane & 3);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int t = 2 * wn + nt, r1 = 8 * (fc + 4 * ks) + q, r2 = r1 + 4;
+          const uint2 lo = tr_rd(img + r1 * 256 + 32 * (t ^ kn_s(r1)) + p8);
+          const uint2 hi = tr_rd(img + r2 * 256 + 32 * (t ^ kn_s(r2)) + p8);
+          f[nt][ks] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        }
+      return;
+    }
     const char* img = smem + buf * kBuf + kImg;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
@@ -326,7 +365,7 @@ bool gemm_nt_eligible(int64_t M, int64_t N, int64_t K) {
          (M / kT) * (N / kT) < (1LL << 31);
 }
 
-hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st) {
+hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st, bool b_kn) {
   if (!gemm_nt_eligible(a.M, a.N, a.K)) return hipErrorInvalidValue;
   if ((a.lda % 8) || (a.ldb % 8) || (a.ldy % 8)) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(a.a) | reinterpret_cast<uintptr_t>(a.b) |
@@ -335,25 +374,20 @@ hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st) {
   if ((ep == EP_GELU || ep == EP_DGELU) && (a.aux == nullptr || reinterpret_cast<uintptr_t>(a.aux) % 16))
     return hipErrorInvalidValue;
   const int tiles = (a.M / kT) * (a.N / kT);
+#define CML_GEMM(E, T)                                                                       \
+  do {                                                                                       \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<E, T>),                 \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kLds);                   \
+    gemm_nt_kernel<E, T><<<tiles, kThreads, kLds, st>>>(a);                                  \
+  } while (0)
   switch (ep) {
-    case EP_STORE:
-      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<EP_STORE>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-      gemm_nt_kernel<EP_STORE><<<tiles, kThreads, kLds, st>>>(a);
-      break;
-    case EP_GELU:
-      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<EP_GELU>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-      gemm_nt_kernel<EP_GELU><<<tiles, kThreads, kLds, st>>>(a);
-      break;
-    case EP_DGELU:
-      hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<EP_DGELU>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-      gemm_nt_kernel<EP_DGELU><<<tiles, kThreads, kLds, st>>>(a);
-      break;
+    case EP_STORE: if (b_kn) CML_GEMM(EP_STORE, true); else CML_GEMM(EP_STORE, false); break;
+    case EP_GELU: if (b_kn) CML_GEMM(EP_GELU, true); else CML_GEMM(EP_GELU, false); break;
+    case EP_DGELU: if (b_kn) CML_GEMM(EP_DGELU, true); else CML_GEMM(EP_DGELU, false); break;
     default:
       return hipErrorInvalidValue;
   }
+#undef CML_GEMM
   return hipGetLastError();
 }
 

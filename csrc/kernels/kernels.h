@@ -501,7 +501,8 @@ struct GemmArgs {
   int64_t lda, ldb, ldy;
 };
 bool gemm_nt_eligible(int64_t M, int64_t N, int64_t K);
-hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st);
+// b_kn: b is [K][N] (row stride ldb), read through transposed LDS reads
+hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st, bool b_kn = false);
 // out[s][n] = sum of the 128-row partial column sums of segment s of M rows (nseg equal
 // segments, fixed order); out bf16 [nseg][ldo] or fp32 when out_f32
 hipError_t launch_colsum_fold(const float* part, int64_t M, int N, int nseg, void* out, int64_t ldo,

@@ -36,17 +36,11 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
 
 
-_MODE = [1]
-
-
-@pytest.fixture(autouse=True, params=[1, 3], ids=["glds2", "quad"])
-def _glds_mode(request):
-    _MODE[0] = request.param
-    yield
+_MODE = [3]
 
 
 def _both(fn):
-    """fn() under the old kernels (mode 0) and the glds kernels (mode 1 or 3)."""
+    """fn() under conv1x1.hip (mode 0) and the quad-phase DMA kernel (mode 3, where eligible)."""
     L = _lib()
     prev = L.conv1x1g_mode()
     try:

@@ -14,7 +14,7 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("V", [510, 1000, 30522])
+@pytest.mark.parametrize("V", [510, 1003, 30522])
 def test_padded_logits_ce_and_bias_grad(cuda, V):
     from consensusml_amd.ops import transformer as T
     torch.manual_seed(V)
@@ -48,11 +48,14 @@ def test_ce_bwd_cs_matches_plain_backward(cuda):
     labels = torch.randint(0, V, (R,), device=cuda)
     lse, rows = lib().ce_fwd(logits, labels, -100)
     lse2, rows2 = lib().ce_fwd(logits.contiguous(), labels, -100)
-    assert torch.equal(lse, lse2) and torch.equal(rows, rows2)
+    # (the contiguous rows are misaligned: another split between scalar edges and vector interior,
+    # so another summation order)
+    torch.testing.assert_close(lse, lse2, rtol=1e-6, atol=1e-5)
+    torch.testing.assert_close(rows, rows2, rtol=1e-6, atol=1e-5)
     scale = torch.tensor([0.5], device=cuda)
     g, part = lib().ce_bwd_cs(logits, labels, lse, scale, -100)
     g_ref = lib().ce_bwd(logits.contiguous(), labels, lse, scale, -100)
-    assert torch.equal(g, g_ref)
+    assert torch.equal(g, g_ref)   # same lse: the elementwise formula is order-free
     for nseg in (1, 4):
         out = torch.empty(nseg, V, device=cuda, dtype=torch.float32)
         lib().ce_part_fold(part, V, nseg, out)
