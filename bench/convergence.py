@@ -100,7 +100,7 @@ def run(name: str, pol, cfg, steps: int, eval_batches: int, eval_bs: int,
         t0 = time.perf_counter()
         for s in range(steps):
             losses.append(float(tr.train_step()))
-            if (s + 1) % 10 == 0:
+            if (s + 1) % 10 == 0 or s < 3:   # early steps too: the first one compiles / finds
                 print(f"{name} step {s + 1} loss {losses[-1]:.4f}", flush=True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0

@@ -56,21 +56,20 @@ CONV_MM_STATS = {"own": 0, "blas": 0}   # which path conv_mm took (tests)
 
 def conv_mm(a: torch.Tensor, w_nk: torch.Tensor, acc: Optional[torch.Tensor] = None) -> torch.Tensor:
     """a [M, K] @ w_nk^T (+ acc, in place) for a 1x1 conv as a plain GEMM: the forward (w_nk = W
-    [Co, C]) or the data gradient (w_nk = W^T [C, Co], typically the transposed view of a
-    contiguous W, which gemm.hip reads as [K][N] without a copy; acc = a parked residual
-    gradient). On ``gemm.hip`` (acc added in its epilogue: bf16(bf16(a w^T) + acc)) when eligible,
-    else hipBLASLt (mm / addmm_ beta = 1). Replaces the layer-3/4 hipBLASLt GEMMs of the ResNet
-    step (4.8 ms/step in profiles/r04_07/)."""
+    [Co, C]) or the data gradient (w_nk = W^T [C, Co]; acc = a parked residual gradient). On
+    ``gemm.hip`` (NT, acc added in its epilogue: bf16(bf16(a w^T) + acc)) when eligible, else
+    hipBLASLt (mm / addmm_ beta = 1). Replaces the layer-3/4 hipBLASLt GEMMs of the ResNet step
+    (4.8 ms/step in profiles/r04_07/)."""
     M, K = a.shape
     N = w_nk.shape[0]
     if (_nt_ok(a, M, N, K) and a.is_contiguous() and a.data_ptr() % 16 == 0
             and (acc is None or (acc.is_contiguous() and acc.data_ptr() % 16 == 0))):
-        kn = w_nk.stride(0) == 1 and w_nk.stride(1) == N   # a transposed contiguous [K][N]
-        w = w_nk.t() if kn else w_nk.contiguous()
+        w = (lib().transpose_bf16(w_nk.t()) if (w_nk.stride(0) == 1 and w_nk.dim() == 2)
+             else w_nk.contiguous())
         CONV_MM_STATS["own"] += 1
         if acc is not None:
-            return lib().gemm_nt(a, w, 0, out=acc, cin=acc, b_kn=kn)
-        return lib().gemm_nt(a, w, 0, b_kn=kn)
+            return lib().gemm_nt(a, w, 0, out=acc, cin=acc)
+        return lib().gemm_nt(a, w, 0)
     CONV_MM_STATS["blas"] += 1
     if acc is not None:
         return acc.addmm_(a, w_nk.t()) if acc.is_contiguous() else torch.addmm(acc, a, w_nk.t())

@@ -459,13 +459,14 @@ def _linear_grads(ctx, dy2: torch.Tensor, x: torch.Tensor, w: torch.Tensor):
         K = x.shape[-1]
         own = _own_gemm(dy2.shape[0], K, w.shape[0]) and dy2.is_contiguous()
         if own and (g is None or (g.is_contiguous() and g.shape == x.shape)):
-            # data gradient on gemm.hip with W read as [K][N] (no transposed copy), the parked
-            # residual gradient added in the epilogue (in place)
+            # data gradient on gemm.hip against the transposed weight, the parked residual
+            # gradient added in the epilogue (in place)
+            wt = lib().transpose_bf16(w)
             if g is not None:
                 g2 = g.view(-1, K)
-                dx = lib().gemm_nt(dy2, w, 0, out=g2, cin=g2, b_kn=True).view(x.shape)
+                dx = lib().gemm_nt(dy2, wt, 0, out=g2, cin=g2).view(x.shape)
             else:
-                dx = lib().gemm_nt(dy2, w, 0, b_kn=True).view(x.shape)
+                dx = lib().gemm_nt(dy2, wt, 0).view(x.shape)
         elif g is not None and g.is_contiguous() and g.shape == x.shape:
             dx = g.view(-1, x.shape[-1]).addmm_(dy2, w).view(x.shape)   # beta = 1 epilogue
         elif g is not None:
@@ -595,7 +596,7 @@ class _FFNGeluFn(torch.autograd.Function):
 
     forward   fc1 on gemm.hip, epilogue h = x W1^T + b1 (kept for the backward) and a = gelu(h);
               fc2 = a W2^T + b2 (hipBLASLt)
-    backward  dh = (dy W2) * gelu'(h) as ONE gemm.hip launch (W2 read as [K][N]), with
+    backward  dh = (dy W2) * gelu'(h) as ONE gemm.hip launch (dy against the transposed W2), with
               the fc1 bias gradient as column sums in the same epilogue (per worker segment for
               batched virtual workers); weight gradients and dx on hipBLASLt
     The unfused composition rounds h, a, da and dh to bf16 at the same points."""
@@ -626,7 +627,7 @@ class _FFNGeluFn(torch.autograd.Function):
         wg = WG.current()
         V = wg.V if wg is not None and (wg.has(pb1) or wg.has(pw1)) else 1
         cs, post = _bias_grad_rows(pb1, V)
-        dh = lib().gemm_nt(dy2, w2, 2, aux=h, colsum_out=cs, b_kn=True)
+        dh = lib().gemm_nt(dy2, lib().transpose_bf16(w2), 2, aux=h, colsum_out=cs)
         if post is not None:
             post()
         dx = None
@@ -635,11 +636,12 @@ class _FFNGeluFn(torch.autograd.Function):
             K = x2.shape[-1]
             if _own_gemm(dh.shape[0], K, dh.shape[1]) and (
                     g is None or (g.is_contiguous() and g.shape == ctx.xshape)):
+                w1t = lib().transpose_bf16(w1)
                 if g is not None:
                     g2 = g.view(-1, K)
-                    dx = lib().gemm_nt(dh, w1, 0, out=g2, cin=g2, b_kn=True).view(ctx.xshape)
+                    dx = lib().gemm_nt(dh, w1t, 0, out=g2, cin=g2).view(ctx.xshape)
                 else:
-                    dx = lib().gemm_nt(dh, w1, 0, b_kn=True).view(ctx.xshape)
+                    dx = lib().gemm_nt(dh, w1t, 0).view(ctx.xshape)
             elif g is not None and g.is_contiguous() and g.shape == ctx.xshape:
                 dx = g.view(-1, x2.shape[-1]).addmm_(dh, w1).view(ctx.xshape)
             elif g is not None:

@@ -1552,6 +1552,22 @@ std::vector<Tensor> ce_bwd_cs(const Tensor& logits, const Tensor& labels, const 
   return {gbuf.narrow(1, 0, V), part};
 }
 
+// w.t().contiguous() for bf16 [R, C] with R, C multiples of 64 (LDS-tiled kernel); other inputs
+// fall back to ATen
+Tensor transpose_bf16(const Tensor& w) {
+  check_dev(w, "w");
+  TORCH_CHECK(w.dim() == 2, "transpose_bf16: 2-D");
+  const int64_t R = w.size(0), C = w.size(1);
+  if (w.scalar_type() != at::kBFloat16 || w.stride(1) != 1 || R % 64 || C % 64 || w.stride(0) % 8 ||
+      (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15))
+    return w.t().contiguous();
+  const c10::DeviceGuard guard(w.device());
+  Tensor out = at::empty({C, R}, w.options());
+  CML_CHECK_HIP(cml::launch_transpose_bf16(w.data_ptr(), out.data_ptr(), static_cast<int>(R),
+                                           static_cast<int>(C), w.stride(0), R, cur_stream()));
+  return out;
+}
+
 Tensor gelu_bwd(const Tensor& da, const Tensor& h) {
   check_bf16c(da, "da");
   check_bf16c(h, "h");
@@ -1919,14 +1935,14 @@ int64_t lasso_slices(int64_t p) { return cml::lasso_slices(static_cast<int>(p));
 // column stride, any row stride).
 Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tensor>& bias,
                const optional<Tensor>& aux, const optional<Tensor>& out,
-               const optional<Tensor>& colsum_out, const optional<Tensor>& cin, bool b_kn) {
+               const optional<Tensor>& colsum_out, const optional<Tensor>& cin) {
   check_dev(a, "a");
   check_dev(b, "b");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm_nt: bf16");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1,
               "gemm_nt: 2-D operands with unit column stride");
-  const int64_t M = a.size(0), K = a.size(1), N = b_kn ? b.size(1) : b.size(0);
-  TORCH_CHECK((b_kn ? b.size(0) : b.size(1)) == K, "gemm_nt: K mismatch");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "gemm_nt: K mismatch");
   TORCH_CHECK(cml::gemm_nt_eligible(M, N, K), "gemm_nt: needs M % 256 == 0, N % 256 == 0, K % 64 == 0");
   const c10::DeviceGuard guard(a.device());
   Tensor y;
@@ -1967,7 +1983,7 @@ Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tens
     part = at::empty({M / 128, N}, a.options().dtype(at::kFloat));
     g.part = part.data_ptr<float>();
   }
-  CML_CHECK_HIP(cml::launch_gemm_nt(g, static_cast<int>(ep), cur_stream(), b_kn));
+  CML_CHECK_HIP(cml::launch_gemm_nt(g, static_cast<int>(ep), cur_stream()));
   if (cs) {
     const bool f32 = colsum_out->scalar_type() == at::kFloat;
     TORCH_CHECK(f32 || colsum_out->scalar_type() == at::kBFloat16, "colsum_out: bf16 or fp32");
@@ -2175,6 +2191,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_bwd", &ce_bwd, "fused cross-entropy backward (bf16 logits gradient)");
   m.def("ce_bwd_cs", &ce_bwd_cs, "cross-entropy backward over row-strided logits + bias-gradient "
         "column partials");
+  m.def("transpose_bf16", &transpose_bf16, "w.t().contiguous() (LDS-tiled bf16 transpose)");
   m.def("gelu_bwd", &gelu_bwd, "dh = da * gelu'(h) (erf GELU), bf16");
   m.def("ce_part_fold", &ce_part_fold, "per-segment fold of ce_bwd_cs's column partials");
   m.def("norm_fwd", &norm_fwd, "LayerNorm / RMSNorm (+ residual add) forward");
@@ -2195,8 +2212,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, "NT GEMM with fused epilogues (bias / bias+GELU / GELU backward + "
         "column sums)", py::arg("a"), py::arg("b"), py::arg("ep"), py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("out") = py::none(),
-        py::arg("colsum_out") = py::none(), py::arg("cin") = py::none(),
-        py::arg("b_kn") = false);
+        py::arg("colsum_out") = py::none(), py::arg("cin") = py::none());
   m.def("gemm_nt_ok", &gemm_nt_ok, "shape eligibility of gemm_nt");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);

@@ -375,6 +375,22 @@ int smallm_variant() {
   return v;
 }
 
+int pick_variant(int64_t M, int N, int* BM, int* BN);
+
+// CML_CONV_GEMM2 (A/B, default 1): stride-1 3x3 convs whose 256 x 256 grid is used (variant 4)
+// and whose pixel count is a multiple of 256 run on gemm.hip's schedule instead (launch_gemm_conv:
+// 16x16x32 MFMAs, four staggered phases per k-tile with 4 DMA units in flight and counted vmcnt,
+// no per-step drain) with the same epilogues
+bool use_gemm2(int64_t M, int N, int C, int taps, int stride) {
+  static const bool on = [] {
+    const char* e = getenv("CML_CONV_GEMM2");
+    return !e || e[0] != '0';
+  }();
+  if (!on || taps != 9 || stride != 1 || !gemm_conv_eligible(M, N, C)) return false;
+  int BM = 0, BN = 0;
+  return pick_variant(M, N, &BM, &BN) == 4;
+}
+
 // the variant and tile (BM, BN) for an M x N output
 int pick_variant(int64_t M, int N, int* BM, int* BN) {
   const bool wide = N % 128 == 0;
@@ -458,6 +474,25 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
   a.KS = taps * C / kBK;
   a.part = part;
   a.shift = shift;
+  if (use_gemm2(M, N, C, taps, stride)) {
+    GemmArgs g{};
+    g.a = a.x;
+    g.b = a.w;
+    g.y = a.y;
+    g.zero = a.zero;
+    g.M = M;
+    g.N = N;
+    g.C = C;
+    g.H = OH;
+    g.W = OW;
+    g.part = part;
+    g.shift = shift;
+    hipError_t e = launch_gemm_conv(g, part ? EP_CONV_ST : EP_STORE, st);
+    if (e != hipSuccess || !part || !mean) return e;
+    const int R = static_cast<int>(M / 256) * 2;
+    return launch_bn_stats_finalize(part, R, 256, N, M, shift, eps, momentum, mean, invstd, rmean,
+                                    rvar, st, part + static_cast<size_t>(N / 256) * R * 2 * 256);
+  }
   hipError_t e = taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
   if (e != hipSuccess || !part || !mean) return e;
   int BM, BN;
@@ -498,6 +533,28 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
   a.sz = reinterpret_cast<const uint16_t*>(z);
   a.ep_sc = sc;
   a.ep_bi = bi;
+  if (use_gemm2(M, N, C, taps, 1)) {
+    GemmArgs g{};
+    g.a = a.x;
+    g.b = a.w;
+    g.y = a.y;
+    g.zero = a.zero;
+    g.M = M;
+    g.N = N;
+    g.C = C;
+    g.H = H;
+    g.W = W;
+    g.part = part;
+    g.shift = mean;
+    g.sz = a.sz;
+    g.ep_sc = sc;
+    g.ep_bi = bi;
+    hipError_t e = launch_gemm_conv(g, EP_CONV_BB, st);
+    if (e != hipSuccess) return e;
+    const int R = static_cast<int>(M / 256) * 2;
+    return launch_bnbwd_sums_finalize(part, R, 256, N, invstd, sdz, sdzx, st,
+                                      part + static_cast<size_t>(N / 256) * R * 2 * 256);
+  }
   hipError_t e = taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
   if (e != hipSuccess) return e;
   int BM, BN;

@@ -2,8 +2,7 @@
 // backward + bias-gradient column sums), gfx950 / CDNA4:
 //
 //   y[m][n] = epi( sum_k A[m][k] B[n][k] )           A [M][K], B [N][K]: both K-contiguous ("NT",
-//                                                     nn.Linear's x W^T), or B given as [K][N]
-//                                                     (b_kn: a data gradient dy W, no W^T copy)
+//                                                     nn.Linear's x W^T)
 //   EP_STORE   y = bf16(acc + bias[n]) [+ cin[m][n]]  (bias, cin optional; cin may alias y: the
 //                                                     residual-gradient add of a data gradient)
 //   EP_GELU    h = bf16(acc + bias[n]) -> aux,  y = bf16(gelu(h))   (erf GELU, from the bf16 h)
@@ -67,21 +66,7 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_t a, bf16x8_t b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// BKN: B given as [K][N] (row-major, contraction-major: a weight W [out][in] used as the B of a data
-// gradient dx = dy W), staged without a transposed copy. Its K-tile is two sub-images, one per
-// 32-column half of every 64-column wave group (units U2 / U3), each [64 k][128 n] with 256-B rows;
-// 32-B slot t of row r holds columns 16 (t ^ kn_s(r)) .. +15 (the XOR lives in the per-lane DMA
-// source address), and the fragments are read with ds_read_b64_tr_b16: lane group fc takes k rows
-// 8 (fc + 4 ks) + 0..3 and + 4..7 of 16 columns, so a 32-lane half reads 8 rows whose kn_s values
-// are distinct: conflict-free.
-__device__ __forceinline__ int kn_s(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
-__device__ __forceinline__ uint2 tr_rd(const char* p) {
-  return __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p)));
-}
-
-template <int EP, bool BKN>
+template <int EP, bool CONV>
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -99,6 +84,19 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   // ---- staging: unit u (0..3 = U1..U4) of K-tile kt into buffer buf; this wave's 2 of the
   // unit's 16 wave-instructions (8 rows x 128 B each)
   const int lrow = lane >> 3, lp = lane & 7;
+  // CONV: this lane's 4 A rows (j = 2 s + (u == 3): tile rows 64 j + 8 wave + lrow) as pixels
+  int pbase[CONV ? 4 : 1], poh[CONV ? 4 : 1], pow_[CONV ? 4 : 1];
+  if constexpr (CONV) {
+    const int HW = a.H * a.W;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + 64 * j + 8 * wave + lrow;
+      const int img = m / HW, rem = m - img * HW;
+      pbase[j] = img * HW;
+      poh[j] = rem / a.W;
+      pow_[j] = rem - poh[j] * a.W;
+    }
+  }
   auto stage = [&](int u, int kt, int buf) {
     kt = kt < nk ? kt : nk - 1;                 // past the end: a harmless repeat (dead buffer)
     const int64_t kofs = static_cast<int64_t>(kt) * kBK;
@@ -108,21 +106,23 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
       int row0;
       if (u == 0 || u == 3) row0 = (i >> 3) * 128 + (u == 3 ? 64 : 0) + (i & 7) * 8;   // A
       else row0 = (i >> 2) * 64 + (u == 2 ? 32 : 0) + (i & 3) * 8;                  // B
-      const bool isA = (u == 0 || u == 3);
-      if (BKN && !isA) {
-        // sub-image u - 1, rows 4 i .. 4 i + 3 (1 KB); lane: row 4 i + lane / 16, 16-B piece lane & 15
-        const int r = 4 * i + (lane >> 4);
-        const int np = 16 * (((lane & 15) >> 1) ^ kn_s(r)) + 8 * (lane & 1);   // column in sub-image
-        const int n = n0 + (np >> 5) * 64 + (u - 1) * 32 + (np & 31);
-        const uint16_t* src = a.b + (kofs + r) * a.ldb + n;
-        char* dst = smem + buf * kBuf + kImg + (u - 1) * (kImg / 2) + i * 1024;
-        __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
-        continue;
-      }
       const int row = row0 + lrow;
       const int c = lp ^ ((row >> 1) & 7);
-      const uint16_t* src = isA ? a.a + static_cast<int64_t>(m0 + row) * a.lda + kofs + 8 * c
-                                : a.b + static_cast<int64_t>(n0 + row) * a.ldb + kofs + 8 * c;
+      const bool isA = (u == 0 || u == 3);
+      const uint16_t* src;
+      if (CONV && isA) {
+        // k-tile kt = tap (C / 64) + cc: input pixel (oh + ky - 1, ow + kx - 1), channels cc 64 ..
+        const int cs = a.C >> 6, tap = kt / cs, cc = kt - tap * cs;
+        const int j = 2 * s + (u == 3 ? 1 : 0);
+        const int ih = poh[j] + tap / 3 - 1, iw = pow_[j] + (tap - 3 * (tap / 3)) - 1;
+        const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(a.H) &&
+                        static_cast<unsigned>(iw) < static_cast<unsigned>(a.W);
+        src = ok ? a.a + (static_cast<int64_t>(pbase[j]) + ih * a.W + iw) * a.C + cc * kBK + 8 * c
+                 : a.zero;
+      } else {
+        src = isA ? a.a + static_cast<int64_t>(m0 + row) * a.lda + kofs + 8 * c
+                  : a.b + static_cast<int64_t>(n0 + row) * a.ldb + kofs + 8 * c;
+      }
       char* dst = smem + buf * kBuf + (isA ? 0 : kImg) + row0 * 128;
       __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
     }
@@ -141,20 +141,6 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
             img + swz(wm * 128 + mh * 64 + mt * 16 + fr, fc + 4 * ks));
   };
   auto readB = [&](bf16x8_t (&f)[2][2], int nh, int buf) {
-    if constexpr (BKN) {
-      const char* img = smem + buf * kBuf + kImg + nh * (kImg / 2);
-      const int q = (lane >> 2) & 3, p8 = 8 * (lane & 3);
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int t = 2 * wn + nt, r1 = 8 * (fc + 4 * ks) + q, r2 = r1 + 4;
-          const uint2 lo = tr_rd(img + r1 * 256 + 32 * (t ^ kn_s(r1)) + p8);
-          const uint2 hi = tr_rd(img + r2 * 256 + 32 * (t ^ kn_s(r2)) + p8);
-          f[nt][ks] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
-        }
-      return;
-    }
     const char* img = smem + buf * kBuf + kImg;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
@@ -237,14 +223,19 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   // of stalling every row (a dependent load per row cost ~13 us per tile).
   const int c8 = lane & 7;
   const int ncol = n0 + wn * 64 + 8 * c8;
-  constexpr bool kPre = EP == EP_DGELU || EP == EP_STORE;
-  const uint16_t* psrc = EP == EP_DGELU ? a.aux : a.cin;
-  uint4 pre[kPre ? 16 : 1];
+  constexpr bool kPre = EP == EP_DGELU || EP == EP_STORE || EP == EP_CONV_BB;
+  const uint16_t* psrc = EP == EP_DGELU ? a.aux : (EP == EP_CONV_BB ? a.sz : a.cin);
+  // (EP_CONV_BB holds more per-channel state: an 8-row window, each slot refilled with row it + 8
+  // once row it is consumed, so 8 loads stay in flight without spilling)
+  constexpr int kPN = EP == EP_CONV_BB ? 8 : 16;
+  uint4 pre[kPre ? kPN : 1];
+  auto pre_row = [&](int it) {
+    return *reinterpret_cast<const uint4*>(
+        psrc + static_cast<int64_t>(m0 + wm * 128 + 8 * it + lrow) * a.ldy + ncol);
+  };
   if (kPre && psrc) {
 #pragma unroll
-    for (int it = 0; it < 16; ++it)
-      pre[it] = *reinterpret_cast<const uint4*>(
-          psrc + static_cast<int64_t>(m0 + wm * 128 + 8 * it + lrow) * a.ldy + ncol);
+    for (int it = 0; it < kPN; ++it) pre[it] = pre_row(it);
   }
   char* img = smem + wave * (128 * 128);
   // lane's 16 output channels (4 per accumulator column group): n = ni 16 + 4 fc + j
@@ -278,16 +269,59 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 
-  float cs[8];
+  float cs[8], cq[8], sh[8], esc[8], ebi[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) cs[e] = 0.f;
+  for (int e = 0; e < 8; ++e) {
+    cs[e] = 0.f;
+    cq[e] = 0.f;
+  }
+  if constexpr (EP == EP_CONV_ST || EP == EP_CONV_BB) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sh[e] = a.shift ? a.shift[ncol + e] : 0.f;
+  }
+  if constexpr (EP == EP_CONV_BB) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      esc[e] = a.ep_sc[ncol + e];
+      ebi[e] = a.ep_bi[ncol + e];
+    }
+  }
 #pragma unroll
   for (int it = 0; it < 16; ++it) {
     const int row = 8 * it + lrow;
     const uint4 v = *reinterpret_cast<const uint4*>(img + swz(row, c8));
     const int64_t m = m0 + wm * 128 + row;
     uint16_t* yp = a.y + m * a.ldy + ncol;
-    if constexpr (EP == EP_STORE) {
+    if constexpr (EP == EP_CONV_ST || EP == EP_CONV_BB) {
+      *reinterpret_cast<uint4*>(yp) = v;
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      if constexpr (EP == EP_CONV_ST) {   // shifted sums of the stored bf16 values
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float lo = __uint_as_float(w4[q] << 16) - sh[2 * q];
+          const float hi = __uint_as_float(w4[q] & 0xffff0000u) - sh[2 * q + 1];
+          cs[2 * q] += lo;
+          cs[2 * q + 1] += hi;
+          cq[2 * q] = fmaf(lo, lo, cq[2 * q]);
+          cq[2 * q + 1] = fmaf(hi, hi, cq[2 * q + 1]);
+        }
+      } else {   // BN + ReLU backward sums: y' = relu'(z sc + bi) y, s += y', q += y' (z - mean)
+        const uint4 zv = pre[it % kPN];
+        if (kPN == 8 && it + 8 < 16) pre[it % kPN] = pre_row(it + 8);
+        const uint32_t z4[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float zlo = __uint_as_float(z4[q] << 16), zhi = __uint_as_float(z4[q] & 0xffff0000u);
+          const float lo = fmaf(zlo, esc[2 * q], ebi[2 * q]) > 0.f ? __uint_as_float(w4[q] << 16) : 0.f;
+          const float hi = fmaf(zhi, esc[2 * q + 1], ebi[2 * q + 1]) > 0.f
+                               ? __uint_as_float(w4[q] & 0xffff0000u) : 0.f;
+          cs[2 * q] += lo;
+          cs[2 * q + 1] += hi;
+          cq[2 * q] = fmaf(lo, zlo - sh[2 * q], cq[2 * q]);
+          cq[2 * q + 1] = fmaf(hi, zhi - sh[2 * q + 1], cq[2 * q + 1]);
+        }
+      }
+    } else if constexpr (EP == EP_STORE) {
       if (a.cin) {   // y = bf16(bf16(acc + bias) + cin): a residual gradient added on the way out
         const uint4 cv = pre[it];
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, c4[4] = {cv.x, cv.y, cv.z, cv.w};
@@ -322,6 +356,30 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
         cs[2 * q + 1] += __uint_as_float(o[q] & 0xffff0000u);
       }
       *reinterpret_cast<uint4*>(yp) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  if constexpr (EP == EP_CONV_ST || EP == EP_CONV_BB) {
+    // lanes with equal lane & 7 hold the same 8 channels: fixed-order xor tree over lane >> 3;
+    // one partial row per (tile, wave row) of conv_gemm.hip's slab layout
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float s1 = cs[e], s2 = cq[e];
+      s1 += __shfl_xor(s1, 8, 64);
+      s2 += __shfl_xor(s2, 8, 64);
+      s1 += __shfl_xor(s1, 16, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      cs[e] = s1;
+      cq[e] = s2;
+    }
+    if (lane < 8) {
+      const int R = static_cast<int>(a.M / kT) * 2;
+      float* p = a.part + (static_cast<int64_t>(ntile) * R + mtile * 2 + wm) * 2 * kT + wn * 64 + 8 * lane;
+      reinterpret_cast<float4*>(p)[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+      reinterpret_cast<float4*>(p)[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
+      reinterpret_cast<float4*>(p + kT)[0] = make_float4(cq[0], cq[1], cq[2], cq[3]);
+      reinterpret_cast<float4*>(p + kT)[1] = make_float4(cq[4], cq[5], cq[6], cq[7]);
     }
   }
   if constexpr (EP == EP_DGELU) {
@@ -365,7 +423,7 @@ bool gemm_nt_eligible(int64_t M, int64_t N, int64_t K) {
          (M / kT) * (N / kT) < (1LL << 31);
 }
 
-hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st, bool b_kn) {
+hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st) {
   if (!gemm_nt_eligible(a.M, a.N, a.K)) return hipErrorInvalidValue;
   if ((a.lda % 8) || (a.ldb % 8) || (a.ldy % 8)) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(a.a) | reinterpret_cast<uintptr_t>(a.b) |
@@ -374,21 +432,53 @@ hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st, bool b_kn) 
   if ((ep == EP_GELU || ep == EP_DGELU) && (a.aux == nullptr || reinterpret_cast<uintptr_t>(a.aux) % 16))
     return hipErrorInvalidValue;
   const int tiles = (a.M / kT) * (a.N / kT);
-#define CML_GEMM(E, T)                                                                       \
+#define CML_GEMM(E, CV)                                                                      \
   do {                                                                                       \
-    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<E, T>),                 \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<E, CV>),                \
                         hipFuncAttributeMaxDynamicSharedMemorySize, kLds);                   \
-    gemm_nt_kernel<E, T><<<tiles, kThreads, kLds, st>>>(a);                                  \
+    gemm_nt_kernel<E, CV><<<tiles, kThreads, kLds, st>>>(a);                                 \
   } while (0)
-  switch (ep) {
-    case EP_STORE: if (b_kn) CML_GEMM(EP_STORE, true); else CML_GEMM(EP_STORE, false); break;
-    case EP_GELU: if (b_kn) CML_GEMM(EP_GELU, true); else CML_GEMM(EP_GELU, false); break;
-    case EP_DGELU: if (b_kn) CML_GEMM(EP_DGELU, true); else CML_GEMM(EP_DGELU, false); break;
-    default:
-      return hipErrorInvalidValue;
+  if (a.conv) {
+    switch (ep) {
+      case EP_STORE: CML_GEMM(EP_STORE, true); break;
+      case EP_CONV_ST: CML_GEMM(EP_CONV_ST, true); break;
+      case EP_CONV_BB: CML_GEMM(EP_CONV_BB, true); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (ep) {
+      case EP_STORE: CML_GEMM(EP_STORE, false); break;
+      case EP_GELU: CML_GEMM(EP_GELU, false); break;
+      case EP_DGELU: CML_GEMM(EP_DGELU, false); break;
+      default: return hipErrorInvalidValue;
+    }
   }
 #undef CML_GEMM
   return hipGetLastError();
+}
+
+bool gemm_conv_eligible(int64_t M, int N, int C) {
+  return M > 0 && M % kT == 0 && N % kT == 0 && C % kBK == 0 && M < (1LL << 31) &&
+         9LL * C <= 65536;
+}
+
+hipError_t launch_gemm_conv(const GemmArgs& a0, int ep, hipStream_t st) {
+  GemmArgs a = a0;
+  a.conv = 1;
+  a.K = 9LL * a.C;
+  a.lda = a.C;
+  a.ldb = a.K;
+  a.ldy = a.N;
+  if (!gemm_conv_eligible(a.M, static_cast<int>(a.N), a.C) || !a.zero || !a.a || !a.b || !a.y)
+    return hipErrorInvalidValue;
+  if (static_cast<int64_t>(a.H) * a.W < 1 || a.M % (static_cast<int64_t>(a.H) * a.W))
+    return hipErrorInvalidValue;
+  if ((ep == EP_CONV_ST || ep == EP_CONV_BB) && !a.part) return hipErrorInvalidValue;
+  if (ep == EP_CONV_BB && (!a.sz || !a.ep_sc || !a.ep_bi)) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(a.a) | reinterpret_cast<uintptr_t>(a.b) |
+       reinterpret_cast<uintptr_t>(a.y) | reinterpret_cast<uintptr_t>(a.zero)) % 16)
+    return hipErrorInvalidValue;
+  return launch_gemm_nt(a, ep, st);
 }
 
 hipError_t launch_colsum_fold(const float* part, int64_t M, int N, int nseg, void* out, int64_t ldo,

@@ -158,6 +158,9 @@ struct MultiCopyArgs {
   int n;
 };
 hipError_t launch_multi_copy(const MultiCopyArgs& args, hipStream_t stream);
+// dst [C][R] = src [R][C]^T, bf16, R and C multiples of 64, row strides lds / ldd (% 8 == 0)
+hipError_t launch_transpose_bf16(const void* src, void* dst, int R, int C, int64_t lds, int64_t ldd,
+                                 hipStream_t stream);
 
 // 3x3/s2/p1 max-pool backward that also returns the channel sums of dx (fp32 [C]; the stem BN's
 // dbeta). dy2 (nullable): a second output gradient, summed on load. work:
@@ -488,7 +491,7 @@ hipError_t launch_smo(const double* K, const double* y, const int* ns, int B, in
 // y = bf16(gelu(h)); EP_DGELU: y = bf16(bf16(acc) * gelu'(aux)) and, when part is set, fp32
 // column sums of y per 128-row block into part [M / 128][N]. M % 256 == 0, N % 256 == 0,
 // K % 64 == 0, leading dimensions % 8 == 0, 16-B aligned bases.
-enum { EP_STORE = 0, EP_GELU = 1, EP_DGELU = 2 };
+enum { EP_STORE = 0, EP_GELU = 1, EP_DGELU = 2, EP_CONV_ST = 3, EP_CONV_BB = 4 };
 struct GemmArgs {
   const uint16_t* a;
   const uint16_t* b;
@@ -499,10 +502,24 @@ struct GemmArgs {
   const uint16_t* cin;    // EP_STORE: y = bf16(bf16(acc + bias) + cin), cin [M][ldy] (may be y)
   int64_t M, N, K;
   int64_t lda, ldb, ldy;
+  // implicit-GEMM 3x3 / stride 1 / padding 1 convolution (conv = 1): A = the NHWC input x
+  // [Nimg][H][W][C] gathered per tap (a = x, K = 9 C, b = wf [N][9 C]); padded taps read `zero`.
+  // EP_CONV_ST: the BN statistics of the stored bf16 output (minus shift[n]) as partial rows
+  // part[(ntile R + 2 mtile + wave row)][2][256], R = 2 M / 256; EP_CONV_BB: instead the sums of
+  // the BN + ReLU backward that y feeds (z = sz [M][N], ReLU bit z ep_sc + ep_bi > 0, shift = mean)
+  int conv, C, H, W;
+  const uint16_t* zero;
+  const float* shift;
+  const uint16_t* sz;
+  const float* ep_sc;
+  const float* ep_bi;
 };
 bool gemm_nt_eligible(int64_t M, int64_t N, int64_t K);
-// b_kn: b is [K][N] (row stride ldb), read through transposed LDS reads
-hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st, bool b_kn = false);
+hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st);
+// the conv form (a.conv = 1; M % 256 == 0, N % 256 == 0, C % 64 == 0), ep EP_STORE /
+// EP_CONV_ST / EP_CONV_BB (conv_gemm.hip's 256 x 256 path for stride-1 3x3 convs)
+bool gemm_conv_eligible(int64_t M, int N, int C);
+hipError_t launch_gemm_conv(const GemmArgs& a, int ep, hipStream_t st);
 // out[s][n] = sum of the 128-row partial column sums of segment s of M rows (nseg equal
 // segments, fixed order); out bf16 [nseg][ldo] or fp32 when out_f32
 hipError_t launch_colsum_fold(const float* part, int64_t M, int N, int nseg, void* out, int64_t ldo,

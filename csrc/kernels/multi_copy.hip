@@ -59,6 +59,54 @@ __global__ __launch_bounds__(kCB) void multi_copy_kernel(MultiCopyArgs a) {
 
 }  // namespace
 
+namespace {
+// dst [C][R] = src [R][C]^T (bf16, R % 64 == 0, C % 64 == 0, 16-B aligned rows): one 64 x 64
+// tile per workgroup, 16-B loads into a padded LDS tile and 16-B stores of the transposed rows
+// (the weight transposes of the data-gradient GEMMs: ATen's strided copy ran them at ~0.6 TB/s,
+// 12 us per BERT weight, profiles/r04_06/bert_kernels.md)
+__global__ __launch_bounds__(256) void transpose64_kernel(const uint16_t* __restrict__ src,
+                                                         uint16_t* __restrict__ dst, int R, int C,
+                                                         int64_t lds_, int64_t ldd) {
+  __shared__ uint16_t t[64][64 + 2];   // +2: a row read down a column hits distinct banks
+  const int tc = blockIdx.x, tr = blockIdx.y;
+  const int r0 = tr * 64, c0 = tc * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {   // 64 rows x 8 chunks of 8 elements
+    const int i = tid + 256 * it, r = i >> 3, c = (i & 7) * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(src + static_cast<int64_t>(r0 + r) * lds_ + c0 + c);
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      t[r][c + 2 * q] = static_cast<uint16_t>(w4[q] & 0xffffu);
+      t[r][c + 2 * q + 1] = static_cast<uint16_t>(w4[q] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {   // output row c (a source column), 8 consecutive source rows
+    const int i = tid + 256 * it, c = i >> 3, r = (i & 7) * 8;
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      o[q] = static_cast<uint32_t>(t[r + 2 * q][c]) | (static_cast<uint32_t>(t[r + 2 * q + 1][c]) << 16);
+    *reinterpret_cast<uint4*>(dst + static_cast<int64_t>(c0 + c) * ldd + r0 + r) =
+        make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_transpose_bf16(const void* src, void* dst, int R, int C, int64_t lds_,
+                                 int64_t ldd, hipStream_t st) {
+  if (R < 64 || C < 64 || R % 64 || C % 64 || lds_ % 8 || ldd % 8 ||
+      ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15))
+    return hipErrorInvalidValue;
+  transpose64_kernel<<<dim3(C / 64, R / 64), 256, 0, st>>>(
+      reinterpret_cast<const uint16_t*>(src), reinterpret_cast<uint16_t*>(dst), R, C, lds_, ldd);
+  return hipGetLastError();
+}
+
 hipError_t launch_multi_copy(const MultiCopyArgs& a, hipStream_t st) {
   if (a.n < 1 || a.n > kMaxCopy) return hipErrorInvalidValue;
   for (int e = 0; e < a.n; ++e) {

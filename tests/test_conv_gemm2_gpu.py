@@ -1,0 +1,110 @@
+"""Stride-1 3x3 convolutions on gemm.hip's schedule (``launch_gemm_conv``: implicit-GEMM A
+operand gathered per tap by the DMA path, 16x16x32 MFMAs, four staggered phases per k-tile), which
+conv_gemm.hip routes to when the 256 x 256 tile grid applies and the pixel count is a multiple of
+256: plain output, the BN-statistics epilogue and the BN + ReLU backward sums epilogue, against
+fp32 / fp64 PyTorch oracles. Shapes: ResNet-50 layer-3 / layer-4 channel counts (256 / 512),
+image borders on every side (padded taps read the zero row)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from consensusml_amd.ops.native import lib
+    return lib()
+
+
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _rows(t):
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
+
+
+# (images, C, Co, H): M = images H H is a multiple of 256
+SHAPES = [(4, 256, 256, 16), (16, 512, 512, 8), (4, 64, 256, 16), (16, 256, 512, 14),
+          (64, 512, 512, 7)]
+
+
+@pytest.mark.parametrize("N,C,Co,H", SHAPES)
+def test_gemm_conv_forward_vs_fp32(cuda, N, C, Co, H):
+    g0 = torch.Generator(device=cuda).manual_seed(31)
+    x = _nhwc((torch.randn(N, C, H, H, device=cuda, generator=g0) + 0.25).bfloat16())
+    w = (torch.randn(Co, C, 3, 3, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
+    assert (N * H * H) % 256 == 0
+    wf = w.permute(0, 2, 3, 1).reshape(Co, 9 * C).contiguous()
+    y = _lib().conv_gemm(x, wf, 9)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    assert _rel(y, ref) < 5e-3
+    # every pixel: the border rows / columns (padded taps) are as close as the interior
+    err = (y.float() - ref).abs().amax(1)
+    assert float(err[:, 0, :].max()) < 8 * float(err[:, H // 2, :].max()) + 1e-2
+
+
+@pytest.mark.parametrize("N,C,Co,H", SHAPES[:4])
+def test_gemm_conv_bn_stats_and_grads(cuda, N, C, Co, H):
+    """conv3x3_bn_stats (forward + statistics epilogue) and the data gradient through the rotated
+    weights (a plain gemm conv when C % 256 == 0) vs fp32 autograd."""
+    from consensusml_amd.ops import conv as fconv
+    g0 = torch.Generator(device=cuda).manual_seed(32)
+    x = _nhwc((torch.randn(N, C, H, H, device=cuda, generator=g0) + 0.3).bfloat16())
+    w = (torch.randn(Co, C, 3, 3, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
+    conv = torch.nn.Conv2d(C, Co, 3, padding=1, bias=False).to(cuda, torch.bfloat16)
+    bn = torch.nn.BatchNorm2d(Co).to(cuda)
+    with torch.no_grad():
+        conv.weight.copy_(w)
+        bn.running_mean.copy_(torch.randn(Co, device=cuda, generator=g0) * 0.1)
+    xi = x.clone().requires_grad_(True)
+    z, (mean, invstd) = fconv.conv3x3_bn_stats(xi, conv, bn)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    assert _rel(z, ref) < 5e-3
+    zb = z.float()
+    torch.testing.assert_close(mean, zb.mean((0, 2, 3)), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(invstd, (zb.var((0, 2, 3), unbiased=False) + bn.eps).rsqrt(),
+                               rtol=1e-3, atol=1e-3)
+    gy = _nhwc(torch.randn(z.shape, device=cuda, generator=g0).bfloat16())
+    z.backward(gy)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    F.conv2d(xr, wr, padding=1).backward(gy.float())
+    assert _rel(xi.grad, xr.grad) < 5e-3
+    assert _rel(conv.weight.grad, wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,C,Co,H", SHAPES[:4])
+def test_gemm_conv_bnsums_vs_fp64(cuda, N, C, Co, H):
+    g0 = torch.Generator(device=cuda).manual_seed(33)
+    x = _nhwc(torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16())
+    z = _nhwc(torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16())
+    w = (torch.randn(Co, 9 * C, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
+    zero = torch.zeros(64, device=cuda, dtype=torch.bfloat16)
+    gam = (torch.rand(Co, device=cuda, generator=g0) + 0.5).bfloat16()
+    bet = (torch.randn(Co, device=cuda, generator=g0) * 0.1).bfloat16()
+    Z = _rows(z).double()
+    mean = Z.mean(0).float()
+    invstd = (Z.var(0, unbiased=False) + 1e-5).rsqrt().float()
+    sc = gam.float() * invstd
+    bi = bet.float() - mean * sc
+    y, s, q = _lib().conv_gemm_bnsums(x, w, 9, zero, z, sc, bi, mean, invstd)
+    assert torch.equal(y, _lib().conv_gemm(x, w, 9, zero))
+    m = (torch.addcmul(bi, _rows(z), sc) > 0).double()
+    dyv = _rows(y).double() * m
+    torch.testing.assert_close(s.double(), dyv.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(q.double(), (dyv * (Z - mean.double()) * invstd.double()).sum(0),
+                               rtol=1e-5, atol=1e-3)
+
+
+def test_gemm_conv_deterministic(cuda):
+    g0 = torch.Generator(device=cuda).manual_seed(34)
+    x = _nhwc(torch.randn(16, 256, 14, 14, device=cuda, generator=g0).bfloat16())
+    w = (torch.randn(256, 9 * 256, device=cuda, generator=g0) * 0.02).bfloat16()
+    a = _lib().conv_gemm(x, w, 9)
+    b = _lib().conv_gemm(x, w, 9)
+    assert torch.equal(a, b)

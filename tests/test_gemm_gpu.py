@@ -108,41 +108,13 @@ def test_gemm_cin_inplace(cuda):
     assert _rel(c, ref) < 4e-3
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 768), (1024, 3072, 768),
-                                   (768, 512, 3072)])
-@pytest.mark.parametrize("ep", [0, 2])
-def test_gemm_b_kn_layout(cuda, M, N, K, ep):
-    """B given as [K][N] (a weight used as a data gradient's B, read by transposed LDS reads) gives
-    the same result as the [N][K] copy, bit for bit (same summation order), including the GELU
-    backward epilogue and its column sums."""
+@pytest.mark.parametrize("R,C", [(768, 3072), (2304, 768), (64, 64), (256, 1024)])
+def test_transpose_bf16(cuda, R, C):
     from consensusml_amd.ops.native import lib
-    a = _rand(M, K, dev=cuda, seed=4)
-    b_kn = _rand(K, N, dev=cuda, seed=5)
-    b_nk = b_kn.t().contiguous()
-    if ep == 0:
-        y1 = lib().gemm_nt(a, b_nk, 0)
-        y2 = lib().gemm_nt(a, b_kn, 0, b_kn=True)
-        assert torch.equal(y1, y2)
-        assert _rel(y2, a.float() @ b_kn.float()) < 4e-3
-        # integer data: exact, so every element (and the layout) is checked
-        ai = torch.randint(-2, 3, (M, K), device=cuda).bfloat16()
-        bi = torch.randint(-2, 3, (K, N), device=cuda).bfloat16()
-        if K <= 64:
-            assert torch.equal(lib().gemm_nt(ai, bi, 0, b_kn=True).float(), ai.float() @ bi.float())
-    else:
-        h = _rand(M, N, dev=cuda, seed=6, scale=2.0)
-        cs1 = torch.empty(1, N, device=cuda, dtype=torch.float32)
-        cs2 = torch.empty(1, N, device=cuda, dtype=torch.float32)
-        y1 = lib().gemm_nt(a, b_nk, 2, aux=h, colsum_out=cs1)
-        y2 = lib().gemm_nt(a, b_kn, 2, aux=h, colsum_out=cs2, b_kn=True)
-        assert torch.equal(y1, y2) and torch.equal(cs1, cs2)
-
-
-def test_gemm_b_kn_strided_rows(cuda):
-    """[K][N] B as a column slice of a wider matrix (row stride > N)."""
-    from consensusml_amd.ops.native import lib
-    a = _rand(512, 256, dev=cuda, seed=7)
-    big = _rand(256, 1024, dev=cuda, seed=8)
-    b = big[:, 256:768]
-    y = lib().gemm_nt(a, b, 0, b_kn=True)
-    assert _rel(y, a.float() @ b.float()) < 4e-3
+    w = _rand(R, C, dev=cuda, seed=9)
+    assert torch.equal(lib().transpose_bf16(w), w.t().contiguous())
+    big = _rand(R, C + 64, dev=cuda, seed=10)
+    v = big[:, 64:]
+    assert torch.equal(lib().transpose_bf16(v), v.t().contiguous())
+    odd = _rand(R, 40, dev=cuda, seed=11)   # not a 64-multiple: ATen fallback
+    assert torch.equal(lib().transpose_bf16(odd), odd.t().contiguous())
