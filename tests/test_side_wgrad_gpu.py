@@ -1,7 +1,9 @@
 """Weight gradients on a side HIP stream (ops.side, PerfPolicy.side_wgrad): the same kernels on
-the same inputs, so three ResNet-50 training steps through the consensus engine give bit-identical
-parameters with and without the side stream; and a plain autograd backward outside the engine
-(not armed) never uses it."""
+the same inputs. Three ResNet-50 training steps through the consensus engine with and without the
+side stream agree as closely as two runs without it (MIOpen's split-K weight-gradient kernels for
+the library shapes sum with atomics, so even those two need not be bit-identical; a race would
+show as a far larger difference); and a plain autograd backward outside the engine (not armed)
+never uses the side stream."""
 import pytest
 import torch
 
@@ -34,13 +36,19 @@ def _train(cuda, side_on: bool, steps: int = 3):
     return losses, params
 
 
-def test_side_wgrad_bit_identical(cuda):
+def test_side_wgrad_matches_inline(cuda):
     from consensusml_amd.ops import side
     l0, p0 = _train(cuda, False)
+    l0b, p0b = _train(cuda, False)
     l1, p1 = _train(cuda, True)
-    assert l0 == l1
-    assert torch.equal(p0, p1)
     assert side._S.armed is None   # step() disarmed it
+    floor = float((p0b.float() - p0.float()).norm())
+    diff = float((p1.float() - p0.float()).norm())
+    scale = float(p0.float().norm())
+    assert l1[0] == l0[0]          # the first step's loss precedes any weight gradient
+    assert diff <= max(4 * floor, 1e-5 * scale), (diff, floor, scale)
+    for a, b, c in zip(l0, l0b, l1):
+        assert abs(c - a) <= max(4 * abs(b - a), 1e-5 * abs(a)), (l0, l0b, l1)
 
 
 def test_side_not_armed_outside_engine(cuda):
