@@ -15,7 +15,6 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import conv as fconv
-from ..ops import side
 from ..ops.bn import BatchNormAct2d, ResidualLink, bn_add_bn_relu, fused_ok, link_tap
 from ..ops.pool import bn_relu_max_pool2d, max_pool2d
 from ..ops.stem import stem_conv_bn_relu_pool, stem_ok
@@ -101,17 +100,13 @@ class _Conv1x1Fn(torch.autograd.Function):
         own_dw = ctx.own_wgrad and ctx.needs_input_grad[1]
         mio_dw = ctx.needs_input_grad[1] and not own_dw
         dx_m, dw = None, None
-        if mio_dx:
+        if mio_dx or mio_dw:
             dx_m, dw, _ = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                 [mio_dx, mio_dw, False])
-        elif mio_dw:   # weight gradient alone: off the critical path (ops.side)
-            dw = side.run(lambda: torch.ops.aten.convolution_backward(
-                dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                [False, True, False])[1], dy, x)
         if own_dw:
             from ..ops.native import lib
-            dw = side.run(lambda: lib().wgrad1x1(dy, x, w.dtype).view_as(w), dy, x)
+            dw = lib().wgrad1x1(dy, x, w.dtype).view_as(w)
         dx = dx_m if mio_dx else None
         if need_dx and ctx.dgrad_gemm:
             dy2 = dy.permute(0, 2, 3, 1).reshape(N * H * W, Co)

@@ -29,7 +29,6 @@ import torch
 import torch.nn.functional as F
 
 from ..perf import policy as _P
-from . import side
 from .bn import MaskedGrad
 from .native import lib
 
@@ -131,14 +130,14 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, own:
     """dW of a 1x1 conv. ``pro`` = (sc, bi): the conv's real input is max(x * sc + bi, 0)."""
     if own and stride == 1:
         sc, bi = pro if pro is not None else (None, None)
-        return side.run(lambda: lib().wgrad1x1(dy, x, w.dtype, sc, bi).view_as(w), dy, x, sc, bi)
+        return lib().wgrad1x1(dy, x, w.dtype, sc, bi).view_as(w)
     if pro is not None:   # library weight gradient needs the materialised input
         sc, bi = pro
         x = torch.relu(x.float() * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)).to(x.dtype)
         x = x.contiguous(memory_format=torch.channels_last)
-    return side.run(lambda: torch.ops.aten.convolution_backward(
-        dy, x, w, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1,
-        [False, True, False])[1], dy, x)
+    _, dw, _ = torch.ops.aten.convolution_backward(
+        dy, x, w, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])
+    return dw
 
 
 class _Conv1x1BNStatsFn(torch.autograd.Function):
@@ -232,8 +231,7 @@ class _BNReLUConv1x1BNResFn(torch.autograd.Function):
         Co, Ci = w.shape[0], w.shape[1]
         dw = None
         if ctx.needs_input_grad[5]:
-            dw = side.run(lambda: lib().wgrad1x1(gy, z, w.dtype, sc, bi, z3, mask, ca, cb,
-                                                 cc).view_as(w), gy, z, sc, bi, z3, mask, ca, cb, cc)
+            dw = lib().wgrad1x1(gy, z, w.dtype, sc, bi, z3, mask, ca, cb, cc).view_as(w)
         dy2 = lib().conv1x1_bnbwd(gy, z3, mask, ca, cb, cc, w.reshape(Co, Ci).t().contiguous())
         dz, dg2, db2, _ = lib().bn_bwd(dy2, None, z, None, g2, b2, mean2, invstd2, True, False)
         dres = None
@@ -625,11 +623,9 @@ def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tenso
     N, Ci, H, W = x.shape
     Co = dy.shape[1]
     if _P().own_wgrad3x3 and lib().wgrad3x3_direct_ok(N, H, W, Co, Ci):
-        zr = _zero_row(dy.device)
-        return side.run(lambda: lib().wgrad3x3(dy, x, w.dtype, zr), dy, x)
-    return side.run(lambda: torch.ops.aten.convolution_backward(
-        dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1],
-        dy, x)
+        return lib().wgrad3x3(dy, x, w.dtype, _zero_row(dy.device))
+    return torch.ops.aten.convolution_backward(
+        dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
 
 
 def _w3x3_layouts(w: torch.Tensor, want_wf: bool):
@@ -734,9 +730,8 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
 
 def _wgrad3x3_s2(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """Weight gradient of a stride-2 / padding-1 3x3 conv (MIOpen)."""
-    return side.run(lambda: torch.ops.aten.convolution_backward(
-        dy, x, w, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1],
-        dy, x)
+    return torch.ops.aten.convolution_backward(
+        dy, x, w, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
 
 
 class _Conv3x3S2BNStatsFn(torch.autograd.Function):

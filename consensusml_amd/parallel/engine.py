@@ -40,7 +40,6 @@ import torch.distributed as dist
 
 from ..config import TrainConfig
 from ..ops import kernels as K
-from ..ops import side
 from ..ops import worker_grads as WG
 from ..perf import policy as _P
 from ..ops.native import lib
@@ -216,9 +215,6 @@ class ConsensusEngine:
         gradients are zero-filled at flush), so no memset is needed."""
         for p in self.flat.params:
             p.grad = None
-        # every .grad is None and read only by the capture hooks until step(): weight gradients
-        # may run on a side stream (ops.side, PerfPolicy.side_wgrad)
-        side.arm(self.device)
         for v in self._ready.values():
             v.clear()
         self._flushed.clear()
@@ -313,7 +309,6 @@ class ConsensusEngine:
     def step(self) -> None:
         """Exchange, aggregate and update (call after all backward passes of the step)."""
         fl = self.flat
-        side.disarm()
         if self.param_prefetch:
             self.wait_params()          # params no forward touched
             if self._invoked:
@@ -366,7 +361,6 @@ class ConsensusEngine:
         fl = self.flat
         views = fl.grad_views(fl.grad_row)
         lst = self._ready[b.index]
-        side.join()   # side-stream weight gradients finished before the copy reads them
         if lst:
             dst = [views[i] for i in lst]
             src = [fl.params[i].grad for i in lst]

@@ -85,7 +85,6 @@ class PerfPolicy:
     padded_logits: bool = True            # biased linears with N % 8 != 0 (BERT MLM head) write
                                           # 16-B aligned padded rows; the CE backward emits the
                                           # bias gradient (no column-sum pass over R x V)
-    side_wgrad: bool = False              # conv weight gradients on a second HIP stream (ops.side)
     own_gemm_conv1x1: bool = True         # ResNet 1x1 convs that run as plain GEMMs (layers 3-4
                                           # forward / data gradient) on gemm.hip, not hipBLASLt
 
@@ -131,7 +130,6 @@ class PerfPolicy:
             own_gemm=_env_bool("CML_OWN_GEMM", True),
             fused_ffn=_env_bool("CML_FUSED_FFN", True),
             own_gemm_conv1x1=_env_bool("CML_OWN_GEMM_CONV1X1", True),
-            side_wgrad=_env_bool("CML_SIDE_WGRAD", False),
             padded_logits=_env_bool("CML_PADDED_LOGITS", True),
         )
 

@@ -29,8 +29,8 @@ def _rel(a, b):
 
 
 # (images, C, Co, H): M = images H H is a multiple of 256
-SHAPES = [(4, 256, 256, 16), (16, 512, 512, 8), (4, 64, 256, 16), (16, 256, 512, 14),
-          (64, 512, 512, 7)]
+SHAPES = [(4, 256, 256, 16), (16, 512, 512, 8), (4, 64, 256, 16), (64, 256, 512, 14),
+          (256, 512, 512, 7)]
 
 
 @pytest.mark.parametrize("N,C,Co,H", SHAPES)
