@@ -377,14 +377,15 @@ int smallm_variant() {
 
 int pick_variant(int64_t M, int N, int* BM, int* BN);
 
-// CML_CONV_GEMM2 (A/B, default 0): stride-1 3x3 convs whose 256 x 256 grid is used (variant 4)
+// CML_CONV_GEMM2 (A/B, default 1; profiles/r04_12: 3x3 class 23.00 -> 22.60 ms per step):
+// stride-1 3x3 convs whose 256 x 256 grid is used (variant 4)
 // and whose pixel count is a multiple of 256 run on gemm.hip's schedule instead (launch_gemm_conv:
 // 16x16x32 MFMAs, four staggered phases per k-tile with 4 DMA units in flight and counted vmcnt,
 // no per-step drain) with the same epilogues
 bool use_gemm2(int64_t M, int N, int C, int taps, int stride) {
   static const bool on = [] {
     const char* e = getenv("CML_CONV_GEMM2");
-    return e && e[0] == '1';
+    return !e || e[0] != '0';
   }();
   if (!on || taps != 9 || stride != 1 || !gemm_conv_eligible(M, N, C)) return false;
   int BM = 0, BN = 0;
