@@ -443,8 +443,9 @@ size_t conv_gemm_part_floats(int64_t M, int N) {
   const int64_t mtiles = (M + BM - 1) / BM;
   const int R = static_cast<int>(mtiles * (BM / 64));
   // the slab, then the fold area of launch_bn_stats_finalize
-  return static_cast<size_t>(N / BN) * (static_cast<size_t>(R) + bn_part_fold_slices(R, N / BN)) *
-         2 * BN;
+  const size_t g = static_cast<size_t>(N / BN) *
+                   (static_cast<size_t>(R) + bn_part_fold_slices(R, N / BN)) * 2 * BN;
+  return N == 64 && g < conv3x3p_part_floats() ? conv3x3p_part_floats() : g;
 }
 
 hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* zero, int Nimg,
@@ -475,6 +476,14 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
   a.KS = taps * C / kBK;
   a.part = part;
   a.shift = shift;
+  if (conv3x3p_eligible(Nimg, H, W, C, N, taps, stride)) {
+    int R = 0;
+    hipError_t e = launch_conv3x3p(x, w, y, zero, Nimg, H, part ? 1 : 0, part, shift, nullptr,
+                                   nullptr, nullptr, st, &R);
+    if (e != hipSuccess || !part || !mean) return e;
+    return launch_bn_stats_finalize(part, R, 64, 64, M, shift, eps, momentum, mean, invstd, rmean,
+                                    rvar, st, nullptr);
+  }
   if (use_gemm2(M, N, C, taps, stride)) {
     GemmArgs g{};
     g.a = a.x;
@@ -534,6 +543,12 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
   a.sz = reinterpret_cast<const uint16_t*>(z);
   a.ep_sc = sc;
   a.ep_bi = bi;
+  if (conv3x3p_eligible(Nimg, H, W, C, N, taps, 1)) {
+    int R = 0;
+    hipError_t e = launch_conv3x3p(x, w, y, zero, Nimg, H, 2, part, mean, z, sc, bi, st, &R);
+    if (e != hipSuccess) return e;
+    return launch_bnbwd_sums_finalize(part, R, 64, 64, invstd, sdz, sdzx, st, nullptr);
+  }
   if (use_gemm2(M, N, C, taps, 1)) {
     GemmArgs g{};
     g.a = a.x;
@@ -610,8 +625,9 @@ size_t conv_gemm_s2dgrad_part_floats(int64_t Mc, int N) {
   int BM, BN, WTN;
   tile_par(Mc, N, &BM, &BN, &WTN);
   const int R = static_cast<int>(4 * ((Mc + BM - 1) / BM) * (BM / 64));
-  return static_cast<size_t>(N / BN) * (static_cast<size_t>(R) + bn_part_fold_slices(R, N / BN)) *
-         2 * BN;
+  const size_t g = static_cast<size_t>(N / BN) *
+                   (static_cast<size_t>(R) + bn_part_fold_slices(R, N / BN)) * 2 * BN;
+  return N == 64 && g < conv3x3p_part_floats() ? conv3x3p_part_floats() : g;
 }
 
 // dx [Nimg, 2 Ho, 2 Wo, Ci] of a stride-2 / padding-1 3x3 conv from dy [Nimg, Ho, Wo, Co] and

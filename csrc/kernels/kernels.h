@@ -390,6 +390,15 @@ hipError_t launch_conv_gemm_s2dgrad(const void* dy, const void* wr, void* dx, co
 // 3x3 conv weight with strides s0..s3 (elements), in one launch; wf may be null.
 hipError_t launch_conv3x3_wlayouts(const void* w, int Co, int Ci, int64_t s0, int64_t s1,
                                    int64_t s2, int64_t s3, void* wf, void* wr, hipStream_t st);
+// Stride-1 3x3 conv of 64 -> 64 channels on 56-wide images from an LDS-resident input patch
+// (conv3x3p.hip; launch_conv_gemm / launch_conv_gemm_bnsums route there when eligible). ep 0: y
+// only; 1: + shifted BN statistics; 2: + BN + ReLU backward sums (z, sc, bi, shift = mean); one
+// partial row [2][64] per workgroup into part (*rows of them).
+bool conv3x3p_eligible(int Nimg, int H, int W, int C, int N, int taps, int stride);
+size_t conv3x3p_part_floats();
+hipError_t launch_conv3x3p(const void* x, const void* w, void* y, const void* zero, int Nimg, int H,
+                           int ep, float* part, const float* shift, const void* z, const float* sc,
+                           const float* bi, hipStream_t st, int* rows);
 hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* zero, int Nimg,
                             int H, int W, int C, int N, int taps, hipStream_t st,
                             float* part = nullptr, const float* shift = nullptr,
