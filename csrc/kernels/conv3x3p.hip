@@ -13,10 +13,10 @@
 // 1.5 x 128 B per output pixel); the 9 taps read shifted windows of the same patch.
 //
 // Layout (gfx950, one 448-thread workgroup per CU, persistent over a contiguous tile range):
-//   LDS = W image [9 x 64 rows][128 B] | two patch buffers [336 rows][128 B] | a zero row | the
-//   per-channel epilogue coefficients -- 160.6 KB. Rows are 128 B (64 channels), XOR-swizzled
-//   (16-B chunk c of row r at c ^ ((r >> 1) & 7); the DMA image is lane-linear, so the swizzle is
-//   applied through the per-lane SOURCE address, as in conv_gemm.hip).
+//   LDS = W image [9 x 64 rows][128 B] | two patch buffers [336 rows][128 B] | a zero row --
+//   156 KB. Rows are 128 B (64 channels), XOR-swizzled (16-B chunk c of row r at
+//   c ^ ((r >> 1) & 7); the DMA image is lane-linear, so the swizzle is applied through the
+//   per-lane SOURCE address, as in conv_gemm.hip).
 //   Patch row q = pr 56 + pc holds input pixel (r0 - 1 + pr, pc); rows outside the image are
 //   DMA'd from the zero buffer. Output pixel f of the tile (f = 56 tr + tc) reads tap (dy, dx)
 //   at patch row q = f + 56 (1 + dy) + dx -- linear in f, so a 32-pixel fragment is 32
@@ -24,16 +24,19 @@
 //   off the image (tc + dx outside [0, 56)) reads the zero row instead.
 //   Waves: 7, wave w owns the 32-pixel fragment w of the tile and all 64 output channels:
 //   2 accumulators of v_mfma_f32_32x32x16_bf16 (C^T = W X^T: a lane holds one pixel, 4 channels
-//   per accumulator row group), 72 MFMAs per tile, 1 patch + 2 weight ds_read_b128 per 2 MFMAs.
-//   Pipeline: the patch of tile j + 2 is DMA'd into tile j's buffer as soon as every wave has
-//   finished reading it (one barrier per tile), so each patch has a whole tile of compute to
-//   land; a counted vmcnt (the 6 DMA instructions of the next patch + the 8 stores of the last
-//   epilogue stay in flight) retires exactly the current patch.
-//   Epilogue straight from the accumulators: 8-B stores (4 channels of one pixel); EP 1: shifted
-//   BN statistics of the stored bf16 values, EP 2: the BN + ReLU backward sums of the data
-//   gradient (s += y', q += y' (z - mean), y' = (z sc + bi > 0) ? y : 0), both accumulated per
-//   lane over the workgroup's tiles and reduced once at the end into ONE partial row per
-//   workgroup (fixed order: deterministic), folded by conv1x1.hip's finalize kernels.
+//   per accumulator row group), 72 MFMAs per tile, 1 patch + 2 weight ds_read_b128 per 2 MFMAs,
+//   read two steps ahead.
+//   Epilogue: each wave rounds its 32 x 64 block into its own rows of the just-consumed patch
+//   buffer and reads them back as whole 128-B rows (8 lanes per pixel): full-line 16-B stores,
+//   8 fixed channels per lane. EP 1: shifted BN statistics of the stored bf16 values; EP 2: the
+//   BN + ReLU backward sums of the data gradient (s += y', q += y' (z - mean),
+//   y' = (z sc + bi > 0) ? y : 0), both accumulated per lane over the workgroup's tiles and
+//   reduced once at the end into ONE partial row per workgroup (fixed order: deterministic),
+//   folded by conv1x1.hip's finalize kernels.
+//   Pipeline: once every wave has read its image back (the tile's third barrier), the patch of
+//   tile j + 2 is DMA'd into that buffer, so each patch has a whole tile (MFMAs + epilogue) to
+//   land; a counted vmcnt (the 4 stores of the last epilogue + the 6 DMA instructions of the next
+//   patch stay in flight) retires exactly the current patch.
 #include <cstdlib>
 
 #include "common.h"
@@ -57,11 +60,10 @@ constexpr int kWImg = 9 * 64 * 128;        // 73728 B
 constexpr int kPImg = kPQ * 128;           // 43008 B
 constexpr int kOffP = kWImg;
 constexpr int kOffZ = kOffP + 2 * kPImg;   // 159744
-constexpr int kOffC = kOffZ + 128;         // shift / mean, sc, bi: 3 x 64 floats
-constexpr int kLds = kOffC + 3 * 64 * 4;   // 160640
+constexpr int kLds = kOffZ + 128;          // 159872
 constexpr int kPS = kPQ / 8 / kNW;         // 6 patch DMA instructions per wave
 constexpr int kWI = 9 * 64 / 8;            // 72 weight DMA instructions
-constexpr int kStores = 8;                 // epilogue stores per lane per tile
+constexpr int kStores = 4;                 // epilogue stores per lane per tile (16 B each)
 static_assert(kPS * 8 * kNW == kPQ, "patch rows split evenly over the waves");
 static_assert(kLds <= 163840, "LDS budget");
 
@@ -76,6 +78,7 @@ struct P3Args {
   const float* ep_sc;     // EP 2: that BN's affine (ReLU bit: z sc + bi > 0)
   const float* ep_bi;
   int H, tpi, tiles;      // image height, tiles per image (H / 4), tiles
+  int dbg;                // bench/conv3x3p.py only: 1 skip the MFMAs, 2 skip the per-tile patch DMA
 };
 
 __device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
@@ -90,12 +93,12 @@ __device__ __forceinline__ void bar() {
 
 // s_waitcnt vmcnt(n) for the four counts the loop uses (n is wave-uniform)
 __device__ __forceinline__ void wait_vm(int n) {
-  if (n >= kPS + kStores) asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
-  else if (n >= kStores) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  if (n >= kPS + kStores) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
   else if (n >= kPS) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n >= kStores) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
-static_assert(kPS == 6 && kStores == 8, "wait_vm's immediates");
+static_assert(kPS == 6 && kStores == 4, "wait_vm's immediates");
 
 template <int EP>
 __global__ __launch_bounds__(kThr, 1) __attribute__((amdgpu_waves_per_eu(1, 2))) void conv3x3p_kernel(
@@ -107,16 +110,17 @@ __global__ __launch_bounds__(kThr, 1) __attribute__((amdgpu_waves_per_eu(1, 2)))
   const int t0 = static_cast<int>(static_cast<int64_t>(a.tiles) * b / G);
   const int nloc = static_cast<int>(static_cast<int64_t>(a.tiles) * (b + 1) / G) - t0;
   const int lrow = lane >> 3, lp = lane & 7;
-  float* cf = reinterpret_cast<float*>(smem + kOffC);
 
-  // zero row and epilogue coefficients (plain loads: before any DMA is in flight)
+  // zero row; this lane's 8 epilogue channels' coefficients (plain loads: before any DMA is in
+  // flight)
   if (tid < 8) *reinterpret_cast<uint4*>(smem + kOffZ + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
-  if (EP >= 1 && tid < 64) {
-    cf[tid] = a.shift ? a.shift[tid] : 0.f;
-    if (EP == 2) {
-      cf[64 + tid] = a.ep_sc[tid];
-      cf[128 + tid] = a.ep_bi[tid];
-    }
+  const int c8 = lane & 7;   // epilogue: 16-B chunk (channels 8 c8 .. 8 c8 + 7) of a pixel row
+  float sh[8], esc[8], ebi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sh[e] = EP >= 1 && a.shift ? a.shift[8 * c8 + e] : 0.f;
+    esc[e] = EP == 2 ? a.ep_sc[8 * c8 + e] : 0.f;
+    ebi[e] = EP == 2 ? a.ep_bi[8 * c8 + e] : 0.f;
   }
 
   // weight image: row tap 64 + n = w[n][tap 64 .. tap 64 + 63]
@@ -168,9 +172,9 @@ __global__ __launch_bounds__(kThr, 1) __attribute__((amdgpu_waves_per_eu(1, 2)))
     xo[tap] = ok ? kOffP + q * 128 + 16 * (h ^ ((q >> 1) & 7)) : -1;
   }
 
-  float cs[32], cq[32];
+  float cs[8], cq[8];
 #pragma unroll
-  for (int e = 0; e < 32; ++e) {
+  for (int e = 0; e < 8; ++e) {
     cs[e] = 0.f;
     cq[e] = 0.f;
   }
@@ -180,16 +184,17 @@ __global__ __launch_bounds__(kThr, 1) __attribute__((amdgpu_waves_per_eu(1, 2)))
 
   for (int j = 0; j < nloc; ++j) {
     const int t = t0 + j, buf = j & 1;
-    // retire patch j: younger are the last epilogue's stores and patch j + 1
+    // retire patch j: younger are the last epilogue's stores and patch j + 1 (issued after them)
     wait_vm((j > 0 ? kStores : 0) + (j + 1 < nloc ? kPS : 0));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
-    const int64_t m = static_cast<int64_t>(t) * kTP + f;
-    uint2 zr[EP == 2 ? 8 : 1];
+    // epilogue rows of this lane: tile pixels 32 wave + 8 k + lrow, chunk c8
+    const int64_t mrow = static_cast<int64_t>(t) * kTP + 32 * wave + lrow;
+    uint4 zr[EP == 2 ? 4 : 1];
     if constexpr (EP == 2) {   // the BN input at this lane's outputs (latency under the MFMAs)
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        zr[e] = *reinterpret_cast<const uint2*>(a.sz + m * 64 + 32 * (e >> 2) + 8 * (e & 3) + 4 * h);
+      for (int k = 0; k < 4; ++k)
+        zr[k] = *reinterpret_cast<const uint4*>(a.sz + (mrow + 8 * k) * 64 + 8 * c8);
     }
     f32x16 acc[2];
 #pragma unroll
@@ -211,6 +216,7 @@ __global__ __launch_bounds__(kThr, 1) __attribute__((amdgpu_waves_per_eu(1, 2)))
       d[1] = *reinterpret_cast<const bf16x8_t*>(smem + tap * 8192 + (wl ^ (32 * kk)));
       d[2] = *reinterpret_cast<const bf16x8_t*>(smem + tap * 8192 + 4096 + (wl ^ (32 * kk)));
     };
+    if (!(a.dbg & 1)) {
     rd(0, fr[0]);
     rd(1, fr[1]);
 #pragma unroll
@@ -221,57 +227,70 @@ __global__ __launch_bounds__(kThr, 1) __attribute__((amdgpu_waves_per_eu(1, 2)))
       acc[1] = mfma32(fr[s % 3][2], fr[s % 3][0], acc[1]);
       __builtin_amdgcn_sched_barrier(0);
     }
+    }
     bar();   // every wave is done with this buffer
 
-    if (EP != 2 && j + 2 < nloc) stage(t + 2, buf);
-    uint16_t* yp = a.y + m * 64 + 4 * h;
-    int cofs = kOffC;   // opaque to the compiler: the coefficient reads stay in the loop
-    asm volatile("" : "+v"(cofs));
-    const float* cfl = reinterpret_cast<const float*>(smem + cofs);
+    // epilogue: the wave's 32 pixels x 64 channels as a bf16 image in its own 32 rows of the
+    // consumed buffer (same swizzle), read back as whole 128-B rows (8 lanes per pixel): full-line
+    // 16-B stores, 8 fixed channels per lane for the statistics
+    char* img = smem + kOffP + pb;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int e = 4 * i + g, n = 32 * i + 8 * g + 4 * h;
         const uint32_t lo = pk_bf16(acc[i][4 * g], acc[i][4 * g + 1]);
         const uint32_t hi = pk_bf16(acc[i][4 * g + 2], acc[i][4 * g + 3]);
-        *reinterpret_cast<uint2*>(yp + 32 * i + 8 * g) = make_uint2(lo, hi);
-        const float v[4] = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
-                            __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
-        if constexpr (EP == 1) {
-          const float4 sh = *reinterpret_cast<const float4*>(cfl + n);
-          const float d[4] = {v[0] - sh.x, v[1] - sh.y, v[2] - sh.z, v[3] - sh.w};
+        const int row = 32 * wave + r32, ch = 4 * i + g;
+        *reinterpret_cast<uint2*>(img + row * 128 + 16 * (ch ^ ((row >> 1) & 7)) + 8 * h) =
+            make_uint2(lo, hi);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            cs[4 * e + r] += d[r];
-            cq[4 * e + r] = fmaf(d[r], d[r], cq[4 * e + r]);
-          }
-        } else if constexpr (EP == 2) {
-          const float4 mu = *reinterpret_cast<const float4*>(cfl + n);
-          const float4 sc = *reinterpret_cast<const float4*>(cfl + 64 + n);
-          const float4 bi = *reinterpret_cast<const float4*>(cfl + 128 + n);
-          const float zv[4] = {__uint_as_float(zr[e].x << 16), __uint_as_float(zr[e].x & 0xffff0000u),
-                               __uint_as_float(zr[e].y << 16), __uint_as_float(zr[e].y & 0xffff0000u)};
-          const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, scv[4] = {sc.x, sc.y, sc.z, sc.w},
-                      biv[4] = {bi.x, bi.y, bi.z, bi.w};
+    for (int k = 0; k < 4; ++k) {
+      const int row = 32 * wave + 8 * k + lrow;
+      const uint4 v = *reinterpret_cast<const uint4*>(img + row * 128 + 16 * (c8 ^ ((row >> 1) & 7)));
+      *reinterpret_cast<uint4*>(a.y + (mrow + 8 * k) * 64 + 8 * c8) = v;
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      if constexpr (EP == 1) {   // shifted sums of the stored bf16 values
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float yv = fmaf(zv[r], scv[r], biv[r]) > 0.f ? v[r] : 0.f;
-            cs[4 * e + r] += yv;
-            cq[4 * e + r] = fmaf(yv, zv[r] - muv[r], cq[4 * e + r]);
-          }
+        for (int q = 0; q < 4; ++q) {
+          const float lo = __uint_as_float(w4[q] << 16) - sh[2 * q];
+          const float hi = __uint_as_float(w4[q] & 0xffff0000u) - sh[2 * q + 1];
+          cs[2 * q] += lo;
+          cs[2 * q + 1] += hi;
+          cq[2 * q] = fmaf(lo, lo, cq[2 * q]);
+          cq[2 * q + 1] = fmaf(hi, hi, cq[2 * q + 1]);
+        }
+      } else if constexpr (EP == 2) {   // y' = relu'(z sc + bi) y; s += y', q += y' (z - mean)
+        const uint32_t z4[4] = {zr[k].x, zr[k].y, zr[k].z, zr[k].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float zlo = __uint_as_float(z4[q] << 16), zhi = __uint_as_float(z4[q] & 0xffff0000u);
+          const float lo = fmaf(zlo, esc[2 * q], ebi[2 * q]) > 0.f ? __uint_as_float(w4[q] << 16) : 0.f;
+          const float hi = fmaf(zhi, esc[2 * q + 1], ebi[2 * q + 1]) > 0.f
+                               ? __uint_as_float(w4[q] & 0xffff0000u) : 0.f;
+          cs[2 * q] += lo;
+          cs[2 * q + 1] += hi;
+          cq[2 * q] = fmaf(lo, zlo - sh[2 * q], cq[2 * q]);
+          cq[2 * q + 1] = fmaf(hi, zhi - sh[2 * q + 1], cq[2 * q + 1]);
         }
       }
-    if (EP == 2 && j + 2 < nloc) stage(t + 2, buf);
+    }
+    if (j + 2 < nloc && !(a.dbg & 2)) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bar();   // every wave's image reads are done: the buffer takes patch j + 2
+      stage(t + 2, buf);
+    }
   }
 
   if constexpr (EP >= 1) {
-    // lanes with equal h hold the same 32 channels: fixed-order xor tree over r32
+    // lanes with equal c8 hold the same 8 channels: fixed-order xor tree over lane >> 3
 #pragma unroll
-    for (int e = 0; e < 32; ++e) {
+    for (int e = 0; e < 8; ++e) {
       float s1 = cs[e], s2 = cq[e];
 #pragma unroll
-      for (int k = 1; k < 32; k <<= 1) {
+      for (int k = 8; k < 64; k <<= 1) {
         s1 += __shfl_xor(s1, k, 64);
         s2 += __shfl_xor(s2, k, 64);
       }
@@ -281,15 +300,12 @@ __global__ __launch_bounds__(kThr, 1) __attribute__((amdgpu_waves_per_eu(1, 2)))
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
     float* red = reinterpret_cast<float*>(smem + kOffP);   // [wave][2][64] over the dead patches
-    if (r32 == 0) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int n = 32 * (e >> 2) + 8 * (e & 3) + 4 * h;
-        *reinterpret_cast<float4*>(red + wave * 128 + n) =
-            make_float4(cs[4 * e], cs[4 * e + 1], cs[4 * e + 2], cs[4 * e + 3]);
-        *reinterpret_cast<float4*>(red + wave * 128 + 64 + n) =
-            make_float4(cq[4 * e], cq[4 * e + 1], cq[4 * e + 2], cq[4 * e + 3]);
-      }
+    if (lane < 8) {
+      float* rp = red + wave * 128 + 8 * c8;
+      reinterpret_cast<float4*>(rp)[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
+      reinterpret_cast<float4*>(rp)[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
+      reinterpret_cast<float4*>(rp + 64)[0] = make_float4(cq[0], cq[1], cq[2], cq[3]);
+      reinterpret_cast<float4*>(rp + 64)[1] = make_float4(cq[4], cq[5], cq[6], cq[7]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
@@ -349,6 +365,11 @@ hipError_t launch_conv3x3p(const void* x, const void* w, void* y, const void* ze
   a.H = H;
   a.tpi = H / kTR;
   a.tiles = Nimg * a.tpi;
+  static const int dbg = [] {
+    const char* d = getenv("CML_CONV3P_DBG");
+    return d ? atoi(d) : 0;
+  }();
+  a.dbg = dbg;
   const int G = a.tiles < num_cus() ? a.tiles : num_cus();
   if (rows) *rows = G;
 #define CML_P3(E)                                                                              \
