@@ -85,6 +85,13 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// one 16-B LDS read; the caller waits for it (s_waitcnt lgkmcnt) before using the value
+__device__ __forceinline__ bf16x8_t lds_rd(int addr) {
+  bf16x8_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
 __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -209,12 +216,14 @@ __global__ __launch_bounds__(kThr, 1) __attribute__((amdgpu_waves_per_eu(1, 2)))
     for (int tap = 0; tap < 9; ++tap) xb[tap] = xo[tap] >= 0 ? xo[tap] + pb : kOffZ + 16 * h;
     // (sched_barriers pin the order: the reads of step s + 2 are issued before the MFMAs of step
     // s, so each MFMA pair waits only for reads two steps old)
+    // The reads are inline asm with explicit counted lgkmcnt waits: the compiler's own waits for
+    // this loop were lgkmcnt(0) every third step (draining the reads it had just issued).
     bf16x8_t fr[3][3];
     auto rd = [&](int s, bf16x8_t (&d)[3]) {
       const int tap = s >> 2, kk = s & 3;
-      d[0] = *reinterpret_cast<const bf16x8_t*>(smem + (xb[tap] ^ (32 * kk)));
-      d[1] = *reinterpret_cast<const bf16x8_t*>(smem + tap * 8192 + (wl ^ (32 * kk)));
-      d[2] = *reinterpret_cast<const bf16x8_t*>(smem + tap * 8192 + 4096 + (wl ^ (32 * kk)));
+      d[0] = lds_rd(xb[tap] ^ (32 * kk));
+      d[1] = lds_rd(tap * 8192 + (wl ^ (32 * kk)));
+      d[2] = lds_rd(tap * 8192 + 4096 + (wl ^ (32 * kk)));
     };
     if (!(a.dbg & 1)) {
     rd(0, fr[0]);
@@ -222,6 +231,10 @@ __global__ __launch_bounds__(kThr, 1) __attribute__((amdgpu_waves_per_eu(1, 2)))
 #pragma unroll
     for (int s = 0; s < 36; ++s) {
       if (s + 2 < 36) rd(s + 2, fr[(s + 2) % 3]);
+      // step s's reads retired; steps s + 1, s + 2 (3 reads each) may stay in flight
+      if (s + 2 < 36) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+      else if (s + 1 < 36) asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       acc[0] = mfma32(fr[s % 3][1], fr[s % 3][0], acc[0]);
       acc[1] = mfma32(fr[s % 3][2], fr[s % 3][0], acc[1]);
