@@ -729,13 +729,8 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
 
 
 def _wgrad3x3_s2(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """Weight gradient of a stride-2 / padding-1 3x3 conv: ``wgrad3x3s2.hip`` (nine taps per
-    workgroup from the raw input rows) for even inputs, else MIOpen."""
-    N, Co, Ho, Wo = dy.shape
-    Ci = x.shape[1]
-    if (_P().own_wgrad3x3_s2 and x.shape[2] == 2 * Ho and x.shape[3] == 2 * Wo
-            and lib().wgrad3x3_s2_ok(N, Ho, Wo, Co, Ci)):
-        return lib().wgrad3x3_s2(dy, x, w.dtype, _zero_row(dy.device))
+    """Weight gradient of a stride-2 / padding-1 3x3 conv (MIOpen; an own nine-tap kernel over the
+    raw input rows measured 1.1-1.45x slower, docs/PERFORMANCE.md "Round 4")."""
     return torch.ops.aten.convolution_backward(
         dy, x, w, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
 

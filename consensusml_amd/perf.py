@@ -75,8 +75,6 @@ class PerfPolicy:
     own_wgrad3x3: bool = True             # wgrad3x3.hip weight gradient
     own_conv3x3_s2: bool = True           # stride-2 3x3: conv_gemm forward + BN stats, parity-class
                                           # data gradient (+ bn1 backward sums)
-    own_wgrad3x3_s2: bool = True          # stride-2 3x3 weight gradient on wgrad3x3s2.hip (MIOpen
-                                          # igemm_wrw before)
     # ---------------------------------------------------------------- transformers / engine
     attn_kernel: bool = True              # MFMA attention for short sequences (BERT)
     multi_copy: bool = True               # multi-tensor HIP copy for gradient capture
@@ -126,7 +124,6 @@ class PerfPolicy:
             bn1_sums_lib_conv1=_env_bool("CML_BN1_SUMS_LIB_CONV1", False),
             own_wgrad3x3=_env_bool("CML_WGRAD3X3", True),
             own_conv3x3_s2=_env_bool("CML_CONV3X3_S2", True),
-            own_wgrad3x3_s2=_env_bool("CML_WGRAD3X3_S2", True),
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),
             multi_copy=_env_bool("CML_MULTI_COPY", True),
             batched_workers=_env_bool("CML_BATCHED_WORKERS", True),

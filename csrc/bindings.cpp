@@ -1207,41 +1207,6 @@ Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
   return dw.permute({0, 3, 1, 2});
 }
 
-// Weight gradient of a 3x3 / stride 2 / padding 1 conv with an even input (wgrad3x3s2.hip):
-// dy [N, Co, Ho, Wo], x [N, Ci, 2 Ho, 2 Wo], both NHWC bf16 -> dW [Co, Ci, 3, 3] (channels_last).
-Tensor wgrad3x3_s2(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
-                   const optional<Tensor>& zero_in) {
-  check_nhwc(x, "x");
-  Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
-  check_nhwc(dy, "dy");
-  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(0) == x.size(0) &&
-                  x.size(2) == 2 * dy.size(2) && x.size(3) == 2 * dy.size(3),
-              "wgrad3x3_s2: x must be [N, Ci, 2 Ho, 2 Wo] for dy [N, Co, Ho, Wo]");
-  TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "wgrad3x3_s2: bf16 or fp32 output");
-  const int64_t N = x.size(0), Ci = x.size(1), Ho = dy.size(2), Wo = dy.size(3), Co = dy.size(1);
-  const c10::DeviceGuard guard(x.device());
-  int S = 1;
-  TORCH_CHECK(cml::wgrad3x3_s2_plan(static_cast<int>(N), static_cast<int>(Ho), static_cast<int>(Wo),
-                                    static_cast<int>(Co), static_cast<int>(Ci), &S),
-              "wgrad3x3_s2: no plan for this shape (check wgrad3x3_s2_ok first)");
-  Tensor zero;
-  if (zero_in.has_value() && zero_in->defined()) {
-    zero = *zero_in;
-    TORCH_CHECK(zero.is_cuda() && zero.device() == x.device() && zero.scalar_type() == at::kBFloat16 &&
-                    zero.is_contiguous() && zero.numel() >= 8, "wgrad3x3_s2: zero must be >= 8 bf16");
-  } else {
-    zero = at::zeros({64}, x.options());
-  }
-  Tensor part = at::empty({S, Co, 9, Ci}, x.options().dtype(at::kFloat));
-  Tensor dw = at::empty({Co, 3, 3, Ci}, x.options().dtype(dtype));
-  CML_CHECK_HIP(cml::launch_wgrad3x3_s2(dy.data_ptr(), x.data_ptr(), zero.data_ptr(),
-                                        part.data_ptr<float>(), dw.data_ptr(),
-                                        dtype == at::kBFloat16, static_cast<int>(N),
-                                        static_cast<int>(Ho), static_cast<int>(Wo),
-                                        static_cast<int>(Co), static_cast<int>(Ci), cur_stream()));
-  return dw.permute({0, 3, 1, 2});
-}
-
 // Implicit-GEMM conv (conv_gemm.hip): x [N, C, H, W] NHWC bf16, w [Cout, taps * C] contiguous
 // bf16 (k = tap C + c), taps 1 or 9 (3x3, padding 1) -> y [N, Cout, H, W] NHWC.
 // Stride-1 conv_gemm whose output is the gradient of relu(bn(z)) (z [N, Cout, H, W] NHWC bf16, sc /
@@ -2155,15 +2120,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("zero") = py::none(),
         "weight gradient of a 3x3 stride-1 conv (MFMA, split-K, all nine taps per workgroup: "
         "wgrad3x3.hip) for shapes with wgrad3x3_direct_ok");
-  m.def("wgrad3x3_s2", &wgrad3x3_s2, py::arg("dy"), py::arg("x"), py::arg("dtype"),
-        py::arg("zero") = py::none(),
-        "weight gradient of a 3x3 stride-2 conv with an even input (MFMA, split-K, nine taps per "
-        "workgroup from the raw input rows: wgrad3x3s2.hip) for shapes with wgrad3x3_s2_ok");
-  m.def("wgrad3x3_s2_ok", [](int64_t B, int64_t Ho, int64_t Wo, int64_t Co, int64_t Ci) {
-    int S;
-    return cml::wgrad3x3_s2_plan(static_cast<int>(B), static_cast<int>(Ho), static_cast<int>(Wo),
-                                 static_cast<int>(Co), static_cast<int>(Ci), &S);
-  }, "whether wgrad3x3_s2 has a plan for this shape (CML_WGRAD3X3_S2=0 disables it)");
   m.def("conv1x1_link_s2", &conv1x1_link_s2,
         "1x1 data gradient + a stride-2 conv's compact data gradient at the even pixels");
   m.def("subsample2", &subsample2, "x[:, :, ::2, ::2] of an NHWC bf16 tensor, dense NHWC");

@@ -342,10 +342,6 @@ hipError_t launch_wgrad_fold(const float* part, int S, int64_t n, void* out, boo
 // dw [Co][3][3][Ci] (bf16 or fp32). Co % 64 == 0, Ci == 64 or Ci % 128 == 0; the plan also needs a
 // chunk geometry that fits LDS (false: the library's weight gradient).
 bool wgrad3x3_direct_plan(int B, int H, int W, int Co, int Ci, int* splits, int* tci);
-// 3x3 / stride 2 / padding 1 weight gradient, even input (wgrad3x3s2.hip): partials [splits][Co][9][Ci]
-bool wgrad3x3_s2_plan(int B, int Ho, int Wo, int Co, int Ci, int* splits);
-hipError_t launch_wgrad3x3_s2(const void* dy, const void* x, const void* zero, float* part, void* dw,
-                              bool dw_bf16, int B, int Ho, int Wo, int Co, int Ci, hipStream_t st);
 hipError_t launch_wgrad3x3_direct(const void* dy, const void* x, const void* zero, float* part,
                                   void* dw, bool dw_bf16, int B, int H, int W, int Co, int Ci,
                                   hipStream_t st);
