@@ -414,6 +414,8 @@ def main():
                              if torch.cuda.is_available() else None),
             # every kernel / fusion switch in force (consensusml_amd.perf.PerfPolicy)
             "perf_policy": perf.policy().to_dict(),
+            # CML_* overrides of the native launchers' switches (CML_CONV3P, CML_CONV_GEMM2, ...)
+            "env_switches": perf.env_switches(),
         }
         if info.distributed:
             out["dist_backend"] = main_res["dist_backend"]

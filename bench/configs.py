@@ -143,7 +143,7 @@ def main():
            "batched_workers": bool(n > info.world and tr.task.batched_workers
                                    and perf.policy().batched_workers
                                    and info.device.type == "cuda" and cfg.dtype == "bf16"),
-           "perf_policy": perf.policy().to_dict()}
+           "perf_policy": perf.policy().to_dict(), "env_switches": perf.env_switches()}
     if info.device.type == "cuda":
         out["max_mem_gb"] = round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)
     out["loopback"] = info.loopback

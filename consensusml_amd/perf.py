@@ -164,6 +164,14 @@ _CURRENT = PerfPolicy.from_env().validate()
 _NATIVE_SYNCED = None
 
 
+def env_switches() -> Dict[str, str]:
+    """The ``CML_*`` variables set in this process (the policy's overrides and the native
+    launchers' A/B switches such as CML_CONV3P / CML_CONV_GEMM2, which the policy does not hold),
+    recorded beside the policy in benchmark lines; the bench launcher's own are left out."""
+    return {k: v for k, v in sorted(os.environ.items())
+            if k.startswith("CML_") and not k.startswith("CML_BENCH_")}
+
+
 def policy() -> PerfPolicy:
     """The policy in force (read by the models at call time)."""
     return _CURRENT

@@ -42,3 +42,12 @@ def test_use_policy_is_scoped():
 def test_validate_rejects_unknown_modes(kw):
     with pytest.raises(ValueError):
         perf.PerfPolicy().replace(**kw).validate()
+
+
+def test_env_switches_recorded(monkeypatch):
+    from consensusml_amd import perf
+    monkeypatch.setenv("CML_CONV3P", "0")
+    monkeypatch.setenv("CML_BENCH_SELF_LAUNCHED", "1")
+    sw = perf.env_switches()
+    assert sw.get("CML_CONV3P") == "0"
+    assert "CML_BENCH_SELF_LAUNCHED" not in sw
