@@ -1448,9 +1448,15 @@ std::vector<int64_t> multi_copy(const std::vector<Tensor>& dsts, const std::vect
   for (size_t i = 0; i < dsts.size(); ++i) {
     const Tensor& d = dsts[i];
     const Tensor& s = srcs[i];
+    // both contiguous, or both dense with identical sizes and strides (channels_last conv
+    // weights and their gradients): either way the bytes are in the same order, starting at
+    // data_ptr (positive strides)
+    const bool same_dense = d.sizes() == s.sizes() && d.strides() == s.strides() &&
+                            d.is_non_overlapping_and_dense();
     const bool ok = d.is_cuda() && s.is_cuda() && d.device() == s.device() &&
                     d.scalar_type() == s.scalar_type() && d.numel() == s.numel() &&
-                    d.is_contiguous() && s.is_contiguous() && d.element_size() % 2 == 0 &&
+                    ((d.is_contiguous() && s.is_contiguous()) || same_dense) &&
+                    d.element_size() % 2 == 0 &&
                     (reinterpret_cast<uintptr_t>(d.data_ptr()) & 15) == 0 &&
                     (reinterpret_cast<uintptr_t>(s.data_ptr()) & 15) == 0;
     if (!ok) {

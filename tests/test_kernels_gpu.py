@@ -283,3 +283,20 @@ def test_multi_copy(cuda, dtype):
     torch.cuda.synchronize()
     for d, s in zip(dst, src):
         assert torch.equal(d, s)
+
+
+def test_multi_copy_channels_last(cuda):
+    """Same-strided dense 4-D tensors (channels_last conv weights and their gradients) go through
+    the byte copy; a contiguous destination for a channels_last source stays with the caller."""
+    from consensusml_amd.ops.native import lib
+    torch.manual_seed(1)
+    cl = torch.channels_last
+    src = [torch.randn(64, 32, 3, 3, device=cuda).bfloat16().contiguous(memory_format=cl),
+           torch.randn(128, 64, 3, 3, device=cuda).bfloat16().contiguous(memory_format=cl)]
+    dst = [torch.zeros_like(t, memory_format=cl) for t in src]
+    mixed = torch.zeros(64, 32, 3, 3, device=cuda, dtype=torch.bfloat16)   # contiguous
+    rest = lib().multi_copy(dst + [mixed], src + [src[0]])
+    assert rest == [2]
+    torch.cuda.synchronize()
+    for d, s in zip(dst, src):
+        assert torch.equal(d, s)
