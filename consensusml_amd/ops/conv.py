@@ -254,6 +254,15 @@ def _affine(gamma: torch.Tensor, beta: torch.Tensor, mean: torch.Tensor, invstd:
     return ab[0], ab[1]
 
 
+def _stats_gram_affine(L, gram, cy, w, M, rmean, rvar, eps, momentum, gamma, beta):
+    """``bn_stats_gram`` -> (mean, invstd, sc, bi): the affine from the finalize launch itself
+    (bit-identical to ``_affine``) when PerfPolicy.bn_affine_kernel is on, else ``_affine``."""
+    if _P().bn_affine_kernel:
+        m, i, sc, bi = L.bn_stats_gram(gram, cy, w, M, rmean, rvar, eps, momentum, gamma, beta)
+        return m, i, sc, bi
+    m, i = L.bn_stats_gram(gram, cy, w, M, rmean, rvar, eps, momentum)
+    return (m, i) + _affine(gamma, beta, m, i)
+
 
 _CONST = {}
 
@@ -333,13 +342,14 @@ class _RecomputeTailFn(torch.autograd.Function):
         L = lib()
         gram = cy = None
         if _P().gram_stats:
-            # bn3's statistics from y2's Gram matrix (also the backward's), not a conv pass
+            # bn3's statistics from y2's Gram matrix (also the backward's), not a conv pass; bn3's
+            # affine from the same finalize launch
             gram, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
-            m3, i3 = L.bn_stats_gram(gram, cy, wc, z.numel() // z.shape[1], rmean3, rvar3, eps,
-                                     momentum)
+            m3, i3, sc3, bi3 = _stats_gram_affine(L, gram, cy, wc, z.numel() // z.shape[1], rmean3,
+                                                  rvar3, eps, momentum, g3, b3)
         else:
             m3, i3 = L.conv1x1_bn_stats_only(z, wc, sc, bi, rmean3, rmean3, rvar3, eps, momentum)
-        sc3, bi3 = _affine(g3, b3, m3, i3)
+            sc3, bi3 = _affine(g3, b3, m3, i3)
         y, mask = L.conv1x1_bnres(z, wc, sc, bi, sc3, bi3, res)
         ctx.gram = (gram, cy)
         ctx.save_for_backward(z, g2, b2, mean2, invstd2, w, sc, bi, mask, g3, m3, i3)
@@ -409,16 +419,18 @@ class _RecomputeDownTailFn(torch.autograd.Function):
             M_ = z.numel() // z.shape[1]
             gram3, cy = L.wgrad1x1_ex(z, z, sc, bi, 3, None, sc, bi, None, True)
             gramd, cx = L.wgrad1x1_ex(x, x, None, None, 0, None, None, None, None, True)
-            m3, i3 = L.bn_stats_gram(gram3, cy, w3c, M_, rm3, rv3, eps, momentum)
-            md, idd = L.bn_stats_gram(gramd, cx, wdc, M_, rmd, rvd, eps, momentum)
+            m3, i3, sc3, bi3 = _stats_gram_affine(L, gram3, cy, w3c, M_, rm3, rv3, eps, momentum,
+                                                  g3, b3)
+            md, idd, scd, bid = _stats_gram_affine(L, gramd, cx, wdc, M_, rmd, rvd, eps, momentum,
+                                                   gd, bd)
             grams = (gram3, cy, gramd, cx)
         else:
             m3, i3 = L.conv1x1_bn_stats_only(z, w3c, sc, bi, rm3, rm3, rv3, eps, momentum)
             md, idd = L.conv1x1_bn_stats_only(x, wdc, None, None, rmd, rmd, rvd, eps, momentum)
+            sc3, bi3 = _affine(g3, b3, m3, i3)
+            scd, bid = _affine(gd, bd, md, idd)
         ctx.grams = grams
         Co, P_, Cin = w3.shape[0], w3.shape[1], wd.shape[1]
-        sc3, bi3 = _affine(g3, b3, m3, i3)
-        scd, bid = _affine(gd, bd, md, idd)
         bias = bi3 + bid
         w_cat = torch.cat([w3c.view(Co, P_).float() * sc3[:, None],
                            wdc.view(Co, Cin).float() * scd[:, None]], 1).to(torch.bfloat16)

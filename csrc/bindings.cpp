@@ -800,7 +800,8 @@ std::vector<Tensor> conv1x1_link(const Tensor& x, const Tensor& w, const Tensor&
 // -> {mean, invstd}; running stats updated in place when given.
 std::vector<Tensor> bn_stats_gram(const Tensor& G, const Tensor& cy, const Tensor& w, int64_t M,
                                   const optional<Tensor>& rmean, const optional<Tensor>& rvar,
-                                  double eps, double momentum) {
+                                  double eps, double momentum, const optional<Tensor>& gamma,
+                                  const optional<Tensor>& beta) {
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() > 0,
               "bn_stats_gram: contiguous bf16 weights");
   const int64_t Co = w.size(0), P = w.numel() / Co;
@@ -813,13 +814,22 @@ std::vector<Tensor> bn_stats_gram(const Tensor& G, const Tensor& cy, const Tenso
   TORCH_CHECK(P % 64 == 0, "bn_stats_gram: P must be a multiple of 64");
   Tensor mean = at::empty({Co}, f32), invstd = at::empty({Co}, f32);
   Tensor part = at::empty({P / 64, Co}, w.options().dtype(at::kDouble));
+  // gamma / beta given: also the BN affine (sc, bi) of these statistics (bn_affine, no launch)
+  const bool aff = gamma.has_value() && gamma->defined();
+  const void* gp = aff ? opt_ptr<const void>(gamma, at::kBFloat16, "gamma", Co) : nullptr;
+  const void* bp = aff ? opt_ptr<const void>(beta, at::kBFloat16, "beta", Co) : nullptr;
+  TORCH_CHECK(!aff || bp, "bn_stats_gram: beta with gamma");
+  Tensor sc = aff ? at::empty({Co}, f32) : Tensor(), bi = aff ? at::empty({Co}, f32) : Tensor();
   CML_CHECK_HIP(cml::launch_bn_stats_gram(G.data_ptr<float>(), cp, w.data_ptr(), static_cast<int>(P),
                                           static_cast<int>(Co), M, static_cast<float>(eps),
                                           static_cast<float>(momentum), mean.data_ptr<float>(),
                                           invstd.data_ptr<float>(),
                                           opt_ptr<float>(rmean, at::kFloat, "running_mean", Co),
                                           opt_ptr<float>(rvar, at::kFloat, "running_var", Co),
-                                          part.data_ptr<double>(), cur_stream()));
+                                          part.data_ptr<double>(), cur_stream(), gp, bp,
+                                          aff ? sc.data_ptr<float>() : nullptr,
+                                          aff ? bi.data_ptr<float>() : nullptr));
+  if (aff) return {mean, invstd, sc, bi};
   return {mean, invstd};
 }
 
@@ -2179,8 +2189,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "1x1 data gradient + masked residual gradient (+ the consumer BN's backward sums)");
   m.def("bn_stats_gram", &bn_stats_gram, py::arg("G"), py::arg("cy"), py::arg("w"), py::arg("M"),
         py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
-        py::arg("eps") = 1e-5, py::arg("momentum") = 0.1,
-        "BN statistics of a 1x1 conv's output from its input's Gram matrix and column sums");
+        py::arg("eps") = 1e-5, py::arg("momentum") = 0.1, py::arg("gamma") = py::none(),
+        py::arg("beta") = py::none(),
+        "BN statistics of a 1x1 conv's output from its input's Gram matrix and column sums "
+        "(+ the BN affine sc, bi when gamma / beta are given)");
   m.def("bn_bwd_coeffs", &bn_bwd_coeffs, "BN + ReLU backward coefficients from its sums");
   m.def("bn_bwd_sums", &bn_bwd_sums, "reduction half of a BN (+ ReLU) backward");
   m.def("stem_wgrad_pool", &stem_wgrad_pool, py::arg("dy"), py::arg("idx"), py::arg("dy2"),

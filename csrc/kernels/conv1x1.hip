@@ -512,7 +512,9 @@ __global__ __launch_bounds__(256) void bn_stats_gram_kernel(
 __global__ __launch_bounds__(256) void bn_stats_gram_fin_kernel(
     const double* __restrict__ part, const float* __restrict__ cy, const uint16_t* __restrict__ W,
     int P, int Co, int64_t M, float eps, float momentum, float* __restrict__ mean,
-    float* __restrict__ invstd, float* __restrict__ rmean, float* __restrict__ rvar) {
+    float* __restrict__ invstd, float* __restrict__ rmean, float* __restrict__ rvar,
+    const uint16_t* __restrict__ gamma, const uint16_t* __restrict__ beta, float* __restrict__ sc,
+    float* __restrict__ bi) {
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= Co) return;
@@ -527,8 +529,16 @@ __global__ __launch_bounds__(256) void bn_stats_gram_fin_kernel(
   const double mu = S / static_cast<double>(M);
   double var = Q / static_cast<double>(M) - mu * mu;
   if (var < 0.0) var = 0.0;
-  mean[n] = static_cast<float>(mu);
-  invstd[n] = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+  const float mf = static_cast<float>(mu), isf = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+  mean[n] = mf;
+  invstd[n] = isf;
+  if (sc) {   // the BN affine (sc, bi) as bn_affine computes it from the stored fp32 mean / invstd
+#pragma clang fp contract(off)
+    const float s = __uint_as_float(static_cast<uint32_t>(gamma[n]) << 16) * isf;
+    sc[n] = s;
+    const float ms = mf * s;
+    bi[n] = __uint_as_float(static_cast<uint32_t>(beta[n]) << 16) - ms;
+  }
   if (rmean) {
     const double unb = M > 1 ? var * static_cast<double>(M) / static_cast<double>(M - 1) : var;
     rmean[n] = static_cast<float>((1.0 - momentum) * rmean[n] + momentum * mu);
@@ -829,8 +839,10 @@ hipError_t launch_conv1x1_link_s2(const void* x, const void* w, void* y, const v
 
 hipError_t launch_bn_stats_gram(const float* G, const float* cy, const void* w, int P, int Co,
                                 int64_t M, float eps, float momentum, float* mean, float* invstd,
-                                float* rmean, float* rvar, double* part, hipStream_t st) {
+                                float* rmean, float* rvar, double* part, hipStream_t st,
+                                const void* gamma, const void* beta, float* sc, float* bi) {
   if (P < 64 || P % 64 || P > 2048 || Co < 1 || M < 1 || !part) return hipErrorInvalidValue;
+  if (sc && (!gamma || !beta || !bi)) return hipErrorInvalidValue;
   const size_t lds = static_cast<size_t>(kGramNC) * P * sizeof(float);
   if (lds > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bn_stats_gram_kernel),
@@ -838,8 +850,9 @@ hipError_t launch_bn_stats_gram(const float* G, const float* cy, const void* w, 
   const uint16_t* W = reinterpret_cast<const uint16_t*>(w);
   bn_stats_gram_kernel<<<dim3((Co + kGramNC - 1) / kGramNC, P / 64), 256, lds, st>>>(G, W, P, Co,
                                                                                      part);
-  bn_stats_gram_fin_kernel<<<(Co + 3) / 4, 256, 0, st>>>(part, cy, W, P, Co, M, eps, momentum, mean,
-                                                         invstd, rmean, rvar);
+  bn_stats_gram_fin_kernel<<<(Co + 3) / 4, 256, 0, st>>>(
+      part, cy, W, P, Co, M, eps, momentum, mean, invstd, rmean, rvar,
+      reinterpret_cast<const uint16_t*>(gamma), reinterpret_cast<const uint16_t*>(beta), sc, bi);
   return hipGetLastError();
 }
 

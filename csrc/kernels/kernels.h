@@ -466,10 +466,13 @@ hipError_t launch_conv1x1_link_s2(const void* x, const void* w, void* y, const v
                                   int Nimg, int H, int W, int K, int N, hipStream_t st);
 // BN training statistics (mean, invstd; running stats updated when given) of z = y W^T from the
 // Gram matrix G = y^T y [P][P] and column sums cy [P] of y over M rows; W [Co][P] bf16 (conv1x1.hip).
-// part: fp64 scratch [P / 64][Co]; P % 64 == 0.
+// part: fp64 scratch [P / 64][Co]; P % 64 == 0. sc != nullptr: also the BN affine
+// sc = gamma invstd, bi = beta - mean sc (gamma / beta bf16 [Co]) bit-identical to launch_bn_affine.
 hipError_t launch_bn_stats_gram(const float* G, const float* cy, const void* w, int P, int Co,
                                 int64_t M, float eps, float momentum, float* mean, float* invstd,
-                                float* rmean, float* rvar, double* part, hipStream_t st);
+                                float* rmean, float* rvar, double* part, hipStream_t st,
+                                const void* gamma = nullptr, const void* beta = nullptr,
+                                float* sc = nullptr, float* bi = nullptr);
 // Recompute-tail backward algebra (tail_prep.hip): from conv3's W bf16 [Co][p], P = u^T y2 and
 // s = sum u (fp32), y2's Gram / column sums and bn3's gamma (bf16) / mean / invstd: bn3's backward
 // coefficients, dgamma / dbeta (bf16 [Co]), conv3's weight gradient dW (bf16 [Co][p], skipped when

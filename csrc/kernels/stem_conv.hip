@@ -50,6 +50,7 @@ constexpr int kFT = 256;                // forward workgroup: 4 waves
 constexpr int kBT = 512;                // backward workgroup: 8 waves
 constexpr int kCh = 128;                // backward pixel chunk: 8 x 16 pixels, 8 MFMA k-steps
 constexpr int kPartW = 2 * kCo * kKP + 2 * kCo;   // floats per backward partial: G, X, s2, s1
+constexpr int kColaS = 8;               // input column sums: pixel slices (workgroups) per tap
 
 __host__ __device__ constexpr int tile_cols(int OW) { return 2 * OW + 6; }   // ix = -3 .. 2 OW + 2
 __host__ __device__ constexpr int tile_rows(int TY) { return 2 * TY + 5; }
@@ -630,8 +631,10 @@ __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __r
     const int kc = (ky * 8 + kx) * 4 + c;
     const double a = static_cast<double>(bf2f(gamma[co])) * invstd[co];
     const double s1 = gsum ? static_cast<double>(gsum[co]) : S1[co];
+    double ca = 0.0;
+    for (int sl = 0; sl < kColaS; ++sl) ca += cola[sl * kKP + kc];
     dw[e] = static_cast<float>(
-        a * (G[co * kKP + kc] - s1 / M * cola[kc] - S2[co] / M * X[co * kKP + kc]));
+        a * (G[co * kKP + kc] - s1 / M * ca - S2[co] / M * X[co * kKP + kc]));
   }
   if (e < kCo) {
     dgamma[e] = static_cast<float>(S2[e]);
@@ -643,8 +646,8 @@ __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __r
 // patch value x[n][2 oy + ky - 3][2 ox + kx - 3][c] (0 outside the image). Pass 1 sums x over
 // chunks of kColaChunk images per input pixel (grid = input rows x image chunks, a thread per
 // (column, channel), images in order, 8 loads in flight) into fp32 partials [chunk][H][W][C];
-// pass 2 (one workgroup per tap) adds, in fp64 and a fixed order, the partials of the pixels that
-// tap (ky, kx) reaches: rows ky - 3 + 2 oy and columns kx - 3 + 2 ox inside the image.
+// pass 2 (kColaS workgroups per tap) adds, in fp64 and a fixed order, the partials of the pixels
+// that tap (ky, kx) reaches: rows ky - 3 + 2 oy and columns kx - 3 + 2 ox inside the image.
 constexpr int kColaChunk = 128;   // images per partial
 // V: 16-B loads (W C a multiple of 8): thread = 8 consecutive (column, channel) values of the row
 // x one of 256 / (W C / 8) image slices (fixed-order LDS combine of the slices)
@@ -715,31 +718,58 @@ __global__ __launch_bounds__(256) void stem_cola_rows_kernel(const uint16_t* __r
   }
 }
 
-__global__ __launch_bounds__(256) void stem_cola_kernel(const float* __restrict__ part, int nchunk,
-                                                       int H, int W, int C, int OH, int OW,
-                                                       double* __restrict__ cola) {
-  __shared__ double red[256][4];
+// kColaS 1024-thread workgroups per tap, each over every kColaS-th block of kColaT output pixels;
+// a thread issues the kColaU chunk partials of a pixel (x C channels) as independent loads before
+// adding them (one workgroup per tap with a serial chain of dependent loads per pixel made this
+// pass latency bound: 423 us at batch 2048, profiles/r04_26/), then a fixed-order wave shuffle +
+// LDS combine into cola[slice][tap][4]; stem_wgrad_final adds the slices in order (deterministic)
+constexpr int kColaT = 1024, kColaU = 8;
+__global__ __launch_bounds__(kColaT) void stem_cola_kernel(const float* __restrict__ part, int nchunk,
+                                                          int H, int W, int C, int OH, int OW,
+                                                          double* __restrict__ cola) {
+  __shared__ double red[kColaT / 64][4];
   const int t = blockIdx.x;                 // tap ky * 8 + kx (kx = 7: the zero tap)
   const int ky = t / 8, kx = t - 8 * (t / 8);
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   if (kx < 7) {
     const int64_t plane = static_cast<int64_t>(H) * W * C;
-    for (int q = threadIdx.x; q < OH * OW; q += 256) {
+    for (int q = blockIdx.y * kColaT + threadIdx.x; q < OH * OW; q += kColaS * kColaT) {
       const int oy = q / OW, ox = q - oy * OW;
       const int iy = ky - 3 + 2 * oy, ix = kx - 3 + 2 * ox;
       if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
       const float* d = part + (static_cast<int64_t>(iy) * W + ix) * C;
-      for (int k = 0; k < nchunk; ++k)
+      int k = 0;
+      for (; k + kColaU <= nchunk; k += kColaU) {
+        float v[kColaU][4];
+#pragma unroll
+        for (int u = 0; u < kColaU; ++u)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {   // channel C..3 reads clamp to C - 1 and count 0
+            const float e = d[(k + u) * plane + (c < C ? c : C - 1)];
+            v[u][c] = c < C ? e : 0.f;
+          }
+#pragma unroll
+        for (int u = 0; u < kColaU; ++u)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[c] += v[u][c];
+      }
+      for (; k < nchunk; ++k)
         for (int c = 0; c < C; ++c) acc[c] += d[k * plane + c];
     }
   }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) red[threadIdx.x][c] = acc[c];
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[wave][c] = acc[c];
   __syncthreads();
   if (threadIdx.x < 4) {
     double s = 0.0;
-    for (int k = 0; k < 256; ++k) s += red[k][threadIdx.x];
-    cola[t * 4 + threadIdx.x] = threadIdx.x < C ? s : 0.0;
+    for (int k = 0; k < kColaT / 64; ++k) s += red[k][threadIdx.x];
+    cola[blockIdx.y * kKP + t * 4 + threadIdx.x] = threadIdx.x < C ? s : 0.0;
   }
 }
 
@@ -803,7 +833,7 @@ int stem_bwd_grid(int N, int OH, int OW, int C) {
 }
 
 size_t stem_wgrad_part_floats() { return kPartW; }
-size_t stem_wgrad_tot_doubles() { return kPartW + kKP; }   // partial totals + colA
+size_t stem_wgrad_tot_doubles() { return kPartW + kColaS * kKP; }   // partial totals + colA slices
 size_t stem_cola_work_floats(int N, int H, int W, int C) {
   return static_cast<size_t>((N + kColaChunk - 1) / kColaChunk) * H * W * C;
 }
@@ -866,7 +896,7 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
   const bool v16 = (W * C) % 8 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   if (v16) stem_cola_rows_kernel<true><<<dim3(H, nchunk), 256, 0, st>>>(xp, N, H, W, C, cola_work);
   else stem_cola_rows_kernel<false><<<dim3(H, nchunk), 256, 0, st>>>(xp, N, H, W, C, cola_work);
-  stem_cola_kernel<<<kKP / 4, 256, 0, st>>>(cola_work, nchunk, H, W, C, OH, OW, cola);
+  stem_cola_kernel<<<dim3(kKP / 4, kColaS), kColaT, 0, st>>>(cola_work, nchunk, H, W, C, OH, OW, cola);
   stem_wgrad_final_kernel<<<(kCo * C * 49 + 255) / 256, 256, 0, st>>>(
       tot, reinterpret_cast<const uint16_t*>(gamma), invstd, pidx ? nullptr : gsum, cola,
       static_cast<double>(N) * OH * OW, C, dw, dgamma, dbeta);

@@ -448,6 +448,13 @@ def test_bn_stats_gram_vs_fp64(cuda, N, K, H):
     torch.testing.assert_close(rm.double(), 0.9 * rm0.double() + 0.1 * m_ref, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(rv.double(), 0.9 * rv0.double() + 0.1 * z3.var(0, unbiased=True),
                                rtol=1e-4, atol=1e-5)
+    # with gamma / beta the same launch also returns the BN affine, bit-identical to bn_affine
+    gam = (torch.rand(Co, device=cuda, generator=g0) + 0.5).bfloat16()
+    bet = (torch.randn(Co, device=cuda, generator=g0) * 0.1).bfloat16()
+    m2, i2, sc3, bi3 = _lib().bn_stats_gram(gram, cy, w, M, None, None, 1e-5, 0.1, gam, bet)
+    assert torch.equal(m2, mean) and torch.equal(i2, invstd)
+    ab = _lib().bn_affine(gam, bet, mean, invstd)
+    assert torch.equal(sc3, ab[0]) and torch.equal(bi3, ab[1])
 
 
 @pytest.mark.parametrize("N,C,H,W", [(2, 256, 56, 56), (3, 64, 7, 9), (1, 512, 14, 14)])

@@ -178,12 +178,15 @@ def test_stem_pool_link_second_gradient(cuda):
 
 @pytest.mark.parametrize("N,C,H,W,two", [(4, 3, 64, 64, False), (3, 4, 50, 46, True),
                                          (2, 3, 224, 224, False), (2, 3, 224, 224, True),
-                                         (5, 3, 30, 62, False)])
+                                         (5, 3, 30, 62, False), (1100, 3, 16, 16, True),
+                                         (1030, 4, 18, 14, False)])
 def test_stem_wgrad_pool_gather(cuda, N, C, H, W, two):
     """stem_wgrad_pool (the pool's input gradient gathered from the pooled gradient inside the
     weight-gradient kernel, after a routed channel-sum pass) vs the two-pass path (maxpool_bwd_sum
     writes the full-resolution gradient, stem_wgrad reads it) and vs float64. 224 x 224 runs the
-    fixed-width (OW = 112) instance of the bench; (5, 3, 30, 62) has partial bands and chunks."""
+    fixed-width (OW = 112) instance of the bench; (5, 3, 30, 62) has partial bands and chunks;
+    N > 1024 runs the input column sums (stem_cola) over > 8 chunk partials (the unrolled batch
+    plus the remainder)."""
     from consensusml_amd.ops.native import lib
     torch.manual_seed(N + H + int(two))
     x = torch.randn(N, C, H, W, device=cuda).to(torch.bfloat16).contiguous(
