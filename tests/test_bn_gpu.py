@@ -324,3 +324,31 @@ def test_stem_bn_relu_maxpool_fused(cuda):
     for i, (f, u, r) in enumerate(zip(res[0], res[1], ref)):
         ef, eu = rel(f, r), rel(u, r)
         assert ef <= max(2 * eu, 0.03), (i, ef, eu)
+
+
+@pytest.mark.parametrize("N,H,W", [(3, 23, 30), (5, 112, 112), (1, 9, 9), (9, 56, 40)])
+def test_stem_maxpool_band_mapping(cuda, N, H, W):
+    """The stem's fused BN + ReLU + 3x3 / s2 max-pool forward (2 x 2 outputs per thread, a band of
+    two output rows per workgroup; odd output heights / widths, band counts that do not divide by
+    8) vs fp32 PyTorch on the same affine: every output row written."""
+    from consensusml_amd.ops.native import lib
+    torch.manual_seed(N + H)
+    C = 64
+    z = (torch.randn(N, C, H, W, device=cuda) + 0.2).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    gam = torch.empty(C, device=cuda).uniform_(-1.0, 1.5).to(torch.bfloat16)
+    bet = torch.empty(C, device=cuda).uniform_(-0.5, 0.5).to(torch.bfloat16)
+    mean = torch.randn(C, device=cuda) * 0.1
+    invstd = torch.rand(C, device=cuda) + 0.5
+    y, idx, _, _ = lib().bn_relu_maxpool_fwd(z, gam, bet, None, None, mean, invstd, 1e-5, 0.1,
+                                             False, 3, 2, 1)
+    sc = invstd * gam.float()
+    bi = bet.float() - mean * sc
+    u = z.float() * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)
+    ref = F.max_pool2d(torch.relu(u), 3, 2, 1)
+    assert y.shape == ref.shape
+    err = (y.float() - ref).abs()
+    assert float(err.max()) <= 1e-2 * float(ref.abs().max()) + 1e-3
+    # ReLU-masked windows (argmax 255) where the reference max is <= 0 (layout-free count; an
+    # affine output within rounding of 0 may land either side)
+    assert abs(int((idx == 255).sum()) - int((ref <= 0).sum())) <= max(2, ref.numel() // 10000)
