@@ -284,6 +284,18 @@ def _const(n: int, v: float, device) -> torch.Tensor:
 # did: profiles/r02_prof53_*).
 
 
+def scaled_cat(w1: torch.Tensor, s1: torch.Tensor, w2: torch.Tensor, s2: torch.Tensor):
+    """bf16 [Co, K1 + K2] = [diag(s1) w1 | diag(s2) w2] (w bf16 [Co, K], s fp32 [Co]): each product
+    in fp32, rounded once into its half of the output -- two launches, bit-identical to
+    ``torch.cat([w1.float() * s1[:, None], w2.float() * s2[:, None]], 1).to(torch.bfloat16)``
+    (six)."""
+    k1 = w1.shape[1]
+    out = torch.empty(w1.shape[0], k1 + w2.shape[1], dtype=torch.bfloat16, device=w1.device)
+    torch.mul(w1, s1[:, None], out=out[:, :k1])
+    torch.mul(w2, s2[:, None], out=out[:, k1:])
+    return out
+
+
 def fold_cat(w1: torch.Tensor, a: torch.Tensor, c: torch.Tensor, w2: torch.Tensor):
     """Weights and bias of a two-source GEMM whose first source is a BN + ReLU backward,
     a (mask ? g : 0) + c (a, c fp32 [K1]; w1 [Co, K1], w2 [Co, K2] fp32): the kernels stage only
@@ -432,11 +444,10 @@ class _RecomputeDownTailFn(torch.autograd.Function):
         ctx.grams = grams
         Co, P_, Cin = w3.shape[0], w3.shape[1], wd.shape[1]
         bias = bi3 + bid
-        w_cat = torch.cat([w3c.view(Co, P_).float() * sc3[:, None],
-                           wdc.view(Co, Cin).float() * scd[:, None]], 1).to(torch.bfloat16)
+        w_cat = scaled_cat(w3c.view(Co, P_), sc3, wdc.view(Co, Cin), scd)
         dev = z.device
         # x: the block input, a ReLU output, staged as is
-        y, mask = L.conv1x1_cat_bnres(z, x, sc, bi, None, None, w_cat.contiguous(),
+        y, mask = L.conv1x1_cat_bnres(z, x, sc, bi, None, None, w_cat,
                                       _const(Co, 1.0, dev), bias)
         ctx.save_for_backward(z, g2, b2, mean2, invstd2, w3, sc, bi, mask, g3, m3, i3, x, wd, gd,
                               md, idd)
