@@ -415,6 +415,20 @@ def _own_gemm(M: int, N: int, K: int) -> bool:
         return False
 
 
+def _linear_wgrad(gout: torch.Tensor, gin: torch.Tensor) -> torch.Tensor:
+    """dW [N, K] = gout^T gin over T token rows (gout [T, N], gin [T, K]). PerfPolicy.own_linear_wgrad:
+    on the 1x1-conv weight-gradient kernel (wgrad1x1.hip: row-major [T, C] activations are NHWC
+    [T, C, 1, 1]; split-K over the rows, fixed-order fold, bench/linear_wgrad.py), else hipBLASLt."""
+    T, N = gout.shape
+    K = gin.shape[-1]
+    if (_P().own_linear_wgrad and gout.is_cuda and gout.dtype == torch.bfloat16
+            and gin.dtype == torch.bfloat16 and N % 128 == 0 and K % 128 == 0
+            and gout.is_contiguous() and gin.is_contiguous()):
+        return lib().wgrad1x1(gout.view(T, 1, 1, N).permute(0, 3, 1, 2),
+                              gin.view(T, 1, 1, K).permute(0, 3, 1, 2), torch.bfloat16).view(N, K)
+    return gout.t() @ gin
+
+
 class _LinearFn(torch.autograd.Function):
     """y = x W^T + b with the bias gradient from the column-sum kernel (PyTorch's generic column
     reduction runs these at ~0.4 TB/s: 7 % of the BERT step in profiles/r01_prof13)."""
@@ -481,12 +495,14 @@ def _linear_grads(ctx, dy2: torch.Tensor, x: torch.Tensor, w: torch.Tensor):
         T = dy2.shape[0] // V
         if ctx.needs_input_grad[1] and wg.has(pw):
             dst, first = wg.out(pw)
-            a = dy2.view(V, T, N).transpose(1, 2)
-            bm = x.reshape(V, T, K)
-            if first:
-                torch.bmm(a, bm, out=dst.view(V, N, K))
+            if V == 1 and _P().own_linear_wgrad:
+                d = _linear_wgrad(dy2, x.reshape(T, K))
+                (dst.view(N, K).copy_ if first else dst.view(N, K).add_)(d)
+            elif first:
+                torch.bmm(dy2.view(V, T, N).transpose(1, 2), x.reshape(V, T, K),
+                          out=dst.view(V, N, K))
             else:
-                dst.view(V, N, K).baddbmm_(a, bm)
+                dst.view(V, N, K).baddbmm_(dy2.view(V, T, N).transpose(1, 2), x.reshape(V, T, K))
         if ctx.needs_input_grad[2] and pb is not None and wg.has(pb):
             dst, first = wg.out(pb)
             if parts is not None and T % 64 == 0:
@@ -502,7 +518,7 @@ def _linear_grads(ctx, dy2: torch.Tensor, x: torch.Tensor, w: torch.Tensor):
                 (dst.copy_ if first else dst.add_)(g)
         return dx, None, None
     if ctx.needs_input_grad[1]:
-        dw = dy2.t() @ x.reshape(-1, x.shape[-1])
+        dw = _linear_wgrad(dy2, x.reshape(-1, x.shape[-1]))
     if ctx.needs_input_grad[2]:
         if parts is not None:
             db = torch.empty(1, dy2.shape[-1], dtype=dy2.dtype, device=dy2.device)
@@ -652,6 +668,10 @@ class _FFNGeluFn(torch.autograd.Function):
             T = dy2.shape[0] // wg.V
             for pw, gout, gin in ((pw1, dh, x2), (pw2, dy2, a)):
                 dst, first = wg.out(pw)
+                if wg.V == 1 and _P().own_linear_wgrad:
+                    d = _linear_wgrad(gout, gin)
+                    (dst.view_as(d).copy_ if first else dst.view_as(d).add_)(d)
+                    continue
                 A = gout.view(wg.V, T, -1).transpose(1, 2)
                 Bm = gin.view(wg.V, T, -1)
                 if first:
@@ -665,9 +685,9 @@ class _FFNGeluFn(torch.autograd.Function):
                 else:
                     dst.view(wg.V, -1).add_(dy2.view(wg.V, T, -1).sum(1))
             return dx, None, None, None, None, None
-        dw1 = dh.t() @ x2 if ctx.needs_input_grad[1] else None
+        dw1 = _linear_wgrad(dh, x2) if ctx.needs_input_grad[1] else None
         db1 = cs.view(-1) if ctx.needs_input_grad[2] else None
-        dw2 = dy2.t() @ a if ctx.needs_input_grad[3] else None
+        dw2 = _linear_wgrad(dy2, a) if ctx.needs_input_grad[3] else None
         db2 = lib().colsum(dy2) if ctx.needs_input_grad[4] else None
         return dx, dw1, db1, dw2, db2, None
 

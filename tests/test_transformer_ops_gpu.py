@@ -201,3 +201,30 @@ def test_mfma_attention_matches_sdpa_path(cuda):
     with perf.use_policy(perf.policy().replace(attn_kernel=False)):
         b = T.fused_qkv_attention(qkv, 12, 64)
     torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("Tn,N,K", [(8192, 768, 768), (4096, 3072, 768), (1024, 768, 3072),
+                                    (640, 256, 128)])
+def test_linear_wgrad_on_wgrad1x1(cuda, Tn, N, K):
+    """Transformer-linear weight gradient dY^T X on the 1x1-conv weight-gradient kernel
+    (PerfPolicy.own_linear_wgrad) vs fp32, and through a linear's autograd with the policy on vs
+    off (hipBLASLt)."""
+    from consensusml_amd import perf
+    g = torch.Generator(device=cuda).manual_seed(Tn + N)
+    dy = torch.randn(Tn, N, device=cuda, generator=g).bfloat16()
+    x = torch.randn(Tn, K, device=cuda, generator=g).bfloat16()
+    ref = dy.float().t() @ x.float()
+    with perf.use_policy(perf.policy().replace(own_linear_wgrad=True)):
+        dw = T._linear_wgrad(dy, x)
+    assert dw.shape == (N, K) and dw.dtype == torch.bfloat16
+    assert float((dw.float() - ref).norm() / ref.norm()) < 5e-3
+    w = (torch.randn(N, K, device=cuda, generator=g) * K ** -0.5).bfloat16()
+    b = torch.zeros(N, device=cuda, dtype=torch.bfloat16)
+    grads = []
+    for on in (True, False):
+        wi, bi_ = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        with perf.use_policy(perf.policy().replace(own_linear_wgrad=on)):
+            T.linear(x, wi, bi_).backward(dy)
+        grads.append(wi.grad.float())
+    assert float((grads[0] - grads[1]).norm() / grads[1].norm()) < 5e-3
+    assert float((grads[0] - ref).norm() / ref.norm()) < 5e-3
