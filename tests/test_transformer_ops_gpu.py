@@ -204,7 +204,7 @@ def test_mfma_attention_matches_sdpa_path(cuda):
 
 
 @pytest.mark.parametrize("Tn,N,K", [(8192, 768, 768), (4096, 3072, 768), (1024, 768, 3072),
-                                    (640, 256, 128)])
+                                    (1024, 256, 128)])
 def test_linear_wgrad_on_wgrad1x1(cuda, Tn, N, K):
     """Transformer-linear weight gradient dY^T X on the 1x1-conv weight-gradient kernel
     (PerfPolicy.own_linear_wgrad) vs fp32, and through a linear's autograd with the policy on vs
