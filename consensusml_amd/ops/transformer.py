@@ -418,11 +418,15 @@ def _own_gemm(M: int, N: int, K: int) -> bool:
 def _linear_wgrad(gout: torch.Tensor, gin: torch.Tensor) -> torch.Tensor:
     """dW [N, K] = gout^T gin over T token rows (gout [T, N], gin [T, K]). PerfPolicy.own_linear_wgrad:
     on the 1x1-conv weight-gradient kernel (wgrad1x1.hip: row-major [T, C] activations are NHWC
-    [T, C, 1, 1]; split-K over the rows, fixed-order fold, bench/linear_wgrad.py), else hipBLASLt."""
+    [T, C, 1, 1]; split-K over the rows, fixed-order fold), else hipBLASLt. Up to BERT-base sizes
+    (N K <= 4 M): at T = 8192 the kernel matches hipBLASLt on 2304 / 3072-wide shapes and is 1.5x
+    faster on 768 x 768 (bench/linear_wgrad.py), and the BERT V = 1 x 64 step drops 13.55 -> 12.94
+    ms (profiles/r04_38/); Llama-size weights are unmeasured on it and stay on hipBLASLt."""
     T, N = gout.shape
     K = gin.shape[-1]
     if (_P().own_linear_wgrad and gout.is_cuda and gout.dtype == torch.bfloat16
             and gin.dtype == torch.bfloat16 and N % 128 == 0 and K % 128 == 0
+            and N * K <= 4 * 1024 * 1024
             and gout.is_contiguous() and gin.is_contiguous()):
         return lib().wgrad1x1(gout.view(T, 1, 1, N).permute(0, 3, 1, 2),
                               gin.view(T, 1, 1, K).permute(0, 3, 1, 2), torch.bfloat16).view(N, K)

@@ -87,8 +87,9 @@ class PerfPolicy:
                                           # bias gradient (no column-sum pass over R x V)
     own_gemm_conv1x1: bool = True         # ResNet 1x1 convs that run as plain GEMMs (layers 3-4
                                           # forward / data gradient) on gemm.hip, not hipBLASLt
-    own_linear_wgrad: bool = False        # transformer-linear weight gradients dY^T X on
-                                          # wgrad1x1.hip (token rows as NHWC pixels), not hipBLASLt
+    own_linear_wgrad: bool = True         # transformer-linear weight gradients dY^T X on
+                                          # wgrad1x1.hip (token rows as NHWC pixels), not hipBLASLt,
+                                          # up to BERT-base sizes (N K <= 4 M)
 
     @classmethod
     def from_env(cls) -> "PerfPolicy":
@@ -132,7 +133,7 @@ class PerfPolicy:
             own_gemm=_env_bool("CML_OWN_GEMM", True),
             fused_ffn=_env_bool("CML_FUSED_FFN", True),
             own_gemm_conv1x1=_env_bool("CML_OWN_GEMM_CONV1X1", True),
-            own_linear_wgrad=_env_bool("CML_OWN_LINEAR_WGRAD", False),
+            own_linear_wgrad=_env_bool("CML_OWN_LINEAR_WGRAD", True),
             padded_logits=_env_bool("CML_PADDED_LOGITS", True),
         )
 
