@@ -239,56 +239,9 @@ def run(args, rule: str, topology: str, steps: int, warmup: int, info, *, V: int
 
 
 def self_launch(n: int) -> int:
-    """``--gpus N`` without a launcher: start N ranks of this script (RANK / LOCAL_RANK /
-    WORLD_SIZE / MASTER_* on 127.0.0.1), one process per GPU. The parent never touches the GPU
-    (nothing here initialises HIP), waits for every rank, and returns the first non-zero exit
-    code; once one rank has failed the others get 60 s to fail on their own (a collective
-    timeout) and are then killed, so a broken rank can never leave the run hanging."""
-    import signal
-    import socket
-    import subprocess
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
-                   CML_BENCH_SELF_LAUNCHED="1")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
-                                      env=env, start_new_session=True))
-    print(f"[bench] self-launched {n} ranks (pids {[p.pid for p in procs]}, port {port})",
-          file=sys.stderr, flush=True)
-    rc, failed_at = 0, None
-    grace = float(os.environ.get("CML_BENCH_KILL_GRACE_S", "60"))
-    alive = set(range(n))
-    try:
-        while alive:
-            for r in sorted(alive):
-                c = procs[r].poll()
-                if c is None:
-                    continue
-                alive.discard(r)
-                if c != 0 and rc == 0:
-                    rc = c if c > 0 else 128 - c
-                    failed_at = time.monotonic()
-                    print(f"[bench] rank {r} exited with {c}", file=sys.stderr, flush=True)
-            if alive and failed_at is not None and time.monotonic() - failed_at > grace:
-                for r in alive:
-                    print(f"[bench] killing rank {r} (pid {procs[r].pid})", file=sys.stderr,
-                          flush=True)
-                    os.killpg(procs[r].pid, signal.SIGKILL)
-                for r in alive:
-                    procs[r].wait()
-                alive.clear()
-            time.sleep(0.2)
-    except KeyboardInterrupt:
-        for p in procs:
-            if p.poll() is None:
-                os.killpg(p.pid, signal.SIGKILL)
-        raise
-    return rc
+    """``--gpus N`` without a launcher: N ranks of this script (consensusml_amd.utils.launch)."""
+    from consensusml_amd.utils.launch import self_launch as _launch
+    return _launch(n, __file__)
 
 
 def main():

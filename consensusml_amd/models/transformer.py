@@ -1,12 +1,14 @@
 """BERT-base and Llama-3 transformer families (N12).
 
-Attention is ``F.scaled_dot_product_attention`` (ROCm flash kernels); the GEMMs are hipBLASLt via
-``F.linear``. Everything between them runs the hand-written HIP kernels of
+Attention runs own MFMA kernels: BERT's short sequences ``csrc/kernels/attention.hip``, Llama's
+causal GQA attention (head dim 128) ``csrc/kernels/flash_attn.hip`` forward and backward. The
+GEMMs are gemm.hip or hipBLASLt. Everything between them runs the hand-written HIP kernels of
 ``csrc/kernels/transformer.hip`` (``ops.transformer``) on bf16 GPU tensors:
   * the q / k / v projections are ONE fused GEMM. BERT's attention (S <= 128, head dim 64) runs
     the MFMA kernel of ``csrc/kernels/attention.hip`` straight from that fused output to the
-    output projection's input layout; Llama's output is split and rotated into SDPA's head-major
-    layout by one kernel (backward: one kernel back);
+    output projection's input layout; Llama's is split and rotated into head-major q / k / v by
+    one kernel, the flash kernels write O in the output projection's row layout, and the backward
+    returns through one RoPE-backward kernel that also sums the GQA group's dk / dv;
   * every residual add is fused with the following norm (``add_norm``: the residual stream and the
     normalised sublayer input come out of one pass, and the backward adds the stream's gradient
     on the way out);
@@ -26,12 +28,11 @@ from dataclasses import dataclass
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ..ops.bn import ResidualLink
 from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, bert_embed, ffn_gelu,
-                               fused_qkv_attention, linear, linear_gelu, qkv_split, rope_tables,
-                               swiglu)
+                               fused_qkv_attention, linear, linear_gelu, qkv_attention,
+                               rope_tables, swiglu)
 
 
 # =============================================================================== BERT
@@ -138,11 +139,8 @@ class LlamaBlock(nn.Module):
     def forward(self, x, m, cos, sin):
         B, S, D = x.shape
         x, h = add_norm(x, m, self.n1.weight, None, self.c.eps)
-        q, k, v = qkv_split(self.wqkv(h), self.c.heads, self.c.kv_heads, self.hd, cos, sin)
-        a = F.scaled_dot_product_attention(q, k, v, is_causal=True,
-                                           enable_gqa=self.c.heads != self.c.kv_heads)
-        x, h = add_norm(x, self.wo(a.transpose(1, 2).reshape(B, S, D)), self.n2.weight, None,
-                        self.c.eps)
+        a = qkv_attention(self.wqkv(h), self.c.heads, self.c.kv_heads, self.hd, cos, sin)
+        x, h = add_norm(x, self.wo(a), self.n2.weight, None, self.c.eps)
         return x, self.w2(swiglu(self.w13(h)))
 
 

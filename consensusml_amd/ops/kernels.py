@@ -156,8 +156,8 @@ def gram(X: torch.Tensor, rows: Optional[torch.Tensor] = None, n: Optional[int] 
         return out
     Xr = X[rows.long()] if rows is not None else X[:n]
     Xr = Xr[:, :D]
-    if center is not None:
-        c = min(max(int(center[0]), 0), n - 1)
+    if center is not None and int(center[0]) >= 0:   # a negative center: uncentered pass
+        c = min(int(center[0]), n - 1)
         xc = Xr[c].double()
         Xr = Xr.double() - torch.where(torch.isfinite(xc), xc, torch.zeros_like(xc))
     G = ref.gram(Xr)
@@ -182,18 +182,57 @@ def gram_center(G: torch.Tensor, n: int, out: Optional[torch.Tensor] = None) -> 
     return out
 
 
+def gram_sum(Gb: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out = Gb[0] + Gb[1] + ... in bucket order (one launch on GPU; the same fp64 adds as
+    accumulating the buckets' Grams one after another)."""
+    if Gb.is_cuda:
+        lib().gram_sum(Gb, out)
+        return out
+    out.copy_(Gb[0])
+    for k in range(1, Gb.shape[0]):
+        out.add_(Gb[k])
+    return out
+
+
 def robust_weights(G: torch.Tensor, rule: str, n: int, f: int = 0, m: Optional[int] = None,
                    iters: int = 8, eps: float = 1e-6, tol: float = 0.0, tau: float = 10.0,
                    w_out: Optional[torch.Tensor] = None, scores: Optional[torch.Tensor] = None,
-                   sel: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Weights over worker rows (fp32 [n] or [n+1] for centered clipping) from the Gram matrix."""
+                   sel: Optional[torch.Tensor] = None, guard: bool = False,
+                   center_out: Optional[torch.Tensor] = None,
+                   sel_counts: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Weights over worker rows (fp32 [n] or [n+1] for centered clipping) from the Gram matrix.
+
+    In the same launch (weights.hip): ``sel_counts`` += (w > 0); ``center_out`` = the medoid of
+    G (the next step's Gram center); ``guard`` (G from a pass centered on the previous step's
+    medoid): at least half the worker rows non-finite = a captured center -> weights zeroed
+    (centered clipping keeps its previous aggregate) and ``center_out`` = -1."""
     dim = n + 1 if rule == "centered_clip" else n
     if G.is_cuda:
         if w_out is None:
             w_out = torch.empty(dim, dtype=torch.float32, device=G.device)
         lib().robust_weights(G.contiguous(), RULE_IDS[rule], n, f, m or 0, iters, eps, tol, tau,
-                             w_out, scores, sel)
+                             w_out, scores, sel, guard, center_out, sel_counts)
         return w_out
+    w = _robust_weights_ref(G, rule, n, f, m, iters, eps, tol, tau, scores, sel)
+    nbad = int((~torch.isfinite(torch.diagonal(G)[:n])).sum())
+    trip = guard and nbad > 0 and 2 * nbad >= n
+    if trip:
+        w = torch.zeros_like(w)
+        if rule == "centered_clip":
+            w[n] = 1.0
+        if sel is not None and rule != "bulyan_select":
+            sel[:n].zero_()
+    if sel_counts is not None:
+        sel_counts += (w[:n] > 0).double()
+    if center_out is not None:
+        center_out.fill_(-1 if trip else ref.gram_center(G[:n, :n]))
+    if w_out is not None:
+        w_out.copy_(w)
+        return w_out
+    return w
+
+
+def _robust_weights_ref(G, rule, n, f, m, iters, eps, tol, tau, scores, sel) -> torch.Tensor:
     if rule == "mean":
         bad = ~torch.isfinite(torch.diagonal(G))
         good = (~bad).double()
@@ -221,11 +260,7 @@ def robust_weights(G: torch.Tensor, rule: str, n: int, f: int = 0, m: Optional[i
         raise ValueError(rule)
     if sel is not None and rule != "bulyan_select":
         sel[:n].copy_((w[:n] > 0).to(sel.dtype))
-    w = w.float()
-    if w_out is not None:
-        w_out.copy_(w)
-        return w_out
-    return w
+    return w.float()
 
 
 # --------------------------------------------------------------------------- high level

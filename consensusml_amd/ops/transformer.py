@@ -381,6 +381,94 @@ def fused_qkv_attention(qkv: torch.Tensor, H: int, hd: int) -> torch.Tensor:
     return F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, S, H * hd)
 
 
+# ============================================================================ flash attention
+def _flash_ok(*ts: torch.Tensor) -> bool:
+    return (_P().flash_attn and _gpu_bf16(*ts)
+            and all(t.is_contiguous() and t.data_ptr() % 16 == 0 for t in ts))
+
+
+class _FlashFn(torch.autograd.Function):
+    """softmax(q k^T scale [+ causal mask]) v on csrc/kernels/flash_attn.hip: q [B, H, S, 128],
+    k / v [B, KV, S, 128] -> o [B, S, H * 128]. The backward's per-query-head dk / dv are summed
+    over each kv head's group here (the fused QKV path, ``_RopeFlashFn``, sums them inside the RoPE
+    backward kernel instead)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        o, lse = lib().flash_fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dkh, dvh = lib().flash_bwd(q, k, v, o, do, lse, ctx.causal, ctx.scale)
+        B, H, S, D = q.shape
+        KV = k.shape[1]
+        if H != KV:
+            dkh = dkh.view(B, KV, H // KV, S, D).float().sum(2).to(q.dtype)
+            dvh = dvh.view(B, KV, H // KV, S, D).float().sum(2).to(q.dtype)
+        return dq, dkh, dvh, None, None
+
+
+def _sdpa_rows(q, k, v, causal: bool, scale: float) -> torch.Tensor:
+    """Reference composition of flash_attention (any device / dtype): [B, S, H * hd]."""
+    B, H, S, hd = q.shape
+    o = F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=scale,
+                                       enable_gqa=H != k.shape[1])
+    return o.transpose(1, 2).reshape(B, S, H * hd)
+
+
+def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True,
+                    scale: Optional[float] = None) -> torch.Tensor:
+    """Multi-head attention with grouped-query heads (H % KV == 0): q [B, H, S, hd], k / v
+    [B, KV, S, hd] -> [B, S, H * hd] (the output projection's input rows). bf16 GPU tensors with
+    hd = 128 run the flash kernels of csrc/kernels/flash_attn.hip (forward and backward);
+    anything else runs SDPA."""
+    hd = q.shape[-1]
+    scale = float(scale) if scale is not None else 1.0 / math.sqrt(hd)
+    if hd == 128 and _flash_ok(q, k, v):
+        return _FlashFn.apply(q, k, v, bool(causal), scale)
+    return _sdpa_rows(q, k, v, causal, scale)
+
+
+class _RopeFlashFn(torch.autograd.Function):
+    """QKV split + RoPE + flash attention from the fused projection ``qkv [B, S, (H + 2 KV) 128]``
+    to ``o [B, S, H 128]``. Backward: the flash backward, then ONE RoPE-backward pass that also
+    sums the per-query-head dk / dv of each kv head's group (transformer.hip rope_bwd, grp) and
+    writes dqkv in the fused layout."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, H, KV, causal, scale):
+        q, k, v = lib().rope_fwd(qkv, cos, sin, H, KV, 128)
+        o, lse = lib().flash_fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(q, k, v, o, lse, cos, sin)
+        ctx.cfg = (H, KV, causal, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, cos, sin = ctx.saved_tensors
+        H, KV, causal, scale = ctx.cfg
+        dq, dkh, dvh = lib().flash_bwd(q, k, v, o, do, lse, causal, scale)
+        dqkv = lib().rope_bwd(dq, dkh, dvh, cos, sin, H // KV)
+        return dqkv, None, None, None, None, None, None
+
+
+def qkv_attention(qkv: torch.Tensor, H: int, KV: int, hd: int,
+                  cos: Optional[torch.Tensor] = None, sin: Optional[torch.Tensor] = None,
+                  causal: bool = True) -> torch.Tensor:
+    """Attention straight from the fused projection ``qkv [B, S, (H + 2 KV) hd]`` (RoPE on q / k
+    when cos / sin are given) to ``[B, S, H hd]``. bf16 GPU tensors with hd = 128 run
+    ``_RopeFlashFn`` (own kernels end to end); otherwise qkv_split + SDPA."""
+    scale = 1.0 / math.sqrt(hd)
+    if hd == 128 and _flash_ok(qkv) and (cos is None or (cos.is_cuda and sin.is_cuda)):
+        return _RopeFlashFn.apply(qkv, cos, sin, H, KV, bool(causal), scale)
+    q, k, v = qkv_split(qkv, H, KV, hd, cos, sin)
+    return _sdpa_rows(q, k, v, causal, scale)
+
+
 # ============================================================================ SwiGLU
 class _SwiGLUFn(torch.autograd.Function):
     @staticmethod

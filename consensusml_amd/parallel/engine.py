@@ -200,6 +200,13 @@ class ConsensusEngine:
         self._gram_done: set = set()
         self.early_grams = 0       # bucket Grams computed before step() (all steps)
         self._gram_eager = False   # tests: wait for each exchange in its hook (forces the path)
+        # GPU ordering of the early Grams: bucket b's Gram is enqueued at its flush on a side
+        # stream that waits (device-side) for the main stream's work so far and for b's
+        # collective, so it runs as soon as the exchange lands, beside the rest of backward, with
+        # no host polling (a host-side is_completed() poll sees nothing finished: the host runs
+        # ahead of the GPU). CPU / gloo runs keep the polled form.
+        self._gram_stream = (torch.cuda.Stream(device=dev)
+                             if self.early_gram and dev.type == "cuda" else None)
         # training-side consensus table (SURVEY.md §5.4 b): when set, the next step() records
         # per-worker / per-parameter gradient statistics (consensus_table())
         self.record_stats = False
@@ -384,7 +391,10 @@ class ConsensusEngine:
         if self.overlap and b.index not in self._pending:
             self._launch_bucket(b, inject=True)
             if self.early_gram:
-                self._poll_grams()
+                if self._gram_stream is not None:
+                    self._enqueue_gram(b)
+                else:
+                    self._poll_grams()
         if self.early_update and complete:
             self._early_update(b)
 
@@ -458,6 +468,24 @@ class ConsensusEngine:
         K.gram(X, n=self.rows_total, D=length, out=self.Gb[b.index], center=self._pass_center())
         self._gram_done.add(b.index)
 
+    def _enqueue_gram(self, b: Bucket) -> None:
+        """Bucket b's Gram partial on the side stream, ordered after b's flush (main stream) and
+        b's collective (``work.wait()`` inside the side-stream context: a device-side wait)."""
+        if b.index in self._gram_done:
+            return
+        st = self._gram_stream
+        st.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(st):
+            w = self._pending.get(b.index)
+            if w is not None:
+                w.wait()
+            X = self._cclip_rows(b) if self.rule == "centered_clip" else self._rows(b)
+            length = b.shard if self.topo == "sharded" else X.shape[1]
+            K.gram(X, n=self.rows_total, D=length, out=self.Gb[b.index],
+                   center=self._pass_center())
+        self._gram_done.add(b.index)
+        self.early_grams += 1
+
     def _poll_grams(self) -> None:
         """Gram partials of every bucket whose exchange has completed (non-blocking test), so
         they run during backward instead of after the last all-to-all."""
@@ -526,13 +554,13 @@ class ConsensusEngine:
         cfg = self.cfg.agg
         center = self._pass_center()
         if self.early_gram:
-            # per-bucket partials (most computed during backward), summed in bucket order:
-            # G = ((g0 + g1) + g2) ..., the same fp64 adds as accumulating bucket by bucket
+            # per-bucket partials (computed during backward), summed in bucket order in one
+            # launch: G = ((g0 + g1) + g2) ..., the same fp64 adds as accumulating bucket by bucket
+            if self._gram_stream is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self._gram_stream)
             for b, _, _ in cols:
                 self._bucket_gram(b)
-            self.G.copy_(self.Gb[0])
-            for k in range(1, len(cols)):
-                self.G.add_(self.Gb[k])
+            K.gram_sum(self.Gb, self.G)
         else:
             self.G.zero_()
             for b, X, length in cols:
@@ -550,17 +578,22 @@ class ConsensusEngine:
                        center=self.center)
             if self.group_active and self.topo == "sharded":
                 dist.all_reduce(self.G)
-        if cfg.centered_gram:
-            # the medoid of this step's (precise) G centers the next step's single pass; it is
-            # computed on the device from the all-reduced G, so every rank holds the same row
-            K.gram_center(self.G, self.rows_total, out=self.center)
-            self.have_center = True
         rule = "bulyan_select" if self.rule == "bulyan" else self.rule
         m = cfg.m if cfg.m is not None else self.n - cfg.f
         iters = cfg.clip_iters if rule == "centered_clip" else cfg.iters
+        # one launch: weights, selection counts and -- centered Gram -- the medoid of this step's
+        # (precise) G, which centers the next step's single pass (computed on the device from the
+        # all-reduced G, so every rank holds the same row). ``guard``: this G came from the single
+        # pass centered on the PREVIOUS step's medoid, which a center turned Byzantine could
+        # capture with huge finite values (weights.hip); a tripped guard zeroes this step's
+        # weights and runs the next pass uncentered (center -1).
         K.robust_weights(self.G, rule, self.n, f=cfg.f, m=m, iters=iters, eps=cfg.eps,
-                         tol=cfg.tol, tau=cfg.tau, w_out=self.w, scores=self.scores, sel=self.sel)
-        self.sel_counts += (self.w[: self.n] > 0).double()
+                         tol=cfg.tol, tau=cfg.tau, w_out=self.w, scores=self.scores, sel=self.sel,
+                         guard=center is not None,
+                         center_out=self.center if cfg.centered_gram else None,
+                         sel_counts=self.sel_counts)
+        if cfg.centered_gram:
+            self.have_center = True
 
     def _bucket_cols(self) -> list:
         out = []

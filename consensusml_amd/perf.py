@@ -77,6 +77,8 @@ class PerfPolicy:
                                           # data gradient (+ bn1 backward sums)
     # ---------------------------------------------------------------- transformers / engine
     attn_kernel: bool = True              # MFMA attention for short sequences (BERT)
+    flash_attn: bool = True               # flash_attn.hip for head-dim-128 (GQA, causal) attention
+                                          # (Llama); False: SDPA (AOTriton kernels on ROCm torch)
     multi_copy: bool = True               # multi-tensor HIP copy for gradient capture
     batched_workers: bool = True          # virtual workers as one batched fwd/bwd (BERT)
     own_gemm: bool = True                 # gemm.hip for transformer linears with >= 128 tiles
@@ -128,6 +130,7 @@ class PerfPolicy:
             own_wgrad3x3=_env_bool("CML_WGRAD3X3", True),
             own_conv3x3_s2=_env_bool("CML_CONV3X3_S2", True),
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),
+            flash_attn=_env_bool("CML_FLASH_ATTN", True),
             multi_copy=_env_bool("CML_MULTI_COPY", True),
             batched_workers=_env_bool("CML_BATCHED_WORKERS", True),
             own_gemm=_env_bool("CML_OWN_GEMM", True),

@@ -135,18 +135,34 @@ void gram_center(const Tensor& G, int64_t n, Tensor& out) {
 
 void robust_weights(const Tensor& G, int64_t rule, int64_t n, int64_t f, int64_t m, int64_t iters,
                     double eps, double tol, double tau, Tensor& w, const optional<Tensor>& scores,
-                    const optional<Tensor>& sel) {
+                    const optional<Tensor>& sel, bool guard, const optional<Tensor>& center_out,
+                    const optional<Tensor>& sel_counts) {
   TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kDouble && G.is_contiguous(), "G: fp64 GPU");
   const int64_t dim = rule == cml::RULE_CCLIP ? n + 1 : n;
   TORCH_CHECK(G.numel() >= dim * dim, "G too small");
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kFloat && w.numel() >= dim, "w: fp32 GPU [n(+1)]");
-  const c10::DeviceGuard guard(G.device());
+  const c10::DeviceGuard guard_(G.device());
   double* sc = opt_ptr<double>(scores, at::kDouble, "scores", n);
   int* se = opt_ptr<int>(sel, at::kInt, "sel", n + 1);
+  int* co = opt_ptr<int>(center_out, at::kInt, "center_out", 1);
+  double* cnt = opt_ptr<double>(sel_counts, at::kDouble, "sel_counts", n);
   CML_CHECK_HIP(cml::launch_robust_weights(static_cast<int>(rule), G.data_ptr<double>(),
                                            static_cast<int>(n), static_cast<int>(f),
                                            static_cast<int>(m), static_cast<int>(iters), eps, tol,
-                                           tau, w.data_ptr<float>(), sc, se, cur_stream()));
+                                           tau, w.data_ptr<float>(), sc, se, cur_stream(),
+                                           guard ? 1 : 0, co, cnt));
+}
+
+// G = sum over b of Gb[b] (fp64 [nb, r, r] -> [r, r]) in bucket order
+void gram_sum(const Tensor& Gb, Tensor& G) {
+  TORCH_CHECK(Gb.is_cuda() && Gb.scalar_type() == at::kDouble && Gb.is_contiguous() && Gb.dim() == 3,
+              "Gb: contiguous fp64 [nb, r, r] GPU tensor");
+  TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kDouble && G.is_contiguous() &&
+                  G.numel() == Gb.size(1) * Gb.size(2) && G.get_device() == Gb.get_device(),
+              "G: contiguous fp64 [r, r] on Gb's device");
+  const c10::DeviceGuard guard(G.device());
+  CML_CHECK_HIP(cml::launch_gram_sum(Gb.data_ptr<double>(), static_cast<int>(Gb.size(0)),
+                                     G.numel(), G.data_ptr<double>(), cur_stream()));
 }
 
 int64_t gossip_workspace_bytes(int64_t D) {
@@ -1724,15 +1740,17 @@ std::vector<Tensor> rope_fwd(const Tensor& qkv, const optional<Tensor>& cosb,
 }
 
 Tensor rope_bwd(const Tensor& dq_in, const Tensor& dk_in, const Tensor& dv_in,
-                const optional<Tensor>& cosb, const optional<Tensor>& sinb) {
+                const optional<Tensor>& cosb, const optional<Tensor>& sinb, int64_t grp) {
   Tensor dq = dq_in.contiguous(), dk = dk_in.contiguous(), dv = dv_in.contiguous();
   check_bf16c(dq, "dq");
   check_bf16c(dk, "dk");
   check_bf16c(dv, "dv");
   TORCH_CHECK(dq.dim() == 4 && dk.dim() == 4 && dk.sizes() == dv.sizes() &&
                   dq.size(0) == dk.size(0) && dq.size(2) == dk.size(2) && dq.size(3) == dk.size(3),
-              "dq [B, H, S, hd], dk / dv [B, KV, S, hd]");
-  const int64_t B = dq.size(0), H = dq.size(1), S = dq.size(2), hd = dq.size(3), KV = dk.size(1);
+              "dq [B, H, S, hd], dk / dv [B, KV grp, S, hd]");
+  TORCH_CHECK(grp >= 1 && dk.size(1) % grp == 0, "rope_bwd: dk heads must be a multiple of grp");
+  const int64_t B = dq.size(0), H = dq.size(1), S = dq.size(2), hd = dq.size(3),
+                KV = dk.size(1) / grp;
   TORCH_CHECK(hd % 8 == 0, "hd % 8 == 0");
   check_rope_tables(cosb, sinb, S, hd);
   const c10::DeviceGuard guard(dq.device());
@@ -1741,8 +1759,68 @@ Tensor rope_bwd(const Tensor& dq_in, const Tensor& dk_in, const Tensor& dv_in,
   CML_CHECK_HIP(cml::launch_rope_bwd(dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
                                      rot ? cosb->data_ptr<float>() : nullptr,
                                      rot ? sinb->data_ptr<float>() : nullptr, dqkv.data_ptr(), B,
-                                     S, H, KV, hd, cur_stream()));
+                                     S, H, KV, hd, cur_stream(), static_cast<int>(grp)));
   return dqkv;
+}
+
+// Flash attention (csrc/kernels/flash_attn.hip): q [B, H, S, 128], k / v [B, KV, S, 128] bf16
+// contiguous -> (o [B, S, H * 128], lse fp32 [B, H, S])
+void check_flash_qkv(const Tensor& q, const Tensor& k, const Tensor& v) {
+  check_bf16c(q, "q");
+  check_bf16c(k, "k");
+  check_bf16c(v, "v");
+  TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && k.sizes() == v.sizes() && q.size(0) == k.size(0) &&
+                  q.size(2) == k.size(2) && q.size(3) == 128 && k.size(3) == 128,
+              "flash: q [B, H, S, 128], k / v [B, KV, S, 128]");
+  TORCH_CHECK(q.size(1) % k.size(1) == 0, "flash: H % KV == 0");
+  TORCH_CHECK(q.get_device() == k.get_device() && q.get_device() == v.get_device(),
+              "flash: q / k / v on one device");
+  for (const Tensor* t : {&q, &k, &v})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0, "flash: 16-B aligned q / k / v");
+}
+
+std::vector<Tensor> flash_fwd(const Tensor& q, const Tensor& k, const Tensor& v, bool causal,
+                              double scale) {
+  check_flash_qkv(q, k, v);
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), KV = k.size(1);
+  const c10::DeviceGuard guard(q.device());
+  Tensor o = at::empty({B, S, H * 128}, q.options());
+  Tensor lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  CML_CHECK_HIP(cml::launch_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                      lse.data_ptr<float>(), static_cast<int>(B), static_cast<int>(H),
+                                      static_cast<int>(KV), static_cast<int>(S),
+                                      static_cast<float>(scale), causal, cur_stream()));
+  return {o, lse};
+}
+
+// -> (dq [B, H, S, 128], dk / dv per query head [B, H, S, 128])
+std::vector<Tensor> flash_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                              const Tensor& dout_in, const Tensor& lse, bool causal, double scale) {
+  check_flash_qkv(q, k, v);
+  const int64_t B = q.size(0), H = q.size(1), S = q.size(2), KV = k.size(1);
+  Tensor dout = dout_in.contiguous();
+  check_bf16c(o, "o");
+  check_bf16c(dout, "dout");
+  TORCH_CHECK(o.numel() == B * S * H * 128 && dout.numel() == o.numel() && o.is_contiguous(),
+              "flash_bwd: o / dout [B, S, H * 128]");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(o.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(dout.data_ptr()) & 15) == 0,
+              "flash_bwd: 16-B aligned o / dout");
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.is_contiguous() &&
+                  lse.numel() == B * H * S && lse.get_device() == q.get_device(),
+              "flash_bwd: lse fp32 [B, H, S]");
+  const c10::DeviceGuard guard(q.device());
+  Tensor dq = at::empty_like(q);
+  Tensor dk = at::empty({B, H, S, 128}, q.options());
+  Tensor dv = at::empty({B, H, S, 128}, q.options());
+  Tensor dsum = at::empty({B, H, S}, lse.options());
+  CML_CHECK_HIP(cml::launch_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+                                      dout.data_ptr(), lse.data_ptr<float>(), dsum.data_ptr<float>(),
+                                      dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                                      static_cast<int>(B), static_cast<int>(H), static_cast<int>(KV),
+                                      static_cast<int>(S), static_cast<float>(scale), causal,
+                                      cur_stream()));
+  return {dq, dk, dv};
 }
 
 Tensor swiglu_fwd(const Tensor& h) {
@@ -2105,7 +2183,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("X"), py::arg("n"), py::arg("D"), py::arg("rows"), py::arg("work"), py::arg("G"),
         py::arg("accumulate"), py::arg("center") = py::none());
   m.def("gram_center", &gram_center, "medoid of the finite rows of a Gram matrix");
-  m.def("robust_weights", &robust_weights, "robust weights from a Gram matrix");
+  m.def("robust_weights", &robust_weights, "robust weights from a Gram matrix (+ selection counts, "
+        "next center and the centered-pass guard in the same launch)",
+        py::arg("G"), py::arg("rule"), py::arg("n"), py::arg("f"), py::arg("m"), py::arg("iters"),
+        py::arg("eps"), py::arg("tol"), py::arg("tau"), py::arg("w"), py::arg("scores"),
+        py::arg("sel"), py::arg("guard") = false, py::arg("center_out") = py::none(),
+        py::arg("sel_counts") = py::none());
+  m.def("gram_sum", &gram_sum, "sum of per-bucket Gram partials in bucket order");
   m.def("gossip_workspace_bytes", &gossip_workspace_bytes);
   m.def("gossip_mix", &gossip_mix, "ring gossip mixing with neighbour clipping");
   m.def("gossip_mix_k", &gossip_mix_k, "k-neighbour gossip mixing with neighbour clipping");
@@ -2215,7 +2299,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_fwd", &norm_fwd, "LayerNorm / RMSNorm (+ residual add) forward");
   m.def("norm_bwd", &norm_bwd, "LayerNorm / RMSNorm backward (+ residual gradient)");
   m.def("rope_fwd", &rope_fwd, "QKV split + RoPE into head-major q / k / v");
-  m.def("rope_bwd", &rope_bwd, "inverse of rope_fwd");
+  m.def("rope_bwd", &rope_bwd, "inverse of rope_fwd (grp > 1: sums per-query-head dk / dv)",
+        py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("cos"), py::arg("sin"),
+        py::arg("grp") = 1);
+  m.def("flash_fwd", &flash_fwd, "flash attention forward, head dim 128, GQA, causal / full");
+  m.def("flash_bwd", &flash_bwd, "flash attention backward (dq, per-query-head dk / dv)");
   m.def("swiglu_fwd", &swiglu_fwd, "silu(a) * b over [a | b]");
   m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");
   m.def("attn_fwd", &attn_fwd, "short-sequence MFMA attention forward (fused qkv in)");

@@ -31,6 +31,9 @@
 // rows) of a G; the engine uses the medoid of step t - 1 as step t's center, so one centered pass
 // per step suffices (the medoid of an honest cluster stays inside it from step to step).
 //
+// A negative *center means "no center this step" (the weights kernel's guard sets it when a
+// centered pass looked captured, see weights.hip): the pass runs uncentered.
+//
 // Stage 1 writes one [P, P] fp32 partial per workgroup (fixed-order LDS reduction of its 4
 // waves, folded over column groups); stage 2 sums the partials in fp64 in block order ->
 // bitwise reproducible G. Rows >= n load a valid duplicate row and are zeroed by a select, so
@@ -137,10 +140,10 @@ template <> struct GramLoad<float> {
 // G = column-group packing factor (1, or 16/P2 when TT == 1 and n <= 8).
 // CENTER: rows relative to row *center (see the header).
 template <typename T, int TT, int G, bool CENTER>
-__global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restrict__ X, int64_t ld,
-                                                              int n, const int* __restrict__ rows,
-                                                              int64_t D, float* __restrict__ part,
-                                                              const int* __restrict__ center) {
+__device__ __forceinline__ void gram_partial_body(const T* __restrict__ X, int64_t ld, int n,
+                                                  const int* __restrict__ rows, int64_t D,
+                                                  float* __restrict__ part, int c,
+                                                  float (*red)[16 * TT * 16 * TT]) {
   static_assert(G == 1 || TT == 1, "column-group packing is for a single row tile");
   typedef typename GramLoad<T>::type V;
   constexpr int P = 16 * TT;
@@ -151,7 +154,6 @@ __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restri
   constexpr int GSPAN = Q * STEP;           // columns of one group per iteration
   constexpr int COLS = G * GSPAN;
   constexpr int P2 = 16 / G;
-  __shared__ float red[kGWaves][P * P];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -171,8 +173,7 @@ __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restri
   }
   const T* cp = nullptr;
   if constexpr (CENTER) {
-    int c = *center;
-    c = c < 0 ? 0 : (c >= n ? n - 1 : c);
+    c = c >= n ? n - 1 : c;
     cp = X + static_cast<int64_t>(rows ? rows[c] : c) * ld + grp * GSPAN + VEC * h;
   }
 
@@ -254,6 +255,35 @@ __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restri
       }
     }
     out[e] = v;
+  }
+}
+
+template <typename T, int TT, int G, bool CENTER>
+__global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restrict__ X, int64_t ld,
+                                                              int n, const int* __restrict__ rows,
+                                                              int64_t D, float* __restrict__ part,
+                                                              const int* __restrict__ center) {
+  __shared__ float red[kGWaves][16 * TT * 16 * TT];
+  if constexpr (CENTER) {
+    const int c = *center;   // uniform: one branch for the whole workgroup
+    if (c < 0)
+      gram_partial_body<T, TT, G, false>(X, ld, n, rows, D, part, 0, red);
+    else
+      gram_partial_body<T, TT, G, true>(X, ld, n, rows, D, part, c, red);
+  } else {
+    gram_partial_body<T, TT, G, false>(X, ld, n, rows, D, part, 0, red);
+  }
+}
+
+// G = sum over b of Gb[b] (fp64 [nb][E]), added in bucket order: the same adds as accumulating
+// the per-bucket Grams into G one after another (the engine's early-Gram partials, one launch)
+__global__ __launch_bounds__(256) void gram_sum_kernel(const double* __restrict__ Gb, int nb,
+                                                      int64_t E, double* __restrict__ G) {
+  for (int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; e < E;
+       e += static_cast<int64_t>(gridDim.x) * 256) {
+    double v = Gb[e];
+    for (int b = 1; b < nb; ++b) v += Gb[static_cast<int64_t>(b) * E + e];
+    G[e] = v;
   }
 }
 
@@ -370,6 +400,14 @@ hipError_t launch_gram(int dtype, const void* X, int64_t ld, int n, const int* r
   else
     launch_gram_dispatch(reinterpret_cast<const float*>(X), ld, n, rows, D, part, G, accumulate,
                          center, stream);
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_sum(const double* Gb, int nb, int64_t E, double* G, hipStream_t stream) {
+  if (nb < 1 || E < 1) return hipErrorInvalidValue;
+  int64_t blocks = (E + 255) / 256;
+  if (blocks > 64) blocks = 64;
+  gram_sum_kernel<<<static_cast<unsigned>(blocks), 256, 0, stream>>>(Gb, nb, E, G);
   return hipGetLastError();
 }
 

@@ -64,9 +64,16 @@ hipError_t launch_gram_center(const double* G, int n, int* out, hipStream_t stre
 //   w[n_out] fp32 (n_out = n, or n+1 for centered clipping whose last row is the previous
 //   aggregate), scores[n] fp64 (Krum scores / final distances), sel[n+1] int32
 //   (Bulyan: sorted selected indices then sel[n] = count; others: sel[i] = 1 if w_i > 0).
+// Optional, in the same launch: sel_counts[n] fp64 += (w_i > 0); center_out[0] = medoid of G
+// (the next step's Gram center); guard != 0 (G from a pass centered on the previous step's
+// medoid): if at least half the worker rows are non-finite the weights are zeroed (centered
+// clipping: the previous aggregate kept) and center_out = -1 (next pass uncentered).
 hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m, int iters,
                                  double eps, double tol, double tau, float* w, double* scores,
-                                 int* sel, hipStream_t stream);
+                                 int* sel, hipStream_t stream, int guard = 0,
+                                 int* center_out = nullptr, double* sel_counts = nullptr);
+// G[e] = sum_b Gb[b][e] in b order (the early-Gram per-bucket partials), e < E.
+hipError_t launch_gram_sum(const double* Gb, int nb, int64_t E, double* G, hipStream_t stream);
 
 // Gossip: x <- (w0+w1+w2) x + w1*clip(left-x) + w2*clip(right-x); writes fp32 master and bf16
 // params. clip <= 0 disables clipping. ``work`` must hold gossip_workspace_bytes(D) bytes.
@@ -233,9 +240,21 @@ hipError_t launch_norm_bwd_seg(int ln, const void* dy, const void* dres, const v
 // on q / k from fp32 cos / sin [S, hd / 2] (null: no rotation); backward is the inverse.
 hipError_t launch_rope_fwd(const void* qkv, const float* cosb, const float* sinb, void* q, void* k,
                            void* v, int B, int S, int H, int KV, int hd, hipStream_t stream);
+// grp > 1: dk / dv hold one gradient per QUERY head ([B, KV grp, S, hd]); each kv head's grp
+// heads are summed (fp32) on the way into dqkv.
 hipError_t launch_rope_bwd(const void* dq, const void* dk, const void* dv, const float* cosb,
                            const float* sinb, void* dqkv, int B, int S, int H, int KV, int hd,
-                           hipStream_t stream);
+                           hipStream_t stream, int grp = 1);
+// Flash attention, head dim 128, causal or full, grouped-query heads (H % KV == 0):
+// q [B, H, S, 128], k / v [B, KV, S, 128] -> o [B, S, H, 128], lse fp32 [B, H, S] (log2
+// domain). Backward: dq [B, H, S, 128], dk / dv per query head [B, H, S, 128]; dsum [B, H, S]
+// fp32 scratch (D = rowsum(dO * O)). csrc/kernels/flash_attn.hip.
+hipError_t launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B,
+                            int H, int KV, int S, float scale, bool causal, hipStream_t stream);
+hipError_t launch_flash_bwd(const void* q, const void* k, const void* v, const void* o,
+                            const void* dout, const float* lse, float* dsum, void* dq, void* dk,
+                            void* dv, int B, int H, int KV, int S, float scale, bool causal,
+                            hipStream_t stream);
 // SwiGLU over h = [a | b] ([M, 2F]): y = silu(a) * b; backward writes dh [M, 2F].
 hipError_t launch_swiglu_fwd(const void* h, void* y, int64_t M, int F, hipStream_t stream);
 hipError_t launch_swiglu_bwd(const void* dy, const void* h, void* dh, int64_t M, int F,

@@ -645,7 +645,7 @@ __global__ __launch_bounds__(kTB) void rope_bwd_kernel(const bf16* __restrict__ 
                                                       const float* __restrict__ cosb,
                                                       const float* __restrict__ sinb,
                                                       bf16* __restrict__ dqkv, int B, int S,
-                                                      int H, int KV, int hd) {
+                                                      int H, int KV, int hd, int grp) {
   const int cph = hd / 8;
   const int heads = H + 2 * KV;
   const int64_t total = static_cast<int64_t>(B) * S * heads * cph;
@@ -657,16 +657,24 @@ __global__ __launch_bounds__(kTB) void rope_bwd_kernel(const bf16* __restrict__ 
     const int64_t bs = t1 / heads;
     const int s = static_cast<int>(bs % S);
     const int b = static_cast<int>(bs / S);
-    const bf16* src;
-    if (hh < H) {
-      src = dq + ((static_cast<int64_t>(b) * H + hh) * S + s) * hd + j * 8;
-    } else if (hh < H + KV) {
-      src = dk + ((static_cast<int64_t>(b) * KV + (hh - H)) * S + s) * hd + j * 8;
-    } else {
-      src = dv + ((static_cast<int64_t>(b) * KV + (hh - H - KV)) * S + s) * hd + j * 8;
-    }
     float e[8];
-    ld8(src, e);
+    if (hh < H) {
+      ld8(dq + ((static_cast<int64_t>(b) * H + hh) * S + s) * hd + j * 8, e);
+    } else {
+      // dk / dv per query head ([B, KV grp, S, hd], grp > 1: the flash-attention backward's
+      // per-head gradients): the grp heads of kv head g sum here, in fp32
+      const bool isk = hh < H + KV;
+      const int g = isk ? hh - H : hh - H - KV;
+      const bf16* base = (isk ? dk : dv) +
+                         ((static_cast<int64_t>(b) * KV + g) * grp * S + s) * hd + j * 8;
+      ld8(base, e);
+      for (int x = 1; x < grp; ++x) {
+        float f[8];
+        ld8(base + static_cast<int64_t>(x) * S * hd, f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] += f[i];
+      }
+    }
     if (cosb != nullptr && hh < H + KV) {
       const float* cr = cosb + static_cast<int64_t>(s) * (hd / 2) + j * 4;
       const float* sr = sinb + static_cast<int64_t>(s) * (hd / 2) + j * 4;
@@ -928,13 +936,13 @@ hipError_t launch_rope_fwd(const void* qkv, const float* cosb, const float* sinb
 
 hipError_t launch_rope_bwd(const void* dq, const void* dk, const void* dv, const float* cosb,
                            const float* sinb, void* dqkv, int B, int S, int H, int KV, int hd,
-                           hipStream_t st) {
-  if (hd % 8 || B < 1 || S < 1 || H < 1 || KV < 1) return hipErrorInvalidValue;
+                           hipStream_t st, int grp) {
+  if (hd % 8 || B < 1 || S < 1 || H < 1 || KV < 1 || grp < 1) return hipErrorInvalidValue;
   const int64_t total = static_cast<int64_t>(B) * S * (H + 2 * KV) * (hd / 8);
   rope_bwd_kernel<<<stream_grid(total), kTB, 0, st>>>(
       reinterpret_cast<const bf16*>(dq), reinterpret_cast<const bf16*>(dk),
       reinterpret_cast<const bf16*>(dv), cosb, sinb, reinterpret_cast<bf16*>(dqkv), B, S, H, KV,
-      hd);
+      hd, grp);
   return hipGetLastError();
 }
 

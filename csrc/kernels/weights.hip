@@ -12,6 +12,15 @@
 //                       sorted kernel over those rows.
 // Rows with a non-finite squared norm are Byzantine by definition: score +inf, weight 0.
 // Lane i owns row i; ranks use (value, index) order so every rank computes identical weights.
+//
+// The same launch also (optionally) adds this step's selections to sel_counts, writes the
+// medoid of G (the next step's Gram center, as gram_center_kernel) and -- for a G from the
+// single centered pass around the PREVIOUS step's medoid -- guards against a captured center:
+// a center worker that turns Byzantine with huge finite values overflows every honest centered
+// row (x_i - x_c)^2, leaving its own all-zero row the only finite one. If at least half the
+// worker rows are non-finite, the step is distrusted: gradient weights 0 (centered clipping
+// keeps its previous aggregate), and the next center is -1 (the next Gram pass runs
+// uncentered, where the overflowing row is the non-finite one).
 #include "common.h"
 #include "kernels.h"
 
@@ -51,22 +60,12 @@ __device__ double krum_score(const double* G, int n, int i, int k, const unsigne
   return s;
 }
 
-__global__ __launch_bounds__(64) void robust_weights_kernel(int rule, const double* __restrict__ G,
-                                                           int n, int f, int m, int iters,
-                                                           double eps, double tol, double tau,
-                                                           float* __restrict__ w,
-                                                           double* __restrict__ scores,
-                                                           int* __restrict__ sel) {
-  __shared__ bool bad[kMax];
-  __shared__ double sc[kMax];
-  __shared__ double a[kMax];
+__device__ __forceinline__ void weights_rule(int rule, const double* __restrict__ G, int n, int f,
+                                             int m, int iters, double eps, double tol, double tau,
+                                             float* __restrict__ w, double* __restrict__ scores,
+                                             int* __restrict__ sel, const bool* bad, double* sc,
+                                             double* a) {
   const int i = threadIdx.x;
-  const int nrows = rule == RULE_CCLIP ? n + 1 : n;   // Gram dimension
-  for (int r = i; r < nrows; r += 64) {
-    const double d = G[r * nrows + r];
-    bad[r] = !(d == d) || d == __builtin_inf() || d == -__builtin_inf();
-  }
-  __syncthreads();
 
   if (rule == RULE_MEAN) {
     int good = 0;
@@ -205,15 +204,75 @@ __global__ __launch_bounds__(64) void robust_weights_kernel(int rule, const doub
   }
 }
 
+__global__ __launch_bounds__(64) void robust_weights_kernel(int rule, const double* __restrict__ G,
+                                                           int n, int f, int m, int iters,
+                                                           double eps, double tol, double tau,
+                                                           float* __restrict__ w,
+                                                           double* __restrict__ scores,
+                                                           int* __restrict__ sel, int guard,
+                                                           int* __restrict__ center_out,
+                                                           double* __restrict__ sel_counts) {
+  __shared__ bool bad[kMax];
+  __shared__ double sc[kMax];
+  __shared__ double a[kMax];
+  const int i = threadIdx.x;
+  const int nrows = rule == RULE_CCLIP ? n + 1 : n;   // Gram dimension
+  for (int r = i; r < nrows; r += 64) {
+    const double d = G[r * nrows + r];
+    bad[r] = !(d == d) || d == __builtin_inf() || d == -__builtin_inf();
+  }
+  __syncthreads();
+  weights_rule(rule, G, n, f, m, iters, eps, tol, tau, w, scores, sel, bad, sc, a);
+  __syncthreads();
+  int nbad = 0;
+  for (int r = 0; r < n; ++r) nbad += bad[r];
+  const bool trip = guard && 2 * nbad >= n && nbad > 0;
+  if (trip) {
+    if (i < nrows) w[i] = (rule == RULE_CCLIP && i == n) ? 1.0f : 0.0f;
+    if (sel && rule != RULE_BULYAN_SELECT && i < n) sel[i] = 0;
+  }
+  if (sel_counts && i < n) sel_counts[i] += w[i] > 0.0f ? 1.0 : 0.0;
+  if (center_out) {
+    // medoid of the finite worker rows of G (gram_center_kernel's rule)
+    double s_i = __builtin_inf();
+    if (i < n) {
+      const double gii = G[i * nrows + i];
+      if (isfinite(gii)) {
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) {
+          const double gjj = G[j * nrows + j];
+          if (!isfinite(gjj)) continue;
+          const double d = gii + gjj - 2.0 * G[i * nrows + j];
+          s += d > 0.0 ? d : 0.0;
+        }
+        if (isfinite(s)) s_i = s;
+      }
+    }
+    int idx = i;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double s2 = __shfl_xor(s_i, o, 64);
+      const int i2 = __shfl_xor(idx, o, 64);
+      if (s2 < s_i || (s2 == s_i && i2 < idx)) {
+        s_i = s2;
+        idx = i2;
+      }
+    }
+    if (i == 0) center_out[0] = trip ? -1 : ((idx < n && isfinite(s_i)) ? idx : 0);
+  }
+}
+
 }  // namespace
 
 hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m, int iters,
                                  double eps, double tol, double tau, float* w, double* scores,
-                                 int* sel, hipStream_t stream) {
+                                 int* sel, hipStream_t stream, int guard, int* center_out,
+                                 double* sel_counts) {
   if (n < 1 || n > 64) return hipErrorInvalidValue;
   if (rule == RULE_CCLIP && n > 63) return hipErrorInvalidValue;   // n + 1 rows, one per lane
   if (rule == RULE_BULYAN_SELECT && sel == nullptr) return hipErrorInvalidValue;
-  robust_weights_kernel<<<1, 64, 0, stream>>>(rule, G, n, f, m, iters, eps, tol, tau, w, scores, sel);
+  robust_weights_kernel<<<1, 64, 0, stream>>>(rule, G, n, f, m, iters, eps, tol, tau, w, scores, sel,
+                                              guard, center_out, sel_counts);
   return hipGetLastError();
 }
 

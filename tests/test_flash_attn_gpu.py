@@ -1,0 +1,160 @@
+"""Flash attention (csrc/kernels/flash_attn.hip) against an fp32 softmax(Q K^T) V oracle.
+
+Covers the Llama-3-8B shape (32 q / 8 kv heads, head dim 128, causal, S = 2048), ragged S (129,
+1000: partial key / query tiles), full (non-causal) attention, MHA (H = KV), large-magnitude
+scores (online-softmax rescales at every tile), the fused QKV + RoPE path whose backward sums the
+GQA group's dk / dv inside the RoPE-backward kernel, and bitwise run-to-run determinism (no
+atomics in the backward)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from consensusml_amd.ops.native import lib  # noqa: E402
+from consensusml_amd.ops.transformer import (flash_attention, qkv_attention,  # noqa: E402
+                                             rope_tables)
+
+
+def _ref(q, k, v, causal, scale):
+    """fp32 attention with GQA expansion: [B, S, H * hd]."""
+    B, H, S, D = q.shape
+    KV = k.shape[1]
+    kf = k.float().repeat_interleave(H // KV, 1)
+    vf = v.float().repeat_interleave(H // KV, 1)
+    s = torch.matmul(q.float(), kf.transpose(-1, -2)) * scale
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
+    o = torch.matmul(torch.softmax(s, -1), vf)
+    return o.transpose(1, 2).reshape(B, S, H * D)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30)).item()
+
+
+def _inputs(B, H, KV, S, mag=1.0, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    mk = lambda h: (torch.randn(B, h, S, 128, device="cuda", generator=g) * mag).bfloat16()  # noqa
+    return mk(H), mk(KV), mk(KV)
+
+
+CASES = [  # B, H, KV, S, causal
+    (1, 4, 1, 129, True),
+    (2, 8, 2, 1000, True),
+    (1, 32, 8, 2048, True),
+    (1, 8, 2, 1000, False),
+    (2, 4, 4, 320, True),
+]
+
+
+@pytest.mark.parametrize("B,H,KV,S,causal", CASES)
+def test_flash_fwd_bwd_vs_fp32(B, H, KV, S, causal):
+    q, k, v = _inputs(B, H, KV, S)
+    scale = 1.0 / math.sqrt(128)
+    qa, ka, va = (t.clone().requires_grad_() for t in (q, k, v))
+    o = flash_attention(qa, ka, va, causal=causal)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    ref = _ref(qr, kr, vr, causal, scale)
+    assert o.shape == (B, S, H * 128) and o.dtype == torch.bfloat16
+    assert _rel(o, ref) < 1e-2
+    do = torch.randn_like(ref).bfloat16()
+    o.backward(do)
+    ref.backward(do.float())
+    for got, want, name in ((qa.grad, qr.grad, "dq"), (ka.grad, kr.grad, "dk"),
+                            (va.grad, vr.grad, "dv")):
+        assert torch.isfinite(got.float()).all(), name
+        assert _rel(got, want) < 1e-2, (name, _rel(got, want))
+
+
+def test_flash_large_scores():
+    """Scores of magnitude ~100: the running max jumps inside and across tiles."""
+    B, H, KV, S = 1, 4, 2, 777
+    q, k, v = _inputs(B, H, KV, S, mag=4.0, seed=3)
+    k[0, 1, 300] *= 8          # one spiked key: its row max appears mid-sequence
+    scale = 1.0 / math.sqrt(128)
+    qa, ka, va = (t.clone().requires_grad_() for t in (q, k, v))
+    o = flash_attention(qa, ka, va, causal=True)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    ref = _ref(qr, kr, vr, True, scale)
+    assert _rel(o, ref) < 1e-2
+    do = torch.randn_like(ref).bfloat16()
+    o.backward(do)
+    ref.backward(do.float())
+    for got, want in ((qa.grad, qr.grad), (ka.grad, kr.grad), (va.grad, vr.grad)):
+        assert _rel(got, want) < 2e-2
+
+
+def test_flash_lse_and_layout():
+    q, k, v = _inputs(1, 4, 2, 200, seed=5)
+    scale = 1.0 / math.sqrt(128)
+    o, lse = lib().flash_fwd(q, k, v, True, scale)
+    s = torch.matmul(q.float(), k.float().repeat_interleave(2, 1).transpose(-1, -2)) * scale
+    s = s.masked_fill(torch.ones(200, 200, dtype=torch.bool, device="cuda").triu(1), float("-inf"))
+    want = torch.logsumexp(s, -1) / math.log(2.0)       # log2 domain
+    assert (lse - want).abs().max().item() < 1e-3
+
+
+def test_flash_deterministic():
+    q, k, v = _inputs(2, 8, 2, 1000, seed=7)
+    do = torch.randn(2, 1000, 8 * 128, device="cuda").bfloat16()
+    outs = []
+    for _ in range(2):
+        qa, ka, va = (t.clone().requires_grad_() for t in (q, k, v))
+        o = flash_attention(qa, ka, va, causal=True)
+        o.backward(do)
+        outs.append([o, qa.grad, ka.grad, va.grad])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("S,rot", [(129, True), (1000, True), (256, False)])
+def test_qkv_rope_flash_vs_fp32(S, rot):
+    """Fused path: qkv -> RoPE split -> flash fwd; backward flash -> RoPE bwd with the GQA sum."""
+    B, H, KV, hd = 2, 8, 2, 128
+    g = torch.Generator(device="cuda").manual_seed(11)
+    qkv = torch.randn(B, S, (H + 2 * KV) * hd, device="cuda", generator=g).bfloat16()
+    cos, sin = rope_tables(S, hd, 500000.0, "cuda") if rot else (None, None)
+    x = qkv.clone().requires_grad_()
+    o = qkv_attention(x, H, KV, hd, cos, sin)
+    # fp32 reference: split, rotate, attend
+    xr = qkv.float().requires_grad_()
+    t = xr.view(B, S, H + 2 * KV, hd).transpose(1, 2)
+    q, k, v = t[:, :H], t[:, H:H + KV], t[:, H + KV:]
+    if rot:
+        def rope(z):
+            z1, z2 = z[..., 0::2], z[..., 1::2]
+            c, s_ = cos[None, None], sin[None, None]
+            return torch.stack((z1 * c - z2 * s_, z1 * s_ + z2 * c), -1).flatten(-2)
+        q, k = rope(q), rope(k)
+    ref = _ref(q, k, v, True, 1.0 / math.sqrt(hd))
+    assert _rel(o, ref) < 1e-2
+    do = torch.randn_like(ref).bfloat16()
+    o.backward(do)
+    ref.backward(do.float())
+    assert _rel(x.grad, xr.grad) < 1e-2
+    # per-section (q / k / v columns) as well: the k / v parts carry the group sum
+    for lo, hi in ((0, H * hd), (H * hd, (H + KV) * hd), ((H + KV) * hd, (H + 2 * KV) * hd)):
+        assert _rel(x.grad[..., lo:hi], xr.grad[..., lo:hi]) < 1e-2
+
+
+def test_llama_tiny_block_uses_flash():
+    """A Llama block with head dim 128 goes through _RopeFlashFn (no SDPA)."""
+    from consensusml_amd.models.transformer import Llama, LlamaConfig
+    m = Llama(LlamaConfig(vocab=256, d=512, layers=1, heads=4, kv_heads=2, ffn=512,
+                          max_seq=256)).cuda().bfloat16()
+    ids = torch.randint(0, 256, (2, 256), device="cuda")
+    calls = []
+    orig = torch.nn.functional.scaled_dot_product_attention
+    torch.nn.functional.scaled_dot_product_attention = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    try:
+        loss = m(ids).float().logsumexp(-1).mean()
+        loss.backward()
+    finally:
+        torch.nn.functional.scaled_dot_product_attention = orig
+    assert not calls
+    assert all(torch.isfinite(p.grad.float()).all() for p in m.parameters() if p.grad is not None)

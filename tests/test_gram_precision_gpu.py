@@ -159,3 +159,29 @@ def test_engine_single_pass_center(cuda):
             _, sel_ref = _krum_from_dist(_direct_sqdist(X), 2, 1)
             assert a == sel_ref[0]
         assert one.have_center
+
+
+def test_engine_single_pass_captured_center(cuda):
+    """the previous step's medoid turns Byzantine with huge FINITE values.
+    Centered on it, every honest (x_i - x_c)^2 overflows, leaving the attacker's own row the only
+    finite one. The guard in the weights launch must refuse the step (no weight on the attacker,
+    next center -1) and the following steps select honest workers again, as the two-pass scheme
+    does -- also while the attack continues."""
+    one, two = _engine(cuda, False), _engine(cuda, True)
+    attacker = None
+    for step in range(6):
+        X = _workers(6, 2, one.flat.total, 0.02, 60 + step, cuda)
+        if step >= 3:
+            if attacker is None:
+                attacker = int(one.center)
+            X[attacker] = 1e38                # finite in bf16, overflows every centered square
+        a, _ = _step(one, X)
+        b, _ = _step(two, X)
+        if step == 3:                         # the captured step: refused, not captured
+            assert float(one.w[:8].sum()) == 0.0
+            assert int(one.center) == -1
+        else:
+            assert a == b
+            assert float(one.w[a]) > 0
+        if attacker is not None:
+            assert float(one.w[attacker]) == 0.0
