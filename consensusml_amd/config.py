@@ -96,6 +96,9 @@ class TopologyConfig:
     early_update: bool = True    # gossip, 1 local worker: per-bucket optimizer step in backward
     param_prefetch: bool = True  # sharded: bf16 parameter all-gather overlaps the next forward
     early_gram: bool = True      # Gram-space rules: per-bucket Gram as each exchange lands
+    gram_lag: int = 1            # GPU runs: bucket b's Gram is enqueued on the compute stream at
+                                 # the flush of bucket b + gram_lag (its exchange has had one
+                                 # bucket of backward to land); the last ones run in step()
 
     def validate(self) -> None:
         if self.kind not in TOPOLOGIES:

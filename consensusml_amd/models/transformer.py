@@ -93,7 +93,7 @@ class BertMLM(nn.Module):
         for l in self.layers:
             x = l(x)
         x = self.head_ln(linear_gelu(x, self.head))
-        return linear(x, self.tok.weight, self.bias)
+        return linear(x, self.tok.weight, self.bias, logits=True)
 
 
 def bert_base() -> BertMLM:

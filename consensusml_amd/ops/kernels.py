@@ -134,6 +134,32 @@ class GramWorkspace:
         return buf
 
 
+def agg_update_multi(segs, *, combine: str, lo: int = 0, cnt: int = 1,
+                     w: Optional[torch.Tensor] = None, rows: Optional[torch.Tensor] = None,
+                     n: int, opt: Optional[OptArgs] = None, master: Optional[torch.Tensor] = None,
+                     s1: Optional[torch.Tensor] = None, s2: Optional[torch.Tensor] = None,
+                     gout: Optional[torch.Tensor] = None) -> None:
+    """``agg_update`` over several segments in ONE launch on GPU (the sharded engine's buckets).
+    ``segs``: (X [rows, >= D], D, off, param_out) -- worker rows, element count, offset into the
+    shared master / s1 / s2 / gout vectors, and the segment's parameters."""
+    opt = opt or OptArgs(kind="none")
+    if segs and segs[0][0].is_cuda and len(segs) <= 16:
+        bc1 = 1.0 - opt.beta1 ** opt.step
+        bc2 = 1.0 - opt.beta2 ** opt.step
+        lib().agg_update_multi([_as2d(x) for x, _, _, _ in segs], [int(d) for _, d, _, _ in segs],
+                               [int(o) for _, _, o, _ in segs], [p for _, _, _, p in segs], n,
+                               rows, 0 if combine == "sorted" else 1, lo, cnt, w, opt.opt_id(),
+                               master, s1, s2, gout, opt.lr, opt.momentum, opt.weight_decay,
+                               opt.beta1, opt.beta2, opt.eps, opt.lr / bc1, 1.0 / math.sqrt(bc2),
+                               opt.gscale, opt.nesterov, opt.first)
+        return
+    sl = lambda t, o, d: None if t is None else t[o:o + d]   # noqa: E731
+    for X, D, off, pout in segs:
+        agg_update(X, combine=combine, lo=lo, cnt=cnt, w=w, rows=rows, n=n, D=D, opt=opt,
+                   master=sl(master, off, D), s1=sl(s1, off, D), s2=sl(s2, off, D),
+                   param_out=pout, gout=sl(gout, off, D))
+
+
 def gram(X: torch.Tensor, rows: Optional[torch.Tensor] = None, n: Optional[int] = None,
          D: Optional[int] = None, out: Optional[torch.Tensor] = None,
          accumulate: bool = False, center: Optional[torch.Tensor] = None) -> torch.Tensor:

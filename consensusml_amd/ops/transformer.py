@@ -492,6 +492,12 @@ def swiglu(h: torch.Tensor) -> torch.Tensor:
 
 
 # ============================================================================ linear (bias grad)
+def _al16(*ts: Optional[torch.Tensor]) -> bool:
+    """Contiguous and 16-B aligned (gemm.hip reads 16-B vectors: a contiguous view at an odd
+    element offset would fail the launch instead of falling back)."""
+    return all(t is None or (t.is_contiguous() and t.data_ptr() % 16 == 0) for t in ts)
+
+
 def _own_gemm(M: int, N: int, K: int) -> bool:
     """gemm.hip for a bf16 GEMM of this shape: eligible (256-multiples) and enough 256 x 256
     tiles to fill the chip (>= 128; below that hipBLASLt's smaller tiles win, bench/gemm.py)."""
@@ -521,28 +527,45 @@ def _linear_wgrad(gout: torch.Tensor, gin: torch.Tensor) -> torch.Tensor:
     return gout.t() @ gin
 
 
+# persistent zero-padded copies of logits-head weights / biases (padded_logits): keyed by the
+# parameter's identity, refreshed in place each forward (rows N .. Np stay zero), so the padded
+# path costs one weight copy instead of an allocation + zero-fill + copy per step
+_PAD_CACHE = {}
+
+
+def _padded_wb(w: torch.Tensor, b: torch.Tensor, Np: int):
+    key = (id(w), id(b))
+    hit = _PAD_CACHE.get(key)
+    if hit is None or hit[0].shape[0] != Np or hit[0].device != w.device or hit[0].dtype != w.dtype:
+        hit = (w.new_zeros(Np, w.shape[1]), b.new_zeros(Np))
+        _PAD_CACHE[key] = hit
+    wp, bp = hit
+    N = w.shape[0]
+    wp[:N].copy_(w)
+    bp[:N].copy_(b)
+    return wp, bp
+
+
 class _LinearFn(torch.autograd.Function):
     """y = x W^T + b with the bias gradient from the column-sum kernel (PyTorch's generic column
     reduction runs these at ~0.4 TB/s: 7 % of the BERT step in profiles/r01_prof13)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, link):
+    def forward(ctx, x, w, b, link, pad_logits=False):
         ctx.save_for_backward(x, w)
         ctx.link = link
         ctx.params = (w, b)
         x2 = x.reshape(-1, x.shape[-1])
         N = w.shape[0]
-        if _own_gemm(x2.shape[0], N, w.shape[1]) and x2.is_contiguous():
+        if _own_gemm(x2.shape[0], N, w.shape[1]) and _al16(x2, w, b):
             return lib().gemm_nt(x2, w, 0, bias=b).view(*x.shape[:-1], N)
-        if b is not None and N % 8 and x2.shape[0] % 64 == 0 and _P().padded_logits:
-            # N not a multiple of 8 (BERT's MLM head, V = 30522): the GEMM writes rows padded to
-            # Np (zero weight rows / bias), the output is the [.., N] view -- 16-B aligned rows
-            # for the cross-entropy kernels, whose backward then also emits the bias gradient
+        if pad_logits and b is not None and N % 8 and x2.shape[0] % 64 == 0:
+            # logits feeding the cross-entropy (BertMLM's head, V = 30522, not a multiple of 8):
+            # the GEMM writes rows padded to Np (zero weight rows / bias), the output is the
+            # [.., N] view -- 16-B aligned rows for the cross-entropy kernels, whose backward then
+            # also emits the bias gradient
             Np = (N + 7) // 8 * 8
-            wp = w.new_zeros(Np, w.shape[1])
-            wp[:N].copy_(w)
-            bp = b.new_zeros(Np)
-            bp[:N].copy_(b)
+            wp, bp = _padded_wb(w, b, Np)
             y = F.linear(x2, wp, bp)
             return y.view(*x.shape[:-1], Np)[..., :N]
         return F.linear(x, w, b)
@@ -550,7 +573,7 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        return _linear_grads(ctx, dy.reshape(-1, dy.shape[-1]), x, w) + (None,)
+        return _linear_grads(ctx, dy.reshape(-1, dy.shape[-1]), x, w) + (None, None)
 
 
 def _linear_grads(ctx, dy2: torch.Tensor, x: torch.Tensor, w: torch.Tensor):
@@ -563,8 +586,8 @@ def _linear_grads(ctx, dy2: torch.Tensor, x: torch.Tensor, w: torch.Tensor):
     if ctx.needs_input_grad[0]:
         g = ctx.link.take() if ctx.link is not None else None
         K = x.shape[-1]
-        own = _own_gemm(dy2.shape[0], K, w.shape[0]) and dy2.is_contiguous()
-        if own and (g is None or (g.is_contiguous() and g.shape == x.shape)):
+        own = _own_gemm(dy2.shape[0], K, w.shape[0]) and _al16(dy2)
+        if own and (g is None or (_al16(g) and g.shape == x.shape)):
             # data gradient on gemm.hip against the transposed weight, the parked residual
             # gradient added in the epilogue (in place)
             wt = lib().transpose_bf16(w)
@@ -653,20 +676,25 @@ def linear_gelu(x: torch.Tensor, lin: nn.Linear) -> torch.Tensor:
     """gelu(lin(x)) (erf GELU); gemm.hip-eligible bf16 GPU shapes run the fused-epilogue path."""
     w, b = lin.weight, lin.bias
     M = x.numel() // x.shape[-1]
-    if (_P().fused_ffn and _gpu_bf16(x, w, b) and b is not None
+    if (_P().fused_ffn and _gpu_bf16(x, w, b) and b is not None and _al16(w, b)
+            and (not x.is_contiguous() or x.data_ptr() % 16 == 0)
             and _gemm_ok(M, w.shape[0], w.shape[1])):
         return _LinearGeluFn.apply(x, w, b)
     return F.gelu(lin(x))
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
-           link: Optional[ResidualLink] = None) -> torch.Tensor:
+           link: Optional[ResidualLink] = None, logits: bool = False) -> torch.Tensor:
     """``link``: a ResidualLink on which a later-in-forward op (``add_norm(x_link=...)``) parks
-    another gradient of x; this GEMM's data-gradient absorbs it (beta = 1)."""
+    another gradient of x; this GEMM's data-gradient absorbs it (beta = 1). ``logits``: the
+    output only feeds ``cross_entropy`` -- with N % 8 != 0 it may come back as a view of
+    16-B aligned padded rows (PerfPolicy.padded_logits); other callers always get a plain
+    contiguous [.., N] tensor."""
     wg = WG.current()
-    if _gpu_bf16(x, w, b) and ((b is not None and (w.shape[0] % 8 == 0 or _P().padded_logits))
+    pad = logits and _P().padded_logits
+    if _gpu_bf16(x, w, b) and ((b is not None and (w.shape[0] % 8 == 0 or pad))
                                or (wg is not None and wg.has(w))):
-        return _LinearFn.apply(x, w, b, link)
+        return _LinearFn.apply(x, w, b, link, pad)
     return F.linear(x, w, b)
 
 
@@ -717,7 +745,7 @@ class _FFNGeluFn(torch.autograd.Function):
         M, F1 = x2.shape[0], w1.shape[0]
         h = torch.empty(M, F1, dtype=x.dtype, device=x.device)
         a = lib().gemm_nt(x2, w1, 1, bias=b1, aux=h)
-        y = (lib().gemm_nt(a, w2, 0, bias=b2) if _own_gemm(M, w2.shape[0], F1)
+        y = (lib().gemm_nt(a, w2, 0, bias=b2) if _own_gemm(M, w2.shape[0], F1) and _al16(w2, b2)
              else F.linear(a, w2, b2))
         ctx.save_for_backward(x2, w1, w2, h, a)
         ctx.link = link
@@ -733,7 +761,9 @@ class _FFNGeluFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         wg = WG.current()
-        V = wg.V if wg is not None and (wg.has(pb1) or wg.has(pw1)) else 1
+        # per-worker fc1 bias-gradient rows only when the batched-workers object owns b1 (else
+        # one [1, N] total, returned to autograd below)
+        V = wg.V if wg is not None and wg.has(pb1) else 1
         cs, post = _bias_grad_rows(pb1, V)
         dh = lib().gemm_nt(dy2, lib().transpose_bf16(w2), 2, aux=h, colsum_out=cs)
         if post is not None:
@@ -743,7 +773,7 @@ class _FFNGeluFn(torch.autograd.Function):
             g = ctx.link.take() if ctx.link is not None else None
             K = x2.shape[-1]
             if _own_gemm(dh.shape[0], K, dh.shape[1]) and (
-                    g is None or (g.is_contiguous() and g.shape == ctx.xshape)):
+                    g is None or (_al16(g) and g.shape == ctx.xshape)):
                 w1t = lib().transpose_bf16(w1)
                 if g is not None:
                     g2 = g.view(-1, K)
@@ -770,13 +800,18 @@ class _FFNGeluFn(torch.autograd.Function):
                     torch.bmm(A, Bm, out=dst.view(wg.V, pw.shape[0], pw.shape[1]))
                 else:
                     dst.view(wg.V, pw.shape[0], pw.shape[1]).baddbmm_(A, Bm)
+            db2 = None
             if wg.has(pb2):
                 dst, first = wg.out(pb2)
                 if first:
                     lib().colsum_seg(dy2, wg.V, dst.view(wg.V, -1))
                 else:
                     dst.view(wg.V, -1).add_(dy2.view(wg.V, T, -1).sum(1))
-            return dx, None, None, None, None, None
+            elif ctx.needs_input_grad[4]:
+                db2 = lib().colsum(dy2)
+            # biases the workers object does not own still get their (summed) gradients
+            db1 = cs.view(-1) if (not wg.has(pb1) and ctx.needs_input_grad[2]) else None
+            return dx, None, db1, None, db2, None
         dw1 = _linear_wgrad(dh, x2) if ctx.needs_input_grad[1] else None
         db1 = cs.view(-1) if ctx.needs_input_grad[2] else None
         dw2 = _linear_wgrad(dy2, a) if ctx.needs_input_grad[3] else None
@@ -792,7 +827,9 @@ def ffn_gelu(x: torch.Tensor, fc1: nn.Linear, fc2: nn.Linear,
     M = x.numel() // x.shape[-1]
     wg = WG.current()
     ok = (_P().fused_ffn and _gpu_bf16(x, w1, b1, w2, b2) and b1 is not None
-          and b2 is not None and _gemm_ok(M, w1.shape[0], w1.shape[1])
+          and b2 is not None and _al16(w1, b1, w2, b2)
+          and (not x.is_contiguous() or x.data_ptr() % 16 == 0)
+          and _gemm_ok(M, w1.shape[0], w1.shape[1])
           and _gemm_ok(M, w1.shape[0], w2.shape[0]) and w2.shape[0] % 8 == 0
           and (wg is None or M % (128 * wg.V) == 0))
     if ok:

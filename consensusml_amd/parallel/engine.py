@@ -200,13 +200,17 @@ class ConsensusEngine:
         self._gram_done: set = set()
         self.early_grams = 0       # bucket Grams computed before step() (all steps)
         self._gram_eager = False   # tests: wait for each exchange in its hook (forces the path)
-        # GPU ordering of the early Grams: bucket b's Gram is enqueued at its flush on a side
-        # stream that waits (device-side) for the main stream's work so far and for b's
-        # collective, so it runs as soon as the exchange lands, beside the rest of backward, with
-        # no host polling (a host-side is_completed() poll sees nothing finished: the host runs
-        # ahead of the GPU). CPU / gloo runs keep the polled form.
-        self._gram_stream = (torch.cuda.Stream(device=dev)
-                             if self.early_gram and dev.type == "cuda" else None)
+        # GPU ordering of the early Grams, no host polling (a host-side is_completed() poll
+        # sees nothing finished: the host runs ahead of the GPU). Bucket b's Gram is enqueued on
+        # the compute stream at the flush of bucket b + gram_lag, behind a device-side wait for
+        # b's collective -- by then one bucket of backward has run since that collective was
+        # issued, so the wait is normally already satisfied, and the small Gram kernel slots in
+        # between backward kernels. (A side stream waiting on each collective measured 1.5 ms /
+        # step SLOWER at batch 256: the extra stream's waits share hardware queues with the
+        # compute stream, profiles/r05_02/bench.json.) CPU / gloo runs keep the polled form.
+        self._gram_queue: List[Bucket] = []
+        self._gram_ordered = self.early_gram and dev.type == "cuda"
+        self.gram_lag = max(0, int(cfg.topology.gram_lag))
         # training-side consensus table (SURVEY.md §5.4 b): when set, the next step() records
         # per-worker / per-parameter gradient statistics (consensus_table())
         self.record_stats = False
@@ -227,6 +231,7 @@ class ConsensusEngine:
         self._flushed.clear()
         self._pending.clear()
         self._gram_done.clear()
+        self._gram_queue.clear()
         self.flat.grad_row = 0
 
     def bind_worker(self, v: int) -> None:
@@ -391,8 +396,11 @@ class ConsensusEngine:
         if self.overlap and b.index not in self._pending:
             self._launch_bucket(b, inject=True)
             if self.early_gram:
-                if self._gram_stream is not None:
-                    self._enqueue_gram(b)
+                if self._gram_ordered:
+                    self._gram_queue.append(b)
+                    while len(self._gram_queue) > self.gram_lag:
+                        self._bucket_gram(self._gram_queue.pop(0))
+                        self.early_grams += 1
                 else:
                     self._poll_grams()
         if self.early_update and complete:
@@ -468,24 +476,6 @@ class ConsensusEngine:
         K.gram(X, n=self.rows_total, D=length, out=self.Gb[b.index], center=self._pass_center())
         self._gram_done.add(b.index)
 
-    def _enqueue_gram(self, b: Bucket) -> None:
-        """Bucket b's Gram partial on the side stream, ordered after b's flush (main stream) and
-        b's collective (``work.wait()`` inside the side-stream context: a device-side wait)."""
-        if b.index in self._gram_done:
-            return
-        st = self._gram_stream
-        st.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(st):
-            w = self._pending.get(b.index)
-            if w is not None:
-                w.wait()
-            X = self._cclip_rows(b) if self.rule == "centered_clip" else self._rows(b)
-            length = b.shard if self.topo == "sharded" else X.shape[1]
-            K.gram(X, n=self.rows_total, D=length, out=self.Gb[b.index],
-                   center=self._pass_center())
-        self._gram_done.add(b.index)
-        self.early_grams += 1
-
     def _poll_grams(self) -> None:
         """Gram partials of every bucket whose exchange has completed (non-blocking test), so
         they run during backward instead of after the last all-to-all."""
@@ -556,8 +546,7 @@ class ConsensusEngine:
         if self.early_gram:
             # per-bucket partials (computed during backward), summed in bucket order in one
             # launch: G = ((g0 + g1) + g2) ..., the same fp64 adds as accumulating bucket by bucket
-            if self._gram_stream is not None:
-                torch.cuda.current_stream(self.device).wait_stream(self._gram_stream)
+            self._gram_queue.clear()
             for b, _, _ in cols:
                 self._bucket_gram(b)
             K.gram_sum(self.Gb, self.G)
@@ -626,6 +615,23 @@ class ConsensusEngine:
             K.agg_update(X, combine="weighted", w=self.w, n=self.rows_total, D=length, opt=opt,
                          master=m, s1=s1, s2=s2, param_out=param_out, gout=gout)
 
+    def _aggregate_update_multi(self, segs, opt: K.OptArgs) -> None:
+        """``_aggregate_update`` of several buckets in one launch: segs = (X, length, pout, soff)."""
+        cfg = self.cfg.agg
+        ks = [(X, length, soff, pout) for X, length, pout, soff in segs]
+        st = dict(master=self.master, s1=self.s1, s2=self.s2, opt=opt)
+        if self.rule in ("median", "trimmed_mean"):
+            trim = cfg.trim if cfg.trim is not None else cfg.f
+            lo, cnt = K.sorted_range(self.rule, self.n, trim)
+            K.agg_update_multi(ks, combine="sorted", lo=lo, cnt=cnt, n=self.n, **st)
+        elif self.rule == "bulyan":
+            theta = self.n - 2 * cfg.f
+            lo, cnt = K.sorted_range("trimmed_mean", theta, cfg.f)
+            K.agg_update_multi(ks, combine="sorted", lo=lo, cnt=cnt, rows=self.sel[:theta],
+                               n=theta, **st)
+        else:
+            K.agg_update_multi(ks, combine="weighted", w=self.w, n=self.rows_total, **st)
+
     # ================================================================ topologies
     def _step_allreduce(self) -> None:
         fl = self.flat
@@ -666,18 +672,26 @@ class ConsensusEngine:
             self._record_stats(cols)
         opt = self._opt_args()
         works = []
-        # earliest layers (highest bucket index) first: the next forward needs them first
-        for b, X, length in (reversed(cols) if self.param_prefetch else cols):
+        order = list(reversed(cols)) if self.param_prefetch else cols
+
+        def shard(b):
             if self.group_active:
-                pout = fl.my_shard(fl.flat_param, b, self.rank)
-                soff = b.shard_offset
-            else:
-                pout = fl.flat_param[b.offset:b.offset + b.length]
-                soff = b.offset
-            gout = self.gout[soff:soff + length] if self.gout is not None else None
-            self._aggregate_update(b, X, length, soff, pout, opt, gout)
-            if self.rule == "centered_clip":
-                X[self.n, :length].copy_(gout.to(X.dtype))
+                return fl.my_shard(fl.flat_param, b, self.rank), b.shard_offset
+            return fl.flat_param[b.offset:b.offset + b.length], b.offset
+
+        # every bucket's rule + optimizer step in ONE launch (centered clipping writes its
+        # aggregate back into each bucket's rows, so it stays per bucket)
+        fused = self.rule != "centered_clip" and 1 <= len(cols) <= 16 and self.device.type == "cuda"
+        if fused:
+            self._aggregate_update_multi([(X, length) + shard(b) for b, X, length in order], opt)
+        # earliest layers (highest bucket index) first: the next forward needs them first
+        for b, X, length in order:
+            pout, soff = shard(b)
+            if not fused:
+                gout = self.gout[soff:soff + length] if self.gout is not None else None
+                self._aggregate_update(b, X, length, soff, pout, opt, gout)
+                if self.rule == "centered_clip":
+                    X[self.n, :length].copy_(gout.to(X.dtype))
             if self.group_active:
                 full = fl.flat_param[b.offset:b.offset + b.length]
                 work = dist.all_gather_into_tensor(full, pout, async_op=True)

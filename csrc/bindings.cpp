@@ -98,6 +98,78 @@ void agg_update(const Tensor& X, int64_t n, int64_t D, const optional<Tensor>& r
                                        s, u, D, cur_stream()));
 }
 
+// The same rule + optimizer over several segments (the sharded engine's buckets) in one launch:
+// segment i = worker rows Xs[i] (first Ds[i] columns), state elements [offs[i], offs[i] + Ds[i])
+// of master / s1 / s2 / gout, parameters pouts[i] (bf16 or fp32, >= Ds[i] elements).
+void agg_update_multi(const std::vector<Tensor>& Xs, const std::vector<int64_t>& Ds,
+                      const std::vector<int64_t>& offs, const std::vector<Tensor>& pouts, int64_t n,
+                      const optional<Tensor>& rows, int64_t combine, int64_t lo, int64_t cnt,
+                      const optional<Tensor>& w, int64_t opt, const optional<Tensor>& master,
+                      const optional<Tensor>& s1, const optional<Tensor>& s2,
+                      const optional<Tensor>& gout, double lr, double momentum,
+                      double weight_decay, double beta1, double beta2, double eps,
+                      double step_size, double inv_sqrt_bc2, double gscale, bool nesterov,
+                      bool first) {
+  const size_t ns = Xs.size();
+  TORCH_CHECK(ns >= 1 && ns <= 16 && Ds.size() == ns && offs.size() == ns && pouts.size() == ns,
+              "agg_update_multi: 1..16 segments with matching Xs / Ds / offs / pouts");
+  TORCH_CHECK(n >= 1 && n <= 64, "1 <= n <= 64 workers supported, got ", n);
+  const int adam_l2 = opt == 3 ? 1 : 0;
+  if (adam_l2) opt = cml::OPT_ADAM;
+  const at::ScalarType xt = Xs[0].scalar_type();
+  const bool pf32 = pouts[0].scalar_type() == at::kFloat;
+  int64_t need = 0;
+  std::vector<cml::AggSeg> segs(ns);
+  for (size_t i = 0; i < ns; ++i) {
+    const Tensor& X = Xs[i];
+    check_dev(X, "X");
+    TORCH_CHECK(X.get_device() == Xs[0].get_device() && X.scalar_type() == xt,
+                "agg_update_multi: Xs on one device with one dtype");
+    TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1, "X must be 2-D with unit column stride");
+    TORCH_CHECK(Ds[i] >= 0 && Ds[i] <= X.size(1) && offs[i] >= 0, "segment D / off out of range");
+    if (!(rows.has_value() && rows->defined())) TORCH_CHECK(X.size(0) >= n, "X has fewer rows than n");
+    const Tensor& P = pouts[i];
+    check_dev(P, "param_out");
+    TORCH_CHECK(P.is_contiguous() && P.numel() >= Ds[i] &&
+                    P.scalar_type() == (pf32 ? at::kFloat : at::kBFloat16),
+                "param_out: contiguous, >= D elements, one dtype");
+    segs[i] = cml::AggSeg{X.data_ptr(), X.stride(0), Ds[i], offs[i], P.data_ptr()};
+    need = std::max(need, offs[i] + Ds[i]);
+  }
+  const c10::DeviceGuard guard(Xs[0].device());
+  cml::SrcArgs s{};
+  s.n = static_cast<int>(n);
+  s.rows = opt_ptr<const int>(rows, at::kInt, "rows", n);
+  s.w = opt_ptr<const float>(w, at::kFloat, "w", n);
+  s.lo = static_cast<int>(lo);
+  s.cnt = static_cast<int>(cnt);
+  cml::UpdArgs u{};
+  u.master = opt_ptr<float>(master, at::kFloat, "master", need);
+  u.s1 = opt_ptr<float>(s1, at::kFloat, "s1", need);
+  u.s2 = opt_ptr<float>(s2, at::kFloat, "s2", need);
+  u.gout = opt_ptr<float>(gout, at::kFloat, "gout", need);
+  u.param_f32 = pf32 ? 1 : 0;
+  if (opt != cml::OPT_NONE) TORCH_CHECK(u.master, "optimizer update needs master weights");
+  if (opt == cml::OPT_SGD && momentum != 0.0) TORCH_CHECK(u.s1, "SGD momentum needs s1");
+  if (opt == cml::OPT_ADAM) TORCH_CHECK(u.s1 && u.s2, "Adam needs s1 and s2");
+  if (opt == cml::OPT_NONE) TORCH_CHECK(u.gout, "OPT_NONE needs gout");
+  u.lr = static_cast<float>(lr);
+  u.momentum = static_cast<float>(momentum);
+  u.weight_decay = static_cast<float>(weight_decay);
+  u.beta1 = static_cast<float>(beta1);
+  u.beta2 = static_cast<float>(beta2);
+  u.eps = static_cast<float>(eps);
+  u.step_size = static_cast<float>(step_size);
+  u.inv_sqrt_bc2 = static_cast<float>(inv_sqrt_bc2);
+  u.gscale = static_cast<float>(gscale);
+  u.nesterov = nesterov ? 1 : 0;
+  u.first = first ? 1 : 0;
+  u.adam_l2 = adam_l2;
+  CML_CHECK_HIP(cml::launch_agg_update_multi(dtype_of(Xs[0]), static_cast<int>(combine),
+                                             static_cast<int>(opt), s, u, segs.data(),
+                                             static_cast<int>(ns), cur_stream()));
+}
+
 int64_t gram_workspace_bytes(int64_t n, int64_t D) {
   return static_cast<int64_t>(cml::gram_workspace_bytes(static_cast<int>(n), D));
 }
@@ -1780,7 +1852,7 @@ void check_flash_qkv(const Tensor& q, const Tensor& k, const Tensor& v) {
 }
 
 std::vector<Tensor> flash_fwd(const Tensor& q, const Tensor& k, const Tensor& v, bool causal,
-                              double scale) {
+                              double scale, double rescale_thr) {
   check_flash_qkv(q, k, v);
   const int64_t B = q.size(0), H = q.size(1), S = q.size(2), KV = k.size(1);
   const c10::DeviceGuard guard(q.device());
@@ -1789,7 +1861,8 @@ std::vector<Tensor> flash_fwd(const Tensor& q, const Tensor& k, const Tensor& v,
   CML_CHECK_HIP(cml::launch_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
                                       lse.data_ptr<float>(), static_cast<int>(B), static_cast<int>(H),
                                       static_cast<int>(KV), static_cast<int>(S),
-                                      static_cast<float>(scale), causal, cur_stream()));
+                                      static_cast<float>(scale), causal, cur_stream(),
+                                      static_cast<float>(rescale_thr)));
   return {o, lse};
 }
 
@@ -2038,12 +2111,37 @@ Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tens
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K, "gemm_nt: K mismatch");
   TORCH_CHECK(cml::gemm_nt_eligible(M, N, K), "gemm_nt: needs M % 256 == 0, N % 256 == 0, K % 64 == 0");
+  // every operand on a's device and aligned for its vector width (16-B rows of a / b / y / aux /
+  // cin, 8-B bias reads): a misaligned pointer must be a TORCH_CHECK, not a device fault
+  auto same_dev = [&](const optional<Tensor>& t, const char* name) {
+    if (t.has_value() && t->defined())
+      TORCH_CHECK(t->is_cuda() && t->get_device() == a.get_device(), "gemm_nt: ", name,
+                  " must be on a's device");
+  };
+  auto aligned = [](const Tensor& t, int bytes) {
+    return (reinterpret_cast<uintptr_t>(t.data_ptr()) % bytes) == 0;
+  };
+  TORCH_CHECK(b.get_device() == a.get_device(), "gemm_nt: b must be on a's device");
+  same_dev(bias, "bias");
+  same_dev(aux, "aux");
+  same_dev(out, "out");
+  same_dev(colsum_out, "colsum_out");
+  same_dev(cin, "cin");
+  TORCH_CHECK(aligned(a, 16) && aligned(b, 16) && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0,
+              "gemm_nt: a / b need 16-B aligned rows");
+  if (bias.has_value() && bias->defined()) TORCH_CHECK(aligned(*bias, 8), "gemm_nt: bias must be 8-B aligned");
+  if (cin.has_value() && cin->defined()) TORCH_CHECK(aligned(*cin, 16), "gemm_nt: cin must be 16-B aligned");
+  if (aux.has_value() && aux->defined()) TORCH_CHECK(aligned(*aux, 16), "gemm_nt: aux must be 16-B aligned");
+  if (colsum_out.has_value() && colsum_out->defined())
+    TORCH_CHECK(colsum_out->scalar_type() == at::kFloat || colsum_out->scalar_type() == at::kBFloat16,
+                "colsum_out: bf16 or fp32");
   const c10::DeviceGuard guard(a.device());
   Tensor y;
   if (out.has_value() && out->defined()) {
     y = *out;
     TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 2 && y.size(0) == M &&
-                y.size(1) == N && y.stride(1) == 1, "gemm_nt: out must be bf16 [M, N]");
+                y.size(1) == N && y.stride(1) == 1 && aligned(y, 16) && y.stride(0) % 8 == 0,
+                "gemm_nt: out must be bf16 [M, N] with 16-B aligned rows");
   } else {
     y = at::empty({M, N}, a.options());
   }
@@ -2080,7 +2178,6 @@ Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tens
   CML_CHECK_HIP(cml::launch_gemm_nt(g, static_cast<int>(ep), cur_stream()));
   if (cs) {
     const bool f32 = colsum_out->scalar_type() == at::kFloat;
-    TORCH_CHECK(f32 || colsum_out->scalar_type() == at::kBFloat16, "colsum_out: bf16 or fp32");
     CML_CHECK_HIP(cml::launch_colsum_fold(part.data_ptr<float>(), M, static_cast<int>(N),
                                           static_cast<int>(colsum_out->size(0)),
                                           colsum_out->data_ptr(), colsum_out->stride(0),
@@ -2190,6 +2287,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sel"), py::arg("guard") = false, py::arg("center_out") = py::none(),
         py::arg("sel_counts") = py::none());
   m.def("gram_sum", &gram_sum, "sum of per-bucket Gram partials in bucket order");
+  m.def("agg_update_multi", &agg_update_multi,
+        "fused robust aggregation + optimizer step over several buckets in one launch");
   m.def("gossip_workspace_bytes", &gossip_workspace_bytes);
   m.def("gossip_mix", &gossip_mix, "ring gossip mixing with neighbour clipping");
   m.def("gossip_mix_k", &gossip_mix_k, "k-neighbour gossip mixing with neighbour clipping");
@@ -2302,7 +2401,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rope_bwd", &rope_bwd, "inverse of rope_fwd (grp > 1: sums per-query-head dk / dv)",
         py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("cos"), py::arg("sin"),
         py::arg("grp") = 1);
-  m.def("flash_fwd", &flash_fwd, "flash attention forward, head dim 128, GQA, causal / full");
+  m.def("flash_fwd", &flash_fwd, "flash attention forward, head dim 128, GQA, causal / full",
+        py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"), py::arg("scale"),
+        py::arg("rescale_thr") = 8.0);
   m.def("flash_bwd", &flash_bwd, "flash attention backward (dq, per-query-head dk / dv)");
   m.def("swiglu_fwd", &swiglu_fwd, "silu(a) * b over [a | b]");
   m.def("swiglu_bwd", &swiglu_bwd, "SwiGLU backward");

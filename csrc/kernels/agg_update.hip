@@ -20,6 +20,7 @@ namespace cml {
 
 constexpr int kBlock = 256;
 constexpr int kMaxRows = 64;
+constexpr int kMaxSegs = 16;   // segments of one multi-segment launch
 
 // Optimizer state of VEC coordinates, loaded BEFORE the combine so those HBM reads are in flight
 // while the sort / weighted sum runs (hipcc does not hoist them above the VALU work by itself).
@@ -107,8 +108,8 @@ __device__ __forceinline__ void update_and_store(const UpdArgs& u, int opt, int6
 // fp32 rows (and the bf16 scalar tail): sort fp32 values. The rank window [lo, lo+cnt) is
 // wave-uniform (kernel arguments), so the per-rank test is a scalar branch, not a VALU select.
 template <typename T, int NP, int VEC, int OPT>
-__global__ __launch_bounds__(kBlock) void agg_sorted_kernel(SrcArgs s, UpdArgs u, int64_t base,
-                                                            int64_t nvec) {
+__device__ __forceinline__ void agg_sorted_body(const SrcArgs& s, const UpdArgs& u, int64_t base,
+    int64_t nvec, int blk, int nblk) {
   const T* X = reinterpret_cast<const T*>(s.X);
   int64_t roff[NP];
 #pragma unroll
@@ -118,8 +119,8 @@ __global__ __launch_bounds__(kBlock) void agg_sorted_kernel(SrcArgs s, UpdArgs u
   }
   const float inf = __builtin_inff();
   const float inv = 1.0f / static_cast<float>(s.cnt);
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < nvec; t += stride) {
+  const int64_t stride = static_cast<int64_t>(nblk) * kBlock;
+  for (int64_t t = static_cast<int64_t>(blk) * kBlock + threadIdx.x; t < nvec; t += stride) {
     const int64_t e = t * VEC;
     float a[NP][VEC];
 #pragma unroll
@@ -171,8 +172,8 @@ template <> struct Words<1> {
 };
 
 template <int NP, int VEC, int OPT>
-__global__ __launch_bounds__(kBlock) void agg_sorted_bf16_kernel(SrcArgs s, UpdArgs u,
-                                                                 int64_t base, int64_t nvec) {
+__device__ __forceinline__ void agg_sorted_bf16_body(const SrcArgs& s, const UpdArgs& u, int64_t base,
+    int64_t nvec, int blk, int nblk) {
   constexpr int W = VEC / 2;
   const bf16* X = reinterpret_cast<const bf16*>(s.X);
   int64_t roff[NP];
@@ -183,8 +184,8 @@ __global__ __launch_bounds__(kBlock) void agg_sorted_bf16_kernel(SrcArgs s, UpdA
   }
   const float inv = 1.0f / static_cast<float>(s.cnt);
   const u16x2 kinf = {kKeyInf, kKeyInf};
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < nvec; t += stride) {
+  const int64_t stride = static_cast<int64_t>(nblk) * kBlock;
+  for (int64_t t = static_cast<int64_t>(blk) * kBlock + threadIdx.x; t < nvec; t += stride) {
     const int64_t e = t * VEC;
     uint32_t raw[NP][W];
 #pragma unroll
@@ -222,8 +223,8 @@ __global__ __launch_bounds__(kBlock) void agg_sorted_bf16_kernel(SrcArgs s, UpdA
 
 // ----------------------------------------------------------------------------- weighted combine
 template <typename T, int VEC, int OPT>
-__global__ __launch_bounds__(kBlock) void agg_weighted_kernel(SrcArgs s, UpdArgs u, int64_t base,
-                                                              int64_t nvec) {
+__device__ __forceinline__ void agg_weighted_body(const SrcArgs& s, const UpdArgs& u, int64_t base,
+    int64_t nvec, int blk, int nblk) {
   // Compact the non-zero weights once per workgroup (LDS, broadcast reads in the loop).
   __shared__ int64_t s_off[kMaxRows];
   __shared__ float s_w[kMaxRows];
@@ -243,8 +244,8 @@ __global__ __launch_bounds__(kBlock) void agg_weighted_kernel(SrcArgs s, UpdArgs
   __syncthreads();
   const int nz = s_nz;
   const T* X = reinterpret_cast<const T*>(s.X);
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; t < nvec; t += stride) {
+  const int64_t stride = static_cast<int64_t>(nblk) * kBlock;
+  for (int64_t t = static_cast<int64_t>(blk) * kBlock + threadIdx.x; t < nvec; t += stride) {
     const int64_t e = t * VEC;
     OptState<VEC> st;
     load_state<VEC>(u, OPT, base + e, st);
@@ -272,6 +273,63 @@ __global__ __launch_bounds__(kBlock) void agg_weighted_kernel(SrcArgs s, UpdArgs
     }
     update_and_store<VEC>(u, OPT, base + e, g, st);
   }
+}
+
+
+// ----------------------------------------------------------------------------- kernels
+// Single segment (one bucket / one vector): grid-stride over nvec vectors.
+template <typename T, int NP, int VEC, int OPT>
+__global__ __launch_bounds__(kBlock) void agg_sorted_kernel(SrcArgs s, UpdArgs u, int64_t base,
+                                                            int64_t nvec) {
+  agg_sorted_body<T, NP, VEC, OPT>(s, u, base, nvec, blockIdx.x, gridDim.x);
+}
+template <int NP, int VEC, int OPT>
+__global__ __launch_bounds__(kBlock) void agg_sorted_bf16_kernel(SrcArgs s, UpdArgs u,
+                                                                 int64_t base, int64_t nvec) {
+  agg_sorted_bf16_body<NP, VEC, OPT>(s, u, base, nvec, blockIdx.x, gridDim.x);
+}
+template <typename T, int VEC, int OPT>
+__global__ __launch_bounds__(kBlock) void agg_weighted_kernel(SrcArgs s, UpdArgs u, int64_t base,
+                                                              int64_t nvec) {
+  agg_weighted_body<T, VEC, OPT>(s, u, base, nvec, blockIdx.x, gridDim.x);
+}
+
+// Several segments in ONE launch (the sharded engine's buckets: per-bucket worker matrices and
+// parameter shards, one fp32 optimizer-state vector): blockIdx.y = segment. Every segment is on
+// the vector path (checked by the launcher).
+struct SegTable {
+  const void* X[kMaxSegs];
+  int64_t ld[kMaxSegs];
+  int64_t nvec[kMaxSegs];
+  int64_t off[kMaxSegs];     // element offset into master / s1 / s2 / gout
+  void* pout[kMaxSegs];
+};
+
+__device__ __forceinline__ void seg_args(const SegTable& t, int sg, SrcArgs& s, UpdArgs& u) {
+  s.X = t.X[sg];
+  s.ld = t.ld[sg];
+  const int64_t o = t.off[sg];
+  if (u.master) u.master += o;
+  if (u.s1) u.s1 += o;
+  if (u.s2) u.s2 += o;
+  if (u.gout) u.gout += o;
+  u.param_out = t.pout[sg];
+}
+
+template <typename T, int NP, int VEC, int OPT>
+__global__ __launch_bounds__(kBlock) void agg_sorted_multi(SrcArgs s, UpdArgs u, SegTable t) {
+  seg_args(t, blockIdx.y, s, u);
+  agg_sorted_body<T, NP, VEC, OPT>(s, u, 0, t.nvec[blockIdx.y], blockIdx.x, gridDim.x);
+}
+template <int NP, int VEC, int OPT>
+__global__ __launch_bounds__(kBlock) void agg_sorted_bf16_multi(SrcArgs s, UpdArgs u, SegTable t) {
+  seg_args(t, blockIdx.y, s, u);
+  agg_sorted_bf16_body<NP, VEC, OPT>(s, u, 0, t.nvec[blockIdx.y], blockIdx.x, gridDim.x);
+}
+template <typename T, int VEC, int OPT>
+__global__ __launch_bounds__(kBlock) void agg_weighted_multi(SrcArgs s, UpdArgs u, SegTable t) {
+  seg_args(t, blockIdx.y, s, u);
+  agg_weighted_body<T, VEC, OPT>(s, u, 0, t.nvec[blockIdx.y], blockIdx.x, gridDim.x);
 }
 
 // ----------------------------------------------------------------------------- dispatch
@@ -370,6 +428,98 @@ static hipError_t agg_update_t(int combine, int opt, const SrcArgs& s, const Upd
     else launch_sorted<T, false>(opt, s, u, Dv, D - Dv, st);
   }
   return hipGetLastError();
+}
+
+template <typename T, int NP, int VEC>
+static void launch_sorted_multi_np(int opt, const SrcArgs& s, const UpdArgs& u, const SegTable& t,
+                                   dim3 g, hipStream_t st) {
+  if constexpr (sizeof(T) == 2 && VEC >= 2) {
+    switch (opt) {
+      case OPT_NONE: agg_sorted_bf16_multi<NP, VEC, OPT_NONE><<<g, kBlock, 0, st>>>(s, u, t); break;
+      case OPT_SGD: agg_sorted_bf16_multi<NP, VEC, OPT_SGD><<<g, kBlock, 0, st>>>(s, u, t); break;
+      default: agg_sorted_bf16_multi<NP, VEC, OPT_ADAM><<<g, kBlock, 0, st>>>(s, u, t); break;
+    }
+  } else {
+    switch (opt) {
+      case OPT_NONE: agg_sorted_multi<T, NP, VEC, OPT_NONE><<<g, kBlock, 0, st>>>(s, u, t); break;
+      case OPT_SGD: agg_sorted_multi<T, NP, VEC, OPT_SGD><<<g, kBlock, 0, st>>>(s, u, t); break;
+      default: agg_sorted_multi<T, NP, VEC, OPT_ADAM><<<g, kBlock, 0, st>>>(s, u, t); break;
+    }
+  }
+}
+
+template <typename T>
+static hipError_t agg_update_multi_t(int combine, int opt, const SrcArgs& s, const UpdArgs& u,
+                                     const AggSeg* segs, int nseg, hipStream_t st) {
+  const int esz = sizeof(T);
+  const int vec = combine == CMB_WEIGHTED ? (esz == 2 ? 8 : 4)
+                                          : sorted_vec(esz == 2 ? DT_BF16 : DT_F32, s.n);
+  bool ok = nseg >= 1 && nseg <= kMaxSegs;
+  SegTable t{};
+  int64_t maxv = 0;
+  for (int i = 0; ok && i < nseg; ++i) {
+    const AggSeg& g = segs[i];
+    const int64_t o = g.off;
+    ok = g.D > 0 && g.D % vec == 0 && (g.ld % vec) == 0 && aligned(g.X, vec * esz) &&
+         o % vec == 0 && aligned(u.master, vec * 4) && aligned(u.s1, vec * 4) &&
+         aligned(u.s2, vec * 4) && aligned(u.gout, vec * 4) &&
+         aligned(g.param_out, vec * (u.param_f32 ? 4 : 2));
+    t.X[i] = g.X;
+    t.ld[i] = g.ld;
+    t.nvec[i] = g.D / vec;
+    t.off[i] = o;
+    t.pout[i] = g.param_out;
+    maxv = t.nvec[i] > maxv ? t.nvec[i] : maxv;
+  }
+  if (!ok) {   // per-segment launches (unaligned / ragged segments)
+    for (int i = 0; i < nseg; ++i) {
+      SrcArgs s1 = s;
+      s1.X = segs[i].X;
+      s1.ld = segs[i].ld;
+      UpdArgs u1 = u;
+      const int64_t o = segs[i].off;
+      if (u1.master) u1.master += o;
+      if (u1.s1) u1.s1 += o;
+      if (u1.s2) u1.s2 += o;
+      if (u1.gout) u1.gout += o;
+      u1.param_out = segs[i].param_out;
+      hipError_t e = agg_update_t<T>(combine, opt, s1, u1, segs[i].D, st);
+      if (e != hipSuccess) return e;
+    }
+    return hipGetLastError();
+  }
+  int gx = grid_for(maxv);
+  const int cap = 2048 / nseg;
+  if (gx > cap) gx = cap < 1 ? 1 : cap;
+  const dim3 g(static_cast<unsigned>(gx), static_cast<unsigned>(nseg));
+  if (combine == CMB_WEIGHTED) {
+    constexpr int V = sizeof(T) == 2 ? 8 : 4;
+    switch (opt) {
+      case OPT_NONE: agg_weighted_multi<T, V, OPT_NONE><<<g, kBlock, 0, st>>>(s, u, t); break;
+      case OPT_SGD: agg_weighted_multi<T, V, OPT_SGD><<<g, kBlock, 0, st>>>(s, u, t); break;
+      default: agg_weighted_multi<T, V, OPT_ADAM><<<g, kBlock, 0, st>>>(s, u, t); break;
+    }
+  } else {
+    constexpr bool BF = sizeof(T) == 2;
+    const int n = s.n;
+    if (n <= 2) launch_sorted_multi_np<T, 2, BF ? 8 : 4>(opt, s, u, t, g, st);
+    else if (n <= 4) launch_sorted_multi_np<T, 4, BF ? 8 : 4>(opt, s, u, t, g, st);
+    else if (n <= 8) launch_sorted_multi_np<T, 8, BF ? 8 : 4>(opt, s, u, t, g, st);
+    else if (n <= 16) launch_sorted_multi_np<T, 16, BF ? 8 : 4>(opt, s, u, t, g, st);
+    else if (n <= 32) launch_sorted_multi_np<T, 32, BF ? 8 : 4>(opt, s, u, t, g, st);
+    else launch_sorted_multi_np<T, 64, 2>(opt, s, u, t, g, st);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_agg_update_multi(int dtype, int combine, int opt, const SrcArgs& src,
+                                   const UpdArgs& upd, const AggSeg* segs, int nseg,
+                                   hipStream_t stream) {
+  if (src.n < 1 || src.n > kMaxRows || nseg < 1) return hipErrorInvalidValue;
+  if (combine == CMB_SORTED && (src.cnt < 1 || src.lo < 0 || src.lo + src.cnt > src.n))
+    return hipErrorInvalidValue;
+  if (dtype == DT_BF16) return agg_update_multi_t<bf16>(combine, opt, src, upd, segs, nseg, stream);
+  return agg_update_multi_t<float>(combine, opt, src, upd, segs, nseg, stream);
 }
 
 hipError_t launch_agg_update(int dtype, int combine, int opt, const SrcArgs& src,

@@ -76,6 +76,7 @@ struct FaArgs {
   int B, H, KV, S;
   float c;                // scale * log2(e)
   float scale;
+  float thr;              // forward: deferred-rescale threshold (log2 units), see fa_fwd_kernel
 };
 
 __device__ __forceinline__ f32x16 mfma(bf16x8_t a, bf16x8_t b, f32x16 c) {
@@ -114,6 +115,28 @@ __device__ __forceinline__ bf16x8_t acc_frag(const f32x16& x, int u) {
                                                  pk_bf16(x[o + 6], x[o + 7])));
 }
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// One row of 128 outputs times sc as bf16: o[dt][4g..4g+3] = elements 32 dt + 8 g + 4 h + 0..3
+// of the lane's row (lanes r and r + 32 hold one row). permlane32_swap pairs groups g, g + 1 so
+// each lane stores 16 contiguous bytes (8 dwordx4 per lane instead of 16 dwordx2; the store tail
+// is issue-bound). Every lane must execute it (a cross-lane op): `ok` only gates the stores.
+__device__ __forceinline__ void store_row(uint16_t* row, const f32x16 (&o)[4], float sc, int h,
+                                          bool ok) {
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; g += 2) {
+      uint32_t a0 = pk_bf16(o[dt][4 * g] * sc, o[dt][4 * g + 1] * sc);
+      uint32_t a1 = pk_bf16(o[dt][4 * g + 2] * sc, o[dt][4 * g + 3] * sc);
+      uint32_t b0 = pk_bf16(o[dt][4 * g + 4] * sc, o[dt][4 * g + 5] * sc);
+      uint32_t b1 = pk_bf16(o[dt][4 * g + 6] * sc, o[dt][4 * g + 7] * sc);
+      const auto x = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+      const auto y = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+      a0 = x[0]; b0 = x[1];
+      a1 = y[0]; b1 = y[1];
+      if (ok) *reinterpret_cast<uint4*>(row + 32 * dt + 8 * g + 8 * h) = make_uint4(a0, a1, b0, b1);
+    }
+}
 
 // rows [row0, row0 + ROWS) of a [S][ld] bf16 tensor (rows past S clamped to S - 1) into an
 // image: ROWS / 4 LDS-DMA wave-instructions of 4 rows x 256 B, wave w of NW issues w, w + NW, ..
@@ -205,22 +228,30 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FaArgs a) {
     float mt = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 16; ++i) mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt * a.c);   // finite from the first tile on (key 0 is visible)
-    const float alpha = fexp2(m - mn);
-    m = mn;
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * a.c;
+    // deferred rescale: the running max m moves (and O, l are rescaled) only when some row's
+    // tile max exceeds it by more than thr (log2 units), so exponentiated scores stay <= 2^thr
+    // (fp32 O / l accumulators, bf16 P keeps its relative precision); the first tile always
+    // sets m (finite from then on: key 0 is visible to every query). thr = 0: the textbook
+    // rescale at every max increase.
+    if (__any(mt > m + a.thr)) {
+      const float mn = fmaxf(m, mt);
+      const float alpha = fexp2(m - mn);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+    }
     float ls = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      s0[i] = fexp2(fmaf(s0[i], a.c, -mn));
-      s1[i] = fexp2(fmaf(s1[i], a.c, -mn));
+      s0[i] = fexp2(fmaf(s0[i], a.c, -m));
+      s1[i] = fexp2(fmaf(s1[i], a.c, -m));
       ls += s0[i] + s1[i];
     }
-    l = fmaf(l, alpha, ls);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+    l += ls;
     // O^T += V^T P^T over the 64 keys (4 k-steps of 16)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -234,18 +265,9 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FaArgs a) {
     }
   }
   l += __shfl_xor(l, 32, 64);
-  if (qrow < S) {
-    const float inv = 1.f / l;
-    uint16_t* og = a.out + ((static_cast<int64_t>(b) * S + qrow) * a.H + hh) * kD;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<uint2*>(og + 32 * dt + 8 * g + 4 * h) =
-            make_uint2(pk_bf16(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv),
-                       pk_bf16(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv));
-    if (h == 0) a.lse[static_cast<int64_t>(bh) * S + qrow] = m + __log2f(l);
-  }
+  store_row(a.out + ((static_cast<int64_t>(b) * S + min(qrow, S - 1)) * a.H + hh) * kD, o, 1.f / l,
+            h, qrow < S);
+  if (h == 0 && qrow < S) a.lse[static_cast<int64_t>(bh) * S + qrow] = m + __log2f(l);
 }
 
 // ------------------------------------------------------------------------------ backward: dQ
@@ -337,17 +359,8 @@ __global__ __launch_bounds__(kThreads, 2) void fa_dq_kernel(FaArgs a) {
       }
     }
   }
-  if (qrow < S) {
-    uint16_t* gq = a.out + (static_cast<int64_t>(bh) * S + qrow) * kD;
-    const float sc = a.scale;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<uint2*>(gq + 32 * dt + 8 * g + 4 * h) =
-            make_uint2(pk_bf16(dq[dt][4 * g] * sc, dq[dt][4 * g + 1] * sc),
-                       pk_bf16(dq[dt][4 * g + 2] * sc, dq[dt][4 * g + 3] * sc));
-  }
+  store_row(a.out + (static_cast<int64_t>(bh) * S + min(qrow, S - 1)) * kD, dq, a.scale, h,
+            qrow < S);
 }
 
 // --------------------------------------------------------------------------- backward: dK, dV
@@ -456,24 +469,9 @@ __global__ __launch_bounds__(kKVThreads, 2) void fa_dkdv_kernel(FaArgs a) {
       }
     }
   }
-  if (key < S) {
-    const int64_t row = (static_cast<int64_t>(bh) * S + key) * kD;
-    uint16_t* gk = a.dk + row;
-    uint16_t* gv = a.dv + row;
-    const float sc = a.scale;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * dt + 8 * g + 4 * h;
-        *reinterpret_cast<uint2*>(gk + d) =
-            make_uint2(pk_bf16(dk[dt][4 * g] * sc, dk[dt][4 * g + 1] * sc),
-                       pk_bf16(dk[dt][4 * g + 2] * sc, dk[dt][4 * g + 3] * sc));
-        *reinterpret_cast<uint2*>(gv + d) =
-            make_uint2(pk_bf16(dv[dt][4 * g], dv[dt][4 * g + 1]),
-                       pk_bf16(dv[dt][4 * g + 2], dv[dt][4 * g + 3]));
-      }
-  }
+  const int64_t row = (static_cast<int64_t>(bh) * S + min(key, S - 1)) * kD;
+  store_row(a.dk + row, dk, a.scale, h, key < S);
+  store_row(a.dv + row, dv, 1.f, h, key < S);
 }
 
 typedef void (*FaKernel)(FaArgs);
@@ -508,7 +506,8 @@ bool fa_shape_ok(int B, int H, int KV, int S) {
 }  // namespace
 
 hipError_t launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B,
-                            int H, int KV, int S, float scale, bool causal, hipStream_t st) {
+                            int H, int KV, int S, float scale, bool causal, hipStream_t st,
+                            float rescale_thr) {
   if (!fa_shape_ok(B, H, KV, S)) return hipErrorInvalidValue;
   FaArgs a{};
   a.q = static_cast<const uint16_t*>(q);
@@ -519,6 +518,7 @@ hipError_t launch_flash_fwd(const void* q, const void* k, const void* v, void* o
   a.B = B; a.H = H; a.KV = KV; a.S = S;
   a.scale = scale;
   a.c = scale * 1.4426950408889634f;
+  a.thr = rescale_thr < 0.f ? 0.f : rescale_thr;
   return causal ? launch_fa(fa_fwd_kernel<true>, a, 4 * kImg, st)
                 : launch_fa(fa_fwd_kernel<false>, a, 4 * kImg, st);
 }

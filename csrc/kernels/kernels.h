@@ -48,6 +48,20 @@ struct UpdArgs {
 // Returns hipSuccess or the launch error.
 hipError_t launch_agg_update(int dtype, int combine, int opt, const SrcArgs& src,
                              const UpdArgs& upd, int64_t D, hipStream_t stream);
+// The same over up to 16 segments in ONE launch (the sharded engine's buckets): segment i reads
+// worker rows from X (row stride ld) over D elements, updates the optimizer state at element
+// offset off and writes param_out; src / upd carry the shared rule, weights and state bases
+// (upd.param_out unused). Ragged or unaligned segments fall back to one launch each.
+struct AggSeg {
+  const void* X;
+  int64_t ld;
+  int64_t D;
+  int64_t off;
+  void* param_out;
+};
+hipError_t launch_agg_update_multi(int dtype, int combine, int opt, const SrcArgs& src,
+                                   const UpdArgs& upd, const AggSeg* segs, int nseg,
+                                   hipStream_t stream);
 
 // Gram matrix G = X X^T (fp64, [n, n], row-major) of n <= 64 worker rows. ``work`` must hold
 // gram_workspace_bytes(n, D) bytes. accumulate != 0: G += X X^T (bucket-by-bucket Gram).
@@ -249,8 +263,11 @@ hipError_t launch_rope_bwd(const void* dq, const void* dk, const void* dv, const
 // q [B, H, S, 128], k / v [B, KV, S, 128] -> o [B, S, H, 128], lse fp32 [B, H, S] (log2
 // domain). Backward: dq [B, H, S, 128], dk / dv per query head [B, H, S, 128]; dsum [B, H, S]
 // fp32 scratch (D = rowsum(dO * O)). csrc/kernels/flash_attn.hip.
+// rescale_thr: deferred online-softmax rescale threshold in log2 units (0 = rescale at every
+// max increase; 8 = scores exponentiated against a max up to 2^8 stale, see flash_attn.hip).
 hipError_t launch_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B,
-                            int H, int KV, int S, float scale, bool causal, hipStream_t stream);
+                            int H, int KV, int S, float scale, bool causal, hipStream_t stream,
+                            float rescale_thr = 8.f);
 hipError_t launch_flash_bwd(const void* q, const void* k, const void* v, const void* o,
                             const void* dout, const float* lse, float* dsum, void* dq, void* dk,
                             void* dv, int B, int H, int KV, int S, float scale, bool causal,

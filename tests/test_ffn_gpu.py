@@ -91,3 +91,32 @@ def test_linear_own_gemm_with_link(cuda):
     assert _rel(x.grad, xf.grad + g_res.float()) < 6e-3
     assert _rel(w.grad, wf.grad) < 6e-3
     assert _rel(b.grad, bf.grad) < 1e-2
+
+
+def test_ffn_batched_workers_unowned_biases(cuda):
+    """a worker-gradients object owning W1 / W2 but NOT b1 / b2 -- the bias gradients
+    must still reach autograd (summed over the batch), not vanish into a scratch row."""
+    from consensusml_amd.ops import worker_grads as WG
+    from consensusml_amd.ops.transformer import ffn_gelu
+    V, S, d, f = 2, 128, 256, 1024
+    fc1, fc2 = _layers(d, f, cuda, seed=5)
+    views = {id(fc1.weight): torch.zeros(V, f, d, device=cuda, dtype=torch.bfloat16),
+             id(fc2.weight): torch.zeros(V, d, f, device=cuda, dtype=torch.bfloat16)}
+    wg = WG.WorkerGrads(V, views)
+    x = torch.randn(V * 2, S, d, device=cuda).bfloat16()
+    prev = WG.activate(wg)
+    try:
+        y = ffn_gelu(x, fc1, fc2)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+    finally:
+        WG.activate(prev)
+    assert fc1.bias.grad is not None and fc2.bias.grad is not None
+    W1, b1, W2, b2 = (p.detach().float().requires_grad_(True)
+                      for p in (fc1.weight, fc1.bias, fc2.weight, fc2.bias))
+    yf = F.linear(F.gelu(F.linear(x.float(), W1, b1)), W2, b2)
+    yf.backward(dy.float())
+    assert _rel(fc1.bias.grad, b1.grad) < 1.5e-2
+    assert _rel(fc2.bias.grad, b2.grad) < 1.5e-2
+    # the owned weights got per-worker rows summing to the full gradient
+    assert _rel(views[id(fc1.weight)].float().sum(0), W1.grad) < 2e-2

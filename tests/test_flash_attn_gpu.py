@@ -158,3 +158,21 @@ def test_llama_tiny_block_uses_flash():
         torch.nn.functional.scaled_dot_product_attention = orig
     assert not calls
     assert all(torch.isfinite(p.grad.float()).all() for p in m.parameters() if p.grad is not None)
+
+
+@pytest.mark.parametrize("mag", [1.0, 4.0])
+def test_flash_deferred_rescale_threshold(mag):
+    """Rule 26 (rare data-dependent branch): the deferred online-softmax rescale (threshold 8 in
+    log2 units, the default) vs the textbook rescale at every max increase (threshold 0): both
+    match the fp32 oracle, agree with each other to rounding, and give the same lse. A spiked key
+    forces a large mid-sequence max jump."""
+    B, H, KV, S = 1, 8, 2, 1500
+    q, k, v = _inputs(B, H, KV, S, mag=mag, seed=13)
+    k[0, 0, 700] *= 6
+    scale = 1.0 / math.sqrt(128)
+    o8, l8 = lib().flash_fwd(q, k, v, True, scale, 8.0)
+    o0, l0 = lib().flash_fwd(q, k, v, True, scale, 0.0)
+    ref = _ref(q, k, v, True, scale)
+    assert _rel(o8, ref) < 1e-2 and _rel(o0, ref) < 1e-2
+    assert _rel(o8, o0) < 1e-2
+    assert (l8 - l0).abs().max().item() < 1e-3

@@ -24,8 +24,11 @@ def test_padded_logits_ce_and_bias_grad(cuda, V):
     b = (torch.randn(V, device=cuda) * 0.1).bfloat16().requires_grad_(True)
     labels = torch.randint(0, V, (M,), device=cuda)
     labels[::7] = -100
-    logits = T.linear(x, w, b)
+    logits = T.linear(x, w, b, logits=True)
     assert logits.shape == (M, V) and logits.stride(0) % 8 == 0 and logits.stride(0) > V
+    # any other biased linear of that width returns plain contiguous rows
+    plain = T.linear(x.detach(), w.detach(), b.detach())
+    assert plain.is_contiguous() and plain.view(-1).numel() == M * V
     loss = T.cross_entropy(logits, labels)
     loss.backward()
     xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
