@@ -40,10 +40,11 @@ def main():
     ap.add_argument("--H", type=int, default=32)
     ap.add_argument("--KV", type=int, default=8)
     ap.add_argument("--S", type=int, default=2048)
-    ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--full", action="store_true", help="non-causal")
-    ap.add_argument("--impl", default="flash,sdpa")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--impl", default="flash,flash_thr0,sdpa")
     a = ap.parse_args()
     from consensusml_amd.ops.native import lib
     B, H, KV, S, D = a.B, a.H, a.KV, a.S, 128
@@ -56,27 +57,38 @@ def main():
     do = torch.randn(B, S, H * D, device="cuda", generator=g).bfloat16()
     fwd_flop = 4.0 * B * H * S * S * D * (0.5 if causal else 1.0)
     L = lib()
+    fns = {}
     for impl in a.impl.split(","):
-        if impl == "flash":
-            o, lse = L.flash_fwd(q, k, v, causal, scale)
-            fwd = lambda: L.flash_fwd(q, k, v, causal, scale)  # noqa: E731
-            bwd = lambda: L.flash_bwd(q, k, v, o, do, lse, causal, scale)  # noqa: E731
+        if impl in ("flash", "flash_thr0"):
+            thr = 8.0 if impl == "flash" else 0.0    # deferred-rescale threshold (log2 units)
+            o, lse = L.flash_fwd(q, k, v, causal, scale, thr)
+            fns[impl] = (lambda thr=thr: L.flash_fwd(q, k, v, causal, scale, thr),
+                         lambda o=o, lse=lse: L.flash_bwd(q, k, v, o, do, lse, causal, scale))
         else:
             qa, ka, va = (t.clone().requires_grad_() for t in (q, k, v))
 
-            def run_f():
+            def run_f(qa=qa, ka=ka, va=va):
                 return F.scaled_dot_product_attention(qa, ka, va, is_causal=causal, scale=scale,
                                                       enable_gqa=H != KV)
             out = run_f()
             dos = do.view(B, S, H, D).transpose(1, 2)
-            fwd = run_f
-            bwd = lambda: torch.autograd.grad(out, (qa, ka, va), dos, retain_graph=True)  # noqa
-        for name, fn, flop in (("fwd", fwd, fwd_flop), ("bwd", bwd, 2.5 * fwd_flop)):
-            med, best = timed(fn, a.iters, a.warmup)
-            print(json.dumps({"bench": "flash_attn", "impl": impl, "pass": name, "B": B, "H": H,
-                              "KV": KV, "S": S, "causal": causal, "ms": round(med, 4),
-                              "ms_min": round(best, 4),
-                              "tflops": round(flop / med / 1e9, 1)}), flush=True)
+            fns[impl] = (run_f, lambda out=out, qa=qa, ka=ka, va=va: torch.autograd.grad(
+                out, (qa, ka, va), dos, retain_graph=True))
+    # interleaved rounds in one process (variants share the clock / thermal state)
+    res = {(i, p): [] for i in fns for p in ("fwd", "bwd")}
+    for _ in range(a.rounds):
+        for impl, (fwd, bwd) in fns.items():
+            for name, fn in (("fwd", fwd), ("bwd", bwd)):
+                med, _ = timed(fn, a.iters, a.warmup)
+                res[(impl, name)].append(med)
+    for (impl, name), ts in res.items():
+        ts.sort()
+        flop = fwd_flop * (1.0 if name == "fwd" else 2.5)
+        med = ts[len(ts) // 2]
+        print(json.dumps({"bench": "flash_attn", "impl": impl, "pass": name, "B": B, "H": H,
+                          "KV": KV, "S": S, "causal": causal, "ms": round(med, 4),
+                          "ms_min": round(ts[0], 4), "rounds": a.rounds,
+                          "tflops": round(flop / med / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":

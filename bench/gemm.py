@@ -19,6 +19,9 @@ SHAPES = [  # (name, M, N, K)
     ("qkv", 32768, 2304, 768), ("oproj", 32768, 768, 768), ("fc1", 32768, 3072, 768),
     ("fc2", 32768, 768, 3072), ("fc1_dgrad", 32768, 768, 3072), ("fc2_dgrad", 32768, 3072, 768),
     ("qkv_r", 4096, 2304, 768), ("fc1_r", 4096, 3072, 768), ("fc2_r", 4096, 768, 3072),
+    # the per-rank BERT step (V = 1 x 64 x 128 tokens): outputs 768 wide -> 96 tiles of 256^2
+    ("oproj_v1", 8192, 768, 768), ("fc2_v1", 8192, 768, 3072), ("qkv_dgrad_v1", 8192, 768, 2304),
+    ("fc1_dgrad_v1", 8192, 768, 3072), ("qkv_v1", 8192, 2304, 768),
     ("sq8k", 8192, 8192, 8192),
 ]
 
@@ -59,9 +62,13 @@ def main():
         h = torch.empty_like(y)
         flop = 2.0 * M * N * K
         r = {"shape": name, "M": M, "N": N, "K": K}
-        r["own_ms"] = timeit(lambda: lib().gemm_nt(x, w, 0, out=y), a.reps)
+        L = lib()
+        if L.gemm_nt_ok(M, N, K):
+            r["own_ms"] = timeit(lambda: L.gemm_nt(x, w, 0, out=y, tile=256), a.reps)
+        r["own128_ms"] = timeit(lambda: L.gemm_nt(x, w, 0, out=y, tile=128), a.reps)
+        r["pick"] = int(L.gemm_nt_pick(M, N, K))
         r["blas_ms"] = timeit(lambda: torch.matmul(x, w.t(), out=y), a.reps)
-        r["own_bias_ms"] = timeit(lambda: lib().gemm_nt(x, w, 0, bias=bias, out=y), a.reps)
+        r["own_bias_ms"] = timeit(lambda: L.gemm_nt(x, w, 0, bias=bias, out=y), a.reps)
         r["blas_bias_ms"] = timeit(lambda: F.linear(x, w, bias), a.reps)
         if name.startswith("fc1") and not name.endswith("dgrad"):
             r["own_gelu_ms"] = timeit(lambda: lib().gemm_nt(x, w, 1, bias=bias, aux=h, out=y), a.reps)
@@ -80,7 +87,9 @@ def main():
         for k in list(r):
             if k.endswith("_ms"):
                 r[k] = round(r[k], 4)
-        r["own_tflops"] = round(flop / r["own_ms"] / 1e9, 1)
+        if "own_ms" in r:
+            r["own_tflops"] = round(flop / r["own_ms"] / 1e9, 1)
+        r["own128_tflops"] = round(flop / r["own128_ms"] / 1e9, 1)
         r["blas_tflops"] = round(flop / r["blas_ms"] / 1e9, 1)
         rows.append(r)
         print(json.dumps(r), flush=True)

@@ -86,14 +86,24 @@ def main():
              "blas_ms": timeit(lambda: dy.t() @ x, a.reps)}
         if N % 128 == 0 and K % 128 == 0:
             r["own_ms"] = timeit(lambda: L.wgrad1x1(nhwc(dy), nhwc(x), torch.bfloat16), a.reps)
+        # NT forms on transposed operands (dW = (dy^T) (x^T)^T): transposes + gemm.hip / hipBLASLt
+        r["transpose_ms"] = timeit(lambda: (L.transpose_bf16(dy), L.transpose_bf16(x)), a.reps)
+        dyT, xT = L.transpose_bf16(dy), L.transpose_bf16(x)
+        if L.gemm_nt_pick(N, K, M) > 0:
+            dw = torch.empty(N, K, dtype=torch.bfloat16, device=dev)
+            r["own_nt_ms"] = timeit(lambda: L.gemm_nt(dyT, xT, 0, out=dw), a.reps)
+            del dw
+        r["blas_nt_ms"] = timeit(lambda: torch.matmul(dyT, xT.t()), a.reps)
+        del dyT, xT
         rows.append(r)
         for r in rows:
             for k in list(r):
                 if k.endswith("_ms"):
                     r[k] = round(r[k], 4)
             r["blas_tflops"] = round(flop / r["blas_ms"] / 1e9, 1)
-            if "own_ms" in r:
-                r["own_tflops"] = round(flop / r["own_ms"] / 1e9, 1)
+            for k in ("own", "own_nt", "blas_nt"):
+                if k + "_ms" in r:
+                    r[k + "_tflops"] = round(flop / r[k + "_ms"] / 1e9, 1)
             print(json.dumps(r), flush=True)
             out_rows.append(r)
         del x, w, dy

@@ -30,8 +30,8 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import ResidualLink
-from ..ops.transformer import (LayerNorm, Linear, RMSNorm, add_norm, bert_embed, ffn_gelu,
-                               fused_qkv_attention, linear, linear_gelu, qkv_attention,
+from ..ops.transformer import (LayerNorm, Linear, LinearNB, RMSNorm, add_norm, bert_embed,
+                               ffn_gelu, fused_qkv_attention, linear, linear_gelu, qkv_attention,
                                rope_tables, swiglu)
 
 
@@ -129,10 +129,10 @@ class LlamaBlock(nn.Module):
         self.c = c
         hd = c.d // c.heads
         self.hd = hd
-        self.wqkv = nn.Linear(c.d, (c.heads + 2 * c.kv_heads) * hd, bias=False)
-        self.wo = nn.Linear(c.heads * hd, c.d, bias=False)
-        self.w13 = nn.Linear(c.d, 2 * c.ffn, bias=False)   # [gate | up]
-        self.w2 = nn.Linear(c.ffn, c.d, bias=False)
+        self.wqkv = LinearNB(c.d, (c.heads + 2 * c.kv_heads) * hd)
+        self.wo = LinearNB(c.heads * hd, c.d)
+        self.w13 = LinearNB(c.d, 2 * c.ffn)   # [gate | up]
+        self.w2 = LinearNB(c.ffn, c.d)
         self.n1 = RMSNorm(c.d, c.eps)
         self.n2 = RMSNorm(c.d, c.eps)
 
@@ -152,7 +152,7 @@ class Llama(nn.Module):
         self.tok = nn.Embedding(c.vocab, c.d)
         self.layers = nn.ModuleList([LlamaBlock(c) for _ in range(c.layers)])
         self.norm = RMSNorm(c.d, c.eps)
-        self.out = nn.Linear(c.d, c.vocab, bias=False)
+        self.out = LinearNB(c.d, c.vocab)
         for m in self.modules():
             if isinstance(m, (nn.Linear, nn.Embedding)):
                 nn.init.normal_(m.weight, std=0.02)

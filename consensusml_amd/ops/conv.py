@@ -68,8 +68,8 @@ def conv_mm(a: torch.Tensor, w_nk: torch.Tensor, acc: Optional[torch.Tensor] = N
              else w_nk.contiguous())
         CONV_MM_STATS["own"] += 1
         if acc is not None:
-            return lib().gemm_nt(a, w, 0, out=acc, cin=acc)
-        return lib().gemm_nt(a, w, 0)
+            return lib().gemm_nt(a, w, 0, out=acc, cin=acc, tile=256)
+        return lib().gemm_nt(a, w, 0, tile=256)
     CONV_MM_STATS["blas"] += 1
     if acc is not None:
         return acc.addmm_(a, w_nk.t()) if acc.is_contiguous() else torch.addmm(acc, a, w_nk.t())

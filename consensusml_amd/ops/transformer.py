@@ -499,14 +499,16 @@ def _al16(*ts: Optional[torch.Tensor]) -> bool:
 
 
 def _own_gemm(M: int, N: int, K: int) -> bool:
-    """gemm.hip for a bf16 GEMM of this shape: eligible (256-multiples) and enough 256 x 256
-    tiles to fill the chip (>= 128; below that hipBLASLt's smaller tiles win, bench/gemm.py)."""
+    """Own NT GEMM (gemm_nt, ep 0) for a bf16 GEMM of this shape: gemm.hip's 256 x 256 tiles when
+    they fill the chip (>= 128 tiles), else gemm128.hip's 128 x 128 tiles (PerfPolicy.own_gemm128;
+    at the BERT per-rank shapes 1.15-1.8x hipBLASLt, profiles/r05_05/gemm.jsonl)."""
     if not _P().own_gemm:
         return False
     try:
-        return bool(lib().gemm_nt_ok(M, N, K)) and (M // 256) * (N // 256) >= 128
+        pick = int(lib().gemm_nt_pick(M, N, K))
     except Exception:
         return False
+    return pick == 256 or (pick == 128 and _P().own_gemm128)
 
 
 def _linear_wgrad(gout: torch.Tensor, gin: torch.Tensor) -> torch.Tensor:
@@ -696,6 +698,66 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
                                or (wg is not None and wg.has(w))):
         return _LinearFn.apply(x, w, b, link, pad)
     return F.linear(x, w, b)
+
+
+# own data gradient (gemm.hip against the transposed weight) for bias-free linears up to this
+# many weight elements: wqkv / wo of Llama-3-8B run 1.13-1.17x hipBLASLt there, the larger
+# w13 / w2 / output-head weights tie (profiles/r05_03/llama_gemm.jsonl)
+_NB_OWN_DGRAD_MAX = 32 * 1024 * 1024
+
+
+class _LinearNBFn(torch.autograd.Function):
+    """y = x W^T without bias (Llama's projections), forward on hipBLASLt (NT, its best layout).
+    Backward: dx = dy W on gemm.hip for weights up to _NB_OWN_DGRAD_MAX elements, else hipBLASLt;
+    dW = dy^T x as an NT GEMM on transposed operands -- (dy^T) (x^T)^T, two bandwidth-bound
+    transposes + hipBLASLt NT at 1.3-1.57 PFLOP/s instead of its dy^T x kernels at 0.9-1.15
+    (PerfPolicy.nt_wgrad; -0.5 ms per Llama-3-8B layer, profiles/r05_06/llama_gemm.jsonl)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return F.linear(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        N, K = w.shape
+        x2 = x.reshape(-1, K)
+        dy2 = dy.reshape(-1, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        M = dy2.shape[0]
+        L = lib()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if w.numel() <= _NB_OWN_DGRAD_MAX and _own_gemm(M, K, N) and _al16(dy2):
+                dx = L.gemm_nt(dy2, L.transpose_bf16(w), 0)
+            else:
+                dx = dy2 @ w
+            dx = dx.view(x.shape)
+        if ctx.needs_input_grad[1]:
+            if _P().nt_wgrad:
+                dw = torch.matmul(L.transpose_bf16(dy2), L.transpose_bf16(x2).t())
+            else:
+                dw = dy2.t() @ x2
+        return dx, dw
+
+
+def linear_nb(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """Bias-free linear (``_LinearNBFn`` on bf16 GPU tensors, F.linear otherwise)."""
+    if _gpu_bf16(x, w) and WG.current() is None:
+        return _LinearNBFn.apply(x, w)
+    return F.linear(x, w)
+
+
+class LinearNB(nn.Linear):
+    """Bias-free nn.Linear whose bf16 GPU backward runs ``_LinearNBFn``."""
+
+    def __init__(self, in_features: int, out_features: int):
+        super().__init__(in_features, out_features, bias=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return linear_nb(x, self.weight)
 
 
 class Linear(nn.Linear):

@@ -209,6 +209,7 @@ class ConsensusEngine:
         # step SLOWER at batch 256: the extra stream's waits share hardware queues with the
         # compute stream, profiles/r05_02/bench.json.) CPU / gloo runs keep the polled form.
         self._gram_queue: List[Bucket] = []
+        self._gram_arg_cache: Dict[int, tuple] = {}
         self._gram_ordered = self.early_gram and dev.type == "cuda"
         self.gram_lag = max(0, int(cfg.topology.gram_lag))
         # training-side consensus table (SURVEY.md §5.4 b): when set, the next step() records
@@ -471,10 +472,32 @@ class ConsensusEngine:
         if b.index in self._gram_done:
             return
         self._wait(b)
-        X = self._cclip_rows(b) if self.rule == "centered_clip" else self._rows(b)
-        length = b.shard if self.topo == "sharded" else X.shape[1]
-        K.gram(X, n=self.rows_total, D=length, out=self.Gb[b.index], center=self._pass_center())
+        args = (self._gram_args(b) if self.rule != "centered_clip" and self.device.type == "cuda"
+                else None)
+        if args is None:
+            X = self._cclip_rows(b) if self.rule == "centered_clip" else self._rows(b)
+            length = b.shard if self.topo == "sharded" else X.shape[1]
+            K.gram(X, n=self.rows_total, D=length, out=self.Gb[b.index],
+                   center=self._pass_center())
+        else:
+            # the hook-path launch with every argument resolved once (persistent buffers): the
+            # host cost per bucket matters at small per-rank batches (b256: ~700 launches / step)
+            X, length, ws = args
+            lib().gram(X, self.rows_total, length, None, ws, self.Gb[b.index], False,
+                       self._pass_center())
         self._gram_done.add(b.index)
+
+    def _gram_args(self, b: Bucket):
+        hit = self._gram_arg_cache.get(b.index)
+        if hit is None:
+            X = self._rows(b)
+            length = b.shard if self.topo == "sharded" else X.shape[1]
+            if X.data_ptr() % 16 or (X.stride(0) * X.element_size()) % 16 or X.stride(1) != 1:
+                hit = False          # unaligned rows: K.gram pads a copy every call
+            else:
+                hit = (X, length, K.GramWorkspace.get(X.device, self.rows_total, length))
+            self._gram_arg_cache[b.index] = hit
+        return hit or None
 
     def _poll_grams(self) -> None:
         """Gram partials of every bucket whose exchange has completed (non-blocking test), so
@@ -554,8 +577,8 @@ class ConsensusEngine:
             self.G.zero_()
             for b, X, length in cols:
                 K.gram(X, n=self.rows_total, D=length, out=self.G, accumulate=True, center=center)
-        if self.group_active and self.topo == "sharded":
-            dist.all_reduce(self.G)
+        if self.group_active and self.topo == "sharded" and self.N > 1:
+            dist.all_reduce(self.G)      # (one rank: the sum over ranks is G itself)
         if cfg.centered_gram and center is None:
             # no medoid yet (first step) or the two-pass scheme: a second pass relative to the
             # medoid of the uncentered G -- exact distances for near-duplicate workers (the rules
@@ -565,7 +588,7 @@ class ConsensusEngine:
             for b, X, length in cols:
                 K.gram(X, n=self.rows_total, D=length, out=self.G, accumulate=True,
                        center=self.center)
-            if self.group_active and self.topo == "sharded":
+            if self.group_active and self.topo == "sharded" and self.N > 1:
                 dist.all_reduce(self.G)
         rule = "bulyan_select" if self.rule == "bulyan" else self.rule
         m = cfg.m if cfg.m is not None else self.n - cfg.f
@@ -692,7 +715,8 @@ class ConsensusEngine:
                 self._aggregate_update(b, X, length, soff, pout, opt, gout)
                 if self.rule == "centered_clip":
                     X[self.n, :length].copy_(gout.to(X.dtype))
-            if self.group_active:
+            if self.group_active and self.N > 1:
+                # (one rank: the shard IS the bucket, the gather would copy it onto itself)
                 full = fl.flat_param[b.offset:b.offset + b.length]
                 work = dist.all_gather_into_tensor(full, pout, async_op=True)
                 if self.param_prefetch:

@@ -82,6 +82,9 @@ class PerfPolicy:
     multi_copy: bool = True               # multi-tensor HIP copy for gradient capture
     batched_workers: bool = True          # virtual workers as one batched fwd/bwd (BERT)
     own_gemm: bool = True                 # gemm.hip for transformer linears with >= 128 tiles
+    own_gemm128: bool = True              # ... and gemm128.hip (128 x 128 tiles) below that: the
+                                          # BERT per-rank shapes (8192 x 768 outputs) run 1.15-1.8x
+                                          # hipBLASLt (profiles/r05_05/gemm.jsonl)
     fused_ffn: bool = True                # BERT FFN on gemm.hip: bias + GELU in fc1's epilogue,
                                           # GELU backward + bias gradient in the dgrad epilogue
     padded_logits: bool = True            # biased linears with N % 8 != 0 (BERT MLM head) write
@@ -89,6 +92,9 @@ class PerfPolicy:
                                           # bias gradient (no column-sum pass over R x V)
     own_gemm_conv1x1: bool = True         # ResNet 1x1 convs that run as plain GEMMs (layers 3-4
                                           # forward / data gradient) on gemm.hip, not hipBLASLt
+    nt_wgrad: bool = True                 # bias-free (Llama) linears: weight gradient as an NT GEMM
+                                          # on transposed operands (1.3-1.57 vs 0.9-1.15 PFLOP/s for
+                                          # hipBLASLt's dY^T X layout, profiles/r05_06/llama_gemm.jsonl)
     own_linear_wgrad: bool = True         # transformer-linear weight gradients dY^T X on
                                           # wgrad1x1.hip (token rows as NHWC pixels), not hipBLASLt,
                                           # up to BERT-base sizes (N K <= 4 M)
@@ -134,9 +140,11 @@ class PerfPolicy:
             multi_copy=_env_bool("CML_MULTI_COPY", True),
             batched_workers=_env_bool("CML_BATCHED_WORKERS", True),
             own_gemm=_env_bool("CML_OWN_GEMM", True),
+            own_gemm128=_env_bool("CML_OWN_GEMM128", True),
             fused_ffn=_env_bool("CML_FUSED_FFN", True),
             own_gemm_conv1x1=_env_bool("CML_OWN_GEMM_CONV1X1", True),
             own_linear_wgrad=_env_bool("CML_OWN_LINEAR_WGRAD", True),
+            nt_wgrad=_env_bool("CML_NT_WGRAD", True),
             padded_logits=_env_bool("CML_PADDED_LOGITS", True),
         )
 

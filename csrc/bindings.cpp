@@ -2100,9 +2100,18 @@ int64_t lasso_slices(int64_t p) { return cml::lasso_slices(static_cast<int>(p));
 // ep 0: + bias; ep 1: aux <- h = a b^T + bias, y = gelu(h); ep 2: y = (a b^T) * gelu'(aux) and,
 // with colsum_out, its column sums per row segment (colsum_out [nseg, N], bf16 or fp32, unit
 // column stride, any row stride).
+// EP_STORE tile choice: the 256 x 256 kernel once it has >= 128 tiles (it fills the chip), else
+// the 128 x 128 kernel (bench/gemm.py: BERT per-rank and Llama shapes), 0 = neither eligible.
+int64_t gemm_nt_pick(int64_t M, int64_t N, int64_t K) {
+  if (cml::gemm_nt_eligible(M, N, K) && (M / 256) * (N / 256) >= 128) return 256;
+  if (cml::gemm128_eligible(M, N, K)) return 128;
+  if (cml::gemm_nt_eligible(M, N, K)) return 256;
+  return 0;
+}
+
 Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tensor>& bias,
                const optional<Tensor>& aux, const optional<Tensor>& out,
-               const optional<Tensor>& colsum_out, const optional<Tensor>& cin) {
+               const optional<Tensor>& colsum_out, const optional<Tensor>& cin, int64_t tile) {
   check_dev(a, "a");
   check_dev(b, "b");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm_nt: bf16");
@@ -2110,13 +2119,18 @@ Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tens
               "gemm_nt: 2-D operands with unit column stride");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K, "gemm_nt: K mismatch");
-  TORCH_CHECK(cml::gemm_nt_eligible(M, N, K), "gemm_nt: needs M % 256 == 0, N % 256 == 0, K % 64 == 0");
+  if (tile == 0) tile = ep == cml::EP_STORE ? gemm_nt_pick(M, N, K) : 256;
+  TORCH_CHECK(tile == 128 || tile == 256, "gemm_nt: tile must be 0 (auto), 128 or 256");
+  TORCH_CHECK(tile == 256 || ep == cml::EP_STORE, "gemm_nt: the 128 x 128 kernel has ep 0 only");
+  TORCH_CHECK(tile == 128 ? cml::gemm128_eligible(M, N, K) : cml::gemm_nt_eligible(M, N, K),
+              "gemm_nt: needs M, N multiples of the tile (", tile, ") and K % 64 == 0");
   // every operand on a's device and aligned for its vector width (16-B rows of a / b / y / aux /
   // cin, 8-B bias reads): a misaligned pointer must be a TORCH_CHECK, not a device fault
   auto same_dev = [&](const optional<Tensor>& t, const char* name) {
-    if (t.has_value() && t->defined())
+    if (t.has_value() && t->defined()) {
       TORCH_CHECK(t->is_cuda() && t->get_device() == a.get_device(), "gemm_nt: ", name,
                   " must be on a's device");
+    }
   };
   auto aligned = [](const Tensor& t, int bytes) {
     return (reinterpret_cast<uintptr_t>(t.data_ptr()) % bytes) == 0;
@@ -2129,12 +2143,14 @@ Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tens
   same_dev(cin, "cin");
   TORCH_CHECK(aligned(a, 16) && aligned(b, 16) && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0,
               "gemm_nt: a / b need 16-B aligned rows");
-  if (bias.has_value() && bias->defined()) TORCH_CHECK(aligned(*bias, 8), "gemm_nt: bias must be 8-B aligned");
-  if (cin.has_value() && cin->defined()) TORCH_CHECK(aligned(*cin, 16), "gemm_nt: cin must be 16-B aligned");
-  if (aux.has_value() && aux->defined()) TORCH_CHECK(aligned(*aux, 16), "gemm_nt: aux must be 16-B aligned");
-  if (colsum_out.has_value() && colsum_out->defined())
-    TORCH_CHECK(colsum_out->scalar_type() == at::kFloat || colsum_out->scalar_type() == at::kBFloat16,
-                "colsum_out: bf16 or fp32");
+  const bool has_bias = bias.has_value() && bias->defined(), has_cin = cin.has_value() && cin->defined();
+  const bool has_aux = aux.has_value() && aux->defined();
+  TORCH_CHECK(!has_bias || aligned(*bias, 8), "gemm_nt: bias must be 8-B aligned");
+  TORCH_CHECK(!has_cin || aligned(*cin, 16), "gemm_nt: cin must be 16-B aligned");
+  TORCH_CHECK(!has_aux || aligned(*aux, 16), "gemm_nt: aux must be 16-B aligned");
+  TORCH_CHECK(!(colsum_out.has_value() && colsum_out->defined()) ||
+                  colsum_out->scalar_type() == at::kFloat || colsum_out->scalar_type() == at::kBFloat16,
+              "colsum_out: bf16 or fp32");
   const c10::DeviceGuard guard(a.device());
   Tensor y;
   if (out.has_value() && out->defined()) {
@@ -2175,7 +2191,11 @@ Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tens
     part = at::empty({M / 128, N}, a.options().dtype(at::kFloat));
     g.part = part.data_ptr<float>();
   }
-  CML_CHECK_HIP(cml::launch_gemm_nt(g, static_cast<int>(ep), cur_stream()));
+  if (tile == 128) {
+    CML_CHECK_HIP(cml::launch_gemm128_nt(g, cur_stream()));
+  } else {
+    CML_CHECK_HIP(cml::launch_gemm_nt(g, static_cast<int>(ep), cur_stream()));
+  }
   if (cs) {
     const bool f32 = colsum_out->scalar_type() == at::kFloat;
     CML_CHECK_HIP(cml::launch_colsum_fold(part.data_ptr<float>(), M, static_cast<int>(N),
@@ -2419,8 +2439,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, "NT GEMM with fused epilogues (bias / bias+GELU / GELU backward + "
         "column sums)", py::arg("a"), py::arg("b"), py::arg("ep"), py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("out") = py::none(),
-        py::arg("colsum_out") = py::none(), py::arg("cin") = py::none());
-  m.def("gemm_nt_ok", &gemm_nt_ok, "shape eligibility of gemm_nt");
+        py::arg("colsum_out") = py::none(), py::arg("cin") = py::none(), py::arg("tile") = 0);
+  m.def("gemm_nt_ok", &gemm_nt_ok, "shape eligibility of gemm_nt's 256 x 256 kernel");
+  m.def("gemm_nt_pick", &gemm_nt_pick, "EP_STORE tile choice of gemm_nt: 256, 128 or 0 (none)");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);
   m.attr("OPT_NONE") = static_cast<int>(cml::OPT_NONE);

@@ -564,6 +564,10 @@ struct GemmArgs {
 };
 bool gemm_nt_eligible(int64_t M, int64_t N, int64_t K);
 hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st);
+// 128 x 128-tile NT GEMM (gemm128.hip), EP_STORE only (bias, cin): M % 128 == 0, N % 128 == 0,
+// K % 64 == 0 -- the grids that 256 x 256 tiles leave under-filled.
+bool gemm128_eligible(int64_t M, int64_t N, int64_t K);
+hipError_t launch_gemm128_nt(const GemmArgs& a, hipStream_t st);
 // the conv form (a.conv = 1; M % 256 == 0, N % 256 == 0, C % 64 == 0), ep EP_STORE /
 // EP_CONV_ST / EP_CONV_BB (conv_gemm.hip's 256 x 256 path for stride-1 3x3 convs)
 bool gemm_conv_eligible(int64_t M, int N, int C);

@@ -32,7 +32,8 @@ def test_multi_equals_per_bucket(cuda, combine, opt_kind, ragged):
 
     def state():
         g = torch.Generator(device=cuda).manual_seed(1)
-        return [torch.randn(total, device=cuda, generator=g) for _ in range(3)]
+        m, a, b = (torch.randn(total, device=cuda, generator=g) for _ in range(3))
+        return m, a, b.abs()          # Adam's second moment is non-negative
 
     m1, a1, b1 = state()
     p1 = [torch.zeros(L, device=cuda, dtype=torch.bfloat16) for L in lens]

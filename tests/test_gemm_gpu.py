@@ -19,22 +19,55 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 768), (1024, 3072, 768),
                                    (768, 512, 3072), (2048, 2304, 128)])
-def test_gemm_store_vs_fp32(cuda, M, N, K):
+@pytest.mark.parametrize("tile", [256, 128])
+def test_gemm_store_vs_fp32(cuda, M, N, K, tile):
     from consensusml_amd.ops.native import lib
     a, b = _rand(M, K, dev=cuda, seed=1), _rand(N, K, dev=cuda, seed=2)
     bias = _rand(N, dev=cuda, seed=3)
     ref = a.float() @ b.float().t()
-    y = lib().gemm_nt(a, b, 0)
+    y = lib().gemm_nt(a, b, 0, tile=tile)
     assert _rel(y, ref) < 4e-3
-    yb = lib().gemm_nt(a, b, 0, bias=bias)
+    yb = lib().gemm_nt(a, b, 0, bias=bias, tile=tile)
     assert _rel(yb, ref + bias.float()) < 4e-3
     # exactness of the layout: integer-valued operands give exact fp32 sums (|sum| < 2^8 keeps
     # the bf16 output exact), so every element must match, not just the norm
     ai = torch.randint(-2, 3, (M, K), device=cuda).bfloat16()
     bi = torch.randint(-2, 3, (N, K), device=cuda).bfloat16()
     if K <= 64:
-        yi = lib().gemm_nt(ai, bi, 0)
+        yi = lib().gemm_nt(ai, bi, 0, tile=tile)
         assert torch.equal(yi.float(), ai.float() @ bi.float().t())
+
+
+# 128 x 128 tiles (gemm128.hip): M and N multiples of 128 that are NOT multiples of 256, the
+# BERT per-rank shapes, an asymmetric integer check of the C^T layout, bias + residual (cin)
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (384, 640, 192), (8192, 768, 768),
+                                   (8192, 768, 3072), (1152, 2304, 704), (640, 128, 4096)])
+def test_gemm128_vs_fp32(cuda, M, N, K):
+    from consensusml_amd.ops.native import lib
+    a, b = _rand(M, K, dev=cuda, seed=11), _rand(N, K, dev=cuda, seed=12)
+    bias = _rand(N, dev=cuda, seed=13)
+    cin = _rand(M, N, dev=cuda, seed=14, scale=4.0)
+    ref = a.float() @ b.float().t()
+    y = lib().gemm_nt(a, b, 0, bias=bias, tile=128)
+    assert _rel(y, ref + bias.float()) < 4e-3
+    # in-place residual add (out = cin): bf16(bf16(acc + bias) + cin), gemm.hip's rounding points
+    yc = cin.clone()
+    lib().gemm_nt(a, b, 0, bias=bias, out=yc, cin=yc, tile=128)
+    want = (y.float() + cin.float()).bfloat16()
+    assert (yc.float() - want.float()).abs().max().item() <= 2 ** -6 * want.float().abs().max().item()
+    ai = torch.randint(-2, 3, (M, 64), device=cuda).bfloat16()
+    bi = (torch.arange(N * 64, device=cuda).view(N, 64) % 5 - 2).bfloat16()   # asymmetric
+    yi = lib().gemm_nt(ai, bi, 0, tile=128)
+    assert torch.equal(yi.float(), ai.float() @ bi.float().t())
+
+
+def test_gemm_pick():
+    from consensusml_amd.ops.native import lib
+    L = lib()
+    assert L.gemm_nt_pick(8192, 768, 768) == 128          # 96 tiles of 256^2: under-filled
+    assert L.gemm_nt_pick(8192, 28672, 4096) == 256       # Llama w13: 3584 tiles
+    assert L.gemm_nt_pick(8192, 4096, 4096) == 256        # 512 tiles
+    assert L.gemm_nt_pick(1000, 768, 768) == 0
 
 
 def test_gemm_strided_rows(cuda):

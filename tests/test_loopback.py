@@ -136,14 +136,18 @@ def _check(res, backend):
         lc = c["loop_calls"]
         assert not c["plain_calls"], c
         if topo == "sharded":
-            assert lc.get("all_to_all_single", 0) > 0 and lc.get("all_gather_into_tensor", 0) > 0
+            # the gradient all-to-all runs on the 1-rank group; the parameter all-gather and the
+            # Gram all-reduce are identities at one rank and are skipped (exercised at 2-8 ranks
+            # by tests/test_dist_gloo.py, tests/test_dist_gpu.py)
+            assert lc.get("all_to_all_single", 0) > 0
+            assert lc.get("all_gather_into_tensor", 0) == 0
             assert c["prefetch"]
         if topo == "allgather":
             assert lc.get("all_gather_into_tensor", 0) > 0
         if topo == "allreduce":
             assert lc.get("all_reduce", 0) > 0
         if rule in ("krum", "multi_krum", "geomed") and topo == "sharded":
-            assert lc.get("all_reduce", 0) > 0          # the Gram all-reduce
+            assert lc.get("all_reduce", 0) == 0         # the Gram all-reduce: identity at 1 rank
         if eager:
             assert c["early_grams"] > 0
 
@@ -154,6 +158,7 @@ def test_loopback_gloo_cpu(tmp_path):
 
 @pytest.mark.gpu
 def test_loopback_rccl_gpu(cuda, tmp_path):
-    """RCCL (backend nccl) runs the N > 1 engine on the one GPU: all-to-all + early Gram polling,
-    Gram all-reduce, prefetched in-place all-gather, all-reduce baseline, gossip send/recv."""
+    """RCCL (backend nccl) runs the N > 1 engine on the one GPU: all-to-all + early Grams,
+    all-reduce baseline, gossip send/recv (the 1-rank identities -- parameter all-gather, Gram
+    all-reduce -- are skipped)."""
     _check(_run(tmp_path, "nccl", "cuda:0", "bf16"), "nccl")

@@ -228,3 +228,28 @@ def test_linear_wgrad_on_wgrad1x1(cuda, Tn, N, K):
         grads.append(wi.grad.float())
     assert float((grads[0] - grads[1]).norm() / grads[1].norm()) < 5e-3
     assert float((grads[0] - ref).norm() / ref.norm()) < 5e-3
+
+
+@pytest.mark.parametrize("M,N,K,own", [(1024, 768, 512, True), (512, 1152, 640, True),
+                                       (2048, 512, 1024, False)])
+def test_linear_nb_vs_fp32(cuda, M, N, K, own, monkeypatch):
+    """Bias-free linear (Llama projections): hipBLASLt forward, own-or-library data gradient,
+    weight gradient as an NT GEMM on transposed operands -- all against fp32."""
+    from consensusml_amd.ops import transformer as T
+    if not own:
+        monkeypatch.setattr(T, "_NB_OWN_DGRAD_MAX", 0)
+    torch.manual_seed(M + N)
+    lin = T.LinearNB(K, N).to(cuda, torch.bfloat16)
+    x = torch.randn(2, M // 2, K, device=cuda).bfloat16().requires_grad_(True)
+    y = lin(x)
+    assert "LinearNB" in type(y.grad_fn).__name__
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xf = x.detach().float().requires_grad_(True)
+    wf = lin.weight.detach().float().requires_grad_(True)
+    yf = xf @ wf.t()
+    yf.backward(dy.float())
+    rel = lambda a, b: float((a.float() - b.float()).norm() / b.float().norm())  # noqa: E731
+    assert rel(y, yf) < 1e-2
+    assert rel(x.grad, xf.grad) < 1e-2
+    assert rel(lin.weight.grad, wf.grad) < 1e-2
