@@ -210,6 +210,8 @@ class ConsensusEngine:
         # compute stream, profiles/r05_02/bench.json.) CPU / gloo runs keep the polled form.
         self._gram_queue: List[Bucket] = []
         self._gram_arg_cache: Dict[int, tuple] = {}
+        self._gram_nblk: Dict[int, int] = {}
+        self._fast_gram_ok: Optional[bool] = None
         self._gram_ordered = self.early_gram and dev.type == "cuda"
         self.gram_lag = max(0, int(cfg.topology.gram_lag))
         # training-side consensus table (SURVEY.md §5.4 b): when set, the next step() records
@@ -472,19 +474,19 @@ class ConsensusEngine:
         if b.index in self._gram_done:
             return
         self._wait(b)
-        args = (self._gram_args(b) if self.rule != "centered_clip" and self.device.type == "cuda"
-                else None)
-        if args is None:
+        if self._fast_gram():
+            # stage 1 only, into this bucket's own workspace, every argument resolved once
+            # (persistent buffers: the host cost per bucket matters at small per-rank batches,
+            # b256: ~700 launches / step); the stage-2 reduces of all buckets run as ONE launch
+            # in _compute_weights
+            X, length, ws = self._gram_args(b)
+            self._gram_nblk[b.index] = lib().gram_partial(X, self.rows_total, length, ws,
+                                                          self._pass_center())
+        else:
             X = self._cclip_rows(b) if self.rule == "centered_clip" else self._rows(b)
             length = b.shard if self.topo == "sharded" else X.shape[1]
             K.gram(X, n=self.rows_total, D=length, out=self.Gb[b.index],
                    center=self._pass_center())
-        else:
-            # the hook-path launch with every argument resolved once (persistent buffers): the
-            # host cost per bucket matters at small per-rank batches (b256: ~700 launches / step)
-            X, length, ws = args
-            lib().gram(X, self.rows_total, length, None, ws, self.Gb[b.index], False,
-                       self._pass_center())
         self._gram_done.add(b.index)
 
     def _gram_args(self, b: Bucket):
@@ -495,9 +497,20 @@ class ConsensusEngine:
             if X.data_ptr() % 16 or (X.stride(0) * X.element_size()) % 16 or X.stride(1) != 1:
                 hit = False          # unaligned rows: K.gram pads a copy every call
             else:
-                hit = (X, length, K.GramWorkspace.get(X.device, self.rows_total, length))
+                nbytes = int(lib().gram_workspace_bytes(self.rows_total, length))
+                hit = (X, length, torch.empty(nbytes // 4 + 1, dtype=torch.float32,
+                                              device=X.device))
             self._gram_arg_cache[b.index] = hit
         return hit or None
+
+    def _fast_gram(self) -> bool:
+        """GPU early Grams as per-bucket stage-1 launches + one deferred multi-bucket reduce."""
+        if self._fast_gram_ok is None:
+            self._fast_gram_ok = (self.device.type == "cuda" and self.rule != "centered_clip"
+                                  and len(self.flat.buckets) <= 32
+                                  and all(self._gram_args(b) is not None
+                                          for b in self.flat.buckets))
+        return self._fast_gram_ok
 
     def _poll_grams(self) -> None:
         """Gram partials of every bucket whose exchange has completed (non-blocking test), so
@@ -572,7 +585,13 @@ class ConsensusEngine:
             self._gram_queue.clear()
             for b, _, _ in cols:
                 self._bucket_gram(b)
-            K.gram_sum(self.Gb, self.G)
+            if self._fast_gram():
+                bs = self.flat.buckets
+                lib().gram_reduce_multi([self._gram_args(b)[2] for b in bs],
+                                        [self._gram_nblk[b.index] for b in bs], self.rows_total,
+                                        self.G)
+            else:
+                K.gram_sum(self.Gb, self.G)
         else:
             self.G.zero_()
             for b, X, length in cols:

@@ -194,6 +194,46 @@ void gram(const Tensor& X, int64_t n, int64_t D, const optional<Tensor>& rows, T
                                  cur_stream(), c));
 }
 
+// stage 1 of gram() into `work` (a per-bucket workspace); returns the partial block count
+int64_t gram_partial(const Tensor& X, int64_t n, int64_t D, Tensor& work,
+                     const optional<Tensor>& center) {
+  check_dev(X, "X");
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1 && X.size(0) >= n, "X: 2-D, unit column stride, >= n rows");
+  TORCH_CHECK(n >= 1 && n <= 64 && D >= 1 && D <= X.size(1), "gram_partial: 1 <= n <= 64, D in range");
+  TORCH_CHECK(work.is_cuda() && work.is_contiguous() &&
+                  work.numel() * work.element_size() >= gram_workspace_bytes(n, D),
+              "gram workspace too small");
+  const int* c = opt_ptr<const int>(center, at::kInt, "center", 1);
+  const c10::DeviceGuard guard(X.device());
+  int nblk = 0;
+  CML_CHECK_HIP(cml::launch_gram_partial(dtype_of(X), X.data_ptr(), X.stride(0), static_cast<int>(n),
+                                         nullptr, D, work.data_ptr(), cur_stream(), c, &nblk));
+  return nblk;
+}
+
+// G [n, n] fp64 = the buckets' partials (works[b], nblks[b] blocks) reduced, summed in order
+void gram_reduce_multi(const std::vector<Tensor>& works, const std::vector<int64_t>& nblks,
+                       int64_t n, Tensor& G) {
+  TORCH_CHECK(!works.empty() && works.size() == nblks.size() && works.size() <= 32,
+              "gram_reduce_multi: 1..32 buckets");
+  TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kDouble && G.is_contiguous() && G.numel() >= n * n,
+              "G must be a contiguous fp64 [n, n] GPU tensor");
+  std::vector<const float*> parts;
+  std::vector<int> nb;
+  const int P = 16 * static_cast<int>((n + 15) / 16);
+  for (size_t b = 0; b < works.size(); ++b) {
+    TORCH_CHECK(works[b].is_cuda() && works[b].scalar_type() == at::kFloat && works[b].is_contiguous() &&
+                    works[b].get_device() == G.get_device() &&
+                    works[b].numel() >= nblks[b] * P * P && nblks[b] >= 1,
+                "gram_reduce_multi: fp32 workspaces holding nblk x P x P partials");
+    parts.push_back(works[b].data_ptr<float>());
+    nb.push_back(static_cast<int>(nblks[b]));
+  }
+  const c10::DeviceGuard guard(G.device());
+  CML_CHECK_HIP(cml::launch_gram_reduce_multi(parts.data(), nb.data(), static_cast<int>(parts.size()),
+                                              static_cast<int>(n), G.data_ptr<double>(), cur_stream()));
+}
+
 // out (int32 [1]) = medoid of the finite rows of G (fp64 [n, n])
 void gram_center(const Tensor& G, int64_t n, Tensor& out) {
   TORCH_CHECK(G.is_cuda() && G.scalar_type() == at::kDouble && G.is_contiguous() && G.numel() >= n * n,
@@ -2307,6 +2347,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sel"), py::arg("guard") = false, py::arg("center_out") = py::none(),
         py::arg("sel_counts") = py::none());
   m.def("gram_sum", &gram_sum, "sum of per-bucket Gram partials in bucket order");
+  m.def("gram_partial", &gram_partial, "Gram stage 1 into a per-bucket workspace (block count)",
+        py::arg("X"), py::arg("n"), py::arg("D"), py::arg("work"), py::arg("center") = py::none());
+  m.def("gram_reduce_multi", &gram_reduce_multi,
+        "reduce several buckets' Gram partials into G in one launch (bucket order)");
   m.def("agg_update_multi", &agg_update_multi,
         "fused robust aggregation + optimizer step over several buckets in one launch");
   m.def("gossip_workspace_bytes", &gossip_workspace_bytes);

@@ -275,6 +275,43 @@ __global__ __launch_bounds__(kGBlock) void gram_partial_kernel(const T* __restri
   }
 }
 
+// Deferred reduce of several buckets' stage-1 partials in ONE launch (the engine's early Grams:
+// each bucket's partial kernel runs as its exchange lands, the reduces of all buckets run once in
+// step()): G = sum over b in order of (fixed-order fp64 tree over bucket b's block partials) --
+// the adds of one gram_reduce_kernel per bucket into a slot followed by gram_sum_kernel.
+constexpr int kMaxRedBuckets = 32;
+struct RedTable {
+  const float* part[kMaxRedBuckets];
+  int nblk[kMaxRedBuckets];
+};
+
+__global__ __launch_bounds__(256) void gram_reduce_multi_kernel(RedTable t, int nb, int P, int n,
+                                                               double* __restrict__ G) {
+  __shared__ double red[256];
+  const int e = blockIdx.x;
+  const int row = e / P, col = e % P;
+  if (row >= n || col >= n || (row / 16) > (col / 16)) return;
+  double acc = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    const float* part = t.part[b];
+    double s = 0.0;
+    for (int k = threadIdx.x; k < t.nblk[b]; k += blockDim.x)
+      s += static_cast<double>(part[static_cast<int64_t>(k) * P * P + e]);
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    acc = b == 0 ? red[0] : acc + red[0];
+    __syncthreads();   // red[] is reused by the next bucket
+  }
+  if (threadIdx.x == 0) {
+    G[row * n + col] = acc;
+    if ((row / 16) < (col / 16)) G[col * n + row] = acc;   // mirror off-diagonal tiles
+  }
+}
+
 // G = sum over b of Gb[b] (fp64 [nb][E]), added in bucket order: the same adds as accumulating
 // the per-bucket Grams into G one after another (the engine's early-Gram partials, one launch)
 __global__ __launch_bounds__(256) void gram_sum_kernel(const double* __restrict__ Gb, int nb,
@@ -354,9 +391,10 @@ int gram_blocks(int64_t D, int cols) {
   return static_cast<int>(b);
 }
 
+// Stage 1 (and, with Gm != null, stage 2); returns the number of partial blocks.
 template <typename T, int TT, int G>
-void launch_gram_t(const T* X, int64_t ld, int n, const int* rows, int64_t D, float* part,
-                   double* Gm, int acc, const int* center, hipStream_t st) {
+int launch_gram_t(const T* X, int64_t ld, int n, const int* rows, int64_t D, float* part,
+                  double* Gm, int acc, const int* center, hipStream_t st) {
   const int nb = gram_blocks(D, gram_cols<T, TT, G>());
   if (center)
     gram_partial_kernel<T, TT, G, true><<<nb, kGBlock, 0, st>>>(X, ld, n, rows, D, part, center);
@@ -364,20 +402,21 @@ void launch_gram_t(const T* X, int64_t ld, int n, const int* rows, int64_t D, fl
     gram_partial_kernel<T, TT, G, false><<<nb, kGBlock, 0, st>>>(X, ld, n, rows, D, part, nullptr);
   // (packed launches fold into the top-left block; the reduce skips elements >= n anyway)
   const int P = 16 * TT;
-  gram_reduce_kernel<<<P * P, 256, 0, st>>>(part, nb, P, n, Gm, acc);
+  if (Gm) gram_reduce_kernel<<<P * P, 256, 0, st>>>(part, nb, P, n, Gm, acc);
+  return nb;
 }
 
 template <typename T>
-void launch_gram_dispatch(const T* x, int64_t ld, int n, const int* rows, int64_t D, float* part,
-                          double* G, int acc, const int* c, hipStream_t st) {
-  if (n == 1) launch_gram_t<T, 1, 16>(x, ld, n, rows, D, part, G, acc, c, st);
-  else if (n == 2) launch_gram_t<T, 1, 8>(x, ld, n, rows, D, part, G, acc, c, st);
-  else if (n <= 4) launch_gram_t<T, 1, 4>(x, ld, n, rows, D, part, G, acc, c, st);
-  else if (n <= 8) launch_gram_t<T, 1, 2>(x, ld, n, rows, D, part, G, acc, c, st);
-  else if (n <= 16) launch_gram_t<T, 1, 1>(x, ld, n, rows, D, part, G, acc, c, st);
-  else if (n <= 32) launch_gram_t<T, 2, 1>(x, ld, n, rows, D, part, G, acc, c, st);
-  else if (n <= 48) launch_gram_t<T, 3, 1>(x, ld, n, rows, D, part, G, acc, c, st);
-  else launch_gram_t<T, 4, 1>(x, ld, n, rows, D, part, G, acc, c, st);
+int launch_gram_dispatch(const T* x, int64_t ld, int n, const int* rows, int64_t D, float* part,
+                         double* G, int acc, const int* c, hipStream_t st) {
+  if (n == 1) return launch_gram_t<T, 1, 16>(x, ld, n, rows, D, part, G, acc, c, st);
+  if (n == 2) return launch_gram_t<T, 1, 8>(x, ld, n, rows, D, part, G, acc, c, st);
+  if (n <= 4) return launch_gram_t<T, 1, 4>(x, ld, n, rows, D, part, G, acc, c, st);
+  if (n <= 8) return launch_gram_t<T, 1, 2>(x, ld, n, rows, D, part, G, acc, c, st);
+  if (n <= 16) return launch_gram_t<T, 1, 1>(x, ld, n, rows, D, part, G, acc, c, st);
+  if (n <= 32) return launch_gram_t<T, 2, 1>(x, ld, n, rows, D, part, G, acc, c, st);
+  if (n <= 48) return launch_gram_t<T, 3, 1>(x, ld, n, rows, D, part, G, acc, c, st);
+  return launch_gram_t<T, 4, 1>(x, ld, n, rows, D, part, G, acc, c, st);
 }
 }  // namespace
 
@@ -400,6 +439,34 @@ hipError_t launch_gram(int dtype, const void* X, int64_t ld, int n, const int* r
   else
     launch_gram_dispatch(reinterpret_cast<const float*>(X), ld, n, rows, D, part, G, accumulate,
                          center, stream);
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_partial(int dtype, const void* X, int64_t ld, int n, const int* rows,
+                               int64_t D, void* work, hipStream_t stream, const int* center,
+                               int* nblk) {
+  if (n < 1 || n > 64 || D < 1) return hipErrorInvalidValue;
+  const int es = dtype == DT_BF16 ? 2 : 4;
+  if ((ld % (16 / es)) != 0 || (reinterpret_cast<uintptr_t>(X) % 16) != 0) return hipErrorInvalidValue;
+  float* part = reinterpret_cast<float*>(work);
+  *nblk = dtype == DT_BF16
+              ? launch_gram_dispatch(reinterpret_cast<const bf16*>(X), ld, n, rows, D, part, nullptr,
+                                     0, center, stream)
+              : launch_gram_dispatch(reinterpret_cast<const float*>(X), ld, n, rows, D, part,
+                                     nullptr, 0, center, stream);
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_reduce_multi(const float* const* parts, const int* nblks, int nb, int n,
+                                    double* G, hipStream_t stream) {
+  if (n < 1 || n > 64 || nb < 1 || nb > kMaxRedBuckets) return hipErrorInvalidValue;
+  RedTable t{};
+  for (int b = 0; b < nb; ++b) {
+    t.part[b] = parts[b];
+    t.nblk[b] = nblks[b];
+  }
+  const int P = 16 * gram_tiles(n);
+  gram_reduce_multi_kernel<<<P * P, 256, 0, stream>>>(t, nb, P, n, G);
   return hipGetLastError();
 }
 

@@ -86,6 +86,14 @@ hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m,
                                  double eps, double tol, double tau, float* w, double* scores,
                                  int* sel, hipStream_t stream, int guard = 0,
                                  int* center_out = nullptr, double* sel_counts = nullptr);
+// Stage 1 of launch_gram only: per-workgroup [P, P] fp32 partials into work (*nblk of them, P =
+// 16 ceil(n / 16)); launch_gram_reduce_multi then reduces nb buckets' partials into G in ONE
+// launch, bit-identical to one launch_gram per bucket into slots summed by launch_gram_sum.
+hipError_t launch_gram_partial(int dtype, const void* X, int64_t ld, int n, const int* rows,
+                               int64_t D, void* work, hipStream_t stream, const int* center,
+                               int* nblk);
+hipError_t launch_gram_reduce_multi(const float* const* parts, const int* nblks, int nb, int n,
+                                    double* G, hipStream_t stream);
 // G[e] = sum_b Gb[b][e] in b order (the early-Gram per-bucket partials), e < E.
 hipError_t launch_gram_sum(const double* Gb, int nb, int64_t E, double* G, hipStream_t stream);
 

@@ -117,3 +117,31 @@ def test_gram_sum_and_negative_center_gpu():
     G0 = K.gram(X, n=6)
     G1 = K.gram(X, n=6, center=torch.tensor([-1], dtype=torch.int32, device="cuda"))
     assert torch.equal(G0, G1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 3, 8, 20])
+def test_gram_deferred_multi_reduce_bitwise(n):
+    """Per-bucket stage-1 partials + ONE multi-bucket reduce == one gram() per bucket into slots
+    summed in bucket order (the engine's early-Gram path), bit for bit; centered and not."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from consensusml_amd.ops.native import lib
+    torch.manual_seed(n)
+    lens = [4096, 70000, 1024, 333333 // 8 * 8]
+    Xs = [torch.randn(n, L, device="cuda").bfloat16() for L in lens]
+    for center in (None, torch.tensor([n // 2], dtype=torch.int32, device="cuda")):
+        slots = torch.zeros(len(lens), n, n, dtype=torch.float64, device="cuda")
+        for i, X in enumerate(Xs):
+            K.gram(X, n=n, out=slots[i], center=center)
+        want = torch.empty(n, n, dtype=torch.float64, device="cuda")
+        K.gram_sum(slots, want)
+        works, nblks = [], []
+        for X in Xs:
+            ws = torch.empty(int(lib().gram_workspace_bytes(n, X.shape[1])) // 4 + 1,
+                             dtype=torch.float32, device="cuda")
+            nblks.append(lib().gram_partial(X, n, X.shape[1], ws, center))
+            works.append(ws)
+        got = torch.empty(n, n, dtype=torch.float64, device="cuda")
+        lib().gram_reduce_multi(works, nblks, n, got)
+        assert torch.equal(got, want)
