@@ -53,11 +53,15 @@ def main():
             eb = float((b.float() - ref).abs().max() / ref.abs().max())
             ta = _t(lambda: dy.t() @ x)
             tb = _t(lambda: L.wgrad1x1(nhwc(dy), nhwc(x), torch.bfloat16))
+            # NT on transposed operands (what the bias-free Llama linears do): transposes included
+            tc = _t(lambda: torch.matmul(L.transpose_bf16(dy), L.transpose_bf16(x).t()))
             fl = 2.0 * T * N * K
             print(json.dumps({"T": T, "N": N, "K": K, "hipblaslt_us": round(ta * 1e3, 1),
                               "wgrad1x1_us": round(tb * 1e3, 1),
+                              "nt_transposed_us": round(tc * 1e3, 1),
                               "hipblaslt_tflops": round(fl / ta / 1e9, 1),
                               "wgrad1x1_tflops": round(fl / tb / 1e9, 1),
+                              "nt_transposed_tflops": round(fl / tc / 1e9, 1),
                               "err_hipblaslt": ea, "err_wgrad1x1": eb}), flush=True)
 
 
