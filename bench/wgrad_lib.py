@@ -23,6 +23,10 @@ SHAPES = [
     (1024, 2048, 1, 1, 7, 1),
     (128, 128, 3, 2, 56, 1), (256, 256, 3, 2, 28, 1), (512, 512, 3, 2, 14, 1),
 ]
+# the own-kernel (core) set, for the own-vs-own A/B (CML_WGRAD_DMA=0 / 1); calls = 0: not on the
+# library in the step
+CORE = [(128, 512, 1, 1, 28, 0), (512, 128, 1, 1, 28, 0), (256, 1024, 1, 1, 14, 0),
+        (512, 2048, 1, 1, 7, 0), (2048, 512, 1, 1, 7, 0)]
 
 
 def _time(f, reps):
@@ -44,12 +48,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("batch", nargs="?", type=int, default=2048)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--core", action="store_true", help="also the own-kernel set")
     args = ap.parse_args()
     configure_miopen()
     torch.backends.cudnn.benchmark = True
     N, dev, cl = args.batch, torch.device("cuda"), torch.channels_last
     tot_lib = tot_best = 0.0
-    for cin, cout, k, s, hw, calls in SHAPES:
+    for cin, cout, k, s, hw, calls in SHAPES + (CORE if args.core else []):
         ho = (hw + 2 * (k // 2) - k) // s + 1
         x = torch.randn(N, cin, hw, hw, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
         dy = torch.randn(N, cout, ho, ho, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
@@ -73,7 +78,8 @@ def main():
             f_own = None
         if f_own is not None:
             t_own = _time(f_own, args.reps)
-            out = f_own().float().reshape(cout, -1)
+            out = f_own().float()
+            out = (out.permute(0, 2, 3, 1) if k == 3 else out).reshape(cout, -1)
             r = ref.permute(0, 2, 3, 1).reshape(cout, -1) if k == 3 else ref.reshape(cout, -1)
             err = ((out - r).norm() / r.norm()).item()
         byt = (x.numel() + dy.numel()) * 2

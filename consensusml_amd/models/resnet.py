@@ -136,11 +136,14 @@ class _Conv1x1Fn(torch.autograd.Function):
 # same box). The 64-channel layer-1 shapes are at the HBM floor on MIOpen.
 _CORE = {(128, 512), (512, 128), (256, 1024), (512, 2048), (2048, 512)}
 _ALL = _CORE | {(256, 128), (512, 256), (1024, 256), (1024, 512)}
+# + the layer-4 downsample (its input pre-subsampled to 7 x 7, so a stride-1 1x1)
+_WIDE = _ALL | {(1024, 2048)}
+_SETS = {"core": _CORE, "all": _ALL, "wide": _WIDE}
 
 
 def own_wgrad_ok(cin: int, cout: int) -> bool:
     p = _P()
-    return p.own_wgrad1x1 and (cin, cout) in (_ALL if p.wgrad1x1_set == "all" else _CORE)
+    return p.own_wgrad1x1 and (cin, cout) in _SETS[p.wgrad1x1_set]
 
 
 class Conv1x1(nn.Conv2d):

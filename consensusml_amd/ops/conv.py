@@ -634,7 +634,7 @@ def _zero_row(device: torch.device) -> torch.Tensor:
     """A cached row of zeros (padding source of conv_gemm's gathered loads)."""
     z = _ZERO_ROWS.get(device)
     if z is None:
-        z = _ZERO_ROWS[device] = torch.zeros(64, dtype=torch.bfloat16, device=device)
+        z = _ZERO_ROWS[device] = torch.zeros(256, dtype=torch.bfloat16, device=device)
     return z
 
 
@@ -752,8 +752,19 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
 
 
 def _wgrad3x3_s2(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """Weight gradient of a stride-2 / padding-1 3x3 conv (MIOpen; an own nine-tap kernel over the
-    raw input rows measured 1.1-1.45x slower, docs/PERFORMANCE.md "Round 4")."""
+    """Weight gradient of a stride-2 / padding-1 3x3 conv: ``wgrad3x3s2`` (wgrad1x1.hip's LDS-DMA
+    kernel on the implicit im2col of x, the padding rows gathered from a zero row) when the shape
+    has a plan and PerfPolicy.own_wgrad3x3_s2 is on, else MIOpen. (An own nine-tap kernel over the
+    raw input rows measured 1.1-1.45x slower than MIOpen, docs/PERFORMANCE.md "Round 4".)
+    Batch 2048 (profiles/r05_16/): 256 -> 256 at 28 x 28 585-603 us vs MIOpen 692-704, 512 -> 512
+    at 14 x 14 555-603 vs 644-674; the 128-channel layer-2 conv (128 x 128 tiles, x gathered 2.25x
+    and dy re-read per tap through L2) 969 vs 850 stays on MIOpen (Ci < 256)."""
+    N, Ci, H, W = x.shape
+    if (_P().own_wgrad3x3_s2 and Ci >= 256 and x.is_cuda and dy.dtype == torch.bfloat16
+            and x.dtype == torch.bfloat16
+            and lib().wgrad3x3s2_ok(N, H, W, dy.shape[1], Ci)):
+        return lib().wgrad3x3s2(dy, x.contiguous(memory_format=torch.channels_last), w.dtype,
+                                _zero_row(dy.device))
     return torch.ops.aten.convolution_backward(
         dy, x, w, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
 

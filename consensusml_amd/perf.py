@@ -50,7 +50,7 @@ class PerfPolicy:
     fused_conv1x1: bool = True            # conv1x1 + BN statistics / bn2 prologue kernels
     conv1x1g: str = "auto"                # fused-kernel family: auto | quad | regstage
     own_wgrad1x1: bool = True             # wgrad1x1.hip for the OWN_WGRAD_SHAPES set
-    wgrad1x1_set: str = "core"            # core (5 shapes) | all (9)
+    wgrad1x1_set: str = "wide"            # core (5 shapes) | all (9) | wide (all + downsample)
     fused_bn3_bwd: bool = True            # identity-tail backward inside conv3's kernels
     fused_bn3_bwd_max_planes: int = 128
     recompute_tail: bool = True           # identity tails without a stored z3
@@ -73,6 +73,7 @@ class PerfPolicy:
     bn1_sums_lib_conv1: bool = False      # ... also behind a library conv1 (layers 3-4): 0.4-0.6
                                           # ms/step SLOWER (pass 26, profiles/r03_26/)
     own_wgrad3x3: bool = True             # wgrad3x3.hip weight gradient
+    own_wgrad3x3_s2: bool = True          # stride-2 3x3 weight gradient on the wgrad DMA kernel
     own_conv3x3_s2: bool = True           # stride-2 3x3: conv_gemm forward + BN stats, parity-class
                                           # data gradient (+ bn1 backward sums)
     # ---------------------------------------------------------------- transformers / engine
@@ -114,7 +115,7 @@ class PerfPolicy:
             fused_conv1x1=_env_bool("CML_FUSED_CONV1X1", True),
             conv1x1g={"0": "regstage", "3": "quad"}.get(os.environ.get("CML_C1G", ""), "auto"),
             own_wgrad1x1=_env_bool("CML_WGRAD1X1", True),
-            wgrad1x1_set=_env_str("CML_WGRAD1X1_SET", "core"),
+            wgrad1x1_set=_env_str("CML_WGRAD1X1_SET", "wide"),
             fused_bn3_bwd=_env_bool("CML_FUSED_BN3_BWD", True),
             fused_bn3_bwd_max_planes=_env_int("CML_FUSED_BN3_BWD_MAX_PLANES", 128),
             recompute_tail=_env_bool("CML_RECOMPUTE_TAIL", True),
@@ -134,6 +135,7 @@ class PerfPolicy:
             bn1_dgrad_sums=_env_bool("CML_BN1_DGRAD_SUMS", True),
             bn1_sums_lib_conv1=_env_bool("CML_BN1_SUMS_LIB_CONV1", False),
             own_wgrad3x3=_env_bool("CML_WGRAD3X3", True),
+            own_wgrad3x3_s2=_env_bool("CML_WGRAD3X3_S2", True),
             own_conv3x3_s2=_env_bool("CML_CONV3X3_S2", True),
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),
             flash_attn=_env_bool("CML_FLASH_ATTN", True),
@@ -170,8 +172,9 @@ class PerfPolicy:
         if self.conv1x1g not in ("auto", "quad", "regstage"):
             raise ValueError(f"conv1x1g must be auto | quad | regstage, not "
                              f"{self.conv1x1g!r}")
-        if self.wgrad1x1_set not in ("core", "all"):
-            raise ValueError(f"wgrad1x1_set must be core | all, not {self.wgrad1x1_set!r}")
+        if self.wgrad1x1_set not in ("core", "all", "wide"):
+            raise ValueError(f"wgrad1x1_set must be core | all | wide, not "
+                             f"{self.wgrad1x1_set!r}")
         return self
 
 

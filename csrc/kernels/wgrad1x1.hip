@@ -284,6 +284,172 @@ __global__ __launch_bounds__((TM / 64) * (TN / 64) * 64) void wgrad1x1_kernel(
       }
 }
 
+// ---- plain (no prologue) variant on LDS-DMA staging, deeper pipeline and 256-wide tiles.
+//
+// The register-staged kernel above keeps one 64-pixel chunk in flight per workgroup (the VGPRs
+// it is prefetched into) and moves it to LDS with ds_write_b128 (~79 B/clk/CU); on the 14 x 14
+// and 7 x 7 shapes that leaves it at 0.54-0.74 PFLOP/s, slower than MIOpen on (1024, 256) /
+// (1024, 512) (profiles/r05_12/wgrad_lib.jsonl). Here:
+//   * dy / x rows go global -> LDS by global_load_lds_dwordx4 (no VGPR staging, no LDS store
+//     transfer), NS stages of 32 pixels, NS - 1 chunks in flight per workgroup; each wave waits
+//     for its own DMAs of the chunk with a counted vmcnt, then one s_barrier per chunk (no
+//     vmcnt(0) drain: __syncthreads would wait for the chunks still in flight);
+//   * tiles of 256 (co) x 256 (ci) with 8 waves of 64 x 128 (x re-read Co / 256, dy Ci / 256
+//     times instead of / 128), or 128 x 256 / 256 x 128 with 4 waves when a dimension is 128;
+//   * the swizzle of the register-staged images (img_off) applied on the SOURCE side, since the
+//     DMA writes each 1-KiB wave piece lane-linear; fragment reads unchanged (ds_read_b64_tr_b16);
+//   * work items (split, tile) mapped XCD-aware: the tiles of one pixel range share an XCD's L2
+//     (they read the same dy rows / x rows).
+// Requires P % 32 == 0 and 16-B aligned rows (the launcher falls back otherwise).
+constexpr int kDmaKC = 32;
+
+// s_waitcnt vmcnt(N) expcnt(7) lgkmcnt(0) (gfx9 encoding: vmcnt bits 3:0 and 15:14)
+template <int N>
+__device__ __forceinline__ void vm_wait_lgkm0() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70);
+}
+
+// One staged chunk's MFMAs (wave tile 64 x 32 NB). The __restrict__ operands give the inlined
+// LDS reads alias-scope metadata, which keeps the compiler's LDS-DMA tracking from putting a
+// vmcnt(0) in front of them (it would wait for the chunks still in flight; the kernel orders the
+// DMA itself: counted vmcnt + barrier).
+template <int RA, int RB, int NB>
+__device__ __forceinline__ void dma_chunk(const char* __restrict__ ab, const char* __restrict__ bb,
+                                          f32x16 (&acc)[2][NB], int wm, int wn, int h, int q,
+                                          int grp, int pq) {
+#pragma unroll
+  for (int ks = 0; ks < kDmaKC / 16; ++ks) {
+    bf16x8_t A[2], B[NB];
+    const int r0 = 16 * ks + 8 * h + q;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int cha = 8 * wm + 4 * e + 2 * (grp & 1) + (pq >> 1);
+      A[e] = cat(ld_tr(ab + img_off<RA>(r0, cha) + 8 * (pq & 1)),
+                 ld_tr(ab + img_off<RA>(r0 + 4, cha) + 8 * (pq & 1)));
+    }
+#pragma unroll
+    for (int e = 0; e < NB; ++e) {
+      const int chb = 4 * NB * wn + 4 * e + 2 * (grp & 1) + (pq >> 1);
+      B[e] = cat(ld_tr(bb + img_off<RB>(r0, chb) + 8 * (pq & 1)),
+                 ld_tr(bb + img_off<RB>(r0 + 4, chb) + 8 * (pq & 1)));
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int e = 0; e < NB; ++e) acc[a][e] = mfma(A[a], B[e], acc[a][e]);
+  }
+}
+
+// S2: the B operand is the implicit im2col of a 3x3 / stride-2 / padding-1 conv's input:
+// column n = tap * Ci + ci (tap = 3 dh + dw), row = output pixel o = (img, oh, ow) ->
+// x[img][2 oh + dh - 1][2 ow + dw - 1][ci], or the zero row outside the image. A TN-wide column
+// tile lies inside one tap (TN divides Ci), and the DMA source address is per lane, so the gather
+// costs only its address arithmetic. dW comes out as [Co][tap][Ci] (channels_last [Co, Ci, 3, 3]).
+struct DmaArgs {
+  const uint16_t* dy;     // [P][Co]
+  const uint16_t* x;      // [P][Ci] (1x1) or [img][H][W][Ci] (S2)
+  const uint16_t* zero;   // >= 512 B of zeros (S2)
+  float* part;            // [split][Co][ncol]
+  int Co, ncol, Ci;       // ncol = Ci (1x1) or 9 Ci (S2)
+  int tiles_n, tiles, nwork, nchunk, cps;
+  int H, W, Ho, Wo;       // S2
+};
+
+template <int TM, int TN, int NS, int WN, bool S2>
+__global__ __launch_bounds__((TM / 64) * (TN / WN) * 64) void wgrad_dma_kernel(DmaArgs a) {
+  constexpr int NW = (TM / 64) * (TN / WN), NB = WN / 32;
+  constexpr int RA = TM * 2, RB = TN * 2;                 // staged row bytes
+  constexpr int LPA = RA / 16, LPB = RB / 16;             // lanes per row
+  constexpr int IA = kDmaKC * LPA / 64, IB = kDmaKC * LPB / 64;   // 1-KiB pieces per chunk
+  constexpr int L = (IA + IB) / NW;                       // pieces per wave per chunk
+  static_assert((IA + IB) % NW == 0 && IA % NW == 0, "piece split");
+  constexpr int STG = kDmaKC * (RA + RB);
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) void g_void;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / (TN / WN), wn = wave % (TN / WN);
+  const int h = lane >> 5, r = lane & 31;
+  const int gi = lane & 15, grp = lane >> 4, q = gi >> 2, pq = gi & 3;
+
+  // work item: bijective XCD remap (consecutive items on one XCD), tile fastest
+  const int b = blockIdx.x, xcd = b & 7, q8 = a.nwork >> 3, r8 = a.nwork & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int split = t / a.tiles, tile = t - split * a.tiles;
+  const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+  const int co0 = tm * TM, n0 = tn * TN;
+  const int c_lo = split * a.cps;
+  const int n = min(a.nchunk, c_lo + a.cps) - c_lo;
+  // S2: this tile's tap and channel base (uniform)
+  const int tap = S2 ? n0 / a.Ci : 0, cb = S2 ? n0 - tap * a.Ci : n0;
+  const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+  const int hw = a.Ho * a.Wo;
+
+  // this wave's pieces: j = wave + NW u; j < IA -> dy rows, else x rows
+  auto issue = [&](int c, int s) {
+    char* base = smem + s * STG;
+    const int64_t p0 = static_cast<int64_t>(c) * kDmaKC;
+#pragma unroll
+    for (int u = 0; u < L; ++u) {
+      const int j = wave + NW * u;
+      if (j < IA) {
+        const int row0 = j * (64 / LPA), row = row0 + lane / LPA, pc = lane % LPA;
+        const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        __builtin_amdgcn_global_load_lds(
+            (g_void*)(a.dy + (p0 + row) * a.Co + co0 + 8 * ch), (lds_void*)(base + row0 * RA), 16,
+            0, 0);
+      } else {
+        const int jb = j - IA;
+        const int row0 = jb * (64 / LPB), row = row0 + lane / LPB, pc = lane % LPB;
+        const int ch = pc ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        const uint16_t* src;
+        if constexpr (S2) {
+          const int p = static_cast<int>(p0) + row, img = p / hw, rem = p - img * hw;
+          const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+          const int ih = 2 * oh + dh, iw = 2 * ow + dw;
+          src = (ih >= 0 && iw >= 0 && ih < a.H && iw < a.W)
+                    ? a.x + ((static_cast<int64_t>(img) * a.H + ih) * a.W + iw) * a.Ci + cb + 8 * ch
+                    : a.zero + 8 * ch;
+        } else {
+          src = a.x + (p0 + row) * a.Ci + cb + 8 * ch;
+        }
+        __builtin_amdgcn_global_load_lds((g_void*)src,
+                                         (lds_void*)(base + kDmaKC * RA + row0 * RB), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x16 acc[2][NB] = {};
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < n) issue(c_lo + s, s);
+  for (int i = 0; i < n; ++i) {
+    // chunk i landed for this wave's pieces; every wave done with chunk i - 1
+    if (i + NS - 2 < n) vm_wait_lgkm0<L * (NS - 2)>();
+    else vm_wait_lgkm0<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (i + NS - 1 < n) issue(c_lo + i + NS - 1, (i + NS - 1) % NS);
+    const char* ab = smem + (i % NS) * STG;
+    dma_chunk<RA, RB, NB>(ab, ab + kDmaKC * RA, acc, wm, wn, h, q, grp, pq);
+  }
+  // partial [split][Co][ncol]: lane r = column, register k = co row (k&3) + 8 (k>>2) + 4 h
+  float* pw = a.part + static_cast<int64_t>(split) * a.Co * a.ncol;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < NB; ++e)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int co = co0 + 64 * wm + 32 * i + (k & 3) + 8 * (k >> 2) + 4 * h;
+        const int col = n0 + WN * wn + 32 * e + r;
+        pw[static_cast<int64_t>(co) * a.ncol + col] = acc[i][e][k];
+      }
+}
+
 // dW = sum over S splits (fixed order), 4 elements per thread, bf16 or fp32 out
 template <bool BF16>
 __global__ __launch_bounds__(256) void wgrad1x1_fold_kernel(const float* __restrict__ part, int S,
@@ -464,8 +630,93 @@ bool launch_tile(int TM, int TN, dim3 grid, size_t lds, hipStream_t st, const ui
 // registers, fewer chunks per workgroup)
 int chunk_of(int, int) { return 64; }
 
+namespace {
+// LDS-DMA kernel tile for a plain (no prologue / column sums) weight gradient, or false
+// (CML_WGRAD_DMA=0 disables it: A/B)
+bool dma_tile(int64_t P, int Co, int Ci, int* TM, int* TN) {
+  static const bool on = [] {
+    const char* e = getenv("CML_WGRAD_DMA");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || P < kDmaKC || P % kDmaKC || P >= (1ll << 31)) return false;
+  if (Co % 256 == 0 && Ci % 256 == 0) { *TM = 256; *TN = 256; }
+  else if (Co % 128 == 0 && Ci % 256 == 0) { *TM = 128; *TN = 256; }
+  else if (Co % 256 == 0 && Ci % 128 == 0) { *TM = 256; *TN = 128; }
+  else return false;
+  return true;
+}
+
+void dma_plan(int64_t P, int Co, int ncol, int TM, int TN, int* splits, int* cps) {
+  const int tiles = (Co / TM) * (ncol / TN);
+  const int nchunk = static_cast<int>(P / kDmaKC);
+  // one workgroup per CU (the LDS of the deep pipeline); two for the 64-KiB 128 x 128 tile
+  int s = (TM == 128 && TN == 128 ? 512 : 256) / tiles;
+  s = s < 1 ? 1 : (s > nchunk ? nchunk : s);
+  const int c = (nchunk + s - 1) / s;
+  *cps = c;
+  *splits = (nchunk + c - 1) / c;
+}
+
+template <int TM, int TN, int NS, int WN, bool S2>
+hipError_t launch_dma(DmaArgs a, int64_t P, int S, int cps, hipStream_t st) {
+  constexpr int NW = (TM / 64) * (TN / WN);
+  constexpr int lds = NS * kDmaKC * (TM + TN) * 2;
+  static_assert(lds <= 160 * 1024, "LDS");
+  auto k = &wgrad_dma_kernel<TM, TN, NS, WN, S2>;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  a.tiles_n = a.ncol / TN;
+  a.tiles = (a.Co / TM) * a.tiles_n;
+  a.nwork = a.tiles * S;
+  a.nchunk = static_cast<int>(P / kDmaKC);
+  a.cps = cps;
+  k<<<a.nwork, NW * 64, lds, st>>>(a);
+  return hipSuccess;
+}
+
+hipError_t launch_dma_tile(int TM, int TN, bool s2, const DmaArgs& a, int64_t P, int S, int cps,
+                           hipStream_t st) {
+  if (TM == 256 && TN == 256) return s2 ? launch_dma<256, 256, 4, 128, true>(a, P, S, cps, st)
+                                        : launch_dma<256, 256, 4, 128, false>(a, P, S, cps, st);
+  if (TM == 128 && TN == 256) return s2 ? launch_dma<128, 256, 6, 128, true>(a, P, S, cps, st)
+                                        : launch_dma<128, 256, 6, 128, false>(a, P, S, cps, st);
+  if (TM == 256 && TN == 128) return s2 ? launch_dma<256, 128, 6, 128, true>(a, P, S, cps, st)
+                                        : launch_dma<256, 128, 6, 128, false>(a, P, S, cps, st);
+  if (TM == 128 && TN == 128 && s2) {
+    // 8 stages (1 workgroup / CU) or 4 (2 workgroups / CU): CML_WGRAD_DMA_NS128 (A/B)
+    static const int ns = [] {
+      const char* e = getenv("CML_WGRAD_DMA_NS128");
+      return e ? atoi(e) : 4;
+    }();
+    return ns == 8 ? launch_dma<128, 128, 8, 64, true>(a, P, S, cps, st)
+                   : launch_dma<128, 128, 4, 64, true>(a, P, S, cps, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+// stride-2 3x3 tiles: TN divides Ci (a column tile inside one tap)
+bool s2_tile(int N, int H, int W, int Co, int Ci, int* TM, int* TN) {
+  if (N < 1 || H < 2 || W < 2 || (H & 1) || (W & 1) || Co % 128 || Ci % 128) return false;
+  const int64_t P = static_cast<int64_t>(N) * (H / 2) * (W / 2);
+  if (P % kDmaKC || P >= (1ll << 31) || static_cast<int64_t>(N) * H * W * Ci >= (1ll << 40))
+    return false;
+  *TM = Co % 256 == 0 ? 256 : 128;
+  *TN = Ci % 256 == 0 ? 256 : 128;
+  return true;
+}
+}  // namespace
+
 void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro) {
   int TM, TN;
+  if (!pro && dma_tile(P, Co, Ci, &TM, &TN)) {
+    dma_plan(P, Co, Ci, TM, TN, splits, cps);
+    return;
+  }
   pick_tile(Co, Ci, &TM, &TN, pro);
   const int KC = chunk_of(TM, TN);
   const int tiles = (Co / TM) * (Ci / TN);
@@ -511,6 +762,21 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
   int S, cps, TM, TN;
   // (the column sums have no 1024-thread tile either: it takes the prologue tiles)
   const bool anypro = pro_sc != nullptr || dmode != DP_NONE || cs != nullptr;
+  if (!anypro && dma_tile(P, Co, Ci, &TM, &TN) &&
+      ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) % 16) == 0) {
+    dma_plan(P, Co, Ci, TM, TN, &S, &cps);
+    DmaArgs da{};
+    da.dy = reinterpret_cast<const uint16_t*>(dy);
+    da.x = reinterpret_cast<const uint16_t*>(x);
+    da.part = part;
+    da.Co = Co;
+    da.ncol = Ci;
+    da.Ci = Ci;
+    const hipError_t e = launch_dma_tile(TM, TN, false, da, P, S, cps, st);
+    if (e != hipSuccess) return e;
+    fold_splits(part, S, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, st);
+    return hipGetLastError();
+  }
   wgrad1x1_plan(P, Co, Ci, &S, &cps, anypro);
   pick_tile(Co, Ci, &TM, &TN, anypro);
   const int KC = chunk_of(TM, TN);
@@ -544,6 +810,41 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
   if (!ok) return hipErrorInvalidValue;
   if (cs) fold_splits(cs_part, S, Co, cs, false, st);
   fold_splits(part, S, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, st);
+  return hipGetLastError();
+}
+
+bool wgrad3x3s2_plan(int N, int H, int W, int Co, int Ci, int* splits) {
+  int TM, TN, cps;
+  if (!s2_tile(N, H, W, Co, Ci, &TM, &TN)) return false;
+  dma_plan(static_cast<int64_t>(N) * (H / 2) * (W / 2), Co, 9 * Ci, TM, TN, splits, &cps);
+  return true;
+}
+
+hipError_t launch_wgrad3x3s2(const void* dy, const void* x, const void* zero, float* part,
+                             void* dw, bool dw_bf16, int N, int H, int W, int Co, int Ci,
+                             hipStream_t st) {
+  int TM, TN, S, cps;
+  if (!s2_tile(N, H, W, Co, Ci, &TM, &TN)) return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) |
+       reinterpret_cast<uintptr_t>(zero)) % 16)
+    return hipErrorInvalidValue;
+  const int64_t P = static_cast<int64_t>(N) * (H / 2) * (W / 2);
+  dma_plan(P, Co, 9 * Ci, TM, TN, &S, &cps);
+  DmaArgs da{};
+  da.dy = reinterpret_cast<const uint16_t*>(dy);
+  da.x = reinterpret_cast<const uint16_t*>(x);
+  da.zero = reinterpret_cast<const uint16_t*>(zero);
+  da.part = part;
+  da.Co = Co;
+  da.ncol = 9 * Ci;
+  da.Ci = Ci;
+  da.H = H;
+  da.W = W;
+  da.Ho = H / 2;
+  da.Wo = W / 2;
+  const hipError_t e = launch_dma_tile(TM, TN, true, da, P, S, cps, st);
+  if (e != hipSuccess) return e;
+  fold_splits(part, S, static_cast<int64_t>(Co) * 9 * Ci, dw, dw_bf16, st);
   return hipGetLastError();
 }
 

@@ -61,3 +61,22 @@ def test_split_fold_vs_fp64(cuda, S, n, bf16):
     ref = part.double().sum(0)
     assert _rel(out, ref) < (6e-3 if bf16 else 1e-6)
     assert torch.equal(out, lib().split_fold(part, bf16))
+
+
+@pytest.mark.parametrize("N,ci,co,hw", [(32, 1024, 256, 14), (16, 512, 128, 28), (32, 128, 512, 28),
+                                        (32, 1024, 2048, 7), (64, 256, 256, 4), (2, 256, 256, 4)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_wgrad1x1_dma_vs_fp32(cuda, N, ci, co, hw, dtype):
+    """The LDS-DMA variant (plain weight gradient, P % 32 == 0, 256 x 256 / 128 x 256 / 256 x 128
+    tiles; down to one 32-pixel chunk) against fp32; bitwise repeatable."""
+    torch.manual_seed(ci * 3 + co + hw)
+    x = torch.randn(N, ci, hw, hw, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    dy = torch.randn(N, co, hw, hw, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    dw = lib().wgrad1x1(dy, x, dtype)
+    X = x.permute(0, 2, 3, 1).reshape(-1, ci).float()
+    D = dy.permute(0, 2, 3, 1).reshape(-1, co).float()
+    ref = (D.t() @ X).view(co, ci, 1, 1)
+    assert _rel(dw, ref) < (6e-3 if dtype == torch.bfloat16 else 1e-5)
+    assert torch.equal(dw, lib().wgrad1x1(dy, x, dtype))
