@@ -778,8 +778,8 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
               "wgrad1x1: dz_z, dz_mask, dz_a, dz_b, dz_c together");
   const c10::DeviceGuard guard(x.device());
   int S = 1, cps = 1;
-  cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps,
-                     sc != nullptr || zp != nullptr);
+  cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps, sc != nullptr,
+                     zp != nullptr ? 1 : 0, false);
   Tensor part = at::empty({S, Co, Ci}, x.options().dtype(at::kFloat));
   Tensor dw = at::empty({Co, Ci, 1, 1}, x.options().dtype(dtype));
   CML_CHECK_HIP(cml::launch_wgrad1x1(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(),
@@ -822,8 +822,8 @@ std::vector<Tensor> wgrad1x1_ex(const Tensor& dy_in, const Tensor& x, const opti
   TORCH_CHECK((sc == nullptr) == (bi == nullptr), "wgrad1x1_ex: pro_sc and pro_bi together");
   const c10::DeviceGuard guard(x.device());
   int S = 1, cps = 1;
-  cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps,
-                     sc != nullptr || dmode != 0 || colsum);
+  cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps, sc != nullptr,
+                     static_cast<int>(dmode), colsum);
   auto f32 = x.options().dtype(at::kFloat);
   Tensor part = at::empty({S, Co, Ci}, f32);
   Tensor dw = at::empty({Co, Ci}, f32);

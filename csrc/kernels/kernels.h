@@ -361,7 +361,9 @@ size_t stem_cola_work_floats(int N, int H, int W, int C);
 // Co x Ci floats (wgrad1x1_plan); dw: bf16 (dw_bf16) or fp32 [Co][Ci]. pro_sc / pro_bi (fp32
 // [Ci], both or neither): x is replaced by max(x * sc + bi, 0) (a BN + ReLU never materialised).
 // pro: a dy or x prologue is applied (the plan then avoids the 1024-thread tile)
-void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro = false);
+// pro: x prologue; dmode: dy prologue (0 none, 1 full, 2 mask, 3 BN-ReLU); cs: column sums
+void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro = false,
+                   int dmode = 0, bool cs = false);
 // dz_z / dz_mask / dz_a / dz_b / dz_c (all or none): dy is the output gradient of a BN + ReLU that
 // consumed the conv output z = dz_z; the staging uses dz = a (mask ? dy : 0) + b z + c instead.
 // General form: dmode 0 none, 1 the dz_* BN-backward prologue above, 2 dz = dz_a (mask ? dy : 0)

@@ -354,17 +354,83 @@ struct DmaArgs {
   int Co, ncol, Ci;       // ncol = Ci (1x1) or 9 Ci (S2)
   int tiles_n, tiles, nwork, nchunk, cps;
   int H, W, Ho, Wo;       // S2
+  // XF modes (1x1 only): PRO x -> max(x sc + bi, 0); DPM dy -> da (mask ? dy : 0) + dc;
+  // cs_part [split][Co]: column sums of the transformed dy (tn == 0 workgroups)
+  const float* sc;
+  const float* bi;
+  const uint8_t* mask;    // [P][Co / 8]
+  const float* da;
+  const float* dc;
+  float* cs_part;
 };
 
-template <int TM, int TN, int NS, int WN, bool S2>
+// XF: the prologues of the register-staged kernel (PRO on x, DP_MASK on dy, column sums), applied
+// once per element in LDS between the chunk's landing and its MFMAs (in place, 16-B items: a
+// thread's items all cover the same 8 channels, so its affine constants sit in registers), with the
+// same rounding points as the staging transforms above. Pipelined one chunk ahead: iteration i
+// transforms chunk i + 1 while its waves multiply chunk i, so the transform costs LDS issue slots,
+// not a serial phase. __restrict__ as in dma_chunk (no compiler vmcnt(0) before these accesses).
+template <int RA, int RB, int NT, bool PRO, bool DPM>
+__device__ __forceinline__ void dma_transform(char* __restrict__ ab, char* __restrict__ bb,
+                                              const uint8_t* __restrict__ mk, int tid,
+                                              const float (&psc)[8], const float (&pbi)[8],
+                                              const float (&da)[8], const float (&dc)[8],
+                                              float (&cs)[8], bool csum) {
+  constexpr int CA = RA / 16, CB = RB / 16;   // 16-B chunks per row
+  if constexpr (DPM) {
+#pragma unroll
+    for (int j = 0; j < kDmaKC * CA / NT; ++j) {
+      const int e = tid + NT * j, row = e / CA, ch = e % CA;
+      uint4* ptr = reinterpret_cast<uint4*>(ab + img_off<RA>(row, ch));
+      const uint4 v = *ptr;
+      const uint32_t bits = mk[row * CA + ch];
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float glo = ((bits >> (2 * i)) & 1u) ? __uint_as_float(w4[i] << 16) : 0.f;
+        const float ghi = ((bits >> (2 * i + 1)) & 1u) ? __uint_as_float(w4[i] & 0xffff0000u) : 0.f;
+        w4[i] = static_cast<uint32_t>(f2bf(fmaf(da[2 * i], glo, dc[2 * i]))) |
+                (static_cast<uint32_t>(f2bf(fmaf(da[2 * i + 1], ghi, dc[2 * i + 1]))) << 16);
+        if (csum) {
+          cs[2 * i] += __uint_as_float(w4[i] << 16);
+          cs[2 * i + 1] += __uint_as_float(w4[i] & 0xffff0000u);
+        }
+      }
+      *ptr = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+  }
+  if constexpr (PRO) {
+#pragma unroll
+    for (int j = 0; j < kDmaKC * CB / NT; ++j) {
+      const int e = tid + NT * j, row = e / CB, ch = e % CB;
+      uint4* ptr = reinterpret_cast<uint4*>(bb + img_off<RB>(row, ch));
+      const uint4 v = *ptr;
+      uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float lo = fmaxf(fmaf(__uint_as_float(w4[i] << 16), psc[2 * i], pbi[2 * i]), 0.f);
+        const float hi =
+            fmaxf(fmaf(__uint_as_float(w4[i] & 0xffff0000u), psc[2 * i + 1], pbi[2 * i + 1]), 0.f);
+        w4[i] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+      }
+      *ptr = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+  }
+}
+
+template <int TM, int TN, int NS, int WN, bool S2, bool PRO = false, bool DPM = false>
 __global__ __launch_bounds__((TM / 64) * (TN / WN) * 64) void wgrad_dma_kernel(DmaArgs a) {
-  constexpr int NW = (TM / 64) * (TN / WN), NB = WN / 32;
+  constexpr int NW = (TM / 64) * (TN / WN), NB = WN / 32, NT = NW * 64;
   constexpr int RA = TM * 2, RB = TN * 2;                 // staged row bytes
   constexpr int LPA = RA / 16, LPB = RB / 16;             // lanes per row
   constexpr int IA = kDmaKC * LPA / 64, IB = kDmaKC * LPB / 64;   // 1-KiB pieces per chunk
   constexpr int L = (IA + IB) / NW;                       // pieces per wave per chunk
+  constexpr bool XF = PRO || DPM;
   static_assert((IA + IB) % NW == 0 && IA % NW == 0, "piece split");
-  constexpr int STG = kDmaKC * (RA + RB);
+  static_assert(!DPM || TM == 256, "the mask tile is one 1-KiB piece: TM == 256");
+  static_assert(!XF || (NT % LPA == 0 && NT % LPB == 0 && !S2), "transform items");
+  constexpr int MSK = DPM ? kDmaKC * TM / 8 : 0;          // mask tile bytes per stage
+  constexpr int STG = kDmaKC * (RA + RB) + MSK;
   typedef __attribute__((address_space(3))) void lds_void;
   typedef __attribute__((address_space(1))) void g_void;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -387,7 +453,30 @@ __global__ __launch_bounds__((TM / 64) * (TN / WN) * 64) void wgrad_dma_kernel(D
   const int dh = tap / 3 - 1, dw = tap % 3 - 1;
   const int hw = a.Ho * a.Wo;
 
-  // this wave's pieces: j = wave + NW u; j < IA -> dy rows, else x rows
+  // XF constants: a thread's transform items cover channels 8 (tid % (R / 16)) .. + 7
+  float psc[8], pbi[8], da[8], dc[8], cs[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) psc[k] = pbi[k] = da[k] = dc[k] = cs[k] = 0.f;
+  if constexpr (PRO) {
+    const int c8 = cb + 8 * (tid % LPB);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      psc[k] = a.sc[c8 + k];
+      pbi[k] = a.bi[c8 + k];
+    }
+  }
+  if constexpr (DPM) {
+    const int c8 = co0 + 8 * (tid % LPA);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      da[k] = a.da[c8 + k];
+      dc[k] = a.dc[c8 + k];
+    }
+  }
+  const bool csum = DPM && a.cs_part != nullptr && tn == 0;   // uniform per workgroup
+
+  // this wave's pieces: j = wave + NW u; j < IA -> dy rows, else x rows; DPM: wave 0 also the
+  // mask tile (32 rows x TM / 8 bytes = one piece)
   auto issue = [&](int c, int s) {
     char* base = smem + s * STG;
     const int64_t p0 = static_cast<int64_t>(c) * kDmaKC;
@@ -419,22 +508,79 @@ __global__ __launch_bounds__((TM / 64) * (TN / WN) * 64) void wgrad_dma_kernel(D
                                          (lds_void*)(base + kDmaKC * RA + row0 * RB), 16, 0, 0);
       }
     }
+    if constexpr (DPM) {
+      if (wave == 0)
+        __builtin_amdgcn_global_load_lds(
+            (g_void*)(a.mask + (p0 + (lane >> 1)) * (a.Co / 8) + co0 / 8 + 16 * (lane & 1)),
+            (lds_void*)(base + kDmaKC * (RA + RB)), 16, 0, 0);
+    }
+  };
+  auto xform = [&](int s) {
+    char* ab = smem + s * STG;
+    dma_transform<RA, RB, NT, PRO, DPM>(ab, ab + kDmaKC * RA,
+                                        reinterpret_cast<const uint8_t*>(ab + kDmaKC * (RA + RB)),
+                                        tid, psc, pbi, da, dc, cs, csum);
   };
 
   f32x16 acc[2][NB] = {};
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < n) issue(c_lo + s, s);
+  // the DMA counts of this wave per chunk: L pieces (+ the mask piece on wave 0)
+  const bool w0m = DPM && wave == 0;
+  if constexpr (XF) {
+    // chunk 0 landed everywhere, then transformed (the loop's first barrier publishes it)
+    if (NS - 1 <= n) {
+      if (w0m) vm_wait_lgkm0<(L + 1) * (NS - 2)>();
+      else vm_wait_lgkm0<L * (NS - 2)>();
+    } else {
+      vm_wait_lgkm0<0>();
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    xform(0);
+  }
   for (int i = 0; i < n; ++i) {
-    // chunk i landed for this wave's pieces; every wave done with chunk i - 1
-    if (i + NS - 2 < n) vm_wait_lgkm0<L * (NS - 2)>();
-    else vm_wait_lgkm0<0>();
+    if constexpr (XF) {
+      // chunk i + 1 landed for this wave's pieces (and chunk i transformed: lgkmcnt(0)); every
+      // wave done with chunk i - 1
+      if (i + NS - 2 < n) {
+        if (w0m) vm_wait_lgkm0<(L + 1) * (NS - 3)>();
+        else vm_wait_lgkm0<L * (NS - 3)>();
+      } else {
+        vm_wait_lgkm0<0>();
+      }
+    } else {
+      // chunk i landed for this wave's pieces; every wave done with chunk i - 1
+      if (i + NS - 2 < n) vm_wait_lgkm0<L * (NS - 2)>();
+      else vm_wait_lgkm0<0>();
+    }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (i + NS - 1 < n) issue(c_lo + i + NS - 1, (i + NS - 1) % NS);
+    if constexpr (XF)
+      if (i + 1 < n) xform((i + 1) % NS);
     const char* ab = smem + (i % NS) * STG;
     dma_chunk<RA, RB, NB>(ab, ab + kDmaKC * RA, acc, wm, wn, h, q, grp, pq);
+  }
+  if constexpr (DPM) {
+    if (csum) {   // fold the threads of each 8-channel group (tid % LPA), fixed order
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[tid * 8 + k] = cs[k];
+      __syncthreads();
+      if (tid < LPA) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float v = 0.f;
+          for (int m = tid; m < NT; m += LPA) v += red[m * 8 + k];
+          a.cs_part[static_cast<int64_t>(split) * a.Co + co0 + 8 * tid + k] = v;
+        }
+      }
+    }
   }
   // partial [split][Co][ncol]: lane r = column, register k = co row (k&3) + 8 (k>>2) + 4 h
   float* pw = a.part + static_cast<int64_t>(split) * a.Co * a.ncol;
@@ -657,12 +803,12 @@ void dma_plan(int64_t P, int Co, int ncol, int TM, int TN, int* splits, int* cps
   *splits = (nchunk + c - 1) / c;
 }
 
-template <int TM, int TN, int NS, int WN, bool S2>
+template <int TM, int TN, int NS, int WN, bool S2, bool PRO = false, bool DPM = false>
 hipError_t launch_dma(DmaArgs a, int64_t P, int S, int cps, hipStream_t st) {
   constexpr int NW = (TM / 64) * (TN / WN);
-  constexpr int lds = NS * kDmaKC * (TM + TN) * 2;
+  constexpr int lds = NS * (kDmaKC * (TM + TN) * 2 + (DPM ? kDmaKC * TM / 8 : 0));
   static_assert(lds <= 160 * 1024, "LDS");
-  auto k = &wgrad_dma_kernel<TM, TN, NS, WN, S2>;
+  auto k = &wgrad_dma_kernel<TM, TN, NS, WN, S2, PRO, DPM>;
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
@@ -677,6 +823,16 @@ hipError_t launch_dma(DmaArgs a, int64_t P, int S, int cps, hipStream_t st) {
   a.cps = cps;
   k<<<a.nwork, NW * 64, lds, st>>>(a);
   return hipSuccess;
+}
+
+template <bool PRO, bool DPM>
+hipError_t launch_dma_xf(int TM, int TN, const DmaArgs& a, int64_t P, int S, int cps,
+                         hipStream_t st) {
+  if (TM == 256 && TN == 256) return launch_dma<256, 256, 4, 128, false, PRO, DPM>(a, P, S, cps, st);
+  if (TM == 256 && TN == 128) return launch_dma<256, 128, 6, 128, false, PRO, DPM>(a, P, S, cps, st);
+  if constexpr (!DPM)
+    if (TM == 128 && TN == 256) return launch_dma<128, 256, 6, 128, false, PRO, DPM>(a, P, S, cps, st);
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_dma_tile(int TM, int TN, bool s2, const DmaArgs& a, int64_t P, int S, int cps,
@@ -699,6 +855,25 @@ hipError_t launch_dma_tile(int TM, int TN, bool s2, const DmaArgs& a, int64_t P,
   return hipErrorInvalidValue;
 }
 
+// DMA eligibility of a wgrad1x1 call: plain; x prologue (PRO); DP_MASK dy prologue (TM 256),
+// with its column sums. CML_WGRAD_DMA_XF=0 keeps the prologue variants on the register-staged
+// kernel (A/B).
+bool dma_ok(int64_t P, int Co, int Ci, bool pro, int dmode, bool cs, int* TM, int* TN) {
+  static const bool xf = [] {
+    const char* e = getenv("CML_WGRAD_DMA_XF");
+    return !(e && e[0] == '0');
+  }();
+  if (dmode != DP_NONE && dmode != DP_MASK) return false;
+  if (cs && dmode != DP_MASK) return false;
+  if ((pro || dmode != DP_NONE) && !xf) return false;
+  if (!dma_tile(P, Co, Ci, TM, TN)) return false;
+  // the 4-wave 256 x 128 tile with prologues ran the layer-2 tail (Co 512, Ci 128, 1.6 M pixels)
+  // at 727 us vs 459 on the staged kernel (profiles/r05_17/): one wave per SIMD carrying both the
+  // transforms and the MFMAs
+  if ((pro || dmode != DP_NONE) && *TN == 128) return false;
+  return dmode != DP_MASK || *TM == 256;
+}
+
 // stride-2 3x3 tiles: TN divides Ci (a column tile inside one tap)
 bool s2_tile(int N, int H, int W, int Co, int Ci, int* TM, int* TN) {
   if (N < 1 || H < 2 || W < 2 || (H & 1) || (W & 1) || Co % 128 || Ci % 128) return false;
@@ -711,12 +886,21 @@ bool s2_tile(int N, int H, int W, int Co, int Ci, int* TM, int* TN) {
 }
 }  // namespace
 
-void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro) {
+void staged_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro);
+
+void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro, int dmode,
+                   bool cs) {
   int TM, TN;
-  if (!pro && dma_tile(P, Co, Ci, &TM, &TN)) {
+  if (dma_ok(P, Co, Ci, pro, dmode, cs, &TM, &TN)) {
     dma_plan(P, Co, Ci, TM, TN, splits, cps);
     return;
   }
+  staged_plan(P, Co, Ci, splits, cps, pro || dmode != DP_NONE || cs);
+}
+
+// plan of the register-staged kernel (pro: any prologue or column sums)
+void staged_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro) {
+  int TM, TN;
   pick_tile(Co, Ci, &TM, &TN, pro);
   const int KC = chunk_of(TM, TN);
   const int tiles = (Co / TM) * (Ci / TN);
@@ -762,8 +946,10 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
   int S, cps, TM, TN;
   // (the column sums have no 1024-thread tile either: it takes the prologue tiles)
   const bool anypro = pro_sc != nullptr || dmode != DP_NONE || cs != nullptr;
-  if (!anypro && dma_tile(P, Co, Ci, &TM, &TN) &&
-      ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) % 16) == 0) {
+  if (dma_ok(P, Co, Ci, pro_sc != nullptr, dmode, cs != nullptr, &TM, &TN)) {
+    // (the caller sized `part` from this plan: no fallback to the staged kernel's splits)
+    if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) % 16)
+      return hipErrorInvalidValue;
     dma_plan(P, Co, Ci, TM, TN, &S, &cps);
     DmaArgs da{};
     da.dy = reinterpret_cast<const uint16_t*>(dy);
@@ -772,12 +958,24 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
     da.Co = Co;
     da.ncol = Ci;
     da.Ci = Ci;
-    const hipError_t e = launch_dma_tile(TM, TN, false, da, P, S, cps, st);
+    da.sc = pro_sc;
+    da.bi = pro_bi;
+    da.mask = dz_mask;
+    da.da = dz_a;
+    da.dc = dz_c;
+    da.cs_part = cs_part;
+    hipError_t e;
+    const bool dpm = dmode == DP_MASK;
+    if (pro_sc && dpm) e = launch_dma_xf<true, true>(TM, TN, da, P, S, cps, st);
+    else if (pro_sc) e = launch_dma_xf<true, false>(TM, TN, da, P, S, cps, st);
+    else if (dpm) e = launch_dma_xf<false, true>(TM, TN, da, P, S, cps, st);
+    else e = launch_dma_tile(TM, TN, false, da, P, S, cps, st);
     if (e != hipSuccess) return e;
+    if (cs) fold_splits(cs_part, S, Co, cs, false, st);
     fold_splits(part, S, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, st);
     return hipGetLastError();
   }
-  wgrad1x1_plan(P, Co, Ci, &S, &cps, anypro);
+  staged_plan(P, Co, Ci, &S, &cps, anypro);
   pick_tile(Co, Ci, &TM, &TN, anypro);
   const int KC = chunk_of(TM, TN);
   const int tiles_n = Ci / TN;

@@ -80,3 +80,50 @@ def test_wgrad1x1_dma_vs_fp32(cuda, N, ci, co, hw, dtype):
     ref = (D.t() @ X).view(co, ci, 1, 1)
     assert _rel(dw, ref) < (6e-3 if dtype == torch.bfloat16 else 1e-5)
     assert torch.equal(dw, lib().wgrad1x1(dy, x, dtype))
+
+
+def _rows(t):
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1]).float()
+
+
+def _bits(mask, C):
+    sh = torch.arange(8, device=mask.device, dtype=torch.uint8)
+    return ((mask.unsqueeze(-1) >> sh) & 1).reshape(mask.shape[0], C).float()
+
+
+@pytest.mark.parametrize("N,ci,co,hw", [(32, 256, 1024, 7), (8, 128, 512, 14), (32, 256, 256, 7),
+                                        (8, 512, 128, 14), (2, 256, 256, 4)])
+@pytest.mark.parametrize("pro", [False, True])
+@pytest.mark.parametrize("colsum", [False, True])
+def test_wgrad1x1_dma_prologues(cuda, N, ci, co, hw, pro, colsum):
+    """The DMA kernel's in-LDS transforms: x prologue max(x sc + bi, 0) and the mode-2 dy
+    prologue a (mask ? dy : 0) + c (Co % 256 == 0) with its column sums, against fp32 on the same
+    bf16 rounding points; the plain and x-prologue calls at Co = 128 too (128 x 256 tile)."""
+    g0 = torch.Generator(device=cuda).manual_seed(ci + co + hw + 7 * pro + colsum)
+    dy = torch.randn(N, co, hw, hw, device=cuda, generator=g0).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    x = torch.randn(N, ci, hw, hw, device=cuda, generator=g0).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    M = N * hw * hw
+    sc = torch.rand(ci, device=cuda, generator=g0) + 0.5
+    bi = torch.randn(ci, device=cuda, generator=g0) * 0.1
+    X = torch.relu(_rows(x) * sc + bi).bfloat16().float() if pro else _rows(x)
+    if co % 256:
+        if colsum:
+            pytest.skip("mode 2 needs Co % 256 == 0 on the DMA kernel")
+        dw = lib().wgrad1x1(dy, x, torch.float32, sc if pro else None, bi if pro else None)
+        ref = _rows(dy).t() @ X
+        assert _rel(dw.view(co, ci), ref) < 1e-5
+        return
+    mask = torch.randint(0, 256, (M, co // 8), device=cuda, generator=g0, dtype=torch.uint8)
+    a = torch.randn(co, device=cuda, generator=g0)
+    c = torch.randn(co, device=cuda, generator=g0) * 0.1
+    dw, cs = lib().wgrad1x1_ex(dy, x, sc if pro else None, bi if pro else None, 2, mask, a, None,
+                               c, colsum)
+    D = (a * (_bits(mask, co) * _rows(dy)) + c).bfloat16().float()
+    assert _rel(dw, D.t() @ X) < 2e-4   # (the reference rounds a * u + c unfused: 1-ulp bf16 ties)
+    if colsum:
+        torch.testing.assert_close(cs, D.sum(0), rtol=1e-4, atol=1e-3 * M ** 0.5)
+    dw2, cs2 = lib().wgrad1x1_ex(dy, x, sc if pro else None, bi if pro else None, 2, mask, a,
+                                 None, c, colsum)
+    assert torch.equal(dw, dw2) and (not colsum or torch.equal(cs, cs2))

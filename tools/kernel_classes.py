@@ -10,9 +10,10 @@ CLASSES = [
     ("BatchNorm passes (bn_act.hip)", r"cml::.*bn_(apply|stats|bwd|finalize|apply2|bwd_apply2|bwd_reduce2)"),
     ("fused 1x1 conv + BN (conv1x1.hip, conv1x1g.hip)",
      r"cml::.*(conv1x1_bn|conv1x1_bnbwd|bn_bwd_coeffs|conv1x1g_|conv1x1q_)"),
-    ("3x3 weight gradient (wgrad3x3.hip)", r"cml::.*wgrad3x3"),
+    ("3x3 weight gradient (wgrad3x3.hip, wgrad DMA stride-2)",
+     r"cml::.*(wgrad3x3|wgrad_dma_kernel<\d+, \d+, \d+, \d+, true)"),
     ("recompute-tail algebra (tail_prep.hip, bn_stats_gram)", r"cml::.*(tail_|bn_stats_gram)"),
-    ("1x1 weight gradient (wgrad1x1.hip)", r"cml::.*wgrad1x1"),
+    ("1x1 weight gradient (wgrad1x1.hip)", r"cml::.*(wgrad1x1|wgrad_dma_kernel|wgrad_fold)"),
     ("3x3 conv fwd + data gradient (conv_gemm.hip, gemm.hip conv mode, conv3x3p.hip)",
      r"cml::.*(conv_gemm|gemm_nt_kernel<\d, true>|conv3x3p)"),
     ("own GEMM (gemm.hip: 1x1 convs as GEMMs, transformer linears)", r"cml::.*gemm_nt_kernel"),
