@@ -1,0 +1,23 @@
+#!/bin/bash
+# r05 pass 21: same-box kernel tables with CML_C1_PF2=0 / 1.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r05_21; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+for pf in 0 1; do
+CML_C1_PF2=$pf timeout -k 10 400 rocprofv3 --kernel-trace -d $O/raw$pf -o run -- python3 $R/bench.py --steps 6 --warmup 3 --no-baseline --b256-batch 0 --virtual-workers 0 --profile-marker > $O/prof$pf.log 2>&1 || { tail -20 $O/prof$pf.log; exit 1; }
+db=$(find $O/raw$pf -name '*.db' -print -quit)
+python3 $R/tools/prof_summary.py "$db" --after spin_kernel --steps 6 --top 400 --out $O/kernels_pf$pf.md
+python3 $R/tools/kernel_classes.py $O/kernels_pf$pf.md > $O/classes_pf$pf.md || true
+rm -rf $O/raw$pf
+head -2 $O/kernels_pf$pf.md; head -4 $O/classes_pf$pf.md
+done
+cd $R
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_bwd_fusion_gpu.py tests/test_conv1x1_bn_gpu.py > $O/test.log 2>&1 || { tail -30 $O/test.log; exit 1; }
+tail -1 $O/test.log
+for rep in 1 2; do
+for pf in 0 1; do
+CML_C1_PF2=$pf timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-baseline --b256-batch 0 --virtual-workers 0 > $O/bench_${pf}_${rep}.log 2>&1 || { tail -20 $O/bench_${pf}_${rep}.log; exit 1; }
+echo "pf2=$pf rep=$rep $(grep '^{' $O/bench_${pf}_${rep}.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["ms_per_step"])')"
+done
+done
