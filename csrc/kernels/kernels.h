@@ -177,13 +177,15 @@ hipError_t launch_maxpool_bwd(const void* dy, const void* idx, void* dx, int N, 
                               int C, int OH, int OW, int k, int s, int p, hipStream_t stream);
 
 // Multi-tensor copy of up to kMaxCopy (src -> dst, bytes) entries in one launch (16-B aligned
-// pointers, even byte counts). vpre[e] = number of whole 16-B vectors before entry e.
+// pointers, even byte counts). vpre[e] = number of whole 16-B vectors before entry e; bpre[e] =
+// first workgroup of entry e (filled by launch_multi_copy).
 constexpr int kMaxCopy = 32;
 struct MultiCopyArgs {
   const void* src[kMaxCopy];
   void* dst[kMaxCopy];
   int64_t bytes[kMaxCopy];
   int64_t vpre[kMaxCopy + 1];
+  int bpre[kMaxCopy + 1];
   int n;
 };
 hipError_t launch_multi_copy(const MultiCopyArgs& args, hipStream_t stream);

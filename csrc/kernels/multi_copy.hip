@@ -4,9 +4,13 @@
 // PyTorch's _foreach_copy_ runs these at ~2.8 TB/s (11.6 ms of a 162 ms Llama-3-8B step moves
 // 32 GB, profiles/r01_prof16_llama_fused_kernels.md): its multi_tensor_apply chunks are small and
 // it launches per chunk-list. Here the table of up to kMaxCopy (src, dst, bytes) entries rides in
-// the kernel arguments; every lane moves 16-B vectors of the concatenated byte space (binary
-// search of the entry over the prefix table, 4 vectors in flight), and the sub-16-B tails are
-// copied in 2-B units by the first lanes of the grid.
+// the kernel arguments and every workgroup copies one slice of ONE entry: the launcher gives entry
+// e ceil(vectors / kVB) workgroups (prefix bpre), a workgroup finds its entry by a scalar search
+// of that table, and each lane moves kVB / kCB 16-B vectors with all loads in flight before the
+// stores. (The first form searched the entry per 16-B vector over the vector prefix, a divergent
+// loop of dependent kernel-argument loads per element: 29 us for the ~10 MB of a batch-256 ResNet
+// bucket, profiles/r05_19/kernels_b256.md.) The sub-16-B tails are copied in 2-B units by the first
+// lanes of the grid.
 #include "common.h"
 #include "kernels.h"
 
@@ -14,44 +18,41 @@ namespace cml {
 namespace {
 
 constexpr int kCB = 256;
+constexpr int kVPT = 8;                  // 16-B vectors per lane
+constexpr int kVB = kCB * kVPT;          // vectors per workgroup (32 KiB)
 
 __global__ __launch_bounds__(kCB) void multi_copy_kernel(MultiCopyArgs a) {
-  const int64_t total = a.vpre[a.n];
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kCB;
-  const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kCB + threadIdx.x;
-  for (int64_t base = t0; base < total; base += 4 * stride) {
-    uint4 v[4];
-    int64_t dsti[4];
-    int ent[4];
+  const int b = blockIdx.x;
+  int lo = 0, hi = a.n - 1;              // last entry with bpre[e] <= b (uniform: scalar loads)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (a.bpre[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const int e = lo;
+  const int64_t nv = a.vpre[e + 1] - a.vpre[e];
+  const int64_t v0 = static_cast<int64_t>(b - a.bpre[e]) * kVB + threadIdx.x;
+  const uint4* src = reinterpret_cast<const uint4*>(a.src[e]);
+  uint4* dst = reinterpret_cast<uint4*>(a.dst[e]);
+  uint4 v[kVPT];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t g = base + u * stride;
-      ent[u] = -1;
-      if (g < total) {
-        int lo = 0, hi = a.n - 1;   // last entry with vpre[e] <= g
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (a.vpre[mid] <= g) lo = mid;
-          else hi = mid - 1;
-        }
-        const int64_t off = g - a.vpre[lo];
-        ent[u] = lo;
-        dsti[u] = off;
-        v[u] = reinterpret_cast<const uint4*>(a.src[lo])[off];
-      }
-    }
+  for (int u = 0; u < kVPT; ++u) {
+    const int64_t i = v0 + static_cast<int64_t>(u) * kCB;
+    if (i < nv) v[u] = src[i];
+  }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (ent[u] >= 0) reinterpret_cast<uint4*>(a.dst[ent[u]])[dsti[u]] = v[u];
+  for (int u = 0; u < kVPT; ++u) {
+    const int64_t i = v0 + static_cast<int64_t>(u) * kCB;
+    if (i < nv) dst[i] = v[u];
   }
   // tails: bytes [nvec * 16, bytes) of each entry, 2 B per lane
-  if (blockIdx.x == 0) {
-    for (int e = 0; e < a.n; ++e) {
-      const int64_t nv = a.vpre[e + 1] - a.vpre[e];
-      const int64_t rem = (a.bytes[e] - nv * 16) / 2;
+  if (b == 0) {
+    for (int k = 0; k < a.n; ++k) {
+      const int64_t nvk = a.vpre[k + 1] - a.vpre[k];
+      const int64_t rem = (a.bytes[k] - nvk * 16) / 2;
       if (threadIdx.x < rem) {
-        const int64_t h = nv * 8 + threadIdx.x;
-        reinterpret_cast<uint16_t*>(a.dst[e])[h] = reinterpret_cast<const uint16_t*>(a.src[e])[h];
+        const int64_t h = nvk * 8 + threadIdx.x;
+        reinterpret_cast<uint16_t*>(a.dst[k])[h] = reinterpret_cast<const uint16_t*>(a.src[k])[h];
       }
     }
   }
@@ -114,11 +115,17 @@ hipError_t launch_multi_copy(const MultiCopyArgs& a, hipStream_t st) {
         (a.bytes[e] & 1) || a.vpre[e + 1] - a.vpre[e] != a.bytes[e] / 16)
       return hipErrorInvalidValue;
   }
-  const int64_t total = a.vpre[a.n];
-  int64_t b = (total + 4 * kCB - 1) / (4 * kCB);
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  multi_copy_kernel<<<static_cast<unsigned>(b), kCB, 0, st>>>(a);
+  MultiCopyArgs k = a;
+  int64_t nb = 0;
+  for (int e = 0; e < a.n; ++e) {
+    k.bpre[e] = static_cast<int>(nb);
+    const int64_t nv = a.vpre[e + 1] - a.vpre[e];
+    nb += nv > 0 ? (nv + kVB - 1) / kVB : (e == 0 ? 1 : 0);   // block 0 also copies the tails
+  }
+  if (nb < 1) nb = 1;
+  if (nb >= (1ll << 31)) return hipErrorInvalidValue;
+  k.bpre[a.n] = static_cast<int>(nb);
+  multi_copy_kernel<<<static_cast<unsigned>(nb), kCB, 0, st>>>(k);
   return hipGetLastError();
 }
 
