@@ -187,6 +187,7 @@ struct MultiCopyArgs {
   int64_t vpre[kMaxCopy + 1];
   int bpre[kMaxCopy + 1];
   int n;
+  int slice;    // 1: one 32-KiB slice per workgroup (small copies), 0: striding workgroups
 };
 hipError_t launch_multi_copy(const MultiCopyArgs& args, hipStream_t stream);
 // dst [C][R] = src [R][C]^T, bf16, R and C multiples of 64, row strides lds / ldd (% 8 == 0)

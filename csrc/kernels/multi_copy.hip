@@ -4,13 +4,16 @@
 // PyTorch's _foreach_copy_ runs these at ~2.8 TB/s (11.6 ms of a 162 ms Llama-3-8B step moves
 // 32 GB, profiles/r01_prof16_llama_fused_kernels.md): its multi_tensor_apply chunks are small and
 // it launches per chunk-list. Here the table of up to kMaxCopy (src, dst, bytes) entries rides in
-// the kernel arguments and every workgroup copies one slice of ONE entry: the launcher gives entry
-// e ceil(vectors / kVB) workgroups (prefix bpre), a workgroup finds its entry by a scalar search
-// of that table, and each lane moves kVB / kCB 16-B vectors with all loads in flight before the
-// stores. (The first form searched the entry per 16-B vector over the vector prefix, a divergent
+// the kernel arguments and every workgroup copies part of ONE entry: the launcher splits ~8192
+// workgroups over the entries by size (prefix bpre), a workgroup finds its entry by a scalar
+// search of that table, and the entry's workgroups stride over it with 4 16-B vectors per lane in
+// flight. (The first form searched the entry per 16-B vector over the vector prefix, a divergent
 // loop of dependent kernel-argument loads per element: 29 us for the ~10 MB of a batch-256 ResNet
-// bucket, profiles/r05_19/kernels_b256.md.) The sub-16-B tails are copied in 2-B units by the first
+// bucket, profiles/r05_19/kernels_b256.md; one 32-KiB slice per workgroup moved the 470 MB Llama
+// buckets at only 2.9 TB/s, profiles/r05_25/.) The sub-16-B tails are copied in 2-B units by the first
 // lanes of the grid.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -18,8 +21,8 @@ namespace cml {
 namespace {
 
 constexpr int kCB = 256;
-constexpr int kVPT = 8;                  // 16-B vectors per lane
-constexpr int kVB = kCB * kVPT;          // vectors per workgroup (32 KiB)
+constexpr int kU = 4;                    // 16-B vectors in flight per lane and iteration
+constexpr int kSV = 2048;                // vectors per workgroup of a small copy (32 KiB)
 
 __global__ __launch_bounds__(kCB) void multi_copy_kernel(MultiCopyArgs a) {
   const int b = blockIdx.x;
@@ -31,19 +34,38 @@ __global__ __launch_bounds__(kCB) void multi_copy_kernel(MultiCopyArgs a) {
   }
   const int e = lo;
   const int64_t nv = a.vpre[e + 1] - a.vpre[e];
-  const int64_t v0 = static_cast<int64_t>(b - a.bpre[e]) * kVB + threadIdx.x;
   const uint4* src = reinterpret_cast<const uint4*>(a.src[e]);
   uint4* dst = reinterpret_cast<uint4*>(a.dst[e]);
-  uint4 v[kVPT];
+  if (a.slice) {   // small copies: one kSV-vector slice per workgroup, all loads before the stores
+    const int64_t v0 = static_cast<int64_t>(b - a.bpre[e]) * kSV + threadIdx.x;
+    uint4 v[kSV / kCB];
 #pragma unroll
-  for (int u = 0; u < kVPT; ++u) {
-    const int64_t i = v0 + static_cast<int64_t>(u) * kCB;
-    if (i < nv) v[u] = src[i];
+    for (int u = 0; u < kSV / kCB; ++u) {
+      const int64_t i = v0 + static_cast<int64_t>(u) * kCB;
+      if (i < nv) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kSV / kCB; ++u) {
+      const int64_t i = v0 + static_cast<int64_t>(u) * kCB;
+      if (i < nv) dst[i] = v[u];
+    }
+  } else {
+  // the entry's workgroups stride over it together, kU vectors per lane in flight
+  const int64_t stride = static_cast<int64_t>(a.bpre[e + 1] - a.bpre[e]) * kCB;
+  for (int64_t i0 = static_cast<int64_t>(b - a.bpre[e]) * kCB + threadIdx.x; i0 < nv;
+       i0 += kU * stride) {
+    uint4 v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < nv) v[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < nv) dst[i] = v[u];
+    }
   }
-#pragma unroll
-  for (int u = 0; u < kVPT; ++u) {
-    const int64_t i = v0 + static_cast<int64_t>(u) * kCB;
-    if (i < nv) dst[i] = v[u];
   }
   // tails: bytes [nvec * 16, bytes) of each entry, 2 B per lane
   if (b == 0) {
@@ -116,14 +138,25 @@ hipError_t launch_multi_copy(const MultiCopyArgs& a, hipStream_t st) {
       return hipErrorInvalidValue;
   }
   MultiCopyArgs k = a;
+  // Large copies (>= 8192 slices): 8192 workgroups split by size over the entries, striding
+  // (the Llama-3-8B weight gradients at 4.88 TB/s, ATen's contiguous copy 4.84); small ones: one
+  // 32-KiB slice per workgroup (a ResNet bucket's 10 MB in 11.5 us; striding grids of 664 / 8192
+  // workgroups took 32 / 21 us, profiles/r05_25/, r05_26/). At least one workgroup per entry
+  // (block 0 also copies the tails).
+  const int64_t total = std::max<int64_t>(1, a.vpre[a.n]);
+  k.slice = total < 8192ll * kSV ? 1 : 0;
   int64_t nb = 0;
   for (int e = 0; e < a.n; ++e) {
     k.bpre[e] = static_cast<int>(nb);
     const int64_t nv = a.vpre[e + 1] - a.vpre[e];
-    nb += nv > 0 ? (nv + kVB - 1) / kVB : (e == 0 ? 1 : 0);   // block 0 also copies the tails
+    if (k.slice) {
+      nb += std::max<int64_t>(1, (nv + kSV - 1) / kSV);
+    } else {
+      const int64_t want = (nv * 8192 + total - 1) / total;
+      const int64_t cap = (nv + kCB - 1) / kCB;   // no more workgroups than 256-vector slices
+      nb += std::max<int64_t>(1, std::min(want, cap));
+    }
   }
-  if (nb < 1) nb = 1;
-  if (nb >= (1ll << 31)) return hipErrorInvalidValue;
   k.bpre[a.n] = static_cast<int>(nb);
   multi_copy_kernel<<<static_cast<unsigned>(nb), kCB, 0, st>>>(k);
   return hipGetLastError();
