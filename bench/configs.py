@@ -83,6 +83,8 @@ def parse(argv=None):
     ap.add_argument("--model", default=None, help="override the model (e.g. llama_tiny)")
     ap.add_argument("--seq-len", type=int, default=0, help="override the sequence length")
     ap.add_argument("--f", type=int, default=-1)
+    ap.add_argument("--no-direct-grads", action="store_true",
+                    help="copy-on-ready gradient capture even where ops can write the flat row")
     ap.add_argument("--bucket-mb", type=float, default=0.0, help="0: the config's default")
     ap.add_argument("--no-baseline", action="store_true",
                     help="skip the mean all-reduce baseline run")
@@ -115,6 +117,7 @@ def run_config(c: dict, a, info, rule: str, topology: str) -> dict:
     cfg.agg.rule = rule
     cfg.agg.f = 0 if rule == "mean" else (a.f if a.f >= 0 else default_f(rule, n))
     cfg.topology.kind = topology
+    cfg.topology.direct_grads = not a.no_direct_grads
     cfg.topology.bucket_mb = a.bucket_mb or c.get("bucket_mb", 8)
     cfg.topology.gossip_async = c.get("gossip_async", False)
     cfg.topology.gossip_graph = a.gossip_graph or c.get("gossip_graph", "ring")
@@ -222,6 +225,7 @@ def main(argv=None):
            "per_worker_batch": cfg.batch_per_worker, "seq_len": cfg.model.seq_len,
            "dtype": cfg.dtype, "optimizer": cfg.optim.name, "params": main_res["params"],
            "bucket_mb": cfg.topology.bucket_mb, "buckets": main_res["buckets"],
+           "direct_grads": cfg.topology.direct_grads,
            "samples_per_s": round(samples / dt, 2),
            "tokens_per_s": round(samples * main_res["samples_per_item"] / dt, 1),
            "ms_per_step": round(ms, 3), "phase_ms_per_step": main_res["phases"],

@@ -99,6 +99,10 @@ class TopologyConfig:
     gram_lag: int = 1            # GPU runs: bucket b's Gram is enqueued on the compute stream at
                                  # the flush of bucket b + gram_lag (its exchange has had one
                                  # bucket of backward to land); the last ones run in step()
+    direct_grads: bool = True    # one worker per rank: ops with a per-worker gradient path
+                                 # (ops.worker_grads: transformer linears, norms, embeddings) write
+                                 # their parameter gradients straight into the flat gradient row
+                                 # during backward instead of autograd tensors + the capture copy
 
     def validate(self) -> None:
         if self.kind not in TOPOLOGIES:

@@ -716,6 +716,7 @@ class _LinearNBFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w):
         ctx.save_for_backward(x, w)
+        ctx.param = w   # the Parameter itself (its id keys the direct-gradient destination)
         return F.linear(x, w)
 
     @staticmethod
@@ -736,17 +737,36 @@ class _LinearNBFn(torch.autograd.Function):
                 dx = dy2 @ w
             dx = dx.view(x.shape)
         if ctx.needs_input_grad[1]:
+            wg = WG.current()
+            dst, first = (None, True)
+            if wg is not None and wg.V == 1 and wg.has(ctx.param):
+                # direct gradient (engine TopologyConfig.direct_grads): written into the flat
+                # gradient row, no autograd tensor and no capture copy
+                dst, first = wg.out(ctx.param)
+                dst = dst.view(N, K)
             if _P().nt_wgrad:
-                dw = torch.matmul(L.transpose_bf16(dy2), L.transpose_bf16(x2).t())
+                a, b = L.transpose_bf16(dy2), L.transpose_bf16(x2).t()
             else:
-                dw = dy2.t() @ x2
+                a, b = dy2.t(), x2
+            if dst is None:
+                dw = torch.matmul(a, b)
+            elif first:
+                torch.matmul(a, b, out=dst)
+            else:
+                dst.add_(torch.matmul(a, b))
+        ctx.param = None
         return dx, dw
 
 
 def linear_nb(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """Bias-free linear (``_LinearNBFn`` on bf16 GPU tensors, F.linear otherwise)."""
-    if _gpu_bf16(x, w) and WG.current() is None:
+    """Bias-free linear (``_LinearNBFn`` on bf16 GPU tensors, F.linear otherwise). Under a
+    one-worker gradient destination (direct gradients) the weight gradient goes to the flat row;
+    batched workers (V > 1) take ``linear`` (per-worker strided GEMMs)."""
+    wg = WG.current()
+    if _gpu_bf16(x, w) and (wg is None or wg.V == 1):
         return _LinearNBFn.apply(x, w)
+    if wg is not None and wg.has(w):
+        return linear(x, w, None)
     return F.linear(x, w)
 
 

@@ -157,6 +157,14 @@ class ConsensusEngine:
         self._ready: Dict[int, List[int]] = {b.index: [] for b in fl.buckets}
         self._flushed: set = set()
         self._in_worker_batch = False
+        # TopologyConfig.direct_grads: a one-worker gradient destination (ops.worker_grads) is
+        # active from zero_grad() to step(), so the ops with a per-worker gradient path write
+        # straight into the flat row; their AccumulateGrad hooks still fire (with no gradient)
+        # in autograd order and drive the bucket flushes as before
+        self.direct_grads = bool(getattr(cfg.topology, "direct_grads", False) and self.V == 1
+                                 and self.device.type == "cuda")
+        self._direct_wg = None
+        self._direct_prev = None
         self._hooks = []
         self.overlap = bool(cfg.topology.overlap and self.V == 1 and self.group_active
                             and self.topo in ("allreduce", "allgather", "sharded")
@@ -236,6 +244,18 @@ class ConsensusEngine:
         self._gram_done.clear()
         self._gram_queue.clear()
         self.flat.grad_row = 0
+        if self.direct_grads:
+            self._end_direct()
+            views = self.flat.worker_views()
+            self._direct_wg = WG.WorkerGrads(
+                1, {id(p): views[i] for i, p in enumerate(self.flat.params)})
+            self._direct_prev = WG.activate(self._direct_wg)
+
+    def _end_direct(self) -> None:
+        if self._direct_wg is not None:
+            if WG.current() is self._direct_wg:
+                WG.activate(self._direct_prev)
+            self._direct_wg = self._direct_prev = None
 
     def bind_worker(self, v: int) -> None:
         """Route the next backward's gradients into virtual-worker row v."""
@@ -324,6 +344,7 @@ class ConsensusEngine:
     def step(self) -> None:
         """Exchange, aggregate and update (call after all backward passes of the step)."""
         fl = self.flat
+        self._end_direct()
         if self.param_prefetch:
             self.wait_params()          # params no forward touched
             if self._invoked:
@@ -377,10 +398,21 @@ class ConsensusEngine:
         views = fl.grad_views(fl.grad_row)
         lst = self._ready[b.index]
         if lst:
-            dst = [views[i] for i in lst]
-            src = [fl.params[i].grad for i in lst]
+            # direct gradients (no autograd tensor) are already in the row; a parameter whose
+            # hook fired without a gradient and without a direct write gets a zero row
+            wg = self._direct_wg
+            cp = []
+            for i in lst:
+                if fl.params[i].grad is not None:
+                    cp.append(i)
+                elif wg is None or id(fl.params[i]) not in wg.touched:
+                    views[i].zero_()
+            dst = [views[i] for i in cp]
+            src = [fl.params[i].grad for i in cp]
             # copy-on-ready through the HIP multi-tensor copy (PerfPolicy.multi_copy)
-            if dst[0].is_cuda and _P().multi_copy:
+            if not dst:
+                pass
+            elif dst[0].is_cuda and _P().multi_copy:
                 # one HIP launch per 32 tensors at ~HBM speed (csrc/kernels/multi_copy.hip)
                 rest = lib().multi_copy(dst, src)
                 if rest:
