@@ -433,7 +433,12 @@ bool conv1x1g_pick(int64_t M, int K, int N, int pm, bool bnres) {
   // auto: since the packed prologues (round 3, profiles/r03_11_families.jsonl) the persistent
   // register-staged kernel is as fast or faster everywhere except the downsample tails' forward
   // GEMM (cat_bnres: 256 x 256 tiles, 1.14 / 0.92 vs 1.44 / 1.21 ms at batch 2048)
-  return pm == PM_CAT && bnres && use_quad(M, K, N, pm);
+  // CML_C1G_CAT=1: also the recompute tails' two-source data gradient (A/B)
+  static const bool cat = [] {
+    const char* e = getenv("CML_C1G_CAT");
+    return e && e[0] == '1';
+  }();
+  return pm == PM_CAT && (bnres || cat) && use_quad(M, K, N, pm);
 }
 
 size_t conv1x1g_part_floats(int64_t M, int K, int N, int pm) {

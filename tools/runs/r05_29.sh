@@ -1,0 +1,21 @@
+#!/bin/bash
+# r05 pass 29: the recompute tails' cat data gradient on the quad (DMA) kernel (CML_C1G_CAT):
+# tests with it on, alternating step A/B, kernel table.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r05_29; mkdir -p $O
+cd $R
+CML_C1G_CAT=1 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_bwd_fusion_gpu.py tests/test_conv1x1g_gpu.py > $O/test.log 2>&1 || { tail -40 $O/test.log; exit 1; }
+tail -1 $O/test.log
+for rep in 1 2; do
+for c in 0 1; do
+CML_C1G_CAT=$c timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-baseline --b256-batch 0 --virtual-workers 0 > $O/bench_${c}_${rep}.log 2>&1 || { tail -20 $O/bench_${c}_${rep}.log; exit 1; }
+echo "cat=$c rep=$rep $(grep '^{' $O/bench_${c}_${rep}.log | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["ms_per_step"])')"
+done
+done
+cd /tmp && export TMPDIR=/tmp
+CML_C1G_CAT=1 timeout -k 10 400 rocprofv3 --kernel-trace -d $O/raw -o run -- python3 $R/bench.py --steps 6 --warmup 3 --no-baseline --b256-batch 0 --virtual-workers 0 --profile-marker > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+db=$(find $O/raw -name '*.db' -print -quit)
+python3 $R/tools/prof_summary.py "$db" --after spin_kernel --steps 6 --top 400 --out $O/kernels_cat1.md
+rm -rf $O/raw
+head -2 $O/kernels_cat1.md; grep "conv1x1q\|conv1x1_bn_fwd_kernel<2, 2, 3, false, false, false, 1" $O/kernels_cat1.md | cut -c1-200
