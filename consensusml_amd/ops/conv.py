@@ -755,7 +755,7 @@ def _wgrad3x3_s2(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Te
     """Weight gradient of a stride-2 / padding-1 3x3 conv: ``wgrad3x3s2`` (wgrad1x1.hip's LDS-DMA
     kernel on the implicit im2col of x, the padding rows gathered from a zero row) when the shape
     has a plan and PerfPolicy.own_wgrad3x3_s2 is on, else MIOpen. (An own nine-tap kernel over the
-    raw input rows measured 1.1-1.45x slower than MIOpen, docs/PERFORMANCE.md "Round 4".)
+    raw input rows measured 1.1-1.45x slower than MIOpen, docs/HISTORY.md "Round 4".)
     Batch 2048 (profiles/r05_16/): 256 -> 256 at 28 x 28 585-603 us vs MIOpen 692-704, 512 -> 512
     at 14 x 14 555-603 vs 644-674; the 128-channel layer-2 conv (128 x 128 tiles, x gathered 2.25x
     and dy re-read per tap through L2) 969 vs 850 stays on MIOpen (Ci < 256)."""
