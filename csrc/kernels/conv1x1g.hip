@@ -17,7 +17,8 @@
 // place in LDS once per staged x unit, with conv1x1.hip's arithmetic (same fmaf, same bf16
 // rounding, packed VALU from common.h), so the operands -- and with the same k order the products
 // -- are bit-identical. In production this kernel runs the downsample tails' forward GEMM (cat +
-// BN + residual + ReLU epilogue, conv1x1g_pick); everything else is on conv1x1.hip.
+// BN + residual + ReLU epilogue) and the layer-2/3 recompute tails' data gradient (conv1x1g_pick);
+// everything else is on conv1x1.hip.
 //
 // Epilogue: conv1x1_common.h's per-wave 64 x 64 block epilogue, called for each 64-channel half of
 // the wave's tile through its own 8 KB LDS image (the staging buffers are free by then); BN
@@ -93,6 +94,42 @@ __device__ __forceinline__ bf16x8_t prologue(bf16x8_t v, const float (&sc)[8], c
 // Same products in the same k order and the same prologue arithmetic as conv1x1.hip: outputs are
 // bit-identical to conv1x1.hip. Partial statistics rows per (m-tile, wave m-row), folded by the
 // same finalize.
+// The LDS accesses of the loop below, as functions with __restrict__ LDS operands: inlined, their
+// loads and stores carry alias-scope metadata, which keeps hipcc's LDS-DMA tracking from putting
+// an s_waitcnt vmcnt(0) in front of them (it drained every unit in flight twice per k-step,
+// defeating the 4-units-in-flight schedule); the kernel orders the DMA itself (counted vmcnt +
+// barriers, below).
+__device__ __forceinline__ void q_rd_x(const char* __restrict__ sx, bf16x8_t (&xf)[4], int row,
+                                       int h) {
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+    xf[kk] = *reinterpret_cast<const bf16x8_t*>(sx + swz(row, 2 * kk + h));
+}
+__device__ __forceinline__ void q_rd_w(const char* __restrict__ sw, bf16x8_t (&dst)[4][2],
+                                       int row0, int h) {
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      dst[kk][i] = *reinterpret_cast<const bf16x8_t*>(sw + swz(row0 + 32 * i, 2 * kk + h));
+}
+__device__ __forceinline__ void q_transform(char* __restrict__ sx, const float* __restrict__ sc_p,
+                                            const float* __restrict__ bi_p,
+                                            const uint8_t* __restrict__ smk, int tid,
+                                            bool masked) {
+  const int c = tid & 7;
+  float sc[8], bi[8];
+  ld8f(sc_p + 8 * c, sc);
+  ld8f(bi_p + 8 * c, bi);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (tid >> 3) + 64 * i;
+    bf16x8_t* q = reinterpret_cast<bf16x8_t*>(sx + swz(row, c));
+    if (masked) *q = prologue<true>(*q, sc, bi, smk[row * 8 + c]);
+    else *q = prologue<false>(*q, sc, bi, 0u);
+  }
+}
+
 template <int PM, int SM, bool EL>
 __global__ __launch_bounds__(512, 1) void conv1x1q_kernel(C1Args a) {
   constexpr int NT = 512, WM = 4, BM = 256, BN = 256;
@@ -184,39 +221,18 @@ __global__ __launch_bounds__(512, 1) void conv1x1q_kernel(C1Args a) {
   auto transform = [&](int u, int s) {
     if (ab & 4) return;
     if constexpr (PRO) {
-      char* sx = slot(u, s);
       const int k0 = s * kBK;
       const bool masked = CAT && k0 < K1 && !a.cat_bnrelu;
       if (CAT && k0 >= K1 && a.pro_sc2 == nullptr) return;   // identity second source
-      const int c = tid & 7;
-      float sc[8], bi[8];
-      ld8f(s_aff + k0 + 8 * c, sc);
-      ld8f(s_aff + K + k0 + 8 * c, bi);
-      const uint8_t* smk = reinterpret_cast<const uint8_t*>(mslot(u, s));
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = (tid >> 3) + 64 * i;
-        bf16x8_t* q = reinterpret_cast<bf16x8_t*>(sx + swz(row, c));
-        if (masked) *q = prologue<true>(*q, sc, bi, smk[row * 8 + c]);
-        else *q = prologue<false>(*q, sc, bi, 0u);
-      }
+      q_transform(slot(u, s), s_aff + k0, s_aff + K + k0,
+                  reinterpret_cast<const uint8_t*>(mslot(u, s)), tid, masked);
     }
   };
 
   bf16x8_t xf[4], wc[4][2], wf[4][2];
-  auto rd_x = [&](int u, int s) {
-    const char* sx = slot(u, s);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-      xf[kk] = *reinterpret_cast<const bf16x8_t*>(sx + swz(wm * 32 + r32, 2 * kk + h));
-  };
+  auto rd_x = [&](int u, int s) { q_rd_x(slot(u, s), xf, wm * 32 + r32, h); };
   auto rd_w = [&](bf16x8_t (&dst)[4][2], int u, int s) {
-    const char* sw = slot(u, s);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        dst[kk][i] = *reinterpret_cast<const bf16x8_t*>(sw + swz(wn * 64 + 32 * i + r32, 2 * kk + h));
+    q_rd_w(slot(u, s), dst, wn * 64 + r32, h);
   };
   f32x16 acc[2][2][2];   // [x half][W half][32-channel fragment]
 #pragma unroll
@@ -432,11 +448,13 @@ bool conv1x1g_pick(int64_t M, int K, int N, int pm, bool bnres) {
   if (mode == 3) return use_quad(M, K, N, pm);
   // auto: since the packed prologues (round 3, profiles/r03_11_families.jsonl) the persistent
   // register-staged kernel is as fast or faster everywhere except the downsample tails' forward
-  // GEMM (cat_bnres: 256 x 256 tiles, 1.14 / 0.92 vs 1.44 / 1.21 ms at batch 2048)
-  // CML_C1G_CAT=1: also the recompute tails' two-source data gradient (A/B)
+  // GEMM (cat_bnres: 256 x 256 tiles, 1.14 / 0.92 vs 1.44 / 1.21 ms at batch 2048) ...
+  // and the recompute tails' two-source data gradient with its BN-backward sums (K >= 384: layers
+  // 2-3): 3.12 ms for its 6 calls vs ~3.46 on conv1x1.hip once the quad kernel's loop stopped
+  // draining the DMA queue (profiles/r05_32/); CML_C1G_CAT=0 for the A/B
   static const bool cat = [] {
     const char* e = getenv("CML_C1G_CAT");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return pm == PM_CAT && (bnres || cat) && use_quad(M, K, N, pm);
 }
