@@ -2,10 +2,12 @@
 """Weight gradient of a transformer linear, dW [N, K] = dY^T X over T token rows, on the 1x1-conv
 weight-gradient kernel (csrc/kernels/wgrad1x1.hip: the [T, C] row-major activations ARE NHWC
 [T, C, 1, 1]; split-K over the rows + fixed-order fold) vs PyTorch's `dy.t() @ x` (hipBLASLt), at
-the BERT-base per-rank shapes (T = 64 x 128 or 32 x 128 tokens). Prints one JSON line per shape:
-times, TFLOP/s and the max relative difference to an fp32 reference.
+the BERT-base per-rank shapes (T = 64 x 128 or 32 x 128 tokens), or (--llama) the Llama-3-8B
+ones at T = 4 x 2048 (wqkv, wo, w13, w2, output head: one split on the LDS-DMA kernel, dW written
+directly). Prints one JSON line per shape: times, TFLOP/s and the max relative difference to an
+fp32 reference.
 
-  python bench/linear_wgrad.py
+  python bench/linear_wgrad.py [--llama]
 """
 from __future__ import annotations
 
@@ -42,8 +44,12 @@ def main():
     L = lib()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    for T in (8192, 4096):
-        for N, K in ((768, 768), (2304, 768), (3072, 768), (768, 3072)):
+    if "--llama" in sys.argv:
+        cases = [(8192, (6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096))]
+    else:
+        cases = [(T, (768, 768), (2304, 768), (3072, 768), (768, 3072)) for T in (8192, 4096)]
+    for T, *shapes in cases:
+        for N, K in shapes:
             dy = torch.randn(T, N, device=dev, generator=g).bfloat16()
             x = torch.randn(T, K, device=dev, generator=g).bfloat16()
             ref = dy.float().t() @ x.float()

@@ -517,7 +517,9 @@ def _linear_wgrad(gout: torch.Tensor, gin: torch.Tensor) -> torch.Tensor:
     [T, C, 1, 1]; split-K over the rows, fixed-order fold), else hipBLASLt. Up to BERT-base sizes
     (N K <= 4 M): at T = 8192 the kernel matches hipBLASLt on 2304 / 3072-wide shapes and is 1.5x
     faster on 768 x 768 (bench/linear_wgrad.py), and the BERT V = 1 x 64 step drops 13.55 -> 12.94
-    ms (profiles/r04_38/); Llama-size weights are unmeasured on it and stay on hipBLASLt."""
+    ms (profiles/r04_38/). Llama-3-8B weights (one split on the LDS-DMA kernel, dW written
+    directly) run 0.89-1.12 PFLOP/s there vs 1.0-1.39 for hipBLASLt NT on transposed operands,
+    transposes included (profiles/r05_33/llama_wgrad.jsonl): they stay on the NT path."""
     T, N = gout.shape
     K = gin.shape[-1]
     if (_P().own_linear_wgrad and gout.is_cuda and gout.dtype == torch.bfloat16

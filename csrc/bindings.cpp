@@ -749,7 +749,7 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
                 const optional<Tensor>& pro_sc, const optional<Tensor>& pro_bi,
                 const optional<Tensor>& dz_z, const optional<Tensor>& dz_mask,
                 const optional<Tensor>& dz_a, const optional<Tensor>& dz_b,
-                const optional<Tensor>& dz_c) {
+                const optional<Tensor>& dz_c, const optional<Tensor>& out) {
   check_nhwc(x, "x");
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc(dy, "dy");
@@ -780,9 +780,22 @@ Tensor wgrad1x1(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
   int S = 1, cps = 1;
   cml::wgrad1x1_plan(P, static_cast<int>(Co), static_cast<int>(Ci), &S, &cps, sc != nullptr,
                      zp != nullptr ? 1 : 0, false);
-  Tensor part = at::empty({S, Co, Ci}, x.options().dtype(at::kFloat));
-  Tensor dw = at::empty({Co, Ci, 1, 1}, x.options().dtype(dtype));
-  CML_CHECK_HIP(cml::launch_wgrad1x1(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(),
+  // one-split long-K calls (transformer linears): the kernel writes dw itself, no partial slab
+  const bool direct = cml::wgrad1x1_direct(P, static_cast<int>(Co), static_cast<int>(Ci),
+                                           sc != nullptr, zp != nullptr ? 1 : 0, false);
+  Tensor part = direct ? Tensor() : at::empty({S, Co, Ci}, x.options().dtype(at::kFloat));
+  Tensor dw;
+  if (out.has_value() && out->defined()) {   // caller's destination (e.g. a flat gradient row)
+    check_dev(*out, "out");
+    TORCH_CHECK(out->scalar_type() == dtype && out->is_contiguous() && out->numel() == Co * Ci &&
+                    reinterpret_cast<uintptr_t>(out->data_ptr()) % 16 == 0,
+                "wgrad1x1: out must be a contiguous 16-B aligned [Co, Ci] tensor of dtype");
+    dw = *out;
+  } else {
+    dw = at::empty({Co, Ci, 1, 1}, x.options().dtype(dtype));
+  }
+  CML_CHECK_HIP(cml::launch_wgrad1x1(dy.data_ptr(), x.data_ptr(),
+                                     direct ? nullptr : part.data_ptr<float>(),
                                      dw.data_ptr(), dtype == at::kBFloat16, P,
                                      static_cast<int>(Co), static_cast<int>(Ci), sc, bi,
                                      cur_stream(), zp, zm, za, zb, zc));
@@ -2423,7 +2436,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad1x1", &wgrad1x1, py::arg("dy"), py::arg("x"), py::arg("dtype"),
         py::arg("pro_sc") = py::none(), py::arg("pro_bi") = py::none(),
         py::arg("dz_z") = py::none(), py::arg("dz_mask") = py::none(), py::arg("dz_a") = py::none(),
-        py::arg("dz_b") = py::none(), py::arg("dz_c") = py::none(),
+        py::arg("dz_b") = py::none(), py::arg("dz_c") = py::none(), py::arg("out") = py::none(),
         "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
   m.def("wgrad3x3s2_ok", &wgrad3x3s2_ok, py::arg("N"), py::arg("H"), py::arg("W"),
         py::arg("Co"), py::arg("Ci"));

@@ -202,7 +202,11 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FaArgs a) {
   for (int t = 0; t < nt; ++t) {
     const char* kimg = smem + (t & 1) * 2 * kImg;
     const char* vimg = kimg + kImg;
-    __syncthreads();   // tile t landed; every wave is done with tile t - 1's buffer
+    // tile t landed (this wave's DMAs: a barrier does not wait for global_load_lds, and hipcc
+    // inserts no wait here -- its alias analysis separates the two buffers), then every wave's;
+    // every wave is done with tile t - 1's buffer
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (t + 1 < nt) {
       char* nb = smem + ((t + 1) & 1) * 2 * kImg;
       stage(kg, kD, (t + 1) * kBK, S, nb, w, lane);
@@ -319,6 +323,7 @@ __global__ __launch_bounds__(kThreads, 2) void fa_dq_kernel(FaArgs a) {
   for (int t = 0; t < nt; ++t) {
     const char* kimg = smem + (t & 1) * 2 * kImg;
     const char* vimg = kimg + kImg;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t landed (see fa_fwd_kernel)
     __syncthreads();
     if (t + 1 < nt) {
       char* nb = smem + ((t + 1) & 1) * 2 * kImg;
@@ -418,6 +423,7 @@ __global__ __launch_bounds__(kKVThreads, 2) void fa_dkdv_kernel(FaArgs a) {
     const char* dimg = buf + kImg;
     const float* lsel = reinterpret_cast<const float*>(buf + 2 * kImg);
     const float* dsl = lsel + 64;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t landed (see fa_fwd_kernel)
     __syncthreads();
     if (t + 1 < nt) stage_all(t + 1, bufs + ((t + 1) & 1) * kKVBuf);
     const int q0 = qstart + t * kBK;

@@ -83,7 +83,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm128_nt_kernel(GemmArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   stage(0, 0);
-  __syncthreads();   // tile 0 landed (the barrier waits for the LDS-DMA)
+  // tile 0 landed: the barrier itself does not wait for global_load_lds, so this wave's DMAs are
+  // waited first (as before every barrier below)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) stage(kt + 1, buf ^ 1);   // buffer buf ^ 1 was retired by the barrier above
@@ -105,6 +108,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm128_nt_kernel(GemmArgs a) {
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();   // tile kt + 1 landed; every wave is done reading buffer buf
   }
 

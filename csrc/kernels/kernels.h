@@ -367,6 +367,9 @@ size_t stem_cola_work_floats(int N, int H, int W, int C);
 // pro: x prologue; dmode: dy prologue (0 none, 1 full, 2 mask, 3 BN-ReLU); cs: column sums
 void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro = false,
                    int dmode = 0, bool cs = false);
+// True when that call runs as one split on the LDS-DMA kernel without column sums: the kernel then
+// writes dw itself (bf16 or fp32) and `part` may be null (long-K shapes, e.g. transformer linears).
+bool wgrad1x1_direct(int64_t P, int Co, int Ci, bool pro = false, int dmode = 0, bool cs = false);
 // dz_z / dz_mask / dz_a / dz_b / dz_c (all or none): dy is the output gradient of a BN + ReLU that
 // consumed the conv output z = dz_z; the staging uses dz = a (mask ? dy : 0) + b z + c instead.
 // General form: dmode 0 none, 1 the dz_* BN-backward prologue above, 2 dz = dz_a (mask ? dy : 0)

@@ -362,6 +362,7 @@ struct DmaArgs {
   const float* da;
   const float* dc;
   float* cs_part;
+  uint16_t* outb;         // one split: dW bf16 [Co][ncol] written directly (no partial, no fold)
 };
 
 // XF: the prologues of the register-staged kernel (PRO on x, DP_MASK on dy, column sums), applied
@@ -583,6 +584,19 @@ __global__ __launch_bounds__((TM / 64) * (TN / WN) * 64) void wgrad_dma_kernel(D
     }
   }
   // partial [split][Co][ncol]: lane r = column, register k = co row (k&3) + 8 (k>>2) + 4 h
+  if (a.outb != nullptr) {   // one split: bf16 dW, no fold (uniform branch)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < NB; ++e)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int co = co0 + 64 * wm + 32 * i + (k & 3) + 8 * (k >> 2) + 4 * h;
+          const int col = n0 + WN * wn + 32 * e + r;
+          a.outb[static_cast<int64_t>(co) * a.ncol + col] = f2bf(acc[i][e][k]);
+        }
+    return;
+  }
   float* pw = a.part + static_cast<int64_t>(split) * a.Co * a.ncol;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -898,6 +912,13 @@ void wgrad1x1_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro, i
   staged_plan(P, Co, Ci, splits, cps, pro || dmode != DP_NONE || cs);
 }
 
+bool wgrad1x1_direct(int64_t P, int Co, int Ci, bool pro, int dmode, bool cs) {
+  int TM, TN, S, cps;
+  if (cs || !dma_ok(P, Co, Ci, pro, dmode, cs, &TM, &TN)) return false;
+  dma_plan(P, Co, Ci, TM, TN, &S, &cps);
+  return S == 1;
+}
+
 // plan of the register-staged kernel (pro: any prologue or column sums)
 void staged_plan(int64_t P, int Co, int Ci, int* splits, int* cps, bool pro) {
   int TM, TN;
@@ -951,10 +972,14 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
     if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x)) % 16)
       return hipErrorInvalidValue;
     dma_plan(P, Co, Ci, TM, TN, &S, &cps);
+    // one split, no column sums: the kernel writes dW itself (wgrad1x1_direct; part may be null)
+    const bool direct = S == 1 && cs == nullptr;
+    if (!direct && part == nullptr) return hipErrorInvalidValue;
     DmaArgs da{};
     da.dy = reinterpret_cast<const uint16_t*>(dy);
     da.x = reinterpret_cast<const uint16_t*>(x);
-    da.part = part;
+    da.part = direct && !dw_bf16 ? reinterpret_cast<float*>(dw) : part;
+    da.outb = direct && dw_bf16 ? reinterpret_cast<uint16_t*>(dw) : nullptr;
     da.Co = Co;
     da.ncol = Ci;
     da.Ci = Ci;
@@ -971,10 +996,12 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
     else if (dpm) e = launch_dma_xf<false, true>(TM, TN, da, P, S, cps, st);
     else e = launch_dma_tile(TM, TN, false, da, P, S, cps, st);
     if (e != hipSuccess) return e;
+    if (direct) return hipGetLastError();
     if (cs) fold_splits(cs_part, S, Co, cs, false, st);
     fold_splits(part, S, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, st);
     return hipGetLastError();
   }
+  if (part == nullptr) return hipErrorInvalidValue;
   staged_plan(P, Co, Ci, &S, &cps, anypro);
   pick_tile(Co, Ci, &TM, &TN, anypro);
   const int KC = chunk_of(TM, TN);

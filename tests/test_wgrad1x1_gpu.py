@@ -127,3 +127,27 @@ def test_wgrad1x1_dma_prologues(cuda, N, ci, co, hw, pro, colsum):
     dw2, cs2 = lib().wgrad1x1_ex(dy, x, sc if pro else None, bi if pro else None, 2, mask, a,
                                  None, c, colsum)
     assert torch.equal(dw, dw2) and (not colsum or torch.equal(cs, cs2))
+
+
+@pytest.mark.parametrize("T,N,K", [(8192, 4096, 4096), (4096, 6144, 4096), (2048, 4096, 7168),
+                                   (8192, 2048, 4096)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("use_out", [False, True])
+def test_wgrad1x1_one_split_direct(cuda, T, N, K, dtype, use_out):
+    """Long-K transformer-linear shapes (>= 256 output tiles of 256 x 256: one split on the DMA
+    kernel): dW is written by the kernel itself, no partial slab and no fold, optionally into a
+    caller-given destination (a view of a flat gradient row)."""
+    torch.manual_seed(T + N + K)
+    dy = torch.randn(T, N, device=cuda).to(torch.bfloat16)
+    x = torch.randn(T, K, device=cuda).to(torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    out = None
+    if use_out:
+        row = torch.full((N * K + 64,), float("nan"), device=cuda, dtype=dtype)
+        out = row[64:64 + N * K]          # 16-B aligned view at an offset
+    dw = lib().wgrad1x1(dy.view(T, 1, 1, N).permute(0, 3, 1, 2),
+                        x.view(T, 1, 1, K).permute(0, 3, 1, 2), dtype, out=out)
+    if use_out:
+        assert dw.data_ptr() == out.data_ptr()
+        assert torch.isnan(row[:64]).all()   # nothing written outside the destination
+    assert _rel(dw.view(N, K), ref) < (6e-3 if dtype == torch.bfloat16 else 1e-5)
