@@ -40,36 +40,45 @@ def fused_conv_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and w.shape[0] % 64 == 0 and w.shape[2] == 1 and w.shape[3] == 1)
 
 
-def _nt_ok(a: torch.Tensor, M: int, N: int, K: int) -> bool:
-    """gemm.hip takes this 1x1-conv GEMM: policy on, bf16 GPU operands, 256-multiple M and N,
-    64-multiple K, enough 256 x 256 tiles to fill the chip."""
+def _nt_tile(a: torch.Tensor, M: int, N: int, K: int) -> int:
+    """Tile of the gemm.hip kernel that takes this 1x1-conv GEMM, or 0 (hipBLASLt): policy on,
+    bf16 GPU operands, then ``gemm_nt_pick`` -- the 256 x 256 kernel once it has >= 128 tiles
+    (it fills the chip), else the 128 x 128 one (the layer-4 GEMMs of a batch-256 rank: 34.9-37.0
+    vs 43.2-44.6 us on the 256 tile and 44.9-48.8 on hipBLASLt; at batch 2048 every shape takes
+    the 256 tile, `profiles/r05_35/conv_mm_b*.jsonl`)."""
     if not (_P().own_gemm_conv1x1 and a.is_cuda and a.dtype == torch.bfloat16):
-        return False
+        return 0
     try:
-        return bool(lib().gemm_nt_ok(M, N, K)) and (M // 256) * (N // 256) >= 128
+        t = int(lib().gemm_nt_pick(M, N, K))
     except Exception:
-        return False
+        return 0
+    if t == 256:
+        return 256 if (M // 256) * (N // 256) >= 128 else 0
+    return 128 if t == 128 and _P().own_gemm128 else 0
 
 
-CONV_MM_STATS = {"own": 0, "blas": 0}   # which path conv_mm took (tests)
+CONV_MM_STATS = {"own": 0, "own128": 0, "blas": 0}   # which path conv_mm took (tests)
 
 
 def conv_mm(a: torch.Tensor, w_nk: torch.Tensor, acc: Optional[torch.Tensor] = None) -> torch.Tensor:
     """a [M, K] @ w_nk^T (+ acc, in place) for a 1x1 conv as a plain GEMM: the forward (w_nk = W
     [Co, C]) or the data gradient (w_nk = W^T [C, Co]; acc = a parked residual gradient). On
-    ``gemm.hip`` (NT, acc added in its epilogue: bf16(bf16(a w^T) + acc)) when eligible, else
-    hipBLASLt (mm / addmm_ beta = 1). Replaces the layer-3/4 hipBLASLt GEMMs of the ResNet step
-    (4.8 ms/step in profiles/r04_07/)."""
+    ``gemm.hip`` / ``gemm128.hip`` (NT, acc added in the epilogue: bf16(bf16(a w^T) + acc)) when
+    eligible (``_nt_tile``), else hipBLASLt (mm / addmm_ beta = 1). Replaces the layer-3/4
+    hipBLASLt GEMMs of the ResNet step (4.8 ms/step in profiles/r04_07/)."""
     M, K = a.shape
     N = w_nk.shape[0]
-    if (_nt_ok(a, M, N, K) and a.is_contiguous() and a.data_ptr() % 16 == 0
+    tile = _nt_tile(a, M, N, K)
+    if (tile and a.is_contiguous() and a.data_ptr() % 16 == 0
             and (acc is None or (acc.is_contiguous() and acc.data_ptr() % 16 == 0))):
         w = (lib().transpose_bf16(w_nk.t()) if (w_nk.stride(0) == 1 and w_nk.dim() == 2)
              else w_nk.contiguous())
         CONV_MM_STATS["own"] += 1
+        if tile == 128:
+            CONV_MM_STATS["own128"] += 1
         if acc is not None:
-            return lib().gemm_nt(a, w, 0, out=acc, cin=acc, tile=256)
-        return lib().gemm_nt(a, w, 0, tile=256)
+            return lib().gemm_nt(a, w, 0, out=acc, cin=acc, tile=tile)
+        return lib().gemm_nt(a, w, 0, tile=tile)
     CONV_MM_STATS["blas"] += 1
     if acc is not None:
         return acc.addmm_(a, w_nk.t()) if acc.is_contiguous() else torch.addmm(acc, a, w_nk.t())

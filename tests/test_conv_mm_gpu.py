@@ -11,8 +11,10 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("M,K,N", [(32768, 1024, 256), (32768, 256, 1024), (65536, 512, 2048)])
+@pytest.mark.parametrize("M,K,N", [(32768, 1024, 256), (32768, 256, 1024), (65536, 512, 2048),
+                                   (12544, 2048, 512)])
 def test_conv_mm_vs_fp32(cuda, M, K, N):
+    """(12544, 2048, 512): a batch-256 layer-4 GEMM, 98 tiles of 256 x 256 -> the 128 x 128 kernel"""
     from consensusml_amd.ops import conv as fconv
     g = torch.Generator(device=cuda).manual_seed(0)
     a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
@@ -24,6 +26,8 @@ def test_conv_mm_vs_fp32(cuda, M, K, N):
     acc = acc0.clone()
     y2 = fconv.conv_mm(a, w, acc=acc)
     assert fconv.CONV_MM_STATS["own"] == before["own"] + 2
+    small = (M // 256) * (N // 256) < 128
+    assert fconv.CONV_MM_STATS["own128"] == before["own128"] + (2 if small else 0)
     assert y2.data_ptr() == acc.data_ptr()            # in place into the residual gradient
     assert _rel(y, ref) < 5e-3
     assert _rel(y2, ref + acc0.float()) < 5e-3
