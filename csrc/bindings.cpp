@@ -2306,6 +2306,9 @@ Tensor gemm_nt(const Tensor& a, const Tensor& b, int64_t ep, const optional<Tens
 }
 
 bool gemm_nt_ok(int64_t M, int64_t N, int64_t K) { return cml::gemm_nt_eligible(M, N, K); }
+int64_t gemm_conv_tm(int64_t M, int64_t N, int64_t C) {
+  return cml::gemm_conv_tm(M, static_cast<int>(N), static_cast<int>(C));
+}
 
 // column sums of x viewed as [M, N] (N = last dim) -> bf16 [N]
 Tensor colsum(const Tensor& x_in) {
@@ -2548,6 +2551,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("aux") = py::none(), py::arg("out") = py::none(),
         py::arg("colsum_out") = py::none(), py::arg("cin") = py::none(), py::arg("tile") = 0);
   m.def("gemm_nt_ok", &gemm_nt_ok, "shape eligibility of gemm_nt's 256 x 256 kernel");
+  m.def("gemm_conv_tm", &gemm_conv_tm, "m-tile of gemm.hip's 3x3 conv mode for M x N, C (256, 512, 0)");
   m.def("gemm_nt_pick", &gemm_nt_pick, "EP_STORE tile choice of gemm_nt: 256, 128 or 0 (none)");
   m.attr("CMB_SORTED") = static_cast<int>(cml::CMB_SORTED);
   m.attr("CMB_WEIGHTED") = static_cast<int>(cml::CMB_WEIGHTED);

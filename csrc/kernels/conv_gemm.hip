@@ -14,6 +14,7 @@
 // fragment reads use the same involution (conv1x1.hip's swz). The fp32 accumulators go out through
 // a per-wave LDS image as whole-line 16-B stores. Tiles are mapped XCD-aware (the n-tiles of one
 // m-tile are consecutive on one XCD: x comes from HBM once and from that XCD's L2 after).
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -382,14 +383,19 @@ int pick_variant(int64_t M, int N, int* BM, int* BN);
 // and whose pixel count is a multiple of 256 run on gemm.hip's schedule instead (launch_gemm_conv:
 // 16x16x32 MFMAs, four staggered phases per k-tile with 4 DMA units in flight and counted vmcnt,
 // no per-step drain) with the same epilogues
-bool use_gemm2(int64_t M, int N, int C, int taps, int stride) {
+// The 128-channel convs (layer 2: variant 2's 256 x 128 tiles, 0.6-0.67 PFLOP/s) take gemm.hip's
+// 512 x 128 tile when the grid has enough of them (gemm_conv_tm == 512).
+// Returns the m-tile (256 / 512) or 0.
+int use_gemm2(int64_t M, int N, int C, int taps, int stride) {
   static const bool on = [] {
     const char* e = getenv("CML_CONV_GEMM2");
     return !e || e[0] != '0';
   }();
-  if (!on || taps != 9 || stride != 1 || !gemm_conv_eligible(M, N, C)) return false;
+  if (!on || taps != 9 || stride != 1) return 0;
+  const int tm = gemm_conv_tm(M, N, C);
+  if (tm == 512) return 512;
   int BM = 0, BN = 0;
-  return pick_variant(M, N, &BM, &BN) == 4;
+  return tm == 256 && pick_variant(M, N, &BM, &BN) == 4 ? 256 : 0;
 }
 
 // the variant and tile (BM, BN) for an M x N output
@@ -443,8 +449,14 @@ size_t conv_gemm_part_floats(int64_t M, int N) {
   const int64_t mtiles = (M + BM - 1) / BM;
   const int R = static_cast<int>(mtiles * (BM / 64));
   // the slab, then the fold area of launch_bn_stats_finalize
-  const size_t g = static_cast<size_t>(N / BN) *
-                   (static_cast<size_t>(R) + bn_part_fold_slices(R, N / BN)) * 2 * BN;
+  size_t g = static_cast<size_t>(N / BN) *
+             (static_cast<size_t>(R) + bn_part_fold_slices(R, N / BN)) * 2 * BN;
+  // gemm.hip's slab when a 3x3 conv of this M x N runs there (use_gemm2)
+  if (const int tm = M % 64 == 0 ? gemm_conv_tm(M, N, 64) : 0) {
+    const int tn = 65536 / tm, R2 = static_cast<int>(M / tm) * (tm / 128);
+    g = std::max(g, static_cast<size_t>(N / tn) *
+                        (static_cast<size_t>(R2) + bn_part_fold_slices(R2, N / tn)) * 2 * tn);
+  }
   return N == 64 && g < conv3x3p_part_floats() ? conv3x3p_part_floats() : g;
 }
 
@@ -484,7 +496,7 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
     return launch_bn_stats_finalize(part, R, 64, 64, M, shift, eps, momentum, mean, invstd, rmean,
                                     rvar, st, nullptr);
   }
-  if (use_gemm2(M, N, C, taps, stride)) {
+  if (const int tm = use_gemm2(M, N, C, taps, stride)) {
     GemmArgs g{};
     g.a = a.x;
     g.b = a.w;
@@ -499,9 +511,9 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
     g.shift = shift;
     hipError_t e = launch_gemm_conv(g, part ? EP_CONV_ST : EP_STORE, st);
     if (e != hipSuccess || !part || !mean) return e;
-    const int R = static_cast<int>(M / 256) * 2;
-    return launch_bn_stats_finalize(part, R, 256, N, M, shift, eps, momentum, mean, invstd, rmean,
-                                    rvar, st, part + static_cast<size_t>(N / 256) * R * 2 * 256);
+    const int tn = 65536 / tm, R = static_cast<int>(M / tm) * (tm / 128);
+    return launch_bn_stats_finalize(part, R, tn, N, M, shift, eps, momentum, mean, invstd, rmean,
+                                    rvar, st, part + static_cast<size_t>(N / tn) * R * 2 * tn);
   }
   hipError_t e = taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
   if (e != hipSuccess || !part || !mean) return e;
@@ -549,7 +561,7 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
     if (e != hipSuccess) return e;
     return launch_bnbwd_sums_finalize(part, R, 64, 64, invstd, sdz, sdzx, st, nullptr);
   }
-  if (use_gemm2(M, N, C, taps, 1)) {
+  if (const int tm = use_gemm2(M, N, C, taps, 1)) {
     GemmArgs g{};
     g.a = a.x;
     g.b = a.w;
@@ -567,9 +579,9 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
     g.ep_bi = bi;
     hipError_t e = launch_gemm_conv(g, EP_CONV_BB, st);
     if (e != hipSuccess) return e;
-    const int R = static_cast<int>(M / 256) * 2;
-    return launch_bnbwd_sums_finalize(part, R, 256, N, invstd, sdz, sdzx, st,
-                                      part + static_cast<size_t>(N / 256) * R * 2 * 256);
+    const int tn = 65536 / tm, R = static_cast<int>(M / tm) * (tm / 128);
+    return launch_bnbwd_sums_finalize(part, R, tn, N, invstd, sdz, sdzx, st,
+                                      part + static_cast<size_t>(N / tn) * R * 2 * tn);
   }
   hipError_t e = taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
   if (e != hipSuccess) return e;

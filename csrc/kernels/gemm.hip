@@ -43,6 +43,8 @@
 //     consecutive ids share an XCD under round-robin placement (A read from HBM once).
 // Requirements (checked by the launcher): M % 256 == 0, N % 256 == 0, K % 64 == 0, 16-B aligned
 // rows. Other shapes go to hipBLASLt (ops/transformer.py).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -53,12 +55,27 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void g_void;
 
-constexpr int kT = 256;                 // tile edge
+constexpr int kT = 256;                 // tile edge (square tiles)
 constexpr int kBK = 64;                 // K per tile step
 constexpr int kThreads = 512;
-constexpr int kImg = kT * 128;          // one operand image (256 rows x 128 B)
-constexpr int kBuf = 2 * kImg;          // A image + B image
-constexpr int kLds = 2 * kBuf;          // 128 KB
+
+// Tile TM (m) x TN (n) with TM TN = 256 x 256: TM = 256 is the square tile; TM = 512 (TN = 128) is
+// the tall tile of the 128-channel 3x3 convs (ResNet-50 layer 2), with the same 128 x 64 wave
+// blocks (waves 4 (m) x 2 (n)) and therefore the same MFMA / fragment schedule; its A image is
+// 512 rows, so a buffer is 80 KB and the two buffers take the whole 160 KB of LDS.
+template <int TM>
+struct Tile {
+  static constexpr int TN = kT * kT / TM;
+  static constexpr int WMR = TM / 128;            // wave m-rows
+  static constexpr int WNC = 8 / WMR;             // wave n-columns
+  static constexpr int ImgA = TM * 128, ImgB = TN * 128;
+  static constexpr int Buf = ImgA + ImgB;
+  static constexpr int Lds = 2 * Buf;
+  static constexpr int IA = TM / 128, IB = TN / 128;   // wave-instructions per A / B unit
+  static constexpr int VM = 2 * IA + 2 * IB;      // this wave's instructions of 4 units
+  static_assert(TM == 256 || TM == 512, "tile");
+  static_assert(Lds <= 160 * 1024, "LDS");
+};
 
 __device__ __forceinline__ int swz(int row, int c) { return row * 128 + 16 * (c ^ ((row >> 1) & 7)); }
 
@@ -66,30 +83,33 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_t a, bf16x8_t b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int EP, bool CONV>
+template <int EP, bool CONV, int TM = 256>
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
+  using T = Tile<TM>;
+  constexpr int TN = T::TN;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / T::WNC, wn = wave % T::WNC;
 
   // ---- tile (bijective XCD remap: consecutive ids share an XCD; n fastest)
-  const int ntn = a.N / kT;
-  const int G = (a.M / kT) * ntn, b = blockIdx.x, xcd = b & 7, q8 = G >> 3, r8 = G & 7;
+  const int ntn = a.N / TN;
+  const int G = (a.M / TM) * ntn, b = blockIdx.x, xcd = b & 7, q8 = G >> 3, r8 = G & 7;
   const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int mtile = t / ntn, ntile = t - mtile * ntn;
-  const int m0 = mtile * kT, n0 = ntile * kT;
+  const int m0 = mtile * TM, n0 = ntile * TN;
   const int nk = a.K / kBK;
 
-  // ---- staging: unit u (0..3 = U1..U4) of K-tile kt into buffer buf; this wave's 2 of the
-  // unit's 16 wave-instructions (8 rows x 128 B each)
+  // ---- staging: unit u (0..3 = U1..U4) of K-tile kt into buffer buf; this wave's IA (A units)
+  // or IB (B units) of the unit's wave-instructions (8 rows x 128 B each)
   const int lrow = lane >> 3, lp = lane & 7;
-  // CONV: this lane's 4 A rows (j = 2 s + (u == 3): tile rows 64 j + 8 wave + lrow) as pixels
-  int pbase[CONV ? 4 : 1], poh[CONV ? 4 : 1], pow_[CONV ? 4 : 1];
+  // CONV: this lane's TM / 64 A rows (j = 2 s + (u == 3): tile rows 64 j + 8 wave + lrow) as pixels
+  constexpr int NJ = CONV ? TM / 64 : 1;
+  int pbase[NJ], poh[NJ], pow_[NJ];
   if constexpr (CONV) {
     const int HW = a.H * a.W;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int m = m0 + 64 * j + 8 * wave + lrow;
       const int img = m / HW, rem = m - img * HW;
       pbase[j] = img * HW;
@@ -100,15 +120,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   auto stage = [&](int u, int kt, int buf) {
     kt = kt < nk ? kt : nk - 1;                 // past the end: a harmless repeat (dead buffer)
     const int64_t kofs = static_cast<int64_t>(kt) * kBK;
+    const bool isA = (u == 0 || u == 3);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < (T::IA > T::IB ? T::IA : T::IB); ++s) {
+      if (s >= (isA ? T::IA : T::IB)) break;
       const int i = wave + 8 * s;               // wave-instruction of the unit
       int row0;
-      if (u == 0 || u == 3) row0 = (i >> 3) * 128 + (u == 3 ? 64 : 0) + (i & 7) * 8;   // A
-      else row0 = (i >> 2) * 64 + (u == 2 ? 32 : 0) + (i & 3) * 8;                  // B
+      if (isA) row0 = (i >> 3) * 128 + (u == 3 ? 64 : 0) + (i & 7) * 8;   // A
+      else row0 = (i >> 2) * 64 + (u == 2 ? 32 : 0) + (i & 3) * 8;        // B
       const int row = row0 + lrow;
       const int c = lp ^ ((row >> 1) & 7);
-      const bool isA = (u == 0 || u == 3);
       const uint16_t* src;
       if (CONV && isA) {
         // k-tile kt = tap (C / 64) + cc: input pixel (oh + ky - 1, ow + kx - 1), channels cc 64 ..
@@ -123,7 +144,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
         src = isA ? a.a + static_cast<int64_t>(m0 + row) * a.lda + kofs + 8 * c
                   : a.b + static_cast<int64_t>(n0 + row) * a.ldb + kofs + 8 * c;
       }
-      char* dst = smem + buf * kBuf + (isA ? 0 : kImg) + row0 * 128;
+      char* dst = smem + buf * T::Buf + (isA ? 0 : T::ImgA) + row0 * 128;
       __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
     }
   };
@@ -132,7 +153,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   const int fr = lane & 15, fc = lane >> 4;
   bf16x8_t aF[2][4][2], bF[2][2][2];
   auto readA = [&](bf16x8_t (&f)[4][2], int mh, int buf) {
-    const char* img = smem + buf * kBuf;
+    const char* img = smem + buf * T::Buf;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -141,7 +162,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
             img + swz(wm * 128 + mh * 64 + mt * 16 + fr, fc + 4 * ks));
   };
   auto readB = [&](bf16x8_t (&f)[2][2], int nh, int buf) {
-    const char* img = smem + buf * kBuf + kImg;
+    const char* img = smem + buf * T::Buf + T::ImgA;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
@@ -166,7 +187,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
               mfma16(bF[nh][nt][ks], aF[mh][mt][ks], acc[mh * 4 + mt][nh * 2 + nt]);
     __builtin_amdgcn_s_setprio(0);
   };
-  auto wait8 = [] { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
+  // 4 newer units may stay in flight (the 4 newest units are always one each of U1..U4)
+  auto wait8 = [] { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::VM) : "memory"); };
   auto bar = [] {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -178,9 +200,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   stage(0, 1, 1); stage(1, 1, 1);
   wait8();
   bar();
-  // stagger: the m-row-1 waves (the second wave of every SIMD) run one section behind, so each
-  // SIMD alternates one wave's MFMA section with its partner's read / issue section
-  if (wm) bar();
+  // stagger: the second wave of every SIMD (waves 4-7) runs one section behind, so each SIMD
+  // alternates one wave's MFMA section with its partner's read / issue section
+  const bool lag = wave >= 4;
+  if (lag) bar();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
@@ -213,7 +236,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
     quad(1, 0);
     bar();
   }
-  if (!wm) bar();             // balance the stagger barrier
+  if (!lag) bar();            // balance the stagger barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   bar();
 
@@ -374,12 +397,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
       cq[e] = s2;
     }
     if (lane < 8) {
-      const int R = static_cast<int>(a.M / kT) * 2;
-      float* p = a.part + (static_cast<int64_t>(ntile) * R + mtile * 2 + wm) * 2 * kT + wn * 64 + 8 * lane;
+      const int R = static_cast<int>(a.M / TM) * T::WMR;
+      float* p = a.part + (static_cast<int64_t>(ntile) * R + mtile * T::WMR + wm) * 2 * TN +
+                 wn * 64 + 8 * lane;
       reinterpret_cast<float4*>(p)[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
       reinterpret_cast<float4*>(p)[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
-      reinterpret_cast<float4*>(p + kT)[0] = make_float4(cq[0], cq[1], cq[2], cq[3]);
-      reinterpret_cast<float4*>(p + kT)[1] = make_float4(cq[4], cq[5], cq[6], cq[7]);
+      reinterpret_cast<float4*>(p + TN)[0] = make_float4(cq[0], cq[1], cq[2], cq[3]);
+      reinterpret_cast<float4*>(p + TN)[1] = make_float4(cq[4], cq[5], cq[6], cq[7]);
     }
   }
   if constexpr (EP == EP_DGELU) {
@@ -394,7 +418,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
         cs[e] = s;
       }
       if (lane < 8) {
-        float* p = a.part + static_cast<int64_t>(mtile * 2 + wm) * a.N + ncol;
+        float* p = a.part + static_cast<int64_t>(mtile * T::WMR + wm) * a.N + ncol;
         reinterpret_cast<float4*>(p)[0] = make_float4(cs[0], cs[1], cs[2], cs[3]);
         reinterpret_cast<float4*>(p)[1] = make_float4(cs[4], cs[5], cs[6], cs[7]);
       }
@@ -423,20 +447,16 @@ bool gemm_nt_eligible(int64_t M, int64_t N, int64_t K) {
          (M / kT) * (N / kT) < (1LL << 31);
 }
 
-hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st) {
-  if (!gemm_nt_eligible(a.M, a.N, a.K)) return hipErrorInvalidValue;
-  if ((a.lda % 8) || (a.ldb % 8) || (a.ldy % 8)) return hipErrorInvalidValue;
-  if ((reinterpret_cast<uintptr_t>(a.a) | reinterpret_cast<uintptr_t>(a.b) |
-       reinterpret_cast<uintptr_t>(a.y)) % 16)
-    return hipErrorInvalidValue;
-  if ((ep == EP_GELU || ep == EP_DGELU) && (a.aux == nullptr || reinterpret_cast<uintptr_t>(a.aux) % 16))
-    return hipErrorInvalidValue;
-  const int tiles = (a.M / kT) * (a.N / kT);
+namespace {
+template <int TM>
+hipError_t launch_tm(const GemmArgs& a, int ep, hipStream_t st) {
+  using T = Tile<TM>;
+  const int tiles = static_cast<int>((a.M / TM) * (a.N / T::TN));
 #define CML_GEMM(E, CV)                                                                      \
   do {                                                                                       \
-    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<E, CV>),                \
-                        hipFuncAttributeMaxDynamicSharedMemorySize, kLds);                   \
-    gemm_nt_kernel<E, CV><<<tiles, kThreads, kLds, st>>>(a);                                 \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<E, CV, TM>),            \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, T::Lds);                 \
+    gemm_nt_kernel<E, CV, TM><<<tiles, kThreads, T::Lds, st>>>(a);                           \
   } while (0)
   if (a.conv) {
     switch (ep) {
@@ -446,21 +466,57 @@ hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st) {
       default: return hipErrorInvalidValue;
     }
   } else {
-    switch (ep) {
-      case EP_STORE: CML_GEMM(EP_STORE, false); break;
-      case EP_GELU: CML_GEMM(EP_GELU, false); break;
-      case EP_DGELU: CML_GEMM(EP_DGELU, false); break;
-      default: return hipErrorInvalidValue;
+    if constexpr (TM != 256) {
+      return hipErrorInvalidValue;
+    } else {
+      switch (ep) {
+        case EP_STORE: CML_GEMM(EP_STORE, false); break;
+        case EP_GELU: CML_GEMM(EP_GELU, false); break;
+        case EP_DGELU: CML_GEMM(EP_DGELU, false); break;
+        default: return hipErrorInvalidValue;
+      }
     }
   }
 #undef CML_GEMM
   return hipGetLastError();
 }
 
-bool gemm_conv_eligible(int64_t M, int N, int C) {
-  return M > 0 && M % kT == 0 && N % kT == 0 && C % kBK == 0 && M < (1LL << 31) &&
-         9LL * C <= 65536;
+bool check_ptrs(const GemmArgs& a, int ep) {
+  if ((a.lda % 8) || (a.ldb % 8) || (a.ldy % 8)) return false;
+  if ((reinterpret_cast<uintptr_t>(a.a) | reinterpret_cast<uintptr_t>(a.b) |
+       reinterpret_cast<uintptr_t>(a.y)) % 16)
+    return false;
+  if ((ep == EP_GELU || ep == EP_DGELU) && (a.aux == nullptr || reinterpret_cast<uintptr_t>(a.aux) % 16))
+    return false;
+  return true;
 }
+
+// CML_GEMM2_TALL: the fewest 512 x 128 tiles for which a 128-channel 3x3 conv takes the tall
+// tile (default 1024, four rounds of 256 CUs: batch 2048's 3136 tiles, not batch 256's 392;
+// 0 disables it: A/B)
+int tall_min_tiles() {
+  static const int v = [] {
+    const char* e = getenv("CML_GEMM2_TALL");
+    return e ? atoi(e) : 1024;
+  }();
+  return v;
+}
+}  // namespace
+
+hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st) {
+  if (!gemm_nt_eligible(a.M, a.N, a.K) || !check_ptrs(a, ep)) return hipErrorInvalidValue;
+  return launch_tm<256>(a, ep, st);
+}
+
+int gemm_conv_tm(int64_t M, int N, int C) {
+  if (M <= 0 || M >= (1LL << 31) || C % kBK || 9LL * C > 65536) return 0;
+  if (M % kT == 0 && N % kT == 0) return 256;
+  const int tall = tall_min_tiles();
+  if (tall > 0 && N % 128 == 0 && M % 512 == 0 && (M / 512) * (N / 128) >= tall) return 512;
+  return 0;
+}
+
+bool gemm_conv_eligible(int64_t M, int N, int C) { return gemm_conv_tm(M, N, C) != 0; }
 
 hipError_t launch_gemm_conv(const GemmArgs& a0, int ep, hipStream_t st) {
   GemmArgs a = a0;
@@ -469,16 +525,14 @@ hipError_t launch_gemm_conv(const GemmArgs& a0, int ep, hipStream_t st) {
   a.lda = a.C;
   a.ldb = a.K;
   a.ldy = a.N;
-  if (!gemm_conv_eligible(a.M, static_cast<int>(a.N), a.C) || !a.zero || !a.a || !a.b || !a.y)
-    return hipErrorInvalidValue;
+  const int tm = gemm_conv_tm(a.M, static_cast<int>(a.N), a.C);
+  if (!tm || !a.zero || !a.a || !a.b || !a.y) return hipErrorInvalidValue;
   if (static_cast<int64_t>(a.H) * a.W < 1 || a.M % (static_cast<int64_t>(a.H) * a.W))
     return hipErrorInvalidValue;
   if ((ep == EP_CONV_ST || ep == EP_CONV_BB) && !a.part) return hipErrorInvalidValue;
   if (ep == EP_CONV_BB && (!a.sz || !a.ep_sc || !a.ep_bi)) return hipErrorInvalidValue;
-  if ((reinterpret_cast<uintptr_t>(a.a) | reinterpret_cast<uintptr_t>(a.b) |
-       reinterpret_cast<uintptr_t>(a.y) | reinterpret_cast<uintptr_t>(a.zero)) % 16)
-    return hipErrorInvalidValue;
-  return launch_gemm_nt(a, ep, st);
+  if ((reinterpret_cast<uintptr_t>(a.zero) % 16) || !check_ptrs(a, ep)) return hipErrorInvalidValue;
+  return tm == 512 ? launch_tm<512>(a, ep, st) : launch_tm<256>(a, ep, st);
 }
 
 hipError_t launch_colsum_fold(const float* part, int64_t M, int N, int nseg, void* out, int64_t ldo,

@@ -577,7 +577,8 @@ struct GemmArgs {
   // implicit-GEMM 3x3 / stride 1 / padding 1 convolution (conv = 1): A = the NHWC input x
   // [Nimg][H][W][C] gathered per tap (a = x, K = 9 C, b = wf [N][9 C]); padded taps read `zero`.
   // EP_CONV_ST: the BN statistics of the stored bf16 output (minus shift[n]) as partial rows
-  // part[(ntile R + 2 mtile + wave row)][2][256], R = 2 M / 256; EP_CONV_BB: instead the sums of
+  // part[(ntile R + WMR mtile + wave row)][2][TN], R = WMR M / TM (gemm_conv_tm; WMR = TM / 128,
+  // TN = 65536 / TM; the square tile: R = 2 M / 256, TN = 256); EP_CONV_BB: instead the sums of
   // the BN + ReLU backward that y feeds (z = sz [M][N], ReLU bit z ep_sc + ep_bi > 0, shift = mean)
   int conv, C, H, W;
   const uint16_t* zero;
@@ -595,6 +596,10 @@ hipError_t launch_gemm128_nt(const GemmArgs& a, hipStream_t st);
 // the conv form (a.conv = 1; M % 256 == 0, N % 256 == 0, C % 64 == 0), ep EP_STORE /
 // EP_CONV_ST / EP_CONV_BB (conv_gemm.hip's 256 x 256 path for stride-1 3x3 convs)
 bool gemm_conv_eligible(int64_t M, int N, int C);
+// the m-tile launch_gemm_conv takes: 256 (256 x 256 tiles, N % 256 == 0), 512 (512 x 128 tiles:
+// 128-channel convs with enough tiles, CML_GEMM2_TALL), 0 = not eligible; partial slabs of
+// EP_CONV_ST / EP_CONV_BB then have R = (M / TM) (TM / 128) rows of 2 x (65536 / TM) floats
+int gemm_conv_tm(int64_t M, int N, int C);
 hipError_t launch_gemm_conv(const GemmArgs& a, int ep, hipStream_t st);
 // out[s][n] = sum of the 128-row partial column sums of segment s of M rows (nseg equal
 // segments, fixed order); out bf16 [nseg][ldo] or fp32 when out_f32

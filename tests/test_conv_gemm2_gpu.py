@@ -3,7 +3,8 @@ operand gathered per tap by the DMA path, 16x16x32 MFMAs, four staggered phases 
 conv_gemm.hip routes to when the 256 x 256 tile grid applies and the pixel count is a multiple of
 256: plain output, the BN-statistics epilogue and the BN + ReLU backward sums epilogue, against
 fp32 / fp64 PyTorch oracles. Shapes: ResNet-50 layer-3 / layer-4 channel counts (256 / 512),
-image borders on every side (padded taps read the zero row)."""
+image borders on every side (padded taps read the zero row); and the 512 x 128 tall tile of the
+128-channel (layer-2) convs, taken from 1024 such tiles (672 images of 28 x 28)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -30,7 +31,15 @@ def _rel(a, b):
 
 # (images, C, Co, H): M = images H H is a multiple of 256
 SHAPES = [(4, 256, 256, 16), (16, 512, 512, 8), (4, 64, 256, 16), (64, 256, 512, 14),
-          (256, 512, 512, 7)]
+          (672, 128, 128, 28), (672, 64, 128, 28), (256, 512, 512, 7)]
+TALL = [(672, 128, 128, 28), (672, 64, 128, 28)]
+
+
+@pytest.mark.parametrize("N,C,Co,H", TALL)
+def test_tall_tile_taken(cuda, N, C, Co, H):
+    assert _lib().gemm_conv_tm(N * H * H, Co, C) == 512
+    assert _lib().gemm_conv_tm(N * H * H, 256, C) == 256
+    assert _lib().gemm_conv_tm(256 * H * H, Co, C) == 0      # 392 tiles: conv_gemm.hip
 
 
 @pytest.mark.parametrize("N,C,Co,H", SHAPES)
@@ -48,7 +57,7 @@ def test_gemm_conv_forward_vs_fp32(cuda, N, C, Co, H):
     assert float(err[:, 0, :].max()) < 8 * float(err[:, H // 2, :].max()) + 1e-2
 
 
-@pytest.mark.parametrize("N,C,Co,H", SHAPES[:4])
+@pytest.mark.parametrize("N,C,Co,H", SHAPES[:6])
 def test_gemm_conv_bn_stats_and_grads(cuda, N, C, Co, H):
     """conv3x3_bn_stats (forward + statistics epilogue) and the data gradient through the rotated
     weights (a plain gemm conv when C % 256 == 0) vs fp32 autograd."""
@@ -78,7 +87,7 @@ def test_gemm_conv_bn_stats_and_grads(cuda, N, C, Co, H):
     assert _rel(conv.weight.grad, wr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("N,C,Co,H", SHAPES[:4])
+@pytest.mark.parametrize("N,C,Co,H", SHAPES[:6])
 def test_gemm_conv_bnsums_vs_fp64(cuda, N, C, Co, H):
     g0 = torch.Generator(device=cuda).manual_seed(33)
     x = _nhwc(torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16())
@@ -101,10 +110,11 @@ def test_gemm_conv_bnsums_vs_fp64(cuda, N, C, Co, H):
                                rtol=1e-5, atol=1e-3)
 
 
-def test_gemm_conv_deterministic(cuda):
+@pytest.mark.parametrize("N,C,Co,H", [(16, 256, 256, 14), (672, 128, 128, 28)])
+def test_gemm_conv_deterministic(cuda, N, C, Co, H):
     g0 = torch.Generator(device=cuda).manual_seed(34)
-    x = _nhwc(torch.randn(16, 256, 14, 14, device=cuda, generator=g0).bfloat16())
-    w = (torch.randn(256, 9 * 256, device=cuda, generator=g0) * 0.02).bfloat16()
+    x = _nhwc(torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16())
+    w = (torch.randn(Co, 9 * C, device=cuda, generator=g0) * 0.02).bfloat16()
     a = _lib().conv_gemm(x, w, 9)
     b = _lib().conv_gemm(x, w, 9)
     assert torch.equal(a, b)
