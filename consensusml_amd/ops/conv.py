@@ -23,7 +23,7 @@ Gradients: data gradient as a hipBLASLt GEMM (stride 1, per-shape policy of
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import Optional, Tuple, Dict
 
 import torch
 import torch.nn.functional as F
@@ -647,6 +647,41 @@ def _zero_row(device: torch.device) -> torch.Tensor:
     return z
 
 
+# PerfPolicy.side_wgrad: a weight gradient depends only on the conv's output gradient and saved
+# input, so it can run on a second HIP stream while the data-gradient and BN-backward kernels of
+# the same conv run on the current one (the GPU fills one kernel's tail rounds with the other's
+# workgroups). The side stream first waits for the current stream; the current stream waits for
+# the side stream before the backward returns, so every tensor the side kernels touch stays
+# ordered with the caching allocator's reuse on the current stream.
+_SIDE_STREAMS: Dict[torch.device, "torch.cuda.Stream"] = {}
+
+
+def _wgrad_fork(fn, *args):
+    """(dw, handle): ``fn(*args)`` on the side stream (PerfPolicy.side_wgrad, CUDA tensors), else
+    inline (handle None). ``_wgrad_join`` before the backward returns."""
+    dev = args[0].device
+    if not (_P().side_wgrad and dev.type == "cuda"):
+        return fn(*args), None
+    side = _SIDE_STREAMS.get(dev)
+    if side is None:
+        side = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    main = torch.cuda.current_stream(dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        dw = fn(*args)
+    return dw, (main, side)
+
+
+def _wgrad_join(dw: Optional[torch.Tensor], handle) -> Optional[torch.Tensor]:
+    if handle is None:
+        return dw
+    main, side = handle
+    main.wait_stream(side)
+    if dw is not None:
+        dw.record_stream(main)   # allocated on the side stream, consumed on the current one
+    return dw
+
+
 # PerfPolicy.own_wgrad3x3 -- 3x3 weight gradients on csrc/kernels/wgrad3x3.hip (nine taps per
 # workgroup): 1.4-2.0x faster than MIOpen's at the ResNet-50 shapes (profiles/r02_wgrad3x3_39.jsonl)
 
@@ -750,13 +785,14 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
         dz2 = dz2.contiguous(memory_format=torch.channels_last)
         L = lib()
         wr = ctx.wr   # rotated / transposed layout, made by the forward
+        dw, h = _wgrad_fork(_wgrad3x3, dz2, y1, w) if ctx.needs_input_grad[6] else (None, None)
         sc, bi = _affine(g1, b1, mean1, invstd1)
         dy1, s1, q1 = L.conv_gemm_bnsums(dz2, wr, 9, _zero_row(dz2.device), z1, sc, bi, mean1,
                                          invstd1)
         M = z1.numel() // z1.shape[1]
         _, _, _, dg1, db1 = L.bn_bwd_coeffs(s1, q1, g1, mean1, invstd1, M)
         dz1 = L.bn_bwd_apply(dy1, z1, g1, b1, mean1, invstd1, s1, q1)
-        dw = _wgrad3x3(dz2, y1, w) if ctx.needs_input_grad[6] else None
+        dw = _wgrad_join(dw, h)
         return dz1, dg1, db1, None, None, None, dw, None, None, None, None
 
 
@@ -830,13 +866,14 @@ class _BNReLUConv3x3S2BNStatsFn(torch.autograd.Function):
         z1, g1, b1, mean1, invstd1, y1, w = ctx.saved_tensors
         dz2 = dz2.contiguous(memory_format=torch.channels_last)
         L = lib()
+        dw, h = _wgrad_fork(_wgrad3x3_s2, dz2, y1, w) if ctx.needs_input_grad[6] else (None, None)
         sc, bi = _affine(g1, b1, mean1, invstd1)
         dy1, s1, q1 = L.conv_gemm_s2dgrad(dz2, ctx.wr, _zero_row(dz2.device), z1, sc, bi, mean1,
                                           invstd1)
         M = z1.numel() // z1.shape[1]
         _, _, _, dg1, db1 = L.bn_bwd_coeffs(s1, q1, g1, mean1, invstd1, M)
         dz1 = L.bn_bwd_apply(dy1, z1, g1, b1, mean1, invstd1, s1, q1)
-        dw = _wgrad3x3_s2(dz2, y1, w) if ctx.needs_input_grad[6] else None
+        dw = _wgrad_join(dw, h)
         return dz1, dg1, db1, None, None, None, dw, None, None, None, None
 
 

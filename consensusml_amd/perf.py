@@ -76,6 +76,8 @@ class PerfPolicy:
     own_wgrad3x3_s2: bool = True          # stride-2 3x3 weight gradient on the wgrad DMA kernel
     own_conv3x3_s2: bool = True           # stride-2 3x3: conv_gemm forward + BN stats, parity-class
                                           # data gradient (+ bn1 backward sums)
+    side_wgrad: bool = False              # 3x3 weight gradients on a side stream, concurrent with
+                                          # the same conv's data-gradient / BN-backward kernels
     # ---------------------------------------------------------------- transformers / engine
     attn_kernel: bool = True              # MFMA attention for short sequences (BERT)
     flash_attn: bool = True               # flash_attn.hip for head-dim-128 (GQA, causal) attention
@@ -137,6 +139,7 @@ class PerfPolicy:
             own_wgrad3x3=_env_bool("CML_WGRAD3X3", True),
             own_wgrad3x3_s2=_env_bool("CML_WGRAD3X3_S2", True),
             own_conv3x3_s2=_env_bool("CML_CONV3X3_S2", True),
+            side_wgrad=_env_bool("CML_SIDE_WGRAD", False),
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),
             flash_attn=_env_bool("CML_FLASH_ATTN", True),
             multi_copy=_env_bool("CML_MULTI_COPY", True),

@@ -1,0 +1,52 @@
+"""PerfPolicy.side_wgrad: the 3x3 weight gradients of the BN-fused 3x3 convs run on a second HIP
+stream, concurrent with the same conv's data-gradient and BN-backward kernels. The kernels are the
+same (all deterministic, fixed-order folds), so the backward must be bit-identical to the
+single-stream one, also when the side stream's blocks are reused by the allocator on the next
+call; the current stream waits for the side stream before the backward returns."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+# (the 128-channel stride-2 weight gradient runs on MIOpen, whose weight-gradient kernels are not
+# bitwise reproducible run to run: not a case here)
+@pytest.mark.parametrize("N,C,H,stride", [(16, 64, 56, 1), (16, 128, 28, 1), (8, 256, 14, 1),
+                                          (8, 256, 28, 2), (8, 512, 14, 2)])
+def test_side_wgrad_bit_identical(cuda, N, C, H, stride):
+    from consensusml_amd import perf
+    from consensusml_amd.ops import conv as fconv
+    fn = fconv._BNReLUConv3x3BNStatsFn if stride == 1 else fconv._BNReLUConv3x3S2BNStatsFn
+    g0 = torch.Generator(device=cuda).manual_seed(C + H)
+    z1 = _nhwc(torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16())
+    g1 = (torch.rand(C, device=cuda, generator=g0) + 0.5).bfloat16()
+    b1 = (torch.randn(C, device=cuda, generator=g0) * 0.1).bfloat16()
+    zf = z1.float()
+    mean1 = zf.mean((0, 2, 3))
+    invstd1 = (zf.var((0, 2, 3), unbiased=False) + 1e-5).rsqrt()
+    w = (torch.randn(C, C, 3, 3, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
+    Ho = H // stride
+    gz = _nhwc(torch.randn(N, C, Ho, Ho, device=cuda, generator=g0).bfloat16())
+    out = {}
+    for side in (False, True, False):
+        with perf.use_policy(perf.policy().replace(side_wgrad=side)):
+            res = []
+            for _ in range(2):   # the second call reuses the side stream's freed blocks
+                zi, gi, bi, wi = (t.clone().requires_grad_(True) for t in (z1, g1, b1, w))
+                rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+                z2, _, _ = fn.apply(zi, gi, bi, mean1, invstd1, 1e-5, wi, rm, rv, 1e-5, 0.1)
+                z2.backward(gz)
+                res.append([t.grad.clone() for t in (zi, gi, bi, wi)] + [z2.detach().clone()])
+        torch.cuda.synchronize()
+        out.setdefault(side, []).append(res)
+    ref = out[False][0][0]
+    for runs in (out[False], out[True]):
+        for res in runs:
+            for call in res:
+                for a, b in zip(call, ref):
+                    assert torch.equal(a, b)
+
