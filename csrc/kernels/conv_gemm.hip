@@ -391,9 +391,17 @@ int use_gemm2(int64_t M, int N, int C, int taps, int stride) {
     const char* e = getenv("CML_CONV_GEMM2");
     return !e || e[0] != '0';
   }();
-  if (!on || taps != 9 || stride != 1) return 0;
+  // CML_GEMM2_S2=0: the stride-2 forwards stay on conv_gemm.hip (A/B)
+  static const bool s2 = [] {
+    const char* e = getenv("CML_GEMM2_S2");
+    return !e || e[0] != '0';
+  }();
+  if (!on || taps != 9 || (stride != 1 && !(stride == 2 && s2))) return 0;
   const int tm = gemm_conv_tm(M, N, C);
   if (tm == 512) return 512;
+  // (stride 2 on the square tile measured no faster than conv_gemm.hip's 256 x 256: 529.7 vs
+  // 528.4 us for the layer-3 / 4 forwards, profiles/r05_47/: the tall tile only)
+  if (stride == 2) return 0;
   int BM = 0, BN = 0;
   return tm == 256 && pick_variant(M, N, &BM, &BN) == 4 ? 256 : 0;
 }
@@ -507,6 +515,9 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
     g.C = C;
     g.H = OH;
     g.W = OW;
+    g.s2 = stride == 2 ? 1 : 0;
+    g.IH = H;
+    g.IW = W;
     g.part = part;
     g.shift = shift;
     hipError_t e = launch_gemm_conv(g, part ? EP_CONV_ST : EP_STORE, st);

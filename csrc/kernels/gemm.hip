@@ -83,7 +83,7 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8_t a, bf16x8_t b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-template <int EP, bool CONV, int TM = 256>
+template <int EP, bool CONV, int TM = 256, bool S2 = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   using T = Tile<TM>;
   constexpr int TN = T::TN;
@@ -112,9 +112,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
     for (int j = 0; j < NJ; ++j) {
       const int m = m0 + 64 * j + 8 * wave + lrow;
       const int img = m / HW, rem = m - img * HW;
-      pbase[j] = img * HW;
+      pbase[j] = S2 ? img * (a.IH * a.IW) : img * HW;
       poh[j] = rem / a.W;
       pow_[j] = rem - poh[j] * a.W;
+      if constexpr (S2) {   // the input pixel of tap (1, 1), (2 oh, 2 ow)
+        poh[j] *= 2;
+        pow_[j] *= 2;
+      }
     }
   }
   auto stage = [&](int u, int kt, int buf) {
@@ -136,9 +140,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
         const int cs = a.C >> 6, tap = kt / cs, cc = kt - tap * cs;
         const int j = 2 * s + (u == 3 ? 1 : 0);
         const int ih = poh[j] + tap / 3 - 1, iw = pow_[j] + (tap - 3 * (tap / 3)) - 1;
-        const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(a.H) &&
-                        static_cast<unsigned>(iw) < static_cast<unsigned>(a.W);
-        src = ok ? a.a + (static_cast<int64_t>(pbase[j]) + ih * a.W + iw) * a.C + cc * kBK + 8 * c
+        const int IH = S2 ? a.IH : a.H, IW = S2 ? a.IW : a.W;
+        const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(IH) &&
+                        static_cast<unsigned>(iw) < static_cast<unsigned>(IW);
+        src = ok ? a.a + (static_cast<int64_t>(pbase[j]) + ih * IW + iw) * a.C + cc * kBK + 8 * c
                  : a.zero;
       } else {
         src = isA ? a.a + static_cast<int64_t>(m0 + row) * a.lda + kofs + 8 * c
@@ -452,13 +457,20 @@ template <int TM>
 hipError_t launch_tm(const GemmArgs& a, int ep, hipStream_t st) {
   using T = Tile<TM>;
   const int tiles = static_cast<int>((a.M / TM) * (a.N / T::TN));
-#define CML_GEMM(E, CV)                                                                      \
+#define CML_GEMM_S(E, CV, S)                                                                 \
   do {                                                                                       \
-    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<E, CV, TM>),            \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_nt_kernel<E, CV, TM, S>),         \
                         hipFuncAttributeMaxDynamicSharedMemorySize, T::Lds);                 \
-    gemm_nt_kernel<E, CV, TM><<<tiles, kThreads, T::Lds, st>>>(a);                           \
+    gemm_nt_kernel<E, CV, TM, S><<<tiles, kThreads, T::Lds, st>>>(a);                        \
   } while (0)
-  if (a.conv) {
+#define CML_GEMM(E, CV) CML_GEMM_S(E, CV, false)
+  if (a.conv && a.s2) {   // stride-2 forward: plain or with the BN statistics
+    switch (ep) {
+      case EP_STORE: CML_GEMM_S(EP_STORE, true, true); break;
+      case EP_CONV_ST: CML_GEMM_S(EP_CONV_ST, true, true); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else if (a.conv) {
     switch (ep) {
       case EP_STORE: CML_GEMM(EP_STORE, true); break;
       case EP_CONV_ST: CML_GEMM(EP_CONV_ST, true); break;
@@ -478,6 +490,7 @@ hipError_t launch_tm(const GemmArgs& a, int ep, hipStream_t st) {
     }
   }
 #undef CML_GEMM
+#undef CML_GEMM_S
   return hipGetLastError();
 }
 
@@ -528,6 +541,11 @@ hipError_t launch_gemm_conv(const GemmArgs& a0, int ep, hipStream_t st) {
   const int tm = gemm_conv_tm(a.M, static_cast<int>(a.N), a.C);
   if (!tm || !a.zero || !a.a || !a.b || !a.y) return hipErrorInvalidValue;
   if (static_cast<int64_t>(a.H) * a.W < 1 || a.M % (static_cast<int64_t>(a.H) * a.W))
+    return hipErrorInvalidValue;
+  // stride 2: the output grid must be the input's ((IH - 1) / 2 + 1) x ((IW - 1) / 2 + 1)
+  if (a.s2 && (a.IH < 1 || a.IW < 1 || (a.IH - 1) / 2 + 1 != a.H || (a.IW - 1) / 2 + 1 != a.W ||
+               static_cast<int64_t>(a.M / (static_cast<int64_t>(a.H) * a.W)) * a.IH * a.IW >=
+                   (1LL << 31) || ep == EP_CONV_BB))
     return hipErrorInvalidValue;
   if ((ep == EP_CONV_ST || ep == EP_CONV_BB) && !a.part) return hipErrorInvalidValue;
   if (ep == EP_CONV_BB && (!a.sz || !a.ep_sc || !a.ep_bi)) return hipErrorInvalidValue;

@@ -580,7 +580,8 @@ struct GemmArgs {
   // part[(ntile R + WMR mtile + wave row)][2][TN], R = WMR M / TM (gemm_conv_tm; WMR = TM / 128,
   // TN = 65536 / TM; the square tile: R = 2 M / 256, TN = 256); EP_CONV_BB: instead the sums of
   // the BN + ReLU backward that y feeds (z = sz [M][N], ReLU bit z ep_sc + ep_bi > 0, shift = mean)
-  int conv, C, H, W;
+  int conv, C, H, W;       // H, W: the output grid
+  int s2, IH, IW;         // conv: stride 2 with an IH x IW input grid (s2 = 1), else unused
   const uint16_t* zero;
   const float* shift;
   const uint16_t* sz;

@@ -118,3 +118,32 @@ def test_gemm_conv_deterministic(cuda, N, C, Co, H):
     a = _lib().conv_gemm(x, w, 9)
     b = _lib().conv_gemm(x, w, 9)
     assert torch.equal(a, b)
+
+
+# stride-2 forwards on gemm.hip's gather (input grid IH x IW, output ((IH - 1) / 2 + 1)^2): the
+# tall tile takes the 128-channel one (672 x 28 x 28 outputs); the 256-channel shape stays on
+# conv_gemm.hip (the square tile was no faster there) and checks that route too
+S2_SHAPES = [(672, 128, 128, 56), (768, 128, 256, 28)]
+
+
+@pytest.mark.parametrize("N,C,Co,H", S2_SHAPES)
+def test_gemm_conv_stride2_forward_and_stats(cuda, N, C, Co, H):
+    g0 = torch.Generator(device=cuda).manual_seed(35)
+    x = _nhwc((torch.randn(N, C, H, H, device=cuda, generator=g0) + 0.25).bfloat16())
+    w = (torch.randn(Co, C, 3, 3, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
+    wf = w.permute(0, 2, 3, 1).reshape(Co, 9 * C).contiguous()
+    Ho = (H - 1) // 2 + 1
+    zero = torch.zeros(256, device=cuda, dtype=torch.bfloat16)
+    y = _lib().conv_gemm(x, wf, 9, zero, 2)
+    ref = F.conv2d(x.float(), w.float(), stride=2, padding=1)
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 5e-3
+    err = (y.float() - ref).abs().amax(1)   # the padded top row / left column too
+    assert float(err[:, 0, :].max()) < 8 * float(err[:, Ho // 2, :].max()) + 1e-2
+    rm, rv = torch.zeros(Co, device=cuda), torch.ones(Co, device=cuda)
+    y2, mean, invstd = _lib().conv_gemm_bn(x, wf, 9, zero, rm, rm, rv, 1e-5, 0.1, 2)
+    assert torch.equal(y2, y)
+    yb = y.float()
+    torch.testing.assert_close(mean, yb.mean((0, 2, 3)), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(invstd, (yb.var((0, 2, 3), unbiased=False) + 1e-5).rsqrt(),
+                               rtol=1e-3, atol=1e-3)
