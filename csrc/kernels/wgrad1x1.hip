@@ -612,9 +612,9 @@ __global__ __launch_bounds__((TM / 64) * (TN / WN) * 64) void wgrad_dma_kernel(D
 
 // dW = sum over S splits (fixed order), 4 elements per thread, bf16 or fp32 out
 template <bool BF16>
-__global__ __launch_bounds__(256) void wgrad1x1_fold_kernel(const float* __restrict__ part, int S,
-                                                           int64_t n, void* __restrict__ out) {
-  const int64_t e = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
+__device__ __forceinline__ void fold_body(const float* __restrict__ part, int S, int64_t n,
+                                          void* __restrict__ out, int64_t blk) {
+  const int64_t e = (blk * 256 + threadIdx.x) * 4;
   if (e >= n) return;
   // 8 loads in flight per round (a one-load-per-iteration loop was latency-bound at ~1.7 TB/s);
   // the sum order is fixed: round by round, then split by split within a round
@@ -650,18 +650,23 @@ __global__ __launch_bounds__(256) void wgrad1x1_fold_kernel(const float* __restr
   }
 }
 
+template <bool BF16>
+__global__ __launch_bounds__(256) void wgrad1x1_fold_kernel(const float* __restrict__ part, int S,
+                                                           int64_t n, void* __restrict__ out) {
+  fold_body<BF16>(part, S, n, out, blockIdx.x);
+}
+
 // The same fold for many splits over few outputs (Gram matrices / column sums of 64-channel
 // activations: S up to 2048 over n = 64..4096, where the kernel above runs 1-16 workgroups whose
 // threads each walk all S rows, ~27 us per call). Here 16 split lanes share 64 outputs: lane sl
 // sums splits sl, sl + 16, ... (8 loads in flight; a wave reads 4 split rows x 256 contiguous B),
 // then lane 0 adds the 16 lane sums in lane order. Fixed order: deterministic.
 template <bool BF16>
-__global__ __launch_bounds__(256) void wgrad_fold_wide_kernel(const float* __restrict__ part,
-                                                              int S, int64_t n,
-                                                              void* __restrict__ out) {
+__device__ __forceinline__ void fold_wide_body(const float* __restrict__ part, int S, int64_t n,
+                                               void* __restrict__ out, int64_t blk) {
   __shared__ float4 red[16][17];
   const int cg = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const int64_t e = (static_cast<int64_t>(blockIdx.x) * 16 + cg) * 4;
+  const int64_t e = (blk * 16 + cg) * 4;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e < n) {
     int k = sl;
@@ -707,6 +712,32 @@ __global__ __launch_bounds__(256) void wgrad_fold_wide_kernel(const float* __res
   }
 }
 
+template <bool BF16>
+__global__ __launch_bounds__(256) void wgrad_fold_wide_kernel(const float* __restrict__ part,
+                                                              int S, int64_t n,
+                                                              void* __restrict__ out) {
+  fold_wide_body<BF16>(part, S, n, out, blockIdx.x);
+}
+
+// A weight gradient's two folds in one launch: blocks [0, b1) fold part -> out (dW, bf16 or fp32),
+// blocks [b1, ..) fold part2 -> out2 (the column sums, fp32); the same per-element sums as two
+// launches (the fold's fixed cost, ~5 us, is most of a column-sum fold)
+template <bool WIDE, bool BF16>
+__global__ __launch_bounds__(256) void fold_pair_kernel(const float* __restrict__ part, int64_t n,
+                                                        void* __restrict__ out,
+                                                        const float* __restrict__ part2,
+                                                        int64_t n2, float* __restrict__ out2,
+                                                        int S, int b1) {
+  const int b = blockIdx.x;
+  if (b < b1) {
+    if constexpr (WIDE) fold_wide_body<BF16>(part, S, n, out, b);
+    else fold_body<BF16>(part, S, n, out, b);
+  } else {
+    if constexpr (WIDE) fold_wide_body<false>(part2, S, n2, out2, b - b1);
+    else fold_body<false>(part2, S, n2, out2, b - b1);
+  }
+}
+
 // Splits from which the wide fold is used (CML_FOLD_WIDE_MIN, default 32; 0 disables it: A/B).
 int fold_wide_min() {
   static const int v = [] {
@@ -728,6 +759,31 @@ void fold_splits(const float* part, int S, int64_t n, void* out, bool out_bf16, 
   const int fb = static_cast<int>((n / 4 + 255) / 256);
   if (out_bf16) wgrad1x1_fold_kernel<true><<<fb, 256, 0, st>>>(part, S, n, out);
   else wgrad1x1_fold_kernel<false><<<fb, 256, 0, st>>>(part, S, n, out);
+}
+
+// dW = fold(part, n) and cs = fold(cs_part, ncs) (fp32) in one launch (cs null: dW only)
+void fold_dw_cs(const float* part, int64_t n, void* dw, bool dw_bf16, const float* cs_part,
+                int64_t ncs, float* cs, int S, hipStream_t st) {
+  if (cs == nullptr) {
+    fold_splits(part, S, n, dw, dw_bf16, st);
+    return;
+  }
+  const int wmin = fold_wide_min();
+  const bool wide = wmin > 0 && S >= wmin;
+  const int64_t b1 = wide ? (n + 63) / 64 : (n / 4 + 255) / 256;
+  const int64_t b2 = wide ? (ncs + 63) / 64 : (ncs / 4 + 255) / 256;
+#define CML_FP(W, B)                                                                            \
+  fold_pair_kernel<W, B><<<static_cast<unsigned>(b1 + b2), 256, 0, st>>>(part, n, dw, cs_part, \
+                                                                        ncs, cs, S,            \
+                                                                        static_cast<int>(b1))
+  if (wide) {
+    if (dw_bf16) CML_FP(true, true);
+    else CML_FP(true, false);
+  } else {
+    if (dw_bf16) CML_FP(false, true);
+    else CML_FP(false, false);
+  }
+#undef CML_FP
 }
 
 }  // namespace
@@ -997,8 +1053,7 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
     else e = launch_dma_tile(TM, TN, false, da, P, S, cps, st);
     if (e != hipSuccess) return e;
     if (direct) return hipGetLastError();
-    if (cs) fold_splits(cs_part, S, Co, cs, false, st);
-    fold_splits(part, S, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, st);
+    fold_dw_cs(part, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, cs_part, Co, cs, S, st);
     return hipGetLastError();
   }
   if (part == nullptr) return hipErrorInvalidValue;
@@ -1033,8 +1088,7 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
   }
 #undef CML_WG_TILE
   if (!ok) return hipErrorInvalidValue;
-  if (cs) fold_splits(cs_part, S, Co, cs, false, st);
-  fold_splits(part, S, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, st);
+  fold_dw_cs(part, static_cast<int64_t>(Co) * Ci, dw, dw_bf16, cs_part, Co, cs, S, st);
   return hipGetLastError();
 }
 
