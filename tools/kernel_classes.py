@@ -15,7 +15,7 @@ CLASSES = [
     ("recompute-tail algebra (tail_prep.hip, bn_stats_gram)", r"cml::.*(tail_|bn_stats_gram)"),
     ("1x1 weight gradient (wgrad1x1.hip)", r"cml::.*(wgrad1x1|wgrad_dma_kernel|wgrad_fold)"),
     ("3x3 conv fwd + data gradient (conv_gemm.hip, gemm.hip conv mode, conv3x3p.hip)",
-     r"cml::.*(conv_gemm|gemm_nt_kernel<\d, true(, \d+)?>|conv3x3p)"),
+     r"cml::.*(conv_gemm|gemm_nt_kernel<\d, true(, \d+(, (true|false))?)?>|conv3x3p)"),
     ("own GEMM (gemm.hip: 1x1 convs as GEMMs, transformer linears)", r"cml::.*gemm_nt_kernel"),
     ("stem / pool (stem_conv.hip, pool.hip)", r"cml::.*(stem_|maxpool|bn_relu_max)"),
     ("aggregation + optimizer (agg_update, gram, weights)", r"cml::.*(agg_|gram|robust_weights|weights_kernel|fault)"),
