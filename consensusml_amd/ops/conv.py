@@ -787,10 +787,14 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
         wr = ctx.wr   # rotated / transposed layout, made by the forward
         dw, h = _wgrad_fork(_wgrad3x3, dz2, y1, w) if ctx.needs_input_grad[6] else (None, None)
         sc, bi = _affine(g1, b1, mean1, invstd1)
+        # bn1's parameter gradients come out of the sums' finalize launch (no bn_bwd_coeffs)
+        own_dgb = g1.dtype == torch.bfloat16 and b1.dtype == torch.bfloat16
+        dg1, db1 = (torch.empty_like(g1), torch.empty_like(b1)) if own_dgb else (None, None)
         dy1, s1, q1 = L.conv_gemm_bnsums(dz2, wr, 9, _zero_row(dz2.device), z1, sc, bi, mean1,
-                                         invstd1)
-        M = z1.numel() // z1.shape[1]
-        _, _, _, dg1, db1 = L.bn_bwd_coeffs(s1, q1, g1, mean1, invstd1, M)
+                                         invstd1, dg1, db1)
+        if not own_dgb:
+            M = z1.numel() // z1.shape[1]
+            _, _, _, dg1, db1 = L.bn_bwd_coeffs(s1, q1, g1, mean1, invstd1, M)
         dz1 = L.bn_bwd_apply(dy1, z1, g1, b1, mean1, invstd1, s1, q1)
         dw = _wgrad_join(dw, h)
         return dz1, dg1, db1, None, None, None, dw, None, None, None, None

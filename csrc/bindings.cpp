@@ -1429,7 +1429,9 @@ std::vector<Tensor> conv3x3_wlayouts(const Tensor& w, bool want_wf) {
 
 std::vector<Tensor> conv_gemm_bnsums(const Tensor& x, const Tensor& w, int64_t taps,
                                      const Tensor& zero, const Tensor& z, const Tensor& sc,
-                                     const Tensor& bi, const Tensor& mean, const Tensor& invstd) {
+                                     const Tensor& bi, const Tensor& mean, const Tensor& invstd,
+                                     const optional<Tensor>& dgamma_out,
+                                     const optional<Tensor>& dbeta_out) {
   check_nhwc(x, "x");
   check_nhwc(z, "z");
   TORCH_CHECK(x.dim() == 4, "conv_gemm_bnsums: 4-D NHWC input");
@@ -1448,6 +1450,22 @@ std::vector<Tensor> conv_gemm_bnsums(const Tensor& x, const Tensor& w, int64_t t
   Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor part = at::empty({static_cast<int64_t>(cml::conv_gemm_part_floats(M, static_cast<int>(Co)))}, f32);
   Tensor sdz = at::empty({Co}, f32), sdzx = at::empty({Co}, f32);
+  // optional: the BN's parameter gradients bf16(sdzx) / bf16(sdz) from the same finalize launch
+  void* dg = nullptr;
+  void* db = nullptr;
+  const bool want_dg = dgamma_out.has_value() && dgamma_out->defined();
+  TORCH_CHECK(want_dg == (dbeta_out.has_value() && dbeta_out->defined()),
+              "conv_gemm_bnsums: dgamma_out and dbeta_out together");
+  if (want_dg) {
+    for (const Tensor* t : {&*dgamma_out, &*dbeta_out}) {
+      check_dev(*t, "dgamma_out / dbeta_out");
+      TORCH_CHECK(t->device() == x.device() && t->scalar_type() == at::kBFloat16 &&
+                      t->is_contiguous() && t->numel() == Co,
+                  "conv_gemm_bnsums: dgamma_out / dbeta_out must be contiguous bf16 [Cout]");
+    }
+    dg = dgamma_out->data_ptr();
+    db = dbeta_out->data_ptr();
+  }
   CML_CHECK_HIP(cml::launch_conv_gemm_bnsums(
       x.data_ptr(), w.data_ptr(), y.data_ptr(), zero.data_ptr(), static_cast<int>(N),
       static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(Co),
@@ -1455,7 +1473,7 @@ std::vector<Tensor> conv_gemm_bnsums(const Tensor& x, const Tensor& w, int64_t t
       opt_ptr<const float>(bi, at::kFloat, "bi", Co),
       opt_ptr<const float>(mean, at::kFloat, "mean", Co),
       opt_ptr<const float>(invstd, at::kFloat, "invstd", Co), part.data_ptr<float>(),
-      sdz.data_ptr<float>(), sdzx.data_ptr<float>(), cur_stream()));
+      sdz.data_ptr<float>(), sdzx.data_ptr<float>(), cur_stream(), dg, db));
   return {y, sdz, sdzx};
 }
 
@@ -2459,8 +2477,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return cml::wgrad3x3_direct_plan(static_cast<int>(B), static_cast<int>(H), static_cast<int>(W),
                                      static_cast<int>(Co), static_cast<int>(Ci), &S, &T);
   }, "whether wgrad3x3 takes the nine-tap kernel for this shape");
-  m.def("conv_gemm_bnsums", &conv_gemm_bnsums,
-        "stride-1 conv_gemm + the sums of the BN + ReLU backward its output feeds");
+  m.def("conv_gemm_bnsums", &conv_gemm_bnsums, py::arg("x"), py::arg("w"), py::arg("taps"),
+        py::arg("zero"), py::arg("z"), py::arg("sc"), py::arg("bi"), py::arg("mean"),
+        py::arg("invstd"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
+        "stride-1 conv_gemm + the sums of the BN + ReLU backward its output feeds (+ optionally "
+        "that BN's parameter gradients)");
   m.def("conv_gemm_s2dgrad", &conv_gemm_s2dgrad, py::arg("dy"), py::arg("wr"), py::arg("zero"),
         py::arg("z") = py::none(), py::arg("sc") = py::none(), py::arg("bi") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(),

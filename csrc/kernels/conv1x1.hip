@@ -406,7 +406,8 @@ __global__ __launch_bounds__(256) void part_fold_kernel(const float* __restrict_
 // order as the statistics finalize).
 __global__ __launch_bounds__(256) void conv1x1_bnbwd_finalize_kernel(
     const float* __restrict__ part, int R, int BN, int N, const float* __restrict__ invstd,
-    float* __restrict__ sdz, float* __restrict__ sdzx) {
+    float* __restrict__ sdz, float* __restrict__ sdzx, uint16_t* __restrict__ dgamma,
+    uint16_t* __restrict__ dbeta) {
   __shared__ double ls[32][8], lq[32][8];
   const int cl = threadIdx.x & 7, sl = threadIdx.x >> 3;
   const int c = blockIdx.x * 8 + cl;
@@ -430,8 +431,13 @@ __global__ __launch_bounds__(256) void conv1x1_bnbwd_finalize_kernel(
     S += ls[k][cl];
     Q += lq[k][cl];
   }
-  sdz[c] = static_cast<float>(S);
-  sdzx[c] = static_cast<float>(Q * static_cast<double>(invstd[c]));
+  const float fs = static_cast<float>(S), fq = static_cast<float>(Q * static_cast<double>(invstd[c]));
+  sdz[c] = fs;
+  sdzx[c] = fq;
+  if (dgamma) {   // the BN's parameter gradients, as bn_bwd_coeffs_kernel rounds them
+    dgamma[c] = f2bf(fq);
+    dbeta[c] = f2bf(fs);
+  }
 }
 
 // BN training statistics of z = y W^T (W [Co][P] bf16: the 1x1 conv's weights) from the Gram matrix
@@ -753,7 +759,9 @@ hipError_t launch_bn_stats_finalize(const float* part, int R, int BN, int N, int
 // BN + ReLU backward sums {sdz, sdzx} from a GEMM's partial slab [ntn][R][2][BN] (tall slabs folded
 // first, as launch_bn_stats_finalize does)
 hipError_t launch_bnbwd_sums_finalize(const float* part, int R, int BN, int N, const float* invstd,
-                                      float* sdz, float* sdzx, hipStream_t st, float* fold) {
+                                      float* sdz, float* sdzx, hipStream_t st, float* fold,
+                                      void* dgamma, void* dbeta) {
+  if ((dgamma == nullptr) != (dbeta == nullptr)) return hipErrorInvalidValue;
   const int S = fold ? bn_part_fold_slices(R, N / BN) : 0;
   if (S > 0) {
     const int rp = (R + S - 1) / S;
@@ -762,7 +770,9 @@ hipError_t launch_bnbwd_sums_finalize(const float* part, int R, int BN, int N, c
     part = fold;
     R = S2;
   }
-  conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, R, BN, N, invstd, sdz, sdzx);
+  conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(
+      part, R, BN, N, invstd, sdz, sdzx, reinterpret_cast<uint16_t*>(dgamma),
+      reinterpret_cast<uint16_t*>(dbeta));
   return hipGetLastError();
 }
 
@@ -814,7 +824,7 @@ hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void
   hipError_t e = launch_bwd(a, p, sums ? 2 : 1, st);
   if (e != hipSuccess || !sums) return e;
   conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N,
-                                                             invstd, sdz, sdzx);
+                                                             invstd, sdz, sdzx, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -922,7 +932,7 @@ hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2
   hipError_t e = launch_tail(a, p, true, st);
   if (e != hipSuccess || !sums) return e;
   conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N,
-                                                             invstd, sdz, sdzx);
+                                                             invstd, sdz, sdzx, nullptr, nullptr);
   return hipGetLastError();
 }
 

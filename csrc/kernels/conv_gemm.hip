@@ -539,7 +539,7 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
                                    int Nimg, int H, int W, int C, int N, int taps, const void* z,
                                    const float* sc, const float* bi, const float* mean,
                                    const float* invstd, float* part, float* sdz, float* sdzx,
-                                   hipStream_t st) {
+                                   hipStream_t st, void* dgamma, void* dbeta) {
   const int64_t M = static_cast<int64_t>(Nimg) * H * W;
   if (C % kBK || N % 64 || (taps != 1 && taps != 9) || M < 1 || M >= (1ll << 31) ||
       static_cast<int64_t>(taps) * C > 65536 || !z || !sc || !bi || !mean || !invstd || !part ||
@@ -570,7 +570,8 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
     int R = 0;
     hipError_t e = launch_conv3x3p(x, w, y, zero, Nimg, H, 2, part, mean, z, sc, bi, st, &R);
     if (e != hipSuccess) return e;
-    return launch_bnbwd_sums_finalize(part, R, 64, 64, invstd, sdz, sdzx, st, nullptr);
+    return launch_bnbwd_sums_finalize(part, R, 64, 64, invstd, sdz, sdzx, st, nullptr, dgamma,
+                                      dbeta);
   }
   if (const int tm = use_gemm2(M, N, C, taps, 1)) {
     GemmArgs g{};
@@ -592,7 +593,8 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
     if (e != hipSuccess) return e;
     const int tn = 65536 / tm, R = static_cast<int>(M / tm) * (tm / 128);
     return launch_bnbwd_sums_finalize(part, R, tn, N, invstd, sdz, sdzx, st,
-                                      part + static_cast<size_t>(N / tn) * R * 2 * tn);
+                                      part + static_cast<size_t>(N / tn) * R * 2 * tn, dgamma,
+                                      dbeta);
   }
   hipError_t e = taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
   if (e != hipSuccess) return e;
@@ -600,7 +602,7 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
   tile_of(M, N, &BM, &BN);
   const int R = static_cast<int>((M + BM - 1) / BM) * (BM / 64);
   return launch_bnbwd_sums_finalize(part, R, BN, N, invstd, sdz, sdzx, st,
-                                    part + static_cast<size_t>(N / BN) * R * 2 * BN);
+                                    part + static_cast<size_t>(N / BN) * R * 2 * BN, dgamma, dbeta);
 }
 
 namespace {

@@ -432,9 +432,12 @@ hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const 
                                    int Nimg, int H, int W, int C, int N, int taps, const void* z,
                                    const float* sc, const float* bi, const float* mean,
                                    const float* invstd, float* part, float* sdz, float* sdzx,
-                                   hipStream_t st);
+                                   hipStream_t st, void* dgamma = nullptr, void* dbeta = nullptr);
+// dgamma / dbeta (bf16 [N], both or neither): also bf16(sdzx) / bf16(sdz), the BN's parameter
+// gradients (bn_bwd_coeffs' values), written by the same finalize launch
 hipError_t launch_bnbwd_sums_finalize(const float* part, int R, int BN, int N, const float* invstd,
-                                      float* sdz, float* sdzx, hipStream_t st, float* fold);
+                                      float* sdz, float* sdzx, hipStream_t st, float* fold,
+                                      void* dgamma = nullptr, void* dbeta = nullptr);
 // Data gradient dx [Nimg][2 Ho][2 Wo][Ci] of a stride-2 / padding-1 3x3 conv (even input) from dy
 // [Nimg][Ho][Wo][Co] and wr [Ci][9 Co] (launch_conv3x3_wlayouts), as four output-parity-class
 // implicit GEMMs of 4 / 2 / 2 / 1 taps. With z non-null also the sums of the BN + ReLU backward

@@ -147,3 +147,26 @@ def test_gemm_conv_stride2_forward_and_stats(cuda, N, C, Co, H):
     torch.testing.assert_close(mean, yb.mean((0, 2, 3)), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(invstd, (yb.var((0, 2, 3), unbiased=False) + 1e-5).rsqrt(),
                                rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("N,C,Co,H", [(4, 256, 256, 16), (16, 64, 128, 28)])
+def test_gemm_conv_bnsums_dgamma_dbeta(cuda, N, C, Co, H):
+    """The BN parameter gradients from the sums' finalize launch equal bn_bwd_coeffs' values."""
+    g0 = torch.Generator(device=cuda).manual_seed(36)
+    x = _nhwc(torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16())
+    z = _nhwc(torch.randn(N, Co, H, H, device=cuda, generator=g0).bfloat16())
+    w = (torch.randn(Co, 9 * C, device=cuda, generator=g0) * (9 * C) ** -0.5).bfloat16()
+    zero = torch.zeros(64, device=cuda, dtype=torch.bfloat16)
+    gam = (torch.rand(Co, device=cuda, generator=g0) + 0.5).bfloat16()
+    bet = (torch.randn(Co, device=cuda, generator=g0) * 0.1).bfloat16()
+    Z = _rows(z).double()
+    mean = Z.mean(0).float()
+    invstd = (Z.var(0, unbiased=False) + 1e-5).rsqrt().float()
+    sc = gam.float() * invstd
+    bi = bet.float() - mean * sc
+    dg, db = torch.empty_like(gam), torch.empty_like(bet)
+    y, s, q = _lib().conv_gemm_bnsums(x, w, 9, zero, z, sc, bi, mean, invstd, dg, db)
+    y2, s2, q2 = _lib().conv_gemm_bnsums(x, w, 9, zero, z, sc, bi, mean, invstd)
+    assert torch.equal(y, y2) and torch.equal(s, s2) and torch.equal(q, q2)
+    _, _, _, dg_ref, db_ref = _lib().bn_bwd_coeffs(s, q, gam, mean, invstd, N * H * H)
+    assert torch.equal(dg, dg_ref) and torch.equal(db, db_ref)
