@@ -2329,6 +2329,65 @@ int64_t gemm_conv_tm(int64_t M, int64_t N, int64_t C) {
 }
 
 // column sums of x viewed as [M, N] (N = last dim) -> bf16 [N]
+// Dense GEMM on gemm_w4.hip (4 waves x 128 x 128 per 256 x 256 tile, every operand layout):
+// y [M, N] = A B^T (+ bias[N]) (+ cin), A(m, k) = a[m][k] (mode bit 0 clear) or a[k][m] (set),
+// B(n, k) = b[n][k] (bit 1 clear) or b[k][n] (set). So a linear layer's three products run
+// without a transpose: forward gemm_w4(x, W, 0), data gradient gemm_w4(dy, W, 2), weight
+// gradient gemm_w4(dy, x, 3). K % 64 == 0, M, N multiples of 8.
+Tensor gemm_w4(const Tensor& a, const Tensor& b, int64_t mode, const optional<Tensor>& out,
+               const optional<Tensor>& bias, const optional<Tensor>& cin) {
+  check_dev(a, "a");
+  check_dev(b, "b");
+  TORCH_CHECK(mode >= 0 && mode < 4, "gemm_w4: mode 0..3");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm_w4: bf16");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1,
+              "gemm_w4: 2-D operands with unit column stride");
+  TORCH_CHECK(b.get_device() == a.get_device(), "gemm_w4: b must be on a's device");
+  const bool at_ = mode & 1, bt_ = mode & 2;
+  const int64_t M = at_ ? a.size(1) : a.size(0), K = at_ ? a.size(0) : a.size(1);
+  const int64_t N = bt_ ? b.size(1) : b.size(0), Kb = bt_ ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm_w4: K mismatch (", K, " vs ", Kb, ")");
+  TORCH_CHECK(cml::gemm_w4_eligible(M, N, K, static_cast<int>(mode)),
+              "gemm_w4: needs K % 64 == 0 and M, N multiples of 8 (M ", M, ", N ", N, ", K ", K, ")");
+  auto aligned = [](const Tensor& t, int bytes) {
+    return (reinterpret_cast<uintptr_t>(t.data_ptr()) % bytes) == 0;
+  };
+  TORCH_CHECK(aligned(a, 16) && aligned(b, 16) && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0,
+              "gemm_w4: a / b need 16-B aligned rows");
+  const c10::DeviceGuard guard(a.device());
+  Tensor y;
+  if (out.has_value() && out->defined()) {
+    y = *out;
+    TORCH_CHECK(y.is_cuda() && y.get_device() == a.get_device(), "gemm_w4: out must be on a's device");
+    TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 2 && y.size(0) == M &&
+                y.size(1) == N && y.stride(1) == 1 && aligned(y, 16) && y.stride(0) % 8 == 0,
+                "gemm_w4: out must be bf16 [M, N] with 16-B aligned rows");
+  } else {
+    y = at::empty({M, N}, a.options());
+  }
+  cml::GemmArgs g{};
+  g.a = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  g.b = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  g.y = reinterpret_cast<uint16_t*>(y.data_ptr());
+  g.M = M; g.N = N; g.K = K;
+  g.lda = a.stride(0); g.ldb = b.stride(0); g.ldy = y.stride(0);
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->is_cuda() && bias->get_device() == a.get_device() && aligned(*bias, 8),
+                "gemm_w4: bias must be on a's device, 8-B aligned");
+    g.bias = opt_ptr<const uint16_t>(bias, at::kBFloat16, "bias", N);
+  }
+  if (cin.has_value() && cin->defined()) {
+    TORCH_CHECK(cin->is_cuda() && cin->get_device() == a.get_device(), "gemm_w4: cin device");
+    TORCH_CHECK(cin->scalar_type() == at::kBFloat16 && cin->dim() == 2 && cin->size(0) == M &&
+                cin->size(1) == N && cin->stride(1) == 1 && cin->stride(0) == y.stride(0) &&
+                aligned(*cin, 16),
+                "gemm_w4: cin must be bf16 [M, N] with out's row stride");
+    g.cin = reinterpret_cast<const uint16_t*>(cin->data_ptr());
+  }
+  CML_CHECK_HIP(cml::launch_gemm_w4(g, static_cast<int>(mode), cur_stream()));
+  return y;
+}
+
 Tensor colsum(const Tensor& x_in) {
   Tensor x = x_in.contiguous();
   check_bf16c(x, "x");
@@ -2571,6 +2630,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "column sums)", py::arg("a"), py::arg("b"), py::arg("ep"), py::arg("bias") = py::none(),
         py::arg("aux") = py::none(), py::arg("out") = py::none(),
         py::arg("colsum_out") = py::none(), py::arg("cin") = py::none(), py::arg("tile") = 0);
+  m.def("gemm_w4", &gemm_w4, "GEMM on 4-wave 256 x 256 tiles, any operand layout (mode bit 0: a is "
+        "[K, M], bit 1: b is [K, N])", py::arg("a"), py::arg("b"), py::arg("mode") = 0,
+        py::arg("out") = py::none(), py::arg("bias") = py::none(), py::arg("cin") = py::none());
   m.def("gemm_nt_ok", &gemm_nt_ok, "shape eligibility of gemm_nt's 256 x 256 kernel");
   m.def("gemm_conv_tm", &gemm_conv_tm, "m-tile of gemm.hip's 3x3 conv mode for M x N, C (256, 512, 0)");
   m.def("gemm_nt_pick", &gemm_nt_pick, "EP_STORE tile choice of gemm_nt: 256, 128 or 0 (none)");

@@ -1,0 +1,392 @@
+// Dense bf16 GEMM, one 256 x 256 output tile per 4-wave workgroup, every operand layout
+// (gfx950 / CDNA4):
+//
+//   y[m][n] = bf16( sum_k A(m, k) B(n, k) + bias[n] ) [+ cin[m][n]]
+//
+//   operand layouts (template AT / BT):  A(m, k) = a[m][k] (AT = 0, "k-contiguous") or a[k][m]
+//   (AT = 1, "k-major"); B(n, k) = b[n][k] (BT = 0) or b[k][n] (BT = 1). So one kernel runs every
+//   product of a linear layer without materialising a transpose:
+//     forward      y  = x W^T      A = x  [M][K],   B = W  [N][K]       (AT 0, BT 0)
+//     data grad    dx = dy W       A = dy [M][N],   B = W  [N][K] as k-major   (AT 0, BT 1)
+//     weight grad  dW = dy^T x     A = dy [T][N] k-major, B = x [T][K] k-major (AT 1, BT 1)
+//
+// Why a second GEMM next to gemm.hip (8 waves, 128 x 64 per wave): a wave here owns a 128 x 128
+// block, so per MFMA it reads half the LDS bytes of gemm.hip's waves (every 16 x 16 x 32 product
+// needs 1/8 of an A fragment + 1/8 of a B fragment instead of 1/8 + 1/4), and the accumulators
+// (64 x f32x4 = 256 registers) live in the AGPR half of the 512-register file at one wave per
+// SIMD. Fewer LDS reads per FLOP is what lets the chip hold its clock on random data (DVFS:
+// cdna_hip_programming.md rule 28).
+//
+// Schedule:
+//   * K advances in 32-deep sub-stages through a 4-deep LDS ring (4 x 32 KB: A image 16 KB, B image
+//     16 KB). Step s: counted `s_waitcnt vmcnt(8)` (this wave's loads of stage s + 1 landed, those of
+//     s + 2 may fly) -> raw s_barrier (stage s + 1 visible to every wave; every wave has consumed
+//     stage s - 1) -> issue the 8 global_load_lds of stage s + 3 into stage s - 1's buffer -> issue
+//     the fragment reads of stage s + 1 -> 64 MFMAs of stage s on the fragments read one step
+//     earlier. One barrier per 64 MFMAs per wave, two steps of flight for every load, no vmcnt(0)
+//     in the loop (raw s_barrier, never __syncthreads, which would drain the LDS-DMA queue).
+//   * k-contiguous images: 256 rows x 64 B, the 16-B slot of (row r, chunk c) at 4 r + (c ^ f(r)),
+//     f(r) = (-(r >> 2)) & 3: every ds_read_b128 lane group of a fragment read touches 16 distinct
+//     bank slots. A load instruction covers 16 rows x 64 B; the swizzle lives in each lane's SOURCE
+//     address (global_load_lds writes lane-linear).
+//   * k-major images: 32 k-rows x 512 B (256 columns), 16-B unit (kr, v) holding columns
+//     8 (v ^ g(kr)), g(kr) = 2 ((kr & 3) | ((kr >> 3 & 1) << 2)); a load instruction covers two whole
+//     512-B rows (fully coalesced). Fragments come out of ds_read_b64_tr_b16 (two per fragment:
+//     k-rows 8h .. 8h + 3 and 8h + 4 .. 8h + 7), conflict-free under g.
+//   * MFMA v_mfma_f32_16x16x32_bf16 computed transposed (C^T = B A^T) so that a lane holds 4
+//     consecutive output columns of one row; the epilogue rounds them into a per-wave 32 KB LDS image
+//     (8-B slots XOR-swizzled by row) and reads it back as 16-B row pieces: whole 256-B row segments
+//     per store instruction.
+//   * tiles: XCD-aware bijective remap (consecutive ids share an XCD), then 4 m-tiles x all n-tiles
+//     groups with m fastest, so the 32 tiles an XCD runs at once are 4 (m) x 8 (n): its L2 serves
+//     each A panel to 8 tiles and each B panel to 4.
+// Requirements (launcher): K % 64 == 0; M, N multiples of 8 (ragged edges: loads clamped to the
+// last valid row / column, stores masked); 16-B aligned rows.
+#include <cstdlib>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace cml {
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void g_void;
+
+constexpr int kThr = 256;
+constexpr int kOp = 16384;          // one operand image of one stage
+constexpr int kStage = 2 * kOp;     // A + B
+constexpr int kRing = 4;
+constexpr int kLds = kRing * kStage;   // 128 KB (the epilogue images reuse it)
+constexpr int kGM = 4;              // m-tiles per tile group
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8_t a, bf16x8_t b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+__device__ __forceinline__ uint2 ds_tr16(const char* p) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p)));
+}
+
+// SCH: steady-state schedule (0: barrier, loads, 64 MFMAs; 1 / 2: see step_main). ABL (timing
+// ablations only, wrong results): bit 0 no staging in the loop, bit 1 no fragment reads, bit 2 no
+// barrier.
+template <bool AT, bool BT, int SCH = 0, int ABL = 0>
+__global__ __launch_bounds__(kThr, 1) void gemm_w4_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // ---- tile: bijective XCD remap, then groups of kGM m-tiles (m fastest)
+  const int mtn = static_cast<int>((a.M + 255) / 256), ntn = static_cast<int>((a.N + 255) / 256);
+  const int G = mtn * ntn, bid = blockIdx.x, xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int grp = t / (kGM * ntn), gi = t - grp * (kGM * ntn);
+  const int gm = min(kGM, mtn - grp * kGM);
+  const int mtile = grp * kGM + gi % gm, ntile = gi / gm;
+  const int m0 = mtile * 256, n0 = ntile * 256;
+  const int nks = static_cast<int>(a.K / 32);
+
+  // ---- staging: per stage this wave issues 4 A + 4 B instructions (i = wave + 4 j)
+  // k-contiguous operand: instruction i = rows 16 i .. 16 i + 15; lane -> row 16 i + (lane >> 2),
+  // chunk (lane & 3) ^ f(row); the pointer already includes the chunk, so stage s adds 32 s.
+  // k-major operand: instruction i = k-rows 2 i, 2 i + 1; lane -> k-row 2 i + (lane >> 5), unit
+  // lane & 31 holding columns 8 ((lane & 31) ^ g(k-row)); stage s adds 32 s rows.
+  const uint16_t* pa[4];
+  const uint16_t* pb[4];
+  {
+    const int lr = lane >> 2, lc = (lane & 3) ^ ((-(lane >> 4)) & 3);
+    const int tk = lane >> 5, tv = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = wave + 4 * j;
+      if constexpr (!AT) {
+        const int64_t row = min<int64_t>(m0 + 16 * i + lr, a.M - 1);
+        pa[j] = a.a + row * a.lda + 8 * lc;
+      } else {
+        const int kr = 2 * i + tk;
+        const int g = 2 * ((kr & 3) | (((kr >> 3) & 1) << 2));
+        const int64_t col = min<int64_t>(m0 + 8 * (tv ^ g), a.M - 8);
+        pa[j] = a.a + static_cast<int64_t>(kr) * a.lda + col;
+      }
+      if constexpr (!BT) {
+        const int64_t row = min<int64_t>(n0 + 16 * i + lr, a.N - 1);
+        pb[j] = a.b + row * a.ldb + 8 * lc;
+      } else {
+        const int kr = 2 * i + tk;
+        const int g = 2 * ((kr & 3) | (((kr >> 3) & 1) << 2));
+        const int64_t col = min<int64_t>(n0 + 8 * (tv ^ g), a.N - 8);
+        pb[j] = a.b + static_cast<int64_t>(kr) * a.ldb + col;
+      }
+    }
+  }
+  const int64_t sa = AT ? 32 * a.lda : 32;   // elements per stage
+  const int64_t sb = BT ? 32 * a.ldb : 32;
+  auto stage = [&](int s, int buf) {
+    char* da = smem + buf * kStage;
+    char* db = da + kOp;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = wave + 4 * j;
+      __builtin_amdgcn_global_load_lds((g_void*)(pa[j] + s * sa), (lds_void*)(da + i * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = wave + 4 * j;
+      __builtin_amdgcn_global_load_lds((g_void*)(pb[j] + s * sb), (lds_void*)(db + i * 1024), 16, 0, 0);
+    }
+  };
+
+  // ---- fragment reads: 8 fragments of A (rows wm 128 + 16 mt + (lane & 15)) and of B
+  // k-contiguous: row R, chunk lane >> 4 at 64 R + 16 (chunk ^ f(R)); f(R) = (-(lane >> 2 & 3)) & 3
+  const int nrd = (lane & 15) * 64 + 16 * ((lane >> 4) ^ ((-((lane >> 2) & 3)) & 3));
+  // k-major: lane 4 q + p of 16-lane group h reads k-row 8 h + q (+ 4), columns c0 + 4 p .. + 3;
+  // byte kr 512 + 16 ((c0 / 8 + (p >> 1)) ^ g) + 8 (p & 1) with g = 2 (q | (h & 1) << 2), and
+  // c0 / 8 = 16 w + 2 mt, so the unit is 16 w + 2 (mt ^ (g / 2)) + (p >> 1)
+  const int th = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int tg2 = tq | ((th & 1) << 2);
+  const int trd = (8 * th + tq) * 512 + 16 * (tp >> 1) + 8 * (tp & 1);
+  bf16x8_t fa0[8], fb0[8], fa1[8], fb1[8];
+  auto readop = [&](bf16x8_t (&f)[8], const char* img, int w, bool tr) {
+    if (!tr) {
+      const char* base = img + w * 128 * 64 + nrd;
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) f[mt] = *reinterpret_cast<const bf16x8_t*>(base + mt * 1024);
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        const char* p = img + trd + 16 * (16 * w + 2 * (mt ^ tg2));
+        const uint2 lo = ds_tr16(p), hi = ds_tr16(p + 4 * 512);
+        f[mt] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+    }
+  };
+  auto readst = [&](bf16x8_t (&fa)[8], bf16x8_t (&fb)[8], int buf) {
+    const char* img = smem + buf * kStage;
+    readop(fb, img + kOp, wn, BT);
+    readop(fa, img, wm, AT);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const bf16x8_t (&fa)[8], const bf16x8_t (&fb)[8]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) acc[mt][nt] = mfma16(fb[nt], fa[mt], acc[mt][nt]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto mma_rows = [&](const bf16x8_t (&fa)[8], const bf16x8_t (&fb)[8], int m_lo) {
+#pragma unroll
+    for (int mt = m_lo; mt < m_lo + 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt) acc[mt][nt] = mfma16(fb[nt], fa[mt], acc[mt][nt]);
+  };
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto vm8 = [] { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
+  auto vm16 = [] { asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); };
+  auto vm0 = [] { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+
+  // ---- prologue: stages 0, 1, 2 in flight; stage 0 landed and visible; its fragments read
+  stage(0, 0);
+  if (nks > 1) stage(1, 1);
+  if (nks > 2) stage(2, 2);
+  if (nks > 2) vm16();
+  else if (nks > 1) vm8();
+  else vm0();
+  bar();
+  readst(fa0, fb0, 0);
+
+  auto step = [&](int s, bf16x8_t (&fac)[8], bf16x8_t (&fbc)[8], bf16x8_t (&fan)[8],
+                  bf16x8_t (&fbn)[8]) {
+    if (s + 1 < nks) {
+      if (s + 2 < nks) vm8();
+      else vm0();
+      bar();
+      if (s + 3 < nks) stage(s + 3, (s + 3) & 3);
+      readst(fan, fbn, (s + 1) & 3);
+    }
+    mma(fac, fbc);
+  };
+  // steady-state step (s + 3 < nks): branch-free, so the loads can be interleaved with MFMAs.
+  // SCH 1 / 2: half the MFMAs before the barrier, the other half after it with the staging
+  // and fragment reads (SCH 1 interleaves them by sched_group_barrier).
+  auto step_main = [&](int s, bf16x8_t (&fac)[8], bf16x8_t (&fbc)[8], bf16x8_t (&fan)[8],
+                       bf16x8_t (&fbn)[8]) {
+    if constexpr (SCH == 0) {
+      vm8();
+      if constexpr (!(ABL & 4)) bar();
+      if constexpr (!(ABL & 1)) stage(s + 3, (s + 3) & 3);
+      if constexpr (!(ABL & 2)) readst(fan, fbn, (s + 1) & 3);
+      mma(fac, fbc);
+    } else {
+      mma_rows(fac, fbc, 0);
+      vm8();
+      bar();
+      stage(s + 3, (s + 3) & 3);
+      readst(fan, fbn, (s + 1) & 3);
+      mma_rows(fac, fbc, 4);
+      if constexpr (SCH == 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);   // VMEM (LDS-DMA)
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  int s = 0;
+  for (; s + 4 < nks; s += 2) {
+    step_main(s, fa0, fb0, fa1, fb1);
+    step_main(s + 1, fa1, fb1, fa0, fb0);
+  }
+  for (; s < nks; s += 2) {
+    step(s, fa0, fb0, fa1, fb1);
+    step(s + 1, fa1, fb1, fa0, fb0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bar();
+
+  // ---- epilogue: the wave's 128 (m) x 128 (n) block as bf16 into its own 32 KB image
+  // [m][256 B], 8-B slot (n / 4) ^ (m & 31): the ds_write_b64 of 16 rows hits 16 distinct slots
+  char* img = smem + wave * 32768;
+  const int fr = lane & 15, fc = lane >> 4;
+  const int nw = n0 + wn * 128;
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt) {
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias) {
+      const int n = min(nw + nt * 16 + 4 * fc, static_cast<int>(a.N) - 4);
+      const uint2 bv = *reinterpret_cast<const uint2*>(a.bias + n);
+      bias[0] = __uint_as_float(bv.x << 16);
+      bias[1] = __uint_as_float(bv.x & 0xffff0000u);
+      bias[2] = __uint_as_float(bv.y << 16);
+      bias[3] = __uint_as_float(bv.y & 0xffff0000u);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const f32x4 v = acc[mt][nt];
+      const uint2 w = make_uint2(pk_bf16(v[0] + bias[0], v[1] + bias[1]),
+                                 pk_bf16(v[2] + bias[2], v[3] + bias[3]));
+      const int row = mt * 16 + fr;
+      const int slot = (nt * 4 + fc) ^ (row & 31);
+      *reinterpret_cast<uint2*>(img + row * 256 + slot * 8) = w;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  // read back: lane -> row 4 it + (lane >> 4), 16-B piece k = lane & 15 (columns 8 k .. 8 k + 7)
+  const int k = lane & 15, rr = lane >> 4;
+  const int ncol = nw + 8 * k;
+  const bool nok = ncol < a.N;
+#pragma unroll 4
+  for (int it = 0; it < 32; ++it) {
+    const int row = 4 * it + rr;
+    const uint4 u = *reinterpret_cast<const uint4*>(img + row * 256 + 16 * (k ^ ((row >> 1) & 15)));
+    uint4 v = (row & 1) ? make_uint4(u.z, u.w, u.x, u.y) : u;
+    const int64_t m = m0 + wm * 128 + row;
+    if (m < a.M && nok) {
+      uint16_t* yp = a.y + m * a.ldy + ncol;
+      if (a.cin) {
+        const uint4 cv = *reinterpret_cast<const uint4*>(a.cin + m * a.ldy + ncol);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, c4[4] = {cv.x, cv.y, cv.z, cv.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[q] = pk_bf16(__uint_as_float(w4[q] << 16) + __uint_as_float(c4[q] << 16),
+                         __uint_as_float(w4[q] & 0xffff0000u) + __uint_as_float(c4[q] & 0xffff0000u));
+        v = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+      *reinterpret_cast<uint4*>(yp) = v;
+    }
+  }
+}
+
+// CML_W4_SCHED (0 / 1 / 2: the steady-state schedule, A/B) and CML_W4_ABL (timing ablations
+// of mode 0, wrong results) are read once
+int w4_sched() {
+  static const int v = [] {
+    const char* e = getenv("CML_W4_SCHED");
+    const int x = e ? atoi(e) : 0;
+    return x >= 0 && x <= 2 ? x : 0;
+  }();
+  return v;
+}
+int w4_ablate() {
+  static const int v = [] {
+    const char* e = getenv("CML_W4_ABL");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+}  // namespace
+
+bool gemm_w4_eligible(int64_t M, int64_t N, int64_t K, int mode) {
+  if (M < 8 || N < 8 || K < 64 || K % 64 || M % 8 || N % 8) return false;
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  return tiles < (1LL << 31) && (mode >= 0 && mode < 4);
+}
+
+hipError_t launch_gemm_w4(const GemmArgs& a, int mode, hipStream_t st) {
+  if (!gemm_w4_eligible(a.M, a.N, a.K, mode) || !a.a || !a.b || !a.y) return hipErrorInvalidValue;
+  const bool at = mode & 1, bt = mode & 2;
+  if ((a.lda % 8) || (a.ldb % 8) || (a.ldy % 8)) return hipErrorInvalidValue;
+  if ((at ? a.lda < a.M : a.lda < a.K) || (bt ? a.ldb < a.N : a.ldb < a.K) || a.ldy < a.N)
+    return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(a.a) | reinterpret_cast<uintptr_t>(a.b) |
+       reinterpret_cast<uintptr_t>(a.y) | reinterpret_cast<uintptr_t>(a.cin)) % 16)
+    return hipErrorInvalidValue;
+  if (a.bias && reinterpret_cast<uintptr_t>(a.bias) % 8) return hipErrorInvalidValue;
+  const int tiles = static_cast<int>(((a.M + 255) / 256) * ((a.N + 255) / 256));
+#define CML_W4(AT_, BT_, SCH_, ABL_)                                                        \
+  do {                                                                                      \
+    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_w4_kernel<AT_, BT_, SCH_, ABL_>), \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, kLds);                  \
+    gemm_w4_kernel<AT_, BT_, SCH_, ABL_><<<tiles, kThr, kLds, st>>>(a);                     \
+  } while (0)
+  const int sch = w4_sched(), abl = w4_ablate();
+  if (mode == 0 && abl) {
+    switch (abl) {
+      case 1: CML_W4(false, false, 0, 1); break;
+      case 2: CML_W4(false, false, 0, 2); break;
+      case 4: CML_W4(false, false, 0, 4); break;
+      default: CML_W4(false, false, 0, 7); break;
+    }
+    return hipGetLastError();
+  }
+  switch (mode * 4 + sch) {
+    case 0: CML_W4(false, false, 0, 0); break;
+    case 1: CML_W4(false, false, 1, 0); break;
+    case 2: CML_W4(false, false, 2, 0); break;
+    case 4: CML_W4(true, false, 0, 0); break;
+    case 5: CML_W4(true, false, 1, 0); break;
+    case 6: CML_W4(true, false, 2, 0); break;
+    case 8: CML_W4(false, true, 0, 0); break;
+    case 9: CML_W4(false, true, 1, 0); break;
+    case 10: CML_W4(false, true, 2, 0); break;
+    case 12: CML_W4(true, true, 0, 0); break;
+    case 13: CML_W4(true, true, 1, 0); break;
+    default: CML_W4(true, true, 2, 0); break;
+  }
+#undef CML_W4
+  return hipGetLastError();
+}
+
+}  // namespace cml

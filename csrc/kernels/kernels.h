@@ -605,6 +605,10 @@ bool gemm_conv_eligible(int64_t M, int N, int C);
 // EP_CONV_ST / EP_CONV_BB then have R = (M / TM) (TM / 128) rows of 2 x (65536 / TM) floats
 int gemm_conv_tm(int64_t M, int N, int C);
 hipError_t launch_gemm_conv(const GemmArgs& a, int ep, hipStream_t st);
+// 4-wave 256 x 256-tile GEMM (gemm_w4.hip), EP_STORE (bias, cin), any operand layout: mode bit 0 =
+// A stored [K][M] (lda >= M), bit 1 = B stored [K][N]; K % 64 == 0, M, N multiples of 8.
+bool gemm_w4_eligible(int64_t M, int64_t N, int64_t K, int mode);
+hipError_t launch_gemm_w4(const GemmArgs& a, int mode, hipStream_t st);
 // out[s][n] = sum of the 128-row partial column sums of segment s of M rows (nseg equal
 // segments, fixed order); out bf16 [nseg][ldo] or fp32 when out_f32
 hipError_t launch_colsum_fold(const float* part, int64_t M, int N, int nseg, void* out, int64_t ldo,
