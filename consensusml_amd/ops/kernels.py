@@ -204,7 +204,7 @@ def gram_center(G: torch.Tensor, n: int, out: Optional[torch.Tensor] = None) -> 
     if G.is_cuda:
         lib().gram_center(G.contiguous(), n, out)
         return out
-    out.fill_(ref.gram_center(G[:n, :n]))
+    out.reshape(-1)[0] = ref.gram_center(G[:n, :n])   # (element 1 of an engine center: guard state)
     return out
 
 
@@ -231,7 +231,11 @@ def robust_weights(G: torch.Tensor, rule: str, n: int, f: int = 0, m: Optional[i
     In the same launch (weights.hip): ``sel_counts`` += (w > 0); ``center_out`` = the medoid of
     G (the next step's Gram center); ``guard`` (G from a pass centered on the previous step's
     medoid): at least half the worker rows non-finite = a captured center -> weights zeroed
-    (centered clipping keeps its previous aggregate) and ``center_out`` = -1."""
+    (centered clipping keeps its previous aggregate) and ``center_out`` = -1. ``center_out``
+    holds, on entry, the center this pass used: a negative one (an uncentered pass, e.g. the step
+    after a trip) disarms the guard; a 2-element ``center_out`` also carries the previous pass's
+    count of non-finite rows, and only an increase trips -- so workers that are genuinely
+    non-finite (even half of them) are aggregated around instead of freezing the weights."""
     dim = n + 1 if rule == "centered_clip" else n
     if G.is_cuda:
         if w_out is None:
@@ -239,9 +243,15 @@ def robust_weights(G: torch.Tensor, rule: str, n: int, f: int = 0, m: Optional[i
         lib().robust_weights(G.contiguous(), RULE_IDS[rule], n, f, m or 0, iters, eps, tol, tau,
                              w_out, scores, sel, guard, center_out, sel_counts)
         return w_out
+    if guard and center_out is not None and int(center_out.reshape(-1)[0]) < 0:
+        guard = False
     w = _robust_weights_ref(G, rule, n, f, m, iters, eps, tol, tau, scores, sel)
     nbad = int((~torch.isfinite(torch.diagonal(G)[:n])).sum())
     trip = guard and nbad > 0 and 2 * nbad >= n
+    if center_out is not None and center_out.numel() >= 2:
+        # element 1: the previous pass's non-finite row count (only an INCREASE trips)
+        trip = trip and nbad > int(center_out.reshape(-1)[1])
+        center_out.reshape(-1)[1] = nbad
     if trip:
         w = torch.zeros_like(w)
         if rule == "centered_clip":
@@ -251,7 +261,7 @@ def robust_weights(G: torch.Tensor, rule: str, n: int, f: int = 0, m: Optional[i
     if sel_counts is not None:
         sel_counts += (w[:n] > 0).double()
     if center_out is not None:
-        center_out.fill_(-1 if trip else ref.gram_center(G[:n, :n]))
+        center_out.reshape(-1)[0] = -1 if trip else ref.gram_center(G[:n, :n])
     if w_out is not None:
         w_out.copy_(w)
         return w_out
@@ -344,19 +354,24 @@ def gossip_mix(master: torch.Tensor, left: torch.Tensor, right: torch.Tensor, w0
 
 def gossip_mix_k(master: torch.Tensor, nbrs: List[torch.Tensor], w: List[float], w0: float,
                  clip: float = 0.0, param_out: Optional[torch.Tensor] = None,
-                 work: Optional[torch.Tensor] = None) -> None:
+                 work: Optional[torch.Tensor] = None,
+                 param_out2: Optional[torch.Tensor] = None) -> None:
     """In-place k-neighbour mixing (1 <= k <= 8) of the fp32 master with the neighbours' bf16
-    parameters: x <- (w0 + sum w_k) x + sum_k w_k clip_k(nb_k - x)."""
+    parameters: x <- (w0 + sum w_k) x + sum_k w_k clip_k(nb_k - x). ``param_out2``: a second
+    copy of the rounded parameters (the delayed-gossip send buffer) written in the same pass."""
     if master.is_cuda:
         if work is None:
             work = torch.empty(lib().gossip_workspace_bytes(master.numel()) // 4,
                                dtype=torch.float32, device=master.device)
-        lib().gossip_mix_k(master, param_out, list(nbrs), [float(v) for v in w], w0, clip, work)
+        lib().gossip_mix_k(master, param_out, list(nbrs), [float(v) for v in w], w0, clip, work,
+                           param_out2)
         return
     x = ref.gossip_mix_k(master, nbrs, w, w0, clip)
     master.copy_(x)
     if param_out is not None:
         param_out.copy_(x.to(param_out.dtype))
+    if param_out2 is not None:
+        param_out2.copy_(x.to(param_out2.dtype))
 
 
 FAULT_IDS = {"none": 0, "sign_flip": 1, "gaussian": 2, "scaled": 3, "zero": 4, "nan": 5}

@@ -83,6 +83,18 @@ def max_gossip_peers(graph: str, N: int) -> int:
     return max(len(gossip_peers(graph, N, r, t)[1]) for r in range(N) for t in range(tau))
 
 
+class _EventWork:
+    """A work-like handle (``wait()``) for device work enqueued on a side stream: the waiting
+    stream (the caller's current stream) waits for an event recorded now on ``stream``."""
+
+    def __init__(self, stream: torch.cuda.Stream):
+        self.ev = torch.cuda.Event()
+        self.ev.record(stream)
+
+    def wait(self) -> None:
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
 class ConsensusEngine:
     def __init__(self, model: torch.nn.Module, cfg: TrainConfig, info: DistInfo):
         self.cfg = cfg
@@ -141,7 +153,8 @@ class ConsensusEngine:
         self.scores = torch.zeros(self.n, dtype=torch.float64, device=dev)
         self.sel = torch.zeros(self.n + 1, dtype=torch.int32, device=dev)
         self.sel_counts = torch.zeros(self.n, dtype=torch.float64, device=dev)
-        self.center = torch.zeros(1, dtype=torch.int32, device=dev)   # centered-Gram row
+        # [centered-Gram row, non-finite rows of the previous pass] (weights.hip guard state)
+        self.center = torch.zeros(2, dtype=torch.int32, device=dev)
         self.have_center = False    # self.center holds a medoid from an earlier step
         self.gout = None
         if self.rule == "centered_clip":
@@ -191,8 +204,14 @@ class ConsensusEngine:
         # top-level children are actually called as modules (their params are only read inside
         # their own forward) is learned on the first step, which waits for everything up front.
         self._ag_works: Dict[int, object] = {}
-        self.param_prefetch = bool(cfg.topology.param_prefetch and self.topo == "sharded"
-                                   and self.group_active)
+        # Delayed gossip on the GPU: the end-of-step mix runs on a side stream bucket by bucket
+        # (earliest layers first) and the next forward waits per module for its buckets through
+        # the same hooks, so the mix overlaps the forward instead of preceding it
+        self._mix_stream = (torch.cuda.Stream(device=dev)
+                            if (self.topo == "gossip" and cfg.topology.gossip_async
+                                and dev.type == "cuda" and self.group_active) else None)
+        self.param_prefetch = bool(cfg.topology.param_prefetch and self.group_active
+                                   and (self.topo == "sharded" or self._mix_stream is not None))
         self._prefetch_hooks = []
         if self.param_prefetch:
             self._setup_prefetch()
@@ -220,7 +239,10 @@ class ConsensusEngine:
         self._gram_arg_cache: Dict[int, tuple] = {}
         self._gram_nblk: Dict[int, int] = {}
         self._fast_gram_ok: Optional[bool] = None
-        self._gram_ordered = self.early_gram and dev.type == "cuda"
+        # One rank only: at N > 1 a device-side wait on a collective that has not
+        # landed would hold back every later backward kernel, and no N > 1 run has measured it;
+        # there the Grams use the polled form (at N = 8 a rank's shard Gram is ~10 us at step())
+        self._gram_ordered = self.early_gram and dev.type == "cuda" and self.N == 1
         self.gram_lag = max(0, int(cfg.topology.gram_lag))
         # training-side consensus table (SURVEY.md §5.4 b): when set, the next step() records
         # per-worker / per-parameter gradient statistics (consensus_table())
@@ -292,13 +314,23 @@ class ConsensusEngine:
 
     # ================================================================ parameter prefetch
     def _setup_prefetch(self) -> None:
+        """Forward pre-hooks per unit: the top-level children, except that a container that is
+        never called (ModuleList / ModuleDict, e.g. a transformer's layer stack) contributes its
+        children (one unit per block)."""
         fl = self.flat
         root = fl.model
         pid = {id(p): i for i, p in enumerate(fl.params)}
-        self._root_buckets = {fl.bucket_of[pid[id(p)]] for p in root.parameters(recurse=False)
-                              if id(p) in pid}
-        self._child_buckets: Dict[str, set] = {}
+        units = []
         for name, child in root.named_children():
+            if isinstance(child, (torch.nn.ModuleList, torch.nn.ModuleDict)):
+                units += [(f"{name}.{n2}", c2) for n2, c2 in child.named_children()]
+            else:
+                units.append((name, child))
+        covered = {id(p) for _, u in units for p in u.parameters()}
+        self._root_buckets = {fl.bucket_of[pid[id(p)]] for p in root.parameters()
+                              if id(p) in pid and id(p) not in covered}
+        self._child_buckets: Dict[str, set] = {}
+        for name, child in units:
             self._child_buckets[name] = {fl.bucket_of[pid[id(p)]] for p in child.parameters()
                                          if id(p) in pid}
             self._prefetch_hooks.append(child.register_forward_pre_hook(
@@ -827,10 +859,11 @@ class ConsensusEngine:
         ops += [dist.P2POp(dist.irecv, bufs[k][s - off:e - off], q) for k, q in recv]
         return dist.batch_isend_irecv(ops) if ops else []
 
-    def _gossip_mix(self, t: int, s: int, e: int, off: int = 0) -> None:
+    def _gossip_mix(self, t: int, s: int, e: int, off: int = 0, send: bool = False) -> None:
         _, _, w, w0 = self._gossip_peers(t)
         K.gossip_mix_k(self.master[s:e], [b[s - off:e - off] for b in self.nb_bufs], w, w0,
-                       self.cfg.topology.gossip_clip, param_out=self.flat.flat_param[s:e])
+                       self.cfg.topology.gossip_clip, param_out=self.flat.flat_param[s:e],
+                       param_out2=self._send_buf[s:e] if send else None)
 
     def _step_gossip(self) -> None:
         fl = self.flat
@@ -854,19 +887,40 @@ class ConsensusEngine:
 
         if self.cfg.topology.gossip_async:
             # Delayed gossip: mix with the neighbour parameters that arrived during THIS step's
-            # compute (sent at the end of the previous step, graph of step t - 1), then snapshot
-            # the new local parameters and start the next exchange, which overlaps the next
-            # forward/backward.
-            if self._gossip_reqs is not None or self._gossip_restored:
-                self._drain_gossip()
-                self._gossip_restored = False
-                self._gossip_mix(t - 1, 0, total)
+            # compute (sent at the end of the previous step, graph of step t - 1) and start the
+            # next exchange, which overlaps the next forward/backward. The mix writes the new
+            # parameters AND the send buffer in one pass (no snapshot copy of the parameters:
+            # the next step's early updates overwrite them while the send is in flight). GPU: on
+            # a side stream, bucket by bucket, earliest layers first; the next forward waits per
+            # module (the prefetch hooks), so the mix overlaps it instead of preceding it.
+            mixed = self._gossip_reqs is not None or self._gossip_restored
+            ms = self._mix_stream
             if self._send_buf is None:
                 self._send_buf = torch.empty_like(fl.flat_param)
-            self._send_buf.copy_(fl.flat_param)
-            self._gossip_reqs = [self._gossip_exchange(t, s, min(s + chunk, total),
-                                                       self._send_buf, self.nb_bufs, 0)
-                                 for s in starts]
+            if ms is not None:
+                ms.wait_stream(torch.cuda.current_stream(self.device))
+            with (torch.cuda.stream(ms) if ms is not None else contextlib.nullcontext()):
+                if mixed:
+                    self._drain_gossip()        # (on the side stream: a device-side wait)
+                    self._gossip_restored = False
+                    if ms is None or clip > 0 or not self.param_prefetch:
+                        # (clipping needs whole-vector neighbour distances)
+                        self._gossip_mix(t - 1, 0, total, send=True)
+                        if ms is not None and self.param_prefetch:
+                            ev = _EventWork(ms)
+                            for b in fl.buckets:
+                                self._ag_works[b.index] = ev
+                    else:
+                        for b in reversed(fl.buckets):
+                            self._gossip_mix(t - 1, b.offset, b.offset + b.length, send=True)
+                            self._ag_works[b.index] = _EventWork(ms)
+                else:
+                    self._send_buf.copy_(fl.flat_param)   # first exchange: nothing mixed yet
+                self._gossip_reqs = [self._gossip_exchange(t, s, min(s + chunk, total),
+                                                           self._send_buf, self.nb_bufs, 0)
+                                     for s in starts]
+            if ms is not None and not self.param_prefetch:
+                torch.cuda.current_stream(self.device).wait_stream(ms)
             return
 
         if clip > 0 and len(starts) > 1:
@@ -1027,7 +1081,8 @@ class ConsensusEngine:
         self.step_count = int(sd["step"])
         self.sel_counts.copy_(sd["sel_counts"])
         if "gram_center" in sd:
-            self.center.copy_(sd["gram_center"])
+            c = sd["gram_center"].reshape(-1)
+            self.center[: c.numel()].copy_(c[:2])
             self.have_center = True
         if "v0" in sd and self.gout is not None:
             self.gout.copy_(sd["v0"])

@@ -257,12 +257,14 @@ void robust_weights(const Tensor& G, int64_t rule, int64_t n, int64_t f, int64_t
   double* sc = opt_ptr<double>(scores, at::kDouble, "scores", n);
   int* se = opt_ptr<int>(sel, at::kInt, "sel", n + 1);
   int* co = opt_ptr<int>(center_out, at::kInt, "center_out", 1);
+  // a 2-element center buffer carries the guard's non-finite-row count of the previous pass
+  int* nb = (co && center_out->numel() >= 2) ? co + 1 : nullptr;
   double* cnt = opt_ptr<double>(sel_counts, at::kDouble, "sel_counts", n);
   CML_CHECK_HIP(cml::launch_robust_weights(static_cast<int>(rule), G.data_ptr<double>(),
                                            static_cast<int>(n), static_cast<int>(f),
                                            static_cast<int>(m), static_cast<int>(iters), eps, tol,
                                            tau, w.data_ptr<float>(), sc, se, cur_stream(),
-                                           guard ? 1 : 0, co, cnt));
+                                           guard ? 1 : 0, co, cnt, nb));
 }
 
 // G = sum over b of Gb[b] (fp64 [nb, r, r] -> [r, r]) in bucket order
@@ -299,7 +301,8 @@ void gossip_mix(Tensor& master, const optional<Tensor>& param_out, const Tensor&
 }
 
 void gossip_mix_k(Tensor& master, const optional<Tensor>& param_out, std::vector<Tensor> nbrs,
-                  std::vector<double> w, double w0, double clip, Tensor& work) {
+                  std::vector<double> w, double w0, double clip, Tensor& work,
+                  const optional<Tensor>& param_out2) {
   check_dev(master, "master");
   TORCH_CHECK(master.scalar_type() == at::kFloat && master.is_contiguous(), "master: fp32 contiguous");
   const int64_t D = master.numel();
@@ -316,10 +319,11 @@ void gossip_mix_k(Tensor& master, const optional<Tensor>& param_out, std::vector
   }
   TORCH_CHECK(work.numel() * work.element_size() >= gossip_workspace_bytes(D), "gossip workspace too small");
   void* p = opt_ptr<void>(param_out, nbrs[0].scalar_type(), "param_out", D);
+  void* p2 = opt_ptr<void>(param_out2, nbrs[0].scalar_type(), "param_out2", D);
   const c10::DeviceGuard guard(master.device());
   CML_CHECK_HIP(cml::launch_gossip_mix_k(dtype_of(nbrs[0]), master.data_ptr<float>(), p, ptr.data(),
                                          wf.data(), k, D, static_cast<float>(w0),
-                                         static_cast<float>(clip), work.data_ptr(), cur_stream()));
+                                         static_cast<float>(clip), work.data_ptr(), cur_stream(), p2));
 }
 
 // x / res / y: NHWC-contiguous bf16 (4-D channels_last or 2-D [M, C]).
@@ -2494,7 +2498,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "fused robust aggregation + optimizer step over several buckets in one launch");
   m.def("gossip_workspace_bytes", &gossip_workspace_bytes);
   m.def("gossip_mix", &gossip_mix, "ring gossip mixing with neighbour clipping");
-  m.def("gossip_mix_k", &gossip_mix_k, "k-neighbour gossip mixing with neighbour clipping");
+  m.def("gossip_mix_k", &gossip_mix_k, "k-neighbour gossip mixing with neighbour clipping (optional "
+        "second parameter output: the delayed-gossip send buffer)", py::arg("master"),
+        py::arg("param_out"), py::arg("nbrs"), py::arg("w"), py::arg("w0"), py::arg("clip"),
+        py::arg("work"), py::arg("param_out2") = py::none());
   m.def("colsum_seg", &colsum_seg, "per-segment column sums into strided rows");
   m.def("norm_bwd_seg", &norm_bwd_seg, "LayerNorm / RMSNorm backward with per-segment dgamma / dbeta");
   m.def("conv1x1g_mode", &cml::conv1x1g_mode, "fused 1x1 kernel family: 0 old, 1 glds, 2 auto");

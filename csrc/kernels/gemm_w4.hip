@@ -14,8 +14,17 @@
 // block, so per MFMA it reads half the LDS bytes of gemm.hip's waves (every 16 x 16 x 32 product
 // needs 1/8 of an A fragment + 1/8 of a B fragment instead of 1/8 + 1/4), and the accumulators
 // (64 x f32x4 = 256 registers) live in the AGPR half of the 512-register file at one wave per
-// SIMD. Fewer LDS reads per FLOP is what lets the chip hold its clock on random data (DVFS:
-// cdna_hip_programming.md rule 28).
+// SIMD -- and it reads k-major operands in place (ds_read_b64_tr_b16), which gemm.hip cannot.
+//
+// Measured (profiles/r06_01, r06_03; random operands, interleaved with hipBLASLt in one process):
+// 8192^3 1.02 PFLOP/s vs hipBLASLt 1.60 and gemm.hip 1.49; the Llama-3-8B products 0.7-1.1. So the
+// library / gemm.hip paths stay the defaults and this kernel is the any-layout fallback. Timing
+// ablations at 8192^3 (CML_W4_ABL) put the loss in the serialisation of one wave per SIMD: no
+// staging 0.90 ms, no fragment reads 0.88, no barrier 1.13, none of the three 0.67 ms (1.65
+// PFLOP/s = hipBLASLt: the MFMA ceiling at the clock the chip holds) vs 1.31 ms in that build --
+// with no partner wave on the SIMD, every global_load_lds issue (~100+ cycles among 16 fragment
+// reads, MI355X_MICROARCH.md) stalls the MFMA pipe. Register staging instead of LDS-DMA did not
+// fit: 128 fragment + 32 staging VGPRs next to 256 AGPR accumulators spilled.
 //
 // Schedule:
 //   * K advances in 32-deep sub-stages through a 4-deep LDS ring (4 x 32 KB: A image 16 KB, B image
@@ -71,7 +80,7 @@ __device__ __forceinline__ uint2 ds_tr16(const char* p) {
   return __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p)));
 }
 
-// SCH: steady-state schedule (0: barrier, loads, 64 MFMAs; 1 / 2: see step_main). ABL (timing
+// SCH: steady-state schedule (0: barrier, loads, 64 MFMAs; 2: see step). ABL (timing
 // ablations only, wrong results): bit 0 no staging in the loop, bit 1 no fragment reads, bit 2 no
 // barrier.
 template <bool AT, bool BT, int SCH = 0, int ABL = 0>
@@ -181,7 +190,9 @@ __global__ __launch_bounds__(kThr, 1) void gemm_w4_kernel(GemmArgs a) {
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 8; ++nt) acc[mt][nt] = mfma16(fb[nt], fa[mt], acc[mt][nt]);
+      for (int nt = 0; nt < 8; ++nt) {
+        acc[mt][nt] = mfma16(fb[nt], fa[mt], acc[mt][nt]);
+      }
     __builtin_amdgcn_s_setprio(0);
   };
   auto mma_rows = [&](const bf16x8_t (&fa)[8], const bf16x8_t (&fb)[8], int m_lo) {
@@ -199,67 +210,49 @@ __global__ __launch_bounds__(kThr, 1) void gemm_w4_kernel(GemmArgs a) {
   auto vm16 = [] { asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); };
   auto vm0 = [] { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
 
-  // ---- prologue: stages 0, 1, 2 in flight; stage 0 landed and visible; its fragments read
+  const int last = nks - 1;
+  // ---- prologue: stages 0, 1, 2 in flight (clamped: past the last stage a load repeats it into
+  // a buffer nobody reads, so every step has the same counts and the loop has no branches);
+  // stage 0 landed and visible; its fragments read
   stage(0, 0);
-  if (nks > 1) stage(1, 1);
-  if (nks > 2) stage(2, 2);
-  if (nks > 2) vm16();
-  else if (nks > 1) vm8();
-  else vm0();
+  stage(min(1, last), 1);
+  stage(min(2, last), 2);
+  vm16();
   bar();
   readst(fa0, fb0, 0);
 
+  // step s: stage s + 1 landed (vmcnt 8: stage s + 2's loads may fly) -> barrier -> stage s + 3
+  // into stage s - 1's buffer -> fragments of stage s + 1 -> MFMAs of stage s.
+  // SCH 2: half the MFMAs before the barrier, half after it with the staging and fragment reads.
   auto step = [&](int s, bf16x8_t (&fac)[8], bf16x8_t (&fbc)[8], bf16x8_t (&fan)[8],
                   bf16x8_t (&fbn)[8]) {
-    if (s + 1 < nks) {
-      if (s + 2 < nks) vm8();
-      else vm0();
-      bar();
-      if (s + 3 < nks) stage(s + 3, (s + 3) & 3);
-      readst(fan, fbn, (s + 1) & 3);
-    }
-    mma(fac, fbc);
-  };
-  // steady-state step (s + 3 < nks): branch-free, so the loads can be interleaved with MFMAs.
-  // SCH 1 / 2: half the MFMAs before the barrier, the other half after it with the staging
-  // and fragment reads (SCH 1 interleaves them by sched_group_barrier).
-  auto step_main = [&](int s, bf16x8_t (&fac)[8], bf16x8_t (&fbc)[8], bf16x8_t (&fan)[8],
-                       bf16x8_t (&fbn)[8]) {
+    // retire the fragment reads of the previous step here (they had a whole step of MFMAs to
+    // land): lgkmcnt counts only 15 outstanding operations, so with this step's 16 reads in
+    // flight hipcc could otherwise only wait for the previous ones with lgkmcnt(0) -- i.e. for
+    // the reads it just issued -- in front of the first MFMA. The builtin (not inline asm) is
+    // seen by hipcc's waitcnt bookkeeping. (encoding: vmcnt 63, expcnt 7, lgkmcnt 0)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
     if constexpr (SCH == 0) {
       vm8();
       if constexpr (!(ABL & 4)) bar();
-      if constexpr (!(ABL & 1)) stage(s + 3, (s + 3) & 3);
+      if constexpr (!(ABL & 1)) stage(min(s + 3, last), (s + 3) & 3);
       if constexpr (!(ABL & 2)) readst(fan, fbn, (s + 1) & 3);
       mma(fac, fbc);
     } else {
       mma_rows(fac, fbc, 0);
       vm8();
       bar();
-      stage(s + 3, (s + 3) & 3);
+      stage(min(s + 3, last), (s + 3) & 3);
       readst(fan, fbn, (s + 1) & 3);
       mma_rows(fac, fbc, 4);
-      if constexpr (SCH == 1) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);   // VMEM (LDS-DMA)
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS read
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        }
-      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  int s = 0;
-  for (; s + 4 < nks; s += 2) {
-    step_main(s, fa0, fb0, fa1, fb1);
-    step_main(s + 1, fa1, fb1, fa0, fb0);
-  }
-  for (; s < nks; s += 2) {
+  for (int s = 0; s < nks; s += 2) {
     step(s, fa0, fb0, fa1, fb1);
     step(s + 1, fa1, fb1, fa0, fb0);
   }
+  vm0();                       // the clamped repeats may still be landing
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   bar();
 
@@ -318,13 +311,13 @@ __global__ __launch_bounds__(kThr, 1) void gemm_w4_kernel(GemmArgs a) {
   }
 }
 
-// CML_W4_SCHED (0 / 1 / 2: the steady-state schedule, A/B) and CML_W4_ABL (timing ablations
+// CML_W4_SCHED (0 / 2: the steady-state schedule, A/B) and CML_W4_ABL (timing ablations
 // of mode 0, wrong results) are read once
 int w4_sched() {
   static const int v = [] {
     const char* e = getenv("CML_W4_SCHED");
     const int x = e ? atoi(e) : 0;
-    return x >= 0 && x <= 2 ? x : 0;
+    return x == 2 ? 2 : 0;
   }();
   return v;
 }
@@ -373,17 +366,14 @@ hipError_t launch_gemm_w4(const GemmArgs& a, int mode, hipStream_t st) {
   }
   switch (mode * 4 + sch) {
     case 0: CML_W4(false, false, 0, 0); break;
-    case 1: CML_W4(false, false, 1, 0); break;
     case 2: CML_W4(false, false, 2, 0); break;
     case 4: CML_W4(true, false, 0, 0); break;
-    case 5: CML_W4(true, false, 1, 0); break;
     case 6: CML_W4(true, false, 2, 0); break;
     case 8: CML_W4(false, true, 0, 0); break;
-    case 9: CML_W4(false, true, 1, 0); break;
     case 10: CML_W4(false, true, 2, 0); break;
     case 12: CML_W4(true, true, 0, 0); break;
-    case 13: CML_W4(true, true, 1, 0); break;
-    default: CML_W4(true, true, 2, 0); break;
+    case 14: CML_W4(true, true, 2, 0); break;
+    default: return hipErrorInvalidValue;
   }
 #undef CML_W4
   return hipGetLastError();

@@ -84,6 +84,7 @@ __global__ __launch_bounds__(kBlk) void nbr_sqdist_kernel(const float* __restric
 // kernel's expression). Each workgroup folds the distance slab itself (fixed order).
 template <typename T, int K>
 __global__ __launch_bounds__(kBlk) void gossip_mix_kernel(float* __restrict__ x, T* __restrict__ p,
+                                                         T* __restrict__ p2,
                                                          Nbrs<T> nb, int64_t D, float w0,
                                                          float clip, const float* __restrict__ part,
                                                          int nblk) {
@@ -133,6 +134,10 @@ __global__ __launch_bounds__(kBlk) void gossip_mix_kernel(float* __restrict__ x,
       if constexpr (sizeof(T) == 2) store_bf16<8>(p + t * 8, xv);
       else store_f32<8>(p + t * 8, xv);
     }
+    if (p2) {   // the delayed-gossip send buffer: written here instead of copied from p
+      if constexpr (sizeof(T) == 2) store_bf16<8>(p2 + t * 8, xv);
+      else store_f32<8>(p2 + t * 8, xv);
+    }
   }
   if (blockIdx.x == 0) {
     for (int64_t e = nv * 8 + threadIdx.x; e < D; e += kBlk) {
@@ -145,6 +150,10 @@ __global__ __launch_bounds__(kBlk) void gossip_mix_kernel(float* __restrict__ x,
       if (p) {
         if constexpr (sizeof(T) == 2) reinterpret_cast<uint16_t*>(p)[e] = f2bf(v);
         else p[e] = v;
+      }
+      if (p2) {
+        if constexpr (sizeof(T) == 2) reinterpret_cast<uint16_t*>(p2)[e] = f2bf(v);
+        else p2[e] = v;
       }
     }
   }
@@ -198,32 +207,34 @@ size_t gossip_workspace_bytes(int64_t) { return kMaxNbrs * kMaxBlk * sizeof(floa
 
 namespace {
 template <typename T, int K>
-void gossip_k(float* master, void* param_out, const Nbrs<T>& nb, int64_t D, float w0, float clip,
-              void* work, hipStream_t stream) {
+void gossip_k(float* master, void* param_out, void* param_out2, const Nbrs<T>& nb, int64_t D,
+              float w0, float clip, void* work, hipStream_t stream) {
   float* part = reinterpret_cast<float*>(work);
   const int nb_blocks = nblocks(D / 8, kMaxBlk);
   if (clip > 0.f) nbr_sqdist_kernel<T, K><<<nb_blocks, kBlk, 0, stream>>>(master, nb, D, part);
   gossip_mix_kernel<T, K><<<nblocks(D / 8, 2048), kBlk, 0, stream>>>(
-      master, reinterpret_cast<T*>(param_out), nb, D, w0, clip, part, nb_blocks);
+      master, reinterpret_cast<T*>(param_out), reinterpret_cast<T*>(param_out2), nb, D, w0, clip,
+      part, nb_blocks);
 }
 
 template <typename T>
-hipError_t gossip_t(float* master, void* param_out, const void* const* nbrs, const float* w,
-                    int k, int64_t D, float w0, float clip, void* work, hipStream_t stream) {
+hipError_t gossip_t(float* master, void* param_out, void* param_out2, const void* const* nbrs,
+                    const float* w, int k, int64_t D, float w0, float clip, void* work,
+                    hipStream_t stream) {
   Nbrs<T> nb{};
   for (int i = 0; i < k; ++i) {
     nb.p[i] = reinterpret_cast<const T*>(nbrs[i]);
     nb.w[i] = w[i];
   }
   switch (k) {
-    case 1: gossip_k<T, 1>(master, param_out, nb, D, w0, clip, work, stream); break;
-    case 2: gossip_k<T, 2>(master, param_out, nb, D, w0, clip, work, stream); break;
-    case 3: gossip_k<T, 3>(master, param_out, nb, D, w0, clip, work, stream); break;
-    case 4: gossip_k<T, 4>(master, param_out, nb, D, w0, clip, work, stream); break;
-    case 5: gossip_k<T, 5>(master, param_out, nb, D, w0, clip, work, stream); break;
-    case 6: gossip_k<T, 6>(master, param_out, nb, D, w0, clip, work, stream); break;
-    case 7: gossip_k<T, 7>(master, param_out, nb, D, w0, clip, work, stream); break;
-    case 8: gossip_k<T, 8>(master, param_out, nb, D, w0, clip, work, stream); break;
+    case 1: gossip_k<T, 1>(master, param_out, param_out2, nb, D, w0, clip, work, stream); break;
+    case 2: gossip_k<T, 2>(master, param_out, param_out2, nb, D, w0, clip, work, stream); break;
+    case 3: gossip_k<T, 3>(master, param_out, param_out2, nb, D, w0, clip, work, stream); break;
+    case 4: gossip_k<T, 4>(master, param_out, param_out2, nb, D, w0, clip, work, stream); break;
+    case 5: gossip_k<T, 5>(master, param_out, param_out2, nb, D, w0, clip, work, stream); break;
+    case 6: gossip_k<T, 6>(master, param_out, param_out2, nb, D, w0, clip, work, stream); break;
+    case 7: gossip_k<T, 7>(master, param_out, param_out2, nb, D, w0, clip, work, stream); break;
+    case 8: gossip_k<T, 8>(master, param_out, param_out2, nb, D, w0, clip, work, stream); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -232,13 +243,15 @@ hipError_t gossip_t(float* master, void* param_out, const void* const* nbrs, con
 
 hipError_t launch_gossip_mix_k(int dtype, float* master, void* param_out, const void* const* nbrs,
                                const float* w, int k, int64_t D, float w0, float clip, void* work,
-                               hipStream_t stream) {
+                               hipStream_t stream, void* param_out2) {
   if (k < 1 || k > kMaxNbrs) return hipErrorInvalidValue;
-  uintptr_t a = reinterpret_cast<uintptr_t>(master) | reinterpret_cast<uintptr_t>(param_out);
+  uintptr_t a = reinterpret_cast<uintptr_t>(master) | reinterpret_cast<uintptr_t>(param_out) |
+                reinterpret_cast<uintptr_t>(param_out2);
   for (int i = 0; i < k; ++i) a |= reinterpret_cast<uintptr_t>(nbrs[i]);
   if (a % 16) return hipErrorInvalidValue;
-  return dtype == DT_BF16 ? gossip_t<bf16>(master, param_out, nbrs, w, k, D, w0, clip, work, stream)
-                          : gossip_t<float>(master, param_out, nbrs, w, k, D, w0, clip, work, stream);
+  return dtype == DT_BF16
+             ? gossip_t<bf16>(master, param_out, param_out2, nbrs, w, k, D, w0, clip, work, stream)
+             : gossip_t<float>(master, param_out, param_out2, nbrs, w, k, D, w0, clip, work, stream);
 }
 
 hipError_t launch_gossip_mix(int dtype, float* master, void* param_out, const void* left,

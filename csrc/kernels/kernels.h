@@ -85,7 +85,8 @@ hipError_t launch_gram_center(const double* G, int n, int* out, hipStream_t stre
 hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m, int iters,
                                  double eps, double tol, double tau, float* w, double* scores,
                                  int* sel, hipStream_t stream, int guard = 0,
-                                 int* center_out = nullptr, double* sel_counts = nullptr);
+                                 int* center_out = nullptr, double* sel_counts = nullptr,
+                                 int* nbad_io = nullptr);
 // Stage 1 of launch_gram only: per-workgroup [P, P] fp32 partials into work (*nblk of them, P =
 // 16 ceil(n / 16)); launch_gram_reduce_multi then reduces nb buckets' partials into G in ONE
 // launch, bit-identical to one launch_gram per bucket into slots summed by launch_gram_sum.
@@ -111,7 +112,7 @@ size_t gossip_workspace_bytes(int64_t D);
 // k-neighbour mix (1 <= k <= 8): x <- (w0 + sum w_k) x + sum_k w_k clip_k(nbrs[k] - x)
 hipError_t launch_gossip_mix_k(int dtype, float* master, void* param_out, const void* const* nbrs,
                                const float* w, int k, int64_t D, float w0, float clip, void* work,
-                               hipStream_t stream);
+                               hipStream_t stream, void* param_out2 = nullptr);
 hipError_t launch_gossip_mix(int dtype, float* master, void* param_out, const void* left,
                              const void* right, int64_t D, float w0, float w1, float w2,
                              float clip, void* work, hipStream_t stream);

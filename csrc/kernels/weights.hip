@@ -211,12 +211,23 @@ __global__ __launch_bounds__(64) void robust_weights_kernel(int rule, const doub
                                                            double* __restrict__ scores,
                                                            int* __restrict__ sel, int guard,
                                                            int* __restrict__ center_out,
-                                                           double* __restrict__ sel_counts) {
+                                                           double* __restrict__ sel_counts,
+                                                           int* __restrict__ nbad_io) {
   __shared__ bool bad[kMax];
   __shared__ double sc[kMax];
   __shared__ double a[kMax];
   const int i = threadIdx.x;
   const int nrows = rule == RULE_CCLIP ? n + 1 : n;   // Gram dimension
+  // center_out holds the center THIS pass used (the engine passes one buffer): a pass that ran
+  // uncentered (center < 0, e.g. the step after a trip) cannot have been captured, so the guard
+  // is disarmed -- with half the rows genuinely non-finite it would otherwise trip every step
+  // and freeze training instead of aggregating the finite rows
+  const int center_in = center_out ? center_out[0] : 0;
+  if (center_in < 0) guard = 0;
+  // nbad_io: the previous pass's count of non-finite worker rows. A captured center shows as rows
+  // that TURNED non-finite; workers that were already non-finite (genuine NaN / overflow, up to
+  // half or more of them) are aggregated around as on an uncentered pass, every step
+  const int nbad_prev = nbad_io ? nbad_io[0] : 0;
   for (int r = i; r < nrows; r += 64) {
     const double d = G[r * nrows + r];
     bad[r] = !(d == d) || d == __builtin_inf() || d == -__builtin_inf();
@@ -226,7 +237,8 @@ __global__ __launch_bounds__(64) void robust_weights_kernel(int rule, const doub
   __syncthreads();
   int nbad = 0;
   for (int r = 0; r < n; ++r) nbad += bad[r];
-  const bool trip = guard && 2 * nbad >= n && nbad > 0;
+  const bool trip = guard && 2 * nbad >= n && nbad > 0 && (!nbad_io || nbad > nbad_prev);
+  if (nbad_io && i == 0) nbad_io[0] = nbad;
   if (trip) {
     if (i < nrows) w[i] = (rule == RULE_CCLIP && i == n) ? 1.0f : 0.0f;
     if (sel && rule != RULE_BULYAN_SELECT && i < n) sel[i] = 0;
@@ -267,12 +279,12 @@ __global__ __launch_bounds__(64) void robust_weights_kernel(int rule, const doub
 hipError_t launch_robust_weights(int rule, const double* G, int n, int f, int m, int iters,
                                  double eps, double tol, double tau, float* w, double* scores,
                                  int* sel, hipStream_t stream, int guard, int* center_out,
-                                 double* sel_counts) {
+                                 double* sel_counts, int* nbad_io) {
   if (n < 1 || n > 64) return hipErrorInvalidValue;
   if (rule == RULE_CCLIP && n > 63) return hipErrorInvalidValue;   // n + 1 rows, one per lane
   if (rule == RULE_BULYAN_SELECT && sel == nullptr) return hipErrorInvalidValue;
   robust_weights_kernel<<<1, 64, 0, stream>>>(rule, G, n, f, m, iters, eps, tol, tau, w, scores, sel,
-                                              guard, center_out, sel_counts);
+                                              guard, center_out, sel_counts, nbad_io);
   return hipGetLastError();
 }
 

@@ -149,7 +149,7 @@ def test_engine_single_pass_center(cuda):
     for step in range(4):
         X = _workers(6, 2, one.flat.total, 0.02, 30 + step, cuda)
         if step == 3:                         # the previous medoid's gradient is now NaN
-            X[int(one.center)] = float("nan")
+            X[int(one.center[0])] = float("nan")
         a, sa = _step(one, X)
         b, sb = _step(two, X)
         assert a == b
@@ -173,13 +173,13 @@ def test_engine_single_pass_captured_center(cuda):
         X = _workers(6, 2, one.flat.total, 0.02, 60 + step, cuda)
         if step >= 3:
             if attacker is None:
-                attacker = int(one.center)
+                attacker = int(one.center[0])
             X[attacker] = 1e38                # finite in bf16, overflows every centered square
         a, _ = _step(one, X)
         b, _ = _step(two, X)
         if step == 3:                         # the captured step: refused, not captured
             assert float(one.w[:8].sum()) == 0.0
-            assert int(one.center) == -1
+            assert int(one.center[0]) == -1
         else:
             assert a == b
             assert float(one.w[a]) > 0

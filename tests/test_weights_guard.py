@@ -145,3 +145,30 @@ def test_gram_deferred_multi_reduce_bitwise(n):
         got = torch.empty(n, n, dtype=torch.float64, device="cuda")
         lib().gram_reduce_multi(works, nblks, n, got)
         assert torch.equal(got, want)
+
+
+def test_guard_disarmed_after_trip_half_nan():
+    """n = 2 with one genuinely NaN worker (geomed): half the rows non-finite on EVERY pass. With
+    the engine's 2-element center state the guard trips only when rows TURN non-finite, so the
+    finite worker keeps getting the weight step after step instead of training freezing
+    (ADVICE r05); a 1-element center still disarms the guard on the uncentered pass after a trip."""
+    torch.manual_seed(3)
+    X = torch.randn(2, 16).double()
+    X[1] = float("nan")
+    G = X @ X.T
+    c = torch.tensor([0, 1], dtype=torch.int32)     # centered on worker 0, 1 bad row last pass
+    for _ in range(3):
+        w = K.robust_weights(G, "geomed", 2, guard=True, center_out=c)
+        assert float(w[0]) > 0.0 and float(w[1]) == 0.0
+        assert int(c[0]) == 0 and int(c[1]) == 1
+    # rows turning non-finite on a centered pass (a captured center) still trip
+    c = torch.tensor([0, 0], dtype=torch.int32)
+    w = K.robust_weights(G, "geomed", 2, guard=True, center_out=c)
+    assert float(w.abs().sum()) == 0.0 and int(c[0]) == -1
+    w = K.robust_weights(G, "geomed", 2, guard=True, center_out=c)   # uncentered pass: disarmed
+    assert float(w[0]) > 0.0
+    c1 = torch.zeros(1, dtype=torch.int32)
+    K.robust_weights(G, "geomed", 2, guard=True, center_out=c1)
+    assert int(c1) == -1
+    w = K.robust_weights(G, "geomed", 2, guard=True, center_out=c1)
+    assert float(w[0]) > 0.0

@@ -6,7 +6,10 @@
 
 Per kernel: dispatches, mean duration (from the counter run's own timestamps), mean counter
 values, and derived HBM-side rates: FETCH_SIZE / WRITE_SIZE are KiB per dispatch -> GB/s over the
-dispatch duration; SQ_INSTS_VALU_MFMA_MOPS_BF16 counts 512-FLOP units -> TFLOP/s.
+dispatch duration; SQ_INSTS_VALU_MFMA_MOPS_BF16 counts 512-FLOP units -> TFLOP/s. Derived against
+the MI355X peaks: HBM % = (scaled fetch + write) bytes / duration / 8 TB/s, MFMA % = bf16 MFMA
+FLOP / duration / 2.5 PFLOP/s (dense), and the effective clock GRBM_GUI_ACTIVE / 8 / duration
+(the counter sums the 8 XCDs; reads high on dispatches under ~0.3 ms).
 
 Calibration on this MI355X image (tools/diag/fetch_calibration.py, profiles/
 r02_fetch_size_calibration.md): on kernels with exactly known traffic -- a bf16 copy, a bf16 sum
@@ -44,8 +47,8 @@ def main(dirs, fetch_scale=2.0):
         kd[k].append(v)
     counters = sorted({c for k in acc for c in acc[k]})
     print("| kernel | dispatches | mean us | " + " | ".join(counters) +
-          " | fetch GB/s | write GB/s | bf16 MFMA TFLOP/s |")
-    print("|---|---|---|" + "---|" * len(counters) + "---|---|---|")
+          " | fetch GB/s | write GB/s | bf16 MFMA TFLOP/s | HBM % of 8 TB/s | MFMA % of 2.5 PF | clock GHz |")
+    print("|---|---|---|" + "---|" * len(counters) + "---|---|---|---|---|---|")
     for k in sorted(kd, key=lambda k: -sum(kd[k])):
         us = sum(kd[k]) / len(kd[k]) / 1e3
         mean = {c: sum(v) / len(v) for c, v in acc[k].items()}
@@ -56,8 +59,15 @@ def main(dirs, fetch_scale=2.0):
         rate = lambda kib, sc=1.0: (f"{sc * kib * 1024 / (us * 1e-6) / 1e9:.0f}"
                                     if kib is not None and us > 0 else "")
         tf = f"{mops * 512 / (us * 1e-6) / 1e12:.1f}" if mops is not None and us > 0 else ""
+        hbm = ""
+        if (fetch is not None or write is not None) and us > 0:
+            by = fetch_scale * (fetch or 0.0) * 1024 + (write or 0.0) * 1024
+            hbm = f"{100 * by / (us * 1e-6) / 8e12:.1f}"
+        mf = f"{100 * mops * 512 / (us * 1e-6) / 2.5e15:.1f}" if mops is not None and us > 0 else ""
+        gui = mean.get("GRBM_GUI_ACTIVE")
+        clk = f"{gui / 8 / (us * 1e-6) / 1e9:.2f}" if gui is not None and us > 0 else ""
         print(f"| `{k}` | {len(kd[k]) // max(1, len(dirs))} | {us:.1f} | " +
-              " | ".join(cells) + f" | {rate(fetch, fetch_scale)} | {rate(write)} | {tf} |")
+              " | ".join(cells) + f" | {rate(fetch, fetch_scale)} | {rate(write)} | {tf} | {hbm} | {mf} | {clk} |")
 
 
 if __name__ == "__main__":

@@ -1,9 +1,9 @@
 #!/bin/bash
-# r06 pass 2: gemm_w4 schedule variants (CML_W4_SCHED 0/1/2) and timing ablations of mode 0
+# r06 pass 3: gemm_w4 after retiring the previous fragment reads at the step start (no lgkmcnt(0)
 # (CML_W4_ABL: 1 no staging, 2 no fragment reads, 4 no barrier, 7 none of them) at 8192^3.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r06_02; mkdir -p $O
+O=$R/gpurun_out/r06_03; mkdir -p $O
 cd $R
 timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_w4_gpu.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
