@@ -13,9 +13,13 @@ and ``agg_overhead_vs_allreduce`` = (t_krum - t_allreduce) / t_allreduce is repo
 
 Data: synthetic ImageNet-shaped batches (random bf16 images, random labels) generated on
 device; random-init weights. Every timed step runs the full forward, backward, exchange,
-aggregation and optimizer update. Per-GPU batch 2048 by default: 288 GB of HBM holds it many
-times over (peak ~52 GiB), and throughput still rises with batch (larger conv / GEMM problems,
-fewer fixed per-step costs).
+aggregation and optimizer update. Per-GPU batch 2560 by default: 288 GB of HBM holds it many
+times over (peak ~65 GiB), and throughput still rises with batch. 2560 (not 2048) because the
+MFMA-bound 3x3 convs of layers 3 / 4 run 256 x 256 output tiles: at 2048 they are 1568 / 784
+tiles = 6.1 / 3.1 rounds of the 256 CUs (7 / 4 launched), at 2560 1960 / 980 = 7.7 / 3.8 rounds
+(8 / 4): +1.6-2.2 % samples/s on one box (profiles/r06_07/). 2560 is also the largest batch whose
+112 x 112 x 64 stem activations stay under 2^31 elements (int32 element indexing in the stem
+kernels).
 
 Communication-visible block (``b256_*`` keys, every N): at batch 2048 the step is ~127 ms of
 compute, so at N = 8 the exposed exchange is far below 1 % and "agg overhead vs all-reduce" says
@@ -54,10 +58,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=2048,
+    ap.add_argument("--batch", type=int, default=2560,
                     help="per-GPU batch (samples/s on MI355X rise with batch, see README; peak "
-                         "memory ~52 GiB at 2048 of 288; the shipped MIOpen find-db covers "
-                         "256 / 512 / 1024 / 1536 / 2048)")
+                         "memory ~65 GiB at 2560 of 288; the shipped MIOpen find-db covers "
+                         "256 / 512 / 1024 / 1536 / 2048 / 2560)")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--rule", default="krum")
     ap.add_argument("--f", type=int, default=-1,

@@ -71,6 +71,30 @@ def test_flash_fwd_bwd_vs_fp32(B, H, KV, S, causal):
         assert _rel(got, want) < 1e-2, (name, _rel(got, want))
 
 
+@pytest.mark.parametrize("S", [4096, 8192])
+def test_flash_long_sequence_gqa(S):
+    """The lengths the kernel header claims (S up to 8192) at the Llama-3-8B head layout (32 q /
+    8 kv heads, causal), forward and backward, against the fp32 oracle (B = 1: the fp32 score
+    tensors of the oracle are 32 x S x S)."""
+    B, H, KV = 1, 32, 8
+    q, k, v = _inputs(B, H, KV, S, seed=11)
+    scale = 1.0 / math.sqrt(128)
+    qa, ka, va = (t.clone().requires_grad_() for t in (q, k, v))
+    o = flash_attention(qa, ka, va, causal=True)
+    qr, kr, vr = (t.float().requires_grad_() for t in (q, k, v))
+    ref = _ref(qr, kr, vr, True, scale)
+    assert _rel(o, ref) < 1e-2
+    do = torch.randn_like(ref).bfloat16()
+    o.backward(do)
+    ref.backward(do.float())
+    for got, want, name in ((qa.grad, qr.grad, "dq"), (ka.grad, kr.grad, "dk"),
+                            (va.grad, vr.grad, "dv")):
+        assert torch.isfinite(got.float()).all(), name
+        assert _rel(got, want) < 1e-2, (name, _rel(got, want))
+    del ref, qr, kr, vr
+    torch.cuda.empty_cache()
+
+
 def test_flash_large_scores():
     """Scores of magnitude ~100: the running max jumps inside and across tiles."""
     B, H, KV, S = 1, 4, 2, 777

@@ -2,10 +2,11 @@
 """Driver for the rocprofv3 --pmc passes over this round's hot kernels (one process, a few
 dispatches each, real shapes):
 
-  agg     the consensus step at n = 8 virtual workers on ResNet-50 (D = 25.6 M, bf16 rows, batch
-          32 per worker): per-bucket Gram stage 1 (gram_partial), the deferred multi-bucket reduce
-          (gram_reduce_multi), the Krum weights (robust_weights) and the one-launch multi-bucket
-          rule + SGD update (agg_update_multi: weighted combine for Krum, sorted for the median)
+  agg     the consensus step at n = 8 virtual workers on D = 25.6 M bf16 coordinates (ResNet-50's
+          size; synthetic worker gradients, no model compute): per-bucket Gram stage 1
+          (gram_partial), the deferred multi-bucket reduce (gram_reduce_multi), the Krum weights
+          (robust_weights) and the one-launch multi-bucket rule + SGD update (agg_update_multi:
+          weighted combine for Krum, sorted for the median)
   flash   flash attention forward + backward, Llama-3-8B layer (B 4, 32 q / 8 kv heads, S 2048,
           hd 128, causal)
   gemm    gemm.hip (8 waves) and gemm_w4.hip (4 waves, modes 0 / 2 / 3) at 8192^3 and the Llama
@@ -32,22 +33,32 @@ def rnd(shape, dev, seed=0):
 
 
 def run_agg(dev, steps):
+    """The engine's consensus step on synthetic worker gradients (no model compute): 8 virtual
+    workers x D = 25.6 M bf16 coordinates (ResNet-50's size, one 64 MB bucket), sharded topology
+    at one rank: per-bucket Gram stage 1, the deferred multi-bucket reduce, the weights launch and
+    the one-launch multi-bucket rule + SGD update."""
     from consensusml_amd import TrainConfig
     from consensusml_amd.parallel.dist import DistInfo
-    from consensusml_amd.trainer.trainer import ConsensusTrainer
+    from consensusml_amd.parallel.engine import ConsensusEngine
     for rule in ("krum", "median"):
         cfg = TrainConfig()
-        cfg.model.name = "resnet50"
-        cfg.batch_per_worker = 32
         cfg.virtual_workers = 8
         cfg.agg.rule = rule
         cfg.agg.f = 2
         cfg.topology.kind = "sharded"
-        tr = ConsensusTrainer(cfg, info=DistInfo(0, 1, 0, dev, "none"))
+        model = torch.nn.Linear(5056, 5056, bias=False).to(dev).bfloat16()   # 25.56 M params
+        eng = ConsensusEngine(model, cfg, DistInfo(0, 1, 0, dev, "none"))
+        g = torch.Generator(device=dev).manual_seed(0)
+        base = torch.randn(eng.flat.total, generator=g, device=dev)
+        X = (base + 0.01 * torch.randn(8, eng.flat.total, generator=g, device=dev))
         for _ in range(steps):
-            tr.train_step()
-        torch.cuda.synchronize()
-        del tr
+            eng.zero_grad()
+            eng.flat.flat_grad.copy_(X.to(eng.flat.flat_grad.dtype))
+            eng._flushed = {b.index for b in eng.flat.buckets}
+            eng.step()
+            torch.cuda.synchronize()
+            print("agg", rule, "step", flush=True)
+        del eng, model, X, base
         torch.cuda.empty_cache()
 
 

@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--db", default=None, help="seed user-db directory")
     ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--only", nargs="*", default=None,
+                    help="shape keys cin x h x w x cout x k x stride x pad to tune (default: all)")
     ap.add_argument("--budget", type=float, default=1000.0, help="seconds; stop starting shapes after")
     ap.add_argument("--mode", choices=["search", "find"], default="search",
                     help="search: exhaustive (SEARCH_DB_UPDATE); find: MIOpen's normal find only")
@@ -81,6 +83,8 @@ def main():
     os.makedirs(a.out, exist_ok=True)
     for s in shapes:
         key = f"b{a.batch}:" + "x".join(map(str, s))
+        if a.only and "x".join(map(str, s)) not in a.only:
+            continue
         if key in done:
             continue
         if time.time() - t0 > a.budget:

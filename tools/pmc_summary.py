@@ -31,7 +31,7 @@ def short(name: str) -> str:
     return name[:70]
 
 
-def main(dirs, fetch_scale=2.0):
+def main(dirs, fetch_scale=2.0, match=None):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
     for d in dirs:
@@ -40,6 +40,8 @@ def main(dirs, fetch_scale=2.0):
             continue
         for r in csv.DictReader(open(path)):
             k = short(r["Kernel_Name"])
+            if match is not None and not re.search(match, k):
+                continue
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             dur[(k, d, r["Dispatch_Id"])] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
     kd = collections.defaultdict(list)
@@ -77,4 +79,9 @@ if __name__ == "__main__":
         i = args.index("--fetch-scale")
         scale = float(args[i + 1])
         del args[i:i + 2]
-    main(args, scale)
+    match = None
+    if "--match" in args:
+        i = args.index("--match")
+        match = args[i + 1]
+        del args[i:i + 2]
+    main(args, scale, match)
