@@ -531,19 +531,20 @@ def _linear_wgrad(gout: torch.Tensor, gin: torch.Tensor) -> torch.Tensor:
     return gout.t() @ gin
 
 
-# persistent zero-padded copies of logits-head weights / biases (padded_logits): keyed by the
-# parameter's identity, refreshed in place each forward (rows N .. Np stay zero), so the padded
-# path costs one weight copy instead of an allocation + zero-fill + copy per step
-_PAD_CACHE = {}
+# persistent zero-padded copies of logits-head weights / biases (padded_logits), held ON the weight
+# parameter itself (attribute ``_cml_pad``, keyed by the bias's identity): released together with
+# the parameter, never matched by a new tensor that reuses an id; refreshed in place each forward
+# (rows N .. Np stay zero), so the padded path costs one weight copy instead of an allocation +
+# zero-fill + copy per step
 
 
 def _padded_wb(w: torch.Tensor, b: torch.Tensor, Np: int):
-    key = (id(w), id(b))
-    hit = _PAD_CACHE.get(key)
-    if hit is None or hit[0].shape[0] != Np or hit[0].device != w.device or hit[0].dtype != w.dtype:
-        hit = (w.new_zeros(Np, w.shape[1]), b.new_zeros(Np))
-        _PAD_CACHE[key] = hit
-    wp, bp = hit
+    hit = getattr(w, "_cml_pad", None)
+    if (hit is None or hit[2] is not b or hit[0].shape[0] != Np or hit[0].device != w.device
+            or hit[0].dtype != w.dtype):
+        hit = (w.new_zeros(Np, w.shape[1]), b.new_zeros(Np), b)
+        w._cml_pad = hit
+    wp, bp = hit[0], hit[1]
     N = w.shape[0]
     wp[:N].copy_(w)
     bp[:N].copy_(b)

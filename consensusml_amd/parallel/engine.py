@@ -273,6 +273,14 @@ class ConsensusEngine:
                 1, {id(p): views[i] for i, p in enumerate(self.flat.params)})
             self._direct_prev = WG.activate(self._direct_wg)
 
+    def abort_step(self) -> None:
+        """Undo zero_grad()'s per-step state after a failed forward / backward: deactivate the
+        direct-gradient destination (module-global) and drop the half-filled bucket state."""
+        self._end_direct()
+        for v in self._ready.values():
+            v.clear()
+        self._flushed.clear()
+
     def _end_direct(self) -> None:
         if self._direct_wg is not None:
             if WG.current() is self._direct_wg:
@@ -435,9 +443,15 @@ class ConsensusEngine:
             wg = self._direct_wg
             cp = []
             for i in lst:
-                if fl.params[i].grad is not None:
-                    cp.append(i)
-                elif wg is None or id(fl.params[i]) not in wg.touched:
+                p = fl.params[i]
+                if p.grad is not None:
+                    if wg is not None and id(p) in wg.touched:
+                        # a direct write AND an autograd gradient (a tied weight with one use on
+                        # the direct path): add, never overwrite the direct contribution
+                        views[i].add_(p.grad.view_as(views[i]))
+                    else:
+                        cp.append(i)
+                elif wg is None or id(p) not in wg.touched:
                     views[i].zero_()
             dst = [views[i] for i in cp]
             src = [fl.params[i].grad for i in cp]

@@ -70,14 +70,20 @@ class ConsensusTrainer:
                 and e.device.type == "cuda" and self.cfg.dtype == "bf16"):
             return self._batched_step()
         total = None
-        for v in range(e.V):
-            e.bind_worker(v)
-            with t.phase("data"):
-                batch = self._worker_batch(v)
-            with t.phase("fwd_bwd"):
-                loss = self.task.loss_fn(self.model, batch)
-                loss.backward()
-            total = loss.detach() if total is None else total + loss.detach()
+        try:
+            for v in range(e.V):
+                e.bind_worker(v)
+                with t.phase("data"):
+                    batch = self._worker_batch(v)
+                with t.phase("fwd_bwd"):
+                    loss = self.task.loss_fn(self.model, batch)
+                    loss.backward()
+                total = loss.detach() if total is None else total + loss.detach()
+        except BaseException:
+            # the direct-gradient destination zero_grad() activated is module-global: never
+            # leave it active (keyed by id(p), reusable after GC) past a failed step
+            e.abort_step()
+            raise
         with t.phase("exchange_aggregate_update"):
             e.step()
         return total / e.V
