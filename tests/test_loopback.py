@@ -109,6 +109,29 @@ def _loopback_worker(_rank, backend, device, dtype, steps, out_path):
         scale = float(oracle.abs().max())
         res["cases"].append({"case": ["gossip", graph], "mix_err": err, "scale": scale,
                              "loop_calls": ms["loop"][2], "plain_calls": ms["plain"][2]})
+    # delayed gossip: the end-of-step mix on a side stream, waited per block by the next forward
+    # (param_prefetch), must be bit-identical to the same mix waited for at once
+    for graph in GOSSIP:
+        outs = {}
+        for pf in (True, False):
+            cfg = _cfg("mean", "gossip", 1, 0, 3)
+            cfg.dtype = dtype
+            cfg.backend = backend
+            cfg.topology.gossip_graph = graph
+            cfg.topology.gossip_async = True
+            cfg.topology.param_prefetch = pf
+            tr = ConsensusTrainer(cfg, info=info)
+            tr.fit(3, log_every=0)
+            tr.engine.wait_params()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            outs[pf] = ([p.detach().float().cpu().clone() for p in tr.model.parameters()],
+                        tr.engine.master.detach().cpu().clone(), tr.engine.param_prefetch)
+            tr.close()
+        same = (all(torch.equal(a, b) for a, b in zip(outs[True][0], outs[False][0]))
+                and torch.equal(outs[True][1], outs[False][1]))
+        res["cases"].append({"case": ["gossip_async", graph], "bit_identical": same,
+                             "prefetch": outs[True][2]})
     with open(out_path, "w") as fh:
         json.dump(res, fh)
     dist.destroy_process_group()
@@ -124,6 +147,10 @@ def _run(tmp_path, backend, device, dtype, steps=3):
 def _check(res, backend):
     assert res["backend"] == backend
     for c in res["cases"]:
+        if c["case"][0] == "gossip_async":
+            assert c["bit_identical"], c
+            assert c["prefetch"] == (backend == "nccl"), c   # the side-stream mix: GPU only
+            continue
         if c["case"][0] == "gossip":
             assert c["mix_err"] <= 1e-6 * max(c["scale"], 1.0), c
             if backend == "nccl":   # gloo has no self pairs: the engine copies instead
