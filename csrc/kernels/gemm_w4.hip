@@ -24,7 +24,9 @@
 // PFLOP/s = hipBLASLt: the MFMA ceiling at the clock the chip holds) vs 1.31 ms in that build --
 // with no partner wave on the SIMD, every global_load_lds issue (~100+ cycles among 16 fragment
 // reads, MI355X_MICROARCH.md) stalls the MFMA pipe. Register staging instead of LDS-DMA did not
-// fit: 128 fragment + 32 staging VGPRs next to 256 AGPR accumulators spilled.
+// fit: 128 fragment + 32 staging VGPRs next to 256 AGPR accumulators spilled, and so did a split
+// schedule with B double-buffered, A in two halves and 32 staging VGPRs (~180 live VGPRs): hipcc
+// shuffles values between the VGPR and AGPR halves and spills the staging registers to scratch.
 //
 // Schedule:
 //   * K advances in 32-deep sub-stages through a 4-deep LDS ring (4 x 32 KB: A image 16 KB, B image
