@@ -13,6 +13,8 @@
 // <= 2048 workgroups of 256 threads. Row addresses are hoisted out of the loop; padded rows load
 // a clamped (valid) row and are replaced by +inf with a select, so no per-row branch sits
 // between the loads (hipcc would otherwise wait vmcnt(0) per row).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -333,9 +335,18 @@ __global__ __launch_bounds__(kBlock) void agg_weighted_multi(SrcArgs s, UpdArgs 
 }
 
 // ----------------------------------------------------------------------------- dispatch
+// CML_AGG_GRID_CAP: the most workgroups of an update launch (default 0 = no cap: one vector per
+// thread, the form that streams fastest on MI355X -- tools/diag/hbm_copy.py: a one-pass copy
+// 6.0-6.6 TB/s vs 4.7-5.7 for grid-stride loops; the fused rule + SGD update 8.6-12.7 % faster
+// than at the former cap of 2048 workgroups, profiles/r06_13/agg_*.jsonl).
 static inline int grid_for(int64_t nvec) {
+  static const int cap = [] {
+    const char* e = getenv("CML_AGG_GRID_CAP");
+    return e ? atoi(e) : 0;
+  }();
   int64_t b = (nvec + kBlock - 1) / kBlock;
-  if (b > 2048) b = 2048;
+  if (cap > 0 && b > cap) b = cap;
+  if (b > (1LL << 30)) b = 1LL << 30;
   if (b < 1) b = 1;
   return static_cast<int>(b);
 }

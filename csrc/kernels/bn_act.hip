@@ -11,6 +11,8 @@
 // instruction is a dense 1-KiB wave access. Per-workgroup partial sums go to a [nb][2][C] slab
 // that a per-channel finalize kernel folds in fp64 in block order (deterministic). Variance uses
 // sums shifted by the first row's value (cancellation-safe for post-conv activations).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -547,10 +549,22 @@ __global__ __launch_bounds__(kBT) void bn_bwd_apply2_kernel(const bf16* __restri
   }
 }
 
+// CML_BN_GRID_CAP: the most workgroups an apply pass launches (default 2048: grid-stride loops
+// with two rows in flight; 0 = no cap, one row iteration per workgroup). A/B switch.
+int apply_cap() {
+  static const int v = [] {
+    const char* e = getenv("CML_BN_GRID_CAP");
+    return e ? atoi(e) : 2048;
+  }();
+  return v;
+}
+
 int apply_grid(int64_t M, int C) {
   const int rpi = kBT / (C / 8);
   int64_t b = (M + rpi - 1) / rpi;
-  if (b > 2048) b = 2048;
+  const int cap = apply_cap();
+  if (cap > 0 && b > cap) b = cap;
+  if (b > (1LL << 30)) b = 1LL << 30;
   return static_cast<int>(b < 1 ? 1 : b);
 }
 

@@ -9,6 +9,8 @@
 // sums go to a per-workgroup slab and the mix kernel's workgroups each fold the slab (<= 2048
 // values, L2-resident) in a fixed order, so the result is deterministic and needs no extra
 // launch or host sync.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -212,7 +214,11 @@ void gossip_k(float* master, void* param_out, void* param_out2, const Nbrs<T>& n
   float* part = reinterpret_cast<float*>(work);
   const int nb_blocks = nblocks(D / 8, kMaxBlk);
   if (clip > 0.f) nbr_sqdist_kernel<T, K><<<nb_blocks, kBlk, 0, stream>>>(master, nb, D, part);
-  gossip_mix_kernel<T, K><<<nblocks(D / 8, 2048), kBlk, 0, stream>>>(
+  static const int cap = [] {   // CML_GOSSIP_GRID_CAP (default 0: one vector per thread, the
+    const char* e = getenv("CML_GOSSIP_GRID_CAP");   // fastest streaming form; 2048: the former
+    return e ? atoi(e) : 0;                          // grid-stride launch)
+  }();
+  gossip_mix_kernel<T, K><<<nblocks(D / 8, cap > 0 ? cap : (1 << 30)), kBlk, 0, stream>>>(
       master, reinterpret_cast<T*>(param_out), reinterpret_cast<T*>(param_out2), nb, D, w0, clip,
       part, nb_blocks);
 }

@@ -17,6 +17,8 @@
 //   * SwiGLU: silu(a) * b over the fused [M, 2F] gate|up projection, backward in one pass.
 #include <math.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -772,9 +774,15 @@ __global__ __launch_bounds__(kTB) void colsum_partial_kernel(const bf16* __restr
   }
 }
 
+// CML_STREAM_GRID_CAP: the most workgroups of an elementwise launch (default 8192; 0 = no cap)
 int stream_grid(int64_t work_items) {
+  static const int cap = [] {
+    const char* e = getenv("CML_STREAM_GRID_CAP");
+    return e ? atoi(e) : 8192;
+  }();
   int64_t b = (work_items + kTB - 1) / kTB;
-  if (b > 8192) b = 8192;
+  if (cap > 0 && b > cap) b = cap;
+  if (b > (1LL << 30)) b = 1LL << 30;
   return static_cast<int>(b < 1 ? 1 : b);
 }
 
