@@ -704,13 +704,19 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
 
 
 # own data gradient (gemm.hip against the transposed weight) for bias-free linears up to this
-# many weight elements: wqkv / wo of Llama-3-8B run 1.13-1.17x hipBLASLt there, the larger
-# w13 / w2 / output-head weights tie (profiles/r05_03/llama_gemm.jsonl)
-_NB_OWN_DGRAD_MAX = 32 * 1024 * 1024
+# many weight elements. With gemm.hip's grouped tile order (round 6) its data gradients run
+# 1.05-1.31x hipBLASLt on every Llama-3-8B weight before the transpose: wqkv / wo / w2 (<= 64 M
+# elements) still win with it, the w13 / output-head ones tie (profiles/r06_16/llama_gemm.jsonl)
+_NB_OWN_DGRAD_MAX = 64 * 1024 * 1024
+# own forward (gemm.hip NT, x W^T as stored) up to this many weight elements: Llama-3-8B wqkv
+# 1.37 vs 1.31 PFLOP/s for hipBLASLt, wo 1.35 vs 1.40; the larger w13 / w2 / output head stay on
+# hipBLASLt (1.43-1.51 vs own 1.43-1.46) (profiles/r06_16/llama_gemm.jsonl)
+_NB_OWN_FWD_MAX = 32 * 1024 * 1024
 
 
 class _LinearNBFn(torch.autograd.Function):
-    """y = x W^T without bias (Llama's projections), forward on hipBLASLt (NT, its best layout).
+    """y = x W^T without bias (Llama's projections): forward on gemm.hip for weights up to
+    _NB_OWN_FWD_MAX elements, else hipBLASLt (NT, its best layout).
     Backward: dx = dy W on gemm.hip for weights up to _NB_OWN_DGRAD_MAX elements, else hipBLASLt;
     dW = dy^T x as an NT GEMM on transposed operands -- (dy^T) (x^T)^T, two bandwidth-bound
     transposes + hipBLASLt NT at 1.3-1.57 PFLOP/s instead of its dy^T x kernels at 0.9-1.15
@@ -720,6 +726,12 @@ class _LinearNBFn(torch.autograd.Function):
     def forward(ctx, x, w):
         ctx.save_for_backward(x, w)
         ctx.param = w   # the Parameter itself (its id keys the direct-gradient destination)
+        N, K = w.shape
+        if x.is_contiguous() and w.numel() <= _NB_OWN_FWD_MAX:
+            x2 = x.view(-1, K)
+            if _own_gemm(x2.shape[0], N, K) and lib().gemm_nt_pick(x2.shape[0], N, K) == 256 \
+                    and _al16(x2, w):
+                return lib().gemm_nt(x2, w, 0).view(*x.shape[:-1], N)
         return F.linear(x, w)
 
     @staticmethod

@@ -41,7 +41,32 @@ BNGeom geom(int64_t M, int C) {
   return g;
 }
 
-__device__ __forceinline__ void ld8(const bf16* p, float (&o)[8]) { load_vec<bf16, 8>(p, o); }
+// Every activation the BN passes read is read once per pass: CML_BN_NT = 1 makes those loads
+// nontemporal (A/B switch, a device flag set once per process before the first BN launch)
+__device__ int g_bn_nt = 0;
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ld8(const bf16* p, float (&o)[8]) {
+  if (g_bn_nt) {
+    const v4u_t t = __builtin_nontemporal_load(reinterpret_cast<const v4u_t*>(p));
+    const uint32_t w[4] = {t[0], t[1], t[2], t[3]};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[2 * i] = __uint_as_float(w[i] << 16);
+      o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  } else {
+    load_vec<bf16, 8>(p, o);
+  }
+}
+void bn_nt_init() {
+  static const bool done = [] {
+    const char* e = getenv("CML_BN_NT");
+    const int v = e ? atoi(e) : 0;
+    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bn_nt), &v, sizeof(int));
+    return true;
+  }();
+  (void)done;
+}
 
 // Fold per-thread accumulators [8] x 2 across the rows of a workgroup (same channel group) and
 // write one [2][C] partial per workgroup.
@@ -579,6 +604,7 @@ hipError_t launch_bn_fwd(const void* x, const void* res, void* y, void* mask, in
                          const void* gamma, const void* beta, float* mean, float* invstd,
                          float* rmean, float* rvar, float eps, float momentum, int relu,
                          int training, void* work, hipStream_t st) {
+  bn_nt_init();
   if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1) return hipErrorInvalidValue;
   if (mask && !(res && relu)) return hipErrorInvalidValue;
   const bf16* xb = reinterpret_cast<const bf16*>(x);
@@ -640,6 +666,7 @@ hipError_t launch_bn_bwd(const void* dy, const void* dy2, const void* x, const v
                          const void* beta, const float* mean, const float* invstd, void* dgamma,
                          void* dbeta, float* sdz, float* sdzx, int relu, void* work,
                          hipStream_t st) {
+  bn_nt_init();
   if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1) return hipErrorInvalidValue;
   const int rm = !relu ? RM_NONE : (mask ? RM_MASK : RM_RECOMP);
   const bf16* d = reinterpret_cast<const bf16*>(dy);
@@ -684,6 +711,7 @@ __global__ __launch_bounds__(256) void bn_affine_kernel(const uint16_t* __restri
 
 hipError_t launch_bn_affine(const void* gamma, const void* beta, const float* mean,
                             const float* invstd, int C, float* sc, float* bi, hipStream_t st) {
+  bn_nt_init();
   if (C < 1) return hipErrorInvalidValue;
   bn_affine_kernel<<<(C + 255) / 256, 256, 0, st>>>(reinterpret_cast<const uint16_t*>(gamma),
                                                    reinterpret_cast<const uint16_t*>(beta), mean,
@@ -695,6 +723,7 @@ hipError_t launch_bn_bwd_apply(const void* dy, const void* x, void* dx, int64_t 
                                const void* gamma, const void* beta, const float* mean,
                                const float* invstd, const float* sdz, const float* sdzx,
                                hipStream_t st) {
+  bn_nt_init();
   if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1) return hipErrorInvalidValue;
   bn_bwd_apply_kernel<RM_RECOMP, false, false><<<apply_grid(M, C), kBT, 0, st>>>(
       reinterpret_cast<const bf16*>(dy), nullptr, reinterpret_cast<const bf16*>(x), nullptr,
@@ -709,6 +738,7 @@ hipError_t launch_bn_fwd2(const void* x1, const void* x2, void* y, void* mask, i
                           float* invstd2, float* rmean1, float* rvar1, float* rmean2,
                           float* rvar2, float eps, float momentum, int training, void* work,
                           hipStream_t st) {
+  bn_nt_init();
   if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1) return hipErrorInvalidValue;
   const bf16* a = reinterpret_cast<const bf16*>(x1);
   const bf16* b = reinterpret_cast<const bf16*>(x2);
@@ -742,6 +772,7 @@ hipError_t launch_bn_bwd2(const void* dy, const void* dy2, const void* x1, const
                           const float* invstd1, const float* mean2, const float* invstd2,
                           void* dgamma1, void* dbeta1, void* dgamma2, void* dbeta2, float* sdz,
                           float* sdzx1, float* sdz_b, float* sdzx2, void* work, hipStream_t st) {
+  bn_nt_init();
   if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1 || !mask) return hipErrorInvalidValue;
   const BNGeom g = geom(M, C);
   float* part1 = reinterpret_cast<float*>(work);
@@ -773,6 +804,7 @@ hipError_t launch_bn_bwd2(const void* dy, const void* dy2, const void* x1, const
 hipError_t launch_bn_stats(const void* x, int64_t M, int C, float* mean, float* invstd,
                            float* rmean, float* rvar, float eps, float momentum, void* work,
                            hipStream_t st) {
+  bn_nt_init();
   if (C % 8 != 0 || C / 8 > kBT || (kBT % (C / 8)) != 0 || M < 1) return hipErrorInvalidValue;
   const bf16* xb = reinterpret_cast<const bf16*>(x);
   const BNGeom g = geom(M, C);

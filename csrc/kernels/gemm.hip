@@ -96,7 +96,19 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   const int ntn = a.N / TN;
   const int G = (a.M / TM) * ntn, b = blockIdx.x, xcd = b & 7, q8 = G >> 3, r8 = G & 7;
   const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int mtile = t / ntn, ntile = t - mtile * ntn;
+  // a.gm > 1: groups of gm m-tiles with m fastest, so the tiles an XCD runs at once form a
+  // gm x (32 / gm) block (each A panel serves 32 / gm tiles, each B panel gm) instead of one m-row
+  int mtile, ntile;
+  if (a.gm > 1) {
+    const int mtn = static_cast<int>(a.M / TM);
+    const int grp = t / (a.gm * ntn), gi = t - grp * (a.gm * ntn);
+    const int gmr = min(a.gm, mtn - grp * a.gm);
+    mtile = grp * a.gm + gi % gmr;
+    ntile = gi / gmr;
+  } else {
+    mtile = t / ntn;
+    ntile = t - mtile * ntn;
+  }
   const int m0 = mtile * TM, n0 = ntile * TN;
   const int nk = a.K / kBK;
 
@@ -516,8 +528,22 @@ int tall_min_tiles() {
 }
 }  // namespace
 
-hipError_t launch_gemm_nt(const GemmArgs& a, int ep, hipStream_t st) {
-  if (!gemm_nt_eligible(a.M, a.N, a.K) || !check_ptrs(a, ep)) return hipErrorInvalidValue;
+// CML_GEMM_GM: m-tiles per tile group of the plain (non-conv) GEMM (default 8; 0 / 1: n
+// fastest, the round-5 order). An XCD then runs an 8 (m) x 4 (n) block of tiles instead of one
+// m-row: 8192^3 1.28 -> 1.35 PFLOP/s, Llama-3-8B w13 / output-head forwards 1.34 -> 1.44-1.46
+// (hipBLASLt 1.46-1.49 on that box), profiles/r06_15/
+int gemm_gm() {
+  static const int v = [] {
+    const char* e = getenv("CML_GEMM_GM");
+    return e ? atoi(e) : 8;
+  }();
+  return v;
+}
+
+hipError_t launch_gemm_nt(const GemmArgs& a0, int ep, hipStream_t st) {
+  if (!gemm_nt_eligible(a0.M, a0.N, a0.K) || !check_ptrs(a0, ep)) return hipErrorInvalidValue;
+  GemmArgs a = a0;
+  a.gm = gemm_gm();
   return launch_tm<256>(a, ep, st);
 }
 

@@ -586,6 +586,7 @@ struct GemmArgs {
   // the BN + ReLU backward that y feeds (z = sz [M][N], ReLU bit z ep_sc + ep_bi > 0, shift = mean)
   int conv, C, H, W;       // H, W: the output grid
   int s2, IH, IW;         // conv: stride 2 with an IH x IW input grid (s2 = 1), else unused
+  int gm;                 // gemm.hip tile order: > 1 = groups of gm m-tiles, m fastest
   const uint16_t* zero;
   const float* shift;
   const uint16_t* sz;
