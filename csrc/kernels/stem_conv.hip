@@ -28,6 +28,7 @@
 //          blocks 0, 1) x (kernel rows 0-3 | 4-6), 7 accumulators per SIMD.
 #include <math.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -112,6 +113,12 @@ __device__ __forceinline__ void stage_input(const uint16_t* __restrict__ x, uint
         v[k][1] = src[1];
         v[k][2] = src[2];
       }
+      // all loads in flight before the first LDS write: hipcc sinks each load into the guarded
+      // write block that uses it (one memory round trip per item); the empty asm consumes them here
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(v[k][i].x), "+v"(v[k][i].y));
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int e = e0 + k * nthr;
@@ -308,7 +315,12 @@ __device__ __forceinline__ int chunk_off(int rho, int ch) {
 // route to it. (Per-pixel window loads straight to registers needed 4 x 24 B per pixel and spilled.)
 constexpr int kPR = 6, kPC = 10;                      // pooled rows / cols of a chunk's windows
 constexpr int kPoolLds = kPR * kPC * (kCo * 2 + kCo);  // gradient [60][64] bf16 + argmax [60][64] B
-template <int C, bool VEC, int OWC, bool GATHER>
+// CLS (GATHER only): staging pixels are dealt to waves by pooled-window parity class -- (row & 1,
+// col & 1) of a wave's pixels is wave-uniform, so a wave visits only the 1, 2 or 4 windows that
+// can route to them (the per-pixel form evaluates all 4 per pixel, masked by tap); the SIMD
+// partners w, w + 4 take complementary classes: (even, even) + (odd, odd) = 1 + 4 windows,
+// (even, odd) + (odd, even) = 2 + 2, instead of 4 + 4
+template <int C, bool VEC, int OWC, bool GATHER, bool CLS = false>
 __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restrict__ g,
                                                         const uint16_t* __restrict__ z,
                                                         const uint16_t* __restrict__ x,
@@ -346,6 +358,13 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
   // a chunk is an 8 x 16 block of output pixels, pixel rho = 16 row + col: the pixel rows of
   // k-step ks's transposed reads, rho = 16 ks + 8 h + 4 e + q, are row ks, col 8 h + 4 e + q
   const int cc = tid & 7, srho = tid >> 3;             // staging: pixels srho, srho + 64
+  // CLS: class (pr, pc) = (wave >> 2, pr ^ (wave >> 1 & 1)), pixel rows pr + 2 (wave & 1) + 4 j,
+  // columns pc + 2 (lane >> 3)
+  const int cpr = wave >> 2, cpc = cpr ^ ((wave >> 1) & 1);
+  auto pix_of = [&](int j) {
+    if constexpr (CLS) return (cpr + 2 * (wave & 1) + 4 * j) * 16 + cpc + 2 * (lane >> 3);
+    else return srho + 64 * j;
+  };
   // g is staged as it is and mean(g) enters the finalize through the column sums of the input
   // patches (colA): staging g - mean(g) rounded every unrouted pixel's 0 - mean(g) to the same
   // bf16 value, a per-channel bias whose share of dW grew with the batch (profiles/r03_26/)
@@ -381,7 +400,7 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
     const int oyend = min(OH, oy0 + kTYB);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int rho = srho + 64 * j;
+      const int rho = pix_of(j);
       const int oy = oy0 + 8 * cy + (rho >> 4), ox = 16 * cx + (rho & 15);
       okv[j] = tl < ntiles && oy < oyend && ox < OW;
       const int pix = okv[j] ? (n * OH + oy) * OW + ox : 0;
@@ -425,15 +444,17 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
         if constexpr (GATHER) {
           // pixel (r, c) of the chunk (oyc, oxc even): windows (r + 1) / 2 + 1 - a, (c + 1) / 2 +
           // 1 - b of the tile, tap (ta + 2a, tb + 2b) with ta = (r + 1) & 1, tb = (c + 1) & 1
-          const int rr = (srho + 64 * j) >> 4, rc = (srho + 64 * j) & 15;
+          const int rr = pix_of(j) >> 4, rc = pix_of(j) & 15;
           const int lr = ((rr + 1) >> 1) + 1, lc = ((rc + 1) >> 1) + 1;
-          const int ta = (rr + 1) & 1, tb = (rc + 1) & 1;
+          // CLS: the parities come from the (scalar) wave index, so the skips below are uniform
+          const int ta = CLS ? 1 - cpr : (rr + 1) & 1, tb = CLS ? 1 - cpc : (rc + 1) & 1;
 #pragma unroll
           for (int k = 0; k < 8; ++k) gf[k] = 0.f;
 #pragma unroll
           for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) {
+              if (CLS && ((a == 1 && ta == 1) || (b == 1 && tb == 1))) continue;   // tap 3: none
               const int tta = ta + 2 * a, ttb = tb + 2 * b;
               const uint32_t me = tta <= 2 && ttb <= 2 ? static_cast<uint32_t>(3 * tta + ttb) : 0x100u;
               const int w = (lr - a) * kPC + (lc - b);
@@ -477,7 +498,7 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
           xw[k] = static_cast<uint32_t>(f2bf(x0)) | (static_cast<uint32_t>(f2bf(x1)) << 16);
           cw[k] = static_cast<uint32_t>(f2bf(c0)) | (static_cast<uint32_t>(f2bf(c1)) << 16);
         }
-        const int rho = srho + 64 * j;
+        const int rho = pix_of(j);
         *reinterpret_cast<uint4*>(gbuf + chunk_off(rho, cc)) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
         *reinterpret_cast<uint4*>(xbuf + chunk_off(rho, cc)) = make_uint4(xw[0], xw[1], xw[2], xw[3]);
       }
@@ -581,6 +602,315 @@ __global__ __launch_bounds__(kBT) void stem_wgrad_kernel(const uint16_t* __restr
       for (int k = 0; k < kBT / 8; ++k) s += red[k * kCo + tid];
       pw[2 * kCo * kKP + kCo + tid] = s;
     }
+  }
+}
+
+// ------------------------------------------------------- backward, producer / consumer form
+// stem_wgrad_kernel<3, true, OWC, true> (the pool-gradient gather at a fixed width, OH % 16 == 0)
+// with the two halves of the workgroup in fixed roles instead of alternating phases: waves 0-3
+// (producers) stage chunk s -- pooled-gradient gather, BN terms, the bf16 g / xhat images -- while
+// waves 4-7 (consumers) run chunk s - 1's MFMAs; one barrier per chunk. Each SIMD holds one wave
+// of each role (w, w + 4), so its vector ALU (staging) and matrix pipe (products) work side by
+// side; the alternating form ran them one after the other (rocprofv3 at batch 2560: MFMA busy
+// 23 %, 42 % of wave time waiting, profiles/r06_19/). Chunk images and pooled tiles have two
+// buffers each (pooled tile s + 1 is written during chunk s, so the one barrier orders it); the
+// single input tile is restaged by all waves at a band change, between two barriers. A producer
+// thread stages 4 pixels, one per pooled-window parity class (row & 1, col & 1) -- a compile-time
+// constant per item, so each item visits exactly its 1, 2 or 4 windows. A consumer owns one M
+// block (g or xhat x channel half) over all 7 kernel rows. Same partial layout and the same
+// summation order per accumulator as the alternating kernel; the BN sums (s1, s2) are per-thread
+// in a different pixel order.
+constexpr int kPoolBuf = kPR * kPC * (kCo * 2 + kCo);      // one pooled tile: gradient + argmax
+constexpr int kChunkBuf = 2 * kCh * 128;                   // one chunk's g and xhat images
+template <int OWC>
+constexpr int pc_tile_bytes() { return (tile_rows(kTYB) * tile_cols(OWC) * 8 + 15) & ~15; }
+template <int OWC>
+constexpr int pc_lds() { return 2 * kChunkBuf + pc_tile_bytes<OWC>() + 2 * kPoolBuf; }
+
+template <int OWC>
+__global__ __launch_bounds__(kBT) void stem_wgrad_pc_kernel(const uint16_t* __restrict__ g,
+                                                           const uint16_t* __restrict__ z,
+                                                           const uint16_t* __restrict__ x,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           float* __restrict__ part, int N, int H,
+                                                           int W, int OH,
+                                                           const uint8_t* __restrict__ pidx, int PH,
+                                                           int PW, int abl) {
+  static_assert(OWC % 16 == 0 && pc_lds<OWC>() <= 160 * 1024, "stem_wgrad_pc shape");
+  constexpr int OW = OWC, WT = tile_cols(OWC);
+  constexpr int ncx = OWC / 16, nch = 2 * ncx;          // chunks per band (cy 0..1, cx)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* cbuf = smem;                                     // [2][g | xhat] chunk images
+  uint2* tile = reinterpret_cast<uint2*>(smem + 2 * kChunkBuf);
+  char* pbuf = smem + 2 * kChunkBuf + pc_tile_bytes<OWC>();   // [2] pooled tiles
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool prod = wave < 4;
+  const int bands = OH / kTYB;
+  const int ntiles = N * bands;
+  const int mytiles =
+      static_cast<int>(blockIdx.x) < ntiles ? (ntiles - 1 - static_cast<int>(blockIdx.x)) / gridDim.x + 1 : 0;
+  const int S = mytiles * nch;
+  // chunk s of this workgroup -> image, band origin, chunk (cy, cx); false (clamped) past the end
+  auto chunk_pos = [&](int s, int& n, int& oy0, int& cy, int& cx) {
+    const int k = s / nch, ch = s - k * nch;
+    const bool ok = s < S;
+    const int tl = ok ? static_cast<int>(blockIdx.x) + k * static_cast<int>(gridDim.x)
+                      : static_cast<int>(blockIdx.x) % (ntiles > 0 ? ntiles : 1);
+    n = tl / bands;
+    oy0 = (tl - n * bands) * kTYB;
+    cy = ch >= ncx ? 1 : 0;
+    cx = ch - cy * ncx;
+    return ok;
+  };
+
+  // ---- producer state: channel group cc, column pair pk, row pair pw (pixel row pr + 2 pw,
+  // column pc + 2 pk of class j = 2 pr + pc)
+  const int cc = tid & 7, pk = (tid >> 3) & 7, pwv = wave & 3;
+  float mu[8], is[8], s2[8], s1[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    is[k] = invstd[8 * cc + k];
+    mu[k] = -mean[8 * cc + k] * is[k];
+    s2[k] = 0.f;
+    s1[k] = 0.f;
+  }
+  // register sets of even / odd chunks (A / B): z of chunk s is loaded two iterations ahead, the
+  // pooled tile of chunk s three ahead (it is written to LDS one iteration before it is read)
+  uint4 zA[4], zB[4];
+  struct PoolRegs {
+    uint4 v[2];
+    uint2 i[2];
+    bool ok[2];
+  } pA, pB;
+  auto fetch_z = [&](uint4 (&zv)[4], int s) {
+    int n, oy0, cy, cx;
+    const bool ok = chunk_pos(s, n, oy0, cy, cx);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = (j >> 1) + 2 * pwv, col = (j & 1) + 2 * pk;
+      const int pix = ok ? (n * OH + oy0 + 8 * cy + row) * OW + 16 * cx + col : 0;
+      zv[j] = *reinterpret_cast<const uint4*>(z + static_cast<int64_t>(pix) * kCo + 8 * cc);
+    }
+  };
+  // pooled tile items: window e = tid / 8 + 32 u (60 of 64 used), channels 8 cc ..
+  auto fetch_pool = [&](PoolRegs& pr, int s) {
+    int n, oy0, cy, cx;
+    const bool ok = chunk_pos(s, n, oy0, cy, cx);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = (tid >> 3) + 32 * u;
+      const int pj = (oy0 + 8 * cy) / 2 - 1 + e / kPC, pi = 8 * cx - 1 + e % kPC;
+      const bool pok = ok && e < kPR * kPC && pj >= 0 && pj < PH && pi >= 0 && pi < PW;
+      pr.ok[u] = pok;
+      const int64_t po =
+          ((static_cast<int64_t>(pok ? n : 0) * PH + (pok ? pj : 0)) * PW + (pok ? pi : 0)) * kCo +
+          8 * cc;
+      pr.v[u] = *reinterpret_cast<const uint4*>(g + po);
+      pr.i[u] = *reinterpret_cast<const uint2*>(pidx + po);
+    }
+  };
+  // the buffer parity of chunk s is a compile-time constant at every call (PAR = s & 1): the two
+  // halves of the unrolled producer loop then differ in their LDS offsets, so they are not merged
+  // back into one body (hipcc did, rotating the A / B sets through copies that waited on the loads)
+  auto put_pool = [&](const PoolRegs& pr, auto par_c) {   // a chunk's tile -> pooled buffer PAR
+    constexpr int PAR = decltype(par_c)::value;
+    char* pg = pbuf + PAR * kPoolBuf;
+    char* pi = pg + kPR * kPC * 128;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = (tid >> 3) + 32 * u;
+      if (e < kPR * kPC) {   // windows outside the pooled image route nothing (argmax 0xff)
+        *reinterpret_cast<uint4*>(pg + e * 128 + 16 * cc) =
+            pr.ok[u] ? pr.v[u] : make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint2*>(pi + e * 64 + 8 * cc) =
+            pr.ok[u] ? pr.i[u] : make_uint2(0xffffffffu, 0xffffffffu);
+      }
+    }
+  };
+  auto produce = [&](const uint4 (&zv)[4], auto par_c) {    // a chunk -> chunk buffer PAR
+    constexpr int PAR = decltype(par_c)::value;
+    const char* pg = pbuf + PAR * kPoolBuf;
+    const char* pi = pg + kPR * kPC * 128;
+    char* gb = cbuf + PAR * kChunkBuf;
+    char* xb = gb + kCh * 128;
+    auto item = [&](auto j_c) {
+      constexpr int j = decltype(j_c)::value;
+      constexpr int pr = j >> 1, pc = j & 1, ta = 1 - pr, tb = 1 - pc;
+      const int row = pr + 2 * pwv, col = pc + 2 * pk;
+      const int lr = ((row + 1) >> 1) + 1, lc = ((col + 1) >> 1) + 1;
+      float gf[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gf[k] = 0.f;
+#pragma unroll
+      for (int a = 0; a <= pr; ++a)
+#pragma unroll
+        for (int b = 0; b <= pc; ++b) {   // taps (ta + 2 a, tb + 2 b) <= 2: the routing windows
+          const uint32_t me = static_cast<uint32_t>(3 * (ta + 2 * a) + tb + 2 * b);
+          const int w = (lr - a) * kPC + (lc - b);
+          const uint4 pw4v = *reinterpret_cast<const uint4*>(pg + w * 128 + 16 * cc);
+          const uint2 iw = *reinterpret_cast<const uint2*>(pi + w * 64 + 8 * cc);
+          const uint32_t pw4[4] = {pw4v.x, pw4v.y, pw4v.z, pw4v.w};
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t byte = ((k < 4 ? iw.x : iw.y) >> (8 * (k & 3))) & 0xffu;
+            const float d = (k & 1) ? __uint_as_float(pw4[k >> 1] & 0xffff0000u)
+                                    : __uint_as_float(pw4[k >> 1] << 16);
+            gf[k] += byte == me ? d : 0.f;
+          }
+        }
+      const uint32_t zw[4] = {zv[j].x, zv[j].y, zv[j].z, zv[j].w};
+      uint32_t xw[4], cw[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float g0 = gf[2 * k], g1 = gf[2 * k + 1];
+        const float x0 = fmaf(__uint_as_float(zw[k] << 16), is[2 * k], mu[2 * k]);
+        const float x1 = fmaf(__uint_as_float(zw[k] & 0xffff0000u), is[2 * k + 1], mu[2 * k + 1]);
+        s2[2 * k] = fmaf(g0, x0, s2[2 * k]);
+        s2[2 * k + 1] = fmaf(g1, x1, s2[2 * k + 1]);
+        s1[2 * k] += g0;
+        s1[2 * k + 1] += g1;
+        xw[k] = pk_bf16(x0, x1);
+        cw[k] = pk_bf16(g0, g1);
+      }
+      const int rho = row * 16 + col;
+      *reinterpret_cast<uint4*>(gb + chunk_off(rho, cc)) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+      *reinterpret_cast<uint4*>(xb + chunk_off(rho, cc)) = make_uint4(xw[0], xw[1], xw[2], xw[3]);
+    };
+    item(std::integral_constant<int, 0>{});
+    item(std::integral_constant<int, 1>{});
+    item(std::integral_constant<int, 2>{});
+    item(std::integral_constant<int, 3>{});
+  };
+
+  // ---- consumer state: M block mb (0, 1: g channels 0-31 / 32-63; 2, 3: xhat), kernel rows 0-6
+  const int mb = wave & 3;
+  const int h = lane >> 5, r = lane & 31;
+  const int gi = lane & 15, grp = lane >> 4;
+  const int q = gi >> 2, pq = gi & 3;
+  const int chn0 = 4 * (mb & 1) + 2 * (grp & 1) + (pq >> 1);
+  f32x16 acc[7] = {};
+  auto consume = [&](int s) {
+    int n, oy0, cy, cx;
+    chunk_pos(s, n, oy0, cy, cx);
+    const int r0 = 8 * cy, c0 = 16 * cx;
+    const char* abuf = cbuf + (s & 1) * kChunkBuf + (mb < 2 ? 0 : kCh * 128) + 8 * (pq & 1);
+    // B (input tile) address of k-step ks, half e: pixel (r0 + ks, c0 + 8 h + 4 e + q), row ky 0
+    const int bbase = 2 * r0 * WT + 2 * (c0 + 8 * h + q) + 4 * (grp & 1) + pq;
+    s16x4 fa[2][2], fb[2][7][2];
+    auto load = [&](int ks, int buf) {
+      const int rho0 = 16 * ks + 8 * h + q;
+      fa[buf][0] = ld_tr(abuf + chunk_off(rho0, chn0));
+      fa[buf][1] = ld_tr(abuf + chunk_off(rho0 + 4, chn0));
+      const int b0 = bbase + 2 * ks * WT;
+#pragma unroll
+      for (int kk = 0; kk < 7; ++kk) {
+        fb[buf][kk][0] = ld_tr(reinterpret_cast<const char*>(tile + b0 + kk * WT));
+        fb[buf][kk][1] = ld_tr(reinterpret_cast<const char*>(tile + b0 + kk * WT + 8));
+      }
+    };
+    auto step = [&](int buf) {
+      const bf16x8_t A = cat(fa[buf][0], fa[buf][1]);
+#pragma unroll
+      for (int kk = 0; kk < 7; ++kk) acc[kk] = mfma(A, cat(fb[buf][kk][0], fb[buf][kk][1]), acc[kk]);
+    };
+    load(0, 0);
+#pragma unroll 1
+    for (int ks = 0; ks < kCh / 16; ks += 2) {
+      load(ks + 1, 1);
+      step(0);
+      if (ks + 2 < kCh / 16) load(ks + 2, 0);
+      step(1);
+    }
+  };
+
+  // ---- pipeline: iteration s = producers stage chunk s, consumers multiply chunk s - 1. The two
+  // roles run separate loops with the same barrier sequence (wave-uniform roles), so neither
+  // role's registers are live in the other's loop.
+  // abl (timing ablations, CML_STEM_PC_ABL; results are wrong when set): 1 no staging compute,
+  // 2 no products, 4 no input-tile restage
+  auto band_change = [&](int s) {   // consumers enter a new band at chunk s - 1: restage the tile
+    if (s >= 1 && (s - 1) % nch == 0) {
+      int n, oy0, cy, cx;
+      chunk_pos(s - 1, n, oy0, cy, cx);
+      if (!(abl & 4)) stage_input<3, kTYB, true>(x, tile, n, oy0, H, W, WT, tid, kBT);
+      __syncthreads();
+    }
+  };
+  float* pw = part + static_cast<int64_t>(blockIdx.x) * kPartW;
+  if (prod) {
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    fetch_pool(pA, 0);
+    put_pool(pA, P0{});
+    fetch_pool(pB, 1);
+    fetch_pool(pA, 2);
+    fetch_z(zA, 0);
+    fetch_z(zB, 1);
+    __syncthreads();
+    // unrolled by two so the A / B register sets are named statically
+    for (int s = 0; s <= S; s += 2) {
+      band_change(s);
+      if (s < S) {
+        if (!(abl & 1)) produce(zA, P0{});
+        put_pool(pB, P1{});
+      }
+      // loads unconditional (clamped past the end): a path without them would make the compiler's
+      // in-order vmcnt accounting wait for the newest loads at the next use
+      fetch_pool(pB, s + 3);
+      fetch_z(zA, s + 2);
+      __syncthreads();
+      if (s + 1 > S) break;
+      band_change(s + 1);
+      if (s + 1 < S) {
+        if (!(abl & 1)) produce(zB, P1{});
+        put_pool(pA, P0{});
+      }
+      fetch_pool(pA, s + 4);
+      fetch_z(zB, s + 3);
+      __syncthreads();
+    }
+  } else {
+    __syncthreads();
+    for (int s = 0; s <= S; ++s) {
+      band_change(s);
+      if (s >= 1 && !(abl & 2)) consume(s - 1);
+      __syncthreads();
+    }
+    // G [64][224], X [64][224]
+#pragma unroll
+    for (int kk = 0; kk < 7; ++kk)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int co = 32 * (mb & 1) + (i & 3) + 8 * (i >> 2) + 4 * h;
+        pw[(mb >> 1) * kCo * kKP + co * kKP + kk * 32 + r] = acc[kk][i];
+      }
+  }
+
+  // ---- s2 [64], s1 [64] from the producers' per-thread sums
+  float* red = reinterpret_cast<float*>(smem);           // [32 producer rows][64]
+  const int prow = tid >> 3;
+  if (prod) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[prow * kCo + 8 * cc + k] = s2[k];
+  }
+  __syncthreads();
+  if (tid < kCo) {
+    float sum = 0.f;
+    for (int k = 0; k < 32; ++k) sum += red[k * kCo + tid];
+    pw[2 * kCo * kKP + tid] = sum;
+  }
+  __syncthreads();
+  if (prod) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[prow * kCo + 8 * cc + k] = s1[k];
+  }
+  __syncthreads();
+  if (tid < kCo) {
+    float sum = 0.f;
+    for (int k = 0; k < 32; ++k) sum += red[k * kCo + tid];
+    pw[2 * kCo * kKP + kCo + tid] = sum;
   }
 }
 
@@ -800,7 +1130,8 @@ int persistent_grid(const void* fn, int threads, size_t lds, int ntiles) {
 // the backward tile needs > 64 KiB of dynamic LDS: opt in once per kernel instance
 void wgrad_lds_optin() {
   static const bool done = [] {
-    const void* fns[8] = {reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 112, false>),
+    const void* fns[9] = {reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 112, true, true>),
+                          reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 112, false>),
                           reinterpret_cast<const void*>(&stem_wgrad_kernel<3, true, 0, false>),
                           reinterpret_cast<const void*>(&stem_wgrad_kernel<3, false, 0, false>),
                           reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false, 0, false>),
@@ -810,6 +1141,8 @@ void wgrad_lds_optin() {
                           reinterpret_cast<const void*>(&stem_wgrad_kernel<4, false, 0, true>)};
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_wgrad_pc_kernel<112>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, pc_lds<112>());
     return true;
   }();
   (void)done;
@@ -878,12 +1211,25 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
   const int PH = (OH - 1) / 2 + 1, PW = (OW - 1) / 2 + 1;   // the 3x3 / s2 / p1 pool's output
   const bool vec = C == 3 && W % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 7) == 0;
 #define CML_WG(CC, V, OWC, G) stem_wgrad_kernel<CC, V, OWC, G><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, gsum, part, N, H, W, OH, OW, pidx, PH, PW)
+  // CML_STEM_CLS=0: the per-pixel window form of the bench-shape gather instance (A/B)
+  const char* cls_env = std::getenv("CML_STEM_CLS");
+  const bool cls = !(cls_env && cls_env[0] == '0');
 #define CML_WG_ALL(G)                                       \
   if (C == 4) CML_WG(4, false, 0, G);                        \
+  else if (G && cls && vec && OW == 112 && OH % kTYB == 0)   \
+    stem_wgrad_kernel<3, true, 112, true, true><<<grid, kBT, lds, st>>>(gp, zp, xp, mean, invstd, gsum, part, N, H, W, OH, OW, pidx, PH, PW); \
   else if (vec && OW == 112 && OH % kTYB == 0) CML_WG(3, true, 112, G); \
   else if (vec) CML_WG(3, true, 0, G);                       \
   else CML_WG(3, false, 0, G);
-  if (pidx) {
+  // CML_STEM_PC=0: the alternating kernel at the bench shape too (A/B)
+  const char* pc_env = std::getenv("CML_STEM_PC");
+  const bool pc = !(pc_env && pc_env[0] == '0');
+  if (pidx && pc && C == 3 && vec && OW == 112 && OH % kTYB == 0) {
+    const char* abl_env = std::getenv("CML_STEM_PC_ABL");
+    const int abl = abl_env ? std::atoi(abl_env) : 0;
+    stem_wgrad_pc_kernel<112><<<grid, kBT, pc_lds<112>(), st>>>(gp, zp, xp, mean, invstd, part, N,
+                                                               H, W, OH, pidx, PH, PW, abl);
+  } else if (pidx) {
     CML_WG_ALL(true)
   } else {
     CML_WG_ALL(false)

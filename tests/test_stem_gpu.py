@@ -226,3 +226,30 @@ def test_stem_wgrad_pool_gather(cuda, N, C, H, W, two):
     e_gather, e_two = _rel(dw.double(), wq.grad), _rel(dw2.double(), wq.grad)
     assert e_gather < 5e-3, (e_gather, e_two)
     assert e_gather <= 1.25 * e_two + 5e-4, (e_gather, e_two)
+
+
+@pytest.mark.parametrize("N,two", [(3, False), (40, True)])
+def test_stem_wgrad_pc_matches_alternating(cuda, monkeypatch, N, two):
+    """stem_wgrad_pc_kernel (fixed producer / consumer waves, the 224 x 224 bench shape) vs the
+    alternating kernel (CML_STEM_PC=0) on the same inputs. The products are summed in the same
+    order; only the BN sums (s1, s2) take a different per-thread pixel order. N = 40: 280 bands
+    over the persistent grid, so workgroups cross band changes (input tile restaged mid-loop)."""
+    from consensusml_amd.ops.native import lib
+    torch.manual_seed(N)
+    x = torch.randn(N, 3, 224, 224, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, device=cuda) * 0.1).to(torch.bfloat16)
+    gam = torch.empty(64, device=cuda).uniform_(-0.5, 1.5).to(torch.bfloat16)
+    bet = torch.empty(64, device=cuda).uniform_(-0.5, 0.5).to(torch.bfloat16)
+    z, mean, invstd = lib().stem_conv_fwd(x, pack_stem_weight(w), None, None, 1e-5, 0.1, True)
+    y, idx, _, _ = lib().bn_relu_maxpool_fwd(z, gam, bet, None, None, mean, invstd, 1e-5, 0.1,
+                                             False, 3, 2, 1)
+    dy = torch.randn_like(y)
+    dy2 = torch.randn_like(y) if two else None
+    out = {}
+    for pc in ("1", "0"):
+        monkeypatch.setenv("CML_STEM_PC", pc)
+        out[pc] = lib().stem_wgrad_pool(dy, idx, dy2, z, x, mean, invstd, gam)
+    for a, b in zip(out["1"], out["0"]):
+        assert torch.isfinite(a).all()
+        assert _rel(a, b) < 2e-5, _rel(a, b)

@@ -11,6 +11,8 @@ dispatches each, real shapes):
           hd 128, causal)
   gemm    gemm.hip (8 waves) and gemm_w4.hip (4 waves, modes 0 / 2 / 3) at 8192^3 and the Llama
           w13 shapes; gemm128.hip at the BERT per-rank fc2 shape (8192 x 768 x 3072)
+  stem    the stem weight gradient with the pool-gradient gather (stem_wgrad_pool) at the bench
+          shape (batch 2560, 224 x 224), parity-class staging on and off (CML_STEM_CLS)
   wgrad   the LDS-DMA 1x1 weight gradient (wgrad1x1.hip) at ResNet-50 layer-3 (1024 -> 256,
           batch 2048: 401 408 pixels) and a Llama projection (4096 x 4096 over 8192 tokens)
 
@@ -96,6 +98,29 @@ def run_gemm(dev, steps):
     for _ in range(steps):
         L.gemm_nt(a, b, 0, tile=128)
     torch.cuda.synchronize()
+
+
+def run_stem(dev, steps):
+    from consensusml_amd.ops.native import lib
+    from consensusml_amd.ops.stem import pack_stem_weight
+    L = lib()
+    N = 2560
+    x = rnd((N, 224, 224, 3), dev, 14).permute(0, 3, 1, 2)   # channels-last [N, 3, 224, 224]
+    w = (rnd((64, 3, 7, 7), dev, 15).float() * 0.1).bfloat16()
+    gam = (rnd((64,), dev, 16).float() * 0.5 + 1).bfloat16()
+    bet = (rnd((64,), dev, 17).float() * 0.2).bfloat16()
+    z, mean, invstd = L.stem_conv_fwd(x, pack_stem_weight(w), None, None, 1e-5, 0.1, True)
+    y, idx, _, _ = L.bn_relu_maxpool_fwd(z, gam, bet, None, None, mean, invstd, 1e-5, 0.1,
+                                         False, 3, 2, 1)
+    dy = rnd(tuple(y.shape), dev, 18).view(y.shape[0], y.shape[2], y.shape[3], y.shape[1]) \
+        .permute(0, 3, 1, 2)
+    for cls in ("1", "0"):
+        os.environ["CML_STEM_CLS"] = cls
+        for _ in range(steps):
+            L.stem_wgrad_pool(dy, idx, None, z, x, mean, invstd, gam)
+        torch.cuda.synchronize()
+        print("stem cls", cls, flush=True)
+    os.environ.pop("CML_STEM_CLS", None)
 
 
 def run_wgrad(dev, steps):
