@@ -22,6 +22,9 @@ SHAPES = [
     (512, 256, 1, 1, 28, 1), (1024, 256, 1, 1, 14, 5), (1024, 512, 1, 1, 14, 1),
     (1024, 2048, 1, 1, 7, 1),
     (128, 128, 3, 2, 56, 1), (256, 256, 3, 2, 28, 1), (512, 512, 3, 2, 14, 1),
+    # stride-2 1x1 downsamples (layer 4's stays a stride-2 conv in the step; layers 2-3 recompute
+    # from the subsampled input)
+    (1024, 2048, 1, 2, 14, 1), (512, 1024, 1, 2, 28, 0), (256, 512, 1, 2, 56, 0),
 ]
 # the own-kernel (core) set, for the own-vs-own A/B (CML_WGRAD_DMA=0 / 1); calls = 0: not on the
 # library in the step
@@ -70,6 +73,9 @@ def main():
         if k == 1 and s == 1 and (cin == 64 and cout % 256 == 0 or cin % 128 == 0 and cout % 128 == 0):
             def f_own():
                 return lib().wgrad1x1(dy, x, torch.bfloat16)
+        elif k == 1 and s == 2 and lib().wgrad3x3s2_ok(N, hw, hw, cout, cin, 1):
+            def f_own():
+                return lib().wgrad3x3s2(dy, x, torch.bfloat16, taps=1)
         elif k == 3 and s == 2 and hasattr(lib(), "wgrad3x3s2") and lib().wgrad3x3s2_ok(
                 N, hw, hw, cout, cin):
             def f_own():

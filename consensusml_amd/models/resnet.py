@@ -258,7 +258,8 @@ class Bottleneck(nn.Module):
         hw = (x.shape[2] // st) * (x.shape[3] // st)
         if fused_conv1x1_policy(conv.in_channels, conv.out_channels, hw, st, False):
             dg = st == 1 and conv1x1_policy(conv.in_channels, conv.out_channels, hw)[1]
-            own = st == 1 and own_wgrad_ok(conv.in_channels, conv.out_channels)
+            # stride 2: ops.conv._wgrad takes the stride-2 DMA kernel's single-tap form
+            own = own_wgrad_ok(conv.in_channels, conv.out_channels) if st == 1 else True
             z, m, i = fconv.conv1x1_bn_stats(x, conv, bn, st, dg, own, link if dg else None)
             return z, (m, i)
         if st == 1:

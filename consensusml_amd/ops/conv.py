@@ -144,6 +144,13 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, own:
         sc, bi = pro
         x = torch.relu(x.float() * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)).to(x.dtype)
         x = x.contiguous(memory_format=torch.channels_last)
+    N, Ci, H, W = x.shape
+    if (own and stride == 2 and _P().own_wgrad1x1_s2 and x.is_cuda
+            and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and lib().wgrad3x3s2_ok(N, H, W, dy.shape[1], Ci, 1)):
+        # the downsample's weight gradient: the stride-2 DMA kernel with its single tap (2 oh, 2 ow)
+        return lib().wgrad3x3s2(dy, x, w.dtype, _zero_row(dy.device), taps=1).reshape(w.shape)
     _, dw, _ = torch.ops.aten.convolution_backward(
         dy, x, w, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])
     return dw
@@ -809,7 +816,8 @@ def _wgrad3x3_s2(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Te
     at 14 x 14 555-603 vs 644-674; the 128-channel layer-2 conv (128 x 128 tiles, x gathered 2.25x
     and dy re-read per tap through L2) 969 vs 850 stays on MIOpen (Ci < 256)."""
     N, Ci, H, W = x.shape
-    if (_P().own_wgrad3x3_s2 and Ci >= 256 and x.is_cuda and dy.dtype == torch.bfloat16
+    if (_P().own_wgrad3x3_s2 and Ci >= _P().wgrad3x3_s2_min_ci and x.is_cuda
+            and dy.dtype == torch.bfloat16
             and x.dtype == torch.bfloat16
             and lib().wgrad3x3s2_ok(N, H, W, dy.shape[1], Ci)):
         return lib().wgrad3x3s2(dy, x.contiguous(memory_format=torch.channels_last), w.dtype,

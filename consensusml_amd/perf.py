@@ -74,6 +74,9 @@ class PerfPolicy:
                                           # ms/step SLOWER (pass 26, profiles/r03_26/)
     own_wgrad3x3: bool = True             # wgrad3x3.hip weight gradient
     own_wgrad3x3_s2: bool = True          # stride-2 3x3 weight gradient on the wgrad DMA kernel
+    wgrad3x3_s2_min_ci: int = 256         # ... for Ci >= this (the 128-channel layer-2 conv: MIOpen)
+    own_wgrad1x1_s2: bool = True          # stride-2 1x1 (downsample) weight gradient on the same
+                                          # kernel, one tap (was MIOpen)
     own_conv3x3_s2: bool = True           # stride-2 3x3: conv_gemm forward + BN stats, parity-class
                                           # data gradient (+ bn1 backward sums)
     side_wgrad: bool = False              # 3x3 weight gradients on a side stream, concurrent with
@@ -138,6 +141,8 @@ class PerfPolicy:
             bn1_sums_lib_conv1=_env_bool("CML_BN1_SUMS_LIB_CONV1", False),
             own_wgrad3x3=_env_bool("CML_WGRAD3X3", True),
             own_wgrad3x3_s2=_env_bool("CML_WGRAD3X3_S2", True),
+            wgrad3x3_s2_min_ci=int(os.environ.get("CML_WGRAD3X3_S2_MIN_CI", "256")),
+            own_wgrad1x1_s2=_env_bool("CML_WGRAD1X1_S2", True),
             own_conv3x3_s2=_env_bool("CML_CONV3X3_S2", True),
             side_wgrad=_env_bool("CML_SIDE_WGRAD", False),
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),

@@ -1362,18 +1362,19 @@ Tensor wgrad3x3(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
   return dw.permute({0, 3, 1, 2});
 }
 
-bool wgrad3x3s2_ok(int64_t N, int64_t H, int64_t W, int64_t Co, int64_t Ci) {
+bool wgrad3x3s2_ok(int64_t N, int64_t H, int64_t W, int64_t Co, int64_t Ci, int64_t taps) {
   int S = 0;
   return N < (1 << 30) && H < (1 << 15) && W < (1 << 15) && Co < (1 << 20) && Ci < (1 << 20) &&
+         (taps == 9 || taps == 1) &&
          cml::wgrad3x3s2_plan(static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
-                              static_cast<int>(Co), static_cast<int>(Ci), &S);
+                              static_cast<int>(Co), static_cast<int>(Ci), &S, static_cast<int>(taps));
 }
 
 // Weight gradient of a 3x3 / stride 2 / padding 1 conv (wgrad1x1.hip LDS-DMA kernel on the implicit
 // im2col): dy [N, Co, H/2, W/2], x [N, Ci, H, W] NHWC bf16 -> dW [Co, Ci, 3, 3] in `dtype`
-// (channels_last memory).
+// (channels_last memory). taps = 1: a 1x1 / stride 2 / padding 0 conv -> dW [Co, Ci, 1, 1].
 Tensor wgrad3x3s2(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
-                  const optional<Tensor>& zero_in) {
+                  const optional<Tensor>& zero_in, int64_t taps) {
   check_nhwc(x, "x");
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   check_nhwc(dy, "dy");
@@ -1382,12 +1383,12 @@ Tensor wgrad3x3s2(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
                   dy.size(3) * 2 == x.size(3), "wgrad3x3s2: dy [N, Co, H/2, W/2], x [N, Ci, H, W]");
   TORCH_CHECK(dtype == at::kBFloat16 || dtype == at::kFloat, "wgrad3x3s2: bf16 or fp32 output");
   const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1);
-  TORCH_CHECK(wgrad3x3s2_ok(N, H, W, Co, Ci),
+  TORCH_CHECK(wgrad3x3s2_ok(N, H, W, Co, Ci, taps),
               "wgrad3x3s2: no plan for this shape (check wgrad3x3s2_ok first)");
   const c10::DeviceGuard guard(x.device());
   int S = 1;
   cml::wgrad3x3s2_plan(static_cast<int>(N), static_cast<int>(H), static_cast<int>(W),
-                       static_cast<int>(Co), static_cast<int>(Ci), &S);
+                       static_cast<int>(Co), static_cast<int>(Ci), &S, static_cast<int>(taps));
   Tensor zero;
   if (zero_in.has_value() && zero_in->defined()) {
     zero = *zero_in;
@@ -1398,13 +1399,15 @@ Tensor wgrad3x3s2(const Tensor& dy_in, const Tensor& x, at::ScalarType dtype,
   } else {
     zero = at::zeros({256}, x.options());
   }
-  Tensor part = at::empty({S, Co, 9, Ci}, x.options().dtype(at::kFloat));
-  Tensor dw = at::empty({Co, 3, 3, Ci}, x.options().dtype(dtype));
+  const int64_t k = taps == 1 ? 1 : 3;
+  Tensor part = at::empty({S, Co, taps, Ci}, x.options().dtype(at::kFloat));
+  Tensor dw = at::empty({Co, k, k, Ci}, x.options().dtype(dtype));
   CML_CHECK_HIP(cml::launch_wgrad3x3s2(dy.data_ptr(), x.data_ptr(), zero.data_ptr(),
                                        part.data_ptr<float>(), dw.data_ptr(),
                                        dtype == at::kBFloat16, static_cast<int>(N),
                                        static_cast<int>(H), static_cast<int>(W),
-                                       static_cast<int>(Co), static_cast<int>(Ci), cur_stream()));
+                                       static_cast<int>(Co), static_cast<int>(Ci), cur_stream(),
+                                       static_cast<int>(taps)));
   return dw.permute({0, 3, 1, 2});
 }
 
@@ -2526,9 +2529,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dz_b") = py::none(), py::arg("dz_c") = py::none(), py::arg("out") = py::none(),
         "weight gradient of a stride-1 1x1 conv (MFMA, split-K)");
   m.def("wgrad3x3s2_ok", &wgrad3x3s2_ok, py::arg("N"), py::arg("H"), py::arg("W"),
-        py::arg("Co"), py::arg("Ci"));
+        py::arg("Co"), py::arg("Ci"), py::arg("taps") = 9);
   m.def("wgrad3x3s2", &wgrad3x3s2, py::arg("dy"), py::arg("x"), py::arg("dtype"),
-        py::arg("zero") = py::none());
+        py::arg("zero") = py::none(), py::arg("taps") = 9);
   m.def("wgrad3x3", &wgrad3x3, py::arg("dy"), py::arg("x"), py::arg("dtype"),
         py::arg("zero") = py::none(),
         "weight gradient of a 3x3 stride-1 conv (MFMA, split-K, all nine taps per workgroup: "

@@ -43,6 +43,8 @@
 // bwd_preprocess: 84 ms of the 4 x 2048 Llama-3-8B step, profiles/r04_12/llama_kernels.md).
 #include <math.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -173,24 +175,27 @@ __device__ __forceinline__ void work_item(int nblk, int BH, bool heavy_last, int
 }
 
 // ------------------------------------------------------------------------------------- forward
-template <bool CAUSAL>
-__global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FaArgs a) {
+// NWV waves x 32 queries per workgroup: 4 (two workgroups per CU) or 8 (one; each staged K / V
+// tile feeds twice the queries, half the L2 -> LDS traffic per FLOP)
+template <bool CAUSAL, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 8 / NWV) void fa_fwd_kernel(FaArgs a) {
+  constexpr int BQ = 32 * NWV;
   extern __shared__ __attribute__((aligned(16))) char smem[];   // 2 x (K image, V image)
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int S = a.S;
   int qb, bh;
-  work_item((S + kBQ - 1) / kBQ, a.B * a.H, CAUSAL, qb, bh);
+  work_item((S + BQ - 1) / BQ, a.B * a.H, CAUSAL, qb, bh);
   const int b = bh / a.H, hh = bh - b * a.H, kvh = hh / (a.H / a.KV);
-  const int q0 = qb * kBQ, qrow = q0 + 32 * w + r, qmin = q0 + 32 * w;
+  const int q0 = qb * BQ, qrow = q0 + 32 * w + r, qmin = q0 + 32 * w;
   const int64_t kvoff = (static_cast<int64_t>(b) * a.KV + kvh) * S * kD;
   const uint16_t* kg = a.k + kvoff;
   const uint16_t* vg = a.v + kvoff;
-  const int kend = CAUSAL ? min(S, q0 + kBQ) : S;
+  const int kend = CAUSAL ? min(S, q0 + BQ) : S;
   const int nt = (kend + kBK - 1) / kBK;
 
-  stage(kg, kD, 0, S, smem, w, lane);
-  stage(vg, kD, 0, S, smem + kImg, w, lane);
+  stage<NWV>(kg, kD, 0, S, smem, w, lane);
+  stage<NWV>(vg, kD, 0, S, smem + kImg, w, lane);
   bf16x8_t qf[8];   // B operand of S^T = K Q^T: Q[qrow][16 ks + 8 h + j]
   {
     const uint16_t* qp = a.q + (static_cast<int64_t>(bh) * S + min(qrow, S - 1)) * kD + 8 * h;
@@ -209,8 +214,8 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FaArgs a) {
     __syncthreads();
     if (t + 1 < nt) {
       char* nb = smem + ((t + 1) & 1) * 2 * kImg;
-      stage(kg, kD, (t + 1) * kBK, S, nb, w, lane);
-      stage(vg, kD, (t + 1) * kBK, S, nb + kImg, w, lane);
+      stage<NWV>(kg, kD, (t + 1) * kBK, S, nb, w, lane);
+      stage<NWV>(vg, kD, (t + 1) * kBK, S, nb + kImg, w, lane);
     }
     const int k0 = t * kBK;
     if (CAUSAL && k0 > qmin + 31) continue;   // every key of the tile is after every query
@@ -275,25 +280,26 @@ __global__ __launch_bounds__(kThreads, 2) void fa_fwd_kernel(FaArgs a) {
 }
 
 // ------------------------------------------------------------------------------ backward: dQ
-template <bool CAUSAL>
-__global__ __launch_bounds__(kThreads, 2) void fa_dq_kernel(FaArgs a) {
+template <bool CAUSAL, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 8 / NWV) void fa_dq_kernel(FaArgs a) {
+  constexpr int BQ = 32 * NWV;
   extern __shared__ __attribute__((aligned(16))) char smem[];   // 2 x (K image, V image)
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int S = a.S;
   int qb, bh;
-  work_item((S + kBQ - 1) / kBQ, a.B * a.H, CAUSAL, qb, bh);
+  work_item((S + BQ - 1) / BQ, a.B * a.H, CAUSAL, qb, bh);
   const int b = bh / a.H, hh = bh - b * a.H, kvh = hh / (a.H / a.KV);
-  const int q0 = qb * kBQ, qrow = q0 + 32 * w + r, qmin = q0 + 32 * w;
+  const int q0 = qb * BQ, qrow = q0 + 32 * w + r, qmin = q0 + 32 * w;
   const int qc = min(qrow, S - 1);
   const int64_t kvoff = (static_cast<int64_t>(b) * a.KV + kvh) * S * kD;
   const uint16_t* kg = a.k + kvoff;
   const uint16_t* vg = a.v + kvoff;
-  const int kend = CAUSAL ? min(S, q0 + kBQ) : S;
+  const int kend = CAUSAL ? min(S, q0 + BQ) : S;
   const int nt = (kend + kBK - 1) / kBK;
 
-  stage(kg, kD, 0, S, smem, w, lane);
-  stage(vg, kD, 0, S, smem + kImg, w, lane);
+  stage<NWV>(kg, kD, 0, S, smem, w, lane);
+  stage<NWV>(vg, kD, 0, S, smem + kImg, w, lane);
   bf16x8_t qf[8], df[8];
   float dsum;
   {
@@ -327,8 +333,8 @@ __global__ __launch_bounds__(kThreads, 2) void fa_dq_kernel(FaArgs a) {
     __syncthreads();
     if (t + 1 < nt) {
       char* nb = smem + ((t + 1) & 1) * 2 * kImg;
-      stage(kg, kD, (t + 1) * kBK, S, nb, w, lane);
-      stage(vg, kD, (t + 1) * kBK, S, nb + kImg, w, lane);
+      stage<NWV>(kg, kD, (t + 1) * kBK, S, nb, w, lane);
+      stage<NWV>(vg, kD, (t + 1) * kBK, S, nb + kImg, w, lane);
     }
     const int k0 = t * kBK;
     if (CAUSAL && k0 > qmin + 31) continue;
@@ -485,7 +491,7 @@ typedef void (*FaKernel)(FaArgs);
 hipError_t launch_fa(FaKernel kern, const FaArgs& a, int smem, hipStream_t st, int rows = kBQ,
                      int threads = kThreads) {
   // dynamic LDS above the default limit: set once per kernel
-  static const void* done[8] = {};
+  static const void* done[16] = {};
   const void* f = reinterpret_cast<const void*>(kern);
   bool set = false;
   for (const void* d : done) set = set || d == f;
@@ -502,6 +508,15 @@ hipError_t launch_fa(FaKernel kern, const FaArgs& a, int smem, hipStream_t st, i
   const dim3 grid(static_cast<unsigned>(nblk * a.B * a.H));
   kern<<<grid, threads, smem, st>>>(a);
   return hipGetLastError();
+}
+
+// queries per workgroup of the forward and dQ kernels: CML_FA_WAVES = 4 (128) or 8 (256)
+int fa_waves() {
+  static const int w = [] {
+    const char* e = std::getenv("CML_FA_WAVES");
+    return e && std::atoi(e) == 8 ? 8 : 4;
+  }();
+  return w;
 }
 
 bool fa_shape_ok(int B, int H, int KV, int S) {
@@ -525,6 +540,9 @@ hipError_t launch_flash_fwd(const void* q, const void* k, const void* v, void* o
   a.scale = scale;
   a.c = scale * 1.4426950408889634f;
   a.thr = rescale_thr < 0.f ? 0.f : rescale_thr;
+  if (fa_waves() == 8)
+    return causal ? launch_fa(fa_fwd_kernel<true, 8>, a, 4 * kImg, st, 256, 512)
+                  : launch_fa(fa_fwd_kernel<false, 8>, a, 4 * kImg, st, 256, 512);
   return causal ? launch_fa(fa_fwd_kernel<true>, a, 4 * kImg, st)
                 : launch_fa(fa_fwd_kernel<false>, a, 4 * kImg, st);
 }
@@ -549,8 +567,13 @@ hipError_t launch_flash_bwd(const void* q, const void* k, const void* v, const v
   a.scale = scale;
   a.c = scale * 1.4426950408889634f;
   // dQ first: it also writes D = rowsum(dO * O), which the dK / dV kernel reads
-  hipError_t e = causal ? launch_fa(fa_dq_kernel<true>, a, 4 * kImg, st)
-                        : launch_fa(fa_dq_kernel<false>, a, 4 * kImg, st);
+  hipError_t e;
+  if (fa_waves() == 8)
+    e = causal ? launch_fa(fa_dq_kernel<true, 8>, a, 4 * kImg, st, 256, 512)
+               : launch_fa(fa_dq_kernel<false, 8>, a, 4 * kImg, st, 256, 512);
+  else
+    e = causal ? launch_fa(fa_dq_kernel<true>, a, 4 * kImg, st)
+               : launch_fa(fa_dq_kernel<false>, a, 4 * kImg, st);
   if (e != hipSuccess) return e;
   constexpr int smem = kVImg + 2 * kKVBuf;
   return causal ? launch_fa(fa_dkdv_kernel<true>, a, smem, st, kKVKeys, kKVThreads)

@@ -391,11 +391,13 @@ hipError_t launch_wgrad1x1(const void* dy, const void* x, float* part, void* dw,
 // Weight gradient of a 3x3 / stride 2 / padding 1 conv (wgrad1x1.hip's LDS-DMA kernel on the
 // implicit im2col of x): dy [N][H/2][W/2][Co], x [N][H][W][Ci] NHWC bf16 -> dw [Co][3][3][Ci]
 // (bf16 or fp32). H, W even; Co, Ci multiples of 128; N (H/2) (W/2) % 32 == 0. zero: >= 512 B
-// of zeros (the padding rows). part: splits x Co x 9 Ci floats (wgrad3x3s2_plan).
-bool wgrad3x3s2_plan(int N, int H, int W, int Co, int Ci, int* splits);
+// of zeros (the padding rows). part: splits x Co x taps Ci floats (wgrad3x3s2_plan).
+// taps = 1: the 1x1 / stride 2 / padding 0 conv (a downsample's weight gradient, the single tap
+// at (2 oh, 2 ow)) -> dw [Co][Ci].
+bool wgrad3x3s2_plan(int N, int H, int W, int Co, int Ci, int* splits, int taps = 9);
 hipError_t launch_wgrad3x3s2(const void* dy, const void* x, const void* zero, float* part,
                              void* dw, bool dw_bf16, int N, int H, int W, int Co, int Ci,
-                             hipStream_t st);
+                             hipStream_t st, int taps = 9);
 hipError_t launch_wgrad_fold(const float* part, int S, int64_t n, void* out, bool out_bf16,
                              hipStream_t st);
 // 3x3 / stride 1 / padding 1 weight gradient with all nine taps per workgroup (wgrad3x3.hip):

@@ -354,6 +354,7 @@ struct DmaArgs {
   int Co, ncol, Ci;       // ncol = Ci (1x1) or 9 Ci (S2)
   int tiles_n, tiles, nwork, nchunk, cps;
   int H, W, Ho, Wo;       // S2
+  int tap0;               // S2: first tap (0: 3x3 / padding 1; 4: 1x1 / padding 0 = tap (1, 1) only)
   // XF modes (1x1 only): PRO x -> max(x sc + bi, 0); DPM dy -> da (mask ? dy : 0) + dc;
   // cs_part [split][Co]: column sums of the transformed dy (tn == 0 workgroups)
   const float* sc;
@@ -450,7 +451,7 @@ __global__ __launch_bounds__((TM / 64) * (TN / WN) * 64) void wgrad_dma_kernel(D
   const int c_lo = split * a.cps;
   const int n = min(a.nchunk, c_lo + a.cps) - c_lo;
   // S2: this tile's tap and channel base (uniform)
-  const int tap = S2 ? n0 / a.Ci : 0, cb = S2 ? n0 - tap * a.Ci : n0;
+  const int tq = S2 ? n0 / a.Ci : 0, tap = a.tap0 + tq, cb = S2 ? n0 - tq * a.Ci : n0;
   const int dh = tap / 3 - 1, dw = tap % 3 - 1;
   const int hw = a.Ho * a.Wo;
 
@@ -1092,30 +1093,31 @@ hipError_t launch_wgrad1x1_ex(const void* dy, const void* x, float* part, void* 
   return hipGetLastError();
 }
 
-bool wgrad3x3s2_plan(int N, int H, int W, int Co, int Ci, int* splits) {
+bool wgrad3x3s2_plan(int N, int H, int W, int Co, int Ci, int* splits, int taps) {
   int TM, TN, cps;
-  if (!s2_tile(N, H, W, Co, Ci, &TM, &TN)) return false;
-  dma_plan(static_cast<int64_t>(N) * (H / 2) * (W / 2), Co, 9 * Ci, TM, TN, splits, &cps);
+  if ((taps != 9 && taps != 1) || !s2_tile(N, H, W, Co, Ci, &TM, &TN)) return false;
+  dma_plan(static_cast<int64_t>(N) * (H / 2) * (W / 2), Co, taps * Ci, TM, TN, splits, &cps);
   return true;
 }
 
 hipError_t launch_wgrad3x3s2(const void* dy, const void* x, const void* zero, float* part,
                              void* dw, bool dw_bf16, int N, int H, int W, int Co, int Ci,
-                             hipStream_t st) {
+                             hipStream_t st, int taps) {
   int TM, TN, S, cps;
-  if (!s2_tile(N, H, W, Co, Ci, &TM, &TN)) return hipErrorInvalidValue;
+  if ((taps != 9 && taps != 1) || !s2_tile(N, H, W, Co, Ci, &TM, &TN)) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) |
        reinterpret_cast<uintptr_t>(zero)) % 16)
     return hipErrorInvalidValue;
   const int64_t P = static_cast<int64_t>(N) * (H / 2) * (W / 2);
-  dma_plan(P, Co, 9 * Ci, TM, TN, &S, &cps);
+  dma_plan(P, Co, taps * Ci, TM, TN, &S, &cps);
   DmaArgs da{};
   da.dy = reinterpret_cast<const uint16_t*>(dy);
   da.x = reinterpret_cast<const uint16_t*>(x);
   da.zero = reinterpret_cast<const uint16_t*>(zero);
   da.part = part;
   da.Co = Co;
-  da.ncol = 9 * Ci;
+  da.ncol = taps * Ci;
+  da.tap0 = taps == 1 ? 4 : 0;
   da.Ci = Ci;
   da.H = H;
   da.W = W;
@@ -1123,7 +1125,7 @@ hipError_t launch_wgrad3x3s2(const void* dy, const void* x, const void* zero, fl
   da.Wo = W / 2;
   const hipError_t e = launch_dma_tile(TM, TN, true, da, P, S, cps, st);
   if (e != hipSuccess) return e;
-  fold_splits(part, S, static_cast<int64_t>(Co) * 9 * Ci, dw, dw_bf16, st);
+  fold_splits(part, S, static_cast<int64_t>(Co) * taps * Ci, dw, dw_bf16, st);
   return hipGetLastError();
 }
 
