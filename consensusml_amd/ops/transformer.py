@@ -10,6 +10,7 @@ tests, fp32) runs the equivalent PyTorch composition, which is also the numerics
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -708,15 +709,17 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None,
 # 1.05-1.31x hipBLASLt on every Llama-3-8B weight before the transpose: wqkv / wo / w2 (<= 64 M
 # elements) still win with it, the w13 / output-head ones tie (profiles/r06_16/llama_gemm.jsonl)
 _NB_OWN_DGRAD_MAX = 64 * 1024 * 1024
-# own forward (gemm.hip NT, x W^T as stored) up to this many weight elements: Llama-3-8B wqkv
-# 1.37 vs 1.31 PFLOP/s for hipBLASLt, wo 1.35 vs 1.40; the larger w13 / w2 / output head stay on
-# hipBLASLt (1.43-1.51 vs own 1.43-1.46) (profiles/r06_16/llama_gemm.jsonl)
-_NB_OWN_FWD_MAX = 32 * 1024 * 1024
+# own forward (gemm.hip NT, x W^T as stored) for weights up to this many elements with K up to
+# _NB_OWN_FWD_KMAX: Llama-3-8B wqkv 1.37 vs 1.31 PFLOP/s for hipBLASLt, wo 1.35 vs 1.40, w13 1.434
+# vs 1.433; the long-K w2 (K 14336: 1.46 vs 1.51) and the output head (1.44 vs 1.47) stay on
+# hipBLASLt (profiles/r06_16/llama_gemm.jsonl)
+_NB_OWN_FWD_MAX = int(os.environ.get("CML_NB_OWN_FWD_MAX", str(128 * 1024 * 1024)))
+_NB_OWN_FWD_KMAX = 8192
 
 
 class _LinearNBFn(torch.autograd.Function):
     """y = x W^T without bias (Llama's projections): forward on gemm.hip for weights up to
-    _NB_OWN_FWD_MAX elements, else hipBLASLt (NT, its best layout).
+    _NB_OWN_FWD_MAX elements and K <= _NB_OWN_FWD_KMAX, else hipBLASLt (NT, its best layout).
     Backward: dx = dy W on gemm.hip for weights up to _NB_OWN_DGRAD_MAX elements, else hipBLASLt;
     dW = dy^T x as an NT GEMM on transposed operands -- (dy^T) (x^T)^T, two bandwidth-bound
     transposes + hipBLASLt NT at 1.3-1.57 PFLOP/s instead of its dy^T x kernels at 0.9-1.15
@@ -727,7 +730,7 @@ class _LinearNBFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.param = w   # the Parameter itself (its id keys the direct-gradient destination)
         N, K = w.shape
-        if x.is_contiguous() and w.numel() <= _NB_OWN_FWD_MAX:
+        if x.is_contiguous() and w.numel() <= _NB_OWN_FWD_MAX and K <= _NB_OWN_FWD_KMAX:
             x2 = x.view(-1, K)
             if _own_gemm(x2.shape[0], N, K) and lib().gemm_nt_pick(x2.shape[0], N, K) == 256 \
                     and _al16(x2, w):
