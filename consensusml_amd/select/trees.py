@@ -74,15 +74,38 @@ def _best_split(Xn: torch.Tensor, g: torch.Tensor, h: torch.Tensor, crit: str, l
     m, F = Xn.shape
     if m < 2 * max(min_leaf, 1):
         return None
-    vals, order = torch.sort(Xn, dim=0)
+    vals, order = torch.sort(Xn, dim=0, stable=True)
+    if crit == "xgb":
+        # XGBoost's exact greedy split arithmetic: float gradient pairs summed in double, the
+        # split's loss change formed in double and stored as a float (SplitEntry::loss_chg), a
+        # split only when that float exceeds kRtEps = 1e-6, ties to the lower feature index and,
+        # within a feature, to the first threshold of the ascending scan (SplitEntry::NeedReplace).
+        # Float sums and a flat argmax split near-tied deep-tree nodes differently
+        # (tests/test_reference_rdata_parity.py::test_xgb_importance_parity).
+        G = torch.cumsum(g[order].double(), 0)
+        H = torch.cumsum(h[order].double(), 0)
+        Gt, Ht = G[-1:], H[-1:]
+        GL, HL = G[:-1], H[:-1]
+        GR, HR = Gt - GL, Ht - HL
+        chg = (GL * GL / (HL + lam) + GR * GR / (HR + lam) - Gt * Gt / (Ht + lam)).float()
+        ok = (HL >= min_child) & (HR >= min_child) & (vals[1:] > vals[:-1])
+        chg = torch.where(ok, chg, torch.full_like(chg, -float("inf")))
+        kbest = torch.argmax(chg, dim=0)                       # first max per feature
+        fbest = chg.gather(0, kbest.view(1, -1)).view(-1)
+        j = int(torch.argmax(fbest))                           # first (lowest) feature of the max
+        k = int(kbest[j])
+        best = float(fbest[j])
+        if not math.isfinite(best) or best <= 1e-6:
+            return None
+        thr = float((vals[k, j] + vals[k + 1, j]) / 2)
+        return 0.5 * best, j, thr
     G = torch.cumsum(g[order], 0)
     H = torch.cumsum(h[order], 0)
     Gt, Ht = G[-1:], H[-1:]
     GL, HL = G[:-1], H[:-1]
     GR, HR = Gt - GL, Ht - HL
-    if crit == "xgb":
-        gain = 0.5 * (GL * GL / (HL + lam) + GR * GR / (HR + lam) - Gt * Gt / (Ht + lam))
-        ok = (HL >= min_child) & (HR >= min_child)
+    if False:
+        pass
     else:
         def gini_w(pos, n):   # n * gini impurity
             p = pos / n.clamp_min(1e-12)
