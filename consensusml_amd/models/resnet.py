@@ -65,6 +65,12 @@ def conv1x1_policy(cin: int, cout: int, hw: int):
         return True, True
     if mode is False or mode == "miopen":
         return False, False
+    # PerfPolicy.c1_dgrad64_gemm: layer 1.0's 64 -> 64 conv1 data gradient as a GEMM too, so the
+    # downsample's dX is absorbed by its beta = 1 epilogue (one pass) instead of MIOpen's data
+    # gradient plus the stem pool backward's two-gradient sum (pool_gsum): -0.4 ms/step at batch
+    # 2560 (profiles/r06_30/)
+    if cin == 64 and cout == 64 and _P().c1_dgrad64_gemm:
+        return False, True
     return cin >= 1024, (cout < cin) or hw <= 196
 
 

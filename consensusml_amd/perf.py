@@ -77,6 +77,8 @@ class PerfPolicy:
     wgrad3x3_s2_min_ci: int = 256         # ... for Ci >= this (the 128-channel layer-2 conv: MIOpen)
     own_wgrad1x1_s2: bool = True          # stride-2 1x1 (downsample) weight gradient on the same
                                           # kernel, one tap (was MIOpen)
+    c1_dgrad64_gemm: bool = True          # layer 1.0 conv1 (64 -> 64) data gradient as a GEMM that
+                                          # absorbs the downsample's dX (no pool two-gradient sum)
     own_conv3x3_s2: bool = True           # stride-2 3x3: conv_gemm forward + BN stats, parity-class
                                           # data gradient (+ bn1 backward sums)
     side_wgrad: bool = False              # 3x3 weight gradients on a side stream, concurrent with
@@ -143,6 +145,7 @@ class PerfPolicy:
             own_wgrad3x3_s2=_env_bool("CML_WGRAD3X3_S2", True),
             wgrad3x3_s2_min_ci=int(os.environ.get("CML_WGRAD3X3_S2_MIN_CI", "256")),
             own_wgrad1x1_s2=_env_bool("CML_WGRAD1X1_S2", True),
+            c1_dgrad64_gemm=_env_bool("CML_C1_DGRAD64", True),
             own_conv3x3_s2=_env_bool("CML_CONV3X3_S2", True),
             side_wgrad=_env_bool("CML_SIDE_WGRAD", False),
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),

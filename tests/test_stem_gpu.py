@@ -161,7 +161,9 @@ def test_stem_pool_link_second_gradient(cuda):
     for on in (True, False):
         from consensusml_amd import perf
         TAP_STATS.update(parked=0, fallback=0)
-        with perf.use_policy(perf.policy().replace(pool_link=on)):
+        # c1_dgrad64_gemm off: layer1.0's conv1 data gradient on the library conv, so the
+        # downsample's dX takes the pool link (with it on, conv1's GEMM absorbs it instead)
+        with perf.use_policy(perf.policy().replace(pool_link=on, c1_dgrad64_gemm=False)):
             m.zero_grad(set_to_none=True)
             F.cross_entropy(m(x).float(), y).backward()
             out[on] = [m.conv1.weight.grad.float().clone(), m.bn1.weight.grad.float().clone(),
@@ -253,3 +255,31 @@ def test_stem_wgrad_pc_matches_alternating(cuda, monkeypatch, N, two):
     for a, b in zip(out["1"], out["0"]):
         assert torch.isfinite(a).all()
         assert _rel(a, b) < 2e-5, _rel(a, b)
+
+
+def test_layer1_conv1_dgrad_gemm_absorbs_downsample(cuda):
+    """PerfPolicy.c1_dgrad64_gemm: layer1.0's conv1 data gradient as a GEMM whose beta = 1
+    epilogue takes the downsample's dX (no pool two-gradient sum) vs the library data gradient +
+    the pool link: the stem gradients of both paths against the same model in fp32."""
+    import copy
+
+    import consensusml_amd.models.resnet as R
+    from consensusml_amd import perf
+    torch.manual_seed(1)
+    m32 = R.resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last)
+    m = copy.deepcopy(m32).to(torch.bfloat16)
+    x = torch.randn(8, 3, 96, 96, device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device=cuda)
+    F.cross_entropy(m32(x.float()), y).backward()
+    ref = [m32.conv1.weight.grad, m32.layer1[0].conv1.weight.grad]
+    out = {}
+    for on in (True, False):
+        with perf.use_policy(perf.policy().replace(c1_dgrad64_gemm=on)):
+            m.zero_grad(set_to_none=True)
+            F.cross_entropy(m(x).float(), y).backward()
+            out[on] = [m.conv1.weight.grad.float().clone(),
+                       m.layer1[0].conv1.weight.grad.float().clone()]
+    for a, b, r in zip(out[True], out[False], ref):
+        e_on, e_off = _rel(a, r), _rel(b, r)
+        assert e_on <= max(1.5 * e_off, 0.1), (e_on, e_off)
