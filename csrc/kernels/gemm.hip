@@ -528,14 +528,16 @@ int tall_min_tiles() {
 }
 }  // namespace
 
-// CML_GEMM_GM: m-tiles per tile group of the plain (non-conv) GEMM (default 8; 0 / 1: n
-// fastest, the round-5 order). An XCD then runs an 8 (m) x 4 (n) block of tiles instead of one
-// m-row: 8192^3 1.28 -> 1.35 PFLOP/s, Llama-3-8B w13 / output-head forwards 1.34 -> 1.44-1.46
-// (hipBLASLt 1.46-1.49 on that box), profiles/r06_15/
+// CML_GEMM_GM: m-tiles per tile group of the plain (non-conv) GEMM (default 4; 0 / 1: n
+// fastest, the round-5 order). An XCD then runs a 4 (m) x 8 (n) block of tiles instead of one
+// m-row: with 8, 8192^3 1.28 -> 1.35 PFLOP/s and the Llama-3-8B w13 / output-head forwards 1.34
+// -> 1.44-1.46 (profiles/r06_15/); 4 is 1-4 % faster again on most Llama shapes (w13 forward /
+// NT weight gradient, wo, w2 data gradient; w2 forward 1.5 % slower) and the Llama step -1.3 ms,
+// ResNet unchanged (profiles/r06_32/, profiles/r06_33/)
 int gemm_gm() {
   static const int v = [] {
     const char* e = getenv("CML_GEMM_GM");
-    return e ? atoi(e) : 8;
+    return e ? atoi(e) : 4;
   }();
   return v;
 }
