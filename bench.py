@@ -249,6 +249,11 @@ def self_launch(n: int) -> int:
 
 
 def main():
+    # CML_TRACEBACK_AFTER=S: dump every thread's Python stack to stderr every S seconds (finds
+    # where a rank waits when a multi-rank run stops making progress)
+    if os.environ.get("CML_TRACEBACK_AFTER"):
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["CML_TRACEBACK_AFTER"]), repeat=True)
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
