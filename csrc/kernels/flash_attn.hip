@@ -510,11 +510,13 @@ hipError_t launch_fa(FaKernel kern, const FaArgs& a, int smem, hipStream_t st, i
   return hipGetLastError();
 }
 
-// queries per workgroup of the forward and dQ kernels: CML_FA_WAVES = 4 (128) or 8 (256)
+// queries per workgroup of the forward and dQ kernels: CML_FA_WAVES = 8 (256, default: each staged
+// K / V tile feeds twice the queries; backward 0.574-0.580 vs 0.588-0.590 ms per Llama-3-8B layer,
+// forward within 1 %, profiles/r06_24/fa_*.jsonl) or 4 (128)
 int fa_waves() {
   static const int w = [] {
     const char* e = std::getenv("CML_FA_WAVES");
-    return e && std::atoi(e) == 8 ? 8 : 4;
+    return e && std::atoi(e) == 4 ? 4 : 8;
   }();
   return w;
 }
