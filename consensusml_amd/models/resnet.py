@@ -463,7 +463,17 @@ class ResNet(nn.Module):
             x = bn_relu_max_pool2d(self.stem(x), self.bn1, 3, 2, 1)
         else:
             x = max_pool2d(self.bn1(self.stem(x)), 3, 2, 1)
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        # every block's 3x3 weight layouts (implicit-GEMM forward / data gradient) in one launch
+        # for this forward (PerfPolicy.batch_wlayouts) instead of one per conv
+        batched = (pol.batch_wlayouts and self.training and torch.is_grad_enabled()
+                   and fconv.prefetch_w3x3_layouts(
+                       [b.conv2.weight for layer in (self.layer1, self.layer2, self.layer3,
+                                                     self.layer4) for b in layer]))
+        try:
+            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        finally:
+            if batched:
+                fconv.clear_w3x3_layouts()
         return self.fc(global_avg_pool(x))
 
 

@@ -158,9 +158,13 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, own:
 
 class _Conv1x1BNStatsFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, rmean, rvar, stride, eps, momentum, dgrad_gemm, own_wgrad, link):
-        y, mean, invstd = lib().conv1x1_bn_fwd(x, w, None, None, rmean, rmean, rvar, stride, True,
-                                               eps, momentum)
+    def forward(ctx, x, w, rmean, rvar, stride, eps, momentum, dgrad_gemm, own_wgrad, link,
+                aff=None):
+        out = lib().conv1x1_bn_fwd(x, w, None, None, rmean, rmean, rvar, stride, True, eps,
+                                   momentum, *(aff or (None, None)))
+        y, mean, invstd = out[:3]
+        if aff is not None:   # the next BN's affine from the statistics' finalize launch
+            _stash_affine(mean, out[3], out[4], aff)
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.dgrad_gemm, ctx.own_wgrad, ctx.link = stride, dgrad_gemm, own_wgrad, link
         ctx.mark_non_differentiable(mean, invstd)
@@ -174,7 +178,7 @@ class _Conv1x1BNStatsFn(torch.autograd.Function):
         dx = _dgrad(dy, x, w, ctx.stride, ctx.dgrad_gemm, ctx.link) \
             if ctx.needs_input_grad[0] else None
         dw = _wgrad(dy, x, w, ctx.stride, ctx.own_wgrad) if ctx.needs_input_grad[1] else None
-        return dx, dw, None, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None, None
 
 
 class _BNReLUConv1x1BNStatsFn(torch.autograd.Function):
@@ -260,9 +264,39 @@ class _BNReLUConv1x1BNResFn(torch.autograd.Function):
         return (dz, dg2, db2, None, None, dw, dg3, db3, dres) + (None,) * 6
 
 
+def _fin_aff(bn):
+    """(gamma, beta) of ``bn`` for a statistics finalize that also writes its affine
+    (PerfPolicy.fin_affine, bf16 parameters), else None."""
+    g, b = bn.weight, bn.bias
+    if (_P().fin_affine and _P().bn_affine_kernel and g is not None and b is not None
+            and g.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+            and g.is_contiguous() and b.is_contiguous()):
+        return g, b
+    return None
+
+
+def _stash_affine(mean: torch.Tensor, sc: torch.Tensor, bi: torch.Tensor, aff) -> None:
+    """Park the finalize's affine (sc, bi) of (gamma, beta) = aff on its mean tensor, for the
+    consumer's ``_affine`` (valid while gamma / beta are unchanged: pointer and version checked)."""
+    g, b = aff
+    mean._cml_affine = (sc, bi, g.data_ptr(), b.data_ptr(), g._version, b._version)
+
+
+def _cached_affine(gamma: torch.Tensor, beta: torch.Tensor, mean: torch.Tensor):
+    a = getattr(mean, "_cml_affine", None)
+    if (a is not None and a[2] == gamma.data_ptr() and a[3] == beta.data_ptr()
+            and a[4] == gamma._version and a[5] == beta._version):
+        return a[0], a[1]
+    return None
+
+
 def _affine(gamma: torch.Tensor, beta: torch.Tensor, mean: torch.Tensor, invstd: torch.Tensor):
     """(sc, bi) = (gamma invstd, beta - mean sc) in fp32: one ``bn_affine`` launch (bit-identical to
-    ``gamma.float() * invstd`` and ``beta.float() - mean * sc``, which take five)."""
+    ``gamma.float() * invstd`` and ``beta.float() - mean * sc``, which take five), or none when the
+    statistics' finalize already wrote it (``_stash_affine``)."""
+    a = _cached_affine(gamma, beta, mean)
+    if a is not None:
+        return a
     if not _P().bn_affine_kernel:
         sc = gamma.float() * invstd
         return sc, beta.float() - mean * sc
@@ -322,14 +356,27 @@ def fold_cat(w1: torch.Tensor, a: torch.Tensor, c: torch.Tensor, w2: torch.Tenso
     return w_cat, torch.mv(w1, c)
 
 
+def _own_dgb(gamma: torch.Tensor, beta: torch.Tensor) -> bool:
+    """Whether a BN's parameter gradients come out of its backward sums' finalize launch (bf16
+    parameters: the values ``bn_bwd_coeffs`` rounds, without its launch;
+    PerfPolicy.fin_dgamma)."""
+    return (_P().fin_dgamma and gamma.dtype == torch.bfloat16 and beta.dtype == torch.bfloat16
+            and gamma.is_contiguous() and beta.is_contiguous())
+
+
 def _cat_dgrad_bn2(L, gy, mask, z, sc, bi, w_cat, bias, g2, b2, mean2, invstd2):
     """dy2 = [(mask ? gy : 0) | relu(z sc + bi)] w_cat^T + bias (``fold_cat``), then bn2's
     (BN + ReLU on z) backward: (dz, dgamma2, dbeta2)."""
     pol = _P()
     if pol.cat_bnsums and z.shape[1] <= pol.cat_bnsums_maxc:
-        dy2, s2, q2 = L.conv1x1_cat_bnsums(gy, mask, z, sc, bi, w_cat, bias, mean2, invstd2)
-        M = z.numel() // z.shape[1]
-        _, _, _, dg2, db2 = L.bn_bwd_coeffs(s2, q2, g2, mean2, invstd2, M)
+        if _own_dgb(g2, b2):   # bn2's parameter gradients from the sums' finalize launch
+            dg2, db2 = torch.empty_like(g2), torch.empty_like(b2)
+            dy2, s2, q2 = L.conv1x1_cat_bnsums(gy, mask, z, sc, bi, w_cat, bias, mean2, invstd2,
+                                               dg2, db2)
+        else:
+            dy2, s2, q2 = L.conv1x1_cat_bnsums(gy, mask, z, sc, bi, w_cat, bias, mean2, invstd2)
+            M = z.numel() // z.shape[1]
+            _, _, _, dg2, db2 = L.bn_bwd_coeffs(s2, q2, g2, mean2, invstd2, M)
         return L.bn_bwd_apply(dy2, z, g2, b2, mean2, invstd2, s2, q2), dg2, db2
     dy2 = L.conv1x1_cat(gy, mask, z, sc, bi, w_cat, bias)
     dz, dg2, db2, _ = L.bn_bwd(dy2, None, z, None, g2, b2, mean2, invstd2, True, False)
@@ -702,11 +749,36 @@ def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tenso
         dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
 
 
+_WL_BATCH = {}   # id(weight) -> (weight, wf, wr): this forward's prefetched 3x3 layouts
+
+
+def prefetch_w3x3_layouts(ws) -> bool:
+    """Make the ``_w3x3_layouts`` of all bf16 GPU 3x3 weights ``ws`` in one launch
+    (``conv3x3_wlayouts_multi``) for the forward about to run; the caller clears them with
+    ``clear_w3x3_layouts`` when it ends (the weights must not change in between). False (nothing
+    done) for fewer than two eligible weights."""
+    ws = [w for w in ws if w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 4
+          and w.shape[2] == 3 and w.shape[3] == 3]
+    if len(ws) < 2:
+        return False
+    for w, (wf, wr) in zip(ws, lib().conv3x3_wlayouts_multi(ws)):
+        _WL_BATCH[id(w)] = (w, wf, wr)
+    return True
+
+
+def clear_w3x3_layouts() -> None:
+    _WL_BATCH.clear()
+
+
 def _w3x3_layouts(w: torch.Tensor, want_wf: bool):
     """(wf or None, wr): the implicit-GEMM forward layout wf [Co, 9 Ci] (k = (3 ky + kx) Ci + ci)
     and the data-gradient layout wr [Ci, 9 Co] (rotated, transposed: wr[ci][(3 ky + kx) Co + co] =
     w[co][ci][2 - ky][2 - kx]) of a 3x3 weight, in one launch (``conv3x3_wlayouts``) instead of a
-    permute copy, a flip and another permute copy per conv and step."""
+    permute copy, a flip and another permute copy per conv and step -- or none when the model's
+    forward prefetched every block's layouts together (``prefetch_w3x3_layouts``)."""
+    e = _WL_BATCH.get(id(w))
+    if e is not None and e[0] is w:
+        return (e[1] if want_wf else None), e[2]
     if w.is_cuda and w.dtype == torch.bfloat16:
         wf, wr = lib().conv3x3_wlayouts(w, want_wf)
         return wf, wr
@@ -748,10 +820,9 @@ class _Conv3x3BNStatsFn(torch.autograd.Function):
     as ``_Conv3x3Fn``."""
 
     @staticmethod
-    def forward(ctx, x, w, rmean, rvar, eps, momentum):
+    def forward(ctx, x, w, rmean, rvar, eps, momentum, aff=None):
         wf, wr = _w3x3_layouts(w, True)   # both layouts now: the backward reuses wr
-        y, mean, invstd = lib().conv_gemm_bn(x, wf, 9, _zero_row(x.device), rmean, rmean, rvar,
-                                             eps, momentum)
+        y, mean, invstd = _conv_gemm_bn(x, wf, rmean, rvar, eps, momentum, 1, aff)
         ctx.save_for_backward(x, w)
         ctx.wr = wr
         ctx.mark_non_differentiable(mean, invstd)
@@ -761,7 +832,17 @@ class _Conv3x3BNStatsFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dm, _di):
         dx, dw = _Conv3x3Fn.backward(ctx, dy)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
+
+
+def _conv_gemm_bn(x, wf, rmean, rvar, eps, momentum, stride, aff):
+    """``conv_gemm_bn`` (3x3 taps) -> (y, mean, invstd); with aff = (gamma, beta) the next BN's
+    affine comes out of the same finalize launch and is parked on mean (``_stash_affine``)."""
+    out = lib().conv_gemm_bn(x, wf, 9, _zero_row(x.device), rmean, rmean, rvar, eps, momentum,
+                             stride, *(aff or (None, None)))
+    if aff is not None:
+        _stash_affine(out[1], out[3], out[4], aff)
+    return out[0], out[1], out[2]
 
 
 class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
@@ -773,15 +854,15 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
     (the separate reduction re-read dy1 and z1)."""
 
     @staticmethod
-    def forward(ctx, z1, g1, b1, mean1, invstd1, eps1, w, rmean, rvar, eps, momentum):
+    def forward(ctx, z1, g1, b1, mean1, invstd1, eps1, w, rmean, rvar, eps, momentum, aff=None):
         L = lib()
         y1 = L.bn_fwd(z1, None, g1, b1, None, None, mean1, invstd1, eps1, momentum, True, False,
                       False)[0]
         wf, wr = _w3x3_layouts(w, True)   # both layouts now: the backward reuses wr
-        z2, m2, i2 = L.conv_gemm_bn(y1, wf, 9, _zero_row(z1.device), rmean, rmean, rvar, eps,
-                                    momentum)
+        z2, m2, i2 = _conv_gemm_bn(y1, wf, rmean, rvar, eps, momentum, 1, aff)
         ctx.save_for_backward(z1, g1, b1, mean1, invstd1, y1, w)
         ctx.wr = wr
+        ctx.aff1 = _cached_affine(g1, b1, mean1)   # bn1's affine, for the backward
         ctx.mark_non_differentiable(m2, i2)
         ctx.set_materialize_grads(False)   # no zero-filled grads for the statistics outputs
         return z2, m2, i2
@@ -793,7 +874,7 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
         L = lib()
         wr = ctx.wr   # rotated / transposed layout, made by the forward
         dw, h = _wgrad_fork(_wgrad3x3, dz2, y1, w) if ctx.needs_input_grad[6] else (None, None)
-        sc, bi = _affine(g1, b1, mean1, invstd1)
+        sc, bi = ctx.aff1 or _affine(g1, b1, mean1, invstd1)
         # bn1's parameter gradients come out of the sums' finalize launch (no bn_bwd_coeffs)
         own_dgb = g1.dtype == torch.bfloat16 and b1.dtype == torch.bfloat16
         dg1, db1 = (torch.empty_like(g1), torch.empty_like(b1)) if own_dgb else (None, None)
@@ -804,7 +885,7 @@ class _BNReLUConv3x3BNStatsFn(torch.autograd.Function):
             _, _, _, dg1, db1 = L.bn_bwd_coeffs(s1, q1, g1, mean1, invstd1, M)
         dz1 = L.bn_bwd_apply(dy1, z1, g1, b1, mean1, invstd1, s1, q1)
         dw = _wgrad_join(dw, h)
-        return dz1, dg1, db1, None, None, None, dw, None, None, None, None
+        return dz1, dg1, db1, None, None, None, dw, None, None, None, None, None
 
 
 def _wgrad3x3_s2(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
@@ -834,10 +915,9 @@ class _Conv3x3S2BNStatsFn(torch.autograd.Function):
     weight gradient on MIOpen."""
 
     @staticmethod
-    def forward(ctx, x, w, rmean, rvar, eps, momentum):
+    def forward(ctx, x, w, rmean, rvar, eps, momentum, aff=None):
         wf, wr = _w3x3_layouts(w, True)
-        y, mean, invstd = lib().conv_gemm_bn(x, wf, 9, _zero_row(x.device), rmean, rmean, rvar,
-                                             eps, momentum, 2)
+        y, mean, invstd = _conv_gemm_bn(x, wf, rmean, rvar, eps, momentum, 2, aff)
         ctx.save_for_backward(x, w)
         ctx.wr = wr
         ctx.mark_non_differentiable(mean, invstd)
@@ -851,7 +931,7 @@ class _Conv3x3S2BNStatsFn(torch.autograd.Function):
         dx = lib().conv_gemm_s2dgrad(dy, ctx.wr, _zero_row(dy.device))[0] \
             if ctx.needs_input_grad[0] else None
         dw = _wgrad3x3_s2(dy, x, w) if ctx.needs_input_grad[1] else None
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 class _BNReLUConv3x3S2BNStatsFn(torch.autograd.Function):
@@ -860,15 +940,15 @@ class _BNReLUConv3x3S2BNStatsFn(torch.autograd.Function):
     backward is its apply pass only."""
 
     @staticmethod
-    def forward(ctx, z1, g1, b1, mean1, invstd1, eps1, w, rmean, rvar, eps, momentum):
+    def forward(ctx, z1, g1, b1, mean1, invstd1, eps1, w, rmean, rvar, eps, momentum, aff=None):
         L = lib()
         y1 = L.bn_fwd(z1, None, g1, b1, None, None, mean1, invstd1, eps1, momentum, True, False,
                       False)[0]
         wf, wr = _w3x3_layouts(w, True)
-        z2, m2, i2 = L.conv_gemm_bn(y1, wf, 9, _zero_row(z1.device), rmean, rmean, rvar, eps,
-                                    momentum, 2)
+        z2, m2, i2 = _conv_gemm_bn(y1, wf, rmean, rvar, eps, momentum, 2, aff)
         ctx.save_for_backward(z1, g1, b1, mean1, invstd1, y1, w)
         ctx.wr = wr
+        ctx.aff1 = _cached_affine(g1, b1, mean1)
         ctx.mark_non_differentiable(m2, i2)
         ctx.set_materialize_grads(False)
         return z2, m2, i2
@@ -879,14 +959,19 @@ class _BNReLUConv3x3S2BNStatsFn(torch.autograd.Function):
         dz2 = dz2.contiguous(memory_format=torch.channels_last)
         L = lib()
         dw, h = _wgrad_fork(_wgrad3x3_s2, dz2, y1, w) if ctx.needs_input_grad[6] else (None, None)
-        sc, bi = _affine(g1, b1, mean1, invstd1)
-        dy1, s1, q1 = L.conv_gemm_s2dgrad(dz2, ctx.wr, _zero_row(dz2.device), z1, sc, bi, mean1,
-                                          invstd1)
-        M = z1.numel() // z1.shape[1]
-        _, _, _, dg1, db1 = L.bn_bwd_coeffs(s1, q1, g1, mean1, invstd1, M)
+        sc, bi = ctx.aff1 or _affine(g1, b1, mean1, invstd1)
+        if _own_dgb(g1, b1):   # bn1's parameter gradients from the sums' finalize launch
+            dg1, db1 = torch.empty_like(g1), torch.empty_like(b1)
+            dy1, s1, q1 = L.conv_gemm_s2dgrad(dz2, ctx.wr, _zero_row(dz2.device), z1, sc, bi,
+                                              mean1, invstd1, dg1, db1)
+        else:
+            dy1, s1, q1 = L.conv_gemm_s2dgrad(dz2, ctx.wr, _zero_row(dz2.device), z1, sc, bi,
+                                              mean1, invstd1)
+            M = z1.numel() // z1.shape[1]
+            _, _, _, dg1, db1 = L.bn_bwd_coeffs(s1, q1, g1, mean1, invstd1, M)
         dz1 = L.bn_bwd_apply(dy1, z1, g1, b1, mean1, invstd1, s1, q1)
         dw = _wgrad_join(dw, h)
-        return dz1, dg1, db1, None, None, None, dw, None, None, None, None
+        return dz1, dg1, db1, None, None, None, dw, None, None, None, None, None
 
 
 def conv3x3_s2_ok(x: torch.Tensor, conv) -> bool:
@@ -904,7 +989,7 @@ def conv3x3_s2_bn_stats(x: torch.Tensor, conv, bn):
     """(z, (mean, invstd)) of a stride-2 ``conv(x)`` and bn's training statistics; callers check
     ``conv3x3_s2_ok``."""
     z, m, i = _Conv3x3S2BNStatsFn.apply(x, conv.weight, bn.running_mean, bn.running_var, bn.eps,
-                                        bn.momentum)
+                                        bn.momentum, _fin_aff(bn))
     return z, (m, i)
 
 
@@ -912,7 +997,7 @@ def bnrelu_conv3x3_s2_bn_stats(z1: torch.Tensor, bn_a, stats_a, conv, bn):
     """``bnrelu_conv3x3_bn_stats`` for a stride-2 conv; callers check ``conv3x3_s2_ok`` on z1."""
     z, m, i = _BNReLUConv3x3S2BNStatsFn.apply(z1, bn_a.weight, bn_a.bias, stats_a[0], stats_a[1],
                                               bn_a.eps, conv.weight, bn.running_mean,
-                                              bn.running_var, bn.eps, bn.momentum)
+                                              bn.running_var, bn.eps, bn.momentum, _fin_aff(bn))
     return z, (m, i)
 
 
@@ -925,7 +1010,7 @@ def bnrelu_conv3x3_bn_stats(z1: torch.Tensor, bn_a, stats_a, conv, bn):
     bn's training statistics; callers check ``conv3x3_ok`` on z1 first."""
     z, m, i = _BNReLUConv3x3BNStatsFn.apply(z1, bn_a.weight, bn_a.bias, stats_a[0], stats_a[1],
                                             bn_a.eps, conv.weight, bn.running_mean, bn.running_var,
-                                            bn.eps, bn.momentum)
+                                            bn.eps, bn.momentum, _fin_aff(bn))
     return z, (m, i)
 
 
@@ -933,7 +1018,7 @@ def conv3x3_bn_stats(x: torch.Tensor, conv, bn):
     """(z, (mean, invstd)) of ``conv(x)`` and bn's training statistics (running stats updated),
     from one implicit-GEMM kernel; callers check ``conv3x3_ok`` first."""
     z, m, i = _Conv3x3BNStatsFn.apply(x, conv.weight, bn.running_mean, bn.running_var, bn.eps,
-                                      bn.momentum)
+                                      bn.momentum, _fin_aff(bn))
     return z, (m, i)
 
 
@@ -958,7 +1043,7 @@ def conv1x1_bn_stats(x: torch.Tensor, conv, bn, stride: int = 1, dgrad_gemm: boo
     """(z, mean, invstd): 1x1 conv output and its training BN statistics (bn's running stats are
     updated). ``conv`` / ``bn``: nn.Conv2d-like (weight) and BatchNormAct2d modules."""
     return _Conv1x1BNStatsFn.apply(x, conv.weight, bn.running_mean, bn.running_var, stride,
-                                   bn.eps, bn.momentum, dgrad_gemm, own_wgrad, link)
+                                   bn.eps, bn.momentum, dgrad_gemm, own_wgrad, link, _fin_aff(bn))
 
 
 def bnrelu_conv1x1_bn_stats(z: torch.Tensor, bn_a, stats_a, conv, bn_b, dgrad_gemm: bool = False,

@@ -83,6 +83,11 @@ class PerfPolicy:
                                           # data gradient (+ bn1 backward sums)
     side_wgrad: bool = False              # 3x3 weight gradients on a side stream, concurrent with
                                           # the same conv's data-gradient / BN-backward kernels
+    fin_dgamma: bool = True               # BN parameter gradients from the backward sums' finalize
+                                          # launch (no bn_bwd_coeffs launch: batch-256 tails)
+    fin_affine: bool = True               # BN affine (gamma invstd, beta - mean sc) from the
+                                          # statistics' finalize launch (no bn_affine launch)
+    batch_wlayouts: bool = True           # all 3x3 weight layouts of a ResNet forward in one launch
     # ---------------------------------------------------------------- transformers / engine
     attn_kernel: bool = True              # MFMA attention for short sequences (BERT)
     flash_attn: bool = True               # flash_attn.hip for head-dim-128 (GQA, causal) attention
@@ -148,6 +153,9 @@ class PerfPolicy:
             c1_dgrad64_gemm=_env_bool("CML_C1_DGRAD64", True),
             own_conv3x3_s2=_env_bool("CML_CONV3X3_S2", True),
             side_wgrad=_env_bool("CML_SIDE_WGRAD", False),
+            fin_dgamma=_env_bool("CML_FIN_DGAMMA", True),
+            fin_affine=_env_bool("CML_FIN_AFFINE", True),
+            batch_wlayouts=_env_bool("CML_BATCH_WLAYOUTS", True),
             attn_kernel=_env_bool("CML_ATTN_KERNEL", True),
             flash_attn=_env_bool("CML_FLASH_ATTN", True),
             multi_copy=_env_bool("CML_MULTI_COPY", True),

@@ -1037,6 +1037,46 @@ std::vector<Tensor> tail_bwd_prep(const Tensor& W, const Tensor& P, const Tensor
   return {wcat, bias, dW, dg, db};
 }
 
+// Optional bf16 [C] output tensors for a BN's parameter gradients bf16(sum dy' xhat) /
+// bf16(sum dy'), written by the finalize launch of the sums that produce them (both or neither).
+std::pair<void*, void*> dgb_ptrs(const optional<Tensor>& dgamma_out,
+                                 const optional<Tensor>& dbeta_out, int64_t C, const Tensor& like,
+                                 const char* name) {
+  const bool want = dgamma_out.has_value() && dgamma_out->defined();
+  TORCH_CHECK(want == (dbeta_out.has_value() && dbeta_out->defined()), name,
+              ": dgamma_out and dbeta_out together");
+  if (!want) return {nullptr, nullptr};
+  for (const Tensor* t : {&*dgamma_out, &*dbeta_out}) {
+    check_dev(*t, "dgamma_out / dbeta_out");
+    TORCH_CHECK(t->device() == like.device() && t->scalar_type() == at::kBFloat16 &&
+                    t->is_contiguous() && t->numel() == C,
+                name, ": dgamma_out / dbeta_out must be contiguous bf16 [C]");
+  }
+  return {dgamma_out->data_ptr(), dbeta_out->data_ptr()};
+}
+
+// Optional BN affine output of a statistics finalize (gamma / beta: the BN's bf16 [C] parameters,
+// both or neither): allocates sc / bi fp32 [C] and fills `out`; nullptr when not requested.
+const cml::BnAffineOut* aff_out(const optional<Tensor>& gamma, const optional<Tensor>& beta,
+                                int64_t C, const Tensor& like, const char* name, Tensor& sc,
+                                Tensor& bi, cml::BnAffineOut& out) {
+  const bool want = gamma.has_value() && gamma->defined();
+  TORCH_CHECK(want == (beta.has_value() && beta->defined()), name, ": gamma and beta together");
+  if (!want) return nullptr;
+  for (const Tensor* t : {&*gamma, &*beta}) {
+    check_dev(*t, "gamma / beta");
+    TORCH_CHECK(t->device() == like.device() && t->scalar_type() == at::kBFloat16 &&
+                    t->is_contiguous() && t->numel() == C,
+                name, ": gamma / beta must be contiguous bf16 [C]");
+  }
+  auto f32 = like.options().dtype(at::kFloat);
+  sc = at::empty({C}, f32);
+  bi = at::empty({C}, f32);
+  out = cml::BnAffineOut{gamma->data_ptr(), beta->data_ptr(), sc.data_ptr<float>(),
+                         bi.data_ptr<float>()};
+  return &out;
+}
+
 // Fused 1x1 conv forward (conv1x1.hip): x [N, K, H, W] NHWC bf16, w [Cout, K, 1, 1] bf16 ->
 // {y [N, Cout, OH, OW] NHWC, mean, invstd} (mean / invstd: training BN statistics of y, undefined
 // when !stats). pro_sc / pro_bi (fp32 [K]): apply max(x * sc + bi, 0) to the input on load.
@@ -1044,7 +1084,8 @@ std::vector<Tensor> tail_bwd_prep(const Tensor& W, const Tensor& P, const Tensor
 std::vector<Tensor> conv1x1_bn_fwd(const Tensor& x, const Tensor& w, const optional<Tensor>& pro_sc,
                                    const optional<Tensor>& pro_bi, const optional<Tensor>& shift,
                                    const optional<Tensor>& rmean, const optional<Tensor>& rvar,
-                                   int64_t stride, bool stats, double eps, double momentum) {
+                                   int64_t stride, bool stats, double eps, double momentum,
+                                   const optional<Tensor>& gamma, const optional<Tensor>& beta) {
   check_nhwc(x, "x");
   TORCH_CHECK(x.dim() == 4, "conv1x1_bn_fwd: 4-D NHWC input");
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 1 && w.size(3) == 1 &&
@@ -1070,6 +1111,10 @@ std::vector<Tensor> conv1x1_bn_fwd(const Tensor& x, const Tensor& w, const optio
     part = at::empty({static_cast<int64_t>(cml::conv1x1_bn_part_floats(M, static_cast<int>(K),
                                                                      static_cast<int>(Co), pro))}, f32);
   }
+  Tensor asc, abi;
+  cml::BnAffineOut ao{};
+  const cml::BnAffineOut* aff = aff_out(gamma, beta, Co, x, "conv1x1_bn_fwd", asc, abi, ao);
+  TORCH_CHECK(stats || !aff, "conv1x1_bn_fwd: the affine needs stats");
   CML_CHECK_HIP(cml::launch_conv1x1_bn_fwd(
       x.data_ptr(), w.data_ptr(), y.data_ptr(), stats ? part.data_ptr<float>() : nullptr, sc, bi,
       opt_ptr<const float>(shift, at::kFloat, "shift", Co), M, static_cast<int>(K),
@@ -1077,7 +1122,8 @@ std::vector<Tensor> conv1x1_bn_fwd(const Tensor& x, const Tensor& w, const optio
       stats ? mean.data_ptr<float>() : nullptr, stats ? invstd.data_ptr<float>() : nullptr,
       stats ? opt_ptr<float>(rmean, at::kFloat, "running_mean", Co) : nullptr,
       stats ? opt_ptr<float>(rvar, at::kFloat, "running_var", Co) : nullptr,
-      static_cast<float>(eps), static_cast<float>(momentum), cur_stream()));
+      static_cast<float>(eps), static_cast<float>(momentum), cur_stream(), aff));
+  if (aff) return {y, mean, invstd, asc, abi};
   return {y, mean, invstd};
 }
 
@@ -1208,7 +1254,8 @@ Tensor conv1x1_cat(const Tensor& g, const Tensor& mask, const Tensor& x2,
 std::vector<Tensor> conv1x1_cat_bnsums(const Tensor& g, const Tensor& mask, const Tensor& x2,
                                        const Tensor& sc2, const Tensor& bi2, const Tensor& w,
                                        const optional<Tensor>& bias, const Tensor& mean,
-                                       const Tensor& invstd) {
+                                       const Tensor& invstd, const optional<Tensor>& dgamma_out,
+                                       const optional<Tensor>& dbeta_out) {
   const auto [N, K1, H, W, K2, M, K, Co] = cat_shape(g, x2, w, "conv1x1_cat_bnsums");
   TORCH_CHECK(Co == K2, "conv1x1_cat_bnsums: w must be [K2, K1 + K2]");
   const c10::DeviceGuard guard(g.device());
@@ -1216,6 +1263,7 @@ std::vector<Tensor> conv1x1_cat_bnsums(const Tensor& g, const Tensor& mask, cons
   Tensor y = at::empty({N, Co, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor part = at::empty({static_cast<int64_t>(cml::conv1x1_cat_part_floats(M, K, Co))}, f32);
   Tensor sdz = at::empty({Co}, f32), sdzx = at::empty({Co}, f32);
+  const auto [dg, db] = dgb_ptrs(dgamma_out, dbeta_out, Co, g, "conv1x1_cat_bnsums");
   CML_CHECK_HIP(cml::launch_conv1x1_cat(
       g.data_ptr(), opt_ptr<const uint8_t>(mask, at::kByte, "mask", M * K1 / 8), x2.data_ptr(),
       opt_ptr<const float>(sc2, at::kFloat, "sc2", K2),
@@ -1224,7 +1272,7 @@ std::vector<Tensor> conv1x1_cat_bnsums(const Tensor& g, const Tensor& mask, cons
       static_cast<int>(K1), static_cast<int>(K), static_cast<int>(Co), cur_stream(),
       opt_ptr<const float>(mean, at::kFloat, "mean", Co),
       opt_ptr<const float>(invstd, at::kFloat, "invstd", Co), part.data_ptr<float>(),
-      sdz.data_ptr<float>(), sdzx.data_ptr<float>()));
+      sdz.data_ptr<float>(), sdzx.data_ptr<float>(), dg, db));
   return {y, sdz, sdzx};
 }
 
@@ -1434,6 +1482,29 @@ std::vector<Tensor> conv3x3_wlayouts(const Tensor& w, bool want_wf) {
   return {wf, wr};   // wf undefined (None) unless asked for
 }
 
+// conv3x3_wlayouts of several weights (all bf16 [Co, Ci, 3, 3] on one device, any strides) in one
+// launch: [(wf, wr), ...] (wf always made).
+std::vector<std::vector<Tensor>> conv3x3_wlayouts_multi(const std::vector<Tensor>& ws) {
+  std::vector<std::vector<Tensor>> out;
+  if (ws.empty()) return out;
+  const c10::DeviceGuard guard(ws[0].device());
+  std::vector<cml::WlDesc> d;
+  for (const Tensor& w : ws) {
+    TORCH_CHECK(w.is_cuda() && w.device() == ws[0].device() && w.scalar_type() == at::kBFloat16 &&
+                    w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3,
+                "conv3x3_wlayouts_multi: bf16 [Co, Ci, 3, 3] weights on one device");
+    const int64_t Co = w.size(0), Ci = w.size(1);
+    Tensor wr = at::empty({Ci, 9 * Co}, w.options().memory_format(at::MemoryFormat::Contiguous));
+    Tensor wf = at::empty({Co, 9 * Ci}, w.options().memory_format(at::MemoryFormat::Contiguous));
+    d.push_back(cml::WlDesc{w.data_ptr(), wf.data_ptr(), wr.data_ptr(), w.stride(0), w.stride(1),
+                            w.stride(2), w.stride(3), static_cast<int>(Co), static_cast<int>(Ci)});
+    out.push_back({wf, wr});
+  }
+  CML_CHECK_HIP(cml::launch_conv3x3_wlayouts_multi(d.data(), static_cast<int>(d.size()),
+                                                   cur_stream()));
+  return out;
+}
+
 std::vector<Tensor> conv_gemm_bnsums(const Tensor& x, const Tensor& w, int64_t taps,
                                      const Tensor& zero, const Tensor& z, const Tensor& sc,
                                      const Tensor& bi, const Tensor& mean, const Tensor& invstd,
@@ -1458,21 +1529,7 @@ std::vector<Tensor> conv_gemm_bnsums(const Tensor& x, const Tensor& w, int64_t t
   Tensor part = at::empty({static_cast<int64_t>(cml::conv_gemm_part_floats(M, static_cast<int>(Co)))}, f32);
   Tensor sdz = at::empty({Co}, f32), sdzx = at::empty({Co}, f32);
   // optional: the BN's parameter gradients bf16(sdzx) / bf16(sdz) from the same finalize launch
-  void* dg = nullptr;
-  void* db = nullptr;
-  const bool want_dg = dgamma_out.has_value() && dgamma_out->defined();
-  TORCH_CHECK(want_dg == (dbeta_out.has_value() && dbeta_out->defined()),
-              "conv_gemm_bnsums: dgamma_out and dbeta_out together");
-  if (want_dg) {
-    for (const Tensor* t : {&*dgamma_out, &*dbeta_out}) {
-      check_dev(*t, "dgamma_out / dbeta_out");
-      TORCH_CHECK(t->device() == x.device() && t->scalar_type() == at::kBFloat16 &&
-                      t->is_contiguous() && t->numel() == Co,
-                  "conv_gemm_bnsums: dgamma_out / dbeta_out must be contiguous bf16 [Cout]");
-    }
-    dg = dgamma_out->data_ptr();
-    db = dbeta_out->data_ptr();
-  }
+  const auto [dg, db] = dgb_ptrs(dgamma_out, dbeta_out, Co, x, "conv_gemm_bnsums");
   CML_CHECK_HIP(cml::launch_conv_gemm_bnsums(
       x.data_ptr(), w.data_ptr(), y.data_ptr(), zero.data_ptr(), static_cast<int>(N),
       static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(Co),
@@ -1491,7 +1548,9 @@ std::vector<Tensor> conv_gemm_bnsums(const Tensor& x, const Tensor& w, int64_t t
 std::vector<Tensor> conv_gemm_s2dgrad(const Tensor& dy, const Tensor& wr, const Tensor& zero,
                                       const optional<Tensor>& z, const optional<Tensor>& sc,
                                       const optional<Tensor>& bi, const optional<Tensor>& mean,
-                                      const optional<Tensor>& invstd) {
+                                      const optional<Tensor>& invstd,
+                                      const optional<Tensor>& dgamma_out,
+                                      const optional<Tensor>& dbeta_out) {
   check_nhwc(dy, "dy");
   TORCH_CHECK(dy.dim() == 4, "conv_gemm_s2dgrad: 4-D NHWC dy");
   const int64_t N = dy.size(0), Co = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
@@ -1518,6 +1577,8 @@ std::vector<Tensor> conv_gemm_s2dgrad(const Tensor& dy, const Tensor& wr, const 
     sdz = at::empty({Ci}, f32);
     sdzx = at::empty({Ci}, f32);
   }
+  const auto [dg, db] = dgb_ptrs(dgamma_out, dbeta_out, Ci, dy, "conv_gemm_s2dgrad");
+  TORCH_CHECK(sums || dg == nullptr, "conv_gemm_s2dgrad: dgamma_out needs z");
   CML_CHECK_HIP(cml::launch_conv_gemm_s2dgrad(
       dy.data_ptr(), wr.data_ptr(), dx.data_ptr(), zero.data_ptr(), static_cast<int>(N),
       static_cast<int>(Ho), static_cast<int>(Wo), static_cast<int>(Co), static_cast<int>(Ci),
@@ -1527,7 +1588,7 @@ std::vector<Tensor> conv_gemm_s2dgrad(const Tensor& dy, const Tensor& wr, const 
       sums ? opt_ptr<const float>(mean, at::kFloat, "mean", Ci) : nullptr,
       sums ? opt_ptr<const float>(invstd, at::kFloat, "invstd", Ci) : nullptr,
       sums ? part.data_ptr<float>() : nullptr, sums ? sdz.data_ptr<float>() : nullptr,
-      sums ? sdzx.data_ptr<float>() : nullptr, cur_stream()));
+      sums ? sdzx.data_ptr<float>() : nullptr, cur_stream(), dg, db));
   return {dx, sdz, sdzx};
 }
 
@@ -1568,7 +1629,8 @@ Tensor conv_gemm(const Tensor& x, const Tensor& w, int64_t taps, const optional<
 std::vector<Tensor> conv_gemm_bn(const Tensor& x, const Tensor& w, int64_t taps,
                                  const optional<Tensor>& zero_in, const optional<Tensor>& shift,
                                  const optional<Tensor>& rmean, const optional<Tensor>& rvar,
-                                 double eps, double momentum, int64_t stride) {
+                                 double eps, double momentum, int64_t stride,
+                                 const optional<Tensor>& gamma, const optional<Tensor>& beta) {
   check_nhwc(x, "x");
   TORCH_CHECK(x.dim() == 4, "conv_gemm_bn: 4-D NHWC input");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -1592,6 +1654,9 @@ std::vector<Tensor> conv_gemm_bn(const Tensor& x, const Tensor& w, int64_t taps,
   }
   Tensor mean = at::empty({Co}, f32), invstd = at::empty({Co}, f32);
   Tensor part = at::empty({static_cast<int64_t>(cml::conv_gemm_part_floats(M, static_cast<int>(Co)))}, f32);
+  Tensor asc, abi;
+  cml::BnAffineOut ao{};
+  const cml::BnAffineOut* aff = aff_out(gamma, beta, Co, x, "conv_gemm_bn", asc, abi, ao);
   CML_CHECK_HIP(cml::launch_conv_gemm(
       x.data_ptr(), w.data_ptr(), y.data_ptr(), zero.data_ptr(), static_cast<int>(N),
       static_cast<int>(H), static_cast<int>(W), static_cast<int>(C), static_cast<int>(Co),
@@ -1599,7 +1664,8 @@ std::vector<Tensor> conv_gemm_bn(const Tensor& x, const Tensor& w, int64_t taps,
       opt_ptr<const float>(shift, at::kFloat, "shift", Co), mean.data_ptr<float>(),
       invstd.data_ptr<float>(), opt_ptr<float>(rmean, at::kFloat, "running_mean", Co),
       opt_ptr<float>(rvar, at::kFloat, "running_var", Co), static_cast<float>(eps),
-      static_cast<float>(momentum), static_cast<int>(stride)));
+      static_cast<float>(momentum), static_cast<int>(stride), aff));
+  if (aff) return {y, mean, invstd, asc, abi};
   return {y, mean, invstd};
 }
 
@@ -2520,8 +2586,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_wgrad", &stem_wgrad, "ResNet stem weight gradient through BN (MFMA, one pass)");
   m.def("maxpool_fwd", &maxpool_fwd, "NHWC bf16 max-pool forward (uint8 argmax)");
   m.def("maxpool_bwd", &maxpool_bwd, "NHWC bf16 max-pool backward (gather)");
-  m.def("conv1x1_bn_fwd", &conv1x1_bn_fwd,
-        "fused 1x1 conv forward (MFMA) + BN statistics epilogue + optional BN-ReLU prologue");
+  m.def("conv1x1_bn_fwd", &conv1x1_bn_fwd, py::arg("x"), py::arg("w"), py::arg("pro_sc"),
+        py::arg("pro_bi"), py::arg("shift"), py::arg("running_mean"), py::arg("running_var"),
+        py::arg("stride"), py::arg("stats"), py::arg("eps"), py::arg("momentum"),
+        py::arg("gamma") = py::none(), py::arg("beta") = py::none(),
+        "fused 1x1 conv forward (MFMA) + BN statistics epilogue + optional BN-ReLU prologue "
+        "(+ with gamma / beta that BN's affine sc, bi from the statistics' finalize)");
   m.def("bn_stats", &bn_stats, "training BatchNorm statistics (mean, invstd) only");
   m.def("wgrad1x1", &wgrad1x1, py::arg("dy"), py::arg("x"), py::arg("dtype"),
         py::arg("pro_sc") = py::none(), py::arg("pro_bi") = py::none(),
@@ -2554,7 +2624,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_gemm_s2dgrad", &conv_gemm_s2dgrad, py::arg("dy"), py::arg("wr"), py::arg("zero"),
         py::arg("z") = py::none(), py::arg("sc") = py::none(), py::arg("bi") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(),
-        "stride-2 3x3 data gradient as four parity-class implicit GEMMs (+ BN + ReLU backward sums)");
+        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
+        "stride-2 3x3 data gradient as four parity-class implicit GEMMs (+ BN + ReLU backward sums, "
+        "+ optionally that BN's parameter gradients)");
   m.def("conv_gemm", &conv_gemm, py::arg("x"), py::arg("w"), py::arg("taps"),
         py::arg("zero") = py::none(), py::arg("stride") = 1,
         "implicit-GEMM NHWC conv (1x1 / 3x3 padding 1, stride 1 or 2), glds staging");
@@ -2566,8 +2638,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_bnres", &conv1x1_bnres, "recomputed conv1x1 + BN apply + residual + ReLU -> {y, mask}");
   m.def("conv1x1_cat_bnres", &conv1x1_cat_bnres,
         "two BN'd 1x1 convs summed + ReLU in one K-concatenated GEMM -> {y, mask}");
-  m.def("conv1x1_cat_bnsums", &conv1x1_cat_bnsums,
-        "conv1x1_cat + the sums of the BN + ReLU backward its output feeds");
+  m.def("conv1x1_cat_bnsums", &conv1x1_cat_bnsums, py::arg("g"), py::arg("mask"), py::arg("x2"),
+        py::arg("sc2"), py::arg("bi2"), py::arg("w"), py::arg("bias"), py::arg("mean"),
+        py::arg("invstd"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
+        "conv1x1_cat + the sums of the BN + ReLU backward its output feeds (+ optionally that "
+        "BN's parameter gradients)");
   m.def("bn_affine", &bn_affine, "BN affine (gamma invstd, beta - mean sc) of batch statistics");
   m.def("bn_bwd_apply", &bn_bwd_apply, "apply half of a BN + ReLU backward from its sums");
   m.def("split_search_sampled", &split_search_sampled,
@@ -2584,7 +2659,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("zero") = py::none(), py::arg("shift") = py::none(),
         py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
         py::arg("eps") = 1e-5, py::arg("momentum") = 0.1, py::arg("stride") = 1,
-        "implicit-GEMM conv + BN statistics of the output in the epilogue -> {y, mean, invstd}");
+        py::arg("gamma") = py::none(), py::arg("beta") = py::none(),
+        "implicit-GEMM conv + BN statistics of the output in the epilogue -> {y, mean, invstd} "
+        "(+ sc, bi: the BN's affine from the finalize, with gamma / beta)");
   m.def("conv1x1_bnbwd", &conv1x1_bnbwd, "1x1 data gradient through a BN + ReLU backward prologue");
   m.def("conv1x1_link", &conv1x1_link, py::arg("x"), py::arg("w"), py::arg("link"),
         py::arg("lmask"), py::arg("sz") = py::none(), py::arg("smask") = py::none(),
@@ -2602,6 +2679,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("z"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"),
         "stem backward (conv weight gradient through BN, dgamma, dbeta) from the pool output "
         "gradient, the pool input gradient gathered inside the kernel");
+  m.def("conv3x3_wlayouts_multi", &conv3x3_wlayouts_multi, py::arg("ws"),
+        "conv3x3_wlayouts of several 3x3 weights in one launch -> [(wf, wr), ...]");
   m.def("conv3x3_wlayouts", &conv3x3_wlayouts, py::arg("w"), py::arg("want_wf"),
         "forward / data-gradient GEMM layouts of a 3x3 conv weight in one launch");
   m.def("maxpool_bwd_sum", &maxpool_bwd_sum, "3x3/s2 max-pool backward + channel sums of dx",

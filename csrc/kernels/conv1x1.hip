@@ -319,7 +319,8 @@ __global__ __launch_bounds__(kThreads, 2) void conv1x1_bn_fwd_kernel(C1Args a) {
 __global__ __launch_bounds__(256) void conv1x1_bn_finalize_kernel(
     const float* __restrict__ part, int R, int BN, int N, int64_t M, const float* shift,
     float eps, float momentum, float* __restrict__ mean, float* __restrict__ invstd,
-    float* __restrict__ rmean, float* __restrict__ rvar) {
+    float* __restrict__ rmean, float* __restrict__ rvar, const uint16_t* __restrict__ gamma,
+    const uint16_t* __restrict__ beta, float* __restrict__ sc, float* __restrict__ bi) {
   __shared__ double ls[32][8], lq[32][8];
   const int cl = threadIdx.x & 7, sl = threadIdx.x >> 3;
   const int c = blockIdx.x * 8 + cl;
@@ -361,8 +362,16 @@ __global__ __launch_bounds__(256) void conv1x1_bn_finalize_kernel(
   double var = Q / static_cast<double>(M) - ms * ms;
   if (var < 0.0) var = 0.0;
   const double mu = (shift ? static_cast<double>(shift[c]) : 0.0) + ms;
-  mean[c] = static_cast<float>(mu);
-  invstd[c] = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+  const float mf = static_cast<float>(mu), isf = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+  mean[c] = mf;
+  invstd[c] = isf;
+  if (sc) {   // the BN affine as bn_affine computes it from the stored fp32 mean / invstd
+#pragma clang fp contract(off)
+    const float s = __uint_as_float(static_cast<uint32_t>(gamma[c]) << 16) * isf;
+    sc[c] = s;
+    const float mfs = mf * s;
+    bi[c] = __uint_as_float(static_cast<uint32_t>(beta[c]) << 16) - mfs;
+  }
   if (rmean) {
     const double unb = M > 1 ? var * static_cast<double>(M) / static_cast<double>(M - 1) : var;
     rmean[c] = static_cast<float>((1.0 - momentum) * rmean[c] + momentum * mu);
@@ -742,7 +751,8 @@ int bn_part_fold_slices(int R, int ntn) {
 hipError_t launch_bn_stats_finalize(const float* part, int R, int BN, int N, int64_t M,
                                    const float* shift, float eps, float momentum, float* mean,
                                    float* invstd, float* rmean, float* rvar, hipStream_t st,
-                                   float* fold) {
+                                   float* fold, const BnAffineOut* aff) {
+  if (aff && (!aff->gamma || !aff->beta || !aff->sc || !aff->bi)) return hipErrorInvalidValue;
   const int S = fold ? bn_part_fold_slices(R, N / BN) : 0;
   if (S > 0) {
     const int rp = (R + S - 1) / S;
@@ -751,8 +761,11 @@ hipError_t launch_bn_stats_finalize(const float* part, int R, int BN, int N, int
     part = fold;
     R = S2;
   }
-  conv1x1_bn_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, R, BN, N, M, shift, eps, momentum,
-                                                          mean, invstd, rmean, rvar);
+  conv1x1_bn_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(
+      part, R, BN, N, M, shift, eps, momentum, mean, invstd, rmean, rvar,
+      aff ? reinterpret_cast<const uint16_t*>(aff->gamma) : nullptr,
+      aff ? reinterpret_cast<const uint16_t*>(aff->beta) : nullptr, aff ? aff->sc : nullptr,
+      aff ? aff->bi : nullptr);
   return hipGetLastError();
 }
 
@@ -901,7 +914,9 @@ hipError_t launch_conv1x1_bnres(const void* x, const void* w, void* y, uint8_t* 
 hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2, const float* sc2,
                               const float* bi2, const float* bias, const void* w, void* y,
                               int64_t M, int K1, int K, int N, hipStream_t st, const float* mean,
-                              const float* invstd, float* part, float* sdz, float* sdzx) {
+                              const float* invstd, float* part, float* sdz, float* sdzx,
+                              void* dgamma, void* dbeta) {
+  if ((dgamma == nullptr) != (dbeta == nullptr) || (dgamma && !mean)) return hipErrorInvalidValue;
   if (bad_shape(M, K, N) || K1 % kBK || K1 <= 0 || K1 >= K || !mask || (!sc2 != !bi2))
     return hipErrorInvalidValue;
   const bool sums = mean != nullptr;
@@ -927,12 +942,14 @@ hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2
     hipError_t e = launch_conv1x1g(a, PM_CAT, sums ? SM_BNBWD : SM_OFF, false, st, &R, &BN);
     if (e != hipSuccess || !sums) return e;
     return launch_bnbwd_sums_finalize(part, R, BN, N, invstd, sdz, sdzx, st,
-                                      part + static_cast<size_t>(N / BN) * R * 2 * BN);
+                                      part + static_cast<size_t>(N / BN) * R * 2 * BN, dgamma,
+                                      dbeta);
   }
   hipError_t e = launch_tail(a, p, true, st);
   if (e != hipSuccess || !sums) return e;
-  conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, p.wgpn * p.WM, p.BN, N,
-                                                             invstd, sdz, sdzx, nullptr, nullptr);
+  conv1x1_bnbwd_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(
+      part, p.wgpn * p.WM, p.BN, N, invstd, sdz, sdzx, reinterpret_cast<uint16_t*>(dgamma),
+      reinterpret_cast<uint16_t*>(dbeta));
   return hipGetLastError();
 }
 
@@ -974,7 +991,7 @@ hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* p
                                  const float* pro_sc, const float* pro_bi, const float* shift,
                                  int64_t M, int K, int N, int stride, int H, int W, float* mean,
                                  float* invstd, float* rmean, float* rvar, float eps,
-                                 float momentum, hipStream_t st) {
+                                 float momentum, hipStream_t st, const BnAffineOut* aff) {
   if (K % kBK || N % 64 || M < 1 || M >= (1ll << 31) || K > 4096 || N > 4096)
     return hipErrorInvalidValue;
   if (stride != 1 && stride != 2) return hipErrorInvalidValue;
@@ -1007,17 +1024,15 @@ hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* p
     hipError_t e = launch_conv1x1g(a, pro ? PM_BNRELU : PM_NONE, SM_BN, false, st, &R, &BN);
     if (e != hipSuccess || !part || !mean) return e;
     return launch_bn_stats_finalize(part, R, BN, N, M, shift, eps, momentum, mean, invstd, rmean,
-                                    rvar, st, part + static_cast<size_t>(N / BN) * R * 2 * BN);
+                                    rvar, st, part + static_cast<size_t>(N / BN) * R * 2 * BN, aff);
   }
   hipError_t e;
   if (p.WN == 4) e = launch_w<4, 1>(a, p, pro, s2, st);
   else if (p.WN == 2) e = launch_w<2, 2>(a, p, pro, s2, st);
   else e = launch_w<1, 4>(a, p, pro, s2, st);
   if (e != hipSuccess || !part || !mean) return e;
-  const int R = p.wgpn * p.WM;
-  conv1x1_bn_finalize_kernel<<<(N + 7) / 8, 256, 0, st>>>(part, R, p.BN, N, M, shift, eps,
-                                                          momentum, mean, invstd, rmean, rvar);
-  return hipGetLastError();
+  return launch_bn_stats_finalize(part, p.wgpn * p.WM, p.BN, N, M, shift, eps, momentum, mean,
+                                  invstd, rmean, rvar, st, nullptr, aff);
 }
 
 }  // namespace cml

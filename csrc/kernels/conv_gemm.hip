@@ -471,7 +471,8 @@ size_t conv_gemm_part_floats(int64_t M, int N) {
 hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* zero, int Nimg,
                             int H, int W, int C, int N, int taps, hipStream_t st, float* part,
                             const float* shift, float* mean, float* invstd, float* rmean,
-                            float* rvar, float eps, float momentum, int stride) {
+                            float* rvar, float eps, float momentum, int stride,
+                            const BnAffineOut* aff) {
   if (stride != 1 && stride != 2) return hipErrorInvalidValue;
   const int OH = (H - 1) / stride + 1, OW = (W - 1) / stride + 1;
   const int64_t M = static_cast<int64_t>(Nimg) * OH * OW;
@@ -502,7 +503,7 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
                                    nullptr, nullptr, st, &R);
     if (e != hipSuccess || !part || !mean) return e;
     return launch_bn_stats_finalize(part, R, 64, 64, M, shift, eps, momentum, mean, invstd, rmean,
-                                    rvar, st, nullptr);
+                                    rvar, st, nullptr, aff);
   }
   if (const int tm = use_gemm2(M, N, C, taps, stride)) {
     GemmArgs g{};
@@ -524,7 +525,7 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
     if (e != hipSuccess || !part || !mean) return e;
     const int tn = 65536 / tm, R = static_cast<int>(M / tm) * (tm / 128);
     return launch_bn_stats_finalize(part, R, tn, N, M, shift, eps, momentum, mean, invstd, rmean,
-                                    rvar, st, part + static_cast<size_t>(N / tn) * R * 2 * tn);
+                                    rvar, st, part + static_cast<size_t>(N / tn) * R * 2 * tn, aff);
   }
   hipError_t e = taps == 1 ? launch_v<1>(a, M, st) : launch_v<9>(a, M, st);
   if (e != hipSuccess || !part || !mean) return e;
@@ -532,7 +533,7 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
   tile_of(M, N, &BM, &BN);
   const int R = static_cast<int>((M + BM - 1) / BM) * (BM / 64);
   return launch_bn_stats_finalize(part, R, BN, N, M, shift, eps, momentum, mean, invstd, rmean,
-                                  rvar, st, part + static_cast<size_t>(N / BN) * R * 2 * BN);
+                                  rvar, st, part + static_cast<size_t>(N / BN) * R * 2 * BN, aff);
 }
 
 hipError_t launch_conv_gemm_bnsums(const void* x, const void* w, void* y, const void* zero,
@@ -663,7 +664,7 @@ hipError_t launch_conv_gemm_s2dgrad(const void* dy, const void* wr, void* dx, co
                                     int Nimg, int Ho, int Wo, int Co, int Ci, const void* z,
                                     const float* sc, const float* bi, const float* mean,
                                     const float* invstd, float* part, float* sdz, float* sdzx,
-                                    hipStream_t st) {
+                                    hipStream_t st, void* dgamma, void* dbeta) {
   const int64_t Mc = static_cast<int64_t>(Nimg) * Ho * Wo;
   if (Co % kBK || Ci % 64 || Mc < 1 || 4 * Mc >= (1ll << 31) || 9ll * Co > 65536 || !zero)
     return hipErrorInvalidValue;
@@ -701,7 +702,8 @@ hipError_t launch_conv_gemm_s2dgrad(const void* dy, const void* wr, void* dx, co
   if (e != hipSuccess || !z) return e;
   const int R = static_cast<int>(4 * ((Mc + BM - 1) / BM) * (BM / 64));
   return launch_bnbwd_sums_finalize(part, R, BN, Ci, invstd, sdz, sdzx, st,
-                                    part + static_cast<size_t>(Ci / BN) * R * 2 * BN);
+                                    part + static_cast<size_t>(Ci / BN) * R * 2 * BN, dgamma,
+                                    dbeta);
 }
 
 namespace {
@@ -726,7 +728,51 @@ __global__ __launch_bounds__(256) void conv3x3_wlayouts_kernel(const uint16_t* _
   if (wf) wf[e] = v;
   wr[(static_cast<int64_t>(ci) * 9 + (8 - t)) * Co + co] = v;
 }
+
+// Several weights' layouts in one launch (the 16 3x3 convs of a ResNet-50 forward: one launch
+// instead of 16 ~9 us ones): descriptors by value, workgroups [blk0[d], blk0[d + 1]) on weight d.
+struct WlMulti {
+  WlDesc d[kWlMax];
+  int blk0[kWlMax + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void conv3x3_wlayouts_multi_kernel(const WlMulti m) {
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < m.n && b >= m.blk0[i + 1]) ++i;
+  const WlDesc& d = m.d[i];
+  const int64_t e = static_cast<int64_t>(b - m.blk0[i]) * 256 + threadIdx.x;
+  if (e >= static_cast<int64_t>(d.Co) * d.Ci * 9) return;
+  const int ci = static_cast<int>(e % d.Ci);
+  const int t = static_cast<int>((e / d.Ci) % 9);
+  const int co = static_cast<int>(e / (static_cast<int64_t>(d.Ci) * 9));
+  const int ky = t / 3, kx = t - 3 * (t / 3);
+  const uint16_t* w = reinterpret_cast<const uint16_t*>(d.w);
+  const uint16_t v = w[co * d.s0 + ci * d.s1 + ky * d.s2 + kx * d.s3];
+  if (d.wf) reinterpret_cast<uint16_t*>(d.wf)[e] = v;
+  reinterpret_cast<uint16_t*>(d.wr)[(static_cast<int64_t>(ci) * 9 + (8 - t)) * d.Co + co] = v;
+}
 }  // namespace
+
+hipError_t launch_conv3x3_wlayouts_multi(const WlDesc* d, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += kWlMax) {
+    WlMulti m{};
+    m.n = n - i0 < kWlMax ? n - i0 : kWlMax;
+    int64_t blk = 0;
+    for (int i = 0; i < m.n; ++i) {
+      const WlDesc& x = d[i0 + i];
+      if (x.Co < 1 || x.Ci < 1 || !x.w || !x.wr) return hipErrorInvalidValue;
+      m.d[i] = x;
+      m.blk0[i] = static_cast<int>(blk);
+      blk += (static_cast<int64_t>(x.Co) * x.Ci * 9 + 255) / 256;
+      if (blk >= (1ll << 31)) return hipErrorInvalidValue;
+    }
+    m.blk0[m.n] = static_cast<int>(blk);
+    conv3x3_wlayouts_multi_kernel<<<static_cast<unsigned>(blk), 256, 0, st>>>(m);
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_conv3x3_wlayouts(const void* w, int Co, int Ci, int64_t s0, int64_t s1,
                                    int64_t s2, int64_t s3, void* wf, void* wr, hipStream_t st) {

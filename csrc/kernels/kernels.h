@@ -415,11 +415,20 @@ hipError_t launch_wgrad3x3_direct(const void* dy, const void* x, const void* zer
 // training BatchNorm statistics of y (shifted by `shift`, e.g. the running mean; finalize updates
 // rmean / rvar when non-null). K % 64 == 0, N % 64 == 0. part: conv1x1_bn_part_floats floats.
 size_t conv1x1_bn_part_floats(int64_t M, int K, int N, bool pro);
+// Optional output of a BN statistics finalize: the BN's affine sc = gamma invstd,
+// bi = beta - mean sc (fp32, from the stored fp32 mean / invstd, bit-identical to bn_affine) for
+// bf16 gamma / beta -- the consumer's bn_affine launch folded into the finalize.
+struct BnAffineOut {
+  const void* gamma;
+  const void* beta;
+  float* sc;
+  float* bi;
+};
 hipError_t launch_conv1x1_bn_fwd(const void* x, const void* w, void* y, float* part,
                                  const float* pro_sc, const float* pro_bi, const float* shift,
                                  int64_t M, int K, int N, int stride, int H, int W, float* mean,
                                  float* invstd, float* rmean, float* rvar, float eps,
-                                 float momentum, hipStream_t st);
+                                 float momentum, hipStream_t st, const BnAffineOut* aff = nullptr);
 
 // Implicit-GEMM NHWC conv, stride 1, 1x1 (taps 1) or 3x3 padding 1 (taps 9), global_load_lds
 // double-buffered (conv_gemm.hip): x [Nimg][H][W][C], w [N][taps][C], y [Nimg][H][W][N]; zero:
@@ -450,12 +459,22 @@ hipError_t launch_conv_gemm_s2dgrad(const void* dy, const void* wr, void* dx, co
                                     int Nimg, int Ho, int Wo, int Co, int Ci, const void* z,
                                     const float* sc, const float* bi, const float* mean,
                                     const float* invstd, float* part, float* sdz, float* sdzx,
-                                    hipStream_t st);
+                                    hipStream_t st, void* dgamma = nullptr, void* dbeta = nullptr);
 // The forward (wf [Co][9 Ci], k = (3 ky + kx) Ci + ci) and data-gradient (wr [Ci][9 Co], rotated
 // and transposed: wr[ci][(3 ky + kx) Co + co] = w[co][ci][2 - ky][2 - kx]) GEMM layouts of a bf16
 // 3x3 conv weight with strides s0..s3 (elements), in one launch; wf may be null.
 hipError_t launch_conv3x3_wlayouts(const void* w, int Co, int Ci, int64_t s0, int64_t s1,
                                    int64_t s2, int64_t s3, void* wf, void* wr, hipStream_t st);
+// The same for n weights in ceil(n / kWlMax) launches (descriptors passed by value).
+struct WlDesc {
+  const void* w;
+  void* wf;   // may be null
+  void* wr;
+  int64_t s0, s1, s2, s3;
+  int Co, Ci;
+};
+constexpr int kWlMax = 24;
+hipError_t launch_conv3x3_wlayouts_multi(const WlDesc* d, int n, hipStream_t st);
 // Stride-1 3x3 conv of 64 -> 64 channels on 56-wide images from an LDS-resident input patch
 // (conv3x3p.hip; launch_conv_gemm / launch_conv_gemm_bnsums route there when eligible). ep 0: y
 // only; 1: + shifted BN statistics; 2: + BN + ReLU backward sums (z, sc, bi, shift = mean); one
@@ -470,7 +489,8 @@ hipError_t launch_conv_gemm(const void* x, const void* w, void* y, const void* z
                             float* part = nullptr, const float* shift = nullptr,
                             float* mean = nullptr, float* invstd = nullptr,
                             float* rmean = nullptr, float* rvar = nullptr, float eps = 1e-5f,
-                            float momentum = 0.1f, int stride = 1);
+                            float momentum = 0.1f, int stride = 1,
+                            const BnAffineOut* aff = nullptr);
 // BN statistics from a [ntn][R][2][BN] partial slab of shifted sums (conv1x1.hip's finalize).
 // With `fold` (>= ntn * bn_part_fold_slices(R, ntn) * 2 * BN floats) a tall slab is first folded
 // to bn_part_fold_slices rows per column tile by a wide kernel.
@@ -478,7 +498,7 @@ int bn_part_fold_slices(int R, int ntn);
 hipError_t launch_bn_stats_finalize(const float* part, int R, int BN, int N, int64_t M,
                                    const float* shift, float eps, float momentum, float* mean,
                                    float* invstd, float* rmean, float* rvar, hipStream_t st,
-                                   float* fold = nullptr);
+                                   float* fold = nullptr, const BnAffineOut* aff = nullptr);
 
 // Backward variants of the fused 1x1 conv (conv1x1.hip), stride 1, W given as [N][K] (for a data
 // gradient: the forward weight transposed).
@@ -515,7 +535,8 @@ hipError_t launch_conv1x1_cat(const void* g, const uint8_t* mask, const void* x2
                               const float* bi2, const float* bias, const void* w, void* y,
                               int64_t M, int K1, int K, int N, hipStream_t st,
                               const float* mean = nullptr, const float* invstd = nullptr,
-                              float* part = nullptr, float* sdz = nullptr, float* sdzx = nullptr);
+                              float* part = nullptr, float* sdz = nullptr, float* sdzx = nullptr,
+                              void* dgamma = nullptr, void* dbeta = nullptr);
 size_t conv1x1_cat_part_floats(int64_t M, int K, int N);
 hipError_t launch_conv1x1_bnbwd(const void* g, const void* z, const uint8_t* mask, const float* ca,
                                 const float* cb, const float* cc, const void* w, void* y,

@@ -268,6 +268,12 @@ def test_conv1x1_cat_bnsums(cuda, N, K1, K2, H):
     dz = _lib().bn_bwd_apply(y, x2, gam, bet, mean, invstd, s, q)
     dz_ref, _, _, _ = _lib().bn_bwd(y, None, x2, None, gam, bet, mean, invstd, True, False)
     _close(_rows(dz), _rows(dz_ref), 1e-2)
+    # the BN's parameter gradients from the sums' finalize launch == bn_bwd_coeffs' values
+    dg, db = torch.empty_like(gam), torch.empty_like(bet)
+    y2, s2, q2 = _lib().conv1x1_cat_bnsums(g, mask, x2, sc, bi, w_cat, bias, mean, invstd, dg, db)
+    assert torch.equal(y2, y) and torch.equal(s2, s) and torch.equal(q2, q)
+    _, _, _, dg_ref, db_ref = _lib().bn_bwd_coeffs(s, q, gam, mean, invstd, M)
+    assert torch.equal(dg, dg_ref) and torch.equal(db, db_ref)
 
 
 @pytest.mark.parametrize("N,Cin,Co,H", [(2, 64, 64, 20), (2, 128, 128, 14), (3, 256, 256, 7),

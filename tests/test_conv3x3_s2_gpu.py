@@ -67,6 +67,12 @@ def test_s2dgrad_bnsums(cuda, N, Co, Ci, Ho):
     dz = lib().bn_bwd_apply(y, z, gam, bet, mean, invstd, s, q)
     dz_ref, _, _, _ = lib().bn_bwd(y, None, z, None, gam, bet, mean, invstd, True, False)
     assert _rel(_rows(dz), _rows(dz_ref)) < 1e-2
+    # the BN's parameter gradients from the sums' finalize launch == bn_bwd_coeffs' values
+    dg, db = torch.empty_like(gam), torch.empty_like(bet)
+    y2, s2, q2 = lib().conv_gemm_s2dgrad(dy, wr, zero, z, sc, bi, mean, invstd, dg, db)
+    assert torch.equal(y2, y) and torch.equal(s2, s) and torch.equal(q2, q)
+    _, _, _, dg_ref, db_ref = lib().bn_bwd_coeffs(s, q, gam, mean, invstd, Z.shape[0])
+    assert torch.equal(dg, dg_ref) and torch.equal(db, db_ref)
 
 
 @pytest.mark.parametrize("inplanes,planes,H", [(256, 128, 28), (512, 256, 14)])
