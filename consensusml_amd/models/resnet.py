@@ -87,6 +87,7 @@ class _Conv1x1Fn(torch.autograd.Function):
     def forward(ctx, x, w, link, fwd_gemm, dgrad_gemm, own_wgrad=False):
         ctx.save_for_backward(x, w)
         ctx.link = link
+        ctx.wt = fconv.cached_wt(w)   # W^T from the forward's layout prefetch, if any
         ctx.dgrad_gemm = dgrad_gemm
         ctx.own_wgrad = own_wgrad
         N, C, H, W = x.shape
@@ -120,17 +121,19 @@ class _Conv1x1Fn(torch.autograd.Function):
             link = ctx.link
             g = link.take() if link is not None else None
             if isinstance(g, fconv.MaskedGrad):
-                return fconv.masked_link_dgrad(dy, w, g, link), dw, None, None, None, None
+                return (fconv.masked_link_dgrad(dy, w, g, link, ctx.wt), dw, None, None, None,
+                        None)
             if isinstance(g, fconv.S2Grad):
                 g = g.materialize()
+            w_nk = ctx.wt if ctx.wt is not None else w2.t()
             if g is not None:
                 dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
                 if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
-                    d2 = fconv.conv_mm(dy2, w2.t(), acc=dres)   # beta = 1 epilogue, in place
+                    d2 = fconv.conv_mm(dy2, w_nk, acc=dres)   # beta = 1 epilogue, in place
                 else:
                     d2 = torch.addmm(dres, dy2, w2)
             else:
-                d2 = fconv.conv_mm(dy2, w2.t())
+                d2 = fconv.conv_mm(dy2, w_nk)
             dx = d2.view(N, H, W, C).permute(0, 3, 1, 2)
         return dx, dw, None, None, None, None
 
@@ -463,17 +466,19 @@ class ResNet(nn.Module):
             x = bn_relu_max_pool2d(self.stem(x), self.bn1, 3, 2, 1)
         else:
             x = max_pool2d(self.bn1(self.stem(x)), 3, 2, 1)
-        # every block's 3x3 weight layouts (implicit-GEMM forward / data gradient) in one launch
-        # for this forward (PerfPolicy.batch_wlayouts) instead of one per conv
+        # every block's 3x3 weight layouts (implicit-GEMM forward / data gradient) and conv1
+        # transpose (1x1 data-gradient operand) in one launch for this forward
+        # (PerfPolicy.batch_wlayouts) instead of one per conv
+        blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4)
+                  for b in layer]
         batched = (pol.batch_wlayouts and self.training and torch.is_grad_enabled()
-                   and fconv.prefetch_w3x3_layouts(
-                       [b.conv2.weight for layer in (self.layer1, self.layer2, self.layer3,
-                                                     self.layer4) for b in layer]))
+                   and fconv.prefetch_wlayouts([b.conv2.weight for b in blocks]
+                                               + [b.conv1.weight for b in blocks]))
         try:
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         finally:
             if batched:
-                fconv.clear_w3x3_layouts()
+                fconv.clear_wlayouts()
         return self.fc(global_avg_pool(x))
 
 

@@ -86,7 +86,7 @@ def conv_mm(a: torch.Tensor, w_nk: torch.Tensor, acc: Optional[torch.Tensor] = N
 
 
 def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm: bool,
-           link) -> torch.Tensor:
+           link, wt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dX of a 1x1 conv (x only supplies the shape for MIOpen). GEMM path: dX = dY W, with a
     residual gradient parked on ``link`` absorbed by the beta = 1 epilogue."""
     N, C, H, W = x.shape
@@ -96,35 +96,40 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm
         w2 = w.reshape(Co, C)
         g = link.take() if link is not None else None
         if isinstance(g, MaskedGrad):
-            return masked_link_dgrad(dy, w, g, link)
+            return masked_link_dgrad(dy, w, g, link, wt)
         if isinstance(g, S2Grad):
             if (_P().s2_link_dgrad and dy.dtype == torch.bfloat16 and C % 64 == 0 and Co % 64 == 0
                     and g.H == H and g.W == W):
-                wt = w.reshape(Co, C).t().contiguous()
+                if wt is None:
+                    wt = w.reshape(Co, C).t().contiguous()
                 return lib().conv1x1_link_s2(dy.contiguous(memory_format=torch.channels_last), wt,
                                              g.g)
             g = g.materialize()
+        w_nk = wt if wt is not None else w2.t()   # W^T: prefetched, or transposed by conv_mm
         if g is not None:
             dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
             if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
-                d2 = conv_mm(dy2, w2.t(), acc=dres)
+                d2 = conv_mm(dy2, w_nk, acc=dres)
             else:
                 d2 = torch.addmm(dres, dy2, w2)
         else:
-            d2 = conv_mm(dy2, w2.t())
+            d2 = conv_mm(dy2, w_nk)
         return d2.view(N, H, W, C).permute(0, 3, 1, 2)
     dx, _, _ = torch.ops.aten.convolution_backward(
         dy, x, w, None, [stride, stride], [0, 0], [1, 1], False, [0, 0], 1, [True, False, False])
     return dx
 
 
-def masked_link_dgrad(dy: torch.Tensor, w: torch.Tensor, mg: MaskedGrad, link) -> torch.Tensor:
+def masked_link_dgrad(dy: torch.Tensor, w: torch.Tensor, mg: MaskedGrad, link,
+                      wt: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dX = dY W + m * g of a stride-1 1x1 conv in one kernel (``conv1x1_link``: the masked
     residual gradient is added in the epilogue, never materialised). If the link carries the
     producer's BN context (its bn3 applies its backward in its own convs), the same epilogue
-    emits that BN's backward sums over dX and leaves them on the link."""
+    emits that BN's backward sums over dX and leaves them on the link. ``wt``: W^T [Ci, Co]
+    if the forward already has it (``cached_wt``)."""
     Co, Ci = w.shape[0], w.shape[1]
-    wt = w.reshape(Co, Ci).t().contiguous()
+    if wt is None:
+        wt = w.reshape(Co, Ci).t().contiguous()
     bctx = link.bn_ctx if link is not None else None
     if bctx is not None:
         z, mask, mean, invstd = bctx
@@ -165,6 +170,7 @@ class _Conv1x1BNStatsFn(torch.autograd.Function):
         y, mean, invstd = out[:3]
         if aff is not None:   # the next BN's affine from the statistics' finalize launch
             _stash_affine(mean, out[3], out[4], aff)
+        ctx.wt = cached_wt(w)
         ctx.save_for_backward(x, w)
         ctx.stride, ctx.dgrad_gemm, ctx.own_wgrad, ctx.link = stride, dgrad_gemm, own_wgrad, link
         ctx.mark_non_differentiable(mean, invstd)
@@ -175,7 +181,7 @@ class _Conv1x1BNStatsFn(torch.autograd.Function):
     def backward(ctx, dy, _dm, _di):
         x, w = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dx = _dgrad(dy, x, w, ctx.stride, ctx.dgrad_gemm, ctx.link) \
+        dx = _dgrad(dy, x, w, ctx.stride, ctx.dgrad_gemm, ctx.link, ctx.wt) \
             if ctx.needs_input_grad[0] else None
         dw = _wgrad(dy, x, w, ctx.stride, ctx.own_wgrad) if ctx.needs_input_grad[1] else None
         return dx, dw, None, None, None, None, None, None, None, None, None
@@ -506,8 +512,13 @@ class _RecomputeDownTailFn(torch.autograd.Function):
             scd, bid = _affine(gd, bd, md, idd)
         ctx.grams = grams
         Co, P_, Cin = w3.shape[0], w3.shape[1], wd.shape[1]
-        bias = bi3 + bid
-        w_cat = scaled_cat(w3c.view(Co, P_), sc3, wdc.view(Co, Cin), scd)
+        if z.is_cuda and w3c.dtype == torch.bfloat16 and wdc.dtype == torch.bfloat16:
+            # both halves and the bias sum in one launch (bit-identical to the three below)
+            w_cat, bias = L.scaled_cat_bias(w3c.view(Co, P_), sc3, wdc.view(Co, Cin), scd, bi3,
+                                            bid)
+        else:
+            bias = bi3 + bid
+            w_cat = scaled_cat(w3c.view(Co, P_), sc3, wdc.view(Co, Cin), scd)
         dev = z.device
         # x: the block input, a ReLU output, staged as is
         y, mask = L.conv1x1_cat_bnres(z, x, sc, bi, None, None, w_cat,
@@ -749,25 +760,33 @@ def _wgrad3x3(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor) -> torch.Tenso
         dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1]
 
 
-_WL_BATCH = {}   # id(weight) -> (weight, wf, wr): this forward's prefetched 3x3 layouts
+_WL_BATCH = {}   # id(weight) -> (weight, wf, wr): this forward's prefetched weight layouts
 
 
-def prefetch_w3x3_layouts(ws) -> bool:
-    """Make the ``_w3x3_layouts`` of all bf16 GPU 3x3 weights ``ws`` in one launch
-    (``conv3x3_wlayouts_multi``) for the forward about to run; the caller clears them with
-    ``clear_w3x3_layouts`` when it ends (the weights must not change in between). False (nothing
-    done) for fewer than two eligible weights."""
+def prefetch_wlayouts(ws) -> bool:
+    """Make the GEMM layouts of all bf16 GPU conv weights ``ws`` in one launch
+    (``conv_wlayouts_multi``) for the forward about to run: 3x3 weights' ``_w3x3_layouts``, 1x1
+    weights' transposes W^T (``cached_wt``: the 1x1 data-gradient operand, which the conv's
+    forward keeps for its backward). The caller clears them with ``clear_wlayouts`` when the
+    forward ends (the weights must not change in between). False (nothing done) for fewer than
+    two eligible weights."""
     ws = [w for w in ws if w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 4
-          and w.shape[2] == 3 and w.shape[3] == 3]
+          and w.shape[2] == w.shape[3] and w.shape[2] in (1, 3)]
     if len(ws) < 2:
         return False
-    for w, (wf, wr) in zip(ws, lib().conv3x3_wlayouts_multi(ws)):
+    for w, (wf, wr) in zip(ws, lib().conv_wlayouts_multi(ws)):
         _WL_BATCH[id(w)] = (w, wf, wr)
     return True
 
 
-def clear_w3x3_layouts() -> None:
+def clear_wlayouts() -> None:
     _WL_BATCH.clear()
+
+
+def cached_wt(w: torch.Tensor) -> Optional[torch.Tensor]:
+    """W^T [Ci, Co] of a prefetched 1x1 weight (``prefetch_wlayouts``), else None."""
+    e = _WL_BATCH.get(id(w))
+    return e[2] if e is not None and e[0] is w and w.shape[2] == 1 else None
 
 
 def _w3x3_layouts(w: torch.Tensor, want_wf: bool):
@@ -775,7 +794,7 @@ def _w3x3_layouts(w: torch.Tensor, want_wf: bool):
     and the data-gradient layout wr [Ci, 9 Co] (rotated, transposed: wr[ci][(3 ky + kx) Co + co] =
     w[co][ci][2 - ky][2 - kx]) of a 3x3 weight, in one launch (``conv3x3_wlayouts``) instead of a
     permute copy, a flip and another permute copy per conv and step -- or none when the model's
-    forward prefetched every block's layouts together (``prefetch_w3x3_layouts``)."""
+    forward prefetched every block's layouts together (``prefetch_wlayouts``)."""
     e = _WL_BATCH.get(id(w))
     if e is not None and e[0] is w:
         return (e[1] if want_wf else None), e[2]

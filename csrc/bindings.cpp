@@ -1482,27 +1482,51 @@ std::vector<Tensor> conv3x3_wlayouts(const Tensor& w, bool want_wf) {
   return {wf, wr};   // wf undefined (None) unless asked for
 }
 
-// conv3x3_wlayouts of several weights (all bf16 [Co, Ci, 3, 3] on one device, any strides) in one
-// launch: [(wf, wr), ...] (wf always made).
-std::vector<std::vector<Tensor>> conv3x3_wlayouts_multi(const std::vector<Tensor>& ws) {
+// GEMM layouts of several conv weights (bf16, one device, any strides) in one launch: a 3x3
+// [Co, Ci, 3, 3] gives (wf, wr) as conv3x3_wlayouts, a 1x1 [Co, Ci, 1, 1] gives (None, W^T
+// [Ci, Co] contiguous) -- [(wf, wr), ...].
+std::vector<std::vector<Tensor>> conv_wlayouts_multi(const std::vector<Tensor>& ws) {
   std::vector<std::vector<Tensor>> out;
   if (ws.empty()) return out;
   const c10::DeviceGuard guard(ws[0].device());
   std::vector<cml::WlDesc> d;
   for (const Tensor& w : ws) {
     TORCH_CHECK(w.is_cuda() && w.device() == ws[0].device() && w.scalar_type() == at::kBFloat16 &&
-                    w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3,
-                "conv3x3_wlayouts_multi: bf16 [Co, Ci, 3, 3] weights on one device");
-    const int64_t Co = w.size(0), Ci = w.size(1);
-    Tensor wr = at::empty({Ci, 9 * Co}, w.options().memory_format(at::MemoryFormat::Contiguous));
-    Tensor wf = at::empty({Co, 9 * Ci}, w.options().memory_format(at::MemoryFormat::Contiguous));
-    d.push_back(cml::WlDesc{w.data_ptr(), wf.data_ptr(), wr.data_ptr(), w.stride(0), w.stride(1),
-                            w.stride(2), w.stride(3), static_cast<int>(Co), static_cast<int>(Ci)});
+                    w.dim() == 4 && w.size(2) == w.size(3) && (w.size(2) == 3 || w.size(2) == 1),
+                "conv_wlayouts_multi: bf16 [Co, Ci, 3, 3] or [Co, Ci, 1, 1] weights on one device");
+    const int64_t Co = w.size(0), Ci = w.size(1), T = w.size(2) * w.size(3);
+    Tensor wr = at::empty({Ci, T * Co}, w.options().memory_format(at::MemoryFormat::Contiguous));
+    Tensor wf;
+    if (T == 9) wf = at::empty({Co, 9 * Ci}, w.options().memory_format(at::MemoryFormat::Contiguous));
+    d.push_back(cml::WlDesc{w.data_ptr(), T == 9 ? wf.data_ptr() : nullptr, wr.data_ptr(),
+                            w.stride(0), w.stride(1), w.stride(2), w.stride(3),
+                            static_cast<int>(Co), static_cast<int>(Ci), static_cast<int>(T)});
     out.push_back({wf, wr});
   }
   CML_CHECK_HIP(cml::launch_conv3x3_wlayouts_multi(d.data(), static_cast<int>(d.size()),
                                                    cur_stream()));
   return out;
+}
+
+// {w_cat bf16 [Co, k1 + k2] = [diag(s1) w1 | diag(s2) w2], bias fp32 [Co] = b1 + b2} in one
+// launch (bit-identical to two torch.mul into the halves and one add).
+std::vector<Tensor> scaled_cat_bias(const Tensor& w1, const Tensor& s1, const Tensor& w2,
+                                    const Tensor& s2, const Tensor& b1, const Tensor& b2) {
+  TORCH_CHECK(w1.is_cuda() && w2.device() == w1.device() && w1.scalar_type() == at::kBFloat16 &&
+                  w2.scalar_type() == at::kBFloat16 && w1.dim() == 2 && w2.dim() == 2 &&
+                  w1.is_contiguous() && w2.is_contiguous() && w1.size(0) == w2.size(0) &&
+                  w1.size(1) % 8 == 0 && w2.size(1) % 8 == 0,
+              "scaled_cat_bias: contiguous bf16 [Co, k1], [Co, k2] on one device, k % 8 == 0");
+  const int64_t Co = w1.size(0), k1 = w1.size(1), k2 = w2.size(1);
+  const c10::DeviceGuard guard(w1.device());
+  Tensor out = at::empty({Co, k1 + k2}, w1.options());
+  Tensor bias = at::empty({Co}, w1.options().dtype(at::kFloat));
+  CML_CHECK_HIP(cml::launch_scaled_cat_bias(
+      w1.data_ptr(), opt_ptr<const float>(s1, at::kFloat, "s1", Co), static_cast<int>(k1),
+      w2.data_ptr(), opt_ptr<const float>(s2, at::kFloat, "s2", Co), static_cast<int>(k2),
+      opt_ptr<const float>(b1, at::kFloat, "b1", Co), opt_ptr<const float>(b2, at::kFloat, "b2", Co),
+      static_cast<int>(Co), out.data_ptr(), bias.data_ptr<float>(), cur_stream()));
+  return {out, bias};
 }
 
 std::vector<Tensor> conv_gemm_bnsums(const Tensor& x, const Tensor& w, int64_t taps,
@@ -2679,8 +2703,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("z"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"),
         "stem backward (conv weight gradient through BN, dgamma, dbeta) from the pool output "
         "gradient, the pool input gradient gathered inside the kernel");
-  m.def("conv3x3_wlayouts_multi", &conv3x3_wlayouts_multi, py::arg("ws"),
-        "conv3x3_wlayouts of several 3x3 weights in one launch -> [(wf, wr), ...]");
+  m.def("conv_wlayouts_multi", &conv_wlayouts_multi, py::arg("ws"),
+        "GEMM layouts of several 3x3 / 1x1 conv weights in one launch -> [(wf, wr), ...]");
+  m.def("scaled_cat_bias", &scaled_cat_bias, py::arg("w1"), py::arg("s1"), py::arg("w2"),
+        py::arg("s2"), py::arg("b1"), py::arg("b2"),
+        "[diag(s1) w1 | diag(s2) w2] (bf16) and b1 + b2 in one launch");
   m.def("conv3x3_wlayouts", &conv3x3_wlayouts, py::arg("w"), py::arg("want_wf"),
         "forward / data-gradient GEMM layouts of a 3x3 conv weight in one launch");
   m.def("maxpool_bwd_sum", &maxpool_bwd_sum, "3x3/s2 max-pool backward + channel sums of dx",

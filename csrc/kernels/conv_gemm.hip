@@ -729,8 +729,9 @@ __global__ __launch_bounds__(256) void conv3x3_wlayouts_kernel(const uint16_t* _
   wr[(static_cast<int64_t>(ci) * 9 + (8 - t)) * Co + co] = v;
 }
 
-// Several weights' layouts in one launch (the 16 3x3 convs of a ResNet-50 forward: one launch
-// instead of 16 ~9 us ones): descriptors by value, workgroups [blk0[d], blk0[d + 1]) on weight d.
+// Several weights' layouts in one launch (the 16 3x3 convs of a ResNet-50 forward and its 1x1
+// transposes: one launch instead of 16 + 12 ~5-9 us ones): descriptors by value, workgroups
+// [blk0[d], blk0[d + 1]) on weight d.
 struct WlMulti {
   WlDesc d[kWlMax];
   int blk0[kWlMax + 1];
@@ -742,16 +743,17 @@ __global__ __launch_bounds__(256) void conv3x3_wlayouts_multi_kernel(const WlMul
   int i = 0;
   while (i + 1 < m.n && b >= m.blk0[i + 1]) ++i;
   const WlDesc& d = m.d[i];
+  const int T = d.taps;   // 9 (3x3) or 1 (1x1: wr is the plain transpose)
   const int64_t e = static_cast<int64_t>(b - m.blk0[i]) * 256 + threadIdx.x;
-  if (e >= static_cast<int64_t>(d.Co) * d.Ci * 9) return;
+  if (e >= static_cast<int64_t>(d.Co) * d.Ci * T) return;
   const int ci = static_cast<int>(e % d.Ci);
-  const int t = static_cast<int>((e / d.Ci) % 9);
-  const int co = static_cast<int>(e / (static_cast<int64_t>(d.Ci) * 9));
+  const int t = static_cast<int>((e / d.Ci) % T);
+  const int co = static_cast<int>(e / (static_cast<int64_t>(d.Ci) * T));
   const int ky = t / 3, kx = t - 3 * (t / 3);
   const uint16_t* w = reinterpret_cast<const uint16_t*>(d.w);
   const uint16_t v = w[co * d.s0 + ci * d.s1 + ky * d.s2 + kx * d.s3];
   if (d.wf) reinterpret_cast<uint16_t*>(d.wf)[e] = v;
-  reinterpret_cast<uint16_t*>(d.wr)[(static_cast<int64_t>(ci) * 9 + (8 - t)) * d.Co + co] = v;
+  reinterpret_cast<uint16_t*>(d.wr)[(static_cast<int64_t>(ci) * T + (T - 1 - t)) * d.Co + co] = v;
 }
 }  // namespace
 
@@ -762,10 +764,11 @@ hipError_t launch_conv3x3_wlayouts_multi(const WlDesc* d, int n, hipStream_t st)
     int64_t blk = 0;
     for (int i = 0; i < m.n; ++i) {
       const WlDesc& x = d[i0 + i];
-      if (x.Co < 1 || x.Ci < 1 || !x.w || !x.wr) return hipErrorInvalidValue;
+      if (x.Co < 1 || x.Ci < 1 || !x.w || !x.wr || (x.taps != 1 && x.taps != 9))
+        return hipErrorInvalidValue;
       m.d[i] = x;
       m.blk0[i] = static_cast<int>(blk);
-      blk += (static_cast<int64_t>(x.Co) * x.Ci * 9 + 255) / 256;
+      blk += (static_cast<int64_t>(x.Co) * x.Ci * x.taps + 255) / 256;
       if (blk >= (1ll << 31)) return hipErrorInvalidValue;
     }
     m.blk0[m.n] = static_cast<int>(blk);

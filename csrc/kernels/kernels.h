@@ -465,13 +465,14 @@ hipError_t launch_conv_gemm_s2dgrad(const void* dy, const void* wr, void* dx, co
 // 3x3 conv weight with strides s0..s3 (elements), in one launch; wf may be null.
 hipError_t launch_conv3x3_wlayouts(const void* w, int Co, int Ci, int64_t s0, int64_t s1,
                                    int64_t s2, int64_t s3, void* wf, void* wr, hipStream_t st);
-// The same for n weights in ceil(n / kWlMax) launches (descriptors passed by value).
+// The same for n weights in ceil(n / kWlMax) launches (descriptors passed by value); taps 1: a
+// 1x1 weight [Co][Ci][1][1], wr = its transpose [Ci][Co] (a 1x1 data gradient's GEMM operand).
 struct WlDesc {
   const void* w;
   void* wf;   // may be null
   void* wr;
   int64_t s0, s1, s2, s3;
-  int Co, Ci;
+  int Co, Ci, taps;
 };
 constexpr int kWlMax = 24;
 hipError_t launch_conv3x3_wlayouts_multi(const WlDesc* d, int n, hipStream_t st);
@@ -571,6 +572,11 @@ hipError_t launch_tail_bwd_prep(const void* W, const float* P, const float* s, c
                                 void* dW, void* wcat, float* bias, void* dgamma, void* dbeta,
                                 hipStream_t st);
 size_t tail_bwd_prep_work_floats(int Co, int p);
+// w_cat = [diag(s1) w1 | diag(s2) w2] (bf16 [Co][k1 + k2], each product rounded once from fp32)
+// and bias = b1 + b2 (fp32 [Co]) in one launch (the downsample recompute tail's folded weights).
+hipError_t launch_scaled_cat_bias(const void* w1, const float* s1, int k1, const void* w2,
+                                  const float* s2, int k2, const float* b1, const float* b2,
+                                  int Co, void* out, float* bias, hipStream_t st);
 hipError_t launch_bn_bwd_coeffs(const float* sdz, const float* sdzx, const void* gamma,
                                 const float* mean, const float* invstd, int C, int64_t M,
                                 float* ca, float* cb, float* cc, void* dgamma, void* dbeta,

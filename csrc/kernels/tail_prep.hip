@@ -211,7 +211,41 @@ __global__ __launch_bounds__(256) void tail_fin_kernel(const float* __restrict__
   }
 }
 
+// 8 consecutive outputs of a row per thread (k1, k2 multiples of 8)
+__global__ __launch_bounds__(256) void scaled_cat_bias_kernel(
+    const uint16_t* __restrict__ w1, const float* __restrict__ s1, int k1,
+    const uint16_t* __restrict__ w2, const float* __restrict__ s2, int k2,
+    const float* __restrict__ b1, const float* __restrict__ b2, int Co,
+    uint16_t* __restrict__ out, float* __restrict__ bias) {
+  const int cpr = (k1 + k2) / 8;
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= static_cast<int64_t>(Co) * cpr) return;
+  const int r = static_cast<int>(e / cpr), c = static_cast<int>(e - static_cast<int64_t>(r) * cpr) * 8;
+  const bool first = c < k1;
+  const uint4 u = first ? *reinterpret_cast<const uint4*>(w1 + static_cast<int64_t>(r) * k1 + c)
+                        : *reinterpret_cast<const uint4*>(w2 + static_cast<int64_t>(r) * k2 + c - k1);
+  const float sv = first ? s1[r] : s2[r];
+  const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    o[q] = pk_bf16(__uint_as_float(w4[q] << 16) * sv, __uint_as_float(w4[q] & 0xffff0000u) * sv);
+  *reinterpret_cast<uint4*>(out + static_cast<int64_t>(r) * (k1 + k2) + c) =
+      make_uint4(o[0], o[1], o[2], o[3]);
+  if (c == 0) bias[r] = b1[r] + b2[r];
+}
 }  // namespace
+
+hipError_t launch_scaled_cat_bias(const void* w1, const float* s1, int k1, const void* w2,
+                                  const float* s2, int k2, const float* b1, const float* b2,
+                                  int Co, void* out, float* bias, hipStream_t st) {
+  if (Co < 1 || k1 < 8 || k2 < 8 || k1 % 8 || k2 % 8) return hipErrorInvalidValue;
+  const int64_t n = static_cast<int64_t>(Co) * ((k1 + k2) / 8);
+  scaled_cat_bias_kernel<<<static_cast<unsigned>((n + 255) / 256), 256, 0, st>>>(
+      reinterpret_cast<const uint16_t*>(w1), s1, k1, reinterpret_cast<const uint16_t*>(w2), s2,
+      k2, b1, b2, Co, reinterpret_cast<uint16_t*>(out), bias);
+  return hipGetLastError();
+}
 
 hipError_t launch_tail_bwd_prep(const void* W, const float* P, const float* s, const float* gram,
                                 const float* cy, const void* gamma, const float* mean,

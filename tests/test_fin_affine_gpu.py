@@ -125,11 +125,26 @@ def test_conv3x3_wlayouts_multi_matches_single(cuda):
     for i, (co, ci) in enumerate(shapes):
         w = torch.randn(co, ci, 3, 3, device=cuda, generator=g0).bfloat16()
         ws.append(_nhwc(w) if i % 2 else w)
-    outs = lib().conv3x3_wlayouts_multi(ws)
-    assert len(outs) == len(ws)
+    w1 = [torch.randn(co, ci, 1, 1, device=cuda, generator=g0).bfloat16()
+          for co, ci in [(64, 256), (512, 1024), (128, 64)]]
+    outs = lib().conv_wlayouts_multi(ws + w1)
+    assert len(outs) == len(ws) + len(w1)
     for w, (wf, wr) in zip(ws, outs):
         rf, rr = lib().conv3x3_wlayouts(w, True)
         assert torch.equal(wf, rf) and torch.equal(wr, rr)
+    for w, (wf, wr) in zip(w1, outs[len(ws):]):   # 1x1: the transpose only
+        assert wf is None and torch.equal(wr, w.reshape(w.shape[0], -1).t().contiguous())
+
+
+def test_scaled_cat_bias(cuda):
+    from consensusml_amd.ops.conv import scaled_cat
+    g0 = torch.Generator(device=cuda).manual_seed(8)
+    for co, k1, k2 in [(256, 64, 64), (1024, 256, 512), (2048, 512, 1024)]:
+        w1 = torch.randn(co, k1, device=cuda, generator=g0).bfloat16()
+        w2 = torch.randn(co, k2, device=cuda, generator=g0).bfloat16()
+        s1, s2, b1, b2 = (torch.randn(co, device=cuda, generator=g0) for _ in range(4))
+        w_cat, bias = lib().scaled_cat_bias(w1, s1, w2, s2, b1, b2)
+        assert torch.equal(w_cat, scaled_cat(w1, s1, w2, s2)) and torch.equal(bias, b1 + b2)
 
 
 def test_resnet_forward_prefetches_layouts(cuda, monkeypatch):
@@ -139,7 +154,7 @@ def test_resnet_forward_prefetches_layouts(cuda, monkeypatch):
     from consensusml_amd.ops import conv as fconv
     L = lib()
     n = {"single": 0, "multi": 0}
-    single, multi = L.conv3x3_wlayouts, L.conv3x3_wlayouts_multi
+    single, multi = L.conv3x3_wlayouts, L.conv_wlayouts_multi
 
     def cs(*a, **k):
         n["single"] += 1
@@ -149,7 +164,7 @@ def test_resnet_forward_prefetches_layouts(cuda, monkeypatch):
         n["multi"] += 1
         return multi(*a, **k)
     monkeypatch.setattr(L, "conv3x3_wlayouts", cs)
-    monkeypatch.setattr(L, "conv3x3_wlayouts_multi", cm)
+    monkeypatch.setattr(L, "conv_wlayouts_multi", cm)
     m = R.resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last).bfloat16()
     x = _nhwc(torch.randn(4, 3, 64, 64, device=cuda).bfloat16())
     m(x).float().sum().backward()
