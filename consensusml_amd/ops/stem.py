@@ -55,12 +55,14 @@ class _StemFn(torch.autograd.Function):
         dy2 = ctx.link.take_tensor() if ctx.link is not None else None
         if dy2 is not None and dy2.shape != dy.shape:
             dy, dy2 = dy + dy2, None
+        wt, gt, bt = ctx.dtypes
         if _P().stem_pool_gather:
-            dw, dg, db = lib().stem_wgrad_pool(dy, idx, dy2, z, x, mean, invstd, gamma)
+            # bf16 parameters: the final kernel writes bf16 itself (no three cast launches)
+            bf = wt == gt == bt == torch.bfloat16
+            dw, dg, db = lib().stem_wgrad_pool(dy, idx, dy2, z, x, mean, invstd, gamma, bf)
         else:
             g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3], dy2)
             dw, dg, db = lib().stem_wgrad(g, z, x, mean, invstd, gamma, gsum)
-        wt, gt, bt = ctx.dtypes
         return None, dw.to(wt), dg.to(gt), db.to(bt), None, None, None, None, None, None
 
 

@@ -676,7 +676,7 @@ std::vector<Tensor> stem_wgrad(const Tensor& g_in, const Tensor& z, const Tensor
 std::vector<Tensor> stem_wgrad_pool(const Tensor& dy_in, const Tensor& idx,
                                     const optional<Tensor>& dy2_in, const Tensor& z,
                                     const Tensor& x, const Tensor& mean, const Tensor& invstd,
-                                    const Tensor& gamma) {
+                                    const Tensor& gamma, bool bf16_out) {
   check_nhwc(x, "x");
   check_nhwc(z, "z");
   Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
@@ -723,15 +723,17 @@ std::vector<Tensor> stem_wgrad_pool(const Tensor& dy_in, const Tensor& idx,
   Tensor part = at::empty({grid, pw}, f32);
   Tensor tot = at::empty({static_cast<int64_t>(cml::stem_wgrad_tot_doubles())},
                          x.options().dtype(at::kDouble));
-  Tensor dw = at::empty({64, C, 7, 7}, f32);
-  Tensor dg = at::empty({64}, f32), db = at::empty({64}, f32);
+  // bf16_out: the outputs in the (bf16) parameters' dtype from the final kernel itself
+  auto odt = bf16_out ? x.options().dtype(at::kBFloat16) : f32;
+  Tensor dw = at::empty({64, C, 7, 7}, odt);
+  Tensor dg = at::empty({64}, odt), db = at::empty({64}, odt);
   CML_CHECK_HIP(cml::launch_stem_wgrad(pg.data_ptr(), z.data_ptr(), x.data_ptr(),
                                        mean.data_ptr<float>(), invstd.data_ptr<float>(),
                                        gamma.data_ptr(), nullptr, part.data_ptr<float>(), grid,
-                                       tot.data_ptr<double>(), dw.data_ptr<float>(),
-                                       dg.data_ptr<float>(), db.data_ptr<float>(), N, H, W, C, OH,
-                                       OW, cur_stream(), idx.data_ptr<uint8_t>(),
-                                       cwork.data_ptr<float>()));
+                                       tot.data_ptr<double>(), dw.data_ptr(), dg.data_ptr(),
+                                       db.data_ptr(), N, H, W, C, OH, OW, cur_stream(),
+                                       idx.data_ptr<uint8_t>(), cwork.data_ptr<float>(),
+                                       bf16_out));
   return {dw, dg, db};
 }
 
@@ -1480,6 +1482,21 @@ std::vector<Tensor> conv3x3_wlayouts(const Tensor& w, bool want_wf) {
                                              want_wf ? wf.data_ptr() : nullptr, wr.data_ptr(),
                                              cur_stream()));
   return {wf, wr};   // wf undefined (None) unless asked for
+}
+
+// Global-average-pool backward: g [N, C] bf16 -> dx [N, C, H, W] channels_last, g / (H W) at every
+// pixel (one write-only pass; bit-identical to (g.float() / (H W)).to(bf16) broadcast).
+Tensor avgpool_bwd(const Tensor& g_in, int64_t H, int64_t W) {
+  Tensor g = g_in.contiguous();
+  TORCH_CHECK(g.is_cuda() && g.scalar_type() == at::kBFloat16 && g.dim() == 2 && g.size(1) % 8 == 0,
+              "avgpool_bwd: bf16 [N, C] CUDA gradient, C % 8 == 0");
+  const c10::DeviceGuard guard(g.device());
+  const int64_t N = g.size(0), C = g.size(1);
+  Tensor dx = at::empty({N, C, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  CML_CHECK_HIP(cml::launch_avgpool_bwd(g.data_ptr(), dx.data_ptr(), static_cast<int>(N),
+                                        static_cast<int>(H * W), static_cast<int>(C),
+                                        cur_stream()));
+  return dx;
 }
 
 // GEMM layouts of several conv weights (bf16, one device, any strides) in one launch: a 3x3
@@ -2701,8 +2718,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_sums", &bn_bwd_sums, "reduction half of a BN (+ ReLU) backward");
   m.def("stem_wgrad_pool", &stem_wgrad_pool, py::arg("dy"), py::arg("idx"), py::arg("dy2"),
         py::arg("z"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"),
+        py::arg("bf16_out") = false,
         "stem backward (conv weight gradient through BN, dgamma, dbeta) from the pool output "
         "gradient, the pool input gradient gathered inside the kernel");
+  m.def("avgpool_bwd", &avgpool_bwd, py::arg("g"), py::arg("H"), py::arg("W"),
+        "global-average-pool backward into NHWC in one write-only pass");
   m.def("conv_wlayouts_multi", &conv_wlayouts_multi, py::arg("ws"),
         "GEMM layouts of several 3x3 / 1x1 conv weights in one launch -> [(wf, wr), ...]");
   m.def("scaled_cat_bias", &scaled_cat_bias, py::arg("w1"), py::arg("s1"), py::arg("w2"),

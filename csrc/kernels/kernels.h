@@ -169,6 +169,8 @@ hipError_t launch_bn_bwd2(const void* dy, const void* dy2, const void* x1, const
 // y = x[:, ::2, ::2, :] of NHWC bf16 x [N][H][W][C] (y [N][ceil(H/2)][ceil(W/2)][C]); the
 // scatter writes the full-resolution dx with g at the even pixels and zeros elsewhere. C % 8 == 0.
 hipError_t launch_subsample2(const void* x, void* y, int N, int H, int W, int C, hipStream_t st);
+// Global-average-pool backward: g bf16 [N][C] -> dx NHWC bf16 [N][HW][C], bf16(g / HW) everywhere.
+hipError_t launch_avgpool_bwd(const void* g, void* dx, int N, int HW, int C, hipStream_t st);
 hipError_t launch_upsample2_scatter(const void* g, void* dx, int N, int H, int W, int C,
                                     hipStream_t st);
 // NHWC bf16 max-pool with a one-byte argmax per output element; backward is a gather.
@@ -350,12 +352,14 @@ hipError_t launch_stem_conv_fwd(const void* x, const void* wpk, void* z, float* 
 hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const float* mean,
                              const float* invstd, const void* gamma, const float* gsum,
                              float* part, int grid,
-                             double* tot, float* dw, float* dgamma, float* dbeta, int N, int H,
+                             double* tot, void* dw, void* dgamma, void* dbeta, int N, int H,
                              int W, int C, int OH, int OW, hipStream_t stream,
-                             const uint8_t* pidx = nullptr, float* cola_work = nullptr);
+                             const uint8_t* pidx = nullptr, float* cola_work = nullptr,
+                             bool out_bf16 = false);
 // pidx != nullptr: g is the 3x3 / s2 / p1 max-pool's output gradient [N][PH][PW][64] and pidx its
 // forward argmax bytes; the kernel gathers the pool's input gradient itself and takes dbeta and
 // mean(g) from its own sums (gsum unused). cola_work (always): stem_cola_work_floats floats.
+// out_bf16: dw / dgamma / dbeta written as bf16 (else fp32).
 // tot: stem_wgrad_tot_doubles() doubles.
 size_t stem_wgrad_tot_doubles();
 size_t stem_cola_work_floats(int N, int H, int W, int C);

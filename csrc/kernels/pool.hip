@@ -542,7 +542,36 @@ __global__ __launch_bounds__(256) void upsample2_scatter_kernel(const uint4* __r
   dx[e] = v;
 }
 
+// Global-average-pool backward into NHWC: dx[n][p][c] = bf16(float(g[n][c]) / HW) for every pixel
+// p (one write-only pass; 8 channels per thread, the same fp32 division as g.float() / HW).
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const uint4* __restrict__ g,
+                                                          uint4* __restrict__ dx, int64_t total,
+                                                          int C8, int HW, float hw) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int64_t pix = e / C8;
+  const int c = static_cast<int>(e - pix * C8);
+  const int64_t n = pix / HW;
+  const uint4 u = g[n * C8 + c];
+  const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    o[q] = pk_bf16(__uint_as_float(w4[q] << 16) / hw, __uint_as_float(w4[q] & 0xffff0000u) / hw);
+  dx[e] = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 }  // namespace
+
+hipError_t launch_avgpool_bwd(const void* g, void* dx, int N, int HW, int C, hipStream_t st) {
+  if (C % 8 || N < 1 || HW < 1) return hipErrorInvalidValue;
+  const int C8 = C / 8;
+  const int64_t total = static_cast<int64_t>(N) * HW * C8;
+  avgpool_bwd_kernel<<<static_cast<unsigned>((total + 255) / 256), 256, 0, st>>>(
+      reinterpret_cast<const uint4*>(g), reinterpret_cast<uint4*>(dx), total, C8, HW,
+      static_cast<float>(HW));
+  return hipGetLastError();
+}
 
 // CML_POOL_BLOCKS=0 selects the one-output-per-thread forward for the stem (A/B)
 static bool k3s2_blocks() {

@@ -939,15 +939,30 @@ __global__ __launch_bounds__(256) void stem_wgrad_fold_kernel(const float* __res
 // X = sum xhat (x) im2col, colA[k] = sum over pixels of im2col[.][k] (stem_cola); dgamma = s2,
 // dbeta = s1 = sum g: the channel sums of the pool backward (gsum) or, without them (GATHER), the
 // kernel's own partials.
+// BF: the three outputs in bf16 (RNE of the fp32 values: the parameters' dtype, no cast launches)
+// (the empty asm keeps the fp32 rounding step: without it the fp64 -> fp32 -> bf16 conversion chain
+// may be folded into one fp64 -> bf16 rounding, which differs from casting the fp32 output where
+// the fp32 value is a bf16 tie)
+template <bool BF>
+__device__ __forceinline__ void stem_out(void* p, int i, float v) {
+  if constexpr (BF) {
+    asm volatile("" : "+v"(v));
+    reinterpret_cast<uint16_t*>(p)[i] = f2bf(v);
+  } else {
+    reinterpret_cast<float*>(p)[i] = v;
+  }
+}
+
+template <bool BF>
 __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __restrict__ tot,
                                                               const uint16_t* __restrict__ gamma,
                                                               const float* __restrict__ invstd,
                                                               const float* __restrict__ gsum,
                                                               const double* __restrict__ cola,
                                                               double M, int C,
-                                                              float* __restrict__ dw,
-                                                              float* __restrict__ dgamma,
-                                                              float* __restrict__ dbeta) {
+                                                              void* __restrict__ dw,
+                                                              void* __restrict__ dgamma,
+                                                              void* __restrict__ dbeta) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   const double* G = tot;
   const double* X = tot + kCo * kKP;
@@ -963,12 +978,12 @@ __global__ __launch_bounds__(256) void stem_wgrad_final_kernel(const double* __r
     const double s1 = gsum ? static_cast<double>(gsum[co]) : S1[co];
     double ca = 0.0;
     for (int sl = 0; sl < kColaS; ++sl) ca += cola[sl * kKP + kc];
-    dw[e] = static_cast<float>(
-        a * (G[co * kKP + kc] - s1 / M * ca - S2[co] / M * X[co * kKP + kc]));
+    stem_out<BF>(dw, e, static_cast<float>(
+        a * (G[co * kKP + kc] - s1 / M * ca - S2[co] / M * X[co * kKP + kc])));
   }
   if (e < kCo) {
-    dgamma[e] = static_cast<float>(S2[e]);
-    dbeta[e] = gsum ? gsum[e] : static_cast<float>(S1[e]);
+    stem_out<BF>(dgamma, e, static_cast<float>(S2[e]));
+    stem_out<BF>(dbeta, e, gsum ? gsum[e] : static_cast<float>(S1[e]));
   }
 }
 
@@ -1194,9 +1209,10 @@ hipError_t launch_stem_conv_fwd(const void* x, const void* wpk, void* z, float* 
 
 hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const float* mean,
                              const float* invstd, const void* gamma, const float* gsum,
-                             float* part, int grid, double* tot, float* dw, float* dgamma,
-                             float* dbeta, int N, int H, int W, int C, int OH, int OW,
-                             hipStream_t st, const uint8_t* pidx, float* cola_work) {
+                             float* part, int grid, double* tot, void* dw, void* dgamma,
+                             void* dbeta, int N, int H, int W, int C, int OH, int OW,
+                             hipStream_t st, const uint8_t* pidx, float* cola_work,
+                             bool out_bf16) {
   if (!cola_work || (!pidx && !gsum)) return hipErrorInvalidValue;
   if ((C != 3 && C != 4) || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1 || N < 1 || grid < 1)
     return hipErrorInvalidValue;
@@ -1243,9 +1259,14 @@ hipError_t launch_stem_wgrad(const void* g, const void* z, const void* x, const 
   if (v16) stem_cola_rows_kernel<true><<<dim3(H, nchunk), 256, 0, st>>>(xp, N, H, W, C, cola_work);
   else stem_cola_rows_kernel<false><<<dim3(H, nchunk), 256, 0, st>>>(xp, N, H, W, C, cola_work);
   stem_cola_kernel<<<dim3(kKP / 4, kColaS), kColaT, 0, st>>>(cola_work, nchunk, H, W, C, OH, OW, cola);
-  stem_wgrad_final_kernel<<<(kCo * C * 49 + 255) / 256, 256, 0, st>>>(
-      tot, reinterpret_cast<const uint16_t*>(gamma), invstd, pidx ? nullptr : gsum, cola,
-      static_cast<double>(N) * OH * OW, C, dw, dgamma, dbeta);
+  if (out_bf16)
+    stem_wgrad_final_kernel<true><<<(kCo * C * 49 + 255) / 256, 256, 0, st>>>(
+        tot, reinterpret_cast<const uint16_t*>(gamma), invstd, pidx ? nullptr : gsum, cola,
+        static_cast<double>(N) * OH * OW, C, dw, dgamma, dbeta);
+  else
+    stem_wgrad_final_kernel<false><<<(kCo * C * 49 + 255) / 256, 256, 0, st>>>(
+        tot, reinterpret_cast<const uint16_t*>(gamma), invstd, pidx ? nullptr : gsum, cola,
+        static_cast<double>(N) * OH * OW, C, dw, dgamma, dbeta);
   return hipGetLastError();
 }
 

@@ -170,3 +170,15 @@ def test_resnet_forward_prefetches_layouts(cuda, monkeypatch):
     m(x).float().sum().backward()
     assert n["multi"] == 1 and n["single"] == 0, n
     assert not fconv._WL_BATCH
+
+
+def test_avgpool_bwd_matches_reference(cuda):
+    from consensusml_amd.models.resnet import global_avg_pool
+    for N, C, H in [(8, 2048, 7), (3, 64, 5), (2, 512, 1)]:
+        g = torch.randn(N, C, device=cuda).bfloat16()
+        dx = lib().avgpool_bwd(g, H, H)
+        ref = (g.float() / (H * H)).bfloat16()[:, :, None, None].expand(N, C, H, H)
+        assert dx.is_contiguous(memory_format=torch.channels_last) and torch.equal(dx, ref)
+        x = _nhwc(torch.randn(N, C, H, H, device=cuda).bfloat16()).requires_grad_(True)
+        global_avg_pool(x).backward(g)
+        assert torch.equal(x.grad, ref)

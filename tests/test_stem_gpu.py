@@ -203,6 +203,10 @@ def test_stem_wgrad_pool_gather(cuda, N, C, H, W, two):
     dy = torch.randn_like(y)
     dy2 = torch.randn_like(y) if two else None
     dw, dg, db = lib().stem_wgrad_pool(dy, idx, dy2, z, x, mean, invstd, gam)
+    # bf16 outputs from the final kernel == the fp32 ones cast (the parameters' dtype)
+    for a, b in zip(lib().stem_wgrad_pool(dy, idx, dy2, z, x, mean, invstd, gam, True),
+                    (dw, dg, db)):
+        assert a.dtype == torch.bfloat16 and torch.equal(a, b.to(torch.bfloat16))
     g, gsum = lib().maxpool_bwd_sum(dy, idx, z.shape[2], z.shape[3], dy2)
     dw2, dg2, db2 = lib().stem_wgrad(g, z, x, mean, invstd, gam, gsum)
     gabs = g.double().abs().sum((0, 2, 3)).clamp_min(1e-6)
