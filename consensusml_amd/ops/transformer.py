@@ -45,23 +45,26 @@ class _CEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, ignore_index):
         lse, rows = lib().ce_fwd(logits, labels, ignore_index)
-        count = (labels != ignore_index).sum().clamp_(min=1).float()
+        # mean loss and the valid-label count in one launch (fixed-order fp64 sums; was five
+        # ATen launches: ne, sum, clamp, cast, sum + divide)
+        loss, count = lib().ce_mean(rows, labels, ignore_index)
         ctx.save_for_backward(logits, labels, lse, count)
         ctx.ignore = ignore_index
-        return rows.sum() / count
+        return loss
 
     @staticmethod
     def backward(ctx, go):
         logits, labels, lse, count = ctx.saved_tensors
-        scale = (go.float() / count).reshape(1)
+        # the kernels divide grad_output by the count themselves (no divide launch)
+        go = go.float().reshape(1)
         if _row_strided(logits) and logits.shape[0] % 64 == 0:
             # padded logits of a biased linear: gradient rows with the same stride, and the bias
             # gradient's column partials from the same pass
-            g, part = lib().ce_bwd_cs(logits, labels, lse, scale, ctx.ignore)
+            g, part = lib().ce_bwd_cs(logits, labels, lse, go, ctx.ignore, count)
             _LOGIT_BIAS_PARTS.clear()
             _LOGIT_BIAS_PARTS[g.data_ptr()] = (part, g.shape)
             return g, None, None
-        return lib().ce_bwd(logits, labels, lse, scale, ctx.ignore), None, None
+        return lib().ce_bwd(logits, labels, lse, go, ctx.ignore, count), None, None
 
 
 def cross_entropy(logits: torch.Tensor, labels: torch.Tensor,

@@ -1867,7 +1867,7 @@ std::vector<Tensor> ce_fwd(const Tensor& logits, const Tensor& labels, int64_t i
 // [R, ld] buffer, part [R / 64, ld] fp32 column sums per 64-row block) -- ce_part_fold turns part
 // into the logits bias gradient.
 std::vector<Tensor> ce_bwd_cs(const Tensor& logits, const Tensor& labels, const Tensor& lse,
-                              const Tensor& scale, int64_t ignore) {
+                              const Tensor& scale, int64_t ignore, const optional<Tensor>& div) {
   const int64_t ld = ce_row_stride(logits);
   const int64_t R = logits.size(0), V = logits.size(1);
   TORCH_CHECK(ld % 8 == 0 && R % 64 == 0, "ce_bwd_cs: needs a row stride % 8 == 0 and R % 64 == 0");
@@ -1883,7 +1883,8 @@ std::vector<Tensor> ce_bwd_cs(const Tensor& logits, const Tensor& labels, const 
   CML_CHECK_HIP(cml::launch_ce_bwd_cs(logits.data_ptr(), R, static_cast<int>(V), ld,
                                       labels.data_ptr<int64_t>(), ignore, lse.data_ptr<float>(),
                                       scale.data_ptr<float>(), gbuf.data_ptr(),
-                                      part.data_ptr<float>(), cur_stream()));
+                                      part.data_ptr<float>(), cur_stream(),
+                                      opt_ptr<const float>(div, at::kFloat, "div", 1)));
   return {gbuf.narrow(1, 0, V), part};
 }
 
@@ -1929,7 +1930,7 @@ void ce_part_fold(const Tensor& part, int64_t V, int64_t nseg, Tensor& out) {
 }
 
 Tensor ce_bwd(const Tensor& logits, const Tensor& labels, const Tensor& lse, const Tensor& scale,
-              int64_t ignore) {
+              int64_t ignore, const optional<Tensor>& div) {
   check_bf16c(logits, "logits");
   const int64_t R = logits.size(0), V = logits.size(1);
   TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.numel() == R &&
@@ -1942,8 +1943,24 @@ Tensor ce_bwd(const Tensor& logits, const Tensor& labels, const Tensor& lse, con
   Tensor g = at::empty_like(logits);
   CML_CHECK_HIP(cml::launch_ce_bwd(logits.data_ptr(), R, static_cast<int>(V),
                                    labels.data_ptr<int64_t>(), ignore, lse.data_ptr<float>(),
-                                   scale.data_ptr<float>(), g.data_ptr(), cur_stream()));
+                                   scale.data_ptr<float>(), g.data_ptr(), cur_stream(),
+                                   opt_ptr<const float>(div, at::kFloat, "div", 1)));
   return g;
+}
+
+// {mean loss (0-dim), n_valid [1]} fp32 from ce_fwd's per-row losses in one launch (fixed-order
+// fp64 sums; n_valid = max(#labels != ignore, 1)).
+std::vector<Tensor> ce_mean(const Tensor& loss, const Tensor& labels, int64_t ignore) {
+  TORCH_CHECK(loss.is_cuda() && loss.scalar_type() == at::kFloat && loss.is_contiguous() &&
+                  labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() &&
+                  labels.numel() == loss.numel() && loss.numel() >= 1,
+              "ce_mean: contiguous fp32 loss [R] and int64 labels [R] on the GPU");
+  const c10::DeviceGuard guard(loss.device());
+  Tensor out = at::empty({}, loss.options()), count = at::empty({1}, loss.options());
+  CML_CHECK_HIP(cml::launch_ce_mean(loss.data_ptr<float>(), labels.data_ptr<int64_t>(),
+                                    loss.numel(), ignore, out.data_ptr<float>(),
+                                    count.data_ptr<float>(), cur_stream()));
+  return {out, count};
 }
 
 // x (and res) [.., D] bf16 contiguous; w (and b) [D] bf16. Returns (y, sum|undef, mean|undef, rstd).
@@ -2735,9 +2752,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("multi_copy", &multi_copy, "multi-tensor copy in one launch per 32 tensors");
   m.def("pad_c4", &pad_c4, "NHWC bf16 channel zero-padding to 4");
   m.def("ce_fwd", &ce_fwd, "fused cross-entropy forward over bf16 logits (lse, per-row loss)");
-  m.def("ce_bwd", &ce_bwd, "fused cross-entropy backward (bf16 logits gradient)");
-  m.def("ce_bwd_cs", &ce_bwd_cs, "cross-entropy backward over row-strided logits + bias-gradient "
-        "column partials");
+  m.def("ce_bwd", &ce_bwd, py::arg("logits"), py::arg("labels"), py::arg("lse"), py::arg("scale"),
+        py::arg("ignore"), py::arg("div") = py::none(),
+        "fused cross-entropy backward (bf16 logits gradient; scale / div when div is given)");
+  m.def("ce_bwd_cs", &ce_bwd_cs, py::arg("logits"), py::arg("labels"), py::arg("lse"),
+        py::arg("scale"), py::arg("ignore"), py::arg("div") = py::none(),
+        "cross-entropy backward over row-strided logits + bias-gradient column partials");
+  m.def("ce_mean", &ce_mean, py::arg("loss"), py::arg("labels"), py::arg("ignore"),
+        "{mean loss, n_valid} from ce_fwd's per-row losses in one launch");
   m.def("transpose_bf16", &transpose_bf16, "w.t().contiguous() (LDS-tiled bf16 transpose)");
   m.def("gelu_bwd", &gelu_bwd, "dh = da * gelu'(h) (erf GELU), bf16");
   m.def("ce_part_fold", &ce_part_fold, "per-segment fold of ce_bwd_cs's column partials");

@@ -234,15 +234,21 @@ hipError_t launch_fault(int dtype, void* g, int64_t D, int kind, float scale, fl
 // grad = (*scale) * (softmax - onehot) (0 rows for ignored labels), scale = dloss / n_valid.
 hipError_t launch_ce_fwd(const void* logits, int64_t R, int V, int64_t ld, const int64_t* labels,
                          int64_t ignore, float* lse, float* loss, hipStream_t stream);
+// div (optional): scale = scale[0] / div[0] in the kernel (grad_output / n_valid, no divide launch)
 hipError_t launch_ce_bwd(const void* logits, int64_t R, int V, const int64_t* labels,
                          int64_t ignore, const float* lse, const float* scale, void* grad,
-                         hipStream_t stream);
+                         hipStream_t stream, const float* div = nullptr);
+// The mean loss from the forward's per-row losses in one launch (one workgroup, fixed order, fp64
+// sums): *out = sum(loss) / n_valid, *count = n_valid = max(#labels != ignore, 1) (fp32).
+hipError_t launch_ce_mean(const float* loss, const int64_t* labels, int64_t R, int64_t ignore,
+                          float* out, float* count, hipStream_t stream);
 // Row-strided form (ld % 8 == 0, R % 64 == 0): grad gets the same stride (columns [V, ld) = 0),
 // and part [R / 64][ld] fp32 the column sums of each 64-row block of the stored gradient;
 // launch_ce_part_fold sums them per segment of R / nseg rows into out [nseg][ldo] (bf16 / fp32).
 hipError_t launch_ce_bwd_cs(const void* logits, int64_t R, int V, int64_t ld,
                             const int64_t* labels, int64_t ignore, const float* lse,
-                            const float* scale, void* grad, float* part, hipStream_t stream);
+                            const float* scale, void* grad, float* part, hipStream_t stream,
+                            const float* div = nullptr);
 hipError_t launch_ce_part_fold(const float* part, int64_t R, int V, int64_t ld, int nseg, void* out,
                                int64_t ldo, int out_f32, hipStream_t stream);
 // dh = bf16(da * gelu'(h)) (erf GELU), n % 8 == 0, 16-B aligned

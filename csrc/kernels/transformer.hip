@@ -131,7 +131,8 @@ __global__ __launch_bounds__(kTB) void ce_bwd_kernel(const bf16* __restrict__ x,
                                                     const int64_t* __restrict__ labels,
                                                     int64_t ignore, const float* __restrict__ lse,
                                                     const float* __restrict__ scale_ptr,
-                                                    bf16* __restrict__ g) {
+                                                    bf16* __restrict__ g,
+                                                    const float* __restrict__ div_ptr) {
   const int64_t r = blockIdx.x;
   const int t = threadIdx.x;
   const int64_t e0 = r * static_cast<int64_t>(V);
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(kTB) void ce_bwd_kernel(const bf16* __restrict__ x,
   if (ci0 > ci1) ci0 = ci1 = end;
   const int64_t lab = labels[r];
   const bool valid = lab != ignore && lab >= 0 && lab < V;
-  const float sc = valid ? *scale_ptr : 0.f;
+  const float sc = valid ? (div_ptr ? *scale_ptr / *div_ptr : *scale_ptr) : 0.f;
   const float L = lse[r];
   const int64_t le = valid ? e0 + lab : -1;
   auto one = [&](int64_t e, float v) { return sc * __expf(v - L) - (e == le ? sc : 0.f); };
@@ -181,7 +182,8 @@ __global__ __launch_bounds__(kTB) void ce_bwd_cs_kernel(const bf16* __restrict__
                                                        const int64_t* __restrict__ labels,
                                                        int64_t ignore, const float* __restrict__ lse,
                                                        const float* __restrict__ scale_ptr,
-                                                       bf16* __restrict__ g, float* __restrict__ part) {
+                                                       bf16* __restrict__ g, float* __restrict__ part,
+                                                       const float* __restrict__ div_ptr) {
   __shared__ float sL[kCeRows], sS[kCeRows];
   __shared__ int sLab[kCeRows];
   const int t = threadIdx.x;
@@ -190,7 +192,7 @@ __global__ __launch_bounds__(kTB) void ce_bwd_cs_kernel(const bf16* __restrict__
     const int64_t lab = labels[r0 + t];
     const bool valid = lab != ignore && lab >= 0 && lab < V;
     sL[t] = lse[r0 + t];
-    sS[t] = valid ? *scale_ptr : 0.f;
+    sS[t] = valid ? (div_ptr ? *scale_ptr / *div_ptr : *scale_ptr) : 0.f;
     sLab[t] = valid ? static_cast<int>(lab) : -1;
   }
   __syncthreads();
@@ -799,26 +801,67 @@ hipError_t launch_ce_fwd(const void* logits, int64_t R, int V, int64_t ld, const
 
 hipError_t launch_ce_bwd(const void* logits, int64_t R, int V, const int64_t* labels,
                          int64_t ignore, const float* lse, const float* scale, void* grad,
-                         hipStream_t st) {
+                         hipStream_t st, const float* div) {
   if (R < 1 || V < 1 || (reinterpret_cast<uintptr_t>(logits) & 15) ||
       (reinterpret_cast<uintptr_t>(grad) & 15))
     return hipErrorInvalidValue;
   ce_bwd_kernel<<<static_cast<unsigned>(R), kTB, 0, st>>>(reinterpret_cast<const bf16*>(logits), V,
                                                           labels, ignore, lse, scale,
-                                                          reinterpret_cast<bf16*>(grad));
+                                                          reinterpret_cast<bf16*>(grad), div);
+  return hipGetLastError();
+}
+
+namespace {
+__global__ __launch_bounds__(1024) void ce_mean_kernel(const float* __restrict__ loss,
+                                                      const int64_t* __restrict__ labels,
+                                                      int64_t R, int64_t ignore,
+                                                      float* __restrict__ out,
+                                                      float* __restrict__ cnt) {
+  __shared__ double ss[1024];
+  __shared__ long long sc[1024];
+  const int t = threadIdx.x;
+  double s = 0.0;
+  long long c = 0;
+  for (int64_t r = t; r < R; r += 1024) {
+    s += static_cast<double>(loss[r]);
+    c += labels[r] != ignore ? 1 : 0;
+  }
+  ss[t] = s;
+  sc[t] = c;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (t < o) {
+      ss[t] += ss[t + o];
+      sc[t] += sc[t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const float n = static_cast<float>(sc[0] > 0 ? sc[0] : 1);
+    out[0] = static_cast<float>(ss[0]) / n;
+    cnt[0] = n;
+  }
+}
+}  // namespace
+
+hipError_t launch_ce_mean(const float* loss, const int64_t* labels, int64_t R, int64_t ignore,
+                          float* out, float* count, hipStream_t st) {
+  if (R < 1) return hipErrorInvalidValue;
+  ce_mean_kernel<<<1, 1024, 0, st>>>(loss, labels, R, ignore, out, count);
   return hipGetLastError();
 }
 
 hipError_t launch_ce_bwd_cs(const void* logits, int64_t R, int V, int64_t ld,
                             const int64_t* labels, int64_t ignore, const float* lse,
-                            const float* scale, void* grad, float* part, hipStream_t st) {
+                            const float* scale, void* grad, float* part, hipStream_t st,
+                            const float* div) {
   if (R < kCeRows || R % kCeRows || V < 1 || ld < V || ld % 8 ||
       ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(grad) |
         reinterpret_cast<uintptr_t>(part)) & 15))
     return hipErrorInvalidValue;
   ce_bwd_cs_kernel<<<static_cast<unsigned>(R / kCeRows), kTB, 0, st>>>(
       reinterpret_cast<const bf16*>(logits), V, ld, labels, ignore, lse, scale,
-      reinterpret_cast<bf16*>(grad), part);
+      reinterpret_cast<bf16*>(grad), part, div);
   return hipGetLastError();
 }
 

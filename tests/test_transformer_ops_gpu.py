@@ -14,7 +14,8 @@ def _leaf(t):
     return t.detach().clone().requires_grad_(True)
 
 
-@pytest.mark.parametrize("R,V", [(7, 1000), (33, 30522), (5, 13), (4, 128256), (3, 3)])
+@pytest.mark.parametrize("R,V", [(7, 1000), (33, 30522), (5, 13), (4, 128256), (3, 3),
+                                 (3000, 50)])
 def test_cross_entropy(cuda, R, V):
     torch.manual_seed(R + V)
     x = (torch.randn(R, V, device=cuda) * 3).to(torch.bfloat16).requires_grad_(True)
@@ -30,6 +31,16 @@ def test_cross_entropy(cuda, R, V):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=2e-2, atol=2e-4)
     if R > 4:
         assert x.grad[1].abs().max().item() == 0.0
+
+
+def test_cross_entropy_all_ignored(cuda):
+    """Every label ignored: loss 0 and a zero gradient (the valid count clamps to 1, as
+    F.cross_entropy's reduction would divide by zero)."""
+    x = torch.randn(9, 40, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    y = torch.full((9,), -100, device=cuda, dtype=torch.long)
+    loss = T.cross_entropy(x, y)
+    loss.backward()
+    assert loss.item() == 0.0 and x.grad.abs().max().item() == 0.0
 
 
 def test_cross_entropy_misaligned_view(cuda):
