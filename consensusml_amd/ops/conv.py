@@ -722,10 +722,12 @@ _SIDE_STREAMS: Dict[torch.device, "torch.cuda.Stream"] = {}
 
 
 def _wgrad_fork(fn, *args):
-    """(dw, handle): ``fn(*args)`` on the side stream (PerfPolicy.side_wgrad, CUDA tensors), else
-    inline (handle None). ``_wgrad_join`` before the backward returns."""
+    """(dw, handle): ``fn(*args)`` on the side stream (PerfPolicy.side_wgrad, CUDA tensors, batch
+    ``args[0].shape[0]`` >= side_wgrad_min_batch), else inline (handle None). ``_wgrad_join``
+    before the backward returns."""
     dev = args[0].device
-    if not (_P().side_wgrad and dev.type == "cuda"):
+    pol = _P()
+    if not (pol.side_wgrad and dev.type == "cuda" and args[0].shape[0] >= pol.side_wgrad_min_batch):
         return fn(*args), None
     side = _SIDE_STREAMS.get(dev)
     if side is None:

@@ -81,8 +81,10 @@ class PerfPolicy:
                                           # absorbs the downsample's dX (no pool two-gradient sum)
     own_conv3x3_s2: bool = True           # stride-2 3x3: conv_gemm forward + BN stats, parity-class
                                           # data gradient (+ bn1 backward sums)
-    side_wgrad: bool = False              # 3x3 weight gradients on a side stream, concurrent with
-                                          # the same conv's data-gradient / BN-backward kernels
+    side_wgrad: bool = True               # 3x3 weight gradients on a side stream, concurrent with
+                                          # the same conv's data-gradient / BN-backward kernels,
+    side_wgrad_min_batch: int = 1024      # ... at per-GPU batches >= this: batch 2560 -0.2 to
+                                          # -0.6 ms/step, batch 256 +0.3 ms (profiles/r06_53/)
     fin_dgamma: bool = True               # BN parameter gradients from the backward sums' finalize
                                           # launch (no bn_bwd_coeffs launch: batch-256 tails)
     fin_affine: bool = True               # BN affine (gamma invstd, beta - mean sc) from the
@@ -152,7 +154,8 @@ class PerfPolicy:
             own_wgrad1x1_s2=_env_bool("CML_WGRAD1X1_S2", True),
             c1_dgrad64_gemm=_env_bool("CML_C1_DGRAD64", True),
             own_conv3x3_s2=_env_bool("CML_CONV3X3_S2", True),
-            side_wgrad=_env_bool("CML_SIDE_WGRAD", False),
+            side_wgrad=_env_bool("CML_SIDE_WGRAD", True),
+            side_wgrad_min_batch=_env_int("CML_SIDE_WGRAD_MIN_BATCH", 1024),
             fin_dgamma=_env_bool("CML_FIN_DGAMMA", True),
             fin_affine=_env_bool("CML_FIN_AFFINE", True),
             batch_wlayouts=_env_bool("CML_BATCH_WLAYOUTS", True),

@@ -33,7 +33,7 @@ def test_side_wgrad_bit_identical(cuda, N, C, H, stride):
     gz = _nhwc(torch.randn(N, C, Ho, Ho, device=cuda, generator=g0).bfloat16())
     out = {}
     for side in (False, True, False):
-        with perf.use_policy(perf.policy().replace(side_wgrad=side)):
+        with perf.use_policy(perf.policy().replace(side_wgrad=side, side_wgrad_min_batch=0)):
             res = []
             for _ in range(2):   # the second call reuses the side stream's freed blocks
                 zi, gi, bi, wi = (t.clone().requires_grad_(True) for t in (z1, g1, b1, w))
