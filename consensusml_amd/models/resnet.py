@@ -106,14 +106,17 @@ class _Conv1x1Fn(torch.autograd.Function):
         mio_dx = need_dx and not ctx.dgrad_gemm
         own_dw = ctx.own_wgrad and ctx.needs_input_grad[1]
         mio_dw = ctx.needs_input_grad[1] and not own_dw
-        dx_m, dw = None, None
+        dx_m, dw, h = None, None, None
+        if own_dw:   # on the side stream (large batches) while the data gradient runs
+            from ..ops.native import lib
+            dw, h = fconv._wgrad_fork(lambda d, a, b: lib().wgrad1x1(d, a, b.dtype).view_as(b),
+                                      dy, x, w, conv1x1=True)
         if mio_dx or mio_dw:
-            dx_m, dw, _ = torch.ops.aten.convolution_backward(
+            dx_m, dw_m, _ = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                 [mio_dx, mio_dw, False])
-        if own_dw:
-            from ..ops.native import lib
-            dw = lib().wgrad1x1(dy, x, w.dtype).view_as(w)
+            if mio_dw:
+                dw = dw_m
         dx = dx_m if mio_dx else None
         if need_dx and ctx.dgrad_gemm:
             dy2 = dy.permute(0, 2, 3, 1).reshape(N * H * W, Co)
@@ -121,8 +124,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             link = ctx.link
             g = link.take() if link is not None else None
             if isinstance(g, fconv.MaskedGrad):
-                return (fconv.masked_link_dgrad(dy, w, g, link, ctx.wt), dw, None, None, None,
-                        None)
+                dx = fconv.masked_link_dgrad(dy, w, g, link, ctx.wt)
+                return dx, fconv._wgrad_join(dw, h), None, None, None, None
             if isinstance(g, fconv.S2Grad):
                 g = g.materialize()
             w_nk = ctx.wt if ctx.wt is not None else w2.t()
@@ -135,7 +138,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 d2 = fconv.conv_mm(dy2, w_nk)
             dx = d2.view(N, H, W, C).permute(0, 3, 1, 2)
-        return dx, dw, None, None, None, None
+        return dx, fconv._wgrad_join(dw, h), None, None, None, None
 
 
 # (cin, cout) of the stride-1 1x1 convs whose weight gradient runs on wgrad1x1.hip. In isolation the

@@ -181,9 +181,12 @@ class _Conv1x1BNStatsFn(torch.autograd.Function):
     def backward(ctx, dy, _dm, _di):
         x, w = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
+        # the weight gradient on the side stream (large batches) while the data gradient runs
+        dw, h = _wgrad_fork(lambda d, a, b: _wgrad(d, a, b, ctx.stride, ctx.own_wgrad), dy, x, w,
+                            conv1x1=True) if ctx.needs_input_grad[1] else (None, None)
         dx = _dgrad(dy, x, w, ctx.stride, ctx.dgrad_gemm, ctx.link, ctx.wt) \
             if ctx.needs_input_grad[0] else None
-        dw = _wgrad(dy, x, w, ctx.stride, ctx.own_wgrad) if ctx.needs_input_grad[1] else None
+        dw = _wgrad_join(dw, h)
         return dx, dw, None, None, None, None, None, None, None, None, None
 
 
@@ -721,13 +724,14 @@ def _zero_row(device: torch.device) -> torch.Tensor:
 _SIDE_STREAMS: Dict[torch.device, "torch.cuda.Stream"] = {}
 
 
-def _wgrad_fork(fn, *args):
+def _wgrad_fork(fn, *args, conv1x1: bool = False):
     """(dw, handle): ``fn(*args)`` on the side stream (PerfPolicy.side_wgrad, CUDA tensors, batch
     ``args[0].shape[0]`` >= side_wgrad_min_batch), else inline (handle None). ``_wgrad_join``
     before the backward returns."""
     dev = args[0].device
     pol = _P()
-    if not (pol.side_wgrad and dev.type == "cuda" and args[0].shape[0] >= pol.side_wgrad_min_batch):
+    if not (pol.side_wgrad and dev.type == "cuda" and args[0].shape[0] >= pol.side_wgrad_min_batch
+            and (pol.side_wgrad_1x1 or not conv1x1)):
         return fn(*args), None
     side = _SIDE_STREAMS.get(dev)
     if side is None:

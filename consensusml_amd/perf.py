@@ -85,6 +85,9 @@ class PerfPolicy:
                                           # the same conv's data-gradient / BN-backward kernels,
     side_wgrad_min_batch: int = 1024      # ... at per-GPU batches >= this: batch 2560 -0.2 to
                                           # -0.6 ms/step, batch 256 +0.3 ms (profiles/r06_53/)
+    side_wgrad_1x1: bool = False          # ... also the 1x1 convs' weight gradients: batch 2560
+                                          # 141.77 / 140.83 / 141.58 vs 141.15 / 140.73 / 141.84 ms
+                                          # (noise level, profiles/r06_55/)
     fin_dgamma: bool = True               # BN parameter gradients from the backward sums' finalize
                                           # launch (no bn_bwd_coeffs launch: batch-256 tails)
     fin_affine: bool = True               # BN affine (gamma invstd, beta - mean sc) from the
@@ -156,6 +159,7 @@ class PerfPolicy:
             own_conv3x3_s2=_env_bool("CML_CONV3X3_S2", True),
             side_wgrad=_env_bool("CML_SIDE_WGRAD", True),
             side_wgrad_min_batch=_env_int("CML_SIDE_WGRAD_MIN_BATCH", 1024),
+            side_wgrad_1x1=_env_bool("CML_SIDE_WGRAD_1X1", False),
             fin_dgamma=_env_bool("CML_FIN_DGAMMA", True),
             fin_affine=_env_bool("CML_FIN_AFFINE", True),
             batch_wlayouts=_env_bool("CML_BATCH_WLAYOUTS", True),

@@ -50,3 +50,29 @@ def test_side_wgrad_bit_identical(cuda, N, C, H, stride):
                 for a, b in zip(call, ref):
                     assert torch.equal(a, b)
 
+
+
+def test_side_wgrad_1x1_model_bit_identical(cuda):
+    """The 1x1 convs' weight gradients on the side stream too (side_wgrad_1x1): a ResNet-50
+    training backward at 64 x 64 gives the same 1x1 weight gradients with the side stream on and
+    off (loosely: MIOpen may pick another algorithm between runs, tools/diag/det_diag.py, so the
+    check is for ordering errors -- a missing join reads a half-written gradient)."""
+    import copy
+
+    import consensusml_amd.models.resnet as R
+    from consensusml_amd import perf
+    torch.manual_seed(2)
+    base = R.resnet50(num_classes=10).to(cuda).to(memory_format=torch.channels_last).bfloat16()
+    x = _nhwc(torch.randn(8, 3, 64, 64, device=cuda).bfloat16())
+    out = {}
+    for side in (False, True):
+        m = copy.deepcopy(base)
+        with perf.use_policy(perf.policy().replace(side_wgrad=side, side_wgrad_min_batch=0,
+                                                   side_wgrad_1x1=True)):
+            m(x).float().square().mean().backward()
+        torch.cuda.synchronize()
+        out[side] = {n: p.grad.clone() for n, p in m.named_parameters()
+                     if p.dim() == 4 and p.shape[2] == 1}
+    for n, g in out[False].items():
+        rel = ((out[True][n].float() - g.float()).norm() / g.float().norm().clamp_min(1e-12)).item()
+        assert rel < 2e-2, (n, rel)
