@@ -128,7 +128,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 return dx, fconv._wgrad_join(dw, h), None, None, None, None
             if isinstance(g, fconv.S2Grad):
                 g = g.materialize()
-            w_nk = ctx.wt if ctx.wt is not None else w2.t()
+            w_nk = fconv.dgrad_wnk(dy2, w2, ctx.wt)
             if g is not None:
                 dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
                 if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():

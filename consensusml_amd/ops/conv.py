@@ -60,6 +60,16 @@ def _nt_tile(a: torch.Tensor, M: int, N: int, K: int) -> int:
 CONV_MM_STATS = {"own": 0, "own128": 0, "blas": 0}   # which path conv_mm took (tests)
 
 
+def dgrad_wnk(a: torch.Tensor, w2: torch.Tensor, wt: Optional[torch.Tensor]) -> torch.Tensor:
+    """conv_mm's weight operand for a 1x1 data gradient a [M, Co] @ W [Co, Ci]: the prefetched
+    transpose ``wt`` when gemm.hip takes the GEMM (no transpose launch), else the view ``w2.t()``
+    (hipBLASLt then reads W as stored: 892 vs 917 us through a transposed view at the layer-1
+    shape, tools/diag/addmm_layout.py)."""
+    if wt is not None and _nt_tile(a, a.shape[0], w2.shape[1], w2.shape[0]):
+        return wt
+    return w2.t()
+
+
 def conv_mm(a: torch.Tensor, w_nk: torch.Tensor, acc: Optional[torch.Tensor] = None) -> torch.Tensor:
     """a [M, K] @ w_nk^T (+ acc, in place) for a 1x1 conv as a plain GEMM: the forward (w_nk = W
     [Co, C]) or the data gradient (w_nk = W^T [C, Co]; acc = a parked residual gradient). On
@@ -105,7 +115,7 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm
                 return lib().conv1x1_link_s2(dy.contiguous(memory_format=torch.channels_last), wt,
                                              g.g)
             g = g.materialize()
-        w_nk = wt if wt is not None else w2.t()   # W^T: prefetched, or transposed by conv_mm
+        w_nk = dgrad_wnk(dy2, w2, wt)
         if g is not None:
             dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
             if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():
