@@ -116,6 +116,15 @@ def _dgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, gemm
                                              g.g)
             g = g.materialize()
         w_nk = dgrad_wnk(dy2, w2, wt)
+        if (g is not None and g.dim() == 4 and _P().link_dgrad_plain and dy.dtype == torch.bfloat16
+                and g.dtype == torch.bfloat16 and C % 64 == 0 and Co % 64 == 0
+                and g.is_contiguous(memory_format=torch.channels_last)
+                and not _nt_tile(dy2, N * H * W, C, Co)):
+            # the GEMM would go to hipBLASLt (e.g. layer 1.0's 64 -> 64 with the downsample's dX):
+            # the fused 1x1 kernel with the parked gradient added in its epilogue instead
+            wt2 = wt if wt is not None else w2.t().contiguous()
+            return lib().conv1x1_link(dy.contiguous(memory_format=torch.channels_last), wt2, g,
+                                      None)[0]
         if g is not None:
             dres = g.permute(0, 2, 3, 1).reshape(N * H * W, C) if g.dim() == 4 else g
             if dres.data_ptr() == g.data_ptr() and dres.is_contiguous():

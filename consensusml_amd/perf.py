@@ -85,6 +85,9 @@ class PerfPolicy:
                                           # the same conv's data-gradient / BN-backward kernels,
     side_wgrad_min_batch: int = 1024      # ... at per-GPU batches >= this: batch 2560 -0.2 to
                                           # -0.6 ms/step, batch 256 +0.3 ms (profiles/r06_53/)
+    link_dgrad_plain: bool = True         # 1x1 data gradients that absorb a plain parked gradient
+                                          # and would run on hipBLASLt (N 64): the fused 1x1 kernel
+                                          # with the add in its epilogue (conv1x1_link, no mask)
     side_wgrad_1x1: bool = False          # ... also the 1x1 convs' weight gradients: batch 2560
                                           # 141.77 / 140.83 / 141.58 vs 141.15 / 140.73 / 141.84 ms
                                           # (noise level, profiles/r06_55/)
@@ -160,6 +163,7 @@ class PerfPolicy:
             side_wgrad=_env_bool("CML_SIDE_WGRAD", True),
             side_wgrad_min_batch=_env_int("CML_SIDE_WGRAD_MIN_BATCH", 1024),
             side_wgrad_1x1=_env_bool("CML_SIDE_WGRAD_1X1", False),
+            link_dgrad_plain=_env_bool("CML_LINK_DGRAD_PLAIN", True),
             fin_dgamma=_env_bool("CML_FIN_DGAMMA", True),
             fin_affine=_env_bool("CML_FIN_AFFINE", True),
             batch_wlayouts=_env_bool("CML_BATCH_WLAYOUTS", True),

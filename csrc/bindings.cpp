@@ -899,7 +899,7 @@ Tensor conv1x1_bnbwd(const Tensor& g, const Tensor& z, const Tensor& mask, const
 // w [Nout, K], link [N, Nout, H, W] + lmask [M, Nout/8] -> y = x w^T + (lmask ? link : 0). With sz /
 // smask / mean / invstd (the BN + ReLU that consumes y): also {sdz, sdzx} = its backward sums.
 std::vector<Tensor> conv1x1_link(const Tensor& x, const Tensor& w, const Tensor& link,
-                                 const Tensor& lmask, const optional<Tensor>& sz,
+                                 const optional<Tensor>& lmask, const optional<Tensor>& sz,
                                  const optional<Tensor>& smask, const optional<Tensor>& mean,
                                  const optional<Tensor>& invstd) {
   check_nhwc(x, "x");
@@ -2724,7 +2724,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_link", &conv1x1_link, py::arg("x"), py::arg("w"), py::arg("link"),
         py::arg("lmask"), py::arg("sz") = py::none(), py::arg("smask") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(),
-        "1x1 data gradient + masked residual gradient (+ the consumer BN's backward sums)");
+        "1x1 data gradient + masked residual gradient (lmask None: plain residual add) (+ the "
+        "consumer BN's backward sums)");
   m.def("bn_stats_gram", &bn_stats_gram, py::arg("G"), py::arg("cy"), py::arg("w"), py::arg("M"),
         py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
         py::arg("eps") = 1e-5, py::arg("momentum") = 0.1, py::arg("gamma") = py::none(),

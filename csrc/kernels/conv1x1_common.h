@@ -176,7 +176,7 @@ __device__ __forceinline__ void epilogue(const C1Args& a, f32x16 (&acc)[2][2], f
           lbv[k] = ev ? 0xffu : 0u;
         } else {
           lv[k] = *reinterpret_cast<const uint4*>(a.link + e0);
-          lbv[k] = a.lm[e0 >> 3];
+          lbv[k] = a.lm ? a.lm[e0 >> 3] : 0xffu;   // no mask: a plain residual add
         }
       }
       if constexpr (SM == SM_BNRES)   // (no residual: link null)

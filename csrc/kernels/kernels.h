@@ -552,6 +552,7 @@ size_t conv1x1_cat_part_floats(int64_t M, int K, int N);
 hipError_t launch_conv1x1_bnbwd(const void* g, const void* z, const uint8_t* mask, const float* ca,
                                 const float* cb, const float* cc, const void* w, void* y,
                                 int64_t M, int K, int N, hipStream_t st);
+// (lm null: the link is added everywhere)
 hipError_t launch_conv1x1_link(const void* x, const void* w, void* y, const void* link,
                                const uint8_t* lm, const void* sz, const uint8_t* sm,
                                const float* mean, const float* invstd, float* part, float* sdz,

@@ -182,3 +182,16 @@ def test_avgpool_bwd_matches_reference(cuda):
         x = _nhwc(torch.randn(N, C, H, H, device=cuda).bfloat16()).requires_grad_(True)
         global_avg_pool(x).backward(g)
         assert torch.equal(x.grad, ref)
+
+
+@pytest.mark.parametrize("N,K,C,H", [(4, 64, 64, 56), (2, 128, 64, 28), (3, 64, 128, 14)])
+def test_conv1x1_link_plain(cuda, N, K, C, H):
+    """conv1x1_link without a mask: dX = dY W + g everywhere (bf16(bf16(dY W) + g)) vs fp32."""
+    g0 = torch.Generator(device=cuda).manual_seed(N + K + C + H)
+    dy = _nhwc(torch.randn(N, K, H, H, device=cuda, generator=g0).bfloat16())
+    w = (torch.randn(K, C, device=cuda, generator=g0) * K ** -0.5).bfloat16()   # forward [Co, Ci]
+    g = _nhwc(torch.randn(N, C, H, H, device=cuda, generator=g0).bfloat16())
+    dx = lib().conv1x1_link(dy, w.t().contiguous(), g, None)[0]
+    ref = torch.einsum("nkhw,kc->nchw", dy.float(), w.float()) + g.float()
+    assert dx.shape == g.shape and dx.is_contiguous(memory_format=torch.channels_last)
+    assert ((dx.float() - ref).norm() / ref.norm()).item() < 8e-3
